@@ -1,0 +1,118 @@
+/*
+ * slamhot.h — C-ABI of the MI355X-native ORB-SLAM3 hot path (gfx950, HIP).
+ *
+ * This is the drop-in boundary.  Every entry point replaces one reference interface;
+ * the citation after each declaration names it (paths relative to the ORB-SLAM3-Noted
+ * reference tree).  Conventions:
+ *   - plain C types only: pointers + sizes, no C++ / OpenCV / torch types;
+ *   - the caller owns every host buffer; a handle owns its device memory and a private
+ *     HIP stream;
+ *   - every call returns a slam_status; negative = error; nothing throws across the ABI;
+ *   - handles are independent (thread-safe across handles, not within one handle),
+ *     mirroring "one ORBextractor per camera, used by one thread at a time"
+ *     (Frame.cc:119-122).
+ *   - there is no CPU fallback: without a usable gfx950 device, create() fails with
+ *     SLAM_ENODEV.
+ */
+#ifndef SLAMHOT_H
+#define SLAMHOT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int32_t slam_status;
+enum {
+    SLAM_OK = 0,
+    SLAM_EINVAL = -1,  /* bad argument / shape */
+    SLAM_ENOMEM = -2,  /* device or host allocation failed */
+    SLAM_EHIP = -3,    /* HIP runtime error */
+    SLAM_ECAP = -4,    /* output capacity too small (n holds the required size) */
+    SLAM_ENODEV = -5,  /* no gfx950 device */
+    SLAM_EEMPTY = -6   /* empty image (reference returns -1, ORBextractor.cc:1072-1073) */
+};
+
+/* cv::KeyPoint memory layout (28 bytes): pt.x, pt.y, size, angle, response, octave, class_id */
+typedef struct slam_keypoint {
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+} slam_keypoint;
+
+/* ORBextractor(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST)
+ * (ORBextractor.h:49-50, ORBextractor.cc:408-468) */
+typedef struct slam_orb_params {
+    int32_t nfeatures;
+    float scale_factor;
+    int32_t nlevels;
+    int32_t ini_th_fast;
+    int32_t min_th_fast;
+} slam_orb_params;
+
+typedef struct slam_extractor slam_extractor;
+
+/* Library / device probing. */
+const char* slamhot_version(void);
+const char* slamhot_status_string(slam_status s);
+slam_status slamhot_device_count(int* n);
+
+/* ---------------------------------------------------------------------------------
+ * ORB extractor
+ * ------------------------------------------------------------------------------- */
+
+/* Replaces ORBextractor::ORBextractor (ORBextractor.cc:408-468).  max_width/max_height
+ * bound the frames; max_batch bounds slamhot_extract_batch*.  The scale tables are built
+ * on the host exactly as the reference builds them. */
+slam_status slamhot_extractor_create(const slam_orb_params* params, int device, int max_width,
+                                     int max_height, int max_batch, slam_extractor** out);
+void slamhot_extractor_destroy(slam_extractor* ex);
+
+/* Replaces GetLevels/GetScaleFactors/GetInverseScaleFactors/GetScaleSigmaSquares/
+ * GetInverseScaleSigmaSquares (ORBextractor.h:61-81) and the private mnFeaturesPerLevel.
+ * Each array has nlevels entries; any pointer may be NULL. */
+slam_status slamhot_extractor_levels(const slam_extractor* ex, int* nlevels, float* scale,
+                                     float* inv_scale, float* sigma2, float* inv_sigma2,
+                                     int32_t* nfeatures_per_level);
+
+/* Replaces int ORBextractor::operator()(img, mask, keypoints, descriptors, vLappingArea)
+ * (ORBextractor.cc:1068-1150) for ONE host image (CV_8UC1, row stride `stride` bytes).
+ * Writes up to `cap` keypoints (cv::KeyPoint layout) and cap*32 descriptor bytes, in the
+ * reference's output order (level-major, octree order, lapping split from the back).
+ * *n = number of keypoints, *mono_index = operator()'s return value.  Returns SLAM_ECAP
+ * (with *n set) if cap is too small. */
+slam_status slamhot_extract(slam_extractor* ex, const uint8_t* img, int width, int height,
+                            size_t stride, int lap0, int lap1, slam_keypoint* kps,
+                            uint8_t* desc, int cap, int* n, int* mono_index);
+
+/* Batched form: nframes host images of identical size, frame f at img + f*height*stride.
+ * Outputs are strided by cap per frame: kps[f*cap + i], desc[(f*cap + i)*32].  n and
+ * mono_index have nframes entries. */
+slam_status slamhot_extract_batch(slam_extractor* ex, int nframes, const uint8_t* imgs,
+                                  int width, int height, size_t stride, int lap0, int lap1,
+                                  slam_keypoint* kps, uint8_t* desc, int cap, int* n,
+                                  int* mono_index);
+
+/* Device-resident batch (inputs already in HBM).  d_imgs: nframes*height*width bytes
+ * (tight rows).  Outputs are device pointers with the same layout as the host batch form.
+ * `hip_stream` may be NULL (the handle's stream).  Asynchronous: synchronise the stream
+ * before reading outputs.  Capacity overflow is reported per frame by n[f] > cap. */
+slam_status slamhot_extract_batch_device(slam_extractor* ex, int nframes, const void* d_imgs,
+                                         int width, int height, int lap0, int lap1,
+                                         void* d_kps, void* d_desc, int cap, void* d_n,
+                                         void* d_mono_index, void* hip_stream);
+
+/* Public ORBextractor::mvImagePyramid (ORBextractor.h:83), read by
+ * Frame::ComputeStereoMatches: copies level `level` of batch frame `frame` of the last
+ * extraction into dst (tight rows, capacity dst_cap bytes) and returns its size. */
+slam_status slamhot_pyramid_level(slam_extractor* ex, int frame, int level, uint8_t* dst,
+                                  size_t dst_cap, int* width, int* height);
+
+/* Stream the handle works on (hipStream_t as void*). */
+void* slamhot_extractor_stream(slam_extractor* ex);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SLAMHOT_H */

@@ -1,0 +1,1156 @@
+// extractor.hip — MI355X (gfx950) ORB extractor: the device side of
+// ORBextractor::operator() (ORBextractor.cc:1068-1150), batched over frames.
+//
+// Pipeline per batch (one HIP stream, captured in a hipGraph per geometry):
+//   k_resize      x (L-1)  chained INTER_LINEAR pyramid            ComputePyramid :1152
+//   k_fast_cells  x 1      per-cell FAST-9 score + per-cell 3x3 NMS ComputeKeyPointsOctTree :787-853
+//   k_octree      x 1      quadtree distribution, 1 WG/(frame,lvl) DistributeOctTree :537-761
+//   k_layout      x 1      lapping-area output order, 1 WG/frame   operator() :1100-1146
+//   k_blur        x 1      GaussianBlur 7x7 sigma 2 fixed point    operator() :1114-1115
+//   k_orb         x 1      IC angle + rBRIEF, one wave per kp      IC_Angle :75, computeOrbDescriptor :106
+//
+// Data layout in HBM (per handle, batch-major): input frames (level 0, tight rows); pyramid
+// levels 1.. per frame, rows padded to 64 B; blurred levels per frame; per-cell candidate
+// slots; per-(frame,level) octree keypoints; per-frame output index map.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "common.hpp"
+#include "device_math.hpp"
+#include "extractor_plan.hpp"
+
+namespace slamhot {
+
+__constant__ int c_pattern[256 * 4] = {
+#include "orb_pattern.inc"
+};
+
+// Device copy of the plan (uploaded once per geometry).
+struct DevLevel {
+    int w, h, pitch;
+    int64_t pyr_off, blur_off;
+    int minBX, minBY, maxBX, maxBY;
+    int cell_begin, cell_end;
+    int nfeat, kbase, kcap, key_base, key_cap;
+    float scale, size;
+    int nIni;
+    int root_x0[kMaxRoots], root_x1[kMaxRoots], root_first_x[kMaxRoots];
+    int xtab_off, ytab_off, xmax;
+};
+
+struct DevPlan {
+    int nlevels, W, H;
+    int ncells, slot_cap, kslots, key_slots, max_nodes;
+    int ini_th, min_th;
+    int64_t pyr_frame, blur_frame;
+    int umax[kHalfPatch + 1];
+    DevLevel lv[kMaxLevels];
+};
+
+// Buffers of one batch launch (device pointers).
+struct Bufs {
+    const uint8_t* img;     // level 0 frames, tight rows (W bytes)
+    uint8_t* pyr;           // levels >= 1, per frame pyr_frame bytes
+    uint8_t* blur;          // all levels blurred, per frame blur_frame bytes
+    uint32_t* cell_keys;    // per frame ncells*slot_cap packed candidates
+    int32_t* cell_cnt;      // per frame ncells
+    uint32_t* keys_g;       // per frame key_slots (octree overflow scratch: keys)
+    uint16_t* knode_g;      // per frame key_slots (octree overflow scratch: node ids)
+    uint32_t* okp;          // per frame kslots packed octree keypoints (level coords)
+    int32_t* ocnt;          // per frame nlevels octree counts
+    int32_t* oidx;          // per frame kslots final output index
+    int32_t* err;           // per frame error flags
+    slam_keypoint* out_kps; // per frame cap
+    uint8_t* out_desc;      // per frame cap*32
+    int32_t* out_n;         // per frame
+    int32_t* out_mono;      // per frame
+    const ResizeX* xtab;
+    const ResizeY* ytab;
+    const CellDesc* cells;
+    const DevPlan* plan;
+    int nframes, cap, lap0, lap1;
+};
+
+__device__ __forceinline__ const uint8_t* level_ptr(const Bufs& b, const DevPlan& P, int f, int l) {
+    if (l == 0) return b.img + (size_t)f * P.H * P.W;
+    return b.pyr + (size_t)f * P.pyr_frame + P.lv[l].pyr_off;
+}
+__device__ __forceinline__ int level_pitch(const DevPlan& P, int l) {
+    return l == 0 ? P.W : P.lv[l].pitch;
+}
+
+// packed candidate / keypoint: x (12 b) | y (12 b) | score (8 b)
+__device__ __forceinline__ uint32_t pack_kp(int x, int y, int s) {
+    return (uint32_t)x | ((uint32_t)y << 12) | ((uint32_t)s << 24);
+}
+__device__ __forceinline__ int kp_x(uint32_t k) { return (int)(k & 0xFFF); }
+__device__ __forceinline__ int kp_y(uint32_t k) { return (int)((k >> 12) & 0xFFF); }
+__device__ __forceinline__ int kp_s(uint32_t k) { return (int)(k >> 24); }
+
+// ---------------------------------------------------------------------------------------
+// k_resize: level l from level l-1 (cv::resize INTER_LINEAR 8U, OpenCV 4.2.0 generic fixed
+// point path).  Integer-only on the device: coefficient tables come from the host plan.
+// Block 64x4 threads, 4 output pixels per thread (one 32-bit store, rows padded to 64 B).
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_resize(Bufs b, int l) {
+    const DevPlan& P = *b.plan;
+    const DevLevel& L = P.lv[l];
+    const int f = blockIdx.z;
+    const int dy = blockIdx.y * 4 + threadIdx.y;
+    const int dx0 = (blockIdx.x * 64 + threadIdx.x) * 4;
+    if (dy >= L.h || dx0 >= L.w) return;
+    const uint8_t* src = level_ptr(b, P, f, l - 1);
+    const int spitch = level_pitch(P, l - 1);
+    uint8_t* dst = b.pyr + (size_t)f * P.pyr_frame + L.pyr_off + (size_t)dy * L.pitch;
+    const ResizeY ry = b.ytab[L.ytab_off + dy];
+    const uint8_t* S0 = src + (size_t)ry.y0 * spitch;
+    const uint8_t* S1 = src + (size_t)ry.y1 * spitch;
+    uint32_t word = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int dx = dx0 + k;
+        int v = 0;
+        if (dx < L.w) {
+            const ResizeX rx = b.xtab[L.xtab_off + dx];
+            int d0, d1;
+            if (dx < L.xmax) {
+                d0 = S0[rx.sx] * rx.a0 + S0[rx.sx + 1] * rx.a1;
+                d1 = S1[rx.sx] * rx.a0 + S1[rx.sx + 1] * rx.a1;
+            } else {
+                d0 = S0[rx.sx] * 2048;
+                d1 = S1[rx.sx] * 2048;
+            }
+            v = (((ry.b0 * (d0 >> 4)) >> 16) + ((ry.b1 * (d1 >> 4)) >> 16) + 2) >> 2;
+        }
+        word |= (uint32_t)(v & 0xFF) << (8 * k);
+    }
+    *reinterpret_cast<uint32_t*>(dst + dx0) = word;
+}
+
+// ---------------------------------------------------------------------------------------
+// FAST-9/16 corner measure (OpenCV 4.2.0 FAST_t<16> + cornerScore<16>, closed form).
+// For centre v and circle p[0..15], d_k = v - p_k.  With window minima/maxima over the 16
+// circular windows of 9:  Mdark = max_s min(d[s..s+8]),  Mbright = -min_s max(d[s..s+8]),
+// M = max(Mdark, Mbright).  The pixel is a FAST corner at threshold t iff M > t, and then
+// cornerScore<16>(t) = M - 1 (independent of t; the early-outs of the reference loop only
+// prune).  M <= 0 is stored as 0 (not a corner at any t >= 0).
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ int fast_measure(const uint8_t* c, int stride, int tlow) {
+    const int v = c[0];
+    int p[16];
+    p[0] = c[3 * stride];
+    p[1] = c[3 * stride + 1];
+    p[2] = c[2 * stride + 2];
+    p[3] = c[stride + 3];
+    p[4] = c[3];
+    p[5] = c[-stride + 3];
+    p[6] = c[-2 * stride + 2];
+    p[7] = c[-3 * stride + 1];
+    p[8] = c[-3 * stride];
+    p[9] = c[-3 * stride - 1];
+    p[10] = c[-2 * stride - 2];
+    p[11] = c[-stride - 3];
+    p[12] = c[-3];
+    p[13] = c[stride - 3];
+    p[14] = c[2 * stride - 2];
+    p[15] = c[3 * stride - 1];
+    // corner test at the lowest threshold: 9 contiguous darker or brighter
+    uint32_t dk = 0, br = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        dk |= (uint32_t)(p[k] < v - tlow) << k;
+        br |= (uint32_t)(p[k] > v + tlow) << k;
+    }
+    uint32_t a = dk | (dk << 16), bb = br | (br << 16);
+    uint32_t ra = a, rb = bb;
+#pragma unroll
+    for (int s = 1; s < 9; s++) {
+        ra &= a >> s;
+        rb &= bb >> s;
+    }
+    if (((ra | rb) & 0xFFFFu) == 0) return 0;
+    int d[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) d[k] = v - p[k];
+    int m2[16], x2[16];
+#pragma unroll
+    for (int s = 0; s < 16; s++) {
+        m2[s] = min(d[s], d[(s + 1) & 15]);
+        x2[s] = max(d[s], d[(s + 1) & 15]);
+    }
+    int m4[16], x4[16];
+#pragma unroll
+    for (int s = 0; s < 16; s++) {
+        m4[s] = min(m2[s], m2[(s + 2) & 15]);
+        x4[s] = max(x2[s], x2[(s + 2) & 15]);
+    }
+    int mdark = -1000, mbr = 1000;
+#pragma unroll
+    for (int s = 0; s < 16; s++) {
+        const int mn9 = min(min(m4[s], m4[(s + 4) & 15]), d[(s + 8) & 15]);
+        const int mx9 = max(max(x4[s], x4[(s + 4) & 15]), d[(s + 8) & 15]);
+        mdark = max(mdark, mn9);
+        mbr = min(mbr, mx9);
+    }
+    const int M = max(mdark, -mbr);
+    return M > 0 ? M : 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// k_fast_cells: one workgroup per (cell, frame).  The cell ROI [iniY,maxY)x[iniX,maxX) is
+// exactly what the reference hands cv::FAST (ORBextractor.cc:808); its tested pixels are
+// rows/cols 3..size-4, and NMS compares against 0 outside them (cell-local NMS).  The
+// second threshold is used only when the first yields no keypoint after NMS (:825-841).
+// Output: candidates in row-major order, packed with LEVEL coordinates.
+// ---------------------------------------------------------------------------------------
+constexpr int kCellMaxW = 80, kCellMaxH = 80;
+
+__global__ void __launch_bounds__(256) k_fast_cells(Bufs b) {
+    __shared__ uint8_t roi[kCellMaxH * kCellMaxW];
+    __shared__ uint8_t meas[kCellMaxH * kCellMaxW];
+    __shared__ int scratch[20];
+    const DevPlan& P = *b.plan;
+    const int f = blockIdx.y;
+    const CellDesc cd = b.cells[blockIdx.x];
+    const int l = cd.level;
+    const uint8_t* img = level_ptr(b, P, f, l);
+    const int pitch = level_pitch(P, l);
+    const int cw = cd.cw, ch = cd.ch;
+    // stage the ROI (row stride cw in LDS)
+    for (int i = threadIdx.x; i < cw * ch; i += blockDim.x) {
+        const int r = i / cw, c = i - r * cw;
+        roi[i] = img[(size_t)(cd.iniY + r) * pitch + cd.iniX + c];
+    }
+    __syncthreads();
+    const int tw = cw - 6, th = ch - 6;
+    const int npx = (tw > 0 && th > 0) ? tw * th : 0;
+    const int ti = min(max(P.ini_th, 0), 255), tm = min(max(P.min_th, 0), 255);
+    const int tlow = min(ti, tm);
+    const int per = (npx + blockDim.x - 1) / blockDim.x;
+    const int p0 = threadIdx.x * per, p1 = min(npx, p0 + per);
+    for (int i = p0; i < p1; i++) {
+        const int r = i / tw, c = i - r * tw;
+        meas[i] = (uint8_t)fast_measure(&roi[(r + 3) * cw + c + 3], cw, tlow);
+    }
+    __syncthreads();
+    // NMS at threshold t: corner iff M > t, score M-1; neighbours that are not corners at t
+    // (or lie outside the tested region) count as 0.
+    auto keep = [&](int i, int t) -> bool {
+        const int M = meas[i];
+        if (M <= t) return false;
+        const int s = M - 1;
+        const int r = i / tw, c = i - r * tw;
+#pragma unroll
+        for (int dr = -1; dr <= 1; dr++) {
+#pragma unroll
+            for (int dc = -1; dc <= 1; dc++) {
+                if (!dr && !dc) continue;
+                const int rr = r + dr, cc = c + dc;
+                if (rr < 0 || rr >= th || cc < 0 || cc >= tw) continue;
+                const int Mn = meas[rr * tw + cc];
+                const int sn = Mn > t ? Mn - 1 : 0;
+                if (!(s > sn)) return false;
+            }
+        }
+        return true;
+    };
+    int cnt = 0;
+    for (int i = p0; i < p1; i++) cnt += keep(i, ti);
+    int total = block_reduce_sum(cnt, scratch);
+    int t = ti;
+    if (total == 0) {
+        t = tm;
+        cnt = 0;
+        for (int i = p0; i < p1; i++) cnt += keep(i, tm);
+    }
+    int tot2;
+    const int incl = block_scan_incl(cnt, scratch, &tot2);
+    int w = incl - cnt;
+    uint32_t* slot = b.cell_keys + ((size_t)f * P.ncells + cd.slot) * P.slot_cap;
+    for (int i = p0; i < p1; i++) {
+        if (keep(i, t)) {
+            const int r = i / tw, c = i - r * tw;
+            slot[w++] = pack_kp(cd.iniX + 3 + c, cd.iniY + 3 + r, meas[i] - 1);
+        }
+    }
+    if (threadIdx.x == 0) b.cell_cnt[(size_t)f * P.ncells + cd.slot] = tot2;
+}
+
+// exclusive scan over n items (in chunks of blockDim.x) of per-item value fn(i);
+// out(i, excl) is called for every item; returns the total.
+template <class ValFn, class OutFn>
+__device__ int chunked_scan(int n, int* scratch, ValFn fn, OutFn out) {
+    int carry = 0;
+    for (int base = 0; base < n; base += blockDim.x) {
+        const int i = base + threadIdx.x;
+        const int v = i < n ? fn(i) : 0;
+        int tot;
+        const int incl = block_scan_incl(v, scratch, &tot);
+        if (i < n) out(i, carry + incl - v);
+        carry += tot;
+    }
+    __syncthreads();
+    return carry;
+}
+
+
+// ---------------------------------------------------------------------------------------
+// k_octree: DistributeOctTree (ORBextractor.cc:537-761) for one (level, frame) per
+// workgroup of 256 threads.
+//
+// The reference's std::list<ExtractorNode> is represented by the array of alive nodes in
+// list order.  A pass that splits the nodes of a set S in push order pi (children n1..n4
+// of each, empty ones dropped, pushed to the FRONT; parent erased) yields
+//     [children in reverse push order] ++ [unsplit nodes in their previous order],
+// i.e. two prefix sums.  Phase A (:592-671) splits every node holding >1 key in list
+// order; the careful phase (:671-736) splits candidates ordered by (size desc, sequence
+// desc) and stops at the first split that reaches N.  Children receive creation sequence
+// numbers in push order; sequence replaces the reference's heap-pointer tie-break (:682,
+// nondeterministic in the reference) — documented deviation, identical in the oracle.
+// Keys keep their original (cell-major) order; each node keeps its max-response key, the
+// first in original order on ties (:742-758).
+// ---------------------------------------------------------------------------------------
+struct NodeArr {
+    int16_t *x0, *x1, *y0, *y1;
+    int32_t *cnt, *seq;
+};
+
+__device__ __forceinline__ int quadrant_of(uint32_t key, const NodeArr& A, int nd) {
+    const int xm = A.x0[nd] + ((A.x1[nd] - A.x0[nd] + 1) >> 1);  // ceil((x1-x0)/2), :481
+    const int ym = A.y0[nd] + ((A.y1[nd] - A.y0[nd] + 1) >> 1);
+    const int x = kp_x(key), y = kp_y(key);
+    return (x < xm ? 0 : 1) + (y < ym ? 0 : 2);  // n1, n2, n3, n4 (:513-523)
+}
+
+__host__ __device__ inline size_t octree_node_bytes(int maxn) {
+    // A, B (2x(4*2 + 2*4) B), cc 16 B, cmap 8 B, ord/rnk/oarr 12 B, best 4 B per node
+    return (size_t)maxn * (32 + 16 + 8 + 12 + 4) + 16 * 16;
+}
+
+enum { kErrOctreeIters = 1, kErrOctreeNodes = 2, kErrCap = 4 };
+
+__global__ void __launch_bounds__(256) k_octree(Bufs b, int key_lds_cap) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ int scratch[20];
+    __shared__ int cell_off[256];
+    __shared__ int sh[8];
+    const DevPlan& P = *b.plan;
+    const int l = blockIdx.x, f = blockIdx.y;
+    const DevLevel& L = P.lv[l];
+    const int MAXN = P.max_nodes;
+    const int tid = threadIdx.x, NT = blockDim.x;
+    const int lane = tid & 63, wid = tid >> 6, nwv = NT >> 6;
+
+    uint8_t* p = smem;
+    auto carve = [&](size_t bytes) {
+        uint8_t* r = p;
+        p += (bytes + 15) & ~(size_t)15;
+        return r;
+    };
+    NodeArr A, B;
+    A.x0 = (int16_t*)carve(2 * MAXN); A.x1 = (int16_t*)carve(2 * MAXN);
+    A.y0 = (int16_t*)carve(2 * MAXN); A.y1 = (int16_t*)carve(2 * MAXN);
+    A.cnt = (int32_t*)carve(4 * MAXN); A.seq = (int32_t*)carve(4 * MAXN);
+    B.x0 = (int16_t*)carve(2 * MAXN); B.x1 = (int16_t*)carve(2 * MAXN);
+    B.y0 = (int16_t*)carve(2 * MAXN); B.y1 = (int16_t*)carve(2 * MAXN);
+    B.cnt = (int32_t*)carve(4 * MAXN); B.seq = (int32_t*)carve(4 * MAXN);
+    int32_t* cc = (int32_t*)carve(16 * MAXN);   // child key counts [node][4]
+    int16_t* cmap = (int16_t*)carve(8 * MAXN);  // new position of child [node][4]
+    int32_t* ord = (int32_t*)carve(4 * MAXN);   // split nodes in push order
+    int32_t* rnk = (int32_t*)carve(4 * MAXN);   // push index of a node, -1 = not split
+    int32_t* oarr = (int32_t*)carve(4 * MAXN);  // child offset of a split node (by push idx)
+    uint32_t* best = (uint32_t*)carve(4 * MAXN);
+    uint32_t* keys_l = (uint32_t*)carve(4 * (size_t)key_lds_cap);
+    uint16_t* knode_l = (uint16_t*)carve(2 * (size_t)key_lds_cap);
+
+    // ---- gather the level's candidates in cell order, relative to (minBX, minBY)
+    const int cb = L.cell_begin, ncl = L.cell_end - L.cell_begin;
+    const int32_t* ccount = b.cell_cnt + (size_t)f * P.ncells;
+    int nk = 0;
+    for (int base = 0; base < ncl; base += NT) {
+        const int i = base + tid;
+        const int v = i < ncl ? ccount[cb + i] : 0;
+        int tot;
+        const int incl = block_scan_incl(v, scratch, &tot);
+        cell_off[tid] = nk + incl - v;
+        nk += tot;
+    }
+    const bool in_lds = nk <= key_lds_cap;
+    uint32_t* keys = in_lds ? keys_l : b.keys_g + (size_t)f * P.key_slots + L.key_base;
+    uint16_t* knode = in_lds ? knode_l : b.knode_g + (size_t)f * P.key_slots + L.key_base;
+    {
+        int carry = 0;
+        for (int base = 0; base < ncl; base += NT) {
+            const int i = base + tid;
+            const int v = i < ncl ? ccount[cb + i] : 0;
+            int tot;
+            const int incl = block_scan_incl(v, scratch, &tot);
+            cell_off[tid] = carry + incl - v;
+            carry += tot;
+            __syncthreads();
+            const int nc = min(NT, ncl - base);
+            for (int c = wid; c < nc; c += nwv) {
+                const int cell = cb + base + c;
+                const int n = ccount[cell];
+                const uint32_t* src = b.cell_keys + ((size_t)f * P.ncells + cell) * P.slot_cap;
+                uint32_t* dst = keys + cell_off[c];
+                for (int j = lane; j < n; j += 64) {
+                    const uint32_t k = src[j];
+                    dst[j] = pack_kp(kp_x(k) - L.minBX, kp_y(k) - L.minBY, kp_s(k));
+                }
+            }
+            __syncthreads();
+        }
+    }
+    const int N = L.nfeat;
+    int32_t* out_cnt = b.ocnt + (size_t)f * P.nlevels + l;
+    uint32_t* okp = b.okp + (size_t)f * P.kslots + L.kbase;
+    if (nk == 0) {
+        if (tid == 0) *out_cnt = 0;
+        return;
+    }
+
+    // ---- roots (:541-583): key -> root (int)(x / hX); empty roots erased
+    if (tid < L.nIni) cc[tid] = 0;
+    __syncthreads();
+    for (int k = tid; k < nk; k += NT) {
+        const int x = kp_x(keys[k]);
+        int r = 0;
+        for (int i = 1; i < L.nIni; i++) r += x >= L.root_first_x[i];
+        knode[k] = (uint16_t)r;
+        atomicAdd(&cc[r], 1);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int n = 0;
+        for (int i = 0; i < L.nIni; i++) {
+            if (cc[i] > 0) {
+                A.x0[n] = (int16_t)L.root_x0[i];
+                A.x1[n] = (int16_t)L.root_x1[i];
+                A.y0[n] = 0;
+                A.y1[n] = (int16_t)(L.maxBY - L.minBY);
+                A.cnt[n] = cc[i];
+                A.seq[n] = i;
+                cmap[i] = (int16_t)n;
+                n++;
+            }
+        }
+        sh[0] = n;
+    }
+    __syncthreads();
+    for (int k = tid; k < nk; k += NT) knode[k] = (uint16_t)cmap[knode[k]];
+    int n = sh[0];
+    int seq_next = L.nIni;
+    int tprev = 0;        // children region [0, tprev) of the last pass
+    bool careful = false;
+    bool finish = false;
+    int err = 0;
+    __syncthreads();
+
+    for (int iter = 0; !finish; iter++) {
+        if (iter >= 512) { err |= kErrOctreeIters; break; }
+        const int prev = n;
+        // -- candidate set and quadrant counts
+        for (int i = tid; i < 4 * n; i += NT) cc[i] = 0;
+        for (int i = tid; i < n; i += NT) rnk[i] = -1;
+        __syncthreads();
+        auto is_cand = [&](int nd) -> bool {
+            return careful ? (nd < tprev && A.cnt[nd] > 1) : (A.cnt[nd] > 1);
+        };
+        for (int k = tid; k < nk; k += NT) {
+            const int nd = knode[k];
+            if (is_cand(nd)) atomicAdd(&cc[nd * 4 + quadrant_of(keys[k], A, nd)], 1);
+        }
+        __syncthreads();
+        auto nonempty = [&](int nd) -> int {
+            return (cc[nd * 4] > 0) + (cc[nd * 4 + 1] > 0) + (cc[nd * 4 + 2] > 0) + (cc[nd * 4 + 3] > 0);
+        };
+        int nsplit;
+        if (!careful) {
+            // phase A: split every node with >1 key, push order = list order
+            nsplit = chunked_scan(n, scratch, [&](int i) { return is_cand(i) ? 1 : 0; },
+                                  [&](int i, int ex) {
+                                      if (is_cand(i)) { rnk[i] = ex; ord[ex] = i; }
+                                  });
+        } else {
+            // careful phase: E = children of the last pass with >1 key; order by
+            // (size desc, sequence desc) = (cnt desc, position asc) inside [0, tprev)
+            for (int i = tid; i < tprev; i += NT) {
+                if (A.cnt[i] > 1) {
+                    const int ci = A.cnt[i];
+                    int r = 0;
+                    for (int j = 0; j < tprev; j++) {
+                        const int cj = A.cnt[j];
+                        r += (cj > 1) && (cj > ci || (cj == ci && j < i));
+                    }
+                    ord[r] = i;
+                }
+            }
+            __syncthreads();
+            int ne = chunked_scan(tprev, scratch, [&](int i) { return A.cnt[i] > 1 ? 1 : 0; },
+                                  [&](int, int) {});
+            // cut: first rank r with n + sum_{r'<=r}(nonempty-1) >= N (:728-729)
+            if (tid == 0) sh[1] = ne;
+            __syncthreads();
+            chunked_scan(ne, scratch, [&](int r) { return nonempty(ord[r]) - 1; },
+                         [&](int r, int ex) {
+                             const int incl = ex + nonempty(ord[r]) - 1;
+                             oarr[r] = (n + incl >= N) ? 1 : 0;
+                         });
+            // first r with flag
+            int firstcut = ne - 1;
+            {
+                int mine = 0x7fffffff;
+                for (int r = tid; r < ne; r += NT) if (oarr[r]) { mine = r; break; }
+                // block min
+                __syncthreads();
+                if (tid == 0) sh[2] = 0x7fffffff;
+                __syncthreads();
+                atomicMin(&sh[2], mine);
+                __syncthreads();
+                if (sh[2] != 0x7fffffff) firstcut = sh[2];
+            }
+            nsplit = firstcut + 1;
+            for (int r = tid; r < nsplit; r += NT) rnk[ord[r]] = r;
+            __syncthreads();
+        }
+        __syncthreads();
+        // -- children offsets in push order
+        const int T = chunked_scan(nsplit, scratch, [&](int r) { return nonempty(ord[r]); },
+                                   [&](int r, int ex) { oarr[r] = ex; });
+        if (T + (n - nsplit) > MAXN) { err |= kErrOctreeNodes; break; }
+        // -- write the new list into B
+        int nexp_local = 0;
+        const int U = chunked_scan(n, scratch, [&](int i) { return rnk[i] < 0 ? 1 : 0; },
+            [&](int i, int ex) {
+                const int r = rnk[i];
+                if (r < 0) {
+                    const int pos = T + ex;
+                    B.x0[pos] = A.x0[i]; B.x1[pos] = A.x1[i];
+                    B.y0[pos] = A.y0[i]; B.y1[pos] = A.y1[i];
+                    B.cnt[pos] = A.cnt[i]; B.seq[pos] = A.seq[i];
+                    cmap[i * 4] = (int16_t)pos;
+                } else {
+                    const int o = oarr[r];
+                    const int x0 = A.x0[i], x1 = A.x1[i], y0 = A.y0[i], y1 = A.y1[i];
+                    const int xm = x0 + ((x1 - x0 + 1) >> 1), ym = y0 + ((y1 - y0 + 1) >> 1);
+                    int kk = 0;
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        const int c = cc[i * 4 + q];
+                        if (c > 0) {
+                            const int pos = T - 1 - (o + kk);
+                            B.x0[pos] = (int16_t)((q & 1) ? xm : x0);
+                            B.x1[pos] = (int16_t)((q & 1) ? x1 : xm);
+                            B.y0[pos] = (int16_t)((q & 2) ? ym : y0);
+                            B.y1[pos] = (int16_t)((q & 2) ? y1 : ym);
+                            B.cnt[pos] = c;
+                            B.seq[pos] = seq_next + o + kk;
+                            cmap[i * 4 + q] = (int16_t)pos;
+                            nexp_local += c > 1;
+                            kk++;
+                        }
+                    }
+                }
+            });
+        const int n_to_expand = block_reduce_sum(nexp_local, scratch);
+        // -- remap keys
+        for (int k = tid; k < nk; k += NT) {
+            const int nd = knode[k];
+            const int q = rnk[nd] >= 0 ? quadrant_of(keys[k], A, nd) : 0;
+            knode[k] = (uint16_t)cmap[nd * 4 + q];
+        }
+        __syncthreads();
+        // swap A <-> B
+        { NodeArr t = A; A = B; B = t; }
+        n = T + U;
+        seq_next += T;
+        tprev = T;
+        if (!careful) {
+            if (n >= N || n == prev) finish = true;               // :667-670
+            else if (n + n_to_expand * 3 > N) careful = true;      // :671
+        } else {
+            if (n >= N || n == prev) finish = true;               // :732-733
+        }
+        __syncthreads();
+    }
+
+    // ---- retain the best key of each node (:740-758)
+    for (int i = tid; i < n; i += NT) best[i] = 0;
+    __syncthreads();
+    for (int k = tid; k < nk; k += NT) {
+        const uint32_t key = keys[k];
+        atomicMax(&best[knode[k]], ((uint32_t)kp_s(key) << 24) | (uint32_t)(0xFFFFFF - k));
+    }
+    __syncthreads();
+    const int nout = min(n, L.kcap);
+    for (int i = tid; i < nout; i += NT) {
+        const int k = 0xFFFFFF - (int)(best[i] & 0xFFFFFF);
+        const uint32_t key = keys[k];
+        okp[i] = pack_kp(kp_x(key) + L.minBX, kp_y(key) + L.minBY, kp_s(key));
+    }
+    if (n > L.kcap) err |= kErrOctreeNodes;
+    if (tid == 0) {
+        *out_cnt = nout;
+        if (err) atomicOr(&b.err[f], err);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// k_layout: output order of operator() (ORBextractor.cc:1100-1146), one workgroup per
+// frame.  Keypoints are visited level-major in octree order; those whose scaled x lies in
+// [lap0, lap1] are written from the back, the rest from the front; returns monoIndex.
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_layout(Bufs b) {
+    __shared__ int scratch[20];
+    const DevPlan& P = *b.plan;
+    const int f = blockIdx.x, tid = threadIdx.x, NT = blockDim.x;
+    const int32_t* ocnt = b.ocnt + (size_t)f * P.nlevels;
+    int total = 0;
+    for (int l = 0; l < P.nlevels; l++) total += ocnt[l];
+    const float lap0 = (float)b.lap0, lap1 = (float)b.lap1;
+    int mono_carry = 0, stereo_carry = 0;
+    for (int l = 0; l < P.nlevels; l++) {
+        const DevLevel& L = P.lv[l];
+        const int n = ocnt[l];
+        const uint32_t* okp = b.okp + (size_t)f * P.kslots + L.kbase;
+        int32_t* oidx = b.oidx + (size_t)f * P.kslots + L.kbase;
+        for (int base = 0; base < n; base += NT) {
+            const int i = base + tid;
+            bool lap = false;
+            if (i < n) {
+                float x = (float)kp_x(okp[i]);
+                if (l != 0) x = x * L.scale;  // keypoint->pt *= scale (:1131-1133)
+                lap = x >= lap0 && x <= lap1;
+            }
+            int tot;
+            const int incl = block_scan_incl(lap ? 1 : 0, scratch, &tot);
+            if (i < n) {
+                const int ls = stereo_carry + incl - 1;          // laps before me (incl. me) - 1
+                const int lm = mono_carry + (i - base + 1) - incl;  // monos before me (incl. me)
+                oidx[i] = lap ? (total - 1 - ls) : (lm - 1);
+            }
+            stereo_carry += tot;
+            mono_carry += min(NT, n - base) - tot;
+        }
+    }
+    if (tid == 0) {
+        b.out_n[f] = total;
+        b.out_mono[f] = mono_carry;
+        if (total > b.cap) atomicOr(&b.err[f], kErrCap);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// k_blur: GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101) of every level (OpenCV 4.2.0
+// fixed-point 8U path: Q8 taps [18,34,48,56,48,34,18], exact u16 row sums, Q16 column sums
+// rounded >> 16).  Tile 64 x 32 output pixels per 256-thread workgroup.
+// ---------------------------------------------------------------------------------------
+constexpr int kBlurTW = 64, kBlurTH = 32;
+
+__device__ __forceinline__ int refl101(int i, int n) {
+    if (i < 0) i = -i;
+    if (i >= n) i = 2 * n - 2 - i;
+    return i;
+}
+
+__global__ void __launch_bounds__(256) k_blur(Bufs b, int l, int ed) {
+    __shared__ uint8_t src[(kBlurTH + 6) * (kBlurTW + 8)];
+    __shared__ uint16_t hs[(kBlurTH + 6) * kBlurTW];
+    const DevPlan& P = *b.plan;
+    const DevLevel& L = P.lv[l];
+    const int f = blockIdx.z;
+    const int x0 = blockIdx.x * kBlurTW, y0 = blockIdx.y * kBlurTH;
+    const uint8_t* img = level_ptr(b, P, f, l);
+    const int pitch = level_pitch(P, l);
+    const int k0 = 18, k1 = 34, k2 = ed ? 48 : 49, k3 = ed ? 56 : 55;
+    const int SW = kBlurTW + 6, SH = kBlurTH + 6;
+    for (int i = threadIdx.x; i < SW * SH; i += blockDim.x) {
+        const int r = i / SW, c = i - r * SW;
+        const int yy = refl101(min(y0 + r - 3, L.h - 1 + 3), L.h);
+        const int xx = refl101(min(x0 + c - 3, L.w - 1 + 3), L.w);
+        src[r * (kBlurTW + 8) + c] = img[(size_t)yy * pitch + xx];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kBlurTW * SH; i += blockDim.x) {
+        const int r = i / kBlurTW, c = i - r * kBlurTW;
+        const uint8_t* s = &src[r * (kBlurTW + 8) + c];
+        hs[i] = (uint16_t)(k0 * (s[0] + s[6]) + k1 * (s[1] + s[5]) + k2 * (s[2] + s[4]) + k3 * s[3]);
+    }
+    __syncthreads();
+    uint8_t* dst = b.blur + (size_t)f * P.blur_frame + L.blur_off;
+    for (int i = threadIdx.x; i < kBlurTW * kBlurTH; i += blockDim.x) {
+        const int r = i / kBlurTW, c = i - r * kBlurTW;
+        const int y = y0 + r, x = x0 + c;
+        if (y >= L.h || x >= L.w) continue;
+        const uint16_t* h = &hs[r * kBlurTW + c];
+        const uint32_t acc = (uint32_t)k0 * (h[0] + h[6 * kBlurTW]) + (uint32_t)k1 * (h[kBlurTW] + h[5 * kBlurTW]) +
+                             (uint32_t)k2 * (h[2 * kBlurTW] + h[4 * kBlurTW]) + (uint32_t)k3 * h[3 * kBlurTW];
+        dst[(size_t)y * L.pitch + x] = (uint8_t)min((acc + (1u << 15)) >> 16, 255u);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// k_orb: one wave per keypoint.  IC_Angle (ORBextractor.cc:75-102) on the unblurred level:
+// lane v (0..30) sums row v-15 of the radius-15 disc; exact integer wave reduction; then
+// cv::fastAtan2.  rBRIEF (computeOrbDescriptor :106-145) on the blurred level: bit
+// i = lane + 64*w is the pattern pair i; one __ballot per 64 bits gives 8 descriptor bytes
+// (little-endian bit order = the reference's byte/bit order).
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_orb(Bufs b) {
+    const DevPlan& P = *b.plan;
+    const int f = blockIdx.y;
+    const int slot = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (slot >= P.kslots) return;
+    int l = 0;
+    while (l + 1 < P.nlevels && slot >= P.lv[l + 1].kbase) l++;
+    const DevLevel& L = P.lv[l];
+    const int i = slot - L.kbase;
+    if (i >= b.ocnt[(size_t)f * P.nlevels + l]) return;
+    const int oi = b.oidx[(size_t)f * P.kslots + slot];
+    if (oi >= b.cap) return;
+    const uint32_t key = b.okp[(size_t)f * P.kslots + slot];
+    const int kx = kp_x(key), ky = kp_y(key);
+
+    // --- orientation
+    const uint8_t* img = level_ptr(b, P, f, l);
+    const int pitch = level_pitch(P, l);
+    int m01 = 0, m10 = 0;
+    if (lane < 2 * kHalfPatch + 1) {
+        const int v = lane - kHalfPatch;
+        const int d = P.umax[v < 0 ? -v : v];
+        const uint8_t* row = img + (size_t)(ky + v) * pitch + kx;
+        int s0 = 0, s1 = 0;
+        for (int u = -d; u <= d; u++) {
+            const int val = row[u];
+            s0 += val;
+            s1 += u * val;
+        }
+        m10 = s1;
+        m01 = v * s0;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        m10 += __shfl_xor(m10, o, 64);
+        m01 += __shfl_xor(m01, o, 64);
+    }
+    const float angle = cv_fast_atan2((float)m01, (float)m10);
+
+    // --- descriptor
+    const float factor_pi = (float)(3.14159265358979323846 / 180.f);
+    float sn, cs;
+    glibc_sincosf(angle * factor_pi, &sn, &cs);
+    const float a = cs, bb = sn;
+    const uint8_t* bl = b.blur + (size_t)f * P.blur_frame + L.blur_off;
+    const uint8_t* center = bl + (size_t)ky * L.pitch + kx;
+    uint8_t* desc = b.out_desc + ((size_t)f * b.cap + oi) * 32;
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        const int bit = w * 64 + lane;
+        const float x0 = (float)c_pattern[4 * bit], y0 = (float)c_pattern[4 * bit + 1];
+        const float x1 = (float)c_pattern[4 * bit + 2], y1 = (float)c_pattern[4 * bit + 3];
+        const int r0 = cv_round(fmaf(x0, bb, y0 * a)), c0 = cv_round(fmaf(x0, a, -(y0 * bb)));
+        const int r1 = cv_round(fmaf(x1, bb, y1 * a)), c1 = cv_round(fmaf(x1, a, -(y1 * bb)));
+        const int t0 = center[r0 * L.pitch + c0];
+        const int t1 = center[r1 * L.pitch + c1];
+        const uint64_t m = __ballot(t0 < t1);
+        if (lane == 0) reinterpret_cast<uint64_t*>(desc)[w] = m;
+    }
+    if (lane == 0) {
+        slam_keypoint kp;
+        const float sx = l ? (float)kx * L.scale : (float)kx;
+        const float sy = l ? (float)ky * L.scale : (float)ky;
+        kp.x = sx;
+        kp.y = sy;
+        kp.size = L.size;
+        kp.angle = angle;
+        kp.response = (float)kp_s(key);
+        kp.octave = l;
+        kp.class_id = -1;
+        b.out_kps[(size_t)f * b.cap + oi] = kp;
+    }
+}
+
+}  // namespace slamhot
+
+// =======================================================================================
+// Host side: the slam_extractor handle and the C-ABI (include/slamhot.h).
+// =======================================================================================
+namespace slamhot {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    slam_status ensure(size_t need) {
+        if (need <= bytes) return SLAM_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        if (need == 0) return SLAM_OK;
+        if (hipMalloc(&p, need) != hipSuccess) return SLAM_ENOMEM;
+        bytes = need;
+        return SLAM_OK;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+constexpr int kOctreeKeyLdsCap = 6144;  // keys held in LDS per octree workgroup
+
+static size_t octree_lds_bytes(int maxn, int keycap) {
+    size_t s = 0;
+    auto add = [&](size_t b) { s += (b + 15) & ~(size_t)15; };
+    for (int i = 0; i < 2; i++) { add(2 * maxn); add(2 * maxn); add(2 * maxn); add(2 * maxn); add(4 * maxn); add(4 * maxn); }
+    add(16 * (size_t)maxn); add(8 * (size_t)maxn); add(4 * (size_t)maxn); add(4 * (size_t)maxn);
+    add(4 * (size_t)maxn); add(4 * (size_t)maxn);
+    add(4 * (size_t)keycap); add(2 * (size_t)keycap);
+    return s;
+}
+
+}  // namespace slamhot
+
+using namespace slamhot;
+
+struct slam_extractor {
+    slam_orb_params prm{};
+    int device = 0;
+    int max_w = 0, max_h = 0, max_batch = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    // geometry
+    bool have_plan = false;
+    Plan plan;
+    DevBuf d_plan, d_xtab, d_ytab, d_cells;
+    // per-batch buffers
+    DevBuf d_img, d_pyr, d_blur, d_cell_keys, d_cell_cnt, d_keys_g, d_knode_g, d_okp, d_ocnt,
+        d_oidx, d_err, d_kps, d_desc, d_n, d_mono;
+    int last_frames = 0;
+    const uint8_t* last_img = nullptr;  // level-0 pointer of the last run (for pyramid_level)
+    int key_lds_cap = kOctreeKeyLdsCap;
+    size_t octree_lds = 0;
+};
+
+static slam_status ensure_plan(slam_extractor* ex, int W, int H) {
+    if (ex->have_plan && ex->plan.W == W && ex->plan.H == H) return SLAM_OK;
+    Plan P;
+    if (!build_plan(ex->prm, W, H, P)) return SLAM_EINVAL;
+    DevPlan dp{};
+    dp.nlevels = P.nlevels;
+    dp.W = W;
+    dp.H = H;
+    dp.ncells = P.ncells;
+    dp.slot_cap = P.slot_cap;
+    dp.kslots = P.kslots;
+    dp.key_slots = P.key_slots;
+    dp.max_nodes = P.max_nodes;
+    dp.ini_th = ex->prm.ini_th_fast;
+    dp.min_th = ex->prm.min_th_fast;
+    dp.pyr_frame = P.pyr_frame;
+    dp.blur_frame = P.blur_frame;
+    {
+        // umax (ORBextractor.cc:452-467)
+        int umax[kHalfPatch + 1];
+        const int vmax = (int)std::floor(kHalfPatch * std::sqrt(2.f) / 2 + 1);
+        const int vmin = (int)std::ceil(kHalfPatch * std::sqrt(2.f) / 2);
+        const double hp2 = kHalfPatch * kHalfPatch;
+        for (int v = 0; v <= vmax; ++v) umax[v] = (int)std::lrint(std::sqrt(hp2 - v * v));
+        for (int v = kHalfPatch, v0 = 0; v >= vmin; --v) {
+            while (umax[v0] == umax[v0 + 1]) ++v0;
+            umax[v] = v0;
+            ++v0;
+        }
+        for (int v = 0; v <= kHalfPatch; v++) dp.umax[v] = umax[v];
+    }
+    for (int l = 0; l < P.nlevels; l++) {
+        const LevelPlan& L = P.lv[l];
+        DevLevel& D = dp.lv[l];
+        D.w = L.w; D.h = L.h; D.pitch = L.pitch;
+        D.pyr_off = L.pyr_off; D.blur_off = L.blur_off;
+        D.minBX = L.minBX; D.minBY = L.minBY; D.maxBX = L.maxBX; D.maxBY = L.maxBY;
+        D.cell_begin = L.cell_begin; D.cell_end = L.cell_end;
+        D.nfeat = L.nfeat; D.kbase = L.kbase; D.kcap = L.kcap;
+        D.key_base = L.key_base; D.key_cap = L.key_cap;
+        D.scale = L.scale; D.size = L.size; D.nIni = L.nIni;
+        for (int i = 0; i < kMaxRoots; i++) {
+            D.root_x0[i] = L.root_x0[i]; D.root_x1[i] = L.root_x1[i]; D.root_first_x[i] = L.root_first_x[i];
+        }
+        D.xtab_off = L.xtab_off; D.ytab_off = L.ytab_off; D.xmax = L.xmax;
+    }
+    slam_status st;
+    if ((st = ex->d_plan.ensure(sizeof(DevPlan))) ||
+        (st = ex->d_xtab.ensure(std::max<size_t>(16, P.xtab.size() * sizeof(ResizeX)))) ||
+        (st = ex->d_ytab.ensure(std::max<size_t>(16, P.ytab.size() * sizeof(ResizeY)))) ||
+        (st = ex->d_cells.ensure(P.cells.size() * sizeof(CellDesc))))
+        return st;
+    SLAM_HIP_TRY(hipMemcpy(ex->d_plan.p, &dp, sizeof(DevPlan), hipMemcpyHostToDevice));
+    if (!P.xtab.empty())
+        SLAM_HIP_TRY(hipMemcpy(ex->d_xtab.p, P.xtab.data(), P.xtab.size() * sizeof(ResizeX), hipMemcpyHostToDevice));
+    if (!P.ytab.empty())
+        SLAM_HIP_TRY(hipMemcpy(ex->d_ytab.p, P.ytab.data(), P.ytab.size() * sizeof(ResizeY), hipMemcpyHostToDevice));
+    SLAM_HIP_TRY(hipMemcpy(ex->d_cells.p, P.cells.data(), P.cells.size() * sizeof(CellDesc), hipMemcpyHostToDevice));
+    ex->plan = P;
+    ex->have_plan = true;
+    // keys stay in LDS behind the node arrays when they fit (else global scratch)
+    const size_t lds_max = 160 * 1024;
+    const size_t node_bytes = octree_lds_bytes(P.max_nodes, 0);
+    if (node_bytes > lds_max) return SLAM_EINVAL;
+    ex->key_lds_cap = (int)std::min<size_t>(kOctreeKeyLdsCap, (lds_max - node_bytes - 64) / 6);
+    ex->octree_lds = octree_lds_bytes(P.max_nodes, ex->key_lds_cap);
+    SLAM_HIP_TRY(hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)ex->octree_lds));
+    return SLAM_OK;
+}
+
+static slam_status ensure_batch(slam_extractor* ex, int nframes, int cap) {
+    const Plan& P = ex->plan;
+    const size_t F = (size_t)nframes;
+    slam_status st;
+    if ((st = ex->d_pyr.ensure(F * P.pyr_frame)) || (st = ex->d_blur.ensure(F * P.blur_frame)) ||
+        (st = ex->d_cell_keys.ensure(F * P.ncells * P.slot_cap * 4)) ||
+        (st = ex->d_cell_cnt.ensure(F * P.ncells * 4)) ||
+        (st = ex->d_keys_g.ensure(F * P.key_slots * 4)) ||
+        (st = ex->d_knode_g.ensure(F * P.key_slots * 2)) ||
+        (st = ex->d_okp.ensure(F * P.kslots * 4)) || (st = ex->d_ocnt.ensure(F * P.nlevels * 4)) ||
+        (st = ex->d_oidx.ensure(F * P.kslots * 4)) || (st = ex->d_err.ensure(F * 4)))
+        return st;
+    (void)cap;
+    return SLAM_OK;
+}
+
+static slam_status launch_pipeline(slam_extractor* ex, int nframes, const uint8_t* d_img, int lap0,
+                                   int lap1, slam_keypoint* d_kps, uint8_t* d_desc, int cap,
+                                   int32_t* d_n, int32_t* d_mono, hipStream_t s) {
+    const Plan& P = ex->plan;
+    Bufs b{};
+    b.img = d_img;
+    b.pyr = ex->d_pyr.as<uint8_t>();
+    b.blur = ex->d_blur.as<uint8_t>();
+    b.cell_keys = ex->d_cell_keys.as<uint32_t>();
+    b.cell_cnt = ex->d_cell_cnt.as<int32_t>();
+    b.keys_g = ex->d_keys_g.as<uint32_t>();
+    b.knode_g = ex->d_knode_g.as<uint16_t>();
+    b.okp = ex->d_okp.as<uint32_t>();
+    b.ocnt = ex->d_ocnt.as<int32_t>();
+    b.oidx = ex->d_oidx.as<int32_t>();
+    b.err = ex->d_err.as<int32_t>();
+    b.out_kps = d_kps;
+    b.out_desc = d_desc;
+    b.out_n = d_n;
+    b.out_mono = d_mono;
+    b.xtab = ex->d_xtab.as<ResizeX>();
+    b.ytab = ex->d_ytab.as<ResizeY>();
+    b.cells = ex->d_cells.as<CellDesc>();
+    b.plan = ex->d_plan.as<DevPlan>();
+    b.nframes = nframes;
+    b.cap = cap;
+    b.lap0 = lap0;
+    b.lap1 = lap1;
+    SLAM_HIP_TRY(hipMemsetAsync(b.err, 0, (size_t)nframes * 4, s));
+    for (int l = 1; l < P.nlevels; l++) {
+        dim3 grid((P.lv[l].w + 255) / 256, (P.lv[l].h + 3) / 4, nframes);
+        hipLaunchKernelGGL(k_resize, grid, dim3(64, 4), 0, s, b, l);
+    }
+    hipLaunchKernelGGL(k_fast_cells, dim3(P.ncells, nframes), dim3(256), 0, s, b);
+    hipLaunchKernelGGL(k_octree, dim3(P.nlevels, nframes), dim3(256), ex->octree_lds, s, b,
+                       ex->key_lds_cap);
+    hipLaunchKernelGGL(k_layout, dim3(nframes), dim3(256), 0, s, b);
+    for (int l = 0; l < P.nlevels; l++) {
+        dim3 grid((P.lv[l].w + kBlurTW - 1) / kBlurTW, (P.lv[l].h + kBlurTH - 1) / kBlurTH, nframes);
+        hipLaunchKernelGGL(k_blur, grid, dim3(256), 0, s, b, l, 1);
+    }
+    hipLaunchKernelGGL(k_orb, dim3((P.kslots + 3) / 4, nframes), dim3(256), 0, s, b);
+    SLAM_HIP_TRY(hipGetLastError());
+    ex->last_frames = nframes;
+    ex->last_img = d_img;
+    return SLAM_OK;
+}
+
+extern "C" {
+
+const char* slamhot_version(void) { return "slamhot 0.1 (gfx950)"; }
+
+const char* slamhot_status_string(slam_status s) {
+    switch (s) {
+        case SLAM_OK: return "ok";
+        case SLAM_EINVAL: return "invalid argument";
+        case SLAM_ENOMEM: return "out of memory";
+        case SLAM_EHIP: return "HIP runtime error";
+        case SLAM_ECAP: return "output capacity too small";
+        case SLAM_ENODEV: return "no gfx950 device";
+        case SLAM_EEMPTY: return "empty image";
+        default: return "unknown status";
+    }
+}
+
+slam_status slamhot_device_count(int* n) {
+    if (!n) return SLAM_EINVAL;
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+    *n = c;
+    return SLAM_OK;
+}
+
+slam_status slamhot_extractor_create(const slam_orb_params* params, int device, int max_width,
+                                     int max_height, int max_batch, slam_extractor** out) {
+    if (!params || !out || max_width <= 0 || max_height <= 0 || max_batch <= 0) return SLAM_EINVAL;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return SLAM_ENODEV;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return SLAM_ENODEV;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return SLAM_ENODEV;
+    Plan probe;
+    if (!build_plan(*params, max_width, max_height, probe)) return SLAM_EINVAL;
+    slam_extractor* ex = new slam_extractor();
+    ex->prm = *params;
+    ex->device = device;
+    ex->max_w = max_width;
+    ex->max_h = max_height;
+    ex->max_batch = max_batch;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ex->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ex;
+        return SLAM_EHIP;
+    }
+    *out = ex;
+    return SLAM_OK;
+}
+
+void slamhot_extractor_destroy(slam_extractor* ex) {
+    if (!ex) return;
+    (void)hipSetDevice(ex->device);
+    if (ex->stream) (void)hipStreamSynchronize(ex->stream);
+    DevBuf* bufs[] = {&ex->d_plan, &ex->d_xtab, &ex->d_ytab, &ex->d_cells, &ex->d_img, &ex->d_pyr,
+                      &ex->d_blur, &ex->d_cell_keys, &ex->d_cell_cnt, &ex->d_keys_g, &ex->d_knode_g,
+                      &ex->d_okp, &ex->d_ocnt, &ex->d_oidx, &ex->d_err, &ex->d_kps, &ex->d_desc,
+                      &ex->d_n, &ex->d_mono};
+    for (DevBuf* b : bufs) b->release();
+    if (ex->stream) (void)hipStreamDestroy(ex->stream);
+    delete ex;
+}
+
+slam_status slamhot_extractor_levels(const slam_extractor* ex, int* nlevels, float* scale,
+                                     float* inv_scale, float* sigma2, float* inv_sigma2,
+                                     int32_t* nfeatures_per_level) {
+    if (!ex) return SLAM_EINVAL;
+    Plan P;
+    build_scale_tables(ex->prm, P);
+    const int L = ex->prm.nlevels;
+    if (nlevels) *nlevels = L;
+    for (int l = 0; l < L; l++) {
+        if (scale) scale[l] = P.scale[l];
+        if (inv_scale) inv_scale[l] = P.inv_scale[l];
+        if (sigma2) sigma2[l] = P.sigma2[l];
+        if (inv_sigma2) inv_sigma2[l] = P.inv_sigma2[l];
+        if (nfeatures_per_level) nfeatures_per_level[l] = P.nfeat[l];
+    }
+    return SLAM_OK;
+}
+
+slam_status slamhot_extract_batch_device(slam_extractor* ex, int nframes, const void* d_imgs,
+                                         int width, int height, int lap0, int lap1, void* d_kps,
+                                         void* d_desc, int cap, void* d_n, void* d_mono_index,
+                                         void* hip_stream) {
+    if (!ex || nframes <= 0 || !d_imgs || !d_kps || !d_desc || !d_n || !d_mono_index || cap < 0)
+        return SLAM_EINVAL;
+    if (width > ex->max_w || height > ex->max_h || nframes > ex->max_batch) return SLAM_EINVAL;
+    std::lock_guard<std::mutex> g(ex->mu);
+    SLAM_HIP_TRY(hipSetDevice(ex->device));
+    slam_status st;
+    if ((st = ensure_plan(ex, width, height)) || (st = ensure_batch(ex, nframes, cap))) return st;
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : ex->stream;
+    return launch_pipeline(ex, nframes, (const uint8_t*)d_imgs, lap0, lap1, (slam_keypoint*)d_kps,
+                           (uint8_t*)d_desc, cap, (int32_t*)d_n, (int32_t*)d_mono_index, s);
+}
+
+slam_status slamhot_extract_batch(slam_extractor* ex, int nframes, const uint8_t* imgs, int width,
+                                  int height, size_t stride, int lap0, int lap1,
+                                  slam_keypoint* kps, uint8_t* desc, int cap, int* n,
+                                  int* mono_index) {
+    if (!ex || nframes <= 0 || !n || !mono_index || cap < 0 || (cap > 0 && (!kps || !desc)))
+        return SLAM_EINVAL;
+    if (!imgs || width <= 0 || height <= 0) return SLAM_EEMPTY;
+    if (stride < (size_t)width || width > ex->max_w || height > ex->max_h || nframes > ex->max_batch)
+        return SLAM_EINVAL;
+    std::lock_guard<std::mutex> g(ex->mu);
+    SLAM_HIP_TRY(hipSetDevice(ex->device));
+    slam_status st;
+    if ((st = ensure_plan(ex, width, height)) || (st = ensure_batch(ex, nframes, cap))) return st;
+    const size_t F = (size_t)nframes, fb = (size_t)width * height;
+    const int dcap = std::max(cap, 1);
+    if ((st = ex->d_img.ensure(F * fb)) || (st = ex->d_kps.ensure(F * dcap * sizeof(slam_keypoint))) ||
+        (st = ex->d_desc.ensure(F * dcap * 32)) || (st = ex->d_n.ensure(F * 4)) ||
+        (st = ex->d_mono.ensure(F * 4)))
+        return st;
+    hipStream_t s = ex->stream;
+    for (int f = 0; f < nframes; f++)
+        SLAM_HIP_TRY(hipMemcpy2DAsync(ex->d_img.as<uint8_t>() + f * fb, width, imgs + f * height * stride,
+                                      stride, width, height, hipMemcpyHostToDevice, s));
+    if ((st = launch_pipeline(ex, nframes, ex->d_img.as<uint8_t>(), lap0, lap1, ex->d_kps.as<slam_keypoint>(),
+                              ex->d_desc.as<uint8_t>(), cap, ex->d_n.as<int32_t>(), ex->d_mono.as<int32_t>(), s)))
+        return st;
+    std::vector<int32_t> err(nframes);
+    SLAM_HIP_TRY(hipMemcpyAsync(n, ex->d_n.p, F * 4, hipMemcpyDeviceToHost, s));
+    SLAM_HIP_TRY(hipMemcpyAsync(mono_index, ex->d_mono.p, F * 4, hipMemcpyDeviceToHost, s));
+    SLAM_HIP_TRY(hipMemcpyAsync(err.data(), ex->d_err.p, F * 4, hipMemcpyDeviceToHost, s));
+    if (cap > 0) {
+        SLAM_HIP_TRY(hipMemcpyAsync(kps, ex->d_kps.p, F * cap * sizeof(slam_keypoint), hipMemcpyDeviceToHost, s));
+        SLAM_HIP_TRY(hipMemcpyAsync(desc, ex->d_desc.p, F * cap * 32, hipMemcpyDeviceToHost, s));
+    }
+    SLAM_HIP_TRY(hipStreamSynchronize(s));
+    slam_status res = SLAM_OK;
+    for (int f = 0; f < nframes; f++) {
+        if (err[f] & ~kErrCap) {
+            std::fprintf(stderr, "slamhot: extractor internal error flags 0x%x on frame %d\n", err[f], f);
+            return SLAM_EINVAL;
+        }
+        if (n[f] > cap) res = SLAM_ECAP;
+    }
+    return res;
+}
+
+slam_status slamhot_extract(slam_extractor* ex, const uint8_t* img, int width, int height,
+                            size_t stride, int lap0, int lap1, slam_keypoint* kps, uint8_t* desc,
+                            int cap, int* n, int* mono_index) {
+    return slamhot_extract_batch(ex, 1, img, width, height, stride, lap0, lap1, kps, desc, cap, n,
+                                 mono_index);
+}
+
+slam_status slamhot_pyramid_level(slam_extractor* ex, int frame, int level, uint8_t* dst,
+                                  size_t dst_cap, int* width, int* height) {
+    if (!ex || !ex->have_plan || frame < 0 || frame >= ex->last_frames || level < 0 ||
+        level >= ex->plan.nlevels || !width || !height)
+        return SLAM_EINVAL;
+    std::lock_guard<std::mutex> g(ex->mu);
+    SLAM_HIP_TRY(hipSetDevice(ex->device));
+    const Plan& P = ex->plan;
+    const LevelPlan& L = P.lv[level];
+    *width = L.w;
+    *height = L.h;
+    if (!dst) return SLAM_OK;
+    if (dst_cap < (size_t)L.w * L.h) return SLAM_ECAP;
+    const uint8_t* src;
+    size_t spitch;
+    if (level == 0) {
+        src = ex->last_img + (size_t)frame * P.W * P.H;
+        spitch = P.W;
+    } else {
+        src = ex->d_pyr.as<uint8_t>() + (size_t)frame * P.pyr_frame + L.pyr_off;
+        spitch = L.pitch;
+    }
+    SLAM_HIP_TRY(hipMemcpy2DAsync(dst, L.w, src, spitch, L.w, L.h, hipMemcpyDeviceToHost, ex->stream));
+    SLAM_HIP_TRY(hipStreamSynchronize(ex->stream));
+    return SLAM_OK;
+}
+
+void* slamhot_extractor_stream(slam_extractor* ex) { return ex ? (void*)ex->stream : nullptr; }
+
+}  // extern "C"

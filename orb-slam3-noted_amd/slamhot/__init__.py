@@ -1,0 +1,180 @@
+"""Python host mirror of the ORB-SLAM3 hot path over the libslamhot C-ABI (include/slamhot.h).
+
+The classes mirror the reference's operator interface: ``ORBextractor(nfeatures, scaleFactor,
+nlevels, iniThFAST, minThFAST)`` with ``__call__(image, lapping) -> (keypoints, descriptors,
+monoIndex)`` and the ``Get*`` accessors (ORBextractor.h:49-83).  Compute always runs in the
+HIP library; there is no CPU fallback — a missing library or device raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+import numpy as np
+
+PKG_ROOT = Path(__file__).resolve().parents[1]
+LIB_PATH = PKG_ROOT / "lib" / "libslamhot.so"
+
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                     ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+
+SLAM_OK, SLAM_EINVAL, SLAM_ENOMEM, SLAM_EHIP, SLAM_ECAP, SLAM_ENODEV, SLAM_EEMPTY = 0, -1, -2, -3, -4, -5, -6
+
+
+class SlamError(RuntimeError):
+    def __init__(self, status: int, what: str):
+        super().__init__(f"{what}: {status_string(status)} ({status})")
+        self.status = status
+
+
+class OrbParams(C.Structure):
+    _fields_ = [("nfeatures", C.c_int32), ("scale_factor", C.c_float), ("nlevels", C.c_int32),
+                ("ini_th_fast", C.c_int32), ("min_th_fast", C.c_int32)]
+
+
+_lib = None
+P = C.c_void_p
+I = C.c_int
+
+
+def lib() -> C.CDLL:
+    """Load libslamhot.so (built in-tree by __graft_entry__.build()); raises if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise RuntimeError(f"libslamhot.so not built: {LIB_PATH} (run __graft_entry__.build())")
+    L = C.CDLL(str(LIB_PATH))
+    L.slamhot_version.restype = C.c_char_p
+    L.slamhot_status_string.argtypes = [I]
+    L.slamhot_status_string.restype = C.c_char_p
+    L.slamhot_device_count.argtypes = [C.POINTER(I)]
+    L.slamhot_extractor_create.argtypes = [C.POINTER(OrbParams), I, I, I, I, C.POINTER(P)]
+    L.slamhot_extractor_destroy.argtypes = [P]
+    L.slamhot_extractor_destroy.restype = None
+    L.slamhot_extractor_levels.argtypes = [P, C.POINTER(I), P, P, P, P, P]
+    L.slamhot_extract.argtypes = [P, P, I, I, C.c_size_t, I, I, P, P, I, C.POINTER(I), C.POINTER(I)]
+    L.slamhot_extract_batch.argtypes = [P, I, P, I, I, C.c_size_t, I, I, P, P, I, P, P]
+    L.slamhot_extract_batch_device.argtypes = [P, I, P, I, I, I, I, P, P, I, P, P, P]
+    L.slamhot_pyramid_level.argtypes = [P, I, I, P, C.c_size_t, C.POINTER(I), C.POINTER(I)]
+    L.slamhot_extractor_stream.argtypes = [P]
+    L.slamhot_extractor_stream.restype = P
+    _lib = L
+    return L
+
+
+def status_string(st: int) -> str:
+    return lib().slamhot_status_string(st).decode()
+
+
+def check(st: int, what: str) -> int:
+    if st < 0:
+        raise SlamError(st, what)
+    return st
+
+
+def device_count() -> int:
+    n = I(0)
+    check(lib().slamhot_device_count(C.byref(n)), "device_count")
+    return n.value
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(P)
+
+
+class ORBextractor:
+    """Mirror of ORB_SLAM3::ORBextractor (ORBextractor.h:44-110) on one gfx950 device."""
+
+    def __init__(self, nfeatures: int = 1000, scaleFactor: float = 1.2, nlevels: int = 8,
+                 iniThFAST: int = 20, minThFAST: int = 7, device: int = 0,
+                 max_size=(1280, 720), max_batch: int = 1):
+        self.params = OrbParams(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST)
+        self.nlevels = nlevels
+        self._h = P()
+        check(lib().slamhot_extractor_create(C.byref(self.params), device, max_size[0], max_size[1],
+                                             max_batch, C.byref(self._h)), "slamhot_extractor_create")
+        self.cap = nfeatures * 2 + 64
+
+    def close(self):
+        if self._h:
+            lib().slamhot_extractor_destroy(self._h)
+            self._h = P()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _levels(self):
+        L = self.nlevels
+        out = [np.zeros(L, np.float32) for _ in range(4)] + [np.zeros(L, np.int32)]
+        n = I(0)
+        check(lib().slamhot_extractor_levels(self._h, C.byref(n), *[_ptr(a) for a in out]), "levels")
+        return out
+
+    def GetLevels(self) -> int:
+        return self.nlevels
+
+    def GetScaleFactor(self) -> float:
+        return float(np.float32(self.params.scale_factor))
+
+    def GetScaleFactors(self):
+        return self._levels()[0]
+
+    def GetInverseScaleFactors(self):
+        return self._levels()[1]
+
+    def GetScaleSigmaSquares(self):
+        return self._levels()[2]
+
+    def GetInverseScaleSigmaSquares(self):
+        return self._levels()[3]
+
+    def GetFeaturesPerLevel(self):
+        return self._levels()[4]
+
+    def __call__(self, image: np.ndarray, vLappingArea=(0, 0)):
+        """operator()(image, mask, keypoints, descriptors, vLappingArea) -> monoIndex.
+
+        Returns (keypoints structured array in cv::KeyPoint layout, descriptors N x 32 u8,
+        monoIndex)."""
+        kps, desc, n, mono = self.extract_batch(image[None], vLappingArea)
+        return kps[0][: n[0]].copy(), desc[0][: n[0]].copy(), int(mono[0])
+
+    def extract_batch(self, images: np.ndarray, vLappingArea=(0, 0)):
+        images = np.ascontiguousarray(images, dtype=np.uint8)
+        nf, h, w = images.shape
+        cap = self.cap
+        kps = np.zeros((nf, cap), KP_DTYPE)
+        desc = np.zeros((nf, cap, 32), np.uint8)
+        n = np.zeros(nf, np.int32)
+        mono = np.zeros(nf, np.int32)
+        st = lib().slamhot_extract_batch(self._h, nf, _ptr(images), w, h, w, int(vLappingArea[0]),
+                                         int(vLappingArea[1]), _ptr(kps), _ptr(desc), cap, _ptr(n), _ptr(mono))
+        check(st, "slamhot_extract_batch")
+        return kps, desc, n, mono
+
+    def pyramid_level(self, level: int, frame: int = 0) -> np.ndarray:
+        w, h = I(0), I(0)
+        check(lib().slamhot_pyramid_level(self._h, frame, level, None, 0, C.byref(w), C.byref(h)), "pyramid")
+        out = np.zeros((h.value, w.value), np.uint8)
+        check(lib().slamhot_pyramid_level(self._h, frame, level, _ptr(out), out.size, C.byref(w), C.byref(h)),
+              "pyramid")
+        return out
+
+    @property
+    def mvImagePyramid(self):
+        return [self.pyramid_level(l) for l in range(self.nlevels)]
+
+    def extract_batch_device(self, d_imgs: int, nframes: int, width: int, height: int, d_kps: int, d_desc: int,
+                             cap: int, d_n: int, d_mono: int, lap=(0, 0), stream: int | None = None):
+        """Device-resident batch: all pointers are device addresses (ints)."""
+        st = lib().slamhot_extract_batch_device(self._h, nframes, P(d_imgs), width, height, int(lap[0]), int(lap[1]),
+                                                P(d_kps), P(d_desc), cap, P(d_n), P(d_mono),
+                                                P(stream) if stream else None)
+        check(st, "slamhot_extract_batch_device")
+
+    def stream(self) -> int:
+        return lib().slamhot_extractor_stream(self._h) or 0

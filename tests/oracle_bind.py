@@ -1,0 +1,166 @@
+"""ctypes binding of oracle/build/liboracle.so — the CPU checker (test infrastructure)."""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+LIB_PATH = ROOT / "oracle" / "build" / "liboracle.so"
+
+
+class KeyPoint(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("size", C.c_float), ("angle", C.c_float),
+                ("response", C.c_float), ("octave", C.c_int32), ("class_id", C.c_int32)]
+
+
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                     ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+
+
+class OrbParams(C.Structure):
+    _fields_ = [("nfeatures", C.c_int32), ("scale_factor", C.c_float), ("nlevels", C.c_int32),
+                ("ini_th_fast", C.c_int32), ("min_th_fast", C.c_int32)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise RuntimeError(f"oracle library missing: {LIB_PATH} (run __graft_entry__.build())")
+        L = C.CDLL(str(LIB_PATH))
+        P = C.c_void_p
+        L.oracle_extract.argtypes = [C.POINTER(OrbParams), P, C.c_int, C.c_int, C.c_size_t, C.c_int,
+                                     C.c_int, P, P, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        L.oracle_extract.restype = C.c_int
+        L.oracle_levels.argtypes = [C.POINTER(OrbParams), P, P, P, P, P]
+        L.oracle_pyramid.argtypes = [C.POINTER(OrbParams), P, C.c_int, C.c_int, C.c_size_t, P,
+                                     C.c_size_t, P, P, P]
+        L.oracle_pyramid.restype = C.c_int
+        L.oracle_resize_linear.argtypes = [P, C.c_int, C.c_int, C.c_size_t, P, C.c_int, C.c_int, C.c_size_t]
+        L.oracle_fast.argtypes = [P, C.c_int, C.c_int, C.c_size_t, C.c_int, P, C.c_int]
+        L.oracle_fast.restype = C.c_int
+        L.oracle_gaussian_blur7.argtypes = [P, C.c_int, C.c_int, C.c_size_t, P, C.c_size_t, C.c_int]
+        L.oracle_fast_atan2.argtypes = [C.c_float, C.c_float]
+        L.oracle_fast_atan2.restype = C.c_float
+        L.oracle_sincosf.argtypes = [C.c_float, C.POINTER(C.c_float), C.POINTER(C.c_float)]
+        L.oracle_keypoints_octree.argtypes = [C.POINTER(OrbParams), P, C.c_int, C.c_int, C.c_size_t, P,
+                                              C.c_int, P]
+        L.oracle_keypoints_octree.restype = C.c_int
+        L.oracle_descriptor_distance.argtypes = [P, P]
+        L.oracle_descriptor_distance.restype = C.c_int
+        L.oracle_extract_many.argtypes = [C.POINTER(OrbParams), C.c_int, P, C.c_int, C.c_int, C.c_size_t,
+                                          C.c_int, C.c_int, C.c_int]
+        L.oracle_extract_many.restype = C.c_long
+        _lib = L
+    return _lib
+
+
+def params(nfeatures=1000, scale=1.2, nlevels=8, ini=20, mn=7) -> OrbParams:
+    return OrbParams(nfeatures, scale, nlevels, ini, mn)
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def extract(img: np.ndarray, p: OrbParams | None = None, lap=(0, 0)):
+    p = p or params()
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    cap = p.nfeatures * 2 + 64
+    kps = np.zeros(cap, KP_DTYPE)
+    desc = np.zeros((cap, 32), np.uint8)
+    n, mono = C.c_int(0), C.c_int(0)
+    st = lib().oracle_extract(C.byref(p), _ptr(img), w, h, w, lap[0], lap[1], _ptr(kps), _ptr(desc), cap,
+                              C.byref(n), C.byref(mono))
+    if st != 0:
+        raise RuntimeError(f"oracle_extract status {st}")
+    return kps[:n.value].copy(), desc[:n.value].copy(), mono.value
+
+
+def levels(p: OrbParams | None = None):
+    p = p or params()
+    L = p.nlevels
+    arrs = [np.zeros(L, np.float32) for _ in range(4)] + [np.zeros(L, np.int32)]
+    lib().oracle_levels(C.byref(p), *[_ptr(a) for a in arrs])
+    return arrs
+
+
+def pyramid(img: np.ndarray, p: OrbParams | None = None):
+    p = p or params()
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    cap = w * h * 4
+    out = np.zeros(cap, np.uint8)
+    lw = np.zeros(p.nlevels, np.int32)
+    lh = np.zeros(p.nlevels, np.int32)
+    off = np.zeros(p.nlevels, np.uint64)
+    st = lib().oracle_pyramid(C.byref(p), _ptr(img), w, h, w, _ptr(out), cap, _ptr(lw), _ptr(lh), _ptr(off))
+    assert st == 0
+    return [out[int(off[l]): int(off[l]) + lw[l] * lh[l]].reshape(lh[l], lw[l]).copy() for l in range(p.nlevels)]
+
+
+def resize_linear(src: np.ndarray, dw: int, dh: int) -> np.ndarray:
+    src = np.ascontiguousarray(src, dtype=np.uint8)
+    sh, sw = src.shape
+    dst = np.zeros((dh, dw), np.uint8)
+    lib().oracle_resize_linear(_ptr(src), sw, sh, sw, _ptr(dst), dw, dh, dw)
+    return dst
+
+
+def fast(roi: np.ndarray, threshold: int) -> np.ndarray:
+    roi = np.ascontiguousarray(roi, dtype=np.uint8)
+    h, w = roi.shape
+    cap = w * h
+    out = np.zeros((cap, 3), np.int32)
+    n = lib().oracle_fast(_ptr(roi), w, h, w, threshold, _ptr(out), cap)
+    assert n >= 0
+    return out[:n].copy()
+
+
+def gaussian_blur7(img: np.ndarray, ed: bool = True) -> np.ndarray:
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    out = np.zeros_like(img)
+    lib().oracle_gaussian_blur7(_ptr(img), w, h, w, _ptr(out), w, 1 if ed else 0)
+    return out
+
+
+def fast_atan2(y: float, x: float) -> float:
+    return lib().oracle_fast_atan2(y, x)
+
+
+def sincosf(x: float):
+    s, c = C.c_float(), C.c_float()
+    lib().oracle_sincosf(x, C.byref(s), C.byref(c))
+    return s.value, c.value
+
+
+def keypoints_octree(img: np.ndarray, p: OrbParams | None = None):
+    p = p or params()
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    cap = p.nfeatures * 2 + 64
+    kps = np.zeros(cap, KP_DTYPE)
+    counts = np.zeros(p.nlevels, np.int32)
+    n = lib().oracle_keypoints_octree(C.byref(p), _ptr(img), w, h, w, _ptr(kps), cap, _ptr(counts))
+    assert n >= 0
+    return kps[:n].copy(), counts
+
+
+def descriptor_distance(a: np.ndarray, b: np.ndarray) -> int:
+    a = np.ascontiguousarray(a, dtype=np.uint8)
+    b = np.ascontiguousarray(b, dtype=np.uint8)
+    return lib().oracle_descriptor_distance(_ptr(a), _ptr(b))
+
+
+def extract_many(imgs: np.ndarray, p: OrbParams | None = None, lap=(0, 0), nthreads=1) -> int:
+    p = p or params()
+    imgs = np.ascontiguousarray(imgs, dtype=np.uint8)
+    n, h, w = imgs.shape
+    return lib().oracle_extract_many(C.byref(p), n, _ptr(imgs), w, h, w, lap[0], lap[1], nthreads)

@@ -1,0 +1,87 @@
+"""GPU parity: libslamhot extractor vs the CPU oracle (ORBextractor.cc restated).
+
+Bit-exact: pyramid pixels, keypoint order/coords/size/angle/response/octave, descriptor bits.
+"""
+import numpy as np
+import pytest
+
+import oracle_bind as ob
+from slamhot import synth
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [(640, 480), (752, 480), (1280, 720)]
+
+
+def _compare(kg, dg, mg, ko, do, mo):
+    assert len(kg) == len(ko), (len(kg), len(ko))
+    assert mg == mo
+    for f in ("x", "y", "size", "response", "octave", "class_id"):
+        bad = np.nonzero(kg[f] != ko[f])[0]
+        assert bad.size == 0, (f, bad[:10], kg[bad[:3]], ko[bad[:3]])
+    bad = np.nonzero(kg["angle"].view(np.uint32) != ko["angle"].view(np.uint32))[0]
+    assert bad.size == 0, ("angle", bad[:10], kg[bad[:3]], ko[bad[:3]])
+    bad = np.nonzero((dg != do).any(axis=1))[0]
+    assert bad.size == 0, ("desc", bad[:10])
+
+
+@pytest.mark.parametrize("size", SIZES)
+def test_pyramid_bitexact(gpu_extractor_factory, size):
+    w, h = size
+    ex = gpu_extractor_factory(nfeatures=1000, max_size=size)
+    img = synth.frame(7, w, h)
+    ex(img)
+    ref = ob.pyramid(img)
+    for l in range(8):
+        got = ex.pyramid_level(l)
+        assert got.shape == ref[l].shape
+        assert np.array_equal(got, ref[l]), (l, np.argwhere(got != ref[l])[:5])
+
+
+@pytest.mark.parametrize("size", SIZES)
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_extract_bitexact(gpu_extractor_factory, size, seed):
+    w, h = size
+    nf = 1200 if size == (752, 480) else 1000
+    ex = gpu_extractor_factory(nfeatures=nf, max_size=size)
+    img = synth.frame(100 + seed, w, h)
+    kg, dg, mg = ex(img)
+    ko, do, mo = ob.extract(img, ob.params(nfeatures=nf))
+    _compare(kg, dg, mg, ko, do, mo)
+
+
+@pytest.mark.parametrize("lap", [(0, 0), (0, 1000), (100, 400)])
+def test_lapping_order(gpu_extractor_factory, lap):
+    ex = gpu_extractor_factory(nfeatures=1000, max_size=(640, 480))
+    img = synth.frame(5)
+    kg, dg, mg = ex(img, lap)
+    ko, do, mo = ob.extract(img, ob.params(), lap=lap)
+    _compare(kg, dg, mg, ko, do, mo)
+
+
+def test_batch_matches_single(gpu_extractor_factory):
+    ex = gpu_extractor_factory(nfeatures=1000, max_size=(640, 480), max_batch=8)
+    imgs = synth.frames(range(20, 28))
+    kps, desc, n, mono = ex.extract_batch(imgs)
+    for f in range(8):
+        ko, do, mo = ob.extract(imgs[f])
+        _compare(kps[f][: n[f]], desc[f][: n[f]], mono[f], ko, do, mo)
+
+
+@pytest.mark.parametrize("nf", [500, 2000, 5000])
+def test_feature_budgets(gpu_extractor_factory, nf):
+    ex = gpu_extractor_factory(nfeatures=nf, max_size=(752, 480))
+    img = synth.frame(33, 752, 480)
+    kg, dg, mg = ex(img)
+    ko, do, mo = ob.extract(img, ob.params(nfeatures=nf))
+    _compare(kg, dg, mg, ko, do, mo)
+
+
+def test_flat_and_noise_images(gpu_extractor_factory):
+    ex = gpu_extractor_factory(nfeatures=1000, max_size=(640, 480))
+    rng = np.random.default_rng(3)
+    for img in (np.full((480, 640), 128, np.uint8),
+                rng.integers(0, 256, (480, 640), dtype=np.uint8)):
+        kg, dg, mg = ex(img)
+        ko, do, mo = ob.extract(img)
+        _compare(kg, dg, mg, ko, do, mo)
