@@ -1,0 +1,252 @@
+#!/usr/bin/env python3
+"""bench.py — MI355X throughput of the ORB-SLAM3 hot path (BASELINE.json configs).
+
+Headline (N=1 default): BASELINE.json configs[1] — synthetic 640x480, 8-level pyramid,
+1000 features/frame, ORBextractor only.  One step = one pass of the extractor over a batch
+of B synthetic frames already resident in HBM.  value = frames/s of the whole job.
+
+Multi-GPU: one process per GPU (torch.distributed.run); each rank extracts its own batch
+(frames are independent: weak scaling, no collective on the data path).  Timing is
+barrier + synchronize on both sides of exactly K steps; the max over ranks is reported.
+
+Also reported: the dominant kernel's roofline (HIP events around every stage during the
+timed steps), and the CPU baseline (the oracle restatement, rank 0 at N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "orb-slam3-noted_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def level_sizes(w, h, nlevels=8, scale=1.2):
+    """ComputePyramid level sizes (ORBextractor.cc:1157) in the reference's float arithmetic."""
+    sizes = []
+    s = [1.0]
+    for i in range(1, nlevels):
+        s.append(float(np.float32(np.float64(np.float32(s[-1])) * np.float64(np.float32(scale)))))
+    for l in range(nlevels):
+        inv = np.float32(1.0) / np.float32(s[l])
+        sizes.append((int(np.rint(np.float32(w) * inv)), int(np.rint(np.float32(h) * inv))))
+    return sizes
+
+
+def algorithmic_bytes(w, h, kps_per_frame):
+    """Per-frame algorithmic HBM bytes of each stage."""
+    sz = level_sizes(w, h)
+    P = [a * b for a, b in sz]
+    out = {
+        "k_resize": sum(P[:-1]) + sum(P[1:]),        # read level l-1, write level l
+        "k_fast_cells": sum(P),                       # read every level pixel once (+ candidates, small)
+        "k_octree": 0,                                # candidate lists only (KB, L2-resident)
+        "k_layout": 0,
+        "k_blur": 2 * sum(P),                         # read + write every level
+        "k_orb": kps_per_frame * (4 + 28 + 32),       # kp in, kp + descriptor out
+    }
+    pipeline = P[0] + sum(P[1:]) + sum(P) + kps_per_frame * 60  # SURVEY.md §8(d) B_frame
+    return out, pipeline
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256, help="frames per GPU per step")
+    ap.add_argument("--width", type=int, default=640)
+    ap.add_argument("--height", type=int, default=480)
+    ap.add_argument("--nfeatures", type=int, default=1000)
+    ap.add_argument("--unique", type=int, default=64, help="distinct synthetic frames per rank")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-frames", type=int, default=384)
+    args = ap.parse_args()
+
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    device = torch.device("cuda", local_rank)
+    torch.cuda.set_device(device)
+
+    import slamhot
+    from slamhot import synth
+
+    W, H, B = args.width, args.height, args.batch
+    nuniq = min(args.unique, B)
+    base = synth.frames(range(rank * 100000, rank * 100000 + nuniq), W, H)
+    frames_np = np.concatenate([base] * ((B + nuniq - 1) // nuniq))[:B]
+    d_imgs = torch.from_numpy(frames_np).to(device)
+    ex = slamhot.ORBextractor(nfeatures=args.nfeatures, device=local_rank, max_size=(W, H), max_batch=B)
+    cap = ex.cap
+    d_kps = torch.zeros((B, cap, 28), dtype=torch.uint8, device=device)
+    d_desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device=device)
+    d_n = torch.zeros(B, dtype=torch.int32, device=device)
+    d_mono = torch.zeros(B, dtype=torch.int32, device=device)
+    stream = torch.cuda.current_stream(device)
+
+    def step():
+        ex.extract_batch_device(d_imgs.data_ptr(), B, W, H, d_kps.data_ptr(), d_desc.data_ptr(), cap,
+                                d_n.data_ptr(), d_mono.data_ptr(), lap=(0, 0), stream=stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(device)
+    if dist:
+        dist.barrier()
+    ex.stage_stats(reset=True)
+    ex.set_profiling(True)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(device)
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ex.set_profiling(False)
+    stages = ex.stage_stats(reset=True)
+
+    n_host = d_n.cpu().numpy()
+    kps_per_frame = float(n_host.mean())
+    digest = int(np.bitwise_xor.reduce(d_desc[:, :64].cpu().numpy().view(np.uint64).ravel()) & ((1 << 62) - 1))
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        g = [torch.zeros(2, dtype=torch.int64, device=device) for _ in range(world)]
+        dist.all_gather(g, torch.tensor([int(n_host.sum()), digest], dtype=torch.int64, device=device))
+        total_kps = int(sum(int(x[0].item()) for x in g))
+    else:
+        total_kps = int(n_host.sum())
+
+    frames_total = B * args.steps * world
+    value = frames_total / elapsed
+    ms_per_step = elapsed / args.steps * 1000.0
+
+    # dominant kernel roofline (HIP events around each stage, on the launch stream)
+    alg, pipe_bytes = algorithmic_bytes(W, H, kps_per_frame)
+    dom = max(stages, key=lambda k: stages[k][0])
+    dom_ms, dom_launches = stages[dom]
+    dom_avg_s = dom_ms / 1000.0 / max(dom_launches, 1)
+    dom_bytes = alg.get(dom, 0) * B
+    achieved = dom_bytes / dom_avg_s / 1e9 if dom_avg_s > 0 else 0.0
+    stage_avg_ms = {k: (v[0] / max(v[1], 1)) for k, v in stages.items()}
+    per_step_stage_ms = sum(stage_avg_ms.values())
+    traffic = None
+    tf = ROOT / "profiles" / "traffic_latest.json"
+    if tf.exists():
+        try:
+            tj = json.loads(tf.read_text())
+            if tj.get("kernel") == dom and tj.get("batch") == B and tj.get("width") == W:
+                traffic = tj.get("bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    result = {
+        "metric": "ORB extract+match frames/s and LocalBA iters/s per GPU; ATE vs reference",
+        "value": round(value, 2),
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seeded procedural textures, slamhot/synth.py)",
+        "config": {
+            "workload": f"ORBextractor-only, synthetic {W}x{H} 8-level pyramid, {args.nfeatures} feat/frame "
+                        f"(BASELINE.json configs[1])",
+            "frames_per_gpu_per_step": B,
+            "nfeatures": args.nfeatures,
+            "levels": 8,
+            "scale_factor": 1.2,
+            "fast_thresholds": [20, 7],
+            "parallelism": f"frame-sharded x{world}",
+            "keypoints_per_frame": round(kps_per_frame, 1),
+            "total_keypoints": total_kps,
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": dom,
+            "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5),
+            "traffic": traffic,
+            "algorithmic_bytes_per_launch": int(dom_bytes),
+            "avg_launch_ms": round(dom_avg_s * 1000.0, 5),
+        },
+        "stages_ms_per_step": {k: round(v, 5) for k, v in stage_avg_ms.items()},
+        "pipeline_roofline": {
+            "bytes_per_frame": int(pipe_bytes),
+            "achieved_GBps": round(pipe_bytes * B / (per_step_stage_ms / 1000.0) / 1e9, 2) if per_step_stage_ms else None,
+        },
+    }
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(args, W, H)
+
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    ex.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, W, H):
+    """The oracle (restated reference CPU path, oracle/orb_oracle.cpp) on the host cores:
+    one frame per std::thread at a time, as Frame.cc:119-122 runs extraction."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_bind as ob
+    from slamhot import synth
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(cores, 16))
+    nuniq = 32
+    imgs = synth.frames(range(5000, 5000 + nuniq), W, H)
+    imgs = np.concatenate([imgs] * ((args.cpu_frames + nuniq - 1) // nuniq))[: args.cpu_frames]
+    p = ob.params(nfeatures=args.nfeatures)
+    ob.extract_many(imgs[:cores], p, nthreads=cores)  # warm-up
+    t0 = time.perf_counter()
+    ob.extract_many(imgs, p, nthreads=cores)
+    dt = time.perf_counter() - t0
+    t1 = time.perf_counter()
+    single = 16
+    ob.extract_many(imgs[:single], p, nthreads=1)
+    dt1 = time.perf_counter() - t1
+    return {
+        "value": round(len(imgs) / dt, 2),
+        "unit": "frames/s",
+        "cores": cores,
+        "kind": "port",
+        "sample": f"{len(imgs)} synthetic {W}x{H} frames, {args.nfeatures} feat, {cores} threads "
+                  f"(one frame per thread); oracle/orb_oracle.cpp -O3 -march=x86-64-v3",
+        "per_core_frames_per_s": round(single / dt1, 2),
+    }
+
+
+if __name__ == "__main__":
+    main()

@@ -112,6 +112,17 @@ slam_status slamhot_pyramid_level(slam_extractor* ex, int frame, int level, uint
 /* Stream the handle works on (hipStream_t as void*). */
 void* slamhot_extractor_stream(slam_extractor* ex);
 
+/* Measurement hooks (no reference counterpart; the reference's REGISTER_TIMES timers,
+ * Config.h:4 / Frame.cc:116-127, play this role there).  With profiling on, every stage
+ * of every launch is bracketed by HIP events on the launch stream; stage_stats syncs on
+ * them and returns per-stage accumulated milliseconds and launch counts
+ * (slamhot_extractor_num_stages() entries each). */
+slam_status slamhot_extractor_set_profiling(slam_extractor* ex, int enable);
+int slamhot_extractor_num_stages(void);
+const char* slamhot_extractor_stage_name(int stage);
+slam_status slamhot_extractor_stage_stats(slam_extractor* ex, double* total_ms, long* launches,
+                                          int reset);
+
 #ifdef __cplusplus
 }
 #endif

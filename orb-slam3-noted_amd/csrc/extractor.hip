@@ -816,6 +816,10 @@ static size_t octree_lds_bytes(int maxn, int keycap) {
     return s;
 }
 
+enum Stage { kStResize = 0, kStFast, kStOctree, kStLayout, kStBlur, kStOrb, kNumStages };
+static const char* kStageNames[kNumStages] = {"k_resize", "k_fast_cells", "k_octree",
+                                              "k_layout", "k_blur", "k_orb"};
+
 }  // namespace slamhot
 
 using namespace slamhot;
@@ -837,6 +841,23 @@ struct slam_extractor {
     const uint8_t* last_img = nullptr;  // level-0 pointer of the last run (for pyramid_level)
     int key_lds_cap = kOctreeKeyLdsCap;
     size_t octree_lds = 0;
+    // per-stage HIP-event timing (slamhot_extractor_set_profiling)
+    bool profiling = false;
+    struct Mark { int stage; hipEvent_t a, b; };
+    std::vector<Mark> marks;
+    std::vector<hipEvent_t> pool;
+    double stage_ms[kNumStages] = {};
+    long stage_launches[kNumStages] = {};
+    hipEvent_t ev() {
+        if (pool.empty()) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return nullptr;
+            return e;
+        }
+        hipEvent_t e = pool.back();
+        pool.pop_back();
+        return e;
+    }
 };
 
 static slam_status ensure_plan(slam_extractor* ex, int W, int H) {
@@ -955,19 +976,42 @@ static slam_status launch_pipeline(slam_extractor* ex, int nframes, const uint8_
     b.lap0 = lap0;
     b.lap1 = lap1;
     SLAM_HIP_TRY(hipMemsetAsync(b.err, 0, (size_t)nframes * 4, s));
+    hipEvent_t e0 = nullptr;
+    auto begin = [&](int) {
+        if (ex->profiling) { e0 = ex->ev(); (void)hipEventRecord(e0, s); }
+    };
+    auto end = [&](int st) {
+        if (ex->profiling) {
+            hipEvent_t e1 = ex->ev();
+            (void)hipEventRecord(e1, s);
+            ex->marks.push_back({st, e0, e1});
+        }
+    };
+    begin(kStResize);
     for (int l = 1; l < P.nlevels; l++) {
         dim3 grid((P.lv[l].w + 255) / 256, (P.lv[l].h + 3) / 4, nframes);
         hipLaunchKernelGGL(k_resize, grid, dim3(64, 4), 0, s, b, l);
     }
+    end(kStResize);
+    begin(kStFast);
     hipLaunchKernelGGL(k_fast_cells, dim3(P.ncells, nframes), dim3(256), 0, s, b);
+    end(kStFast);
+    begin(kStOctree);
     hipLaunchKernelGGL(k_octree, dim3(P.nlevels, nframes), dim3(256), ex->octree_lds, s, b,
                        ex->key_lds_cap);
+    end(kStOctree);
+    begin(kStLayout);
     hipLaunchKernelGGL(k_layout, dim3(nframes), dim3(256), 0, s, b);
+    end(kStLayout);
+    begin(kStBlur);
     for (int l = 0; l < P.nlevels; l++) {
         dim3 grid((P.lv[l].w + kBlurTW - 1) / kBlurTW, (P.lv[l].h + kBlurTH - 1) / kBlurTH, nframes);
         hipLaunchKernelGGL(k_blur, grid, dim3(256), 0, s, b, l, 1);
     }
+    end(kStBlur);
+    begin(kStOrb);
     hipLaunchKernelGGL(k_orb, dim3((P.kslots + 3) / 4, nframes), dim3(256), 0, s, b);
+    end(kStOrb);
     SLAM_HIP_TRY(hipGetLastError());
     ex->last_frames = nframes;
     ex->last_img = d_img;
@@ -1033,6 +1077,8 @@ void slamhot_extractor_destroy(slam_extractor* ex) {
                       &ex->d_okp, &ex->d_ocnt, &ex->d_oidx, &ex->d_err, &ex->d_kps, &ex->d_desc,
                       &ex->d_n, &ex->d_mono};
     for (DevBuf* b : bufs) b->release();
+    for (auto& m : ex->marks) { ex->pool.push_back(m.a); ex->pool.push_back(m.b); }
+    for (hipEvent_t e : ex->pool) (void)hipEventDestroy(e);
     if (ex->stream) (void)hipStreamDestroy(ex->stream);
     delete ex;
 }
@@ -1152,5 +1198,41 @@ slam_status slamhot_pyramid_level(slam_extractor* ex, int frame, int level, uint
 }
 
 void* slamhot_extractor_stream(slam_extractor* ex) { return ex ? (void*)ex->stream : nullptr; }
+
+slam_status slamhot_extractor_set_profiling(slam_extractor* ex, int enable) {
+    if (!ex) return SLAM_EINVAL;
+    std::lock_guard<std::mutex> g(ex->mu);
+    ex->profiling = enable != 0;
+    return SLAM_OK;
+}
+
+int slamhot_extractor_num_stages(void) { return kNumStages; }
+
+const char* slamhot_extractor_stage_name(int stage) {
+    return (stage >= 0 && stage < kNumStages) ? kStageNames[stage] : "";
+}
+
+slam_status slamhot_extractor_stage_stats(slam_extractor* ex, double* total_ms, long* launches,
+                                          int reset) {
+    if (!ex) return SLAM_EINVAL;
+    std::lock_guard<std::mutex> g(ex->mu);
+    SLAM_HIP_TRY(hipSetDevice(ex->device));
+    for (auto& m : ex->marks) {
+        SLAM_HIP_TRY(hipEventSynchronize(m.b));
+        float ms = 0.f;
+        SLAM_HIP_TRY(hipEventElapsedTime(&ms, m.a, m.b));
+        ex->stage_ms[m.stage] += ms;
+        ex->stage_launches[m.stage] += 1;
+        ex->pool.push_back(m.a);
+        ex->pool.push_back(m.b);
+    }
+    ex->marks.clear();
+    for (int i = 0; i < kNumStages; i++) {
+        if (total_ms) total_ms[i] = ex->stage_ms[i];
+        if (launches) launches[i] = ex->stage_launches[i];
+        if (reset) { ex->stage_ms[i] = 0; ex->stage_launches[i] = 0; }
+    }
+    return SLAM_OK;
+}
 
 }  // extern "C"

@@ -59,6 +59,11 @@ def lib() -> C.CDLL:
     L.slamhot_pyramid_level.argtypes = [P, I, I, P, C.c_size_t, C.POINTER(I), C.POINTER(I)]
     L.slamhot_extractor_stream.argtypes = [P]
     L.slamhot_extractor_stream.restype = P
+    L.slamhot_extractor_set_profiling.argtypes = [P, I]
+    L.slamhot_extractor_num_stages.restype = I
+    L.slamhot_extractor_stage_name.argtypes = [I]
+    L.slamhot_extractor_stage_name.restype = C.c_char_p
+    L.slamhot_extractor_stage_stats.argtypes = [P, P, P, I]
     _lib = L
     return L
 
@@ -178,3 +183,15 @@ class ORBextractor:
 
     def stream(self) -> int:
         return lib().slamhot_extractor_stream(self._h) or 0
+
+    def set_profiling(self, enable: bool):
+        check(lib().slamhot_extractor_set_profiling(self._h, 1 if enable else 0), "set_profiling")
+
+    def stage_stats(self, reset: bool = False):
+        """{stage name: (total ms, launches)} accumulated while profiling was on."""
+        L = lib()
+        ns = L.slamhot_extractor_num_stages()
+        ms = np.zeros(ns, np.float64)
+        cnt = np.zeros(ns, np.int64)
+        check(L.slamhot_extractor_stage_stats(self._h, _ptr(ms), _ptr(cnt), 1 if reset else 0), "stage_stats")
+        return {L.slamhot_extractor_stage_name(i).decode(): (float(ms[i]), int(cnt[i])) for i in range(ns)}

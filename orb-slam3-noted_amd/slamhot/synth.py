@@ -36,11 +36,17 @@ def frame(seed: int, width: int = 640, height: int = 480) -> np.ndarray:
         x0, y0 = rng.integers(0, width), rng.integers(0, height)
         rw, rh = rng.integers(8, 120), rng.integers(8, 120)
         img[y0:y0 + rh, x0:x0 + rw] += rng.uniform(-70, 70)
-    yy, xx = np.mgrid[0:height, 0:width]
     for _ in range(25):
         cx, cy = rng.uniform(0, width), rng.uniform(0, height)
         s = rng.uniform(3, 25)
-        img += rng.uniform(-80, 80) * np.exp(-((xx - cx) ** 2 + (yy - cy) ** 2) / (2 * s * s))
+        amp = rng.uniform(-80, 80)
+        r = int(np.ceil(4 * s))
+        x0, x1 = max(0, int(cx) - r), min(width, int(cx) + r + 1)
+        y0, y1 = max(0, int(cy) - r), min(height, int(cy) + r + 1)
+        if x0 >= x1 or y0 >= y1:
+            continue
+        yy, xx = np.mgrid[y0:y1, x0:x1]
+        img[y0:y1, x0:x1] += amp * np.exp(-((xx - cx) ** 2 + (yy - cy) ** 2) / (2 * s * s))
     img += rng.normal(0.0, 4.0, size=img.shape)
     return np.clip(np.rint(img), 0, 255).astype(np.uint8)
 
