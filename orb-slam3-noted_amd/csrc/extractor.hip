@@ -132,6 +132,81 @@ __global__ void __launch_bounds__(256) k_resize(Bufs b, int l) {
 }
 
 // ---------------------------------------------------------------------------------------
+// k_resize2: same arithmetic as k_resize, but each block produces kRzRows full output rows:
+// the <= kRzSrcRows source rows they read are staged in LDS with 32-bit loads, so every
+// source byte is fetched from L2/HBM once per block instead of 4 times per output pixel.
+// ---------------------------------------------------------------------------------------
+constexpr int kRzRows = 8, kRzSrcRows = 16;
+
+__global__ void __launch_bounds__(256) k_resize2(Bufs b, int l) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t rz_smem[];
+    const DevPlan& P = *b.plan;
+    const DevLevel& L = P.lv[l];
+    const DevLevel& S = P.lv[l - 1];
+    const int f = blockIdx.y;
+    const int dy0 = blockIdx.x * kRzRows;
+    const int nrow = min(kRzRows, L.h - dy0);
+    const uint8_t* src = level_ptr(b, P, f, l - 1);
+    const int spitch = level_pitch(P, l - 1);
+    const int sw = S.w;
+    const int sstride = (sw + 15) & ~15;
+    const int ys = b.ytab[L.ytab_off + dy0].y0;
+    const int ye = b.ytab[L.ytab_off + dy0 + nrow - 1].y1;
+    const int nsrc = ye - ys + 1;
+    if ((spitch & 3) == 0) {
+        const int w4 = (sw + 3) >> 2;
+        for (int r = 0; r < nsrc; r++) {
+            const uint32_t* srow = reinterpret_cast<const uint32_t*>(src + (size_t)(ys + r) * spitch);
+            uint32_t* drow = reinterpret_cast<uint32_t*>(&rz_smem[r * sstride]);
+            for (int c4 = threadIdx.x; c4 < w4; c4 += blockDim.x) drow[c4] = srow[c4];
+        }
+    } else {
+        for (int r = 0; r < nsrc; r++)
+            for (int c = threadIdx.x; c < sw; c += blockDim.x)
+                rz_smem[r * sstride + c] = src[(size_t)(ys + r) * spitch + c];
+    }
+    __syncthreads();
+    const int qw = (L.w + 3) >> 2;
+    uint8_t* dbase = b.pyr + (size_t)f * P.pyr_frame + L.pyr_off;
+    for (int q = threadIdx.x; q < qw; q += blockDim.x) {
+        // this thread's 4 output columns: coefficients loaded once, reused for every row
+        int sx[4], a0[4], a1[4];
+        bool inner[4], live[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int dx = 4 * q + k;
+            live[k] = dx < L.w;
+            const ResizeX rx = b.xtab[L.xtab_off + min(dx, L.w - 1)];
+            sx[k] = rx.sx;
+            a0[k] = rx.a0;
+            a1[k] = rx.a1;
+            inner[k] = dx < L.xmax;
+        }
+        for (int r = 0; r < nrow; r++) {
+            const int dy = dy0 + r;
+            const ResizeY ry = b.ytab[L.ytab_off + dy];
+            const uint8_t* S0 = rz_smem + (ry.y0 - ys) * sstride;
+            const uint8_t* S1 = rz_smem + (ry.y1 - ys) * sstride;
+            uint32_t word = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                int d0, d1;
+                if (inner[k]) {
+                    d0 = S0[sx[k]] * a0[k] + S0[sx[k] + 1] * a1[k];
+                    d1 = S1[sx[k]] * a0[k] + S1[sx[k] + 1] * a1[k];
+                } else {
+                    d0 = S0[sx[k]] * 2048;
+                    d1 = S1[sx[k]] * 2048;
+                }
+                const int v = (((ry.b0 * (d0 >> 4)) >> 16) + ((ry.b1 * (d1 >> 4)) >> 16) + 2) >> 2;
+                word |= (uint32_t)(live[k] ? (v & 0xFF) : 0) << (8 * k);
+            }
+            *reinterpret_cast<uint32_t*>(dbase + (size_t)dy * L.pitch + 4 * q) = word;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------
 // FAST-9/16 corner measure (OpenCV 4.2.0 FAST_t<16> + cornerScore<16>, closed form).
 // For centre v and circle p[0..15], d_k = v - p_k.  With window minima/maxima over the 16
 // circular windows of 9:  Mdark = max_s min(d[s..s+8]),  Mbright = -min_s max(d[s..s+8]),
@@ -209,13 +284,13 @@ __device__ __forceinline__ int fast_measure(const uint8_t* c, int stride, int tl
 // ---------------------------------------------------------------------------------------
 constexpr int kCellMaxW = 80, kCellMaxH = 80;
 
-__global__ void __launch_bounds__(256) k_fast_cells(Bufs b) {
+__global__ void __launch_bounds__(256) k_fast_cells(Bufs b, const int32_t* list) {
     __shared__ uint8_t roi[kCellMaxH * kCellMaxW];
     __shared__ uint8_t meas[kCellMaxH * kCellMaxW];
     __shared__ int scratch[20];
     const DevPlan& P = *b.plan;
     const int f = blockIdx.y;
-    const CellDesc cd = b.cells[blockIdx.x];
+    const CellDesc cd = b.cells[list[blockIdx.x]];
     const int l = cd.level;
     const uint8_t* img = level_ptr(b, P, f, l);
     const int pitch = level_pitch(P, l);
@@ -278,6 +353,211 @@ __global__ void __launch_bounds__(256) k_fast_cells(Bufs b) {
         }
     }
     if (threadIdx.x == 0) b.cell_cnt[(size_t)f * P.ncells + cd.slot] = tot2;
+}
+
+// ---------------------------------------------------------------------------------------
+// Exact FAST measure without a threshold: M = max(max_s min d[s..s+8], -min_s max d[s..s+8])
+// with d_k = v - p_k over the 16-pixel Bresenham circle (windows by min3/max3 doubling).
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ int fast_M(const uint8_t* c, int stride) {
+    const int v = c[0];
+    int d[16];
+    d[0] = v - c[3 * stride];
+    d[1] = v - c[3 * stride + 1];
+    d[2] = v - c[2 * stride + 2];
+    d[3] = v - c[stride + 3];
+    d[4] = v - c[3];
+    d[5] = v - c[-stride + 3];
+    d[6] = v - c[-2 * stride + 2];
+    d[7] = v - c[-3 * stride + 1];
+    d[8] = v - c[-3 * stride];
+    d[9] = v - c[-3 * stride - 1];
+    d[10] = v - c[-2 * stride - 2];
+    d[11] = v - c[-stride - 3];
+    d[12] = v - c[-3];
+    d[13] = v - c[stride - 3];
+    d[14] = v - c[2 * stride - 2];
+    d[15] = v - c[3 * stride - 1];
+    int mn3[16], mx3[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        mn3[k] = min(min(d[k], d[(k + 1) & 15]), d[(k + 2) & 15]);
+        mx3[k] = max(max(d[k], d[(k + 1) & 15]), d[(k + 2) & 15]);
+    }
+    int mdark = -1024, mbr = 1024;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int mn9 = min(min(mn3[k], mn3[(k + 3) & 15]), mn3[(k + 6) & 15]);
+        const int mx9 = max(max(mx3[k], mx3[(k + 3) & 15]), mx3[(k + 6) & 15]);
+        mdark = max(mdark, mn9);
+        mbr = min(mbr, mx9);
+    }
+    const int M = max(mdark, -mbr);
+    return M > 0 ? M : 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// k_fast_wave: one WAVE per cell whose tested region is <= 64 columns wide (all cells of
+// the standard geometries).  Three order-preserving, wave-compacted passes over the cell:
+//   A  compass pre-test on every tested pixel (necessary for a 9-arc at the lower
+//      threshold: it covers one of each opposite pair 0/8 and 4/12)  -> list of survivors
+//   B  exact measure M (fast_M) on the survivors; M > tlow goes to a zero-padded M map and
+//      stays in the (in-place) list
+//   C  cell-local 3x3 NMS at both thresholds on the remaining corners (one ballot each)
+// Lists keep row-major order, so the survivors are emitted in cv::FAST's order.  The cell
+// keeps the iniThFAST result unless it is empty (ORBextractor.cc:808-841).
+// LDS per wave (host-sized): ROI ch x 72 | M map (th+2) x 66 | list | keep masks.
+// ---------------------------------------------------------------------------------------
+constexpr int kRoiStride = 80, kRoiRows = 80, kMapStride = 66;
+
+struct FastWaveLds {
+    int roi, map, lst, kmask, total;  // byte offsets inside one wave's region, total size
+};
+
+__global__ void __launch_bounds__(256) k_fast_wave(Bufs b, const int32_t* list, int nlist,
+                                                   FastWaveLds lay) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t fw_smem[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int idx = blockIdx.x * 4 + wave;
+    if (idx >= nlist) return;
+    const DevPlan& P = *b.plan;
+    const int f = blockIdx.y;
+    const CellDesc cd = b.cells[list[idx]];
+    const int l = cd.level;
+    const uint8_t* img = level_ptr(b, P, f, l);
+    const int pitch = level_pitch(P, l);
+    const int cw = cd.cw, ch = cd.ch;
+    const int tw = cw - 6, th = ch - 6;
+    uint8_t* base_ptr = fw_smem + wave * lay.total;
+    uint8_t* roi = base_ptr + lay.roi;
+    uint8_t* map = base_ptr + lay.map;
+    uint16_t* lst = reinterpret_cast<uint16_t*>(base_ptr + lay.lst);
+    uint64_t* kmask = reinterpret_cast<uint64_t*>(base_ptr + lay.kmask);
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const int ti = min(max(P.ini_th, 0), 255), tm = min(max(P.min_th, 0), 255);
+    const int tlow = min(ti, tm);
+
+    // stage the ROI with independent 32-bit loads (row start aligned down to 4 bytes; the
+    // ROI origin inside LDS is then `sh` bytes into each row), zero the M map
+    const int sh = (pitch & 3) ? 0 : (cd.iniX & 3);
+    {
+        const uint8_t* src = img + (size_t)cd.iniY * pitch + (cd.iniX - sh);
+        if ((pitch & 3) == 0) {
+            const int wd = (sh + cw + 3) >> 2;
+            const int nd = wd * ch;
+            uint32_t* roi32 = reinterpret_cast<uint32_t*>(roi);
+            for (int base = 0; base < nd; base += 64 * 8) {
+                uint32_t v[8];
+                int dst[8];
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const int i = base + k * 64 + lane;
+                    dst[k] = -1;
+                    if (i < nd) {
+                        const int r = i / wd, c = i - r * wd;
+                        v[k] = *reinterpret_cast<const uint32_t*>(src + (size_t)r * pitch + 4 * c);
+                        dst[k] = r * (kRoiStride / 4) + c;
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < 8; k++)
+                    if (dst[k] >= 0) roi32[dst[k]] = v[k];
+            }
+        } else {
+            for (int r = 0; r < ch; r++)
+                for (int c = lane; c < cw; c += 64) roi[r * kRoiStride + c] = src[(size_t)r * pitch + c];
+        }
+    }
+    roi += sh;
+    {
+        uint32_t* m32 = reinterpret_cast<uint32_t*>(map);
+        const int nw = ((th + 2) * kMapStride + 3) >> 2;
+        for (int i = lane; i < nw; i += 64) m32[i] = 0;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+
+    // pass A
+    int na = 0;
+    for (int r = 0; r < th; r++) {
+        bool pass = false;
+        if (lane < tw) {
+            const uint8_t* c = roi + (r + 3) * kRoiStride + lane + 3;
+            const int v = c[0];
+            const int d0 = v - c[3 * kRoiStride], d8 = v - c[-3 * kRoiStride];
+            const int d4 = v - c[3], d12 = v - c[-3];
+            pass = (max(d0, d8) > tlow && max(d4, d12) > tlow) || (min(d0, d8) < -tlow && min(d4, d12) < -tlow);
+        }
+        const uint64_t m = __ballot(pass);
+        if (pass) lst[na + __popcll(m & lt)] = (uint16_t)(r * 64 + lane);
+        na += __popcll(m);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+
+    // pass B (compacts the list in place: writes never pass the chunk being read)
+    int nb = 0;
+    for (int j = 0; j < na; j += 64) {
+        const int e = j + lane;
+        const bool valid = e < na;
+        const int code = valid ? lst[e] : 0;
+        const int r = code >> 6, c = code & 63;
+        int M = 0;
+        if (valid) M = fast_M(roi + (r + 3) * kRoiStride + c + 3, kRoiStride);
+        const bool corner = M > tlow;
+        if (corner) map[(r + 1) * kMapStride + c + 1] = (uint8_t)M;
+        const uint64_t m = __ballot(corner);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (corner) lst[nb + __popcll(m & lt)] = (uint16_t)code;
+        nb += __popcll(m);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+
+    // pass C
+    int cnt_i = 0;
+    for (int j = 0; j < nb; j += 64) {
+        const int e = j + lane;
+        const bool valid = e < nb;
+        bool ki = false, km = false;
+        if (valid) {
+            const int code = lst[e];
+            const int r = code >> 6, c = code & 63;
+            const uint8_t* q = map + (r + 1) * kMapStride + c + 1;
+            const int M = q[0];
+            const int n0 = q[-kMapStride - 1], n1 = q[-kMapStride], n2 = q[-kMapStride + 1];
+            const int n3 = q[-1], n4 = q[1];
+            const int n5 = q[kMapStride - 1], n6 = q[kMapStride], n7 = q[kMapStride + 1];
+            auto keep = [&](int t) -> bool {
+                auto sc = [&](int x) { return x > t ? x - 1 : 0; };
+                const int sc0 = M - 1;
+                int mx = max(max(sc(n0), sc(n1)), max(sc(n2), sc(n3)));
+                mx = max(mx, max(max(sc(n4), sc(n5)), max(sc(n6), sc(n7))));
+                return (M > t) & (sc0 > mx);
+            };
+            ki = keep(ti);
+            km = keep(tm);
+        }
+        const uint64_t bi = __ballot(ki), bm = __ballot(km);
+        if (lane == 0) {
+            kmask[2 * (j >> 6)] = bi;
+            kmask[2 * (j >> 6) + 1] = bm;
+        }
+        cnt_i += __popcll(bi);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+
+    const int sel = cnt_i ? 0 : 1;
+    uint32_t* slot = b.cell_keys + ((size_t)f * P.ncells + cd.slot) * P.slot_cap;
+    int base = 0;
+    for (int j = 0; j < nb; j += 64) {
+        const uint64_t m = kmask[2 * (j >> 6) + sel];
+        if ((m >> lane) & 1ull) {
+            const int code = lst[j + lane];
+            const int r = code >> 6, c = code & 63;
+            const int M = map[(r + 1) * kMapStride + c + 1];
+            slot[base + __popcll(m & lt)] = pack_kp(cd.iniX + 3 + c, cd.iniY + 3 + r, M - 1);
+        }
+        base += __popcll(m);
+    }
+    if (lane == 0) b.cell_cnt[(size_t)f * P.ncells + cd.slot] = base;
 }
 
 // exclusive scan over n items (in chunks of blockDim.x) of per-item value fn(i);
@@ -695,6 +975,92 @@ __global__ void __launch_bounds__(256) k_blur(Bufs b, int l, int ed) {
 }
 
 // ---------------------------------------------------------------------------------------
+// k_blur2: the same GaussianBlur for ALL levels in one launch.  Tile = 128 x 16 output
+// pixels of one level (tile table from the host plan).  Source bytes are staged with
+// 32-bit loads (byte loads + reflect-101 only on border tiles), the horizontal pass writes
+// exact u16 row sums to LDS, and each thread produces 8 outputs of one row from one
+// 16-byte LDS read per tap row and stores them with one 64-bit store.
+// ---------------------------------------------------------------------------------------
+constexpr int kB2W = 128, kB2H = 16, kB2SW = kB2W + 8, kB2SH = kB2H + 6;
+
+struct BlurTile {
+    int16_t level, pad;
+    int16_t x0, y0;
+};
+
+__global__ void __launch_bounds__(256) k_blur2(Bufs b, const BlurTile* tiles, int ed) {
+    __shared__ __attribute__((aligned(16))) uint8_t src[kB2SH * kB2SW];
+    __shared__ __attribute__((aligned(16))) uint16_t hs[kB2SH * kB2W];
+    const DevPlan& P = *b.plan;
+    const BlurTile t = tiles[blockIdx.x];
+    const int l = t.level, f = blockIdx.y;
+    const DevLevel& L = P.lv[l];
+    const uint8_t* img = level_ptr(b, P, f, l);
+    const int pitch = level_pitch(P, l);
+    const int x0 = t.x0, y0 = t.y0;
+    const int k0 = 18, k1 = 34, k2 = ed ? 48 : 49, k3 = ed ? 56 : 55;
+    // staged columns: x0-4 .. x0+kB2W+3 (136 bytes), rows y0-3 .. y0+kB2H+2
+    const bool interior = x0 >= 4 && x0 + kB2W + 4 <= L.w && y0 >= 3 && y0 + kB2H + 3 <= L.h &&
+                          (pitch & 3) == 0;
+    if (interior) {
+        for (int i = threadIdx.x; i < kB2SH * (kB2SW / 4); i += blockDim.x) {
+            const int r = i / (kB2SW / 4), c4 = i - r * (kB2SW / 4);
+            const uint32_t v = *reinterpret_cast<const uint32_t*>(img + (size_t)(y0 - 3 + r) * pitch + x0 - 4 + 4 * c4);
+            *reinterpret_cast<uint32_t*>(&src[r * kB2SW + 4 * c4]) = v;
+        }
+    } else {
+        for (int i = threadIdx.x; i < kB2SH * kB2SW; i += blockDim.x) {
+            const int r = i / kB2SW, c = i - r * kB2SW;
+            const int yy = refl101(min(y0 - 3 + r, L.h + 2), L.h);
+            const int xx = refl101(min(x0 - 4 + c, L.w + 2), L.w);
+            src[i] = img[(size_t)yy * pitch + xx];
+        }
+    }
+    __syncthreads();
+    // horizontal pass: output column c uses staged columns c+1 .. c+7
+    for (int i = threadIdx.x; i < kB2SH * (kB2W / 8); i += blockDim.x) {
+        const int r = i / (kB2W / 8), g = i - r * (kB2W / 8);
+        const uint8_t* sp = &src[r * kB2SW + 8 * g];
+        uint8_t v[16];
+        *reinterpret_cast<uint2*>(v) = *reinterpret_cast<const uint2*>(sp);
+        *reinterpret_cast<uint2*>(v + 8) = *reinterpret_cast<const uint2*>(sp + 8);
+        uint32_t o[4];
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) {
+            const uint32_t a = k0 * (v[j + 1] + v[j + 7]) + k1 * (v[j + 2] + v[j + 6]) + k2 * (v[j + 3] + v[j + 5]) + k3 * v[j + 4];
+            const uint32_t c = k0 * (v[j + 2] + v[j + 8]) + k1 * (v[j + 3] + v[j + 7]) + k2 * (v[j + 4] + v[j + 6]) + k3 * v[j + 5];
+            o[j / 2] = a | (c << 16);
+        }
+        *reinterpret_cast<uint4*>(&hs[r * kB2W + 8 * g]) = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+    __syncthreads();
+    // vertical pass: thread -> (row, 8 columns)
+    const int r = threadIdx.x >> 4, g = threadIdx.x & 15;
+    const int y = y0 + r, x = x0 + 8 * g;
+    if (y >= L.h || x >= L.w) return;
+    uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const uint32_t kk[7] = {(uint32_t)k0, (uint32_t)k1, (uint32_t)k2, (uint32_t)k3, (uint32_t)k2, (uint32_t)k1, (uint32_t)k0};
+#pragma unroll
+    for (int j = 0; j < 7; j++) {
+        const uint4 q = *reinterpret_cast<const uint4*>(&hs[(r + j) * kB2W + 8 * g]);
+        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            acc[2 * e] += kk[j] * (w[e] & 0xFFFF);
+            acc[2 * e + 1] += kk[j] * (w[e] >> 16);
+        }
+    }
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        lo |= min((acc[e] + (1u << 15)) >> 16, 255u) << (8 * e);
+        hi |= min((acc[e + 4] + (1u << 15)) >> 16, 255u) << (8 * e);
+    }
+    uint8_t* dst = b.blur + (size_t)f * P.blur_frame + L.blur_off + (size_t)y * L.pitch + x;
+    *reinterpret_cast<uint2*>(dst) = make_uint2(lo, hi);
+}
+
+// ---------------------------------------------------------------------------------------
 // k_orb: one wave per keypoint.  IC_Angle (ORBextractor.cc:75-102) on the unblurred level:
 // lane v (0..30) sums row v-15 of the radius-15 disc; exact integer wave reduction; then
 // cv::fastAtan2.  rBRIEF (computeOrbDescriptor :106-145) on the blurred level: bit
@@ -720,19 +1086,34 @@ __global__ void __launch_bounds__(256) k_orb(Bufs b) {
     // --- orientation
     const uint8_t* img = level_ptr(b, P, f, l);
     const int pitch = level_pitch(P, l);
+    // lanes 0..30 own column u = lane-15 for rows v = -15..0, lanes 32..62 the same
+    // columns for rows 1..15; disc membership |u| <= umax[|v|] masks the (independent) loads
     int m01 = 0, m10 = 0;
-    if (lane < 2 * kHalfPatch + 1) {
-        const int v = lane - kHalfPatch;
-        const int d = P.umax[v < 0 ? -v : v];
-        const uint8_t* row = img + (size_t)(ky + v) * pitch + kx;
-        int s0 = 0, s1 = 0;
-        for (int u = -d; u <= d; u++) {
-            const int val = row[u];
-            s0 += val;
-            s1 += u * val;
+    {
+        const int cl = lane & 31, half = lane >> 5;
+        if (cl < 2 * kHalfPatch + 1) {
+            const int u = cl - kHalfPatch;
+            const int au = u < 0 ? -u : u;
+            const uint8_t* colp = img + (size_t)ky * pitch + kx + u;
+            int s0 = 0, s1 = 0;
+            if (half == 0) {
+#pragma unroll
+                for (int v = -kHalfPatch; v <= 0; v++) {
+                    const int val = colp[(ptrdiff_t)v * pitch] & -(int)(au <= P.umax[-v]);
+                    s0 += val;
+                    s1 += v * val;
+                }
+            } else {
+#pragma unroll
+                for (int v = 1; v <= kHalfPatch; v++) {
+                    const int val = colp[(ptrdiff_t)v * pitch] & -(int)(au <= P.umax[v]);
+                    s0 += val;
+                    s1 += v * val;
+                }
+            }
+            m10 = u * s0;
+            m01 = s1;
         }
-        m10 = s1;
-        m01 = v * s0;
     }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
@@ -749,6 +1130,7 @@ __global__ void __launch_bounds__(256) k_orb(Bufs b) {
     const uint8_t* bl = b.blur + (size_t)f * P.blur_frame + L.blur_off;
     const uint8_t* center = bl + (size_t)ky * L.pitch + kx;
     uint8_t* desc = b.out_desc + ((size_t)f * b.cap + oi) * 32;
+    int t0[4], t1[4];
 #pragma unroll
     for (int w = 0; w < 4; w++) {
         const int bit = w * 64 + lane;
@@ -756,11 +1138,13 @@ __global__ void __launch_bounds__(256) k_orb(Bufs b) {
         const float x1 = (float)c_pattern[4 * bit + 2], y1 = (float)c_pattern[4 * bit + 3];
         const int r0 = cv_round(fmaf(x0, bb, y0 * a)), c0 = cv_round(fmaf(x0, a, -(y0 * bb)));
         const int r1 = cv_round(fmaf(x1, bb, y1 * a)), c1 = cv_round(fmaf(x1, a, -(y1 * bb)));
-        const int t0 = center[r0 * L.pitch + c0];
-        const int t1 = center[r1 * L.pitch + c1];
-        const uint64_t m = __ballot(t0 < t1);
-        if (lane == 0) reinterpret_cast<uint64_t*>(desc)[w] = m;
+        t0[w] = center[r0 * L.pitch + c0];
+        t1[w] = center[r1 * L.pitch + c1];
     }
+    uint64_t m[4];
+#pragma unroll
+    for (int w = 0; w < 4; w++) m[w] = __ballot(t0[w] < t1[w]);
+    if (lane < 4) reinterpret_cast<uint64_t*>(desc)[lane] = m[0] * (lane == 0) + m[1] * (lane == 1) + m[2] * (lane == 2) + m[3] * (lane == 3);
     if (lane == 0) {
         slam_keypoint kp;
         const float sx = l ? (float)kx * L.scale : (float)kx;
@@ -833,7 +1217,9 @@ struct slam_extractor {
     // geometry
     bool have_plan = false;
     Plan plan;
-    DevBuf d_plan, d_xtab, d_ytab, d_cells;
+    DevBuf d_plan, d_xtab, d_ytab, d_cells, d_wave_cells, d_wide_cells, d_blur_tiles;
+    int n_wave_cells = 0, n_wide_cells = 0, n_blur_tiles = 0;
+    FastWaveLds fw_lay{};
     // per-batch buffers
     DevBuf d_img, d_pyr, d_blur, d_cell_keys, d_cell_cnt, d_keys_g, d_knode_g, d_okp, d_ocnt,
         d_oidx, d_err, d_kps, d_desc, d_n, d_mono;
@@ -918,6 +1304,51 @@ static slam_status ensure_plan(slam_extractor* ex, int W, int H) {
     if (!P.ytab.empty())
         SLAM_HIP_TRY(hipMemcpy(ex->d_ytab.p, P.ytab.data(), P.ytab.size() * sizeof(ResizeY), hipMemcpyHostToDevice));
     SLAM_HIP_TRY(hipMemcpy(ex->d_cells.p, P.cells.data(), P.cells.size() * sizeof(CellDesc), hipMemcpyHostToDevice));
+    {
+        // cells whose tested region fits one wave (<= 64 columns, <= kRoiRows rows) take the
+        // wave-per-cell kernel; the rest (tiny levels of small images) the workgroup kernel
+        std::vector<int32_t> wave, wide;
+        int ch_max = 0, th_max = 0, tw_max = 0;
+        for (const CellDesc& c : P.cells) {
+            if (c.cw - 6 <= 64 && c.ch <= kRoiRows && c.cw + 3 <= kRoiStride) {
+                wave.push_back(c.slot);
+                ch_max = std::max(ch_max, (int)c.ch);
+                th_max = std::max(th_max, c.ch - 6);
+                tw_max = std::max(tw_max, c.cw - 6);
+            } else {
+                wide.push_back(c.slot);
+            }
+        }
+        auto r16 = [](int v) { return (v + 15) & ~15; };
+        FastWaveLds lay;
+        lay.roi = 0;
+        lay.map = r16(ch_max * kRoiStride);
+        lay.lst = lay.map + r16((th_max + 2) * kMapStride);
+        lay.kmask = lay.lst + r16(std::max(1, tw_max * th_max) * 2);
+        lay.total = lay.kmask + r16(((std::max(1, tw_max * th_max) + 63) / 64) * 16);
+        ex->fw_lay = lay;
+        if (4 * lay.total > 160 * 1024) return SLAM_EINVAL;
+        SLAM_HIP_TRY(hipFuncSetAttribute((const void*)k_fast_wave, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         4 * lay.total));
+        if ((st = ex->d_wave_cells.ensure(std::max<size_t>(4, wave.size() * 4))) ||
+            (st = ex->d_wide_cells.ensure(std::max<size_t>(4, wide.size() * 4))))
+            return st;
+        if (!wave.empty())
+            SLAM_HIP_TRY(hipMemcpy(ex->d_wave_cells.p, wave.data(), wave.size() * 4, hipMemcpyHostToDevice));
+        if (!wide.empty())
+            SLAM_HIP_TRY(hipMemcpy(ex->d_wide_cells.p, wide.data(), wide.size() * 4, hipMemcpyHostToDevice));
+        ex->n_wave_cells = (int)wave.size();
+        ex->n_wide_cells = (int)wide.size();
+    }
+    {
+        std::vector<BlurTile> tiles;
+        for (int l = 0; l < P.nlevels; l++)
+            for (int y = 0; y < P.lv[l].h; y += kB2H)
+                for (int x = 0; x < P.lv[l].w; x += kB2W) tiles.push_back({(int16_t)l, 0, (int16_t)x, (int16_t)y});
+        if ((st = ex->d_blur_tiles.ensure(tiles.size() * sizeof(BlurTile)))) return st;
+        SLAM_HIP_TRY(hipMemcpy(ex->d_blur_tiles.p, tiles.data(), tiles.size() * sizeof(BlurTile), hipMemcpyHostToDevice));
+        ex->n_blur_tiles = (int)tiles.size();
+    }
     ex->plan = P;
     ex->have_plan = true;
     // keys stay in LDS behind the node arrays when they fit (else global scratch)
@@ -928,6 +1359,18 @@ static slam_status ensure_plan(slam_extractor* ex, int W, int H) {
     ex->octree_lds = octree_lds_bytes(P.max_nodes, ex->key_lds_cap);
     SLAM_HIP_TRY(hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)ex->octree_lds));
+    {
+        const int rz_lds = kRzSrcRows * ((W + 15) & ~15);
+        if (rz_lds > 160 * 1024) return SLAM_EINVAL;
+        SLAM_HIP_TRY(hipFuncSetAttribute((const void*)k_resize2, hipFuncAttributeMaxDynamicSharedMemorySize, rz_lds));
+        // the staged source rows of one block must fit kRzSrcRows
+        for (int l = 1; l < P.nlevels; l++)
+            for (int dy0 = 0; dy0 < P.lv[l].h; dy0 += kRzRows) {
+                const int last = std::min(dy0 + kRzRows, P.lv[l].h) - 1;
+                if (P.ytab[P.lv[l].ytab_off + last].y1 - P.ytab[P.lv[l].ytab_off + dy0].y0 + 1 > kRzSrcRows)
+                    return SLAM_EINVAL;
+            }
+    }
     return SLAM_OK;
 }
 
@@ -989,12 +1432,18 @@ static slam_status launch_pipeline(slam_extractor* ex, int nframes, const uint8_
     };
     begin(kStResize);
     for (int l = 1; l < P.nlevels; l++) {
-        dim3 grid((P.lv[l].w + 255) / 256, (P.lv[l].h + 3) / 4, nframes);
-        hipLaunchKernelGGL(k_resize, grid, dim3(64, 4), 0, s, b, l);
+        const size_t lds = (size_t)kRzSrcRows * ((P.lv[l - 1].w + 15) & ~15);
+        hipLaunchKernelGGL(k_resize2, dim3((P.lv[l].h + kRzRows - 1) / kRzRows, nframes), dim3(256), lds, s, b, l);
     }
     end(kStResize);
     begin(kStFast);
-    hipLaunchKernelGGL(k_fast_cells, dim3(P.ncells, nframes), dim3(256), 0, s, b);
+    if (ex->n_wave_cells)
+        hipLaunchKernelGGL(k_fast_wave, dim3((ex->n_wave_cells + 3) / 4, nframes), dim3(256),
+                           4 * ex->fw_lay.total, s, b, ex->d_wave_cells.as<int32_t>(), ex->n_wave_cells,
+                           ex->fw_lay);
+    if (ex->n_wide_cells)
+        hipLaunchKernelGGL(k_fast_cells, dim3(ex->n_wide_cells, nframes), dim3(256), 0, s, b,
+                           ex->d_wide_cells.as<int32_t>());
     end(kStFast);
     begin(kStOctree);
     hipLaunchKernelGGL(k_octree, dim3(P.nlevels, nframes), dim3(256), ex->octree_lds, s, b,
@@ -1004,10 +1453,8 @@ static slam_status launch_pipeline(slam_extractor* ex, int nframes, const uint8_
     hipLaunchKernelGGL(k_layout, dim3(nframes), dim3(256), 0, s, b);
     end(kStLayout);
     begin(kStBlur);
-    for (int l = 0; l < P.nlevels; l++) {
-        dim3 grid((P.lv[l].w + kBlurTW - 1) / kBlurTW, (P.lv[l].h + kBlurTH - 1) / kBlurTH, nframes);
-        hipLaunchKernelGGL(k_blur, grid, dim3(256), 0, s, b, l, 1);
-    }
+    hipLaunchKernelGGL(k_blur2, dim3(ex->n_blur_tiles, nframes), dim3(256), 0, s, b,
+                       ex->d_blur_tiles.as<BlurTile>(), 1);
     end(kStBlur);
     begin(kStOrb);
     hipLaunchKernelGGL(k_orb, dim3((P.kslots + 3) / 4, nframes), dim3(256), 0, s, b);
@@ -1072,7 +1519,8 @@ void slamhot_extractor_destroy(slam_extractor* ex) {
     if (!ex) return;
     (void)hipSetDevice(ex->device);
     if (ex->stream) (void)hipStreamSynchronize(ex->stream);
-    DevBuf* bufs[] = {&ex->d_plan, &ex->d_xtab, &ex->d_ytab, &ex->d_cells, &ex->d_img, &ex->d_pyr,
+    DevBuf* bufs[] = {&ex->d_plan, &ex->d_xtab, &ex->d_ytab, &ex->d_cells, &ex->d_wave_cells,
+                      &ex->d_wide_cells, &ex->d_blur_tiles, &ex->d_img, &ex->d_pyr,
                       &ex->d_blur, &ex->d_cell_keys, &ex->d_cell_cnt, &ex->d_keys_g, &ex->d_knode_g,
                       &ex->d_okp, &ex->d_ocnt, &ex->d_oidx, &ex->d_err, &ex->d_kps, &ex->d_desc,
                       &ex->d_n, &ex->d_mono};
