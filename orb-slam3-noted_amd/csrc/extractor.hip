@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -91,6 +92,39 @@ __device__ __forceinline__ int kp_x(uint32_t k) { return (int)(k & 0xFFF); }
 __device__ __forceinline__ int kp_y(uint32_t k) { return (int)((k >> 12) & 0xFFF); }
 __device__ __forceinline__ int kp_s(uint32_t k) { return (int)(k >> 24); }
 
+// Stage nrows x ndw dwords (row pitch spitch bytes, 4-aligned) into LDS (row stride dstride
+// dwords): K independent loads per thread are in flight before their LDS stores.
+__device__ __forceinline__ void split_rc(int i, int ndw, float inv, int& r, int& c) {
+    r = (int)(((float)i + 0.5f) * inv);
+    c = i - r * ndw;
+    if (c < 0) { r--; c += ndw; } else if (c >= ndw) { r++; c -= ndw; }
+}
+
+template <int K>
+__device__ __forceinline__ void stage_u32(uint32_t* dst, int dstride, const uint8_t* src, size_t spitch,
+                                          int nrows, int ndw) {
+    const int total = nrows * ndw;
+    const float inv = 1.0f / (float)ndw;
+    for (int base = 0; base < total; base += blockDim.x * K) {
+        uint32_t v[K];
+        int d[K];
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const int i = base + k * blockDim.x + threadIdx.x;
+            d[k] = -1;
+            if (i < total) {
+                int r, c;
+                split_rc(i, ndw, inv, r, c);
+                v[k] = *reinterpret_cast<const uint32_t*>(src + (size_t)r * spitch + 4 * c);
+                d[k] = r * dstride + c;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < K; k++)
+            if (d[k] >= 0) dst[d[k]] = v[k];
+    }
+}
+
 // ---------------------------------------------------------------------------------------
 // k_resize: level l from level l-1 (cv::resize INTER_LINEAR 8U, OpenCV 4.2.0 generic fixed
 // point path).  Integer-only on the device: coefficient tables come from the host plan.
@@ -136,16 +170,16 @@ __global__ void __launch_bounds__(256) k_resize(Bufs b, int l) {
 // the <= kRzSrcRows source rows they read are staged in LDS with 32-bit loads, so every
 // source byte is fetched from L2/HBM once per block instead of 4 times per output pixel.
 // ---------------------------------------------------------------------------------------
-constexpr int kRzRows = 8, kRzSrcRows = 16;
+constexpr int kRzRows = 16, kRzSrcRows = 24;
 
-__global__ void __launch_bounds__(256) k_resize2(Bufs b, int l) {
+__global__ void __launch_bounds__(256) k_resize2(Bufs b, int l, int rows) {
     extern __shared__ __attribute__((aligned(16))) uint8_t rz_smem[];
     const DevPlan& P = *b.plan;
     const DevLevel& L = P.lv[l];
     const DevLevel& S = P.lv[l - 1];
     const int f = blockIdx.y;
-    const int dy0 = blockIdx.x * kRzRows;
-    const int nrow = min(kRzRows, L.h - dy0);
+    const int dy0 = blockIdx.x * rows;
+    const int nrow = min(rows, L.h - dy0);
     const uint8_t* src = level_ptr(b, P, f, l - 1);
     const int spitch = level_pitch(P, l - 1);
     const int sw = S.w;
@@ -153,13 +187,18 @@ __global__ void __launch_bounds__(256) k_resize2(Bufs b, int l) {
     const int ys = b.ytab[L.ytab_off + dy0].y0;
     const int ye = b.ytab[L.ytab_off + dy0 + nrow - 1].y1;
     const int nsrc = ye - ys + 1;
+    // coefficient table of this level's output columns, staged next to the source rows
+    ResizeX* xs = reinterpret_cast<ResizeX*>(rz_smem + kRzSrcRows * sstride);
+    ResizeY* ysm = reinterpret_cast<ResizeY*>(xs + ((L.w + 3) & ~3));
+    stage_u32<4>(reinterpret_cast<uint32_t*>(xs), 2 * L.w, reinterpret_cast<const uint8_t*>(b.xtab + L.xtab_off),
+                 0, 1, 2 * L.w);
+    if (threadIdx.x < (((L.w + 3) & ~3) - L.w)) xs[L.w + threadIdx.x] = b.xtab[L.xtab_off + L.w - 1];
+    if (threadIdx.x < 4 * nrow)
+        reinterpret_cast<uint32_t*>(ysm)[threadIdx.x] =
+            reinterpret_cast<const uint32_t*>(b.ytab + L.ytab_off + dy0)[threadIdx.x];
     if ((spitch & 3) == 0) {
-        const int w4 = (sw + 3) >> 2;
-        for (int r = 0; r < nsrc; r++) {
-            const uint32_t* srow = reinterpret_cast<const uint32_t*>(src + (size_t)(ys + r) * spitch);
-            uint32_t* drow = reinterpret_cast<uint32_t*>(&rz_smem[r * sstride]);
-            for (int c4 = threadIdx.x; c4 < w4; c4 += blockDim.x) drow[c4] = srow[c4];
-        }
+        stage_u32<8>(reinterpret_cast<uint32_t*>(rz_smem), sstride >> 2, src + (size_t)ys * spitch, spitch,
+                     nsrc, (sw + 3) >> 2);
     } else {
         for (int r = 0; r < nsrc; r++)
             for (int c = threadIdx.x; c < sw; c += blockDim.x)
@@ -168,42 +207,99 @@ __global__ void __launch_bounds__(256) k_resize2(Bufs b, int l) {
     __syncthreads();
     const int qw = (L.w + 3) >> 2;
     uint8_t* dbase = b.pyr + (size_t)f * P.pyr_frame + L.pyr_off;
-    for (int q = threadIdx.x; q < qw; q += blockDim.x) {
-        // this thread's 4 output columns: coefficients loaded once, reused for every row
-        int sx[4], a0[4], a1[4];
-        bool inner[4], live[4];
+    const float inv_qw = 1.0f / (float)qw;
+    // branch-free body: every LDS read of an item is independent and issued up front
+#pragma unroll 2
+    for (int i = threadIdx.x; i < nrow * qw; i += blockDim.x) {
+        int r, q;
+        split_rc(i, qw, inv_qw, r, q);
+        const ResizeY ry = ysm[r];
+        const uint8_t* S0 = rz_smem + (ry.y0 - ys) * sstride;
+        const uint8_t* S1 = rz_smem + (ry.y1 - ys) * sstride;
+        const uint4 xa = reinterpret_cast<const uint4*>(xs)[2 * q];
+        const uint4 xb = reinterpret_cast<const uint4*>(xs)[2 * q + 1];
+        const uint32_t sxs[4] = {xa.x, xa.z, xb.x, xb.z};
+        const uint32_t aas[4] = {xa.y, xa.w, xb.y, xb.w};
+        int p00[4], p01[4], p10[4], p11[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            const int dx = 4 * q + k;
-            live[k] = dx < L.w;
-            const ResizeX rx = b.xtab[L.xtab_off + min(dx, L.w - 1)];
-            sx[k] = rx.sx;
-            a0[k] = rx.a0;
-            a1[k] = rx.a1;
-            inner[k] = dx < L.xmax;
+            const int sx = (int)sxs[k];
+            p00[k] = S0[sx];
+            p01[k] = S0[sx + 1];
+            p10[k] = S1[sx];
+            p11[k] = S1[sx + 1];
         }
-        for (int r = 0; r < nrow; r++) {
-            const int dy = dy0 + r;
-            const ResizeY ry = b.ytab[L.ytab_off + dy];
-            const uint8_t* S0 = rz_smem + (ry.y0 - ys) * sstride;
-            const uint8_t* S1 = rz_smem + (ry.y1 - ys) * sstride;
-            uint32_t word = 0;
+        uint32_t word = 0;
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
-                int d0, d1;
-                if (inner[k]) {
-                    d0 = S0[sx[k]] * a0[k] + S0[sx[k] + 1] * a1[k];
-                    d1 = S1[sx[k]] * a0[k] + S1[sx[k] + 1] * a1[k];
-                } else {
-                    d0 = S0[sx[k]] * 2048;
-                    d1 = S1[sx[k]] * 2048;
-                }
-                const int v = (((ry.b0 * (d0 >> 4)) >> 16) + ((ry.b1 * (d1 >> 4)) >> 16) + 2) >> 2;
-                word |= (uint32_t)(live[k] ? (v & 0xFF) : 0) << (8 * k);
-            }
-            *reinterpret_cast<uint32_t*>(dbase + (size_t)dy * L.pitch + 4 * q) = word;
+        for (int k = 0; k < 4; k++) {
+            const int a0 = (int)(int16_t)(aas[k] & 0xFFFF), a1 = (int)(int16_t)(aas[k] >> 16);
+            const int d0 = __mul24(p00[k], a0) + __mul24(p01[k], a1);
+            const int d1 = __mul24(p10[k], a0) + __mul24(p11[k], a1);
+            const int v = ((__mul24((int)ry.b0, d0 >> 4) >> 16) + (__mul24((int)ry.b1, d1 >> 4) >> 16) + 2) >> 2;
+            word |= (uint32_t)(v & 0xFF) << (8 * k);
         }
+        *reinterpret_cast<uint32_t*>(dbase + (size_t)(dy0 + r) * L.pitch + 4 * q) = word;
     }
+}
+
+// ---------------------------------------------------------------------------------------
+// k_resize3: the resize with its coefficients recomputed per pixel in the reference's own
+// arithmetic (double (dx+0.5)*scale-0.5 -> float, cvFloor, saturate_cast<short> by
+// round-half-even) instead of gathered from tables: bit-identical to the host plan, and
+// the table gathers were what bound k_resize/k_resize2 (microbench: 199 -> 74 us at L1).
+// Thread = 4 output pixels of a row; source rows come from L2.
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_resize3(Bufs b, int l, double scale_x, double scale_y) {
+    const DevPlan& P = *b.plan;
+    const DevLevel& L = P.lv[l];
+    const DevLevel& S = P.lv[l - 1];
+    const int qw = (L.w + 3) >> 2;
+    const int f = blockIdx.y;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= qw * L.h) return;
+    const int dy = i / qw, q = i - dy * qw;
+    const uint8_t* src = level_ptr(b, P, f, l - 1);
+    const int spitch = level_pitch(P, l - 1);
+    float fy = (float)((dy + 0.5) * scale_y - 0.5);
+    const int sy = (int)floorf(fy);
+    fy -= (float)sy;
+    const int b0 = (int)rintf((1.f - fy) * 2048), b1 = (int)rintf(fy * 2048);
+    const int y0 = min(max(sy, 0), S.h - 1), y1 = min(max(sy + 1, 0), S.h - 1);
+    const uint8_t* S0 = src + (size_t)y0 * spitch;
+    const uint8_t* S1 = src + (size_t)y1 * spitch;
+    int sxs[4], a0s[4], a1s[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int dx = min(4 * q + k, L.w - 1);
+        float fx = (float)((dx + 0.5) * scale_x - 0.5);
+        int sx = (int)floorf(fx);
+        fx -= (float)sx;
+        if (sx < 0) { fx = 0.f; sx = 0; }
+        if (sx >= S.w - 1) { fx = 0.f; sx = S.w - 1; }
+        int a0 = (int)rintf((1.f - fx) * 2048), a1 = (int)rintf(fx * 2048);
+        if (dx >= L.xmax) { a0 = 2048; a1 = 0; }  // HResizeLinear tail: S[sx] * 2048
+        sxs[k] = sx;
+        a0s[k] = a0;
+        a1s[k] = a1;
+    }
+    int p00[4], p01[4], p10[4], p11[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        p00[k] = S0[sxs[k]];
+        p01[k] = S0[sxs[k] + 1];
+        p10[k] = S1[sxs[k]];
+        p11[k] = S1[sxs[k] + 1];
+    }
+    uint32_t word = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int d0 = __mul24(p00[k], a0s[k]) + __mul24(p01[k], a1s[k]);
+        const int d1 = __mul24(p10[k], a0s[k]) + __mul24(p11[k], a1s[k]);
+        const int v = ((__mul24(b0, d0 >> 4) >> 16) + (__mul24(b1, d1 >> 4) >> 16) + 2) >> 2;
+        word |= (uint32_t)(v & 0xFF) << (8 * k);
+    }
+    uint8_t* dbase = b.pyr + (size_t)f * P.pyr_frame + L.pyr_off;
+    *reinterpret_cast<uint32_t*>(dbase + (size_t)dy * L.pitch + 4 * q) = word;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -445,6 +541,7 @@ __global__ void __launch_bounds__(256) k_fast_wave(Bufs b, const int32_t* list, 
         if ((pitch & 3) == 0) {
             const int wd = (sh + cw + 3) >> 2;
             const int nd = wd * ch;
+            const float inv_wd = 1.0f / (float)wd;
             uint32_t* roi32 = reinterpret_cast<uint32_t*>(roi);
             for (int base = 0; base < nd; base += 64 * 8) {
                 uint32_t v[8];
@@ -454,7 +551,7 @@ __global__ void __launch_bounds__(256) k_fast_wave(Bufs b, const int32_t* list, 
                     const int i = base + k * 64 + lane;
                     dst[k] = -1;
                     if (i < nd) {
-                        const int r = i / wd, c = i - r * wd;
+                        const int r = (int)(((float)i + 0.5f) * inv_wd), c = i - r * wd;
                         v[k] = *reinterpret_cast<const uint32_t*>(src + (size_t)r * pitch + 4 * c);
                         dst[k] = r * (kRoiStride / 4) + c;
                     }
@@ -476,20 +573,30 @@ __global__ void __launch_bounds__(256) k_fast_wave(Bufs b, const int32_t* list, 
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 
-    // pass A
+    // pass A over the row-major linear index i = r*tw + c (all 64 lanes busy whatever tw);
+    // r = floor((i + 0.5) / tw) in float is exact here (i < 2^13, tw <= 64)
     int na = 0;
-    for (int r = 0; r < th; r++) {
-        bool pass = false;
-        if (lane < tw) {
-            const uint8_t* c = roi + (r + 3) * kRoiStride + lane + 3;
-            const int v = c[0];
-            const int d0 = v - c[3 * kRoiStride], d8 = v - c[-3 * kRoiStride];
-            const int d4 = v - c[3], d12 = v - c[-3];
-            pass = (max(d0, d8) > tlow && max(d4, d12) > tlow) || (min(d0, d8) < -tlow && min(d4, d12) < -tlow);
+    {
+        const int npx = tw * th;
+        const float inv_tw = 1.0f / (float)tw;
+        for (int j = 0; j < npx; j += 64) {
+            const int i = j + lane;
+            bool pass = false;
+            int code = 0;
+            if (i < npx) {
+                const int r = (int)(((float)i + 0.5f) * inv_tw);
+                const int cc = i - r * tw;
+                code = r * 64 + cc;
+                const uint8_t* c = roi + (r + 3) * kRoiStride + cc + 3;
+                const int v = c[0];
+                const int d0 = v - c[3 * kRoiStride], d8 = v - c[-3 * kRoiStride];
+                const int d4 = v - c[3], d12 = v - c[-3];
+                pass = (max(d0, d8) > tlow && max(d4, d12) > tlow) || (min(d0, d8) < -tlow && min(d4, d12) < -tlow);
+            }
+            const uint64_t m = __ballot(pass);
+            if (pass) lst[na + __popcll(m & lt)] = (uint16_t)code;
+            na += __popcll(m);
         }
-        const uint64_t m = __ballot(pass);
-        if (pass) lst[na + __popcll(m & lt)] = (uint16_t)(r * 64 + lane);
-        na += __popcll(m);
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 
@@ -1061,6 +1168,113 @@ __global__ void __launch_bounds__(256) k_blur2(Bufs b, const BlurTile* tiles, in
 }
 
 // ---------------------------------------------------------------------------------------
+// k_blur3: GaussianBlur for all levels, one launch, 128 x 32 output tiles.
+//  horizontal: output x needs bytes x-3..x+3 = 2 x v_alignbyte + 2 x v_dot4_u32_u8 against
+//              the packed Q8 taps (k0 k1 k2 k3 | k2 k1 k0 0); exact u32 row sums in LDS
+//  vertical:   each thread 4 columns x 4 rows from one 16-byte LDS read per tap row
+// Integer-exact: same sums as the OpenCV fixed-point path (u16 row sums never exceed
+// 255*256), rounded (acc + 2^15) >> 16.
+// ---------------------------------------------------------------------------------------
+constexpr int kB3W = 128, kB3H = 32, kB3SH = kB3H + 6, kB3SW = 144;  // staged stride (bytes)
+
+__global__ void __launch_bounds__(256) k_blur3(Bufs b, const BlurTile* tiles, int ed) {
+    __shared__ __attribute__((aligned(16))) uint8_t src[kB3SH * kB3SW];
+    __shared__ __attribute__((aligned(16))) uint32_t hs[kB3SH * kB3W];
+    const DevPlan& P = *b.plan;
+    const BlurTile t = tiles[blockIdx.x];
+    const int l = t.level, f = blockIdx.y;
+    const DevLevel& L = P.lv[l];
+    const uint8_t* img = level_ptr(b, P, f, l);
+    const int pitch = level_pitch(P, l);
+    const int x0 = t.x0, y0 = t.y0;
+    const uint32_t k0 = 18, k1 = 34, k2 = ed ? 48 : 49, k3 = ed ? 56 : 55;
+    const uint32_t KA = k0 | (k1 << 8) | (k2 << 16) | (k3 << 24);
+    const uint32_t KB = k2 | (k1 << 8) | (k0 << 16);
+    // staged byte i of a row <-> image column x0 - 4 + i (i in [0, 136)); rows and columns
+    // outside the level reflect (BORDER_REFLECT_101).  Whole in-range dwords are loaded as
+    // dwords; only the dwords that straddle the left/right border go byte by byte.
+    const int wfull = (pitch & 3) ? 0 : (L.w & ~3);  // columns [0, wfull) loadable as dwords
+    constexpr int KSTG = (kB3SH * 34 + 255) / 256;
+    uint32_t v[KSTG];
+#pragma unroll
+    for (int k = 0; k < KSTG; k++) {
+        const int i = threadIdx.x + 256 * k;
+        v[k] = 0;
+        if (i < kB3SH * 34) {
+            const int r = i / 34, c4 = i - r * 34;
+            const int yy = refl101(min(max(y0 - 3 + r, -3), L.h + 2), L.h);
+            const uint8_t* rowp = img + (size_t)yy * pitch;
+            const int x = x0 - 4 + 4 * c4;
+            if (x >= 0 && x + 4 <= wfull) {
+                v[k] = *reinterpret_cast<const uint32_t*>(rowp + x);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    const int xx = refl101(min(max(x + e, -4), L.w + 3), L.w);
+                    v[k] |= (uint32_t)rowp[xx] << (8 * e);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < KSTG; k++) {
+        const int i = threadIdx.x + 256 * k;
+        if (i < kB3SH * 34) {
+            const int r = i / 34, c4 = i - r * 34;
+            *reinterpret_cast<uint32_t*>(&src[r * kB3SW + 4 * c4]) = v[k];
+        }
+    }
+    __syncthreads();
+    // horizontal: thread -> (staged row, 4 output columns 4q..4q+3); output column c uses
+    // staged bytes c+1 .. c+7
+    for (int i = threadIdx.x; i < kB3SH * (kB3W / 4); i += blockDim.x) {
+        const int r = i >> 5, q = i & 31;
+        const uint32_t* row = reinterpret_cast<const uint32_t*>(&src[r * kB3SW]);
+        const uint32_t D0 = row[q], D1 = row[q + 1], D2 = row[q + 2];
+        uint4 o;
+        o.x = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(D2, D1, 1), KB,
+                                     __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(D1, D0, 1), KA, 0u, false), false);
+        o.y = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(D2, D1, 2), KB,
+                                     __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(D1, D0, 2), KA, 0u, false), false);
+        o.z = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(D2, D1, 3), KB,
+                                     __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(D1, D0, 3), KA, 0u, false), false);
+        o.w = __builtin_amdgcn_udot4(D2, KB, __builtin_amdgcn_udot4(D1, KA, 0u, false), false);
+        *reinterpret_cast<uint4*>(&hs[r * kB3W + 4 * q]) = o;
+    }
+    __syncthreads();
+    // vertical: thread -> 4 columns (cq) x 4 rows (rq)
+    const int cq = threadIdx.x & 31, rq = threadIdx.x >> 5;
+    const int x = x0 + 4 * cq;
+    if (x >= L.w) return;
+    uint32_t acc[4][4] = {};
+    const uint32_t kk[7] = {k0, k1, k2, k3, k2, k1, k0};
+#pragma unroll
+    for (int j = 0; j < 10; j++) {
+        const uint4 h = *reinterpret_cast<const uint4*>(&hs[(4 * rq + j) * kB3W + 4 * cq]);
+#pragma unroll
+        for (int o = 0; o < 4; o++) {
+            const int tap = j - o;
+            if (tap >= 0 && tap < 7) {
+                acc[o][0] += kk[tap] * h.x;
+                acc[o][1] += kk[tap] * h.y;
+                acc[o][2] += kk[tap] * h.z;
+                acc[o][3] += kk[tap] * h.w;
+            }
+        }
+    }
+    uint8_t* dst = b.blur + (size_t)f * P.blur_frame + L.blur_off + x;
+#pragma unroll
+    for (int o = 0; o < 4; o++) {
+        const int y = y0 + 4 * rq + o;
+        if (y >= L.h) break;
+        uint32_t w = 0;
+#pragma unroll
+        for (int e = 0; e < 4; e++) w |= min((acc[o][e] + (1u << 15)) >> 16, 255u) << (8 * e);
+        *reinterpret_cast<uint32_t*>(dst + (size_t)y * L.pitch) = w;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
 // k_orb: one wave per keypoint.  IC_Angle (ORBextractor.cc:75-102) on the unblurred level:
 // lane v (0..30) sums row v-15 of the radius-15 disc; exact integer wave reduction; then
 // cv::fastAtan2.  rBRIEF (computeOrbDescriptor :106-145) on the blurred level: bit
@@ -1160,6 +1374,155 @@ __global__ void __launch_bounds__(256) k_orb(Bufs b) {
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// k_orb2: k_orb with both windows staged in LDS by wide loads: the 31x31 raw disc window
+// (IC_Angle) and the 37x37 blurred window (the rotated pattern never leaves radius 18.38,
+// so rounded offsets stay within +-18).  9 + 10 dwords per row, rows spread over lanes;
+// every later access is an LDS byte read.  One wave per keypoint, 4 per workgroup.
+// ---------------------------------------------------------------------------------------
+constexpr int kOrbRawS = 36, kOrbBlS = 40;
+
+__global__ void __launch_bounds__(256) k_orb2(Bufs b) {
+    __shared__ __attribute__((aligned(16))) uint8_t raw_all[4][31 * kOrbRawS];
+    __shared__ __attribute__((aligned(16))) uint8_t bl_all[4][37 * kOrbBlS];
+    const DevPlan& P = *b.plan;
+    const int f = blockIdx.y;
+    const int wave = threadIdx.x >> 6;
+    const int slot = blockIdx.x * 4 + wave;
+    const int lane = threadIdx.x & 63;
+    if (slot >= P.kslots) return;
+    int l = 0;
+    while (l + 1 < P.nlevels && slot >= P.lv[l + 1].kbase) l++;
+    const DevLevel& L = P.lv[l];
+    const int i = slot - L.kbase;
+    if (i >= b.ocnt[(size_t)f * P.nlevels + l]) return;
+    const int oi = b.oidx[(size_t)f * P.kslots + slot];
+    if (oi >= b.cap) return;
+    const uint32_t key = b.okp[(size_t)f * P.kslots + slot];
+    const int kx = kp_x(key), ky = kp_y(key);
+    const uint8_t* img = level_ptr(b, P, f, l);
+    const int pitch = level_pitch(P, l);
+    const uint8_t* bl = b.blur + (size_t)f * P.blur_frame + L.blur_off;
+    uint8_t* raw = raw_all[wave];
+    uint8_t* blw = bl_all[wave];
+    // stage: raw rows ky-15..ky+15 from xr, blurred rows ky-18..ky+18 from xb (4-aligned)
+    const int xr = (kx - kHalfPatch) & ~3, shr_ = (kx - kHalfPatch) - xr;
+    const int xb = (kx - 18) & ~3, shb = (kx - 18) - xb;
+    if ((pitch & 3) == 0) {
+        uint32_t v[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            const int e = lane + 64 * k;
+            if (e < 31 * 9) {
+                const int r = e / 9, c = e - r * 9;
+                v[k] = *reinterpret_cast<const uint32_t*>(img + (size_t)(ky - kHalfPatch + r) * pitch + xr + 4 * c);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            const int e = lane + 64 * k;
+            if (e < 31 * 9) {
+                const int r = e / 9, c = e - r * 9;
+                *reinterpret_cast<uint32_t*>(&raw[r * kOrbRawS + 4 * c]) = v[k];
+            }
+        }
+    } else {
+        for (int e = lane; e < 31 * kOrbRawS; e += 64) {
+            const int r = e / kOrbRawS, c = e - r * kOrbRawS;
+            raw[e] = img[(size_t)(ky - kHalfPatch + r) * pitch + xr + c];
+        }
+    }
+    {
+        uint32_t v[6];
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+            const int e = lane + 64 * k;
+            if (e < 37 * 10) {
+                const int r = e / 10, c = e - r * 10;
+                v[k] = *reinterpret_cast<const uint32_t*>(bl + (size_t)(ky - 18 + r) * L.pitch + xb + 4 * c);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+            const int e = lane + 64 * k;
+            if (e < 37 * 10) {
+                const int r = e / 10, c = e - r * 10;
+                *reinterpret_cast<uint32_t*>(&blw[r * kOrbBlS + 4 * c]) = v[k];
+            }
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+
+    // --- orientation (IC_Angle, ORBextractor.cc:75-102): lanes 0..30 rows -15..0, 32..62 rows 1..15
+    int m01 = 0, m10 = 0;
+    {
+        const int cl = lane & 31, half = lane >> 5;
+        if (cl < 2 * kHalfPatch + 1) {
+            const int u = cl - kHalfPatch;
+            const int au = u < 0 ? -u : u;
+            const uint8_t* colp = raw + kHalfPatch * kOrbRawS + shr_ + kHalfPatch + u;
+            int s0 = 0, s1 = 0;
+            if (half == 0) {
+#pragma unroll
+                for (int v = -kHalfPatch; v <= 0; v++) {
+                    const int val = colp[v * kOrbRawS] & -(int)(au <= P.umax[-v]);
+                    s0 += val;
+                    s1 += v * val;
+                }
+            } else {
+#pragma unroll
+                for (int v = 1; v <= kHalfPatch; v++) {
+                    const int val = colp[v * kOrbRawS] & -(int)(au <= P.umax[v]);
+                    s0 += val;
+                    s1 += v * val;
+                }
+            }
+            m10 = u * s0;
+            m01 = s1;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        m10 += __shfl_xor(m10, o, 64);
+        m01 += __shfl_xor(m01, o, 64);
+    }
+    const float angle = cv_fast_atan2((float)m01, (float)m10);
+
+    // --- descriptor (computeOrbDescriptor, ORBextractor.cc:106-145)
+    const float factor_pi = (float)(3.14159265358979323846 / 180.f);
+    float sn, cs;
+    glibc_sincosf(angle * factor_pi, &sn, &cs);
+    const float a = cs, bb = sn;
+    const uint8_t* center = blw + 18 * kOrbBlS + shb + 18;
+    int t0[4], t1[4];
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        const int bit = w * 64 + lane;
+        const float x0 = (float)c_pattern[4 * bit], y0 = (float)c_pattern[4 * bit + 1];
+        const float x1 = (float)c_pattern[4 * bit + 2], y1 = (float)c_pattern[4 * bit + 3];
+        const int r0 = cv_round(fmaf(x0, bb, y0 * a)), c0 = cv_round(fmaf(x0, a, -(y0 * bb)));
+        const int r1 = cv_round(fmaf(x1, bb, y1 * a)), c1 = cv_round(fmaf(x1, a, -(y1 * bb)));
+        t0[w] = center[r0 * kOrbBlS + c0];
+        t1[w] = center[r1 * kOrbBlS + c1];
+    }
+    uint64_t m[4];
+#pragma unroll
+    for (int w = 0; w < 4; w++) m[w] = __ballot(t0[w] < t1[w]);
+    uint8_t* desc = b.out_desc + ((size_t)f * b.cap + oi) * 32;
+    if (lane < 4) reinterpret_cast<uint64_t*>(desc)[lane] = lane == 0 ? m[0] : lane == 1 ? m[1] : lane == 2 ? m[2] : m[3];
+    if (lane == 4) {
+        slam_keypoint kp;
+        kp.x = l ? (float)kx * L.scale : (float)kx;
+        kp.y = l ? (float)ky * L.scale : (float)ky;
+        kp.size = L.size;
+        kp.angle = angle;
+        kp.response = (float)kp_s(key);
+        kp.octave = l;
+        kp.class_id = -1;
+        b.out_kps[(size_t)f * b.cap + oi] = kp;
+    }
+}
+
 }  // namespace slamhot
 
 // =======================================================================================
@@ -1188,7 +1551,7 @@ struct DevBuf {
     template <class T> T* as() const { return reinterpret_cast<T*>(p); }
 };
 
-constexpr int kOctreeKeyLdsCap = 6144;  // keys held in LDS per octree workgroup
+constexpr int kOctreeKeyLdsCap = 4096;  // keys held in LDS per octree workgroup
 
 static size_t octree_lds_bytes(int maxn, int keycap) {
     size_t s = 0;
@@ -1213,6 +1576,10 @@ struct slam_extractor {
     int device = 0;
     int max_w = 0, max_h = 0, max_batch = 0;
     hipStream_t stream = nullptr;
+    hipStream_t side = nullptr;             // blur runs here, concurrent with FAST + octree
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    bool serial = false;
+    int rz_rows[kMaxLevels] = {};
     std::mutex mu;
     // geometry
     bool have_plan = false;
@@ -1343,8 +1710,8 @@ static slam_status ensure_plan(slam_extractor* ex, int W, int H) {
     {
         std::vector<BlurTile> tiles;
         for (int l = 0; l < P.nlevels; l++)
-            for (int y = 0; y < P.lv[l].h; y += kB2H)
-                for (int x = 0; x < P.lv[l].w; x += kB2W) tiles.push_back({(int16_t)l, 0, (int16_t)x, (int16_t)y});
+            for (int y = 0; y < P.lv[l].h; y += kB3H)
+                for (int x = 0; x < P.lv[l].w; x += kB3W) tiles.push_back({(int16_t)l, 0, (int16_t)x, (int16_t)y});
         if ((st = ex->d_blur_tiles.ensure(tiles.size() * sizeof(BlurTile)))) return st;
         SLAM_HIP_TRY(hipMemcpy(ex->d_blur_tiles.p, tiles.data(), tiles.size() * sizeof(BlurTile), hipMemcpyHostToDevice));
         ex->n_blur_tiles = (int)tiles.size();
@@ -1360,16 +1727,23 @@ static slam_status ensure_plan(slam_extractor* ex, int W, int H) {
     SLAM_HIP_TRY(hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)ex->octree_lds));
     {
-        const int rz_lds = kRzSrcRows * ((W + 15) & ~15);
+        const int rz_lds = kRzSrcRows * ((W + 15) & ~15) + (int)sizeof(ResizeX) * (W + 4) + (int)sizeof(ResizeY) * kRzRows;
         if (rz_lds > 160 * 1024) return SLAM_EINVAL;
         SLAM_HIP_TRY(hipFuncSetAttribute((const void*)k_resize2, hipFuncAttributeMaxDynamicSharedMemorySize, rz_lds));
-        // the staged source rows of one block must fit kRzSrcRows
-        for (int l = 1; l < P.nlevels; l++)
-            for (int dy0 = 0; dy0 < P.lv[l].h; dy0 += kRzRows) {
-                const int last = std::min(dy0 + kRzRows, P.lv[l].h) - 1;
-                if (P.ytab[P.lv[l].ytab_off + last].y1 - P.ytab[P.lv[l].ytab_off + dy0].y0 + 1 > kRzSrcRows)
-                    return SLAM_EINVAL;
+        // rows per block: the largest R <= kRzRows whose staged source rows fit kRzSrcRows
+        for (int l = 1; l < P.nlevels; l++) {
+            int R = kRzRows;
+            for (; R >= 1; R--) {
+                bool ok = true;
+                for (int dy0 = 0; dy0 < P.lv[l].h && ok; dy0 += R) {
+                    const int last = std::min(dy0 + R, P.lv[l].h) - 1;
+                    ok = P.ytab[P.lv[l].ytab_off + last].y1 - P.ytab[P.lv[l].ytab_off + dy0].y0 + 1 <= kRzSrcRows;
+                }
+                if (ok) break;
             }
+            if (R < 1) return SLAM_EINVAL;
+            ex->rz_rows[l] = R;
+        }
     }
     return SLAM_OK;
 }
@@ -1420,22 +1794,36 @@ static slam_status launch_pipeline(slam_extractor* ex, int nframes, const uint8_
     b.lap1 = lap1;
     SLAM_HIP_TRY(hipMemsetAsync(b.err, 0, (size_t)nframes * 4, s));
     hipEvent_t e0 = nullptr;
-    auto begin = [&](int) {
-        if (ex->profiling) { e0 = ex->ev(); (void)hipEventRecord(e0, s); }
+    auto begin = [&](int, hipStream_t st_ = nullptr) {
+        if (ex->profiling) { e0 = ex->ev(); (void)hipEventRecord(e0, st_ ? st_ : s); }
     };
-    auto end = [&](int st) {
+    auto end = [&](int st, hipStream_t st_ = nullptr) {
         if (ex->profiling) {
             hipEvent_t e1 = ex->ev();
-            (void)hipEventRecord(e1, s);
+            (void)hipEventRecord(e1, st_ ? st_ : s);
             ex->marks.push_back({st, e0, e1});
         }
     };
     begin(kStResize);
     for (int l = 1; l < P.nlevels; l++) {
-        const size_t lds = (size_t)kRzSrcRows * ((P.lv[l - 1].w + 15) & ~15);
-        hipLaunchKernelGGL(k_resize2, dim3((P.lv[l].h + kRzRows - 1) / kRzRows, nframes), dim3(256), lds, s, b, l);
+        const int qw = (P.lv[l].w + 3) / 4;
+        const double sxv = 1. / ((double)P.lv[l].w / P.lv[l - 1].w);
+        const double syv = 1. / ((double)P.lv[l].h / P.lv[l - 1].h);
+        hipLaunchKernelGGL(k_resize3, dim3((qw * P.lv[l].h + 255) / 256, nframes), dim3(256), 0, s, b, l, sxv, syv);
     }
     end(kStResize);
+    // fork: the blur needs only the pyramid (SLAMHOT_SERIAL=1 keeps it on the main stream,
+    // for isolated per-kernel timing)
+    hipStream_t bs = ex->serial ? s : ex->side;
+    if (!ex->serial) {
+        SLAM_HIP_TRY(hipEventRecord(ex->ev_fork, s));
+        SLAM_HIP_TRY(hipStreamWaitEvent(ex->side, ex->ev_fork, 0));
+    }
+    begin(kStBlur, bs);
+    hipLaunchKernelGGL(k_blur3, dim3(ex->n_blur_tiles, nframes), dim3(256), 0, bs, b,
+                       ex->d_blur_tiles.as<BlurTile>(), 1);
+    end(kStBlur, bs);
+    if (!ex->serial) SLAM_HIP_TRY(hipEventRecord(ex->ev_join, ex->side));
     begin(kStFast);
     if (ex->n_wave_cells)
         hipLaunchKernelGGL(k_fast_wave, dim3((ex->n_wave_cells + 3) / 4, nframes), dim3(256),
@@ -1452,12 +1840,9 @@ static slam_status launch_pipeline(slam_extractor* ex, int nframes, const uint8_
     begin(kStLayout);
     hipLaunchKernelGGL(k_layout, dim3(nframes), dim3(256), 0, s, b);
     end(kStLayout);
-    begin(kStBlur);
-    hipLaunchKernelGGL(k_blur2, dim3(ex->n_blur_tiles, nframes), dim3(256), 0, s, b,
-                       ex->d_blur_tiles.as<BlurTile>(), 1);
-    end(kStBlur);
+    if (!ex->serial) SLAM_HIP_TRY(hipStreamWaitEvent(s, ex->ev_join, 0));
     begin(kStOrb);
-    hipLaunchKernelGGL(k_orb, dim3((P.kslots + 3) / 4, nframes), dim3(256), 0, s, b);
+    hipLaunchKernelGGL(k_orb2, dim3((P.kslots + 3) / 4, nframes), dim3(256), 0, s, b);
     end(kStOrb);
     SLAM_HIP_TRY(hipGetLastError());
     ex->last_frames = nframes;
@@ -1502,12 +1887,19 @@ slam_status slamhot_extractor_create(const slam_orb_params* params, int device, 
     Plan probe;
     if (!build_plan(*params, max_width, max_height, probe)) return SLAM_EINVAL;
     slam_extractor* ex = new slam_extractor();
+    {
+        const char* e = std::getenv("SLAMHOT_SERIAL");
+        ex->serial = e && e[0] == '1';
+    }
     ex->prm = *params;
     ex->device = device;
     ex->max_w = max_width;
     ex->max_h = max_height;
     ex->max_batch = max_batch;
-    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ex->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ex->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&ex->side, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&ex->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ex->ev_join, hipEventDisableTiming) != hipSuccess) {
         delete ex;
         return SLAM_EHIP;
     }
@@ -1527,6 +1919,10 @@ void slamhot_extractor_destroy(slam_extractor* ex) {
     for (DevBuf* b : bufs) b->release();
     for (auto& m : ex->marks) { ex->pool.push_back(m.a); ex->pool.push_back(m.b); }
     for (hipEvent_t e : ex->pool) (void)hipEventDestroy(e);
+    if (ex->side) (void)hipStreamSynchronize(ex->side);
+    if (ex->ev_fork) (void)hipEventDestroy(ex->ev_fork);
+    if (ex->ev_join) (void)hipEventDestroy(ex->ev_join);
+    if (ex->side) (void)hipStreamDestroy(ex->side);
     if (ex->stream) (void)hipStreamDestroy(ex->stream);
     delete ex;
 }

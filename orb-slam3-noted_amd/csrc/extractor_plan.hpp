@@ -125,6 +125,12 @@ inline void build_resize_tables(int sw, int sh, int dw, int dh, Plan& P, LevelPl
         P.xtab.push_back(e);
     }
     L.xmax = xmax;
+    // columns at/after xmax use D = S[sx] * 2048 (HResizeLinear's tail loop): encode them as
+    // (a0, a1) = (2048, 0) so the device formula S[sx]*a0 + S[sx+1]*a1 is branch-free
+    for (int dx = xmax; dx < dw; dx++) {
+        P.xtab[L.xtab_off + dx].a0 = 2048;
+        P.xtab[L.xtab_off + dx].a1 = 0;
+    }
     for (int dy = 0; dy < dh; dy++) {
         float fy = (float)((dy + 0.5) * scale_y - 0.5);
         int sy = (int)std::floor(fy);
