@@ -123,6 +123,65 @@ const char* slamhot_extractor_stage_name(int stage);
 slam_status slamhot_extractor_stage_stats(slam_extractor* ex, double* total_ms, long* launches,
                                           int reset);
 
+/* ---------------------------------------------------------------------------------
+ * Vocabulary (DBoW2 TemplatedVocabulary<FORB>, ORBVocabulary.h:29-30)
+ * ------------------------------------------------------------------------------- */
+typedef struct slam_vocab slam_vocab;
+
+/* Node table in DBoW2 order: node 0 is the root; parent[0] = -1.  Children of a node are
+ * the nodes naming it as parent, in table order (loadFromTextFile, TemplatedVocabulary.h:
+ * 1350-1436).  is_leaf marks words; weight is the node weight (word idf). */
+slam_status slamhot_vocab_create(int device, int k, int L, int scoring, int weighting, int n_nodes,
+                                 const int32_t* parent, const uint8_t* is_leaf,
+                                 const uint8_t* desc, const double* weight, slam_vocab** out);
+/* TemplatedVocabulary::loadFromTextFile (TemplatedVocabulary.h:1350-1436), ORBvoc.txt. */
+slam_status slamhot_vocab_load_text(int device, const char* path, slam_vocab** out);
+void slamhot_vocab_destroy(slam_vocab* v);
+slam_status slamhot_vocab_info(const slam_vocab* v, int* k, int* L, int* n_nodes, int* n_words);
+
+/* TemplatedVocabulary::transform(desc, word_id, weight, &node_id, levelsup) for n
+ * descriptors (TemplatedVocabulary.h:1229-1271); the per-feature results from which
+ * Frame::ComputeBoW / KeyFrame::ComputeBoW (Frame.cc:721-728) build mBowVec/mFeatVec
+ * (features with weight <= 0 are dropped, :1169). */
+slam_status slamhot_vocab_transform(slam_vocab* v, int n, const uint8_t* desc, int levelsup,
+                                    int32_t* word_id, double* weight, int32_t* node_id);
+/* Device-resident form: d_desc n x 32 (row stride desc_stride bytes), outputs on device. */
+slam_status slamhot_vocab_transform_device(slam_vocab* v, int n, const void* d_desc,
+                                           int desc_stride, int levelsup, void* d_word_id,
+                                           void* d_weight, void* d_node_id, void* hip_stream);
+
+/* ---------------------------------------------------------------------------------
+ * ORBmatcher (ORBmatcher.h:39-91), pinhole cameras (Frame::Nleft == -1)
+ * ------------------------------------------------------------------------------- */
+typedef struct slam_matcher slam_matcher;
+
+slam_status slamhot_matcher_create(int device, slam_matcher** out);
+void slamhot_matcher_destroy(slam_matcher* m);
+
+/* One side of SearchByBoW: descriptors, keypoint angles, MapPoint validity
+ * (pMP != NULL && !pMP->isBad(); NULL = all valid) and the DBoW2 FeatureVector as CSR
+ * (node ids ascending, feature indices ascending inside each node). */
+typedef struct slam_bow_side {
+    int32_t n;
+    const uint8_t* desc;
+    const float* angle;
+    const uint8_t* valid;
+    int32_t n_nodes;
+    const uint32_t* node_id;
+    const int32_t* node_off;
+    const uint32_t* node_feat;
+} slam_bow_side;
+
+/* int ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, vector<MapPoint*>& matches)
+ * (ORBmatcher.cc:269-471) when strict == 0: A = KF (valid = MapPoint flags), B = Frame
+ * (valid NULL); b2a[i] = KF feature whose MapPoint F.feature i matched, -1 otherwise.
+ * int ORBmatcher::SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*>& m12)
+ * (ORBmatcher.cc:823-963) when strict == 1: a2b[i] = KF2 feature matched by KF1 feature i.
+ * *nmatches = the reference's return value. */
+slam_status slamhot_search_by_bow(slam_matcher* m, const slam_bow_side* A, const slam_bow_side* B,
+                                  float nnratio, int check_ori, int strict, int32_t* a2b,
+                                  int32_t* b2a, int* nmatches);
+
 #ifdef __cplusplus
 }
 #endif

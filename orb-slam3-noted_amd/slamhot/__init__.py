@@ -32,6 +32,24 @@ class OrbParams(C.Structure):
                 ("ini_th_fast", C.c_int32), ("min_th_fast", C.c_int32)]
 
 
+class BowSide(C.Structure):
+    _fields_ = [("n", C.c_int32), ("desc", C.c_void_p), ("angle", C.c_void_p), ("valid", C.c_void_p),
+                ("n_nodes", C.c_int32), ("node_id", C.c_void_p), ("node_off", C.c_void_p),
+                ("node_feat", C.c_void_p)]
+
+
+def make_bow_side(desc, angle, valid, node_id, node_off, node_feat):
+    """slam_bow_side over numpy arrays; returns (struct, keepalive list)."""
+    arrs = [np.ascontiguousarray(desc, np.uint8), np.ascontiguousarray(angle, np.float32),
+            None if valid is None else np.ascontiguousarray(valid, np.uint8),
+            np.ascontiguousarray(node_id, np.uint32), np.ascontiguousarray(node_off, np.int32),
+            np.ascontiguousarray(node_feat, np.uint32)]
+    ptr = lambda a: None if a is None else a.ctypes.data_as(C.c_void_p)
+    s = BowSide(len(arrs[0]), ptr(arrs[0]), ptr(arrs[1]), ptr(arrs[2]), len(arrs[3]), ptr(arrs[3]), ptr(arrs[4]),
+                ptr(arrs[5]))
+    return s, arrs
+
+
 _lib = None
 P = C.c_void_p
 I = C.c_int
@@ -64,6 +82,18 @@ def lib() -> C.CDLL:
     L.slamhot_extractor_stage_name.argtypes = [I]
     L.slamhot_extractor_stage_name.restype = C.c_char_p
     L.slamhot_extractor_stage_stats.argtypes = [P, P, P, I]
+    L.slamhot_vocab_create.argtypes = [I, I, I, I, I, I, P, P, P, P, C.POINTER(P)]
+    L.slamhot_vocab_load_text.argtypes = [I, C.c_char_p, C.POINTER(P)]
+    L.slamhot_vocab_destroy.argtypes = [P]
+    L.slamhot_vocab_destroy.restype = None
+    L.slamhot_vocab_info.argtypes = [P, C.POINTER(I), C.POINTER(I), C.POINTER(I), C.POINTER(I)]
+    L.slamhot_vocab_transform.argtypes = [P, I, P, I, P, P, P]
+    L.slamhot_vocab_transform_device.argtypes = [P, I, P, I, I, P, P, P, P]
+    L.slamhot_matcher_create.argtypes = [I, C.POINTER(P)]
+    L.slamhot_matcher_destroy.argtypes = [P]
+    L.slamhot_matcher_destroy.restype = None
+    L.slamhot_search_by_bow.argtypes = [P, C.POINTER(BowSide), C.POINTER(BowSide), C.c_float, I, I, P, P,
+                                        C.POINTER(I)]
     _lib = L
     return L
 
@@ -195,3 +225,93 @@ class ORBextractor:
         cnt = np.zeros(ns, np.int64)
         check(L.slamhot_extractor_stage_stats(self._h, _ptr(ms), _ptr(cnt), 1 if reset else 0), "stage_stats")
         return {L.slamhot_extractor_stage_name(i).decode(): (float(ms[i]), int(cnt[i])) for i in range(ns)}
+
+
+class Vocabulary:
+    """ORBVocabulary (DBoW2 TemplatedVocabulary<FORB>) resident on one gfx950 device."""
+
+    def __init__(self, parent=None, is_leaf=None, desc=None, weight=None, k=10, L=6, scoring=0, weighting=0,
+                 path: str | None = None, device: int = 0):
+        self._h = P()
+        if path is not None:
+            check(lib().slamhot_vocab_load_text(device, path.encode(), C.byref(self._h)), "vocab_load_text")
+        else:
+            parent = np.ascontiguousarray(parent, np.int32)
+            is_leaf = np.ascontiguousarray(is_leaf, np.uint8)
+            desc = np.ascontiguousarray(desc, np.uint8)
+            weight = np.ascontiguousarray(weight, np.float64)
+            check(lib().slamhot_vocab_create(device, k, L, scoring, weighting, len(parent), _ptr(parent),
+                                             _ptr(is_leaf), _ptr(desc), _ptr(weight), C.byref(self._h)),
+                  "vocab_create")
+        k_, L_, nn, nw = I(0), I(0), I(0), I(0)
+        check(lib().slamhot_vocab_info(self._h, C.byref(k_), C.byref(L_), C.byref(nn), C.byref(nw)), "vocab_info")
+        self.k, self.L, self.n_nodes, self.n_words = k_.value, L_.value, nn.value, nw.value
+
+    def close(self):
+        if self._h:
+            lib().slamhot_vocab_destroy(self._h)
+            self._h = P()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def transform(self, desc: np.ndarray, levelsup: int = 4):
+        """Per-feature (word id, word weight, node id at level L-levelsup)."""
+        desc = np.ascontiguousarray(desc, np.uint8)
+        n = len(desc)
+        w = np.zeros(n, np.int32)
+        wt = np.zeros(n, np.float64)
+        nid = np.zeros(n, np.int32)
+        check(lib().slamhot_vocab_transform(self._h, n, _ptr(desc), levelsup, _ptr(w), _ptr(wt), _ptr(nid)),
+              "vocab_transform")
+        return w, wt, nid
+
+
+class ORBmatcher:
+    """Mirror of ORB_SLAM3::ORBmatcher(nnratio, checkOri) (ORBmatcher.h:39-91), pinhole."""
+
+    TH_HIGH, TH_LOW, HISTO_LENGTH = 100, 50, 30
+
+    def __init__(self, nnratio: float = 0.6, checkOri: bool = True, device: int = 0):
+        self.mfNNratio = nnratio
+        self.mbCheckOrientation = checkOri
+        self._h = P()
+        check(lib().slamhot_matcher_create(device, C.byref(self._h)), "matcher_create")
+
+    def close(self):
+        if self._h:
+            lib().slamhot_matcher_destroy(self._h)
+            self._h = P()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _bow(self, A, B, strict):
+        sa, ka = make_bow_side(*A)
+        sb, kb = make_bow_side(*B)
+        a2b = np.full(sa.n, -1, np.int32)
+        b2a = np.full(sb.n, -1, np.int32)
+        nm = I(0)
+        check(lib().slamhot_search_by_bow(self._h, C.byref(sa), C.byref(sb), self.mfNNratio,
+                                          1 if self.mbCheckOrientation else 0, strict, _ptr(a2b), _ptr(b2a),
+                                          C.byref(nm)), "search_by_bow")
+        return nm.value, a2b, b2a
+
+    def SearchByBoW_KF_F(self, kf, frame):
+        """int SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&): kf / frame are tuples
+        (desc, angle, valid, node_id, node_off, node_feat); returns (nmatches, per-frame-feature
+        matched KF feature index or -1)."""
+        n, a2b, b2a = self._bow(kf, frame, 0)
+        return n, b2a
+
+    def SearchByBoW_KF_KF(self, kf1, kf2):
+        """int SearchByBoW(KeyFrame*, KeyFrame*, vector<MapPoint*>&): returns (nmatches,
+        per-KF1-feature matched KF2 feature index or -1)."""
+        n, a2b, b2a = self._bow(kf1, kf2, 1)
+        return n, a2b

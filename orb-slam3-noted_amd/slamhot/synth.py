@@ -70,3 +70,48 @@ def shifted(img: np.ndarray, dx: float, dy: float, angle_deg: float, seed: int) 
     yi = np.clip(np.rint(ys), 0, h - 1).astype(np.int64)
     out = img[yi, xi].astype(np.float64) + rng.normal(0.0, 2.0, size=img.shape)
     return np.clip(np.rint(out), 0, 255).astype(np.uint8)
+
+
+def vocab(k: int = 10, L: int = 6, seed: int = 0, stop_frac: float = 0.01):
+    """Synthetic DBoW2-shaped vocabulary in breadth-first node order (node 0 = root):
+    returns (parent int32, is_leaf uint8, desc (n,32) uint8, weight float64).  Node
+    descriptors are random; a child is its parent with ~25% of bits flipped, so nearby
+    descriptors descend alike.  A fraction of words get weight 0 (stopped words)."""
+    rng = np.random.default_rng(seed)
+    n = (k ** (L + 1) - 1) // (k - 1)
+    parent = np.empty(n, np.int32)
+    parent[0] = -1
+    idx = np.arange(1, n)
+    parent[1:] = (idx - 1) // k
+    desc = np.empty((n, 32), np.uint8)
+    desc[0] = rng.integers(0, 256, 32, dtype=np.uint8)
+    first = 1
+    for lvl in range(1, L + 1):
+        cnt = k ** lvl
+        par = desc[parent[first:first + cnt]]
+        flips = rng.random((cnt, 256)) < 0.25
+        bits = np.unpackbits(par, axis=1, bitorder="little") ^ flips.astype(np.uint8)
+        desc[first:first + cnt] = np.packbits(bits, axis=1, bitorder="little")
+        first += cnt
+    is_leaf = np.zeros(n, np.uint8)
+    nleaf = k ** L
+    is_leaf[n - nleaf:] = 1
+    weight = np.zeros(n, np.float64)
+    w = rng.uniform(0.5, 3.0, nleaf)
+    w[rng.random(nleaf) < stop_frac] = 0.0
+    weight[n - nleaf:] = w
+    return parent, is_leaf, desc, weight
+
+
+def feature_vector(node_id: np.ndarray, weight: np.ndarray):
+    """DBoW2 FeatureVector as CSR from per-feature (node id, word weight): features whose
+    word weight is <= 0 are dropped (TemplatedVocabulary.h:1169), ascending node ids,
+    ascending feature indices (FeatureVector::addFeature, FeatureVector.cpp:31-45)."""
+    keep = np.nonzero(weight > 0)[0]
+    nid = node_id[keep]
+    order = np.lexsort((keep, nid))
+    nid_s = nid[order]
+    feats = keep[order].astype(np.uint32)
+    uniq, starts = np.unique(nid_s, return_index=True)
+    off = np.append(starts, len(nid_s)).astype(np.int32)
+    return uniq.astype(np.uint32), off, feats

@@ -164,3 +164,63 @@ def extract_many(imgs: np.ndarray, p: OrbParams | None = None, lap=(0, 0), nthre
     imgs = np.ascontiguousarray(imgs, dtype=np.uint8)
     n, h, w = imgs.shape
     return lib().oracle_extract_many(C.byref(p), n, _ptr(imgs), w, h, w, lap[0], lap[1], nthreads)
+
+
+# ---- matchers / vocabulary (oracle/matcher_oracle.cpp)
+def _mlib():
+    L = lib()
+    if not hasattr(L, "_m_ready"):
+        P = C.c_void_p
+        L.oracle_hamming.argtypes = [P, P]
+        L.oracle_hamming.restype = C.c_int
+        L.oracle_three_maxima.argtypes = [P, C.c_int, P]
+        L.oracle_vocab_transform.argtypes = [C.c_int, P, P, P, P, P, P, C.c_int, P, C.c_int, P, P, P]
+        L.oracle_search_by_bow.argtypes = [P, P, C.c_float, C.c_int, C.c_int, P, P]
+        L.oracle_search_by_bow.restype = C.c_int
+        L._m_ready = True
+    return L
+
+
+def three_maxima(counts):
+    counts = np.ascontiguousarray(counts, np.int32)
+    ind = np.zeros(3, np.int32)
+    _mlib().oracle_three_maxima(_ptr(counts), len(counts), _ptr(ind))
+    return tuple(int(x) for x in ind)
+
+
+def vocab_children(parent):
+    n = len(parent)
+    cnt = np.bincount(parent[1:], minlength=n)
+    ptr = np.zeros(n + 1, np.int32)
+    ptr[1:] = np.cumsum(cnt)
+    order = np.argsort(parent[1:], kind="stable") + 1
+    return ptr, order.astype(np.int32)
+
+
+def vocab_transform(parent, is_leaf, desc_nodes, weight_nodes, L, desc, levelsup=4):
+    ptr, idx = vocab_children(parent)
+    leaf = np.ascontiguousarray(is_leaf, np.uint8).copy()
+    leaf[ptr[1:] == ptr[:-1]] = 1
+    word = np.full(len(parent), -1, np.int32)
+    word[np.nonzero(is_leaf)[0]] = np.arange(int(np.count_nonzero(is_leaf)), dtype=np.int32)
+    desc = np.ascontiguousarray(desc, np.uint8)
+    n = len(desc)
+    w = np.zeros(n, np.int32)
+    wt = np.zeros(n, np.float64)
+    nid = np.zeros(n, np.int32)
+    dn = np.ascontiguousarray(desc_nodes, np.uint8)
+    wn = np.ascontiguousarray(weight_nodes, np.float64)
+    _mlib().oracle_vocab_transform(L, _ptr(ptr), _ptr(idx), _ptr(dn), _ptr(leaf), _ptr(word), _ptr(wn), n,
+                                   _ptr(desc), levelsup, _ptr(w), _ptr(wt), _ptr(nid))
+    return w, wt, nid
+
+
+def search_by_bow(A, B, nnratio, check_ori, strict):
+    import slamhot
+    sa, ka = slamhot.make_bow_side(*A)
+    sb, kb = slamhot.make_bow_side(*B)
+    a2b = np.full(sa.n, -1, np.int32)
+    b2a = np.full(sb.n, -1, np.int32)
+    n = _mlib().oracle_search_by_bow(C.addressof(sa), C.addressof(sb), nnratio, int(check_ori), int(strict),
+                                     _ptr(a2b), _ptr(b2a))
+    return n, a2b, b2a

@@ -1,0 +1,103 @@
+"""GPU parity: vocabulary descent and SearchByBoW (both variants) vs the CPU oracle."""
+import numpy as np
+import pytest
+
+import oracle_bind as ob
+from slamhot import synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def vocab_arrays():
+    return synth.vocab(10, 6, 0)
+
+
+@pytest.fixture(scope="module")
+def gpu_vocab(vocab_arrays):
+    import slamhot
+    par, leaf, d, w = vocab_arrays
+    v = slamhot.Vocabulary(par, leaf, d, w, k=10, L=6)
+    yield v
+    v.close()
+
+
+@pytest.fixture(scope="module")
+def frames():
+    img0 = synth.frame(1, 752, 480)
+    out = []
+    for i, (dx, dy, a) in enumerate([(0, 0, 0), (3, 2, 2.0), (-4, 5, -4.0), (6, -3, 9.0)]):
+        img = img0 if i == 0 else synth.shifted(img0, dx, dy, a, 7 + i)
+        k, d, _ = ob.extract(img, ob.params(nfeatures=1200))
+        out.append((k, d))
+    return out
+
+
+def test_vocab_transform_bitexact(gpu_vocab, vocab_arrays, frames):
+    par, leaf, d, w = vocab_arrays
+    for levelsup in (4, 2, 6, 0):
+        for k, desc in frames:
+            wg, wtg, ng = gpu_vocab.transform(desc, levelsup)
+            wo, wto, no = ob.vocab_transform(par, leaf, d, w, 6, desc, levelsup)
+            assert np.array_equal(wg, wo)
+            assert np.array_equal(wtg, wto)
+            assert np.array_equal(ng, no)
+
+
+def _side(gpu_vocab, k, desc, valid):
+    _, wt, nid = gpu_vocab.transform(desc, 4)
+    return (desc, k["angle"], valid) + synth.feature_vector(nid, wt)
+
+
+@pytest.mark.parametrize("nnratio,check_ori", [(0.7, True), (0.75, True), (0.9, False), (0.6, True)])
+def test_search_by_bow_kf_frame(gpu_vocab, frames, nnratio, check_ori):
+    import slamhot
+    m = slamhot.ORBmatcher(nnratio, check_ori)
+    rng = np.random.default_rng(0)
+    for j in range(1, len(frames)):
+        k0, d0 = frames[0]
+        k1, d1 = frames[j]
+        valid = (rng.random(len(k0)) < 0.85).astype(np.uint8)
+        A = _side(gpu_vocab, k0, d0, valid)
+        B = _side(gpu_vocab, k1, d1, None)
+        ng, b2a_g = m.SearchByBoW_KF_F(A, B)
+        no, a2b_o, b2a_o = ob.search_by_bow(A, B, nnratio, check_ori, False)
+        assert ng == no
+        assert np.array_equal(b2a_g, b2a_o)
+    m.close()
+
+
+def test_search_by_bow_kf_kf(gpu_vocab, frames):
+    import slamhot
+    m = slamhot.ORBmatcher(0.75, True)
+    rng = np.random.default_rng(1)
+    k0, d0 = frames[0]
+    for j in range(1, len(frames)):
+        k1, d1 = frames[j]
+        A = _side(gpu_vocab, k0, d0, (rng.random(len(k0)) < 0.9).astype(np.uint8))
+        B = _side(gpu_vocab, k1, d1, (rng.random(len(k1)) < 0.9).astype(np.uint8))
+        ng, a2b_g = m.SearchByBoW_KF_KF(A, B)
+        no, a2b_o, b2a_o = ob.search_by_bow(A, B, 0.75, True, True)
+        assert ng == no
+        assert np.array_equal(a2b_g, a2b_o)
+    m.close()
+
+
+def test_search_by_bow_duplicates_and_ties(gpu_vocab):
+    """Identical descriptors inside one node: ties must resolve to the first candidate."""
+    import slamhot
+    rng = np.random.default_rng(5)
+    base = rng.integers(0, 256, (40, 32), dtype=np.uint8)
+    d0 = np.repeat(base, 3, axis=0)
+    d1 = np.repeat(base, 2, axis=0)
+    k0 = np.zeros(len(d0), ob.KP_DTYPE)
+    k1 = np.zeros(len(d1), ob.KP_DTYPE)
+    k0["angle"] = rng.uniform(0, 360, len(d0)).astype(np.float32)
+    k1["angle"] = rng.uniform(0, 360, len(d1)).astype(np.float32)
+    m = slamhot.ORBmatcher(1.0, True)
+    A = _side(gpu_vocab, k0, d0, None)
+    B = _side(gpu_vocab, k1, d1, None)
+    ng, b2a_g = m.SearchByBoW_KF_F(A, B)
+    no, _, b2a_o = ob.search_by_bow(A, B, 1.0, True, False)
+    assert ng == no and np.array_equal(b2a_g, b2a_o)
+    m.close()
