@@ -758,3 +758,26 @@ long oracle_extract_many(const slam_orb_params* p, int nframes, const uint8_t* i
 }
 
 }  // extern "C"
+
+// Exhaustive check of the device sincosf restatement (device_math.hpp, compiled for the host
+// here) against this host's glibc sincosf over every float in [lo, hi).  Returns mismatches.
+#include "../orb-slam3-noted_amd/csrc/device_math_host.hpp"
+extern "C" long oracle_check_sincosf(float lo, float hi) {
+    long bad = 0;
+    for (float f = lo; f < hi; f = std::nextafter(f, 1e30f)) {
+        float s1, c1, s2, c2;
+        sincosf(f, &s1, &c1);
+        slamhot::glibc_sincosf(f, &s2, &c2);
+        if (std::memcmp(&s1, &s2, 4) || std::memcmp(&c1, &c2, 4)) bad++;
+    }
+    return bad;
+}
+// device cv_fast_atan2 restatement vs the oracle's (same algorithm, separate code)
+extern "C" long oracle_check_atan2(int n, const float* ys, const float* xs) {
+    long bad = 0;
+    for (int i = 0; i < n; i++) {
+        const float a = fast_atan2(ys[i], xs[i]), b = slamhot::cv_fast_atan2(ys[i], xs[i]);
+        if (std::memcmp(&a, &b, 4)) bad++;
+    }
+    return bad;
+}

@@ -224,3 +224,19 @@ def search_by_bow(A, B, nnratio, check_ori, strict):
     n = _mlib().oracle_search_by_bow(C.addressof(sa), C.addressof(sb), nnratio, int(check_ori), int(strict),
                                      _ptr(a2b), _ptr(b2a))
     return n, a2b, b2a
+
+
+def check_sincosf(lo: float, hi: float) -> int:
+    L = lib()
+    L.oracle_check_sincosf.argtypes = [C.c_float, C.c_float]
+    L.oracle_check_sincosf.restype = C.c_long
+    return L.oracle_check_sincosf(lo, hi)
+
+
+def check_atan2(ys, xs) -> int:
+    L = lib()
+    L.oracle_check_atan2.argtypes = [C.c_int, C.c_void_p, C.c_void_p]
+    L.oracle_check_atan2.restype = C.c_long
+    ys = np.ascontiguousarray(ys, np.float32)
+    xs = np.ascontiguousarray(xs, np.float32)
+    return L.oracle_check_atan2(len(ys), _ptr(ys), _ptr(xs))
