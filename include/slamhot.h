@@ -182,6 +182,76 @@ slam_status slamhot_search_by_bow(slam_matcher* m, const slam_bow_side* A, const
                                   float nnratio, int check_ori, int strict, int32_t* a2b,
                                   int32_t* b2a, int* nmatches);
 
+/* ---------------------------------------------------------------------------------
+ * SearchByProjection (pinhole, Nleft == -1).  The current Frame as the matchers read it.
+ * ------------------------------------------------------------------------------- */
+typedef struct slam_frame_view {
+    int32_t n;
+    const slam_keypoint* kps_un;  /* mvKeysUn (pt, octave, angle) */
+    const float* uright;          /* mvuRight, -1 = no stereo; NULL = all -1 */
+    const uint8_t* desc;          /* mDescriptors, n x 32 */
+    const int8_t* mp_state;       /* mvpMapPoints on entry: -1 empty, 0 MapPoint without
+                                     observations, 1 MapPoint with Observations() > 0 */
+    float min_x, min_y, max_x, max_y;   /* mnMinX.. (Frame::ComputeImageBounds) */
+    float grid_inv_w, grid_inv_h;       /* mfGridElementWidthInv / HeightInv */
+    int32_t nlevels;
+    const float* scale;           /* mvScaleFactors */
+    float log_scale;              /* mfLogScaleFactor */
+    float fx, fy, cx, cy, bf, b;  /* Pinhole parameters, mbf, mb */
+    const float* Tcw;             /* 4x4 row-major float pose (B4, B6); NULL for B5 */
+} slam_frame_view;
+
+/* Per local MapPoint, the tracking fields Frame::isInFrustum (Frame.cc:493-570) leaves. */
+typedef struct slam_mp_track {
+    float proj_x, proj_y, proj_xr, depth, view_cos;
+    int32_t scale_level;
+    uint8_t in_view, is_bad, has_obs, pad;
+} slam_mp_track;
+
+/* int SearchByProjection(Frame& F, const vector<MapPoint*>& vpMapPoints, float th,
+ * bool bFarPoints, float thFarPoints) (ORBmatcher.cc:44-214).  f_match[i] = index of the
+ * MapPoint this call assigned to F feature i (the last assignment wins, as in the
+ * reference), -1 if untouched. */
+slam_status slamhot_search_by_projection_local(slam_matcher* m, const slam_frame_view* F, int n_mp,
+                                               const slam_mp_track* mps, const uint8_t* mp_desc,
+                                               float nnratio, float th, int far_points,
+                                               float th_far, int32_t* f_match, int* nmatches);
+
+/* The previous Frame for SearchByProjection(Frame&, const Frame& LastFrame, th, bMono)
+ * (ORBmatcher.cc:2173-2389): per last-frame feature its MapPoint (has_mp, outlier flag,
+ * world position, descriptor, Observations()>0) and keypoint octave/angle. */
+typedef struct slam_last_frame {
+    int32_t n;
+    const float* Tcw;             /* 4x4 row-major */
+    const slam_keypoint* kps;     /* mvKeys (octave) */
+    const slam_keypoint* kps_un;  /* mvKeysUn (angle) */
+    const uint8_t* has_mp;
+    const uint8_t* outlier;       /* mvbOutlier */
+    const float* mp_pos;          /* n x 3 world position */
+    const uint8_t* mp_desc;       /* n x 32 */
+    const uint8_t* mp_has_obs;
+} slam_last_frame;
+
+slam_status slamhot_search_by_projection_last(slam_matcher* m, const slam_frame_view* F,
+                                              const slam_last_frame* LF, float nnratio, int check_ori,
+                                              float th, int mono, int32_t* f_match, int* nmatches);
+
+/* Per KeyFrame feature for SearchByProjection(Frame&, KeyFrame*, const set<MapPoint*>&
+ * sAlreadyFound, float th, int ORBdist) (ORBmatcher.cc:2391-2513). */
+typedef struct slam_kf_points {
+    int32_t n;
+    const slam_keypoint* kps_un;  /* KF mvKeysUn (angle) */
+    const uint8_t* use;           /* MapPoint present, !isBad, not in sAlreadyFound */
+    const float* mp_pos;          /* n x 3 */
+    const float* max_dist;        /* mfMaxDistance */
+    const float* min_dist;        /* mfMinDistance */
+    const uint8_t* mp_desc;       /* n x 32 */
+} slam_kf_points;
+
+slam_status slamhot_search_by_projection_kf(slam_matcher* m, const slam_frame_view* F,
+                                            const slam_kf_points* KF, float nnratio, int check_ori,
+                                            float th, int orb_dist, int32_t* f_match, int* nmatches);
+
 #ifdef __cplusplus
 }
 #endif

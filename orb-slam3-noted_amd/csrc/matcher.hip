@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <functional>
 #include <mutex>
 #include <sstream>
 #include <string>
@@ -596,4 +597,591 @@ extern "C" slam_status slamhot_search_by_bow(slam_matcher* m, const slam_bow_sid
     std::copy(out.begin() + A->n, out.begin() + A->n + B->n, b2a);
     *nmatches = out[(size_t)A->n + B->n];
     return SLAM_OK;
+}
+
+// =======================================================================================
+// SearchByProjection (ORBmatcher.cc:44-214, 2173-2389, 2391-2513), pinhole.
+//
+// One workgroup per frame (1024 threads), one launch:
+//   1. per query (MapPoint): its search window — from Frame::isInFrustum's fields (local
+//      map), from projecting the last frame's MapPoints on the device (last frame; cv::Mat
+//      float products restated as double-accumulated gemm), or host-prepared (KeyFrame
+//      variant, whose PredictScale needs glibc logf);
+//   2. per query: Frame::GetFeaturesInArea over the 64x48 grid in the reference's
+//      candidate order (cell column, cell row, insertion order), static filters (levels,
+//      box, stereo gate, entry occupancy) and Hamming distances -> candidate lists;
+//   3. the reference processes queries sequentially and a match occupies the feature for
+//      the later queries.  Jacobi iteration of  choice(q) = f(candidates of q minus features
+//      owned by an earlier blocking query)  converges to exactly the sequential result
+//      (induction on q) — iterate until no choice changes;
+//   4. last assignment per feature wins; rotation histogram + ComputeThreeMaxima.
+// =======================================================================================
+namespace slamhot {
+
+constexpr int kGridCols = 64, kGridRows = 48;  // Frame.h:37-38
+
+struct DevProjFrame {
+    int n;
+    const slam_keypoint* kps;
+    const float* uright;
+    const uint8_t* desc;
+    const int8_t* state;          // entry mvpMapPoints state
+    const int32_t* cell_start;    // kGridCols*kGridRows + 1
+    const int32_t* cell_feat;
+    float min_x, min_y, max_x, max_y, inv_w, inv_h;
+    float fx, fy, cx, cy, bf, b;
+    float T[16];
+    float scale[16];
+    int nlevels;
+};
+
+struct ProjQuery {
+    float u, v, r;      // window centre and half size
+    float ur, er;       // stereo gate: skip candidates with uright > 0 && |ur - uright| > er (er < 0: off)
+    int16_t min_level, max_level;
+    int32_t valid;
+    float angle;        // for the rotation histogram
+    int32_t blocking;   // a match by this query occupies the feature for later queries
+};
+
+enum { kProjLocal = 0, kProjLast = 1, kProjKF = 2 };
+
+struct DevProjCall {
+    DevProjFrame F;
+    int mode, nq;
+    // local-map inputs
+    const slam_mp_track* mps;
+    float th, th_far, nnratio;
+    int far_points;
+    // last-frame inputs
+    const slam_keypoint* lf_kps;
+    const slam_keypoint* lf_kps_un;
+    const uint8_t* lf_has_mp;
+    const uint8_t* lf_outlier;
+    const float* lf_pos;
+    const uint8_t* lf_has_obs;
+    float LT[16];
+    int mono;
+    // prepared queries (KF variant) or scratch for computed ones
+    ProjQuery* queries;
+    const uint8_t* qdesc;   // nq x 32 query descriptors
+    int th_dist;            // acceptance threshold (TH_HIGH or ORBdist)
+    int check_ori;
+    // scratch / outputs
+    int32_t* cand_off;      // nq + 1
+    uint32_t* cand;         // (feature << 12) | dist   (capacity cand_cap)
+    int cand_cap;
+    int32_t* f_match;       // F.n
+    int32_t* out;           // [0] nmatches, [1] status (1 = candidate overflow), [2] iterations
+};
+
+__device__ __forceinline__ void gemm_rx_t(const float* T, const float* X, float* o) {
+    for (int i = 0; i < 3; i++) {
+        const double acc = (double)T[4 * i] * (double)X[0] + (double)T[4 * i + 1] * (double)X[1] +
+                           (double)T[4 * i + 2] * (double)X[2];
+        o[i] = (float)(acc * 1.0 + (double)T[4 * i + 3] * 1.0);
+    }
+}
+__device__ __forceinline__ void neg_rtt(const float* T, float* o) {
+    for (int i = 0; i < 3; i++) {
+        const double acc = (double)T[i] * (double)T[3] + (double)T[4 + i] * (double)T[7] +
+                           (double)T[8 + i] * (double)T[11];
+        o[i] = (float)(-1.0 * acc);
+    }
+}
+
+__device__ __forceinline__ int hamming_bytes(const uint8_t* a, const uint8_t* b) {
+    const uint4* pa = reinterpret_cast<const uint4*>(a);
+    const uint4* pb = reinterpret_cast<const uint4*>(b);
+    return hamming32(pa[0], pa[1], pb[0], pb[1]);
+}
+
+// Frame::GetFeaturesInArea window (Frame.cc:646-673); returns false when empty
+__device__ __forceinline__ bool grid_window(const DevProjFrame& F, float x, float y, float r, int& x0,
+                                            int& x1, int& y0, int& y1) {
+    x0 = max(0, (int)floorf((x - F.min_x - r) * F.inv_w));
+    if (x0 >= kGridCols) return false;
+    x1 = min(kGridCols - 1, (int)ceilf((x - F.min_x + r) * F.inv_w));
+    if (x1 < 0) return false;
+    y0 = max(0, (int)floorf((y - F.min_y - r) * F.inv_h));
+    if (y0 >= kGridRows) return false;
+    y1 = min(kGridRows - 1, (int)ceilf((y - F.min_y + r) * F.inv_h));
+    if (y1 < 0) return false;
+    return true;
+}
+
+// visit the candidates of query q in reference order; fn(feature)
+template <class Fn>
+__device__ __forceinline__ void for_candidates(const DevProjFrame& F, const ProjQuery& Q, Fn fn) {
+    int x0, x1, y0, y1;
+    if (!grid_window(F, Q.u, Q.v, Q.r, x0, x1, y0, y1)) return;
+    const bool check = (Q.min_level > 0) || (Q.max_level >= 0);
+    for (int ix = x0; ix <= x1; ix++) {
+        const int c0 = F.cell_start[ix * kGridRows + y0], c1 = F.cell_start[ix * kGridRows + y1 + 1];
+        for (int c = c0; c < c1; c++) {
+            const int idx = F.cell_feat[c];
+            const slam_keypoint kp = F.kps[idx];
+            if (check) {
+                if (kp.octave < Q.min_level) continue;
+                if (Q.max_level >= 0 && kp.octave > Q.max_level) continue;
+            }
+            const float dx = kp.x - Q.u, dy = kp.y - Q.v;
+            if (fabsf(dx) < Q.r && fabsf(dy) < Q.r) fn(idx, kp);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(1024) k_search_by_projection(DevProjCall C) {
+    __shared__ int scratch[20];
+    __shared__ int s_flag, s_hist[32], s_keep[3], s_count;
+    const DevProjFrame& F = C.F;
+    const int tid = threadIdx.x, NT = blockDim.x;
+    const int nq = C.nq;
+    // ---- 1. queries
+    if (C.mode == kProjLocal) {
+        const bool bFactor = C.th != 1.0f;
+        for (int q = tid; q < nq; q += NT) {
+            const slam_mp_track mp = C.mps[q];
+            ProjQuery Q;
+            Q.valid = mp.in_view && !(C.far_points && mp.depth > C.th_far) && !mp.is_bad;
+            const int level = min(max(mp.scale_level, 0), F.nlevels - 1);
+            float r = mp.view_cos > 0.998 ? 2.5f : 4.0f;  // RadiusByViewingCos
+            if (bFactor) r *= C.th;
+            Q.u = mp.proj_x;
+            Q.v = mp.proj_y;
+            Q.r = r * F.scale[level];
+            Q.ur = mp.proj_xr;
+            Q.er = r * F.scale[level];
+            Q.min_level = (int16_t)(mp.scale_level - 1);
+            Q.max_level = (int16_t)mp.scale_level;
+            Q.angle = 0.f;
+            Q.blocking = mp.has_obs;
+            C.queries[q] = Q;
+        }
+    } else if (C.mode == kProjLast) {
+        float twc[3], tlc[3];
+        neg_rtt(F.T, twc);
+        gemm_rx_t(C.LT, twc, tlc);
+        const bool fwd = tlc[2] > F.b && !C.mono;
+        const bool bwd = -tlc[2] > F.b && !C.mono;
+        for (int q = tid; q < nq; q += NT) {
+            ProjQuery Q;
+            Q.valid = 0;
+            Q.blocking = C.lf_has_obs[q];
+            Q.angle = C.lf_kps_un[q].angle;
+            Q.er = -1.f;
+            if (C.lf_has_mp[q] && !C.lf_outlier[q]) {
+                float xc[3];
+                gemm_rx_t(F.T, C.lf_pos + 3 * (size_t)q, xc);
+                const float invzc = (float)(1.0 / (double)xc[2]);
+                if (invzc >= 0) {
+                    const float u = F.fx * xc[0] / xc[2] + F.cx;
+                    const float v = F.fy * xc[1] / xc[2] + F.cy;
+                    if (!(u < F.min_x || u > F.max_x) && !(v < F.min_y || v > F.max_y)) {
+                        const int oct = C.lf_kps[q].octave;
+                        Q.valid = 1;
+                        Q.u = u;
+                        Q.v = v;
+                        Q.r = C.th * F.scale[min(max(oct, 0), F.nlevels - 1)];
+                        Q.ur = u - F.bf * invzc;
+                        Q.er = Q.r;
+                        if (fwd) { Q.min_level = (int16_t)oct; Q.max_level = -1; }
+                        else if (bwd) { Q.min_level = 0; Q.max_level = (int16_t)oct; }
+                        else { Q.min_level = (int16_t)(oct - 1); Q.max_level = (int16_t)(oct + 1); }
+                    }
+                }
+            }
+            C.queries[q] = Q;
+        }
+    }
+    __syncthreads();
+    // ---- 2. candidate lists: count, scan, fill (static filters + distances)
+    const bool any_blocks = C.mode == kProjKF;  // KF variant: any MapPoint occupies
+    auto pre_blocked = [&](int idx) -> bool {
+        const int st = F.state ? F.state[idx] : -1;
+        return any_blocks ? st >= 0 : st == 1;
+    };
+    auto stereo_ok = [&](const ProjQuery& Q, int idx) -> bool {
+        if (Q.er < 0.f || !F.uright) return true;
+        const float urr = F.uright[idx];
+        if (!(urr > 0)) return true;
+        return !(fabsf(Q.ur - urr) > Q.er);
+    };
+    int carry = 0;
+    for (int base = 0; base < nq; base += NT) {
+        const int q = base + tid;
+        int cnt = 0;
+        if (q < nq) {
+            const ProjQuery Q = C.queries[q];
+            if (Q.valid)
+                for_candidates(F, Q, [&](int idx, const slam_keypoint&) {
+                    if (!pre_blocked(idx) && stereo_ok(Q, idx)) cnt++;
+                });
+        }
+        int tot;
+        const int incl = block_scan_incl(cnt, scratch, &tot);
+        if (q < nq) C.cand_off[q] = carry + incl - cnt;
+        carry += tot;
+    }
+    if (tid == 0) C.cand_off[nq] = carry;
+    if (carry > C.cand_cap) {
+        if (tid == 0) C.out[1] = 1;
+        return;
+    }
+    __syncthreads();
+    for (int q = tid; q < nq; q += NT) {
+        const ProjQuery Q = C.queries[q];
+        if (!Q.valid) continue;
+        int w = C.cand_off[q];
+        const uint8_t* qd = C.qdesc + (size_t)q * 32;
+        for_candidates(F, Q, [&](int idx, const slam_keypoint&) {
+            if (!pre_blocked(idx) && stereo_ok(Q, idx))
+                C.cand[w++] = ((uint32_t)idx << 12) | (uint32_t)hamming_bytes(qd, F.desc + (size_t)idx * 32);
+        });
+    }
+    // ---- 3. Jacobi resolution of the sequential greedy (state in LDS: owner per
+    //         feature, two assignment buffers per query, final match per feature)
+    extern __shared__ __attribute__((aligned(16))) int32_t proj_smem[];
+    int32_t* owner = proj_smem;
+    int32_t* fm = owner + F.n;
+    int32_t* cur = fm + F.n;
+    int32_t* nxt = cur + nq;
+    for (int q = tid; q < nq; q += NT) cur[q] = -2;  // "not computed yet"
+    __syncthreads();
+    auto choose = [&](int q) -> int {
+        const int c0 = C.cand_off[q], c1 = C.cand_off[q + 1];
+        if (C.mode == kProjLocal) {
+            int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+            for (int c = c0; c < c1; c++) {
+                const int idx = (int)(C.cand[c] >> 12), dist = (int)(C.cand[c] & 0xFFF);
+                if (owner[idx] < q) continue;
+                if (dist < bestDist) {
+                    bestDist2 = bestDist;
+                    bestDist = dist;
+                    bestLevel2 = bestLevel;
+                    bestLevel = F.kps[idx].octave;
+                    bestIdx = idx;
+                } else if (dist < bestDist2) {
+                    bestLevel2 = F.kps[idx].octave;
+                    bestDist2 = dist;
+                }
+            }
+            if (bestDist <= 100) {
+                if (bestLevel == bestLevel2 && (float)bestDist > C.nnratio * (float)bestDist2) return -1;
+                if (bestLevel != bestLevel2 || (float)bestDist <= C.nnratio * (float)bestDist2) return bestIdx;
+            }
+            return -1;
+        }
+        int bestDist = 256, bestIdx = -1;
+        for (int c = c0; c < c1; c++) {
+            const int idx = (int)(C.cand[c] >> 12), dist = (int)(C.cand[c] & 0xFFF);
+            if (owner[idx] < q) continue;
+            if (dist < bestDist) {
+                bestDist = dist;
+                bestIdx = idx;
+            }
+        }
+        return bestDist <= C.th_dist ? bestIdx : -1;
+    };
+    int iters = 0;
+    for (; iters < nq + 2; iters++) {
+        for (int i = tid; i < F.n; i += NT) owner[i] = 0x7fffffff;
+        if (tid == 0) s_flag = 0;
+        __syncthreads();
+        for (int q = tid; q < nq; q += NT) {
+            const int a = cur[q];
+            if (a >= 0 && (any_blocks || C.queries[q].blocking)) atomicMin(&owner[a], q);
+        }
+        __syncthreads();
+        int changed = 0;
+        for (int q = tid; q < nq; q += NT) {
+            const int a = C.queries[q].valid ? choose(q) : -1;
+            nxt[q] = a;
+            changed |= a != cur[q];
+        }
+        if (changed) s_flag = 1;
+        __syncthreads();
+        int32_t* t = cur;
+        cur = nxt;
+        nxt = t;
+        const int fl = s_flag;
+        __syncthreads();
+        if (!fl) break;
+    }
+    // ---- 4. finalize: last assignment per feature wins; rotation consistency
+    for (int i = tid; i < F.n; i += NT) fm[i] = -1;
+    if (tid < 32) s_hist[tid] = 0;
+    if (tid == 0) s_count = 0;
+    __syncthreads();
+    int cnt = 0;
+    for (int q = tid; q < nq; q += NT) {
+        const int a = cur[q];
+        if (a >= 0) {
+            atomicMax(&fm[a], q);
+            cnt++;
+            if (C.check_ori) atomicAdd(&s_hist[rot_bin(C.queries[q].angle, F.kps[a].angle)], 1);
+        }
+    }
+    atomicAdd(&s_count, cnt);
+    __syncthreads();
+    if (C.check_ori) {
+        if (tid == 0) {
+            int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+            for (int i = 0; i < 30; i++) {
+                const int sv = s_hist[i];
+                if (sv > max1) { max3 = max2; max2 = max1; max1 = sv; ind3 = ind2; ind2 = ind1; ind1 = i; }
+                else if (sv > max2) { max3 = max2; max2 = sv; ind3 = ind2; ind2 = i; }
+                else if (sv > max3) { max3 = sv; ind3 = i; }
+            }
+            if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+            else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
+            s_keep[0] = ind1; s_keep[1] = ind2; s_keep[2] = ind3;
+        }
+        __syncthreads();
+        int drop = 0;
+        for (int q = tid; q < nq; q += NT) {
+            const int a = cur[q];
+            if (a >= 0) {
+                const int bin = rot_bin(C.queries[q].angle, F.kps[a].angle);
+                if (bin != s_keep[0] && bin != s_keep[1] && bin != s_keep[2]) {
+                    fm[a] = -1;  // nulled after all assignments (ORBmatcher.cc:2371-2386)
+                    drop++;
+                }
+            }
+        }
+        atomicSub(&s_count, drop);
+        __syncthreads();
+    }
+    for (int i = tid; i < F.n; i += NT) C.f_match[i] = fm[i];
+    if (tid == 0) {
+        C.out[0] = s_count;
+        C.out[2] = iters + 1;
+    }
+}
+
+}  // namespace slamhot
+
+namespace {
+
+// Frame::AssignFeaturesToGrid (Frame.cc:380-411) as CSR, cells ordered [ix][iy]
+void build_grid_csr(const slam_frame_view* F, std::vector<int32_t>& start, std::vector<int32_t>& feat) {
+    const int ncell = kGridCols * kGridRows;
+    std::vector<int32_t> cell(F->n, -1), cnt(ncell, 0);
+    for (int i = 0; i < F->n; i++) {
+        const slam_keypoint& kp = F->kps_un[i];
+        const int px = (int)std::round((kp.x - F->min_x) * F->grid_inv_w);
+        const int py = (int)std::round((kp.y - F->min_y) * F->grid_inv_h);
+        if (px < 0 || px >= kGridCols || py < 0 || py >= kGridRows) continue;
+        cell[i] = px * kGridRows + py;
+        cnt[cell[i]]++;
+    }
+    start.assign(ncell + 1, 0);
+    for (int c = 0; c < ncell; c++) start[c + 1] = start[c] + cnt[c];
+    feat.assign(std::max(1, start[ncell]), 0);
+    std::vector<int32_t> fill(start.begin(), start.end() - 1);
+    for (int i = 0; i < F->n; i++)
+        if (cell[i] >= 0) feat[fill[cell[i]]++] = i;
+}
+
+struct Blob {  // bump allocator over one device buffer, uploads from host
+    uint8_t* base;
+    size_t off = 0;
+    hipStream_t s;
+    template <class T>
+    const T* put(const T* host, size_t count) {
+        if (!host || !count) return nullptr;
+        uint8_t* p = base + off;
+        off += (count * sizeof(T) + 255) & ~(size_t)255;
+        (void)hipMemcpyAsync(p, host, count * sizeof(T), hipMemcpyHostToDevice, s);
+        return reinterpret_cast<const T*>(p);
+    }
+    template <class T>
+    T* take(size_t count) {
+        uint8_t* p = base + off;
+        off += (count * sizeof(T) + 255) & ~(size_t)255;
+        return reinterpret_cast<T*>(p);
+    }
+};
+
+bool frame_ok(const slam_frame_view* F) {
+    return F && F->n >= 0 && F->n < (1 << 20) && (F->n == 0 || (F->kps_un && F->desc)) && F->nlevels >= 1 &&
+           F->nlevels <= 16 && F->scale;
+}
+
+slam_status run_projection(slam_matcher* m, const slam_frame_view* F, DevProjCall& Cc, int nq,
+                           const std::vector<ProjQuery>* host_queries, const uint8_t* qdesc,
+                           int32_t* f_match, int* nmatches,
+                           const std::function<void(Blob&, DevProjCall&)>& put_inputs) {
+    std::lock_guard<std::mutex> g(m->mu);
+    SLAM_HIP_TRY(hipSetDevice(m->device));
+    std::vector<int32_t> start, feat;
+    build_grid_csr(F, start, feat);
+    int cap = std::max(4096, nq * 64);
+    for (int attempt = 0; attempt < 2; attempt++) {
+        const size_t need = (size_t)F->n * (sizeof(slam_keypoint) + 4 + 32 + 1 + 4 * 2) + start.size() * 4 +
+                            feat.size() * 4 + (size_t)nq * (sizeof(ProjQuery) + 32 + 4 * 3 + sizeof(slam_mp_track) + 64) +
+                            (size_t)cap * 4 + 64 * 1024;
+        slam_status st;
+        if ((st = m->d_a.ensure(need * 2))) return st;
+        Blob B{m->d_a.as<uint8_t>(), 0, m->stream};
+        DevProjCall C = Cc;
+        C.F.n = F->n;
+        C.F.kps = B.put(F->kps_un, F->n);
+        C.F.uright = B.put(F->uright, F->n);
+        C.F.desc = B.put(F->desc, (size_t)F->n * 32);
+        C.F.state = B.put(F->mp_state, F->n);
+        C.F.cell_start = B.put(start.data(), start.size());
+        C.F.cell_feat = B.put(feat.data(), feat.size());
+        put_inputs(B, C);
+        C.nq = nq;
+        if (host_queries) C.queries = const_cast<ProjQuery*>(B.put(host_queries->data(), host_queries->size()));
+        else C.queries = B.take<ProjQuery>(std::max(1, nq));
+        C.qdesc = B.put(qdesc, (size_t)nq * 32);
+        C.cand_off = B.take<int32_t>(nq + 1);
+        C.cand = B.take<uint32_t>(cap);
+        C.cand_cap = cap;
+        C.f_match = B.take<int32_t>(std::max(1, F->n));
+        C.out = B.take<int32_t>(4);
+        SLAM_HIP_TRY(hipMemsetAsync(C.out, 0, 16, m->stream));
+        const size_t lds = (size_t)4 * (2 * (size_t)F->n + 2 * (size_t)nq);
+        if (lds > 150 * 1024) return SLAM_EINVAL;
+        SLAM_HIP_TRY(hipFuncSetAttribute((const void*)k_search_by_projection,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds + 16));
+        hipLaunchKernelGGL(k_search_by_projection, dim3(1), dim3(1024), lds, m->stream, C);
+        SLAM_HIP_TRY(hipGetLastError());
+        int32_t out[4];
+        SLAM_HIP_TRY(hipMemcpyAsync(out, C.out, 16, hipMemcpyDeviceToHost, m->stream));
+        if (F->n) SLAM_HIP_TRY(hipMemcpyAsync(f_match, C.f_match, (size_t)F->n * 4, hipMemcpyDeviceToHost, m->stream));
+        SLAM_HIP_TRY(hipStreamSynchronize(m->stream));
+        if (out[1] == 1) {  // candidate overflow: exact size is cand_off[nq]
+            int32_t total = 0;
+            SLAM_HIP_TRY(hipMemcpy(&total, C.cand_off + nq, 4, hipMemcpyDeviceToHost));
+            cap = total + 1024;
+            continue;
+        }
+        *nmatches = out[0];
+        return SLAM_OK;
+    }
+    return SLAM_EINVAL;
+}
+
+void fill_frame(DevProjCall& C, const slam_frame_view* F) {
+    C.F.min_x = F->min_x;
+    C.F.min_y = F->min_y;
+    C.F.max_x = F->max_x;
+    C.F.max_y = F->max_y;
+    C.F.inv_w = F->grid_inv_w;
+    C.F.inv_h = F->grid_inv_h;
+    C.F.fx = F->fx;
+    C.F.fy = F->fy;
+    C.F.cx = F->cx;
+    C.F.cy = F->cy;
+    C.F.bf = F->bf;
+    C.F.b = F->b;
+    C.F.nlevels = F->nlevels;
+    for (int i = 0; i < 16; i++) {
+        C.F.T[i] = F->Tcw ? F->Tcw[i] : 0.f;
+        C.F.scale[i] = i < F->nlevels ? F->scale[i] : 1.f;
+    }
+}
+
+}  // namespace
+
+extern "C" slam_status slamhot_search_by_projection_local(slam_matcher* m, const slam_frame_view* F, int n_mp,
+                                                          const slam_mp_track* mps, const uint8_t* mp_desc,
+                                                          float nnratio, float th, int far_points, float th_far,
+                                                          int32_t* f_match, int* nmatches) {
+    if (!m || !frame_ok(F) || n_mp < 0 || (n_mp && (!mps || !mp_desc)) || !f_match || !nmatches) return SLAM_EINVAL;
+    DevProjCall C{};
+    fill_frame(C, F);
+    C.mode = kProjLocal;
+    C.th = th;
+    C.th_far = th_far;
+    C.far_points = far_points;
+    C.nnratio = nnratio;
+    C.th_dist = 100;
+    C.check_ori = 0;
+    return run_projection(m, F, C, n_mp, nullptr, mp_desc, f_match, nmatches,
+                          [&](Blob& B, DevProjCall& c) { c.mps = B.put(mps, n_mp); });
+}
+
+extern "C" slam_status slamhot_search_by_projection_last(slam_matcher* m, const slam_frame_view* F,
+                                                         const slam_last_frame* LF, float nnratio, int check_ori,
+                                                         float th, int mono, int32_t* f_match, int* nmatches) {
+    if (!m || !frame_ok(F) || !F->Tcw || !LF || !LF->Tcw || LF->n < 0 || !f_match || !nmatches) return SLAM_EINVAL;
+    if (LF->n && (!LF->kps || !LF->kps_un || !LF->has_mp || !LF->outlier || !LF->mp_pos || !LF->mp_desc ||
+                  !LF->mp_has_obs))
+        return SLAM_EINVAL;
+    DevProjCall C{};
+    fill_frame(C, F);
+    C.mode = kProjLast;
+    C.th = th;
+    C.mono = mono;
+    C.nnratio = nnratio;
+    C.th_dist = 100;
+    C.check_ori = check_ori;
+    for (int i = 0; i < 16; i++) C.LT[i] = LF->Tcw[i];
+    return run_projection(m, F, C, LF->n, nullptr, LF->mp_desc, f_match, nmatches, [&](Blob& B, DevProjCall& c) {
+        c.lf_kps = B.put(LF->kps, LF->n);
+        c.lf_kps_un = B.put(LF->kps_un, LF->n);
+        c.lf_has_mp = B.put(LF->has_mp, LF->n);
+        c.lf_outlier = B.put(LF->outlier, LF->n);
+        c.lf_pos = B.put(LF->mp_pos, (size_t)LF->n * 3);
+        c.lf_has_obs = B.put(LF->mp_has_obs, LF->n);
+    });
+}
+
+// The KeyFrame variant's per-MapPoint geometry (projection, distance gate and
+// MapPoint::PredictScale with glibc logf, MapPoint.cc:551-566) runs here on the host, in
+// the reference's arithmetic; candidate search and resolution run on the device.
+extern "C" slam_status slamhot_search_by_projection_kf(slam_matcher* m, const slam_frame_view* F,
+                                                       const slam_kf_points* KF, float nnratio, int check_ori,
+                                                       float th, int orb_dist, int32_t* f_match, int* nmatches) {
+    if (!m || !frame_ok(F) || !F->Tcw || !KF || KF->n < 0 || !f_match || !nmatches) return SLAM_EINVAL;
+    if (KF->n && (!KF->kps_un || !KF->use || !KF->mp_pos || !KF->max_dist || !KF->min_dist || !KF->mp_desc))
+        return SLAM_EINVAL;
+    (void)nnratio;
+    const float* T = F->Tcw;
+    float Ow[3];
+    for (int i = 0; i < 3; i++) {
+        const double acc = (double)T[i] * T[3] + (double)T[4 + i] * T[7] + (double)T[8 + i] * T[11];
+        Ow[i] = (float)(-1.0 * acc);
+    }
+    std::vector<ProjQuery> qs(KF->n);
+    for (int i = 0; i < KF->n; i++) {
+        ProjQuery& Q = qs[i];
+        Q.valid = 0;
+        Q.blocking = 1;
+        Q.er = -1.f;
+        Q.angle = KF->kps_un[i].angle;
+        if (!KF->use[i]) continue;
+        const float* X = KF->mp_pos + 3 * (size_t)i;
+        float xc[3];
+        for (int r = 0; r < 3; r++) {
+            const double acc = (double)T[4 * r] * X[0] + (double)T[4 * r + 1] * X[1] + (double)T[4 * r + 2] * X[2];
+            xc[r] = (float)(acc * 1.0 + (double)T[4 * r + 3] * 1.0);
+        }
+        const float u = F->fx * xc[0] / xc[2] + F->cx;
+        const float v = F->fy * xc[1] / xc[2] + F->cy;
+        if (u < F->min_x || u > F->max_x || v < F->min_y || v > F->max_y) continue;
+        const float PO[3] = {X[0] - Ow[0], X[1] - Ow[1], X[2] - Ow[2]};
+        const float dist3D = (float)std::sqrt((double)PO[0] * PO[0] + (double)PO[1] * PO[1] + (double)PO[2] * PO[2]);
+        if (dist3D < 0.8f * KF->min_dist[i] || dist3D > 1.2f * KF->max_dist[i]) continue;
+        const float ratio = KF->max_dist[i] / dist3D;
+        int level = (int)std::ceil(std::log(ratio) / F->log_scale);
+        if (level < 0) level = 0;
+        else if (level >= F->nlevels) level = F->nlevels - 1;
+        Q.valid = 1;
+        Q.u = u;
+        Q.v = v;
+        Q.r = th * F->scale[level];
+        Q.min_level = (int16_t)(level - 1);
+        Q.max_level = (int16_t)(level + 1);
+    }
+    DevProjCall C{};
+    fill_frame(C, F);
+    C.mode = kProjKF;
+    C.th_dist = orb_dist;
+    C.check_ori = check_ori;
+    return run_projection(m, F, C, KF->n, &qs, KF->mp_desc, f_match, nmatches, [](Blob&, DevProjCall&) {});
 }

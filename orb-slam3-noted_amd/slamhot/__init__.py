@@ -50,6 +50,83 @@ def make_bow_side(desc, angle, valid, node_id, node_off, node_feat):
     return s, arrs
 
 
+class FrameView(C.Structure):
+    _fields_ = [("n", C.c_int32), ("kps_un", C.c_void_p), ("uright", C.c_void_p), ("desc", C.c_void_p),
+                ("mp_state", C.c_void_p), ("min_x", C.c_float), ("min_y", C.c_float), ("max_x", C.c_float),
+                ("max_y", C.c_float), ("grid_inv_w", C.c_float), ("grid_inv_h", C.c_float),
+                ("nlevels", C.c_int32), ("scale", C.c_void_p), ("log_scale", C.c_float), ("fx", C.c_float),
+                ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float), ("bf", C.c_float), ("b", C.c_float),
+                ("Tcw", C.c_void_p)]
+
+
+MP_TRACK_DTYPE = np.dtype([("proj_x", "<f4"), ("proj_y", "<f4"), ("proj_xr", "<f4"), ("depth", "<f4"),
+                           ("view_cos", "<f4"), ("scale_level", "<i4"), ("in_view", "u1"), ("is_bad", "u1"),
+                           ("has_obs", "u1"), ("pad", "u1")])
+
+
+class LastFrameView(C.Structure):
+    _fields_ = [("n", C.c_int32), ("Tcw", C.c_void_p), ("kps", C.c_void_p), ("kps_un", C.c_void_p),
+                ("has_mp", C.c_void_p), ("outlier", C.c_void_p), ("mp_pos", C.c_void_p), ("mp_desc", C.c_void_p),
+                ("mp_has_obs", C.c_void_p)]
+
+
+class KFPointsView(C.Structure):
+    _fields_ = [("n", C.c_int32), ("kps_un", C.c_void_p), ("use", C.c_void_p), ("mp_pos", C.c_void_p),
+                ("max_dist", C.c_void_p), ("min_dist", C.c_void_p), ("mp_desc", C.c_void_p)]
+
+
+def _keep(a, dt):
+    return None if a is None else np.ascontiguousarray(a, dt)
+
+
+def make_frame_view(kps_un, desc, uright=None, mp_state=None, width=752, height=480, scale=None,
+                    scale_factor=1.2, cam=(435.2047, 435.2047, 367.4517, 252.2009), bf=47.9064, Tcw=None):
+    """slam_frame_view for an undistorted pinhole frame (bounds 0..width/height,
+    Frame::ComputeImageBounds with k1 = 0); returns (struct, keepalive)."""
+    kps_un = np.ascontiguousarray(kps_un)
+    assert kps_un.dtype == KP_DTYPE
+    if scale is None:
+        scale = [1.0]
+        for _ in range(7):
+            scale.append(float(np.float32(np.float64(np.float32(scale[-1])) * np.float64(np.float32(scale_factor)))))
+    arrs = dict(kps=kps_un, desc=_keep(desc, np.uint8), uright=_keep(uright, np.float32),
+                state=_keep(mp_state, np.int8), scale=np.ascontiguousarray(scale, np.float32),
+                T=_keep(Tcw, np.float32))
+    ptr = lambda a: None if a is None else a.ctypes.data_as(C.c_void_p)
+    f32 = np.float32
+    v = FrameView()
+    v.n = len(kps_un)
+    v.kps_un, v.uright, v.desc, v.mp_state = ptr(arrs["kps"]), ptr(arrs["uright"]), ptr(arrs["desc"]), ptr(arrs["state"])
+    v.min_x, v.min_y, v.max_x, v.max_y = 0.0, 0.0, float(width), float(height)
+    v.grid_inv_w = float(f32(64) / f32(width))
+    v.grid_inv_h = float(f32(48) / f32(height))
+    v.nlevels = len(scale)
+    v.scale = ptr(arrs["scale"])
+    v.log_scale = float(np.log(f32(scale_factor)))
+    v.fx, v.fy, v.cx, v.cy = cam
+    v.bf = bf
+    v.b = float(f32(bf) / f32(cam[0]))
+    v.Tcw = ptr(arrs["T"])
+    return v, arrs
+
+
+def make_last_frame(Tcw, kps, kps_un, has_mp, outlier, mp_pos, mp_desc, mp_has_obs):
+    arrs = [np.ascontiguousarray(Tcw, np.float32), np.ascontiguousarray(kps), np.ascontiguousarray(kps_un),
+            np.ascontiguousarray(has_mp, np.uint8), np.ascontiguousarray(outlier, np.uint8),
+            np.ascontiguousarray(mp_pos, np.float32), np.ascontiguousarray(mp_desc, np.uint8),
+            np.ascontiguousarray(mp_has_obs, np.uint8)]
+    p = [a.ctypes.data_as(C.c_void_p) for a in arrs]
+    return LastFrameView(len(arrs[2]), *p), arrs
+
+
+def make_kf_points(kps_un, use, mp_pos, max_dist, min_dist, mp_desc):
+    arrs = [np.ascontiguousarray(kps_un), np.ascontiguousarray(use, np.uint8), np.ascontiguousarray(mp_pos, np.float32),
+            np.ascontiguousarray(max_dist, np.float32), np.ascontiguousarray(min_dist, np.float32),
+            np.ascontiguousarray(mp_desc, np.uint8)]
+    p = [a.ctypes.data_as(C.c_void_p) for a in arrs]
+    return KFPointsView(len(arrs[0]), *p), arrs
+
+
 _lib = None
 P = C.c_void_p
 I = C.c_int
@@ -94,6 +171,12 @@ def lib() -> C.CDLL:
     L.slamhot_matcher_destroy.restype = None
     L.slamhot_search_by_bow.argtypes = [P, C.POINTER(BowSide), C.POINTER(BowSide), C.c_float, I, I, P, P,
                                         C.POINTER(I)]
+    L.slamhot_search_by_projection_local.argtypes = [P, C.POINTER(FrameView), I, P, P, C.c_float, C.c_float, I,
+                                                     C.c_float, P, C.POINTER(I)]
+    L.slamhot_search_by_projection_last.argtypes = [P, C.POINTER(FrameView), C.POINTER(LastFrameView), C.c_float, I,
+                                                    C.c_float, I, P, C.POINTER(I)]
+    L.slamhot_search_by_projection_kf.argtypes = [P, C.POINTER(FrameView), C.POINTER(KFPointsView), C.c_float, I,
+                                                  C.c_float, I, P, C.POINTER(I)]
     _lib = L
     return L
 
@@ -315,3 +398,41 @@ class ORBmatcher:
         per-KF1-feature matched KF2 feature index or -1)."""
         n, a2b, b2a = self._bow(kf1, kf2, 1)
         return n, a2b
+
+
+def _matcher_methods():
+    def SearchByProjection_local(self, frame_view, mps, mp_desc, th=3.0, bFarPoints=False, thFarPoints=50.0):
+        """int SearchByProjection(Frame&, const vector<MapPoint*>&, th, bFarPoints, thFarPoints)."""
+        mps = np.ascontiguousarray(mps, MP_TRACK_DTYPE)
+        mp_desc = np.ascontiguousarray(mp_desc, np.uint8)
+        fm = np.full(frame_view.n, -1, np.int32)
+        nm = I(0)
+        check(lib().slamhot_search_by_projection_local(self._h, C.byref(frame_view), len(mps), _ptr(mps),
+                                                       _ptr(mp_desc), self.mfNNratio, th, int(bFarPoints),
+                                                       thFarPoints, _ptr(fm), C.byref(nm)), "search_by_projection_local")
+        return nm.value, fm
+
+    def SearchByProjection_last(self, frame_view, last_view, th, bMono):
+        """int SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, th, bMono)."""
+        fm = np.full(frame_view.n, -1, np.int32)
+        nm = I(0)
+        check(lib().slamhot_search_by_projection_last(self._h, C.byref(frame_view), C.byref(last_view),
+                                                      self.mfNNratio, int(self.mbCheckOrientation), th, int(bMono),
+                                                      _ptr(fm), C.byref(nm)), "search_by_projection_last")
+        return nm.value, fm
+
+    def SearchByProjection_kf(self, frame_view, kf_view, th, ORBdist):
+        """int SearchByProjection(Frame&, KeyFrame*, const set<MapPoint*>&, th, ORBdist)."""
+        fm = np.full(frame_view.n, -1, np.int32)
+        nm = I(0)
+        check(lib().slamhot_search_by_projection_kf(self._h, C.byref(frame_view), C.byref(kf_view), self.mfNNratio,
+                                                    int(self.mbCheckOrientation), th, int(ORBdist), _ptr(fm),
+                                                    C.byref(nm)), "search_by_projection_kf")
+        return nm.value, fm
+
+    ORBmatcher.SearchByProjection_local = SearchByProjection_local
+    ORBmatcher.SearchByProjection_last = SearchByProjection_last
+    ORBmatcher.SearchByProjection_kf = SearchByProjection_kf
+
+
+_matcher_methods()

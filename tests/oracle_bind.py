@@ -240,3 +240,42 @@ def check_atan2(ys, xs) -> int:
     ys = np.ascontiguousarray(ys, np.float32)
     xs = np.ascontiguousarray(xs, np.float32)
     return L.oracle_check_atan2(len(ys), _ptr(ys), _ptr(xs))
+
+
+# ---- projection matchers (oracle/projection_oracle.cpp)
+def _plib():
+    L = lib()
+    if not hasattr(L, "_p_ready"):
+        P = C.c_void_p
+        L.oracle_search_by_projection_local.argtypes = [P, C.c_int, P, P, C.c_float, C.c_float, C.c_int, C.c_float, P]
+        L.oracle_search_by_projection_local.restype = C.c_int
+        L.oracle_search_by_projection_last.argtypes = [P, P, C.c_float, C.c_int, C.c_float, C.c_int, P]
+        L.oracle_search_by_projection_last.restype = C.c_int
+        L.oracle_search_by_projection_kf.argtypes = [P, P, C.c_float, C.c_int, C.c_float, C.c_int, P]
+        L.oracle_search_by_projection_kf.restype = C.c_int
+        L._p_ready = True
+    return L
+
+
+def search_by_projection_local(fv, mps, mp_desc, nnratio, th, far, th_far):
+    import slamhot
+    mps = np.ascontiguousarray(mps, slamhot.MP_TRACK_DTYPE)
+    mp_desc = np.ascontiguousarray(mp_desc, np.uint8)
+    fm = np.full(fv.n, -1, np.int32)
+    n = _plib().oracle_search_by_projection_local(C.addressof(fv), len(mps), _ptr(mps), _ptr(mp_desc), nnratio, th,
+                                                  int(far), th_far, _ptr(fm))
+    return n, fm
+
+
+def search_by_projection_last(fv, lf, nnratio, check_ori, th, mono):
+    fm = np.full(fv.n, -1, np.int32)
+    n = _plib().oracle_search_by_projection_last(C.addressof(fv), C.addressof(lf), nnratio, int(check_ori), th, int(mono),
+                                                 _ptr(fm))
+    return n, fm
+
+
+def search_by_projection_kf(fv, kf, nnratio, check_ori, th, orb_dist):
+    fm = np.full(fv.n, -1, np.int32)
+    n = _plib().oracle_search_by_projection_kf(C.addressof(fv), C.addressof(kf), nnratio, int(check_ori), th,
+                                               int(orb_dist), _ptr(fm))
+    return n, fm

@@ -1,0 +1,129 @@
+"""Seeded synthetic tracking scenes for the projection matchers (shared by CPU and GPU tests).
+EuRoC stereo intrinsics (Examples/Stereo/EuRoC.yaml:8-31)."""
+import numpy as np
+
+import oracle_bind as ob
+import slamhot
+from slamhot import synth
+
+FX = FY = np.float32(435.2047)
+CX, CY = np.float32(367.4517), np.float32(252.2009)
+BF = np.float32(47.9064)
+
+
+def rot(ax, ay, az):
+    cx, sx, cy, sy, cz, sz = np.cos(ax), np.sin(ax), np.cos(ay), np.sin(ay), np.cos(az), np.sin(az)
+    Rx = np.array([[1, 0, 0], [0, cx, -sx], [0, sx, cx]])
+    Ry = np.array([[cy, 0, sy], [0, 1, 0], [-sy, 0, cy]])
+    Rz = np.array([[cz, -sz, 0], [sz, cz, 0], [0, 0, 1]])
+    return Rz @ Ry @ Rx
+
+
+def pose(R, t):
+    T = np.eye(4)
+    T[:3, :3] = R
+    T[:3, 3] = t
+    return T.astype(np.float32)
+
+
+def flip_bits(desc, rng, max_flips):
+    bits = np.unpackbits(desc, axis=1)
+    for i in range(len(bits)):
+        k = rng.integers(0, max_flips + 1)
+        bits[i, rng.choice(256, size=k, replace=False)] ^= 1
+    return np.packbits(bits, axis=1)
+
+
+def current_frame(seed, n_feat=1200):
+    img = synth.frame(seed, 752, 480)
+    k, d, _ = ob.extract(img, ob.params(nfeatures=n_feat))
+    return k, d
+
+
+def scene(seed, n_feat=1200):
+    rng = np.random.default_rng(seed)
+    k, d = current_frame(seed, n_feat)
+    n = len(k)
+    uright = np.where(rng.random(n) < 0.6, k["x"] - rng.uniform(5, 40, n), -1).astype(np.float32)
+    state = np.full(n, -1, np.int8)
+    r = rng.random(n)
+    state[r < 0.05] = 0
+    state[(r >= 0.05) & (r < 0.10)] = 1
+    Tcw = pose(rot(*rng.normal(0, 0.05, 3)), rng.normal(0, 0.3, 3))
+    return dict(rng=rng, k=k, d=d, uright=uright, state=state, Tcw=Tcw)
+
+
+def frame_view(S, with_pose=True):
+    return slamhot.make_frame_view(S["k"], S["d"], S["uright"], S["state"], Tcw=S["Tcw"] if with_pose else None)
+
+
+def local_map(S, n_extra=400):
+    rng, k, d = S["rng"], S["k"], S["d"]
+    n = len(k)
+    sel = rng.permutation(n)[: int(n * 0.8)]
+    m = len(sel) + n_extra
+    mps = np.zeros(m, slamhot.MP_TRACK_DTYPE)
+    desc = np.zeros((m, 32), np.uint8)
+    jit = rng.normal(0, 1.2, (len(sel), 2)).astype(np.float32)
+    mps["proj_x"][: len(sel)] = k["x"][sel] + jit[:, 0]
+    mps["proj_y"][: len(sel)] = k["y"][sel] + jit[:, 1]
+    mps["scale_level"][: len(sel)] = np.clip(k["octave"][sel] + rng.integers(-1, 2, len(sel)), 0, 7)
+    desc[: len(sel)] = flip_bits(d[sel], rng, 40)
+    mps["proj_x"][len(sel):] = rng.uniform(0, 752, n_extra)
+    mps["proj_y"][len(sel):] = rng.uniform(0, 480, n_extra)
+    mps["scale_level"][len(sel):] = rng.integers(0, 8, n_extra)
+    desc[len(sel):] = flip_bits(d[rng.integers(0, n, n_extra)], rng, 90)
+    ur = S["uright"]
+    base_ur = np.concatenate([np.where(ur[sel] > 0, ur[sel], mps["proj_x"][: len(sel)] - 20), mps["proj_x"][len(sel):] - 15])
+    mps["proj_xr"] = (base_ur + rng.normal(0, 3, m)).astype(np.float32)
+    mps["depth"] = rng.uniform(0.5, 80, m)
+    mps["view_cos"] = rng.uniform(0.99, 1.0, m)
+    mps["in_view"] = rng.random(m) < 0.95
+    mps["is_bad"] = rng.random(m) < 0.03
+    mps["has_obs"] = rng.random(m) < 0.9
+    order = rng.permutation(m)
+    return mps[order], desc[order]
+
+
+def backproject(S, x, y, depth):
+    Xc = np.stack([(x - CX) / FX * depth, (y - CY) / FY * depth, depth], 1)
+    T = S["Tcw"].astype(np.float64)
+    R, t = T[:3, :3], T[:3, 3]
+    return ((Xc - t) @ R).astype(np.float32)
+
+
+def last_frame(S, mono=False, motion=0.02):
+    rng, k, d = S["rng"], S["k"], S["d"]
+    n = len(k)
+    depth = rng.uniform(1.0, 20.0, n).astype(np.float32)
+    Xw = backproject(S, k["x"] + rng.normal(0, 1.0, n), k["y"] + rng.normal(0, 1.0, n), depth)
+    T = S["Tcw"].astype(np.float64)
+    Tl = pose(rot(*rng.normal(0, 0.01, 3)) @ T[:3, :3], T[:3, 3] + rng.normal(0, motion, 3))
+    kl = k.copy()
+    kl["octave"] = np.clip(k["octave"] + rng.integers(-1, 2, n), 0, 7)
+    kl_un = kl.copy()
+    kl_un["angle"] = np.where(rng.random(n) < 0.8, (k["angle"] + rng.normal(0, 8, n)) % 360,
+                              rng.uniform(0, 360, n)).astype(np.float32)
+    has_mp = rng.random(n) < 0.85
+    outlier = rng.random(n) < 0.05
+    has_obs = rng.random(n) < 0.9
+    desc = flip_bits(d, rng, 45)
+    order = rng.permutation(n)
+    return slamhot.make_last_frame(Tl, kl[order], kl_un[order], has_mp[order], outlier[order], Xw[order], desc[order],
+                                   has_obs[order])
+
+
+def kf_points(S):
+    rng, k, d = S["rng"], S["k"], S["d"]
+    n = len(k)
+    depth = rng.uniform(1.0, 20.0, n).astype(np.float32)
+    Xw = backproject(S, k["x"] + rng.normal(0, 1.0, n), k["y"] + rng.normal(0, 1.0, n), depth)
+    max_d = (depth * rng.uniform(1.0, 3.0, n)).astype(np.float32)
+    min_d = (max_d / np.float32(1.2 ** 7)).astype(np.float32)
+    kk = k.copy()
+    kk["angle"] = np.where(rng.random(n) < 0.8, (k["angle"] + rng.normal(0, 8, n)) % 360,
+                           rng.uniform(0, 360, n)).astype(np.float32)
+    use = rng.random(n) < 0.9
+    desc = flip_bits(d, rng, 45)
+    order = rng.permutation(n)
+    return slamhot.make_kf_points(kk[order], use[order], Xw[order], max_d[order], min_d[order], desc[order])

@@ -1,0 +1,54 @@
+"""GPU parity: SearchByProjection (local map, last frame, keyframe) vs the CPU oracle."""
+import numpy as np
+import pytest
+
+import oracle_bind as ob
+import scenes
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+@pytest.mark.parametrize("th,far,nnratio", [(1.0, False, 0.8), (3.0, False, 0.8), (5.0, True, 0.9), (1.0, False, 0.6)])
+def test_local_map(seed, th, far, nnratio):
+    import slamhot
+    S = scenes.scene(seed)
+    fv, keep = scenes.frame_view(S, with_pose=False)
+    mps, desc = scenes.local_map(S)
+    m = slamhot.ORBmatcher(nnratio)
+    ng, fg = m.SearchByProjection_local(fv, mps, desc, th, far, 20.0)
+    no, fo = ob.search_by_projection_local(fv, mps, desc, nnratio, th, far, 20.0)
+    m.close()
+    assert ng == no and ng > 50
+    assert np.array_equal(fg, fo)
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+@pytest.mark.parametrize("th,mono,check_ori", [(7.0, False, True), (15.0, True, True), (7.0, False, False),
+                                               (14.0, False, True)])
+def test_last_frame(seed, th, mono, check_ori):
+    import slamhot
+    S = scenes.scene(seed)
+    fv, keep = scenes.frame_view(S)
+    lf, lkeep = scenes.last_frame(S, mono, motion=0.02 if seed == 3 else 0.2)
+    m = slamhot.ORBmatcher(0.9, check_ori)
+    ng, fg = m.SearchByProjection_last(fv, lf, th, mono)
+    no, fo = ob.search_by_projection_last(fv, lf, 0.9, check_ori, th, mono)
+    m.close()
+    assert ng == no and no > 20
+    assert np.array_equal(fg, fo)
+
+
+@pytest.mark.parametrize("seed", [5, 6])
+@pytest.mark.parametrize("th,orb_dist", [(10.0, 100), (3.0, 64)])
+def test_keyframe(seed, th, orb_dist):
+    import slamhot
+    S = scenes.scene(seed)
+    fv, keep = scenes.frame_view(S)
+    kf, kkeep = scenes.kf_points(S)
+    m = slamhot.ORBmatcher(0.75, True)
+    ng, fg = m.SearchByProjection_kf(fv, kf, th, orb_dist)
+    no, fo = ob.search_by_projection_kf(fv, kf, 0.75, True, th, orb_dist)
+    m.close()
+    assert ng == no and no > 20
+    assert np.array_equal(fg, fo)
