@@ -252,6 +252,73 @@ slam_status slamhot_search_by_projection_kf(slam_matcher* m, const slam_frame_vi
                                             const slam_kf_points* KF, float nnratio, int check_ori,
                                             float th, int orb_dist, int32_t* f_match, int* nmatches);
 
+/* ------------------------------------------------------------------------------------------
+ * Local bundle adjustment: the g2o LM/Schur solve inside
+ *   static void Optimizer::LocalBundleAdjustment(KeyFrame* pKF, bool* pbStopFlag, Map* pMap,
+ *       int& num_fixedKF, int& num_OptKF, int& num_MPs, int& num_edges)
+ *   (Optimizer.h:59, Optimizer.cc:1611-2078).
+ * The caller (the shim in INTEGRATION.md) builds the window exactly as Optimizer.cc:1613-1718
+ * does and flattens it: KeyFrames in vertex-id (mnId) order, MapPoints in lLocalMapPoints
+ * order, edges in insertion order (point-major: the edges of one MapPoint are contiguous,
+ * Optimizer.cc:1801-1920).  The solver then runs the reference schedule on the device:
+ * optimize(5) -> [stop flag] -> initializeOptimization(0) + optimize(10) (:1925-1987), and
+ * classifies the final outliers (chi2 > 5.991 mono / 7.815 stereo, or depth <= 0,
+ * :1995-2038).  The caller erases those observations and writes poses/points back
+ * (:2041-2077).  Many independent windows may be solved in one call (batched mode).
+ * ------------------------------------------------------------------------------------------ */
+
+/* KeyFrame intrinsics used by the edges: fx, fy, cx, cy, mbf (KeyFrame.h float members;
+ * Pinhole mvParameters for the mono edge, EdgeStereoSE3ProjectXYZ::fx.. for stereo). */
+typedef struct slam_camera {
+    float fx, fy, cx, cy, bf;
+} slam_camera;
+
+typedef struct slam_lba_problem {
+    int32_t n_kf;               /* KeyFrame vertices (local + fixed), mnId order */
+    const float* kf_Tcw;        /* n_kf x 16, row-major KeyFrame::GetPose() (cv::Mat 4x4 f32) */
+    const uint8_t* kf_fixed;    /* 1 = setFixed (init KF or lFixedCameras) */
+    int32_t n_pt;               /* MapPoint vertices (all marginalized) */
+    const float* pt_pos;        /* n_pt x 3, MapPoint::GetWorldPos() */
+    int32_t n_edge;             /* edges, insertion order, edge_pt non-decreasing */
+    const int32_t* edge_pt;     /* vertex 0: MapPoint index */
+    const int32_t* edge_kf;     /* vertex 1: KeyFrame index */
+    const float* edge_obs;      /* n_edge x 3: kpUn.pt.x, kpUn.pt.y, mvuRight (< 0 -> mono) */
+    const float* edge_inv_sigma2; /* mvInvLevelSigma2[kpUn.octave] */
+    slam_camera cam;
+} slam_lba_problem;
+
+typedef struct slam_lba_options {
+    int32_t iters_first;        /* 5  (Optimizer.cc:1926) */
+    int32_t iters_second;       /* 10 (Optimizer.cc:1986) */
+    double user_lambda_init;    /* 0 -> tau * max diag(H); 100 if pMap->IsInertial() (:1726) */
+} slam_lba_options;
+
+typedef struct slam_lba_result {
+    float* kf_Tcw;              /* out n_kf x 16 (fixed KFs are copied through) */
+    float* pt_pos;              /* out n_pt x 3 */
+    uint8_t* edge_outlier;      /* out n_edge: 1 = goes to vToErase (Optimizer.cc:1995-2038) */
+    int32_t iterations[2];      /* LM iterations run by each optimize() call */
+    int32_t trials;             /* total LM trials (linear solves) */
+    int32_t n_outlier;
+    double chi2_initial;        /* activeRobustChi2 at the first iteration */
+    double chi2_final;          /* activeRobustChi2 after the last accepted step */
+    double lambda_final;
+} slam_lba_result;
+
+typedef struct slam_lba slam_lba;
+
+/* A solver handle keeps device buffers sized for the largest batch seen (grown on demand). */
+slam_status slamhot_lba_create(int device, slam_lba** out);
+void slamhot_lba_destroy(slam_lba* s);
+/* Solve n_prob independent windows.  stop_flag (may be NULL) is the pbStopFlag: it is read
+ * between LM trials and, when non-zero, ends every window's optimize() as
+ * SparseOptimizer::terminate() does (sparse_optimizer.h:188, Optimizer.cc:1929-1934). */
+slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* probs,
+                              const slam_lba_options* opt, const volatile int32_t* stop_flag,
+                              slam_lba_result* results);
+/* Device time (ms) of the last solve and the number of host<->device round trips it used. */
+slam_status slamhot_lba_last_stats(const slam_lba* s, double* device_ms, int* syncs);
+
 #ifdef __cplusplus
 }
 #endif

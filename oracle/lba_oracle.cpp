@@ -1,0 +1,728 @@
+/*
+ * lba_oracle.cpp — CPU restatement of the g2o Levenberg-Marquardt / Schur solve that
+ * Optimizer::LocalBundleAdjustment runs (Optimizer.cc:1611-2078).  TEST INFRASTRUCTURE ONLY
+ * (see oracle.h): the checker for the device LBA and the CPU baseline of bench.py.
+ *
+ * Parity status: "parity unpinned" — g2o + Eigen cannot be built here (no Eigen, SURVEY.md
+ * §8c) and the reference ships no BA fixtures.  Every step restates the g2o / Eigen code
+ * cited next to it, in the reference's evaluation order, with the reference's float quirks
+ * (float camera parameters, float Huber dsqr, float invz + float bf*invz in the stereo edge).
+ * One documented deviation: LinearSolverEigen's SimplicialLDLT with AMD ordering
+ * (linear_solver_eigen.h:60-237) is restated as a dense LDL^T in natural order; both factor
+ * the same matrix exactly (no pivoting), so only rounding differs (<< the 1e-5 tolerance).
+ */
+#include <cfloat>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <limits>
+#include <vector>
+
+#include "../include/slamhot.h"
+
+namespace {
+
+struct Quat {
+    double x, y, z, w;  // Eigen coeffs() order
+};
+
+struct SE3 {
+    Quat r;
+    double t[3];
+};
+
+// Eigen::Quaternion from a rotation matrix (Eigen/src/Geometry/Quaternion.h,
+// quaternion_assign_impl<Other,3,3>).  R row-major.
+Quat quat_from_R(const double* R) {
+    auto m = [&](int i, int j) { return R[3 * i + j]; };
+    Quat q;
+    double c[3];
+    double t = m(0, 0) + m(1, 1) + m(2, 2);
+    if (t > 0.0) {
+        t = std::sqrt(t + 1.0);
+        q.w = 0.5 * t;
+        t = 0.5 / t;
+        q.x = (m(2, 1) - m(1, 2)) * t;
+        q.y = (m(0, 2) - m(2, 0)) * t;
+        q.z = (m(1, 0) - m(0, 1)) * t;
+        return q;
+    }
+    int i = 0;
+    if (m(1, 1) > m(0, 0)) i = 1;
+    if (m(2, 2) > m(i, i)) i = 2;
+    const int j = (i + 1) % 3, k = (j + 1) % 3;
+    t = std::sqrt(m(i, i) - m(j, j) - m(k, k) + 1.0);
+    c[i] = 0.5 * t;
+    t = 0.5 / t;
+    q.w = (m(k, j) - m(j, k)) * t;
+    c[j] = (m(j, i) + m(i, j)) * t;
+    c[k] = (m(k, i) + m(i, k)) * t;
+    q.x = c[0];
+    q.y = c[1];
+    q.z = c[2];
+    return q;
+}
+
+// SE3Quat::normalizeRotation (se3quat.h:280-285): w >= 0, then Quaternion::normalize.
+void normalize_rotation(Quat& q) {
+    if (q.w < 0) {
+        q.x = -q.x;
+        q.y = -q.y;
+        q.z = -q.z;
+        q.w = -q.w;
+    }
+    const double n = std::sqrt(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
+    q.x /= n;
+    q.y /= n;
+    q.z /= n;
+    q.w /= n;
+}
+
+// Quaternion::toRotationMatrix (Eigen Quaternion.h).
+void rot_matrix(const Quat& q, double* R) {
+    const double tx = 2.0 * q.x, ty = 2.0 * q.y, tz = 2.0 * q.z;
+    const double twx = tx * q.w, twy = ty * q.w, twz = tz * q.w;
+    const double txx = tx * q.x, txy = ty * q.x, txz = tz * q.x;
+    const double tyy = ty * q.y, tyz = tz * q.y, tzz = tz * q.z;
+    R[0] = 1.0 - (tyy + tzz);
+    R[1] = txy - twz;
+    R[2] = txz + twy;
+    R[3] = txy + twz;
+    R[4] = 1.0 - (txx + tzz);
+    R[5] = tyz - twx;
+    R[6] = txz - twy;
+    R[7] = tyz + twx;
+    R[8] = 1.0 - (txx + tyy);
+}
+
+// Quaternion * Vector3 (Eigen _transformVector): uv = v x p; uv += uv; p + w uv + v x uv.
+void quat_rotate(const Quat& q, const double* p, double* out) {
+    double uv[3] = {q.y * p[2] - q.z * p[1], q.z * p[0] - q.x * p[2], q.x * p[1] - q.y * p[0]};
+    uv[0] += uv[0];
+    uv[1] += uv[1];
+    uv[2] += uv[2];
+    const double c[3] = {q.y * uv[2] - q.z * uv[1], q.z * uv[0] - q.x * uv[2],
+                         q.x * uv[1] - q.y * uv[0]};
+    out[0] = p[0] + q.w * uv[0] + c[0];
+    out[1] = p[1] + q.w * uv[1] + c[1];
+    out[2] = p[2] + q.w * uv[2] + c[2];
+}
+
+// Quaternion product (Eigen quat_product).
+Quat quat_mul(const Quat& a, const Quat& b) {
+    Quat r;
+    r.w = a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z;
+    r.x = a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y;
+    r.y = a.w * b.y + a.y * b.w + a.z * b.x - a.x * b.z;
+    r.z = a.w * b.z + a.z * b.w + a.x * b.y - a.y * b.x;
+    return r;
+}
+
+// SE3Quat::map (se3quat.h:217-220)
+void se3_map(const SE3& T, const double* X, double* out) {
+    quat_rotate(T.r, X, out);
+    out[0] += T.t[0];
+    out[1] += T.t[1];
+    out[2] += T.t[2];
+}
+
+// SE3Quat::exp (se3quat.h:223-257), including the small-angle branch R = I + W + W^2.
+SE3 se3_exp(const double* upd) {
+    const double om[3] = {upd[0], upd[1], upd[2]};
+    const double up[3] = {upd[3], upd[4], upd[5]};
+    const double theta = std::sqrt(om[0] * om[0] + om[1] * om[1] + om[2] * om[2]);
+    double W[9] = {0, -om[2], om[1], om[2], 0, -om[0], -om[1], om[0], 0};  // skew (se3_ops.hpp:27)
+    double W2[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++)
+            W2[3 * i + j] = W[3 * i + 0] * W[0 + j] + W[3 * i + 1] * W[3 + j] + W[3 * i + 2] * W[6 + j];
+    double R[9], V[9];
+    if (theta < 0.00001) {
+        for (int k = 0; k < 9; k++) R[k] = ((k % 4 == 0) ? 1.0 : 0.0) + W[k] + W2[k];
+        for (int k = 0; k < 9; k++) V[k] = R[k];
+    } else {
+        const double a = std::sin(theta) / theta;
+        const double b = (1 - std::cos(theta)) / (theta * theta);
+        const double c = (theta - std::sin(theta)) / std::pow(theta, 3);
+        for (int k = 0; k < 9; k++) {
+            const double I = (k % 4 == 0) ? 1.0 : 0.0;
+            R[k] = I + a * W[k] + b * W2[k];
+            V[k] = I + b * W[k] + c * W2[k];
+        }
+    }
+    SE3 T;
+    T.r = quat_from_R(R);
+    for (int i = 0; i < 3; i++) T.t[i] = V[3 * i + 0] * up[0] + V[3 * i + 1] * up[1] + V[3 * i + 2] * up[2];
+    normalize_rotation(T.r);  // SE3Quat(const Quaterniond&, const Vector3d&)
+    return T;
+}
+
+// SE3Quat::operator* (se3quat.h:104-110)
+SE3 se3_mul(const SE3& a, const SE3& b) {
+    SE3 r;
+    double rt[3];
+    quat_rotate(a.r, b.t, rt);
+    for (int i = 0; i < 3; i++) r.t[i] = a.t[i] + rt[i];
+    r.r = quat_mul(a.r, b.r);
+    normalize_rotation(r.r);
+    return r;
+}
+
+// Converter::toSE3Quat (Converter.cc:34-44) -> SE3Quat(R, t) (se3quat.h:56-58)
+SE3 se3_from_cv(const float* T) {
+    double R[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) R[3 * i + j] = T[4 * i + j];
+    SE3 s;
+    s.r = quat_from_R(R);
+    for (int i = 0; i < 3; i++) s.t[i] = T[4 * i + 3];
+    normalize_rotation(s.r);
+    return s;
+}
+
+// Converter::toCvMat(SE3Quat) (Converter.cc:46-68): to_homogeneous_matrix -> float
+void se3_to_cv(const SE3& s, float* T) {
+    double R[9];
+    rot_matrix(s.r, R);
+    for (int i = 0; i < 3; i++) {
+        for (int j = 0; j < 3; j++) T[4 * i + j] = (float)R[3 * i + j];
+        T[4 * i + 3] = (float)s.t[i];
+    }
+    T[12] = 0.f;
+    T[13] = 0.f;
+    T[14] = 0.f;
+    T[15] = 1.f;
+}
+
+// Eigen 3x3 inverse (Eigen/src/LU/InverseImpl.h, compute_inverse<.., 3>): cofactors.
+void inverse3(const double* m, double* out) {
+    auto M = [&](int i, int j) { return m[3 * i + j]; };
+    auto cof = [&](int i, int j) {
+        const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+        return M(i1, j1) * M(i2, j2) - M(i1, j2) * M(i2, j1);
+    };
+    const double c0[3] = {cof(0, 0), cof(1, 0), cof(2, 0)};
+    const double det = c0[0] * M(0, 0) + c0[1] * M(1, 0) + c0[2] * M(2, 0);
+    const double invdet = 1.0 / det;
+    out[0] = c0[0] * invdet;
+    out[1] = c0[1] * invdet;
+    out[2] = c0[2] * invdet;
+    out[3] = cof(0, 1) * invdet;
+    out[4] = cof(1, 1) * invdet;
+    out[5] = cof(2, 1) * invdet;
+    out[6] = cof(0, 2) * invdet;
+    out[7] = cof(1, 2) * invdet;
+    out[8] = cof(2, 2) * invdet;
+}
+
+struct Edge {
+    int pt, kf;
+    bool stereo;
+    double obs[3];
+    double info;            // invSigma2 (float) promoted: Information = I * invSigma2
+    double err[3];          // _error of the last computeActiveErrors
+    double A[9];            // _jacobianOplusXi (point), D x 3 row-major
+    double B[18];           // _jacobianOplusXj (pose),  D x 6 row-major
+    double Hpl[18];         // pose-landmark block B^T W A, 6 x 3 row-major
+};
+
+struct Solver {
+    const slam_lba_problem* P;
+    double fx, fy, cx, cy, bf;  // float parameters promoted
+    double delta_mono, delta_stereo;
+    float dsqr_mono, dsqr_stereo;  // RobustKernelHuber::dsqr is float (robust_kernel_impl.h:84)
+    std::vector<SE3> pose, pose_bak;
+    std::vector<double> pt, pt_bak;
+    std::vector<int> hidx;   // pose Hessian index (-1 fixed)
+    int np = 0;              // free poses
+    std::vector<Edge> E;
+    std::vector<std::vector<int>> pt_edges;  // per point: edges with free pose, by pose index
+    // system
+    std::vector<double> Hpp;   // np x 36 diagonal blocks
+    std::vector<double> Hll;   // npt x 9
+    std::vector<double> b;     // 6 np + 3 npt
+    std::vector<double> x;
+    std::vector<double> Hs;    // dense (6 np)^2, row-major
+    double lambda = -1, ni = 2;
+    int nBad = 0;
+    int stop = 0;
+    int trials = 0;
+
+    int npt() const { return P->n_pt; }
+
+    // EdgeSE3ProjectXYZ::computeError (OptimizableTypes.h:97-102) + Pinhole::project
+    // (Pinhole.cpp:42-48); EdgeStereoSE3ProjectXYZ::computeError / cam_project
+    // (types_six_dof_expmap.h:157-162, types_six_dof_expmap.cpp:190-197).
+    void compute_error(Edge& e) {
+        double Xc[3];
+        se3_map(pose[e.kf], &pt[3 * e.pt], Xc);
+        if (!e.stereo) {
+            const double u = fx * Xc[0] / Xc[2] + cx;
+            const double v = fy * Xc[1] / Xc[2] + cy;
+            e.err[0] = e.obs[0] - u;
+            e.err[1] = e.obs[1] - v;
+        } else {
+            const float invz = (float)(1.0 / Xc[2]);
+            const float bff = (float)bf;
+            const double u = Xc[0] * (double)invz * fx + cx;
+            const double v = Xc[1] * (double)invz * fy + cy;
+            const double ur = u - (double)(bff * invz);
+            e.err[0] = e.obs[0] - u;
+            e.err[1] = e.obs[1] - v;
+            e.err[2] = e.obs[2] - ur;
+        }
+    }
+
+    // BaseEdge::chi2 (base_edge.h:58-61) with Information = invSigma2 * I
+    double chi2(const Edge& e) const {
+        double s = e.err[0] * (e.info * e.err[0]) + e.err[1] * (e.info * e.err[1]);
+        if (e.stereo) s += e.err[2] * (e.info * e.err[2]);
+        return s;
+    }
+
+    // RobustKernelHuber::robustify (robust_kernel_impl.cpp:79-91)
+    void robustify(const Edge& e, double c, double* rho) const {
+        const double delta = e.stereo ? delta_stereo : delta_mono;
+        const float dsqr = e.stereo ? dsqr_stereo : dsqr_mono;
+        if (c <= dsqr) {
+            rho[0] = c;
+            rho[1] = 1.;
+        } else {
+            const double sqrte = std::sqrt(c);
+            rho[0] = 2 * sqrte * delta - dsqr;
+            rho[1] = delta / sqrte;
+        }
+    }
+
+    bool depth_positive(const Edge& e) const {
+        double Xc[3];
+        se3_map(pose[e.kf], &pt[3 * e.pt], Xc);
+        return Xc[2] > 0.0;
+    }
+
+    // SparseOptimizer::computeActiveErrors + activeRobustChi2 (sparse_optimizer.cpp:61-114)
+    double active_errors() {
+        for (Edge& e : E) compute_error(e);
+        double chi = 0.0;
+        for (const Edge& e : E) {
+            double rho[2];
+            robustify(e, chi2(e), rho);
+            chi += rho[0];
+        }
+        return chi;
+    }
+
+    // EdgeSE3ProjectXYZ::linearizeOplus (OptimizableTypes.cpp:139-160) + Pinhole::projectJac
+    // (Pinhole.cpp:88-97); EdgeStereoSE3ProjectXYZ::linearizeOplus (types_six_dof_expmap.cpp:228-275)
+    void linearize(Edge& e) {
+        const SE3& T = pose[e.kf];
+        double R[9], Xc[3];
+        se3_map(T, &pt[3 * e.pt], Xc);
+        rot_matrix(T.r, R);
+        const double x = Xc[0], y = Xc[1], z = Xc[2];
+        if (!e.stereo) {
+            // projectJac = -Jac, Jac(0,2) = -fx * x / (z*z) with fx float
+            const double pj[6] = {-(fx / z), -0.0, -((-fx) * x / (z * z)),
+                                  -0.0, -(fy / z), -((-fy) * y / (z * z))};
+            for (int r = 0; r < 2; r++)
+                for (int c = 0; c < 3; c++)
+                    e.A[3 * r + c] = pj[3 * r + 0] * R[0 + c] + pj[3 * r + 1] * R[3 + c] +
+                                     pj[3 * r + 2] * R[6 + c];
+            const double S[18] = {0.0, z, -y, 1.0, 0.0, 0.0,
+                                  -z, 0.0, x, 0.0, 1.0, 0.0,
+                                  y, -x, 0.0, 0.0, 0.0, 1.0};
+            for (int r = 0; r < 2; r++)
+                for (int c = 0; c < 6; c++)
+                    e.B[6 * r + c] = pj[3 * r + 0] * S[0 + c] + pj[3 * r + 1] * S[6 + c] +
+                                     pj[3 * r + 2] * S[12 + c];
+        } else {
+            const double z_2 = z * z;
+            double* A = e.A;
+            A[0] = -fx * R[0] / z + fx * x * R[6] / z_2;
+            A[1] = -fx * R[1] / z + fx * x * R[7] / z_2;
+            A[2] = -fx * R[2] / z + fx * x * R[8] / z_2;
+            A[3] = -fy * R[3] / z + fy * y * R[6] / z_2;
+            A[4] = -fy * R[4] / z + fy * y * R[7] / z_2;
+            A[5] = -fy * R[5] / z + fy * y * R[8] / z_2;
+            A[6] = A[0] - bf * R[6] / z_2;
+            A[7] = A[1] - bf * R[7] / z_2;
+            A[8] = A[2] - bf * R[8] / z_2;
+            double* B = e.B;
+            B[0] = x * y / z_2 * fx;
+            B[1] = -(1 + (x * x / z_2)) * fx;
+            B[2] = y / z * fx;
+            B[3] = -1. / z * fx;
+            B[4] = 0;
+            B[5] = x / z_2 * fx;
+            B[6] = (1 + y * y / z_2) * fy;
+            B[7] = -x * y / z_2 * fy;
+            B[8] = -x / z * fy;
+            B[9] = 0;
+            B[10] = -1. / z * fy;
+            B[11] = y / z_2 * fy;
+            B[12] = B[0] - bf * y / z_2;
+            B[13] = B[1] + bf * x / z_2;
+            B[14] = B[2];
+            B[15] = B[3];
+            B[16] = 0;
+            B[17] = B[5] - bf / z_2;
+        }
+    }
+
+    // BaseBinaryEdge::constructQuadraticForm, robust branch (base_binary_edge.hpp:55-120),
+    // robustInformation (base_edge.h:96-102): W = rho' * Omega.
+    void quadratic_form(Edge& e) {
+        const int D = e.stereo ? 3 : 2;
+        double rho[2];
+        robustify(e, chi2(e), rho);
+        const double w = rho[1] * e.info;  // weightedOmega diagonal
+        double om_r[3];
+        for (int k = 0; k < D; k++) om_r[k] = (-(e.info * e.err[k])) * rho[1];
+        const int ip = 3 * e.pt;
+        // from = point: b += A^T om_r, Hll += A^T W A
+        for (int c = 0; c < 3; c++) {
+            double s = 0;
+            for (int k = 0; k < D; k++) s += e.A[3 * k + c] * om_r[k];
+            b[6 * np + ip + c] += s;
+        }
+        for (int r = 0; r < 3; r++)
+            for (int c = 0; c < 3; c++) {
+                double s = 0;
+                for (int k = 0; k < D; k++) s += (e.A[3 * k + r] * w) * e.A[3 * k + c];
+                Hll[9 * e.pt + 3 * r + c] += s;
+            }
+        const int h = hidx[e.kf];
+        if (h < 0) return;
+        // Hpl (pose row, landmark col) = B^T W A (the transposed-block write)
+        for (int r = 0; r < 6; r++)
+            for (int c = 0; c < 3; c++) {
+                double s = 0;
+                for (int k = 0; k < D; k++) s += (e.B[6 * k + r] * w) * e.A[3 * k + c];
+                e.Hpl[3 * r + c] = s;
+            }
+        for (int c = 0; c < 6; c++) {
+            double s = 0;
+            for (int k = 0; k < D; k++) s += e.B[6 * k + c] * om_r[k];
+            b[6 * h + c] += s;
+        }
+        for (int r = 0; r < 6; r++)
+            for (int c = 0; c < 6; c++) {
+                double s = 0;
+                for (int k = 0; k < D; k++) s += (e.B[6 * k + r] * w) * e.B[6 * k + c];
+                Hpp[36 * h + 6 * r + c] += s;
+            }
+    }
+
+    // BlockSolver::buildSystem (block_solver.hpp:501-560)
+    void build_system() {
+        std::fill(Hpp.begin(), Hpp.end(), 0.0);
+        std::fill(Hll.begin(), Hll.end(), 0.0);
+        std::fill(b.begin(), b.end(), 0.0);
+        for (Edge& e : E) {
+            linearize(e);
+            quadratic_form(e);
+        }
+    }
+
+    // OptimizationAlgorithmLevenberg::computeLambdaInit (optimization_algorithm_levenberg.cpp:171-185)
+    double lambda_init(double user) const {
+        if (user > 0) return user;
+        double m = 0.;
+        for (int i = 0; i < np; i++)
+            for (int j = 0; j < 6; j++) m = std::max(std::fabs(Hpp[36 * i + 7 * j]), m);
+        for (int i = 0; i < npt(); i++)
+            for (int j = 0; j < 3; j++) m = std::max(std::fabs(Hll[9 * i + 4 * j]), m);
+        return 1e-5 * m;
+    }
+
+    // Dense LDL^T of the Schur complement (deviation from SimplicialLDLT + AMD, see header).
+    // Fails like Eigen's factorize when a pivot is exactly zero.
+    bool ldlt_solve(std::vector<double>& A, int n, const double* rhs, double* out) {
+        std::vector<double> d(n);
+        for (int j = 0; j < n; j++) {
+            double dj = A[(size_t)j * n + j];
+            for (int k = 0; k < j; k++) dj -= A[(size_t)j * n + k] * A[(size_t)j * n + k] * d[k];
+            if (dj == 0.0) return false;
+            d[j] = dj;
+            for (int i = j + 1; i < n; i++) {
+                double s = A[(size_t)i * n + j];
+                for (int k = 0; k < j; k++) s -= A[(size_t)i * n + k] * A[(size_t)j * n + k] * d[k];
+                A[(size_t)i * n + j] = s / dj;
+            }
+        }
+        std::vector<double> y(rhs, rhs + n);
+        for (int i = 0; i < n; i++)
+            for (int k = 0; k < i; k++) y[i] -= A[(size_t)i * n + k] * y[k];
+        for (int i = 0; i < n; i++) y[i] /= d[i];
+        for (int i = n - 1; i >= 0; i--)
+            for (int k = i + 1; k < n; k++) y[i] -= A[(size_t)k * n + i] * y[k];
+        std::memcpy(out, y.data(), sizeof(double) * n);
+        return true;
+    }
+
+    // BlockSolver::solve, Schur branch (block_solver.hpp:353-486), lambda already on the
+    // diagonals (setLambda, :563-590).
+    bool solve_system() {
+        const int n = 6 * np;
+        Hs.assign((size_t)n * n, 0.0);
+        for (int i = 0; i < np; i++)
+            for (int r = 0; r < 6; r++)
+                for (int c = r; c < 6; c++) Hs[(size_t)(6 * i + r) * n + 6 * i + c] = Hpp[36 * i + 6 * r + c];
+        std::vector<double> coeff(n, 0.0);
+        std::vector<double> Dinv(9 * (size_t)npt());
+        for (int l = 0; l < npt(); l++) {
+            inverse3(&Hll[9 * l], &Dinv[9 * l]);
+            const double* Di = &Dinv[9 * l];
+            const double* bl = &b[n + 3 * l];
+            double db[3];
+            for (int r = 0; r < 3; r++) db[r] = Di[3 * r] * bl[0] + Di[3 * r + 1] * bl[1] + Di[3 * r + 2] * bl[2];
+            const std::vector<int>& col = pt_edges[l];
+            for (size_t a = 0; a < col.size(); a++) {
+                const Edge& ei = E[col[a]];
+                const int i1 = hidx[ei.kf];
+                double BD[18];
+                for (int r = 0; r < 6; r++)
+                    for (int c = 0; c < 3; c++)
+                        BD[3 * r + c] = ei.Hpl[3 * r] * Di[c] + ei.Hpl[3 * r + 1] * Di[3 + c] +
+                                        ei.Hpl[3 * r + 2] * Di[6 + c];
+                for (int r = 0; r < 6; r++)
+                    coeff[6 * i1 + r] += ei.Hpl[3 * r] * db[0] + ei.Hpl[3 * r + 1] * db[1] + ei.Hpl[3 * r + 2] * db[2];
+                for (size_t bq = a; bq < col.size(); bq++) {
+                    const Edge& ej = E[col[bq]];
+                    const int i2 = hidx[ej.kf];
+                    for (int r = 0; r < 6; r++)
+                        for (int c = 0; c < 6; c++)
+                            Hs[(size_t)(6 * i1 + r) * n + 6 * i2 + c] -=
+                                BD[3 * r] * ej.Hpl[3 * c] + BD[3 * r + 1] * ej.Hpl[3 * c + 1] +
+                                BD[3 * r + 2] * ej.Hpl[3 * c + 2];
+                }
+            }
+        }
+        // the upper triangle is authoritative (SimplicialLDLT<.., Upper>): mirror it
+        for (int r = 0; r < n; r++)
+            for (int c = 0; c < r; c++) Hs[(size_t)r * n + c] = Hs[(size_t)c * n + r];
+        std::vector<double> bs(n);
+        for (int i = 0; i < n; i++) bs[i] = b[i] - coeff[i];
+        if (!ldlt_solve(Hs, n, bs.data(), x.data())) return false;
+        // cl = bl - Hpl^T xp ; xl = Dinv cl (block_solver.hpp:456-481)
+        for (int l = 0; l < npt(); l++) {
+            double cl[3] = {b[n + 3 * l], b[n + 3 * l + 1], b[n + 3 * l + 2]};
+            for (int ei : pt_edges[l]) {
+                const Edge& e = E[ei];
+                const double* xp = &x[6 * hidx[e.kf]];
+                for (int c = 0; c < 3; c++)
+                    for (int r = 0; r < 6; r++) cl[c] += e.Hpl[3 * r + c] * (-xp[r]);
+            }
+            const double* Di = &Dinv[9 * l];
+            for (int r = 0; r < 3; r++)
+                x[n + 3 * l + r] = Di[3 * r] * cl[0] + Di[3 * r + 1] * cl[1] + Di[3 * r + 2] * cl[2];
+        }
+        return true;
+    }
+
+    // BlockSolver::setLambda(lambda, backup=true) / restoreDiagonal (block_solver.hpp:563-604)
+    std::vector<double> diag_bak;
+    void set_lambda(double lam) {
+        diag_bak.clear();
+        for (int i = 0; i < np; i++)
+            for (int j = 0; j < 6; j++) {
+                diag_bak.push_back(Hpp[36 * i + 7 * j]);
+                Hpp[36 * i + 7 * j] += lam;
+            }
+        for (int i = 0; i < npt(); i++)
+            for (int j = 0; j < 3; j++) {
+                diag_bak.push_back(Hll[9 * i + 4 * j]);
+                Hll[9 * i + 4 * j] += lam;
+            }
+    }
+    void restore_diagonal() {
+        size_t k = 0;
+        for (int i = 0; i < np; i++)
+            for (int j = 0; j < 6; j++) Hpp[36 * i + 7 * j] = diag_bak[k++];
+        for (int i = 0; i < npt(); i++)
+            for (int j = 0; j < 3; j++) Hll[9 * i + 4 * j] = diag_bak[k++];
+    }
+
+    // SparseOptimizer::update (sparse_optimizer.cpp:422-435): VertexSE3Expmap::oplusImpl
+    // (types_six_dof_expmap.h:71-74) and VertexSBAPointXYZ::oplusImpl (types_sba.h:52-56).
+    void update() {
+        for (size_t k = 0; k < pose.size(); k++) {
+            const int h = hidx[k];
+            if (h >= 0) pose[k] = se3_mul(se3_exp(&x[6 * h]), pose[k]);
+        }
+        for (int l = 0; l < npt(); l++)
+            for (int c = 0; c < 3; c++) pt[3 * l + c] += x[6 * np + 3 * l + c];
+    }
+
+    double compute_scale() const {
+        double s = 0.;
+        for (size_t j = 0; j < x.size(); j++) s += x[j] * (lambda * x[j] + b[j]);
+        return s;
+    }
+
+    enum { OK, TERMINATE };
+
+    // OptimizationAlgorithmLevenberg::solve (optimization_algorithm_levenberg.cpp:61-169)
+    int lm_solve(int iteration, double user_lambda, double* chi_ini_out, double* chi_out) {
+        double currentChi = active_errors();
+        const double iniChi = currentChi;
+        if (chi_ini_out) *chi_ini_out = currentChi;
+        build_system();
+        if (iteration == 0) {
+            lambda = lambda_init(user_lambda);
+            ni = 2;
+            nBad = 0;
+        }
+        double rho = 0;
+        int qmax = 0;
+        do {
+            pose_bak = pose;  // push
+            pt_bak = pt;
+            set_lambda(lambda);
+            const bool ok2 = solve_system();
+            trials++;
+            update();
+            restore_diagonal();
+            double tempChi = active_errors();
+            if (!ok2) tempChi = std::numeric_limits<double>::max();
+            rho = currentChi - tempChi;
+            double scale = compute_scale();
+            scale += 1e-3;
+            rho /= scale;
+            if (rho > 0 && std::isfinite(tempChi)) {
+                double alpha = 1. - std::pow((2 * rho - 1), 3);
+                alpha = std::min(alpha, 2. / 3.);
+                const double scaleFactor = std::max(1. / 3., alpha);
+                lambda *= scaleFactor;
+                ni = 2;
+                currentChi = tempChi;
+            } else {
+                lambda *= ni;
+                ni *= 2;
+                pose = pose_bak;  // pop
+                pt = pt_bak;
+            }
+            qmax++;
+        } while (rho < 0 && qmax < 10 && !stop);
+        *chi_out = currentChi;
+        if (qmax == 10 || rho == 0) return TERMINATE;
+        if ((iniChi - currentChi) * 1e3 < iniChi)
+            nBad++;
+        else
+            nBad = 0;
+        if (nBad >= 3) return TERMINATE;
+        return OK;
+    }
+
+    // SparseOptimizer::optimize (sparse_optimizer.cpp:354-420)
+    int optimize(int iterations, double user_lambda, double* chi_ini, double* chi_fin) {
+        int it = 0;
+        bool ok = true;
+        for (int i = 0; i < iterations && !stop && ok; i++) {
+            double ci, cf;
+            const int r = lm_solve(i, user_lambda, &ci, &cf);
+            if (chi_ini && i == 0) *chi_ini = ci;
+            *chi_fin = cf;
+            ok = r == OK;
+            ++it;
+        }
+        return it;
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+/* Optimizer::LocalBundleAdjustment from the vertex/edge setup on (Optimizer.cc:1722-2077).
+ * kf_fixed: 0 free, 1 fixed and written back (the init KF inside lLocalKeyFrames),
+ * 2 fixed camera (lFixedCameras, not written back).  stop = *pbStopFlag (static here). */
+int oracle_lba_solve(const slam_lba_problem* P, const slam_lba_options* opt, int stop,
+                     slam_lba_result* R) {
+    Solver S;
+    S.P = P;
+    S.stop = stop;
+    S.fx = P->cam.fx;
+    S.fy = P->cam.fy;
+    S.cx = P->cam.cx;
+    S.cy = P->cam.cy;
+    S.bf = P->cam.bf;
+    const float thMono = std::sqrt(5.991), thStereo = std::sqrt(7.815);  // Optimizer.cc:1794-1795
+    S.delta_mono = thMono;
+    S.delta_stereo = thStereo;
+    S.dsqr_mono = (float)(S.delta_mono * S.delta_mono);  // RobustKernelHuber::setDelta
+    S.dsqr_stereo = (float)(S.delta_stereo * S.delta_stereo);
+    const int nk = P->n_kf, npt = P->n_pt, ne = P->n_edge;
+    S.pose.resize(nk);
+    S.hidx.assign(nk, -1);
+    // vertices without edges are not active (sparse_optimizer.cpp:262-300)
+    std::vector<int> kf_edges(nk, 0);
+    for (int i = 0; i < ne; i++) kf_edges[P->edge_kf[i]]++;
+    for (int k = 0; k < nk; k++) {
+        S.pose[k] = se3_from_cv(P->kf_Tcw + 16 * k);
+        if (P->kf_fixed[k] == 0 && kf_edges[k] > 0) S.hidx[k] = S.np++;
+    }
+    S.pt.resize(3 * (size_t)npt);
+    for (int i = 0; i < 3 * npt; i++) S.pt[i] = P->pt_pos[i];
+    S.E.resize(ne);
+    S.pt_edges.assign(npt, {});
+    for (int i = 0; i < ne; i++) {
+        Edge& e = S.E[i];
+        e.pt = P->edge_pt[i];
+        e.kf = P->edge_kf[i];
+        e.stereo = P->edge_obs[3 * i + 2] >= 0;  // mvuRight < 0 -> mono (Optimizer.cc:1822, 1852)
+        for (int c = 0; c < 3; c++) e.obs[c] = P->edge_obs[3 * i + c];
+        e.info = P->edge_inv_sigma2[i];
+        e.err[0] = e.err[1] = e.err[2] = 0;
+        if (S.hidx[e.kf] >= 0) S.pt_edges[e.pt].push_back(i);
+    }
+    // HplCCS columns are sorted by pose row (block_solver.hpp:247, fillSparseBlockMatrixCCS)
+    for (auto& col : S.pt_edges) {
+        for (size_t a = 1; a < col.size(); a++)
+            for (size_t b = a; b > 0 && S.hidx[S.E[col[b - 1]].kf] > S.hidx[S.E[col[b]].kf]; b--)
+                std::swap(col[b - 1], col[b]);
+    }
+    S.Hpp.assign(36 * (size_t)S.np, 0.0);
+    S.Hll.assign(9 * (size_t)npt, 0.0);
+    S.b.assign(6 * (size_t)S.np + 3 * (size_t)npt, 0.0);
+    S.x.assign(S.b.size(), 0.0);
+
+    R->iterations[0] = R->iterations[1] = 0;
+    R->trials = 0;
+    R->chi2_initial = 0;
+    R->chi2_final = 0;
+    R->lambda_final = 0;
+    R->n_outlier = 0;
+    if (stop) {  // Optimizer.cc:1921-1923: return before optimizing, nothing written back
+        std::memcpy(R->kf_Tcw, P->kf_Tcw, sizeof(float) * 16 * nk);
+        std::memcpy(R->pt_pos, P->pt_pos, sizeof(float) * 3 * npt);
+        std::memset(R->edge_outlier, 0, ne);
+        return 0;
+    }
+    double cf = 0;
+    // an empty graph makes initializeOptimization / optimize fail (sparse_optimizer.cpp:282-285)
+    if (ne > 0) R->iterations[0] = S.optimize(opt->iters_first, opt->user_lambda_init, &R->chi2_initial, &cf);
+    if (!S.stop && ne > 0) R->iterations[1] = S.optimize(opt->iters_second, opt->user_lambda_init, nullptr, &cf);
+    R->chi2_final = cf;
+    R->lambda_final = S.lambda;
+    R->trials = S.trials;
+    int nout = 0;
+    for (int i = 0; i < ne; i++) {
+        const Edge& e = S.E[i];
+        const double th = e.stereo ? 7.815 : 5.991;
+        const bool bad = S.chi2(e) > th || !S.depth_positive(e);
+        R->edge_outlier[i] = bad;
+        nout += bad;
+    }
+    R->n_outlier = nout;
+    for (int k = 0; k < nk; k++) {
+        if (P->kf_fixed[k] == 2)
+            std::memcpy(R->kf_Tcw + 16 * k, P->kf_Tcw + 16 * k, sizeof(float) * 16);
+        else
+            se3_to_cv(S.pose[k], R->kf_Tcw + 16 * k);
+    }
+    for (int i = 0; i < 3 * npt; i++) R->pt_pos[i] = (float)S.pt[i];
+    return 0;
+}
+
+}  // extern "C"

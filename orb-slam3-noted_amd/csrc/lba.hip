@@ -1,0 +1,1461 @@
+// lba.hip — the LM / Schur inner loop of Optimizer::LocalBundleAdjustment on gfx950.
+//
+// Reference: Optimizer.cc:1611-2078 drives g2o's SparseOptimizer + OptimizationAlgorithmLevenberg
+// + BlockSolver<6,3> + LinearSolverEigen (SimplicialLDLT).  Here one call solves a batch of
+// independent windows; every window's state (poses, points, Hessian blocks, the dense Schur
+// complement, the LM scalars) lives in HBM for the whole solve, and each LM decision is taken
+// on the device by a per-window control kernel.  The host only launches kernels and reads
+// back two counters per trial (windows still trying / still iterating) plus the stop flag.
+//
+// Kernels (per LM iteration, all windows of the batch in one launch each):
+//   k_linearize      thread / edge  : error, Huber rho, Jacobians, per-edge quadratic form
+//   k_point_reduce   thread / point : Hll (3x3) and b_l, summed over the point's edges
+//   k_pose_reduce    thread / (pose, entry) : Hpp (6x6) and b_p over the pose's edges
+//   k_iter_begin     block / window : chi2 = sum rho, lambda init (iteration 0)
+// per LM trial:
+//   k_schur_point    thread / point : Dinv = (Hll + lambda I)^-1, B_e Dinv, B_e Dinv b_l
+//   k_schur_block    wave / 6x6 block of the Schur complement (lower triangle + rhs row)
+//   k_ldlt           block / window : dense LDL^T of the (n+1) x (n+1) augmented system
+//   k_backsub        thread / point : x_l = Dinv (b_l - Hpl^T x_p), trial point
+//   k_pose_update    thread / KF    : trial pose = exp(x_p) * pose
+//   k_trial_error    thread / edge  : error + rho at the trial state
+//   k_trial_control  block / window : rho, accept (swap state) or reject, lambda, stop rules
+// FP64 throughout, with the reference's float quirks (see oracle/lba_oracle.cpp).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "common.hpp"
+
+namespace slamhot {
+namespace lba {
+
+constexpr int kNB = 32;           // LDL^T panel width
+constexpr int kMaxN = 480;        // 80 free KeyFrames per window
+constexpr int kLinStride = 56;    // doubles per edge of linearization output
+constexpr int kLinHpl = 0, kLinHpp = 18, kLinBp = 39, kLinHll = 45, kLinBl = 51;
+constexpr int kTrStride = 24;     // doubles per edge of Schur trial output: B Dinv (18), B db (6)
+constexpr int kCtlThreads = 256;
+
+// 6x6 symmetric upper-triangle packing, row-major (r <= c)
+__host__ __device__ constexpr int sym6(int r, int c) { return r * 6 - (r * (r - 1)) / 2 + (c - r); }
+__host__ __device__ constexpr int sym3(int r, int c) { return r * 3 - (r * (r - 1)) / 2 + (c - r); }
+
+struct EdgeS {
+    int pt, kf, hp, win;   // global point, global KF, global free-pose index (-1 fixed), window
+    float obs[3];          // u, v, ur (ur < 0 -> mono)
+    float info;            // invSigma2
+};
+
+struct WinDesc {
+    int kf0, nk, pt0, npt, e0, ne, pose0, np;
+    int n, ld, blk0, nblk;
+    long long hs_off;      // doubles
+};
+
+struct WinCtl {
+    double lambda, ni, cur_chi, ini_chi, chi2_initial, chi2_final, user_lambda, tmp_chi;
+    int sel, active, need_trial, ok2;
+    int qmax, nbad, it, iters;
+    int trials, opt, result, n_outlier;
+    int iters_run[2];
+};
+
+struct Counters {
+    int need_trial, active;
+};
+
+struct Cam {
+    double fx, fy, cx, cy, bf;
+    float bff;
+};
+
+// ---------------------------------------------------------------- SE3Quat math (device)
+struct Quat {
+    double x, y, z, w;
+};
+
+__device__ inline Quat quat_from_R(const double* R) {
+    Quat q;
+    double t = R[0] + R[4] + R[8];
+    if (t > 0.0) {
+        t = sqrt(t + 1.0);
+        q.w = 0.5 * t;
+        t = 0.5 / t;
+        q.x = (R[7] - R[5]) * t;
+        q.y = (R[2] - R[6]) * t;
+        q.z = (R[3] - R[1]) * t;
+        return q;
+    }
+    int i = 0;
+    if (R[4] > R[0]) i = 1;
+    if (R[8] > R[4 * i]) i = 2;
+    const int j = (i + 1) % 3, k = (j + 1) % 3;
+    double c[3];
+    t = sqrt(R[4 * i] - R[4 * j] - R[4 * k] + 1.0);
+    c[i] = 0.5 * t;
+    t = 0.5 / t;
+    q.w = (R[3 * k + j] - R[3 * j + k]) * t;
+    c[j] = (R[3 * j + i] + R[3 * i + j]) * t;
+    c[k] = (R[3 * k + i] + R[3 * i + k]) * t;
+    q.x = c[0];
+    q.y = c[1];
+    q.z = c[2];
+    return q;
+}
+
+__device__ inline void normalize_rotation(Quat& q) {
+    if (q.w < 0) {
+        q.x = -q.x;
+        q.y = -q.y;
+        q.z = -q.z;
+        q.w = -q.w;
+    }
+    const double n = sqrt(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
+    q.x /= n;
+    q.y /= n;
+    q.z /= n;
+    q.w /= n;
+}
+
+__device__ inline void rot_matrix(const Quat& q, double* R) {
+    const double tx = 2.0 * q.x, ty = 2.0 * q.y, tz = 2.0 * q.z;
+    const double twx = tx * q.w, twy = ty * q.w, twz = tz * q.w;
+    const double txx = tx * q.x, txy = ty * q.x, txz = tz * q.x;
+    const double tyy = ty * q.y, tyz = tz * q.y, tzz = tz * q.z;
+    R[0] = 1.0 - (tyy + tzz);
+    R[1] = txy - twz;
+    R[2] = txz + twy;
+    R[3] = txy + twz;
+    R[4] = 1.0 - (txx + tzz);
+    R[5] = tyz - twx;
+    R[6] = txz - twy;
+    R[7] = tyz + twx;
+    R[8] = 1.0 - (txx + tyy);
+}
+
+__device__ inline void quat_rotate(const Quat& q, const double* p, double* out) {
+    double uv[3] = {q.y * p[2] - q.z * p[1], q.z * p[0] - q.x * p[2], q.x * p[1] - q.y * p[0]};
+    uv[0] += uv[0];
+    uv[1] += uv[1];
+    uv[2] += uv[2];
+    const double c0 = q.y * uv[2] - q.z * uv[1], c1 = q.z * uv[0] - q.x * uv[2],
+                 c2 = q.x * uv[1] - q.y * uv[0];
+    out[0] = p[0] + q.w * uv[0] + c0;
+    out[1] = p[1] + q.w * uv[1] + c1;
+    out[2] = p[2] + q.w * uv[2] + c2;
+}
+
+// pose record: qx qy qz qw tx ty tz pad
+__device__ inline Quat load_q(const double* P) { return Quat{P[0], P[1], P[2], P[3]}; }
+
+__device__ inline void se3_map(const double* P, const double* X, double* out) {
+    quat_rotate(load_q(P), X, out);
+    out[0] += P[4];
+    out[1] += P[5];
+    out[2] += P[6];
+}
+
+// ---------------------------------------------------------------- edge math
+__device__ inline void edge_error(const EdgeS& e, const Cam& cam, const double* P, const double* X,
+                                  double* err) {
+    double Xc[3];
+    se3_map(P, X, Xc);
+    if (e.obs[2] < 0.f) {
+        const double u = cam.fx * Xc[0] / Xc[2] + cam.cx;
+        const double v = cam.fy * Xc[1] / Xc[2] + cam.cy;
+        err[0] = (double)e.obs[0] - u;
+        err[1] = (double)e.obs[1] - v;
+        err[2] = 0.0;
+    } else {
+        const float invz = (float)(1.0 / Xc[2]);
+        const double u = Xc[0] * (double)invz * cam.fx + cam.cx;
+        const double v = Xc[1] * (double)invz * cam.fy + cam.cy;
+        const double ur = u - (double)(cam.bff * invz);
+        err[0] = (double)e.obs[0] - u;
+        err[1] = (double)e.obs[1] - v;
+        err[2] = (double)e.obs[2] - ur;
+    }
+}
+
+__device__ inline double edge_chi2(const EdgeS& e, const double* err) {
+    const double info = e.info;
+    double s = err[0] * (info * err[0]) + err[1] * (info * err[1]);
+    if (e.obs[2] >= 0.f) s += err[2] * (info * err[2]);
+    return s;
+}
+
+struct Huber {
+    double delta_mono, delta_stereo;
+    float dsqr_mono, dsqr_stereo;
+};
+
+__device__ inline void robustify(const Huber& hk, bool stereo, double c, double& rho0, double& rho1) {
+    const double delta = stereo ? hk.delta_stereo : hk.delta_mono;
+    const float dsqr = stereo ? hk.dsqr_stereo : hk.dsqr_mono;
+    if (c <= dsqr) {
+        rho0 = c;
+        rho1 = 1.;
+    } else {
+        const double sqrte = sqrt(c);
+        rho0 = 2 * sqrte * delta - dsqr;
+        rho1 = delta / sqrte;
+    }
+}
+
+// ---------------------------------------------------------------- iteration kernels
+__global__ void k_linearize(int ne_total, const EdgeS* __restrict__ E, const WinCtl* __restrict__ ctl,
+                            const double* __restrict__ poses, const double* __restrict__ pts,
+                            long long pose_stride, long long pt_stride, Cam cam, Huber hk,
+                            double* __restrict__ err_out, double* __restrict__ rho_out,
+                            double* __restrict__ lin) {
+    const int ei = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ei >= ne_total) return;
+    const EdgeS e = E[ei];
+    const WinCtl& C = ctl[e.win];
+    if (!C.active) return;
+    const double* P = poses + C.sel * pose_stride + 8 * (long long)e.kf;
+    const double* Xw = pts + C.sel * pt_stride + 4 * (long long)e.pt;
+    const double X[3] = {Xw[0], Xw[1], Xw[2]};
+    double err[3];
+    edge_error(e, cam, P, X, err);
+    err_out[4 * (long long)ei + 0] = err[0];
+    err_out[4 * (long long)ei + 1] = err[1];
+    err_out[4 * (long long)ei + 2] = err[2];
+    const bool stereo = e.obs[2] >= 0.f;
+    const double c = edge_chi2(e, err);
+    double rho0, rho1;
+    robustify(hk, stereo, c, rho0, rho1);
+    rho_out[ei] = rho0;
+
+    // Jacobians (OptimizableTypes.cpp:139-160, types_six_dof_expmap.cpp:228-275)
+    double R[9], Xc[3];
+    const Quat q = load_q(P);
+    se3_map(P, X, Xc);
+    rot_matrix(q, R);
+    const double x = Xc[0], y = Xc[1], z = Xc[2];
+    double A[9], B[18];
+    int D;
+    if (!stereo) {
+        D = 2;
+        const double pj[6] = {-(cam.fx / z), -0.0, -((-cam.fx) * x / (z * z)),
+                              -0.0, -(cam.fy / z), -((-cam.fy) * y / (z * z))};
+#pragma unroll
+        for (int r = 0; r < 2; r++)
+#pragma unroll
+            for (int cc = 0; cc < 3; cc++)
+                A[3 * r + cc] = pj[3 * r + 0] * R[0 + cc] + pj[3 * r + 1] * R[3 + cc] + pj[3 * r + 2] * R[6 + cc];
+        const double S[18] = {0.0, z, -y, 1.0, 0.0, 0.0, -z, 0.0, x, 0.0, 1.0, 0.0, y, -x, 0.0, 0.0, 0.0, 1.0};
+#pragma unroll
+        for (int r = 0; r < 2; r++)
+#pragma unroll
+            for (int cc = 0; cc < 6; cc++)
+                B[6 * r + cc] = pj[3 * r + 0] * S[0 + cc] + pj[3 * r + 1] * S[6 + cc] + pj[3 * r + 2] * S[12 + cc];
+        A[6] = A[7] = A[8] = 0;
+#pragma unroll
+        for (int cc = 0; cc < 6; cc++) B[12 + cc] = 0;
+    } else {
+        D = 3;
+        const double fx = cam.fx, fy = cam.fy, bf = cam.bf;
+        const double z_2 = z * z;
+        A[0] = -fx * R[0] / z + fx * x * R[6] / z_2;
+        A[1] = -fx * R[1] / z + fx * x * R[7] / z_2;
+        A[2] = -fx * R[2] / z + fx * x * R[8] / z_2;
+        A[3] = -fy * R[3] / z + fy * y * R[6] / z_2;
+        A[4] = -fy * R[4] / z + fy * y * R[7] / z_2;
+        A[5] = -fy * R[5] / z + fy * y * R[8] / z_2;
+        A[6] = A[0] - bf * R[6] / z_2;
+        A[7] = A[1] - bf * R[7] / z_2;
+        A[8] = A[2] - bf * R[8] / z_2;
+        B[0] = x * y / z_2 * fx;
+        B[1] = -(1 + (x * x / z_2)) * fx;
+        B[2] = y / z * fx;
+        B[3] = -1. / z * fx;
+        B[4] = 0;
+        B[5] = x / z_2 * fx;
+        B[6] = (1 + y * y / z_2) * fy;
+        B[7] = -x * y / z_2 * fy;
+        B[8] = -x / z * fy;
+        B[9] = 0;
+        B[10] = -1. / z * fy;
+        B[11] = y / z_2 * fy;
+        B[12] = B[0] - bf * y / z_2;
+        B[13] = B[1] + bf * x / z_2;
+        B[14] = B[2];
+        B[15] = B[3];
+        B[16] = 0;
+        B[17] = B[5] - bf / z_2;
+    }
+    // constructQuadraticForm, robust branch (base_binary_edge.hpp:88-112)
+    const double info = e.info;
+    const double w = rho1 * info;
+    double om_r[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) om_r[k] = (-(info * err[k])) * rho1;
+    double* L = lin + (long long)kLinStride * ei;
+#pragma unroll
+    for (int cc = 0; cc < 3; cc++) {
+        double s = 0;
+        for (int k = 0; k < D; k++) s += A[3 * k + cc] * om_r[k];
+        L[kLinBl + cc] = s;
+    }
+#pragma unroll
+    for (int r = 0; r < 3; r++)
+#pragma unroll
+        for (int cc = r; cc < 3; cc++) {
+            double s = 0;
+            for (int k = 0; k < D; k++) s += (A[3 * k + r] * w) * A[3 * k + cc];
+            L[kLinHll + sym3(r, cc)] = s;
+        }
+    if (e.hp < 0) return;
+#pragma unroll
+    for (int r = 0; r < 6; r++)
+#pragma unroll
+        for (int cc = 0; cc < 3; cc++) {
+            double s = 0;
+            for (int k = 0; k < D; k++) s += (B[6 * k + r] * w) * A[3 * k + cc];
+            L[kLinHpl + 3 * r + cc] = s;
+        }
+#pragma unroll
+    for (int cc = 0; cc < 6; cc++) {
+        double s = 0;
+        for (int k = 0; k < D; k++) s += B[6 * k + cc] * om_r[k];
+        L[kLinBp + cc] = s;
+    }
+#pragma unroll
+    for (int r = 0; r < 6; r++)
+#pragma unroll
+        for (int cc = r; cc < 6; cc++) {
+            double s = 0;
+            for (int k = 0; k < D; k++) s += (B[6 * k + r] * w) * B[6 * k + cc];
+            L[kLinHpp + sym6(r, cc)] = s;
+        }
+}
+
+// Hll / b_l per point: sum over the point's edges in insertion order.
+__global__ void k_point_reduce(int npt_total, const int* __restrict__ pt_off, const int* __restrict__ pt_win,
+                               const WinCtl* __restrict__ ctl, const double* __restrict__ lin,
+                               double* __restrict__ Hll, double* __restrict__ bl) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npt_total) return;
+    if (!ctl[pt_win[p]].active) return;
+    double h[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
+    for (int e = pt_off[p]; e < pt_off[p + 1]; e++) {
+        const double* L = lin + (long long)kLinStride * e;
+#pragma unroll
+        for (int k = 0; k < 6; k++) h[k] += L[kLinHll + k];
+#pragma unroll
+        for (int k = 0; k < 3; k++) b[k] += L[kLinBl + k];
+    }
+#pragma unroll
+    for (int k = 0; k < 6; k++) Hll[8 * (long long)p + k] = h[k];
+#pragma unroll
+    for (int k = 0; k < 3; k++) bl[4 * (long long)p + k] = b[k];
+}
+
+// Hpp / b_p per free pose: thread per (pose, entry); edges of the pose in insertion order.
+__global__ void k_pose_reduce(int npose_total, const int* __restrict__ pe_off, const int* __restrict__ pe,
+                              const int* __restrict__ pose_win, const WinCtl* __restrict__ ctl,
+                              const double* __restrict__ lin, double* __restrict__ Hpp,
+                              double* __restrict__ bp) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int pose = t / 27, k = t % 27;
+    if (pose >= npose_total) return;
+    if (!ctl[pose_win[pose]].active) return;
+    const int src = k < 21 ? kLinHpp + k : kLinBp + (k - 21);
+    double s = 0;
+    for (int i = pe_off[pose]; i < pe_off[pose + 1]; i++) s += lin[(long long)kLinStride * pe[i] + src];
+    if (k < 21)
+        Hpp[24 * (long long)pose + k] = s;
+    else
+        bp[8 * (long long)pose + (k - 21)] = s;
+}
+
+// deterministic block sum / max (fixed tree over kCtlThreads lanes)
+__device__ inline double block_sum(double v, double* sh) {
+    sh[threadIdx.x] = v;
+    __syncthreads();
+    for (int s = kCtlThreads / 2; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) sh[threadIdx.x] += sh[threadIdx.x + s];
+        __syncthreads();
+    }
+    const double r = sh[0];
+    __syncthreads();
+    return r;
+}
+
+__device__ inline double block_max(double v, double* sh) {
+    sh[threadIdx.x] = v;
+    __syncthreads();
+    for (int s = kCtlThreads / 2; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) sh[threadIdx.x] = fmax(sh[threadIdx.x], sh[threadIdx.x + s]);
+        __syncthreads();
+    }
+    const double r = sh[0];
+    __syncthreads();
+    return r;
+}
+
+// OptimizationAlgorithmLevenberg::solve prologue (optimization_algorithm_levenberg.cpp:61-104)
+__global__ void __launch_bounds__(kCtlThreads) k_iter_begin(const WinDesc* __restrict__ wins,
+                                                            WinCtl* __restrict__ ctl,
+                                                            const double* __restrict__ rho,
+                                                            const double* __restrict__ Hpp,
+                                                            const double* __restrict__ Hll) {
+    __shared__ double sh[kCtlThreads];
+    const WinDesc W = wins[blockIdx.x];
+    WinCtl& C = ctl[blockIdx.x];
+    if (!C.active) return;
+    double s = 0;
+    for (int i = threadIdx.x; i < W.ne; i += kCtlThreads) s += rho[W.e0 + i];
+    const double chi = block_sum(s, sh);
+    double m = 0;
+    if (C.it == 0) {
+        for (int i = threadIdx.x; i < W.np; i += kCtlThreads)
+            for (int j = 0; j < 6; j++) m = fmax(m, fabs(Hpp[24 * (long long)(W.pose0 + i) + sym6(j, j)]));
+        for (int i = threadIdx.x; i < W.npt; i += kCtlThreads)
+            for (int j = 0; j < 3; j++) m = fmax(m, fabs(Hll[8 * (long long)(W.pt0 + i) + sym3(j, j)]));
+        m = block_max(m, sh);
+    }
+    if (threadIdx.x == 0) {
+        C.cur_chi = chi;
+        C.ini_chi = chi;
+        if (C.opt == 0 && C.it == 0) C.chi2_initial = chi;
+        if (C.it == 0) {
+            C.lambda = C.user_lambda > 0 ? C.user_lambda : 1e-5 * m;
+            C.ni = 2;
+            C.nbad = 0;
+        }
+        C.qmax = 0;
+        C.need_trial = 1;
+    }
+}
+
+// ---------------------------------------------------------------- trial kernels
+// Eigen 3x3 inverse by cofactors (Eigen/src/LU/InverseImpl.h)
+__device__ inline void inverse3(const double* m, double* out) {
+#define M_(i, j) m[3 * (i) + (j)]
+#define COF(i, j) (M_(((i) + 1) % 3, ((j) + 1) % 3) * M_(((i) + 2) % 3, ((j) + 2) % 3) - \
+                   M_(((i) + 1) % 3, ((j) + 2) % 3) * M_(((i) + 2) % 3, ((j) + 1) % 3))
+    const double c00 = COF(0, 0), c10 = COF(1, 0), c20 = COF(2, 0);
+    const double det = c00 * M_(0, 0) + c10 * M_(1, 0) + c20 * M_(2, 0);
+    const double invdet = 1.0 / det;
+    out[0] = c00 * invdet;
+    out[1] = c10 * invdet;
+    out[2] = c20 * invdet;
+    out[3] = COF(0, 1) * invdet;
+    out[4] = COF(1, 1) * invdet;
+    out[5] = COF(2, 1) * invdet;
+    out[6] = COF(0, 2) * invdet;
+    out[7] = COF(1, 2) * invdet;
+    out[8] = COF(2, 2) * invdet;
+#undef COF
+#undef M_
+}
+
+// Schur per landmark (block_solver.hpp:381-432): Dinv, db, then B Dinv and B db per edge.
+__global__ void k_schur_point(int npt_total, const int* __restrict__ spe_off, const int* __restrict__ spe,
+                              const int* __restrict__ pt_win, const WinCtl* __restrict__ ctl,
+                              const double* __restrict__ Hll, const double* __restrict__ bl,
+                              const double* __restrict__ lin, double* __restrict__ Dinv_out,
+                              double* __restrict__ tr) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npt_total) return;
+    const WinCtl& C = ctl[pt_win[p]];
+    if (!C.need_trial) return;
+    const double lam = C.lambda;
+    const double* h = Hll + 8 * (long long)p;
+    const double D[9] = {h[0] + lam, h[1], h[2], h[1], h[3] + lam, h[4], h[2], h[4], h[5] + lam};
+    double Di[9];
+    inverse3(D, Di);
+#pragma unroll
+    for (int k = 0; k < 9; k++) Dinv_out[12 * (long long)p + k] = Di[k];
+    const double* b = bl + 4 * (long long)p;
+    double db[3];
+#pragma unroll
+    for (int r = 0; r < 3; r++) db[r] = Di[3 * r] * b[0] + Di[3 * r + 1] * b[1] + Di[3 * r + 2] * b[2];
+    for (int i = spe_off[p]; i < spe_off[p + 1]; i++) {
+        const int e = spe[i];
+        const double* H = lin + (long long)kLinStride * e + kLinHpl;
+        double* T = tr + (long long)kTrStride * e;
+#pragma unroll
+        for (int r = 0; r < 6; r++) {
+            const double h0 = H[3 * r], h1 = H[3 * r + 1], h2 = H[3 * r + 2];
+#pragma unroll
+            for (int c = 0; c < 3; c++) T[3 * r + c] = h0 * Di[c] + h1 * Di[3 + c] + h2 * Di[6 + c];
+            T[18 + r] = h0 * db[0] + h1 * db[1] + h2 * db[2];
+        }
+    }
+}
+
+__device__ inline void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One wave per 6x6 block (i1 <= i2) of the Schur complement.  The reference block (i1, i2)
+// (upper) is written transposed into the lower triangle of the dense row-major matrix;
+// diagonal blocks also produce the rhs row b_s = b_p - sum B db (augmented row n).
+__global__ void k_schur_block(int nblk_total, const int2* __restrict__ blk_pose, const int* __restrict__ blk_win,
+                              const int* __restrict__ ct_off, const int2* __restrict__ ct,
+                              const WinDesc* __restrict__ wins, const WinCtl* __restrict__ ctl,
+                              const double* __restrict__ Hpp, const double* __restrict__ bp,
+                              const int* __restrict__ pe_off, const int* __restrict__ pe,
+                              const double* __restrict__ lin, const double* __restrict__ tr,
+                              double* __restrict__ Hs) {
+    const int blk = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (blk >= nblk_total) return;
+    const int lane = threadIdx.x & 63;
+    const int win = blk_win[blk];
+    const WinCtl& C = ctl[win];
+    if (!C.need_trial) return;
+    const WinDesc W = wins[win];
+    const int2 ij = blk_pose[blk];  // local free-pose indices i1 <= i2
+    const int i1 = ij.x, i2 = ij.y;
+    double* H = Hs + W.hs_off;
+    if (lane < 36) {
+        const int r = lane / 6, c = lane % 6;
+        double v = 0.0;
+        if (i1 == i2) {
+            const int rr = r <= c ? r : c, cc = r <= c ? c : r;
+            v = Hpp[24 * (long long)(W.pose0 + i1) + sym6(rr, cc)];
+            if (r == c) v += C.lambda;
+        }
+        for (int k = ct_off[blk]; k < ct_off[blk + 1]; k++) {
+            const int2 ab = ct[k];
+            const double* BD = tr + (long long)kTrStride * ab.x + 3 * r;
+            const double* Bj = lin + (long long)kLinStride * ab.y + kLinHpl + 3 * c;
+            v -= BD[0] * Bj[0] + BD[1] * Bj[1] + BD[2] * Bj[2];
+        }
+        // upper (i1, i2)[r][c] -> lower element (6 i2 + c, 6 i1 + r)
+        if (i1 != i2 || r <= c) H[(long long)(6 * i2 + c) * W.ld + 6 * i1 + r] = v;
+    } else if (lane < 42 && i1 == i2) {
+        const int r = lane - 36;
+        const int gp = W.pose0 + i1;
+        double s = 0;
+        for (int k = pe_off[gp]; k < pe_off[gp + 1]; k++) s += tr[(long long)kTrStride * pe[k] + 18 + r];
+        H[(long long)W.n * W.ld + 6 * i1 + r] = bp[8 * (long long)gp + r] - s;
+    }
+}
+
+// Dense LDL^T of the augmented lower-triangular (n+1) x (n+1) system [[Hs, .], [b_s^T, .]] in
+// place (row-major, leading dimension ld); the last row becomes z = D^-1 L^-1 b_s, then
+// L^T x = z.  Fails like Eigen's SimplicialLDLT::factorize only on an exactly zero pivot.
+// One 512-thread block per window; panels of kNB columns:
+//   (1) diagonal kNB x kNB block factored by wave 0 in registers (lane = row),
+//   (2) rows below: forward substitution, one thread per row,
+//   (3) trailing update with 4x4 register tiles against the panel held in LDS.
+__global__ void __launch_bounds__(512) k_ldlt(const WinDesc* __restrict__ wins, WinCtl* __restrict__ ctl,
+                                               double* __restrict__ Hs, double* __restrict__ xp_out) {
+    extern __shared__ double smem[];
+    const WinDesc W = wins[blockIdx.x];
+    WinCtl& C = ctl[blockIdx.x];
+    if (!C.need_trial) return;
+    const int n = W.n, N = n + 1, ld = W.ld;
+    double* A = Hs + W.hs_off;
+    double* PL = smem;                  // N x kNB panel (L values)
+    double* dsh = smem + (size_t)N * kNB;  // kNB pivots of the panel
+    double* rowbuf = dsh + kNB;            // pivot-row broadcast
+    double* WL = rowbuf + kNB;             // kNB x kNB: d_q L[j][q]
+    __shared__ int fail;
+    if (threadIdx.x == 0) fail = 0;
+    __syncthreads();
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    for (int kb = 0; kb < n; kb += kNB) {
+        const int nb = min(kNB, n - kb);
+        // (1) diagonal block: wave 0, lane = row (full symmetric row in registers); the
+        //     pivot row is broadcast through LDS each step
+        if (wid == 0) {
+            double row[kNB];
+#pragma unroll
+            for (int c = 0; c < kNB; c++) {
+                double v = 0.0;
+                if (lane < nb && c < nb) {
+                    const int gr = kb + lane, gc = kb + c;
+                    v = gc <= gr ? A[(long long)gr * ld + gc] : A[(long long)gc * ld + gr];
+                } else if (lane == c) {
+                    v = 1.0;
+                }
+                row[c] = v;
+            }
+            bool bad = false;
+#pragma unroll
+            for (int j = 0; j < kNB; j++) {
+                if (lane == j) {
+#pragma unroll
+                    for (int c = j; c < kNB; c++) rowbuf[c] = row[c];
+                }
+                wave_sync();
+                const double dj = rowbuf[j];
+                if (j < nb && dj == 0.0) bad = true;
+                if (lane > j) {
+                    const double lj = row[j] / dj;
+#pragma unroll
+                    for (int c = j + 1; c < kNB; c++) row[c] -= lj * rowbuf[c];
+                    row[j] = lj;
+                }
+                if (lane == j) dsh[j] = dj;
+                wave_sync();
+            }
+            if (bad && lane == 0) fail = 1;
+            if (lane < nb) {
+#pragma unroll
+                for (int c = 0; c < kNB; c++) {
+                    if (c < lane) {
+                        PL[(size_t)(kb + lane) * kNB + c] = row[c];
+                        A[(long long)(kb + lane) * ld + kb + c] = row[c];
+                    }
+                }
+            }
+            wave_sync();
+            if (lane < nb) {
+                A[(long long)(kb + lane) * ld + kb + lane] = dsh[lane];
+                // WL[j][q] = d_q L[j][q] for the forward substitution of the rows below
+#pragma unroll
+                for (int q = 0; q < kNB; q++) WL[lane * kNB + q] = q < lane ? dsh[q] * row[q] : 0.0;
+            }
+        }
+        __syncthreads();
+        if (fail) break;
+        // (2) rows below the diagonal block (including the rhs row n): one thread per row,
+        //     right-looking within the row
+        for (int r = kb + nb + tid; r < N; r += blockDim.x) {
+            double a[kNB];
+            double* Ar = A + (long long)r * ld + kb;
+#pragma unroll
+            for (int j = 0; j < kNB; j++) a[j] = j < nb ? Ar[j] : 0.0;
+#pragma unroll
+            for (int j = 0; j < kNB; j++) {
+                if (j < nb) {
+                    a[j] = a[j] / dsh[j];
+#pragma unroll
+                    for (int q = j + 1; q < kNB; q++) a[q] -= a[j] * WL[q * kNB + j];
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < kNB; j++) {
+                if (j < nb) {
+                    Ar[j] = a[j];
+                    PL[(size_t)r * kNB + j] = a[j];
+                }
+            }
+        }
+        __syncthreads();
+        // (3) trailing update: rows r >= R0 (to N-1), cols c in [R0, min(r, n-1)]
+        const int R0 = kb + nb;
+        const int mr = N - R0, mc = n - R0;
+        if (mc > 0) {
+            const int tr_n = (mr + 3) / 4, tc_n = (mc + 3) / 4;
+            for (int t = tid; t < tr_n * tc_n; t += blockDim.x) {
+                const int ti = t / tc_n, tj = t % tc_n;
+                if (tj > ti) continue;
+                const int r0 = R0 + 4 * ti, c0 = R0 + 4 * tj;
+                double acc[4][4];
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+#pragma unroll
+                    for (int j = 0; j < 4; j++) acc[i][j] = 0.0;
+                for (int q = 0; q < nb; q++) {
+                    const double dq = dsh[q];
+                    double a[4], b[4];
+#pragma unroll
+                    for (int i = 0; i < 4; i++) a[i] = (r0 + i < N) ? PL[(size_t)(r0 + i) * kNB + q] * dq : 0.0;
+#pragma unroll
+                    for (int j = 0; j < 4; j++) b[j] = (c0 + j < n) ? PL[(size_t)(c0 + j) * kNB + q] : 0.0;
+#pragma unroll
+                    for (int i = 0; i < 4; i++)
+#pragma unroll
+                        for (int j = 0; j < 4; j++) acc[i][j] += a[i] * b[j];
+                }
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const int r = r0 + i;
+                    if (r >= N) continue;
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const int c = c0 + j;
+                        if (c < n && c <= r) A[(long long)r * ld + c] -= acc[i][j];
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (fail) {
+        if (tid == 0) C.ok2 = 0;
+        return;
+    }
+    // backward solve L^T x = z; z lives in row n.  Blocks from the last one.
+    double* z = A + (long long)n * ld;
+    const int nblocks = (n + kNB - 1) / kNB;
+    for (int bi = nblocks - 1; bi >= 0; bi--) {
+        const int kb = bi * kNB, nb = min(kNB, n - kb);
+        if (wid == 0) {
+            double zi = lane < nb ? z[kb + lane] : 0.0;
+            for (int k = nb - 1; k >= 0; k--) {
+                const double xk = __shfl(zi, k, 64);
+                if (lane < k) zi -= A[(long long)(kb + k) * ld + kb + lane] * xk;
+            }
+            if (lane < nb) z[kb + lane] = zi;
+        }
+        __syncthreads();
+        for (int i = tid; i < kb; i += blockDim.x) {
+            double s = z[i];
+            for (int k = 0; k < nb; k++) s -= A[(long long)(kb + k) * ld + i] * z[kb + k];
+            z[i] = s;
+        }
+        __syncthreads();
+    }
+    for (int i = tid; i < n; i += blockDim.x) xp_out[6 * (long long)W.pose0 + i] = z[i];
+    if (tid == 0) C.ok2 = 1;
+}
+
+// x_l = Dinv (b_l - Hpl^T x_p) (block_solver.hpp:456-481) and the trial point estimate.
+__global__ void k_backsub(int npt_total, const int* __restrict__ spe_off, const int* __restrict__ spe,
+                          const EdgeS* __restrict__ E, const int* __restrict__ pt_win,
+                          const WinCtl* __restrict__ ctl, const double* __restrict__ bl,
+                          const double* __restrict__ Dinv, const double* __restrict__ lin,
+                          const double* __restrict__ xp, double* __restrict__ xl, double* __restrict__ pts,
+                          long long pt_stride) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npt_total) return;
+    const WinCtl& C = ctl[pt_win[p]];
+    if (!C.need_trial) return;
+    double* x = xl + 4 * (long long)p;
+    if (C.ok2) {  // a failed factorization leaves x untouched (block_solver.hpp:451-452)
+        double cl[3] = {bl[4 * (long long)p], bl[4 * (long long)p + 1], bl[4 * (long long)p + 2]};
+        for (int i = spe_off[p]; i < spe_off[p + 1]; i++) {
+            const int e = spe[i];
+            const double* H = lin + (long long)kLinStride * e + kLinHpl;
+            const double* xpp = xp + 6 * (long long)E[e].hp;
+#pragma unroll
+            for (int c = 0; c < 3; c++)
+#pragma unroll
+                for (int r = 0; r < 6; r++) cl[c] += H[3 * r + c] * (-xpp[r]);
+        }
+        const double* Di = Dinv + 12 * (long long)p;
+#pragma unroll
+        for (int r = 0; r < 3; r++) x[r] = Di[3 * r] * cl[0] + Di[3 * r + 1] * cl[1] + Di[3 * r + 2] * cl[2];
+    }
+    const double* cur = pts + C.sel * pt_stride + 4 * (long long)p;
+    double* nxt = pts + (1 - C.sel) * pt_stride + 4 * (long long)p;
+#pragma unroll
+    for (int k = 0; k < 3; k++) nxt[k] = cur[k] + x[k];
+}
+
+// VertexSE3Expmap::oplusImpl: T <- exp(x) * T  (types_six_dof_expmap.h:71-74, se3quat.h:223-257)
+__global__ void k_pose_update(int nkf_total, const int* __restrict__ kf_hp, const int* __restrict__ kf_win,
+                              const WinCtl* __restrict__ ctl, const double* __restrict__ xp,
+                              double* __restrict__ poses, long long pose_stride) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nkf_total) return;
+    const WinCtl& C = ctl[kf_win[k]];
+    if (!C.need_trial) return;
+    const double* cur = poses + C.sel * pose_stride + 8 * (long long)k;
+    double* nxt = poses + (1 - C.sel) * pose_stride + 8 * (long long)k;
+    const int h = kf_hp[k];
+    if (h < 0) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) nxt[i] = cur[i];
+        return;
+    }
+    const double* u = xp + 6 * (long long)h;
+    const double om[3] = {u[0], u[1], u[2]}, up[3] = {u[3], u[4], u[5]};
+    const double theta = sqrt(om[0] * om[0] + om[1] * om[1] + om[2] * om[2]);
+    const double Wm[9] = {0, -om[2], om[1], om[2], 0, -om[0], -om[1], om[0], 0};
+    double W2[9];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++)
+            W2[3 * i + j] = Wm[3 * i + 0] * Wm[0 + j] + Wm[3 * i + 1] * Wm[3 + j] + Wm[3 * i + 2] * Wm[6 + j];
+    double R[9], V[9];
+    if (theta < 0.00001) {
+#pragma unroll
+        for (int i = 0; i < 9; i++) {
+            R[i] = ((i % 4 == 0) ? 1.0 : 0.0) + Wm[i] + W2[i];
+            V[i] = R[i];
+        }
+    } else {
+        const double st = sin(theta), ct = cos(theta);
+        const double a = st / theta;
+        const double b = (1 - ct) / (theta * theta);
+        const double c = (theta - st) / pow(theta, 3);
+#pragma unroll
+        for (int i = 0; i < 9; i++) {
+            const double I = (i % 4 == 0) ? 1.0 : 0.0;
+            R[i] = I + a * Wm[i] + b * W2[i];
+            V[i] = I + b * Wm[i] + c * W2[i];
+        }
+    }
+    Quat qe = quat_from_R(R);
+    double te[3];
+#pragma unroll
+    for (int i = 0; i < 3; i++) te[i] = V[3 * i + 0] * up[0] + V[3 * i + 1] * up[1] + V[3 * i + 2] * up[2];
+    normalize_rotation(qe);
+    // exp * T  (SE3Quat::operator*)
+    const Quat qt = load_q(cur);
+    double rt[3];
+    quat_rotate(qe, cur + 4, rt);
+    Quat r;
+    r.w = qe.w * qt.w - qe.x * qt.x - qe.y * qt.y - qe.z * qt.z;
+    r.x = qe.w * qt.x + qe.x * qt.w + qe.y * qt.z - qe.z * qt.y;
+    r.y = qe.w * qt.y + qe.y * qt.w + qe.z * qt.x - qe.x * qt.z;
+    r.z = qe.w * qt.z + qe.z * qt.w + qe.x * qt.y - qe.y * qt.x;
+    normalize_rotation(r);
+    nxt[0] = r.x;
+    nxt[1] = r.y;
+    nxt[2] = r.z;
+    nxt[3] = r.w;
+    nxt[4] = te[0] + rt[0];
+    nxt[5] = te[1] + rt[1];
+    nxt[6] = te[2] + rt[2];
+    nxt[7] = 0.0;
+}
+
+__global__ void k_trial_error(int ne_total, const EdgeS* __restrict__ E, const WinCtl* __restrict__ ctl,
+                              const double* __restrict__ poses, const double* __restrict__ pts,
+                              long long pose_stride, long long pt_stride, Cam cam, Huber hk,
+                              double* __restrict__ err_out, double* __restrict__ rho_out) {
+    const int ei = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ei >= ne_total) return;
+    const EdgeS e = E[ei];
+    const WinCtl& C = ctl[e.win];
+    if (!C.need_trial) return;
+    const double* P = poses + (1 - C.sel) * pose_stride + 8 * (long long)e.kf;
+    const double* Xw = pts + (1 - C.sel) * pt_stride + 4 * (long long)e.pt;
+    const double X[3] = {Xw[0], Xw[1], Xw[2]};
+    double err[3];
+    edge_error(e, cam, P, X, err);
+    err_out[4 * (long long)ei + 0] = err[0];
+    err_out[4 * (long long)ei + 1] = err[1];
+    err_out[4 * (long long)ei + 2] = err[2];
+    double rho0, rho1;
+    robustify(hk, e.obs[2] >= 0.f, edge_chi2(e, err), rho0, rho1);
+    rho_out[ei] = rho0;
+}
+
+// The trial-loop body after the error pass (optimization_algorithm_levenberg.cpp:117-166).
+__global__ void __launch_bounds__(kCtlThreads) k_trial_control(const WinDesc* __restrict__ wins,
+                                                               WinCtl* __restrict__ ctl,
+                                                               const double* __restrict__ rho,
+                                                               const double* __restrict__ xp,
+                                                               const double* __restrict__ xl,
+                                                               const double* __restrict__ bp,
+                                                               const double* __restrict__ bl, int stop) {
+    __shared__ double sh[kCtlThreads];
+    const WinDesc W = wins[blockIdx.x];
+    WinCtl& C = ctl[blockIdx.x];
+    if (!C.need_trial) return;
+    double s = 0;
+    for (int i = threadIdx.x; i < W.ne; i += kCtlThreads) s += rho[W.e0 + i];
+    double tmpChi = block_sum(s, sh);
+    const double lam = C.lambda;
+    double sc = 0;
+    for (int i = threadIdx.x; i < 6 * W.np; i += kCtlThreads) {
+        const double xv = xp[6 * (long long)W.pose0 + i];
+        sc += xv * (lam * xv + bp[8 * (long long)(W.pose0 + i / 6) + i % 6]);
+    }
+    for (int i = threadIdx.x; i < 3 * W.npt; i += kCtlThreads) {
+        const long long p = W.pt0 + i / 3;
+        const double xv = xl[4 * p + i % 3];
+        sc += xv * (lam * xv + bl[4 * p + i % 3]);
+    }
+    double scale = block_sum(sc, sh);
+    if (threadIdx.x != 0) return;
+    if (!C.ok2) tmpChi = __DBL_MAX__;
+    double rho_ = C.cur_chi - tmpChi;
+    scale += 1e-3;
+    rho_ /= scale;
+    C.tmp_chi = tmpChi;
+    if (rho_ > 0 && isfinite(tmpChi)) {
+        double alpha = 1. - pow((2 * rho_ - 1), 3);
+        alpha = fmin(alpha, 2. / 3.);
+        const double f = fmax(1. / 3., alpha);
+        C.lambda = lam * f;
+        C.ni = 2;
+        C.cur_chi = tmpChi;
+        C.sel = 1 - C.sel;  // discardTop: the trial state becomes the estimate
+    } else {
+        C.lambda = lam * C.ni;
+        C.ni *= 2;           // pop: keep the previous estimate
+    }
+    C.qmax++;
+    C.trials++;
+    const bool again = rho_ < 0 && C.qmax < 10 && !stop;
+    if (again) {
+        C.need_trial = 1;
+        return;
+    }
+    C.need_trial = 0;
+    int result = 0;  // OK
+    if (C.qmax == 10 || rho_ == 0) {
+        result = 1;  // Terminate
+    } else {
+        if ((C.ini_chi - C.cur_chi) * 1e3 < C.ini_chi)
+            C.nbad++;
+        else
+            C.nbad = 0;
+        if (C.nbad >= 3) result = 1;
+    }
+    C.iters_run[C.opt]++;
+    C.it++;
+    C.chi2_final = C.cur_chi;
+    C.active = (result == 0) && C.it < C.iters && !stop;
+}
+
+// windows still in the trial loop / still iterating (read back by the host once per trial)
+__global__ void k_count(int nwin, const WinCtl* __restrict__ ctl, Counters* __restrict__ cnt) {
+    __shared__ int need, act;
+    if (threadIdx.x == 0) need = act = 0;
+    __syncthreads();
+    int a = 0, b = 0;
+    for (int w = threadIdx.x; w < nwin; w += blockDim.x) {
+        a += ctl[w].need_trial;
+        b += ctl[w].active;
+    }
+    atomicAdd(&need, a);
+    atomicAdd(&act, b);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        cnt->need_trial = need;
+        cnt->active = act;
+    }
+}
+
+// start of SparseOptimizer::optimize(iters) for every window
+__global__ void k_opt_begin(int nwin, const WinDesc* __restrict__ wins, WinCtl* __restrict__ ctl, int opt,
+                            int iters) {
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= nwin) return;
+    WinCtl& C = ctl[w];
+    C.opt = opt;
+    C.it = 0;
+    C.iters = iters;
+    C.active = iters > 0 && wins[w].ne > 0;  // no edges: initializeOptimization fails
+    C.need_trial = 0;
+}
+
+// final outlier classification (Optimizer.cc:1995-2038) and float write-back (:2041-2077)
+__global__ void k_finalize_edges(int ne_total, const EdgeS* __restrict__ E, const WinCtl* __restrict__ ctl,
+                                 const double* __restrict__ poses, const double* __restrict__ pts,
+                                 long long pose_stride, long long pt_stride, const double* __restrict__ err,
+                                 uint8_t* __restrict__ outlier) {
+    const int ei = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ei >= ne_total) return;
+    const EdgeS e = E[ei];
+    const WinCtl& C = ctl[e.win];
+    const double* P = poses + C.sel * pose_stride + 8 * (long long)e.kf;
+    const double* Xw = pts + C.sel * pt_stride + 4 * (long long)e.pt;
+    const double X[3] = {Xw[0], Xw[1], Xw[2]};
+    double Xc[3];
+    se3_map(P, X, Xc);
+    const double ev[3] = {err[4 * (long long)ei], err[4 * (long long)ei + 1], err[4 * (long long)ei + 2]};
+    const bool stereo = e.obs[2] >= 0.f;
+    const double c = edge_chi2(e, ev);
+    outlier[ei] = (c > (stereo ? 7.815 : 5.991) || !(Xc[2] > 0.0)) ? 1 : 0;
+}
+
+__global__ void k_finalize_state(int nkf_total, int npt_total, const int* __restrict__ kf_win,
+                                 const int* __restrict__ pt_win, const WinCtl* __restrict__ ctl,
+                                 const double* __restrict__ poses, const double* __restrict__ pts,
+                                 long long pose_stride, long long pt_stride, float* __restrict__ kf_out,
+                                 float* __restrict__ pt_out) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < nkf_total) {
+        const double* P = poses + ctl[kf_win[t]].sel * pose_stride + 8 * (long long)t;
+        double R[9];
+        rot_matrix(load_q(P), R);
+        float* T = kf_out + 16 * (long long)t;
+        for (int i = 0; i < 3; i++) {
+            for (int j = 0; j < 3; j++) T[4 * i + j] = (float)R[3 * i + j];
+            T[4 * i + 3] = (float)P[4 + i];
+        }
+        T[12] = T[13] = T[14] = 0.f;
+        T[15] = 1.f;
+    } else if (t < nkf_total + npt_total) {
+        const int p = t - nkf_total;
+        const double* X = pts + ctl[pt_win[p]].sel * pt_stride + 4 * (long long)p;
+        for (int k = 0; k < 3; k++) pt_out[3 * (long long)p + k] = (float)X[k];
+    }
+}
+
+// Converter::toSE3Quat on the device for the initial estimates
+__global__ void k_init_state(int nkf_total, int npt_total, const float* __restrict__ kf_in,
+                             const float* __restrict__ pt_in, double* __restrict__ poses,
+                             double* __restrict__ pts) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < nkf_total) {
+        const float* T = kf_in + 16 * (long long)t;
+        double R[9];
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) R[3 * i + j] = T[4 * i + j];
+        Quat q = quat_from_R(R);
+        normalize_rotation(q);
+        double* P = poses + 8 * (long long)t;
+        P[0] = q.x;
+        P[1] = q.y;
+        P[2] = q.z;
+        P[3] = q.w;
+        P[4] = T[3];
+        P[5] = T[7];
+        P[6] = T[11];
+        P[7] = 0.0;
+    } else if (t < nkf_total + npt_total) {
+        const int p = t - nkf_total;
+        double* X = pts + 4 * (long long)p;
+        for (int k = 0; k < 3; k++) X[k] = pt_in[3 * (long long)p + k];
+        X[3] = 0.0;
+    }
+}
+
+}  // namespace lba
+}  // namespace slamhot
+
+// ==================================================================== host side
+using namespace slamhot;
+using namespace slamhot::lba;
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        hipError_t e = hipMalloc(&p, std::max<size_t>(bytes, 256));
+        if (e == hipSuccess) cap = std::max<size_t>(bytes, 256);
+        return e;
+    }
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+};
+
+template <class T>
+T* as(DevBuf& b) {
+    return (T*)b.p;
+}
+
+}  // namespace
+
+struct slam_lba {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    Counters* h_cnt = nullptr;  // pinned
+    double last_ms = 0;
+    int last_syncs = 0;
+    // device buffers
+    DevBuf edges, wins, ctl, cnt, pt_off, pt_win, spe_off, spe, pe_off, pe, pose_win, kf_hp, kf_win;
+    DevBuf blk_pose, blk_win, ct_off, ct;
+    DevBuf poses, pts, err, rho, lin, Hll, bl, Hpp, bp, Dinv, tr, xp, xl, Hs;
+    DevBuf kf_in, pt_in, kf_out, pt_out, outl;
+};
+
+namespace {
+
+struct HostPlan {
+    std::vector<EdgeS> edges;
+    std::vector<WinDesc> wins;
+    std::vector<int> pt_off, pt_win, spe_off, spe, pe_off, pe, pose_win, kf_hp, kf_win;
+    std::vector<int2> blk_pose, ct;
+    std::vector<int> blk_win, ct_off;
+    std::vector<float> kf_in, pt_in;
+    int nkf = 0, npt = 0, ne = 0, npose = 0, nblk = 0;
+    long long hs_total = 0;
+};
+
+slam_status build_plan(int n_prob, const slam_lba_problem* probs, HostPlan& H) {
+    for (int w = 0; w < n_prob; w++) {
+        const slam_lba_problem& P = probs[w];
+        if (P.n_kf < 0 || P.n_pt < 0 || P.n_edge < 0) return SLAM_EINVAL;
+        if ((P.n_kf && (!P.kf_Tcw || !P.kf_fixed)) || (P.n_pt && !P.pt_pos) ||
+            (P.n_edge && (!P.edge_pt || !P.edge_kf || !P.edge_obs || !P.edge_inv_sigma2)))
+            return SLAM_EINVAL;
+        WinDesc D{};
+        D.kf0 = H.nkf;
+        D.nk = P.n_kf;
+        D.pt0 = H.npt;
+        D.npt = P.n_pt;
+        D.e0 = H.ne;
+        D.ne = P.n_edge;
+        D.pose0 = H.npose;
+        // a KeyFrame without edges is not an active vertex (sparse_optimizer.cpp:262-300):
+        // it stays out of the Hessian and keeps its estimate
+        std::vector<int> kf_edges(P.n_kf, 0);
+        for (int i = 0; i < P.n_edge; i++)
+            if (P.edge_kf[i] >= 0 && P.edge_kf[i] < P.n_kf) kf_edges[P.edge_kf[i]]++;
+        std::vector<int> hidx(P.n_kf, -1);
+        int np = 0;
+        for (int k = 0; k < P.n_kf; k++) {
+            if (P.kf_fixed[k] == 0 && kf_edges[k] > 0) hidx[k] = np++;
+            H.kf_hp.push_back(hidx[k] >= 0 ? H.npose + hidx[k] : -1);
+            H.kf_win.push_back(w);
+            for (int i = 0; i < 16; i++) H.kf_in.push_back(P.kf_Tcw[16 * k + i]);
+        }
+        D.np = np;
+        D.n = 6 * np;
+        if (D.n > kMaxN) return SLAM_ECAP;
+        D.ld = D.n + 1;
+        D.hs_off = H.hs_total;
+        H.hs_total += (long long)(D.n + 1) * D.ld;
+        for (int i = 0; i < 3 * P.n_pt; i++) H.pt_in.push_back(P.pt_pos[i]);
+        // edges (point-major), point CSR
+        std::vector<int> cnt(P.n_pt + 1, 0);
+        for (int i = 0; i < P.n_edge; i++) {
+            const int p = P.edge_pt[i], k = P.edge_kf[i];
+            if (p < 0 || p >= P.n_pt || k < 0 || k >= P.n_kf) return SLAM_EINVAL;
+            if (i && p < P.edge_pt[i - 1]) return SLAM_EINVAL;  // point-major insertion order
+            cnt[p + 1]++;
+            EdgeS e;
+            e.pt = H.npt + p;
+            e.kf = H.nkf + k;
+            e.hp = hidx[k] >= 0 ? H.npose + hidx[k] : -1;
+            e.win = w;
+            e.obs[0] = P.edge_obs[3 * i];
+            e.obs[1] = P.edge_obs[3 * i + 1];
+            e.obs[2] = P.edge_obs[3 * i + 2];
+            e.info = P.edge_inv_sigma2[i];
+            H.edges.push_back(e);
+        }
+        for (int p = 0; p < P.n_pt; p++) {
+            H.pt_off.push_back(H.ne + cnt[p]);
+            cnt[p + 1] += cnt[p];
+            H.pt_win.push_back(w);
+        }
+        // per point: edges with a free pose, sorted by pose (HplCCS column order)
+        std::vector<std::vector<int>> pose_edges(np);
+        std::vector<int> col;
+        std::vector<std::vector<int2>> blist((size_t)np * (np + 1) / 2);
+        for (int p = 0; p < P.n_pt; p++) {
+            H.spe_off.push_back((int)H.spe.size());
+            col.clear();
+            for (int i = cnt[p]; i < cnt[p + 1]; i++)
+                if (hidx[P.edge_kf[i]] >= 0) col.push_back(i);
+            std::stable_sort(col.begin(), col.end(),
+                             [&](int a, int b) { return hidx[P.edge_kf[a]] < hidx[P.edge_kf[b]]; });
+            for (size_t a = 0; a < col.size(); a++) {
+                H.spe.push_back(H.ne + col[a]);
+                const int i1 = hidx[P.edge_kf[col[a]]];
+                for (size_t b = a; b < col.size(); b++) {
+                    const int i2 = hidx[P.edge_kf[col[b]]];
+                    if (i2 == i1 && b != a) return SLAM_EINVAL;  // two observations of one point in one KF
+                    blist[(size_t)i2 * (i2 + 1) / 2 + i1].push_back(int2{H.ne + col[a], H.ne + col[b]});
+                }
+            }
+        }
+        for (int i = 0; i < P.n_edge; i++)
+            if (hidx[P.edge_kf[i]] >= 0) pose_edges[hidx[P.edge_kf[i]]].push_back(H.ne + i);
+        for (int i = 0; i < np; i++) {
+            H.pe_off.push_back((int)H.pe.size());
+            for (int e : pose_edges[i]) H.pe.push_back(e);
+            H.pose_win.push_back(w);
+        }
+        D.blk0 = H.nblk;
+        D.nblk = (int)blist.size();
+        for (int i2 = 0; i2 < np; i2++)
+            for (int i1 = 0; i1 <= i2; i1++) {
+                const auto& L = blist[(size_t)i2 * (i2 + 1) / 2 + i1];
+                H.blk_pose.push_back(int2{i1, i2});
+                H.blk_win.push_back(w);
+                H.ct_off.push_back((int)H.ct.size());
+                H.ct.insert(H.ct.end(), L.begin(), L.end());
+            }
+        H.nblk += D.nblk;
+        H.nkf += P.n_kf;
+        H.npt += P.n_pt;
+        H.ne += P.n_edge;
+        H.npose += np;
+        H.wins.push_back(D);
+    }
+    H.pt_off.push_back(H.ne);
+    H.spe_off.push_back((int)H.spe.size());
+    H.pe_off.push_back((int)H.pe.size());
+    H.ct_off.push_back((int)H.ct.size());
+    return SLAM_OK;
+}
+
+template <class T>
+hipError_t upload(DevBuf& b, const std::vector<T>& v, hipStream_t s) {
+    hipError_t e = b.ensure(sizeof(T) * std::max<size_t>(v.size(), 1));
+    if (e != hipSuccess || v.empty()) return e;
+    return hipMemcpyAsync(b.p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, s);
+}
+
+inline unsigned blocks(long long n, int t) { return (unsigned)std::max<long long>(1, (n + t - 1) / t); }
+
+}  // namespace
+
+extern "C" {
+
+slam_status slamhot_lba_create(int device, slam_lba** out) {
+    if (!out) return SLAM_EINVAL;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return SLAM_ENODEV;
+    if (device < 0 || device >= n) return SLAM_EINVAL;
+    slam_lba* s = new (std::nothrow) slam_lba();
+    if (!s) return SLAM_ENOMEM;
+    s->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&s->ev0) != hipSuccess || hipEventCreate(&s->ev1) != hipSuccess ||
+        hipHostMalloc((void**)&s->h_cnt, sizeof(Counters), hipHostMallocDefault) != hipSuccess) {
+        slamhot_lba_destroy(s);
+        return SLAM_EHIP;
+    }
+    if (hipFuncSetAttribute((const void*)k_ldlt, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)(((kMaxN + 1) * kNB + 2 * kNB + kNB * kNB) * sizeof(double))) != hipSuccess) {
+        slamhot_lba_destroy(s);
+        return SLAM_EHIP;
+    }
+    *out = s;
+    return SLAM_OK;
+}
+
+void slamhot_lba_destroy(slam_lba* s) {
+    if (!s) return;
+    (void)hipSetDevice(s->device);
+    if (s->stream) (void)hipStreamSynchronize(s->stream);
+    if (s->h_cnt) (void)hipHostFree(s->h_cnt);
+    if (s->ev0) (void)hipEventDestroy(s->ev0);
+    if (s->ev1) (void)hipEventDestroy(s->ev1);
+    if (s->stream) (void)hipStreamDestroy(s->stream);
+    delete s;
+}
+
+slam_status slamhot_lba_last_stats(const slam_lba* s, double* device_ms, int* syncs) {
+    if (!s) return SLAM_EINVAL;
+    if (device_ms) *device_ms = s->last_ms;
+    if (syncs) *syncs = s->last_syncs;
+    return SLAM_OK;
+}
+
+slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* probs,
+                              const slam_lba_options* opt, const volatile int32_t* stop_flag,
+                              slam_lba_result* results) {
+    if (!s || n_prob < 0 || (n_prob && (!probs || !results)) || !opt) return SLAM_EINVAL;
+    if (opt->iters_first < 0 || opt->iters_second < 0) return SLAM_EINVAL;
+    for (int w = 0; w < n_prob; w++)
+        if ((probs[w].n_kf && !results[w].kf_Tcw) || (probs[w].n_pt && !results[w].pt_pos) ||
+            (probs[w].n_edge && !results[w].edge_outlier))
+            return SLAM_EINVAL;
+    if (n_prob == 0) return SLAM_OK;
+    HostPlan H;
+    slam_status st = build_plan(n_prob, probs, H);
+    if (st != SLAM_OK) return st;
+    const bool stop0 = stop_flag && *stop_flag;
+    for (int w = 0; w < n_prob; w++) {
+        slam_lba_result& R = results[w];
+        R.iterations[0] = R.iterations[1] = 0;
+        R.trials = 0;
+        R.n_outlier = 0;
+        R.chi2_initial = R.chi2_final = R.lambda_final = 0;
+    }
+    if (stop0) {  // Optimizer.cc:1921-1923: nothing optimized, nothing written back
+        for (int w = 0; w < n_prob; w++) {
+            const slam_lba_problem& P = probs[w];
+            std::memcpy(results[w].kf_Tcw, P.kf_Tcw, sizeof(float) * 16 * P.n_kf);
+            std::memcpy(results[w].pt_pos, P.pt_pos, sizeof(float) * 3 * P.n_pt);
+            std::memset(results[w].edge_outlier, 0, P.n_edge);
+        }
+        s->last_ms = 0;
+        s->last_syncs = 0;
+        return SLAM_OK;
+    }
+    SLAM_HIP_TRY(hipSetDevice(s->device));
+    hipStream_t S = s->stream;
+    const int nw = n_prob;
+    // host-side LM options per window
+    std::vector<WinCtl> ctl0(nw);
+    for (int w = 0; w < nw; w++) {
+        WinCtl c{};
+        c.user_lambda = opt->user_lambda_init;
+        c.lambda = -1;
+        c.ni = 2;
+        ctl0[w] = c;
+    }
+    const long long pose_stride = 8LL * std::max(H.nkf, 1), pt_stride = 4LL * std::max(H.npt, 1);
+    SLAM_HIP_TRY(upload(s->edges, H.edges, S));
+    SLAM_HIP_TRY(upload(s->wins, H.wins, S));
+    SLAM_HIP_TRY(upload(s->ctl, ctl0, S));
+    SLAM_HIP_TRY(s->cnt.ensure(sizeof(Counters)));
+    SLAM_HIP_TRY(upload(s->pt_off, H.pt_off, S));
+    SLAM_HIP_TRY(upload(s->pt_win, H.pt_win, S));
+    SLAM_HIP_TRY(upload(s->spe_off, H.spe_off, S));
+    SLAM_HIP_TRY(upload(s->spe, H.spe, S));
+    SLAM_HIP_TRY(upload(s->pe_off, H.pe_off, S));
+    SLAM_HIP_TRY(upload(s->pe, H.pe, S));
+    SLAM_HIP_TRY(upload(s->pose_win, H.pose_win, S));
+    SLAM_HIP_TRY(upload(s->kf_hp, H.kf_hp, S));
+    SLAM_HIP_TRY(upload(s->kf_win, H.kf_win, S));
+    SLAM_HIP_TRY(upload(s->blk_pose, H.blk_pose, S));
+    SLAM_HIP_TRY(upload(s->blk_win, H.blk_win, S));
+    SLAM_HIP_TRY(upload(s->ct_off, H.ct_off, S));
+    SLAM_HIP_TRY(upload(s->ct, H.ct, S));
+    SLAM_HIP_TRY(upload(s->kf_in, H.kf_in, S));
+    SLAM_HIP_TRY(upload(s->pt_in, H.pt_in, S));
+    const size_t ne = std::max(H.ne, 1), npt = std::max(H.npt, 1), nps = std::max(H.npose, 1);
+    SLAM_HIP_TRY(s->poses.ensure(sizeof(double) * 2 * pose_stride));
+    SLAM_HIP_TRY(s->pts.ensure(sizeof(double) * 2 * pt_stride));
+    SLAM_HIP_TRY(s->err.ensure(sizeof(double) * 4 * ne));
+    SLAM_HIP_TRY(s->rho.ensure(sizeof(double) * ne));
+    SLAM_HIP_TRY(s->lin.ensure(sizeof(double) * kLinStride * ne));
+    SLAM_HIP_TRY(s->tr.ensure(sizeof(double) * kTrStride * ne));
+    SLAM_HIP_TRY(s->Hll.ensure(sizeof(double) * 8 * npt));
+    SLAM_HIP_TRY(s->bl.ensure(sizeof(double) * 4 * npt));
+    SLAM_HIP_TRY(s->Dinv.ensure(sizeof(double) * 12 * npt));
+    SLAM_HIP_TRY(s->xl.ensure(sizeof(double) * 4 * npt));
+    SLAM_HIP_TRY(s->Hpp.ensure(sizeof(double) * 24 * nps));
+    SLAM_HIP_TRY(s->bp.ensure(sizeof(double) * 8 * nps));
+    SLAM_HIP_TRY(s->xp.ensure(sizeof(double) * 6 * nps));
+    SLAM_HIP_TRY(s->Hs.ensure(sizeof(double) * std::max<long long>(H.hs_total, 1)));
+    SLAM_HIP_TRY(s->kf_out.ensure(sizeof(float) * 16 * std::max(H.nkf, 1)));
+    SLAM_HIP_TRY(s->pt_out.ensure(sizeof(float) * 3 * npt));
+    SLAM_HIP_TRY(s->outl.ensure(ne));
+    SLAM_HIP_TRY(hipMemsetAsync(s->xp.p, 0, sizeof(double) * 6 * nps, S));
+    SLAM_HIP_TRY(hipMemsetAsync(s->xl.p, 0, sizeof(double) * 4 * npt, S));
+    SLAM_HIP_TRY(hipMemsetAsync(s->err.p, 0, sizeof(double) * 4 * ne, S));
+
+    Cam cam;
+    const slam_camera& c0 = probs[0].cam;
+    for (int w = 1; w < nw; w++) {
+        const slam_camera& c = probs[w].cam;
+        if (c.fx != c0.fx || c.fy != c0.fy || c.cx != c0.cx || c.cy != c0.cy || c.bf != c0.bf)
+            return SLAM_EINVAL;  // one camera per batch
+    }
+    cam.fx = c0.fx;
+    cam.fy = c0.fy;
+    cam.cx = c0.cx;
+    cam.cy = c0.cy;
+    cam.bf = c0.bf;
+    cam.bff = c0.bf;
+    Huber hk;
+    const float thMono = std::sqrt(5.991), thStereo = std::sqrt(7.815);  // Optimizer.cc:1794-1795
+    hk.delta_mono = thMono;
+    hk.delta_stereo = thStereo;
+    hk.dsqr_mono = (float)(hk.delta_mono * hk.delta_mono);
+    hk.dsqr_stereo = (float)(hk.delta_stereo * hk.delta_stereo);
+
+    EdgeS* dE = as<EdgeS>(s->edges);
+    WinDesc* dW = as<WinDesc>(s->wins);
+    WinCtl* dC = as<WinCtl>(s->ctl);
+    Counters* dCnt = as<Counters>(s->cnt);
+    double* poses = as<double>(s->poses);
+    double* pts = as<double>(s->pts);
+    const int T = 256;
+    int syncs = 0;
+    SLAM_HIP_TRY(hipEventRecord(s->ev0, S));
+    k_init_state<<<blocks(H.nkf + H.npt, T), T, 0, S>>>(H.nkf, H.npt, as<float>(s->kf_in), as<float>(s->pt_in),
+                                                         poses, pts);
+    int max_n = 0;
+    for (const WinDesc& D : H.wins) max_n = std::max(max_n, D.n);
+    const size_t lds_bytes = ((size_t)(max_n + 1) * kNB + 2 * kNB + kNB * kNB) * sizeof(double);
+    bool stopped = false;
+    const int iters_of[2] = {opt->iters_first, opt->iters_second};
+    for (int o = 0; o < 2 && !stopped; o++) {
+        k_opt_begin<<<blocks(nw, 64), 64, 0, S>>>(nw, dW, dC, o, iters_of[o]);
+        for (int it = 0; it < iters_of[o]; it++) {
+            if (stop_flag && *stop_flag) {
+                stopped = true;
+                break;
+            }
+            k_linearize<<<blocks(H.ne, T), T, 0, S>>>(H.ne, dE, dC, poses, pts, pose_stride, pt_stride, cam, hk,
+                                                       as<double>(s->err), as<double>(s->rho), as<double>(s->lin));
+            k_point_reduce<<<blocks(H.npt, T), T, 0, S>>>(H.npt, as<int>(s->pt_off), as<int>(s->pt_win), dC,
+                                                           as<double>(s->lin), as<double>(s->Hll), as<double>(s->bl));
+            k_pose_reduce<<<blocks(27LL * H.npose, T), T, 0, S>>>(H.npose, as<int>(s->pe_off), as<int>(s->pe),
+                                                                   as<int>(s->pose_win), dC, as<double>(s->lin),
+                                                                   as<double>(s->Hpp), as<double>(s->bp));
+            k_iter_begin<<<nw, kCtlThreads, 0, S>>>(dW, dC, as<double>(s->rho), as<double>(s->Hpp),
+                                                    as<double>(s->Hll));
+            bool any_active = false;
+            for (int t = 0; t < 10; t++) {
+                k_schur_point<<<blocks(H.npt, T), T, 0, S>>>(H.npt, as<int>(s->spe_off), as<int>(s->spe),
+                                                              as<int>(s->pt_win), dC, as<double>(s->Hll),
+                                                              as<double>(s->bl), as<double>(s->lin),
+                                                              as<double>(s->Dinv), as<double>(s->tr));
+                if (H.nblk)
+                    k_schur_block<<<blocks(H.nblk, 4), 256, 0, S>>>(
+                        H.nblk, as<int2>(s->blk_pose), as<int>(s->blk_win), as<int>(s->ct_off), as<int2>(s->ct), dW,
+                        dC, as<double>(s->Hpp), as<double>(s->bp), as<int>(s->pe_off), as<int>(s->pe),
+                        as<double>(s->lin), as<double>(s->tr), as<double>(s->Hs));
+                k_ldlt<<<nw, 512, lds_bytes, S>>>(dW, dC, as<double>(s->Hs), as<double>(s->xp));
+                k_backsub<<<blocks(H.npt, T), T, 0, S>>>(H.npt, as<int>(s->spe_off), as<int>(s->spe), dE,
+                                                          as<int>(s->pt_win), dC, as<double>(s->bl),
+                                                          as<double>(s->Dinv), as<double>(s->lin), as<double>(s->xp),
+                                                          as<double>(s->xl), pts, pt_stride);
+                k_pose_update<<<blocks(H.nkf, T), T, 0, S>>>(H.nkf, as<int>(s->kf_hp), as<int>(s->kf_win), dC,
+                                                              as<double>(s->xp), poses, pose_stride);
+                k_trial_error<<<blocks(H.ne, T), T, 0, S>>>(H.ne, dE, dC, poses, pts, pose_stride, pt_stride, cam, hk,
+                                                             as<double>(s->err), as<double>(s->rho));
+                const int stop_now = (stop_flag && *stop_flag) ? 1 : 0;
+                k_trial_control<<<nw, kCtlThreads, 0, S>>>(dW, dC, as<double>(s->rho), as<double>(s->xp),
+                                                           as<double>(s->xl), as<double>(s->bp), as<double>(s->bl),
+                                                           stop_now);
+                k_count<<<1, 256, 0, S>>>(nw, dC, dCnt);
+                SLAM_HIP_TRY(hipGetLastError());
+                SLAM_HIP_TRY(hipMemcpyAsync(s->h_cnt, dCnt, sizeof(Counters), hipMemcpyDeviceToHost, S));
+                SLAM_HIP_TRY(hipStreamSynchronize(S));
+                syncs++;
+                if (stop_now) stopped = true;
+                any_active = s->h_cnt->active > 0;
+                if (s->h_cnt->need_trial == 0) break;
+            }
+            if (!any_active || stopped) break;
+        }
+    }
+    k_finalize_edges<<<blocks(H.ne, T), T, 0, S>>>(H.ne, dE, dC, poses, pts, pose_stride, pt_stride,
+                                                    as<double>(s->err), as<uint8_t>(s->outl));
+    k_finalize_state<<<blocks(H.nkf + H.npt, T), T, 0, S>>>(H.nkf, H.npt, as<int>(s->kf_win), as<int>(s->pt_win), dC,
+                                                             poses, pts, pose_stride, pt_stride,
+                                                             as<float>(s->kf_out), as<float>(s->pt_out));
+    SLAM_HIP_TRY(hipGetLastError());
+    SLAM_HIP_TRY(hipEventRecord(s->ev1, S));
+    std::vector<float> kf_out(16 * (size_t)H.nkf), pt_out(3 * (size_t)H.npt);
+    std::vector<uint8_t> outl(H.ne);
+    std::vector<WinCtl> ctl1(nw);
+    if (H.nkf) SLAM_HIP_TRY(hipMemcpyAsync(kf_out.data(), s->kf_out.p, sizeof(float) * kf_out.size(), hipMemcpyDeviceToHost, S));
+    if (H.npt) SLAM_HIP_TRY(hipMemcpyAsync(pt_out.data(), s->pt_out.p, sizeof(float) * pt_out.size(), hipMemcpyDeviceToHost, S));
+    if (H.ne) SLAM_HIP_TRY(hipMemcpyAsync(outl.data(), s->outl.p, outl.size(), hipMemcpyDeviceToHost, S));
+    SLAM_HIP_TRY(hipMemcpyAsync(ctl1.data(), s->ctl.p, sizeof(WinCtl) * nw, hipMemcpyDeviceToHost, S));
+    SLAM_HIP_TRY(hipStreamSynchronize(S));
+    float ms = 0;
+    SLAM_HIP_TRY(hipEventElapsedTime(&ms, s->ev0, s->ev1));
+    s->last_ms = ms;
+    s->last_syncs = syncs + 1;
+    for (int w = 0; w < nw; w++) {
+        const slam_lba_problem& P = probs[w];
+        const WinDesc& D = H.wins[w];
+        slam_lba_result& R = results[w];
+        for (int k = 0; k < P.n_kf; k++) {
+            const float* src = P.kf_fixed[k] == 2 ? P.kf_Tcw + 16 * k : &kf_out[16 * (size_t)(D.kf0 + k)];
+            std::memcpy(R.kf_Tcw + 16 * k, src, sizeof(float) * 16);
+        }
+        std::memcpy(R.pt_pos, &pt_out[3 * (size_t)D.pt0], sizeof(float) * 3 * P.n_pt);
+        int no = 0;
+        for (int i = 0; i < P.n_edge; i++) {
+            R.edge_outlier[i] = outl[D.e0 + i];
+            no += outl[D.e0 + i];
+        }
+        R.n_outlier = no;
+        const WinCtl& C = ctl1[w];
+        R.iterations[0] = C.iters_run[0];
+        R.iterations[1] = C.iters_run[1];
+        R.trials = C.trials;
+        R.chi2_initial = C.chi2_initial;
+        R.chi2_final = C.chi2_final;
+        R.lambda_final = C.lambda;
+    }
+    return SLAM_OK;
+}
+
+}  // extern "C"

@@ -436,3 +436,110 @@ def _matcher_methods():
 
 
 _matcher_methods()
+
+
+# ------------------------------------------------------------------------------------------
+# Local bundle adjustment (Optimizer::LocalBundleAdjustment, Optimizer.cc:1611-2078)
+# ------------------------------------------------------------------------------------------
+class Camera(C.Structure):
+    _fields_ = [("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float), ("bf", C.c_float)]
+
+
+class LbaProblem(C.Structure):
+    _fields_ = [("n_kf", C.c_int32), ("kf_Tcw", C.c_void_p), ("kf_fixed", C.c_void_p), ("n_pt", C.c_int32),
+                ("pt_pos", C.c_void_p), ("n_edge", C.c_int32), ("edge_pt", C.c_void_p), ("edge_kf", C.c_void_p),
+                ("edge_obs", C.c_void_p), ("edge_inv_sigma2", C.c_void_p), ("cam", Camera)]
+
+
+class LbaOptions(C.Structure):
+    _fields_ = [("iters_first", C.c_int32), ("iters_second", C.c_int32), ("user_lambda_init", C.c_double)]
+
+
+class LbaResult(C.Structure):
+    _fields_ = [("kf_Tcw", C.c_void_p), ("pt_pos", C.c_void_p), ("edge_outlier", C.c_void_p),
+                ("iterations", C.c_int32 * 2), ("trials", C.c_int32), ("n_outlier", C.c_int32),
+                ("chi2_initial", C.c_double), ("chi2_final", C.c_double), ("lambda_final", C.c_double)]
+
+
+_LBA_KEYS = {"kf_Tcw": np.float32, "kf_fixed": np.uint8, "pt_pos": np.float32, "edge_pt": np.int32,
+             "edge_kf": np.int32, "edge_obs": np.float32, "edge_inv_sigma2": np.float32}
+
+
+def make_lba_problem(w: dict):
+    """slam_lba_problem over a window dict (see synth.lba_window).  Returns (problem, result,
+    outputs) where outputs holds the numpy arrays the result points into."""
+    arrs = {k: np.ascontiguousarray(w[k], dt) for k, dt in _LBA_KEYS.items()}
+    n_kf, n_pt, n_e = len(arrs["kf_fixed"]), len(arrs["pt_pos"]), len(arrs["edge_pt"])
+    p = LbaProblem(n_kf, arrs["kf_Tcw"].ctypes.data, arrs["kf_fixed"].ctypes.data, n_pt,
+                   arrs["pt_pos"].ctypes.data, n_e, arrs["edge_pt"].ctypes.data, arrs["edge_kf"].ctypes.data,
+                   arrs["edge_obs"].ctypes.data, arrs["edge_inv_sigma2"].ctypes.data, Camera(*w["cam"]))
+    p._keep = arrs
+    out = dict(kf_Tcw=np.zeros((n_kf, 16), np.float32), pt_pos=np.zeros((n_pt, 3), np.float32),
+               edge_outlier=np.zeros(n_e, np.uint8))
+    r = LbaResult(out["kf_Tcw"].ctypes.data, out["pt_pos"].ctypes.data, out["edge_outlier"].ctypes.data)
+    r._keep = out
+    return p, r, out
+
+
+def lba_result_dict(r: LbaResult, out: dict) -> dict:
+    d = dict(out)
+    d.update(iterations=tuple(r.iterations), trials=r.trials, n_outlier=r.n_outlier,
+             chi2_initial=r.chi2_initial, chi2_final=r.chi2_final, lambda_final=r.lambda_final)
+    return d
+
+
+class LocalBundleAdjustment:
+    """Device LM/Schur solver behind ``slamhot_lba_solve`` — the numeric core of
+    ``Optimizer::LocalBundleAdjustment`` (Optimizer.h:59).  ``solve`` takes one window dict or
+    a list of them (batched mode) and returns result dicts."""
+
+    def __init__(self, device: int = 0):
+        L = lib()
+        _bind_lba(L)
+        h = P()
+        check(L.slamhot_lba_create(device, C.byref(h)), "lba_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().slamhot_lba_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def solve(self, windows, iters_first=5, iters_second=10, user_lambda_init=0.0, stop_flag=None):
+        single = isinstance(windows, dict)
+        ws = [windows] if single else list(windows)
+        probs = (LbaProblem * len(ws))()
+        ress = (LbaResult * len(ws))()
+        outs = []
+        for i, w in enumerate(ws):
+            p, r, o = make_lba_problem(w)
+            probs[i] = p
+            ress[i] = r
+            outs.append((p, r, o))
+        opt = LbaOptions(iters_first, iters_second, user_lambda_init)
+        stop = None if stop_flag is None else C.byref(C.c_int32(int(stop_flag)))
+        check(lib().slamhot_lba_solve(self._h, len(ws), probs, C.byref(opt), stop, ress), "lba_solve")
+        res = [lba_result_dict(ress[i], outs[i][2]) for i in range(len(ws))]
+        return res[0] if single else res
+
+    def last_stats(self):
+        ms, syncs = C.c_double(0), I(0)
+        check(lib().slamhot_lba_last_stats(self._h, C.byref(ms), C.byref(syncs)), "lba_last_stats")
+        return ms.value, syncs.value
+
+
+def _bind_lba(L):
+    if getattr(L, "_lba_ready", False):
+        return
+    L.slamhot_lba_create.argtypes = [I, C.POINTER(P)]
+    L.slamhot_lba_destroy.argtypes = [P]
+    L.slamhot_lba_destroy.restype = None
+    L.slamhot_lba_solve.argtypes = [P, I, C.POINTER(LbaProblem), C.POINTER(LbaOptions), P, C.POINTER(LbaResult)]
+    L.slamhot_lba_last_stats.argtypes = [P, C.POINTER(C.c_double), C.POINTER(I)]
+    L._lba_ready = True

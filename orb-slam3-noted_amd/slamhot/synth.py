@@ -115,3 +115,135 @@ def feature_vector(node_id: np.ndarray, weight: np.ndarray):
     uniq, starts = np.unique(nid_s, return_index=True)
     off = np.append(starts, len(nid_s)).astype(np.int32)
     return uniq.astype(np.uint32), off, feats
+
+
+# ------------------------------------------------------------------------------------------
+# Synthetic local-BA windows
+# ------------------------------------------------------------------------------------------
+EUROC_CAM = dict(fx=435.2047, fy=435.2047, cx=367.4517, cy=252.2009, bf=47.9064, w=752, h=480)
+
+
+def _axis_angle(axis, ang):
+    axis = axis / np.linalg.norm(axis)
+    K = np.array([[0, -axis[2], axis[1]], [axis[2], 0, -axis[0]], [-axis[1], axis[0], 0]])
+    return np.eye(3) + np.sin(ang) * K + (1 - np.cos(ang)) * K @ K
+
+
+def _level_tables(nfeatures=1000, scale_factor=1.2, nlevels=8):
+    """Float scale / inverse-sigma^2 tables and per-level feature split as ORBextractor builds
+    them (ORBextractor.cc:413-444)."""
+    sf = np.float64(np.float32(scale_factor))
+    scale = [np.float32(1.0)]
+    for _ in range(1, nlevels):
+        scale.append(np.float32(np.float64(scale[-1]) * sf))
+    scale = np.array(scale, np.float32)
+    inv_sigma2 = (np.float32(1.0) / (scale * scale)).astype(np.float32)
+    factor = 1.0 / sf
+    per = nfeatures * (1 - factor) / (1 - factor ** nlevels)
+    nf = []
+    for _ in range(nlevels - 1):
+        nf.append(round(per))
+        per *= factor
+    nf.append(max(nfeatures - sum(nf), 0))
+    return scale, inv_sigma2, np.array(nf, np.float64)
+
+
+def lba_window(seed: int, n_kf: int = 50, n_pt: int = 2000, obs_per_pt: int = 8,
+               stereo_frac: float = 0.0, outlier_frac: float = 0.02, arc_deg: float = 80.0,
+               radius: float = 3.0):
+    """A seeded local-BA window in the layout of slam_lba_problem.
+
+    50 KeyFrames on a ``radius`` arc facing a 4 x 2 x 4 m box of points; every point is seen
+    by exactly ``obs_per_pt`` KeyFrames drawn among those where it projects in-image with
+    z > 0.3 m; octave drawn with the extractor's per-level feature split; pixel noise
+    N(0, 1.2^l); ``outlier_frac`` observations replaced by uniform in-image points;
+    KF poses perturbed by 0.5 deg / 2 cm and points by 3 cm.  KF 0 is the map-init KF
+    (fixed, written back) and KF 1 is the fallback fixed camera (kf_fixed = 2), so 48 KFs
+    are free.  Edges are point-major, KFs in id order."""
+    rng = np.random.default_rng(seed)
+    cam = EUROC_CAM
+    scale, inv_sigma2, nf = _level_tables()
+    p_level = nf / nf.sum()
+    # ground-truth poses Tcw
+    Rs, ts = [], []
+    for k in range(n_kf):
+        a = np.deg2rad(-arc_deg / 2 + arc_deg * k / max(n_kf - 1, 1))
+        C = np.array([radius * np.sin(a), 0.3 * np.sin(3 * a), -radius * np.cos(a)])
+        z = -C / np.linalg.norm(C)
+        x = np.cross(np.array([0.0, -1.0, 0.0]), z)
+        x /= np.linalg.norm(x)
+        y = np.cross(z, x)
+        R = np.stack([x, y, z])  # rows: camera axes in world
+        Rs.append(R)
+        ts.append(-R @ C)
+    Rs, ts = np.array(Rs), np.array(ts)
+    # points: resample until each has enough observing KFs
+    pts = np.zeros((n_pt, 3))
+    obs_kf = []
+    i = 0
+    while i < n_pt:
+        X = rng.uniform([-2, -1, -2], [2, 1, 2])
+        Xc = np.einsum("kij,j->ki", Rs, X) + ts
+        z = Xc[:, 2]
+        with np.errstate(divide="ignore", invalid="ignore"):
+            u = cam["fx"] * Xc[:, 0] / z + cam["cx"]
+            v = cam["fy"] * Xc[:, 1] / z + cam["cy"]
+        ok = (z > 0.3) & (u >= 0) & (u < cam["w"]) & (v >= 0) & (v < cam["h"])
+        cand = np.flatnonzero(ok)
+        if len(cand) < obs_per_pt:
+            continue
+        pts[i] = X
+        obs_kf.append(np.sort(rng.choice(cand, obs_per_pt, replace=False)))
+        i += 1
+    edge_pt, edge_kf, obs, isig = [], [], [], []
+    for p in range(n_pt):
+        for k in obs_kf[p]:
+            Xc = Rs[k] @ pts[p] + ts[k]
+            lvl = rng.choice(len(p_level), p=p_level)
+            s = float(scale[lvl])
+            u = cam["fx"] * Xc[0] / Xc[2] + cam["cx"] + rng.normal(0, s)
+            v = cam["fy"] * Xc[1] / Xc[2] + cam["cy"] + rng.normal(0, s)
+            ur = -1.0
+            stereo = rng.random() < stereo_frac
+            if stereo:
+                ur = u - cam["bf"] / Xc[2] + rng.normal(0, s)
+            if rng.random() < outlier_frac:
+                u = rng.uniform(0, cam["w"])
+                v = rng.uniform(0, cam["h"])
+                if stereo:
+                    ur = u - rng.uniform(0, 40)
+            if stereo and ur < 0:
+                ur = 0.0
+            edge_pt.append(p)
+            edge_kf.append(k)
+            obs.append((u, v, ur))
+            isig.append(inv_sigma2[lvl])
+    # perturbed initial estimates
+    T0 = np.zeros((n_kf, 16), np.float32)
+    for k in range(n_kf):
+        R, t = Rs[k], ts[k]
+        if k >= 2:
+            R = _axis_angle(rng.normal(size=3), np.deg2rad(0.5)) @ R
+            d = rng.normal(size=3)
+            t = t + 0.02 * d / np.linalg.norm(d)
+        M = np.eye(4)
+        M[:3, :3] = R
+        M[:3, 3] = t
+        T0[k] = M.reshape(-1).astype(np.float32)
+    d = rng.normal(size=(n_pt, 3))
+    P0 = (pts + 0.03 * d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
+    fixed = np.zeros(n_kf, np.uint8)
+    fixed[0] = 1
+    if n_kf > 2:
+        fixed[1] = 2
+    gt_T = np.zeros((n_kf, 4, 4))
+    gt_T[:, :3, :3] = Rs
+    gt_T[:, :3, 3] = ts
+    gt_T[:, 3, 3] = 1
+    return dict(
+        kf_Tcw=T0, kf_fixed=fixed, pt_pos=P0,
+        edge_pt=np.array(edge_pt, np.int32), edge_kf=np.array(edge_kf, np.int32),
+        edge_obs=np.array(obs, np.float32), edge_inv_sigma2=np.array(isig, np.float32),
+        cam=(np.float32(cam["fx"]), np.float32(cam["fy"]), np.float32(cam["cx"]),
+             np.float32(cam["cy"]), np.float32(cam["bf"])),
+        gt_T=gt_T, gt_pts=pts)

@@ -279,3 +279,17 @@ def search_by_projection_kf(fv, kf, nnratio, check_ori, th, orb_dist):
     n = _plib().oracle_search_by_projection_kf(C.addressof(fv), C.addressof(kf), nnratio, int(check_ori), th,
                                                int(orb_dist), _ptr(fm))
     return n, fm
+
+
+# ---- local bundle adjustment (oracle/lba_oracle.cpp)
+def lba_solve(w, iters_first=5, iters_second=10, user_lambda_init=0.0, stop=0):
+    import slamhot
+    L = lib()
+    if not hasattr(L, "_lba_ready"):
+        L.oracle_lba_solve.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
+        L.oracle_lba_solve.restype = C.c_int
+        L._lba_ready = True
+    p, r, out = slamhot.make_lba_problem(w)
+    opt = slamhot.LbaOptions(iters_first, iters_second, user_lambda_init)
+    L.oracle_lba_solve(C.addressof(p), C.addressof(opt), int(stop), C.addressof(r))
+    return slamhot.lba_result_dict(r, out)
