@@ -11,6 +11,12 @@ barrier + synchronize on both sides of exactly K steps; the max over ranks is re
 
 Also reported: the dominant kernel's roofline (HIP events around every stage during the
 timed steps), and the CPU baseline (the oracle restatement, rank 0 at N=1 only).
+
+Second leg ("lba", BASELINE.json configs[3]): Optimizer::LocalBundleAdjustment's LM/Schur
+solve on synthetic 50 KF x 2000 point x 8 observation windows (2% outliers, 48 free KFs),
+a batch of independent windows per GPU per call (windows shard across ranks like frames).
+Reported as LM iterations/s (one OptimizationAlgorithmLevenberg::solve incl. its trials),
+whole job, plus LBA calls/s, the single-window latency and the oracle's single-core rate.
 """
 from __future__ import annotations
 
@@ -69,6 +75,8 @@ def main():
     ap.add_argument("--unique", type=int, default=64, help="distinct synthetic frames per rank")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=384)
+    ap.add_argument("--lba-windows", type=int, default=64, help="LBA windows per GPU per call (0 = skip)")
+    ap.add_argument("--lba-calls", type=int, default=3)
     args = ap.parse_args()
 
     import torch
@@ -207,11 +215,88 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args, W, H)
 
+    if args.lba_windows > 0:
+        result["lba"] = lba_leg(args, rank, world, local_rank, dist, device)
+
     if rank == 0:
         print(json.dumps(result), flush=True)
     ex.close()
     if dist:
         dist.destroy_process_group()
+
+
+def lba_leg(args, rank, world, local_rank, dist, device):
+    """LM iterations/s of the device LBA solver on config-4 windows (BASELINE.json configs[3])."""
+    import torch
+
+    import slamhot
+    from slamhot import synth
+    nwin = args.lba_windows
+    pool = [synth.lba_window(1000 * rank + s) for s in range(8)]
+    windows = [pool[i % len(pool)] for i in range(nwin)]
+    S = slamhot.LocalBundleAdjustment(device=local_rank)
+    S.solve(windows[: min(4, nwin)])  # warm-up
+    single = S.solve(pool[0])
+    dev1, plan1, _ = S.last_stats()
+    it1 = single["iterations"][0] + single["iterations"][1]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    iters = 0
+    dev_ms = plan_ms = 0.0
+    for _ in range(args.lba_calls):
+        res = S.solve(windows)
+        d, pl, _ = S.last_stats()
+        dev_ms += d
+        plan_ms += pl
+        iters += sum(r["iterations"][0] + r["iterations"][1] for r in res)
+    torch.cuda.synchronize(device)
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed, float(iters), dev_ms], dtype=torch.float64, device=device)
+        tmax = t.clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        tsum = t.clone()
+        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+        elapsed, iters_all, dev_max = float(tmax[0]), float(tsum[1]), float(tmax[2])
+    else:
+        iters_all, dev_max = float(iters), dev_ms
+    out = {
+        "metric": "LocalBundleAdjustment LM iterations/s",
+        "value": round(iters_all / elapsed, 1),
+        "unit": "LM iterations/s",
+        "dtype": "f64",
+        "config": {"workload": "synthetic LocalBA 50 KF x 2000 pts x 8 obs, 2% outliers, 48 free KFs, "
+                               "schedule 5 + 10 (BASELINE.json configs[3])",
+                   "windows_per_gpu_per_call": nwin, "calls": args.lba_calls,
+                   "parallelism": f"window-sharded x{world}"},
+        "lba_calls_per_s": round(nwin * args.lba_calls * world / elapsed, 2),
+        "ms_per_call": round(elapsed / args.lba_calls * 1e3, 3),
+        "device_lm_iters_per_s": round(iters_all / (dev_max / 1e3), 1) if dev_max > 0 else None,
+        "host_plan_ms_per_call": round(plan_ms / args.lba_calls, 3),
+        "single_window": {"lm_iterations": it1, "device_ms": round(dev1, 3),
+                          "ms_per_lm_iteration": round(dev1 / max(it1, 1), 4)},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, str(ROOT / "tests"))
+        import oracle_bind as ob
+        reps, cpu_iters = 0, 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < 3.0 and reps < len(pool):
+            r = ob.lba_solve(pool[reps])
+            cpu_iters += r["iterations"][0] + r["iterations"][1]
+            reps += 1
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {
+            "value": round(cpu_iters / dt, 2), "unit": "LM iterations/s", "cores": 1, "kind": "port",
+            "sample": f"{reps} config-4 windows, one at a time on one core; oracle/lba_oracle.cpp "
+                      f"(g2o LM/Schur restatement, dense LDL^T) -O3 -march=x86-64-v3",
+        }
+    S.close()
+    return out
 
 
 def cpu_baseline(args, W, H):

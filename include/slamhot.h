@@ -316,8 +316,9 @@ void slamhot_lba_destroy(slam_lba* s);
 slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* probs,
                               const slam_lba_options* opt, const volatile int32_t* stop_flag,
                               slam_lba_result* results);
-/* Device time (ms) of the last solve and the number of host<->device round trips it used. */
-slam_status slamhot_lba_last_stats(const slam_lba* s, double* device_ms, int* syncs);
+/* Last solve: device time (ms, kernels + copies), host plan time (ms: graph structure build
+ * and upload, buildStructure in g2o), and the number of host<->device round trips. */
+slam_status slamhot_lba_last_stats(const slam_lba* s, double* device_ms, double* plan_ms, int* syncs);
 
 #ifdef __cplusplus
 }

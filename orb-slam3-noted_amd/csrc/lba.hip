@@ -8,9 +8,8 @@
 // back two counters per trial (windows still trying / still iterating) plus the stop flag.
 //
 // Kernels (per LM iteration, all windows of the batch in one launch each):
-//   k_linearize      thread / edge  : error, Huber rho, Jacobians, per-edge quadratic form
-//   k_point_reduce   thread / point : Hll (3x3) and b_l, summed over the point's edges
-//   k_pose_reduce    thread / (pose, entry) : Hpp (6x6) and b_p over the pose's edges
+//   k_lin_points     thread / point : errors, Huber rho, Hpl = B^T W A per edge, Hll and b_l
+//   k_lin_poses      wave / pose    : Hpp (6x6) and b_p over the pose's edges
 //   k_iter_begin     block / window : chi2 = sum rho, lambda init (iteration 0)
 // per LM trial:
 //   k_schur_point    thread / point : Dinv = (Hll + lambda I)^-1, B_e Dinv, B_e Dinv b_l
@@ -27,6 +26,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "common.hpp"
@@ -36,10 +36,19 @@ namespace lba {
 
 constexpr int kNB = 32;           // LDL^T panel width
 constexpr int kMaxN = 480;        // 80 free KeyFrames per window
-constexpr int kLinStride = 56;    // doubles per edge of linearization output
-constexpr int kLinHpl = 0, kLinHpp = 18, kLinBp = 39, kLinHll = 45, kLinBl = 51;
+constexpr int kHplStride = 18;    // doubles per edge: pose-landmark block Hpl = B^T W A (6 x 3)
 constexpr int kTrStride = 24;     // doubles per edge of Schur trial output: B Dinv (18), B db (6)
 constexpr int kCtlThreads = 256;
+typedef double double4_t __attribute__((ext_vector_type(4)));
+
+// dense Schur system geometry: pose dimension padded to a multiple of kNB, rhs in row npad
+__host__ __device__ constexpr int ldlt_npad(int n) { return (n + kNB - 1) / kNB * kNB; }
+__host__ __device__ constexpr int ldlt_ld(int n) { return ldlt_npad(n) + 8; }
+// k_ldlt LDS: PLT kNB x NP (NP = npad rounded to 16 + 16 for the rhs row), T 32x33, rowbuf, d, 1/d, WL
+__host__ __device__ constexpr int ldlt_np(int n) { return ldlt_npad(n) + 16; }
+__host__ __device__ constexpr size_t ldlt_lds_bytes(int n) {
+    return ((size_t)kNB * ldlt_np(n) + kNB * (kNB + 1) + 3 * kNB + kNB * kNB) * sizeof(double);
+}
 
 // 6x6 symmetric upper-triangle packing, row-major (r <= c)
 __host__ __device__ constexpr int sym6(int r, int c) { return r * 6 - (r * (r - 1)) / 2 + (c - r); }
@@ -208,40 +217,15 @@ __device__ inline void robustify(const Huber& hk, bool stereo, double c, double&
 }
 
 // ---------------------------------------------------------------- iteration kernels
-__global__ void k_linearize(int ne_total, const EdgeS* __restrict__ E, const WinCtl* __restrict__ ctl,
-                            const double* __restrict__ poses, const double* __restrict__ pts,
-                            long long pose_stride, long long pt_stride, Cam cam, Huber hk,
-                            double* __restrict__ err_out, double* __restrict__ rho_out,
-                            double* __restrict__ lin) {
-    const int ei = blockIdx.x * blockDim.x + threadIdx.x;
-    if (ei >= ne_total) return;
-    const EdgeS e = E[ei];
-    const WinCtl& C = ctl[e.win];
-    if (!C.active) return;
-    const double* P = poses + C.sel * pose_stride + 8 * (long long)e.kf;
-    const double* Xw = pts + C.sel * pt_stride + 4 * (long long)e.pt;
-    const double X[3] = {Xw[0], Xw[1], Xw[2]};
-    double err[3];
-    edge_error(e, cam, P, X, err);
-    err_out[4 * (long long)ei + 0] = err[0];
-    err_out[4 * (long long)ei + 1] = err[1];
-    err_out[4 * (long long)ei + 2] = err[2];
-    const bool stereo = e.obs[2] >= 0.f;
-    const double c = edge_chi2(e, err);
-    double rho0, rho1;
-    robustify(hk, stereo, c, rho0, rho1);
-    rho_out[ei] = rho0;
-
-    // Jacobians (OptimizableTypes.cpp:139-160, types_six_dof_expmap.cpp:228-275)
+// Jacobians of one edge at estimate (P, X): A = d e / d X (D x 3), B = d e / d pose (D x 6),
+// OptimizableTypes.cpp:139-160 (mono) and types_six_dof_expmap.cpp:228-275 (stereo).
+__device__ inline void edge_jacobians(bool stereo, const Cam& cam, const double* P, const double* X, double* A,
+                                      double* B) {
     double R[9], Xc[3];
-    const Quat q = load_q(P);
     se3_map(P, X, Xc);
-    rot_matrix(q, R);
+    rot_matrix(load_q(P), R);
     const double x = Xc[0], y = Xc[1], z = Xc[2];
-    double A[9], B[18];
-    int D;
     if (!stereo) {
-        D = 2;
         const double pj[6] = {-(cam.fx / z), -0.0, -((-cam.fx) * x / (z * z)),
                               -0.0, -(cam.fy / z), -((-cam.fy) * y / (z * z))};
 #pragma unroll
@@ -259,7 +243,6 @@ __global__ void k_linearize(int ne_total, const EdgeS* __restrict__ E, const Win
 #pragma unroll
         for (int cc = 0; cc < 6; cc++) B[12 + cc] = 0;
     } else {
-        D = 3;
         const double fx = cam.fx, fy = cam.fy, bf = cam.bf;
         const double z_2 = z * z;
         A[0] = -fx * R[0] / z + fx * x * R[6] / z_2;
@@ -290,89 +273,141 @@ __global__ void k_linearize(int ne_total, const EdgeS* __restrict__ E, const Win
         B[16] = 0;
         B[17] = B[5] - bf / z_2;
     }
-    // constructQuadraticForm, robust branch (base_binary_edge.hpp:88-112)
-    const double info = e.info;
-    const double w = rho1 * info;
-    double om_r[3];
-#pragma unroll
-    for (int k = 0; k < 3; k++) om_r[k] = (-(info * err[k])) * rho1;
-    double* L = lin + (long long)kLinStride * ei;
-#pragma unroll
-    for (int cc = 0; cc < 3; cc++) {
-        double s = 0;
-        for (int k = 0; k < D; k++) s += A[3 * k + cc] * om_r[k];
-        L[kLinBl + cc] = s;
-    }
-#pragma unroll
-    for (int r = 0; r < 3; r++)
-#pragma unroll
-        for (int cc = r; cc < 3; cc++) {
-            double s = 0;
-            for (int k = 0; k < D; k++) s += (A[3 * k + r] * w) * A[3 * k + cc];
-            L[kLinHll + sym3(r, cc)] = s;
-        }
-    if (e.hp < 0) return;
-#pragma unroll
-    for (int r = 0; r < 6; r++)
-#pragma unroll
-        for (int cc = 0; cc < 3; cc++) {
-            double s = 0;
-            for (int k = 0; k < D; k++) s += (B[6 * k + r] * w) * A[3 * k + cc];
-            L[kLinHpl + 3 * r + cc] = s;
-        }
-#pragma unroll
-    for (int cc = 0; cc < 6; cc++) {
-        double s = 0;
-        for (int k = 0; k < D; k++) s += B[6 * k + cc] * om_r[k];
-        L[kLinBp + cc] = s;
-    }
-#pragma unroll
-    for (int r = 0; r < 6; r++)
-#pragma unroll
-        for (int cc = r; cc < 6; cc++) {
-            double s = 0;
-            for (int k = 0; k < D; k++) s += (B[6 * k + r] * w) * B[6 * k + cc];
-            L[kLinHpp + sym6(r, cc)] = s;
-        }
 }
 
-// Hll / b_l per point: sum over the point's edges in insertion order.
-__global__ void k_point_reduce(int npt_total, const int* __restrict__ pt_off, const int* __restrict__ pt_win,
-                               const WinCtl* __restrict__ ctl, const double* __restrict__ lin,
-                               double* __restrict__ Hll, double* __restrict__ bl) {
+// Point side of BlockSolver::buildSystem (block_solver.hpp:501-560): thread per MapPoint,
+// its edges in insertion order.  Per edge: computeError (error, robust rho) and the
+// pose-landmark block Hpl = B^T W A (constructQuadraticForm's transposed-block write,
+// base_binary_edge.hpp:88-112); per point: Hll = sum A^T W A and b_l = sum A^T (-rho' Omega e).
+__global__ void __launch_bounds__(128) k_lin_points(int npt_total, const int* __restrict__ pt_off, const int* __restrict__ pt_win,
+                             const EdgeS* __restrict__ E, const WinCtl* __restrict__ ctl,
+                             const double* __restrict__ poses, const double* __restrict__ pts,
+                             long long pose_stride, long long pt_stride, Cam cam, Huber hk,
+                             double* __restrict__ err_out, double* __restrict__ rho_out,
+                             double* __restrict__ Hpl_out, double* __restrict__ Hll, double* __restrict__ bl) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= npt_total) return;
-    if (!ctl[pt_win[p]].active) return;
-    double h[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
-    for (int e = pt_off[p]; e < pt_off[p + 1]; e++) {
-        const double* L = lin + (long long)kLinStride * e;
+    const WinCtl& C = ctl[pt_win[p]];
+    if (!C.active) return;
+    const double* Xw = pts + C.sel * pt_stride + 4 * (long long)p;
+    const double X[3] = {Xw[0], Xw[1], Xw[2]};
+    double h[6] = {0, 0, 0, 0, 0, 0}, bb[3] = {0, 0, 0};
+    for (int ei = pt_off[p]; ei < pt_off[p + 1]; ei++) {
+        const EdgeS e = E[ei];
+        const double* P = poses + C.sel * pose_stride + 8 * (long long)e.kf;
+        double err[3];
+        edge_error(e, cam, P, X, err);
+        *(double4_t*)(err_out + 4 * (long long)ei) = double4_t{err[0], err[1], err[2], 0.0};
+        const bool stereo = e.obs[2] >= 0.f;
+        double rho0, rho1;
+        robustify(hk, stereo, edge_chi2(e, err), rho0, rho1);
+        rho_out[ei] = rho0;
+        double A[9], B[18];
+        edge_jacobians(stereo, cam, P, X, A, B);
+        const double info = e.info;
+        const double w = rho1 * info;
+        double om_r[3];
 #pragma unroll
-        for (int k = 0; k < 6; k++) h[k] += L[kLinHll + k];
+        for (int k = 0; k < 3; k++) om_r[k] = (-(info * err[k])) * rho1;
 #pragma unroll
-        for (int k = 0; k < 3; k++) b[k] += L[kLinBl + k];
+        for (int cc = 0; cc < 3; cc++) {
+            double sacc = 0;
+            for (int k = 0; k < 3; k++) sacc += A[3 * k + cc] * om_r[k];  // mono: row 2 is zero
+            bb[cc] += sacc;
+        }
+#pragma unroll
+        for (int r = 0; r < 3; r++)
+#pragma unroll
+            for (int cc = r; cc < 3; cc++) {
+                double sacc = 0;
+                for (int k = 0; k < 3; k++) sacc += (A[3 * k + r] * w) * A[3 * k + cc];  // mono: row 2 is zero
+                h[sym3(r, cc)] += sacc;
+            }
+        if (e.hp < 0) continue;
+        double hpl[18];
+#pragma unroll
+        for (int r = 0; r < 6; r++)
+#pragma unroll
+            for (int cc = 0; cc < 3; cc++) {
+                double sacc = 0;
+                for (int k = 0; k < 3; k++) sacc += (B[6 * k + r] * w) * A[3 * k + cc];  // mono: row 2 is zero
+                hpl[3 * r + cc] = sacc;
+            }
+        double* out = Hpl_out + (long long)kHplStride * ei;
+#pragma unroll
+        for (int k = 0; k < 18; k += 2) *(double2*)(out + k) = double2{hpl[k], hpl[k + 1]};
     }
-#pragma unroll
-    for (int k = 0; k < 6; k++) Hll[8 * (long long)p + k] = h[k];
-#pragma unroll
-    for (int k = 0; k < 3; k++) bl[4 * (long long)p + k] = b[k];
+    double* ho = Hll + 8 * (long long)p;
+    *(double4_t*)ho = double4_t{h[0], h[1], h[2], h[3]};
+    *(double2*)(ho + 4) = double2{h[4], h[5]};
+    *(double4_t*)(bl + 4 * (long long)p) = double4_t{bb[0], bb[1], bb[2], 0.0};
 }
 
-// Hpp / b_p per free pose: thread per (pose, entry); edges of the pose in insertion order.
-__global__ void k_pose_reduce(int npose_total, const int* __restrict__ pe_off, const int* __restrict__ pe,
-                              const int* __restrict__ pose_win, const WinCtl* __restrict__ ctl,
-                              const double* __restrict__ lin, double* __restrict__ Hpp,
-                              double* __restrict__ bp) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    const int pose = t / 27, k = t % 27;
+// wave-wide sum by xor butterfly (fixed order: every lane ends with the same total)
+__device__ inline double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Pose side of buildSystem: one wave per free KeyFrame, lanes stride over its edges and
+// recompute error, robust weight and the pose Jacobian B; Hpp = sum B^T W B,
+// b_p = sum B^T (-rho' Omega e), then a butterfly reduction of the 27 sums.
+__global__ void __launch_bounds__(256) k_lin_poses(int npose_total, const int* __restrict__ pe_off,
+                                                   const int* __restrict__ pe, const int* __restrict__ pose_win,
+                                                   const EdgeS* __restrict__ E, const WinCtl* __restrict__ ctl,
+                                                   const double* __restrict__ poses, const double* __restrict__ pts,
+                                                   long long pose_stride, long long pt_stride, Cam cam, Huber hk,
+                                                   double* __restrict__ Hpp, double* __restrict__ bp) {
+    const int pose = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (pose >= npose_total) return;
-    if (!ctl[pose_win[pose]].active) return;
-    const int src = k < 21 ? kLinHpp + k : kLinBp + (k - 21);
-    double s = 0;
-    for (int i = pe_off[pose]; i < pe_off[pose + 1]; i++) s += lin[(long long)kLinStride * pe[i] + src];
-    if (k < 21)
-        Hpp[24 * (long long)pose + k] = s;
-    else
-        bp[8 * (long long)pose + (k - 21)] = s;
+    const WinCtl& C = ctl[pose_win[pose]];
+    if (!C.active) return;
+    double acc[27];
+#pragma unroll
+    for (int k = 0; k < 27; k++) acc[k] = 0.0;
+    for (int i = pe_off[pose] + lane; i < pe_off[pose + 1]; i += 64) {
+        const EdgeS e = E[pe[i]];
+        const double* P = poses + C.sel * pose_stride + 8 * (long long)e.kf;
+        const double* Xw = pts + C.sel * pt_stride + 4 * (long long)e.pt;
+        const double X[3] = {Xw[0], Xw[1], Xw[2]};
+        double err[3];
+        edge_error(e, cam, P, X, err);
+        const bool stereo = e.obs[2] >= 0.f;
+        double rho0, rho1;
+        robustify(hk, stereo, edge_chi2(e, err), rho0, rho1);
+        double A[9], B[18];
+        edge_jacobians(stereo, cam, P, X, A, B);
+        const double info = e.info;
+        const double w = rho1 * info;
+        double om_r[3];
+#pragma unroll
+        for (int k = 0; k < 3; k++) om_r[k] = (-(info * err[k])) * rho1;
+#pragma unroll
+        for (int r = 0; r < 6; r++)
+#pragma unroll
+            for (int cc = r; cc < 6; cc++) {
+                double sacc = 0;
+                for (int k = 0; k < 3; k++) sacc += (B[6 * k + r] * w) * B[6 * k + cc];  // mono: row 2 is zero
+                acc[sym6(r, cc)] += sacc;
+            }
+#pragma unroll
+        for (int cc = 0; cc < 6; cc++) {
+            double sacc = 0;
+            for (int k = 0; k < 3; k++) sacc += B[6 * k + cc] * om_r[k];  // mono: row 2 is zero
+            acc[21 + cc] += sacc;
+        }
+    }
+    double mine = 0.0;
+#pragma unroll
+    for (int k = 0; k < 27; k++) {
+        const double t = wave_sum(acc[k]);
+        if (lane == k) mine = t;
+    }
+    if (lane < 21)
+        Hpp[24 * (long long)pose + lane] = mine;
+    else if (lane < 27)
+        bp[8 * (long long)pose + (lane - 21)] = mine;
 }
 
 // deterministic block sum / max (fixed tree over kCtlThreads lanes)
@@ -480,7 +515,7 @@ __global__ void k_schur_point(int npt_total, const int* __restrict__ spe_off, co
     for (int r = 0; r < 3; r++) db[r] = Di[3 * r] * b[0] + Di[3 * r + 1] * b[1] + Di[3 * r + 2] * b[2];
     for (int i = spe_off[p]; i < spe_off[p + 1]; i++) {
         const int e = spe[i];
-        const double* H = lin + (long long)kLinStride * e + kLinHpl;
+        const double* H = lin + (long long)kHplStride * e;
         double* T = tr + (long long)kTrStride * e;
 #pragma unroll
         for (int r = 0; r < 6; r++) {
@@ -492,25 +527,32 @@ __global__ void k_schur_point(int npt_total, const int* __restrict__ spe_off, co
     }
 }
 
+__device__ inline double readlane_d(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
 __device__ inline void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// One wave per 6x6 block (i1 <= i2) of the Schur complement.  The reference block (i1, i2)
-// (upper) is written transposed into the lower triangle of the dense row-major matrix;
-// diagonal blocks also produce the rhs row b_s = b_p - sum B db (augmented row n).
-__global__ void k_schur_block(int nblk_total, const int2* __restrict__ blk_pose, const int* __restrict__ blk_win,
-                              const int* __restrict__ ct_off, const int2* __restrict__ ct,
-                              const WinDesc* __restrict__ wins, const WinCtl* __restrict__ ctl,
-                              const double* __restrict__ Hpp, const double* __restrict__ bp,
-                              const int* __restrict__ pe_off, const int* __restrict__ pe,
-                              const double* __restrict__ lin, const double* __restrict__ tr,
-                              double* __restrict__ Hs) {
-    const int blk = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+// One wave per 6x6 block (i1 <= i2) of the Schur complement: lanes stride over the block's
+// contributions (one per point observed by both poses), each accumulating the full 6x6
+// B_a Dinv Hpl_b^T, then a butterfly reduction.  The reference block (i1, i2) (upper) is written
+// transposed into the lower triangle of the dense row-major matrix; diagonal blocks also
+// produce the rhs row b_s = b_p - sum B db (augmented row n).
+__global__ void __launch_bounds__(256) k_schur_block(int nblk_total, const int2* __restrict__ blk_pose,
+                                                     const int* __restrict__ blk_win, const int* __restrict__ ct_off,
+                                                     const int2* __restrict__ ct, const WinDesc* __restrict__ wins,
+                                                     const WinCtl* __restrict__ ctl, const double* __restrict__ Hpp,
+                                                     const double* __restrict__ bp, const int* __restrict__ pe_off,
+                                                     const int* __restrict__ pe, const double* __restrict__ lin,
+                                                     const double* __restrict__ tr, double* __restrict__ Hs) {
+    const int blk = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (blk >= nblk_total) return;
-    const int lane = threadIdx.x & 63;
     const int win = blk_win[blk];
     const WinCtl& C = ctl[win];
     if (!C.need_trial) return;
@@ -518,6 +560,46 @@ __global__ void k_schur_block(int nblk_total, const int2* __restrict__ blk_pose,
     const int2 ij = blk_pose[blk];  // local free-pose indices i1 <= i2
     const int i1 = ij.x, i2 = ij.y;
     double* H = Hs + W.hs_off;
+    double acc[36];
+#pragma unroll
+    for (int k = 0; k < 36; k++) acc[k] = 0.0;
+    for (int k = ct_off[blk] + lane; k < ct_off[blk + 1]; k += 64) {
+        const int2 ab = ct[k];
+        const double* BD = tr + (long long)kTrStride * ab.x;
+        const double* Bj = lin + (long long)kHplStride * ab.y;
+        double bd[18], bj[18];
+#pragma unroll
+        for (int t = 0; t < 18; t++) {
+            bd[t] = BD[t];
+            bj[t] = Bj[t];
+        }
+#pragma unroll
+        for (int r = 0; r < 6; r++)
+#pragma unroll
+            for (int c = 0; c < 6; c++)
+                acc[6 * r + c] += bd[3 * r] * bj[3 * c] + bd[3 * r + 1] * bj[3 * c + 1] + bd[3 * r + 2] * bj[3 * c + 2];
+    }
+    double mine = 0.0;
+#pragma unroll
+    for (int k = 0; k < 36; k++) {
+        const double t = wave_sum(acc[k]);
+        if (lane == k) mine = t;
+    }
+    double rhs = 0.0;
+    if (i1 == i2) {
+        const int gp = W.pose0 + i1;
+        double sb[6] = {0, 0, 0, 0, 0, 0};
+        for (int k = pe_off[gp] + lane; k < pe_off[gp + 1]; k += 64) {
+            const double* T = tr + (long long)kTrStride * pe[k] + 18;
+#pragma unroll
+            for (int r = 0; r < 6; r++) sb[r] += T[r];
+        }
+#pragma unroll
+        for (int r = 0; r < 6; r++) {
+            const double t = wave_sum(sb[r]);
+            if (lane == 36 + r) rhs = bp[8 * (long long)gp + r] - t;
+        }
+    }
     if (lane < 36) {
         const int r = lane / 6, c = lane % 6;
         double v = 0.0;
@@ -526,193 +608,235 @@ __global__ void k_schur_block(int nblk_total, const int2* __restrict__ blk_pose,
             v = Hpp[24 * (long long)(W.pose0 + i1) + sym6(rr, cc)];
             if (r == c) v += C.lambda;
         }
-        for (int k = ct_off[blk]; k < ct_off[blk + 1]; k++) {
-            const int2 ab = ct[k];
-            const double* BD = tr + (long long)kTrStride * ab.x + 3 * r;
-            const double* Bj = lin + (long long)kLinStride * ab.y + kLinHpl + 3 * c;
-            v -= BD[0] * Bj[0] + BD[1] * Bj[1] + BD[2] * Bj[2];
-        }
+        v -= mine;
         // upper (i1, i2)[r][c] -> lower element (6 i2 + c, 6 i1 + r)
         if (i1 != i2 || r <= c) H[(long long)(6 * i2 + c) * W.ld + 6 * i1 + r] = v;
     } else if (lane < 42 && i1 == i2) {
-        const int r = lane - 36;
-        const int gp = W.pose0 + i1;
-        double s = 0;
-        for (int k = pe_off[gp]; k < pe_off[gp + 1]; k++) s += tr[(long long)kTrStride * pe[k] + 18 + r];
-        H[(long long)W.n * W.ld + 6 * i1 + r] = bp[8 * (long long)gp + r] - s;
+        H[(long long)ldlt_npad(W.n) * W.ld + 6 * i1 + (lane - 36)] = rhs;
     }
 }
 
-// Dense LDL^T of the augmented lower-triangular (n+1) x (n+1) system [[Hs, .], [b_s^T, .]] in
-// place (row-major, leading dimension ld); the last row becomes z = D^-1 L^-1 b_s, then
-// L^T x = z.  Fails like Eigen's SimplicialLDLT::factorize only on an exactly zero pivot.
-// One 512-thread block per window; panels of kNB columns:
-//   (1) diagonal kNB x kNB block factored by wave 0 in registers (lane = row),
-//   (2) rows below: forward substitution, one thread per row,
-//   (3) trailing update with 4x4 register tiles against the panel held in LDS.
+// Dense LDL^T of the augmented lower-triangular system [[Hs, .], [b_s^T, .]] in place
+// (row-major, leading dimension ld).  The pose dimension n is padded to npad (a multiple of
+// kNB) with an identity block, which the factorization leaves invariant; the rhs is row npad
+// and becomes z = D^-1 L^-1 b_s, then L^T x = z.  Fails like Eigen's
+// SimplicialLDLT::factorize only on an exactly zero pivot.
+// One 512-thread block per window; per panel of kNB columns:
+//   (1) diagonal block: wave 0, lane = row, pivot rows broadcast through LDS,
+//   (2) rows below: one thread per row (right-looking inside the row),
+//   (3) trailing update C -= (L D) L^T on 16x16 tiles with v_mfma_f64_16x16x4_f64, the panel
+//       held column-major in LDS; the rhs row is a GEMV on the side.
+#ifdef LBA_PHASE_TIMING
+__device__ unsigned long long g_ldlt_phase[8];
+#define PHASE_MARK(i)                                                        \
+    do {                                                                     \
+        if (threadIdx.x == 0 && blockIdx.x == 0) {                           \
+            const unsigned long long now = wall_clock64();                   \
+            if ((i) > 0) g_ldlt_phase[(i)] += now - g_ldlt_phase[0];         \
+            g_ldlt_phase[0] = now;                                           \
+        }                                                                    \
+    } while (0)
+#else
+#define PHASE_MARK(i) \
+    do {              \
+    } while (0)
+#endif
+
+
+
 __global__ void __launch_bounds__(512) k_ldlt(const WinDesc* __restrict__ wins, WinCtl* __restrict__ ctl,
                                                double* __restrict__ Hs, double* __restrict__ xp_out) {
-    extern __shared__ double smem[];
+    extern __shared__ __attribute__((aligned(16))) double smem[];
     const WinDesc W = wins[blockIdx.x];
     WinCtl& C = ctl[blockIdx.x];
     if (!C.need_trial) return;
-    const int n = W.n, N = n + 1, ld = W.ld;
+    const int n = W.n, npad = ldlt_npad(n), ld = W.ld, NP = ldlt_np(n);
     double* A = Hs + W.hs_off;
-    double* PL = smem;                  // N x kNB panel (L values)
-    double* dsh = smem + (size_t)N * kNB;  // kNB pivots of the panel
-    double* rowbuf = dsh + kNB;            // pivot-row broadcast
-    double* WL = rowbuf + kNB;             // kNB x kNB: d_q L[j][q]
+    double* PLT = smem;                          // kNB x NP: panel column q, rows from R0
+    double* T = PLT + (size_t)kNB * NP;          // 32 x 33 diagonal block
+    double* rowbuf = T + kNB * (kNB + 1);        // pivot-row broadcast
+    double* dsh = rowbuf + kNB;                  // pivots
+    double* dinv = dsh + kNB;                    // 1 / pivots
+    double* WL = dinv + kNB;                     // kNB x kNB: WL[q][j] = d_j L[q][j]
     __shared__ int fail;
     if (threadIdx.x == 0) fail = 0;
     __syncthreads();
+    PHASE_MARK(0);
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    for (int kb = 0; kb < n; kb += kNB) {
-        const int nb = min(kNB, n - kb);
-        // (1) diagonal block: wave 0, lane = row (full symmetric row in registers); the
-        //     pivot row is broadcast through LDS each step
+    for (int kb = 0; kb < npad; kb += kNB) {
+        const int R0 = kb + kNB;
+        // (1) diagonal block
+        for (int e = tid; e < kNB * kNB; e += blockDim.x) {
+            const int r = e / kNB, c = e % kNB;
+            if (c <= r) T[r * (kNB + 1) + c] = A[(long long)(kb + r) * ld + kb + c];
+        }
+        __syncthreads();
         if (wid == 0) {
             double row[kNB];
+            const int rl = lane & (kNB - 1);
 #pragma unroll
-            for (int c = 0; c < kNB; c++) {
-                double v = 0.0;
-                if (lane < nb && c < nb) {
-                    const int gr = kb + lane, gc = kb + c;
-                    v = gc <= gr ? A[(long long)gr * ld + gc] : A[(long long)gc * ld + gr];
-                } else if (lane == c) {
-                    v = 1.0;
-                }
-                row[c] = v;
-            }
+            for (int c = 0; c < kNB; c++) row[c] = c <= rl ? T[rl * (kNB + 1) + c] : T[c * (kNB + 1) + rl];
             bool bad = false;
 #pragma unroll
             for (int j = 0; j < kNB; j++) {
-                if (lane == j) {
+                // pivot row j broadcast from lane j through scalar registers
+                double rb[kNB];
 #pragma unroll
-                    for (int c = j; c < kNB; c++) rowbuf[c] = row[c];
-                }
-                wave_sync();
-                const double dj = rowbuf[j];
-                if (j < nb && dj == 0.0) bad = true;
-                if (lane > j) {
+                for (int c = j; c < kNB; c++) rb[c] = readlane_d(row[c], j);
+                const double dj = rb[j];
+                if (dj == 0.0) bad = true;
+                if (lane > j && lane < kNB) {
                     const double lj = row[j] / dj;
 #pragma unroll
-                    for (int c = j + 1; c < kNB; c++) row[c] -= lj * rowbuf[c];
+                    for (int c = j + 1; c < kNB; c++) row[c] -= lj * rb[c];
                     row[j] = lj;
                 }
-                if (lane == j) dsh[j] = dj;
-                wave_sync();
-            }
-            if (bad && lane == 0) fail = 1;
-            if (lane < nb) {
-#pragma unroll
-                for (int c = 0; c < kNB; c++) {
-                    if (c < lane) {
-                        PL[(size_t)(kb + lane) * kNB + c] = row[c];
-                        A[(long long)(kb + lane) * ld + kb + c] = row[c];
-                    }
+                if (lane == j) {
+                    dsh[j] = dj;
+                    dinv[j] = 1.0 / dj;
                 }
             }
-            wave_sync();
-            if (lane < nb) {
-                A[(long long)(kb + lane) * ld + kb + lane] = dsh[lane];
-                // WL[j][q] = d_q L[j][q] for the forward substitution of the rows below
+            if (bad && lane == 0) fail = 1;
+            if (lane < kNB) {
 #pragma unroll
-                for (int q = 0; q < kNB; q++) WL[lane * kNB + q] = q < lane ? dsh[q] * row[q] : 0.0;
+                for (int c = 0; c < kNB; c++)
+                    if (c < lane) A[(long long)(kb + lane) * ld + kb + c] = row[c];
+                A[(long long)(kb + lane) * ld + kb + lane] = dsh[lane];
+#pragma unroll
+                for (int j = 0; j < kNB; j++) WL[lane * kNB + j] = j < lane ? dsh[j] * row[j] : 0.0;
             }
         }
         __syncthreads();
         if (fail) break;
-        // (2) rows below the diagonal block (including the rhs row n): one thread per row,
-        //     right-looking within the row
-        for (int r = kb + nb + tid; r < N; r += blockDim.x) {
+        PHASE_MARK(1);
+        // (2) rows below (R0 .. npad, the last one is the rhs row)
+        for (int r = R0 + tid; r <= npad; r += blockDim.x) {
             double a[kNB];
             double* Ar = A + (long long)r * ld + kb;
 #pragma unroll
-            for (int j = 0; j < kNB; j++) a[j] = j < nb ? Ar[j] : 0.0;
-#pragma unroll
-            for (int j = 0; j < kNB; j++) {
-                if (j < nb) {
-                    a[j] = a[j] / dsh[j];
-#pragma unroll
-                    for (int q = j + 1; q < kNB; q++) a[q] -= a[j] * WL[q * kNB + j];
-                }
+            for (int j = 0; j < kNB; j += 2) {
+                const double2 v = *(const double2*)(Ar + j);
+                a[j] = v.x;
+                a[j + 1] = v.y;
             }
 #pragma unroll
             for (int j = 0; j < kNB; j++) {
-                if (j < nb) {
-                    Ar[j] = a[j];
-                    PL[(size_t)r * kNB + j] = a[j];
-                }
+                a[j] = a[j] * dinv[j];
+#pragma unroll
+                for (int q = j + 1; q < kNB; q++) a[q] -= a[j] * WL[q * kNB + j];
+            }
+#pragma unroll
+            for (int j = 0; j < kNB; j += 2) *(double2*)(Ar + j) = double2{a[j], a[j + 1]};
+#pragma unroll
+            for (int j = 0; j < kNB; j++) PLT[(size_t)j * NP + (r - R0)] = a[j];
+        }
+        __syncthreads();
+        PHASE_MARK(2);
+        // (3) trailing update of rows/cols [R0, npad) and of the rhs row npad
+        const int mt = (npad - R0) / 16;  // 16-row tiles
+        const int ntiles = mt * (mt + 1) / 2;
+        const int nwv = (int)(blockDim.x >> 6);
+        const int li = lane & 15, lk = lane >> 4;
+        auto tile_of = [&](int t, int& ti, int& tj) {
+            ti = (int)((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
+            while ((ti + 1) * (ti + 2) / 2 <= t) ti++;
+            while (ti * (ti + 1) / 2 > t) ti--;
+            tj = t - ti * (ti + 1) / 2;
+        };
+        double cn[4] = {0.0, 0.0, 0.0, 0.0};
+        int ti = 0, tj = 0;
+        if (wid < ntiles) {
+            tile_of(wid, ti, tj);
+            const double* Cp = A + (long long)(R0 + 16 * ti + lk) * ld + R0 + 16 * tj + li;
+#pragma unroll
+            for (int v = 0; v < 4; v++) cn[v] = Cp[(long long)(4 * v) * ld];
+        }
+        for (int t = wid; t < ntiles; t += nwv) {
+            const double cc0 = cn[0], cc1 = cn[1], cc2 = cn[2], cc3 = cn[3];
+            const int ci = ti, cj = tj;
+            double4_t acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int s4 = 0; s4 < kNB; s4 += 4) {
+                const int q = s4 + lk;
+                const double av = PLT[(size_t)q * NP + 16 * ci + li] * dsh[q];
+                const double bv = PLT[(size_t)q * NP + 16 * cj + li];
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+            }
+            if (t + nwv < ntiles) {  // prefetch the next tile of this wave
+                tile_of(t + nwv, ti, tj);
+                const double* Cp = A + (long long)(R0 + 16 * ti + lk) * ld + R0 + 16 * tj + li;
+#pragma unroll
+                for (int v = 0; v < 4; v++) cn[v] = Cp[(long long)(4 * v) * ld];
+            }
+            double* Ct = A + (long long)(R0 + 16 * ci + lk) * ld + R0 + 16 * cj + li;
+            Ct[0] = cc0 - acc[0];
+            Ct[(long long)4 * ld] = cc1 - acc[1];
+            Ct[(long long)8 * ld] = cc2 - acc[2];
+            Ct[(long long)12 * ld] = cc3 - acc[3];
+        }
+        if (wid == (int)(blockDim.x >> 6) - 1 || ntiles == 0) {
+            // rhs row: z[c] -= sum_q (L[npad][q] d_q) L[c][q], c in [R0, npad)
+            const double* zl = PLT + (npad - R0);
+            double* z = A + (long long)npad * ld;
+            for (int c = R0 + lane; c < npad; c += 64) {
+                double s = 0.0;
+#pragma unroll
+                for (int q = 0; q < kNB; q++) s += (zl[(size_t)q * NP] * dsh[q]) * PLT[(size_t)q * NP + (c - R0)];
+                z[c] -= s;
             }
         }
         __syncthreads();
-        // (3) trailing update: rows r >= R0 (to N-1), cols c in [R0, min(r, n-1)]
-        const int R0 = kb + nb;
-        const int mr = N - R0, mc = n - R0;
-        if (mc > 0) {
-            const int tr_n = (mr + 3) / 4, tc_n = (mc + 3) / 4;
-            for (int t = tid; t < tr_n * tc_n; t += blockDim.x) {
-                const int ti = t / tc_n, tj = t % tc_n;
-                if (tj > ti) continue;
-                const int r0 = R0 + 4 * ti, c0 = R0 + 4 * tj;
-                double acc[4][4];
-#pragma unroll
-                for (int i = 0; i < 4; i++)
-#pragma unroll
-                    for (int j = 0; j < 4; j++) acc[i][j] = 0.0;
-                for (int q = 0; q < nb; q++) {
-                    const double dq = dsh[q];
-                    double a[4], b[4];
-#pragma unroll
-                    for (int i = 0; i < 4; i++) a[i] = (r0 + i < N) ? PL[(size_t)(r0 + i) * kNB + q] * dq : 0.0;
-#pragma unroll
-                    for (int j = 0; j < 4; j++) b[j] = (c0 + j < n) ? PL[(size_t)(c0 + j) * kNB + q] : 0.0;
-#pragma unroll
-                    for (int i = 0; i < 4; i++)
-#pragma unroll
-                        for (int j = 0; j < 4; j++) acc[i][j] += a[i] * b[j];
-                }
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    const int r = r0 + i;
-                    if (r >= N) continue;
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        const int c = c0 + j;
-                        if (c < n && c <= r) A[(long long)r * ld + c] -= acc[i][j];
-                    }
-                }
-            }
-        }
-        __syncthreads();
+        PHASE_MARK(3);
     }
     if (fail) {
         if (tid == 0) C.ok2 = 0;
         return;
     }
-    // backward solve L^T x = z; z lives in row n.  Blocks from the last one.
-    double* z = A + (long long)n * ld;
-    const int nblocks = (n + kNB - 1) / kNB;
-    for (int bi = nblocks - 1; bi >= 0; bi--) {
-        const int kb = bi * kNB, nb = min(kNB, n - kb);
+    // backward solve L^T x = z (z in row npad), block by block from the last one
+    double* z = A + (long long)npad * ld;
+    for (int kb = npad - kNB; kb >= 0; kb -= kNB) {
+        for (int e = tid; e < kNB * kNB; e += blockDim.x) {
+            const int r = e / kNB, c = e % kNB;
+            if (c < r) T[r * (kNB + 1) + c] = A[(long long)(kb + r) * ld + kb + c];
+        }
+        __syncthreads();
         if (wid == 0) {
-            double zi = lane < nb ? z[kb + lane] : 0.0;
-            for (int k = nb - 1; k >= 0; k--) {
-                const double xk = __shfl(zi, k, 64);
-                if (lane < k) zi -= A[(long long)(kb + k) * ld + kb + lane] * xk;
+            const int cl = lane & (kNB - 1);
+            double lc[kNB];  // column `lane` of the block: L[k][lane], k > lane
+#pragma unroll
+            for (int k = 0; k < kNB; k++) lc[k] = k > cl ? T[k * (kNB + 1) + cl] : 0.0;
+            double zi = lane < kNB ? z[kb + lane] : 0.0;
+#pragma unroll
+            for (int k = kNB - 1; k >= 0; k--) {
+                const double xk = readlane_d(zi, k);
+                if (lane < k) zi -= lc[k] * xk;
             }
-            if (lane < nb) z[kb + lane] = zi;
+            if (lane < kNB) z[kb + lane] = zi;
         }
         __syncthreads();
         for (int i = tid; i < kb; i += blockDim.x) {
-            double s = z[i];
-            for (int k = 0; k < nb; k++) s -= A[(long long)(kb + k) * ld + i] * z[kb + k];
-            z[i] = s;
+            double sacc = z[i];
+#pragma unroll 8
+            for (int k = 0; k < kNB; k++) sacc -= A[(long long)(kb + k) * ld + i] * z[kb + k];
+            z[i] = sacc;
         }
         __syncthreads();
+        PHASE_MARK(4);
     }
     for (int i = tid; i < n; i += blockDim.x) xp_out[6 * (long long)W.pose0 + i] = z[i];
     if (tid == 0) C.ok2 = 1;
+}
+
+// Identity padding of the dense systems (rows/cols n..npad-1) and a zero rhs tail; the
+// factorization keeps it invariant, so it is written once per solve.
+__global__ void k_ldlt_pad(const WinDesc* __restrict__ wins, double* __restrict__ Hs) {
+    const WinDesc W = wins[blockIdx.x];
+    const int n = W.n, npad = ldlt_npad(n), ld = W.ld;
+    double* A = Hs + W.hs_off;
+    for (int i = n + threadIdx.x; i < npad; i += blockDim.x) {
+        for (int j = 0; j <= i; j++) A[(long long)i * ld + j] = (i == j) ? 1.0 : 0.0;
+        A[(long long)npad * ld + i] = 0.0;
+    }
 }
 
 // x_l = Dinv (b_l - Hpl^T x_p) (block_solver.hpp:456-481) and the trial point estimate.
@@ -731,7 +855,7 @@ __global__ void k_backsub(int npt_total, const int* __restrict__ spe_off, const 
         double cl[3] = {bl[4 * (long long)p], bl[4 * (long long)p + 1], bl[4 * (long long)p + 2]};
         for (int i = spe_off[p]; i < spe_off[p + 1]; i++) {
             const int e = spe[i];
-            const double* H = lin + (long long)kLinStride * e + kLinHpl;
+            const double* H = lin + (long long)kHplStride * e;
             const double* xpp = xp + 6 * (long long)E[e].hp;
 #pragma unroll
             for (int c = 0; c < 3; c++)
@@ -1047,148 +1171,294 @@ T* as(DevBuf& b) {
 
 }  // namespace
 
+// Every per-call input structure lives in one arena: built in place in pinned host memory and
+// shipped with a single copy (the reference builds the same graph in g2o: buildStructure).
+struct Plan {
+    EdgeS* edges;
+    WinDesc* wins;
+    WinCtl* ctl;
+    int *pt_off, *pt_win, *spe_off, *spe, *pe_off, *pe, *pose_win, *kf_hp, *kf_win, *blk_win, *ct_off;
+    int2 *blk_pose, *ct;
+    float *kf_in, *pt_in;
+};
+
 struct slam_lba {
     int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     Counters* h_cnt = nullptr;  // pinned
-    double last_ms = 0;
+    double last_ms = 0, last_plan_ms = 0;
     int last_syncs = 0;
-    // device buffers
-    DevBuf edges, wins, ctl, cnt, pt_off, pt_win, spe_off, spe, pe_off, pe, pose_win, kf_hp, kf_win;
-    DevBuf blk_pose, blk_win, ct_off, ct;
+    unsigned char* harena = nullptr;  // pinned
+    size_t harena_cap = 0;
+    DevBuf arena, cnt;
     DevBuf poses, pts, err, rho, lin, Hll, bl, Hpp, bp, Dinv, tr, xp, xl, Hs;
-    DevBuf kf_in, pt_in, kf_out, pt_out, outl;
+    DevBuf kf_out, pt_out, outl;
 };
 
 namespace {
 
-struct HostPlan {
-    std::vector<EdgeS> edges;
-    std::vector<WinDesc> wins;
-    std::vector<int> pt_off, pt_win, spe_off, spe, pe_off, pe, pose_win, kf_hp, kf_win;
-    std::vector<int2> blk_pose, ct;
-    std::vector<int> blk_win, ct_off;
-    std::vector<float> kf_in, pt_in;
-    int nkf = 0, npt = 0, ne = 0, npose = 0, nblk = 0;
-    long long hs_total = 0;
+struct WinStart {
+    int kf0, pt0, e0, pose0, blk0, spe0;
+    long long ct0, hs0;
+    size_t h0;
 };
 
-slam_status build_plan(int n_prob, const slam_lba_problem* probs, HostPlan& H) {
+struct PlanSizes {
+    std::vector<WinStart> starts;
+    int nkf = 0, npt = 0, ne = 0, npose = 0, nblk = 0, nspe = 0, nw = 0;
+    long long nct = 0, hs_total = 0;
+    int max_n = 0;
+};
+
+struct Layout {
+    size_t edges, wins, ctl, pt_off, pt_win, spe_off, spe, pe_off, pe, pose_win, kf_hp, kf_win, blk_win, ct_off,
+        blk_pose, ct, kf_in, pt_in, total;
+};
+
+Layout make_layout(const PlanSizes& z) {
+    Layout L{};
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        const size_t o = off;
+        off += (bytes + 255) & ~(size_t)255;
+        return o;
+    };
+    L.edges = take(sizeof(EdgeS) * z.ne);
+    L.wins = take(sizeof(WinDesc) * z.nw);
+    L.ctl = take(sizeof(WinCtl) * z.nw);
+    L.pt_off = take(sizeof(int) * (z.npt + 1));
+    L.pt_win = take(sizeof(int) * z.npt);
+    L.spe_off = take(sizeof(int) * (z.npt + 1));
+    L.spe = take(sizeof(int) * z.nspe);
+    L.pe_off = take(sizeof(int) * (z.npose + 1));
+    L.pe = take(sizeof(int) * z.nspe);
+    L.pose_win = take(sizeof(int) * z.npose);
+    L.kf_hp = take(sizeof(int) * z.nkf);
+    L.kf_win = take(sizeof(int) * z.nkf);
+    L.blk_win = take(sizeof(int) * z.nblk);
+    L.ct_off = take(sizeof(int) * (z.nblk + 1));
+    L.blk_pose = take(sizeof(int2) * z.nblk);
+    L.ct = take(sizeof(int2) * z.nct);
+    L.kf_in = take(sizeof(float) * 16 * z.nkf);
+    L.pt_in = take(sizeof(float) * 3 * z.npt);
+    L.total = off;
+    return L;
+}
+
+Plan bind(unsigned char* base, const Layout& L) {
+    Plan P;
+    P.edges = (EdgeS*)(base + L.edges);
+    P.wins = (WinDesc*)(base + L.wins);
+    P.ctl = (WinCtl*)(base + L.ctl);
+    P.pt_off = (int*)(base + L.pt_off);
+    P.pt_win = (int*)(base + L.pt_win);
+    P.spe_off = (int*)(base + L.spe_off);
+    P.spe = (int*)(base + L.spe);
+    P.pe_off = (int*)(base + L.pe_off);
+    P.pe = (int*)(base + L.pe);
+    P.pose_win = (int*)(base + L.pose_win);
+    P.kf_hp = (int*)(base + L.kf_hp);
+    P.kf_win = (int*)(base + L.kf_win);
+    P.blk_win = (int*)(base + L.blk_win);
+    P.ct_off = (int*)(base + L.ct_off);
+    P.blk_pose = (int2*)(base + L.blk_pose);
+    P.ct = (int2*)(base + L.ct);
+    P.kf_in = (float*)(base + L.kf_in);
+    P.pt_in = (float*)(base + L.pt_in);
+    return P;
+}
+
+// Pass 1: validation and sizes.  hidx: free-pose index of every KF of every window.
+slam_status plan_sizes(int n_prob, const slam_lba_problem* probs, PlanSizes& z, std::vector<int>& hidx_all,
+                       std::vector<int>& np_of) {
+    z.nw = n_prob;
+    np_of.assign(n_prob, 0);
+    z.starts.resize(n_prob);
+    std::vector<int> cnt;
     for (int w = 0; w < n_prob; w++) {
         const slam_lba_problem& P = probs[w];
         if (P.n_kf < 0 || P.n_pt < 0 || P.n_edge < 0) return SLAM_EINVAL;
+        z.starts[w] = WinStart{z.nkf, z.npt, z.ne, z.npose, z.nblk, z.nspe, z.nct, z.hs_total, hidx_all.size()};
         if ((P.n_kf && (!P.kf_Tcw || !P.kf_fixed)) || (P.n_pt && !P.pt_pos) ||
             (P.n_edge && (!P.edge_pt || !P.edge_kf || !P.edge_obs || !P.edge_inv_sigma2)))
             return SLAM_EINVAL;
-        WinDesc D{};
-        D.kf0 = H.nkf;
-        D.nk = P.n_kf;
-        D.pt0 = H.npt;
-        D.npt = P.n_pt;
-        D.e0 = H.ne;
-        D.ne = P.n_edge;
-        D.pose0 = H.npose;
-        // a KeyFrame without edges is not an active vertex (sparse_optimizer.cpp:262-300):
-        // it stays out of the Hessian and keeps its estimate
-        std::vector<int> kf_edges(P.n_kf, 0);
-        for (int i = 0; i < P.n_edge; i++)
-            if (P.edge_kf[i] >= 0 && P.edge_kf[i] < P.n_kf) kf_edges[P.edge_kf[i]]++;
-        std::vector<int> hidx(P.n_kf, -1);
-        int np = 0;
-        for (int k = 0; k < P.n_kf; k++) {
-            if (P.kf_fixed[k] == 0 && kf_edges[k] > 0) hidx[k] = np++;
-            H.kf_hp.push_back(hidx[k] >= 0 ? H.npose + hidx[k] : -1);
-            H.kf_win.push_back(w);
-            for (int i = 0; i < 16; i++) H.kf_in.push_back(P.kf_Tcw[16 * k + i]);
-        }
-        D.np = np;
-        D.n = 6 * np;
-        if (D.n > kMaxN) return SLAM_ECAP;
-        D.ld = D.n + 1;
-        D.hs_off = H.hs_total;
-        H.hs_total += (long long)(D.n + 1) * D.ld;
-        for (int i = 0; i < 3 * P.n_pt; i++) H.pt_in.push_back(P.pt_pos[i]);
-        // edges (point-major), point CSR
-        std::vector<int> cnt(P.n_pt + 1, 0);
+        cnt.assign(P.n_kf, 0);
         for (int i = 0; i < P.n_edge; i++) {
             const int p = P.edge_pt[i], k = P.edge_kf[i];
             if (p < 0 || p >= P.n_pt || k < 0 || k >= P.n_kf) return SLAM_EINVAL;
             if (i && p < P.edge_pt[i - 1]) return SLAM_EINVAL;  // point-major insertion order
-            cnt[p + 1]++;
-            EdgeS e;
-            e.pt = H.npt + p;
-            e.kf = H.nkf + k;
-            e.hp = hidx[k] >= 0 ? H.npose + hidx[k] : -1;
-            e.win = w;
-            e.obs[0] = P.edge_obs[3 * i];
-            e.obs[1] = P.edge_obs[3 * i + 1];
-            e.obs[2] = P.edge_obs[3 * i + 2];
-            e.info = P.edge_inv_sigma2[i];
-            H.edges.push_back(e);
+            cnt[k]++;
         }
-        for (int p = 0; p < P.n_pt; p++) {
-            H.pt_off.push_back(H.ne + cnt[p]);
-            cnt[p + 1] += cnt[p];
-            H.pt_win.push_back(w);
-        }
-        // per point: edges with a free pose, sorted by pose (HplCCS column order)
-        std::vector<std::vector<int>> pose_edges(np);
-        std::vector<int> col;
-        std::vector<std::vector<int2>> blist((size_t)np * (np + 1) / 2);
-        for (int p = 0; p < P.n_pt; p++) {
-            H.spe_off.push_back((int)H.spe.size());
-            col.clear();
-            for (int i = cnt[p]; i < cnt[p + 1]; i++)
-                if (hidx[P.edge_kf[i]] >= 0) col.push_back(i);
-            std::stable_sort(col.begin(), col.end(),
-                             [&](int a, int b) { return hidx[P.edge_kf[a]] < hidx[P.edge_kf[b]]; });
-            for (size_t a = 0; a < col.size(); a++) {
-                H.spe.push_back(H.ne + col[a]);
-                const int i1 = hidx[P.edge_kf[col[a]]];
-                for (size_t b = a; b < col.size(); b++) {
-                    const int i2 = hidx[P.edge_kf[col[b]]];
-                    if (i2 == i1 && b != a) return SLAM_EINVAL;  // two observations of one point in one KF
-                    blist[(size_t)i2 * (i2 + 1) / 2 + i1].push_back(int2{H.ne + col[a], H.ne + col[b]});
-                }
+        // a KeyFrame without edges is not an active vertex (sparse_optimizer.cpp:262-300): it
+        // stays out of the Hessian and keeps its estimate
+        const size_t h0 = hidx_all.size();
+        int np = 0;
+        for (int k = 0; k < P.n_kf; k++) hidx_all.push_back(P.kf_fixed[k] == 0 && cnt[k] > 0 ? np++ : -1);
+        np_of[w] = np;
+        if (6 * np > kMaxN) return SLAM_ECAP;
+        // free-pose edges per point -> Schur contributions k(k+1)/2
+        int run = 0, prev = -1;
+        for (int i = 0; i <= P.n_edge; i++) {
+            const int p = i < P.n_edge ? P.edge_pt[i] : -2;
+            if (p != prev) {
+                z.nct += (long long)run * (run + 1) / 2;
+                run = 0;
+                prev = p;
+            }
+            if (i < P.n_edge && hidx_all[h0 + P.edge_kf[i]] >= 0) {
+                run++;
+                z.nspe++;
             }
         }
-        for (int i = 0; i < P.n_edge; i++)
-            if (hidx[P.edge_kf[i]] >= 0) pose_edges[hidx[P.edge_kf[i]]].push_back(H.ne + i);
-        for (int i = 0; i < np; i++) {
-            H.pe_off.push_back((int)H.pe.size());
-            for (int e : pose_edges[i]) H.pe.push_back(e);
-            H.pose_win.push_back(w);
-        }
-        D.blk0 = H.nblk;
-        D.nblk = (int)blist.size();
-        for (int i2 = 0; i2 < np; i2++)
-            for (int i1 = 0; i1 <= i2; i1++) {
-                const auto& L = blist[(size_t)i2 * (i2 + 1) / 2 + i1];
-                H.blk_pose.push_back(int2{i1, i2});
-                H.blk_win.push_back(w);
-                H.ct_off.push_back((int)H.ct.size());
-                H.ct.insert(H.ct.end(), L.begin(), L.end());
-            }
-        H.nblk += D.nblk;
-        H.nkf += P.n_kf;
-        H.npt += P.n_pt;
-        H.ne += P.n_edge;
-        H.npose += np;
-        H.wins.push_back(D);
+        z.nkf += P.n_kf;
+        z.npt += P.n_pt;
+        z.ne += P.n_edge;
+        z.npose += np;
+        z.nblk += np * (np + 1) / 2;
+        z.hs_total += (long long)(ldlt_npad(6 * np) + 1) * ldlt_ld(6 * np);
+        z.max_n = std::max(z.max_n, 6 * np);
     }
-    H.pt_off.push_back(H.ne);
-    H.spe_off.push_back((int)H.spe.size());
-    H.pe_off.push_back((int)H.pe.size());
-    H.ct_off.push_back((int)H.ct.size());
     return SLAM_OK;
 }
 
-template <class T>
-hipError_t upload(DevBuf& b, const std::vector<T>& v, hipStream_t s) {
-    hipError_t e = b.ensure(sizeof(T) * std::max<size_t>(v.size(), 1));
-    if (e != hipSuccess || v.empty()) return e;
-    return hipMemcpyAsync(b.p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, s);
+// Pass 2: fill the arena in place.
+slam_status plan_fill(int n_prob, const slam_lba_problem* probs, const std::vector<int>& hidx_all,
+                      const std::vector<int>& np_of, const slam_lba_options* opt, const PlanSizes& Z,
+                      const Plan& P) {
+    // windows are independent given their start offsets: fill them on host threads
+    auto fill_one = [&](int w, std::vector<int>& col, std::vector<int>& bcnt,
+                        std::vector<int>& pcnt) -> slam_status {
+        const WinStart& ws = Z.starts[w];
+        int nkf = ws.kf0, npt = ws.pt0, ne = ws.e0, npose = ws.pose0, nblk = ws.blk0, nspe = ws.spe0;
+        long long nct = ws.ct0, hs = ws.hs0;
+        const slam_lba_problem& Q = probs[w];
+        const int* hidx = &hidx_all[ws.h0];
+        const int np = np_of[w];
+        WinDesc D{};
+        D.kf0 = nkf;
+        D.nk = Q.n_kf;
+        D.pt0 = npt;
+        D.npt = Q.n_pt;
+        D.e0 = ne;
+        D.ne = Q.n_edge;
+        D.pose0 = npose;
+        D.np = np;
+        D.n = 6 * np;
+        D.ld = ldlt_ld(D.n);
+        D.blk0 = nblk;
+        D.nblk = np * (np + 1) / 2;
+        D.hs_off = hs;
+        hs += (long long)(ldlt_npad(D.n) + 1) * D.ld;
+        P.wins[w] = D;
+        WinCtl c{};
+        c.user_lambda = opt->user_lambda_init;
+        c.lambda = -1;
+        c.ni = 2;
+        P.ctl[w] = c;
+        for (int k = 0; k < Q.n_kf; k++) {
+            P.kf_hp[nkf + k] = hidx[k] >= 0 ? npose + hidx[k] : -1;
+            P.kf_win[nkf + k] = w;
+        }
+        std::memcpy(P.kf_in + 16 * (size_t)nkf, Q.kf_Tcw, sizeof(float) * 16 * Q.n_kf);
+        std::memcpy(P.pt_in + 3 * (size_t)npt, Q.pt_pos, sizeof(float) * 3 * Q.n_pt);
+        for (int i = 0; i < Q.n_edge; i++) {
+            EdgeS& e = P.edges[ne + i];
+            const int k = Q.edge_kf[i];
+            e.pt = npt + Q.edge_pt[i];
+            e.kf = nkf + k;
+            e.hp = hidx[k] >= 0 ? npose + hidx[k] : -1;
+            e.win = w;
+            e.obs[0] = Q.edge_obs[3 * i];
+            e.obs[1] = Q.edge_obs[3 * i + 1];
+            e.obs[2] = Q.edge_obs[3 * i + 2];
+            e.info = Q.edge_inv_sigma2[i];
+        }
+        // point CSR + per-point free-pose edges sorted by pose (HplCCS column order) + Schur
+        // contribution counts per block (i1 <= i2: blk = i2 (i2 + 1) / 2 + i1)
+        const int spe_start = nspe;
+        bcnt.assign(D.nblk + 1, 0);
+        pcnt.assign(np + 1, 0);
+        int i = 0;
+        for (int p = 0; p < Q.n_pt; p++) {
+            P.pt_off[npt + p] = ne + i;
+            P.pt_win[npt + p] = w;
+            P.spe_off[npt + p] = nspe;
+            col.clear();
+            for (; i < Q.n_edge && Q.edge_pt[i] == p; i++)
+                if (hidx[Q.edge_kf[i]] >= 0) col.push_back(i);
+            for (size_t x = 1; x < col.size(); x++)  // stable insertion sort by pose
+                for (size_t y = x; y > 0 && hidx[Q.edge_kf[col[y - 1]]] > hidx[Q.edge_kf[col[y]]]; y--)
+                    std::swap(col[y - 1], col[y]);
+            for (size_t x = 0; x < col.size(); x++) {
+                const int i1 = hidx[Q.edge_kf[col[x]]];
+                if (x && i1 == hidx[Q.edge_kf[col[x - 1]]]) return SLAM_EINVAL;  // 2 obs of 1 point in 1 KF
+                P.spe[nspe++] = ne + col[x];
+                pcnt[i1 + 1]++;
+                for (size_t y = x; y < col.size(); y++) {
+                    const int i2 = hidx[Q.edge_kf[col[y]]];
+                    bcnt[i2 * (i2 + 1) / 2 + i1 + 1]++;
+                }
+            }
+        }
+        // blocks and their contribution lists, filled in point order
+        for (int b = 0; b < D.nblk; b++) bcnt[b + 1] += bcnt[b];
+        const long long wct = bcnt[D.nblk];
+        for (int i2 = 0, b = 0; i2 < np; i2++)
+            for (int i1 = 0; i1 <= i2; i1++, b++) {
+                P.blk_pose[nblk + b] = int2{i1, i2};
+                P.blk_win[nblk + b] = w;
+                P.ct_off[nblk + b] = (int)(nct + bcnt[b]);
+            }
+        for (int p = 0; p < Q.n_pt; p++) {
+            const int s0 = P.spe_off[npt + p], s1 = p + 1 < Q.n_pt ? P.spe_off[npt + p + 1] : nspe;
+            for (int x = s0; x < s1; x++) {
+                const int i1 = P.edges[P.spe[x]].hp - npose;
+                for (int y = x; y < s1; y++) {
+                    const int i2 = P.edges[P.spe[y]].hp - npose;
+                    P.ct[nct + bcnt[i2 * (i2 + 1) / 2 + i1]++] = int2{P.spe[x], P.spe[y]};
+                }
+            }
+        }
+        // edges of every free pose, in insertion order (shares the index space of spe)
+        for (int k = 0; k < np; k++) pcnt[k + 1] += pcnt[k];
+        for (int k = 0; k < np; k++) {
+            P.pe_off[npose + k] = spe_start + pcnt[k];
+            P.pose_win[npose + k] = w;
+        }
+        for (int e = 0; e < Q.n_edge; e++) {
+            const int h = hidx[Q.edge_kf[e]];
+            if (h >= 0) P.pe[spe_start + pcnt[h]++] = ne + e;
+        }
+        (void)wct;
+        (void)nkf;
+        return SLAM_OK;
+    };
+    const int hw = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const int nth = std::min(hw, n_prob);
+    std::vector<slam_status> rs(nth, SLAM_OK);
+    auto run = [&](int t) {
+        std::vector<int> col, bcnt, pcnt;
+        for (int w = t; w < n_prob; w += nth) {
+            const slam_status r = fill_one(w, col, bcnt, pcnt);
+            if (r != SLAM_OK) rs[t] = r;
+        }
+    };
+    if (nth <= 1) {
+        run(0);
+    } else {
+        std::vector<std::thread> th;
+        for (int t = 1; t < nth; t++) th.emplace_back(run, t);
+        run(0);
+        for (auto& x : th) x.join();
+    }
+    for (slam_status r : rs)
+        if (r != SLAM_OK) return r;
+    P.pt_off[Z.npt] = Z.ne;
+    P.spe_off[Z.npt] = Z.nspe;
+    P.pe_off[Z.npose] = Z.nspe;
+    P.ct_off[Z.nblk] = (int)Z.nct;
+    return SLAM_OK;
 }
 
 inline unsigned blocks(long long n, int t) { return (unsigned)std::max<long long>(1, (n + t - 1) / t); }
@@ -1213,7 +1483,7 @@ slam_status slamhot_lba_create(int device, slam_lba** out) {
         return SLAM_EHIP;
     }
     if (hipFuncSetAttribute((const void*)k_ldlt, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)(((kMaxN + 1) * kNB + 2 * kNB + kNB * kNB) * sizeof(double))) != hipSuccess) {
+                            (int)ldlt_lds_bytes(kMaxN)) != hipSuccess) {
         slamhot_lba_destroy(s);
         return SLAM_EHIP;
     }
@@ -1226,15 +1496,17 @@ void slamhot_lba_destroy(slam_lba* s) {
     (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     if (s->h_cnt) (void)hipHostFree(s->h_cnt);
+    if (s->harena) (void)hipHostFree(s->harena);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     delete s;
 }
 
-slam_status slamhot_lba_last_stats(const slam_lba* s, double* device_ms, int* syncs) {
+slam_status slamhot_lba_last_stats(const slam_lba* s, double* device_ms, double* plan_ms, int* syncs) {
     if (!s) return SLAM_EINVAL;
     if (device_ms) *device_ms = s->last_ms;
+    if (plan_ms) *plan_ms = s->last_plan_ms;
     if (syncs) *syncs = s->last_syncs;
     return SLAM_OK;
 }
@@ -1249,8 +1521,10 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
             (probs[w].n_edge && !results[w].edge_outlier))
             return SLAM_EINVAL;
     if (n_prob == 0) return SLAM_OK;
-    HostPlan H;
-    slam_status st = build_plan(n_prob, probs, H);
+    const auto t_plan0 = std::chrono::steady_clock::now();
+    PlanSizes Z;
+    std::vector<int> hidx_all, np_of;
+    slam_status st = plan_sizes(n_prob, probs, Z, hidx_all, np_of);
     if (st != SLAM_OK) return st;
     const bool stop0 = stop_flag && *stop_flag;
     for (int w = 0; w < n_prob; w++) {
@@ -1268,47 +1542,39 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
             std::memset(results[w].edge_outlier, 0, P.n_edge);
         }
         s->last_ms = 0;
+        s->last_plan_ms = 0;
         s->last_syncs = 0;
         return SLAM_OK;
     }
     SLAM_HIP_TRY(hipSetDevice(s->device));
     hipStream_t S = s->stream;
     const int nw = n_prob;
-    // host-side LM options per window
-    std::vector<WinCtl> ctl0(nw);
-    for (int w = 0; w < nw; w++) {
-        WinCtl c{};
-        c.user_lambda = opt->user_lambda_init;
-        c.lambda = -1;
-        c.ni = 2;
-        ctl0[w] = c;
+    const Layout LY = make_layout(Z);
+    if (LY.total > s->harena_cap) {
+        SLAM_HIP_TRY(hipStreamSynchronize(S));
+        if (s->harena) (void)hipHostFree(s->harena);
+        s->harena = nullptr;
+        s->harena_cap = 0;
+        SLAM_HIP_TRY(hipHostMalloc((void**)&s->harena, LY.total, hipHostMallocDefault));
+        s->harena_cap = LY.total;
     }
+    const Plan HP = bind(s->harena, LY);
+    st = plan_fill(n_prob, probs, hidx_all, np_of, opt, Z, HP);
+    if (st != SLAM_OK) return st;
+    SLAM_HIP_TRY(s->arena.ensure(LY.total));
+    SLAM_HIP_TRY(hipMemcpyAsync(s->arena.p, s->harena, LY.total, hipMemcpyHostToDevice, S));
+    const Plan DP = bind((unsigned char*)s->arena.p, LY);
+    struct {
+        int nkf, npt, ne, npose, nblk;
+    } H{Z.nkf, Z.npt, Z.ne, Z.npose, Z.nblk};
     const long long pose_stride = 8LL * std::max(H.nkf, 1), pt_stride = 4LL * std::max(H.npt, 1);
-    SLAM_HIP_TRY(upload(s->edges, H.edges, S));
-    SLAM_HIP_TRY(upload(s->wins, H.wins, S));
-    SLAM_HIP_TRY(upload(s->ctl, ctl0, S));
     SLAM_HIP_TRY(s->cnt.ensure(sizeof(Counters)));
-    SLAM_HIP_TRY(upload(s->pt_off, H.pt_off, S));
-    SLAM_HIP_TRY(upload(s->pt_win, H.pt_win, S));
-    SLAM_HIP_TRY(upload(s->spe_off, H.spe_off, S));
-    SLAM_HIP_TRY(upload(s->spe, H.spe, S));
-    SLAM_HIP_TRY(upload(s->pe_off, H.pe_off, S));
-    SLAM_HIP_TRY(upload(s->pe, H.pe, S));
-    SLAM_HIP_TRY(upload(s->pose_win, H.pose_win, S));
-    SLAM_HIP_TRY(upload(s->kf_hp, H.kf_hp, S));
-    SLAM_HIP_TRY(upload(s->kf_win, H.kf_win, S));
-    SLAM_HIP_TRY(upload(s->blk_pose, H.blk_pose, S));
-    SLAM_HIP_TRY(upload(s->blk_win, H.blk_win, S));
-    SLAM_HIP_TRY(upload(s->ct_off, H.ct_off, S));
-    SLAM_HIP_TRY(upload(s->ct, H.ct, S));
-    SLAM_HIP_TRY(upload(s->kf_in, H.kf_in, S));
-    SLAM_HIP_TRY(upload(s->pt_in, H.pt_in, S));
     const size_t ne = std::max(H.ne, 1), npt = std::max(H.npt, 1), nps = std::max(H.npose, 1);
     SLAM_HIP_TRY(s->poses.ensure(sizeof(double) * 2 * pose_stride));
     SLAM_HIP_TRY(s->pts.ensure(sizeof(double) * 2 * pt_stride));
     SLAM_HIP_TRY(s->err.ensure(sizeof(double) * 4 * ne));
     SLAM_HIP_TRY(s->rho.ensure(sizeof(double) * ne));
-    SLAM_HIP_TRY(s->lin.ensure(sizeof(double) * kLinStride * ne));
+    SLAM_HIP_TRY(s->lin.ensure(sizeof(double) * kHplStride * ne));
     SLAM_HIP_TRY(s->tr.ensure(sizeof(double) * kTrStride * ne));
     SLAM_HIP_TRY(s->Hll.ensure(sizeof(double) * 8 * npt));
     SLAM_HIP_TRY(s->bl.ensure(sizeof(double) * 4 * npt));
@@ -1317,13 +1583,14 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     SLAM_HIP_TRY(s->Hpp.ensure(sizeof(double) * 24 * nps));
     SLAM_HIP_TRY(s->bp.ensure(sizeof(double) * 8 * nps));
     SLAM_HIP_TRY(s->xp.ensure(sizeof(double) * 6 * nps));
-    SLAM_HIP_TRY(s->Hs.ensure(sizeof(double) * std::max<long long>(H.hs_total, 1)));
+    SLAM_HIP_TRY(s->Hs.ensure(sizeof(double) * std::max<long long>(Z.hs_total, 1)));
     SLAM_HIP_TRY(s->kf_out.ensure(sizeof(float) * 16 * std::max(H.nkf, 1)));
     SLAM_HIP_TRY(s->pt_out.ensure(sizeof(float) * 3 * npt));
     SLAM_HIP_TRY(s->outl.ensure(ne));
     SLAM_HIP_TRY(hipMemsetAsync(s->xp.p, 0, sizeof(double) * 6 * nps, S));
     SLAM_HIP_TRY(hipMemsetAsync(s->xl.p, 0, sizeof(double) * 4 * npt, S));
     SLAM_HIP_TRY(hipMemsetAsync(s->err.p, 0, sizeof(double) * 4 * ne, S));
+    s->last_plan_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_plan0).count();
 
     Cam cam;
     const slam_camera& c0 = probs[0].cam;
@@ -1345,20 +1612,19 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     hk.dsqr_mono = (float)(hk.delta_mono * hk.delta_mono);
     hk.dsqr_stereo = (float)(hk.delta_stereo * hk.delta_stereo);
 
-    EdgeS* dE = as<EdgeS>(s->edges);
-    WinDesc* dW = as<WinDesc>(s->wins);
-    WinCtl* dC = as<WinCtl>(s->ctl);
+    EdgeS* dE = DP.edges;
+    WinDesc* dW = DP.wins;
+    WinCtl* dC = DP.ctl;
     Counters* dCnt = as<Counters>(s->cnt);
     double* poses = as<double>(s->poses);
     double* pts = as<double>(s->pts);
     const int T = 256;
     int syncs = 0;
     SLAM_HIP_TRY(hipEventRecord(s->ev0, S));
-    k_init_state<<<blocks(H.nkf + H.npt, T), T, 0, S>>>(H.nkf, H.npt, as<float>(s->kf_in), as<float>(s->pt_in),
+    k_init_state<<<blocks(H.nkf + H.npt, T), T, 0, S>>>(H.nkf, H.npt, DP.kf_in, DP.pt_in,
                                                          poses, pts);
-    int max_n = 0;
-    for (const WinDesc& D : H.wins) max_n = std::max(max_n, D.n);
-    const size_t lds_bytes = ((size_t)(max_n + 1) * kNB + 2 * kNB + kNB * kNB) * sizeof(double);
+    k_ldlt_pad<<<nw, 64, 0, S>>>(dW, as<double>(s->Hs));
+    const size_t lds_bytes = ldlt_lds_bytes(Z.max_n);
     bool stopped = false;
     const int iters_of[2] = {opt->iters_first, opt->iters_second};
     for (int o = 0; o < 2 && !stopped; o++) {
@@ -1368,32 +1634,32 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
                 stopped = true;
                 break;
             }
-            k_linearize<<<blocks(H.ne, T), T, 0, S>>>(H.ne, dE, dC, poses, pts, pose_stride, pt_stride, cam, hk,
-                                                       as<double>(s->err), as<double>(s->rho), as<double>(s->lin));
-            k_point_reduce<<<blocks(H.npt, T), T, 0, S>>>(H.npt, as<int>(s->pt_off), as<int>(s->pt_win), dC,
-                                                           as<double>(s->lin), as<double>(s->Hll), as<double>(s->bl));
-            k_pose_reduce<<<blocks(27LL * H.npose, T), T, 0, S>>>(H.npose, as<int>(s->pe_off), as<int>(s->pe),
-                                                                   as<int>(s->pose_win), dC, as<double>(s->lin),
-                                                                   as<double>(s->Hpp), as<double>(s->bp));
+            k_lin_points<<<blocks(H.npt, 128), 128, 0, S>>>(H.npt, DP.pt_off, DP.pt_win, dE, dC, poses, pts, pose_stride,
+                                                              pt_stride, cam, hk, as<double>(s->err),
+                                                              as<double>(s->rho), as<double>(s->lin),
+                                                              as<double>(s->Hll), as<double>(s->bl));
+            k_lin_poses<<<blocks(H.npose, 4), 256, 0, S>>>(H.npose, DP.pe_off, DP.pe, DP.pose_win, dE, dC, poses, pts,
+                                                            pose_stride, pt_stride, cam, hk, as<double>(s->Hpp),
+                                                            as<double>(s->bp));
             k_iter_begin<<<nw, kCtlThreads, 0, S>>>(dW, dC, as<double>(s->rho), as<double>(s->Hpp),
                                                     as<double>(s->Hll));
             bool any_active = false;
             for (int t = 0; t < 10; t++) {
-                k_schur_point<<<blocks(H.npt, T), T, 0, S>>>(H.npt, as<int>(s->spe_off), as<int>(s->spe),
-                                                              as<int>(s->pt_win), dC, as<double>(s->Hll),
+                k_schur_point<<<blocks(H.npt, T), T, 0, S>>>(H.npt, DP.spe_off, DP.spe,
+                                                              DP.pt_win, dC, as<double>(s->Hll),
                                                               as<double>(s->bl), as<double>(s->lin),
                                                               as<double>(s->Dinv), as<double>(s->tr));
                 if (H.nblk)
                     k_schur_block<<<blocks(H.nblk, 4), 256, 0, S>>>(
-                        H.nblk, as<int2>(s->blk_pose), as<int>(s->blk_win), as<int>(s->ct_off), as<int2>(s->ct), dW,
-                        dC, as<double>(s->Hpp), as<double>(s->bp), as<int>(s->pe_off), as<int>(s->pe),
+                        H.nblk, DP.blk_pose, DP.blk_win, DP.ct_off, DP.ct, dW,
+                        dC, as<double>(s->Hpp), as<double>(s->bp), DP.pe_off, DP.pe,
                         as<double>(s->lin), as<double>(s->tr), as<double>(s->Hs));
                 k_ldlt<<<nw, 512, lds_bytes, S>>>(dW, dC, as<double>(s->Hs), as<double>(s->xp));
-                k_backsub<<<blocks(H.npt, T), T, 0, S>>>(H.npt, as<int>(s->spe_off), as<int>(s->spe), dE,
-                                                          as<int>(s->pt_win), dC, as<double>(s->bl),
+                k_backsub<<<blocks(H.npt, T), T, 0, S>>>(H.npt, DP.spe_off, DP.spe, dE,
+                                                          DP.pt_win, dC, as<double>(s->bl),
                                                           as<double>(s->Dinv), as<double>(s->lin), as<double>(s->xp),
                                                           as<double>(s->xl), pts, pt_stride);
-                k_pose_update<<<blocks(H.nkf, T), T, 0, S>>>(H.nkf, as<int>(s->kf_hp), as<int>(s->kf_win), dC,
+                k_pose_update<<<blocks(H.nkf, T), T, 0, S>>>(H.nkf, DP.kf_hp, DP.kf_win, dC,
                                                               as<double>(s->xp), poses, pose_stride);
                 k_trial_error<<<blocks(H.ne, T), T, 0, S>>>(H.ne, dE, dC, poses, pts, pose_stride, pt_stride, cam, hk,
                                                              as<double>(s->err), as<double>(s->rho));
@@ -1415,7 +1681,7 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     }
     k_finalize_edges<<<blocks(H.ne, T), T, 0, S>>>(H.ne, dE, dC, poses, pts, pose_stride, pt_stride,
                                                     as<double>(s->err), as<uint8_t>(s->outl));
-    k_finalize_state<<<blocks(H.nkf + H.npt, T), T, 0, S>>>(H.nkf, H.npt, as<int>(s->kf_win), as<int>(s->pt_win), dC,
+    k_finalize_state<<<blocks(H.nkf + H.npt, T), T, 0, S>>>(H.nkf, H.npt, DP.kf_win, DP.pt_win, dC,
                                                              poses, pts, pose_stride, pt_stride,
                                                              as<float>(s->kf_out), as<float>(s->pt_out));
     SLAM_HIP_TRY(hipGetLastError());
@@ -1426,7 +1692,7 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     if (H.nkf) SLAM_HIP_TRY(hipMemcpyAsync(kf_out.data(), s->kf_out.p, sizeof(float) * kf_out.size(), hipMemcpyDeviceToHost, S));
     if (H.npt) SLAM_HIP_TRY(hipMemcpyAsync(pt_out.data(), s->pt_out.p, sizeof(float) * pt_out.size(), hipMemcpyDeviceToHost, S));
     if (H.ne) SLAM_HIP_TRY(hipMemcpyAsync(outl.data(), s->outl.p, outl.size(), hipMemcpyDeviceToHost, S));
-    SLAM_HIP_TRY(hipMemcpyAsync(ctl1.data(), s->ctl.p, sizeof(WinCtl) * nw, hipMemcpyDeviceToHost, S));
+    SLAM_HIP_TRY(hipMemcpyAsync(ctl1.data(), DP.ctl, sizeof(WinCtl) * nw, hipMemcpyDeviceToHost, S));
     SLAM_HIP_TRY(hipStreamSynchronize(S));
     float ms = 0;
     SLAM_HIP_TRY(hipEventElapsedTime(&ms, s->ev0, s->ev1));
@@ -1434,7 +1700,7 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     s->last_syncs = syncs + 1;
     for (int w = 0; w < nw; w++) {
         const slam_lba_problem& P = probs[w];
-        const WinDesc& D = H.wins[w];
+        const WinDesc& D = HP.wins[w];
         slam_lba_result& R = results[w];
         for (int k = 0; k < P.n_kf; k++) {
             const float* src = P.kf_fixed[k] == 2 ? P.kf_Tcw + 16 * k : &kf_out[16 * (size_t)(D.kf0 + k)];

@@ -529,9 +529,10 @@ class LocalBundleAdjustment:
         return res[0] if single else res
 
     def last_stats(self):
-        ms, syncs = C.c_double(0), I(0)
-        check(lib().slamhot_lba_last_stats(self._h, C.byref(ms), C.byref(syncs)), "lba_last_stats")
-        return ms.value, syncs.value
+        """(device_ms, plan_ms, syncs) of the last solve."""
+        ms, plan, syncs = C.c_double(0), C.c_double(0), I(0)
+        check(lib().slamhot_lba_last_stats(self._h, C.byref(ms), C.byref(plan), C.byref(syncs)), "lba_last_stats")
+        return ms.value, plan.value, syncs.value
 
 
 def _bind_lba(L):
@@ -541,5 +542,5 @@ def _bind_lba(L):
     L.slamhot_lba_destroy.argtypes = [P]
     L.slamhot_lba_destroy.restype = None
     L.slamhot_lba_solve.argtypes = [P, I, C.POINTER(LbaProblem), C.POINTER(LbaOptions), P, C.POINTER(LbaResult)]
-    L.slamhot_lba_last_stats.argtypes = [P, C.POINTER(C.c_double), C.POINTER(I)]
+    L.slamhot_lba_last_stats.argtypes = [P, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(I)]
     L._lba_ready = True

@@ -1,0 +1,76 @@
+// Microbenchmark of the dense LDL^T kernel (k_ldlt) on one n x n SPD system, with per-phase
+// wall-clock accounting (LBA_PHASE_TIMING).  Build: see tools/microbench/Makefile.
+#define LBA_PHASE_TIMING 1
+#include "../../orb-slam3-noted_amd/csrc/lba.hip"
+
+#include <cstdio>
+#include <random>
+
+int main(int argc, char** argv) {
+    const int n = argc > 1 ? atoi(argv[1]) : 288;
+    const int reps = argc > 2 ? atoi(argv[2]) : 20;
+    const int npad = ldlt_npad(n), N = npad + 1, ld = ldlt_ld(n);
+    std::mt19937_64 rng(1);
+    std::normal_distribution<double> g;
+    std::vector<double> M((size_t)n * n), A((size_t)N * ld, 0.0), b(n);
+    for (auto& v : M) v = g(rng);
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j <= i; j++) {
+            double s = (i == j) ? n : 0.0;
+            for (int k = 0; k < n; k++) s += M[(size_t)i * n + k] * M[(size_t)j * n + k] / n;
+            A[(size_t)i * ld + j] = s;
+        }
+    for (int i = 0; i < n; i++) A[(size_t)npad * ld + i] = b[i] = g(rng);
+    for (int i = n; i < npad; i++) A[(size_t)i * ld + i] = 1.0;
+    WinDesc W{};
+    W.n = n;
+    W.ld = ld;
+    W.hs_off = 0;
+    WinCtl C{};
+    C.need_trial = 1;
+    double *dA, *dA0, *dx;
+    WinDesc* dW;
+    WinCtl* dC;
+    hipMalloc(&dA, sizeof(double) * A.size());
+    hipMalloc(&dA0, sizeof(double) * A.size());
+    hipMalloc(&dx, sizeof(double) * n);
+    hipMalloc(&dW, sizeof(W));
+    hipMalloc(&dC, sizeof(C));
+    hipMemcpy(dA0, A.data(), sizeof(double) * A.size(), hipMemcpyHostToDevice);
+    hipMemcpy(dW, &W, sizeof(W), hipMemcpyHostToDevice);
+    hipMemcpy(dC, &C, sizeof(C), hipMemcpyHostToDevice);
+    const size_t lds = ldlt_lds_bytes(n);
+    hipFuncSetAttribute((const void*)k_ldlt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    float total = 0;
+    unsigned long long zero[8] = {0};
+    for (int r = 0; r < reps + 1; r++) {
+        hipMemcpy(dA, dA0, sizeof(double) * A.size(), hipMemcpyDeviceToDevice);
+        if (r == 1) hipMemcpyToSymbol(HIP_SYMBOL(g_ldlt_phase), zero, sizeof(zero));
+        hipEventRecord(e0);
+        k_ldlt<<<1, 512, lds>>>(dW, dC, dA, dx);
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+        float ms;
+        hipEventElapsedTime(&ms, e0, e1);
+        if (r) total += ms;
+    }
+    unsigned long long ph[8];
+    hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_ldlt_phase), sizeof(ph));
+    std::vector<double> x(n);
+    hipMemcpy(x.data(), dx, sizeof(double) * n, hipMemcpyDeviceToHost);
+    double res = 0, nb = 0;
+    for (int i = 0; i < n; i++) {
+        double s = 0;
+        for (int j = 0; j < n; j++) s += (j <= i ? A[(size_t)i * ld + j] : A[(size_t)j * ld + i]) * x[j];
+        res = std::max(res, std::fabs(s - b[i]));
+        nb = std::max(nb, std::fabs(b[i]));
+    }
+    const double us = 1e3 * total / reps;
+    // wall_clock64 runs at 100 MHz on gfx9
+    printf("n=%d ldlt %.1f us  residual %.3e  phases(us): diag %.1f  rows %.1f  trailing %.1f  backsolve %.1f\n", n,
+           us, res / nb, ph[1] / 100.0 / reps, ph[2] / 100.0 / reps, ph[3] / 100.0 / reps, ph[4] / 100.0 / reps);
+    return 0;
+}
