@@ -94,6 +94,7 @@ def main():
     torch.cuda.set_device(device)
 
     import slamhot
+    from slamhot import dist as sdist
     from slamhot import synth
 
     W, H, B = args.width, args.height, args.batch
@@ -135,16 +136,9 @@ def main():
 
     n_host = d_n.cpu().numpy()
     kps_per_frame = float(n_host.mean())
-    digest = int(np.bitwise_xor.reduce(d_desc[:, :64].cpu().numpy().view(np.uint64).ravel()) & ((1 << 62) - 1))
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        g = [torch.zeros(2, dtype=torch.int64, device=device) for _ in range(world)]
-        dist.all_gather(g, torch.tensor([int(n_host.sum()), digest], dtype=torch.int64, device=device))
-        total_kps = int(sum(int(x[0].item()) for x in g))
-    else:
-        total_kps = int(n_host.sum())
+    dig = sdist.digest(d_desc[:, :64].cpu().numpy())
+    elapsed, _ = sdist.reduce_run(dist, device, elapsed, B * args.steps)
+    total_kps = sum(c for c, _ in sdist.gather_digests(dist, device, world, int(n_host.sum()), dig))
 
     frames_total = B * args.steps * world
     value = frames_total / elapsed
@@ -225,6 +219,11 @@ def main():
         dist.destroy_process_group()
 
 
+def sdist_shard_seeds(rank, world, n):
+    from slamhot import dist as sdist
+    return sdist.shard(n * world, rank, world)
+
+
 def lba_leg(args, rank, world, local_rank, dist, device):
     """LM iterations/s of the device LBA solver on config-4 windows (BASELINE.json configs[3])."""
     import torch
@@ -232,7 +231,8 @@ def lba_leg(args, rank, world, local_rank, dist, device):
     import slamhot
     from slamhot import synth
     nwin = args.lba_windows
-    pool = [synth.lba_window(1000 * rank + s) for s in range(8)]
+    # windows are sharded by rank: rank r solves its own seeds (independent units)
+    pool = [synth.lba_window(s) for s in sdist_shard_seeds(rank, world, 8)]
     windows = [pool[i % len(pool)] for i in range(nwin)]
     S = slamhot.LocalBundleAdjustment(device=local_rank)
     S.solve(windows[: min(4, nwin)])  # warm-up
@@ -255,15 +255,9 @@ def lba_leg(args, rank, world, local_rank, dist, device):
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed, float(iters), dev_ms], dtype=torch.float64, device=device)
-        tmax = t.clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        tsum = t.clone()
-        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
-        elapsed, iters_all, dev_max = float(tmax[0]), float(tsum[1]), float(tmax[2])
-    else:
-        iters_all, dev_max = float(iters), dev_ms
+    from slamhot import dist as sdist
+    dev_max, _ = sdist.reduce_run(dist, device, dev_ms, 0.0)
+    elapsed, iters_all = sdist.reduce_run(dist, device, elapsed, float(iters))
     out = {
         "metric": "LocalBundleAdjustment LM iterations/s",
         "value": round(iters_all / elapsed, 1),

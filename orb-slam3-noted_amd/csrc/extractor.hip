@@ -1,13 +1,14 @@
 // extractor.hip — MI355X (gfx950) ORB extractor: the device side of
 // ORBextractor::operator() (ORBextractor.cc:1068-1150), batched over frames.
 //
-// Pipeline per batch (one HIP stream, captured in a hipGraph per geometry):
-//   k_resize      x (L-1)  chained INTER_LINEAR pyramid            ComputePyramid :1152
-//   k_fast_cells  x 1      per-cell FAST-9 score + per-cell 3x3 NMS ComputeKeyPointsOctTree :787-853
+// Pipeline per batch (launch stream + a side stream for the blur):
+//   k_resize3     x (L-1)  chained INTER_LINEAR pyramid            ComputePyramid :1152
+//   k_fast_wave   x 1      FAST-9 score + per-cell 3x3 NMS, 1 wave/cell ComputeKeyPointsOctTree :787-853
+//   k_fast_cells  x 1      the same for cells wider than one wave (1 WG/cell)
 //   k_octree      x 1      quadtree distribution, 1 WG/(frame,lvl) DistributeOctTree :537-761
 //   k_layout      x 1      lapping-area output order, 1 WG/frame   operator() :1100-1146
-//   k_blur        x 1      GaussianBlur 7x7 sigma 2 fixed point    operator() :1114-1115
-//   k_orb         x 1      IC angle + rBRIEF, one wave per kp      IC_Angle :75, computeOrbDescriptor :106
+//   k_blur3       x 1      GaussianBlur 7x7 sigma 2 fixed point    operator() :1114-1115
+//   k_orb2        x 1      IC angle + rBRIEF, one wave per kp      IC_Angle :75, computeOrbDescriptor :106
 //
 // Data layout in HBM (per handle, batch-major): input frames (level 0, tight rows); pyramid
 // levels 1.. per frame, rows padded to 64 B; blurred levels per frame; per-cell candidate
@@ -125,122 +126,8 @@ __device__ __forceinline__ void stage_u32(uint32_t* dst, int dstride, const uint
     }
 }
 
-// ---------------------------------------------------------------------------------------
-// k_resize: level l from level l-1 (cv::resize INTER_LINEAR 8U, OpenCV 4.2.0 generic fixed
-// point path).  Integer-only on the device: coefficient tables come from the host plan.
-// Block 64x4 threads, 4 output pixels per thread (one 32-bit store, rows padded to 64 B).
-// ---------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_resize(Bufs b, int l) {
-    const DevPlan& P = *b.plan;
-    const DevLevel& L = P.lv[l];
-    const int f = blockIdx.z;
-    const int dy = blockIdx.y * 4 + threadIdx.y;
-    const int dx0 = (blockIdx.x * 64 + threadIdx.x) * 4;
-    if (dy >= L.h || dx0 >= L.w) return;
-    const uint8_t* src = level_ptr(b, P, f, l - 1);
-    const int spitch = level_pitch(P, l - 1);
-    uint8_t* dst = b.pyr + (size_t)f * P.pyr_frame + L.pyr_off + (size_t)dy * L.pitch;
-    const ResizeY ry = b.ytab[L.ytab_off + dy];
-    const uint8_t* S0 = src + (size_t)ry.y0 * spitch;
-    const uint8_t* S1 = src + (size_t)ry.y1 * spitch;
-    uint32_t word = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int dx = dx0 + k;
-        int v = 0;
-        if (dx < L.w) {
-            const ResizeX rx = b.xtab[L.xtab_off + dx];
-            int d0, d1;
-            if (dx < L.xmax) {
-                d0 = S0[rx.sx] * rx.a0 + S0[rx.sx + 1] * rx.a1;
-                d1 = S1[rx.sx] * rx.a0 + S1[rx.sx + 1] * rx.a1;
-            } else {
-                d0 = S0[rx.sx] * 2048;
-                d1 = S1[rx.sx] * 2048;
-            }
-            v = (((ry.b0 * (d0 >> 4)) >> 16) + ((ry.b1 * (d1 >> 4)) >> 16) + 2) >> 2;
-        }
-        word |= (uint32_t)(v & 0xFF) << (8 * k);
-    }
-    *reinterpret_cast<uint32_t*>(dst + dx0) = word;
-}
 
-// ---------------------------------------------------------------------------------------
-// k_resize2: same arithmetic as k_resize, but each block produces kRzRows full output rows:
-// the <= kRzSrcRows source rows they read are staged in LDS with 32-bit loads, so every
-// source byte is fetched from L2/HBM once per block instead of 4 times per output pixel.
-// ---------------------------------------------------------------------------------------
-constexpr int kRzRows = 16, kRzSrcRows = 24;
 
-__global__ void __launch_bounds__(256) k_resize2(Bufs b, int l, int rows) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t rz_smem[];
-    const DevPlan& P = *b.plan;
-    const DevLevel& L = P.lv[l];
-    const DevLevel& S = P.lv[l - 1];
-    const int f = blockIdx.y;
-    const int dy0 = blockIdx.x * rows;
-    const int nrow = min(rows, L.h - dy0);
-    const uint8_t* src = level_ptr(b, P, f, l - 1);
-    const int spitch = level_pitch(P, l - 1);
-    const int sw = S.w;
-    const int sstride = (sw + 15) & ~15;
-    const int ys = b.ytab[L.ytab_off + dy0].y0;
-    const int ye = b.ytab[L.ytab_off + dy0 + nrow - 1].y1;
-    const int nsrc = ye - ys + 1;
-    // coefficient table of this level's output columns, staged next to the source rows
-    ResizeX* xs = reinterpret_cast<ResizeX*>(rz_smem + kRzSrcRows * sstride);
-    ResizeY* ysm = reinterpret_cast<ResizeY*>(xs + ((L.w + 3) & ~3));
-    stage_u32<4>(reinterpret_cast<uint32_t*>(xs), 2 * L.w, reinterpret_cast<const uint8_t*>(b.xtab + L.xtab_off),
-                 0, 1, 2 * L.w);
-    if (threadIdx.x < (((L.w + 3) & ~3) - L.w)) xs[L.w + threadIdx.x] = b.xtab[L.xtab_off + L.w - 1];
-    if (threadIdx.x < 4 * nrow)
-        reinterpret_cast<uint32_t*>(ysm)[threadIdx.x] =
-            reinterpret_cast<const uint32_t*>(b.ytab + L.ytab_off + dy0)[threadIdx.x];
-    if ((spitch & 3) == 0) {
-        stage_u32<8>(reinterpret_cast<uint32_t*>(rz_smem), sstride >> 2, src + (size_t)ys * spitch, spitch,
-                     nsrc, (sw + 3) >> 2);
-    } else {
-        for (int r = 0; r < nsrc; r++)
-            for (int c = threadIdx.x; c < sw; c += blockDim.x)
-                rz_smem[r * sstride + c] = src[(size_t)(ys + r) * spitch + c];
-    }
-    __syncthreads();
-    const int qw = (L.w + 3) >> 2;
-    uint8_t* dbase = b.pyr + (size_t)f * P.pyr_frame + L.pyr_off;
-    const float inv_qw = 1.0f / (float)qw;
-    // branch-free body: every LDS read of an item is independent and issued up front
-#pragma unroll 2
-    for (int i = threadIdx.x; i < nrow * qw; i += blockDim.x) {
-        int r, q;
-        split_rc(i, qw, inv_qw, r, q);
-        const ResizeY ry = ysm[r];
-        const uint8_t* S0 = rz_smem + (ry.y0 - ys) * sstride;
-        const uint8_t* S1 = rz_smem + (ry.y1 - ys) * sstride;
-        const uint4 xa = reinterpret_cast<const uint4*>(xs)[2 * q];
-        const uint4 xb = reinterpret_cast<const uint4*>(xs)[2 * q + 1];
-        const uint32_t sxs[4] = {xa.x, xa.z, xb.x, xb.z};
-        const uint32_t aas[4] = {xa.y, xa.w, xb.y, xb.w};
-        int p00[4], p01[4], p10[4], p11[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int sx = (int)sxs[k];
-            p00[k] = S0[sx];
-            p01[k] = S0[sx + 1];
-            p10[k] = S1[sx];
-            p11[k] = S1[sx + 1];
-        }
-        uint32_t word = 0;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int a0 = (int)(int16_t)(aas[k] & 0xFFFF), a1 = (int)(int16_t)(aas[k] >> 16);
-            const int d0 = __mul24(p00[k], a0) + __mul24(p01[k], a1);
-            const int d1 = __mul24(p10[k], a0) + __mul24(p11[k], a1);
-            const int v = ((__mul24((int)ry.b0, d0 >> 4) >> 16) + (__mul24((int)ry.b1, d1 >> 4) >> 16) + 2) >> 2;
-            word |= (uint32_t)(v & 0xFF) << (8 * k);
-        }
-        *reinterpret_cast<uint32_t*>(dbase + (size_t)(dy0 + r) * L.pitch + 4 * q) = word;
-    }
-}
 
 // ---------------------------------------------------------------------------------------
 // k_resize3: the resize with its coefficients recomputed per pixel in the reference's own
@@ -1032,140 +919,21 @@ __global__ void __launch_bounds__(256) k_layout(Bufs b) {
     }
 }
 
-// ---------------------------------------------------------------------------------------
-// k_blur: GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101) of every level (OpenCV 4.2.0
-// fixed-point 8U path: Q8 taps [18,34,48,56,48,34,18], exact u16 row sums, Q16 column sums
-// rounded >> 16).  Tile 64 x 32 output pixels per 256-thread workgroup.
-// ---------------------------------------------------------------------------------------
-constexpr int kBlurTW = 64, kBlurTH = 32;
-
+// GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101) (OpenCV 4.2.0 fixed-point 8U path: Q8 taps
+// [18,34,48,56,48,34,18], exact u16 row sums, Q16 column sums rounded >> 16) helpers.
 __device__ __forceinline__ int refl101(int i, int n) {
     if (i < 0) i = -i;
     if (i >= n) i = 2 * n - 2 - i;
     return i;
 }
 
-__global__ void __launch_bounds__(256) k_blur(Bufs b, int l, int ed) {
-    __shared__ uint8_t src[(kBlurTH + 6) * (kBlurTW + 8)];
-    __shared__ uint16_t hs[(kBlurTH + 6) * kBlurTW];
-    const DevPlan& P = *b.plan;
-    const DevLevel& L = P.lv[l];
-    const int f = blockIdx.z;
-    const int x0 = blockIdx.x * kBlurTW, y0 = blockIdx.y * kBlurTH;
-    const uint8_t* img = level_ptr(b, P, f, l);
-    const int pitch = level_pitch(P, l);
-    const int k0 = 18, k1 = 34, k2 = ed ? 48 : 49, k3 = ed ? 56 : 55;
-    const int SW = kBlurTW + 6, SH = kBlurTH + 6;
-    for (int i = threadIdx.x; i < SW * SH; i += blockDim.x) {
-        const int r = i / SW, c = i - r * SW;
-        const int yy = refl101(min(y0 + r - 3, L.h - 1 + 3), L.h);
-        const int xx = refl101(min(x0 + c - 3, L.w - 1 + 3), L.w);
-        src[r * (kBlurTW + 8) + c] = img[(size_t)yy * pitch + xx];
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < kBlurTW * SH; i += blockDim.x) {
-        const int r = i / kBlurTW, c = i - r * kBlurTW;
-        const uint8_t* s = &src[r * (kBlurTW + 8) + c];
-        hs[i] = (uint16_t)(k0 * (s[0] + s[6]) + k1 * (s[1] + s[5]) + k2 * (s[2] + s[4]) + k3 * s[3]);
-    }
-    __syncthreads();
-    uint8_t* dst = b.blur + (size_t)f * P.blur_frame + L.blur_off;
-    for (int i = threadIdx.x; i < kBlurTW * kBlurTH; i += blockDim.x) {
-        const int r = i / kBlurTW, c = i - r * kBlurTW;
-        const int y = y0 + r, x = x0 + c;
-        if (y >= L.h || x >= L.w) continue;
-        const uint16_t* h = &hs[r * kBlurTW + c];
-        const uint32_t acc = (uint32_t)k0 * (h[0] + h[6 * kBlurTW]) + (uint32_t)k1 * (h[kBlurTW] + h[5 * kBlurTW]) +
-                             (uint32_t)k2 * (h[2 * kBlurTW] + h[4 * kBlurTW]) + (uint32_t)k3 * h[3 * kBlurTW];
-        dst[(size_t)y * L.pitch + x] = (uint8_t)min((acc + (1u << 15)) >> 16, 255u);
-    }
-}
 
-// ---------------------------------------------------------------------------------------
-// k_blur2: the same GaussianBlur for ALL levels in one launch.  Tile = 128 x 16 output
-// pixels of one level (tile table from the host plan).  Source bytes are staged with
-// 32-bit loads (byte loads + reflect-101 only on border tiles), the horizontal pass writes
-// exact u16 row sums to LDS, and each thread produces 8 outputs of one row from one
-// 16-byte LDS read per tap row and stores them with one 64-bit store.
-// ---------------------------------------------------------------------------------------
-constexpr int kB2W = 128, kB2H = 16, kB2SW = kB2W + 8, kB2SH = kB2H + 6;
 
 struct BlurTile {
     int16_t level, pad;
     int16_t x0, y0;
 };
 
-__global__ void __launch_bounds__(256) k_blur2(Bufs b, const BlurTile* tiles, int ed) {
-    __shared__ __attribute__((aligned(16))) uint8_t src[kB2SH * kB2SW];
-    __shared__ __attribute__((aligned(16))) uint16_t hs[kB2SH * kB2W];
-    const DevPlan& P = *b.plan;
-    const BlurTile t = tiles[blockIdx.x];
-    const int l = t.level, f = blockIdx.y;
-    const DevLevel& L = P.lv[l];
-    const uint8_t* img = level_ptr(b, P, f, l);
-    const int pitch = level_pitch(P, l);
-    const int x0 = t.x0, y0 = t.y0;
-    const int k0 = 18, k1 = 34, k2 = ed ? 48 : 49, k3 = ed ? 56 : 55;
-    // staged columns: x0-4 .. x0+kB2W+3 (136 bytes), rows y0-3 .. y0+kB2H+2
-    const bool interior = x0 >= 4 && x0 + kB2W + 4 <= L.w && y0 >= 3 && y0 + kB2H + 3 <= L.h &&
-                          (pitch & 3) == 0;
-    if (interior) {
-        for (int i = threadIdx.x; i < kB2SH * (kB2SW / 4); i += blockDim.x) {
-            const int r = i / (kB2SW / 4), c4 = i - r * (kB2SW / 4);
-            const uint32_t v = *reinterpret_cast<const uint32_t*>(img + (size_t)(y0 - 3 + r) * pitch + x0 - 4 + 4 * c4);
-            *reinterpret_cast<uint32_t*>(&src[r * kB2SW + 4 * c4]) = v;
-        }
-    } else {
-        for (int i = threadIdx.x; i < kB2SH * kB2SW; i += blockDim.x) {
-            const int r = i / kB2SW, c = i - r * kB2SW;
-            const int yy = refl101(min(y0 - 3 + r, L.h + 2), L.h);
-            const int xx = refl101(min(x0 - 4 + c, L.w + 2), L.w);
-            src[i] = img[(size_t)yy * pitch + xx];
-        }
-    }
-    __syncthreads();
-    // horizontal pass: output column c uses staged columns c+1 .. c+7
-    for (int i = threadIdx.x; i < kB2SH * (kB2W / 8); i += blockDim.x) {
-        const int r = i / (kB2W / 8), g = i - r * (kB2W / 8);
-        const uint8_t* sp = &src[r * kB2SW + 8 * g];
-        uint8_t v[16];
-        *reinterpret_cast<uint2*>(v) = *reinterpret_cast<const uint2*>(sp);
-        *reinterpret_cast<uint2*>(v + 8) = *reinterpret_cast<const uint2*>(sp + 8);
-        uint32_t o[4];
-#pragma unroll
-        for (int j = 0; j < 8; j += 2) {
-            const uint32_t a = k0 * (v[j + 1] + v[j + 7]) + k1 * (v[j + 2] + v[j + 6]) + k2 * (v[j + 3] + v[j + 5]) + k3 * v[j + 4];
-            const uint32_t c = k0 * (v[j + 2] + v[j + 8]) + k1 * (v[j + 3] + v[j + 7]) + k2 * (v[j + 4] + v[j + 6]) + k3 * v[j + 5];
-            o[j / 2] = a | (c << 16);
-        }
-        *reinterpret_cast<uint4*>(&hs[r * kB2W + 8 * g]) = make_uint4(o[0], o[1], o[2], o[3]);
-    }
-    __syncthreads();
-    // vertical pass: thread -> (row, 8 columns)
-    const int r = threadIdx.x >> 4, g = threadIdx.x & 15;
-    const int y = y0 + r, x = x0 + 8 * g;
-    if (y >= L.h || x >= L.w) return;
-    uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    const uint32_t kk[7] = {(uint32_t)k0, (uint32_t)k1, (uint32_t)k2, (uint32_t)k3, (uint32_t)k2, (uint32_t)k1, (uint32_t)k0};
-#pragma unroll
-    for (int j = 0; j < 7; j++) {
-        const uint4 q = *reinterpret_cast<const uint4*>(&hs[(r + j) * kB2W + 8 * g]);
-        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-        for (int e = 0; e < 4; e++) {
-            acc[2 * e] += kk[j] * (w[e] & 0xFFFF);
-            acc[2 * e + 1] += kk[j] * (w[e] >> 16);
-        }
-    }
-    uint32_t lo = 0, hi = 0;
-#pragma unroll
-    for (int e = 0; e < 4; e++) {
-        lo |= min((acc[e] + (1u << 15)) >> 16, 255u) << (8 * e);
-        hi |= min((acc[e + 4] + (1u << 15)) >> 16, 255u) << (8 * e);
-    }
-    uint8_t* dst = b.blur + (size_t)f * P.blur_frame + L.blur_off + (size_t)y * L.pitch + x;
-    *reinterpret_cast<uint2*>(dst) = make_uint2(lo, hi);
-}
 
 // ---------------------------------------------------------------------------------------
 // k_blur3: GaussianBlur for all levels, one launch, 128 x 32 output tiles.
@@ -1274,105 +1042,6 @@ __global__ void __launch_bounds__(256) k_blur3(Bufs b, const BlurTile* tiles, in
     }
 }
 
-// ---------------------------------------------------------------------------------------
-// k_orb: one wave per keypoint.  IC_Angle (ORBextractor.cc:75-102) on the unblurred level:
-// lane v (0..30) sums row v-15 of the radius-15 disc; exact integer wave reduction; then
-// cv::fastAtan2.  rBRIEF (computeOrbDescriptor :106-145) on the blurred level: bit
-// i = lane + 64*w is the pattern pair i; one __ballot per 64 bits gives 8 descriptor bytes
-// (little-endian bit order = the reference's byte/bit order).
-// ---------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_orb(Bufs b) {
-    const DevPlan& P = *b.plan;
-    const int f = blockIdx.y;
-    const int slot = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (slot >= P.kslots) return;
-    int l = 0;
-    while (l + 1 < P.nlevels && slot >= P.lv[l + 1].kbase) l++;
-    const DevLevel& L = P.lv[l];
-    const int i = slot - L.kbase;
-    if (i >= b.ocnt[(size_t)f * P.nlevels + l]) return;
-    const int oi = b.oidx[(size_t)f * P.kslots + slot];
-    if (oi >= b.cap) return;
-    const uint32_t key = b.okp[(size_t)f * P.kslots + slot];
-    const int kx = kp_x(key), ky = kp_y(key);
-
-    // --- orientation
-    const uint8_t* img = level_ptr(b, P, f, l);
-    const int pitch = level_pitch(P, l);
-    // lanes 0..30 own column u = lane-15 for rows v = -15..0, lanes 32..62 the same
-    // columns for rows 1..15; disc membership |u| <= umax[|v|] masks the (independent) loads
-    int m01 = 0, m10 = 0;
-    {
-        const int cl = lane & 31, half = lane >> 5;
-        if (cl < 2 * kHalfPatch + 1) {
-            const int u = cl - kHalfPatch;
-            const int au = u < 0 ? -u : u;
-            const uint8_t* colp = img + (size_t)ky * pitch + kx + u;
-            int s0 = 0, s1 = 0;
-            if (half == 0) {
-#pragma unroll
-                for (int v = -kHalfPatch; v <= 0; v++) {
-                    const int val = colp[(ptrdiff_t)v * pitch] & -(int)(au <= P.umax[-v]);
-                    s0 += val;
-                    s1 += v * val;
-                }
-            } else {
-#pragma unroll
-                for (int v = 1; v <= kHalfPatch; v++) {
-                    const int val = colp[(ptrdiff_t)v * pitch] & -(int)(au <= P.umax[v]);
-                    s0 += val;
-                    s1 += v * val;
-                }
-            }
-            m10 = u * s0;
-            m01 = s1;
-        }
-    }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        m10 += __shfl_xor(m10, o, 64);
-        m01 += __shfl_xor(m01, o, 64);
-    }
-    const float angle = cv_fast_atan2((float)m01, (float)m10);
-
-    // --- descriptor
-    const float factor_pi = (float)(3.14159265358979323846 / 180.f);
-    float sn, cs;
-    glibc_sincosf(angle * factor_pi, &sn, &cs);
-    const float a = cs, bb = sn;
-    const uint8_t* bl = b.blur + (size_t)f * P.blur_frame + L.blur_off;
-    const uint8_t* center = bl + (size_t)ky * L.pitch + kx;
-    uint8_t* desc = b.out_desc + ((size_t)f * b.cap + oi) * 32;
-    int t0[4], t1[4];
-#pragma unroll
-    for (int w = 0; w < 4; w++) {
-        const int bit = w * 64 + lane;
-        const float x0 = (float)c_pattern[4 * bit], y0 = (float)c_pattern[4 * bit + 1];
-        const float x1 = (float)c_pattern[4 * bit + 2], y1 = (float)c_pattern[4 * bit + 3];
-        const int r0 = cv_round(fmaf(x0, bb, y0 * a)), c0 = cv_round(fmaf(x0, a, -(y0 * bb)));
-        const int r1 = cv_round(fmaf(x1, bb, y1 * a)), c1 = cv_round(fmaf(x1, a, -(y1 * bb)));
-        t0[w] = center[r0 * L.pitch + c0];
-        t1[w] = center[r1 * L.pitch + c1];
-    }
-    uint64_t m[4];
-#pragma unroll
-    for (int w = 0; w < 4; w++) m[w] = __ballot(t0[w] < t1[w]);
-    if (lane < 4) reinterpret_cast<uint64_t*>(desc)[lane] = m[0] * (lane == 0) + m[1] * (lane == 1) + m[2] * (lane == 2) + m[3] * (lane == 3);
-    if (lane == 0) {
-        slam_keypoint kp;
-        const float sx = l ? (float)kx * L.scale : (float)kx;
-        const float sy = l ? (float)ky * L.scale : (float)ky;
-        kp.x = sx;
-        kp.y = sy;
-        kp.size = L.size;
-        kp.angle = angle;
-        kp.response = (float)kp_s(key);
-        kp.octave = l;
-        kp.class_id = -1;
-        b.out_kps[(size_t)f * b.cap + oi] = kp;
-    }
-}
 
 // ---------------------------------------------------------------------------------------
 // k_orb2: k_orb with both windows staged in LDS by wide loads: the 31x31 raw disc window
@@ -1579,7 +1248,6 @@ struct slam_extractor {
     hipStream_t side = nullptr;             // blur runs here, concurrent with FAST + octree
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     bool serial = false;
-    int rz_rows[kMaxLevels] = {};
     std::mutex mu;
     // geometry
     bool have_plan = false;
@@ -1726,25 +1394,6 @@ static slam_status ensure_plan(slam_extractor* ex, int W, int H) {
     ex->octree_lds = octree_lds_bytes(P.max_nodes, ex->key_lds_cap);
     SLAM_HIP_TRY(hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)ex->octree_lds));
-    {
-        const int rz_lds = kRzSrcRows * ((W + 15) & ~15) + (int)sizeof(ResizeX) * (W + 4) + (int)sizeof(ResizeY) * kRzRows;
-        if (rz_lds > 160 * 1024) return SLAM_EINVAL;
-        SLAM_HIP_TRY(hipFuncSetAttribute((const void*)k_resize2, hipFuncAttributeMaxDynamicSharedMemorySize, rz_lds));
-        // rows per block: the largest R <= kRzRows whose staged source rows fit kRzSrcRows
-        for (int l = 1; l < P.nlevels; l++) {
-            int R = kRzRows;
-            for (; R >= 1; R--) {
-                bool ok = true;
-                for (int dy0 = 0; dy0 < P.lv[l].h && ok; dy0 += R) {
-                    const int last = std::min(dy0 + R, P.lv[l].h) - 1;
-                    ok = P.ytab[P.lv[l].ytab_off + last].y1 - P.ytab[P.lv[l].ytab_off + dy0].y0 + 1 <= kRzSrcRows;
-                }
-                if (ok) break;
-            }
-            if (R < 1) return SLAM_EINVAL;
-            ex->rz_rows[l] = R;
-        }
-    }
     return SLAM_OK;
 }
 

@@ -150,7 +150,7 @@ def _level_tables(nfeatures=1000, scale_factor=1.2, nlevels=8):
 
 def lba_window(seed: int, n_kf: int = 50, n_pt: int = 2000, obs_per_pt: int = 8,
                stereo_frac: float = 0.0, outlier_frac: float = 0.02, arc_deg: float = 80.0,
-               radius: float = 3.0):
+               radius: float = 3.0, noise: float = 1.0):
     """A seeded local-BA window in the layout of slam_lba_problem.
 
     50 KeyFrames on a ``radius`` arc facing a 4 x 2 x 4 m box of points; every point is seen
@@ -201,12 +201,12 @@ def lba_window(seed: int, n_kf: int = 50, n_pt: int = 2000, obs_per_pt: int = 8,
             Xc = Rs[k] @ pts[p] + ts[k]
             lvl = rng.choice(len(p_level), p=p_level)
             s = float(scale[lvl])
-            u = cam["fx"] * Xc[0] / Xc[2] + cam["cx"] + rng.normal(0, s)
-            v = cam["fy"] * Xc[1] / Xc[2] + cam["cy"] + rng.normal(0, s)
+            u = cam["fx"] * Xc[0] / Xc[2] + cam["cx"] + noise * rng.normal(0, s)
+            v = cam["fy"] * Xc[1] / Xc[2] + cam["cy"] + noise * rng.normal(0, s)
             ur = -1.0
             stereo = rng.random() < stereo_frac
             if stereo:
-                ur = u - cam["bf"] / Xc[2] + rng.normal(0, s)
+                ur = u - cam["bf"] / Xc[2] + noise * rng.normal(0, s)
             if rng.random() < outlier_frac:
                 u = rng.uniform(0, cam["w"])
                 v = rng.uniform(0, cam["h"])

@@ -1,0 +1,98 @@
+"""The N>1 path of bench.py on CPU: two gloo ranks shard frames and BA windows exactly as the
+nccl ranks do on GPUs (slamhot/dist.py), run the CPU oracle on their shard, and combine with
+the same collectives (max time, summed units, gathered digests).  The combined result must
+equal a single-process run over all units."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+import oracle_bind as ob
+from slamhot import dist as sdist
+from slamhot import synth
+
+N_FRAMES, N_WIN = 5, 3
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _frame_digest(idx):
+    descs, count = [], 0
+    for i in idx:
+        img = synth.frame(700 + i, 320, 240)
+        kps, desc, _ = ob.extract(img)
+        descs.append(desc)
+        count += len(kps)
+    return count, sdist.digest(*descs) if descs else 0
+
+
+def _lba_digest(idx):
+    outs, iters = [], 0
+    for i in idx:
+        w = synth.lba_window(900 + i, n_kf=8, n_pt=60, obs_per_pt=3)
+        r = ob.lba_solve(w)
+        outs += [r["kf_Tcw"], r["pt_pos"], r["edge_outlier"]]
+        iters += r["iterations"][0] + r["iterations"][1]
+    return iters, sdist.digest(*outs) if outs else 0
+
+
+def _worker(rank, world, port, q):
+    import time
+
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    t0 = time.perf_counter()
+    fidx = sdist.shard(N_FRAMES, rank, world)
+    kcount, kdig = _frame_digest(fidx)
+    widx = sdist.shard(N_WIN, rank, world)
+    lit, ldig = _lba_digest(widx)
+    elapsed = time.perf_counter() - t0
+    el_max, units = sdist.reduce_run(dist, "cpu", elapsed, float(len(fidx)))
+    _, wunits = sdist.reduce_run(dist, "cpu", elapsed, float(len(widx)))
+    kg = sdist.gather_digests(dist, "cpu", world, kcount, kdig)
+    lg = sdist.gather_digests(dist, "cpu", world, lit, ldig)
+    q.put((rank, elapsed, el_max, units, wunits, kg, lg))
+    dist.destroy_process_group()
+
+
+def test_shard_partitions_units():
+    for n in (0, 1, 7, 64):
+        for world in (1, 2, 3, 8):
+            parts = [sdist.shard(n, r, world) for r in range(world)]
+            assert sorted(sum(parts, [])) == list(range(n))
+
+
+def test_two_rank_gloo_matches_single_process():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    out.sort()
+    elapsed = [o[1] for o in out]
+    for o in out:
+        assert o[2] == pytest.approx(max(elapsed))
+        assert o[3] == N_FRAMES and o[4] == N_WIN
+        assert o[5] == out[0][5] and o[6] == out[0][6]  # every rank sees the same gather
+    kg, lg = out[0][5], out[0][6]
+    kc, kd = _frame_digest(range(N_FRAMES))
+    assert sum(c for c, _ in kg) == kc
+    assert np.bitwise_xor.reduce(np.array([d for _, d in kg], np.int64)) == kd
+    li, ld = _lba_digest(range(N_WIN))
+    assert sum(c for c, _ in lg) == li
+    assert np.bitwise_xor.reduce(np.array([d for _, d in lg], np.int64)) == ld
