@@ -461,28 +461,36 @@ __global__ void __launch_bounds__(256) k_fast_wave(Bufs b, const int32_t* list, 
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 
     // pass A over the row-major linear index i = r*tw + c (all 64 lanes busy whatever tw);
-    // r = floor((i + 0.5) / tw) in float is exact here (i < 2^13, tw <= 64)
+    // r = floor((i + 0.5) / tw) in float is exact here (i < 2^13, tw <= 64).  Four chunks of
+    // 64 pixels per iteration: their LDS loads are all issued before any is consumed.
     int na = 0;
     {
         const int npx = tw * th;
         const float inv_tw = 1.0f / (float)tw;
-        for (int j = 0; j < npx; j += 64) {
-            const int i = j + lane;
-            bool pass = false;
-            int code = 0;
-            if (i < npx) {
-                const int r = (int)(((float)i + 0.5f) * inv_tw);
-                const int cc = i - r * tw;
-                code = r * 64 + cc;
+        for (int j = 0; j < npx; j += 256) {
+            bool pass[4];
+            int code[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int i = j + 64 * u + lane;
+                const bool in = i < npx;
+                const int ii = in ? i : 0;
+                const int r = (int)(((float)ii + 0.5f) * inv_tw);
+                const int cc = ii - r * tw;
+                code[u] = r * 64 + cc;
                 const uint8_t* c = roi + (r + 3) * kRoiStride + cc + 3;
                 const int v = c[0];
                 const int d0 = v - c[3 * kRoiStride], d8 = v - c[-3 * kRoiStride];
                 const int d4 = v - c[3], d12 = v - c[-3];
-                pass = (max(d0, d8) > tlow && max(d4, d12) > tlow) || (min(d0, d8) < -tlow && min(d4, d12) < -tlow);
+                pass[u] = in && ((max(d0, d8) > tlow && max(d4, d12) > tlow) ||
+                                 (min(d0, d8) < -tlow && min(d4, d12) < -tlow));
             }
-            const uint64_t m = __ballot(pass);
-            if (pass) lst[na + __popcll(m & lt)] = (uint16_t)code;
-            na += __popcll(m);
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint64_t m = __ballot(pass[u]);
+                if (pass[u]) lst[na + __popcll(m & lt)] = (uint16_t)code[u];
+                na += __popcll(m);
+            }
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
