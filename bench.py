@@ -77,6 +77,7 @@ def main():
     ap.add_argument("--cpu-frames", type=int, default=384)
     ap.add_argument("--lba-windows", type=int, default=64, help="LBA windows per GPU per call (0 = skip)")
     ap.add_argument("--lba-calls", type=int, default=3)
+    ap.add_argument("--match-pairs", type=int, default=128, help="(keyframe, frame) pairs per GPU per step (0 = skip)")
     args = ap.parse_args()
 
     import torch
@@ -209,6 +210,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args, W, H)
 
+    if args.match_pairs > 0:
+        result["match"] = match_leg(args, rank, world, local_rank, dist, device)
     if args.lba_windows > 0:
         result["lba"] = lba_leg(args, rank, world, local_rank, dist, device)
 
@@ -217,6 +220,101 @@ def main():
     ex.close()
     if dist:
         dist.destroy_process_group()
+
+
+def match_leg(args, rank, world, local_rank, dist, device):
+    """Extract + ComputeBoW + SearchByBoW(KF, Frame) frames/s (BASELINE.json configs[2] shape on
+    synthetic data: no EuRoC images here).  A step extracts 2P frames (P keyframes and P frames
+    that are shifted / rotated copies of them), builds every FeatureVector on the device and
+    matches the P pairs; everything stays in HBM."""
+    import torch
+
+    import slamhot
+    from slamhot import dist as sdist
+    from slamhot import synth
+    Pn, W, H = args.match_pairs, args.width, args.height
+    nuniq = min(16, Pn)
+    seeds = sdist.shard(nuniq * world, rank, world)
+    kfs = [synth.frame(20000 + s, W, H) for s in seeds]
+    rng = np.random.default_rng(rank)
+    pairs_img = []
+    for i in range(nuniq):
+        dx, dy, a = rng.uniform(-8, 8), rng.uniform(-6, 6), rng.uniform(-10, 10)
+        pairs_img.append((kfs[i], synth.shifted(kfs[i], dx, dy, a, 40000 + seeds[i])))
+    imgs = np.stack([im for i in range(Pn) for im in pairs_img[i % nuniq]])
+    F = len(imgs)
+    par, leaf, dn, wn = synth.vocab(10, 6, 0)
+    voc = slamhot.Vocabulary(par, leaf, dn, wn, k=10, L=6, device=local_rank)
+    m = slamhot.ORBmatcher(0.7, True, device=local_rank)
+    ex = slamhot.ORBextractor(nfeatures=args.nfeatures, device=local_rank, max_size=(W, H), max_batch=F)
+    cap = ex.cap
+    d_img = torch.from_numpy(imgs).to(device)
+    d_kps = torch.zeros((F, cap, 28), dtype=torch.uint8, device=device)
+    d_desc = torch.zeros((F, cap, 32), dtype=torch.uint8, device=device)
+    d_n = torch.zeros(F, dtype=torch.int32, device=device)
+    d_mono = torch.zeros(F, dtype=torch.int32, device=device)
+    pairs = [(2 * i, 2 * i + 1) for i in range(Pn)]
+    d_a2b = torch.zeros((Pn, cap), dtype=torch.int32, device=device)
+    d_b2a = torch.zeros((Pn, cap), dtype=torch.int32, device=device)
+    d_nm = torch.zeros(Pn, dtype=torch.int32, device=device)
+    stream = torch.cuda.current_stream(device).cuda_stream
+
+    def step():
+        ex.extract_batch_device(d_img.data_ptr(), F, W, H, d_kps.data_ptr(), d_desc.data_ptr(), cap,
+                                d_n.data_ptr(), d_mono.data_ptr(), stream=stream)
+        m.bow_match_batch_device(voc, F, d_kps.data_ptr(), d_desc.data_ptr(), cap, d_n.data_ptr(), pairs,
+                                 d_a2b.data_ptr(), d_b2a.data_ptr(), d_nm.data_ptr(), stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(device)
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(device)
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    skipped = m.bow_match_batch_status(stream)
+    nm = d_nm.cpu().numpy()
+    elapsed, frames_all = sdist.reduce_run(dist, device, elapsed, float(F * args.steps))
+    out = {
+        "metric": "ORB extract + ComputeBoW + SearchByBoW frames/s",
+        "value": round(frames_all / elapsed, 2),
+        "unit": "frames/s",
+        "dtype": "u8",
+        "config": {"workload": f"synthetic {W}x{H}, {args.nfeatures} feat/frame, {Pn} (keyframe, frame) pairs "
+                               f"per GPU per step, synthetic k=10 L=6 vocabulary, levelsup 4, nnratio 0.7, "
+                               f"checkOri (BASELINE.json configs[2] shape)",
+                   "parallelism": f"pair-sharded x{world}"},
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "matches_per_pair": round(float(nm.mean()), 1),
+        "skipped_pairs": skipped,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, str(ROOT / "tests"))
+        import oracle_bind as ob
+        p = ob.params(nfeatures=args.nfeatures)
+        t0 = time.perf_counter()
+        done = 0
+        while done < min(8, nuniq) and time.perf_counter() - t0 < 10.0:
+            sides = []
+            for im in pairs_img[done]:
+                k, d, _ = ob.extract(im, p)
+                _, wt, nid = ob.vocab_transform(par, leaf, dn, wn, 6, d, 4)
+                sides.append((d, k["angle"], None) + synth.feature_vector(nid, wt))
+            ob.search_by_bow(sides[0], sides[1], 0.7, True, False)
+            done += 1
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(2 * done / dt, 2), "unit": "frames/s", "cores": 1, "kind": "port",
+                               "sample": f"{done} pairs ({2 * done} frames) one at a time on one core: oracle "
+                                         f"extract + vocabulary transform + FeatureVector + SearchByBoW"}
+    ex.close()
+    m.close()
+    voc.close()
+    return out
 
 
 def sdist_shard_seeds(rank, world, n):

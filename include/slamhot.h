@@ -236,6 +236,23 @@ slam_status slamhot_search_by_projection_last(slam_matcher* m, const slam_frame_
                                               const slam_last_frame* LF, float nnratio, int check_ori,
                                               float th, int mono, int32_t* f_match, int* nmatches);
 
+/* Batched, device-resident Frame::ComputeBoW + SearchByBoW(KeyFrame*, Frame&) (ORBmatcher.cc:
+ * 269-471; strict = 1 gives the KF-KF acceptance of :823-963) over frame pairs, for
+ * extraction output left in HBM by slamhot_extract_batch_device: d_kps (nframes x cap
+ * slam_keypoint), d_desc (nframes x cap x 32), d_n (nframes int32).  Every frame's
+ * FeatureVector at level L-levelsup is built on the device (TemplatedVocabulary.h:1139-1206,
+ * FeatureVector.cpp:31-45).  pairs (host, 2 x npairs): (keyframe index, frame index).
+ * d_valid (nframes x cap u8, may be NULL = all valid) marks keyframe features with a usable
+ * MapPoint.  Outputs (device, cap per pair): d_a2b, d_b2a (-1 = none), d_nmatches (npairs).
+ * Asynchronous on hip_stream (NULL = the matcher's stream); slamhot_bow_match_batch_status
+ * synchronises and reports pairs the kernel could not hold (skipped, outputs undefined). */
+slam_status slamhot_bow_match_batch_device(slam_matcher* m, slam_vocab* v, int nframes, const void* d_kps,
+                                           const void* d_desc, int cap, const void* d_n, const void* d_valid,
+                                           int npairs, const int32_t* pairs, float nnratio, int check_ori,
+                                           int strict, int levelsup, void* d_a2b, void* d_b2a,
+                                           void* d_nmatches, void* hip_stream);
+slam_status slamhot_bow_match_batch_status(slam_matcher* m, void* hip_stream, int* skipped_pairs);
+
 /* Per KeyFrame feature for SearchByProjection(Frame&, KeyFrame*, const set<MapPoint*>&
  * sAlreadyFound, float th, int ORBdist) (ORBmatcher.cc:2391-2513). */
 typedef struct slam_kf_points {

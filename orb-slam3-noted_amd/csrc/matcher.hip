@@ -278,6 +278,126 @@ using namespace slamhot;
 
 namespace {
 
+// ---------------------------------------------------------------------------------------
+// Batched device path: Frame::ComputeBoW's FeatureVector per frame, then SearchByBoW per
+// (KeyFrame, Frame) pair, without leaving HBM.
+// k_featvec: one 1024-thread workgroup per frame.  FeatureVector::addFeature
+// (FeatureVector.cpp:31-45) appends feature i to the entry of its level-(L-levelsup) node,
+// features whose word weight is <= 0 are skipped (TemplatedVocabulary.h:1169), std::map
+// keeps nodes ascending: a bitonic sort of (node << 16 | i) gives exactly that CSR.
+// ---------------------------------------------------------------------------------------
+constexpr int kFvMax = 4096;
+
+__global__ void __launch_bounds__(1024) k_featvec(int cap, const int32_t* __restrict__ n_per_frame,
+                                                  const int32_t* __restrict__ node, const double* __restrict__ weight,
+                                                  uint32_t* __restrict__ fv_id, int32_t* __restrict__ fv_off,
+                                                  uint32_t* __restrict__ fv_feat, int32_t* __restrict__ fv_n) {
+    __shared__ uint64_t keys[kFvMax];
+    __shared__ int wsum[16], vsum[16];
+    const int f = blockIdx.x, tid = threadIdx.x;
+    const int n = min(n_per_frame[f], min(cap, kFvMax));
+    int P = 1;
+    while (P < n) P <<= 1;
+    const size_t base = (size_t)f * cap;
+    for (int i = tid; i < P; i += blockDim.x)
+        keys[i] = (i < n && weight[base + i] > 0) ? (((uint64_t)(uint32_t)node[base + i] << 16) | (uint64_t)i)
+                                                   : ~0ull;
+    __syncthreads();
+    for (int k = 2; k <= P; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = tid; i < P; i += blockDim.x) {
+                const int x = i ^ j;
+                if (x > i) {
+                    const uint64_t a = keys[i], b = keys[x];
+                    const bool up = (i & k) == 0;
+                    if ((a > b) == up) {
+                        keys[i] = b;
+                        keys[x] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    // node boundaries -> CSR (chunks of blockDim.x, block-wide scan of the head flags)
+    int carry = 0, nvalid = 0;
+    for (int c0 = 0; c0 < P; c0 += blockDim.x) {
+        const int i = c0 + tid;
+        const uint64_t k = i < P ? keys[i] : ~0ull;
+        const bool valid = k != ~0ull;
+        const bool head = valid && (i == 0 || (keys[i - 1] >> 16) != (k >> 16));
+        const uint64_t bal = __ballot(head);
+        const int lane = tid & 63, wid = tid >> 6;
+        const int before = __popcll(bal & (lane ? (~0ull >> (64 - lane)) : 0ull));
+        const uint64_t vbal = __ballot(valid);
+        if (lane == 0) {
+            wsum[wid] = __popcll(bal);
+            vsum[wid] = __popcll(vbal);
+        }
+        __syncthreads();
+        int woff = 0, tot = 0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); w++) {
+            if (w < wid) woff += wsum[w];
+            tot += wsum[w];
+            nvalid += vsum[w];
+        }
+        if (valid) fv_feat[base + i] = (uint32_t)(k & 0xffff);
+        if (head) {
+            const int idx = carry + woff + before;
+            fv_id[base + idx] = (uint32_t)(k >> 16);
+            fv_off[(size_t)f * (cap + 1) + idx] = i;
+        }
+        carry += tot;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        fv_n[f] = carry;
+        fv_off[(size_t)f * (cap + 1) + carry] = nvalid;
+    }
+}
+
+// Pair table for k_bow_match from per-frame counts (device side).  Pairs the kernel cannot
+// hold (side > kBowCap features, > 4096 nodes, or a Frame node over 4 x 64 candidates) are
+// skipped and counted in *status.
+__global__ void k_make_pairs(int npairs, const int2* __restrict__ pairs, int cap, const uint8_t* __restrict__ kps,
+                             const uint8_t* __restrict__ desc, const int32_t* __restrict__ n_per_frame,
+                             const uint8_t* __restrict__ valid, const uint32_t* __restrict__ fv_id,
+                             const int32_t* __restrict__ fv_off, const uint32_t* __restrict__ fv_feat,
+                             const int32_t* __restrict__ fv_n, int32_t* __restrict__ a2b, int32_t* __restrict__ b2a,
+                             int32_t* __restrict__ nmatch, DevBowPair* __restrict__ out, int* __restrict__ status) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npairs) return;
+    const int2 ab = pairs[p];
+    auto side = [&](int f, bool use_valid) {
+        DevBowSide S;
+        S.desc = desc + (size_t)f * cap * 32;
+        S.angle = reinterpret_cast<const float*>(kps + (size_t)f * cap * sizeof(slam_keypoint)) + 3;
+        S.angle_stride = (int)(sizeof(slam_keypoint) / 4);
+        S.valid = (use_valid && valid) ? valid + (size_t)f * cap : nullptr;
+        S.n = min(n_per_frame[f], cap);
+        S.n_nodes = fv_n[f];
+        S.node_id = fv_id + (size_t)f * cap;
+        S.node_off = fv_off + (size_t)f * (cap + 1);
+        S.node_feat = fv_feat + (size_t)f * cap;
+        return S;
+    };
+    DevBowPair pr;
+    pr.A = side(ab.x, true);
+    pr.B = side(ab.y, false);
+    pr.a2b = a2b + (size_t)p * cap;
+    pr.b2a = b2a + (size_t)p * cap;
+    pr.nmatches = nmatch + p;
+    bool ok = pr.A.n <= kBowCap && pr.B.n <= kBowCap && pr.A.n_nodes <= 4096 && pr.B.n_nodes <= 4096;
+    for (int i = 0; ok && i < pr.B.n_nodes; i++)
+        if (pr.B.node_off[i + 1] - pr.B.node_off[i] > 64 * kBowNodeChunks) ok = false;
+    if (!ok) {
+        atomicAdd(status, 1);
+        pr.A.n = 0;
+        pr.A.n_nodes = 0;
+        pr.B.n_nodes = 0;
+    }
+    out[p] = pr;
+}
+
 struct Buf {
     void* p = nullptr;
     size_t bytes = 0;
@@ -332,6 +452,8 @@ struct slam_matcher {
     int device = 0;
     hipStream_t stream = nullptr;
     Buf d_pair, d_a, d_b, d_out;
+    // batched device path (slamhot_bow_match_batch_device)
+    Buf b_word, b_weight, b_node, b_fv_id, b_fv_off, b_fv_feat, b_fv_n, b_pairs, b_devpairs, b_status;
     std::mutex mu;
 };
 
@@ -503,6 +625,9 @@ void slamhot_matcher_destroy(slam_matcher* m) {
     m->d_a.release();
     m->d_b.release();
     m->d_out.release();
+    for (Buf* b : {&m->b_word, &m->b_weight, &m->b_node, &m->b_fv_id, &m->b_fv_off, &m->b_fv_feat, &m->b_fv_n,
+                   &m->b_pairs, &m->b_devpairs, &m->b_status})
+        b->release();
     if (m->stream) (void)hipStreamDestroy(m->stream);
     delete m;
 }
@@ -596,6 +721,64 @@ extern "C" slam_status slamhot_search_by_bow(slam_matcher* m, const slam_bow_sid
     std::copy(out.begin(), out.begin() + A->n, a2b);
     std::copy(out.begin() + A->n, out.begin() + A->n + B->n, b2a);
     *nmatches = out[(size_t)A->n + B->n];
+    return SLAM_OK;
+}
+
+extern "C" slam_status slamhot_bow_match_batch_device(slam_matcher* m, slam_vocab* v, int nframes, const void* d_kps,
+                                                      const void* d_desc, int cap, const void* d_n,
+                                                      const void* d_valid, int npairs, const int32_t* pairs,
+                                                      float nnratio, int check_ori, int strict, int levelsup,
+                                                      void* d_a2b, void* d_b2a, void* d_nmatches, void* hip_stream) {
+    if (!m || !v || nframes < 0 || npairs < 0 || cap <= 0 || cap > kFvMax || (nframes && (!d_kps || !d_desc || !d_n)) ||
+        (npairs && (!pairs || !d_a2b || !d_b2a || !d_nmatches)) || m->device != v->device)
+        return SLAM_EINVAL;
+    for (int i = 0; i < 2 * npairs; i++)
+        if (pairs[i] < 0 || pairs[i] >= nframes) return SLAM_EINVAL;
+    std::lock_guard<std::mutex> g(m->mu);
+    SLAM_HIP_TRY(hipSetDevice(m->device));
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : m->stream;
+    const size_t nf = (size_t)nframes * cap;
+    slam_status st;
+    if ((st = m->b_word.ensure(nf * 4)) || (st = m->b_weight.ensure(nf * 8)) || (st = m->b_node.ensure(nf * 4)) ||
+        (st = m->b_fv_id.ensure(nf * 4)) || (st = m->b_fv_off.ensure((size_t)nframes * (cap + 1) * 4)) ||
+        (st = m->b_fv_feat.ensure(nf * 4)) || (st = m->b_fv_n.ensure((size_t)nframes * 4 + 4)) ||
+        (st = m->b_pairs.ensure((size_t)npairs * 8 + 8)) || (st = m->b_devpairs.ensure((size_t)npairs * sizeof(DevBowPair) + 8)) ||
+        (st = m->b_status.ensure(4)))
+        return st;
+    if (nframes == 0) return SLAM_OK;
+    // Frame::ComputeBoW (Frame.cc:721-728): transform every descriptor slot of every frame
+    if ((st = slamhot_vocab_transform_device(v, (int)nf, d_desc, 32, levelsup, m->b_word.p, m->b_weight.p,
+                                             m->b_node.p, s)))
+        return st;
+    hipLaunchKernelGGL(k_featvec, dim3(nframes), dim3(1024), 0, s, cap, (const int32_t*)d_n,
+                       m->b_node.as<int32_t>(), m->b_weight.as<double>(), m->b_fv_id.as<uint32_t>(),
+                       m->b_fv_off.as<int32_t>(), m->b_fv_feat.as<uint32_t>(), m->b_fv_n.as<int32_t>());
+    SLAM_HIP_TRY(hipGetLastError());
+    if (npairs == 0) return SLAM_OK;
+    SLAM_HIP_TRY(hipMemcpyAsync(m->b_pairs.p, pairs, (size_t)npairs * 8, hipMemcpyHostToDevice, s));
+    SLAM_HIP_TRY(hipMemsetAsync(m->b_status.p, 0, 4, s));
+    hipLaunchKernelGGL(k_make_pairs, dim3((npairs + 127) / 128), dim3(128), 0, s, npairs, m->b_pairs.as<int2>(), cap,
+                       (const uint8_t*)d_kps, (const uint8_t*)d_desc, (const int32_t*)d_n, (const uint8_t*)d_valid,
+                       m->b_fv_id.as<uint32_t>(), m->b_fv_off.as<int32_t>(), m->b_fv_feat.as<uint32_t>(),
+                       m->b_fv_n.as<int32_t>(), (int32_t*)d_a2b, (int32_t*)d_b2a, (int32_t*)d_nmatches,
+                       m->b_devpairs.as<DevBowPair>(), m->b_status.as<int>());
+    hipLaunchKernelGGL(k_bow_match, dim3(npairs), dim3(256), 0, s, m->b_devpairs.as<DevBowPair>(), nnratio,
+                       check_ori, strict);
+    SLAM_HIP_TRY(hipGetLastError());
+    return SLAM_OK;
+}
+
+extern "C" slam_status slamhot_bow_match_batch_status(slam_matcher* m, void* hip_stream, int* skipped_pairs) {
+    if (!m || !skipped_pairs) return SLAM_EINVAL;
+    std::lock_guard<std::mutex> g(m->mu);
+    SLAM_HIP_TRY(hipSetDevice(m->device));
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : m->stream;
+    int v = 0;
+    if (m->b_status.p) {
+        SLAM_HIP_TRY(hipMemcpyAsync(&v, m->b_status.p, 4, hipMemcpyDeviceToHost, s));
+        SLAM_HIP_TRY(hipStreamSynchronize(s));
+    }
+    *skipped_pairs = v;
     return SLAM_OK;
 }
 

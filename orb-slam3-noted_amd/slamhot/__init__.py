@@ -430,6 +430,30 @@ def _matcher_methods():
                                                     C.byref(nm)), "search_by_projection_kf")
         return nm.value, fm
 
+    def bow_match_batch_device(self, vocab, nframes, d_kps, d_desc, cap, d_n, pairs, d_a2b, d_b2a, d_nmatches,
+                               d_valid=None, levelsup=4, strict=False, stream=None):
+        """Device-resident Frame::ComputeBoW + SearchByBoW over (keyframe, frame) index pairs
+        (slamhot_bow_match_batch_device); asynchronous on `stream`."""
+        L = lib()
+        if not getattr(L, "_bowb_ready", False):
+            L.slamhot_bow_match_batch_device.argtypes = [P, P, I, P, P, I, P, P, I, P, C.c_float, I, I, I, P, P, P, P]
+            L.slamhot_bow_match_batch_status.argtypes = [P, P, C.POINTER(I)]
+            L._bowb_ready = True
+        pr = np.ascontiguousarray(np.asarray(pairs, np.int32).reshape(-1, 2))
+        check(L.slamhot_bow_match_batch_device(self._h, vocab._h, nframes, P(d_kps), P(d_desc), cap, P(d_n),
+                                               P(d_valid) if d_valid else None, len(pr), _ptr(pr), self.mfNNratio,
+                                               int(self.mbCheckOrientation), int(strict), levelsup, P(d_a2b),
+                                               P(d_b2a), P(d_nmatches), P(stream) if stream else None),
+              "bow_match_batch_device")
+
+    def bow_match_batch_status(self, stream=None) -> int:
+        sk = I(0)
+        check(lib().slamhot_bow_match_batch_status(self._h, P(stream) if stream else None, C.byref(sk)),
+              "bow_match_batch_status")
+        return sk.value
+
+    ORBmatcher.bow_match_batch_device = bow_match_batch_device
+    ORBmatcher.bow_match_batch_status = bow_match_batch_status
     ORBmatcher.SearchByProjection_local = SearchByProjection_local
     ORBmatcher.SearchByProjection_last = SearchByProjection_last
     ORBmatcher.SearchByProjection_kf = SearchByProjection_kf

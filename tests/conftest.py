@@ -11,6 +11,16 @@ for p in (ROOT / "orb-slam3-noted_amd", ROOT / "tests", ROOT):
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a gfx950 (MI355X) device")
+    # torch's HIP runtime must come up before libslamhot's first device call in this process
+    # (the device-resident tests hand torch allocations to the library)
+    markexpr = getattr(config.option, "markexpr", "") or ""
+    if "not gpu" not in markexpr:
+        try:
+            import torch
+            if torch.cuda.is_available():
+                torch.cuda.init()
+        except Exception:
+            pass
 
 
 @pytest.fixture(scope="session")

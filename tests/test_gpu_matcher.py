@@ -101,3 +101,59 @@ def test_search_by_bow_duplicates_and_ties(gpu_vocab):
     no, _, b2a_o = ob.search_by_bow(A, B, 1.0, True, False)
     assert ng == no and np.array_equal(b2a_g, b2a_o)
     m.close()
+
+
+def test_bow_match_batch_device(gpu_vocab, vocab_arrays):
+    """Device-resident extract -> ComputeBoW -> SearchByBoW over frame pairs equals the
+    host path (oracle transform, FeatureVector, oracle SearchByBoW) on the same keypoints."""
+    import torch
+
+    import slamhot
+    par, leaf, dn, wn = vocab_arrays
+    img0 = synth.frame(11, 640, 480)
+    imgs = np.stack([img0] + [synth.shifted(img0, dx, dy, a, 30 + i)
+                              for i, (dx, dy, a) in enumerate([(3, 2, 2.0), (-5, 4, -6.0), (7, -2, 11.0)])])
+    F, H, W = imgs.shape
+    dev = torch.device("cuda", 0)
+    ex = slamhot.ORBextractor(nfeatures=1000, max_size=(W, H), max_batch=F)
+    cap = ex.cap
+    d_img = torch.from_numpy(imgs).to(dev)
+    d_kps = torch.zeros((F, cap, 28), dtype=torch.uint8, device=dev)
+    d_desc = torch.zeros((F, cap, 32), dtype=torch.uint8, device=dev)
+    d_n = torch.zeros(F, dtype=torch.int32, device=dev)
+    d_mono = torch.zeros(F, dtype=torch.int32, device=dev)
+    pairs = [(0, 1), (0, 2), (0, 3), (1, 2), (3, 1)]
+    d_a2b = torch.zeros((len(pairs), cap), dtype=torch.int32, device=dev)
+    d_b2a = torch.zeros((len(pairs), cap), dtype=torch.int32, device=dev)
+    d_nm = torch.zeros(len(pairs), dtype=torch.int32, device=dev)
+    rng = np.random.default_rng(3)
+    valid = (rng.random((F, cap)) < 0.9).astype(np.uint8)
+    d_valid = torch.from_numpy(valid).to(dev)
+    m = slamhot.ORBmatcher(0.75, True)
+    torch.cuda.synchronize()
+    ex.extract_batch_device(d_img.data_ptr(), F, W, H, d_kps.data_ptr(), d_desc.data_ptr(), cap, d_n.data_ptr(),
+                            d_mono.data_ptr())
+    torch.cuda.synchronize()
+    m.bow_match_batch_device(gpu_vocab, F, d_kps.data_ptr(), d_desc.data_ptr(), cap, d_n.data_ptr(), pairs,
+                             d_a2b.data_ptr(), d_b2a.data_ptr(), d_nm.data_ptr(), d_valid=d_valid.data_ptr())
+    assert m.bow_match_batch_status() == 0
+    n = d_n.cpu().numpy()
+    kps = d_kps.cpu().numpy().view(ob.KP_DTYPE)
+    desc = d_desc.cpu().numpy()
+    a2b, b2a, nm = d_a2b.cpu().numpy(), d_b2a.cpu().numpy(), d_nm.cpu().numpy()
+    total = 0
+    for p, (a, b) in enumerate(pairs):
+        ka, da = kps[a, : n[a]].ravel(), desc[a, : n[a]]
+        kb, db = kps[b, : n[b]].ravel(), desc[b, : n[b]]
+        _, wta, nia = ob.vocab_transform(par, leaf, dn, wn, 6, da, 4)
+        _, wtb, nib = ob.vocab_transform(par, leaf, dn, wn, 6, db, 4)
+        A = (da, ka["angle"], valid[a, : n[a]]) + synth.feature_vector(nia, wta)
+        B = (db, kb["angle"], None) + synth.feature_vector(nib, wtb)
+        no, a2b_o, b2a_o = ob.search_by_bow(A, B, 0.75, True, False)
+        assert nm[p] == no
+        assert np.array_equal(a2b[p, : n[a]], a2b_o)
+        assert np.array_equal(b2a[p, : n[b]], b2a_o)
+        total += no
+    assert total > 100
+    m.close()
+    ex.close()
