@@ -12,7 +12,7 @@
 //   k_lin_poses      wave / pose    : Hpp (6x6) and b_p over the pose's edges
 //   k_iter_begin     block / window : chi2 = sum rho, lambda init (iteration 0)
 // per LM trial:
-//   k_schur_point    thread / point : Dinv = (Hll + lambda I)^-1, B_e Dinv, B_e Dinv b_l
+//   k_schur_edges    thread / edge  : Dinv = (Hll + lambda I)^-1, B_e Dinv, B_e Dinv b_l
 //   k_schur_block    wave / 6x6 block of the Schur complement (lower triangle + rhs row)
 //   k_ldlt           block / window : dense LDL^T of the (n+1) x (n+1) augmented system
 //   k_backsub        thread / point : x_l = Dinv (b_l - Hpl^T x_p), trial point
@@ -38,7 +38,7 @@ constexpr int kNB = 32;           // LDL^T panel width
 constexpr int kMaxN = 480;        // 80 free KeyFrames per window
 constexpr int kHplStride = 18;    // doubles per edge: pose-landmark block Hpl = B^T W A (6 x 3)
 constexpr int kTrStride = 24;     // doubles per edge of Schur trial output: B Dinv (18), B db (6)
-constexpr int kCtlThreads = 256;
+constexpr int kCtlThreads = 1024;
 typedef double double4_t __attribute__((ext_vector_type(4)));
 
 // dense Schur system geometry: pose dimension padded to a multiple of kNB, rhs in row npad
@@ -410,29 +410,46 @@ __global__ void __launch_bounds__(256) k_lin_poses(int npose_total, const int* _
         bp[8 * (long long)pose + (lane - 21)] = mine;
 }
 
-// deterministic block sum / max (fixed tree over kCtlThreads lanes)
+// deterministic block sum / max: wave butterflies, then the wave partials in wave order
+__device__ inline double wave_max(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
 __device__ inline double block_sum(double v, double* sh) {
-    sh[threadIdx.x] = v;
+    v = wave_sum(v);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
     __syncthreads();
-    for (int s = kCtlThreads / 2; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) sh[threadIdx.x] += sh[threadIdx.x + s];
-        __syncthreads();
-    }
-    const double r = sh[0];
+    double r = 0.0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); w++) r += sh[w];
     __syncthreads();
     return r;
 }
 
 __device__ inline double block_max(double v, double* sh) {
-    sh[threadIdx.x] = v;
+    v = wave_max(v);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
     __syncthreads();
-    for (int s = kCtlThreads / 2; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) sh[threadIdx.x] = fmax(sh[threadIdx.x], sh[threadIdx.x + s]);
-        __syncthreads();
-    }
-    const double r = sh[0];
+    double r = 0.0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); w++) r = fmax(r, sh[w]);
     __syncthreads();
     return r;
+}
+
+// strided per-thread partial sum with four independent accumulators (loads in flight)
+__device__ inline double strided_sum(const double* __restrict__ p, int n) {
+    const int T = blockDim.x;
+    double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    int i = threadIdx.x;
+    for (; i + 3 * T < n; i += 4 * T) {
+        a0 += p[i];
+        a1 += p[i + T];
+        a2 += p[i + 2 * T];
+        a3 += p[i + 3 * T];
+    }
+    for (; i < n; i += T) a0 += p[i];
+    return (a0 + a1) + (a2 + a3);
 }
 
 // OptimizationAlgorithmLevenberg::solve prologue (optimization_algorithm_levenberg.cpp:61-104)
@@ -441,13 +458,11 @@ __global__ void __launch_bounds__(kCtlThreads) k_iter_begin(const WinDesc* __res
                                                             const double* __restrict__ rho,
                                                             const double* __restrict__ Hpp,
                                                             const double* __restrict__ Hll) {
-    __shared__ double sh[kCtlThreads];
+    __shared__ double sh[kCtlThreads / 64];
     const WinDesc W = wins[blockIdx.x];
     WinCtl& C = ctl[blockIdx.x];
     if (!C.active) return;
-    double s = 0;
-    for (int i = threadIdx.x; i < W.ne; i += kCtlThreads) s += rho[W.e0 + i];
-    const double chi = block_sum(s, sh);
+    const double chi = block_sum(strided_sum(rho + W.e0, W.ne), sh);
     double m = 0;
     if (C.it == 0) {
         for (int i = threadIdx.x; i < W.np; i += kCtlThreads)
@@ -492,39 +507,49 @@ __device__ inline void inverse3(const double* m, double* out) {
 #undef M_
 }
 
-// Schur per landmark (block_solver.hpp:381-432): Dinv, db, then B Dinv and B db per edge.
-__global__ void k_schur_point(int npt_total, const int* __restrict__ spe_off, const int* __restrict__ spe,
-                              const int* __restrict__ pt_win, const WinCtl* __restrict__ ctl,
-                              const double* __restrict__ Hll, const double* __restrict__ bl,
-                              const double* __restrict__ lin, double* __restrict__ Dinv_out,
-                              double* __restrict__ tr) {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= npt_total) return;
-    const WinCtl& C = ctl[pt_win[p]];
-    if (!C.need_trial) return;
-    const double lam = C.lambda;
-    const double* h = Hll + 8 * (long long)p;
+__device__ inline void point_dinv(const double* __restrict__ Hll, long long p, double lam, double* Di) {
+    const double* h = Hll + 8 * p;
     const double D[9] = {h[0] + lam, h[1], h[2], h[1], h[3] + lam, h[4], h[2], h[4], h[5] + lam};
-    double Di[9];
     inverse3(D, Di);
-#pragma unroll
-    for (int k = 0; k < 9; k++) Dinv_out[12 * (long long)p + k] = Di[k];
-    const double* b = bl + 4 * (long long)p;
+}
+
+// Schur per landmark (block_solver.hpp:381-432), one thread per (landmark, free-pose edge):
+// Dinv = (Hll + lambda I)^-1 of the edge's point (Eigen cofactor inverse, recomputed per edge),
+// db = Dinv b_l, then B Dinv and B db for the edge.
+__global__ void k_schur_edges(int nspe_total, const int* __restrict__ spe, const EdgeS* __restrict__ E,
+                              const WinCtl* __restrict__ ctl, const double* __restrict__ Hll,
+                              const double* __restrict__ bl, const double* __restrict__ lin,
+                              double* __restrict__ tr) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nspe_total) return;
+    const int e = spe[i];
+    const EdgeS ed = E[e];
+    const WinCtl& C = ctl[ed.win];
+    if (!C.need_trial) return;
+    double Di[9];
+    point_dinv(Hll, ed.pt, C.lambda, Di);
+    const double* b = bl + 4 * (long long)ed.pt;
     double db[3];
 #pragma unroll
     for (int r = 0; r < 3; r++) db[r] = Di[3 * r] * b[0] + Di[3 * r + 1] * b[1] + Di[3 * r + 2] * b[2];
-    for (int i = spe_off[p]; i < spe_off[p + 1]; i++) {
-        const int e = spe[i];
-        const double* H = lin + (long long)kHplStride * e;
-        double* T = tr + (long long)kTrStride * e;
+    const double* H = lin + (long long)kHplStride * e;
+    double* T = tr + (long long)kTrStride * e;
 #pragma unroll
-        for (int r = 0; r < 6; r++) {
-            const double h0 = H[3 * r], h1 = H[3 * r + 1], h2 = H[3 * r + 2];
+    for (int r = 0; r < 6; r++) {
+        const double h0 = H[3 * r], h1 = H[3 * r + 1], h2 = H[3 * r + 2];
 #pragma unroll
-            for (int c = 0; c < 3; c++) T[3 * r + c] = h0 * Di[c] + h1 * Di[3 + c] + h2 * Di[6 + c];
-            T[18 + r] = h0 * db[0] + h1 * db[1] + h2 * db[2];
-        }
+        for (int c = 0; c < 3; c++) T[3 * r + c] = h0 * Di[c] + h1 * Di[3 + c] + h2 * Di[6 + c];
+        T[18 + r] = h0 * db[0] + h1 * db[1] + h2 * db[2];
     }
+}
+
+// value of lane j (compile-time) within each 32-lane half: ds_swizzle bit mode, and_mask 0,
+// or_mask j (no LDS memory traffic, no SGPR round trip)
+template <int J>
+__device__ inline double bcast32_t(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_ds_swizzle((int)b, J << 5), hi = __builtin_amdgcn_ds_swizzle((int)(b >> 32), J << 5);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
 __device__ inline double readlane_d(double v, int l) {
@@ -644,6 +669,29 @@ __device__ unsigned long long g_ldlt_phase[8];
 
 
 
+// One pivot step of the diagonal-block LDL^T (lane = row, full symmetric rows in registers):
+// pivot row J broadcast by ds_swizzle, rows below eliminate with it.
+template <int J>
+__device__ __forceinline__ void diag_step(double (&row)[kNB], int lane, bool& bad, double* dsh, double* dinv) {
+    double rb[kNB];
+#pragma unroll
+    for (int c = J; c < kNB; c++) rb[c] = bcast32_t<J>(row[c]);
+    const double dj = rb[J];
+    if (dj == 0.0) bad = true;
+    const int rl = lane & (kNB - 1);
+    if (rl > J) {
+        const double lj = row[J] / dj;
+#pragma unroll
+        for (int c = J + 1; c < kNB; c++) row[c] = __builtin_fma(-lj, rb[c], row[c]);
+        row[J] = lj;
+    }
+    if (lane == J) {
+        dsh[J] = dj;
+        dinv[J] = 1.0 / dj;
+    }
+    if constexpr (J + 1 < kNB) diag_step<J + 1>(row, lane, bad, dsh, dinv);
+}
+
 __global__ void __launch_bounds__(512) k_ldlt(const WinDesc* __restrict__ wins, WinCtl* __restrict__ ctl,
                                                double* __restrict__ Hs, double* __restrict__ xp_out) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -671,31 +719,15 @@ __global__ void __launch_bounds__(512) k_ldlt(const WinDesc* __restrict__ wins, 
             if (c <= r) T[r * (kNB + 1) + c] = A[(long long)(kb + r) * ld + kb + c];
         }
         __syncthreads();
+        PHASE_MARK(5);
         if (wid == 0) {
             double row[kNB];
             const int rl = lane & (kNB - 1);
 #pragma unroll
             for (int c = 0; c < kNB; c++) row[c] = c <= rl ? T[rl * (kNB + 1) + c] : T[c * (kNB + 1) + rl];
             bool bad = false;
-#pragma unroll
-            for (int j = 0; j < kNB; j++) {
-                // pivot row j broadcast from lane j through scalar registers
-                double rb[kNB];
-#pragma unroll
-                for (int c = j; c < kNB; c++) rb[c] = readlane_d(row[c], j);
-                const double dj = rb[j];
-                if (dj == 0.0) bad = true;
-                if (lane > j && lane < kNB) {
-                    const double lj = row[j] / dj;
-#pragma unroll
-                    for (int c = j + 1; c < kNB; c++) row[c] -= lj * rb[c];
-                    row[j] = lj;
-                }
-                if (lane == j) {
-                    dsh[j] = dj;
-                    dinv[j] = 1.0 / dj;
-                }
-            }
+            diag_step<0>(row, lane, bad, dsh, dinv);
+            PHASE_MARK(6);
             if (bad && lane == 0) fail = 1;
             if (lane < kNB) {
 #pragma unroll
@@ -723,7 +755,7 @@ __global__ void __launch_bounds__(512) k_ldlt(const WinDesc* __restrict__ wins, 
             for (int j = 0; j < kNB; j++) {
                 a[j] = a[j] * dinv[j];
 #pragma unroll
-                for (int q = j + 1; q < kNB; q++) a[q] -= a[j] * WL[q * kNB + j];
+                for (int q = j + 1; q < kNB; q++) a[q] = __builtin_fma(-a[j], WL[q * kNB + j], a[q]);
             }
 #pragma unroll
             for (int j = 0; j < kNB; j += 2) *(double2*)(Ar + j) = double2{a[j], a[j + 1]};
@@ -809,7 +841,7 @@ __global__ void __launch_bounds__(512) k_ldlt(const WinDesc* __restrict__ wins, 
 #pragma unroll
             for (int k = kNB - 1; k >= 0; k--) {
                 const double xk = readlane_d(zi, k);
-                if (lane < k) zi -= lc[k] * xk;
+                if (lane < k) zi = __builtin_fma(-lc[k], xk, zi);
             }
             if (lane < kNB) z[kb + lane] = zi;
         }
@@ -817,7 +849,7 @@ __global__ void __launch_bounds__(512) k_ldlt(const WinDesc* __restrict__ wins, 
         for (int i = tid; i < kb; i += blockDim.x) {
             double sacc = z[i];
 #pragma unroll 8
-            for (int k = 0; k < kNB; k++) sacc -= A[(long long)(kb + k) * ld + i] * z[kb + k];
+            for (int k = 0; k < kNB; k++) sacc = __builtin_fma(-A[(long long)(kb + k) * ld + i], z[kb + k], sacc);
             z[i] = sacc;
         }
         __syncthreads();
@@ -843,7 +875,7 @@ __global__ void k_ldlt_pad(const WinDesc* __restrict__ wins, double* __restrict_
 __global__ void k_backsub(int npt_total, const int* __restrict__ spe_off, const int* __restrict__ spe,
                           const EdgeS* __restrict__ E, const int* __restrict__ pt_win,
                           const WinCtl* __restrict__ ctl, const double* __restrict__ bl,
-                          const double* __restrict__ Dinv, const double* __restrict__ lin,
+                          const double* __restrict__ Hll, const double* __restrict__ lin,
                           const double* __restrict__ xp, double* __restrict__ xl, double* __restrict__ pts,
                           long long pt_stride) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -862,7 +894,8 @@ __global__ void k_backsub(int npt_total, const int* __restrict__ spe_off, const 
 #pragma unroll
                 for (int r = 0; r < 6; r++) cl[c] += H[3 * r + c] * (-xpp[r]);
         }
-        const double* Di = Dinv + 12 * (long long)p;
+        double Di[9];
+        point_dinv(Hll, p, C.lambda, Di);
 #pragma unroll
         for (int r = 0; r < 3; r++) x[r] = Di[3 * r] * cl[0] + Di[3 * r + 1] * cl[1] + Di[3 * r + 2] * cl[2];
     }
@@ -972,13 +1005,11 @@ __global__ void __launch_bounds__(kCtlThreads) k_trial_control(const WinDesc* __
                                                                const double* __restrict__ xl,
                                                                const double* __restrict__ bp,
                                                                const double* __restrict__ bl, int stop) {
-    __shared__ double sh[kCtlThreads];
+    __shared__ double sh[kCtlThreads / 64];
     const WinDesc W = wins[blockIdx.x];
     WinCtl& C = ctl[blockIdx.x];
     if (!C.need_trial) return;
-    double s = 0;
-    for (int i = threadIdx.x; i < W.ne; i += kCtlThreads) s += rho[W.e0 + i];
-    double tmpChi = block_sum(s, sh);
+    double tmpChi = block_sum(strided_sum(rho + W.e0, W.ne), sh);
     const double lam = C.lambda;
     double sc = 0;
     for (int i = threadIdx.x; i < 6 * W.np; i += kCtlThreads) {
@@ -1192,7 +1223,7 @@ struct slam_lba {
     unsigned char* harena = nullptr;  // pinned
     size_t harena_cap = 0;
     DevBuf arena, cnt;
-    DevBuf poses, pts, err, rho, lin, Hll, bl, Hpp, bp, Dinv, tr, xp, xl, Hs;
+    DevBuf poses, pts, err, rho, lin, Hll, bl, Hpp, bp, tr, xp, xl, Hs;
     DevBuf kf_out, pt_out, outl;
 };
 
@@ -1578,7 +1609,6 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     SLAM_HIP_TRY(s->tr.ensure(sizeof(double) * kTrStride * ne));
     SLAM_HIP_TRY(s->Hll.ensure(sizeof(double) * 8 * npt));
     SLAM_HIP_TRY(s->bl.ensure(sizeof(double) * 4 * npt));
-    SLAM_HIP_TRY(s->Dinv.ensure(sizeof(double) * 12 * npt));
     SLAM_HIP_TRY(s->xl.ensure(sizeof(double) * 4 * npt));
     SLAM_HIP_TRY(s->Hpp.ensure(sizeof(double) * 24 * nps));
     SLAM_HIP_TRY(s->bp.ensure(sizeof(double) * 8 * nps));
@@ -1645,10 +1675,9 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
                                                     as<double>(s->Hll));
             bool any_active = false;
             for (int t = 0; t < 10; t++) {
-                k_schur_point<<<blocks(H.npt, T), T, 0, S>>>(H.npt, DP.spe_off, DP.spe,
-                                                              DP.pt_win, dC, as<double>(s->Hll),
-                                                              as<double>(s->bl), as<double>(s->lin),
-                                                              as<double>(s->Dinv), as<double>(s->tr));
+                k_schur_edges<<<blocks(Z.nspe, T), T, 0, S>>>(Z.nspe, DP.spe, dE, dC, as<double>(s->Hll),
+                                                               as<double>(s->bl), as<double>(s->lin),
+                                                               as<double>(s->tr));
                 if (H.nblk)
                     k_schur_block<<<blocks(H.nblk, 4), 256, 0, S>>>(
                         H.nblk, DP.blk_pose, DP.blk_win, DP.ct_off, DP.ct, dW,
@@ -1657,7 +1686,7 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
                 k_ldlt<<<nw, 512, lds_bytes, S>>>(dW, dC, as<double>(s->Hs), as<double>(s->xp));
                 k_backsub<<<blocks(H.npt, T), T, 0, S>>>(H.npt, DP.spe_off, DP.spe, dE,
                                                           DP.pt_win, dC, as<double>(s->bl),
-                                                          as<double>(s->Dinv), as<double>(s->lin), as<double>(s->xp),
+                                                          as<double>(s->Hll), as<double>(s->lin), as<double>(s->xp),
                                                           as<double>(s->xl), pts, pt_stride);
                 k_pose_update<<<blocks(H.nkf, T), T, 0, S>>>(H.nkf, DP.kf_hp, DP.kf_win, dC,
                                                               as<double>(s->xp), poses, pose_stride);

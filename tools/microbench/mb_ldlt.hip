@@ -70,7 +70,8 @@ int main(int argc, char** argv) {
     }
     const double us = 1e3 * total / reps;
     // wall_clock64 runs at 100 MHz on gfx9
-    printf("n=%d ldlt %.1f us  residual %.3e  phases(us): diag %.1f  rows %.1f  trailing %.1f  backsolve %.1f\n", n,
-           us, res / nb, ph[1] / 100.0 / reps, ph[2] / 100.0 / reps, ph[3] / 100.0 / reps, ph[4] / 100.0 / reps);
+    printf("n=%d ldlt %.1f us  residual %.3e  phases(us): diag %.1f [load %.1f steps %.1f] rows %.1f  trailing %.1f  "
+           "backsolve %.1f\n", n, us, res / nb, (ph[1] + ph[5] + ph[6]) / 100.0 / reps, ph[5] / 100.0 / reps,
+           ph[6] / 100.0 / reps, ph[2] / 100.0 / reps, ph[3] / 100.0 / reps, ph[4] / 100.0 / reps);
     return 0;
 }
