@@ -1,0 +1,105 @@
+"""Window construction of Optimizer::LocalBundleAdjustment (Optimizer.cc:1613-1718) in the host
+mirror (slamhot/optimizer.py), its flattening into slam_lba_problem, and (GPU) the full mirror
+against a direct slamhot_lba_solve of the same window."""
+import numpy as np
+import pytest
+
+from slamhot import optimizer as opt
+from slamhot import synth
+
+
+def _window():
+    return synth.lba_window(50, n_kf=10, n_pt=120, obs_per_pt=4)
+
+
+def test_fallback_moves_lowest_local_kf_to_fixed():
+    W = _window()
+    pmap, kfs, mps = opt.map_from_window(W)
+    local, fixed, local_mps, nfix = opt.build_window(kfs[-1], pmap)
+    # every KF is covisible with the current one: no fixed cameras, the init KF counts as 1,
+    # so the lowest-id other local KF (id 1) is moved to the fixed list (:1676-1711)
+    assert nfix == 2
+    assert [k.mnId for k in fixed] == [1]
+    assert sorted(k.mnId for k in local) == [0] + list(range(2, 10))
+    # lLocalMapPoints: first-seen order over the local KFs (current KF first, :1631-1655)
+    expect, seen = [], set()
+    for k in [kfs[-1]] + kfs[-1].covisible:
+        for mp in k.mvpMapPoints:
+            if mp is not None and mp.mnId not in seen:
+                seen.add(mp.mnId)
+                expect.append(mp.mnId)
+    assert [mp.mnId for mp in local_mps] == expect
+    Wf, kf_order, refs = opt.flatten_window(local, fixed, local_mps, pmap)
+    assert np.array_equal(Wf["kf_fixed"], W["kf_fixed"])  # KF 0 init-fixed, KF 1 fixed camera
+    assert np.array_equal(Wf["kf_Tcw"], W["kf_Tcw"])
+    # same edge set, point-major in first-seen order, KFs ascending inside a point
+    ids = np.array([mp.mnId for mp in local_mps])
+    got = sorted(zip(ids[Wf["edge_pt"]].tolist(), Wf["edge_kf"].tolist(), Wf["edge_obs"][:, 0].tolist()))
+    ref = sorted(zip(W["edge_pt"].tolist(), W["edge_kf"].tolist(), W["edge_obs"][:, 0].tolist()))
+    assert got == ref
+    assert np.all(np.diff(Wf["edge_pt"]) >= 0)
+
+
+def test_partial_covisibility_yields_fixed_cameras():
+    W = _window()
+    pmap, kfs, mps = opt.map_from_window(W, covis_order=[])
+    kfs[-1].covisible = [kfs[8], kfs[7]]
+    local, fixed, local_mps, nfix = opt.build_window(kfs[-1], pmap)
+    assert [k.mnId for k in local] == [9, 8, 7]
+    # every other KF observing a local point is a fixed camera, in first-seen order
+    assert nfix == len(fixed) >= 2
+    assert all(k.mnId not in (7, 8, 9) for k in fixed)
+    seen = set()
+    order = []
+    for mp in local_mps:
+        for k in mp.GetObservations():
+            if k.mnId not in (7, 8, 9) and k.mnId not in seen:
+                seen.add(k.mnId)
+                order.append(k.mnId)
+    assert [k.mnId for k in fixed] == order
+
+
+def test_bad_and_foreign_keyframes_are_excluded():
+    W = _window()
+    pmap, kfs, mps = opt.map_from_window(W)
+    kfs[4].bad = True
+    kfs[5].map = opt.Map(init_kf_id=99)
+    mps[0].bad = True
+    local, fixed, local_mps, nfix = opt.build_window(kfs[-1], pmap)
+    ids = {k.mnId for k in local} | {k.mnId for k in fixed}
+    assert 4 not in ids and 5 not in ids
+    assert all(mp.mnId != 0 for mp in local_mps)
+
+
+def test_lonely_keyframe_aborts():
+    pmap = opt.Map(init_kf_id=0)
+    keys = np.zeros(1, dtype=[("x", "<f4"), ("y", "<f4"), ("octave", "<i4")])
+    kf = opt.KeyFrame(5, np.eye(4), keys, [-1.0], [1.0], (400, 400, 300, 200, 40), pmap)
+    mp = opt.MapPoint(0, [0, 0, 2], pmap)
+    kf.mvpMapPoints[0] = mp
+    mp.AddObservation(kf, 0)
+    assert opt.build_window(kf, pmap) is None  # 0 fixed KFs: LBA aborted (:1714-1718)
+
+
+@pytest.mark.gpu
+def test_mirror_equals_direct_solve():
+    import slamhot
+    W = synth.lba_window(51, n_kf=12, n_pt=300, obs_per_pt=5, stereo_frac=0.3)
+    S = slamhot.LocalBundleAdjustment()
+    direct = S.solve(W)
+    pmap, kfs, mps = opt.map_from_window(W)
+    counts = opt.LocalBundleAdjustment(kfs[-1], False, pmap, S)
+    assert counts == (2, 11, 300, len(W["edge_pt"]))
+    # the mirror feeds points in first-seen order (the synthetic window is id-ordered), so
+    # only summation order differs: within the LBA tolerance
+    for i, k in enumerate(kfs):
+        if W["kf_fixed"][i] != 2:
+            assert np.abs(k.GetPose().reshape(-1) - direct["kf_Tcw"][i]).max() <= 1e-5
+        else:
+            assert np.array_equal(k.GetPose().reshape(-1), W["kf_Tcw"][i])
+    for i, mp in enumerate(mps):
+        assert np.abs(mp.GetWorldPos() - direct["pt_pos"][i]).max() <= 1e-5
+    n_obs = sum(len(mp.observations) for mp in mps)
+    assert n_obs == len(W["edge_pt"]) - direct["n_outlier"]
+    assert pmap.change_index == 1
+    S.close()
