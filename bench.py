@@ -78,6 +78,7 @@ def main():
     ap.add_argument("--lba-windows", type=int, default=64, help="LBA windows per GPU per call (0 = skip)")
     ap.add_argument("--lba-calls", type=int, default=3)
     ap.add_argument("--match-pairs", type=int, default=128, help="(keyframe, frame) pairs per GPU per step (0 = skip)")
+    ap.add_argument("--pose-frames", type=int, default=512, help="PoseOptimization frames per GPU per call (0 = skip)")
     args = ap.parse_args()
 
     import torch
@@ -214,6 +215,8 @@ def main():
         result["match"] = match_leg(args, rank, world, local_rank, dist, device)
     if args.lba_windows > 0:
         result["lba"] = lba_leg(args, rank, world, local_rank, dist, device)
+    if args.pose_frames > 0:
+        result["pose"] = pose_leg(args, rank, world, local_rank, dist, device)
 
     if rank == 0:
         print(json.dumps(result), flush=True)
@@ -314,6 +317,55 @@ def match_leg(args, rank, world, local_rank, dist, device):
     ex.close()
     m.close()
     voc.close()
+    return out
+
+
+def pose_leg(args, rank, world, local_rank, dist, device):
+    """Optimizer::PoseOptimization frames/s: batches of synthetic frames (1000 keypoints, 80%
+    with MapPoints, 10% outliers, EuRoC intrinsics), one workgroup per frame."""
+    import torch
+
+    import slamhot
+    from slamhot import dist as sdist
+    from slamhot import synth
+    nf = args.pose_frames
+    pool = [synth.pose_frame(s) for s in sdist.shard(16 * world, rank, world)]
+    frames = [pool[i % len(pool)] for i in range(nf)]
+    S = slamhot.PoseOptimizer(device=local_rank)
+    S.solve(frames[:8])
+    if dist:
+        dist.barrier()
+    calls = 3
+    t0 = time.perf_counter()
+    for _ in range(calls):
+        res = S.solve(frames)
+    torch.cuda.synchronize(device)
+    if dist:
+        dist.barrier()
+    elapsed, total = sdist.reduce_run(dist, device, time.perf_counter() - t0, float(nf * calls))
+    out = {
+        "metric": "Optimizer::PoseOptimization frames/s",
+        "value": round(total / elapsed, 1),
+        "unit": "frames/s",
+        "dtype": "f64",
+        "config": {"workload": "synthetic frames, 1000 keypoints, ~800 MapPoint observations, 10% outliers, "
+                               "4 x optimize(10)", "frames_per_gpu_per_call": nf,
+                   "parallelism": f"frame-sharded x{world}"},
+        "ms_per_call": round(elapsed / calls * 1e3, 3),
+        "mean_inliers": round(float(np.mean([r["n_inliers"] for r in res])), 1),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, str(ROOT / "tests"))
+        import oracle_bind as ob
+        t0 = time.perf_counter()
+        k = 0
+        while k < len(pool) and time.perf_counter() - t0 < 3.0:
+            ob.pose_optimization(pool[k])
+            k += 1
+        out["cpu_baseline"] = {"value": round(k / (time.perf_counter() - t0), 2), "unit": "frames/s", "cores": 1,
+                               "kind": "port", "sample": f"{k} frames one at a time on one core; "
+                                                         f"oracle/pose_oracle.cpp -O3"}
+    S.close()
     return out
 
 

@@ -337,6 +337,38 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
  * and upload, buildStructure in g2o), and the number of host<->device round trips. */
 slam_status slamhot_lba_last_stats(const slam_lba* s, double* device_ms, double* plan_ms, int* syncs);
 
+/* ------------------------------------------------------------------------------------------
+ * Motion-only BA: int Optimizer::PoseOptimization(Frame* pFrame) (Optimizer.h:55,
+ * Optimizer.cc:824-1118), pinhole (no mpCamera2).  Four rounds of optimize(10) from the
+ * frame's initial pose, each re-classifying every observation by chi2 (5.991 mono / 7.815
+ * stereo) and excluding outliers from the next round; the Huber kernel is dropped after the
+ * third round.  Batched: one workgroup per frame.
+ * ------------------------------------------------------------------------------------------ */
+typedef struct slam_pose_frame {
+    float Tcw[16];               /* pFrame->mTcw, row-major 4x4 */
+    int32_t n;                   /* pFrame->N */
+    const slam_keypoint* kps_un; /* mvKeysUn: x, y, octave used */
+    const float* uright;         /* mvuRight (< 0 -> monocular observation) */
+    const uint8_t* has_mp;       /* mvpMapPoints[i] != NULL */
+    const float* mp_pos;         /* n x 3 MapPoint::GetWorldPos (read where has_mp) */
+    const float* inv_sigma2;     /* mvInvLevelSigma2 */
+    int32_t nlevels;
+    slam_camera cam;
+} slam_pose_frame;
+
+typedef struct slam_pose_result {
+    float Tcw[16];               /* pFrame->SetPose (input pose when fewer than 3 observations) */
+    uint8_t* outlier;            /* n: pFrame->mvbOutlier (only entries with has_mp are written) */
+    int32_t n_initial;           /* nInitialCorrespondences */
+    int32_t n_inliers;           /* return value: nInitialCorrespondences - nBad (0 if < 3) */
+} slam_pose_result;
+
+typedef struct slam_pose_opt slam_pose_opt;
+slam_status slamhot_pose_opt_create(int device, slam_pose_opt** out);
+void slamhot_pose_opt_destroy(slam_pose_opt* h);
+slam_status slamhot_pose_optimization(slam_pose_opt* h, int nframes, const slam_pose_frame* frames,
+                                      slam_pose_result* results);
+
 #ifdef __cplusplus
 }
 #endif

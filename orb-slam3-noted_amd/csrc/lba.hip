@@ -30,6 +30,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "se3_device.hpp"
 
 namespace slamhot {
 namespace lba {
@@ -82,92 +83,6 @@ struct Cam {
     double fx, fy, cx, cy, bf;
     float bff;
 };
-
-// ---------------------------------------------------------------- SE3Quat math (device)
-struct Quat {
-    double x, y, z, w;
-};
-
-__device__ inline Quat quat_from_R(const double* R) {
-    Quat q;
-    double t = R[0] + R[4] + R[8];
-    if (t > 0.0) {
-        t = sqrt(t + 1.0);
-        q.w = 0.5 * t;
-        t = 0.5 / t;
-        q.x = (R[7] - R[5]) * t;
-        q.y = (R[2] - R[6]) * t;
-        q.z = (R[3] - R[1]) * t;
-        return q;
-    }
-    int i = 0;
-    if (R[4] > R[0]) i = 1;
-    if (R[8] > R[4 * i]) i = 2;
-    const int j = (i + 1) % 3, k = (j + 1) % 3;
-    double c[3];
-    t = sqrt(R[4 * i] - R[4 * j] - R[4 * k] + 1.0);
-    c[i] = 0.5 * t;
-    t = 0.5 / t;
-    q.w = (R[3 * k + j] - R[3 * j + k]) * t;
-    c[j] = (R[3 * j + i] + R[3 * i + j]) * t;
-    c[k] = (R[3 * k + i] + R[3 * i + k]) * t;
-    q.x = c[0];
-    q.y = c[1];
-    q.z = c[2];
-    return q;
-}
-
-__device__ inline void normalize_rotation(Quat& q) {
-    if (q.w < 0) {
-        q.x = -q.x;
-        q.y = -q.y;
-        q.z = -q.z;
-        q.w = -q.w;
-    }
-    const double n = sqrt(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
-    q.x /= n;
-    q.y /= n;
-    q.z /= n;
-    q.w /= n;
-}
-
-__device__ inline void rot_matrix(const Quat& q, double* R) {
-    const double tx = 2.0 * q.x, ty = 2.0 * q.y, tz = 2.0 * q.z;
-    const double twx = tx * q.w, twy = ty * q.w, twz = tz * q.w;
-    const double txx = tx * q.x, txy = ty * q.x, txz = tz * q.x;
-    const double tyy = ty * q.y, tyz = tz * q.y, tzz = tz * q.z;
-    R[0] = 1.0 - (tyy + tzz);
-    R[1] = txy - twz;
-    R[2] = txz + twy;
-    R[3] = txy + twz;
-    R[4] = 1.0 - (txx + tzz);
-    R[5] = tyz - twx;
-    R[6] = txz - twy;
-    R[7] = tyz + twx;
-    R[8] = 1.0 - (txx + tyy);
-}
-
-__device__ inline void quat_rotate(const Quat& q, const double* p, double* out) {
-    double uv[3] = {q.y * p[2] - q.z * p[1], q.z * p[0] - q.x * p[2], q.x * p[1] - q.y * p[0]};
-    uv[0] += uv[0];
-    uv[1] += uv[1];
-    uv[2] += uv[2];
-    const double c0 = q.y * uv[2] - q.z * uv[1], c1 = q.z * uv[0] - q.x * uv[2],
-                 c2 = q.x * uv[1] - q.y * uv[0];
-    out[0] = p[0] + q.w * uv[0] + c0;
-    out[1] = p[1] + q.w * uv[1] + c1;
-    out[2] = p[2] + q.w * uv[2] + c2;
-}
-
-// pose record: qx qy qz qw tx ty tz pad
-__device__ inline Quat load_q(const double* P) { return Quat{P[0], P[1], P[2], P[3]}; }
-
-__device__ inline void se3_map(const double* P, const double* X, double* out) {
-    quat_rotate(load_q(P), X, out);
-    out[0] += P[4];
-    out[1] += P[5];
-    out[2] += P[6];
-}
 
 // ---------------------------------------------------------------- edge math
 __device__ inline void edge_error(const EdgeS& e, const Cam& cam, const double* P, const double* X,
@@ -486,26 +401,6 @@ __global__ void __launch_bounds__(kCtlThreads) k_iter_begin(const WinDesc* __res
 }
 
 // ---------------------------------------------------------------- trial kernels
-// Eigen 3x3 inverse by cofactors (Eigen/src/LU/InverseImpl.h)
-__device__ inline void inverse3(const double* m, double* out) {
-#define M_(i, j) m[3 * (i) + (j)]
-#define COF(i, j) (M_(((i) + 1) % 3, ((j) + 1) % 3) * M_(((i) + 2) % 3, ((j) + 2) % 3) - \
-                   M_(((i) + 1) % 3, ((j) + 2) % 3) * M_(((i) + 2) % 3, ((j) + 1) % 3))
-    const double c00 = COF(0, 0), c10 = COF(1, 0), c20 = COF(2, 0);
-    const double det = c00 * M_(0, 0) + c10 * M_(1, 0) + c20 * M_(2, 0);
-    const double invdet = 1.0 / det;
-    out[0] = c00 * invdet;
-    out[1] = c10 * invdet;
-    out[2] = c20 * invdet;
-    out[3] = COF(0, 1) * invdet;
-    out[4] = COF(1, 1) * invdet;
-    out[5] = COF(2, 1) * invdet;
-    out[6] = COF(0, 2) * invdet;
-    out[7] = COF(1, 2) * invdet;
-    out[8] = COF(2, 2) * invdet;
-#undef COF
-#undef M_
-}
 
 __device__ inline void point_dinv(const double* __restrict__ Hll, long long p, double lam, double* Di) {
     const double* h = Hll + 8 * p;
@@ -921,58 +816,7 @@ __global__ void k_pose_update(int nkf_total, const int* __restrict__ kf_hp, cons
         for (int i = 0; i < 8; i++) nxt[i] = cur[i];
         return;
     }
-    const double* u = xp + 6 * (long long)h;
-    const double om[3] = {u[0], u[1], u[2]}, up[3] = {u[3], u[4], u[5]};
-    const double theta = sqrt(om[0] * om[0] + om[1] * om[1] + om[2] * om[2]);
-    const double Wm[9] = {0, -om[2], om[1], om[2], 0, -om[0], -om[1], om[0], 0};
-    double W2[9];
-#pragma unroll
-    for (int i = 0; i < 3; i++)
-#pragma unroll
-        for (int j = 0; j < 3; j++)
-            W2[3 * i + j] = Wm[3 * i + 0] * Wm[0 + j] + Wm[3 * i + 1] * Wm[3 + j] + Wm[3 * i + 2] * Wm[6 + j];
-    double R[9], V[9];
-    if (theta < 0.00001) {
-#pragma unroll
-        for (int i = 0; i < 9; i++) {
-            R[i] = ((i % 4 == 0) ? 1.0 : 0.0) + Wm[i] + W2[i];
-            V[i] = R[i];
-        }
-    } else {
-        const double st = sin(theta), ct = cos(theta);
-        const double a = st / theta;
-        const double b = (1 - ct) / (theta * theta);
-        const double c = (theta - st) / pow(theta, 3);
-#pragma unroll
-        for (int i = 0; i < 9; i++) {
-            const double I = (i % 4 == 0) ? 1.0 : 0.0;
-            R[i] = I + a * Wm[i] + b * W2[i];
-            V[i] = I + b * Wm[i] + c * W2[i];
-        }
-    }
-    Quat qe = quat_from_R(R);
-    double te[3];
-#pragma unroll
-    for (int i = 0; i < 3; i++) te[i] = V[3 * i + 0] * up[0] + V[3 * i + 1] * up[1] + V[3 * i + 2] * up[2];
-    normalize_rotation(qe);
-    // exp * T  (SE3Quat::operator*)
-    const Quat qt = load_q(cur);
-    double rt[3];
-    quat_rotate(qe, cur + 4, rt);
-    Quat r;
-    r.w = qe.w * qt.w - qe.x * qt.x - qe.y * qt.y - qe.z * qt.z;
-    r.x = qe.w * qt.x + qe.x * qt.w + qe.y * qt.z - qe.z * qt.y;
-    r.y = qe.w * qt.y + qe.y * qt.w + qe.z * qt.x - qe.x * qt.z;
-    r.z = qe.w * qt.z + qe.z * qt.w + qe.x * qt.y - qe.y * qt.x;
-    normalize_rotation(r);
-    nxt[0] = r.x;
-    nxt[1] = r.y;
-    nxt[2] = r.z;
-    nxt[3] = r.w;
-    nxt[4] = te[0] + rt[0];
-    nxt[5] = te[1] + rt[1];
-    nxt[6] = te[2] + rt[2];
-    nxt[7] = 0.0;
+    se3_exp_mul(xp + 6 * (long long)h, cur, nxt);
 }
 
 __global__ void k_trial_error(int ne_total, const EdgeS* __restrict__ E, const WinCtl* __restrict__ ctl,

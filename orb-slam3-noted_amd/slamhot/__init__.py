@@ -568,3 +568,80 @@ def _bind_lba(L):
     L.slamhot_lba_solve.argtypes = [P, I, C.POINTER(LbaProblem), C.POINTER(LbaOptions), P, C.POINTER(LbaResult)]
     L.slamhot_lba_last_stats.argtypes = [P, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(I)]
     L._lba_ready = True
+
+
+# ------------------------------------------------------------------------------------------
+# Motion-only BA (Optimizer::PoseOptimization, Optimizer.cc:824-1118)
+# ------------------------------------------------------------------------------------------
+class PoseFrame(C.Structure):
+    _fields_ = [("Tcw", C.c_float * 16), ("n", C.c_int32), ("kps_un", C.c_void_p), ("uright", C.c_void_p),
+                ("has_mp", C.c_void_p), ("mp_pos", C.c_void_p), ("inv_sigma2", C.c_void_p), ("nlevels", C.c_int32),
+                ("cam", Camera)]
+
+
+class PoseResult(C.Structure):
+    _fields_ = [("Tcw", C.c_float * 16), ("outlier", C.c_void_p), ("n_initial", C.c_int32),
+                ("n_inliers", C.c_int32)]
+
+
+def make_pose_frame(f: dict):
+    arrs = dict(kps=np.ascontiguousarray(f["kps"], KP_DTYPE), uright=np.ascontiguousarray(f["uright"], np.float32),
+                has_mp=np.ascontiguousarray(f["has_mp"], np.uint8), mp_pos=np.ascontiguousarray(f["mp_pos"], np.float32),
+                inv_sigma2=np.ascontiguousarray(f["inv_sigma2"], np.float32))
+    T = np.ascontiguousarray(f["Tcw"], np.float32).reshape(-1)
+    pf = PoseFrame((C.c_float * 16)(*T.tolist()), len(arrs["kps"]), arrs["kps"].ctypes.data,
+                   arrs["uright"].ctypes.data, arrs["has_mp"].ctypes.data, arrs["mp_pos"].ctypes.data,
+                   arrs["inv_sigma2"].ctypes.data, len(arrs["inv_sigma2"]), Camera(*f["cam"]))
+    pf._keep = arrs
+    out = np.zeros(len(arrs["kps"]), np.uint8)
+    r = PoseResult((C.c_float * 16)(), out.ctypes.data, 0, 0)
+    r._keep = out
+    return pf, r, out
+
+
+def pose_result_dict(r: PoseResult, out) -> dict:
+    return dict(Tcw=np.array(r.Tcw[:], np.float32).reshape(4, 4), outlier=out.copy(), n_initial=r.n_initial,
+                n_inliers=r.n_inliers)
+
+
+class PoseOptimizer:
+    """Device Optimizer::PoseOptimization (slamhot_pose_optimization); `solve` takes one frame
+    dict or a list (batched: one workgroup per frame)."""
+
+    def __init__(self, device: int = 0):
+        L = lib()
+        if not getattr(L, "_pose_ready", False):
+            L.slamhot_pose_opt_create.argtypes = [I, C.POINTER(P)]
+            L.slamhot_pose_opt_destroy.argtypes = [P]
+            L.slamhot_pose_opt_destroy.restype = None
+            L.slamhot_pose_optimization.argtypes = [P, I, C.POINTER(PoseFrame), C.POINTER(PoseResult)]
+            L._pose_ready = True
+        h = P()
+        check(L.slamhot_pose_opt_create(device, C.byref(h)), "pose_opt_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().slamhot_pose_opt_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def solve(self, frames):
+        single = isinstance(frames, dict)
+        fs = [frames] if single else list(frames)
+        pfs = (PoseFrame * len(fs))()
+        rs = (PoseResult * len(fs))()
+        keep = []
+        for i, f in enumerate(fs):
+            pf, r, out = make_pose_frame(f)
+            pfs[i] = pf
+            rs[i] = r
+            keep.append((pf, r, out))
+        check(lib().slamhot_pose_optimization(self._h, len(fs), pfs, rs), "pose_optimization")
+        res = [pose_result_dict(rs[i], keep[i][2]) for i in range(len(fs))]
+        return res[0] if single else res

@@ -247,3 +247,50 @@ def lba_window(seed: int, n_kf: int = 50, n_pt: int = 2000, obs_per_pt: int = 8,
         cam=(np.float32(cam["fx"]), np.float32(cam["fy"]), np.float32(cam["cx"]),
              np.float32(cam["cy"]), np.float32(cam["bf"])),
         gt_T=gt_T, gt_pts=pts)
+
+
+def pose_frame(seed: int, n: int = 1000, mp_frac: float = 0.8, stereo_frac: float = 0.0,
+               outlier_frac: float = 0.1, rot_deg: float = 1.0, trans_m: float = 0.05):
+    """A seeded Frame for Optimizer::PoseOptimization: `n` undistorted keypoints on EuRoC
+    intrinsics, a fraction with MapPoints (world points 1.5-8 m in front of the true camera),
+    octave from the extractor's level split, noise N(0, 1.2^l) px, `outlier_frac` of the
+    matched observations replaced by uniform in-image points, initial pose perturbed by
+    rot_deg / trans_m (as after motion-model prediction)."""
+    rng = np.random.default_rng(seed)
+    cam = EUROC_CAM
+    scale, inv_sigma2, nf = _level_tables()
+    p_level = nf / nf.sum()
+    Rt = _axis_angle(rng.normal(size=3), np.deg2rad(rng.uniform(0, 30)))
+    tt = rng.normal(0, 1, 3)
+    kps = np.zeros(n, dtype=[("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                             ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+    ur = np.full(n, -1.0, np.float32)
+    has = (rng.random(n) < mp_frac).astype(np.uint8)
+    pos = np.zeros((n, 3), np.float32)
+    for i in range(n):
+        u, v = rng.uniform(5, cam["w"] - 5), rng.uniform(5, cam["h"] - 5)
+        z = rng.uniform(1.5, 8.0)
+        lvl = rng.choice(len(p_level), p=p_level)
+        Xc = np.array([(u - cam["cx"]) * z / cam["fx"], (v - cam["cy"]) * z / cam["fy"], z])
+        Xw = Rt.T @ (Xc - tt)
+        s = float(scale[lvl])
+        uo, vo = u + rng.normal(0, s), v + rng.normal(0, s)
+        st = rng.random() < stereo_frac
+        if rng.random() < outlier_frac:
+            uo, vo = rng.uniform(0, cam["w"]), rng.uniform(0, cam["h"])
+        kps["x"][i], kps["y"][i], kps["octave"][i] = uo, vo, lvl
+        if st:
+            ur[i] = max(0.0, uo - cam["bf"] / z + rng.normal(0, s))
+        pos[i] = Xw
+    Rp = _axis_angle(rng.normal(size=3), np.deg2rad(rot_deg)) @ Rt
+    d = rng.normal(size=3)
+    tp = tt + trans_m * d / np.linalg.norm(d)
+    T0 = np.eye(4, dtype=np.float32)
+    T0[:3, :3] = Rp
+    T0[:3, 3] = tp
+    gt = np.eye(4)
+    gt[:3, :3] = Rt
+    gt[:3, 3] = tt
+    return dict(Tcw=T0, kps=kps, uright=ur, has_mp=has, mp_pos=pos, inv_sigma2=inv_sigma2,
+                cam=(np.float32(cam["fx"]), np.float32(cam["fy"]), np.float32(cam["cx"]),
+                     np.float32(cam["cy"]), np.float32(cam["bf"])), gt_Tcw=gt)

@@ -293,3 +293,16 @@ def lba_solve(w, iters_first=5, iters_second=10, user_lambda_init=0.0, stop=0):
     opt = slamhot.LbaOptions(iters_first, iters_second, user_lambda_init)
     L.oracle_lba_solve(C.addressof(p), C.addressof(opt), int(stop), C.addressof(r))
     return slamhot.lba_result_dict(r, out)
+
+
+# ---- motion-only BA (oracle/pose_oracle.cpp)
+def pose_optimization(f):
+    import slamhot
+    L = lib()
+    if not hasattr(L, "_pose_ready"):
+        L.oracle_pose_optimization.argtypes = [C.c_void_p, C.c_void_p]
+        L.oracle_pose_optimization.restype = C.c_int
+        L._pose_ready = True
+    pf, r, out = slamhot.make_pose_frame(f)
+    L.oracle_pose_optimization(C.addressof(pf), C.addressof(r))
+    return slamhot.pose_result_dict(r, out)
