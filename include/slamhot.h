@@ -109,6 +109,11 @@ slam_status slamhot_extract_batch_device(slam_extractor* ex, int nframes, const 
 slam_status slamhot_pyramid_level(slam_extractor* ex, int frame, int level, uint8_t* dst,
                                   size_t dst_cap, int* width, int* height);
 
+/* Device view of the same level (no copy): pointer, row pitch, size.  Valid until the next
+ * extraction on this handle; level 0 is the caller's device input for extract_batch_device. */
+slam_status slamhot_pyramid_level_device(slam_extractor* ex, int frame, int level, const void** d_ptr,
+                                         int* pitch, int* width, int* height);
+
 /* Stream the handle works on (hipStream_t as void*). */
 void* slamhot_extractor_stream(slam_extractor* ex);
 
@@ -368,6 +373,31 @@ slam_status slamhot_pose_opt_create(int device, slam_pose_opt** out);
 void slamhot_pose_opt_destroy(slam_pose_opt* h);
 slam_status slamhot_pose_optimization(slam_pose_opt* h, int nframes, const slam_pose_frame* frames,
                                       slam_pose_result* results);
+
+/* ------------------------------------------------------------------ stereo matching
+ * Frame::ComputeStereoMatches (Frame.h:112, Frame.cc:794-964) for rectified stereo pairs
+ * extracted by two extractor handles (left, right; same ORB parameters and image size):
+ * row-band ORB matching (best Hamming < (TH_HIGH+TH_LOW)/2), 11x11 SAD search over +-5
+ * columns on the pyramid level the handles hold, parabola sub-pixel fit, disparity gate,
+ * median outlier cut.  mvuRight / mvDepth come back per left keypoint, -1 where unmatched. */
+typedef struct slam_stereo slam_stereo;
+
+slam_status slamhot_stereo_create(int device, slam_stereo** out);
+void slamhot_stereo_destroy(slam_stereo* st);
+
+/* Frame f of the last batch of `left` pairs with frame f of the last batch of `right`
+ * (f < nframes).  Device inputs at cap stride per frame as produced by
+ * slamhot_extract_batch_device: keypoints (slam_keypoint), descriptors (32 B), counts
+ * (int32).  mbf, mb: Frame::mbf, Frame::mb.  Device outputs (float, cap per frame):
+ * d_uright = mvuRight, d_depth = mvDepth; optional d_sad (int32, cap per frame, may be NULL):
+ * the SAD of each kept match before the median cut, -1 otherwise.  Asynchronous on hip_stream
+ * (NULL = the handle's stream); both extractors' work must be complete or ordered before it. */
+slam_status slamhot_stereo_match_batch_device(slam_stereo* st, slam_extractor* left, slam_extractor* right,
+                                              int nframes, const void* d_kps_left, const void* d_desc_left,
+                                              const void* d_n_left, const void* d_kps_right,
+                                              const void* d_desc_right, const void* d_n_right, int cap,
+                                              float mbf, float mb, void* d_uright, void* d_depth, void* d_sad,
+                                              void* hip_stream);
 
 #ifdef __cplusplus
 }

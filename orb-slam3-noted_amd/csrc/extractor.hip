@@ -1671,6 +1671,25 @@ slam_status slamhot_extract(slam_extractor* ex, const uint8_t* img, int width, i
                                  mono_index);
 }
 
+slam_status slamhot_pyramid_level_device(slam_extractor* ex, int frame, int level, const void** d_ptr, int* pitch,
+                                         int* width, int* height) {
+    if (!ex || !ex->have_plan || frame < 0 || frame >= ex->last_frames || level < 0 ||
+        level >= ex->plan.nlevels || !d_ptr || !pitch || !width || !height)
+        return SLAM_EINVAL;
+    const Plan& P = ex->plan;
+    const LevelPlan& L = P.lv[level];
+    *width = L.w;
+    *height = L.h;
+    if (level == 0) {
+        *d_ptr = ex->last_img + (size_t)frame * P.W * P.H;
+        *pitch = P.W;
+    } else {
+        *d_ptr = ex->d_pyr.as<uint8_t>() + (size_t)frame * P.pyr_frame + L.pyr_off;
+        *pitch = L.pitch;
+    }
+    return SLAM_OK;
+}
+
 slam_status slamhot_pyramid_level(slam_extractor* ex, int frame, int level, uint8_t* dst,
                                   size_t dst_cap, int* width, int* height) {
     if (!ex || !ex->have_plan || frame < 0 || frame >= ex->last_frames || level < 0 ||

@@ -1,0 +1,389 @@
+// stereo.hip — MI355X (gfx950) Frame::ComputeStereoMatches (Frame.cc:794-964).
+//
+//   k_stereo_rows    one workgroup per frame: the reference's vRowIndices (:808-824) as a CSR
+//                    table — LDS row counters (atomics), block scan, scatter of right keypoint
+//                    indices.  Entry order inside a row is arbitrary; the match step breaks
+//                    ties by the smallest right index, which is the order the reference's
+//                    push_back loop produces, so the result does not depend on it.
+//   k_stereo_match   one thread per left keypoint (grid: keypoint chunks x frames): band
+//                    candidates filtered by octave and u range, Hamming best < 100 (:849-871),
+//                    threshold 75, then the 11x11 SAD search over +-5 columns on the level's
+//                    pyramid (:874-915) — eleven running sums updated row by row from one
+//                    11-byte left slice and one 21-byte right slice — parabola fit and the
+//                    disparity gate (:917-946).  Integer SADs are exact, the float arithmetic
+//                    is the reference's operation for operation (no contraction).
+//   k_stereo_median  one workgroup per frame: bitonic sort of the kept SADs in LDS, median,
+//                    cut at 1.5f*1.4f*median (:950-963).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <new>
+
+#include "common.hpp"
+
+namespace slamhot {
+namespace {
+
+constexpr int kStMaxLevels = 16;
+constexpr int kStMaxRows = 4096;      // level-0 image height limit (extractor limit 4095)
+constexpr int kStMaxSort = 8192;      // keypoints per frame for the median sort (LDS)
+constexpr int kRowsThreads = 1024;
+constexpr int kMatchThreads = 128;
+constexpr int kMedianThreads = 1024;
+
+struct StereoGeom {
+    const uint8_t* base[2][kStMaxLevels];  // level l of frame 0 (left, right)
+    int64_t fstride[2][kStMaxLevels];      // bytes between frames at level l
+    int pitch[2][kStMaxLevels];
+    int lw[kStMaxLevels], lh[kStMaxLevels];
+    float scale[kStMaxLevels], inv_scale[kStMaxLevels];
+    int nlevels, nrows, cap, ent_cap;
+    float mbf, mb;
+};
+
+__global__ void __launch_bounds__(kRowsThreads) k_stereo_rows(StereoGeom G, const slam_keypoint* kps_r,
+                                                             const int32_t* n_r, int32_t* row_off,
+                                                             uint16_t* ent) {
+    __shared__ int cnt[kStMaxRows];
+    __shared__ int scan_tmp[kRowsThreads / 64 + 1];
+    const int f = blockIdx.x, t = threadIdx.x;
+    const int nrows = G.nrows;
+    const int nr = n_r[f];
+    const slam_keypoint* K = kps_r + (size_t)f * G.cap;
+    for (int r = t; r < nrows; r += kRowsThreads) cnt[r] = 0;
+    __syncthreads();
+    for (int i = t; i < nr; i += kRowsThreads) {
+        const float y = K[i].y;
+        const float r = 2.0f * G.scale[K[i].octave];
+        const int maxr = (int)ceilf(y + r), minr = (int)floorf(y - r);
+        for (int yi = max(minr, 0); yi <= min(maxr, nrows - 1); yi++) atomicAdd(&cnt[yi], 1);
+    }
+    __syncthreads();
+    // exclusive offsets: each thread owns a contiguous chunk of rows
+    const int per = (nrows + kRowsThreads - 1) / kRowsThreads;
+    const int r0 = t * per, r1 = min(r0 + per, nrows);
+    int local = 0;
+    for (int r = r0; r < r1; r++) local += cnt[r];
+    const int incl = block_scan_incl(local, scan_tmp, nullptr);
+    int run = incl - local;
+    int32_t* off = row_off + (size_t)f * (nrows + 1);
+    for (int r = r0; r < r1; r++) {
+        const int c = cnt[r];
+        off[r] = run;
+        cnt[r] = run;  // becomes the scatter cursor
+        run += c;
+    }
+    if (t == kRowsThreads - 1) off[nrows] = incl;
+    __syncthreads();
+    uint16_t* E = ent + (size_t)f * G.ent_cap;
+    for (int i = t; i < nr; i += kRowsThreads) {
+        const float y = K[i].y;
+        const float r = 2.0f * G.scale[K[i].octave];
+        const int maxr = (int)ceilf(y + r), minr = (int)floorf(y - r);
+        for (int yi = max(minr, 0); yi <= min(maxr, nrows - 1); yi++) E[atomicAdd(&cnt[yi], 1)] = (uint16_t)i;
+    }
+}
+
+__device__ __forceinline__ int ham32(const uint4 a0, const uint4 a1, const uint4 b0, const uint4 b1) {
+    return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+           __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+}
+
+__global__ void __launch_bounds__(kMatchThreads) k_stereo_match(StereoGeom G, const slam_keypoint* kps_l,
+                                                               const uint8_t* desc_l, const int32_t* n_l,
+                                                               const slam_keypoint* kps_r, const uint8_t* desc_r,
+                                                               const int32_t* row_off, const uint16_t* ent,
+                                                               float* uright, float* depth, int32_t* sad) {
+    const int f = blockIdx.y;
+    const int iL = blockIdx.x * kMatchThreads + threadIdx.x;
+    if (iL >= G.cap) return;
+    const size_t o = (size_t)f * G.cap + iL;
+    float ur_out = -1.0f, dep_out = -1.0f;
+    int sad_out = -1;
+    const int nl = n_l[f];
+    if (iL < nl) {
+        const slam_keypoint kl = kps_l[o];
+        const int levelL = kl.octave;
+        const float vL = kl.y, uL = kl.x;
+        const int row = (int)vL;
+        const int32_t* off = row_off + (size_t)f * (G.nrows + 1);
+        const float minZ = G.mb, minD = 0.0f;
+        const float maxD = G.mbf / minZ;
+        const float minU = uL - maxD, maxU = uL - minD;
+        int bestDist = 100, bestIdxR = 0;  // ORBmatcher::TH_HIGH
+        if (row >= 0 && row < G.nrows && !(maxU < 0)) {
+            const uint4* dl = reinterpret_cast<const uint4*>(desc_l + o * 32);
+            const uint4 a0 = dl[0], a1 = dl[1];
+            const slam_keypoint* KR = kps_r + (size_t)f * G.cap;
+            const uint8_t* DR = desc_r + (size_t)f * G.cap * 32;
+            const uint16_t* E = ent + (size_t)f * G.ent_cap;
+            const int c0 = off[row], c1 = off[row + 1];
+            for (int c = c0; c < c1; c++) {
+                const int iR = E[c];
+                const int oct = KR[iR].octave;
+                if (oct < levelL - 1 || oct > levelL + 1) continue;
+                const float uR = KR[iR].x;
+                if (uR >= minU && uR <= maxU) {
+                    const uint4* dr = reinterpret_cast<const uint4*>(DR + (size_t)iR * 32);
+                    const int d = ham32(a0, a1, dr[0], dr[1]);
+                    if (d < bestDist || (d == bestDist && d < 100 && iR < bestIdxR)) {
+                        bestDist = d;
+                        bestIdxR = iR;
+                    }
+                }
+            }
+        }
+        if (bestDist < 75) {  // thOrbDist = (TH_HIGH + TH_LOW) / 2
+            const float uR0 = kps_r[(size_t)f * G.cap + bestIdxR].x;
+            const float scaleFactor = G.inv_scale[levelL];
+            const float scaleduL = roundf(uL * scaleFactor);
+            const float scaledvL = roundf(vL * scaleFactor);
+            const float scaleduR0 = roundf(uR0 * scaleFactor);
+            const int w = 5, L = 5;
+            const float iniu = scaleduR0 + L - w;
+            const float endu = scaleduR0 + L + w + 1;
+            const int lw = G.lw[levelL], lh = G.lh[levelL];
+            const int vy0 = (int)scaledvL - w, ux0 = (int)scaleduL - w, ur0 = (int)scaleduR0;
+            const bool inside = !(iniu < 0 || endu >= lw) && vy0 >= 0 && vy0 + 2 * w + 1 <= lh && ux0 >= 0 &&
+                                ux0 + 2 * w + 1 <= lw && ur0 - L - w >= 0 && ur0 + L + w + 1 <= lw;
+            if (inside) {
+                const int pl = G.pitch[0][levelL], pr = G.pitch[1][levelL];
+                const uint8_t* PL = G.base[0][levelL] + f * G.fstride[0][levelL] + (size_t)vy0 * pl + ux0;
+                const uint8_t* PR = G.base[1][levelL] + f * G.fstride[1][levelL] + (size_t)vy0 * pr + (ur0 - L - w);
+                int acc[2 * L + 1];
+#pragma unroll
+                for (int k = 0; k < 2 * L + 1; k++) acc[k] = 0;
+                for (int yy = 0; yy < 2 * w + 1; yy++) {
+                    uint8_t a[2 * w + 1], b[2 * w + 2 * L + 1];
+#pragma unroll
+                    for (int x = 0; x < 2 * w + 1; x++) a[x] = PL[(size_t)yy * pl + x];
+#pragma unroll
+                    for (int x = 0; x < 2 * w + 2 * L + 1; x++) b[x] = PR[(size_t)yy * pr + x];
+#pragma unroll
+                    for (int k = 0; k < 2 * L + 1; k++)
+#pragma unroll
+                        for (int x = 0; x < 2 * w + 1; x++) acc[k] += abs((int)a[x] - (int)b[k + x]);
+                }
+                int bestDist2 = INT_MAX, bestk = 0;
+                float vd[2 * L + 1];
+#pragma unroll
+                for (int k = 0; k < 2 * L + 1; k++) {
+                    const float dist = (float)acc[k];
+                    if (dist < (float)bestDist2) {
+                        bestDist2 = (int)dist;
+                        bestk = k;
+                    }
+                    vd[k] = dist;
+                }
+                const int bestincR = bestk - L;
+                if (bestincR != -L && bestincR != L) {
+                    float dist1 = 0, dist2 = 0, dist3 = 0;
+#pragma unroll
+                    for (int k = 1; k < 2 * L; k++)
+                        if (k == bestk) {
+                            dist1 = vd[k - 1];
+                            dist2 = vd[k];
+                            dist3 = vd[k + 1];
+                        }
+                    const float deltaR = (dist1 - dist3) / (2.0f * (dist1 + dist3 - 2.0f * dist2));
+                    if (!(deltaR < -1 || deltaR > 1)) {
+                        float bestuR = G.scale[levelL] * ((float)scaleduR0 + (float)bestincR + deltaR);
+                        float disparity = (uL - bestuR);
+                        if (disparity >= minD && disparity < maxD) {
+                            if (disparity <= 0) {
+                                disparity = (float)0.01;
+                                bestuR = (float)((double)uL - 0.01);
+                            }
+                            dep_out = G.mbf / disparity;
+                            ur_out = bestuR;
+                            sad_out = bestDist2;
+                        }
+                    }
+                }
+            }
+        }
+    }
+    uright[o] = ur_out;
+    depth[o] = dep_out;
+    sad[o] = sad_out;
+}
+
+__global__ void __launch_bounds__(kMedianThreads) k_stereo_median(int cap, const int32_t* n_l, const int32_t* sad,
+                                                                 float* uright, float* depth) {
+    __shared__ uint32_t keys[kStMaxSort];
+    __shared__ int count;
+    const int f = blockIdx.x, t = threadIdx.x;
+    const int n = n_l[f];
+    const int32_t* S = sad + (size_t)f * cap;
+    if (t == 0) count = 0;
+    __syncthreads();
+    for (int i = t; i < n; i += kMedianThreads) {
+        const int v = S[i];
+        if (v >= 0) keys[atomicAdd(&count, 1)] = (uint32_t)v;
+    }
+    __syncthreads();
+    const int m = count;
+    if (m == 0) return;  // the reference reads vDistIdx[0] of an empty vector here
+    int np = 1;
+    while (np < m) np <<= 1;
+    for (int i = m + t; i < np; i += kMedianThreads) keys[i] = 0xFFFFFFFFu;
+    __syncthreads();
+    for (int k = 2; k <= np; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = t; i < np; i += kMedianThreads) {
+                const int p = i ^ j;
+                if (p > i) {
+                    const uint32_t x = keys[i], y = keys[p];
+                    const bool up = (i & k) == 0;
+                    if ((x > y) == up) {
+                        keys[i] = y;
+                        keys[p] = x;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    const float median = (float)(int)keys[m / 2];
+    const float thDist = 1.5f * 1.4f * median;
+    for (int i = t; i < n; i += kMedianThreads) {
+        const int v = S[i];
+        if (v >= 0 && !((float)v < thDist)) {
+            uright[(size_t)f * cap + i] = -1.0f;
+            depth[(size_t)f * cap + i] = -1.0f;
+        }
+    }
+}
+
+}  // namespace
+}  // namespace slamhot
+
+using namespace slamhot;
+
+struct slam_stereo {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    void *d_rowoff = nullptr, *d_ent = nullptr, *d_sad = nullptr;
+    size_t cap_rowoff = 0, cap_ent = 0, cap_sad = 0;
+};
+
+namespace {
+slam_status grow(void** p, size_t* cap, size_t need) {
+    if (need <= *cap) return SLAM_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    if (hipMalloc(p, need) != hipSuccess) return SLAM_ENOMEM;
+    *cap = need;
+    return SLAM_OK;
+}
+}  // namespace
+
+extern "C" {
+
+slam_status slamhot_stereo_create(int device, slam_stereo** out) {
+    if (!out) return SLAM_EINVAL;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return SLAM_ENODEV;
+    if (device < 0 || device >= n) return SLAM_EINVAL;
+    slam_stereo* st = new (std::nothrow) slam_stereo();
+    if (!st) return SLAM_ENOMEM;
+    st->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&st->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete st;
+        return SLAM_EHIP;
+    }
+    *out = st;
+    return SLAM_OK;
+}
+
+void slamhot_stereo_destroy(slam_stereo* st) {
+    if (!st) return;
+    (void)hipSetDevice(st->device);
+    if (st->stream) (void)hipStreamSynchronize(st->stream);
+    for (void* p : {st->d_rowoff, st->d_ent, st->d_sad})
+        if (p) (void)hipFree(p);
+    if (st->stream) (void)hipStreamDestroy(st->stream);
+    delete st;
+}
+
+slam_status slamhot_stereo_match_batch_device(slam_stereo* st, slam_extractor* left, slam_extractor* right,
+                                              int nframes, const void* d_kps_left, const void* d_desc_left,
+                                              const void* d_n_left, const void* d_kps_right,
+                                              const void* d_desc_right, const void* d_n_right, int cap,
+                                              float mbf, float mb, void* d_uright, void* d_depth, void* d_sad,
+                                              void* hip_stream) {
+    if (!st || !left || !right || nframes < 0 || cap <= 0 || cap > 65535 || !d_kps_left || !d_desc_left ||
+        !d_n_left || !d_kps_right || !d_desc_right || !d_n_right || !d_uright || !d_depth)
+        return SLAM_EINVAL;
+    if (nframes == 0) return SLAM_OK;
+    if (cap > kStMaxSort) return SLAM_EINVAL;
+    StereoGeom G{};
+    float sc[kStMaxLevels], isc[kStMaxLevels];
+    int nl = 0;
+    if (slamhot_extractor_levels(left, &nl, sc, isc, nullptr, nullptr, nullptr) != SLAM_OK || nl < 1 ||
+        nl > kStMaxLevels)
+        return SLAM_EINVAL;
+    G.nlevels = nl;
+    for (int side = 0; side < 2; side++) {
+        slam_extractor* ex = side ? right : left;
+        for (int l = 0; l < nl; l++) {
+            const void* p0 = nullptr;
+            const void* p1 = nullptr;
+            int pitch = 0, w = 0, h = 0, pitch1 = 0, w1 = 0, h1 = 0;
+            if (slamhot_pyramid_level_device(ex, 0, l, &p0, &pitch, &w, &h) != SLAM_OK) return SLAM_EINVAL;
+            if (nframes > 1) {
+                if (slamhot_pyramid_level_device(ex, nframes - 1, l, &p1, &pitch1, &w1, &h1) != SLAM_OK)
+                    return SLAM_EINVAL;  // fewer frames extracted than requested
+                // frames of one batch are evenly spaced
+                G.fstride[side][l] = ((const uint8_t*)p1 - (const uint8_t*)p0) / (nframes - 1);
+            }
+            G.base[side][l] = (const uint8_t*)p0;
+            G.pitch[side][l] = pitch;
+            if (side == 0) {
+                G.lw[l] = w;
+                G.lh[l] = h;
+            } else if (w != G.lw[l] || h != G.lh[l]) {
+                return SLAM_EINVAL;  // left and right images must share a geometry
+            }
+        }
+    }
+    for (int l = 0; l < nl; l++) {
+        G.scale[l] = sc[l];
+        G.inv_scale[l] = isc[l];
+    }
+    G.nrows = G.lh[0];
+    if (G.nrows > kStMaxRows) return SLAM_EINVAL;
+    // rows one right keypoint can cover: ceil(y + r) - floor(y - r) + 1 <= 4 * scale_max + 3
+    G.ent_cap = cap * ((int)std::ceil(4.0f * sc[nl - 1]) + 3);
+    G.cap = cap;
+    G.mbf = mbf;
+    G.mb = mb;
+    (void)hipSetDevice(st->device);
+    slam_status s;
+    if ((s = grow(&st->d_rowoff, &st->cap_rowoff, (size_t)nframes * (G.nrows + 1) * sizeof(int32_t))) ||
+        (s = grow(&st->d_ent, &st->cap_ent, (size_t)nframes * G.ent_cap * sizeof(uint16_t))))
+        return s;
+    int32_t* sad = (int32_t*)d_sad;
+    if (!sad) {
+        if ((s = grow(&st->d_sad, &st->cap_sad, (size_t)nframes * cap * sizeof(int32_t)))) return s;
+        sad = (int32_t*)st->d_sad;
+    }
+    hipStream_t strm = hip_stream ? (hipStream_t)hip_stream : st->stream;
+    hipLaunchKernelGGL(k_stereo_rows, dim3(nframes), dim3(kRowsThreads), 0, strm, G,
+                       (const slam_keypoint*)d_kps_right, (const int32_t*)d_n_right, (int32_t*)st->d_rowoff,
+                       (uint16_t*)st->d_ent);
+    hipLaunchKernelGGL(k_stereo_match, dim3((cap + kMatchThreads - 1) / kMatchThreads, nframes), dim3(kMatchThreads),
+                       0, strm, G, (const slam_keypoint*)d_kps_left, (const uint8_t*)d_desc_left,
+                       (const int32_t*)d_n_left, (const slam_keypoint*)d_kps_right, (const uint8_t*)d_desc_right,
+                       (const int32_t*)st->d_rowoff, (const uint16_t*)st->d_ent, (float*)d_uright, (float*)d_depth,
+                       sad);
+    hipLaunchKernelGGL(k_stereo_median, dim3(nframes), dim3(kMedianThreads), 0, strm, cap,
+                       (const int32_t*)d_n_left, (const int32_t*)sad, (float*)d_uright, (float*)d_depth);
+    SLAM_HIP_TRY(hipGetLastError());
+    return SLAM_OK;
+}
+
+}  // extern "C"

@@ -645,3 +645,93 @@ class PoseOptimizer:
         check(lib().slamhot_pose_optimization(self._h, len(fs), pfs, rs), "pose_optimization")
         res = [pose_result_dict(rs[i], keep[i][2]) for i in range(len(fs))]
         return res[0] if single else res
+
+
+# ------------------------------------------------------------------ stereo matching
+class StereoMatcher:
+    """Device Frame::ComputeStereoMatches (Frame.cc:794-964) over the last batches of two
+    ORBextractor handles (slamhot_stereo_match_batch_device)."""
+
+    def __init__(self, device: int = 0):
+        L = lib()
+        if not getattr(L, "_stereo_ready", False):
+            L.slamhot_stereo_create.argtypes = [I, C.POINTER(P)]
+            L.slamhot_stereo_destroy.argtypes = [P]
+            L.slamhot_stereo_destroy.restype = None
+            L.slamhot_stereo_match_batch_device.argtypes = [P, P, P, I, P, P, P, P, P, P, I, C.c_float, C.c_float,
+                                                            P, P, P, P]
+            L.slamhot_pyramid_level_device.argtypes = [P, I, I, C.POINTER(P), C.POINTER(I), C.POINTER(I),
+                                                       C.POINTER(I)]
+            L._stereo_ready = True
+        h = P()
+        check(L.slamhot_stereo_create(device, C.byref(h)), "stereo_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().slamhot_stereo_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def match_batch_device(self, left: ORBextractor, right: ORBextractor, nframes: int, d_kps_l: int, d_desc_l: int,
+                           d_n_l: int, d_kps_r: int, d_desc_r: int, d_n_r: int, cap: int, mbf: float, mb: float,
+                           d_uright: int, d_depth: int, d_sad: int | None = None, stream: int | None = None):
+        """All pointers are device addresses (ints); outputs mvuRight / mvDepth per left keypoint."""
+        st = lib().slamhot_stereo_match_batch_device(self._h, left._h, right._h, nframes, P(d_kps_l), P(d_desc_l),
+                                                     P(d_n_l), P(d_kps_r), P(d_desc_r), P(d_n_r), cap, mbf, mb,
+                                                     P(d_uright), P(d_depth), P(d_sad) if d_sad else None,
+                                                     P(stream) if stream else None)
+        check(st, "slamhot_stereo_match_batch_device")
+
+
+def ComputeStereoMatches(left: ORBextractor, right: ORBextractor, images_left, images_right, mbf: float, mb: float,
+                         matcher: StereoMatcher | None = None):
+    """Stereo Frame construction for a batch of rectified pairs (Frame.cc:80-180 stereo path:
+    two ORB extractions, then ComputeStereoMatches), device-resident between the steps; torch
+    provides the device buffers.  Returns per frame (kps_left, desc_left, kps_right,
+    desc_right, mvuRight, mvDepth)."""
+    import torch
+    il = np.ascontiguousarray(images_left, np.uint8)
+    ir = np.ascontiguousarray(images_right, np.uint8)
+    if il.ndim == 2:
+        il, ir = il[None], ir[None]
+    F, H, W = il.shape
+    cap = left.cap
+    dev = torch.device("cuda", torch.cuda.current_device())
+    bufs = []
+    for ex, im in ((left, il), (right, ir)):
+        d_img = torch.from_numpy(im).to(dev)
+        d_kps = torch.zeros((F, cap, KP_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+        d_desc = torch.zeros((F, cap, 32), dtype=torch.uint8, device=dev)
+        d_n = torch.zeros(F, dtype=torch.int32, device=dev)
+        d_mono = torch.zeros(F, dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()
+        ex.extract_batch_device(d_img.data_ptr(), F, W, H, d_kps.data_ptr(), d_desc.data_ptr(), cap, d_n.data_ptr(),
+                                d_mono.data_ptr())
+        bufs.append((d_img, d_kps, d_desc, d_n))
+    torch.cuda.synchronize()
+    d_ur = torch.empty((F, cap), dtype=torch.float32, device=dev)
+    d_dep = torch.empty((F, cap), dtype=torch.float32, device=dev)
+    own = matcher is None
+    m = matcher or StereoMatcher(dev.index or 0)
+    (_, kl, dl, nl), (_, kr, dr, nr) = bufs
+    m.match_batch_device(left, right, F, kl.data_ptr(), dl.data_ptr(), nl.data_ptr(), kr.data_ptr(), dr.data_ptr(),
+                         nr.data_ptr(), cap, mbf, mb, d_ur.data_ptr(), d_dep.data_ptr())
+    torch.cuda.synchronize()
+    if own:
+        m.close()
+    nl_h, nr_h = nl.cpu().numpy(), nr.cpu().numpy()
+    kl_h, kr_h = kl.cpu().numpy().view(KP_DTYPE), kr.cpu().numpy().view(KP_DTYPE)
+    dl_h, dr_h = dl.cpu().numpy(), dr.cpu().numpy()
+    ur, dep = d_ur.cpu().numpy(), d_dep.cpu().numpy()
+    out = []
+    for f in range(F):
+        a, b = int(nl_h[f]), int(nr_h[f])
+        out.append((kl_h[f, :a].ravel().copy(), dl_h[f, :a].copy(), kr_h[f, :b].ravel().copy(), dr_h[f, :b].copy(),
+                    ur[f, :a].copy(), dep[f, :a].copy()))
+    return out

@@ -294,3 +294,30 @@ def pose_frame(seed: int, n: int = 1000, mp_frac: float = 0.8, stereo_frac: floa
     return dict(Tcw=T0, kps=kps, uright=ur, has_mp=has, mp_pos=pos, inv_sigma2=inv_sigma2,
                 cam=(np.float32(cam["fx"]), np.float32(cam["fy"]), np.float32(cam["cx"]),
                      np.float32(cam["cy"]), np.float32(cam["bf"])), gt_Tcw=gt)
+
+
+EUROC_STEREO = dict(fx=435.2046959714599, bf=47.90639384423901)  # EuRoC.yaml Camera.fx / Camera.bf
+
+
+def stereo_pair(seed: int, width: int = 752, height: int = 480, d_min: float = 4.0, d_max: float = 40.0,
+                noise: float = 2.0):
+    """Rectified stereo pair (left, right) uint8: the left frame is `frame(seed)`; the right
+    one samples it at x + d(x, y) (linear interpolation, so disparities are sub-pixel) where
+    d is a piecewise-planar disparity field in [d_min, d_max] (a slanted background plane
+    and a few fronto-parallel boxes), plus Gaussian noise."""
+    left = frame(seed, width, height)
+    rng = np.random.default_rng(seed + 7919)
+    yy, xx = np.mgrid[0:height, 0:width].astype(np.float64)
+    d = d_min + (0.35 * (d_max - d_min)) * (xx / width) + 0.1 * (d_max - d_min) * (yy / height)
+    for _ in range(4):
+        x0, y0 = rng.integers(0, width - 60), rng.integers(0, height - 60)
+        bw, bh = rng.integers(60, 240), rng.integers(60, 200)
+        d[y0:y0 + bh, x0:x0 + bw] = rng.uniform(0.5 * (d_min + d_max), d_max)
+    xs = xx + d
+    x0 = np.clip(np.floor(xs).astype(np.int64), 0, width - 1)
+    x1 = np.clip(x0 + 1, 0, width - 1)
+    fx = np.clip(xs - np.floor(xs), 0.0, 1.0)
+    lf = left.astype(np.float64)
+    rows = np.arange(height)[:, None]
+    right = lf[rows, x0] * (1 - fx) + lf[rows, x1] * fx + rng.normal(0.0, noise, size=left.shape)
+    return left, np.clip(np.rint(right), 0, 255).astype(np.uint8)

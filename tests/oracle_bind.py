@@ -306,3 +306,36 @@ def pose_optimization(f):
     pf, r, out = slamhot.make_pose_frame(f)
     L.oracle_pose_optimization(C.addressof(pf), C.addressof(r))
     return slamhot.pose_result_dict(r, out)
+
+
+# ---- stereo matching (oracle/stereo_oracle.cpp)
+def stereo_matches(kl, dl, kr, dr, pyr_left, pyr_right, scale, inv_scale, mbf, mb):
+    """Frame::ComputeStereoMatches on host arrays; pyr_* are lists of 2-D u8 levels."""
+    L = lib()
+    V = C.c_void_p
+    if not hasattr(L, "_stereo_ready"):
+        L.oracle_stereo_matches.argtypes = [C.c_int, V, V, C.c_int, V, V, C.c_int, V, V, V, V, V, V, V, V,
+                                            C.c_float, C.c_float, V, V]
+        L.oracle_stereo_matches.restype = None
+        L._stereo_ready = True
+    nl = len(pyr_left)
+    kl = np.ascontiguousarray(kl)
+    kr = np.ascontiguousarray(kr)
+    dl = np.ascontiguousarray(dl, np.uint8)
+    dr = np.ascontiguousarray(dr, np.uint8)
+    pl = [np.ascontiguousarray(a, np.uint8) for a in pyr_left]
+    pr = [np.ascontiguousarray(a, np.uint8) for a in pyr_right]
+    ptr_l = (C.c_void_p * nl)(*[a.ctypes.data for a in pl])
+    ptr_r = (C.c_void_p * nl)(*[a.ctypes.data for a in pr])
+    pitch_l = np.array([a.shape[1] for a in pl], np.int32)
+    pitch_r = np.array([a.shape[1] for a in pr], np.int32)
+    lw = pitch_l.copy()
+    lh = np.array([a.shape[0] for a in pl], np.int32)
+    sc = np.ascontiguousarray(scale, np.float32)
+    isc = np.ascontiguousarray(inv_scale, np.float32)
+    ur = np.zeros(len(kl), np.float32)
+    dep = np.zeros(len(kl), np.float32)
+    L.oracle_stereo_matches(len(kl), _ptr(kl), _ptr(dl), len(kr), _ptr(kr), _ptr(dr), nl, C.cast(ptr_l, V),
+                            C.cast(ptr_r, V), _ptr(pitch_l), _ptr(pitch_r), _ptr(lw), _ptr(lh), _ptr(sc), _ptr(isc),
+                            mbf, mb, _ptr(ur), _ptr(dep))
+    return ur, dep
