@@ -79,6 +79,7 @@ def main():
     ap.add_argument("--lba-calls", type=int, default=3)
     ap.add_argument("--match-pairs", type=int, default=128, help="(keyframe, frame) pairs per GPU per step (0 = skip)")
     ap.add_argument("--pose-frames", type=int, default=512, help="PoseOptimization frames per GPU per call (0 = skip)")
+    ap.add_argument("--stereo-pairs", type=int, default=128, help="stereo frames per GPU per step (0 = skip)")
     args = ap.parse_args()
 
     import torch
@@ -217,6 +218,8 @@ def main():
         result["lba"] = lba_leg(args, rank, world, local_rank, dist, device)
     if args.pose_frames > 0:
         result["pose"] = pose_leg(args, rank, world, local_rank, dist, device)
+    if args.stereo_pairs > 0:
+        result["stereo"] = stereo_leg(args, rank, world, local_rank, dist, device)
 
     if rank == 0:
         print(json.dumps(result), flush=True)
@@ -260,7 +263,9 @@ def match_leg(args, rank, world, local_rank, dist, device):
     d_a2b = torch.zeros((Pn, cap), dtype=torch.int32, device=device)
     d_b2a = torch.zeros((Pn, cap), dtype=torch.int32, device=device)
     d_nm = torch.zeros(Pn, dtype=torch.int32, device=device)
-    stream = torch.cuda.current_stream(device).cuda_stream
+    # one real stream orders extraction before matching (NULL would mean each handle's own stream)
+    stream_obj = torch.cuda.Stream(device)
+    stream = stream_obj.cuda_stream
 
     def step():
         ex.extract_batch_device(d_img.data_ptr(), F, W, H, d_kps.data_ptr(), d_desc.data_ptr(), cap,
@@ -366,6 +371,109 @@ def pose_leg(args, rank, world, local_rank, dist, device):
                                "kind": "port", "sample": f"{k} frames one at a time on one core; "
                                                          f"oracle/pose_oracle.cpp -O3"}
     S.close()
+    return out
+
+
+def stereo_leg(args, rank, world, local_rank, dist, device):
+    """Stereo Frame construction frames/s (EuRoC stereo shape, BASELINE.json configs[3]:
+    752x480, 1200 features): a step extracts P left and P right images and runs
+    ComputeStereoMatches on the P pairs, all device-resident.  stereo_ms isolates the
+    matching kernels (torch events on the launch stream)."""
+    import torch
+
+    import slamhot
+    from slamhot import dist as sdist
+    from slamhot import synth
+    P, W, H, NF = args.stereo_pairs, 752, 480, 1200
+    seeds = sdist.shard(16 * world, rank, world)
+    prs = [synth.stereo_pair(int(s) + 500, W, H) for s in seeds]
+    il = np.stack([prs[i % len(prs)][0] for i in range(P)])
+    ir = np.stack([prs[i % len(prs)][1] for i in range(P)])
+    mbf = synth.EUROC_STEREO["bf"]
+    mb = mbf / synth.EUROC_STEREO["fx"]
+    left = slamhot.ORBextractor(nfeatures=NF, device=local_rank, max_size=(W, H), max_batch=P)
+    right = slamhot.ORBextractor(nfeatures=NF, device=local_rank, max_size=(W, H), max_batch=P)
+    sm = slamhot.StereoMatcher(device=local_rank)
+    cap = left.cap
+    d_il, d_ir = torch.from_numpy(il).to(device), torch.from_numpy(ir).to(device)
+    bufs = [(torch.zeros((P, cap, 28), dtype=torch.uint8, device=device),
+             torch.zeros((P, cap, 32), dtype=torch.uint8, device=device),
+             torch.zeros(P, dtype=torch.int32, device=device), torch.zeros(P, dtype=torch.int32, device=device))
+            for _ in range(2)]
+    d_ur = torch.empty((P, cap), dtype=torch.float32, device=device)
+    d_dep = torch.empty((P, cap), dtype=torch.float32, device=device)
+    stream = torch.cuda.Stream(device)  # a real stream: NULL would mean each handle's own stream
+    ev = []
+
+    def step(timed=False):
+        for ex, img, (k, d, n, m) in ((left, d_il, bufs[0]), (right, d_ir, bufs[1])):
+            ex.extract_batch_device(img.data_ptr(), P, W, H, k.data_ptr(), d.data_ptr(), cap, n.data_ptr(),
+                                    m.data_ptr(), stream=stream.cuda_stream)
+        (kl, dl, nl, _), (kr, dr, nr, _) = bufs
+        if timed:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+        sm.match_batch_device(left, right, P, kl.data_ptr(), dl.data_ptr(), nl.data_ptr(), kr.data_ptr(),
+                              dr.data_ptr(), nr.data_ptr(), cap, mbf, mb, d_ur.data_ptr(), d_dep.data_ptr(),
+                              stream=stream.cuda_stream)
+        if timed:
+            b.record(stream)
+            ev.append((a, b))
+
+    for _ in range(max(args.warmup, 1)):
+        step()
+    torch.cuda.synchronize(device)
+    if dist:
+        dist.barrier()
+    steps = max(args.steps // 2, 3)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(timed=True)
+    torch.cuda.synchronize(device)
+    if dist:
+        dist.barrier()
+    elapsed, total = sdist.reduce_run(dist, device, time.perf_counter() - t0, float(P * steps))
+    stereo_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    nl_h = bufs[0][2].cpu().numpy()
+    ur = d_ur.cpu().numpy()
+    matched = float(np.mean([(ur[f, : nl_h[f]] >= 0).sum() for f in range(P)]))
+    out = {
+        "metric": "stereo Frame (2x ORB extract + ComputeStereoMatches) frames/s",
+        "value": round(total / elapsed, 1),
+        "unit": "frames/s",
+        "dtype": "u8",
+        "config": {"workload": f"synthetic rectified pairs {W}x{H}, {NF} features, EuRoC bf",
+                   "pairs_per_gpu_per_step": P, "parallelism": f"frame-sharded x{world}"},
+        "ms_per_step": round(elapsed / steps * 1e3, 3),
+        "stereo_match_ms_per_step": round(stereo_ms, 4),
+        "stereo_match_frames_per_s": round(P / (stereo_ms / 1e3), 1),
+        "mean_stereo_matches": round(matched, 1),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, str(ROOT / "tests"))
+        import oracle_bind as ob
+        p = ob.params(nfeatures=NF)
+        sc, isc, _, _, _ = ob.levels(p)
+        t_ex = t_st = 0.0
+        k = 0
+        while k < len(prs) and t_ex + t_st < 10.0:
+            l_img, r_img = prs[k]
+            t1 = time.perf_counter()
+            kl, dl, _ = ob.extract(l_img, p)
+            kr, dr, _ = ob.extract(r_img, p)
+            t_ex += time.perf_counter() - t1
+            pl, pr = ob.pyramid(l_img, p), ob.pyramid(r_img, p)  # built inside extract too; untimed
+            t2 = time.perf_counter()
+            ob.stereo_matches(kl, dl, kr, dr, pl, pr, sc, isc, mbf, mb)
+            t_st += time.perf_counter() - t2
+            k += 1
+        out["cpu_baseline"] = {"value": round(k / (t_ex + t_st), 2), "unit": "frames/s", "cores": 1, "kind": "port",
+                               "sample": f"{k} stereo frames on one core (oracle extract x2 + "
+                                         f"oracle/stereo_oracle.cpp, -O3)",
+                               "stereo_match_only_frames_per_s": round(k / t_st, 1)}
+    left.close()
+    right.close()
+    sm.close()
     return out
 
 

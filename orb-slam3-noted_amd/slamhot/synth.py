@@ -48,12 +48,14 @@ def frame(seed: int, width: int = 640, height: int = 480) -> np.ndarray:
         yy, xx = np.mgrid[y0:y1, x0:x1]
         img[y0:y1, x0:x1] += amp * np.exp(-((xx - cx) ** 2 + (yy - cy) ** 2) / (2 * s * s))
     img += rng.normal(0.0, 4.0, size=img.shape)
-    return np.clip(np.rint(img), 0, 255).astype(np.uint8)
+    # C order: the broadcasting above leaves a Fortran-ordered array, and device uploads
+    # (torch.from_numpy(...).to(dev)) keep strides, so raw data_ptr() users need row-major
+    return np.ascontiguousarray(np.clip(np.rint(img), 0, 255).astype(np.uint8))
 
 
 def frames(seeds, width: int = 640, height: int = 480) -> np.ndarray:
     """Stack of frames (n, height, width) uint8."""
-    return np.stack([frame(int(s), width, height) for s in seeds])
+    return np.ascontiguousarray(np.stack([frame(int(s), width, height) for s in seeds]))
 
 
 def shifted(img: np.ndarray, dx: float, dy: float, angle_deg: float, seed: int) -> np.ndarray:
@@ -320,4 +322,4 @@ def stereo_pair(seed: int, width: int = 752, height: int = 480, d_min: float = 4
     lf = left.astype(np.float64)
     rows = np.arange(height)[:, None]
     right = lf[rows, x0] * (1 - fx) + lf[rows, x1] * fx + rng.normal(0.0, noise, size=left.shape)
-    return left, np.clip(np.rint(right), 0, 255).astype(np.uint8)
+    return left, np.ascontiguousarray(np.clip(np.rint(right), 0, 255).astype(np.uint8))

@@ -128,3 +128,47 @@ def test_stereo_geometry_mismatch_rejected():
     m.close()
     left.close()
     right.close()
+
+
+def test_stereo_stream_ordered_batch():
+    """The bench's shape: both extractions and the matcher queued on one stream with no host
+    sync in between, 16 pairs per batch."""
+    import torch
+
+    import slamhot
+    P, W, H = 16, 752, 480
+    prs = [synth.stereo_pair(500 + s, W, H) for s in range(P)]
+    il = np.stack([p[0] for p in prs])
+    ir = np.stack([p[1] for p in prs])
+    dev = torch.device("cuda", 0)
+    left = slamhot.ORBextractor(nfeatures=1200, max_size=(W, H), max_batch=P)
+    right = slamhot.ORBextractor(nfeatures=1200, max_size=(W, H), max_batch=P)
+    sm = slamhot.StereoMatcher()
+    cap = left.cap
+    d_il, d_ir = torch.from_numpy(il).to(dev), torch.from_numpy(ir).to(dev)
+    bufs = [(torch.zeros((P, cap, 28), dtype=torch.uint8, device=dev),
+             torch.zeros((P, cap, 32), dtype=torch.uint8, device=dev),
+             torch.zeros(P, dtype=torch.int32, device=dev), torch.zeros(P, dtype=torch.int32, device=dev))
+            for _ in range(2)]
+    d_ur = torch.empty((P, cap), dtype=torch.float32, device=dev)
+    d_dep = torch.empty((P, cap), dtype=torch.float32, device=dev)
+    stream = torch.cuda.Stream(dev)  # a real stream: NULL would mean each handle's own stream
+    torch.cuda.synchronize()
+    for ex, img, (k, d, n, m) in ((left, d_il, bufs[0]), (right, d_ir, bufs[1])):
+        ex.extract_batch_device(img.data_ptr(), P, W, H, k.data_ptr(), d.data_ptr(), cap, n.data_ptr(),
+                                m.data_ptr(), stream=stream.cuda_stream)
+    (kl, dl, nl, _), (kr, dr, nr, _) = bufs
+    sm.match_batch_device(left, right, P, kl.data_ptr(), dl.data_ptr(), nl.data_ptr(), kr.data_ptr(), dr.data_ptr(),
+                          nr.data_ptr(), cap, MBF, MB, d_ur.data_ptr(), d_dep.data_ptr(), stream=stream.cuda_stream)
+    torch.cuda.synchronize()
+    nl_h, nr_h = nl.cpu().numpy(), nr.cpu().numpy()
+    kl_h, kr_h = kl.cpu().numpy().view(ob.KP_DTYPE), kr.cpu().numpy().view(ob.KP_DTYPE)
+    dl_h, dr_h = dl.cpu().numpy(), dr.cpu().numpy()
+    ur, dep = d_ur.cpu().numpy(), d_dep.cpu().numpy()
+    out = [(kl_h[f, :nl_h[f]].ravel(), dl_h[f, :nl_h[f]], kr_h[f, :nr_h[f]].ravel(), dr_h[f, :nr_h[f]],
+            ur[f, :nl_h[f]], dep[f, :nl_h[f]]) for f in range(P)]
+    kept = _check(left, right, out, 1200)
+    assert kept > P * 200
+    sm.close()
+    left.close()
+    right.close()
