@@ -222,6 +222,31 @@ slam_status slamhot_search_by_projection_local(slam_matcher* m, const slam_frame
                                                float nnratio, float th, int far_points,
                                                float th_far, int32_t* f_match, int* nmatches);
 
+/* One local MapPoint as Tracking::SearchLocalPoints sees it (Tracking.cc:3213-3231). */
+typedef struct slam_mp_geom {
+    float pos[3];                 /* GetWorldPos2 (mWorldPosx) */
+    float normal[3];              /* GetNormal2 (mNormalVectorx) */
+    float min_dist, max_dist;     /* mfMinDistance, mfMaxDistance (the 0.8f / 1.2f invariance
+                                     factors of GetMin/MaxDistanceInvariance are applied here) */
+    uint8_t seen;                 /* mnLastFrameSeen == mCurrentFrame.mnId (already matched) */
+    uint8_t is_bad;               /* isBad() */
+    uint8_t has_obs;              /* Observations() > 0 */
+    uint8_t pad;
+} slam_mp_geom;
+
+/* Tracking::SearchLocalPoints' second half (Tracking.cc:3213-3258) for a Frame with
+ * Nleft == -1: Frame::isInFrustum(pMP, view_cos_limit) (Frame.cc:493-556, with
+ * MapPoint::PredictScale, MapPoint.cc:551-566) for every MapPoint not seen / not bad, then, when
+ * any is in view, SearchByProjection(F, vpMapPoints, th, bFarPoints, thFarPoints)
+ * (ORBmatcher.cc:44-214) — both on the device, no host round trip between them.  F->Tcw is
+ * required.  Outputs: f_match / nmatches as slamhot_search_by_projection_local; *n_to_match =
+ * the number of MapPoints isInFrustum accepted; track (optional, n_mp) = the tracking fields
+ * isInFrustum leaves (in_view = mbTrackInView). */
+slam_status slamhot_search_local_points(slam_matcher* m, const slam_frame_view* F, int n_mp,
+                                        const slam_mp_geom* mps, const uint8_t* mp_desc, float view_cos_limit,
+                                        float nnratio, float th, int far_points, float th_far,
+                                        slam_mp_track* track, int* n_to_match, int32_t* f_match, int* nmatches);
+
 /* The previous Frame for SearchByProjection(Frame&, const Frame& LastFrame, th, bMono)
  * (ORBmatcher.cc:2173-2389): per last-frame feature its MapPoint (has_mp, outlier flag,
  * world position, descriptor, Observations()>0) and keypoint octave/angle. */

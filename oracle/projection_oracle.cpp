@@ -305,4 +305,86 @@ int oracle_search_by_projection_kf(const slam_frame_view* F, const slam_kf_point
     return nmatches;
 }
 
+/* Frame::isInFrustum (Frame.cc:493-556, Nleft == -1) over a local map as
+ * Tracking::SearchLocalPoints calls it (Tracking.cc:3213-3226): cv::Matx float products and
+ * norms as sequential float sums, PredictScale (MapPoint.cc:551-566) with glibc logf.
+ * Returns nToMatch. */
+int oracle_is_in_frustum(const slam_frame_view* F, int n_mp, const slam_mp_geom* mps, float view_cos_limit,
+                         slam_mp_track* track) {
+    float Ow[3];
+    neg_rt_t(F->Tcw, Ow);
+    const float* T = F->Tcw;
+    int n_in = 0;
+    for (int i = 0; i < n_mp; i++) {
+        const slam_mp_geom& g = mps[i];
+        slam_mp_track& tr = track[i];
+        std::memset(&tr, 0, sizeof(tr));
+        tr.proj_x = -1.0f;
+        tr.proj_y = -1.0f;
+        tr.scale_level = -1;
+        tr.is_bad = g.is_bad;
+        tr.has_obs = g.has_obs;
+        if (g.seen || g.is_bad) continue;  // Tracking.cc:3217-3220
+        float Pc[3];
+        for (int r = 0; r < 3; r++) {
+            float acc = 0.0f;  // Matx_MatMulOp: s = 0; s += a * b
+            for (int k = 0; k < 3; k++) acc += T[4 * r + k] * g.pos[k];
+            Pc[r] = acc + T[4 * r + 3];
+        }
+        float n2 = 0.0f;  // normL2Sqr<float, float>
+        for (int k = 0; k < 3; k++) n2 += Pc[k] * Pc[k];
+        const float Pc_dist = std::sqrt(n2);
+        const float PcZ = Pc[2];
+        const float invz = 1.0f / PcZ;
+        if (PcZ < 0.0f) continue;
+        const float u = F->fx * Pc[0] / PcZ + F->cx;  // Pinhole::project
+        const float v = F->fy * Pc[1] / PcZ + F->cy;
+        if (u < F->min_x || u > F->max_x) continue;
+        if (v < F->min_y || v > F->max_y) continue;
+        tr.proj_x = u;
+        tr.proj_y = v;
+        const float maxDistance = 1.2f * g.max_dist;
+        const float minDistance = 0.8f * g.min_dist;
+        float PO[3];
+        for (int k = 0; k < 3; k++) PO[k] = g.pos[k] - Ow[k];
+        float d2 = 0.0f;
+        for (int k = 0; k < 3; k++) d2 += PO[k] * PO[k];
+        const float dist = std::sqrt(d2);
+        if (dist < minDistance || dist > maxDistance) continue;
+        float dot = 0.0f;  // Matx::dot
+        for (int k = 0; k < 3; k++) dot += PO[k] * g.normal[k];
+        const float viewCos = dot / dist;
+        if (viewCos < view_cos_limit) continue;
+        const float ratio = g.max_dist / dist;
+        int nScale = (int)std::ceil(std::log(ratio) / F->log_scale);  // std::log(float) = logf
+        if (nScale < 0) nScale = 0;
+        else if (nScale >= F->nlevels) nScale = F->nlevels - 1;
+        tr.in_view = 1;
+        tr.proj_xr = u - F->bf * invz;
+        tr.depth = Pc_dist;
+        tr.scale_level = nScale;
+        tr.view_cos = viewCos;
+        n_in++;
+    }
+    return n_in;
+}
+
+/* MapPoint::PredictScale with glibc logf vs with the correctly rounded logf the device uses
+ * ((float)log((double)r)): number of float ratios in [lo, hi] (every bit pattern) whose
+ * predicted level (before clamping) differs. */
+long oracle_check_predict_scale(float lo, float hi, float log_scale) {
+    uint32_t a, b;
+    std::memcpy(&a, &lo, 4);
+    std::memcpy(&b, &hi, 4);
+    long bad = 0;
+    for (uint32_t u = a; u <= b; u++) {
+        float r;
+        std::memcpy(&r, &u, 4);
+        const int g = (int)std::ceil(std::log(r) / log_scale);
+        const int c = (int)std::ceil((float)std::log((double)r) / log_scale);
+        bad += g != c;
+    }
+    return bad;
+}
+
 }  // extern "C"

@@ -1142,6 +1142,75 @@ __global__ void __launch_bounds__(1024) k_search_by_projection(DevProjCall C) {
     }
 }
 
+// Frame::isInFrustum (Frame.cc:493-556) for a Frame with Nleft == -1, one thread per local
+// MapPoint, in the reference's float arithmetic: cv::Matx33f x Matx31f products and
+// cv::norm / Matx::dot as sequential float sums, Pinhole::project as (f * x) / z + c.
+// MapPoint::PredictScale's ceil(logf(ratio) / mfLogScaleFactor) uses the correctly rounded
+// logf ((float)log((double)r)); its ceil equals glibc logf's for every ratio in [1e-3, 1e3]
+// (exhaustive check, tests/test_projection_oracle.py).
+struct FrustumCall {
+    float R[9], t[3], Ow[3];
+    float min_x, max_x, min_y, max_y, fx, fy, cx, cy, bf;
+    float log_scale, view_cos_limit;
+    int nlevels, n;
+    const slam_mp_geom* mps;
+    slam_mp_track* track;
+    int32_t* n_in_view;
+};
+
+__global__ void __launch_bounds__(256) k_is_in_frustum(FrustumCall C) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= C.n) return;
+    const slam_mp_geom g = C.mps[i];
+    slam_mp_track tr{};
+    tr.proj_x = -1.0f;
+    tr.proj_y = -1.0f;
+    tr.scale_level = -1;
+    tr.is_bad = g.is_bad;
+    tr.has_obs = g.has_obs;
+    tr.in_view = 0;
+    bool ok = !g.seen && !g.is_bad;
+    float Pc[3];
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+        float acc = 0.0f;  // Matx_MatMulOp: s = 0; s += a * b
+        acc = acc + C.R[3 * r] * g.pos[0];
+        acc = acc + C.R[3 * r + 1] * g.pos[1];
+        acc = acc + C.R[3 * r + 2] * g.pos[2];
+        Pc[r] = acc + C.t[r];
+    }
+    const float Pc_dist = sqrtf(((0.0f + Pc[0] * Pc[0]) + Pc[1] * Pc[1]) + Pc[2] * Pc[2]);
+    const float PcZ = Pc[2];
+    const float invz = 1.0f / PcZ;
+    if (PcZ < 0.0f) ok = false;
+    const float u = C.fx * Pc[0] / PcZ + C.cx;
+    const float v = C.fy * Pc[1] / PcZ + C.cy;
+    if (u < C.min_x || u > C.max_x || v < C.min_y || v > C.max_y) ok = false;
+    const float maxDistance = 1.2f * g.max_dist;
+    const float minDistance = 0.8f * g.min_dist;
+    const float PO[3] = {g.pos[0] - C.Ow[0], g.pos[1] - C.Ow[1], g.pos[2] - C.Ow[2]};
+    const float dist = sqrtf(((0.0f + PO[0] * PO[0]) + PO[1] * PO[1]) + PO[2] * PO[2]);
+    if (dist < minDistance || dist > maxDistance) ok = false;
+    const float viewCos = (((0.0f + PO[0] * g.normal[0]) + PO[1] * g.normal[1]) + PO[2] * g.normal[2]) / dist;
+    if (viewCos < C.view_cos_limit) ok = false;
+    if (ok) {
+        const float ratio = g.max_dist / dist;
+        const float lr = (float)log((double)ratio);
+        int nScale = (int)ceilf(lr / C.log_scale);
+        if (nScale < 0) nScale = 0;
+        else if (nScale >= C.nlevels) nScale = C.nlevels - 1;
+        tr.in_view = 1;
+        tr.proj_x = u;
+        tr.proj_xr = u - C.bf * invz;
+        tr.depth = Pc_dist;
+        tr.proj_y = v;
+        tr.scale_level = nScale;
+        tr.view_cos = viewCos;
+        atomicAdd(C.n_in_view, 1);
+    }
+    C.track[i] = tr;
+}
+
 }  // namespace slamhot
 
 namespace {
@@ -1202,7 +1271,7 @@ slam_status run_projection(slam_matcher* m, const slam_frame_view* F, DevProjCal
     int cap = std::max(4096, nq * 64);
     for (int attempt = 0; attempt < 2; attempt++) {
         const size_t need = (size_t)F->n * (sizeof(slam_keypoint) + 4 + 32 + 1 + 4 * 2) + start.size() * 4 +
-                            feat.size() * 4 + (size_t)nq * (sizeof(ProjQuery) + 32 + 4 * 3 + sizeof(slam_mp_track) + 64) +
+                            feat.size() * 4 + (size_t)nq * (sizeof(ProjQuery) + 32 + 4 * 3 + 2 * sizeof(slam_mp_track) + sizeof(slam_mp_geom) + 64) +
                             (size_t)cap * 4 + 64 * 1024;
         slam_status st;
         if ((st = m->d_a.ensure(need * 2))) return st;
@@ -1286,6 +1355,63 @@ extern "C" slam_status slamhot_search_by_projection_local(slam_matcher* m, const
     C.check_ori = 0;
     return run_projection(m, F, C, n_mp, nullptr, mp_desc, f_match, nmatches,
                           [&](Blob& B, DevProjCall& c) { c.mps = B.put(mps, n_mp); });
+}
+
+extern "C" slam_status slamhot_search_local_points(slam_matcher* m, const slam_frame_view* F, int n_mp,
+                                                   const slam_mp_geom* mps, const uint8_t* mp_desc,
+                                                   float view_cos_limit, float nnratio, float th, int far_points,
+                                                   float th_far, slam_mp_track* track, int* n_to_match,
+                                                   int32_t* f_match, int* nmatches) {
+    if (!m || !frame_ok(F) || !F->Tcw || n_mp < 0 || (n_mp && (!mps || !mp_desc)) || !n_to_match || !f_match ||
+        !nmatches)
+        return SLAM_EINVAL;
+    DevProjCall C{};
+    fill_frame(C, F);
+    C.mode = kProjLocal;
+    C.th = th;
+    C.th_far = th_far;
+    C.far_points = far_points;
+    C.nnratio = nnratio;
+    C.th_dist = 100;
+    C.check_ori = 0;
+    FrustumCall Fc{};
+    const float* T = F->Tcw;
+    for (int r = 0; r < 3; r++) {
+        for (int c = 0; c < 3; c++) Fc.R[3 * r + c] = T[4 * r + c];
+        Fc.t[r] = T[4 * r + 3];
+        // mOw = -mRcw.t() * mtcw as a cv::Mat product (double accumulation, one rounding)
+        const double acc = (double)T[r] * T[3] + (double)T[4 + r] * T[7] + (double)T[8 + r] * T[11];
+        Fc.Ow[r] = (float)(-1.0 * acc);
+    }
+    Fc.min_x = F->min_x;
+    Fc.max_x = F->max_x;
+    Fc.min_y = F->min_y;
+    Fc.max_y = F->max_y;
+    Fc.fx = F->fx;
+    Fc.fy = F->fy;
+    Fc.cx = F->cx;
+    Fc.cy = F->cy;
+    Fc.bf = F->bf;
+    Fc.log_scale = F->log_scale;
+    Fc.view_cos_limit = view_cos_limit;
+    Fc.nlevels = F->nlevels;
+    Fc.n = n_mp;
+    slam_status st = run_projection(m, F, C, n_mp, nullptr, mp_desc, f_match, nmatches,
+                                    [&](Blob& B, DevProjCall& c) {
+                                        Fc.mps = B.put(mps, n_mp);
+                                        Fc.track = B.take<slam_mp_track>(std::max(1, n_mp));
+                                        Fc.n_in_view = B.take<int32_t>(1);
+                                        (void)hipMemsetAsync(Fc.n_in_view, 0, 4, B.s);
+                                        if (n_mp)
+                                            hipLaunchKernelGGL(k_is_in_frustum, dim3((n_mp + 255) / 256), dim3(256),
+                                                               0, B.s, Fc);
+                                        c.mps = Fc.track;
+                                    });
+    if (st != SLAM_OK) return st;
+    std::lock_guard<std::mutex> g(m->mu);
+    SLAM_HIP_TRY(hipMemcpy(n_to_match, Fc.n_in_view, 4, hipMemcpyDeviceToHost));
+    if (track && n_mp) SLAM_HIP_TRY(hipMemcpy(track, Fc.track, sizeof(slam_mp_track) * n_mp, hipMemcpyDeviceToHost));
+    return SLAM_OK;
 }
 
 extern "C" slam_status slamhot_search_by_projection_last(slam_matcher* m, const slam_frame_view* F,

@@ -59,6 +59,8 @@ class FrameView(C.Structure):
                 ("Tcw", C.c_void_p)]
 
 
+MP_GEOM_DTYPE = np.dtype([("pos", "<f4", 3), ("normal", "<f4", 3), ("min_dist", "<f4"), ("max_dist", "<f4"),
+                          ("seen", "u1"), ("is_bad", "u1"), ("has_obs", "u1"), ("pad", "u1")])
 MP_TRACK_DTYPE = np.dtype([("proj_x", "<f4"), ("proj_y", "<f4"), ("proj_xr", "<f4"), ("depth", "<f4"),
                            ("view_cos", "<f4"), ("scale_level", "<i4"), ("in_view", "u1"), ("is_bad", "u1"),
                            ("has_obs", "u1"), ("pad", "u1")])
@@ -102,7 +104,7 @@ def make_frame_view(kps_un, desc, uright=None, mp_state=None, width=752, height=
     v.grid_inv_h = float(f32(48) / f32(height))
     v.nlevels = len(scale)
     v.scale = ptr(arrs["scale"])
-    v.log_scale = float(np.log(f32(scale_factor)))
+    v.log_scale = float(f32(np.log(np.float64(f32(scale_factor)))))  # logf (numpy's float32 log differs by an ulp)
     v.fx, v.fy, v.cx, v.cy = cam
     v.bf = bf
     v.b = float(f32(bf) / f32(cam[0]))
@@ -412,6 +414,25 @@ def _matcher_methods():
                                                        thFarPoints, _ptr(fm), C.byref(nm)), "search_by_projection_local")
         return nm.value, fm
 
+    def SearchLocalPoints(self, frame_view, mps, mp_desc, th=1.0, bFarPoints=False, thFarPoints=50.0,
+                          viewingCosLimit=0.5):
+        """Tracking::SearchLocalPoints (isInFrustum + SearchByProjection) on the device.
+        mps: MP_GEOM_DTYPE array.  Returns (nmatches, f_match, nToMatch, track)."""
+        L = lib()
+        if not getattr(L, "_slp_ready", False):
+            L.slamhot_search_local_points.argtypes = [P, C.POINTER(FrameView), I, P, P, C.c_float, C.c_float,
+                                                      C.c_float, I, C.c_float, P, C.POINTER(I), P, C.POINTER(I)]
+            L._slp_ready = True
+        mps = np.ascontiguousarray(mps, MP_GEOM_DTYPE)
+        mp_desc = np.ascontiguousarray(mp_desc, np.uint8)
+        fm = np.full(frame_view.n, -1, np.int32)
+        tr = np.zeros(len(mps), MP_TRACK_DTYPE)
+        nm, nt = I(0), I(0)
+        check(L.slamhot_search_local_points(self._h, C.byref(frame_view), len(mps), _ptr(mps), _ptr(mp_desc),
+                                            viewingCosLimit, self.mfNNratio, th, int(bFarPoints), thFarPoints,
+                                            _ptr(tr), C.byref(nt), _ptr(fm), C.byref(nm)), "search_local_points")
+        return nm.value, fm, nt.value, tr
+
     def SearchByProjection_last(self, frame_view, last_view, th, bMono):
         """int SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, th, bMono)."""
         fm = np.full(frame_view.n, -1, np.int32)
@@ -455,6 +476,7 @@ def _matcher_methods():
     ORBmatcher.bow_match_batch_device = bow_match_batch_device
     ORBmatcher.bow_match_batch_status = bow_match_batch_status
     ORBmatcher.SearchByProjection_local = SearchByProjection_local
+    ORBmatcher.SearchLocalPoints = SearchLocalPoints
     ORBmatcher.SearchByProjection_last = SearchByProjection_last
     ORBmatcher.SearchByProjection_kf = SearchByProjection_kf
 

@@ -339,3 +339,27 @@ def stereo_matches(kl, dl, kr, dr, pyr_left, pyr_right, scale, inv_scale, mbf, m
                             C.cast(ptr_r, V), _ptr(pitch_l), _ptr(pitch_r), _ptr(lw), _ptr(lh), _ptr(sc), _ptr(isc),
                             mbf, mb, _ptr(ur), _ptr(dep))
     return ur, dep
+
+
+def _frlib():
+    L = _plib()
+    if not hasattr(L, "_fr_ready"):
+        L.oracle_is_in_frustum.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_float, C.c_void_p]
+        L.oracle_is_in_frustum.restype = C.c_int
+        L.oracle_check_predict_scale.argtypes = [C.c_float, C.c_float, C.c_float]
+        L.oracle_check_predict_scale.restype = C.c_long
+        L._fr_ready = True
+    return L
+
+
+def is_in_frustum(fv, geom, view_cos_limit=0.5):
+    """Frame::isInFrustum over a local map (oracle/projection_oracle.cpp); (nToMatch, track)."""
+    import slamhot
+    geom = np.ascontiguousarray(geom, slamhot.MP_GEOM_DTYPE)
+    tr = np.zeros(len(geom), slamhot.MP_TRACK_DTYPE)
+    n = _frlib().oracle_is_in_frustum(C.addressof(fv), len(geom), _ptr(geom), view_cos_limit, _ptr(tr))
+    return n, tr
+
+
+def check_predict_scale(lo, hi, log_scale):
+    return int(_frlib().oracle_check_predict_scale(lo, hi, log_scale))

@@ -127,3 +127,49 @@ def kf_points(S):
     desc = flip_bits(d, rng, 45)
     order = rng.permutation(n)
     return slamhot.make_kf_points(kk[order], use[order], Xw[order], max_d[order], min_d[order], desc[order])
+
+
+def local_map_geom(S, n_extra=300, boundary_frac=0.15):
+    """Local MapPoints as Tracking::SearchLocalPoints sees them (slamhot.MP_GEOM_DTYPE):
+    most back-projected from current features (so isInFrustum accepts them and the matcher
+    finds them), some behind the camera / off-image / out of the distance range / at grazing
+    view angles, some already seen or bad, and a fraction whose mfMaxDistance puts the
+    predicted level exactly on a scale boundary (ratio = 1.2^l, the MapPoint's creation
+    distance)."""
+    rng, k, d = S["rng"], S["k"], S["d"]
+    n = len(k)
+    sel = rng.permutation(n)[: int(n * 0.75)]
+    depth = rng.uniform(0.8, 25.0, len(sel)).astype(np.float32)
+    X = backproject(S, k["x"][sel] + rng.normal(0, 1.0, len(sel)), k["y"][sel] + rng.normal(0, 1.0, len(sel)), depth)
+    Xe = backproject(S, rng.uniform(-200, 952, n_extra), rng.uniform(-150, 630, n_extra),
+                     rng.uniform(-5.0, 40.0, n_extra).astype(np.float32))
+    pos = np.concatenate([X, Xe]).astype(np.float32)
+    m = len(pos)
+    T = S["Tcw"].astype(np.float64)
+    Ow = -(T[:3, :3].T @ T[:3, 3])
+    PO = pos.astype(np.float64) - Ow
+    dist = np.linalg.norm(PO, axis=1)
+    # normal: mostly towards the camera, some at grazing angles
+    nrm = PO / dist[:, None]
+    tilt = rng.normal(0, 0.3, (m, 3))
+    tilt[rng.random(m) < 0.1] *= 8.0
+    nrm = nrm + tilt
+    nrm = (nrm / np.linalg.norm(nrm, axis=1)[:, None]).astype(np.float32)
+    level = rng.integers(0, 8, m)
+    max_d = (dist * np.float32(1.2) ** level * rng.uniform(0.9, 1.6, m)).astype(np.float32)
+    b = rng.random(m) < boundary_frac
+    # creation distance == current distance: max_d = dist * scaleFactor^level exactly
+    sc = np.float32(1.2) ** np.arange(8, dtype=np.float32)
+    max_d[b] = (dist[b].astype(np.float32) * sc[level[b]]).astype(np.float32)
+    min_d = (max_d / sc[7]).astype(np.float32)
+    geom = np.zeros(m, slamhot.MP_GEOM_DTYPE)
+    geom["pos"] = pos
+    geom["normal"] = nrm
+    geom["min_dist"] = min_d
+    geom["max_dist"] = max_d
+    geom["seen"] = rng.random(m) < 0.05
+    geom["is_bad"] = rng.random(m) < 0.03
+    geom["has_obs"] = rng.random(m) < 0.9
+    desc = np.concatenate([flip_bits(d[sel], rng, 40), flip_bits(d[rng.integers(0, n, n_extra)], rng, 90)])
+    order = rng.permutation(m)
+    return geom[order], desc[order]

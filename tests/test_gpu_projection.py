@@ -52,3 +52,26 @@ def test_keyframe(seed, th, orb_dist):
     m.close()
     assert ng == no and no > 20
     assert np.array_equal(fg, fo)
+
+
+@pytest.mark.parametrize("seed", [7, 8, 9])
+@pytest.mark.parametrize("th,far", [(1.0, False), (3.0, True), (15.0, False)])
+def test_search_local_points(seed, th, far):
+    """Tracking::SearchLocalPoints: device isInFrustum + SearchByProjection vs the oracle's
+    isInFrustum followed by its SearchByProjection."""
+    import slamhot
+    S = scenes.scene(seed)
+    fv, keep = scenes.frame_view(S)
+    geom, desc = scenes.local_map_geom(S)
+    m = slamhot.ORBmatcher(0.8)
+    ng, fg, ntg, trg = m.SearchLocalPoints(fv, geom, desc, th, far, 20.0)
+    m.close()
+    nto, tro = ob.is_in_frustum(fv, geom, 0.5)
+    assert ntg == nto and nto > 300
+    assert np.array_equal(trg["in_view"], tro["in_view"])
+    v = tro["in_view"] == 1
+    for f in ("proj_x", "proj_y", "proj_xr", "depth", "view_cos", "scale_level"):
+        assert np.array_equal(trg[f][v], tro[f][v]), f
+    no, fo = ob.search_by_projection_local(fv, tro, desc, 0.8, th, far, 20.0)
+    assert ng == no and no > 50
+    assert np.array_equal(fg, fo)

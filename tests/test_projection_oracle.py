@@ -113,3 +113,57 @@ def test_grid_area_known_answers():
         idx = py_area(k, cells, inv_w, inv_h, k["x"][i], k["y"][i], 0.5, int(k["octave"][i]), int(k["octave"][i]))
         assert i in idx
     assert py_area(k, cells, inv_w, inv_h, -500.0, 10.0, 3.0, -1, -1) == []
+
+
+def test_predict_scale_logf_equivalence():
+    """MapPoint::PredictScale with glibc logf (the reference) and with the correctly rounded
+    logf the device evaluates give the same level for every float ratio in [1e-3, 1e3]."""
+    lsf = float(np.float32(np.log(np.float64(np.float32(1.2)))))
+    assert ob.check_predict_scale(1e-3, 1e3, lsf) == 0
+
+
+def _py_in_frustum(fv, T, g, limit=0.5):
+    """Frame::isInFrustum restated with numpy float32 scalars (Frame.cc:493-556)."""
+    f32 = np.float32
+    if g["seen"] or g["is_bad"]:
+        return None
+    R, t = T[:3, :3].astype(np.float32), T[:3, 3].astype(np.float32)
+    Tr = T.astype(np.float64)
+    Ow = (-(Tr[:3, :3].T @ Tr[:3, 3])).astype(np.float32)
+    X = g["pos"].astype(np.float32)
+    Pc = [f32(f32(f32(f32(f32(0) + R[r, 0] * X[0]) + R[r, 1] * X[1]) + R[r, 2] * X[2]) + t[r]) for r in range(3)]
+    if Pc[2] < 0:
+        return None
+    u = f32(f32(f32(fv.fx) * Pc[0]) / Pc[2]) + f32(fv.cx)
+    v = f32(f32(f32(fv.fy) * Pc[1]) / Pc[2]) + f32(fv.cy)
+    if u < fv.min_x or u > fv.max_x or v < fv.min_y or v > fv.max_y:
+        return None
+    PO = (X - Ow).astype(np.float32)
+    dist = np.sqrt(f32(f32(f32(f32(0) + PO[0] * PO[0]) + PO[1] * PO[1]) + PO[2] * PO[2]))
+    if dist < f32(0.8) * g["min_dist"] or dist > f32(1.2) * g["max_dist"]:
+        return None
+    n = g["normal"]
+    vc = f32(f32(f32(f32(f32(0) + PO[0] * n[0]) + PO[1] * n[1]) + PO[2] * n[2]) / dist)
+    if vc < limit:
+        return None
+    ratio = f32(g["max_dist"] / dist)
+    lvl = int(np.ceil(f32(f32(np.log(np.float64(ratio))) / f32(fv.log_scale))))
+    return u, v, min(max(lvl, 0), fv.nlevels - 1), vc
+
+
+def test_is_in_frustum_oracle_vs_python():
+    S = scenes.scene(11)
+    fv, keep = scenes.frame_view(S)
+    geom, desc = scenes.local_map_geom(S)
+    n, tr = ob.is_in_frustum(fv, geom, 0.5)
+    cnt = 0
+    for i, g in enumerate(geom):
+        r = _py_in_frustum(fv, S["Tcw"], g)
+        assert bool(tr["in_view"][i]) == (r is not None), i
+        if r is not None:
+            cnt += 1
+            assert tr["proj_x"][i] == r[0] and tr["proj_y"][i] == r[1]
+            assert tr["scale_level"][i] == r[2] and tr["view_cos"][i] == r[3]
+    assert cnt == n and n > 300
+    # the boundary MapPoints (ratio = 1.2^level) land on both sides of the level edges
+    assert len(np.unique(tr["scale_level"][tr["in_view"] == 1])) == 8
