@@ -424,6 +424,58 @@ slam_status slamhot_stereo_match_batch_device(slam_stereo* st, slam_extractor* l
                                               float mbf, float mb, void* d_uright, void* d_depth, void* d_sad,
                                               void* hip_stream);
 
+/* ------------------------------------------------------------------ LocalMapping matchers
+ * The Hamming-heavy work LocalMapping runs around local BA. */
+typedef struct slam_mapper slam_mapper;
+
+slam_status slamhot_mapper_create(int device, slam_mapper** out);
+void slamhot_mapper_destroy(slam_mapper* mp);
+
+/* void MapPoint::ComputeDistinctiveDescriptors() (MapPoint.h, MapPoint.cc:349-423) for n_mp
+ * MapPoints at once.  MapPoint i's observed descriptors — non-bad KeyFrames in observation-map
+ * order, left then right index per KeyFrame, exactly the reference's vDescriptors — are
+ * desc[off[i] .. off[i+1]) (32 B each).  best[i] = the index, relative to off[i], of the
+ * descriptor with the least median distance to the others (vDists[0.5*(N-1)], first on ties),
+ * -1 when MapPoint i has none (mDescriptor unchanged). */
+slam_status slamhot_distinctive_descriptors(slam_mapper* mp, int n_mp, const int32_t* off, const uint8_t* desc,
+                                            int32_t* best);
+
+/* A KeyFrame as SearchForTriangulation_ reads it (pinhole, NLeft == -1). */
+typedef struct slam_tri_kf {
+    int32_t n;
+    const slam_keypoint* kps_un;  /* mvKeysUn (pt, octave, angle) */
+    const float* uright;          /* mvuRight (NULL = all -1) */
+    const uint8_t* desc;          /* mDescriptors, n x 32 */
+    const uint8_t* has_mp;        /* GetMapPoint(i) != NULL */
+    int32_t n_nodes;              /* mFeatVec as CSR: node ids ascending, their feature lists */
+    const int32_t* node_id;       /* n_nodes */
+    const int32_t* node_off;      /* n_nodes + 1 */
+    const int32_t* node_feat;     /* node_off[n_nodes] feature indices */
+    int32_t nlevels;
+    const float* scale;           /* mvScaleFactors */
+    const float* level_sigma2;    /* mvLevelSigma2 */
+} slam_tri_kf;
+
+/* One SearchForTriangulation_ call: KeyFrames kfs[kf1], kfs[kf2]. */
+typedef struct slam_tri_pair {
+    int32_t kf1, kf2;
+    float F12[9];                 /* row-major; LocalMapping::ComputeF12_ (LocalMapping.cc:886-903),
+                                     equal to what Pinhole::epipolarConstrain_ recomputes */
+    float ep[2];                  /* pKF2->mpCamera->project(R2w * Cw1 + t2w) (ORBmatcher.cc:1218-1222) */
+    uint8_t only_stereo, coarse, pad[2];
+} slam_tri_pair;
+
+/* int ORBmatcher::SearchForTriangulation_(KeyFrame* pKF1, KeyFrame* pKF2, cv::Matx33f F12,
+ * vector<pair<size_t,size_t>>& vMatchedPairs, bool bOnlyStereo, bool bCoarse)
+ * (ORBmatcher.h, ORBmatcher.cc:1208-1433) for n_pairs pairs in one launch (LocalMapping::
+ * CreateNewMapPoints calls it for every neighbour of the new KeyFrame, LocalMapping.cc:485).
+ * check_ori = the matcher's mbCheckOrientation.  Outputs: match12[p * cap + idx1] = idx2 or -1
+ * (cap >= kfs[pairs[p].kf1].n; vMatchedPairs = the idx1-ordered non-negative entries),
+ * nmatches[p]. */
+slam_status slamhot_search_for_triangulation(slam_mapper* mp, int n_kfs, const slam_tri_kf* kfs, int n_pairs,
+                                             const slam_tri_pair* pairs, int check_ori, int cap,
+                                             int32_t* match12, int32_t* nmatches);
+
 #ifdef __cplusplus
 }
 #endif

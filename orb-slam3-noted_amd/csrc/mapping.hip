@@ -1,0 +1,382 @@
+// mapping.hip — MI355X (gfx950) LocalMapping matchers.
+//
+//   k_distinctive   MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:349-423): one wave
+//                   per MapPoint.  Lane i owns descriptor i (rows i, i+64, ...); its median
+//                   distance vDists[(N-1)/2] is found by a 9-step binary search over the
+//                   distance range [0, 256] (count of d(i, j) <= v), so no N x N table is
+//                   stored; (median, i) wave-min picks the first least median.
+//   k_triangulation ORBmatcher::SearchForTriangulation_ (ORBmatcher.cc:1208-1433): one
+//                   workgroup per KeyFrame pair, one thread per KF1 feature of its
+//                   FeatureVector.  This fork never sets vbMatched2, so every KF1 feature's
+//                   search is independent: scan its node's KF2 list in order keeping the LAST
+//                   epipolar-consistent candidate of least distance (<= TH_LOW, `dist >
+//                   bestDist` rejects only larger ones), then the rotation histogram.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "common.hpp"
+
+namespace slamhot {
+namespace {
+
+constexpr int kDistThreads = 256;
+
+__device__ __forceinline__ int ham(const uint4 a0, const uint4 a1, const uint4 b0, const uint4 b1) {
+    return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+           __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+}
+
+__global__ void __launch_bounds__(kDistThreads) k_distinctive(int n_mp, const int32_t* off, const uint8_t* desc,
+                                                              int32_t* best) {
+    const int mpi = blockIdx.x * (kDistThreads / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (mpi >= n_mp) return;
+    const int o = off[mpi];
+    const int N = off[mpi + 1] - o;
+    if (N <= 0) {
+        if (lane == 0) best[mpi] = -1;
+        return;
+    }
+    const uint4* D = reinterpret_cast<const uint4*>(desc + (size_t)o * 32);
+    const int k = (N - 1) / 2;  // vDists[0.5*(N-1)]: the double index truncates
+    uint32_t key = 0xFFFFFFFFu;
+    for (int i = lane; i < N; i += 64) {
+        const uint4 a0 = D[2 * i], a1 = D[2 * i + 1];
+        // smallest v with #{j : d(i, j) <= v} > k  (d(i, i) = 0 counts, as Distances[i][i])
+        int lo = 0, hi = 256;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            int c = 0;
+            for (int j = 0; j < N; j++) c += ham(a0, a1, D[2 * j], D[2 * j + 1]) <= mid;
+            if (c > k) hi = mid;
+            else lo = mid + 1;
+        }
+        key = min(key, ((uint32_t)lo << 16) | (uint32_t)i);
+    }
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) key = min(key, (uint32_t)__shfl_xor((int)key, s, 64));
+    if (lane == 0) best[mpi] = (int32_t)(key & 0xFFFFu);
+}
+
+struct TriKF {
+    int n, n_nodes, nlevels;
+    const slam_keypoint* kps;
+    const float* uright;
+    const uint8_t* desc;
+    const uint8_t* has_mp;
+    const int32_t* node_id;
+    const int32_t* node_off;
+    const int32_t* node_feat;
+    float scale[16], sigma2[16];
+};
+
+constexpr int kTriThreads = 256;
+constexpr int kHisto = 30;
+
+__device__ __forceinline__ int rot_bin(float a, float b) {  // ORBmatcher.cc:1390-1396
+    float rot = a - b;
+    if (rot < 0.0f) rot += 360.0f;
+    int bin = (int)roundf(rot * (1.0f / kHisto));
+    if (bin == kHisto) bin = 0;
+    return bin;
+}
+
+// Pinhole::epipolarConstrain_ (Pinhole.cpp:159-181) with the call's F12
+__device__ __forceinline__ bool epipolar_ok(const float* F, const slam_keypoint& k1, const slam_keypoint& k2,
+                                            float unc) {
+    const float a = k1.x * F[0] + k1.y * F[3] + F[6];
+    const float b = k1.x * F[1] + k1.y * F[4] + F[7];
+    const float c = k1.x * F[2] + k1.y * F[5] + F[8];
+    const float num = a * k2.x + b * k2.y + c;
+    const float den = a * a + b * b;
+    if (den == 0) return false;
+    const float dsqr = num * num / den;
+    return (double)dsqr < 3.84 * (double)unc;
+}
+
+__global__ void __launch_bounds__(kTriThreads) k_triangulation(const TriKF* kfs, const slam_tri_pair* pairs,
+                                                              int check_ori, int cap, int32_t* match12,
+                                                              int32_t* nmatches) {
+    __shared__ int hist[kHisto];
+    __shared__ int nm;
+    __shared__ int keep[3];
+    const slam_tri_pair P = pairs[blockIdx.x];
+    const TriKF& A = kfs[P.kf1];
+    const TriKF& B = kfs[P.kf2];
+    int32_t* M = match12 + (size_t)blockIdx.x * cap;
+    const int t = threadIdx.x;
+    if (t < kHisto) hist[t] = 0;
+    if (t == 0) nm = 0;
+    for (int i = t; i < cap; i += kTriThreads) M[i] = -1;
+    __syncthreads();
+    const int total = A.n_nodes ? A.node_off[A.n_nodes] : 0;
+    for (int f = t; f < total; f += kTriThreads) {
+        // node of this entry (largest j with node_off[j] <= f)
+        int lo = 0, hi = A.n_nodes - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (A.node_off[mid] <= f) lo = mid;
+            else hi = mid - 1;
+        }
+        const int nid = A.node_id[lo];
+        int l2 = 0, h2 = B.n_nodes - 1, j2 = -1;
+        while (l2 <= h2) {
+            const int mid = (l2 + h2) >> 1;
+            const int v = B.node_id[mid];
+            if (v == nid) {
+                j2 = mid;
+                break;
+            }
+            if (v < nid) l2 = mid + 1;
+            else h2 = mid - 1;
+        }
+        if (j2 < 0) continue;
+        const int idx1 = A.node_feat[f];
+        if (A.has_mp[idx1]) continue;
+        const bool bStereo1 = A.uright && A.uright[idx1] >= 0;
+        if (P.only_stereo && !bStereo1) continue;
+        const slam_keypoint kp1 = A.kps[idx1];
+        const uint4* d1 = reinterpret_cast<const uint4*>(A.desc + (size_t)idx1 * 32);
+        const uint4 a0 = d1[0], a1 = d1[1];
+        int bestDist = 50, bestIdx2 = -1;  // TH_LOW
+        for (int c = B.node_off[j2]; c < B.node_off[j2 + 1]; c++) {
+            const int idx2 = B.node_feat[c];
+            if (B.has_mp[idx2]) continue;  // vbMatched2 is never set in this fork
+            const bool bStereo2 = B.uright && B.uright[idx2] >= 0;
+            if (P.only_stereo && !bStereo2) continue;
+            const uint4* d2 = reinterpret_cast<const uint4*>(B.desc + (size_t)idx2 * 32);
+            const int dist = ham(a0, a1, d2[0], d2[1]);
+            if (dist > 50 || dist > bestDist) continue;
+            const slam_keypoint kp2 = B.kps[idx2];
+            if (!bStereo1 && !bStereo2) {
+                const float distex = P.ep[0] - kp2.x;
+                const float distey = P.ep[1] - kp2.y;
+                if (distex * distex + distey * distey < 100 * B.scale[kp2.octave]) continue;
+            }
+            if (epipolar_ok(P.F12, kp1, kp2, B.sigma2[kp2.octave]) || P.coarse) {
+                bestIdx2 = idx2;
+                bestDist = dist;
+            }
+        }
+        if (bestIdx2 >= 0) {
+            M[idx1] = bestIdx2;
+            atomicAdd(&nm, 1);
+            if (check_ori) atomicAdd(&hist[rot_bin(kp1.angle, B.kps[bestIdx2].angle)], 1);
+        }
+    }
+    __syncthreads();
+    if (check_ori) {
+        if (t == 0) {  // ComputeThreeMaxima (ORBmatcher.cc:2515-2556)
+            int max1 = 0, max2 = 0, max3 = 0, i1 = -1, i2 = -1, i3 = -1;
+            for (int i = 0; i < kHisto; i++) {
+                const int s = hist[i];
+                if (s > max1) {
+                    max3 = max2; max2 = max1; max1 = s;
+                    i3 = i2; i2 = i1; i1 = i;
+                } else if (s > max2) {
+                    max3 = max2; max2 = s;
+                    i3 = i2; i2 = i;
+                } else if (s > max3) {
+                    max3 = s;
+                    i3 = i;
+                }
+            }
+            if (max2 < 0.1f * (float)max1) {
+                i2 = -1;
+                i3 = -1;
+            } else if (max3 < 0.1f * (float)max1) {
+                i3 = -1;
+            }
+            keep[0] = i1;
+            keep[1] = i2;
+            keep[2] = i3;
+        }
+        __syncthreads();
+        for (int i = t; i < A.n; i += kTriThreads) {
+            const int j = M[i];
+            if (j < 0) continue;
+            const int bin = rot_bin(A.kps[i].angle, B.kps[j].angle);
+            if (bin != keep[0] && bin != keep[1] && bin != keep[2]) {
+                M[i] = -1;
+                atomicSub(&nm, 1);
+            }
+        }
+        __syncthreads();
+    }
+    if (t == 0) nmatches[blockIdx.x] = nm;
+}
+
+struct DBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    slam_status ensure(size_t n) {
+        if (n <= cap) return SLAM_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        if (hipMalloc(&p, std::max<size_t>(n, 256)) != hipSuccess) return SLAM_ENOMEM;
+        cap = std::max<size_t>(n, 256);
+        return SLAM_OK;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+}  // namespace
+}  // namespace slamhot
+
+using namespace slamhot;
+
+struct slam_mapper {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    DBuf d_in, d_out;
+    std::mutex mu;
+};
+
+extern "C" {
+
+slam_status slamhot_mapper_create(int device, slam_mapper** out) {
+    if (!out) return SLAM_EINVAL;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return SLAM_ENODEV;
+    if (device < 0 || device >= n) return SLAM_EINVAL;
+    slam_mapper* m = new (std::nothrow) slam_mapper();
+    if (!m) return SLAM_ENOMEM;
+    m->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete m;
+        return SLAM_EHIP;
+    }
+    *out = m;
+    return SLAM_OK;
+}
+
+void slamhot_mapper_destroy(slam_mapper* m) {
+    if (!m) return;
+    (void)hipSetDevice(m->device);
+    if (m->stream) (void)hipStreamSynchronize(m->stream);
+    m->d_in.release();
+    m->d_out.release();
+    if (m->stream) (void)hipStreamDestroy(m->stream);
+    delete m;
+}
+
+slam_status slamhot_distinctive_descriptors(slam_mapper* m, int n_mp, const int32_t* off, const uint8_t* desc,
+                                            int32_t* best) {
+    if (!m || n_mp < 0 || (n_mp && (!off || !best))) return SLAM_EINVAL;
+    if (n_mp == 0) return SLAM_OK;
+    const int total = off[n_mp];
+    if (off[0] != 0 || total < 0 || (total && !desc)) return SLAM_EINVAL;
+    for (int i = 0; i < n_mp; i++)
+        if (off[i + 1] < off[i] || off[i + 1] - off[i] > 65535) return SLAM_EINVAL;
+    std::lock_guard<std::mutex> g(m->mu);
+    SLAM_HIP_TRY(hipSetDevice(m->device));
+    const size_t off_b = ((size_t)(n_mp + 1) * 4 + 255) & ~(size_t)255;
+    slam_status st;
+    if ((st = m->d_in.ensure(off_b + (size_t)total * 32)) || (st = m->d_out.ensure((size_t)n_mp * 4))) return st;
+    uint8_t* din = m->d_in.as<uint8_t>();
+    SLAM_HIP_TRY(hipMemcpyAsync(din, off, (size_t)(n_mp + 1) * 4, hipMemcpyHostToDevice, m->stream));
+    if (total) SLAM_HIP_TRY(hipMemcpyAsync(din + off_b, desc, (size_t)total * 32, hipMemcpyHostToDevice, m->stream));
+    const int per = kDistThreads / 64;
+    hipLaunchKernelGGL(k_distinctive, dim3((n_mp + per - 1) / per), dim3(kDistThreads), 0, m->stream, n_mp,
+                       (const int32_t*)din, (const uint8_t*)(din + off_b), m->d_out.as<int32_t>());
+    SLAM_HIP_TRY(hipGetLastError());
+    SLAM_HIP_TRY(hipMemcpyAsync(best, m->d_out.p, (size_t)n_mp * 4, hipMemcpyDeviceToHost, m->stream));
+    SLAM_HIP_TRY(hipStreamSynchronize(m->stream));
+    return SLAM_OK;
+}
+
+
+slam_status slamhot_search_for_triangulation(slam_mapper* m, int n_kfs, const slam_tri_kf* kfs, int n_pairs,
+                                             const slam_tri_pair* pairs, int check_ori, int cap,
+                                             int32_t* match12, int32_t* nmatches) {
+    if (!m || n_kfs < 0 || n_pairs < 0 || (n_pairs && (!kfs || !pairs || !match12 || !nmatches)) || cap < 0)
+        return SLAM_EINVAL;
+    if (n_pairs == 0) return SLAM_OK;
+    for (int k = 0; k < n_kfs; k++) {
+        const slam_tri_kf& K = kfs[k];
+        if (K.n < 0 || K.n_nodes < 0 || K.nlevels < 1 || K.nlevels > 16 || !K.scale || !K.level_sigma2) return SLAM_EINVAL;
+        if (K.n && (!K.kps_un || !K.desc || !K.has_mp)) return SLAM_EINVAL;
+        if (K.n_nodes && (!K.node_id || !K.node_off || !K.node_feat)) return SLAM_EINVAL;
+        if (K.n_nodes && (K.node_off[0] != 0 || K.node_off[K.n_nodes] < 0)) return SLAM_EINVAL;
+        for (int j = 0; j < K.n_nodes; j++)
+            if (K.node_off[j + 1] < K.node_off[j] || (j && K.node_id[j] <= K.node_id[j - 1])) return SLAM_EINVAL;
+        for (int f = 0; f < (K.n_nodes ? K.node_off[K.n_nodes] : 0); f++)
+            if (K.node_feat[f] < 0 || K.node_feat[f] >= K.n) return SLAM_EINVAL;
+        for (int i = 0; i < K.n; i++)
+            if (K.kps_un[i].octave < 0 || K.kps_un[i].octave >= K.nlevels) return SLAM_EINVAL;
+    }
+    for (int p = 0; p < n_pairs; p++) {
+        if (pairs[p].kf1 < 0 || pairs[p].kf1 >= n_kfs || pairs[p].kf2 < 0 || pairs[p].kf2 >= n_kfs) return SLAM_EINVAL;
+        if (kfs[pairs[p].kf1].n > cap) return SLAM_ECAP;
+    }
+    std::lock_guard<std::mutex> g(m->mu);
+    SLAM_HIP_TRY(hipSetDevice(m->device));
+    // one staging blob: KF arrays, KF records, pairs
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    size_t need = al(sizeof(TriKF) * n_kfs) + al(sizeof(slam_tri_pair) * n_pairs);
+    for (int k = 0; k < n_kfs; k++) {
+        const slam_tri_kf& K = kfs[k];
+        const int nf = K.n_nodes ? K.node_off[K.n_nodes] : 0;
+        need += al(sizeof(slam_keypoint) * K.n) + al(4 * (size_t)K.n) + al(32 * (size_t)K.n) + al(K.n) +
+                al(4 * (size_t)K.n_nodes) + al(4 * (size_t)(K.n_nodes + 1)) + al(4 * (size_t)nf);
+    }
+    slam_status st;
+    if ((st = m->d_in.ensure(need)) || (st = m->d_out.ensure((size_t)n_pairs * cap * 4 + 4 * (size_t)n_pairs + 256)))
+        return st;
+    std::vector<uint8_t> host(need);
+    size_t off = 0;
+    uint8_t* dbase = m->d_in.as<uint8_t>();
+    auto put = [&](const void* src, size_t bytes) -> const void* {
+        if (!src || !bytes) return nullptr;
+        std::memcpy(host.data() + off, src, bytes);
+        const void* d = dbase + off;
+        off += al(bytes);
+        return d;
+    };
+    std::vector<TriKF> recs(n_kfs);
+    std::vector<float> ur_default;
+    for (int k = 0; k < n_kfs; k++) {
+        const slam_tri_kf& K = kfs[k];
+        TriKF& R = recs[k];
+        R.n = K.n;
+        R.n_nodes = K.n_nodes;
+        R.nlevels = K.nlevels;
+        R.kps = (const slam_keypoint*)put(K.kps_un, sizeof(slam_keypoint) * K.n);
+        R.uright = (const float*)put(K.uright, 4 * (size_t)K.n);
+        R.desc = (const uint8_t*)put(K.desc, 32 * (size_t)K.n);
+        R.has_mp = (const uint8_t*)put(K.has_mp, K.n);
+        R.node_id = (const int32_t*)put(K.node_id, 4 * (size_t)K.n_nodes);
+        R.node_off = (const int32_t*)put(K.node_off, K.n_nodes ? 4 * (size_t)(K.n_nodes + 1) : 0);
+        R.node_feat = (const int32_t*)put(K.node_feat, K.n_nodes ? 4 * (size_t)K.node_off[K.n_nodes] : 0);
+        for (int l = 0; l < 16; l++) {
+            R.scale[l] = l < K.nlevels ? K.scale[l] : 1.0f;
+            R.sigma2[l] = l < K.nlevels ? K.level_sigma2[l] : 1.0f;
+        }
+    }
+    const TriKF* d_recs = (const TriKF*)put(recs.data(), sizeof(TriKF) * n_kfs);
+    const slam_tri_pair* d_pairs = (const slam_tri_pair*)put(pairs, sizeof(slam_tri_pair) * n_pairs);
+    SLAM_HIP_TRY(hipMemcpyAsync(dbase, host.data(), off, hipMemcpyHostToDevice, m->stream));
+    int32_t* d_m12 = m->d_out.as<int32_t>();
+    int32_t* d_nm = d_m12 + (size_t)n_pairs * cap;
+    hipLaunchKernelGGL(k_triangulation, dim3(n_pairs), dim3(kTriThreads), 0, m->stream, d_recs, d_pairs, check_ori,
+                       cap, d_m12, d_nm);
+    SLAM_HIP_TRY(hipGetLastError());
+    SLAM_HIP_TRY(hipMemcpyAsync(match12, d_m12, (size_t)n_pairs * cap * 4, hipMemcpyDeviceToHost, m->stream));
+    SLAM_HIP_TRY(hipMemcpyAsync(nmatches, d_nm, (size_t)n_pairs * 4, hipMemcpyDeviceToHost, m->stream));
+    SLAM_HIP_TRY(hipStreamSynchronize(m->stream));
+    return SLAM_OK;
+}
+
+}  // extern "C"

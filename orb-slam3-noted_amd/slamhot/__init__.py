@@ -757,3 +757,107 @@ def ComputeStereoMatches(left: ORBextractor, right: ORBextractor, images_left, i
         out.append((kl_h[f, :a].ravel().copy(), dl_h[f, :a].copy(), kr_h[f, :b].ravel().copy(), dr_h[f, :b].copy(),
                     ur[f, :a].copy(), dep[f, :a].copy()))
     return out
+
+
+# ------------------------------------------------------------------ LocalMapping matchers
+class TriKF(C.Structure):
+    _fields_ = [("n", I), ("kps_un", P), ("uright", P), ("desc", P), ("has_mp", P), ("n_nodes", I),
+                ("node_id", P), ("node_off", P), ("node_feat", P), ("nlevels", I), ("scale", P),
+                ("level_sigma2", P)]
+
+
+class TriPair(C.Structure):
+    _fields_ = [("kf1", I), ("kf2", I), ("F12", C.c_float * 9), ("ep", C.c_float * 2), ("only_stereo", C.c_uint8),
+                ("coarse", C.c_uint8), ("pad", C.c_uint8 * 2)]
+
+
+def make_tri_kf(kf: dict):
+    """slam_tri_kf from a dict: kps_un (KP_DTYPE), uright, desc, has_mp, node_id/node_off/node_feat
+    (mFeatVec CSR), scale, level_sigma2.  Returns (struct, keepalive)."""
+    keep = dict(kps=np.ascontiguousarray(kf["kps_un"], KP_DTYPE), desc=np.ascontiguousarray(kf["desc"], np.uint8),
+                has=np.ascontiguousarray(kf["has_mp"], np.uint8),
+                nid=np.ascontiguousarray(kf["node_id"], np.int32), noff=np.ascontiguousarray(kf["node_off"], np.int32),
+                nf=np.ascontiguousarray(kf["node_feat"], np.int32), sc=np.ascontiguousarray(kf["scale"], np.float32),
+                s2=np.ascontiguousarray(kf["level_sigma2"], np.float32))
+    ur = kf.get("uright")
+    keep["ur"] = None if ur is None else np.ascontiguousarray(ur, np.float32)
+    t = TriKF()
+    t.n = len(keep["kps"])
+    t.kps_un = keep["kps"].ctypes.data if t.n else None
+    t.uright = keep["ur"].ctypes.data if keep["ur"] is not None and t.n else None
+    t.desc = keep["desc"].ctypes.data if t.n else None
+    t.has_mp = keep["has"].ctypes.data if t.n else None
+    t.n_nodes = len(keep["nid"])
+    t.node_id = keep["nid"].ctypes.data if t.n_nodes else None
+    t.node_off = keep["noff"].ctypes.data if t.n_nodes else None
+    t.node_feat = keep["nf"].ctypes.data if len(keep["nf"]) else None
+    t.nlevels = len(keep["sc"])
+    t.scale = keep["sc"].ctypes.data
+    t.level_sigma2 = keep["s2"].ctypes.data
+    return t, keep
+
+
+def make_tri_pair(kf1: int, kf2: int, F12, ep, only_stereo=False, coarse=False):
+    p = TriPair()
+    p.kf1, p.kf2 = kf1, kf2
+    p.F12[:] = [float(v) for v in np.asarray(F12, np.float32).ravel()]
+    p.ep[:] = [float(v) for v in np.asarray(ep, np.float32).ravel()]
+    p.only_stereo, p.coarse = int(only_stereo), int(coarse)
+    return p
+
+
+class Mapper:
+    """Device LocalMapping matchers: MapPoint::ComputeDistinctiveDescriptors (batched over
+    MapPoints), ORBmatcher::SearchForTriangulation_ and ORBmatcher::Fuse candidate search."""
+
+    def __init__(self, device: int = 0):
+        L = lib()
+        if not getattr(L, "_mapper_ready", False):
+            L.slamhot_mapper_create.argtypes = [I, C.POINTER(P)]
+            L.slamhot_mapper_destroy.argtypes = [P]
+            L.slamhot_mapper_destroy.restype = None
+            L.slamhot_distinctive_descriptors.argtypes = [P, I, P, P, P]
+            L.slamhot_search_for_triangulation.argtypes = [P, I, C.POINTER(TriKF), I, C.POINTER(TriPair), I, I, P, P]
+            L._mapper_ready = True
+        h = P()
+        check(L.slamhot_mapper_create(device, C.byref(h)), "mapper_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().slamhot_mapper_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def ComputeDistinctiveDescriptors(self, off, desc):
+        """off: int32 (n_mp + 1) CSR offsets into desc (total x 32 u8).  Returns best index
+        per MapPoint (relative to its first descriptor), -1 when it has none."""
+        off = np.ascontiguousarray(off, np.int32)
+        desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        best = np.zeros(len(off) - 1, np.int32)
+        check(lib().slamhot_distinctive_descriptors(self._h, len(off) - 1, _ptr(off), _ptr(desc) if len(desc) else None,
+                                                    _ptr(best)), "distinctive_descriptors")
+        return best
+
+    def SearchForTriangulation(self, kfs, pairs, check_ori=False):
+        """kfs: list of KeyFrame dicts (make_tri_kf); pairs: list of (kf1, kf2, F12, ep,
+        only_stereo, coarse).  Returns [(nmatches, vMatchedPairs as an (m, 2) array)]."""
+        built = [make_tri_kf(k) for k in kfs]
+        K = (TriKF * max(1, len(built)))(*[b[0] for b in built])
+        Ps = (TriPair * max(1, len(pairs)))(*[make_tri_pair(*p) for p in pairs])
+        cap = max([b[0].n for b in built] + [1])
+        m12 = np.full((len(pairs), cap), -1, np.int32)
+        nm = np.zeros(len(pairs), np.int32)
+        check(lib().slamhot_search_for_triangulation(self._h, len(built), K, len(pairs), Ps, int(check_ori), cap,
+                                                     _ptr(m12), _ptr(nm)), "search_for_triangulation")
+        out = []
+        for p, (a, *_rest) in enumerate(pairs):
+            row = m12[p, : built[a][0].n]
+            i1 = np.flatnonzero(row >= 0)
+            out.append((int(nm[p]), np.stack([i1, row[i1]], 1).astype(np.int64)))
+        return out

@@ -363,3 +363,30 @@ def is_in_frustum(fv, geom, view_cos_limit=0.5):
 
 def check_predict_scale(lo, hi, log_scale):
     return int(_frlib().oracle_check_predict_scale(lo, hi, log_scale))
+
+
+# ---- LocalMapping matchers (oracle/mapping_oracle.cpp)
+def distinctive_descriptors(off, desc):
+    L = lib()
+    if not hasattr(L, "_dd_ready"):
+        L.oracle_distinctive_descriptors.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.oracle_distinctive_descriptors.restype = None
+        L._dd_ready = True
+    off = np.ascontiguousarray(off, np.int32)
+    desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+    best = np.zeros(len(off) - 1, np.int32)
+    L.oracle_distinctive_descriptors(len(off) - 1, _ptr(off), _ptr(desc), _ptr(best))
+    return best
+
+
+def search_for_triangulation(kf1, kf2, pair, check_ori=False):
+    """(nmatches, match12) for one pair; kf1/kf2 are slamhot.TriKF structs, pair a TriPair."""
+    L = lib()
+    if not hasattr(L, "_tri_ready"):
+        L.oracle_search_for_triangulation.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
+        L.oracle_search_for_triangulation.restype = C.c_int
+        L._tri_ready = True
+    m12 = np.full(max(1, kf1.n), -1, np.int32)
+    n = L.oracle_search_for_triangulation(C.addressof(kf1), C.addressof(kf2), C.addressof(pair), int(check_ori),
+                                          _ptr(m12))
+    return n, m12[: kf1.n]

@@ -173,3 +173,65 @@ def local_map_geom(S, n_extra=300, boundary_frac=0.15):
     desc = np.concatenate([flip_bits(d[sel], rng, 40), flip_bits(d[rng.integers(0, n, n_extra)], rng, 90)])
     order = rng.permutation(m)
     return geom[order], desc[order]
+
+
+def _Rt(T):
+    return T[:3, :3].astype(np.float64), T[:3, 3].astype(np.float64)
+
+
+def tri_keyframes(seed, n_kf=4, n_pts=1500, n_nodes=400):
+    """KeyFrames around a common point cloud for SearchForTriangulation_: features are noisy
+    projections of shared points (descriptor = point pattern + a few flipped bits, FeatureVector
+    node = point id hash, so corresponding features share nodes), plus clutter; ~30% already
+    have a MapPoint, ~40% are stereo.  Returns (kfs dicts, poses)."""
+    rng = np.random.default_rng(seed)
+    sc, isig, _ = synth._level_tables()
+    sigma2 = (sc * sc).astype(np.float32)
+    P = np.stack([rng.uniform(-4, 4, n_pts), rng.uniform(-2.5, 2.5, n_pts), rng.uniform(3, 15, n_pts)], 1)
+    base = rng.integers(0, 256, (n_pts, 32), dtype=np.uint8)
+    node_of_pt = rng.integers(0, n_nodes, n_pts)
+    kfs, poses = [], []
+    for k in range(n_kf):
+        T = pose(rot(*rng.normal(0, 0.04, 3)), np.array([0.25 * k, rng.normal(0, 0.05), rng.normal(0, 0.1)]))
+        R, t = _Rt(T)
+        Xc = P @ R.T + t
+        u = FX * Xc[:, 0] / Xc[:, 2] + CX
+        v = FY * Xc[:, 1] / Xc[:, 2] + CY
+        vis = np.flatnonzero((Xc[:, 2] > 0.5) & (u > 5) & (u < 747) & (v > 5) & (v < 475) & (rng.random(n_pts) < 0.8))
+        nclut = 200
+        n = len(vis) + nclut
+        kps = np.zeros(n, slamhot.KP_DTYPE)
+        kps["x"][: len(vis)] = u[vis] + rng.normal(0, 0.7, len(vis))
+        kps["y"][: len(vis)] = v[vis] + rng.normal(0, 0.7, len(vis))
+        kps["x"][len(vis):] = rng.uniform(5, 747, nclut)
+        kps["y"][len(vis):] = rng.uniform(5, 475, nclut)
+        kps["octave"] = rng.integers(0, 8, n)
+        kps["angle"] = np.concatenate([(rng.normal(90, 6, len(vis))) % 360, rng.uniform(0, 360, nclut)])
+        desc = np.concatenate([flip_bits(base[vis], rng, 12), rng.integers(0, 256, (nclut, 32), dtype=np.uint8)])
+        ur = np.full(n, -1, np.float32)
+        st = rng.random(n) < 0.4
+        ur[: len(vis)][st[: len(vis)]] = (kps["x"][: len(vis)] - BF / Xc[vis, 2].astype(np.float32))[st[: len(vis)]]
+        has_mp = (rng.random(n) < 0.3).astype(np.uint8)
+        nid = np.concatenate([node_of_pt[vis], rng.integers(0, n_nodes, nclut)])
+        order = rng.permutation(n)
+        kps, desc, ur, has_mp, nid = kps[order], desc[order], ur[order], has_mp[order], nid[order]
+        uniq, noff, nfeat = synth.feature_vector(nid, np.ones(n))
+        kfs.append(dict(kps_un=kps, desc=desc, uright=ur, has_mp=has_mp, node_id=uniq.astype(np.int32),
+                        node_off=noff, node_feat=nfeat.astype(np.int32), scale=sc, level_sigma2=sigma2))
+        poses.append(T)
+    return kfs, poses
+
+
+def f12_ep(T1, T2):
+    """LocalMapping::ComputeF12_ and the epipole of KF1's centre in KF2 (float64, rounded once)."""
+    R1, t1 = _Rt(T1)
+    R2, t2 = _Rt(T2)
+    R12 = R1 @ R2.T
+    t12 = -R1 @ R2.T @ t2 + t1
+    tx = np.array([[0, -t12[2], t12[1]], [t12[2], 0, -t12[0]], [-t12[1], t12[0], 0]])
+    K = np.array([[FX, 0, CX], [0, FY, CY], [0, 0, 1]], np.float64)
+    F12 = np.linalg.inv(K.T) @ tx @ R12 @ np.linalg.inv(K)
+    C1 = -R1.T @ t1
+    C2 = R2 @ C1 + t2
+    ep = np.array([FX * C2[0] / C2[2] + CX, FY * C2[1] / C2[2] + CY])
+    return F12.astype(np.float32), ep.astype(np.float32)
