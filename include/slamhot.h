@@ -476,6 +476,21 @@ slam_status slamhot_search_for_triangulation(slam_mapper* mp, int n_kfs, const s
                                              const slam_tri_pair* pairs, int check_ori, int cap,
                                              int32_t* match12, int32_t* nmatches);
 
+/* int ORBmatcher::Fuse(KeyFrame* pKF, const vector<MapPoint*>& vpMapPoints, float th, bool bRight)
+ * (ORBmatcher.cc:1629-1818, bRight = false, NLeft == -1), search half: for every MapPoint the
+ * projection into pKF, distance / viewing-angle gates, PredictScale, GetFeaturesInArea and the
+ * chi2-gated best descriptor (first least distance in the reference's candidate order).
+ * KF: the KeyFrame as a frame view (kps_un, uright, desc, grid bounds, Tcw, camera, level
+ * tables; mp_state unused); inv_level_sigma2 = mvInvLevelSigma2.  mps: pos / normal / distances /
+ * is_bad, seen = IsInKeyFrame(pKF).  Outputs: best_idx[i] (-1 = skipped or no candidate),
+ * best_dist[i] (256 = none).  MapPoint i fuses iff best_dist[i] <= TH_LOW (50), applied in list
+ * order by the caller (Replace / AddObservation, :1789-1812) — the search never depends on those
+ * updates: they change only the skip flags (isBad, IsInKeyFrame), which the caller re-checks, and
+ * the descriptors of MapPoints already processed or already in pKF. */
+slam_status slamhot_fuse_search(slam_mapper* mp, const slam_frame_view* KF, const float* inv_level_sigma2,
+                                int n_mp, const slam_mp_geom* mps, const uint8_t* mp_desc, float th,
+                                int32_t* best_idx, int32_t* best_dist);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,7 +1,8 @@
 /*
  * mapping_oracle.cpp — CPU restatement of the LocalMapping matchers:
  * MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:349-423), ORBmatcher::SearchForTriangulation_
- * (ORBmatcher.cc:1208-1433, pinhole KeyFrames).  TEST INFRASTRUCTURE ONLY
+ * (ORBmatcher.cc:1208-1433, pinhole KeyFrames), the search half of ORBmatcher::Fuse
+ * (ORBmatcher.cc:1629-1788).  TEST INFRASTRUCTURE ONLY
  * (see oracle.h).  Parity unpinned (no reference fixtures for these functions).
  */
 #include <algorithm>
@@ -161,6 +162,89 @@ void oracle_distinctive_descriptors(int n_mp, const int32_t* off, const uint8_t*
             }
         }
         best[m] = BestIdx;
+    }
+}
+
+/* ORBmatcher::Fuse (ORBmatcher.cc:1629-1788), search half, one MapPoint at a time in list order
+ * (bRight = false, NLeft == -1): best_idx / best_dist per MapPoint. */
+void oracle_fuse_search(const slam_frame_view* F, const float* inv_level_sigma2, int n_mp, const slam_mp_geom* mps,
+                        const uint8_t* mp_desc, float th, int32_t* best_idx, int32_t* best_dist) {
+    const int GRID_COLS = 64, GRID_ROWS = 48;
+    std::vector<std::vector<int>> grid(GRID_COLS * GRID_ROWS);  // KeyFrame::mGrid
+    for (int i = 0; i < F->n; i++) {
+        const int px = (int)std::round((F->kps_un[i].x - F->min_x) * F->grid_inv_w);
+        const int py = (int)std::round((F->kps_un[i].y - F->min_y) * F->grid_inv_h);
+        if (px < 0 || px >= GRID_COLS || py < 0 || py >= GRID_ROWS) continue;
+        grid[px * GRID_ROWS + py].push_back(i);
+    }
+    const float* T = F->Tcw;
+    float Ow[3];
+    for (int r = 0; r < 3; r++) {
+        const double acc = (double)T[r] * T[3] + (double)T[4 + r] * T[7] + (double)T[8 + r] * T[11];
+        Ow[r] = (float)(-1.0 * acc);
+    }
+    for (int i = 0; i < n_mp; i++) {
+        const slam_mp_geom& g = mps[i];
+        best_idx[i] = -1;
+        best_dist[i] = 256;
+        if (g.is_bad || g.seen) continue;
+        float p3Dc[3];  // Rcw * p3Dw + tcw (cv::Mat gemm: double accumulation)
+        for (int r = 0; r < 3; r++) {
+            const double acc = (double)T[4 * r] * g.pos[0] + (double)T[4 * r + 1] * g.pos[1] + (double)T[4 * r + 2] * g.pos[2];
+            p3Dc[r] = (float)(acc * 1.0 + (double)T[4 * r + 3] * 1.0);
+        }
+        if (p3Dc[2] < 0.0f) continue;
+        const float invz = 1 / p3Dc[2];
+        const float x = p3Dc[0], y = p3Dc[1], z = p3Dc[2];
+        const float u = F->fx * x / z + F->cx, v = F->fy * y / z + F->cy;
+        if (!(u >= F->min_x && u < F->max_x && v >= F->min_y && v < F->max_y)) continue;
+        const float ur = u - F->bf * invz;
+        const float maxDistance = 1.2f * g.max_dist;
+        const float minDistance = 0.8f * g.min_dist;
+        const float PO[3] = {g.pos[0] - Ow[0], g.pos[1] - Ow[1], g.pos[2] - Ow[2]};
+        const float dist3D = (float)std::sqrt((double)PO[0] * PO[0] + (double)PO[1] * PO[1] + (double)PO[2] * PO[2]);
+        if (dist3D < minDistance || dist3D > maxDistance) continue;
+        const double dot = (double)PO[0] * g.normal[0] + (double)PO[1] * g.normal[1] + (double)PO[2] * g.normal[2];
+        if (dot < 0.5 * dist3D) continue;
+        const float ratio = g.max_dist / dist3D;
+        int nPredictedLevel = (int)std::ceil(std::log(ratio) / F->log_scale);  // logf
+        if (nPredictedLevel < 0) nPredictedLevel = 0;
+        else if (nPredictedLevel >= F->nlevels) nPredictedLevel = F->nlevels - 1;
+        const float radius = th * F->scale[nPredictedLevel];
+        std::vector<int> vIndices;  // KeyFrame::GetFeaturesInArea (KeyFrame.cc:737-781)
+        const int nMinCellX = std::max(0, (int)std::floor((u - F->min_x - radius) * F->grid_inv_w));
+        const int nMaxCellX = std::min(GRID_COLS - 1, (int)std::ceil((u - F->min_x + radius) * F->grid_inv_w));
+        const int nMinCellY = std::max(0, (int)std::floor((v - F->min_y - radius) * F->grid_inv_h));
+        const int nMaxCellY = std::min(GRID_ROWS - 1, (int)std::ceil((v - F->min_y + radius) * F->grid_inv_h));
+        if (nMinCellX < GRID_COLS && nMaxCellX >= 0 && nMinCellY < GRID_ROWS && nMaxCellY >= 0)
+            for (int ix = nMinCellX; ix <= nMaxCellX; ix++)
+                for (int iy = nMinCellY; iy <= nMaxCellY; iy++)
+                    for (int idx : grid[ix * GRID_ROWS + iy]) {
+                        const float distx = F->kps_un[idx].x - u, disty = F->kps_un[idx].y - v;
+                        if (std::fabs(distx) < radius && std::fabs(disty) < radius) vIndices.push_back(idx);
+                    }
+        int bestDist = 256, bestIdx = -1;
+        for (int idx : vIndices) {
+            const slam_keypoint& kp = F->kps_un[idx];
+            const int kpLevel = kp.octave;
+            if (kpLevel < nPredictedLevel - 1 || kpLevel > nPredictedLevel) continue;
+            if (F->uright && F->uright[idx] >= 0) {
+                const float ex = u - kp.x, ey = v - kp.y, er = ur - F->uright[idx];
+                const float e2 = ex * ex + ey * ey + er * er;
+                if (e2 * inv_level_sigma2[kpLevel] > 7.8) continue;
+            } else {
+                const float ex = u - kp.x, ey = v - kp.y;
+                const float e2 = ex * ex + ey * ey;
+                if (e2 * inv_level_sigma2[kpLevel] > 5.99) continue;
+            }
+            const int dist = hamming32(mp_desc + 32 * (size_t)i, F->desc + 32 * (size_t)idx);
+            if (dist < bestDist) {
+                bestDist = dist;
+                bestIdx = idx;
+            }
+        }
+        best_idx[i] = bestIdx;
+        best_dist[i] = bestDist;
     }
 }
 

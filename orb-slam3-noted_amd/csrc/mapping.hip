@@ -11,9 +11,15 @@
 //                   search is independent: scan its node's KF2 list in order keeping the LAST
 //                   epipolar-consistent candidate of least distance (<= TH_LOW, `dist >
 //                   bestDist` rejects only larger ones), then the rotation histogram.
+//   k_fuse_search   ORBmatcher::Fuse (ORBmatcher.cc:1629-1818) search half, one thread per
+//                   MapPoint: cv::Mat products as double accumulation rounded once (as the
+//                   projection matchers), PredictScale with the correctly rounded logf, the
+//                   KeyFrame grid walked in the reference's order (ix outer, iy inner, cell
+//                   insertion order), chi2 gates 7.8 / 5.99, first least Hamming distance.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -211,6 +217,101 @@ __global__ void __launch_bounds__(kTriThreads) k_triangulation(const TriKF* kfs,
     if (t == 0) nmatches[blockIdx.x] = nm;
 }
 
+constexpr int kGridCols = 64, kGridRows = 48;  // FRAME_GRID_COLS / ROWS (Frame.h:42-43)
+constexpr int kFuseThreads = 128;
+
+struct FuseKF {
+    float T[12];  // Rcw | tcw row-major
+    float Ow[3];
+    float fx, fy, cx, cy, bf;
+    float min_x, min_y, max_x, max_y, inv_w, inv_h;
+    float log_scale;
+    int nlevels, n;
+    float scale[16], inv_sigma2[16];
+    const slam_keypoint* kps;
+    const float* uright;
+    const uint8_t* desc;
+    const int32_t* cell_start;  // kGridCols * kGridRows + 1, cells [ix][iy]
+    const int32_t* cell_feat;
+};
+
+__global__ void __launch_bounds__(kFuseThreads) k_fuse_search(FuseKF K, int n_mp, const slam_mp_geom* mps,
+                                                              const uint8_t* mp_desc, float th, int32_t* best_idx,
+                                                              int32_t* best_dist) {
+    const int i = blockIdx.x * kFuseThreads + threadIdx.x;
+    if (i >= n_mp) return;
+    const slam_mp_geom g = mps[i];
+    int bestDist = 256, bestIdx = -1;
+    do {
+        if (g.is_bad || g.seen) break;  // isBad(), IsInKeyFrame(pKF)
+        float p3Dc[3];
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            const double acc = (double)K.T[4 * r] * (double)g.pos[0] + (double)K.T[4 * r + 1] * (double)g.pos[1] +
+                               (double)K.T[4 * r + 2] * (double)g.pos[2];
+            p3Dc[r] = (float)(acc * 1.0 + (double)K.T[4 * r + 3] * 1.0);
+        }
+        if (p3Dc[2] < 0.0f) break;
+        const float invz = 1 / p3Dc[2];
+        const float u = K.fx * p3Dc[0] / p3Dc[2] + K.cx;  // Pinhole::project
+        const float v = K.fy * p3Dc[1] / p3Dc[2] + K.cy;
+        if (!(u >= K.min_x && u < K.max_x && v >= K.min_y && v < K.max_y)) break;  // KeyFrame::IsInImage
+        const float ur = u - K.bf * invz;
+        const float maxDistance = 1.2f * g.max_dist;
+        const float minDistance = 0.8f * g.min_dist;
+        const float PO[3] = {g.pos[0] - K.Ow[0], g.pos[1] - K.Ow[1], g.pos[2] - K.Ow[2]};
+        const float dist3D = (float)sqrt((double)PO[0] * PO[0] + (double)PO[1] * PO[1] + (double)PO[2] * PO[2]);
+        if (dist3D < minDistance || dist3D > maxDistance) break;
+        const double dot = (double)PO[0] * g.normal[0] + (double)PO[1] * g.normal[1] + (double)PO[2] * g.normal[2];
+        if (dot < 0.5 * dist3D) break;
+        const float ratio = g.max_dist / dist3D;
+        int level = (int)ceilf((float)log((double)ratio) / K.log_scale);
+        if (level < 0) level = 0;
+        else if (level >= K.nlevels) level = K.nlevels - 1;
+        const float radius = th * K.scale[level];
+        // KeyFrame::GetFeaturesInArea (KeyFrame.cc:737-781)
+        const int nMinCellX = max(0, (int)floorf((u - K.min_x - radius) * K.inv_w));
+        if (nMinCellX >= kGridCols) break;
+        const int nMaxCellX = min(kGridCols - 1, (int)ceilf((u - K.min_x + radius) * K.inv_w));
+        if (nMaxCellX < 0) break;
+        const int nMinCellY = max(0, (int)floorf((v - K.min_y - radius) * K.inv_h));
+        if (nMinCellY >= kGridRows) break;
+        const int nMaxCellY = min(kGridRows - 1, (int)ceilf((v - K.min_y + radius) * K.inv_h));
+        if (nMaxCellY < 0) break;
+        const uint4* dm = reinterpret_cast<const uint4*>(mp_desc + (size_t)i * 32);
+        const uint4 a0 = dm[0], a1 = dm[1];
+        for (int ix = nMinCellX; ix <= nMaxCellX; ix++)
+            for (int iy = nMinCellY; iy <= nMaxCellY; iy++) {
+                const int c = ix * kGridRows + iy;
+                for (int e = K.cell_start[c]; e < K.cell_start[c + 1]; e++) {
+                    const int idx = K.cell_feat[e];
+                    const slam_keypoint kp = K.kps[idx];
+                    if (!(fabsf(kp.x - u) < radius && fabsf(kp.y - v) < radius)) continue;
+                    const int kpLevel = kp.octave;
+                    if (kpLevel < level - 1 || kpLevel > level) continue;
+                    const float kpr = K.uright ? K.uright[idx] : -1.0f;
+                    if (kpr >= 0) {
+                        const float ex = u - kp.x, ey = v - kp.y, er = ur - kpr;
+                        const float e2 = ex * ex + ey * ey + er * er;
+                        if ((double)(e2 * K.inv_sigma2[kpLevel]) > 7.8) continue;
+                    } else {
+                        const float ex = u - kp.x, ey = v - kp.y;
+                        const float e2 = ex * ex + ey * ey;
+                        if ((double)(e2 * K.inv_sigma2[kpLevel]) > 5.99) continue;
+                    }
+                    const uint4* dk = reinterpret_cast<const uint4*>(K.desc + (size_t)idx * 32);
+                    const int dist = ham(a0, a1, dk[0], dk[1]);
+                    if (dist < bestDist) {
+                        bestDist = dist;
+                        bestIdx = idx;
+                    }
+                }
+            }
+    } while (false);
+    best_idx[i] = bestIdx;
+    best_dist[i] = bestDist;
+}
+
 struct DBuf {
     void* p = nullptr;
     size_t cap = 0;
@@ -375,6 +476,91 @@ slam_status slamhot_search_for_triangulation(slam_mapper* m, int n_kfs, const sl
     SLAM_HIP_TRY(hipGetLastError());
     SLAM_HIP_TRY(hipMemcpyAsync(match12, d_m12, (size_t)n_pairs * cap * 4, hipMemcpyDeviceToHost, m->stream));
     SLAM_HIP_TRY(hipMemcpyAsync(nmatches, d_nm, (size_t)n_pairs * 4, hipMemcpyDeviceToHost, m->stream));
+    SLAM_HIP_TRY(hipStreamSynchronize(m->stream));
+    return SLAM_OK;
+}
+
+
+slam_status slamhot_fuse_search(slam_mapper* m, const slam_frame_view* F, const float* inv_level_sigma2, int n_mp,
+                                const slam_mp_geom* mps, const uint8_t* mp_desc, float th, int32_t* best_idx,
+                                int32_t* best_dist) {
+    if (!m || !F || !F->Tcw || !inv_level_sigma2 || F->n < 0 || F->nlevels < 1 || F->nlevels > 16 || !F->scale ||
+        (F->n && (!F->kps_un || !F->desc)) || n_mp < 0 || (n_mp && (!mps || !mp_desc || !best_idx || !best_dist)))
+        return SLAM_EINVAL;
+    if (n_mp == 0) return SLAM_OK;
+    for (int i = 0; i < F->n; i++)
+        if (F->kps_un[i].octave < 0 || F->kps_un[i].octave >= F->nlevels) return SLAM_EINVAL;
+    // KeyFrame grid (Frame::AssignFeaturesToGrid, copied into the KeyFrame) as CSR
+    const int ncell = kGridCols * kGridRows;
+    std::vector<int32_t> cell(F->n, -1), start(ncell + 1, 0), feat(std::max(1, F->n));
+    for (int i = 0; i < F->n; i++) {
+        const int px = (int)std::round((F->kps_un[i].x - F->min_x) * F->grid_inv_w);
+        const int py = (int)std::round((F->kps_un[i].y - F->min_y) * F->grid_inv_h);
+        if (px < 0 || px >= kGridCols || py < 0 || py >= kGridRows) continue;
+        cell[i] = px * kGridRows + py;
+        start[cell[i] + 1]++;
+    }
+    for (int c = 0; c < ncell; c++) start[c + 1] += start[c];
+    std::vector<int32_t> fill(start.begin(), start.end() - 1);
+    for (int i = 0; i < F->n; i++)
+        if (cell[i] >= 0) feat[fill[cell[i]]++] = i;
+    FuseKF K{};
+    const float* T = F->Tcw;
+    for (int r = 0; r < 3; r++) {
+        for (int c = 0; c < 4; c++) K.T[4 * r + c] = T[4 * r + c];
+        const double acc = (double)T[r] * T[3] + (double)T[4 + r] * T[7] + (double)T[8 + r] * T[11];
+        K.Ow[r] = (float)(-1.0 * acc);  // KeyFrame::GetCameraCenter: -Rcw^T tcw as a cv::Mat product
+    }
+    K.fx = F->fx;
+    K.fy = F->fy;
+    K.cx = F->cx;
+    K.cy = F->cy;
+    K.bf = F->bf;
+    K.min_x = F->min_x;
+    K.min_y = F->min_y;
+    K.max_x = F->max_x;
+    K.max_y = F->max_y;
+    K.inv_w = F->grid_inv_w;
+    K.inv_h = F->grid_inv_h;
+    K.log_scale = F->log_scale;
+    K.nlevels = F->nlevels;
+    K.n = F->n;
+    for (int l = 0; l < 16; l++) {
+        K.scale[l] = l < F->nlevels ? F->scale[l] : 1.0f;
+        K.inv_sigma2[l] = l < F->nlevels ? inv_level_sigma2[l] : 1.0f;
+    }
+    std::lock_guard<std::mutex> g(m->mu);
+    SLAM_HIP_TRY(hipSetDevice(m->device));
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t need = al(sizeof(slam_keypoint) * F->n) + al(4 * (size_t)F->n) + al(32 * (size_t)F->n) +
+                        al(4 * start.size()) + al(4 * feat.size()) + al(sizeof(slam_mp_geom) * n_mp) + al(32 * (size_t)n_mp);
+    slam_status st;
+    if ((st = m->d_in.ensure(need)) || (st = m->d_out.ensure(8 * (size_t)n_mp))) return st;
+    std::vector<uint8_t> host(need);
+    size_t off = 0;
+    uint8_t* dbase = m->d_in.as<uint8_t>();
+    auto put = [&](const void* src, size_t bytes) -> const void* {
+        if (!src || !bytes) return nullptr;
+        std::memcpy(host.data() + off, src, bytes);
+        const void* d = dbase + off;
+        off += al(bytes);
+        return d;
+    };
+    K.kps = (const slam_keypoint*)put(F->kps_un, sizeof(slam_keypoint) * F->n);
+    K.uright = (const float*)put(F->uright, 4 * (size_t)F->n);
+    K.desc = (const uint8_t*)put(F->desc, 32 * (size_t)F->n);
+    K.cell_start = (const int32_t*)put(start.data(), 4 * start.size());
+    K.cell_feat = (const int32_t*)put(feat.data(), 4 * feat.size());
+    const slam_mp_geom* d_mps = (const slam_mp_geom*)put(mps, sizeof(slam_mp_geom) * n_mp);
+    const uint8_t* d_desc = (const uint8_t*)put(mp_desc, 32 * (size_t)n_mp);
+    SLAM_HIP_TRY(hipMemcpyAsync(dbase, host.data(), off, hipMemcpyHostToDevice, m->stream));
+    int32_t* d_bi = m->d_out.as<int32_t>();
+    int32_t* d_bd = d_bi + n_mp;
+    hipLaunchKernelGGL(k_fuse_search, dim3((n_mp + kFuseThreads - 1) / kFuseThreads), dim3(kFuseThreads), 0,
+                       m->stream, K, n_mp, d_mps, d_desc, th, d_bi, d_bd);
+    SLAM_HIP_TRY(hipGetLastError());
+    SLAM_HIP_TRY(hipMemcpyAsync(best_idx, d_bi, 4 * (size_t)n_mp, hipMemcpyDeviceToHost, m->stream));
+    SLAM_HIP_TRY(hipMemcpyAsync(best_dist, d_bd, 4 * (size_t)n_mp, hipMemcpyDeviceToHost, m->stream));
     SLAM_HIP_TRY(hipStreamSynchronize(m->stream));
     return SLAM_OK;
 }

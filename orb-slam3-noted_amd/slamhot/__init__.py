@@ -818,6 +818,7 @@ class Mapper:
             L.slamhot_mapper_destroy.restype = None
             L.slamhot_distinctive_descriptors.argtypes = [P, I, P, P, P]
             L.slamhot_search_for_triangulation.argtypes = [P, I, C.POINTER(TriKF), I, C.POINTER(TriPair), I, I, P, P]
+            L.slamhot_fuse_search.argtypes = [P, C.POINTER(FrameView), P, I, P, P, C.c_float, P, P]
             L._mapper_ready = True
         h = P()
         check(L.slamhot_mapper_create(device, C.byref(h)), "mapper_create")
@@ -861,3 +862,15 @@ class Mapper:
             i1 = np.flatnonzero(row >= 0)
             out.append((int(nm[p]), np.stack([i1, row[i1]], 1).astype(np.int64)))
         return out
+
+    def FuseSearch(self, kf_view, inv_level_sigma2, mps, mp_desc, th=3.0):
+        """Search half of ORBmatcher::Fuse(pKF, vpMapPoints, th): (best_idx, best_dist) per MapPoint
+        (mps: MP_GEOM_DTYPE, seen = IsInKeyFrame(pKF))."""
+        mps = np.ascontiguousarray(mps, MP_GEOM_DTYPE)
+        mp_desc = np.ascontiguousarray(mp_desc, np.uint8)
+        isig = np.ascontiguousarray(inv_level_sigma2, np.float32)
+        bi = np.full(len(mps), -1, np.int32)
+        bd = np.full(len(mps), 256, np.int32)
+        check(lib().slamhot_fuse_search(self._h, C.byref(kf_view), _ptr(isig), len(mps), _ptr(mps), _ptr(mp_desc), th,
+                                        _ptr(bi), _ptr(bd)), "fuse_search")
+        return bi, bd

@@ -63,6 +63,38 @@ class MapPoint:
     def UpdateNormalAndDepth(self):
         self.normal_updates += 1
 
+    # --- what ORBmatcher::Fuse's apply half touches (MapPoint.cc)
+    def IsInKeyFrame(self, kf):
+        return kf in self.observations
+
+    def Observations(self):
+        """nObs: 2 per stereo observation, 1 per monocular one (MapPoint::AddObservation)."""
+        n = 0
+        for kf, (li, ri) in self.observations.items():
+            if li != -1:
+                n += 2 if kf.mvuRight[li] >= 0 else 1
+            if ri != -1:
+                n += 1
+        return n
+
+    def Replace(self, other):
+        """MapPoint::Replace (MapPoint.cc:238-290): observations move to `other` (or are erased
+        where `other` is already seen), this point turns bad."""
+        if other.mnId == self.mnId:
+            return
+        obs = self.GetObservations()
+        self.observations = {}
+        self.bad = True
+        self.replaced = other
+        for kf, (li, ri) in obs.items():
+            if not other.IsInKeyFrame(kf):
+                if li != -1:
+                    kf.mvpMapPoints[li] = other
+                    other.AddObservation(kf, li)
+            else:
+                if li != -1:
+                    kf.mvpMapPoints[li] = None
+
 
 class KeyFrame:
     def __init__(self, mnId: int, Tcw, keys_un, uright, inv_level_sigma2, cam, pmap: Map):
@@ -96,6 +128,12 @@ class KeyFrame:
 
     def GetMapPointMatches(self):
         return list(self.mvpMapPoints)
+
+    def GetMapPoint(self, idx):
+        return self.mvpMapPoints[idx]
+
+    def AddMapPoint(self, mp, idx):
+        self.mvpMapPoints[idx] = mp
 
     def EraseMapPointMatch(self, mp):
         for i, m in enumerate(self.mvpMapPoints):
@@ -248,3 +286,27 @@ def map_from_window(W: dict, covis_order=None):
     cur = kfs[-1]
     cur.covisible = covis_order if covis_order is not None else [kfs[i] for i in range(nk - 2, -1, -1)]
     return pmap, kfs, mps
+
+
+def fuse_apply(pKF: KeyFrame, vpMapPoints, best_idx, best_dist, TH_LOW: int = 50) -> int:
+    """ORBmatcher::Fuse's update half (ORBmatcher.cc:1789-1816) in list order, on the device
+    search results (slamhot_fuse_search).  The skip checks are re-evaluated here because
+    earlier updates of this call can make a later MapPoint bad or put it into pKF."""
+    nFused = 0
+    for i, pMP in enumerate(vpMapPoints):
+        if pMP is None or pMP.isBad() or pMP.IsInKeyFrame(pKF):
+            continue
+        if best_dist[i] <= TH_LOW:
+            idx = int(best_idx[i])
+            pMPinKF = pKF.GetMapPoint(idx)
+            if pMPinKF is not None:
+                if not pMPinKF.isBad():
+                    if pMPinKF.Observations() > pMP.Observations():
+                        pMP.Replace(pMPinKF)
+                    else:
+                        pMPinKF.Replace(pMP)
+            else:
+                pMP.AddObservation(pKF, idx)
+                pKF.AddMapPoint(pMP, idx)
+            nFused += 1
+    return nFused

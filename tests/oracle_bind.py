@@ -390,3 +390,20 @@ def search_for_triangulation(kf1, kf2, pair, check_ori=False):
     n = L.oracle_search_for_triangulation(C.addressof(kf1), C.addressof(kf2), C.addressof(pair), int(check_ori),
                                           _ptr(m12))
     return n, m12[: kf1.n]
+
+
+def fuse_search(fv, inv_sigma2, geom, desc, th=3.0):
+    import slamhot
+    L = lib()
+    if not hasattr(L, "_fuse_ready"):
+        L.oracle_fuse_search.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_float,
+                                         C.c_void_p, C.c_void_p]
+        L.oracle_fuse_search.restype = None
+        L._fuse_ready = True
+    geom = np.ascontiguousarray(geom, slamhot.MP_GEOM_DTYPE)
+    desc = np.ascontiguousarray(desc, np.uint8)
+    isig = np.ascontiguousarray(inv_sigma2, np.float32)
+    bi = np.zeros(len(geom), np.int32)
+    bd = np.zeros(len(geom), np.int32)
+    L.oracle_fuse_search(C.addressof(fv), _ptr(isig), len(geom), _ptr(geom), _ptr(desc), th, _ptr(bi), _ptr(bd))
+    return bi, bd

@@ -235,3 +235,42 @@ def f12_ep(T1, T2):
     C2 = R2 @ C1 + t2
     ep = np.array([FX * C2[0] / C2[2] + CX, FY * C2[1] / C2[2] + CY])
     return F12.astype(np.float32), ep.astype(np.float32)
+
+
+def fuse_mps(S, n_extra=300):
+    """MapPoints to fuse into the scene's frame treated as a KeyFrame: most back-projected near
+    features (descriptor close to the feature's, mfMaxDistance putting the predicted level on
+    the feature's octave, normal along the viewing ray), plus far / behind / off-image / bad /
+    already-in-KF ones and some at grazing angles."""
+    rng, k, d = S["rng"], S["k"], S["d"]
+    n = len(k)
+    sel = rng.permutation(n)[: int(n * 0.7)]
+    depth = rng.uniform(0.8, 25.0, len(sel)).astype(np.float32)
+    X = backproject(S, k["x"][sel] + rng.normal(0, 0.8, len(sel)), k["y"][sel] + rng.normal(0, 0.8, len(sel)), depth)
+    Xe = backproject(S, rng.uniform(-200, 952, n_extra), rng.uniform(-150, 630, n_extra),
+                     rng.uniform(-5.0, 40.0, n_extra).astype(np.float32))
+    pos = np.concatenate([X, Xe]).astype(np.float32)
+    m = len(pos)
+    T = S["Tcw"].astype(np.float64)
+    Ow = -(T[:3, :3].T @ T[:3, 3])
+    PO = pos.astype(np.float64) - Ow
+    dist = np.linalg.norm(PO, axis=1)
+    nrm = PO / dist[:, None] + rng.normal(0, 0.25, PO.shape)
+    graze = rng.random(m) < 0.08
+    nrm[graze] = rng.normal(0, 1, (graze.sum(), 3))
+    nrm = (nrm / np.linalg.norm(nrm, axis=1)[:, None]).astype(np.float32)
+    sc = np.float32(1.2) ** np.arange(8, dtype=np.float32)
+    oct_ = np.concatenate([k["octave"][sel], rng.integers(0, 8, n_extra)])
+    max_d = (dist * sc[oct_] * rng.uniform(1.0, 1.19, m)).astype(np.float32)
+    min_d = (max_d / sc[7]).astype(np.float32)
+    geom = np.zeros(m, slamhot.MP_GEOM_DTYPE)
+    geom["pos"] = pos
+    geom["normal"] = nrm
+    geom["min_dist"] = min_d
+    geom["max_dist"] = max_d
+    geom["seen"] = rng.random(m) < 0.05
+    geom["is_bad"] = rng.random(m) < 0.03
+    geom["has_obs"] = 1
+    desc = np.concatenate([flip_bits(d[sel], rng, 45), flip_bits(d[rng.integers(0, n, n_extra)], rng, 90)])
+    order = rng.permutation(m)
+    return geom[order], desc[order]

@@ -47,3 +47,22 @@ def test_search_for_triangulation_batch(check_ori):
         assert np.array_equal(mp, np.stack([i1, m12[i1]], 1))
         total += n
     assert total > 500
+
+
+@pytest.mark.parametrize("seed,th", [(12, 3.0), (13, 1.0), (14, 5.0)])
+def test_fuse_search(seed, th):
+    import scenes
+
+    import slamhot
+    from slamhot import synth
+    S = scenes.scene(seed)
+    fv, keep = scenes.frame_view(S)
+    geom, desc = scenes.fuse_mps(S)
+    _, isig, _ = synth._level_tables()
+    m = slamhot.Mapper()
+    bi, bd = m.FuseSearch(fv, isig, geom, desc, th)
+    m.close()
+    bo, do = ob.fuse_search(fv, isig, geom, desc, th)
+    assert np.array_equal(bi, bo)
+    assert np.array_equal(bd, do)
+    assert (bd <= 50).sum() > 100

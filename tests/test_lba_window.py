@@ -103,3 +103,34 @@ def test_mirror_equals_direct_solve():
     assert n_obs == len(W["edge_pt"]) - direct["n_outlier"]
     assert pmap.change_index == 1
     S.close()
+
+
+def test_fuse_apply_order_and_replace():
+    """ORBmatcher::Fuse's update half (ORBmatcher.cc:1789-1816): Replace keeps the MapPoint
+    with more observations, a replaced MapPoint later in the list is skipped, a MapPoint that
+    entered the KeyFrame earlier in the call is skipped, free slots get AddObservation."""
+    import numpy as np
+
+    from slamhot.optimizer import KeyFrame, Map, MapPoint, fuse_apply
+    pmap = Map()
+    keys = np.zeros(4, dtype=[("x", "<f4"), ("y", "<f4"), ("octave", "<i4")])
+    cam = (400.0, 400.0, 320.0, 240.0, 40.0)
+    kf = KeyFrame(0, np.eye(4), keys, [-1, 5.0, -1, -1], np.ones(8), cam, pmap)
+    other = KeyFrame(1, np.eye(4), keys, [-1, -1, -1, -1], np.ones(8), cam, pmap)
+    b = MapPoint(10, [0, 0, 1], pmap)            # in kf slot 0, 1 observation
+    kf.mvpMapPoints[0] = b
+    b.AddObservation(kf, 0)
+    a = MapPoint(11, [0, 0, 1], pmap)            # 2 observations elsewhere -> survives
+    a.AddObservation(other, 0)
+    a.AddObservation(KeyFrame(2, np.eye(4), keys, [-1] * 4, np.ones(8), cam, pmap), 1)
+    other.mvpMapPoints[0] = a
+    c = MapPoint(12, [0, 0, 1], pmap)            # free slot 2
+    d = MapPoint(13, [0, 0, 1], pmap)            # also matches slot 2 (after c entered)
+    e = MapPoint(14, [0, 0, 1], pmap)            # too far
+    n = fuse_apply(kf, [a, b, c, d, e, None], [0, 0, 2, 2, 3, -1], [10, 10, 20, 30, 51, 256])
+    assert n == 3                                # a (replace), c (add), d (slot 2 now holds c: replace)
+    assert b.isBad() and kf.GetMapPoint(0) is a and a.IsInKeyFrame(kf)
+    # c has one observation, d none: d.Observations() = 0 < 1 -> c.Replace(d)? no: pMPinKF=c has
+    # more (1 > 0), so d.Replace(c): d turns bad, c keeps the slot
+    assert d.isBad() and kf.GetMapPoint(2) is c
+    assert not e.IsInKeyFrame(kf)
