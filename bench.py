@@ -376,17 +376,27 @@ def pose_leg(args, rank, world, local_rank, dist, device):
 
 def stereo_leg(args, rank, world, local_rank, dist, device):
     """Stereo Frame construction frames/s (EuRoC stereo shape, BASELINE.json configs[3]:
-    752x480, 1200 features): a step extracts P left and P right images and runs
-    ComputeStereoMatches on the P pairs, all device-resident.  stereo_ms isolates the
-    matching kernels (torch events on the launch stream)."""
+    752x480, 1200 features): a step rectifies P raw left and P raw right images with the
+    EuRoC calibration (cv::remap, stereo_euroc.cc:168-169), extracts both and runs
+    ComputeStereoMatches on the P pairs, all device-resident.  rectify_ms / stereo_ms isolate
+    the remap and matching kernels (torch events on the launch stream)."""
     import torch
 
     import slamhot
     from slamhot import dist as sdist
     from slamhot import synth
     P, W, H, NF = args.stereo_pairs, 752, 480, 1200
-    seeds = sdist.shard(16 * world, rank, world)
-    prs = [synth.stereo_pair(int(s) + 500, W, H) for s in seeds]
+    from slamhot import euroc
+    calib = {k: np.array(v) if isinstance(v, list) else v
+             for k, v in json.loads((ROOT / "tests" / "golden" / "euroc_stereo_calib.json").read_text()).items()}
+    maps = [euroc.init_undistort_rectify_map(calib[f"{sd}.K"], calib[f"{sd}.D"], calib[f"{sd}.R"], calib[f"{sd}.P"],
+                                             (W, H)) for sd in ("LEFT", "RIGHT")]
+    # raw camera images: synthetic rectified pairs pushed back through the calibration
+    seeds = sdist.shard(8 * world, rank, world)
+    prs = []
+    for s_ in seeds:
+        lr = synth.stereo_pair(int(s_) + 500, W, H)
+        prs.append(tuple(synth.unrectify(im, *mp) for im, mp in zip(lr, maps)))
     il = np.stack([prs[i % len(prs)][0] for i in range(P)])
     ir = np.stack([prs[i % len(prs)][1] for i in range(P)])
     mbf = synth.EUROC_STEREO["bf"]
@@ -394,8 +404,10 @@ def stereo_leg(args, rank, world, local_rank, dist, device):
     left = slamhot.ORBextractor(nfeatures=NF, device=local_rank, max_size=(W, H), max_batch=P)
     right = slamhot.ORBextractor(nfeatures=NF, device=local_rank, max_size=(W, H), max_batch=P)
     sm = slamhot.StereoMatcher(device=local_rank)
+    rect = [euroc.Rectifier(*mp, device=local_rank) for mp in maps]
     cap = left.cap
-    d_il, d_ir = torch.from_numpy(il).to(device), torch.from_numpy(ir).to(device)
+    d_raw_l, d_raw_r = torch.from_numpy(il).to(device), torch.from_numpy(ir).to(device)
+    d_il, d_ir = torch.empty_like(d_raw_l), torch.empty_like(d_raw_r)
     bufs = [(torch.zeros((P, cap, 28), dtype=torch.uint8, device=device),
              torch.zeros((P, cap, 32), dtype=torch.uint8, device=device),
              torch.zeros(P, dtype=torch.int32, device=device), torch.zeros(P, dtype=torch.int32, device=device))
@@ -404,8 +416,17 @@ def stereo_leg(args, rank, world, local_rank, dist, device):
     d_dep = torch.empty((P, cap), dtype=torch.float32, device=device)
     stream = torch.cuda.Stream(device)  # a real stream: NULL would mean each handle's own stream
     ev = []
+    ev_rect = []
 
     def step(timed=False):
+        if timed:
+            r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            r0.record(stream)
+        for rc, raw, out in ((rect[0], d_raw_l, d_il), (rect[1], d_raw_r, d_ir)):
+            rc.rectify_batch_device(P, raw.data_ptr(), W, W * H, out.data_ptr(), W, W * H, stream=stream.cuda_stream)
+        if timed:
+            r1.record(stream)
+            ev_rect.append((r0, r1))
         for ex, img, (k, d, n, m) in ((left, d_il, bufs[0]), (right, d_ir, bufs[1])):
             ex.extract_batch_device(img.data_ptr(), P, W, H, k.data_ptr(), d.data_ptr(), cap, n.data_ptr(),
                                     m.data_ptr(), stream=stream.cuda_stream)
@@ -434,18 +455,21 @@ def stereo_leg(args, rank, world, local_rank, dist, device):
         dist.barrier()
     elapsed, total = sdist.reduce_run(dist, device, time.perf_counter() - t0, float(P * steps))
     stereo_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    rect_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_rect]))
     nl_h = bufs[0][2].cpu().numpy()
     ur = d_ur.cpu().numpy()
     matched = float(np.mean([(ur[f, : nl_h[f]] >= 0).sum() for f in range(P)]))
     out = {
-        "metric": "stereo Frame (2x ORB extract + ComputeStereoMatches) frames/s",
+        "metric": "stereo Frame (2x remap + 2x ORB extract + ComputeStereoMatches) frames/s",
         "value": round(total / elapsed, 1),
         "unit": "frames/s",
         "dtype": "u8",
-        "config": {"workload": f"synthetic rectified pairs {W}x{H}, {NF} features, EuRoC bf",
+        "config": {"workload": f"synthetic raw stereo pairs {W}x{H} (EuRoC calibration), {NF} features, EuRoC bf",
                    "pairs_per_gpu_per_step": P, "parallelism": f"frame-sharded x{world}"},
         "ms_per_step": round(elapsed / steps * 1e3, 3),
         "stereo_match_ms_per_step": round(stereo_ms, 4),
+        "rectify_ms_per_step": round(rect_ms, 4),
+        "rectify_GBps": round(2 * P * W * H * 2 / (rect_ms / 1e3) / 1e9, 1),
         "stereo_match_frames_per_s": round(P / (stereo_ms / 1e3), 1),
         "mean_stereo_matches": round(matched, 1),
     }
@@ -457,8 +481,9 @@ def stereo_leg(args, rank, world, local_rank, dist, device):
         t_ex = t_st = 0.0
         k = 0
         while k < len(prs) and t_ex + t_st < 10.0:
-            l_img, r_img = prs[k]
             t1 = time.perf_counter()
+            l_img = ob.remap_linear(prs[k][0], rect[0].map_x, rect[0].map_y)
+            r_img = ob.remap_linear(prs[k][1], rect[1].map_x, rect[1].map_y)
             kl, dl, _ = ob.extract(l_img, p)
             kr, dr, _ = ob.extract(r_img, p)
             t_ex += time.perf_counter() - t1
@@ -468,9 +493,11 @@ def stereo_leg(args, rank, world, local_rank, dist, device):
             t_st += time.perf_counter() - t2
             k += 1
         out["cpu_baseline"] = {"value": round(k / (t_ex + t_st), 2), "unit": "frames/s", "cores": 1, "kind": "port",
-                               "sample": f"{k} stereo frames on one core (oracle extract x2 + "
+                               "sample": f"{k} stereo frames on one core (oracle remap x2 + extract x2 + "
                                          f"oracle/stereo_oracle.cpp, -O3)",
                                "stereo_match_only_frames_per_s": round(k / t_st, 1)}
+    for rc in rect:
+        rc.close()
     left.close()
     right.close()
     sm.close()

@@ -491,6 +491,26 @@ slam_status slamhot_fuse_search(slam_mapper* mp, const slam_frame_view* KF, cons
                                 int n_mp, const slam_mp_geom* mps, const uint8_t* mp_desc, float th,
                                 int32_t* best_idx, int32_t* best_dist);
 
+/* ------------------------------------------------------------------ stereo rectification
+ * cv::remap(im, imRect, M1, M2, cv::INTER_LINEAR) with the CV_32F maps of
+ * cv::initUndistortRectifyMap (stereo_euroc.cc:117-118, 168-169), BORDER_CONSTANT 0, for
+ * batches of frames on the device.  The maps are converted once at create time to the
+ * fixed-point form remap uses internally (value * 32 rounded to nearest even, 5-bit fractions,
+ * 2^15-scaled bilinear weights). */
+typedef struct slam_rectifier slam_rectifier;
+
+/* map_x / map_y: host float maps, dst_w x dst_h (row-major); sources are src_w x src_h. */
+slam_status slamhot_rectifier_create(int device, int src_w, int src_h, int dst_w, int dst_h, const float* map_x,
+                                     const float* map_y, slam_rectifier** out);
+void slamhot_rectifier_destroy(slam_rectifier* r);
+
+/* nframes source images (device, u8, row pitch src_pitch, frame stride src_stride bytes) to
+ * nframes destination images (dst_w x dst_h, pitch dst_pitch, stride dst_stride).
+ * Asynchronous on hip_stream (NULL = the handle's stream). */
+slam_status slamhot_rectify_batch_device(slam_rectifier* r, int nframes, const void* d_src, int src_pitch,
+                                         int64_t src_stride, void* d_dst, int dst_pitch, int64_t dst_stride,
+                                         void* hip_stream);
+
 #ifdef __cplusplus
 }
 #endif

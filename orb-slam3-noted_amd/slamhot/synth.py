@@ -323,3 +323,35 @@ def stereo_pair(seed: int, width: int = 752, height: int = 480, d_min: float = 4
     rows = np.arange(height)[:, None]
     right = lf[rows, x0] * (1 - fx) + lf[rows, x1] * fx + rng.normal(0.0, noise, size=left.shape)
     return left, np.ascontiguousarray(np.clip(np.rint(right), 0, 255).astype(np.uint8))
+
+
+def unrectify(rect: np.ndarray, map_x: np.ndarray, map_y: np.ndarray) -> np.ndarray:
+    """A raw (distorted, unrectified) image whose rectification through (map_x, map_y)
+    reproduces `rect` up to resampling: rectified pixel r reads the raw image at
+    (map_x[r], map_y[r]), so each rectified pixel is splatted there (bilinear weights) and
+    the few holes are filled from their neighbours."""
+    h, w = rect.shape
+    acc = np.zeros((h + 2, w + 2))
+    wsum = np.zeros((h + 2, w + 2))
+    x0 = np.floor(map_x).astype(np.int64)
+    y0 = np.floor(map_y).astype(np.int64)
+    fx, fy = map_x - x0, map_y - y0
+    val = rect.astype(np.float64)
+    for dy, dx, wt in ((0, 0, (1 - fx) * (1 - fy)), (0, 1, fx * (1 - fy)), (1, 0, (1 - fx) * fy), (1, 1, fx * fy)):
+        xi, yi = x0 + dx + 1, y0 + dy + 1
+        ok = (xi >= 0) & (xi < w + 2) & (yi >= 0) & (yi < h + 2)
+        np.add.at(acc, (yi[ok], xi[ok]), (val * wt)[ok])
+        np.add.at(wsum, (yi[ok], xi[ok]), wt[ok])
+    acc, wsum = acc[1:-1, 1:-1], wsum[1:-1, 1:-1]
+    out = np.where(wsum > 1e-6, acc / np.maximum(wsum, 1e-6), np.nan)
+    for _ in range(32):
+        holes = np.isnan(out)
+        if not holes.any():
+            break
+        pad = np.pad(out, 1, constant_values=np.nan)
+        nb = np.stack([pad[:-2, 1:-1], pad[2:, 1:-1], pad[1:-1, :-2], pad[1:-1, 2:]])
+        cnt = np.isfinite(nb).sum(0)
+        fill = np.where(cnt > 0, np.nansum(nb, axis=0) / np.maximum(cnt, 1), np.nan)
+        out = np.where(holes & np.isfinite(fill), fill, out)
+    out = np.nan_to_num(out, nan=128.0)
+    return np.ascontiguousarray(np.clip(np.rint(out), 0, 255).astype(np.uint8))

@@ -407,3 +407,21 @@ def fuse_search(fv, inv_sigma2, geom, desc, th=3.0):
     bd = np.zeros(len(geom), np.int32)
     L.oracle_fuse_search(C.addressof(fv), _ptr(isig), len(geom), _ptr(geom), _ptr(desc), th, _ptr(bi), _ptr(bd))
     return bi, bd
+
+
+# ---- rectification (oracle/rectify_oracle.cpp)
+def remap_linear(src, map_x, map_y):
+    L = lib()
+    if not hasattr(L, "_remap_ready"):
+        L.oracle_remap_linear.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_int,
+                                          C.c_int, C.c_void_p, C.c_int]
+        L.oracle_remap_linear.restype = None
+        L._remap_ready = True
+    src = np.ascontiguousarray(src, np.uint8)
+    mx = np.ascontiguousarray(map_x, np.float32)
+    my = np.ascontiguousarray(map_y, np.float32)
+    sh, sw = src.shape
+    dh, dw = mx.shape
+    dst = np.zeros((dh, dw), np.uint8)
+    L.oracle_remap_linear(_ptr(src), sw, sh, sw, _ptr(mx), _ptr(my), dw, dh, _ptr(dst), dw)
+    return dst
