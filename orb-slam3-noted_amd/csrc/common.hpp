@@ -20,6 +20,12 @@ namespace slamhot {
         }                                                                                  \
     } while (0)
 
+#define SLAM_TRY_ST(expr)                         \
+    do {                                          \
+        const slam_status _st = (expr);           \
+        if (_st != SLAM_OK) return _st;           \
+    } while (0)
+
 constexpr int kWave = 64;
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }

@@ -379,6 +379,25 @@ __device__ __forceinline__ int fast_M(const uint8_t* c, int stride) {
     return M > 0 ? M : 0;
 }
 
+// Necessary condition for a 9-arc at threshold t: every 9-run of the 16-pixel circle holds
+// one pixel of each opposite pair (k, k+8), so a bright corner needs min(p_k, p_k+8) < v - t
+// and a dark one max(p_k, p_k+8) > v + t for all eight pairs.  Passes ~7% of the pixels of
+// textured frames at t = 7 (the compass pre-test of pass A, two pairs, passes ~24%).
+__device__ __forceinline__ bool fast_pairs8(const uint8_t* c, int stride, int t) {
+    const int v = c[0];
+    const int p[16] = {c[3 * stride],      c[3 * stride + 1],  c[2 * stride + 2],  c[stride + 3],
+                       c[3],               c[-stride + 3],     c[-2 * stride + 2], c[-3 * stride + 1],
+                       c[-3 * stride],     c[-3 * stride - 1], c[-2 * stride - 2], c[-stride - 3],
+                       c[-3],              c[stride - 3],      c[2 * stride - 2],  c[3 * stride - 1]};
+    int lo = min(p[0], p[8]), hi = max(p[0], p[8]);
+#pragma unroll
+    for (int k = 1; k < 8; k++) {
+        lo = max(lo, min(p[k], p[k + 8]));
+        hi = min(hi, max(p[k], p[k + 8]));
+    }
+    return (lo < v - t) || (hi > v + t);
+}
+
 // ---------------------------------------------------------------------------------------
 // k_fast_wave: one WAVE per cell whose tested region is <= 64 columns wide (all cells of
 // the standard geometries).  Three order-preserving, wave-compacted passes over the cell:
@@ -492,6 +511,24 @@ __global__ void __launch_bounds__(256) k_fast_wave(Bufs b, const int32_t* list, 
                 na += __popcll(m);
             }
         }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+
+    // pass B1: the eight-pair pre-test on the compass survivors (in-place compaction)
+    {
+        int n1 = 0;
+        for (int j = 0; j < na; j += 64) {
+            const int e = j + lane;
+            const bool valid = e < na;
+            const int code = valid ? lst[e] : 0;
+            const int r = code >> 6, c = code & 63;
+            const bool keep = valid && fast_pairs8(roi + (r + 3) * kRoiStride + c + 3, kRoiStride, tlow);
+            const uint64_t m = __ballot(keep);
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            if (keep) lst[n1 + __popcll(m & lt)] = (uint16_t)code;
+            n1 += __popcll(m);
+        }
+        na = n1;
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 
@@ -1241,7 +1278,7 @@ static size_t octree_lds_bytes(int maxn, int keycap) {
 }
 
 enum Stage { kStResize = 0, kStFast, kStOctree, kStLayout, kStBlur, kStOrb, kNumStages };
-static const char* kStageNames[kNumStages] = {"k_resize", "k_fast_cells", "k_octree",
+static const char* kStageNames[kNumStages] = {"k_resize", "k_fast_wave", "k_octree",
                                               "k_layout", "k_blur", "k_orb"};
 
 }  // namespace slamhot
@@ -1255,6 +1292,15 @@ struct slam_extractor {
     hipStream_t stream = nullptr;
     hipStream_t side = nullptr;             // blur runs here, concurrent with FAST + octree
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // sub-batch concurrency: a batch is split into nsub frame ranges, each running the whole
+    // pipeline on its own stream pair (main + blur side stream); latency-bound stages of one
+    // range (octree, orb) overlap the VALU-bound FAST of another
+    static constexpr int kMaxSub = 4;
+    int nsub = 1;
+    bool chain_fast = false;
+    hipStream_t sub[kMaxSub] = {}, sub_side[kMaxSub] = {};
+    hipEvent_t sub_fork = nullptr, sub_join[kMaxSub] = {}, sub_bfork[kMaxSub] = {}, sub_bjoin[kMaxSub] = {},
+              sub_fast[kMaxSub] = {};
     bool serial = false;
     std::mutex mu;
     // geometry
@@ -1421,26 +1467,31 @@ static slam_status ensure_batch(slam_extractor* ex, int nframes, int cap) {
     return SLAM_OK;
 }
 
-static slam_status launch_pipeline(slam_extractor* ex, int nframes, const uint8_t* d_img, int lap0,
-                                   int lap1, slam_keypoint* d_kps, uint8_t* d_desc, int cap,
-                                   int32_t* d_n, int32_t* d_mono, hipStream_t s) {
+// One frame range [f0, f0 + nframes) of a batch: every per-frame buffer is frame-major, so
+// the range is the whole pipeline on pointers advanced by f0 frames.  s = main stream,
+// side = blur stream (nullptr: serial), fork/join = that range's blur events.
+static slam_status launch_range(slam_extractor* ex, int f0, int nframes, const uint8_t* d_img, int lap0,
+                                int lap1, slam_keypoint* d_kps, uint8_t* d_desc, int cap, int32_t* d_n,
+                                int32_t* d_mono, hipStream_t s, hipStream_t side, hipEvent_t bfork,
+                                hipEvent_t bjoin, hipEvent_t fast_after = nullptr, hipEvent_t fast_done = nullptr) {
     const Plan& P = ex->plan;
+    const size_t F = (size_t)f0;
     Bufs b{};
-    b.img = d_img;
-    b.pyr = ex->d_pyr.as<uint8_t>();
-    b.blur = ex->d_blur.as<uint8_t>();
-    b.cell_keys = ex->d_cell_keys.as<uint32_t>();
-    b.cell_cnt = ex->d_cell_cnt.as<int32_t>();
-    b.keys_g = ex->d_keys_g.as<uint32_t>();
-    b.knode_g = ex->d_knode_g.as<uint16_t>();
-    b.okp = ex->d_okp.as<uint32_t>();
-    b.ocnt = ex->d_ocnt.as<int32_t>();
-    b.oidx = ex->d_oidx.as<int32_t>();
-    b.err = ex->d_err.as<int32_t>();
-    b.out_kps = d_kps;
-    b.out_desc = d_desc;
-    b.out_n = d_n;
-    b.out_mono = d_mono;
+    b.img = d_img + F * P.W * P.H;
+    b.pyr = ex->d_pyr.as<uint8_t>() + F * P.pyr_frame;
+    b.blur = ex->d_blur.as<uint8_t>() + F * P.blur_frame;
+    b.cell_keys = ex->d_cell_keys.as<uint32_t>() + F * P.ncells * P.slot_cap;
+    b.cell_cnt = ex->d_cell_cnt.as<int32_t>() + F * P.ncells;
+    b.keys_g = ex->d_keys_g.as<uint32_t>() + F * P.key_slots;
+    b.knode_g = ex->d_knode_g.as<uint16_t>() + F * P.key_slots;
+    b.okp = ex->d_okp.as<uint32_t>() + F * P.kslots;
+    b.ocnt = ex->d_ocnt.as<int32_t>() + F * P.nlevels;
+    b.oidx = ex->d_oidx.as<int32_t>() + F * P.kslots;
+    b.err = ex->d_err.as<int32_t>() + F;
+    b.out_kps = d_kps + F * cap;
+    b.out_desc = d_desc + F * cap * 32;
+    b.out_n = d_n + F;
+    b.out_mono = d_mono + F;
     b.xtab = ex->d_xtab.as<ResizeX>();
     b.ytab = ex->d_ytab.as<ResizeY>();
     b.cells = ex->d_cells.as<CellDesc>();
@@ -1471,16 +1522,19 @@ static slam_status launch_pipeline(slam_extractor* ex, int nframes, const uint8_
     end(kStResize);
     // fork: the blur needs only the pyramid (SLAMHOT_SERIAL=1 keeps it on the main stream,
     // for isolated per-kernel timing)
-    hipStream_t bs = ex->serial ? s : ex->side;
-    if (!ex->serial) {
-        SLAM_HIP_TRY(hipEventRecord(ex->ev_fork, s));
-        SLAM_HIP_TRY(hipStreamWaitEvent(ex->side, ex->ev_fork, 0));
+    hipStream_t bs = side ? side : s;
+    if (side) {
+        SLAM_HIP_TRY(hipEventRecord(bfork, s));
+        SLAM_HIP_TRY(hipStreamWaitEvent(side, bfork, 0));
     }
     begin(kStBlur, bs);
     hipLaunchKernelGGL(k_blur3, dim3(ex->n_blur_tiles, nframes), dim3(256), 0, bs, b,
                        ex->d_blur_tiles.as<BlurTile>(), 1);
     end(kStBlur, bs);
-    if (!ex->serial) SLAM_HIP_TRY(hipEventRecord(ex->ev_join, ex->side));
+    if (side) SLAM_HIP_TRY(hipEventRecord(bjoin, side));
+    // ranges run FAST one after another (each fills the chip); a range's octree / layout /
+    // orb then overlap the next range's FAST
+    if (fast_after) SLAM_HIP_TRY(hipStreamWaitEvent(s, fast_after, 0));
     begin(kStFast);
     if (ex->n_wave_cells)
         hipLaunchKernelGGL(k_fast_wave, dim3((ex->n_wave_cells + 3) / 4, nframes), dim3(256),
@@ -1490,6 +1544,7 @@ static slam_status launch_pipeline(slam_extractor* ex, int nframes, const uint8_
         hipLaunchKernelGGL(k_fast_cells, dim3(ex->n_wide_cells, nframes), dim3(256), 0, s, b,
                            ex->d_wide_cells.as<int32_t>());
     end(kStFast);
+    if (fast_done) SLAM_HIP_TRY(hipEventRecord(fast_done, s));
     begin(kStOctree);
     hipLaunchKernelGGL(k_octree, dim3(P.nlevels, nframes), dim3(256), ex->octree_lds, s, b,
                        ex->key_lds_cap);
@@ -1497,11 +1552,40 @@ static slam_status launch_pipeline(slam_extractor* ex, int nframes, const uint8_
     begin(kStLayout);
     hipLaunchKernelGGL(k_layout, dim3(nframes), dim3(256), 0, s, b);
     end(kStLayout);
-    if (!ex->serial) SLAM_HIP_TRY(hipStreamWaitEvent(s, ex->ev_join, 0));
+    if (side) SLAM_HIP_TRY(hipStreamWaitEvent(s, bjoin, 0));
     begin(kStOrb);
     hipLaunchKernelGGL(k_orb2, dim3((P.kslots + 3) / 4, nframes), dim3(256), 0, s, b);
     end(kStOrb);
     SLAM_HIP_TRY(hipGetLastError());
+    return SLAM_OK;
+}
+
+// Whole batch on the caller's stream s: one range on s (small batches, SLAMHOT_SERIAL=1), or
+// nsub ranges forked from s onto the handle's sub-streams and joined back into s.
+static slam_status launch_pipeline(slam_extractor* ex, int nframes, const uint8_t* d_img, int lap0,
+                                   int lap1, slam_keypoint* d_kps, uint8_t* d_desc, int cap,
+                                   int32_t* d_n, int32_t* d_mono, hipStream_t s) {
+    int nsub = ex->serial ? 1 : std::min(ex->nsub, nframes / 8);
+    if (nsub <= 1) {
+        SLAM_TRY_ST(launch_range(ex, 0, nframes, d_img, lap0, lap1, d_kps, d_desc, cap, d_n, d_mono, s,
+                                 ex->serial ? nullptr : ex->side, ex->ev_fork, ex->ev_join));
+    } else {
+        // range 0 runs on the caller's stream, ranges 1.. on the handle's sub-streams; with the
+        // blur kept in-stream that is nsub hardware queues (GPU_MAX_HW_QUEUES is 4 by default)
+        SLAM_HIP_TRY(hipEventRecord(ex->sub_fork, s));
+        int f0 = 0;
+        for (int k = 0; k < nsub; k++) {
+            const int nf = nframes / nsub + (k < nframes % nsub ? 1 : 0);
+            hipStream_t sk = k ? ex->sub[k] : s;
+            if (k) SLAM_HIP_TRY(hipStreamWaitEvent(sk, ex->sub_fork, 0));
+            SLAM_TRY_ST(launch_range(ex, f0, nf, d_img, lap0, lap1, d_kps, d_desc, cap, d_n, d_mono, sk, nullptr,
+                                     nullptr, nullptr, ex->chain_fast && k ? ex->sub_fast[k - 1] : nullptr,
+                                     ex->chain_fast ? ex->sub_fast[k] : nullptr));
+            if (k) SLAM_HIP_TRY(hipEventRecord(ex->sub_join[k], sk));
+            f0 += nf;
+        }
+        for (int k = 1; k < nsub; k++) SLAM_HIP_TRY(hipStreamWaitEvent(s, ex->sub_join[k], 0));
+    }
     ex->last_frames = nframes;
     ex->last_img = d_img;
     return SLAM_OK;
@@ -1556,10 +1640,27 @@ slam_status slamhot_extractor_create(const slam_orb_params* params, int device, 
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ex->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&ex->side, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&ex->ev_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&ex->ev_join, hipEventDisableTiming) != hipSuccess) {
-        delete ex;
+        hipEventCreateWithFlags(&ex->ev_join, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ex->sub_fork, hipEventDisableTiming) != hipSuccess) {
+        slamhot_extractor_destroy(ex);
         return SLAM_EHIP;
     }
+    {
+        const char* e = std::getenv("SLAMHOT_SUBSTREAMS");
+        if (e) ex->nsub = std::max(1, std::min(slam_extractor::kMaxSub, std::atoi(e)));
+        const char* c = std::getenv("SLAMHOT_CHAIN_FAST");
+        ex->chain_fast = c && c[0] == '1';
+    }
+    for (int k = 0; k < slam_extractor::kMaxSub; k++)
+        if (hipStreamCreateWithFlags(&ex->sub[k], hipStreamNonBlocking) != hipSuccess ||
+            hipStreamCreateWithFlags(&ex->sub_side[k], hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&ex->sub_join[k], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&ex->sub_bfork[k], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&ex->sub_bjoin[k], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&ex->sub_fast[k], hipEventDisableTiming) != hipSuccess) {
+            slamhot_extractor_destroy(ex);
+            return SLAM_EHIP;
+        }
     *out = ex;
     return SLAM_OK;
 }
@@ -1577,6 +1678,15 @@ void slamhot_extractor_destroy(slam_extractor* ex) {
     for (auto& m : ex->marks) { ex->pool.push_back(m.a); ex->pool.push_back(m.b); }
     for (hipEvent_t e : ex->pool) (void)hipEventDestroy(e);
     if (ex->side) (void)hipStreamSynchronize(ex->side);
+    for (int k = 0; k < slam_extractor::kMaxSub; k++) {
+        if (ex->sub[k]) (void)hipStreamSynchronize(ex->sub[k]);
+        if (ex->sub_side[k]) (void)hipStreamSynchronize(ex->sub_side[k]);
+        for (hipEvent_t e : {ex->sub_join[k], ex->sub_bfork[k], ex->sub_bjoin[k], ex->sub_fast[k]})
+            if (e) (void)hipEventDestroy(e);
+        if (ex->sub[k]) (void)hipStreamDestroy(ex->sub[k]);
+        if (ex->sub_side[k]) (void)hipStreamDestroy(ex->sub_side[k]);
+    }
+    if (ex->sub_fork) (void)hipEventDestroy(ex->sub_fork);
     if (ex->ev_fork) (void)hipEventDestroy(ex->ev_fork);
     if (ex->ev_join) (void)hipEventDestroy(ex->ev_join);
     if (ex->side) (void)hipStreamDestroy(ex->side);

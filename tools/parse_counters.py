@@ -35,6 +35,14 @@ def main():
         print(k, {c: round(v, 1) for c, v in sorted(d.items())})
     print("traffic bytes/launch:", {k: int(v) for k, v in traffic.items()})
     (out / "traffic.json").write_text(json.dumps(traffic, indent=1))
+    if len(sys.argv) > 2 and sys.argv[2] in traffic:
+        # bench.py reads this for roofline.traffic: kernel, shape of the run, HBM bytes / launch
+        k = sys.argv[2]
+        meta = dict(kernel=k, batch=int(sys.argv[3]), width=int(sys.argv[4]), bytes_per_launch=int(traffic[k]),
+                    fetch_size_kib=summary[k]["FETCH_SIZE"], write_size_kib=summary[k]["WRITE_SIZE"],
+                    note="2 x FETCH_SIZE + WRITE_SIZE per MI355X_MICROARCH.md HBM section (the x2 is calibrated "
+                         "there for 16 B/lane streaming reads; this kernel stages with 4 B/lane loads)")
+        Path("profiles/traffic_latest.json").write_text(json.dumps(meta, indent=1))
 
 
 if __name__ == "__main__":
