@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <thread>
@@ -1434,8 +1435,15 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
         s->harena_cap = LY.total;
     }
     const Plan HP = bind(s->harena, LY);
+    const auto t_fill0 = std::chrono::steady_clock::now();
     st = plan_fill(n_prob, probs, hidx_all, np_of, opt, Z, HP);
     if (st != SLAM_OK) return st;
+    if (std::getenv("SLAMHOT_LBA_PLAN_TIMING")) {
+        const auto t1 = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "lba plan: sizes+alloc %.3f ms, fill %.3f ms, arena %.1f MB\n",
+                     std::chrono::duration<double, std::milli>(t_fill0 - t_plan0).count(),
+                     std::chrono::duration<double, std::milli>(t1 - t_fill0).count(), LY.total / 1e6);
+    }
     SLAM_HIP_TRY(s->arena.ensure(LY.total));
     SLAM_HIP_TRY(hipMemcpyAsync(s->arena.p, s->harena, LY.total, hipMemcpyHostToDevice, S));
     const Plan DP = bind((unsigned char*)s->arena.p, LY);

@@ -574,6 +574,29 @@ class LocalBundleAdjustment:
         res = [lba_result_dict(ress[i], outs[i][2]) for i in range(len(ws))]
         return res[0] if single else res
 
+    def prepare(self, windows, iters_first=5, iters_second=10, user_lambda_init=0.0):
+        """Flatten windows into C structs once (what a C++ caller already holds); returns a
+        callable that runs slamhot_lba_solve on them and returns the LM iteration total."""
+        ws = list(windows)
+        probs = (LbaProblem * len(ws))()
+        ress = (LbaResult * len(ws))()
+        keep = []
+        for i, w in enumerate(ws):
+            p, r, o = make_lba_problem(w)
+            probs[i] = p
+            ress[i] = r
+            keep.append((p, r, o))
+        opt = LbaOptions(iters_first, iters_second, user_lambda_init)
+        h = self._h
+        fn = lib().slamhot_lba_solve
+
+        def run():
+            check(fn(h, len(ws), probs, C.byref(opt), None, ress), "lba_solve")
+            return sum(ress[i].iterations[0] + ress[i].iterations[1] for i in range(len(ws)))
+
+        run.keep = (probs, ress, keep, opt)
+        return run
+
     def last_stats(self):
         """(device_ms, plan_ms, syncs) of the last solve."""
         ms, plan, syncs = C.c_double(0), C.c_double(0), I(0)
