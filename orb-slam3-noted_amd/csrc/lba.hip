@@ -460,11 +460,24 @@ __device__ inline void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// One wave per 6x6 block (i1 <= i2) of the Schur complement: lanes stride over the block's
-// contributions (one per point observed by both poses), each accumulating the full 6x6
-// B_a Dinv Hpl_b^T, then a butterfly reduction.  The reference block (i1, i2) (upper) is written
-// transposed into the lower triangle of the dense row-major matrix; diagonal blocks also
-// produce the rhs row b_s = b_p - sum B db (augmented row n).
+// kSchurLanes (16) lanes per 6x6 block (i1 <= i2) of the Schur complement, four blocks per wave:
+// lanes stride over the block's contributions (one per point observed by both poses), each
+// accumulating the full 6x6 B_a Dinv Hpl_b^T, then a butterfly inside the lane group (a
+// config-4 off-diagonal block has ~50 contributions: ~3 per lane; 8 or 4 lanes measured slower).  The reference
+// block (i1, i2) (upper) is written transposed into the lower triangle of the dense row-major
+// matrix; diagonal blocks also produce the rhs row b_s = b_p - sum B db (augmented row n).
+#ifndef SCHUR_LANES
+#define SCHUR_LANES 16
+#endif
+constexpr int kSchurLanes = SCHUR_LANES;
+
+template <int W16>
+__device__ inline double group_sum(double v) {
+#pragma unroll
+    for (int o = W16 / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, W16);
+    return v;
+}
+
 __global__ void __launch_bounds__(256) k_schur_block(int nblk_total, const int2* __restrict__ blk_pose,
                                                      const int* __restrict__ blk_win, const int* __restrict__ ct_off,
                                                      const int2* __restrict__ ct, const WinDesc* __restrict__ wins,
@@ -472,68 +485,76 @@ __global__ void __launch_bounds__(256) k_schur_block(int nblk_total, const int2*
                                                      const double* __restrict__ bp, const int* __restrict__ pe_off,
                                                      const int* __restrict__ pe, const double* __restrict__ lin,
                                                      const double* __restrict__ tr, double* __restrict__ Hs) {
-    const int blk = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (blk >= nblk_total) return;
-    const int win = blk_win[blk];
+    const int blk = blockIdx.x * (256 / kSchurLanes) + threadIdx.x / kSchurLanes, lane = threadIdx.x % kSchurLanes;
+    const bool live = blk < nblk_total;
+    const int b = live ? blk : 0;
+    const int win = blk_win[b];
     const WinCtl& C = ctl[win];
-    if (!C.need_trial) return;
+    const bool act = live && C.need_trial;
     const WinDesc W = wins[win];
-    const int2 ij = blk_pose[blk];  // local free-pose indices i1 <= i2
+    const int2 ij = blk_pose[b];  // local free-pose indices i1 <= i2
     const int i1 = ij.x, i2 = ij.y;
-    double* H = Hs + W.hs_off;
     double acc[36];
 #pragma unroll
     for (int k = 0; k < 36; k++) acc[k] = 0.0;
-    for (int k = ct_off[blk] + lane; k < ct_off[blk + 1]; k += 64) {
-        const int2 ab = ct[k];
-        const double* BD = tr + (long long)kTrStride * ab.x;
-        const double* Bj = lin + (long long)kHplStride * ab.y;
-        double bd[18], bj[18];
+    if (act) {
+        for (int k = ct_off[b] + lane; k < ct_off[b + 1]; k += kSchurLanes) {
+            const int2 ab = ct[k];
+            const double* BD = tr + (long long)kTrStride * ab.x;
+            const double* Bj = lin + (long long)kHplStride * ab.y;
+            double bd[18], bj[18];
 #pragma unroll
-        for (int t = 0; t < 18; t++) {
-            bd[t] = BD[t];
-            bj[t] = Bj[t];
+            for (int t = 0; t < 18; t++) {
+                bd[t] = BD[t];
+                bj[t] = Bj[t];
+            }
+#pragma unroll
+            for (int r = 0; r < 6; r++)
+#pragma unroll
+                for (int c = 0; c < 6; c++)
+                    acc[6 * r + c] += bd[3 * r] * bj[3 * c] + bd[3 * r + 1] * bj[3 * c + 1] + bd[3 * r + 2] * bj[3 * c + 2];
         }
-#pragma unroll
-        for (int r = 0; r < 6; r++)
-#pragma unroll
-            for (int c = 0; c < 6; c++)
-                acc[6 * r + c] += bd[3 * r] * bj[3 * c] + bd[3 * r + 1] * bj[3 * c + 1] + bd[3 * r + 2] * bj[3 * c + 2];
     }
-    double mine = 0.0;
 #pragma unroll
-    for (int k = 0; k < 36; k++) {
-        const double t = wave_sum(acc[k]);
-        if (lane == k) mine = t;
-    }
-    double rhs = 0.0;
-    if (i1 == i2) {
-        const int gp = W.pose0 + i1;
-        double sb[6] = {0, 0, 0, 0, 0, 0};
-        for (int k = pe_off[gp] + lane; k < pe_off[gp + 1]; k += 64) {
+    for (int k = 0; k < 36; k++) acc[k] = group_sum<kSchurLanes>(acc[k]);
+    double sb[6] = {0, 0, 0, 0, 0, 0};
+    const int gp = W.pose0 + i1;
+    if (act && i1 == i2) {
+        for (int k = pe_off[gp] + lane; k < pe_off[gp + 1]; k += kSchurLanes) {
             const double* T = tr + (long long)kTrStride * pe[k] + 18;
 #pragma unroll
             for (int r = 0; r < 6; r++) sb[r] += T[r];
         }
-#pragma unroll
-        for (int r = 0; r < 6; r++) {
-            const double t = wave_sum(sb[r]);
-            if (lane == 36 + r) rhs = bp[8 * (long long)gp + r] - t;
-        }
     }
-    if (lane < 36) {
-        const int r = lane / 6, c = lane % 6;
+#pragma unroll
+    for (int r = 0; r < 6; r++) sb[r] = group_sum<kSchurLanes>(sb[r]);
+    if (!act) return;
+    double* H = Hs + W.hs_off;
+#pragma unroll
+    for (int q = 0; q < (36 + kSchurLanes - 1) / kSchurLanes; q++) {
+        const int e = lane + kSchurLanes * q;
+        if (e >= 36) break;
+        const int r = e / 6, c = e % 6;
         double v = 0.0;
         if (i1 == i2) {
             const int rr = r <= c ? r : c, cc = r <= c ? c : r;
-            v = Hpp[24 * (long long)(W.pose0 + i1) + sym6(rr, cc)];
+            v = Hpp[24 * (long long)gp + sym6(rr, cc)];
             if (r == c) v += C.lambda;
         }
-        v -= mine;
+        double m = 0.0;
+#pragma unroll
+        for (int k = 0; k < 36; k++)
+            if (k == e) m = acc[k];
+        v -= m;
         // upper (i1, i2)[r][c] -> lower element (6 i2 + c, 6 i1 + r)
         if (i1 != i2 || r <= c) H[(long long)(6 * i2 + c) * W.ld + 6 * i1 + r] = v;
-    } else if (lane < 42 && i1 == i2) {
-        H[(long long)ldlt_npad(W.n) * W.ld + 6 * i1 + (lane - 36)] = rhs;
+    }
+    if (i1 == i2 && lane < 6) {
+        double s6 = 0.0;
+#pragma unroll
+        for (int r = 0; r < 6; r++)
+            if (r == lane) s6 = sb[r];
+        H[(long long)ldlt_npad(W.n) * W.ld + 6 * i1 + lane] = bp[8 * (long long)gp + lane] - s6;
     }
 }
 
@@ -1531,7 +1552,7 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
                                                                as<double>(s->bl), as<double>(s->lin),
                                                                as<double>(s->tr));
                 if (H.nblk)
-                    k_schur_block<<<blocks(H.nblk, 4), 256, 0, S>>>(
+                    k_schur_block<<<blocks(H.nblk, 256 / kSchurLanes), 256, 0, S>>>(
                         H.nblk, DP.blk_pose, DP.blk_win, DP.ct_off, DP.ct, dW,
                         dC, as<double>(s->Hpp), as<double>(s->bp), DP.pe_off, DP.pe,
                         as<double>(s->lin), as<double>(s->tr), as<double>(s->Hs));

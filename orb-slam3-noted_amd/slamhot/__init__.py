@@ -8,6 +8,7 @@ HIP library; there is no CPU fallback — a missing library or device raises.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from pathlib import Path
 
 import numpy as np
@@ -139,9 +140,10 @@ def lib() -> C.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    if not LIB_PATH.exists():
-        raise RuntimeError(f"libslamhot.so not built: {LIB_PATH} (run __graft_entry__.build())")
-    L = C.CDLL(str(LIB_PATH))
+    path = Path(os.environ.get("SLAMHOT_LIB", str(LIB_PATH)))  # experiment builds (tools/)
+    if not path.exists():
+        raise RuntimeError(f"libslamhot.so not built: {path} (run __graft_entry__.build())")
+    L = C.CDLL(str(path))
     L.slamhot_version.restype = C.c_char_p
     L.slamhot_status_string.argtypes = [I]
     L.slamhot_status_string.restype = C.c_char_p
