@@ -222,7 +222,7 @@ def main():
             "traffic": traffic,
             "algorithmic_bytes_per_launch": int(dom_bytes),
             "frames_per_launch": frames_per_launch,
-            "measured": "HIP events, isolated pass after the timed region (1 batch in flight)",
+            "measured": "HIP events, isolated pass after the timed region (1 batch in flight, stages serialized)",
             "avg_launch_ms": round(dom_avg_s * 1000.0, 5),
         },
         "stages_ms_per_step": {k: round(v, 5) for k, v in stage_avg_ms.items()},

@@ -85,6 +85,16 @@ __device__ __forceinline__ int level_pitch(const DevPlan& P, int l) {
     return l == 0 ? P.W : P.lv[l].pitch;
 }
 
+// packed u16 pairs (v_pk_*_u16) for the SWAR FAST pre-test
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ us2 as_us2(uint32_t x) { return __builtin_bit_cast(us2, x); }
+__device__ __forceinline__ uint32_t as_u32(us2 x) { return __builtin_bit_cast(uint32_t, x); }
+
+// acc + number of set bits of m below this lane (v_mbcnt_lo/hi)
+__device__ __forceinline__ int mbcnt64(uint64_t m, int acc) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, (uint32_t)acc));
+}
+
 // packed candidate / keypoint: x (12 b) | y (12 b) | score (8 b)
 __device__ __forceinline__ uint32_t pack_kp(int x, int y, int s) {
     return (uint32_t)x | ((uint32_t)y << 12) | ((uint32_t)s << 24);
@@ -429,7 +439,7 @@ __global__ void __launch_bounds__(256) k_fast_wave(Bufs b, const int32_t* list, 
     const uint8_t* img = level_ptr(b, P, f, l);
     const int pitch = level_pitch(P, l);
     const int cw = cd.cw, ch = cd.ch;
-    const int tw = cw - 6, th = ch - 6;
+    const int th = ch - 6;
     uint8_t* base_ptr = fw_smem + wave * lay.total;
     uint8_t* roi = base_ptr + lay.roi;
     uint8_t* map = base_ptr + lay.map;
@@ -440,31 +450,30 @@ __global__ void __launch_bounds__(256) k_fast_wave(Bufs b, const int32_t* list, 
     const int tlow = min(ti, tm);
 
     // stage the ROI with independent 32-bit loads (row start aligned down to 4 bytes; the
-    // ROI origin inside LDS is then `sh` bytes into each row), zero the M map
+    // ROI origin inside LDS is then `sh` bytes into each row), zero the M map.  Lane =
+    // (row offset, dword column), fixed for the wave; 8 rows per lane in flight.
     const int sh = (pitch & 3) ? 0 : (cd.iniX & 3);
+    uint32_t* roi32 = reinterpret_cast<uint32_t*>(roi);
     {
         const uint8_t* src = img + (size_t)cd.iniY * pitch + (cd.iniX - sh);
         if ((pitch & 3) == 0) {
-            const int wd = (sh + cw + 3) >> 2;
-            const int nd = wd * ch;
-            const float inv_wd = 1.0f / (float)wd;
-            uint32_t* roi32 = reinterpret_cast<uint32_t*>(roi);
-            for (int base = 0; base < nd; base += 64 * 8) {
-                uint32_t v[8];
-                int dst[8];
+            const int wd = (sh + cw + 3) >> 2;  // <= kRoiStride / 4
+            const int rp = 64 / wd;
+            const int lr = lane / wd, lc = lane - lr * wd;
+            if (lr < rp) {
+                for (int r0 = lr; r0 < ch; r0 += 8 * rp) {
+                    uint32_t v[8];
 #pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    const int i = base + k * 64 + lane;
-                    dst[k] = -1;
-                    if (i < nd) {
-                        const int r = (int)(((float)i + 0.5f) * inv_wd), c = i - r * wd;
-                        v[k] = *reinterpret_cast<const uint32_t*>(src + (size_t)r * pitch + 4 * c);
-                        dst[k] = r * (kRoiStride / 4) + c;
+                    for (int k = 0; k < 8; k++) {
+                        const int r = r0 + k * rp;
+                        if (r < ch) v[k] = *reinterpret_cast<const uint32_t*>(src + (size_t)r * pitch + 4 * lc);
+                    }
+#pragma unroll
+                    for (int k = 0; k < 8; k++) {
+                        const int r = r0 + k * rp;
+                        if (r < ch) roi32[r * (kRoiStride / 4) + lc] = v[k];
                     }
                 }
-#pragma unroll
-                for (int k = 0; k < 8; k++)
-                    if (dst[k] >= 0) roi32[dst[k]] = v[k];
             }
         } else {
             for (int r = 0; r < ch; r++)
@@ -479,37 +488,54 @@ __global__ void __launch_bounds__(256) k_fast_wave(Bufs b, const int32_t* list, 
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 
-    // pass A over the row-major linear index i = r*tw + c (all 64 lanes busy whatever tw);
-    // r = floor((i + 0.5) / tw) in float is exact here (i < 2^13, tw <= 64).  Four chunks of
-    // 64 pixels per iteration: their LDS loads are all issued before any is consumed.
+    // pass A, four pixels per lane in packed u16 pairs (even / odd bytes of an LDS dword).
+    // Lane = (row, dword group) over the dwords covering the tested columns; the compass
+    // test per pixel is  min(p0,p8), min(p4,p12) < v - t  (dark) or  max(..) > v + t
+    // (bright), i.e. saturating (v - t - max of the mins) | (min of the maxes - v - t) != 0.
+    // Four ballots (one per byte) + mbcnt give row-major compaction.
     int na = 0;
     {
-        const int npx = tw * th;
-        const float inv_tw = 1.0f / (float)tw;
-        for (int j = 0; j < npx; j += 256) {
-            bool pass[4];
-            int code[4];
+        const int g0 = (sh + 3) >> 2, g1 = (sh + cw - 4) >> 2;
+        const int ng = g1 - g0 + 1;  // <= 17
+        const int rpi = 64 / ng;     // tested rows per iteration
+        const int ar = lane / ng, gd = g0 + (lane - ar * ng);
+        uint32_t cmask = 0;
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int i = j + 64 * u + lane;
-                const bool in = i < npx;
-                const int ii = in ? i : 0;
-                const int r = (int)(((float)ii + 0.5f) * inv_tw);
-                const int cc = ii - r * tw;
-                code[u] = r * 64 + cc;
-                const uint8_t* c = roi + (r + 3) * kRoiStride + cc + 3;
-                const int v = c[0];
-                const int d0 = v - c[3 * kRoiStride], d8 = v - c[-3 * kRoiStride];
-                const int d4 = v - c[3], d12 = v - c[-3];
-                pass[u] = in && ((max(d0, d8) > tlow && max(d4, d12) > tlow) ||
-                                 (min(d0, d8) < -tlow && min(d4, d12) < -tlow));
-            }
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const uint64_t m = __ballot(pass[u]);
-                if (pass[u]) lst[na + __popcll(m & lt)] = (uint16_t)code[u];
-                na += __popcll(m);
-            }
+        for (int k = 0; k < 4; k++) {
+            const int x = 4 * gd + k - sh;  // ROI column of byte k
+            if (x >= 3 && x <= cw - 4) cmask |= 0xFFu << (8 * k);
+        }
+        if (ar >= rpi) cmask = 0;
+        const int code0 = (4 * gd - sh - 3) + ar * 64;  // code of byte 0 in row 0
+        const us2 T = {(unsigned short)tlow, (unsigned short)tlow};
+        constexpr int RS = kRoiStride / 4;
+        for (int rt = 0; rt < th; rt += rpi) {
+            const int r = rt + ar;
+            const uint32_t m = r < th ? cmask : 0u;
+            const uint32_t* row = roi32 + (min(r, th - 1) + 3) * RS + gd;
+            const uint32_t W0 = row[-1], W1 = row[0], W2 = row[1], U = row[-3 * RS], D = row[3 * RS];
+            auto set = [&](uint32_t v, uint32_t p0, uint32_t p8, uint32_t p4, uint32_t p12) -> uint32_t {
+                const us2 V = as_us2(v), a = as_us2(p0), bq = as_us2(p8), c = as_us2(p4), d = as_us2(p12);
+                const us2 L = __builtin_elementwise_max(__builtin_elementwise_min(a, bq), __builtin_elementwise_min(c, d));
+                const us2 H = __builtin_elementwise_min(__builtin_elementwise_max(a, bq), __builtin_elementwise_max(c, d));
+                return as_u32(__builtin_elementwise_sub_sat(V, L + T) | __builtin_elementwise_sub_sat(H, V + T));
+            };
+            const uint32_t fe = set(__builtin_amdgcn_perm(0u, W1, 0x0c020c00u), __builtin_amdgcn_perm(0u, D, 0x0c020c00u),
+                                    __builtin_amdgcn_perm(0u, U, 0x0c020c00u), __builtin_amdgcn_perm(W2, W1, 0x0c050c03u),
+                                    __builtin_amdgcn_perm(W1, W0, 0x0c030c01u));
+            const uint32_t fo = set(__builtin_amdgcn_perm(0u, W1, 0x0c030c01u), __builtin_amdgcn_perm(0u, D, 0x0c030c01u),
+                                    __builtin_amdgcn_perm(0u, U, 0x0c030c01u), __builtin_amdgcn_perm(W2, W1, 0x0c060c04u),
+                                    __builtin_amdgcn_perm(W1, W0, 0x0c040c02u));
+            const uint32_t F = (fe | (fo << 8)) & m;  // byte k != 0 <=> pixel k survives
+            const bool f0 = (F & 0xFFu) != 0, f1 = (F & 0xFF00u) != 0, f2 = (F & 0xFF0000u) != 0, f3 = (F >> 24) != 0;
+            const uint64_t b0 = __ballot(f0), b1 = __ballot(f1), b2 = __ballot(f2), b3 = __ballot(f3);
+            int pos = mbcnt64(b3, mbcnt64(b2, mbcnt64(b1, mbcnt64(b0, na))));
+            const int code = code0 + rt * 64;
+            if (f0) lst[pos++] = (uint16_t)code;
+            if (f1) lst[pos++] = (uint16_t)(code + 1);
+            if (f2) lst[pos++] = (uint16_t)(code + 2);
+            if (f3) lst[pos] = (uint16_t)(code + 3);
+            na += __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1565,10 +1591,13 @@ static slam_status launch_range(slam_extractor* ex, int f0, int nframes, const u
 static slam_status launch_pipeline(slam_extractor* ex, int nframes, const uint8_t* d_img, int lap0,
                                    int lap1, slam_keypoint* d_kps, uint8_t* d_desc, int cap,
                                    int32_t* d_n, int32_t* d_mono, hipStream_t s) {
-    int nsub = ex->serial ? 1 : std::min(ex->nsub, nframes / 8);
+    // profiling (per-stage HIP events) serializes the stages on s, so each bracket times one
+    // kernel alone (its own launch duration, comparable with rocprofv3's kernel trace)
+    const bool serial = ex->serial || ex->profiling;
+    int nsub = serial ? 1 : std::min(ex->nsub, nframes / 8);
     if (nsub <= 1) {
         SLAM_TRY_ST(launch_range(ex, 0, nframes, d_img, lap0, lap1, d_kps, d_desc, cap, d_n, d_mono, s,
-                                 ex->serial ? nullptr : ex->side, ex->ev_fork, ex->ev_join));
+                                 serial ? nullptr : ex->side, ex->ev_fork, ex->ev_join));
     } else {
         // range 0 runs on the caller's stream, ranges 1.. on the handle's sub-streams; with the
         // blur kept in-stream that is nsub hardware queues (GPU_MAX_HW_QUEUES is 4 by default)
