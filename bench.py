@@ -56,8 +56,7 @@ def algorithmic_bytes(w, h, kps_per_frame):
         "k_fast_wave": sum(P),                        # read every level pixel once (+ candidates, small)
         "k_octree": 0,                                # candidate lists only (KB, L2-resident)
         "k_layout": 0,
-        "k_blur": 2 * sum(P),                         # read + write every level
-        "k_orb": kps_per_frame * (4 + 28 + 32),       # kp in, kp + descriptor out
+        "k_orb": kps_per_frame * (4 + 28 + 32),       # kp in, kp + descriptor out (43x43 raw windows: L2)
     }
     pipeline = P[0] + sum(P[1:]) + sum(P) + kps_per_frame * 60  # SURVEY.md §8(d) B_frame
     return out, pipeline

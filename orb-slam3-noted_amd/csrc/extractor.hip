@@ -1,17 +1,17 @@
 // extractor.hip — MI355X (gfx950) ORB extractor: the device side of
 // ORBextractor::operator() (ORBextractor.cc:1068-1150), batched over frames.
 //
-// Pipeline per batch (launch stream + a side stream for the blur):
+// Pipeline per batch (one stream):
 //   k_resize3     x (L-1)  chained INTER_LINEAR pyramid            ComputePyramid :1152
 //   k_fast_wave   x 1      FAST-9 score + per-cell 3x3 NMS, 1 wave/cell ComputeKeyPointsOctTree :787-853
 //   k_fast_cells  x 1      the same for cells wider than one wave (1 WG/cell)
 //   k_octree      x 1      quadtree distribution, 1 WG/(frame,lvl) DistributeOctTree :537-761
 //   k_layout      x 1      lapping-area output order, 1 WG/frame   operator() :1100-1146
-//   k_blur3       x 1      GaussianBlur 7x7 sigma 2 fixed point    operator() :1114-1115
-//   k_orb2        x 1      IC angle + rBRIEF, one wave per kp      IC_Angle :75, computeOrbDescriptor :106
+//   k_orb3        x 1      IC angle + 7x7 blur window + rBRIEF,    IC_Angle :75, GaussianBlur :1115,
+//                          one wave per kp                         computeOrbDescriptor :106
 //
 // Data layout in HBM (per handle, batch-major): input frames (level 0, tight rows); pyramid
-// levels 1.. per frame, rows padded to 64 B; blurred levels per frame; per-cell candidate
+// levels 1.. per frame, rows padded to 64 B (no blurred copy: k_orb3 blurs windows); per-cell candidate
 // slots; per-(frame,level) octree keypoints; per-frame output index map.
 #include <hip/hip_runtime.h>
 
@@ -57,7 +57,6 @@ struct DevPlan {
 struct Bufs {
     const uint8_t* img;     // level 0 frames, tight rows (W bytes)
     uint8_t* pyr;           // levels >= 1, per frame pyr_frame bytes
-    uint8_t* blur;          // all levels blurred, per frame blur_frame bytes
     uint32_t* cell_keys;    // per frame ncells*slot_cap packed candidates
     int32_t* cell_cnt;      // per frame ncells
     uint32_t* keys_g;       // per frame key_slots (octree overflow scratch: keys)
@@ -1000,131 +999,25 @@ __device__ __forceinline__ int refl101(int i, int n) {
 
 
 
-struct BlurTile {
-    int16_t level, pad;
-    int16_t x0, y0;
-};
-
-
 // ---------------------------------------------------------------------------------------
-// k_blur3: GaussianBlur for all levels, one launch, 128 x 32 output tiles.
-//  horizontal: output x needs bytes x-3..x+3 = 2 x v_alignbyte + 2 x v_dot4_u32_u8 against
-//              the packed Q8 taps (k0 k1 k2 k3 | k2 k1 k0 0); exact u32 row sums in LDS
-//  vertical:   each thread 4 columns x 4 rows from one 16-byte LDS read per tap row
-// Integer-exact: same sums as the OpenCV fixed-point path (u16 row sums never exceed
-// 255*256), rounded (acc + 2^15) >> 16.
+// k_orb3: IC angle + GaussianBlur + rBRIEF fused, one wave per keypoint, 4 per workgroup.
+// The reference blurs a clone of every level (ORBextractor.cc:1113-1115) only to sample it
+// at the 512 pattern points of each keypoint; here each wave blurs just the 37x37 window the
+// rotated pattern can reach (radius 18.38 -> rounded offsets within +-18), from one 43x43
+// raw window that also serves IC_Angle (its 31x31 disc is the window's centre).  Same
+// integer arithmetic as the OpenCV 8U fixed-point path (Q8 taps, exact row sums, rounded
+// (acc + 2^15) >> 16, BORDER_REFLECT_101 at the level bounds), so the bits are those of the
+// whole-level blur; the blurred level is never written to HBM.
+//   raw: 43 (+1) rows x 13 dwords (staged byte j <-> level column xs + j, xs = (kx-21) & ~3)
+//   hp : 22 row pairs x 40 dwords of exact horizontal sums, rows 2p | 2p+1 << 16 (column
+//        c <-> kx - 18 + c)
+//   bl : 37 rows x 40 bytes, aliased onto raw once the horizontal pass has read it
 // ---------------------------------------------------------------------------------------
-constexpr int kB3W = 128, kB3H = 32, kB3SH = kB3H + 6, kB3SW = 144;  // staged stride (bytes)
+constexpr int kO3R = 43, kO3Pairs = 22, kO3RawS = 13, kO3HS = 40, kO3BlS = 40;
 
-__global__ void __launch_bounds__(256) k_blur3(Bufs b, const BlurTile* tiles, int ed) {
-    __shared__ __attribute__((aligned(16))) uint8_t src[kB3SH * kB3SW];
-    __shared__ __attribute__((aligned(16))) uint32_t hs[kB3SH * kB3W];
-    const DevPlan& P = *b.plan;
-    const BlurTile t = tiles[blockIdx.x];
-    const int l = t.level, f = blockIdx.y;
-    const DevLevel& L = P.lv[l];
-    const uint8_t* img = level_ptr(b, P, f, l);
-    const int pitch = level_pitch(P, l);
-    const int x0 = t.x0, y0 = t.y0;
-    const uint32_t k0 = 18, k1 = 34, k2 = ed ? 48 : 49, k3 = ed ? 56 : 55;
-    const uint32_t KA = k0 | (k1 << 8) | (k2 << 16) | (k3 << 24);
-    const uint32_t KB = k2 | (k1 << 8) | (k0 << 16);
-    // staged byte i of a row <-> image column x0 - 4 + i (i in [0, 136)); rows and columns
-    // outside the level reflect (BORDER_REFLECT_101).  Whole in-range dwords are loaded as
-    // dwords; only the dwords that straddle the left/right border go byte by byte.
-    const int wfull = (pitch & 3) ? 0 : (L.w & ~3);  // columns [0, wfull) loadable as dwords
-    constexpr int KSTG = (kB3SH * 34 + 255) / 256;
-    uint32_t v[KSTG];
-#pragma unroll
-    for (int k = 0; k < KSTG; k++) {
-        const int i = threadIdx.x + 256 * k;
-        v[k] = 0;
-        if (i < kB3SH * 34) {
-            const int r = i / 34, c4 = i - r * 34;
-            const int yy = refl101(min(max(y0 - 3 + r, -3), L.h + 2), L.h);
-            const uint8_t* rowp = img + (size_t)yy * pitch;
-            const int x = x0 - 4 + 4 * c4;
-            if (x >= 0 && x + 4 <= wfull) {
-                v[k] = *reinterpret_cast<const uint32_t*>(rowp + x);
-            } else {
-#pragma unroll
-                for (int e = 0; e < 4; e++) {
-                    const int xx = refl101(min(max(x + e, -4), L.w + 3), L.w);
-                    v[k] |= (uint32_t)rowp[xx] << (8 * e);
-                }
-            }
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < KSTG; k++) {
-        const int i = threadIdx.x + 256 * k;
-        if (i < kB3SH * 34) {
-            const int r = i / 34, c4 = i - r * 34;
-            *reinterpret_cast<uint32_t*>(&src[r * kB3SW + 4 * c4]) = v[k];
-        }
-    }
-    __syncthreads();
-    // horizontal: thread -> (staged row, 4 output columns 4q..4q+3); output column c uses
-    // staged bytes c+1 .. c+7
-    for (int i = threadIdx.x; i < kB3SH * (kB3W / 4); i += blockDim.x) {
-        const int r = i >> 5, q = i & 31;
-        const uint32_t* row = reinterpret_cast<const uint32_t*>(&src[r * kB3SW]);
-        const uint32_t D0 = row[q], D1 = row[q + 1], D2 = row[q + 2];
-        uint4 o;
-        o.x = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(D2, D1, 1), KB,
-                                     __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(D1, D0, 1), KA, 0u, false), false);
-        o.y = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(D2, D1, 2), KB,
-                                     __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(D1, D0, 2), KA, 0u, false), false);
-        o.z = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(D2, D1, 3), KB,
-                                     __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(D1, D0, 3), KA, 0u, false), false);
-        o.w = __builtin_amdgcn_udot4(D2, KB, __builtin_amdgcn_udot4(D1, KA, 0u, false), false);
-        *reinterpret_cast<uint4*>(&hs[r * kB3W + 4 * q]) = o;
-    }
-    __syncthreads();
-    // vertical: thread -> 4 columns (cq) x 4 rows (rq)
-    const int cq = threadIdx.x & 31, rq = threadIdx.x >> 5;
-    const int x = x0 + 4 * cq;
-    if (x >= L.w) return;
-    uint32_t acc[4][4] = {};
-    const uint32_t kk[7] = {k0, k1, k2, k3, k2, k1, k0};
-#pragma unroll
-    for (int j = 0; j < 10; j++) {
-        const uint4 h = *reinterpret_cast<const uint4*>(&hs[(4 * rq + j) * kB3W + 4 * cq]);
-#pragma unroll
-        for (int o = 0; o < 4; o++) {
-            const int tap = j - o;
-            if (tap >= 0 && tap < 7) {
-                acc[o][0] += kk[tap] * h.x;
-                acc[o][1] += kk[tap] * h.y;
-                acc[o][2] += kk[tap] * h.z;
-                acc[o][3] += kk[tap] * h.w;
-            }
-        }
-    }
-    uint8_t* dst = b.blur + (size_t)f * P.blur_frame + L.blur_off + x;
-#pragma unroll
-    for (int o = 0; o < 4; o++) {
-        const int y = y0 + 4 * rq + o;
-        if (y >= L.h) break;
-        uint32_t w = 0;
-#pragma unroll
-        for (int e = 0; e < 4; e++) w |= min((acc[o][e] + (1u << 15)) >> 16, 255u) << (8 * e);
-        *reinterpret_cast<uint32_t*>(dst + (size_t)y * L.pitch) = w;
-    }
-}
-
-
-// ---------------------------------------------------------------------------------------
-// k_orb2: k_orb with both windows staged in LDS by wide loads: the 31x31 raw disc window
-// (IC_Angle) and the 37x37 blurred window (the rotated pattern never leaves radius 18.38,
-// so rounded offsets stay within +-18).  9 + 10 dwords per row, rows spread over lanes;
-// every later access is an LDS byte read.  One wave per keypoint, 4 per workgroup.
-// ---------------------------------------------------------------------------------------
-constexpr int kOrbRawS = 36, kOrbBlS = 40;
-
-__global__ void __launch_bounds__(256) k_orb2(Bufs b) {
-    __shared__ __attribute__((aligned(16))) uint8_t raw_all[4][31 * kOrbRawS];
-    __shared__ __attribute__((aligned(16))) uint8_t bl_all[4][37 * kOrbBlS];
+__global__ void __launch_bounds__(256) k_orb3(Bufs b) {
+    __shared__ __attribute__((aligned(16))) uint32_t raw_all[4][2 * kO3Pairs * kO3RawS];
+    __shared__ __attribute__((aligned(16))) uint32_t hp_all[4][kO3Pairs * kO3HS];
     const DevPlan& P = *b.plan;
     const int f = blockIdx.y;
     const int wave = threadIdx.x >> 6;
@@ -1142,77 +1035,62 @@ __global__ void __launch_bounds__(256) k_orb2(Bufs b) {
     const int kx = kp_x(key), ky = kp_y(key);
     const uint8_t* img = level_ptr(b, P, f, l);
     const int pitch = level_pitch(P, l);
-    const uint8_t* bl = b.blur + (size_t)f * P.blur_frame + L.blur_off;
-    uint8_t* raw = raw_all[wave];
-    uint8_t* blw = bl_all[wave];
-    // stage: raw rows ky-15..ky+15 from xr, blurred rows ky-18..ky+18 from xb (4-aligned)
-    const int xr = (kx - kHalfPatch) & ~3, shr_ = (kx - kHalfPatch) - xr;
-    const int xb = (kx - 18) & ~3, shb = (kx - 18) - xb;
-    if ((pitch & 3) == 0) {
-        uint32_t v[5];
-#pragma unroll
-        for (int k = 0; k < 5; k++) {
-            const int e = lane + 64 * k;
-            if (e < 31 * 9) {
-                const int r = e / 9, c = e - r * 9;
-                v[k] = *reinterpret_cast<const uint32_t*>(img + (size_t)(ky - kHalfPatch + r) * pitch + xr + 4 * c);
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < 5; k++) {
-            const int e = lane + 64 * k;
-            if (e < 31 * 9) {
-                const int r = e / 9, c = e - r * 9;
-                *reinterpret_cast<uint32_t*>(&raw[r * kOrbRawS + 4 * c]) = v[k];
-            }
-        }
-    } else {
-        for (int e = lane; e < 31 * kOrbRawS; e += 64) {
-            const int r = e / kOrbRawS, c = e - r * kOrbRawS;
-            raw[e] = img[(size_t)(ky - kHalfPatch + r) * pitch + xr + c];
-        }
-    }
+    uint32_t* raw = raw_all[wave];
+    uint32_t* hp = hp_all[wave];
+    const int xs = (kx - 21) & ~3, sh = (kx - 21) - xs;
+    // ---- stage the raw window (rows ky-21..ky+21 reflected, 12 dwords per row)
     {
-        uint32_t v[6];
+        const int wfull = (pitch & 3) ? 0 : (L.w & ~3);
+        uint32_t v[9];
 #pragma unroll
-        for (int k = 0; k < 6; k++) {
+        for (int k = 0; k < 9; k++) {
             const int e = lane + 64 * k;
-            if (e < 37 * 10) {
-                const int r = e / 10, c = e - r * 10;
-                v[k] = *reinterpret_cast<const uint32_t*>(bl + (size_t)(ky - 18 + r) * L.pitch + xb + 4 * c);
+            v[k] = 0;
+            if (e < kO3R * 12) {
+                const int r = e / 12, c = e - r * 12;
+                const int yy = refl101(ky - 21 + r, L.h);
+                const uint8_t* rowp = img + (size_t)yy * pitch;
+                const int x = xs + 4 * c;
+                if (x >= 0 && x + 4 <= wfull) {
+                    v[k] = *reinterpret_cast<const uint32_t*>(rowp + x);
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 4; q++) v[k] |= (uint32_t)rowp[refl101(min(x + q, L.w + 3), L.w)] << (8 * q);
+                }
             }
         }
 #pragma unroll
-        for (int k = 0; k < 6; k++) {
+        for (int k = 0; k < 9; k++) {
             const int e = lane + 64 * k;
-            if (e < 37 * 10) {
-                const int r = e / 10, c = e - r * 10;
-                *reinterpret_cast<uint32_t*>(&blw[r * kOrbBlS + 4 * c]) = v[k];
+            if (e < kO3R * 12) {
+                const int r = e / 12, c = e - r * 12;
+                raw[r * kO3RawS + c] = v[k];
             }
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const uint8_t* rawb = reinterpret_cast<const uint8_t*>(raw);
 
-    // --- orientation (IC_Angle, ORBextractor.cc:75-102): lanes 0..30 rows -15..0, 32..62 rows 1..15
+    // ---- orientation (IC_Angle, ORBextractor.cc:75-102) on the raw centre 31x31
     int m01 = 0, m10 = 0;
     {
         const int cl = lane & 31, half = lane >> 5;
         if (cl < 2 * kHalfPatch + 1) {
             const int u = cl - kHalfPatch;
             const int au = u < 0 ? -u : u;
-            const uint8_t* colp = raw + kHalfPatch * kOrbRawS + shr_ + kHalfPatch + u;
+            const uint8_t* colp = rawb + 21 * (4 * kO3RawS) + sh + 21 + u;
             int s0 = 0, s1 = 0;
             if (half == 0) {
 #pragma unroll
                 for (int v = -kHalfPatch; v <= 0; v++) {
-                    const int val = colp[v * kOrbRawS] & -(int)(au <= P.umax[-v]);
+                    const int val = colp[v * (4 * kO3RawS)] & -(int)(au <= P.umax[-v]);
                     s0 += val;
                     s1 += v * val;
                 }
             } else {
 #pragma unroll
                 for (int v = 1; v <= kHalfPatch; v++) {
-                    const int val = colp[v * kOrbRawS] & -(int)(au <= P.umax[v]);
+                    const int val = colp[v * (4 * kO3RawS)] & -(int)(au <= P.umax[v]);
                     s0 += val;
                     s1 += v * val;
                 }
@@ -1228,12 +1106,92 @@ __global__ void __launch_bounds__(256) k_orb2(Bufs b) {
     }
     const float angle = cv_fast_atan2((float)m01, (float)m10);
 
-    // --- descriptor (computeOrbDescriptor, ORBextractor.cc:106-145)
+    // ---- horizontal pass: 22 row pairs x 10 groups of 4 output columns; output column c
+    // needs staged bytes sh+c .. sh+c+6 (v_alignbyte by the runtime shift, two v_dot4 per
+    // output).  Rows 2p and 2p+1 go to the low / high half of one dword (hp), so the
+    // vertical pass takes two taps per v_dot2_u32_u16.  Row 43 is never staged: its sums
+    // only reach blurred rows >= 37, which are not kept.
+    constexpr uint32_t KA = 18u | (34u << 8) | (48u << 16) | (56u << 24);
+    constexpr uint32_t KB = 48u | (34u << 8) | (18u << 16);
+    auto hrow4 = [&](const uint32_t* row, uint32_t* h) {
+        const uint32_t D0 = row[0], D1 = row[1], D2 = row[2], D3 = row[3];
+        const uint32_t E0 = __builtin_amdgcn_alignbyte(D1, D0, sh);
+        const uint32_t E1 = __builtin_amdgcn_alignbyte(D2, D1, sh);
+        const uint32_t E2 = __builtin_amdgcn_alignbyte(D3, D2, sh);
+        h[0] = __builtin_amdgcn_udot4(E1, KB, __builtin_amdgcn_udot4(E0, KA, 0u, false), false);
+        h[1] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(E2, E1, 1), KB,
+                                      __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(E1, E0, 1), KA, 0u, false), false);
+        h[2] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(E2, E1, 2), KB,
+                                      __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(E1, E0, 2), KA, 0u, false), false);
+        h[3] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(E2, E1, 3), KB,
+                                      __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(E1, E0, 3), KA, 0u, false), false);
+    };
+    for (int it = lane; it < kO3Pairs * 10; it += 64) {
+        const int p = it / 10, q = it - p * 10;
+        uint32_t h0[4], h1[4];
+        hrow4(raw + (2 * p) * kO3RawS + q, h0);
+        hrow4(raw + (2 * p + 1) * kO3RawS + q, h1);
+        *reinterpret_cast<uint4*>(&hp[p * kO3HS + 4 * q]) =
+            make_uint4(h0[0] | (h1[0] << 16), h0[1] | (h1[1] << 16), h0[2] | (h1[2] << 16), h0[3] | (h1[3] << 16));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    // ---- vertical pass: lane -> 8 columns (g) x 4 output rows 4rb..4rb+3 (rb); 5 x 10 = 50
+    // lanes.  Output row y sums hs rows y..y+6: for even y the pairs y/2 .. y/2+3 with taps
+    // (k0,k1)(k2,k3)(k4,k5)(k6,0), for odd y the pairs (y-1)/2 .. with (0,k0)(k1,k2)(k3,k4)(k5,k6).
+    // acc starts at 2^15 (the rounding term); taps sum to 256, so acc >> 16 <= 255.
+    uint8_t* bl = reinterpret_cast<uint8_t*>(raw);  // raw is dead from here on
+    if (lane < 50) {
+        const int g = lane % 5, rb = lane / 5;
+        const us2 KE[4] = {us2{18, 34}, us2{48, 56}, us2{48, 34}, us2{18, 0}};
+        const us2 KO[4] = {us2{0, 18}, us2{34, 48}, us2{56, 48}, us2{34, 18}};
+        uint32_t acc[4][8];
+#pragma unroll
+        for (int o = 0; o < 4; o++)
+#pragma unroll
+            for (int e = 0; e < 8; e++) acc[o][e] = 1u << 15;
+#pragma unroll
+        for (int j = 0; j < 5; j++) {
+            const int pr = 2 * rb + j;
+            if (pr < kO3Pairs) {
+                const uint4 u0 = *reinterpret_cast<const uint4*>(&hp[pr * kO3HS + 8 * g]);
+                const uint4 u1 = *reinterpret_cast<const uint4*>(&hp[pr * kO3HS + 8 * g + 4]);
+                const uint32_t hv[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+#pragma unroll
+                for (int e = 0; e < 8; e++) {
+                    const us2 v = as_us2(hv[e]);
+                    if (j < 4) {  // rows 4rb (even) and 4rb+1 (odd) use pairs 2rb .. 2rb+3
+                        acc[0][e] = __builtin_amdgcn_udot2(v, KE[j], acc[0][e], false);
+                        acc[1][e] = __builtin_amdgcn_udot2(v, KO[j], acc[1][e], false);
+                    }
+                    if (j >= 1) {  // rows 4rb+2 and 4rb+3 use pairs 2rb+1 .. 2rb+4
+                        acc[2][e] = __builtin_amdgcn_udot2(v, KE[j - 1], acc[2][e], false);
+                        acc[3][e] = __builtin_amdgcn_udot2(v, KO[j - 1], acc[3][e], false);
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int o = 0; o < 4; o++) {
+            const int y = 4 * rb + o;
+            if (y < 37) {
+                uint32_t w0 = 0, w1 = 0;
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    w0 |= (acc[o][e] >> 16) << (8 * e);
+                    w1 |= (acc[o][e + 4] >> 16) << (8 * e);
+                }
+                *reinterpret_cast<uint2*>(&bl[y * kO3BlS + 8 * g]) = make_uint2(w0, w1);
+            }
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+
+    // ---- descriptor (computeOrbDescriptor, ORBextractor.cc:106-145)
     const float factor_pi = (float)(3.14159265358979323846 / 180.f);
     float sn, cs;
     glibc_sincosf(angle * factor_pi, &sn, &cs);
     const float a = cs, bb = sn;
-    const uint8_t* center = blw + 18 * kOrbBlS + shb + 18;
+    const uint8_t* center = bl + 18 * kO3BlS + 18;
     int t0[4], t1[4];
 #pragma unroll
     for (int w = 0; w < 4; w++) {
@@ -1242,8 +1200,8 @@ __global__ void __launch_bounds__(256) k_orb2(Bufs b) {
         const float x1 = (float)c_pattern[4 * bit + 2], y1 = (float)c_pattern[4 * bit + 3];
         const int r0 = cv_round(fmaf(x0, bb, y0 * a)), c0 = cv_round(fmaf(x0, a, -(y0 * bb)));
         const int r1 = cv_round(fmaf(x1, bb, y1 * a)), c1 = cv_round(fmaf(x1, a, -(y1 * bb)));
-        t0[w] = center[r0 * kOrbBlS + c0];
-        t1[w] = center[r1 * kOrbBlS + c1];
+        t0[w] = center[r0 * kO3BlS + c0];
+        t1[w] = center[r1 * kO3BlS + c1];
     }
     uint64_t m[4];
 #pragma unroll
@@ -1303,9 +1261,9 @@ static size_t octree_lds_bytes(int maxn, int keycap) {
     return s;
 }
 
-enum Stage { kStResize = 0, kStFast, kStOctree, kStLayout, kStBlur, kStOrb, kNumStages };
+enum Stage { kStResize = 0, kStFast, kStOctree, kStLayout, kStOrb, kNumStages };
 static const char* kStageNames[kNumStages] = {"k_resize", "k_fast_wave", "k_octree",
-                                              "k_layout", "k_blur", "k_orb"};
+                                              "k_layout", "k_orb"};
 
 }  // namespace slamhot
 
@@ -1316,27 +1274,24 @@ struct slam_extractor {
     int device = 0;
     int max_w = 0, max_h = 0, max_batch = 0;
     hipStream_t stream = nullptr;
-    hipStream_t side = nullptr;             // blur runs here, concurrent with FAST + octree
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     // sub-batch concurrency: a batch is split into nsub frame ranges, each running the whole
-    // pipeline on its own stream pair (main + blur side stream); latency-bound stages of one
+    // pipeline on its own stream; latency-bound stages of one
     // range (octree, orb) overlap the VALU-bound FAST of another
     static constexpr int kMaxSub = 4;
     int nsub = 1;
     bool chain_fast = false;
-    hipStream_t sub[kMaxSub] = {}, sub_side[kMaxSub] = {};
-    hipEvent_t sub_fork = nullptr, sub_join[kMaxSub] = {}, sub_bfork[kMaxSub] = {}, sub_bjoin[kMaxSub] = {},
-              sub_fast[kMaxSub] = {};
+    hipStream_t sub[kMaxSub] = {};
+    hipEvent_t sub_fork = nullptr, sub_join[kMaxSub] = {}, sub_fast[kMaxSub] = {};
     bool serial = false;
     std::mutex mu;
     // geometry
     bool have_plan = false;
     Plan plan;
-    DevBuf d_plan, d_xtab, d_ytab, d_cells, d_wave_cells, d_wide_cells, d_blur_tiles;
-    int n_wave_cells = 0, n_wide_cells = 0, n_blur_tiles = 0;
+    DevBuf d_plan, d_xtab, d_ytab, d_cells, d_wave_cells, d_wide_cells;
+    int n_wave_cells = 0, n_wide_cells = 0;
     FastWaveLds fw_lay{};
     // per-batch buffers
-    DevBuf d_img, d_pyr, d_blur, d_cell_keys, d_cell_cnt, d_keys_g, d_knode_g, d_okp, d_ocnt,
+    DevBuf d_img, d_pyr, d_cell_keys, d_cell_cnt, d_keys_g, d_knode_g, d_okp, d_ocnt,
         d_oidx, d_err, d_kps, d_desc, d_n, d_mono;
     int last_frames = 0;
     const uint8_t* last_img = nullptr;  // level-0 pointer of the last run (for pyramid_level)
@@ -1455,15 +1410,6 @@ static slam_status ensure_plan(slam_extractor* ex, int W, int H) {
         ex->n_wave_cells = (int)wave.size();
         ex->n_wide_cells = (int)wide.size();
     }
-    {
-        std::vector<BlurTile> tiles;
-        for (int l = 0; l < P.nlevels; l++)
-            for (int y = 0; y < P.lv[l].h; y += kB3H)
-                for (int x = 0; x < P.lv[l].w; x += kB3W) tiles.push_back({(int16_t)l, 0, (int16_t)x, (int16_t)y});
-        if ((st = ex->d_blur_tiles.ensure(tiles.size() * sizeof(BlurTile)))) return st;
-        SLAM_HIP_TRY(hipMemcpy(ex->d_blur_tiles.p, tiles.data(), tiles.size() * sizeof(BlurTile), hipMemcpyHostToDevice));
-        ex->n_blur_tiles = (int)tiles.size();
-    }
     ex->plan = P;
     ex->have_plan = true;
     // keys stay in LDS behind the node arrays when they fit (else global scratch)
@@ -1481,7 +1427,7 @@ static slam_status ensure_batch(slam_extractor* ex, int nframes, int cap) {
     const Plan& P = ex->plan;
     const size_t F = (size_t)nframes;
     slam_status st;
-    if ((st = ex->d_pyr.ensure(F * P.pyr_frame)) || (st = ex->d_blur.ensure(F * P.blur_frame)) ||
+    if ((st = ex->d_pyr.ensure(F * P.pyr_frame)) ||
         (st = ex->d_cell_keys.ensure(F * P.ncells * P.slot_cap * 4)) ||
         (st = ex->d_cell_cnt.ensure(F * P.ncells * 4)) ||
         (st = ex->d_keys_g.ensure(F * P.key_slots * 4)) ||
@@ -1495,17 +1441,15 @@ static slam_status ensure_batch(slam_extractor* ex, int nframes, int cap) {
 
 // One frame range [f0, f0 + nframes) of a batch: every per-frame buffer is frame-major, so
 // the range is the whole pipeline on pointers advanced by f0 frames.  s = main stream,
-// side = blur stream (nullptr: serial), fork/join = that range's blur events.
 static slam_status launch_range(slam_extractor* ex, int f0, int nframes, const uint8_t* d_img, int lap0,
                                 int lap1, slam_keypoint* d_kps, uint8_t* d_desc, int cap, int32_t* d_n,
-                                int32_t* d_mono, hipStream_t s, hipStream_t side, hipEvent_t bfork,
-                                hipEvent_t bjoin, hipEvent_t fast_after = nullptr, hipEvent_t fast_done = nullptr) {
+                                int32_t* d_mono, hipStream_t s, hipEvent_t fast_after = nullptr,
+                                hipEvent_t fast_done = nullptr) {
     const Plan& P = ex->plan;
     const size_t F = (size_t)f0;
     Bufs b{};
     b.img = d_img + F * P.W * P.H;
     b.pyr = ex->d_pyr.as<uint8_t>() + F * P.pyr_frame;
-    b.blur = ex->d_blur.as<uint8_t>() + F * P.blur_frame;
     b.cell_keys = ex->d_cell_keys.as<uint32_t>() + F * P.ncells * P.slot_cap;
     b.cell_cnt = ex->d_cell_cnt.as<int32_t>() + F * P.ncells;
     b.keys_g = ex->d_keys_g.as<uint32_t>() + F * P.key_slots;
@@ -1546,18 +1490,6 @@ static slam_status launch_range(slam_extractor* ex, int f0, int nframes, const u
         hipLaunchKernelGGL(k_resize3, dim3((qw * P.lv[l].h + 255) / 256, nframes), dim3(256), 0, s, b, l, sxv, syv);
     }
     end(kStResize);
-    // fork: the blur needs only the pyramid (SLAMHOT_SERIAL=1 keeps it on the main stream,
-    // for isolated per-kernel timing)
-    hipStream_t bs = side ? side : s;
-    if (side) {
-        SLAM_HIP_TRY(hipEventRecord(bfork, s));
-        SLAM_HIP_TRY(hipStreamWaitEvent(side, bfork, 0));
-    }
-    begin(kStBlur, bs);
-    hipLaunchKernelGGL(k_blur3, dim3(ex->n_blur_tiles, nframes), dim3(256), 0, bs, b,
-                       ex->d_blur_tiles.as<BlurTile>(), 1);
-    end(kStBlur, bs);
-    if (side) SLAM_HIP_TRY(hipEventRecord(bjoin, side));
     // ranges run FAST one after another (each fills the chip); a range's octree / layout /
     // orb then overlap the next range's FAST
     if (fast_after) SLAM_HIP_TRY(hipStreamWaitEvent(s, fast_after, 0));
@@ -1578,9 +1510,8 @@ static slam_status launch_range(slam_extractor* ex, int f0, int nframes, const u
     begin(kStLayout);
     hipLaunchKernelGGL(k_layout, dim3(nframes), dim3(256), 0, s, b);
     end(kStLayout);
-    if (side) SLAM_HIP_TRY(hipStreamWaitEvent(s, bjoin, 0));
     begin(kStOrb);
-    hipLaunchKernelGGL(k_orb2, dim3((P.kslots + 3) / 4, nframes), dim3(256), 0, s, b);
+    hipLaunchKernelGGL(k_orb3, dim3((P.kslots + 3) / 4, nframes), dim3(256), 0, s, b);
     end(kStOrb);
     SLAM_HIP_TRY(hipGetLastError());
     return SLAM_OK;
@@ -1596,19 +1527,18 @@ static slam_status launch_pipeline(slam_extractor* ex, int nframes, const uint8_
     const bool serial = ex->serial || ex->profiling;
     int nsub = serial ? 1 : std::min(ex->nsub, nframes / 8);
     if (nsub <= 1) {
-        SLAM_TRY_ST(launch_range(ex, 0, nframes, d_img, lap0, lap1, d_kps, d_desc, cap, d_n, d_mono, s,
-                                 serial ? nullptr : ex->side, ex->ev_fork, ex->ev_join));
+        SLAM_TRY_ST(launch_range(ex, 0, nframes, d_img, lap0, lap1, d_kps, d_desc, cap, d_n, d_mono, s));
     } else {
-        // range 0 runs on the caller's stream, ranges 1.. on the handle's sub-streams; with the
-        // blur kept in-stream that is nsub hardware queues (GPU_MAX_HW_QUEUES is 4 by default)
+        // range 0 runs on the caller's stream, ranges 1.. on the handle's sub-streams (nsub
+        // hardware queues; GPU_MAX_HW_QUEUES is 4 by default)
         SLAM_HIP_TRY(hipEventRecord(ex->sub_fork, s));
         int f0 = 0;
         for (int k = 0; k < nsub; k++) {
             const int nf = nframes / nsub + (k < nframes % nsub ? 1 : 0);
             hipStream_t sk = k ? ex->sub[k] : s;
             if (k) SLAM_HIP_TRY(hipStreamWaitEvent(sk, ex->sub_fork, 0));
-            SLAM_TRY_ST(launch_range(ex, f0, nf, d_img, lap0, lap1, d_kps, d_desc, cap, d_n, d_mono, sk, nullptr,
-                                     nullptr, nullptr, ex->chain_fast && k ? ex->sub_fast[k - 1] : nullptr,
+            SLAM_TRY_ST(launch_range(ex, f0, nf, d_img, lap0, lap1, d_kps, d_desc, cap, d_n, d_mono, sk,
+                                     ex->chain_fast && k ? ex->sub_fast[k - 1] : nullptr,
                                      ex->chain_fast ? ex->sub_fast[k] : nullptr));
             if (k) SLAM_HIP_TRY(hipEventRecord(ex->sub_join[k], sk));
             f0 += nf;
@@ -1667,9 +1597,6 @@ slam_status slamhot_extractor_create(const slam_orb_params* params, int device, 
     ex->max_h = max_height;
     ex->max_batch = max_batch;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ex->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&ex->side, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&ex->ev_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&ex->ev_join, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&ex->sub_fork, hipEventDisableTiming) != hipSuccess) {
         slamhot_extractor_destroy(ex);
         return SLAM_EHIP;
@@ -1682,10 +1609,7 @@ slam_status slamhot_extractor_create(const slam_orb_params* params, int device, 
     }
     for (int k = 0; k < slam_extractor::kMaxSub; k++)
         if (hipStreamCreateWithFlags(&ex->sub[k], hipStreamNonBlocking) != hipSuccess ||
-            hipStreamCreateWithFlags(&ex->sub_side[k], hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&ex->sub_join[k], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&ex->sub_bfork[k], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&ex->sub_bjoin[k], hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&ex->sub_fast[k], hipEventDisableTiming) != hipSuccess) {
             slamhot_extractor_destroy(ex);
             return SLAM_EHIP;
@@ -1699,26 +1623,20 @@ void slamhot_extractor_destroy(slam_extractor* ex) {
     (void)hipSetDevice(ex->device);
     if (ex->stream) (void)hipStreamSynchronize(ex->stream);
     DevBuf* bufs[] = {&ex->d_plan, &ex->d_xtab, &ex->d_ytab, &ex->d_cells, &ex->d_wave_cells,
-                      &ex->d_wide_cells, &ex->d_blur_tiles, &ex->d_img, &ex->d_pyr,
-                      &ex->d_blur, &ex->d_cell_keys, &ex->d_cell_cnt, &ex->d_keys_g, &ex->d_knode_g,
+                      &ex->d_wide_cells, &ex->d_img, &ex->d_pyr,
+                      &ex->d_cell_keys, &ex->d_cell_cnt, &ex->d_keys_g, &ex->d_knode_g,
                       &ex->d_okp, &ex->d_ocnt, &ex->d_oidx, &ex->d_err, &ex->d_kps, &ex->d_desc,
                       &ex->d_n, &ex->d_mono};
     for (DevBuf* b : bufs) b->release();
     for (auto& m : ex->marks) { ex->pool.push_back(m.a); ex->pool.push_back(m.b); }
     for (hipEvent_t e : ex->pool) (void)hipEventDestroy(e);
-    if (ex->side) (void)hipStreamSynchronize(ex->side);
     for (int k = 0; k < slam_extractor::kMaxSub; k++) {
         if (ex->sub[k]) (void)hipStreamSynchronize(ex->sub[k]);
-        if (ex->sub_side[k]) (void)hipStreamSynchronize(ex->sub_side[k]);
-        for (hipEvent_t e : {ex->sub_join[k], ex->sub_bfork[k], ex->sub_bjoin[k], ex->sub_fast[k]})
+        for (hipEvent_t e : {ex->sub_join[k], ex->sub_fast[k]})
             if (e) (void)hipEventDestroy(e);
         if (ex->sub[k]) (void)hipStreamDestroy(ex->sub[k]);
-        if (ex->sub_side[k]) (void)hipStreamDestroy(ex->sub_side[k]);
     }
     if (ex->sub_fork) (void)hipEventDestroy(ex->sub_fork);
-    if (ex->ev_fork) (void)hipEventDestroy(ex->ev_fork);
-    if (ex->ev_join) (void)hipEventDestroy(ex->ev_join);
-    if (ex->side) (void)hipStreamDestroy(ex->side);
     if (ex->stream) (void)hipStreamDestroy(ex->stream);
     delete ex;
 }

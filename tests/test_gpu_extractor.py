@@ -50,6 +50,19 @@ def test_extract_bitexact(gpu_extractor_factory, size, seed):
     _compare(kg, dg, mg, ko, do, mo)
 
 
+@pytest.mark.parametrize("size", [(641, 479), (322, 241), (333, 247)])
+def test_odd_sizes_bitexact(gpu_extractor_factory, size):
+    """Rows that are not dword multiples (byte staging paths) and small levels where the
+    7x7 blur window of a keypoint reflects at the level border (BORDER_REFLECT_101).  Smaller
+    images make the reference divide by zero (ORBextractor.cc:783, nRows = 0 at level 7)."""
+    w, h = size
+    ex = gpu_extractor_factory(nfeatures=1000, max_size=size)
+    img = synth.frame(55, w, h)
+    kg, dg, mg = ex(img)
+    ko, do, mo = ob.extract(img, ob.params(nfeatures=1000))
+    _compare(kg, dg, mg, ko, do, mo)
+
+
 @pytest.mark.parametrize("lap", [(0, 0), (0, 1000), (100, 400)])
 def test_lapping_order(gpu_extractor_factory, lap):
     ex = gpu_extractor_factory(nfeatures=1000, max_size=(640, 480))
