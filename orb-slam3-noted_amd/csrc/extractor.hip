@@ -5,7 +5,7 @@
 //   k_resize3     x (L-1)  chained INTER_LINEAR pyramid            ComputePyramid :1152
 //   k_fast_wave   x 1      FAST-9 score + per-cell 3x3 NMS, 1 wave/cell ComputeKeyPointsOctTree :787-853
 //   k_fast_cells  x 1      the same for cells wider than one wave (1 WG/cell)
-//   k_octree      x 1      quadtree distribution, 1 WG/(frame,lvl) DistributeOctTree :537-761
+//   k_octree      x 2      quadtree distribution, 1 wave/(frame,lvl) DistributeOctTree :537-761
 //   k_layout      x 1      lapping-area output order, 1 WG/frame   operator() :1100-1146
 //   k_orb3        x 1      IC angle + 7x7 blur window + rBRIEF,    IC_Angle :75, GaussianBlur :1115,
 //                          one wave per kp                         computeOrbDescriptor :106
@@ -624,27 +624,8 @@ __global__ void __launch_bounds__(256) k_fast_wave(Bufs b, const int32_t* list, 
     if (lane == 0) b.cell_cnt[(size_t)f * P.ncells + cd.slot] = base;
 }
 
-// exclusive scan over n items (in chunks of blockDim.x) of per-item value fn(i);
-// out(i, excl) is called for every item; returns the total.
-template <class ValFn, class OutFn>
-__device__ int chunked_scan(int n, int* scratch, ValFn fn, OutFn out) {
-    int carry = 0;
-    for (int base = 0; base < n; base += blockDim.x) {
-        const int i = base + threadIdx.x;
-        const int v = i < n ? fn(i) : 0;
-        int tot;
-        const int incl = block_scan_incl(v, scratch, &tot);
-        if (i < n) out(i, carry + incl - v);
-        carry += tot;
-    }
-    __syncthreads();
-    return carry;
-}
-
-
 // ---------------------------------------------------------------------------------------
-// k_octree: DistributeOctTree (ORBextractor.cc:537-761) for one (level, frame) per
-// workgroup of 256 threads.
+// k_octree: DistributeOctTree (ORBextractor.cc:537-761), one WAVE per (frame, level).
 //
 // The reference's std::list<ExtractorNode> is represented by the array of alive nodes in
 // list order.  A pass that splits the nodes of a set S in push order pi (children n1..n4
@@ -657,37 +638,84 @@ __device__ int chunked_scan(int n, int* scratch, ValFn fn, OutFn out) {
 // nondeterministic in the reference) — documented deviation, identical in the oracle.
 // Keys keep their original (cell-major) order; each node keeps its max-response key, the
 // first in original order on ties (:742-758).
+//
+// A level's list never exceeds max(N+3, 4*nIni) nodes (a few hundred) and ~4 passes split
+// it, so the work is a chain of small prefix sums: one wave runs them with ballot/mbcnt
+// and DPP scans and no workgroup barriers (a 256-thread version spent ~10k cycles per pass
+// in s_barrier round trips).  Node arrays and keys live in this wave's LDS (keys spill to
+// the per-frame global scratch past key_cap); levels are launched in groups whose LDS size
+// fits their key counts (level 0 alone, then the rest).
 // ---------------------------------------------------------------------------------------
 struct NodeArr {
-    int16_t *x0, *x1, *y0, *y1;
+    uint32_t* xb;  // x0 | x1 << 16
+    uint32_t* yb;  // y0 | y1 << 16
     int32_t *cnt, *seq;
 };
 
-__device__ __forceinline__ int quadrant_of(uint32_t key, const NodeArr& A, int nd) {
-    const int xm = A.x0[nd] + ((A.x1[nd] - A.x0[nd] + 1) >> 1);  // ceil((x1-x0)/2), :481
-    const int ym = A.y0[nd] + ((A.y1[nd] - A.y0[nd] + 1) >> 1);
-    const int x = kp_x(key), y = kp_y(key);
-    return (x < xm ? 0 : 1) + (y < ym ? 0 : 2);  // n1, n2, n3, n4 (:513-523)
+__device__ __forceinline__ int quadrant_of(uint32_t key, uint32_t xb, uint32_t yb) {
+    const int x0 = (int)(xb & 0xFFFF), x1 = (int)(xb >> 16), y0 = (int)(yb & 0xFFFF), y1 = (int)(yb >> 16);
+    const int xm = x0 + ((x1 - x0 + 1) >> 1);  // ceil((x1-x0)/2), :481
+    const int ym = y0 + ((y1 - y0 + 1) >> 1);
+    return (kp_x(key) < xm ? 0 : 1) + (kp_y(key) < ym ? 0 : 2);  // n1, n2, n3, n4 (:513-523)
 }
 
-__host__ __device__ inline size_t octree_node_bytes(int maxn) {
-    // A, B (2x(4*2 + 2*4) B), cc 16 B, cmap 8 B, ord/rnk/oarr 12 B, best 4 B per node
-    return (size_t)maxn * (32 + 16 + 8 + 12 + 4) + 16 * 16;
+// LDS and global accesses of one wave are ordered for that wave by this fence
+__device__ __forceinline__ void wave_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// exclusive prefix sum over the wave's 64 lanes; total in *tot
+__device__ __forceinline__ int wave_scan_excl(int v, int* tot) {
+    const int lane = threadIdx.x & 63;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    *tot = __shfl(x, 63, 64);
+    return x - v;
+}
+
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
 }
 
 enum { kErrOctreeIters = 1, kErrOctreeNodes = 2, kErrCap = 4 };
 
-__global__ void __launch_bounds__(256) k_octree(Bufs b, int key_lds_cap) {
+__host__ __device__ inline size_t octree_lds_bytes(int maxn, int keycap, int maxcells) {
+    size_t s = 0;
+    auto add = [&](size_t bytes) { s += (bytes + 15) & ~(size_t)15; };
+    for (int i = 0; i < 2; i++) { add(4 * (size_t)maxn); add(4 * (size_t)maxn); add(4 * (size_t)maxn); add(4 * (size_t)maxn); }
+    add(16 * (size_t)maxn);                       // cc
+    add(8 * (size_t)maxn);                        // cmap
+    add(2 * (size_t)maxn); add(2 * (size_t)maxn); add(4 * (size_t)maxn);  // ord, rnk, oarr
+    add(4 * (size_t)maxn);                        // best
+    add(4 * ((size_t)maxcells + 1));              // coff
+    add(4 * (size_t)keycap); add(2 * (size_t)keycap);
+    return s;
+}
+
+__global__ void __launch_bounds__(64) k_octree(Bufs b, int level0, int key_lds_cap, int max_cells) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    __shared__ int scratch[20];
-    __shared__ int cell_off[256];
-    __shared__ int sh[8];
     const DevPlan& P = *b.plan;
-    const int l = blockIdx.x, f = blockIdx.y;
+    const int l = level0 + blockIdx.x, f = blockIdx.y;
     const DevLevel& L = P.lv[l];
     const int MAXN = P.max_nodes;
-    const int tid = threadIdx.x, NT = blockDim.x;
-    const int lane = tid & 63, wid = tid >> 6, nwv = NT >> 6;
+    const int lane = threadIdx.x;
+#ifdef SLAMHOT_OCTREE_TRACE
+    // experiment builds only: phase timestamps of a few waves
+    long long tr[24];
+    int ntr = 0;
+    const bool trace = (f == 100 || f == 101) && lane == 0;
+#define OCT_MARK() do { if (trace && ntr < 24) tr[ntr++] = (long long)__builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define OCT_MARK() do {} while (0)
+#endif
+    OCT_MARK();
 
     uint8_t* p = smem;
     auto carve = [&](size_t bytes) {
@@ -696,252 +724,280 @@ __global__ void __launch_bounds__(256) k_octree(Bufs b, int key_lds_cap) {
         return r;
     };
     NodeArr A, B;
-    A.x0 = (int16_t*)carve(2 * MAXN); A.x1 = (int16_t*)carve(2 * MAXN);
-    A.y0 = (int16_t*)carve(2 * MAXN); A.y1 = (int16_t*)carve(2 * MAXN);
+    A.xb = (uint32_t*)carve(4 * MAXN); A.yb = (uint32_t*)carve(4 * MAXN);
     A.cnt = (int32_t*)carve(4 * MAXN); A.seq = (int32_t*)carve(4 * MAXN);
-    B.x0 = (int16_t*)carve(2 * MAXN); B.x1 = (int16_t*)carve(2 * MAXN);
-    B.y0 = (int16_t*)carve(2 * MAXN); B.y1 = (int16_t*)carve(2 * MAXN);
+    B.xb = (uint32_t*)carve(4 * MAXN); B.yb = (uint32_t*)carve(4 * MAXN);
     B.cnt = (int32_t*)carve(4 * MAXN); B.seq = (int32_t*)carve(4 * MAXN);
-    int32_t* cc = (int32_t*)carve(16 * MAXN);   // child key counts [node][4]
-    int16_t* cmap = (int16_t*)carve(8 * MAXN);  // new position of child [node][4]
-    int32_t* ord = (int32_t*)carve(4 * MAXN);   // split nodes in push order
-    int32_t* rnk = (int32_t*)carve(4 * MAXN);   // push index of a node, -1 = not split
-    int32_t* oarr = (int32_t*)carve(4 * MAXN);  // child offset of a split node (by push idx)
+    uint4* cc = (uint4*)carve(16 * MAXN);       // child key counts per node (n1..n4)
+    uint16_t* cmap = (uint16_t*)carve(8 * MAXN);  // new position of child [node][4]
+    uint16_t* ord = (uint16_t*)carve(2 * MAXN);   // split nodes in push order
+    int16_t* rnk = (int16_t*)carve(2 * MAXN);     // push index of a node, -1 = not split
+    int32_t* oarr = (int32_t*)carve(4 * MAXN);    // child offset of a split node (by push idx)
     uint32_t* best = (uint32_t*)carve(4 * MAXN);
+    int32_t* coff = (int32_t*)carve(4 * ((size_t)max_cells + 1));
     uint32_t* keys_l = (uint32_t*)carve(4 * (size_t)key_lds_cap);
     uint16_t* knode_l = (uint16_t*)carve(2 * (size_t)key_lds_cap);
+    uint32_t* ccu = reinterpret_cast<uint32_t*>(cc);
 
-    // ---- gather the level's candidates in cell order, relative to (minBX, minBY)
+    // ---- gather the level's candidates in cell order, relative to (minBX, minBY): cell
+    // offsets by one scan, then every key independently (its cell by binary search over the
+    // offsets), four loads in flight per lane
     const int cb = L.cell_begin, ncl = L.cell_end - L.cell_begin;
     const int32_t* ccount = b.cell_cnt + (size_t)f * P.ncells;
     int nk = 0;
-    for (int base = 0; base < ncl; base += NT) {
-        const int i = base + tid;
+    for (int base = 0; base < ncl; base += 64) {
+        const int i = base + lane;
         const int v = i < ncl ? ccount[cb + i] : 0;
         int tot;
-        const int incl = block_scan_incl(v, scratch, &tot);
-        cell_off[tid] = nk + incl - v;
+        const int ex = wave_scan_excl(v, &tot);
+        if (i < ncl) coff[i] = nk + ex;
         nk += tot;
     }
+    wave_fence();
     const bool in_lds = nk <= key_lds_cap;
     uint32_t* keys = in_lds ? keys_l : b.keys_g + (size_t)f * P.key_slots + L.key_base;
     uint16_t* knode = in_lds ? knode_l : b.knode_g + (size_t)f * P.key_slots + L.key_base;
     {
-        int carry = 0;
-        for (int base = 0; base < ncl; base += NT) {
-            const int i = base + tid;
-            const int v = i < ncl ? ccount[cb + i] : 0;
-            int tot;
-            const int incl = block_scan_incl(v, scratch, &tot);
-            cell_off[tid] = carry + incl - v;
-            carry += tot;
-            __syncthreads();
-            const int nc = min(NT, ncl - base);
-            for (int c = wid; c < nc; c += nwv) {
-                const int cell = cb + base + c;
-                const int n = ccount[cell];
-                const uint32_t* src = b.cell_keys + ((size_t)f * P.ncells + cell) * P.slot_cap;
-                uint32_t* dst = keys + cell_off[c];
-                for (int j = lane; j < n; j += 64) {
-                    const uint32_t k = src[j];
-                    dst[j] = pack_kp(kp_x(k) - L.minBX, kp_y(k) - L.minBY, kp_s(k));
+        const uint32_t* src = b.cell_keys + ((size_t)f * P.ncells + cb) * P.slot_cap;
+        for (int k0 = lane; k0 < nk; k0 += 4 * 64) {
+            uint32_t v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int k = k0 + u * 64;
+                v[u] = 0;
+                if (k < nk) {
+                    int lo = 0, hi = ncl - 1;  // largest c with coff[c] <= k (a non-empty cell)
+                    while (lo < hi) {
+                        const int mid = (lo + hi + 1) >> 1;
+                        if (coff[mid] <= k) lo = mid; else hi = mid - 1;
+                    }
+                    v[u] = src[(size_t)lo * P.slot_cap + (k - coff[lo])];
                 }
             }
-            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int k = k0 + u * 64;
+                if (k < nk) keys[k] = pack_kp(kp_x(v[u]) - L.minBX, kp_y(v[u]) - L.minBY, kp_s(v[u]));
+            }
         }
     }
+    wave_fence();
+    OCT_MARK();
     const int N = L.nfeat;
     int32_t* out_cnt = b.ocnt + (size_t)f * P.nlevels + l;
     uint32_t* okp = b.okp + (size_t)f * P.kslots + L.kbase;
     if (nk == 0) {
-        if (tid == 0) *out_cnt = 0;
+        if (lane == 0) *out_cnt = 0;
         return;
     }
 
     // ---- roots (:541-583): key -> root (int)(x / hX); empty roots erased
-    if (tid < L.nIni) cc[tid] = 0;
-    __syncthreads();
-    for (int k = tid; k < nk; k += NT) {
+    if (lane < L.nIni) best[lane] = 0;
+    wave_fence();
+    for (int k = lane; k < nk; k += 64) {
         const int x = kp_x(keys[k]);
         int r = 0;
         for (int i = 1; i < L.nIni; i++) r += x >= L.root_first_x[i];
         knode[k] = (uint16_t)r;
-        atomicAdd(&cc[r], 1);
+        atomicAdd(&best[r], 1u);
     }
-    __syncthreads();
-    if (tid == 0) {
-        int n = 0;
-        for (int i = 0; i < L.nIni; i++) {
-            if (cc[i] > 0) {
-                A.x0[n] = (int16_t)L.root_x0[i];
-                A.x1[n] = (int16_t)L.root_x1[i];
-                A.y0[n] = 0;
-                A.y1[n] = (int16_t)(L.maxBY - L.minBY);
-                A.cnt[n] = cc[i];
-                A.seq[n] = i;
-                cmap[i] = (int16_t)n;
-                n++;
-            }
+    wave_fence();
+    int n = 0;
+    {
+        const bool ne = lane < L.nIni && best[lane] > 0;
+        const uint64_t m = __ballot(ne);
+        if (ne) {
+            const int pos = mbcnt64(m, 0);
+            A.xb[pos] = (uint32_t)L.root_x0[lane] | ((uint32_t)L.root_x1[lane] << 16);
+            A.yb[pos] = (uint32_t)(L.maxBY - L.minBY) << 16;
+            A.cnt[pos] = (int)best[lane];
+            A.seq[pos] = lane;
+            cmap[lane] = (uint16_t)pos;
         }
-        sh[0] = n;
+        n = __popcll(m);
     }
-    __syncthreads();
-    for (int k = tid; k < nk; k += NT) knode[k] = (uint16_t)cmap[knode[k]];
-    int n = sh[0];
+    wave_fence();
+    for (int k = lane; k < nk; k += 64) knode[k] = cmap[knode[k]];
+    wave_fence();
+    OCT_MARK();
     int seq_next = L.nIni;
-    int tprev = 0;        // children region [0, tprev) of the last pass
+    int tprev = 0;  // children region [0, tprev) of the last pass
     bool careful = false;
     bool finish = false;
     int err = 0;
-    __syncthreads();
 
     for (int iter = 0; !finish; iter++) {
         if (iter >= 512) { err |= kErrOctreeIters; break; }
         const int prev = n;
         // -- candidate set and quadrant counts
-        for (int i = tid; i < 4 * n; i += NT) cc[i] = 0;
-        for (int i = tid; i < n; i += NT) rnk[i] = -1;
-        __syncthreads();
-        auto is_cand = [&](int nd) -> bool {
-            return careful ? (nd < tprev && A.cnt[nd] > 1) : (A.cnt[nd] > 1);
-        };
-        for (int k = tid; k < nk; k += NT) {
-            const int nd = knode[k];
-            if (is_cand(nd)) atomicAdd(&cc[nd * 4 + quadrant_of(keys[k], A, nd)], 1);
+        for (int i = lane; i < n; i += 64) {
+            cc[i] = make_uint4(0, 0, 0, 0);
+            rnk[i] = -1;
         }
-        __syncthreads();
+        wave_fence();
+        for (int k = lane; k < nk; k += 64) {
+            const int nd = knode[k];
+            const int c = A.cnt[nd];
+            if (c > 1 && (!careful || nd < tprev))
+                atomicAdd(&ccu[nd * 4 + quadrant_of(keys[k], A.xb[nd], A.yb[nd])], 1u);
+        }
+        wave_fence();
         auto nonempty = [&](int nd) -> int {
-            return (cc[nd * 4] > 0) + (cc[nd * 4 + 1] > 0) + (cc[nd * 4 + 2] > 0) + (cc[nd * 4 + 3] > 0);
+            const uint4 q = cc[nd];
+            return (q.x > 0) + (q.y > 0) + (q.z > 0) + (q.w > 0);
         };
-        int nsplit;
+        int nsplit = 0;
         if (!careful) {
             // phase A: split every node with >1 key, push order = list order
-            nsplit = chunked_scan(n, scratch, [&](int i) { return is_cand(i) ? 1 : 0; },
-                                  [&](int i, int ex) {
-                                      if (is_cand(i)) { rnk[i] = ex; ord[ex] = i; }
-                                  });
-        } else {
-            // careful phase: E = children of the last pass with >1 key; order by
-            // (size desc, sequence desc) = (cnt desc, position asc) inside [0, tprev)
-            for (int i = tid; i < tprev; i += NT) {
-                if (A.cnt[i] > 1) {
-                    const int ci = A.cnt[i];
-                    int r = 0;
-                    for (int j = 0; j < tprev; j++) {
-                        const int cj = A.cnt[j];
-                        r += (cj > 1) && (cj > ci || (cj == ci && j < i));
-                    }
-                    ord[r] = i;
+            for (int base = 0; base < n; base += 64) {
+                const int i = base + lane;
+                const bool c = i < n && A.cnt[i] > 1;
+                const uint64_t m = __ballot(c);
+                if (c) {
+                    const int ex = nsplit + mbcnt64(m, 0);
+                    rnk[i] = (int16_t)ex;
+                    ord[ex] = (uint16_t)i;
                 }
+                nsplit += __popcll(m);
             }
-            __syncthreads();
-            int ne = chunked_scan(tprev, scratch, [&](int i) { return A.cnt[i] > 1 ? 1 : 0; },
-                                  [&](int, int) {});
+        } else {
+            // careful phase: E = children of the last pass with >1 key, ordered by
+            // (size desc, sequence desc) = (cnt desc, position asc) inside [0, tprev)
+            int ne = 0;
+            for (int ib = 0; ib < tprev; ib += 64) {
+                const int i = ib + lane;
+                const int ci = i < tprev ? A.cnt[i] : 0;
+                const uint64_t mi = __ballot(ci > 1);
+                ne += __popcll(mi);
+                int r = 0;
+                for (int jb = 0; jb < tprev; jb += 64) {
+                    const int cj = jb + lane < tprev ? A.cnt[jb + lane] : 0;
+                    const int jn = min(64, tprev - jb);
+                    for (int t = 0; t < jn; t++) {
+                        const int c = __builtin_amdgcn_readlane(cj, t);
+                        r += (c > 1) & ((c > ci) | ((c == ci) & (jb + t < i)));
+                    }
+                }
+                if (ci > 1) ord[r] = (uint16_t)i;
+            }
+            wave_fence();
             // cut: first rank r with n + sum_{r'<=r}(nonempty-1) >= N (:728-729)
-            if (tid == 0) sh[1] = ne;
-            __syncthreads();
-            chunked_scan(ne, scratch, [&](int r) { return nonempty(ord[r]) - 1; },
-                         [&](int r, int ex) {
-                             const int incl = ex + nonempty(ord[r]) - 1;
-                             oarr[r] = (n + incl >= N) ? 1 : 0;
-                         });
-            // first r with flag
-            int firstcut = ne - 1;
-            {
-                int mine = 0x7fffffff;
-                for (int r = tid; r < ne; r += NT) if (oarr[r]) { mine = r; break; }
-                // block min
-                __syncthreads();
-                if (tid == 0) sh[2] = 0x7fffffff;
-                __syncthreads();
-                atomicMin(&sh[2], mine);
-                __syncthreads();
-                if (sh[2] != 0x7fffffff) firstcut = sh[2];
+            int firstcut = ne - 1, carry = 0;
+            for (int base = 0; base < ne; base += 64) {
+                const int r = base + lane;
+                const int v = r < ne ? nonempty(ord[r]) - 1 : 0;
+                int tot;
+                const int incl = carry + wave_scan_excl(v, &tot) + v;
+                const uint64_t m = __ballot(r < ne && n + incl >= N);
+                if (m) { firstcut = base + __ffsll((long long)m) - 1; break; }
+                carry += tot;
             }
             nsplit = firstcut + 1;
-            for (int r = tid; r < nsplit; r += NT) rnk[ord[r]] = r;
-            __syncthreads();
+            for (int r = lane; r < nsplit; r += 64) rnk[ord[r]] = (int16_t)r;
         }
-        __syncthreads();
+        wave_fence();
         // -- children offsets in push order
-        const int T = chunked_scan(nsplit, scratch, [&](int r) { return nonempty(ord[r]); },
-                                   [&](int r, int ex) { oarr[r] = ex; });
+        int T = 0;
+        for (int base = 0; base < nsplit; base += 64) {
+            const int r = base + lane;
+            const int v = r < nsplit ? nonempty(ord[r]) : 0;
+            int tot;
+            const int ex = wave_scan_excl(v, &tot);
+            if (r < nsplit) oarr[r] = T + ex;
+            T += tot;
+        }
         if (T + (n - nsplit) > MAXN) { err |= kErrOctreeNodes; break; }
+        wave_fence();
         // -- write the new list into B
-        int nexp_local = 0;
-        const int U = chunked_scan(n, scratch, [&](int i) { return rnk[i] < 0 ? 1 : 0; },
-            [&](int i, int ex) {
-                const int r = rnk[i];
-                if (r < 0) {
-                    const int pos = T + ex;
-                    B.x0[pos] = A.x0[i]; B.x1[pos] = A.x1[i];
-                    B.y0[pos] = A.y0[i]; B.y1[pos] = A.y1[i];
-                    B.cnt[pos] = A.cnt[i]; B.seq[pos] = A.seq[i];
-                    cmap[i * 4] = (int16_t)pos;
-                } else {
-                    const int o = oarr[r];
-                    const int x0 = A.x0[i], x1 = A.x1[i], y0 = A.y0[i], y1 = A.y1[i];
-                    const int xm = x0 + ((x1 - x0 + 1) >> 1), ym = y0 + ((y1 - y0 + 1) >> 1);
-                    int kk = 0;
+        int U = 0, nexp_local = 0;
+        for (int base = 0; base < n; base += 64) {
+            const int i = base + lane;
+            const bool valid = i < n;
+            const int r = valid ? rnk[i] : 0;
+            const bool uns = valid && r < 0;
+            const uint64_t m = __ballot(uns);
+            if (uns) {
+                const int pos = T + U + mbcnt64(m, 0);
+                B.xb[pos] = A.xb[i]; B.yb[pos] = A.yb[i];
+                B.cnt[pos] = A.cnt[i]; B.seq[pos] = A.seq[i];
+                cmap[i * 4] = (uint16_t)pos;
+            } else if (valid) {
+                const int o = oarr[r];
+                const uint32_t xb = A.xb[i], yb = A.yb[i];
+                const int x0 = (int)(xb & 0xFFFF), x1 = (int)(xb >> 16), y0 = (int)(yb & 0xFFFF), y1 = (int)(yb >> 16);
+                const int xm = x0 + ((x1 - x0 + 1) >> 1), ym = y0 + ((y1 - y0 + 1) >> 1);
+                const uint4 q4 = cc[i];
+                const uint32_t cq[4] = {q4.x, q4.y, q4.z, q4.w};
+                int kk = 0;
 #pragma unroll
-                    for (int q = 0; q < 4; q++) {
-                        const int c = cc[i * 4 + q];
-                        if (c > 0) {
-                            const int pos = T - 1 - (o + kk);
-                            B.x0[pos] = (int16_t)((q & 1) ? xm : x0);
-                            B.x1[pos] = (int16_t)((q & 1) ? x1 : xm);
-                            B.y0[pos] = (int16_t)((q & 2) ? ym : y0);
-                            B.y1[pos] = (int16_t)((q & 2) ? y1 : ym);
-                            B.cnt[pos] = c;
-                            B.seq[pos] = seq_next + o + kk;
-                            cmap[i * 4 + q] = (int16_t)pos;
-                            nexp_local += c > 1;
-                            kk++;
-                        }
+                for (int q = 0; q < 4; q++) {
+                    const int c = (int)cq[q];
+                    if (c > 0) {
+                        const int pos = T - 1 - (o + kk);
+                        const int nx0 = (q & 1) ? xm : x0, nx1 = (q & 1) ? x1 : xm;
+                        const int ny0 = (q & 2) ? ym : y0, ny1 = (q & 2) ? y1 : ym;
+                        B.xb[pos] = (uint32_t)nx0 | ((uint32_t)nx1 << 16);
+                        B.yb[pos] = (uint32_t)ny0 | ((uint32_t)ny1 << 16);
+                        B.cnt[pos] = c;
+                        B.seq[pos] = seq_next + o + kk;
+                        cmap[i * 4 + q] = (uint16_t)pos;
+                        nexp_local += c > 1;
+                        kk++;
                     }
                 }
-            });
-        const int n_to_expand = block_reduce_sum(nexp_local, scratch);
-        // -- remap keys
-        for (int k = tid; k < nk; k += NT) {
-            const int nd = knode[k];
-            const int q = rnk[nd] >= 0 ? quadrant_of(keys[k], A, nd) : 0;
-            knode[k] = (uint16_t)cmap[nd * 4 + q];
+            }
+            U += __popcll(m);
         }
-        __syncthreads();
-        // swap A <-> B
+        const int n_to_expand = wave_sum(nexp_local);
+        wave_fence();
+        // -- remap keys
+        for (int k = lane; k < nk; k += 64) {
+            const int nd = knode[k];
+            const int q = rnk[nd] >= 0 ? quadrant_of(keys[k], A.xb[nd], A.yb[nd]) : 0;
+            knode[k] = cmap[nd * 4 + q];
+        }
+        wave_fence();
         { NodeArr t = A; A = B; B = t; }
         n = T + U;
         seq_next += T;
         tprev = T;
+        OCT_MARK();
         if (!careful) {
             if (n >= N || n == prev) finish = true;               // :667-670
             else if (n + n_to_expand * 3 > N) careful = true;      // :671
         } else {
             if (n >= N || n == prev) finish = true;               // :732-733
         }
-        __syncthreads();
     }
 
     // ---- retain the best key of each node (:740-758)
-    for (int i = tid; i < n; i += NT) best[i] = 0;
-    __syncthreads();
-    for (int k = tid; k < nk; k += NT) {
+    for (int i = lane; i < n; i += 64) best[i] = 0;
+    wave_fence();
+    for (int k = lane; k < nk; k += 64) {
         const uint32_t key = keys[k];
         atomicMax(&best[knode[k]], ((uint32_t)kp_s(key) << 24) | (uint32_t)(0xFFFFFF - k));
     }
-    __syncthreads();
+    wave_fence();
     const int nout = min(n, L.kcap);
-    for (int i = tid; i < nout; i += NT) {
+    for (int i = lane; i < nout; i += 64) {
         const int k = 0xFFFFFF - (int)(best[i] & 0xFFFFFF);
         const uint32_t key = keys[k];
         okp[i] = pack_kp(kp_x(key) + L.minBX, kp_y(key) + L.minBY, kp_s(key));
     }
     if (n > L.kcap) err |= kErrOctreeNodes;
-    if (tid == 0) {
+    if (lane == 0) {
         *out_cnt = nout;
         if (err) atomicOr(&b.err[f], err);
     }
+#ifdef SLAMHOT_OCTREE_TRACE
+    OCT_MARK();
+    if (trace) {
+        long long d[10] = {};
+        for (int i = 1; i < ntr && i <= 10; i++) d[i - 1] = tr[i] - tr[i - 1];
+        printf("OCT f=%d l=%d nk=%d n=%d marks=%d: %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld tot=%lld\n", f, l, nk, n,
+               ntr, d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7], d[8], d[9], tr[ntr - 1] - tr[0]);
+    }
+#endif
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1249,18 +1305,6 @@ struct DevBuf {
     template <class T> T* as() const { return reinterpret_cast<T*>(p); }
 };
 
-constexpr int kOctreeKeyLdsCap = 4096;  // keys held in LDS per octree workgroup
-
-static size_t octree_lds_bytes(int maxn, int keycap) {
-    size_t s = 0;
-    auto add = [&](size_t b) { s += (b + 15) & ~(size_t)15; };
-    for (int i = 0; i < 2; i++) { add(2 * maxn); add(2 * maxn); add(2 * maxn); add(2 * maxn); add(4 * maxn); add(4 * maxn); }
-    add(16 * (size_t)maxn); add(8 * (size_t)maxn); add(4 * (size_t)maxn); add(4 * (size_t)maxn);
-    add(4 * (size_t)maxn); add(4 * (size_t)maxn);
-    add(4 * (size_t)keycap); add(2 * (size_t)keycap);
-    return s;
-}
-
 enum Stage { kStResize = 0, kStFast, kStOctree, kStLayout, kStOrb, kNumStages };
 static const char* kStageNames[kNumStages] = {"k_resize", "k_fast_wave", "k_octree",
                                               "k_layout", "k_orb"};
@@ -1295,8 +1339,11 @@ struct slam_extractor {
         d_oidx, d_err, d_kps, d_desc, d_n, d_mono;
     int last_frames = 0;
     const uint8_t* last_img = nullptr;  // level-0 pointer of the last run (for pyramid_level)
-    int key_lds_cap = kOctreeKeyLdsCap;
-    size_t octree_lds = 0;
+    // k_octree launch groups: {first level, levels, keys held in LDS, dynamic LDS bytes}
+    struct OctGroup { int l0, nl, keycap; size_t lds; };
+    OctGroup oct[2] = {};
+    int n_oct = 0;
+    int octree_max_cells = 1;
     // per-stage HIP-event timing (slamhot_extractor_set_profiling)
     bool profiling = false;
     struct Mark { int stage; hipEvent_t a, b; };
@@ -1412,14 +1459,33 @@ static slam_status ensure_plan(slam_extractor* ex, int W, int H) {
     }
     ex->plan = P;
     ex->have_plan = true;
-    // keys stay in LDS behind the node arrays when they fit (else global scratch)
+    // k_octree keeps a level's keys in LDS behind its node arrays when they fit (else in
+    // the per-frame global scratch).  Level 0 (by far the most FAST candidates, one wave per
+    // frame) gets up to 80 KB; the other levels share a launch sized for ~5 waves per CU.
     const size_t lds_max = 160 * 1024;
-    const size_t node_bytes = octree_lds_bytes(P.max_nodes, 0);
-    if (node_bytes > lds_max) return SLAM_EINVAL;
-    ex->key_lds_cap = (int)std::min<size_t>(kOctreeKeyLdsCap, (lds_max - node_bytes - 64) / 6);
-    ex->octree_lds = octree_lds_bytes(P.max_nodes, ex->key_lds_cap);
+    int max_cells = 1;
+    for (int l = 0; l < P.nlevels; l++) max_cells = std::max(max_cells, P.lv[l].cell_end - P.lv[l].cell_begin);
+    ex->octree_max_cells = max_cells;
+    const size_t node_bytes = octree_lds_bytes(P.max_nodes, 0, max_cells);
+    if (node_bytes + 6 * 256 + 64 > lds_max) return SLAM_EINVAL;
+    auto keycap_for = [&](size_t budget) {
+        budget = std::min(lds_max, std::max(budget, node_bytes + 6 * 1024 + 64));
+        return (int)std::min<size_t>(16384, (budget - node_bytes - 64) / 6);
+    };
+    size_t lds_attr = 0;
+    ex->n_oct = 0;
+    for (int g = 0; g < 2; g++) {
+        const int l0 = g == 0 ? 0 : 1, nl = g == 0 ? 1 : P.nlevels - 1;
+        if (nl <= 0) continue;
+        slam_extractor::OctGroup& G = ex->oct[ex->n_oct++];
+        G.l0 = l0;
+        G.nl = nl;
+        G.keycap = keycap_for(g == 0 ? 80 * 1024 : 32 * 1024);
+        G.lds = octree_lds_bytes(P.max_nodes, G.keycap, max_cells);
+        lds_attr = std::max(lds_attr, G.lds);
+    }
     SLAM_HIP_TRY(hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)ex->octree_lds));
+                                     (int)lds_attr));
     return SLAM_OK;
 }
 
@@ -1482,8 +1548,16 @@ static slam_status launch_range(slam_extractor* ex, int f0, int nframes, const u
             ex->marks.push_back({st, e0, e1});
         }
     };
+#ifdef SLAMHOT_EXPERIMENT
+    // experiment builds only: SLAMHOT_SKIP=<stage bitmask> leaves stages out (their inputs
+    // stay those of the previous batch) to price each stage inside the concurrent pipeline
+    static const int skip = std::getenv("SLAMHOT_SKIP") ? std::atoi(std::getenv("SLAMHOT_SKIP")) : 0;
+#define SKIP(st) (skip & (1 << (st)))
+#else
+#define SKIP(st) 0
+#endif
     begin(kStResize);
-    for (int l = 1; l < P.nlevels; l++) {
+    for (int l = 1; l < P.nlevels && !SKIP(kStResize); l++) {
         const int qw = (P.lv[l].w + 3) / 4;
         const double sxv = 1. / ((double)P.lv[l].w / P.lv[l - 1].w);
         const double syv = 1. / ((double)P.lv[l].h / P.lv[l - 1].h);
@@ -1494,7 +1568,7 @@ static slam_status launch_range(slam_extractor* ex, int f0, int nframes, const u
     // orb then overlap the next range's FAST
     if (fast_after) SLAM_HIP_TRY(hipStreamWaitEvent(s, fast_after, 0));
     begin(kStFast);
-    if (ex->n_wave_cells)
+    if (ex->n_wave_cells && !SKIP(kStFast))
         hipLaunchKernelGGL(k_fast_wave, dim3((ex->n_wave_cells + 3) / 4, nframes), dim3(256),
                            4 * ex->fw_lay.total, s, b, ex->d_wave_cells.as<int32_t>(), ex->n_wave_cells,
                            ex->fw_lay);
@@ -1504,16 +1578,20 @@ static slam_status launch_range(slam_extractor* ex, int f0, int nframes, const u
     end(kStFast);
     if (fast_done) SLAM_HIP_TRY(hipEventRecord(fast_done, s));
     begin(kStOctree);
-    hipLaunchKernelGGL(k_octree, dim3(P.nlevels, nframes), dim3(256), ex->octree_lds, s, b,
-                       ex->key_lds_cap);
+    for (int g = 0; g < ex->n_oct && !SKIP(kStOctree); g++) {
+        const slam_extractor::OctGroup& G = ex->oct[g];
+        hipLaunchKernelGGL(k_octree, dim3(G.nl, nframes), dim3(64), G.lds, s, b, G.l0, G.keycap,
+                           ex->octree_max_cells);
+    }
     end(kStOctree);
     begin(kStLayout);
     hipLaunchKernelGGL(k_layout, dim3(nframes), dim3(256), 0, s, b);
     end(kStLayout);
     begin(kStOrb);
-    hipLaunchKernelGGL(k_orb3, dim3((P.kslots + 3) / 4, nframes), dim3(256), 0, s, b);
+    if (!SKIP(kStOrb)) hipLaunchKernelGGL(k_orb3, dim3((P.kslots + 3) / 4, nframes), dim3(256), 0, s, b);
     end(kStOrb);
     SLAM_HIP_TRY(hipGetLastError());
+#undef SKIP
     return SLAM_OK;
 }
 
@@ -1597,6 +1675,7 @@ slam_status slamhot_extractor_create(const slam_orb_params* params, int device, 
     ex->max_h = max_height;
     ex->max_batch = max_batch;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ex->stream, hipStreamNonBlocking) != hipSuccess ||
+
         hipEventCreateWithFlags(&ex->sub_fork, hipEventDisableTiming) != hipSuccess) {
         slamhot_extractor_destroy(ex);
         return SLAM_EHIP;
@@ -1637,6 +1716,7 @@ void slamhot_extractor_destroy(slam_extractor* ex) {
         if (ex->sub[k]) (void)hipStreamDestroy(ex->sub[k]);
     }
     if (ex->sub_fork) (void)hipEventDestroy(ex->sub_fork);
+
     if (ex->stream) (void)hipStreamDestroy(ex->stream);
     delete ex;
 }
