@@ -417,15 +417,17 @@ __device__ __forceinline__ bool fast_pairs8(const uint8_t* c, int stride, int t)
 //   C  cell-local 3x3 NMS at both thresholds on the remaining corners (one ballot each)
 // Lists keep row-major order, so the survivors are emitted in cv::FAST's order.  The cell
 // keeps the iniThFAST result unless it is empty (ORBextractor.cc:808-841).
-// LDS per wave (host-sized): ROI ch x 72 | M map (th+2) x 66 | list | keep masks.
+// LDS per wave (host-sized to the widest cell, VGA: 6.5 KB -> 6 workgroups per CU, with
+// <= 80 VGPRs): ROI ch x rs (keep masks alias it after pass B) | M map (th+2) x ms | list.
 // ---------------------------------------------------------------------------------------
-constexpr int kRoiStride = 80, kRoiRows = 80, kMapStride = 66;
+constexpr int kRoiStride = 80, kRoiRows = 80;  // widest / tallest cell the wave kernel stages
 
 struct FastWaveLds {
     int roi, map, lst, kmask, total;  // byte offsets inside one wave's region, total size
+    int rs, ms;                       // ROI / M-map row strides (bytes), sized to the geometry
 };
 
-__global__ void __launch_bounds__(256) k_fast_wave(Bufs b, const int32_t* list, int nlist,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) k_fast_wave(Bufs b, const int32_t* list, int nlist,
                                                    FastWaveLds lay) {
     extern __shared__ __attribute__((aligned(16))) uint8_t fw_smem[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -470,19 +472,19 @@ __global__ void __launch_bounds__(256) k_fast_wave(Bufs b, const int32_t* list, 
 #pragma unroll
                     for (int k = 0; k < 8; k++) {
                         const int r = r0 + k * rp;
-                        if (r < ch) roi32[r * (kRoiStride / 4) + lc] = v[k];
+                        if (r < ch) roi32[r * (lay.rs >> 2) + lc] = v[k];
                     }
                 }
             }
         } else {
             for (int r = 0; r < ch; r++)
-                for (int c = lane; c < cw; c += 64) roi[r * kRoiStride + c] = src[(size_t)r * pitch + c];
+                for (int c = lane; c < cw; c += 64) roi[r * lay.rs + c] = src[(size_t)r * pitch + c];
         }
     }
     roi += sh;
     {
         uint32_t* m32 = reinterpret_cast<uint32_t*>(map);
-        const int nw = ((th + 2) * kMapStride + 3) >> 2;
+        const int nw = ((th + 2) * lay.ms + 3) >> 2;
         for (int i = lane; i < nw; i += 64) m32[i] = 0;
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -507,7 +509,7 @@ __global__ void __launch_bounds__(256) k_fast_wave(Bufs b, const int32_t* list, 
         if (ar >= rpi) cmask = 0;
         const int code0 = (4 * gd - sh - 3) + ar * 64;  // code of byte 0 in row 0
         const us2 T = {(unsigned short)tlow, (unsigned short)tlow};
-        constexpr int RS = kRoiStride / 4;
+        const int RS = lay.rs >> 2;
         for (int rt = 0; rt < th; rt += rpi) {
             const int r = rt + ar;
             const uint32_t m = r < th ? cmask : 0u;
@@ -547,7 +549,7 @@ __global__ void __launch_bounds__(256) k_fast_wave(Bufs b, const int32_t* list, 
             const bool valid = e < na;
             const int code = valid ? lst[e] : 0;
             const int r = code >> 6, c = code & 63;
-            const bool keep = valid && fast_pairs8(roi + (r + 3) * kRoiStride + c + 3, kRoiStride, tlow);
+            const bool keep = valid && fast_pairs8(roi + (r + 3) * lay.rs + c + 3, lay.rs, tlow);
             const uint64_t m = __ballot(keep);
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             if (keep) lst[n1 + __popcll(m & lt)] = (uint16_t)code;
@@ -565,9 +567,9 @@ __global__ void __launch_bounds__(256) k_fast_wave(Bufs b, const int32_t* list, 
         const int code = valid ? lst[e] : 0;
         const int r = code >> 6, c = code & 63;
         int M = 0;
-        if (valid) M = fast_M(roi + (r + 3) * kRoiStride + c + 3, kRoiStride);
+        if (valid) M = fast_M(roi + (r + 3) * lay.rs + c + 3, lay.rs);
         const bool corner = M > tlow;
-        if (corner) map[(r + 1) * kMapStride + c + 1] = (uint8_t)M;
+        if (corner) map[(r + 1) * lay.ms + c + 1] = (uint8_t)M;
         const uint64_t m = __ballot(corner);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         if (corner) lst[nb + __popcll(m & lt)] = (uint16_t)code;
@@ -584,11 +586,12 @@ __global__ void __launch_bounds__(256) k_fast_wave(Bufs b, const int32_t* list, 
         if (valid) {
             const int code = lst[e];
             const int r = code >> 6, c = code & 63;
-            const uint8_t* q = map + (r + 1) * kMapStride + c + 1;
+            const int MS = lay.ms;
+            const uint8_t* q = map + (r + 1) * MS + c + 1;
             const int M = q[0];
-            const int n0 = q[-kMapStride - 1], n1 = q[-kMapStride], n2 = q[-kMapStride + 1];
+            const int n0 = q[-MS - 1], n1 = q[-MS], n2 = q[-MS + 1];
             const int n3 = q[-1], n4 = q[1];
-            const int n5 = q[kMapStride - 1], n6 = q[kMapStride], n7 = q[kMapStride + 1];
+            const int n5 = q[MS - 1], n6 = q[MS], n7 = q[MS + 1];
             auto keep = [&](int t) -> bool {
                 auto sc = [&](int x) { return x > t ? x - 1 : 0; };
                 const int sc0 = M - 1;
@@ -616,7 +619,7 @@ __global__ void __launch_bounds__(256) k_fast_wave(Bufs b, const int32_t* list, 
         if ((m >> lane) & 1ull) {
             const int code = lst[j + lane];
             const int r = code >> 6, c = code & 63;
-            const int M = map[(r + 1) * kMapStride + c + 1];
+            const int M = map[(r + 1) * lay.ms + c + 1];
             slot[base + __popcll(m & lt)] = pack_kp(cd.iniX + 3 + c, cd.iniY + 3 + r, M - 1);
         }
         base += __popcll(m);
@@ -1425,28 +1428,35 @@ static slam_status ensure_plan(slam_extractor* ex, int W, int H) {
         // cells whose tested region fits one wave (<= 64 columns, <= kRoiRows rows) take the
         // wave-per-cell kernel; the rest (tiny levels of small images) the workgroup kernel
         std::vector<int32_t> wave, wide;
-        int ch_max = 0, th_max = 0, tw_max = 0;
+        int ch_max = 0, th_max = 0, tw_max = 0, cw_max = 0;
         for (const CellDesc& c : P.cells) {
             if (c.cw - 6 <= 64 && c.ch <= kRoiRows && c.cw + 3 <= kRoiStride) {
                 wave.push_back(c.slot);
                 ch_max = std::max(ch_max, (int)c.ch);
                 th_max = std::max(th_max, c.ch - 6);
                 tw_max = std::max(tw_max, c.cw - 6);
+                cw_max = std::max(cw_max, (int)c.cw);
             } else {
                 wide.push_back(c.slot);
             }
         }
         auto r16 = [](int v) { return (v + 15) & ~15; };
         FastWaveLds lay;
+        // ROI rows: staged dwords reach byte sh + cw + 3 and pass A reads one dword past its
+        // last group, so cw + 8 bytes (rounded to dwords) cover every access
+        lay.rs = std::min(kRoiStride, (cw_max + 8 + 3) & ~3);
+        lay.ms = tw_max + 2;
         lay.roi = 0;
-        lay.map = r16(ch_max * kRoiStride);
-        lay.lst = lay.map + r16((th_max + 2) * kMapStride);
-        lay.kmask = lay.lst + r16(std::max(1, tw_max * th_max) * 2);
-        lay.total = lay.kmask + r16(((std::max(1, tw_max * th_max) + 63) / 64) * 16);
+        lay.map = r16(ch_max * lay.rs);
+        lay.lst = lay.map + r16((th_max + 2) * lay.ms);
+        lay.total = lay.lst + r16(std::max(1, tw_max * th_max) * 2);
+        // the keep masks are written after the last ROI read (pass C): they alias the ROI
+        lay.kmask = lay.roi;
+        if (((std::max(1, tw_max * th_max) + 63) / 64) * 16 > lay.map) return SLAM_EINVAL;
         ex->fw_lay = lay;
         if (4 * lay.total > 160 * 1024) return SLAM_EINVAL;
         SLAM_HIP_TRY(hipFuncSetAttribute((const void*)k_fast_wave, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         4 * lay.total));
+                                         160 * 1024));
         if ((st = ex->d_wave_cells.ensure(std::max<size_t>(4, wave.size() * 4))) ||
             (st = ex->d_wide_cells.ensure(std::max<size_t>(4, wide.size() * 4))))
             return st;
@@ -1553,8 +1563,11 @@ static slam_status launch_range(slam_extractor* ex, int f0, int nframes, const u
     // stay those of the previous batch) to price each stage inside the concurrent pipeline
     static const int skip = std::getenv("SLAMHOT_SKIP") ? std::atoi(std::getenv("SLAMHOT_SKIP")) : 0;
 #define SKIP(st) (skip & (1 << (st)))
+    // SLAMHOT_FAST_LDS_PAD=<bytes>: extra dynamic LDS per FAST workgroup (occupancy probe)
+    static const int fast_pad = std::getenv("SLAMHOT_FAST_LDS_PAD") ? std::atoi(std::getenv("SLAMHOT_FAST_LDS_PAD")) : 0;
 #else
 #define SKIP(st) 0
+    constexpr int fast_pad = 0;
 #endif
     begin(kStResize);
     for (int l = 1; l < P.nlevels && !SKIP(kStResize); l++) {
@@ -1570,7 +1583,7 @@ static slam_status launch_range(slam_extractor* ex, int f0, int nframes, const u
     begin(kStFast);
     if (ex->n_wave_cells && !SKIP(kStFast))
         hipLaunchKernelGGL(k_fast_wave, dim3((ex->n_wave_cells + 3) / 4, nframes), dim3(256),
-                           4 * ex->fw_lay.total, s, b, ex->d_wave_cells.as<int32_t>(), ex->n_wave_cells,
+                           4 * ex->fw_lay.total + fast_pad, s, b, ex->d_wave_cells.as<int32_t>(), ex->n_wave_cells,
                            ex->fw_lay);
     if (ex->n_wide_cells)
         hipLaunchKernelGGL(k_fast_cells, dim3(ex->n_wide_cells, nframes), dim3(256), 0, s, b,
