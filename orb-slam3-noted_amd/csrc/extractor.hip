@@ -744,7 +744,7 @@ __global__ void __launch_bounds__(64) k_octree(Bufs b, int level0, int key_lds_c
 
     // ---- gather the level's candidates in cell order, relative to (minBX, minBY): cell
     // offsets by one scan, then every key independently (its cell by binary search over the
-    // offsets), four loads in flight per lane
+    // offsets); eight keys per lane advance together so their LDS and HBM loads overlap
     const int cb = L.cell_begin, ncl = L.cell_end - L.cell_begin;
     const int32_t* ccount = b.cell_cnt + (size_t)f * P.ncells;
     int nk = 0;
@@ -762,23 +762,29 @@ __global__ void __launch_bounds__(64) k_octree(Bufs b, int level0, int key_lds_c
     uint16_t* knode = in_lds ? knode_l : b.knode_g + (size_t)f * P.key_slots + L.key_base;
     {
         const uint32_t* src = b.cell_keys + ((size_t)f * P.ncells + cb) * P.slot_cap;
-        for (int k0 = lane; k0 < nk; k0 += 4 * 64) {
-            uint32_t v[4];
+        const int steps = ncl > 1 ? 32 - __clz(ncl - 1) : 0;  // ceil(log2(ncl))
+        constexpr int U = 8;
+        for (int k0 = lane; k0 < nk; k0 += U * 64) {
+            // largest c with coff[c] <= k (a non-empty cell); extra steps keep lo == hi
+            int lo[U], hi[U];
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int k = k0 + u * 64;
-                v[u] = 0;
-                if (k < nk) {
-                    int lo = 0, hi = ncl - 1;  // largest c with coff[c] <= k (a non-empty cell)
-                    while (lo < hi) {
-                        const int mid = (lo + hi + 1) >> 1;
-                        if (coff[mid] <= k) lo = mid; else hi = mid - 1;
-                    }
-                    v[u] = src[(size_t)lo * P.slot_cap + (k - coff[lo])];
+            for (int u = 0; u < U; u++) { lo[u] = 0; hi[u] = ncl - 1; }
+            for (int st = 0; st < steps; st++) {
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const int k = min(k0 + u * 64, nk - 1);
+                    const int mid = (lo[u] + hi[u] + 1) >> 1;
+                    if (coff[mid] <= k) lo[u] = mid; else hi[u] = mid - 1;
                 }
             }
+            uint32_t v[U];
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
+            for (int u = 0; u < U; u++) {
+                const int k = min(k0 + u * 64, nk - 1);
+                v[u] = src[(size_t)lo[u] * P.slot_cap + (k - coff[lo[u]])];
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) {
                 const int k = k0 + u * 64;
                 if (k < nk) keys[k] = pack_kp(kp_x(v[u]) - L.minBX, kp_y(v[u]) - L.minBY, kp_s(v[u]));
             }
@@ -797,12 +803,21 @@ __global__ void __launch_bounds__(64) k_octree(Bufs b, int level0, int key_lds_c
     // ---- roots (:541-583): key -> root (int)(x / hX); empty roots erased
     if (lane < L.nIni) best[lane] = 0;
     wave_fence();
-    for (int k = lane; k < nk; k += 64) {
-        const int x = kp_x(keys[k]);
-        int r = 0;
-        for (int i = 1; i < L.nIni; i++) r += x >= L.root_first_x[i];
-        knode[k] = (uint16_t)r;
-        atomicAdd(&best[r], 1u);
+    for (int k0 = lane; k0 < nk; k0 += 4 * 64) {
+        uint32_t key[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) key[u] = keys[min(k0 + 64 * u, nk - 1)];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int k = k0 + 64 * u;
+            const int x = kp_x(key[u]);
+            int r = 0;
+            for (int i = 1; i < L.nIni; i++) r += x >= L.root_first_x[i];
+            if (k < nk) {
+                knode[k] = (uint16_t)r;
+                atomicAdd(&best[r], 1u);
+            }
+        }
     }
     wave_fence();
     int n = 0;
@@ -820,7 +835,17 @@ __global__ void __launch_bounds__(64) k_octree(Bufs b, int level0, int key_lds_c
         n = __popcll(m);
     }
     wave_fence();
-    for (int k = lane; k < nk; k += 64) knode[k] = cmap[knode[k]];
+    for (int k0 = lane; k0 < nk; k0 += 4 * 64) {
+        int nd[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) nd[u] = knode[min(k0 + 64 * u, nk - 1)];
+        uint16_t cm[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) cm[u] = cmap[nd[u]];
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            if (k0 + 64 * u < nk) knode[k0 + 64 * u] = cm[u];
+    }
     wave_fence();
     OCT_MARK();
     int seq_next = L.nIni;
@@ -838,11 +863,24 @@ __global__ void __launch_bounds__(64) k_octree(Bufs b, int level0, int key_lds_c
             rnk[i] = -1;
         }
         wave_fence();
-        for (int k = lane; k < nk; k += 64) {
-            const int nd = knode[k];
-            const int c = A.cnt[nd];
-            if (c > 1 && (!careful || nd < tprev))
-                atomicAdd(&ccu[nd * 4 + quadrant_of(keys[k], A.xb[nd], A.yb[nd])], 1u);
+        // four keys per lane per step: their node loads overlap, then the four atomics
+        for (int k0 = lane; k0 < nk; k0 += 4 * 64) {
+            int nd[4];
+            uint32_t key[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int k = min(k0 + 64 * u, nk - 1);
+                nd[u] = knode[k];
+                key[u] = keys[k];
+            }
+            int c[4];
+            uint32_t xb[4], yb[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) { c[u] = A.cnt[nd[u]]; xb[u] = A.xb[nd[u]]; yb[u] = A.yb[nd[u]]; }
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                if (k0 + 64 * u < nk && c[u] > 1 && (!careful || nd[u] < tprev))
+                    atomicAdd(&ccu[nd[u] * 4 + quadrant_of(key[u], xb[u], yb[u])], 1u);
         }
         wave_fence();
         auto nonempty = [&](int nd) -> int {
@@ -954,10 +992,25 @@ __global__ void __launch_bounds__(64) k_octree(Bufs b, int level0, int key_lds_c
         const int n_to_expand = wave_sum(nexp_local);
         wave_fence();
         // -- remap keys
-        for (int k = lane; k < nk; k += 64) {
-            const int nd = knode[k];
-            const int q = rnk[nd] >= 0 ? quadrant_of(keys[k], A.xb[nd], A.yb[nd]) : 0;
-            knode[k] = cmap[nd * 4 + q];
+        for (int k0 = lane; k0 < nk; k0 += 4 * 64) {
+            int nd[4];
+            uint32_t key[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int k = min(k0 + 64 * u, nk - 1);
+                nd[u] = knode[k];
+                key[u] = keys[k];
+            }
+            int r[4];
+            uint32_t xb[4], yb[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) { r[u] = rnk[nd[u]]; xb[u] = A.xb[nd[u]]; yb[u] = A.yb[nd[u]]; }
+            uint16_t cm[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) cm[u] = cmap[nd[u] * 4 + (r[u] >= 0 ? quadrant_of(key[u], xb[u], yb[u]) : 0)];
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                if (k0 + 64 * u < nk) knode[k0 + 64 * u] = cm[u];
         }
         wave_fence();
         { NodeArr t = A; A = B; B = t; }
@@ -976,9 +1029,20 @@ __global__ void __launch_bounds__(64) k_octree(Bufs b, int level0, int key_lds_c
     // ---- retain the best key of each node (:740-758)
     for (int i = lane; i < n; i += 64) best[i] = 0;
     wave_fence();
-    for (int k = lane; k < nk; k += 64) {
-        const uint32_t key = keys[k];
-        atomicMax(&best[knode[k]], ((uint32_t)kp_s(key) << 24) | (uint32_t)(0xFFFFFF - k));
+    for (int k0 = lane; k0 < nk; k0 += 4 * 64) {
+        uint32_t key[4];
+        int nd[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int k = min(k0 + 64 * u, nk - 1);
+            key[u] = keys[k];
+            nd[u] = knode[k];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int k = k0 + 64 * u;
+            if (k < nk) atomicMax(&best[nd[u]], ((uint32_t)kp_s(key[u]) << 24) | (uint32_t)(0xFFFFFF - k));
+        }
     }
     wave_fence();
     const int nout = min(n, L.kcap);
@@ -1471,7 +1535,7 @@ static slam_status ensure_plan(slam_extractor* ex, int W, int H) {
     ex->have_plan = true;
     // k_octree keeps a level's keys in LDS behind its node arrays when they fit (else in
     // the per-frame global scratch).  Level 0 (by far the most FAST candidates, one wave per
-    // frame) gets up to 80 KB; the other levels share a launch sized for ~5 waves per CU.
+    // frame) gets up to 56 KB; the other levels share a launch sized for ~5 waves per CU.
     const size_t lds_max = 160 * 1024;
     int max_cells = 1;
     for (int l = 0; l < P.nlevels; l++) max_cells = std::max(max_cells, P.lv[l].cell_end - P.lv[l].cell_begin);
@@ -1490,7 +1554,7 @@ static slam_status ensure_plan(slam_extractor* ex, int W, int H) {
         slam_extractor::OctGroup& G = ex->oct[ex->n_oct++];
         G.l0 = l0;
         G.nl = nl;
-        G.keycap = keycap_for(g == 0 ? 80 * 1024 : 32 * 1024);
+        G.keycap = keycap_for(g == 0 ? 56 * 1024 : 32 * 1024);
         G.lds = octree_lds_bytes(P.max_nodes, G.keycap, max_cells);
         lds_attr = std::max(lds_attr, G.lds);
     }
