@@ -2,7 +2,7 @@
 // ORBextractor::operator() (ORBextractor.cc:1068-1150), batched over frames.
 //
 // Pipeline per batch (one stream):
-//   k_resize3     x (L-1)  chained INTER_LINEAR pyramid            ComputePyramid :1152
+//   k_resize4     x (L-1)  chained INTER_LINEAR pyramid            ComputePyramid :1152
 //   k_fast_wave   x 1      FAST-9 score + per-cell 3x3 NMS, 1 wave/cell ComputeKeyPointsOctTree :787-853
 //   k_fast_cells  x 1      the same for cells wider than one wave (1 WG/cell)
 //   k_octree      x 2      quadtree distribution, 1 wave/(frame,lvl) DistributeOctTree :537-761
@@ -139,30 +139,28 @@ __device__ __forceinline__ void stage_u32(uint32_t* dst, int dstride, const uint
 
 
 // ---------------------------------------------------------------------------------------
-// k_resize3: the resize with its coefficients recomputed per pixel in the reference's own
-// arithmetic (double (dx+0.5)*scale-0.5 -> float, cvFloor, saturate_cast<short> by
-// round-half-even) instead of gathered from tables: bit-identical to the host plan, and
-// the table gathers were what bound k_resize/k_resize2 (microbench: 199 -> 74 us at L1).
-// Thread = 4 output pixels of a row; source rows come from L2.
+// k_resize4: the resize with its coefficients recomputed in the reference's own arithmetic
+// (double (dx+0.5)*scale-0.5 -> float, cvFloor, saturate_cast<short> by round-half-even)
+// instead of gathered from tables: bit-identical to the host plan (table gathers bound an
+// earlier version: microbench 199 -> 74 us at L1).  Thread = 4 output columns x kRzRows
+// output rows: the four column coefficients (the FP64 part) are computed once, and a source
+// row loaded for output row y is reused for row y+1 when its vertical pair starts there
+// (scale 1.2: most rows).  Byte loads: a wave's 64 quads coalesce into row segments.
 // ---------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_resize3(Bufs b, int l, double scale_x, double scale_y) {
+constexpr int kRzRows = 4;
+
+__global__ void __launch_bounds__(256) k_resize4(Bufs b, int l, double scale_x, double scale_y) {
     const DevPlan& P = *b.plan;
     const DevLevel& L = P.lv[l];
     const DevLevel& S = P.lv[l - 1];
     const int qw = (L.w + 3) >> 2;
+    const int nrb = (L.h + kRzRows - 1) / kRzRows;
     const int f = blockIdx.y;
     const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= qw * L.h) return;
-    const int dy = i / qw, q = i - dy * qw;
+    if (i >= qw * nrb) return;
+    const int rb = i / qw, q = i - rb * qw;
     const uint8_t* src = level_ptr(b, P, f, l - 1);
     const int spitch = level_pitch(P, l - 1);
-    float fy = (float)((dy + 0.5) * scale_y - 0.5);
-    const int sy = (int)floorf(fy);
-    fy -= (float)sy;
-    const int b0 = (int)rintf((1.f - fy) * 2048), b1 = (int)rintf(fy * 2048);
-    const int y0 = min(max(sy, 0), S.h - 1), y1 = min(max(sy + 1, 0), S.h - 1);
-    const uint8_t* S0 = src + (size_t)y0 * spitch;
-    const uint8_t* S1 = src + (size_t)y1 * spitch;
     int sxs[4], a0s[4], a1s[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
@@ -178,24 +176,44 @@ __global__ void __launch_bounds__(256) k_resize3(Bufs b, int l, double scale_x, 
         a0s[k] = a0;
         a1s[k] = a1;
     }
-    int p00[4], p01[4], p10[4], p11[4];
+    // horizontal pass of one source row (HResizeLinear): D[k] = S[sx]*a0 + S[sx+1]*a1
+    auto hrow = [&](int y, int* d) {
+        const uint8_t* r = src + (size_t)min(max(y, 0), S.h - 1) * spitch;
+        int p0[4], p1[4];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        p00[k] = S0[sxs[k]];
-        p01[k] = S0[sxs[k] + 1];
-        p10[k] = S1[sxs[k]];
-        p11[k] = S1[sxs[k] + 1];
-    }
-    uint32_t word = 0;
+        for (int k = 0; k < 4; k++) { p0[k] = r[sxs[k]]; p1[k] = r[sxs[k] + 1]; }
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int d0 = __mul24(p00[k], a0s[k]) + __mul24(p01[k], a1s[k]);
-        const int d1 = __mul24(p10[k], a0s[k]) + __mul24(p11[k], a1s[k]);
-        const int v = ((__mul24(b0, d0 >> 4) >> 16) + (__mul24(b1, d1 >> 4) >> 16) + 2) >> 2;
-        word |= (uint32_t)(v & 0xFF) << (8 * k);
+        for (int k = 0; k < 4; k++) d[k] = __mul24(p0[k], a0s[k]) + __mul24(p1[k], a1s[k]);
+    };
+    uint8_t* dbase = b.pyr + (size_t)f * P.pyr_frame + L.pyr_off + 4 * q;
+    int D0[4], D1[4];
+    int have = INT_MIN;  // source row currently held in D1 (INT_MIN: none)
+#pragma unroll
+    for (int rr = 0; rr < kRzRows; rr++) {
+        const int dy = rb * kRzRows + rr;
+        if (dy >= L.h) break;
+        float fy = (float)((dy + 0.5) * scale_y - 0.5);
+        const int sy = (int)floorf(fy);
+        fy -= (float)sy;
+        const int b0 = (int)rintf((1.f - fy) * 2048), b1 = (int)rintf(fy * 2048);
+        // rows are clamped (VResizeLinear reads clip(sy+k, 0, h-1)); reuse by clamped index
+        const int y0 = min(max(sy, 0), S.h - 1), y1 = min(max(sy + 1, 0), S.h - 1);
+        if (have == y0) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) D0[k] = D1[k];
+        } else {
+            hrow(y0, D0);
+        }
+        hrow(y1, D1);
+        have = y1;
+        uint32_t word = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int v = ((__mul24(b0, D0[k] >> 4) >> 16) + (__mul24(b1, D1[k] >> 4) >> 16) + 2) >> 2;
+            word |= (uint32_t)(v & 0xFF) << (8 * k);
+        }
+        *reinterpret_cast<uint32_t*>(dbase + (size_t)dy * L.pitch) = word;
     }
-    uint8_t* dbase = b.pyr + (size_t)f * P.pyr_frame + L.pyr_off;
-    *reinterpret_cast<uint32_t*>(dbase + (size_t)dy * L.pitch + 4 * q) = word;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1638,7 +1656,8 @@ static slam_status launch_range(slam_extractor* ex, int f0, int nframes, const u
         const int qw = (P.lv[l].w + 3) / 4;
         const double sxv = 1. / ((double)P.lv[l].w / P.lv[l - 1].w);
         const double syv = 1. / ((double)P.lv[l].h / P.lv[l - 1].h);
-        hipLaunchKernelGGL(k_resize3, dim3((qw * P.lv[l].h + 255) / 256, nframes), dim3(256), 0, s, b, l, sxv, syv);
+        const int nrb = (P.lv[l].h + kRzRows - 1) / kRzRows;
+        hipLaunchKernelGGL(k_resize4, dim3((qw * nrb + 255) / 256, nframes), dim3(256), 0, s, b, l, sxv, syv);
     }
     end(kStResize);
     // ranges run FAST one after another (each fills the chip); a range's octree / layout /
