@@ -323,7 +323,7 @@ typedef struct slam_camera {
 typedef struct slam_lba_problem {
     int32_t n_kf;               /* KeyFrame vertices (local + fixed), mnId order */
     const float* kf_Tcw;        /* n_kf x 16, row-major KeyFrame::GetPose() (cv::Mat 4x4 f32) */
-    const uint8_t* kf_fixed;    /* 1 = setFixed (init KF or lFixedCameras) */
+    const uint8_t* kf_fixed;    /* 0 free, 1 the map init KF (setFixed, written back), 2 lFixedCameras */
     int32_t n_pt;               /* MapPoint vertices (all marginalized) */
     const float* pt_pos;        /* n_pt x 3, MapPoint::GetWorldPos() */
     int32_t n_edge;             /* edges, insertion order, edge_pt non-decreasing */

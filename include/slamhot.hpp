@@ -1,0 +1,341 @@
+/* slamhot.hpp — C++ host layer over the slamhot C ABI (include/slamhot.h).
+ *
+ * The reference's host code is C++ (ORB_SLAM3::ORBextractor, ORB_SLAM3::ORBmatcher,
+ * ORB_SLAM3::Optimizer).  These classes keep its names, argument meaning and error
+ * behaviour, so a Tracking / LocalMapping port calls them the way it calls the originals;
+ * only the OpenCV / map types are replaced by plain views (the shims in INTEGRATION.md do
+ * the cv::Mat / KeyFrame conversion on top of this header).  Every method is a thin call
+ * into libslamhot.so: all computation runs on the gfx950 device, and a missing device or
+ * library surfaces as slamhot::Error (SLAM_ENODEV), never as a CPU fallback.
+ *
+ * Header-only; link with -lslamhot.  Thread-safety follows the reference: one extractor per
+ * camera used by one thread at a time, matchers and solvers per calling thread.
+ */
+#ifndef SLAMHOT_HPP
+#define SLAMHOT_HPP
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "slamhot.h"
+
+namespace slamhot {
+
+class Error : public std::runtime_error {
+   public:
+    Error(slam_status st, const std::string& what)
+        : std::runtime_error(what + ": " + slamhot_status_string(st)), status(st) {}
+    slam_status status;
+};
+
+inline void check(slam_status st, const char* what) {
+    if (st != SLAM_OK) throw Error(st, what);
+}
+
+/* cv::KeyPoint memory layout (pt.x, pt.y, size, angle, response, octave, class_id). */
+using KeyPoint = slam_keypoint;
+
+/* A CV_8UC1 image as the reference passes it (cv::InputArray of a grayscale Mat). */
+struct GrayImage {
+    const uint8_t* data = nullptr;
+    int cols = 0, rows = 0;
+    size_t step = 0;  // bytes per row
+    bool empty() const { return data == nullptr || cols <= 0 || rows <= 0; }
+};
+
+/* Owning 8-bit matrix: descriptors (N x 32) and pyramid levels. */
+struct Mat8U {
+    int rows = 0, cols = 0;
+    std::vector<uint8_t> data;
+    const uint8_t* row(int r) const { return data.data() + (size_t)r * cols; }
+};
+
+/* ------------------------------------------------------------------------------------
+ * ORBextractor (ORBextractor.h:45-111).  Construction mirrors
+ * ORBextractor(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST)
+ * (ORBextractor.cc:408-468); the device handle is sized for the frames it sees.
+ * ---------------------------------------------------------------------------------- */
+class ORBextractor {
+   public:
+    ORBextractor(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST,
+                 int device = 0)
+        : device_(device) {
+        prm_.nfeatures = nfeatures;
+        prm_.scale_factor = scaleFactor;
+        prm_.nlevels = nlevels;
+        prm_.ini_th_fast = iniThFAST;
+        prm_.min_th_fast = minThFAST;
+        reserve(752, 480);  // EuRoC; grown on the first larger frame
+        int nl = 0;
+        check(slamhot_extractor_levels(ex_, &nl, nullptr, nullptr, nullptr, nullptr, nullptr), "levels");
+        scale_.resize(nl);
+        inv_scale_.resize(nl);
+        sigma2_.resize(nl);
+        inv_sigma2_.resize(nl);
+        nfeat_.resize(nl);
+        check(slamhot_extractor_levels(ex_, &nl, scale_.data(), inv_scale_.data(), sigma2_.data(),
+                                       inv_sigma2_.data(), nfeat_.data()),
+              "levels");
+    }
+    ~ORBextractor() { slamhot_extractor_destroy(ex_); }
+    ORBextractor(const ORBextractor&) = delete;
+    ORBextractor& operator=(const ORBextractor&) = delete;
+
+    /* int operator()(InputArray image, InputArray mask, vector<KeyPoint>& keypoints,
+     *                OutputArray descriptors, vector<int>& vLappingArea)
+     * (ORBextractor.cc:1068-1150): returns monoIndex, or -1 for an empty image (:1072-1073,
+     * outputs untouched).  The mask is ignored by the reference as well. */
+    int operator()(const GrayImage& image, std::vector<KeyPoint>& keypoints, Mat8U& descriptors,
+                   const std::vector<int>& vLappingArea) {
+        if (image.empty()) return -1;
+        reserve(image.cols, image.rows);
+        const int lap0 = vLappingArea.size() > 0 ? vLappingArea[0] : 0;
+        const int lap1 = vLappingArea.size() > 1 ? vLappingArea[1] : 0;
+        int cap = 2 * prm_.nfeatures + 64, n = 0, mono = 0;
+        for (int attempt = 0; attempt < 2; attempt++) {
+            keypoints.resize(cap);
+            descriptors.data.resize((size_t)cap * 32);
+            const slam_status st = slamhot_extract(ex_, image.data, image.cols, image.rows,
+                                                   image.step ? image.step : (size_t)image.cols, lap0, lap1,
+                                                   keypoints.data(), descriptors.data.data(), cap, &n, &mono);
+            if (st == SLAM_ECAP && attempt == 0) { cap = n; continue; }
+            if (st == SLAM_EEMPTY) return -1;
+            check(st, "ORBextractor::operator()");
+            break;
+        }
+        keypoints.resize(n);
+        descriptors.rows = n;
+        descriptors.cols = 32;
+        descriptors.data.resize((size_t)n * 32);
+        last_frames_ = 1;
+        return mono;
+    }
+
+    int inline GetLevels() const { return (int)scale_.size(); }
+    float inline GetScaleFactor() const { return prm_.scale_factor; }
+    std::vector<float> inline GetScaleFactors() const { return scale_; }
+    std::vector<float> inline GetInverseScaleFactors() const { return inv_scale_; }
+    std::vector<float> inline GetScaleSigmaSquares() const { return sigma2_; }
+    std::vector<float> inline GetInverseScaleSigmaSquares() const { return inv_sigma2_; }
+    /* mnFeaturesPerLevel (private in the reference, ORBextractor.h:99) */
+    std::vector<int> GetFeaturesPerLevel() const { return nfeat_; }
+
+    /* public std::vector<cv::Mat> mvImagePyramid (ORBextractor.h:83): host copies of the
+     * last frame's levels (the device pyramid stays where k_stereo_* reads it). */
+    std::vector<Mat8U> mvImagePyramid() const {
+        std::vector<Mat8U> out;
+        if (!last_frames_) return out;
+        for (int l = 0; l < GetLevels(); l++) {
+            Mat8U m;
+            int w = 0, h = 0;
+            check(slamhot_pyramid_level(ex_, 0, l, nullptr, 0, &w, &h), "pyramid_level size");
+            m.cols = w;
+            m.rows = h;
+            m.data.resize((size_t)w * h);
+            check(slamhot_pyramid_level(ex_, 0, l, m.data.data(), m.data.size(), &w, &h), "pyramid_level");
+            out.push_back(std::move(m));
+        }
+        return out;
+    }
+
+    slam_extractor* handle() { return ex_; }
+
+   private:
+    void reserve(int w, int h) {
+        if (ex_ && w <= max_w_ && h <= max_h_) return;
+        if (ex_) slamhot_extractor_destroy(ex_);
+        ex_ = nullptr;
+        max_w_ = std::max(w, max_w_);
+        max_h_ = std::max(h, max_h_);
+        check(slamhot_extractor_create(&prm_, device_, max_w_, max_h_, 1, &ex_), "ORBextractor");
+    }
+    slam_orb_params prm_{};
+    int device_ = 0, max_w_ = 0, max_h_ = 0, last_frames_ = 0;
+    slam_extractor* ex_ = nullptr;
+    std::vector<float> scale_, inv_scale_, sigma2_, inv_sigma2_;
+    std::vector<int> nfeat_;
+};
+
+/* ------------------------------------------------------------------------------------
+ * ORBmatcher (ORBmatcher.h:36-110).  The KeyFrame / Frame arguments arrive as their
+ * matcher-relevant views; the MapPoint* outputs as indices into the other side (-1 = NULL).
+ * ---------------------------------------------------------------------------------- */
+struct KeyFrameBow : slam_bow_side {};  // pKF: descriptors, angles, MapPoint validity, mFeatVec
+struct FrameBow : slam_bow_side {};     // F: descriptors, angles, mFeatVec (valid ignored)
+
+class ORBmatcher {
+   public:
+    static constexpr int TH_LOW = 50, TH_HIGH = 100, HISTO_LENGTH = 30;  // ORBmatcher.h:90-92
+
+    explicit ORBmatcher(float nnratio = 0.6f, bool checkOri = true, int device = 0)
+        : nnratio_(nnratio), check_ori_(checkOri) {
+        check(slamhot_matcher_create(device, &m_), "ORBmatcher");
+    }
+    ~ORBmatcher() { slamhot_matcher_destroy(m_); }
+    ORBmatcher(const ORBmatcher&) = delete;
+    ORBmatcher& operator=(const ORBmatcher&) = delete;
+
+    /* static int DescriptorDistance(const cv::Mat& a, const cv::Mat& b) (ORBmatcher.cc:
+     * 2561-2577): bit-set count of a XOR b over 8 x 32 bits.  A host utility in the
+     * reference too (MapPoint::ComputeDistinctiveDescriptors etc. call it on the CPU). */
+    static int DescriptorDistance(const uint8_t* a, const uint8_t* b) {
+        int dist = 0;
+        for (int i = 0; i < 8; i++) {
+            uint32_t x, y;
+            std::memcpy(&x, a + 4 * i, 4);
+            std::memcpy(&y, b + 4 * i, 4);
+            dist += __builtin_popcount(x ^ y);
+        }
+        return dist;
+    }
+
+    /* int SearchByBoW(KeyFrame* pKF, Frame& F, vector<MapPoint*>& vpMapPointMatches)
+     * (ORBmatcher.cc:269-471): vpMapPointMatches[i] = KF feature whose MapPoint F's
+     * feature i took, -1 = NULL.  Returns nmatches. */
+    int SearchByBoW(const KeyFrameBow& KF, const FrameBow& F, std::vector<int>& vpMapPointMatches) {
+        vpMapPointMatches.assign(F.n, -1);
+        a2b_.assign(KF.n, -1);
+        int n = 0;
+        check(slamhot_search_by_bow(m_, &KF, &F, nnratio_, check_ori_, 0, a2b_.data(), vpMapPointMatches.data(), &n),
+              "SearchByBoW(KF, F)");
+        return n;
+    }
+
+    /* int SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*>& vpMatches12)
+     * (ORBmatcher.cc:823-963): vpMatches12[i] = KF2 feature matched by KF1 feature i. */
+    int SearchByBoW(const KeyFrameBow& KF1, const KeyFrameBow& KF2, std::vector<int>& vpMatches12) {
+        vpMatches12.assign(KF1.n, -1);
+        b2a_.assign(KF2.n, -1);
+        int n = 0;
+        check(slamhot_search_by_bow(m_, &KF1, &KF2, nnratio_, check_ori_, 1, vpMatches12.data(), b2a_.data(), &n),
+              "SearchByBoW(KF1, KF2)");
+        return n;
+    }
+
+    slam_matcher* handle() { return m_; }
+
+   private:
+    float nnratio_;
+    bool check_ori_;
+    slam_matcher* m_ = nullptr;
+    std::vector<int> a2b_, b2a_;  // the ABI's other-direction output (unused by the caller)
+};
+
+/* ------------------------------------------------------------------------------------
+ * Optimizer::LocalBundleAdjustment (Optimizer.h:59, Optimizer.cc:1611-2078) over a window
+ * the caller has built and flattened (Optimizer.cc:1613-1718; INTEGRATION.md shim).
+ * ---------------------------------------------------------------------------------- */
+struct LocalBAWindow {
+    std::vector<float> kf_Tcw;        // n_kf x 16, KeyFrame::GetPose(), mnId order
+    std::vector<uint8_t> kf_fixed;    // 0 free, 1 the map's init KF (setFixed, in lLocalKeyFrames), 2 lFixedCameras
+    std::vector<float> pt_pos;        // n_pt x 3
+    std::vector<int32_t> edge_pt, edge_kf;
+    std::vector<float> edge_obs;      // n_edge x 3 (u, v, uRight < 0 -> mono)
+    std::vector<float> edge_inv_sigma2;
+    slam_camera cam{};
+    bool inertial = false;            // pMap->IsInertial(): lambda0 = 100 (Optimizer.cc:1726)
+    int n_kf() const { return (int)kf_fixed.size(); }
+    int n_pt() const { return (int)pt_pos.size() / 3; }
+    int n_edge() const { return (int)edge_pt.size(); }
+};
+
+struct LocalBAResult {
+    std::vector<float> kf_Tcw, pt_pos;
+    std::vector<uint8_t> edge_outlier;  // vToErase (Optimizer.cc:1995-2038)
+    int iterations[2] = {0, 0}, trials = 0, n_outlier = 0;
+    double chi2_initial = 0, chi2_final = 0;
+};
+
+class LocalBundleAdjuster {
+   public:
+    explicit LocalBundleAdjuster(int device = 0) { check(slamhot_lba_create(device, &s_), "LocalBundleAdjuster"); }
+    ~LocalBundleAdjuster() { slamhot_lba_destroy(s_); }
+    LocalBundleAdjuster(const LocalBundleAdjuster&) = delete;
+    LocalBundleAdjuster& operator=(const LocalBundleAdjuster&) = delete;
+
+    /* Many independent windows in one call (batched mode); pbStopFlag as the reference's. */
+    void Solve(const std::vector<LocalBAWindow>& ws, const bool* pbStopFlag, std::vector<LocalBAResult>& out) {
+        const int n = (int)ws.size();
+        std::vector<slam_lba_problem> probs(n);
+        std::vector<slam_lba_result> res(n);
+        out.assign(n, LocalBAResult{});
+        for (int i = 0; i < n; i++) {
+            const LocalBAWindow& w = ws[i];
+            slam_lba_problem& p = probs[i];
+            p.n_kf = w.n_kf();
+            p.kf_Tcw = w.kf_Tcw.data();
+            p.kf_fixed = w.kf_fixed.data();
+            p.n_pt = w.n_pt();
+            p.pt_pos = w.pt_pos.data();
+            p.n_edge = w.n_edge();
+            p.edge_pt = w.edge_pt.data();
+            p.edge_kf = w.edge_kf.data();
+            p.edge_obs = w.edge_obs.data();
+            p.edge_inv_sigma2 = w.edge_inv_sigma2.data();
+            p.cam = w.cam;
+            out[i].kf_Tcw.resize(w.kf_Tcw.size());
+            out[i].pt_pos.resize(w.pt_pos.size());
+            out[i].edge_outlier.resize(w.edge_pt.size());
+            res[i] = slam_lba_result{};
+            res[i].kf_Tcw = out[i].kf_Tcw.data();
+            res[i].pt_pos = out[i].pt_pos.data();
+            res[i].edge_outlier = out[i].edge_outlier.data();
+        }
+        slam_lba_options opt{};
+        opt.iters_first = 5;
+        opt.iters_second = 10;
+        opt.user_lambda_init = (n > 0 && ws[0].inertial) ? 100.0 : 0.0;
+        volatile int32_t stop = 0;
+        // the reference polls *pbStopFlag between trials; the ABI polls an int32 the same way
+        const volatile int32_t* sf = nullptr;
+        if (pbStopFlag) {
+            stop = *pbStopFlag ? 1 : 0;
+            sf = &stop;
+        }
+        check(slamhot_lba_solve(s_, n, probs.data(), &opt, sf, res.data()), "LocalBundleAdjustment");
+        for (int i = 0; i < n; i++) {
+            out[i].iterations[0] = res[i].iterations[0];
+            out[i].iterations[1] = res[i].iterations[1];
+            out[i].trials = res[i].trials;
+            out[i].n_outlier = res[i].n_outlier;
+            out[i].chi2_initial = res[i].chi2_initial;
+            out[i].chi2_final = res[i].chi2_final;
+        }
+    }
+
+    slam_lba* handle() { return s_; }
+
+   private:
+    slam_lba* s_ = nullptr;
+};
+
+namespace Optimizer {
+/* static void Optimizer::LocalBundleAdjustment(KeyFrame* pKF, bool* pbStopFlag, Map* pMap,
+ *     int& num_fixedKF, int& num_OptKF, int& num_MPs, int& num_edges)
+ * on a flattened window: the four counters as the reference reports them (:1714-1718,
+ * 1800-1921), the solved poses / points and vToErase in `out`. */
+inline void LocalBundleAdjustment(LocalBundleAdjuster& solver, const LocalBAWindow& w, bool* pbStopFlag,
+                                  LocalBAResult& out, int& num_fixedKF, int& num_OptKF, int& num_MPs,
+                                  int& num_edges) {
+    num_fixedKF = 0;
+    num_OptKF = 0;
+    for (uint8_t f : w.kf_fixed) {
+        num_fixedKF += f ? 1 : 0;      // lFixedCameras.size() + the init KF (:1630-1675)
+        num_OptKF += f == 2 ? 0 : 1;   // lLocalKeyFrames.size() (:1749)
+    }
+    num_MPs = w.n_pt();
+    num_edges = w.n_edge();
+    if (num_fixedKF == 0) return;  // Optimizer.cc:1714-1718
+    std::vector<LocalBAResult> res;
+    solver.Solve({w}, pbStopFlag, res);
+    out = std::move(res[0]);
+}
+}  // namespace Optimizer
+
+}  // namespace slamhot
+
+#endif  // SLAMHOT_HPP
