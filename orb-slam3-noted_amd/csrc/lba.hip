@@ -466,10 +466,10 @@ __device__ inline void wave_sync() {
 // config-4 off-diagonal block has ~50 contributions: ~3 per lane; 8 or 4 lanes measured slower).  The reference
 // block (i1, i2) (upper) is written transposed into the lower triangle of the dense row-major
 // matrix; diagonal blocks also produce the rhs row b_s = b_p - sum B db (augmented row n).
-#ifndef SCHUR_LANES
-#define SCHUR_LANES 16
-#endif
-constexpr int kSchurLanes = SCHUR_LANES;
+// Blocks are visited through an order list: every window's diagonal blocks first (one wave
+// each: a diagonal block sums a contribution per observation of its pose, ~330 at config 4),
+// then the off-diagonal ones (16 lanes each, ~50 contributions).
+constexpr int kSchurLanes = 16, kSchurDiagLanes = 64;
 
 template <int W16>
 __device__ inline double group_sum(double v) {
@@ -478,63 +478,84 @@ __device__ inline double group_sum(double v) {
     return v;
 }
 
-__global__ void __launch_bounds__(256) k_schur_block(int nblk_total, const int2* __restrict__ blk_pose,
+// XCD-aware workgroup order (cdna_hip_programming.md T1, bijective form): hardware
+// round-robins consecutive workgroups over the 8 XCDs; remapped, each XCD takes a contiguous
+// run of the window-major block list, so a window's edge data (B Dinv, Hpl: ~5 MB at config
+// 4) is gathered through one XCD's L2 instead of all eight.  Speed only: any placement is
+// correct.
+__device__ __forceinline__ int xcd_swizzle(int orig, int nwg) {
+    const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
+template <int NL>
+__global__ void __launch_bounds__(256) k_schur_block(int nlist, const int* __restrict__ order,
+                                                     const int2* __restrict__ blk_pose,
                                                      const int* __restrict__ blk_win, const int* __restrict__ ct_off,
                                                      const int2* __restrict__ ct, const WinDesc* __restrict__ wins,
                                                      const WinCtl* __restrict__ ctl, const double* __restrict__ Hpp,
                                                      const double* __restrict__ bp, const int* __restrict__ pe_off,
                                                      const int* __restrict__ pe, const double* __restrict__ lin,
                                                      const double* __restrict__ tr, double* __restrict__ Hs) {
-    const int blk = blockIdx.x * (256 / kSchurLanes) + threadIdx.x / kSchurLanes, lane = threadIdx.x % kSchurLanes;
-    const bool live = blk < nblk_total;
-    const int b = live ? blk : 0;
+    const int wg = xcd_swizzle((int)blockIdx.x, (int)gridDim.x);
+    const int idx = wg * (256 / NL) + threadIdx.x / NL, lane = threadIdx.x % NL;
+    const bool live = idx < nlist;
+    const int b = order[live ? idx : 0];
     const int win = blk_win[b];
     const WinCtl& C = ctl[win];
     const bool act = live && C.need_trial;
     const WinDesc W = wins[win];
     const int2 ij = blk_pose[b];  // local free-pose indices i1 <= i2
     const int i1 = ij.x, i2 = ij.y;
-    double acc[36];
+    // lane = (row half h, contribution stream j): rows 3h..3h+2 of the 6x6 over every 8th
+    // contribution; 18 accumulators instead of 36 keep the kernel at 4 waves per SIMD
+    const int h = lane & 1, j = lane >> 1;
+    constexpr int kStreams = NL / 2;
+    double acc[18];
 #pragma unroll
-    for (int k = 0; k < 36; k++) acc[k] = 0.0;
+    for (int k = 0; k < 18; k++) acc[k] = 0.0;
     if (act) {
-        for (int k = ct_off[b] + lane; k < ct_off[b + 1]; k += kSchurLanes) {
+        for (int k = ct_off[b] + j; k < ct_off[b + 1]; k += kStreams) {
             const int2 ab = ct[k];
-            const double* BD = tr + (long long)kTrStride * ab.x;
+            const double* BD = tr + (long long)kTrStride * ab.x + 9 * h;
             const double* Bj = lin + (long long)kHplStride * ab.y;
-            double bd[18], bj[18];
+            double bd[9], bj[18];
 #pragma unroll
-            for (int t = 0; t < 18; t++) {
-                bd[t] = BD[t];
-                bj[t] = Bj[t];
-            }
+            for (int t = 0; t < 9; t++) bd[t] = BD[t];
 #pragma unroll
-            for (int r = 0; r < 6; r++)
+            for (int t = 0; t < 18; t++) bj[t] = Bj[t];
+#pragma unroll
+            for (int r = 0; r < 3; r++)
 #pragma unroll
                 for (int c = 0; c < 6; c++)
                     acc[6 * r + c] += bd[3 * r] * bj[3 * c] + bd[3 * r + 1] * bj[3 * c + 1] + bd[3 * r + 2] * bj[3 * c + 2];
         }
     }
+    // butterfly over the 8 streams of the same half (lane bits 1..3)
 #pragma unroll
-    for (int k = 0; k < 36; k++) acc[k] = group_sum<kSchurLanes>(acc[k]);
+    for (int k = 0; k < 18; k++) {
+#pragma unroll
+        for (int o = 2; o < NL; o <<= 1) acc[k] += __shfl_xor(acc[k], o, NL);
+    }
     double sb[6] = {0, 0, 0, 0, 0, 0};
     const int gp = W.pose0 + i1;
     if (act && i1 == i2) {
-        for (int k = pe_off[gp] + lane; k < pe_off[gp + 1]; k += kSchurLanes) {
+        for (int k = pe_off[gp] + lane; k < pe_off[gp + 1]; k += NL) {
             const double* T = tr + (long long)kTrStride * pe[k] + 18;
 #pragma unroll
             for (int r = 0; r < 6; r++) sb[r] += T[r];
         }
     }
 #pragma unroll
-    for (int r = 0; r < 6; r++) sb[r] = group_sum<kSchurLanes>(sb[r]);
+    for (int r = 0; r < 6; r++) sb[r] = group_sum<NL>(sb[r]);
     if (!act) return;
     double* H = Hs + W.hs_off;
+    // every lane of a half holds that half's sums: stream j writes its elements j, j+8, j+16
 #pragma unroll
-    for (int q = 0; q < (36 + kSchurLanes - 1) / kSchurLanes; q++) {
-        const int e = lane + kSchurLanes * q;
-        if (e >= 36) break;
-        const int r = e / 6, c = e % 6;
+    for (int q = 0; q < 3; q++) {
+        const int e = j + kStreams * q;  // element of this half (rows 3h.., 6 columns)
+        if (e >= 18) break;
+        const int r = 3 * h + e / 6, c = e % 6;
         double v = 0.0;
         if (i1 == i2) {
             const int rr = r <= c ? r : c, cc = r <= c ? c : r;
@@ -543,7 +564,7 @@ __global__ void __launch_bounds__(256) k_schur_block(int nblk_total, const int2*
         }
         double m = 0.0;
 #pragma unroll
-        for (int k = 0; k < 36; k++)
+        for (int k = 0; k < 18; k++)
             if (k == e) m = acc[k];
         v -= m;
         // upper (i1, i2)[r][c] -> lower element (6 i2 + c, 6 i1 + r)
@@ -1074,7 +1095,7 @@ struct Plan {
     EdgeS* edges;
     WinDesc* wins;
     WinCtl* ctl;
-    int *pt_off, *pt_win, *spe_off, *spe, *pe_off, *pe, *pose_win, *kf_hp, *kf_win, *blk_win, *ct_off;
+    int *pt_off, *pt_win, *spe_off, *spe, *pe_off, *pe, *pose_win, *kf_hp, *kf_win, *blk_win, *ct_off, *blk_order;
     int2 *blk_pose, *ct;
     float *kf_in, *pt_in;
 };
@@ -1110,7 +1131,7 @@ struct PlanSizes {
 
 struct Layout {
     size_t edges, wins, ctl, pt_off, pt_win, spe_off, spe, pe_off, pe, pose_win, kf_hp, kf_win, blk_win, ct_off,
-        blk_pose, ct, kf_in, pt_in, total;
+        blk_order, blk_pose, ct, kf_in, pt_in, total;
 };
 
 Layout make_layout(const PlanSizes& z) {
@@ -1135,6 +1156,7 @@ Layout make_layout(const PlanSizes& z) {
     L.kf_win = take(sizeof(int) * z.nkf);
     L.blk_win = take(sizeof(int) * z.nblk);
     L.ct_off = take(sizeof(int) * (z.nblk + 1));
+    L.blk_order = take(sizeof(int) * z.nblk);
     L.blk_pose = take(sizeof(int2) * z.nblk);
     L.ct = take(sizeof(int2) * z.nct);
     L.kf_in = take(sizeof(float) * 16 * z.nkf);
@@ -1158,6 +1180,7 @@ Plan bind(unsigned char* base, const Layout& L) {
     P.kf_hp = (int*)(base + L.kf_hp);
     P.kf_win = (int*)(base + L.kf_win);
     P.blk_win = (int*)(base + L.blk_win);
+    P.blk_order = (int*)(base + L.blk_order);
     P.ct_off = (int*)(base + L.ct_off);
     P.blk_pose = (int2*)(base + L.blk_pose);
     P.ct = (int2*)(base + L.ct);
@@ -1306,6 +1329,9 @@ slam_status plan_fill(int n_prob, const slam_lba_problem* probs, const std::vect
                 P.blk_pose[nblk + b] = int2{i1, i2};
                 P.blk_win[nblk + b] = w;
                 P.ct_off[nblk + b] = (int)(nct + bcnt[b]);
+                // diagonal blocks of all windows first, then the off-diagonal ones
+                if (i1 == i2) P.blk_order[npose + i2] = nblk + b;
+                else P.blk_order[Z.npose + (nblk - npose) + (b - i2)] = nblk + b;
             }
         for (int p = 0; p < Q.n_pt; p++) {
             const int s0 = P.spe_off[npt + p], s1 = p + 1 < Q.n_pt ? P.spe_off[npt + p + 1] : nspe;
@@ -1551,9 +1577,14 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
                 k_schur_edges<<<blocks(Z.nspe, T), T, 0, S>>>(Z.nspe, DP.spe, dE, dC, as<double>(s->Hll),
                                                                as<double>(s->bl), as<double>(s->lin),
                                                                as<double>(s->tr));
-                if (H.nblk)
-                    k_schur_block<<<blocks(H.nblk, 256 / kSchurLanes), 256, 0, S>>>(
-                        H.nblk, DP.blk_pose, DP.blk_win, DP.ct_off, DP.ct, dW,
+                if (H.npose)
+                    k_schur_block<kSchurDiagLanes><<<blocks(H.npose, 256 / kSchurDiagLanes), 256, 0, S>>>(
+                        H.npose, DP.blk_order, DP.blk_pose, DP.blk_win, DP.ct_off, DP.ct, dW,
+                        dC, as<double>(s->Hpp), as<double>(s->bp), DP.pe_off, DP.pe,
+                        as<double>(s->lin), as<double>(s->tr), as<double>(s->Hs));
+                if (H.nblk > H.npose)
+                    k_schur_block<kSchurLanes><<<blocks(H.nblk - H.npose, 256 / kSchurLanes), 256, 0, S>>>(
+                        H.nblk - H.npose, DP.blk_order + H.npose, DP.blk_pose, DP.blk_win, DP.ct_off, DP.ct, dW,
                         dC, as<double>(s->Hpp), as<double>(s->bp), DP.pe_off, DP.pe,
                         as<double>(s->lin), as<double>(s->tr), as<double>(s->Hs));
                 k_ldlt<<<nw, 512, lds_bytes, S>>>(dW, dC, as<double>(s->Hs), as<double>(s->xp));
