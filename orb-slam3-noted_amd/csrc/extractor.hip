@@ -89,6 +89,18 @@ typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ us2 as_us2(uint32_t x) { return __builtin_bit_cast(us2, x); }
 __device__ __forceinline__ uint32_t as_u32(us2 x) { return __builtin_bit_cast(uint32_t, x); }
 
+// Sum over the wave, result in every lane: DPP within rows of 16 (quad_perm xor 1 / 2,
+// half-row and row mirrors: VALU-speed, no LDS crossbar), then the four row sums by
+// v_readlane (a __shfl_xor butterfly is six dependent ds_bpermute round trips).
+__device__ __forceinline__ int wave_sum_dpp(int x) {
+    x += __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    x += __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    x += __builtin_amdgcn_update_dpp(0, x, 0x141, 0xF, 0xF, false);  // row_half_mirror
+    x += __builtin_amdgcn_update_dpp(0, x, 0x140, 0xF, 0xF, false);  // row_mirror
+    return __builtin_amdgcn_readlane(x, 0) + __builtin_amdgcn_readlane(x, 16) + __builtin_amdgcn_readlane(x, 32) +
+           __builtin_amdgcn_readlane(x, 48);
+}
+
 // acc + number of set bits of m below this lane (v_mbcnt_lo/hi)
 __device__ __forceinline__ int mbcnt64(uint64_t m, int acc) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, (uint32_t)acc));
@@ -1179,59 +1191,82 @@ __global__ void __launch_bounds__(256) k_orb3(Bufs b) {
     uint32_t* raw = raw_all[wave];
     uint32_t* hp = hp_all[wave];
     const int xs = (kx - 21) & ~3, sh = (kx - 21) - xs;
-    // ---- stage the raw window (rows ky-21..ky+21 reflected, 12 dwords per row)
+    const int um = lane <= kHalfPatch ? P.umax[lane] : 0;  // umax[v] in lane v (read once)
+#ifdef SLAMHOT_ORB_TRACE
+    long long otr[8];
+    int notr = 0;
+    const bool otrace = f == 100 && (slot % 97) == 5 && lane == 0;
+#define ORB_MARK() do { if (otrace) otr[notr++] = (long long)__builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define ORB_MARK() do {} while (0)
+#endif
+    ORB_MARK();
+    // ---- stage the raw window (rows ky-21..ky+21 reflected, 12 dwords per row) as three
+    // 16-byte pieces per row: 129 pieces, <= 3 per lane; pieces that leave the level go
+    // byte by byte through BORDER_REFLECT_101
     {
         const int wfull = (pitch & 3) ? 0 : (L.w & ~3);
-        uint32_t v[9];
+        uint4 v[3];
 #pragma unroll
-        for (int k = 0; k < 9; k++) {
+        for (int k = 0; k < 3; k++) {
             const int e = lane + 64 * k;
-            v[k] = 0;
-            if (e < kO3R * 12) {
-                const int r = e / 12, c = e - r * 12;
+            v[k] = make_uint4(0, 0, 0, 0);
+            if (e < kO3R * 3) {
+                const int r = e / 3, part = e - 3 * r;
                 const int yy = refl101(ky - 21 + r, L.h);
                 const uint8_t* rowp = img + (size_t)yy * pitch;
-                const int x = xs + 4 * c;
-                if (x >= 0 && x + 4 <= wfull) {
-                    v[k] = *reinterpret_cast<const uint32_t*>(rowp + x);
+                const int x = xs + 16 * part;
+                if (x >= 0 && x + 16 <= wfull) {
+                    v[k] = *reinterpret_cast<const uint4*>(rowp + x);
                 } else {
+                    uint32_t w[4] = {0, 0, 0, 0};
 #pragma unroll
-                    for (int q = 0; q < 4; q++) v[k] |= (uint32_t)rowp[refl101(min(x + q, L.w + 3), L.w)] << (8 * q);
+                    for (int q = 0; q < 16; q++) w[q >> 2] |= (uint32_t)rowp[refl101(min(x + q, L.w + 3), L.w)] << (8 * (q & 3));
+                    v[k] = make_uint4(w[0], w[1], w[2], w[3]);
                 }
             }
         }
 #pragma unroll
-        for (int k = 0; k < 9; k++) {
+        for (int k = 0; k < 3; k++) {
             const int e = lane + 64 * k;
-            if (e < kO3R * 12) {
-                const int r = e / 12, c = e - r * 12;
-                raw[r * kO3RawS + c] = v[k];
+            if (e < kO3R * 3) {
+                const int r = e / 3, part = e - 3 * r;
+                uint32_t* d = raw + r * kO3RawS + 4 * part;
+                d[0] = v[k].x;
+                d[1] = v[k].y;
+                d[2] = v[k].z;
+                d[3] = v[k].w;
             }
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    ORB_MARK();
     const uint8_t* rawb = reinterpret_cast<const uint8_t*>(raw);
 
     // ---- orientation (IC_Angle, ORBextractor.cc:75-102) on the raw centre 31x31
     int m01 = 0, m10 = 0;
     {
         const int cl = lane & 31, half = lane >> 5;
+        const int u = cl - kHalfPatch;
+        const int au = u < 0 ? -u : u;
+        // umax is non-increasing in v: column u is inside the disc for |v| < nv
+        int nv = 0;
+#pragma unroll
+        for (int v = 0; v <= kHalfPatch; v++) nv += (int)(au <= __builtin_amdgcn_readlane(um, v));
         if (cl < 2 * kHalfPatch + 1) {
-            const int u = cl - kHalfPatch;
-            const int au = u < 0 ? -u : u;
             const uint8_t* colp = rawb + 21 * (4 * kO3RawS) + sh + 21 + u;
             int s0 = 0, s1 = 0;
             if (half == 0) {
 #pragma unroll
                 for (int v = -kHalfPatch; v <= 0; v++) {
-                    const int val = colp[v * (4 * kO3RawS)] & -(int)(au <= P.umax[-v]);
+                    const int val = colp[v * (4 * kO3RawS)] & -(int)(-v < nv);
                     s0 += val;
                     s1 += v * val;
                 }
             } else {
 #pragma unroll
                 for (int v = 1; v <= kHalfPatch; v++) {
-                    const int val = colp[v * (4 * kO3RawS)] & -(int)(au <= P.umax[v]);
+                    const int val = colp[v * (4 * kO3RawS)] & -(int)(v < nv);
                     s0 += val;
                     s1 += v * val;
                 }
@@ -1240,12 +1275,10 @@ __global__ void __launch_bounds__(256) k_orb3(Bufs b) {
             m01 = s1;
         }
     }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        m10 += __shfl_xor(m10, o, 64);
-        m01 += __shfl_xor(m01, o, 64);
-    }
+    m10 = wave_sum_dpp(m10);
+    m01 = wave_sum_dpp(m01);
     const float angle = cv_fast_atan2((float)m01, (float)m10);
+    ORB_MARK();
 
     // ---- horizontal pass: 22 row pairs x 10 groups of 4 output columns; output column c
     // needs staged bytes sh+c .. sh+c+6 (v_alignbyte by the runtime shift, two v_dot4 per
@@ -1276,6 +1309,7 @@ __global__ void __launch_bounds__(256) k_orb3(Bufs b) {
             make_uint4(h0[0] | (h1[0] << 16), h0[1] | (h1[1] << 16), h0[2] | (h1[2] << 16), h0[3] | (h1[3] << 16));
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    ORB_MARK();
     // ---- vertical pass: lane -> 8 columns (g) x 4 output rows 4rb..4rb+3 (rb); 5 x 10 = 50
     // lanes.  Output row y sums hs rows y..y+6: for even y the pairs y/2 .. y/2+3 with taps
     // (k0,k1)(k2,k3)(k4,k5)(k6,0), for odd y the pairs (y-1)/2 .. with (0,k0)(k1,k2)(k3,k4)(k5,k6).
@@ -1326,12 +1360,14 @@ __global__ void __launch_bounds__(256) k_orb3(Bufs b) {
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    ORB_MARK();
 
     // ---- descriptor (computeOrbDescriptor, ORBextractor.cc:106-145)
     const float factor_pi = (float)(3.14159265358979323846 / 180.f);
     float sn, cs;
     glibc_sincosf(angle * factor_pi, &sn, &cs);
     const float a = cs, bb = sn;
+    ORB_MARK();
     const uint8_t* center = bl + 18 * kO3BlS + 18;
     int t0[4], t1[4];
 #pragma unroll
@@ -1360,6 +1396,12 @@ __global__ void __launch_bounds__(256) k_orb3(Bufs b) {
         kp.class_id = -1;
         b.out_kps[(size_t)f * b.cap + oi] = kp;
     }
+#ifdef SLAMHOT_ORB_TRACE
+    ORB_MARK();
+    if (otrace)
+        printf("ORB slot=%d l=%d stage %lld ic %lld horiz %lld vert %lld sincos %lld desc %lld\n", slot, l, otr[1] - otr[0],
+               otr[2] - otr[1], otr[3] - otr[2], otr[4] - otr[3], otr[5] - otr[4], otr[6] - otr[5]);
+#endif
 }
 
 }  // namespace slamhot
