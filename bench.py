@@ -546,6 +546,9 @@ def lba_leg(args, rank, world, local_rank, dist, device):
     S.solve(windows[: min(4, nwin)])  # warm-up
     single = S.solve(pool[0])
     dev1, plan1, _ = S.last_stats()
+    # accuracy: ATE of the solved KeyFrame centres against the windows' ground truth
+    ate_dev = [window_ate(w, r["kf_Tcw"]) for w, r in zip(pool, S.solve(pool))]
+    ate_init = [window_ate(w, w["kf_Tcw"]) for w in pool]
     it1 = single["iterations"][0] + single["iterations"][1]
     # `lba_inflight` solver handles driven from host threads (the C call releases the GIL), each
     # on its own window set: one call's host planning overlaps another's device LM loop.  The
@@ -601,17 +604,25 @@ def lba_leg(args, rank, world, local_rank, dist, device):
         "host_plan_ms_per_call": round(plan_ms / args.lba_calls, 3),
         "single_window": {"lm_iterations": it1, "device_ms": round(dev1, 3),
                           "ms_per_lm_iteration": round(dev1 / max(it1, 1), 4)},
+        "ate": {"metric": "ATE RMSE of the window's KeyFrame centres vs ground truth after LBA "
+                          "(SE3 alignment, slamhot.ate = evaluate_ate_scale.py align)",
+                "unit": "m", "windows": len(pool),
+                "initial": round(float(np.mean(ate_init)), 7), "device": round(float(np.mean(ate_dev)), 7)},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, str(ROOT / "tests"))
         import oracle_bind as ob
-        reps, cpu_iters = 0, 0
+        reps, cpu_iters, ate_cpu = 0, 0, []
         t0 = time.perf_counter()
         while time.perf_counter() - t0 < 3.0 and reps < len(pool):
             r = ob.lba_solve(pool[reps])
             cpu_iters += r["iterations"][0] + r["iterations"][1]
+            ate_cpu.append(window_ate(pool[reps], r["kf_Tcw"]))
             reps += 1
         dt = time.perf_counter() - t0
+        # matched accuracy: the oracle (restated reference solver) on the same windows
+        out["ate"]["oracle_same_windows"] = round(float(np.mean(ate_cpu)), 7)
+        out["ate"]["device_same_windows"] = round(float(np.mean(ate_dev[:reps])), 7)
         out["cpu_baseline"] = {
             "value": round(cpu_iters / dt, 2), "unit": "LM iterations/s", "cores": 1, "kind": "port",
             "sample": f"{reps} config-4 windows, one at a time on one core; oracle/lba_oracle.cpp "
@@ -620,6 +631,18 @@ def lba_leg(args, rank, world, local_rank, dist, device):
     for sv in solvers:
         sv.close()
     return out
+
+
+def window_ate(w, kf_Tcw):
+    """RMSE (m) of KeyFrame camera centres C = -R^T t against the window's ground truth after
+    the SE3 alignment of evaluate_ate_scale.py (slamhot.ate.align)."""
+    from slamhot import ate
+    T = np.asarray(kf_Tcw, np.float64).reshape(-1, 4, 4)
+    est = -np.einsum("kji,kj->ki", T[:, :3, :3], T[:, :3, 3])
+    G = np.asarray(w["gt_T"], np.float64)
+    gt = -np.einsum("kji,kj->ki", G[:, :3, :3], G[:, :3, 3])
+    _, _, _, _, err, _ = ate.align(est.T, gt.T)
+    return float(np.sqrt(np.mean(err * err)))
 
 
 def cpu_baseline(args, W, H):

@@ -50,3 +50,16 @@ def test_read_file_list_and_known_answer(tmp_path):
     assert s == pytest.approx(0.4, rel=1e-12)       # aligns est onto gt: 1 / 2.5
     assert rmse_sim3 == pytest.approx(0.0, abs=1e-9)
     assert rmse > 0.1                                 # SE3-only alignment cannot absorb the scale
+
+
+def test_window_ate_bench_helper():
+    """bench.py's LBA accuracy report: camera-centre ATE is ~0 for the ground truth itself
+    and the restated reference LBA brings a perturbed config-4 window well below its start."""
+    import bench
+    import oracle_bind as ob
+    from slamhot import synth
+    w = synth.lba_window(1)
+    assert bench.window_ate(w, w["gt_T"].reshape(-1, 16)) < 1e-12
+    a0 = bench.window_ate(w, w["kf_Tcw"])
+    a1 = bench.window_ate(w, ob.lba_solve(w)["kf_Tcw"])
+    assert 0.01 < a0 < 0.05 and a1 < 0.5 * a0
