@@ -1594,8 +1594,10 @@ static slam_status ensure_plan(slam_extractor* ex, int W, int H) {
     ex->plan = P;
     ex->have_plan = true;
     // k_octree keeps a level's keys in LDS behind its node arrays when they fit (else in
-    // the per-frame global scratch).  Level 0 (by far the most FAST candidates, one wave per
-    // frame) gets up to 56 KB; the other levels share a launch sized for ~5 waves per CU.
+    // the per-frame global scratch, L2-resident).  The octree is latency-bound and runs
+    // beside other batches' FAST / orb, so its LDS is what it takes from them: level 0 (one
+    // wave per frame, ~4k candidates at VGA) keeps only its nodes in LDS and its keys in L2
+    // (slower alone, +7% for the pipeline); the other levels share a launch at 20 KB / wave.
     const size_t lds_max = 160 * 1024;
     int max_cells = 1;
     for (int l = 0; l < P.nlevels; l++) max_cells = std::max(max_cells, P.lv[l].cell_end - P.lv[l].cell_begin);
@@ -1603,7 +1605,7 @@ static slam_status ensure_plan(slam_extractor* ex, int W, int H) {
     const size_t node_bytes = octree_lds_bytes(P.max_nodes, 0, max_cells);
     if (node_bytes + 6 * 256 + 64 > lds_max) return SLAM_EINVAL;
     auto keycap_for = [&](size_t budget) {
-        budget = std::min(lds_max, std::max(budget, node_bytes + 6 * 1024 + 64));
+        budget = std::min(lds_max, std::max(budget, node_bytes + 6 * 256 + 64));
         return (int)std::min<size_t>(16384, (budget - node_bytes - 64) / 6);
     };
     size_t lds_attr = 0;
@@ -1614,7 +1616,7 @@ static slam_status ensure_plan(slam_extractor* ex, int W, int H) {
         slam_extractor::OctGroup& G = ex->oct[ex->n_oct++];
         G.l0 = l0;
         G.nl = nl;
-        G.keycap = keycap_for(g == 0 ? 56 * 1024 : 32 * 1024);
+        G.keycap = keycap_for(g == 0 ? 0 : 20 * 1024);
         G.lds = octree_lds_bytes(P.max_nodes, G.keycap, max_cells);
         lds_attr = std::max(lds_attr, G.lds);
     }
