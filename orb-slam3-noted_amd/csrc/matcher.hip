@@ -43,6 +43,23 @@ __device__ __forceinline__ int hamming32(const uint4 a0, const uint4 a1, const u
            __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
 }
 
+// min over a DPP row of 16 lanes (quad_perm xor 1 / 2, half-row and row mirrors), in every
+// lane of the row; VALU-speed, unlike a __shfl_xor butterfly (dependent ds_bpermute trips)
+__device__ __forceinline__ uint32_t row16_min_u32(uint32_t x) {
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false));
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false));
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xF, 0xF, false));
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x140, 0xF, 0xF, false));
+    return x;
+}
+
+// min over the whole (fully active) wave: row minima, then the four rows by v_readlane
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
+    x = row16_min_u32(x);
+    return min(min((uint32_t)__builtin_amdgcn_readlane((int)x, 0), (uint32_t)__builtin_amdgcn_readlane((int)x, 16)),
+               min((uint32_t)__builtin_amdgcn_readlane((int)x, 32), (uint32_t)__builtin_amdgcn_readlane((int)x, 48)));
+}
+
 __global__ void __launch_bounds__(256) k_vocab_transform(DevVocab V, int n, const uint8_t* desc,
                                                          int desc_stride, int levelsup,
                                                          int32_t* word_id, double* weight,
@@ -69,9 +86,7 @@ __global__ void __launch_bounds__(256) k_vocab_transform(DevVocab V, int n, cons
                 const uint4* d = reinterpret_cast<const uint4*>(V.desc + (size_t)id * 32);
                 key = ((uint32_t)hamming32(f0, f1, d[0], d[1]) << 20) | (uint32_t)(c - c0);
             }
-#pragma unroll
-            for (int o = 1; o < 16; o <<= 1) key = min(key, (uint32_t)__shfl_xor((int)key, o, 16));
-            bestkey = min(bestkey, key);
+            bestkey = min(bestkey, row16_min_u32(key));  // the 16-lane group is one DPP row
         }
         if (bestkey == 0xFFFFFFFFu) break;  // malformed tree (inner node without children)
         final_id = V.child_idx[c0 + (int)(bestkey & 0xFFFFF)];
@@ -117,7 +132,7 @@ __device__ __forceinline__ int rot_bin(float a, float b) {
     return bin;
 }
 
-__global__ void __launch_bounds__(256) k_bow_match(const DevBowPair* pairs, float nnratio,
+__global__ void __launch_bounds__(512) k_bow_match(const DevBowPair* pairs, float nnratio,
                                                    int check_ori, int strict) {
     __shared__ int16_t matchA[kBowCap];   // B index matched by A feature, -1 none
     __shared__ int8_t binA[kBowCap];
@@ -189,16 +204,14 @@ __global__ void __launch_bounds__(256) k_bow_match(const DevBowPair* pairs, floa
                 const uint32_t key = bok[k] ? (((uint32_t)dist[k] << 16) | (uint32_t)(64 * k + lane)) : 0xFFFFFFFFu;
                 bestkey = min(bestkey, key);
             }
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) bestkey = min(bestkey, (uint32_t)__shfl_xor((int)bestkey, o, 64));
+            bestkey = wave_min_u32(bestkey);
             const int best1 = bestkey == 0xFFFFFFFFu ? 256 : (int)(bestkey >> 16);
             const int bpos = (int)(bestkey & 0xFFFF);
             int sec = 256;
 #pragma unroll
             for (int k = 0; k < kBowNodeChunks; k++)
                 if (bok[k] && (64 * k + lane) != bpos) sec = min(sec, dist[k]);
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) sec = min(sec, __shfl_xor(sec, o, 64));
+            sec = (int)wave_min_u32((uint32_t)sec);
             const bool pass = (strict ? best1 < 50 : best1 <= 50) && ((float)best1 < nnratio * (float)sec);
             if (pass) {
                 // the owner lane marks its candidate taken and records the match
@@ -712,7 +725,7 @@ extern "C" slam_status slamhot_search_by_bow(slam_matcher* m, const slam_bow_sid
     pr.b2a = pr.a2b + A->n;
     pr.nmatches = pr.b2a + B->n;
     SLAM_HIP_TRY(hipMemcpyAsync(m->d_pair.p, &pr, sizeof(pr), hipMemcpyHostToDevice, m->stream));
-    hipLaunchKernelGGL(k_bow_match, dim3(1), dim3(256), 0, m->stream, m->d_pair.as<DevBowPair>(), nnratio,
+    hipLaunchKernelGGL(k_bow_match, dim3(1), dim3(512), 0, m->stream, m->d_pair.as<DevBowPair>(), nnratio,
                        check_ori, strict);
     SLAM_HIP_TRY(hipGetLastError());
     std::vector<int32_t> out((size_t)A->n + B->n + 1);
@@ -762,7 +775,7 @@ extern "C" slam_status slamhot_bow_match_batch_device(slam_matcher* m, slam_voca
                        m->b_fv_id.as<uint32_t>(), m->b_fv_off.as<int32_t>(), m->b_fv_feat.as<uint32_t>(),
                        m->b_fv_n.as<int32_t>(), (int32_t*)d_a2b, (int32_t*)d_b2a, (int32_t*)d_nmatches,
                        m->b_devpairs.as<DevBowPair>(), m->b_status.as<int>());
-    hipLaunchKernelGGL(k_bow_match, dim3(npairs), dim3(256), 0, s, m->b_devpairs.as<DevBowPair>(), nnratio,
+    hipLaunchKernelGGL(k_bow_match, dim3(npairs), dim3(512), 0, s, m->b_devpairs.as<DevBowPair>(), nnratio,
                        check_ori, strict);
     SLAM_HIP_TRY(hipGetLastError());
     return SLAM_OK;
