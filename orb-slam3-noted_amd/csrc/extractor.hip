@@ -440,20 +440,20 @@ __device__ __forceinline__ bool fast_pairs8(const uint8_t* c, int stride, int t)
 // ---------------------------------------------------------------------------------------
 // k_fast_wave: one WAVE per cell whose tested region is <= 64 columns wide (all cells of
 // the standard geometries).  Three order-preserving, wave-compacted passes over the cell:
-//   A  compass pre-test on every tested pixel (necessary for a 9-arc at the lower
-//      threshold: it covers one of each opposite pair 0/8 and 4/12)  -> list of survivors
-//   B  exact measure M (fast_M) on the survivors; M > tlow goes to a zero-padded M map and
-//      stays in the (in-place) list
-//   C  cell-local 3x3 NMS at both thresholds on the remaining corners (one ballot each)
-// Lists keep row-major order, so the survivors are emitted in cv::FAST's order.  The cell
-// keeps the iniThFAST result unless it is empty (ORBextractor.cc:808-841).
+//   A  compass pre-test on every tested pixel (necessary for a 9-arc at threshold t: it
+//      covers one of each opposite pair 0/8 and 4/12)  -> list of survivors
+//   B1 the eight-pair test, B exact measure M (fast_M) on the survivors; M > t goes to a
+//      zero-padded M map and stays in the (in-place) list
+//   C  cell-local 3x3 NMS at t on the remaining corners
+// t = iniThFAST, then minThFAST only for cells left empty (ORBextractor.cc:808-841).  Lists
+// keep row-major order, so the survivors are emitted in cv::FAST's order.
 // LDS per wave (host-sized to the widest cell, VGA: 6.5 KB -> 6 workgroups per CU, with
-// <= 80 VGPRs): ROI ch x rs (keep masks alias it after pass B) | M map (th+2) x ms | list.
+// <= 80 VGPRs): ROI ch x rs | M map (th+2) x ms | list.
 // ---------------------------------------------------------------------------------------
 constexpr int kRoiStride = 80, kRoiRows = 80;  // widest / tallest cell the wave kernel stages
 
 struct FastWaveLds {
-    int roi, map, lst, kmask, total;  // byte offsets inside one wave's region, total size
+    int roi, map, lst, total;  // byte offsets inside one wave's region, total size
     int rs, ms;                       // ROI / M-map row strides (bytes), sized to the geometry
 };
 
@@ -475,10 +475,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))
     uint8_t* roi = base_ptr + lay.roi;
     uint8_t* map = base_ptr + lay.map;
     uint16_t* lst = reinterpret_cast<uint16_t*>(base_ptr + lay.lst);
-    uint64_t* kmask = reinterpret_cast<uint64_t*>(base_ptr + lay.kmask);
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     const int ti = min(max(P.ini_th, 0), 255), tm = min(max(P.min_th, 0), 255);
-    const int tlow = min(ti, tm);
 
     // stage the ROI with independent 32-bit loads (row start aligned down to 4 bytes; the
     // ROI origin inside LDS is then `sh` bytes into each row), zero the M map.  Lane =
@@ -519,142 +517,132 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 
-    // pass A, four pixels per lane in packed u16 pairs (even / odd bytes of an LDS dword).
-    // Lane = (row, dword group) over the dwords covering the tested columns; the compass
-    // test per pixel is  min(p0,p8), min(p4,p12) < v - t  (dark) or  max(..) > v + t
-    // (bright), i.e. saturating (v - t - max of the mins) | (min of the maxes - v - t) != 0.
-    // Four ballots (one per byte) + mbcnt give row-major compaction.
-    int na = 0;
-    {
-        const int g0 = (sh + 3) >> 2, g1 = (sh + cw - 4) >> 2;
-        const int ng = g1 - g0 + 1;  // <= 17
-        const int rpi = 64 / ng;     // tested rows per iteration
-        const int ar = lane / ng, gd = g0 + (lane - ar * ng);
-        uint32_t cmask = 0;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int x = 4 * gd + k - sh;  // ROI column of byte k
-            if (x >= 3 && x <= cw - 4) cmask |= 0xFFu << (8 * k);
+    // The cell keeps the iniThFAST result unless it is empty, then FAST runs again at
+    // minThFAST (ORBextractor.cc:808-841).  Passes A / B1 / B run at the threshold of the
+    // current attempt (far fewer survivors at iniTh = 20 than at minTh = 7); only empty cells
+    // pay for the second attempt.  M is exact, so the map entries of the first attempt stay
+    // valid for the second (NMS reads neighbours as M > t ? M - 1 : 0).
+    auto keep_at = [&](int e, int t) -> bool {
+        const int code = lst[e];
+        const int r = code >> 6, c = code & 63;
+        const int MS = lay.ms;
+        const uint8_t* q = map + (r + 1) * MS + c + 1;
+        const int M = q[0];
+        auto sc = [&](int x) { return x > t ? x - 1 : 0; };
+        int mx = max(max(sc(q[-MS - 1]), sc(q[-MS])), max(sc(q[-MS + 1]), sc(q[-1])));
+        mx = max(mx, max(max(sc(q[1]), sc(q[MS - 1])), max(sc(q[MS]), sc(q[MS + 1]))));
+        return (M > t) & (M - 1 > mx);
+    };
+    for (int attempt = 0; attempt < 2; attempt++) {
+        const int t = attempt == 0 ? ti : tm;
+        // pass A, four pixels per lane in packed u16 pairs (even / odd bytes of an LDS dword).
+        // Lane = (row, dword group) over the dwords covering the tested columns; the compass
+        // test per pixel is  min(p0,p8), min(p4,p12) < v - t  (dark) or  max(..) > v + t
+        // (bright), i.e. saturating (v - t - max of the mins) | (min of the maxes - v - t) != 0.
+        // Four ballots (one per byte) + mbcnt give row-major compaction.
+        int na = 0;
+        {
+            const int g0 = (sh + 3) >> 2, g1 = (sh + cw - 4) >> 2;
+            const int ng = g1 - g0 + 1;  // <= 17
+            const int rpi = 64 / ng;     // tested rows per iteration
+            const int ar = lane / ng, gd = g0 + (lane - ar * ng);
+            uint32_t cmask = 0;
+    #pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int x = 4 * gd + k - sh;  // ROI column of byte k
+                if (x >= 3 && x <= cw - 4) cmask |= 0xFFu << (8 * k);
+            }
+            if (ar >= rpi) cmask = 0;
+            const int code0 = (4 * gd - sh - 3) + ar * 64;  // code of byte 0 in row 0
+            const us2 T = {(unsigned short)t, (unsigned short)t};
+            const int RS = lay.rs >> 2;
+            for (int rt = 0; rt < th; rt += rpi) {
+                const int r = rt + ar;
+                const uint32_t m = r < th ? cmask : 0u;
+                const uint32_t* row = roi32 + (min(r, th - 1) + 3) * RS + gd;
+                const uint32_t W0 = row[-1], W1 = row[0], W2 = row[1], U = row[-3 * RS], D = row[3 * RS];
+                auto set = [&](uint32_t v, uint32_t p0, uint32_t p8, uint32_t p4, uint32_t p12) -> uint32_t {
+                    const us2 V = as_us2(v), a = as_us2(p0), bq = as_us2(p8), c = as_us2(p4), d = as_us2(p12);
+                    const us2 L = __builtin_elementwise_max(__builtin_elementwise_min(a, bq), __builtin_elementwise_min(c, d));
+                    const us2 H = __builtin_elementwise_min(__builtin_elementwise_max(a, bq), __builtin_elementwise_max(c, d));
+                    return as_u32(__builtin_elementwise_sub_sat(V, L + T) | __builtin_elementwise_sub_sat(H, V + T));
+                };
+                const uint32_t fe = set(__builtin_amdgcn_perm(0u, W1, 0x0c020c00u), __builtin_amdgcn_perm(0u, D, 0x0c020c00u),
+                                        __builtin_amdgcn_perm(0u, U, 0x0c020c00u), __builtin_amdgcn_perm(W2, W1, 0x0c050c03u),
+                                        __builtin_amdgcn_perm(W1, W0, 0x0c030c01u));
+                const uint32_t fo = set(__builtin_amdgcn_perm(0u, W1, 0x0c030c01u), __builtin_amdgcn_perm(0u, D, 0x0c030c01u),
+                                        __builtin_amdgcn_perm(0u, U, 0x0c030c01u), __builtin_amdgcn_perm(W2, W1, 0x0c060c04u),
+                                        __builtin_amdgcn_perm(W1, W0, 0x0c040c02u));
+                const uint32_t F = (fe | (fo << 8)) & m;  // byte k != 0 <=> pixel k survives
+                const bool f0 = (F & 0xFFu) != 0, f1 = (F & 0xFF00u) != 0, f2 = (F & 0xFF0000u) != 0, f3 = (F >> 24) != 0;
+                const uint64_t b0 = __ballot(f0), b1 = __ballot(f1), b2 = __ballot(f2), b3 = __ballot(f3);
+                int pos = mbcnt64(b3, mbcnt64(b2, mbcnt64(b1, mbcnt64(b0, na))));
+                const int code = code0 + rt * 64;
+                if (f0) lst[pos++] = (uint16_t)code;
+                if (f1) lst[pos++] = (uint16_t)(code + 1);
+                if (f2) lst[pos++] = (uint16_t)(code + 2);
+                if (f3) lst[pos] = (uint16_t)(code + 3);
+                na += __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
+            }
         }
-        if (ar >= rpi) cmask = 0;
-        const int code0 = (4 * gd - sh - 3) + ar * 64;  // code of byte 0 in row 0
-        const us2 T = {(unsigned short)tlow, (unsigned short)tlow};
-        const int RS = lay.rs >> 2;
-        for (int rt = 0; rt < th; rt += rpi) {
-            const int r = rt + ar;
-            const uint32_t m = r < th ? cmask : 0u;
-            const uint32_t* row = roi32 + (min(r, th - 1) + 3) * RS + gd;
-            const uint32_t W0 = row[-1], W1 = row[0], W2 = row[1], U = row[-3 * RS], D = row[3 * RS];
-            auto set = [&](uint32_t v, uint32_t p0, uint32_t p8, uint32_t p4, uint32_t p12) -> uint32_t {
-                const us2 V = as_us2(v), a = as_us2(p0), bq = as_us2(p8), c = as_us2(p4), d = as_us2(p12);
-                const us2 L = __builtin_elementwise_max(__builtin_elementwise_min(a, bq), __builtin_elementwise_min(c, d));
-                const us2 H = __builtin_elementwise_min(__builtin_elementwise_max(a, bq), __builtin_elementwise_max(c, d));
-                return as_u32(__builtin_elementwise_sub_sat(V, L + T) | __builtin_elementwise_sub_sat(H, V + T));
-            };
-            const uint32_t fe = set(__builtin_amdgcn_perm(0u, W1, 0x0c020c00u), __builtin_amdgcn_perm(0u, D, 0x0c020c00u),
-                                    __builtin_amdgcn_perm(0u, U, 0x0c020c00u), __builtin_amdgcn_perm(W2, W1, 0x0c050c03u),
-                                    __builtin_amdgcn_perm(W1, W0, 0x0c030c01u));
-            const uint32_t fo = set(__builtin_amdgcn_perm(0u, W1, 0x0c030c01u), __builtin_amdgcn_perm(0u, D, 0x0c030c01u),
-                                    __builtin_amdgcn_perm(0u, U, 0x0c030c01u), __builtin_amdgcn_perm(W2, W1, 0x0c060c04u),
-                                    __builtin_amdgcn_perm(W1, W0, 0x0c040c02u));
-            const uint32_t F = (fe | (fo << 8)) & m;  // byte k != 0 <=> pixel k survives
-            const bool f0 = (F & 0xFFu) != 0, f1 = (F & 0xFF00u) != 0, f2 = (F & 0xFF0000u) != 0, f3 = (F >> 24) != 0;
-            const uint64_t b0 = __ballot(f0), b1 = __ballot(f1), b2 = __ballot(f2), b3 = __ballot(f3);
-            int pos = mbcnt64(b3, mbcnt64(b2, mbcnt64(b1, mbcnt64(b0, na))));
-            const int code = code0 + rt * 64;
-            if (f0) lst[pos++] = (uint16_t)code;
-            if (f1) lst[pos++] = (uint16_t)(code + 1);
-            if (f2) lst[pos++] = (uint16_t)(code + 2);
-            if (f3) lst[pos] = (uint16_t)(code + 3);
-            na += __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 
-    // pass B1: the eight-pair pre-test on the compass survivors (in-place compaction)
-    {
-        int n1 = 0;
+        // pass B1: the eight-pair pre-test on the compass survivors (in-place compaction)
+        {
+            int n1 = 0;
+            for (int j = 0; j < na; j += 64) {
+                const int e = j + lane;
+                const bool valid = e < na;
+                const int code = valid ? lst[e] : 0;
+                const int r = code >> 6, c = code & 63;
+                const bool keep = valid && fast_pairs8(roi + (r + 3) * lay.rs + c + 3, lay.rs, t);
+                const uint64_t m = __ballot(keep);
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                if (keep) lst[n1 + __popcll(m & lt)] = (uint16_t)code;
+                n1 += __popcll(m);
+            }
+            na = n1;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+
+        // pass B (compacts the list in place: writes never pass the chunk being read)
+        int nb = 0;
         for (int j = 0; j < na; j += 64) {
             const int e = j + lane;
             const bool valid = e < na;
             const int code = valid ? lst[e] : 0;
             const int r = code >> 6, c = code & 63;
-            const bool keep = valid && fast_pairs8(roi + (r + 3) * lay.rs + c + 3, lay.rs, tlow);
-            const uint64_t m = __ballot(keep);
+            int M = 0;
+            if (valid) M = fast_M(roi + (r + 3) * lay.rs + c + 3, lay.rs);
+            const bool corner = M > t;
+            if (corner) map[(r + 1) * lay.ms + c + 1] = (uint8_t)M;
+            const uint64_t m = __ballot(corner);
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            if (keep) lst[n1 + __popcll(m & lt)] = (uint16_t)code;
-            n1 += __popcll(m);
+            if (corner) lst[nb + __popcll(m & lt)] = (uint16_t)code;
+            nb += __popcll(m);
         }
-        na = n1;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-
-    // pass B (compacts the list in place: writes never pass the chunk being read)
-    int nb = 0;
-    for (int j = 0; j < na; j += 64) {
-        const int e = j + lane;
-        const bool valid = e < na;
-        const int code = valid ? lst[e] : 0;
-        const int r = code >> 6, c = code & 63;
-        int M = 0;
-        if (valid) M = fast_M(roi + (r + 3) * lay.rs + c + 3, lay.rs);
-        const bool corner = M > tlow;
-        if (corner) map[(r + 1) * lay.ms + c + 1] = (uint8_t)M;
-        const uint64_t m = __ballot(corner);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        if (corner) lst[nb + __popcll(m & lt)] = (uint16_t)code;
-        nb += __popcll(m);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 
-    // pass C
-    int cnt_i = 0;
-    for (int j = 0; j < nb; j += 64) {
-        const int e = j + lane;
-        const bool valid = e < nb;
-        bool ki = false, km = false;
-        if (valid) {
-            const int code = lst[e];
-            const int r = code >> 6, c = code & 63;
-            const int MS = lay.ms;
-            const uint8_t* q = map + (r + 1) * MS + c + 1;
-            const int M = q[0];
-            const int n0 = q[-MS - 1], n1 = q[-MS], n2 = q[-MS + 1];
-            const int n3 = q[-1], n4 = q[1];
-            const int n5 = q[MS - 1], n6 = q[MS], n7 = q[MS + 1];
-            auto keep = [&](int t) -> bool {
-                auto sc = [&](int x) { return x > t ? x - 1 : 0; };
-                const int sc0 = M - 1;
-                int mx = max(max(sc(n0), sc(n1)), max(sc(n2), sc(n3)));
-                mx = max(mx, max(max(sc(n4), sc(n5)), max(sc(n6), sc(n7))));
-                return (M > t) & (sc0 > mx);
-            };
-            ki = keep(ti);
-            km = keep(tm);
+        // pass C: cell-local 3x3 NMS at t; count, then emit in list (row-major) order
+        int cnt = 0;
+        for (int j = 0; j < nb; j += 64) cnt += __popcll(__ballot(j + lane < nb && keep_at(j + lane, t)));
+        if (cnt == 0 && attempt == 0 && tm != ti) continue;
+        uint32_t* slot = b.cell_keys + ((size_t)f * P.ncells + cd.slot) * P.slot_cap;
+        int base = 0;
+        for (int j = 0; j < nb; j += 64) {
+            const bool k = j + lane < nb && keep_at(j + lane, t);
+            const uint64_t m = __ballot(k);
+            if (k) {
+                const int code = lst[j + lane];
+                const int r = code >> 6, c = code & 63;
+                const int M = map[(r + 1) * lay.ms + c + 1];
+                slot[base + __popcll(m & lt)] = pack_kp(cd.iniX + 3 + c, cd.iniY + 3 + r, M - 1);
+            }
+            base += __popcll(m);
         }
-        const uint64_t bi = __ballot(ki), bm = __ballot(km);
-        if (lane == 0) {
-            kmask[2 * (j >> 6)] = bi;
-            kmask[2 * (j >> 6) + 1] = bm;
-        }
-        cnt_i += __popcll(bi);
+        if (lane == 0) b.cell_cnt[(size_t)f * P.ncells + cd.slot] = base;
+        return;
     }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-
-    const int sel = cnt_i ? 0 : 1;
-    uint32_t* slot = b.cell_keys + ((size_t)f * P.ncells + cd.slot) * P.slot_cap;
-    int base = 0;
-    for (int j = 0; j < nb; j += 64) {
-        const uint64_t m = kmask[2 * (j >> 6) + sel];
-        if ((m >> lane) & 1ull) {
-            const int code = lst[j + lane];
-            const int r = code >> 6, c = code & 63;
-            const int M = map[(r + 1) * lay.ms + c + 1];
-            slot[base + __popcll(m & lt)] = pack_kp(cd.iniX + 3 + c, cd.iniY + 3 + r, M - 1);
-        }
-        base += __popcll(m);
-    }
-    if (lane == 0) b.cell_cnt[(size_t)f * P.ncells + cd.slot] = base;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1574,9 +1562,6 @@ static slam_status ensure_plan(slam_extractor* ex, int W, int H) {
         lay.map = r16(ch_max * lay.rs);
         lay.lst = lay.map + r16((th_max + 2) * lay.ms);
         lay.total = lay.lst + r16(std::max(1, tw_max * th_max) * 2);
-        // the keep masks are written after the last ROI read (pass C): they alias the ROI
-        lay.kmask = lay.roi;
-        if (((std::max(1, tw_max * th_max) + 63) / 64) * 16 > lay.map) return SLAM_EINVAL;
         ex->fw_lay = lay;
         if (4 * lay.total > 160 * 1024) return SLAM_EINVAL;
         SLAM_HIP_TRY(hipFuncSetAttribute((const void*)k_fast_wave, hipFuncAttributeMaxDynamicSharedMemorySize,

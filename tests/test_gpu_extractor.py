@@ -98,3 +98,17 @@ def test_flat_and_noise_images(gpu_extractor_factory):
         kg, dg, mg = ex(img)
         ko, do, mo = ob.extract(img)
         _compare(kg, dg, mg, ko, do, mo)
+
+
+def test_low_contrast_minth_retry(gpu_extractor_factory):
+    """Low-contrast texture (corners mostly between minThFAST 7 and iniThFAST 20), next to a
+    high-contrast half: most cells of the left half are empty at iniTh and take the minTh
+    attempt (ORBextractor.cc:825-841), the right half does not."""
+    ex = gpu_extractor_factory(nfeatures=1000, max_size=(640, 480))
+    rng = np.random.default_rng(11)
+    img = (128 + rng.integers(-9, 10, (480, 640))).astype(np.uint8)
+    img[:, 320:] = synth.frame(12)[:, 320:]
+    kg, dg, mg = ex(img)
+    ko, do, mo = ob.extract(img)
+    assert len(ko) > 500
+    _compare(kg, dg, mg, ko, do, mo)
