@@ -272,7 +272,8 @@ def match_leg(args, rank, world, local_rank, dist, device):
         pairs_img.append((kfs[i], synth.shifted(kfs[i], dx, dy, a, 40000 + seeds[i])))
     imgs = np.stack([im for i in range(Pn) for im in pairs_img[i % nuniq]])
     F = len(imgs)
-    par, leaf, dn, wn = synth.vocab(10, 6, 0)
+    # the vocabulary is built (or, with ORBvoc.txt, loaded) once and replicated from rank 0
+    par, leaf, dn, wn = sdist.broadcast_arrays(dist, device, synth.vocab(10, 6, 0) if rank == 0 else None)
     voc = slamhot.Vocabulary(par, leaf, dn, wn, k=10, L=6, device=local_rank)
     m = slamhot.ORBmatcher(0.7, True, device=local_rank)
     ex = slamhot.ORBextractor(nfeatures=args.nfeatures, device=local_rank, max_size=(W, H), max_batch=F)

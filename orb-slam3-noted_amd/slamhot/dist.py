@@ -1,7 +1,8 @@
 """Multi-GPU plumbing of the batched path: one process per GPU, independent
 units (frames, BA windows) sharded by rank, no collective on the data path.  The only
 collectives are the timing reduction (max over ranks), the unit count (sum) and an all-gather
-of per-rank parity digests at the end.  Backend-agnostic: "nccl" (RCCL over xGMI) with
+of per-rank parity digests at the end, plus one setup broadcast of the replicated tables (the
+vocabulary) from rank 0.  Backend-agnostic: "nccl" (RCCL over xGMI) with
 device tensors in bench.py, "gloo" with CPU tensors in the tests."""
 from __future__ import annotations
 
@@ -46,3 +47,46 @@ def gather_digests(dist, device, world: int, count: int, dig: int):
     g = [torch.zeros(2, dtype=torch.int64, device=device) for _ in range(world)]
     dist.all_gather(g, torch.tensor([count, dig], dtype=torch.int64, device=device))
     return [(int(x[0].item()), int(x[1].item())) for x in g]
+
+
+def broadcast_arrays(dist, device, arrays):
+    """Rank 0's numpy arrays on every rank (setup only: the vocabulary tree is built or loaded
+    once and replicated).  `arrays` is ignored on ranks > 0.  Shapes and dtypes
+    travel first (one int64 header), then one byte buffer."""
+    import torch
+    if dist is None:
+        return [np.asarray(a) for a in arrays]
+    rank = dist.get_rank()
+    codes = ["u1", "i1", "u2", "i2", "u4", "i4", "u8", "i8", "f4", "f8", "b1"]
+    if rank == 0:
+        arrs = [np.ascontiguousarray(a) for a in arrays]
+        meta = [len(arrs)]
+        for a in arrs:
+            meta += [codes.index(a.dtype.str[1:]), a.ndim] + list(a.shape)
+        hdr = torch.tensor([len(meta)] + meta + [0] * (255 - len(meta)), dtype=torch.int64, device=device)
+    else:
+        hdr = torch.zeros(256, dtype=torch.int64, device=device)
+    dist.broadcast(hdr, src=0)
+    h = hdr.cpu().numpy()
+    meta = list(h[1:1 + int(h[0])])
+    n, pos, specs = int(meta[0]), 1, []
+    for _ in range(n):
+        dt, nd = np.dtype(codes[int(meta[pos])]), int(meta[pos + 1])
+        shape = tuple(int(v) for v in meta[pos + 2:pos + 2 + nd])
+        specs.append((dt, shape))
+        pos += 2 + nd
+    sizes = [int(np.prod(sh)) * dt.itemsize for dt, sh in specs]
+    total = sum(sizes)
+    if rank == 0:
+        buf = torch.from_numpy(np.concatenate([a.view(np.uint8).ravel() for a in arrs]) if total else
+                               np.zeros(0, np.uint8)).to(device)
+    else:
+        buf = torch.zeros(total, dtype=torch.uint8, device=device)
+    if total:
+        dist.broadcast(buf, src=0)
+    raw = buf.cpu().numpy()
+    out, off = [], 0
+    for (dt, sh), nb in zip(specs, sizes):
+        out.append(raw[off:off + nb].view(dt).reshape(sh).copy())
+        off += nb
+    return out

@@ -61,7 +61,9 @@ def _worker(rank, world, port, q):
     _, wunits = sdist.reduce_run(dist, "cpu", elapsed, float(len(widx)))
     kg = sdist.gather_digests(dist, "cpu", world, kcount, kdig)
     lg = sdist.gather_digests(dist, "cpu", world, lit, ldig)
-    q.put((rank, elapsed, el_max, units, wunits, kg, lg))
+    # setup broadcast of the replicated vocabulary tables (bench.py match leg)
+    voc = sdist.broadcast_arrays(dist, "cpu", synth.vocab(4, 3, 7) if rank == 0 else None)
+    q.put((rank, elapsed, el_max, units, wunits, kg, lg, sdist.digest(*voc), [(a.dtype.str, a.shape) for a in voc]))
     dist.destroy_process_group()
 
 
@@ -96,3 +98,7 @@ def test_two_rank_gloo_matches_single_process():
     li, ld = _lba_digest(range(N_WIN))
     assert sum(c for c, _ in lg) == li
     assert np.bitwise_xor.reduce(np.array([d for _, d in lg], np.int64)) == ld
+    ref = synth.vocab(4, 3, 7)
+    for o in out:  # rank 1 received exactly rank 0's tables
+        assert o[7] == sdist.digest(*ref)
+        assert o[8] == [(np.asarray(a).dtype.str, np.asarray(a).shape) for a in ref]
