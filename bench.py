@@ -71,7 +71,7 @@ def main():
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--nfeatures", type=int, default=1000)
-    ap.add_argument("--unique", type=int, default=64, help="distinct synthetic frames per rank")
+    ap.add_argument("--unique", type=int, default=256, help="distinct synthetic frames per rank")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=384)
     ap.add_argument("--lba-windows", type=int, default=64, help="LBA windows per GPU per call (0 = skip)")
