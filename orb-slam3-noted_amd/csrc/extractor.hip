@@ -686,16 +686,19 @@ __device__ __forceinline__ void wave_fence() {
     __builtin_amdgcn_wave_barrier();
 }
 
-// exclusive prefix sum over the wave's 64 lanes; total in *tot
+// exclusive prefix sum over the wave's 64 lanes (all active); total in *tot.  DPP
+// Kogge-Stone inside rows of 16 (row_shr 1/2/4/8, zero-filled), then row_bcast15 / 31
+// carry the row totals into the following rows: VALU-speed steps instead of six dependent
+// ds_bpermute round trips.
 __device__ __forceinline__ int wave_scan_excl(int v, int* tot) {
-    const int lane = threadIdx.x & 63;
     int x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
-    *tot = __shfl(x, 63, 64);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, true);   // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, true);   // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, true);   // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, true);   // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+    *tot = __builtin_amdgcn_readlane(x, 63);
     return x - v;
 }
 
