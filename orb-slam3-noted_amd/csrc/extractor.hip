@@ -723,6 +723,8 @@ __host__ __device__ inline size_t octree_lds_bytes(int maxn, int keycap, int max
     return s;
 }
 
+constexpr int kKU = 8;  // keys per lane in flight in the octree key loops
+
 __global__ void __launch_bounds__(64) k_octree(Bufs b, int level0, int key_lds_cap, int max_cells) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const DevPlan& P = *b.plan;
@@ -824,12 +826,12 @@ __global__ void __launch_bounds__(64) k_octree(Bufs b, int level0, int key_lds_c
     // ---- roots (:541-583): key -> root (int)(x / hX); empty roots erased
     if (lane < L.nIni) best[lane] = 0;
     wave_fence();
-    for (int k0 = lane; k0 < nk; k0 += 4 * 64) {
-        uint32_t key[4];
+    for (int k0 = lane; k0 < nk; k0 += kKU * 64) {
+        uint32_t key[kKU];
 #pragma unroll
-        for (int u = 0; u < 4; u++) key[u] = keys[min(k0 + 64 * u, nk - 1)];
+        for (int u = 0; u < kKU; u++) key[u] = keys[min(k0 + 64 * u, nk - 1)];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < kKU; u++) {
             const int k = k0 + 64 * u;
             const int x = kp_x(key[u]);
             int r = 0;
@@ -856,15 +858,15 @@ __global__ void __launch_bounds__(64) k_octree(Bufs b, int level0, int key_lds_c
         n = __popcll(m);
     }
     wave_fence();
-    for (int k0 = lane; k0 < nk; k0 += 4 * 64) {
-        int nd[4];
+    for (int k0 = lane; k0 < nk; k0 += kKU * 64) {
+        int nd[kKU];
 #pragma unroll
-        for (int u = 0; u < 4; u++) nd[u] = knode[min(k0 + 64 * u, nk - 1)];
-        uint16_t cm[4];
+        for (int u = 0; u < kKU; u++) nd[u] = knode[min(k0 + 64 * u, nk - 1)];
+        uint16_t cm[kKU];
 #pragma unroll
-        for (int u = 0; u < 4; u++) cm[u] = cmap[nd[u]];
+        for (int u = 0; u < kKU; u++) cm[u] = cmap[nd[u]];
 #pragma unroll
-        for (int u = 0; u < 4; u++)
+        for (int u = 0; u < kKU; u++)
             if (k0 + 64 * u < nk) knode[k0 + 64 * u] = cm[u];
     }
     wave_fence();
@@ -885,21 +887,21 @@ __global__ void __launch_bounds__(64) k_octree(Bufs b, int level0, int key_lds_c
         }
         wave_fence();
         // four keys per lane per step: their node loads overlap, then the four atomics
-        for (int k0 = lane; k0 < nk; k0 += 4 * 64) {
-            int nd[4];
-            uint32_t key[4];
+        for (int k0 = lane; k0 < nk; k0 += kKU * 64) {
+            int nd[kKU];
+            uint32_t key[kKU];
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
+            for (int u = 0; u < kKU; u++) {
                 const int k = min(k0 + 64 * u, nk - 1);
                 nd[u] = knode[k];
                 key[u] = keys[k];
             }
-            int c[4];
-            uint32_t xb[4], yb[4];
+            int c[kKU];
+            uint32_t xb[kKU], yb[kKU];
 #pragma unroll
-            for (int u = 0; u < 4; u++) { c[u] = A.cnt[nd[u]]; xb[u] = A.xb[nd[u]]; yb[u] = A.yb[nd[u]]; }
+            for (int u = 0; u < kKU; u++) { c[u] = A.cnt[nd[u]]; xb[u] = A.xb[nd[u]]; yb[u] = A.yb[nd[u]]; }
 #pragma unroll
-            for (int u = 0; u < 4; u++)
+            for (int u = 0; u < kKU; u++)
                 if (k0 + 64 * u < nk && c[u] > 1 && (!careful || nd[u] < tprev))
                     atomicAdd(&ccu[nd[u] * 4 + quadrant_of(key[u], xb[u], yb[u])], 1u);
         }
@@ -1013,24 +1015,24 @@ __global__ void __launch_bounds__(64) k_octree(Bufs b, int level0, int key_lds_c
         const int n_to_expand = wave_sum(nexp_local);
         wave_fence();
         // -- remap keys
-        for (int k0 = lane; k0 < nk; k0 += 4 * 64) {
-            int nd[4];
-            uint32_t key[4];
+        for (int k0 = lane; k0 < nk; k0 += kKU * 64) {
+            int nd[kKU];
+            uint32_t key[kKU];
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
+            for (int u = 0; u < kKU; u++) {
                 const int k = min(k0 + 64 * u, nk - 1);
                 nd[u] = knode[k];
                 key[u] = keys[k];
             }
-            int r[4];
-            uint32_t xb[4], yb[4];
+            int r[kKU];
+            uint32_t xb[kKU], yb[kKU];
 #pragma unroll
-            for (int u = 0; u < 4; u++) { r[u] = rnk[nd[u]]; xb[u] = A.xb[nd[u]]; yb[u] = A.yb[nd[u]]; }
-            uint16_t cm[4];
+            for (int u = 0; u < kKU; u++) { r[u] = rnk[nd[u]]; xb[u] = A.xb[nd[u]]; yb[u] = A.yb[nd[u]]; }
+            uint16_t cm[kKU];
 #pragma unroll
-            for (int u = 0; u < 4; u++) cm[u] = cmap[nd[u] * 4 + (r[u] >= 0 ? quadrant_of(key[u], xb[u], yb[u]) : 0)];
+            for (int u = 0; u < kKU; u++) cm[u] = cmap[nd[u] * 4 + (r[u] >= 0 ? quadrant_of(key[u], xb[u], yb[u]) : 0)];
 #pragma unroll
-            for (int u = 0; u < 4; u++)
+            for (int u = 0; u < kKU; u++)
                 if (k0 + 64 * u < nk) knode[k0 + 64 * u] = cm[u];
         }
         wave_fence();
@@ -1050,17 +1052,17 @@ __global__ void __launch_bounds__(64) k_octree(Bufs b, int level0, int key_lds_c
     // ---- retain the best key of each node (:740-758)
     for (int i = lane; i < n; i += 64) best[i] = 0;
     wave_fence();
-    for (int k0 = lane; k0 < nk; k0 += 4 * 64) {
-        uint32_t key[4];
-        int nd[4];
+    for (int k0 = lane; k0 < nk; k0 += kKU * 64) {
+        uint32_t key[kKU];
+        int nd[kKU];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < kKU; u++) {
             const int k = min(k0 + 64 * u, nk - 1);
             key[u] = keys[k];
             nd[u] = knode[k];
         }
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < kKU; u++) {
             const int k = k0 + 64 * u;
             if (k < nk) atomicMax(&best[nd[u]], ((uint32_t)kp_s(key[u]) << 24) | (uint32_t)(0xFFFFFF - k));
         }
