@@ -454,14 +454,18 @@ typedef struct slam_tri_kf {
     int32_t nlevels;
     const float* scale;           /* mvScaleFactors */
     const float* level_sigma2;    /* mvLevelSigma2 */
+    float Rcw[9], tcw[3];         /* GetRotation_() / GetTranslation_() (Tcw_, KeyFrame.cc:1076-1084) */
+    float Ow[3];                  /* GetCameraCenter_() (Ow_, KeyFrame.cc:1086-1089) */
+    float cam[4];                 /* mpCamera parameters fx, fy, cx, cy (Pinhole::toK_) */
 } slam_tri_kf;
 
-/* One SearchForTriangulation_ call: KeyFrames kfs[kf1], kfs[kf2]. */
+/* One SearchForTriangulation_ call: KeyFrames kfs[kf1], kfs[kf2].  The epipole, R12, t12 and
+ * the F12 that Pinhole::epipolarConstrain_ rebuilds from them on every call are computed on
+ * the device from the two KeyFrames' poses and cameras with the reference binary's arithmetic
+ * (ORBmatcher.cc:1215-1240, Pinhole.cpp:159-181).  The cv::Matx33f F12 argument
+ * of the reference is not read on this (pinhole) path, so it has no field here. */
 typedef struct slam_tri_pair {
     int32_t kf1, kf2;
-    float F12[9];                 /* row-major; LocalMapping::ComputeF12_ (LocalMapping.cc:886-903),
-                                     equal to what Pinhole::epipolarConstrain_ recomputes */
-    float ep[2];                  /* pKF2->mpCamera->project(R2w * Cw1 + t2w) (ORBmatcher.cc:1218-1222) */
     uint8_t only_stereo, coarse, pad[2];
 } slam_tri_pair;
 

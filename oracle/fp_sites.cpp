@@ -1,0 +1,83 @@
+/*
+ * fp_sites.cpp — C exports of oracle/fp_sites.hpp for tests/test_fp_sites.py, which checks them
+ * against C emitted from the reference objects' traced data flow.  TEST INFRASTRUCTURE ONLY.
+ */
+#include <cmath>
+
+#include "fp_sites.hpp"
+
+extern "C" {
+
+int oracle_fp_inv33(const float* a, float* b) { return oracle_fp::inv33(a, b) ? 1 : 0; }
+
+/* SearchForTriangulation_ preamble + the F12 of epipolarConstrain_ (see fp_sites.hpp) */
+void oracle_fp_tri_geometry(const float* R1, const float* t1, const float* Cw1, const float* cam1, const float* R2,
+                            const float* t2, const float* cam2, float* ep, float* R12, float* t12, float* F12) {
+    oracle_fp::tri_geometry(R1, t1, Cw1, cam1, R2, t2, cam2, ep, R12, t12, F12);
+}
+
+/* Pinhole::epipolarConstrain_ for (K1, K2, R12, t12, kp1, kp2, unc): out = {den, dsqr, 3.84 unc};
+ * returns the gate. */
+int oracle_fp_epipolar_vals(const float* cam1, const float* cam2, const float* R12, const float* t12, float x1,
+                            float y1, float x2, float y2, float unc, double* out) {
+    const float K1t[9] = {cam1[0], 0.0f, 0.0f, 0.0f, cam1[1], 0.0f, cam1[2], cam1[3], 1.0f};
+    const float K2[9] = {cam2[0], 0.0f, cam2[2], 0.0f, cam2[1], cam2[3], 0.0f, 0.0f, 1.0f};
+    const float S[9] = {0.0f, -t12[2], t12[1], t12[2], 0.0f, -t12[0], -t12[1], t12[0], 0.0f};
+    float K1ti[9], K2i[9], F[9];
+    oracle_fp::inv33(K1t, K1ti);
+    oracle_fp::inv33(K2, K2i);
+    oracle_fp::mul33(K1ti, S, F);
+    oracle_fp::mul33(F, R12, F);
+    oracle_fp::mul33(F, K2i, F);
+    const float a = std::fma(x1, F[0], y1 * F[3]) + F[6];
+    const float b = std::fma(x1, F[1], y1 * F[4]) + F[7];
+    const float c = std::fma(y1, F[5], x1 * F[2]) + F[8];
+    const float num = std::fma(b, y2, a * x2) + c;
+    const float den = std::fma(a, a, b * b);
+    out[0] = den;
+    out[1] = den == 0.0f ? 0.0 : (double)(num * num / den);
+    out[2] = 3.84 * (double)unc;
+    return oracle_fp::epipolar(F, x1, y1, x2, y2, unc) ? 1 : 0;
+}
+
+/* Frame::isInFrustum's float pieces for one point: out = {Pc0, Pc1, Pc2, Pc_dist, dist, viewCos,
+ * ur} given Rcw|tcw (row-major 3x4), Ow, camera, bf, X, normal. */
+void oracle_fp_frustum_vals(const float* T, const float* Ow, const float* cam, float bf, const float* X,
+                            const float* normal, double* out) {
+    float Pc[3];
+    for (int r = 0; r < 3; r++) Pc[r] = oracle_fp::dot3_chain(T + 4 * r, X) + T[4 * r + 3];
+    float uv[2];
+    oracle_fp::project(cam, Pc, uv);
+    const float PO[3] = {X[0] - Ow[0], X[1] - Ow[1], X[2] - Ow[2]};
+    const float dist = (float)std::sqrt(oracle_fp::norm2_d(PO));
+    out[0] = Pc[0];
+    out[1] = Pc[1];
+    out[2] = Pc[2];
+    out[3] = (float)std::sqrt(oracle_fp::norm2_d(Pc));
+    out[4] = dist;
+    out[5] = oracle_fp::dot3_chain(PO, normal) / dist;
+    out[6] = oracle_fp::ur_of(uv[0], bf, 1.0f / Pc[2]);
+}
+
+}  // extern "C"
+
+extern "C" {
+
+void oracle_fp_project(const float* cam, const float* X, float* uv) { oracle_fp::project(cam, X, uv); }
+
+double oracle_fp_norm2(const float* v) { return oracle_fp::norm2_d(v); }
+
+/* SearchByProjection(F, LastF) stereo gate (ORBmatcher.cc:2252-2258): er = |ur - uright| */
+float oracle_fp_sbp_er(float u, float bf, float invz, float kpr) {
+    return std::fabs(oracle_fp::ur_of(u, bf, invz) - kpr);
+}
+
+/* Fuse stereo chi2 (ORBmatcher.cc:1735-1745): (double)(e2 * invSigma2) */
+double oracle_fp_fuse_e2(float u, float v, float kpx, float kpy, float kpr, float bf, float invz, float inv_sigma2) {
+    const float ur = oracle_fp::ur_of(u, bf, invz);
+    const float ex = u - kpx, ey = v - kpy, er = ur - kpr;
+    const float e2 = std::fma(er, er, std::fma(ex, ex, ey * ey));
+    return (double)(e2 * inv_sigma2);
+}
+
+}  // extern "C"

@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "../include/slamhot.h"
+#include "fp_sites.hpp"
 
 namespace {
 
@@ -44,18 +45,6 @@ void three_maxima(const std::vector<int>* histo, int L, int& ind1, int& ind2, in
     }
 }
 
-// Pinhole::epipolarConstrain_ (Pinhole.cpp:159-181)
-bool epipolar(const float* F, const slam_keypoint& kp1, const slam_keypoint& kp2, float unc) {
-    const float a = kp1.x * F[0] + kp1.y * F[3] + F[6];
-    const float b = kp1.x * F[1] + kp1.y * F[4] + F[7];
-    const float c = kp1.x * F[2] + kp1.y * F[5] + F[8];
-    const float num = a * kp2.x + b * kp2.y + c;
-    const float den = a * a + b * b;
-    if (den == 0) return false;
-    const float dsqr = num * num / den;
-    return dsqr < 3.84 * unc;
-}
-
 }  // namespace
 
 extern "C" {
@@ -64,6 +53,10 @@ extern "C" {
 int oracle_search_for_triangulation(const slam_tri_kf* K1, const slam_tri_kf* K2, const slam_tri_pair* P,
                                     int check_ori, int32_t* match12) {
     const int HISTO_LENGTH = 30, TH_LOW = 50;
+    // epipole, R12, t12 (ORBmatcher.cc:1215-1240) and the F12 Pinhole::epipolarConstrain_
+    // recomputes from them on every call (Pinhole.cpp:161-164); the F12 argument is unused
+    float ep[2], R12[9], t12[3], F12[9];
+    oracle_fp::tri_geometry(K1->Rcw, K1->tcw, K1->Ow, K1->cam, K2->Rcw, K2->tcw, K2->cam, ep, R12, t12, F12);
     int nmatches = 0;
     std::vector<bool> vbMatched2(K2->n, false);  // never set below, as in the reference
     for (int i = 0; i < K1->n; i++) match12[i] = -1;
@@ -87,12 +80,10 @@ int oracle_search_for_triangulation(const slam_tri_kf* K1, const slam_tri_kf* K2
                     const int dist = hamming32(K1->desc + 32 * (size_t)idx1, K2->desc + 32 * (size_t)idx2);
                     if (dist > TH_LOW || dist > bestDist) continue;
                     const slam_keypoint& kp2 = K2->kps_un[idx2];
-                    if (!bStereo1 && !bStereo2) {
-                        const float distex = P->ep[0] - kp2.x;
-                        const float distey = P->ep[1] - kp2.y;
-                        if (distex * distex + distey * distey < 100 * K2->scale[kp2.octave]) continue;
-                    }
-                    if (epipolar(P->F12, kp1, kp2, K2->level_sigma2[kp2.octave]) || P->coarse) {
+                    if (!bStereo1 && !bStereo2 && oracle_fp::near_epipole(ep, kp2.x, kp2.y, K2->scale[kp2.octave]))
+                        continue;
+                    if (oracle_fp::epipolar(F12, kp1.x, kp1.y, kp2.x, kp2.y, K2->level_sigma2[kp2.octave]) ||
+                        P->coarse) {
                         bestIdx2 = idx2;
                         bestDist = dist;
                     }
@@ -198,7 +189,7 @@ void oracle_fuse_search(const slam_frame_view* F, const float* inv_level_sigma2,
         const float x = p3Dc[0], y = p3Dc[1], z = p3Dc[2];
         const float u = F->fx * x / z + F->cx, v = F->fy * y / z + F->cy;
         if (!(u >= F->min_x && u < F->max_x && v >= F->min_y && v < F->max_y)) continue;
-        const float ur = u - F->bf * invz;
+        const float ur = oracle_fp::ur_of(u, F->bf, invz);  // ORBmatcher.cc.o Fuse @0x1be1
         const float maxDistance = 1.2f * g.max_dist;
         const float minDistance = 0.8f * g.min_dist;
         const float PO[3] = {g.pos[0] - Ow[0], g.pos[1] - Ow[1], g.pos[2] - Ow[2]};
@@ -230,11 +221,11 @@ void oracle_fuse_search(const slam_frame_view* F, const float* inv_level_sigma2,
             if (kpLevel < nPredictedLevel - 1 || kpLevel > nPredictedLevel) continue;
             if (F->uright && F->uright[idx] >= 0) {
                 const float ex = u - kp.x, ey = v - kp.y, er = ur - F->uright[idx];
-                const float e2 = ex * ex + ey * ey + er * er;
+                const float e2 = std::fma(er, er, std::fma(ex, ex, ey * ey));  // Fuse @0x1c98, @0x1cb5
                 if (e2 * inv_level_sigma2[kpLevel] > 7.8) continue;
             } else {
                 const float ex = u - kp.x, ey = v - kp.y;
-                const float e2 = ex * ex + ey * ey;
+                const float e2 = std::fma(ex, ex, ey * ey);
                 if (e2 * inv_level_sigma2[kpLevel] > 5.99) continue;
             }
             const int dist = hamming32(mp_desc + 32 * (size_t)i, F->desc + 32 * (size_t)idx);

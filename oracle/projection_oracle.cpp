@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../include/slamhot.h"
+#include "fp_sites.hpp"
 
 namespace {
 
@@ -209,7 +210,7 @@ int oracle_search_by_projection_last(const slam_frame_view* F, const slam_last_f
         for (int i2 : idxs) {
             if (state[i2] == 1) continue;
             if (F->uright && F->uright[i2] > 0) {
-                const float ur = u - F->bf * invzc;
+                const float ur = oracle_fp::ur_of(u, F->bf, invzc);  // ORBmatcher.cc.o @0x95c7
                 const float er = std::fabs(ur - F->uright[i2]);
                 if (er > radius) continue;
             }
@@ -306,9 +307,10 @@ int oracle_search_by_projection_kf(const slam_frame_view* F, const slam_kf_point
 }
 
 /* Frame::isInFrustum (Frame.cc:493-556, Nleft == -1) over a local map as
- * Tracking::SearchLocalPoints calls it (Tracking.cc:3213-3226): cv::Matx float products and
- * norms as sequential float sums, PredictScale (MapPoint.cc:551-566) with glibc logf.
- * Returns nToMatch. */
+ * Tracking::SearchLocalPoints calls it (Tracking.cc:3213-3226), with the contractions of the
+ * reference binary (Frame.cc.o @0x9ee0, oracle/fp_sites.hpp): Matx products as fma chains,
+ * cv::norm in double, PO.dot(Pn) as an fma chain, mTrackProjXR = fma(-mbf, invz, u);
+ * PredictScale (MapPoint.cc:551-566) with glibc logf.  Returns nToMatch. */
 int oracle_is_in_frustum(const slam_frame_view* F, int n_mp, const slam_mp_geom* mps, float view_cos_limit,
                          slam_mp_track* track) {
     float Ow[3];
@@ -326,41 +328,33 @@ int oracle_is_in_frustum(const slam_frame_view* F, int n_mp, const slam_mp_geom*
         tr.has_obs = g.has_obs;
         if (g.seen || g.is_bad) continue;  // Tracking.cc:3217-3220
         float Pc[3];
-        for (int r = 0; r < 3; r++) {
-            float acc = 0.0f;  // Matx_MatMulOp: s = 0; s += a * b
-            for (int k = 0; k < 3; k++) acc += T[4 * r + k] * g.pos[k];
-            Pc[r] = acc + T[4 * r + 3];
-        }
-        float n2 = 0.0f;  // normL2Sqr<float, float>
-        for (int k = 0; k < 3; k++) n2 += Pc[k] * Pc[k];
-        const float Pc_dist = std::sqrt(n2);
+        for (int r = 0; r < 3; r++) Pc[r] = oracle_fp::dot3_chain(T + 4 * r, g.pos) + T[4 * r + 3];
+        const float Pc_dist = (float)std::sqrt(oracle_fp::norm2_d(Pc));
         const float PcZ = Pc[2];
         const float invz = 1.0f / PcZ;
         if (PcZ < 0.0f) continue;
-        const float u = F->fx * Pc[0] / PcZ + F->cx;  // Pinhole::project
-        const float v = F->fy * Pc[1] / PcZ + F->cy;
+        float uv[2];
+        const float cam[4] = {F->fx, F->fy, F->cx, F->cy};
+        oracle_fp::project(cam, Pc, uv);
+        const float u = uv[0], v = uv[1];
         if (u < F->min_x || u > F->max_x) continue;
         if (v < F->min_y || v > F->max_y) continue;
-        tr.proj_x = u;
+        tr.proj_x = u;  // written as soon as the point lands in the image (Frame.cc:521-522)
         tr.proj_y = v;
         const float maxDistance = 1.2f * g.max_dist;
         const float minDistance = 0.8f * g.min_dist;
         float PO[3];
         for (int k = 0; k < 3; k++) PO[k] = g.pos[k] - Ow[k];
-        float d2 = 0.0f;
-        for (int k = 0; k < 3; k++) d2 += PO[k] * PO[k];
-        const float dist = std::sqrt(d2);
+        const float dist = (float)std::sqrt(oracle_fp::norm2_d(PO));
         if (dist < minDistance || dist > maxDistance) continue;
-        float dot = 0.0f;  // Matx::dot
-        for (int k = 0; k < 3; k++) dot += PO[k] * g.normal[k];
-        const float viewCos = dot / dist;
+        const float viewCos = oracle_fp::dot3_chain(PO, g.normal) / dist;
         if (viewCos < view_cos_limit) continue;
         const float ratio = g.max_dist / dist;
         int nScale = (int)std::ceil(std::log(ratio) / F->log_scale);  // std::log(float) = logf
         if (nScale < 0) nScale = 0;
         else if (nScale >= F->nlevels) nScale = F->nlevels - 1;
         tr.in_view = 1;
-        tr.proj_xr = u - F->bf * invz;
+        tr.proj_xr = oracle_fp::ur_of(u, F->bf, invz);
         tr.depth = Pc_dist;
         tr.scale_level = nScale;
         tr.view_cos = viewCos;

@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "gate_fp.hpp"
 
 namespace slamhot {
 namespace {
@@ -79,6 +80,7 @@ struct TriKF {
     const int32_t* node_off;
     const int32_t* node_feat;
     float scale[16], sigma2[16];
+    float R[9], t[3], Ow[3], cam[4];
 };
 
 constexpr int kTriThreads = 256;
@@ -92,32 +94,25 @@ __device__ __forceinline__ int rot_bin(float a, float b) {  // ORBmatcher.cc:139
     return bin;
 }
 
-// Pinhole::epipolarConstrain_ (Pinhole.cpp:159-181) with the call's F12
-__device__ __forceinline__ bool epipolar_ok(const float* F, const slam_keypoint& k1, const slam_keypoint& k2,
-                                            float unc) {
-    const float a = k1.x * F[0] + k1.y * F[3] + F[6];
-    const float b = k1.x * F[1] + k1.y * F[4] + F[7];
-    const float c = k1.x * F[2] + k1.y * F[5] + F[8];
-    const float num = a * k2.x + b * k2.y + c;
-    const float den = a * a + b * b;
-    if (den == 0) return false;
-    const float dsqr = num * num / den;
-    return (double)dsqr < 3.84 * (double)unc;
-}
-
 __global__ void __launch_bounds__(kTriThreads) k_triangulation(const TriKF* kfs, const slam_tri_pair* pairs,
                                                               int check_ori, int cap, int32_t* match12,
                                                               int32_t* nmatches) {
     __shared__ int hist[kHisto];
     __shared__ int nm;
     __shared__ int keep[3];
+    __shared__ gate::TriGeom G;
     const slam_tri_pair P = pairs[blockIdx.x];
     const TriKF& A = kfs[P.kf1];
     const TriKF& B = kfs[P.kf2];
     int32_t* M = match12 + (size_t)blockIdx.x * cap;
     const int t = threadIdx.x;
     if (t < kHisto) hist[t] = 0;
-    if (t == 0) nm = 0;
+    if (t == 0) {
+        nm = 0;
+        // epipole, R12, t12 and epipolarConstrain_'s F12 as compiled (ORBmatcher.cc.o @0x12880,
+        // @0x14880; Pinhole.cpp.o @0x70f0)
+        G = gate::tri_geometry(A.R, A.t, A.Ow, A.cam, B.R, B.t, B.cam);
+    }
     for (int i = t; i < cap; i += kTriThreads) M[i] = -1;
     __syncthreads();
     const int total = A.n_nodes ? A.node_off[A.n_nodes] : 0;
@@ -159,12 +154,8 @@ __global__ void __launch_bounds__(kTriThreads) k_triangulation(const TriKF* kfs,
             const int dist = ham(a0, a1, d2[0], d2[1]);
             if (dist > 50 || dist > bestDist) continue;
             const slam_keypoint kp2 = B.kps[idx2];
-            if (!bStereo1 && !bStereo2) {
-                const float distex = P.ep[0] - kp2.x;
-                const float distey = P.ep[1] - kp2.y;
-                if (distex * distex + distey * distey < 100 * B.scale[kp2.octave]) continue;
-            }
-            if (epipolar_ok(P.F12, kp1, kp2, B.sigma2[kp2.octave]) || P.coarse) {
+            if (!bStereo1 && !bStereo2 && gate::near_epipole(G.ep, kp2.x, kp2.y, B.scale[kp2.octave])) continue;
+            if (gate::epipolar_ok(G.F, kp1.x, kp1.y, kp2.x, kp2.y, B.sigma2[kp2.octave]) || P.coarse) {
                 bestIdx2 = idx2;
                 bestDist = dist;
             }
@@ -256,7 +247,7 @@ __global__ void __launch_bounds__(kFuseThreads) k_fuse_search(FuseKF K, int n_mp
         const float u = K.fx * p3Dc[0] / p3Dc[2] + K.cx;  // Pinhole::project
         const float v = K.fy * p3Dc[1] / p3Dc[2] + K.cy;
         if (!(u >= K.min_x && u < K.max_x && v >= K.min_y && v < K.max_y)) break;  // KeyFrame::IsInImage
-        const float ur = u - K.bf * invz;
+        const float ur = gate::right_u(u, K.bf, invz);  // ORBmatcher.cc.o Fuse @0x1be1
         const float maxDistance = 1.2f * g.max_dist;
         const float minDistance = 0.8f * g.min_dist;
         const float PO[3] = {g.pos[0] - K.Ow[0], g.pos[1] - K.Ow[1], g.pos[2] - K.Ow[2]};
@@ -292,11 +283,11 @@ __global__ void __launch_bounds__(kFuseThreads) k_fuse_search(FuseKF K, int n_mp
                     const float kpr = K.uright ? K.uright[idx] : -1.0f;
                     if (kpr >= 0) {
                         const float ex = u - kp.x, ey = v - kp.y, er = ur - kpr;
-                        const float e2 = ex * ex + ey * ey + er * er;
+                        const float e2 = fmaf(er, er, fmaf(ex, ex, ey * ey));  // Fuse @0x1c98, @0x1cb5
                         if ((double)(e2 * K.inv_sigma2[kpLevel]) > 7.8) continue;
                     } else {
                         const float ex = u - kp.x, ey = v - kp.y;
-                        const float e2 = ex * ex + ey * ey;
+                        const float e2 = fmaf(ex, ex, ey * ey);
                         if ((double)(e2 * K.inv_sigma2[kpLevel]) > 5.99) continue;
                     }
                     const uint4* dk = reinterpret_cast<const uint4*>(K.desc + (size_t)idx * 32);
@@ -465,6 +456,10 @@ slam_status slamhot_search_for_triangulation(slam_mapper* m, int n_kfs, const sl
             R.scale[l] = l < K.nlevels ? K.scale[l] : 1.0f;
             R.sigma2[l] = l < K.nlevels ? K.level_sigma2[l] : 1.0f;
         }
+        std::memcpy(R.R, K.Rcw, sizeof(R.R));
+        std::memcpy(R.t, K.tcw, sizeof(R.t));
+        std::memcpy(R.Ow, K.Ow, sizeof(R.Ow));
+        std::memcpy(R.cam, K.cam, sizeof(R.cam));
     }
     const TriKF* d_recs = (const TriKF*)put(recs.data(), sizeof(TriKF) * n_kfs);
     const slam_tri_pair* d_pairs = (const slam_tri_pair*)put(pairs, sizeof(slam_tri_pair) * n_pairs);

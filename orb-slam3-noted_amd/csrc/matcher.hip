@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "gate_fp.hpp"
 
 namespace slamhot {
 
@@ -979,7 +980,7 @@ __global__ void __launch_bounds__(1024) k_search_by_projection(DevProjCall C) {
                         Q.u = u;
                         Q.v = v;
                         Q.r = C.th * F.scale[min(max(oct, 0), F.nlevels - 1)];
-                        Q.ur = u - F.bf * invzc;
+                        Q.ur = gate::right_u(u, F.bf, invzc);  // ORBmatcher.cc.o @0x95c7
                         Q.er = Q.r;
                         if (fwd) { Q.min_level = (int16_t)oct; Q.max_level = -1; }
                         else if (bwd) { Q.min_level = 0; Q.max_level = (int16_t)oct; }
@@ -1156,8 +1157,8 @@ __global__ void __launch_bounds__(1024) k_search_by_projection(DevProjCall C) {
 }
 
 // Frame::isInFrustum (Frame.cc:493-556) for a Frame with Nleft == -1, one thread per local
-// MapPoint, in the reference's float arithmetic: cv::Matx33f x Matx31f products and
-// cv::norm / Matx::dot as sequential float sums, Pinhole::project as (f * x) / z + c.
+// MapPoint, in the compiled reference's float arithmetic (gate_fp.hpp): cv::Matx33f x Matx31f
+// and Matx::dot as fma chains, cv::norm summed in double, Pinhole::project as (f * x) / z + c.
 // MapPoint::PredictScale's ceil(logf(ratio) / mfLogScaleFactor) uses the correctly rounded
 // logf ((float)log((double)r)); its ceil equals glibc logf's for every ratio in [1e-3, 1e3]
 // (exhaustive check, tests/test_projection_oracle.py).
@@ -1183,28 +1184,29 @@ __global__ void __launch_bounds__(256) k_is_in_frustum(FrustumCall C) {
     tr.has_obs = g.has_obs;
     tr.in_view = 0;
     bool ok = !g.seen && !g.is_bad;
+    // Frame::isInFrustum as compiled (Frame.cc.o @0x9ee0; gate_fp.hpp): Matx products as fma
+    // chains, cv::norm in double, mTrackProjX/Y written once the point is in the image
     float Pc[3];
 #pragma unroll
-    for (int r = 0; r < 3; r++) {
-        float acc = 0.0f;  // Matx_MatMulOp: s = 0; s += a * b
-        acc = acc + C.R[3 * r] * g.pos[0];
-        acc = acc + C.R[3 * r + 1] * g.pos[1];
-        acc = acc + C.R[3 * r + 2] * g.pos[2];
-        Pc[r] = acc + C.t[r];
-    }
-    const float Pc_dist = sqrtf(((0.0f + Pc[0] * Pc[0]) + Pc[1] * Pc[1]) + Pc[2] * Pc[2]);
+    for (int r = 0; r < 3; r++)
+        Pc[r] = gate::chain3(C.R[3 * r], g.pos[0], C.R[3 * r + 1], g.pos[1], C.R[3 * r + 2], g.pos[2]) + C.t[r];
+    const float Pc_dist = (float)sqrt(gate::norm2(Pc[0], Pc[1], Pc[2]));
     const float PcZ = Pc[2];
     const float invz = 1.0f / PcZ;
     if (PcZ < 0.0f) ok = false;
     const float u = C.fx * Pc[0] / PcZ + C.cx;
     const float v = C.fy * Pc[1] / PcZ + C.cy;
     if (u < C.min_x || u > C.max_x || v < C.min_y || v > C.max_y) ok = false;
+    if (ok) {
+        tr.proj_x = u;
+        tr.proj_y = v;
+    }
     const float maxDistance = 1.2f * g.max_dist;
     const float minDistance = 0.8f * g.min_dist;
     const float PO[3] = {g.pos[0] - C.Ow[0], g.pos[1] - C.Ow[1], g.pos[2] - C.Ow[2]};
-    const float dist = sqrtf(((0.0f + PO[0] * PO[0]) + PO[1] * PO[1]) + PO[2] * PO[2]);
+    const float dist = (float)sqrt(gate::norm2(PO[0], PO[1], PO[2]));
     if (dist < minDistance || dist > maxDistance) ok = false;
-    const float viewCos = (((0.0f + PO[0] * g.normal[0]) + PO[1] * g.normal[1]) + PO[2] * g.normal[2]) / dist;
+    const float viewCos = gate::chain3(PO[0], g.normal[0], PO[1], g.normal[1], PO[2], g.normal[2]) / dist;
     if (viewCos < C.view_cos_limit) ok = false;
     if (ok) {
         const float ratio = g.max_dist / dist;
@@ -1214,7 +1216,7 @@ __global__ void __launch_bounds__(256) k_is_in_frustum(FrustumCall C) {
         else if (nScale >= C.nlevels) nScale = C.nlevels - 1;
         tr.in_view = 1;
         tr.proj_x = u;
-        tr.proj_xr = u - C.bf * invz;
+        tr.proj_xr = gate::right_u(u, C.bf, invz);
         tr.depth = Pc_dist;
         tr.proj_y = v;
         tr.scale_level = nScale;

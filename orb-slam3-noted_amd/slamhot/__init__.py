@@ -788,17 +788,24 @@ def ComputeStereoMatches(left: ORBextractor, right: ORBextractor, images_left, i
 class TriKF(C.Structure):
     _fields_ = [("n", I), ("kps_un", P), ("uright", P), ("desc", P), ("has_mp", P), ("n_nodes", I),
                 ("node_id", P), ("node_off", P), ("node_feat", P), ("nlevels", I), ("scale", P),
-                ("level_sigma2", P)]
+                ("level_sigma2", P), ("Rcw", C.c_float * 9), ("tcw", C.c_float * 3), ("Ow", C.c_float * 3),
+                ("cam", C.c_float * 4)]
 
 
 class TriPair(C.Structure):
-    _fields_ = [("kf1", I), ("kf2", I), ("F12", C.c_float * 9), ("ep", C.c_float * 2), ("only_stereo", C.c_uint8),
-                ("coarse", C.c_uint8), ("pad", C.c_uint8 * 2)]
+    _fields_ = [("kf1", I), ("kf2", I), ("only_stereo", C.c_uint8), ("coarse", C.c_uint8), ("pad", C.c_uint8 * 2)]
+
+
+def camera_center(Tcw):
+    """KeyFrame::SetPose's Ow = -Rwc * tcw (cv::Mat product: double accumulation, rounded once)."""
+    T = np.asarray(Tcw, np.float32).astype(np.float64)
+    return (-(T[:3, :3].T @ T[:3, 3])).astype(np.float32)
 
 
 def make_tri_kf(kf: dict):
     """slam_tri_kf from a dict: kps_un (KP_DTYPE), uright, desc, has_mp, node_id/node_off/node_feat
-    (mFeatVec CSR), scale, level_sigma2.  Returns (struct, keepalive)."""
+    (mFeatVec CSR), scale, level_sigma2, Tcw (4x4 float), cam (fx, fy, cx, cy) and optionally Ow
+    (default: camera_center(Tcw)).  Returns (struct, keepalive)."""
     keep = dict(kps=np.ascontiguousarray(kf["kps_un"], KP_DTYPE), desc=np.ascontiguousarray(kf["desc"], np.uint8),
                 has=np.ascontiguousarray(kf["has_mp"], np.uint8),
                 nid=np.ascontiguousarray(kf["node_id"], np.int32), noff=np.ascontiguousarray(kf["node_off"], np.int32),
@@ -819,14 +826,17 @@ def make_tri_kf(kf: dict):
     t.nlevels = len(keep["sc"])
     t.scale = keep["sc"].ctypes.data
     t.level_sigma2 = keep["s2"].ctypes.data
+    T = np.asarray(kf["Tcw"], np.float32)
+    t.Rcw[:] = [float(v) for v in T[:3, :3].ravel()]
+    t.tcw[:] = [float(v) for v in T[:3, 3]]
+    t.Ow[:] = [float(v) for v in np.asarray(kf.get("Ow", camera_center(T)), np.float32)]
+    t.cam[:] = [float(v) for v in np.asarray(kf["cam"], np.float32)]
     return t, keep
 
 
-def make_tri_pair(kf1: int, kf2: int, F12, ep, only_stereo=False, coarse=False):
+def make_tri_pair(kf1: int, kf2: int, only_stereo=False, coarse=False):
     p = TriPair()
     p.kf1, p.kf2 = kf1, kf2
-    p.F12[:] = [float(v) for v in np.asarray(F12, np.float32).ravel()]
-    p.ep[:] = [float(v) for v in np.asarray(ep, np.float32).ravel()]
     p.only_stereo, p.coarse = int(only_stereo), int(coarse)
     return p
 
@@ -871,8 +881,8 @@ class Mapper:
         return best
 
     def SearchForTriangulation(self, kfs, pairs, check_ori=False):
-        """kfs: list of KeyFrame dicts (make_tri_kf); pairs: list of (kf1, kf2, F12, ep,
-        only_stereo, coarse).  Returns [(nmatches, vMatchedPairs as an (m, 2) array)]."""
+        """kfs: list of KeyFrame dicts (make_tri_kf); pairs: list of (kf1, kf2, only_stereo, coarse).
+        Returns [(nmatches, vMatchedPairs as an (m, 2) array)]."""
         built = [make_tri_kf(k) for k in kfs]
         K = (TriKF * max(1, len(built)))(*[b[0] for b in built])
         Ps = (TriPair * max(1, len(pairs)))(*[make_tri_pair(*p) for p in pairs])

@@ -217,24 +217,10 @@ def tri_keyframes(seed, n_kf=4, n_pts=1500, n_nodes=400):
         kps, desc, ur, has_mp, nid = kps[order], desc[order], ur[order], has_mp[order], nid[order]
         uniq, noff, nfeat = synth.feature_vector(nid, np.ones(n))
         kfs.append(dict(kps_un=kps, desc=desc, uright=ur, has_mp=has_mp, node_id=uniq.astype(np.int32),
-                        node_off=noff, node_feat=nfeat.astype(np.int32), scale=sc, level_sigma2=sigma2))
+                        node_off=noff, node_feat=nfeat.astype(np.int32), scale=sc, level_sigma2=sigma2,
+                        Tcw=T.astype(np.float32), cam=np.array([FX, FY, CX, CY], np.float32)))
         poses.append(T)
     return kfs, poses
-
-
-def f12_ep(T1, T2):
-    """LocalMapping::ComputeF12_ and the epipole of KF1's centre in KF2 (float64, rounded once)."""
-    R1, t1 = _Rt(T1)
-    R2, t2 = _Rt(T2)
-    R12 = R1 @ R2.T
-    t12 = -R1 @ R2.T @ t2 + t1
-    tx = np.array([[0, -t12[2], t12[1]], [t12[2], 0, -t12[0]], [-t12[1], t12[0], 0]])
-    K = np.array([[FX, 0, CX], [0, FY, CY], [0, 0, 1]], np.float64)
-    F12 = np.linalg.inv(K.T) @ tx @ R12 @ np.linalg.inv(K)
-    C1 = -R1.T @ t1
-    C2 = R2 @ C1 + t2
-    ep = np.array([FX * C2[0] / C2[2] + CX, FY * C2[1] / C2[2] + CY])
-    return F12.astype(np.float32), ep.astype(np.float32)
 
 
 def fuse_mps(S, n_extra=300):

@@ -32,16 +32,14 @@ def test_search_for_triangulation_batch(check_ori):
     for a, b, only_stereo, coarse in [(0, 1, False, False), (0, 2, False, False), (0, 3, True, False),
                                       (0, 4, False, True), (2, 1, False, False), (4, 3, True, True),
                                       (1, 1, False, False)]:
-        F, ep = scenes.f12_ep(poses[a], poses[b])
-        pairs.append((a, b, F, ep, only_stereo, coarse))
+        pairs.append((a, b, only_stereo, coarse))
     m = slamhot.Mapper()
     res = m.SearchForTriangulation(kfs, pairs, check_ori)
     m.close()
     built = [slamhot.make_tri_kf(k) for k in kfs]
     total = 0
-    for (a, b, F, ep, os_, co), (n, mp) in zip(pairs, res):
-        no, m12 = ob.search_for_triangulation(built[a][0], built[b][0], slamhot.make_tri_pair(a, b, F, ep, os_, co),
-                                              check_ori)
+    for (a, b, os_, co), (n, mp) in zip(pairs, res):
+        no, m12 = ob.search_for_triangulation(built[a][0], built[b][0], slamhot.make_tri_pair(a, b, os_, co), check_ori)
         i1 = np.flatnonzero(m12 >= 0)
         assert n == no
         assert np.array_equal(mp, np.stack([i1, m12[i1]], 1))

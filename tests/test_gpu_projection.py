@@ -69,8 +69,11 @@ def test_search_local_points(seed, th, far):
     nto, tro = ob.is_in_frustum(fv, geom, 0.5)
     assert ntg == nto and nto > 300
     assert np.array_equal(trg["in_view"], tro["in_view"])
+    # mTrackProjX/Y are written as soon as the point is in the image (Frame.cc:521-522)
+    assert np.array_equal(trg["proj_x"], tro["proj_x"]) and np.array_equal(trg["proj_y"], tro["proj_y"])
+    assert (trg["proj_x"][tro["in_view"] == 0] >= 0).sum() > 0
     v = tro["in_view"] == 1
-    for f in ("proj_x", "proj_y", "proj_xr", "depth", "view_cos", "scale_level"):
+    for f in ("proj_xr", "depth", "view_cos", "scale_level"):
         assert np.array_equal(trg[f][v], tro[f][v]), f
     no, fo = ob.search_by_projection_local(fv, tro, desc, 0.8, th, far, 20.0)
     assert ng == no and no > 50

@@ -1,8 +1,11 @@
 """CPU checks of the LocalMapping-matcher oracle (oracle/mapping_oracle.cpp) against
 independent numpy restatements.  Parity unpinned: the reference ships no fixtures for these."""
+import ctypes as C
+
 import numpy as np
 
 import oracle_bind as ob
+from fpexact import fmaf
 
 
 def observation_sets(seed, n_mp=300, max_n=40):
@@ -43,9 +46,21 @@ def test_distinctive_descriptors_oracle():
     assert np.array_equal(ob.distinctive_descriptors(off, desc), np_distinctive(off, desc))
 
 
+def test_fmaf_helper():
+    rng = np.random.default_rng(0)
+    for a, b, c in rng.normal(size=(2000, 3)).astype(np.float32):
+        assert fmaf(a, b, np.float32(0)) == np.float32(a * b)  # one rounding of an exact product
+        assert fmaf(a, np.float32(1), c) == np.float32(a + c)
+    # a product whose low bits an unfused multiply-add would lose
+    x = np.float32(1 + 2 ** -12)
+    assert fmaf(x, x, np.float32(-1)) != np.float32(x * x) - np.float32(1)
+
+
 def _py_triangulation(K1, K2, F, ep, only_stereo, coarse):
     """SearchForTriangulation_ (ORBmatcher.cc:1208-1433) without the rotation check, numpy
-    float32 scalars; FeatureVector co-iteration as a dict intersection."""
+    float32 scalars with the compiled reference's contractions (exact fmaf above); F and ep
+    from the pair's poses (oracle_fp_tri_geometry, pinned by tests/test_fp_sites.py);
+    FeatureVector co-iteration as a dict intersection."""
     f32 = np.float32
     bits1, bits2 = np.unpackbits(K1["desc"], axis=1), np.unpackbits(K2["desc"], axis=1)
     nodes2 = {int(K2["node_id"][j]): K2["node_feat"][K2["node_off"][j]:K2["node_off"][j + 1]]
@@ -75,14 +90,15 @@ def _py_triangulation(K1, K2, F, ep, only_stereo, coarse):
                 k2 = K2["kps_un"][idx2]
                 if not s1 and not s2:
                     ex, ey = f32(ep[0] - k2["x"]), f32(ep[1] - k2["y"])
-                    if f32(f32(ex * ex) + f32(ey * ey)) < f32(100 * K2["scale"][k2["octave"]]):
+                    if fmaf(ex, ex, f32(ey * ey)) < f32(100 * K2["scale"][k2["octave"]]):
                         continue
                 x1, y1 = f32(k1["x"]), f32(k1["y"])
-                a = f32(f32(f32(x1 * F[0, 0]) + f32(y1 * F[1, 0])) + F[2, 0])
-                b = f32(f32(f32(x1 * F[0, 1]) + f32(y1 * F[1, 1])) + F[2, 1])
-                c = f32(f32(f32(x1 * F[0, 2]) + f32(y1 * F[1, 2])) + F[2, 2])
-                num = f32(f32(f32(a * k2["x"]) + f32(b * k2["y"])) + c)
-                den = f32(f32(a * a) + f32(b * b))
+                x2, y2 = f32(k2["x"]), f32(k2["y"])
+                a = f32(fmaf(x1, F[0, 0], f32(y1 * F[1, 0])) + F[2, 0])
+                b = f32(fmaf(x1, F[0, 1], f32(y1 * F[1, 1])) + F[2, 1])
+                c = f32(fmaf(y1, F[1, 2], f32(x1 * F[0, 2])) + F[2, 2])
+                num = f32(fmaf(b, y2, f32(a * x2)) + c)
+                den = fmaf(a, a, f32(b * b))
                 ok = den != 0 and float(f32(f32(num * num) / den)) < 3.84 * float(K2["level_sigma2"][k2["octave"]])
                 if ok or coarse:
                     best, bi = dist, idx2
@@ -94,11 +110,14 @@ def test_triangulation_oracle_vs_python():
     import scenes
     import slamhot
     kfs, poses = scenes.tri_keyframes(5, n_kf=2, n_pts=500)
-    F, ep = scenes.f12_ep(poses[0], poses[1])
     t1, k1 = slamhot.make_tri_kf(kfs[0])
     t2, k2 = slamhot.make_tri_kf(kfs[1])
+    ep, R12, t12, F12 = (C.c_float * 2)(), (C.c_float * 9)(), (C.c_float * 3)(), (C.c_float * 9)()
+    ob.lib().oracle_fp_tri_geometry(t1.Rcw, t1.tcw, t1.Ow, t1.cam, t2.Rcw, t2.tcw, t2.cam, ep, R12, t12, F12)
+    F = np.array(F12[:], np.float32).reshape(3, 3)
+    ep = np.array(ep[:], np.float32)
     for only_stereo, coarse in ((False, False), (True, False), (False, True)):
-        pr = slamhot.make_tri_pair(0, 1, F, ep, only_stereo, coarse)
+        pr = slamhot.make_tri_pair(0, 1, only_stereo, coarse)
         n, m12 = ob.search_for_triangulation(t1, t2, pr, False)
         ref = _py_triangulation(kfs[0], kfs[1], F, ep, only_stereo, coarse)
         assert np.array_equal(m12, ref)

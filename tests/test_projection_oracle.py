@@ -6,6 +6,7 @@ import numpy as np
 import pytest
 
 import oracle_bind as ob
+from fpexact import chain3, norm_d
 import scenes
 
 f32 = np.float32
@@ -123,7 +124,8 @@ def test_predict_scale_logf_equivalence():
 
 
 def _py_in_frustum(fv, T, g, limit=0.5):
-    """Frame::isInFrustum restated with numpy float32 scalars (Frame.cc:493-556)."""
+    """Frame::isInFrustum restated with numpy float32 scalars (Frame.cc:493-556) and the compiled
+    reference's contractions (fpexact: fma chains, cv::norm in double)."""
     f32 = np.float32
     if g["seen"] or g["is_bad"]:
         return None
@@ -131,7 +133,7 @@ def _py_in_frustum(fv, T, g, limit=0.5):
     Tr = T.astype(np.float64)
     Ow = (-(Tr[:3, :3].T @ Tr[:3, 3])).astype(np.float32)
     X = g["pos"].astype(np.float32)
-    Pc = [f32(f32(f32(f32(f32(0) + R[r, 0] * X[0]) + R[r, 1] * X[1]) + R[r, 2] * X[2]) + t[r]) for r in range(3)]
+    Pc = [f32(chain3(R[r], X) + t[r]) for r in range(3)]
     if Pc[2] < 0:
         return None
     u = f32(f32(f32(fv.fx) * Pc[0]) / Pc[2]) + f32(fv.cx)
@@ -139,11 +141,11 @@ def _py_in_frustum(fv, T, g, limit=0.5):
     if u < fv.min_x or u > fv.max_x or v < fv.min_y or v > fv.max_y:
         return None
     PO = (X - Ow).astype(np.float32)
-    dist = np.sqrt(f32(f32(f32(f32(0) + PO[0] * PO[0]) + PO[1] * PO[1]) + PO[2] * PO[2]))
+    dist = norm_d(PO)
     if dist < f32(0.8) * g["min_dist"] or dist > f32(1.2) * g["max_dist"]:
         return None
     n = g["normal"]
-    vc = f32(f32(f32(f32(f32(0) + PO[0] * n[0]) + PO[1] * n[1]) + PO[2] * n[2]) / dist)
+    vc = f32(chain3(PO, n) / dist)
     if vc < limit:
         return None
     ratio = f32(g["max_dist"] / dist)

@@ -1,0 +1,596 @@
+#!/usr/bin/env python3
+"""Static float data-flow extraction from a reference object file (study tool; build container
+only — it needs /root/reference, which never reaches the GPU box).
+
+The reference's objects are READ AS DATA (`objdump -d` text): nothing is executed, emulated on
+concrete values or linked.  The tool walks one straight-line instruction range symbolically and
+prints, as SSA, the expression every scalar float/double store, compare and return value is
+made of — which products GCC 9.3 contracted into FMAs (`-O3 -march=native`, reference
+evaluation/CMakeFiles/ORB_SLAM3.dir/flags.make:5), in which order sums associate, where float
+is widened to double.  The oracle's and the kernels' restatements (explicit fmaf / fma) are
+written from this listing; tests/test_fp_sites.py checks them against C code emitted by
+`--emit-c` from the same listing (oracle/_ref/, git-ignored, only when /root/reference exists).
+
+    python3 tools/disasm/fptrace.py OBJ 'FUNC substring' START END [--names a=rdx+0x0,...]
+                                    [--emit-c NAME --inputs v1,v2,... --outputs o1,o2,...]
+
+Branches are not followed: a conditional jump falls through, which is what the gates of the
+traced functions do on their accepting path.  Supported: the scalar SSE/AVX/FMA subset GCC
+emits for these functions (vmov*, vadd/sub/mul/div/sqrt ss/sd, vfm*/vfnm* 132/213/231,
+vcvt*, vxorps sign flips, vucomis/vcomis, 32-bit GPR moves and stack copies).
+"""
+from __future__ import annotations
+
+import argparse
+import re
+import struct
+import subprocess
+import sys
+
+REG64 = {"rax", "rbx", "rcx", "rdx", "rsi", "rdi", "rbp", "rsp", "r8", "r9", "r10", "r11", "r12",
+         "r13", "r14", "r15"}
+R32 = {"eax": "rax", "ebx": "rbx", "ecx": "rcx", "edx": "rdx", "esi": "rsi", "edi": "rdi",
+       "ebp": "rbp", "r8d": "r8", "r9d": "r9", "r10d": "r10", "r11d": "r11", "r12d": "r12",
+       "r13d": "r13", "r14d": "r14", "r15d": "r15"}
+
+
+class Node:
+    __slots__ = ("op", "args", "ty", "id", "name")
+
+    def __init__(self, op, args, ty, name=None):
+        self.op, self.args, self.ty, self.id, self.name = op, tuple(args), ty, None, name
+
+
+class Tracer:
+    def __init__(self, obj, names):
+        self.obj = obj
+        self.nodes = []
+        self.memo = {}
+        self.regs = {}          # xmmN -> [lane0..lane3] (lane0 of a double holds the f64 node)
+        self.gpr = {"rsp": ("rsp", 0)}
+        self.mem = {}           # (base, off) -> node (4-byte granularity; f64 at off, 'hi' at off+4)
+        self.events = []
+        self.names = names
+        self.consts = self._load_consts()
+        self.ncall = 0
+
+    # ---- constants from .rodata.cst* (read as data) ----
+    def _load_consts(self):
+        syms = {}
+        out = subprocess.run(["objdump", "-t", self.obj], capture_output=True, text=True).stdout
+        for line in out.splitlines():
+            m = re.match(r"^([0-9a-f]+)\s+l\s+(\S+)\s+[0-9a-f]+\s+(\.LC\d+)$", line.strip())
+            if m:
+                syms[m.group(3)] = (m.group(2), int(m.group(1), 16))
+        secs = {}
+        out = subprocess.run(["objdump", "-s", "-j", ".rodata.cst4", "-j", ".rodata.cst8",
+                              "-j", ".rodata.cst16", "-j", ".rodata.cst32", self.obj],
+                             capture_output=True, text=True).stdout
+        cur = None
+        for line in out.splitlines():
+            m = re.match(r"^Contents of section (\S+):", line)
+            if m:
+                cur = m.group(1)
+                secs[cur] = bytearray()
+                continue
+            m = re.match(r"^ ([0-9a-f]{4,}) ((?:[0-9a-f]{2,8} ?)+)", line)
+            if cur and m:
+                hexs = "".join(m.group(2).split())
+                secs[cur] += bytes.fromhex(hexs)
+        self.secs = secs
+        return syms
+
+    def const_bytes(self, reloc, n):
+        m = re.match(r"(\.LC\d+|\.rodata\.cst\d+)([+-]0x[0-9a-f]+)?", reloc)
+        sym, add = m.group(1), int(m.group(2) or "0", 16)
+        # RIP-relative PC32: target = S + A + 4 (the displacement ends the instruction)
+        sec, off = self.consts[sym] if sym.startswith(".LC") else (sym, 0)
+        base = off + add + 4
+        return bytes(self.secs[sec][base: base + n])
+
+    # ---- node construction with hash-consing ----
+    def mk(self, op, args, ty, name=None):
+        key = (op, tuple(id(a) for a in args), ty, name)
+        if key in self.memo:
+            return self.memo[key]
+        n = Node(op, args, ty, name)
+        self.memo[key] = n
+        self.nodes.append(n)
+        return n
+
+    def inp(self, where, ty):
+        nm = self.names.get(where, where)
+        return self.mk("in", [], ty, nm)
+
+    def const(self, val, ty):
+        return self.mk("const", [], ty, repr(val))
+
+    # ---- operands ----
+    def addr(self, s, reloc):
+        if "%rip" in s:
+            return ("const", reloc)
+        m = re.match(r"^(-?0x[0-9a-f]+|-?\d+)?\(%(\w+)(?:,%(\w+),(\d))?\)$", s)
+        if not m:
+            raise ValueError("addr " + s)
+        disp = int(m.group(1), 16) if m.group(1) and "x" in m.group(1) else int(m.group(1) or 0)
+        base = m.group(2)
+        if m.group(3):
+            return ("dyn", s)
+        b = self.gpr.get(base)
+        if b is None:
+            b = ("arg_" + base, 0)
+            self.gpr[base] = b
+        return (b[0], b[1] + disp)
+
+    @staticmethod
+    def where(a):
+        if isinstance(a[1], str):
+            return a[1]
+        return f"{a[0]}+0x{a[1]:x}" if a[1] >= 0 else f"{a[0]}-0x{-a[1]:x}"
+
+    def load32(self, a, ty="f32"):
+        if a[0] == "const":
+            return None
+        key = (a[0], a[1])
+        v = self.mem.get(key)
+        if v is None:
+            v = self.inp(self.where(a), ty)
+            self.mem[key] = v
+        return v
+
+    def load_scalar(self, s, reloc, ty):
+        a = self.addr(s, reloc)
+        if a[0] == "const":
+            b = self.const_bytes(reloc, 4 if ty == "f32" else 8)
+            return self.const(struct.unpack("<f" if ty == "f32" else "<d", b)[0], ty)
+        if ty == "f64":
+            v = self.mem.get((a[0], a[1]))
+            if v is not None and v.ty == "f64":
+                return v
+            if v is None:
+                v = self.inp(self.where(a), "f64")
+                self.mem[(a[0], a[1])] = v
+                return v
+            raise ValueError("f64 load of f32 data at %r" % (a,))
+        return self.load32(a)
+
+    def reg(self, r):
+        if r not in self.regs:
+            self.regs[r] = [self.inp("%" + r, "f32")] + [None] * 7
+        lanes = self.regs[r]
+        if len(lanes) < 8:
+            lanes = self.regs[r] = list(lanes) + [None] * (8 - len(lanes))
+        return lanes
+
+    # ---- events ----
+    def event(self, kind, *nodes, extra=""):
+        self.events.append((kind, nodes, extra))
+
+    def run(self, lines):
+        for addr, ins, ops, reloc in lines:
+            try:
+                self.step(addr, ins, ops, reloc)
+            except Exception as e:  # pragma: no cover - study tool
+                print(f"# {addr:x}: unsupported {ins} {ops}: {e}", file=sys.stderr)
+
+    def step(self, addr, ins, ops, reloc):
+        X = lambda o: o[:4] in ("%xmm", "%ymm", "%zmm")
+        R = lambda o: "xmm" + o[4:] if o[:4] in ("%xmm", "%ymm", "%zmm") else o[1:]
+        W = lambda o: 8 if o.startswith("%ymm") else 4
+        binop = {"vaddss": "+", "vsubss": "-", "vmulss": "*", "vdivss": "/",
+                 "vaddsd": "+", "vsubsd": "-", "vmulsd": "*", "vdivsd": "/",
+                 "vminss": "min", "vmaxss": "max", "vminsd": "min", "vmaxsd": "max"}
+        if ins in ("vmovss", "vmovsd"):
+            ty = "f32" if ins == "vmovss" else "f64"
+            if len(ops) == 2 and X(ops[1]) and not X(ops[0]):
+                v = self.load_scalar(ops[0], reloc, ty)
+                self.regs[R(ops[1])] = [v, None, None, None]
+            elif len(ops) == 2 and X(ops[0]) and not X(ops[1]):
+                a = self.addr(ops[1], reloc)
+                v = self.reg(R(ops[0]))[0]
+                self.mem[(a[0], a[1])] = v
+                if ty == "f64":
+                    self.mem[(a[0], a[1] + 4)] = None
+                self.event("store", v, extra=self.where(a))
+            elif len(ops) == 2:
+                self.regs[R(ops[1])] = list(self.reg(R(ops[0])))
+            else:
+                src, other, dst = ops
+                lanes = list(self.reg(R(other)))
+                lanes[0] = self.reg(R(src))[0]
+                self.regs[R(dst)] = lanes
+            return
+        if ins in ("vmovaps", "vmovups", "vmovdqa64", "vmovdqu64", "vmovdqa", "vmovdqu",
+                   "vmovapd", "vmovupd", "vmovdqa32", "vmovdqu32"):
+            src, dst = ops
+            w = max(W(src), W(dst))
+            if X(src) and X(dst):
+                self.regs[R(dst)] = list(self.reg(R(src)))
+            elif X(dst):
+                a = self.addr(src, reloc)
+                if a[0] == "const":
+                    cb = self.const_bytes(reloc, 4 * w)
+                    self.regs[R(dst)] = [self.const(struct.unpack("<f", cb[4 * k:4 * k + 4])[0], "f32") for k in range(w)] + [None] * (8 - w)
+                else:
+                    self.regs[R(dst)] = [self.load32((a[0], a[1] + 4 * k)) for k in range(w)] + [None] * (8 - w)
+            else:
+                a = self.addr(dst, reloc)
+                lanes = self.reg(R(src))
+                for k in range(w):
+                    self.mem[(a[0], a[1] + 4 * k)] = lanes[k]
+                    if lanes[k] is not None and lanes[k].op not in ("in", "const"):
+                        self.event("store", lanes[k], extra=self.where((a[0], a[1] + 4 * k)))
+            return
+        if ins in ("vmovq", "vmovd"):
+            src, dst = ops
+            n = 2 if ins == "vmovq" else 1
+            if X(src) and not X(dst):
+                if dst.startswith("%"):
+                    self.gpr[R(dst)] = ("xmmval", self.reg(R(src))[:n])
+                    return
+                a = self.addr(dst, reloc)
+                lanes = self.reg(R(src))
+                for k in range(n):
+                    self.mem[(a[0], a[1] + 4 * k)] = lanes[k]
+            elif X(dst):
+                if src.startswith("%"):
+                    g = self.gpr.get(R(src))
+                    self.regs[R(dst)] = (list(g[1]) + [None] * 4)[:4] if g and g[0] == "xmmval" else [None] * 4
+                    return
+                a = self.addr(src, reloc)
+                self.regs[R(dst)] = [self.load32((a[0], a[1] + 4 * k)) for k in range(n)] + [None] * (4 - n)
+            return
+        if ins in ("vandps", "vandpd"):
+            a, b, d = ops  # and with an abs mask constant: fabs
+            src = self.reg(R(b))
+            if "%rip" in a:
+                word = struct.unpack("<I", self.const_bytes(reloc, 4))[0]
+                assert word == 0x7fffffff, hex(word)
+            lanes = list(src)
+            lanes[0] = self.mk("fabs", [src[0]], src[0].ty)
+            self.regs[R(d)] = lanes
+            return
+        if ins in ("vxorps", "vxorpd", "vpxor", "vpxord", "vpxorq"):
+            a, b, d = ops
+            if a == b:
+                ty = "f64" if ins == "vxorpd" else "f32"
+                self.regs[R(d)] = [self.const(0.0, ty)] * 8
+            else:
+                # xor with a sign-mask constant: lane-wise negation (checked against the bytes)
+                w = W(d)
+                mask = self.const_bytes(reloc, 4 * w) if "%rip" in a else None
+                src = self.reg(R(b))
+                lanes = []
+                for k in range(8):
+                    if k < w and src[k] is not None:
+                        if mask is not None:
+                            word = struct.unpack("<I", mask[4 * k:4 * k + 4])[0]
+                            if ins == "vxorpd":
+                                assert mask[4 * k:4 * k + 4] in (b"\x00\x00\x00\x00", b"\x00\x00\x00\x80"), mask
+                            else:
+                                assert word == 0x80000000, hex(word)
+                        lanes.append(self.mk("neg", [src[k]], src[k].ty))
+                    else:
+                        lanes.append(None)
+                self.regs[R(d)] = lanes
+            return
+        if ins in binop:
+            s2, s1, d = ops
+            ty = "f32" if ins.endswith("ss") else "f64"
+            b = self.reg(R(s2))[0] if X(s2) else self.load_scalar(s2, reloc, ty)
+            a = self.reg(R(s1))
+            lanes = list(a)
+            lanes[0] = self.mk(binop[ins], [a[0], b], ty)
+            self.regs[R(d)] = lanes
+            return
+        if ins in ("vsqrtss", "vsqrtsd"):
+            s2, s1, d = ops
+            ty = "f32" if ins.endswith("ss") else "f64"
+            b = self.reg(R(s2))[0] if X(s2) else self.load_scalar(s2, reloc, ty)
+            lanes = list(self.reg(R(s1)))
+            lanes[0] = self.mk("sqrt", [b], ty)
+            self.regs[R(d)] = lanes
+            return
+        m = re.match(r"^v(fn?m)(add|sub)(132|213|231)s([sd])$", ins)
+        if m:
+            neg = m.group(1) == "fnm"
+            sub = m.group(2) == "sub"
+            form = m.group(3)
+            ty = "f32" if m.group(4) == "s" else "f64"
+            o1, o2, d = ops
+            v1 = self.reg(R(o1))[0] if X(o1) else self.load_scalar(o1, reloc, ty)
+            v2 = self.reg(R(o2))[0]
+            vd = self.reg(R(d))[0]
+            if form == "132":  # AT&T operand order: (op1, op2, dst)
+                p, q, c = vd, v1, v2
+            elif form == "213":
+                p, q, c = v2, vd, v1
+            else:
+                p, q, c = v2, v1, vd
+            if neg:
+                p = self.mk("neg", [p], ty)
+            if sub:
+                c = self.mk("neg", [c], ty)
+            lanes = list(self.reg(R(d)))
+            lanes[0] = self.mk("fma", [p, q, c], ty)
+            self.regs[R(d)] = lanes
+            return
+        if ins in ("vcvtss2sd", "vcvtsd2ss"):
+            s, o, d = ops
+            src_ty, ty = ("f32", "f64") if ins == "vcvtss2sd" else ("f64", "f32")
+            v = self.reg(R(s))[0] if X(s) else self.load_scalar(s, reloc, src_ty)
+            lanes = list(self.reg(R(o)))
+            lanes[0] = self.mk("cvt", [v], ty)
+            self.regs[R(d)] = lanes
+            return
+        if ins in ("vcvtsi2ss", "vcvtsi2sd", "vcvtsi2ssl", "vcvtsi2sdl"):
+            s, o, d = ops
+            ty = "f32" if "ss" in ins else "f64"
+            g = self.gpr.get(R(s)) if s.startswith("%") else None
+            v = g[1] if g and g[0] == "ival" else self.inp("int " + s, "i32")
+            lanes = list(self.reg(R(o)))
+            lanes[0] = self.mk("i2f", [v], ty)
+            self.regs[R(d)] = lanes
+            return
+        if ins in ("vcvttss2si", "vcvtss2si", "vcvttsd2si", "vcvtsd2si"):
+            s, d = ops
+            v = self.reg(R(s))[0]
+            op = "trunc" if "tt" in ins else "rint"
+            n = self.mk(op, [v], "i32")
+            self.gpr[R32.get(R(d), R(d))] = ("ival", n)
+            self.event("int", n, extra=d)
+            return
+        if ins in ("vrndscaless", "vrndscalesd", "vroundss", "vroundsd"):
+            imm, s, o, d = ops
+            mode = {"$0xa": "ceil", "$0x9": "floor", "$0xb": "trunc", "$0x8": "rint", "$0xc": "rint",
+                    "$0x4": "rint", "$0x1": "floor", "$0x2": "ceil"}.get(imm, "round" + imm)
+            v = self.reg(R(s))[0]
+            lanes = list(self.reg(R(o)))
+            lanes[0] = self.mk(mode, [v], v.ty)
+            self.regs[R(d)] = lanes
+            return
+        if ins in ("vucomiss", "vcomiss", "vucomisd", "vcomisd"):
+            a, b = ops
+            ty = "f32" if ins.endswith("ss") else "f64"
+            va = self.reg(R(a))[0] if X(a) else self.load_scalar(a, reloc, ty)
+            vb = self.reg(R(b))[0]
+            self.event("cmp", vb, va, extra="(first ? second; branch follows)")
+            return
+        if ins in ("mov", "movl", "movq", "movabs", "lea"):
+            src, dst = ops
+            if ins == "lea":
+                self.gpr[R(dst)] = self.addr(src, reloc)
+                return
+            if src.startswith("$"):
+                imm = int(src[1:], 16)
+                if dst.startswith("%"):
+                    self.gpr[R32.get(R(dst), R(dst))] = ("imm", imm)
+                    return
+                a = self.addr(dst, reloc)
+                if ins == "movl":
+                    self.mem[(a[0], a[1])] = self.const(struct.unpack("<f", struct.pack("<I", imm & 0xffffffff))[0], "f32")
+                else:
+                    lo = imm & 0xffffffff
+                    hi = (imm >> 32) & 0xffffffff if imm >= 0 else 0xffffffff
+                    self.mem[(a[0], a[1])] = self.const(struct.unpack("<f", struct.pack("<I", lo))[0], "f32")
+                    self.mem[(a[0], a[1] + 4)] = self.const(struct.unpack("<f", struct.pack("<I", hi))[0], "f32")
+                return
+            if src.startswith("%") and dst.startswith("%"):
+                s = R32.get(R(src), R(src))
+                self.gpr[R32.get(R(dst), R(dst))] = self.gpr.get(s, ("arg_" + s, 0))
+                return
+            if dst.startswith("%"):
+                d = R(dst)
+                a = self.addr(src, reloc)
+                if a[0] == "const":
+                    self.gpr[R32.get(d, d)] = ("got:" + str(reloc), 0)
+                    return
+                if d in R32:
+                    self.gpr[R32[d]] = ("m32", self.load32(a) if a[0] != "const" else None)
+                else:
+                    self.gpr[d] = (f"*({a[0]}+0x{a[1]:x})" if a[0] != "dyn" else a[1], 0)
+                return
+            s = R(src)
+            a = self.addr(dst, reloc)
+            g = self.gpr.get(R32.get(s, s))
+            if s in R32 and g and g[0] == "m32":
+                self.mem[(a[0], a[1])] = g[1]
+            elif g and g[0] == "imm":
+                self.mem[(a[0], a[1])] = self.const(struct.unpack("<f", struct.pack("<I", g[1] & 0xffffffff))[0], "f32")
+                if s not in R32:
+                    hi = (g[1] >> 32) & 0xffffffff
+                    self.mem[(a[0], a[1] + 4)] = self.const(struct.unpack("<f", struct.pack("<I", hi))[0], "f32")
+            return
+        if ins.startswith("call"):
+            self.ncall += 1
+            callee = (reloc or " ".join(ops)).split("(")[0].replace("-0x4", "").split("::")[-1]
+            tag = f"{callee}#{self.ncall}"
+            self.event("call", extra=tag)
+            for k in range(32):
+                self.regs.pop(f"xmm{k}", None)
+            dret = any(k in callee for k in ("normL2Sqr", "sqrt", "pow", "log", "exp"))
+            self.regs["xmm0"] = ([self.inp(f"{tag}.xmm0d", "f64")] if dret else
+                                 [self.inp(f"{tag}.xmm0[{k}]", "f32") for k in range(4)]) + [None] * 4
+            self.regs["xmm1"] = [self.inp(f"{tag}.xmm1[{k}]", "f32") for k in range(4)] + [None] * 4
+            rdi = self.gpr.get("rdi")
+            # a callee returning a class by value writes it through the hidden pointer in rdi
+            # (Matx33f, Point2f); normL2Sqr only reads its rdi argument
+            sret = "normL2Sqr" not in callee
+            if sret and rdi and isinstance(rdi[1], int) and rdi[0] in ("rsp", "arg_rbp", "rbp"):
+                for k in range(16):
+                    self.mem[(rdi[0], rdi[1] + 4 * k)] = self.inp(f"{tag}.out[{k}]", "f32")
+            return
+        if ins in ("ret", "retq"):
+            self.event("ret", *(x for x in [self.regs.get("xmm0", [None])[0]] if x is not None))
+            return
+        # control flow / integer ops are not followed
+
+    # ---- printing ----
+    def expr(self, n):
+        a = [self.name_of(x) for x in n.args]
+        fm = "fmaf" if n.ty == "f32" else "fma"
+        if n.op == "fma":
+            return f"{fm}({a[0]}, {a[1]}, {a[2]})"
+        if n.op in "+-*/":
+            return f"{a[0]} {n.op} {a[1]}"
+        if n.op == "neg":
+            return f"-{a[0]}"
+        if n.op == "cvt":
+            return f"({'double' if n.ty == 'f64' else 'float'}){a[0]}"
+        return f"{n.op}({', '.join(a)})"
+
+    def report(self):
+        self.counter = 0
+        out = []
+
+        def need(n):
+            if n is None or n.op in ("in", "const") or n.id is not None:
+                return
+            for a in n.args:
+                need(a)
+            self.counter += 1
+            n.id = f"t{self.counter}"
+            out.append(f"  {n.id:>5} : {n.ty} = {self.expr(n)}")
+
+        for kind, nodes, extra in self.events:
+            for n in nodes:
+                need(n)
+            out.append(f"  {kind:>5} : {', '.join(self.name_of(n) for n in nodes)} {extra}")
+        return "\n".join(out)
+
+    def name_of(self, n):
+        if n is None:
+            return "?"
+        if n.op == "in":
+            return n.name
+        if n.op == "const":
+            return n.name + ("f" if n.ty == "f32" else "")
+        return n.id
+
+
+def read_range(obj, func, start, end):
+    out = subprocess.run(["objdump", "-d", "-C", "-r", "--no-show-raw-insn", "-j", ".text",
+                          f"--start-address={start}", f"--stop-address={end}", obj],
+                         capture_output=True, text=True, check=True).stdout
+    res = []
+    pending = None
+    for line in out.splitlines():
+        m = re.match(r"^\s+([0-9a-f]+):\s+(\S+)\s*(.*)$", line)
+        if not m:
+            continue
+        if m.group(2).startswith("R_X86_64"):
+            if pending is not None:
+                pending[3] = m.group(3).strip()
+            continue
+        ins = m.group(2)
+        rest = m.group(3).split("#")[0].strip()
+        ops = re.findall(r"(?:[^,(]|\([^)]*\))+", rest) if rest else []
+        ops = [o.strip() for o in ops]
+        pending = [int(m.group(1), 16), ins, ops, None]
+        res.append(pending)
+    return res
+
+
+def trace(obj, ranges, names=None):
+    """Walk the address ranges ["0xA:0xB", ...] of obj in order; returns the Tracer."""
+    t = Tracer(obj, names or {})
+    for r in ranges:
+        a, b = r.split(":")
+        t.run(read_range(obj, None, a, b))
+    for k in range(32):
+        lanes = t.regs.get(f"xmm{k}")
+        if lanes and lanes[0] is not None and lanes[0].op not in ("in", "const"):
+            t.event("live", lanes[0], extra=f"%xmm{k}")
+    return t
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("obj")
+    ap.add_argument("ranges", nargs="+", help="START:END address ranges, walked in order")
+    ap.add_argument("--names", default="")
+    args = ap.parse_args()
+    names = dict(kv.split("=", 1)[::-1] for kv in args.names.split(",") if kv)
+    print(trace(args.obj, args.ranges, names).report())
+
+
+if __name__ == "__main__":
+    main()
+
+
+# ---------------------------------------------------------------------------------------------
+# C emission (for tests/test_fp_sites.py): the traced data flow as a C function
+#     void NAME(const double* in, double* out)
+# in[k] = the k-th named input (converted to its traced type), out[k] = the k-th selected value
+# (an event operand) widened to double.  Every operation is spelled out (fmaf / fma, casts), and
+# the file must be compiled with -ffp-contract=off.
+def emit_c(tr: Tracer, fname: str, inputs: list[str], outputs: list[tuple[str, int]]) -> str:
+    byname = {}
+    for n in tr.nodes:
+        if n.op == "in":
+            byname.setdefault(n.name, n)
+    sel = []
+    for kind_key, idx in outputs:
+        # kind_key: "store:LOC", "cmp#K", "live:%xmmN", "ret", "int#K"
+        found = None
+        if kind_key.startswith("cmp#") or kind_key.startswith("int#"):
+            kind, k = kind_key.split("#")
+            evs = [e for e in tr.events if e[0] == kind]
+            found = evs[int(k)][1][idx]
+        else:
+            kind, _, loc = kind_key.partition(":")
+            for e in tr.events:
+                if e[0] == kind and (not loc or e[2] == loc):
+                    found = e[1][idx]
+                    break
+        if found is None:
+            raise KeyError(kind_key)
+        sel.append(found)
+    ctype = {"f32": "float", "f64": "double", "i32": "int"}
+    lines = [f"void {fname}(const double* in, double* out) {{"]
+    names = {}
+    for k, nm in enumerate(inputs):
+        n = byname.get(nm)
+        if n is None:
+            continue
+        names[id(n)] = f"i{k}"
+        lines.append(f"    const {ctype[n.ty]} i{k} = ({ctype[n.ty]})in[{k}];")
+    cnt = [0]
+
+    def ref(n):
+        if id(n) in names:
+            return names[id(n)]
+        if n.op == "const":
+            return f"(({ctype[n.ty]}){float(n.name)!r})"
+        if n.op == "in":
+            raise KeyError(f"unbound input {n.name}")
+        a = [ref(x) for x in n.args]
+        cnt[0] += 1
+        v = f"v{cnt[0]}"
+        t = ctype[n.ty]
+        if n.op == "fma":
+            e = f"{'fmaf' if n.ty == 'f32' else 'fma'}({a[0]}, {a[1]}, {a[2]})"
+        elif n.op in "+-*/":
+            e = f"{a[0]} {n.op} {a[1]}"
+        elif n.op == "neg":
+            e = f"-{a[0]}"
+        elif n.op == "cvt":
+            e = f"({t}){a[0]}"
+        elif n.op == "sqrt":
+            e = f"{'sqrtf' if n.ty == 'f32' else 'sqrt'}({a[0]})"
+        elif n.op == "fabs":
+            e = f"{'fabsf' if n.ty == 'f32' else 'fabs'}({a[0]})"
+        elif n.op in ("ceil", "floor", "trunc", "rint"):
+            e = f"{n.op}{'f' if n.ty == 'f32' else ''}({a[0]})"
+        elif n.op == "i2f":
+            e = f"({t}){a[0]}"
+        else:
+            raise ValueError(n.op)
+        lines.append(f"    const {t} {v} = {e};")
+        names[id(n)] = v
+        return v
+
+    for k, n in enumerate(sel):
+        lines.append(f"    out[{k}] = (double){ref(n)};")
+    lines.append("}")
+    return "\n".join(lines)
