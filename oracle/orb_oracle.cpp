@@ -483,7 +483,12 @@ void gaussian_blur7(const uint8_t* src, int w, int h, size_t sstep, uint8_t* dst
 // ---------------------------------------------------------------- rBRIEF
 // computeOrbDescriptor, ORBextractor.cc:106-145.  The reference binary computes
 // a=cos, b=sin through glibc sincosf and contracts the rotation into FMAs:
-// row = rne(fmaf(x, b, y*a)), col = rne(fmaf(x, a, -(y*b))).
+// row = rne(fmaf(x, b, y*a)), col = rne(fmaf(x, a, -(y*b))) (ORBextractor.cc.o @0x6ac5..0x6adb).
+inline void orb_sample_rc(float x, float y, float a, float b, int* r, int* c) {
+    *r = cv_round(std::fmaf(x, b, y * a));
+    *c = cv_round(std::fmaf(x, a, -(y * b)));
+}
+
 void orb_descriptor(const Image& blurred, const Kp& kp, uint8_t* desc) {
     const float factor_pi = (float)(M_PI / 180.f);
     const float angle = kp.angle * factor_pi;
@@ -497,10 +502,9 @@ void orb_descriptor(const Image& blurred, const Kp& kp, uint8_t* desc) {
         for (int bit = 0; bit < 8; ++bit, pat += 4) {
             const float x0 = (float)pat[0], y0 = (float)pat[1];
             const float x1 = (float)pat[2], y1 = (float)pat[3];
-            const int r0 = cv_round(std::fmaf(x0, b, y0 * a));
-            const int c0 = cv_round(std::fmaf(x0, a, -(y0 * b)));
-            const int r1 = cv_round(std::fmaf(x1, b, y1 * a));
-            const int c1 = cv_round(std::fmaf(x1, a, -(y1 * b)));
+            int r0, c0, r1, c1;
+            orb_sample_rc(x0, y0, a, b, &r0, &c0);
+            orb_sample_rc(x1, y1, a, b, &r1, &c1);
             const int t0 = center[r0 * step + c0];
             const int t1 = center[r1 * step + c1];
             val |= (t0 < t1) << bit;
@@ -699,6 +703,9 @@ void oracle_gaussian_blur7(const uint8_t* src, int w, int h, size_t sstep, uint8
 float oracle_fast_atan2(float y, float x) { return fast_atan2(y, x); }
 
 void oracle_sincosf(float x, float* s, float* c) { sincosf(x, s, c); }
+
+/* The descriptor sampler's rotation for one pattern point (for tests/test_fp_sites.py). */
+void oracle_orb_sample_rc(float x, float y, float a, float b, int* r, int* c) { orb_sample_rc(x, y, a, b, r, c); }
 
 int oracle_keypoints_octree(const slam_orb_params* p, const uint8_t* img, int w, int h,
                             size_t stride, slam_keypoint* kps, int cap, int32_t* counts) {

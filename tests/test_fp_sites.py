@@ -63,6 +63,9 @@ SITES = {
     # SearchByProjection(Frame&, const Frame&, th, bMono) stereo gate (ORBmatcher.cc:2252-2258)
     "sbp_er": ("ORBmatcher.cc.o", ["0x95ac:0x95e4"],
                ["arg_rbp-0xc78", "arg_rcx+0x1a8", "arg_rbp-0xcf8", "(%rax,%rbx,4)"], [("live:%xmm0", 0)]),
+    # computeOrbDescriptor's rotated sample (ORBextractor.cc:110-118): a = cos, b = sin (sincosf)
+    "orb_rc": ("ORBextractor.cc.o", ["0x6a63:0x6adf"],
+               ["arg_rbp-0x408", "arg_rbp-0x404", "int (%rbx)", "int 0x4(%rbx)"], [("int#2", 0), ("int#3", 0)]),
     # Fuse stereo reprojection chi2 (ORBmatcher.cc:1697, 1735-1745)
     "fuse_e2": ("ORBmatcher.cc.o", ["0x1bc8:0x1c25", "0x1c60:0x1cca"],
                 ["rsp+0xa0", "rsp+0xbc", "arg_rdx+0x0", "arg_rdx+0x4", "(%rdi,%rax,4)", "rsp+0x8c", "rsp+0xa8",
@@ -209,3 +212,16 @@ def test_projection_stereo_gates(ref_lib, orc):
         assert same(r, [orc.oracle_fp_sbp_er(u, bf, invz, kpr)])
         r = call_site(ref_lib, "fuse_e2", [u, v, kpx, kpy, kpr, bf, invz, isg, u], 1)
         assert same(r, [orc.oracle_fp_fuse_e2(u, v, kpx, kpy, kpr, bf, invz, isg)])
+
+
+def test_orb_descriptor_rotation(ref_lib, orc):
+    rng = np.random.default_rng(5)
+    r, c = C.c_int(), C.c_int()
+    orc.oracle_orb_sample_rc.argtypes = [C.c_float] * 4 + [C.POINTER(C.c_int)] * 2
+    for _ in range(N * 4):
+        th = np.float32(rng.uniform(0, 360)) * np.float32(np.pi / 180)
+        a, b = np.float32(np.cos(th)), np.float32(np.sin(th))
+        x, y = (int(v) for v in rng.integers(-15, 16, 2))
+        ref = call_site(ref_lib, "orb_rc", [a, b, x, y], 2)
+        orc.oracle_orb_sample_rc(float(x), float(y), float(a), float(b), C.byref(r), C.byref(c))
+        assert list(ref) == [r.value, c.value], (ref, r.value, c.value)
