@@ -41,6 +41,12 @@ constexpr int kMaxN = 480;        // 80 free KeyFrames per window
 constexpr int kHplStride = 18;    // doubles per edge: pose-landmark block Hpl = B^T W A (6 x 3)
 constexpr int kTrStride = 24;     // doubles per edge of Schur trial output: B Dinv (18), B db (6)
 constexpr int kCtlThreads = 1024;
+// k_ldlt_t16 geometry
+constexpr int kT16Max = 18;                                  // tile rows (n <= 288)
+constexpr int kT16Waves = 16;
+constexpr int kT16Tiles = kT16Max * (kT16Max + 1) / 2;
+constexpr int kPStride = 17;                                 // panel row stride (doubles): odd, no bank conflicts
+
 typedef double double4_t __attribute__((ext_vector_type(4)));
 
 // dense Schur system geometry: pose dimension padded to a multiple of kNB, rhs in row npad
@@ -488,6 +494,19 @@ __device__ __forceinline__ int xcd_swizzle(int orig, int nwg) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
 }
 
+// tile-major scratch of k_ldlt_t16 (see there): window w's tiles start at w * kT16Tiles * 256
+// doubles, column-major over tile columns; element (R, C), R >= C, of the lower triangle goes to
+// tile (R >> 4, C >> 4) in the transposed accumulator layout (lane (R & 15) + 16 (C & 3),
+// register (C & 15) >> 2), and for a diagonal tile also to its mirror (C, R).
+__device__ __forceinline__ long long blockIdx_win_tiles(int win) { return (long long)win * kT16Tiles * 256; }
+__device__ __forceinline__ void t16_put(double* Tw, int n, int R, int Cc, double v) {
+    const int T = (n + 15) >> 4, I = R >> 4, J = Cc >> 4;
+    const int t = J * T - J * (J - 1) / 2 + (I - J);
+    const int r = R & 15, c = Cc & 15;
+    Tw[256LL * t + 4 * (r + 16 * (c & 3)) + (c >> 2)] = v;
+    if (I == J && r != c) Tw[256LL * t + 4 * (c + 16 * (r & 3)) + (r >> 2)] = v;
+}
+
 template <int NL>
 __global__ void __launch_bounds__(256) k_schur_block(int nlist, const int* __restrict__ order,
                                                      const int2* __restrict__ blk_pose,
@@ -496,7 +515,8 @@ __global__ void __launch_bounds__(256) k_schur_block(int nlist, const int* __res
                                                      const WinCtl* __restrict__ ctl, const double* __restrict__ Hpp,
                                                      const double* __restrict__ bp, const int* __restrict__ pe_off,
                                                      const int* __restrict__ pe, const double* __restrict__ lin,
-                                                     const double* __restrict__ tr, double* __restrict__ Hs) {
+                                                     const double* __restrict__ tr, double* __restrict__ Hs,
+                                                     double* __restrict__ Ts) {
     const int wg = xcd_swizzle((int)blockIdx.x, (int)gridDim.x);
     const int idx = wg * (256 / NL) + threadIdx.x / NL, lane = threadIdx.x % NL;
     const bool live = idx < nlist;
@@ -568,7 +588,10 @@ __global__ void __launch_bounds__(256) k_schur_block(int nlist, const int* __res
             if (k == e) m = acc[k];
         v -= m;
         // upper (i1, i2)[r][c] -> lower element (6 i2 + c, 6 i1 + r)
-        if (i1 != i2 || r <= c) H[(long long)(6 * i2 + c) * W.ld + 6 * i1 + r] = v;
+        if (i1 != i2 || r <= c) {
+            if (Ts) t16_put(Ts + (long long)blockIdx_win_tiles(win), W.n, 6 * i2 + c, 6 * i1 + r, v);
+            else H[(long long)(6 * i2 + c) * W.ld + 6 * i1 + r] = v;
+        }
     }
     if (i1 == i2 && lane < 6) {
         double s6 = 0.0;
@@ -797,6 +820,289 @@ __global__ void __launch_bounds__(512) k_ldlt(const WinDesc* __restrict__ wins, 
     if (tid == 0) C.ok2 = 1;
 }
 
+// Tile LDL^T for windows with n <= 288 (48 free KeyFrames): one 1024-thread workgroup per
+// window, the lower triangle of the Schur system as 16x16 FP64 tiles in a tile-major scratch
+// (2 KB per tile, 32 contiguous bytes per lane: every tile load / store is fully coalesced and
+// stays in the XCD's L2 — 342 KB per window at n = 288), the panel and the rhs in LDS.  A tile
+// (i, j) is held TRANSPOSED in the v_mfma_f64_16x16x4_f64 accumulator layout (lane l, register
+// u = A_ij[l & 15][(l >> 4) + 4u]); in that form register u is directly the operand of k-step u
+// of both products below, so no tile is transposed through LDS.
+// Per 16-column panel k:
+//   (3) tiles (i, k), i > k: W_ik^T = M_k^T A_ik^T (4 MFMAs), W_ik to the LDS panel,
+//       L_ik = W_ik D^-1 back to the scratch, y_i -= L_ik D (M_k^T y_k);
+//   (4) tiles (i, j), i >= j > k: A_ij^T -= W_jk D^-1 W_ik^T (4 MFMAs, both operands from the
+//       panel), waves 1..15 round-robin with the next tile's load in flight, while wave 0
+//       updates the next diagonal tile and factors it (look-ahead, t16_diag: Gauss elimination
+//       of [A_kk | I], DPP row broadcasts, giving D, M_{k+1} = L^-T and z_{k+1} = D^-1 L^-1 y).
+// Then L^T x = z right-looking: x_k = M_k z_k by one wave, tile (k, j) owners subtract
+// L_kj^T x_k from z_j (DPP 16-lane sums).  A zero pivot fails the solve, like Eigen's
+// SimplicialLDLT.  The serial 16-pivot diagonal factorization is the critical path
+// (tools/microbench/mb_ldlt, mb_diag).
+struct T16Lds {
+    double D[256];                         // diagonal tile of the current panel (row-major)
+    double M[kT16Max][256];                // M_k = L_kk^-T per panel (row-major)
+    double dinv[kT16Max][16];              // 1 / d per panel
+    double P[kT16Max][16 * kPStride];      // W_ik of the current panel, row-major with stride 17
+    double y[kT16Max * 16];                // b_s, then z, then the back-substitution right-hand side
+    double wb[16];                         // M_k^T y_k of the current panel
+    double xk[16];
+    unsigned short tij[kT16Tiles];         // tile list, column-major: (i << 8) | j
+    unsigned short col0[kT16Max + 1];      // first tile of column j
+    int fail;
+};
+__host__ __device__ constexpr long long t16_tiles_bytes() { return (long long)kT16Tiles * 256 * sizeof(double); }
+
+template <int R>
+__device__ __forceinline__ double row_ror(double v) {  // DPP row_ror:R on both halves of a double
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x120 + R, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x120 + R, 0xf, 0xf, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ double t16_sum16(double v) {  // sum over the 16 lanes of a DPP row (every lane)
+    v += row_ror<8>(v);
+    v += row_ror<4>(v);
+    v += row_ror<2>(v);
+    v += row_ror<1>(v);
+    return v;
+}
+
+#ifdef LBA_PHASE_TIMING
+__device__ unsigned long long g_t16_phase[8];
+#define T16_MARK(i)                                                          \
+    do {                                                                     \
+        if (threadIdx.x == 0 && blockIdx.x == 0) {                           \
+            const unsigned long long now = wall_clock64();                   \
+            if ((i) > 0) g_t16_phase[(i)] += now - g_t16_phase[0];           \
+            g_t16_phase[0] = now;                                            \
+        }                                                                    \
+    } while (0)
+#else
+#define T16_MARK(i) \
+    do {            \
+    } while (0)
+#endif
+
+__device__ __forceinline__ double4_t t16_load(const double* tile, int lane) {
+    return *(const double4_t*)(tile + 4 * lane);
+}
+__device__ __forceinline__ void t16_store(double* tile, int lane, double4_t v) { *(double4_t*)(tile + 4 * lane) = v; }
+
+// lane J of every 16-lane DPP row, to the whole row (v_mov_b64 DPP row_newbcast, gfx90a+)
+template <int J>
+__device__ __forceinline__ double row_bcast(double v) {  // DPP row_newbcast (64-bit DPP, gfx90a+)
+    return __longlong_as_double(__builtin_amdgcn_update_dpp(0LL, __double_as_longlong(v), 0x150 + J, 0xf, 0xf, false));
+}
+// 1/d: v_rcp_f64 and two Newton steps (the pivot reciprocal is on the serial chain; within
+// the LBA tolerance it equals the divided value)
+__device__ __forceinline__ double rcp_nr(double d) {
+    double x = __builtin_amdgcn_rcp(d);
+    x = __builtin_fma(x, __builtin_fma(-d, x, 1.0), x);
+    x = __builtin_fma(x, __builtin_fma(-d, x, 1.0), x);
+    return x;
+}
+
+// one pivot step J of t16_diag (compile-time J: DPP row_newbcast takes an immediate lane).
+// Lane (r = lane & 15, g = lane >> 4) holds 8 values of row r: g = 0 / 1 columns 0-7 / 8-15 of
+// A, g = 2 / 3 the same of I.  Every group updates all its columns with the pivot row of its own
+// group (A columns <= J hold leftovers that are never read again; I columns > J of the pivot row
+// are zero), so only rows r <= J need masking, through a zero multiplier.  Measured 2.3 us per
+// tile (tools/microbench/mb_diag).
+template <int J>
+__device__ __forceinline__ void t16_pivot(double (&row)[8], int r, int g, int lane, bool& bad, double* dinv) {
+    constexpr int gs = J >> 3, e = J & 7;      // the group / element holding column J of A
+    const double dj = readlane_d(row[e], 16 * gs + J);
+    if (dj == 0.0) bad = true;
+    const double inv = rcp_nr(dj);
+    const double a = row[e];                    // A[r][J] in group gs
+    // A[r][J] from group gs to all four groups of row r: one ds_bpermute (all lanes active; it
+    // measured 2.3 us per diagonal tile against 3.4 us for v_permlane16/32_swap chains)
+    const double arj = __shfl(a, 16 * gs + r);
+    const double m = r > J ? arj * inv : 0.0;
+#pragma unroll
+    for (int c = 0; c < 8; c++) row[c] = __builtin_fma(-m, row_bcast<J>(row[c]), row[c]);
+    if (lane == J) dinv[J] = inv;
+    if constexpr (J + 1 < 16) t16_pivot<J + 1>(row, r, g, lane, bad, dinv);
+}
+
+// The diagonal tile of panel k (held by wave 0 in the transposed accumulator layout, which for
+// a symmetric tile is the tile itself): Gauss elimination of [A_kk | I] without pivoting, the
+// four 16-lane groups of wave 0 holding A columns 0-7, 8-15 and I columns 0-7, 8-15 of row
+// lane & 15.  The A half ends as D L^T (pivots d_j), the I half as L^-1 = M_k^T.  Then
+// z_k = D^-1 M_k^T y_k.
+template <class Lds>
+__device__ __forceinline__ void t16_diag(Lds& L, int k, double4_t dt, int lane) {
+    const int lr = lane & 15, lq = lane >> 4;
+#pragma unroll
+    for (int u = 0; u < 4; u++) L.D[lr * 16 + lq + 4 * u] = dt[u];
+    wave_sync();
+    const int r = lane & 15, g = lane >> 4;
+    double row[8];
+#pragma unroll
+    for (int c = 0; c < 8; c++) {
+        const int col = 8 * (g & 1) + c;
+        row[c] = g < 2 ? L.D[r * 16 + col] : (col == r ? 1.0 : 0.0);
+    }
+    bool bad = false;
+    t16_pivot<0>(row, r, g, lane, bad, L.dinv[k]);
+    if (bad && lane == 0) L.fail = 1;
+    if (g >= 2) {
+#pragma unroll
+        for (int c = 0; c < 8; c++) L.M[k][(8 * (g & 1) + c) * 16 + r] = row[c];  // M_k[col][r] = L^-1[r][col]
+    }
+    wave_sync();
+    if (lane < 16) {
+        const int c = lane;
+        double wb = 0.0;
+#pragma unroll
+        for (int rr = 0; rr < 16; rr++) wb = __builtin_fma(L.M[k][rr * 16 + c], L.y[16 * k + rr], wb);
+        L.wb[c] = wb;
+        L.y[16 * k + c] = wb * L.dinv[k][c];
+    }
+}
+
+__global__ void __launch_bounds__(kT16Waves * 64) k_ldlt_t16(const WinDesc* __restrict__ wins, WinCtl* __restrict__ ctl,
+                                                             const double* __restrict__ Hs, double* __restrict__ Ts,
+                                                             double* __restrict__ xp_out) {
+    __shared__ T16Lds L;
+    const WinDesc W = wins[blockIdx.x];
+    WinCtl& C = ctl[blockIdx.x];
+    if (!C.need_trial) return;
+    const int n = W.n, ld = W.ld, T = (n + 15) >> 4, rhs = ldlt_npad(n);
+    if (T == 0) {  // no free pose: an empty system solves trivially
+        if (threadIdx.x == 0) C.ok2 = 1;
+        return;
+    }
+    const int ntiles = T * (T + 1) / 2;
+    const double* A = Hs + W.hs_off;
+    double* Tw = Ts + blockIdx_win_tiles(blockIdx.x);
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lr = lane & 15, lq = lane >> 4;  // register u of a tile holds [lr][lq + 4u]
+    if (tid == 0) {
+        int t = 0;
+        for (int j = 0; j < T; j++) {
+            L.col0[j] = (unsigned short)t;
+            for (int i = j; i < T; i++) L.tij[t++] = (unsigned short)((i << 8) | j);
+        }
+        L.col0[T] = (unsigned short)t;
+        L.fail = 0;
+    }
+    for (int c = tid; c < 16 * T; c += blockDim.x) L.y[c] = A[(long long)rhs * ld + c];
+    __syncthreads();
+    T16_MARK(0);
+    // the tiles were written by k_schur_block (t16_put); padding by k_t16_pad
+    double4_t d0 = {0.0, 0.0, 0.0, 0.0};
+    if (wid == 0) d0 = t16_load(Tw, lane);
+    if (wid == 0) t16_diag(L, 0, d0, lane);
+    __syncthreads();
+    T16_MARK(1);
+    for (int k = 0; k < T; k++) {
+        if (L.fail) break;
+        // wave 0: the next diagonal tile (final since the previous trailing update) in flight
+        double4_t diag_next = {0.0, 0.0, 0.0, 0.0};
+        if (wid == 0 && k + 1 < T) diag_next = t16_load(Tw + 256 * L.col0[k + 1], lane);
+        const double* Mk = L.M[k];
+        const double* dk = L.dinv[k];
+        // (3) panel tiles (i, k), i > k
+        for (int t = L.col0[k] + 1 + wid; t < L.col0[k + 1]; t += kT16Waves) {
+            const int i = L.tij[t] >> 8;
+            const double4_t a = t16_load(Tw + 256 * t, lane);
+            double4_t acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Mk[(4 * u + lq) * 16 + lr], a[u], acc, 0, 0, 0);
+            double part = 0.0;  // sum_q L_ik[lr][q] (M_k^T y_k)[q] over this lane's q
+            double4_t l;
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int q = lq + 4 * u;
+                L.P[i][lr * kPStride + q] = acc[u];
+                l[u] = acc[u] * dk[q];
+                part = __builtin_fma(l[u], L.wb[q], part);
+            }
+            t16_store(Tw + 256 * t, lane, l);
+            part += __shfl_xor(part, 16);
+            part += __shfl_xor(part, 32);
+            if (lq == 0) L.y[16 * i + lr] -= part;
+        }
+        __syncthreads();
+        T16_MARK(3);
+        // (4) trailing tiles of columns k+1 .. T-1.  Wave 0 takes the next diagonal tile first and
+        // factors it while the other waves update the rest (look-ahead); they keep the next
+        // tile's load in flight.
+        auto update = [&](int t, double4_t cur) -> double4_t {
+            const int i = L.tij[t] >> 8, j = L.tij[t] & 255;
+            double4_t acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int q = 4 * u + lq;
+                const double a = L.P[j][lr * kPStride + q] * dk[q];
+                const double b = L.P[i][lr * kPStride + q];
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+            }
+            const double4_t v = cur - acc;
+            t16_store(Tw + 256 * t, lane, v);
+            return v;
+        };
+        const int t0 = L.col0[k + 1];
+        if (k + 1 < T) {
+            if (wid == 0) {
+                T16_MARK(0);
+                __builtin_amdgcn_s_setprio(3);  // the critical path: ahead of the trailing MFMA waves
+                const double4_t dn = update(t0, diag_next);
+                T16_MARK(6);
+                t16_diag(L, k + 1, dn, lane);
+                __builtin_amdgcn_s_setprio(0);
+                T16_MARK(7);
+            } else {
+                int t = t0 + wid;
+                double4_t cur = t < ntiles ? t16_load(Tw + 256 * t, lane) : double4_t{0.0, 0.0, 0.0, 0.0};
+                while (t < ntiles) {
+                    const int tn = t + kT16Waves - 1;
+                    const double4_t nxt = tn < ntiles ? t16_load(Tw + 256 * tn, lane) : double4_t{0.0, 0.0, 0.0, 0.0};
+                    update(t, cur);
+                    cur = nxt;
+                    t = tn;
+                }
+            }
+        }
+        __syncthreads();
+        T16_MARK(4);
+    }
+    if (L.fail) {
+        if (tid == 0) C.ok2 = 0;
+        return;
+    }
+    // L^T x = z, right-looking from the last tile column; wave w handles tiles (k, w) (and
+    // (k, w + 16) when k > 16), the next step's tile loaded before the barrier
+    double4_t nxt = wid < T - 1 ? t16_load(Tw + 256 * (L.col0[wid] + (T - 1) - wid), lane) : double4_t{0.0, 0.0, 0.0, 0.0};
+    for (int k = T - 1; k >= 0; k--) {
+        if (wid == 0 && lane < 16) {
+            const double* Mk = L.M[k];
+            double x = 0.0;
+#pragma unroll
+            for (int r = 0; r < 16; r++) x = __builtin_fma(Mk[lane * 16 + r], L.y[16 * k + r], x);
+            L.xk[lane] = x;
+            if (16 * k + lane < n) xp_out[6 * (long long)W.pose0 + 16 * k + lane] = x;
+        }
+        const double4_t cur = nxt;
+        if (k >= 1 && wid < k - 1) nxt = t16_load(Tw + 256 * (L.col0[wid] + (k - 1) - wid), lane);
+        __syncthreads();
+        for (int j = wid; j < k; j += kT16Waves) {  // tile (k, j) holds L_kj
+            const double4_t l = j == wid ? cur : t16_load(Tw + 256 * (L.col0[j] + k - j), lane);
+            const double xr = L.xk[lr];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const double sum = t16_sum16(l[u] * xr);
+                if (lr == 0) L.y[16 * j + lq + 4 * u] -= sum;
+            }
+        }
+        __syncthreads();
+    }
+    T16_MARK(5);
+    if (tid == 0) C.ok2 = 1;
+}
+
 // Identity padding of the dense systems (rows/cols n..npad-1) and a zero rhs tail; the
 // factorization keeps it invariant, so it is written once per solve.
 __global__ void k_ldlt_pad(const WinDesc* __restrict__ wins, double* __restrict__ Hs) {
@@ -807,6 +1113,15 @@ __global__ void k_ldlt_pad(const WinDesc* __restrict__ wins, double* __restrict_
         for (int j = 0; j <= i; j++) A[(long long)i * ld + j] = (i == j) ? 1.0 : 0.0;
         A[(long long)npad * ld + i] = 0.0;
     }
+}
+
+// Identity padding of the tile scratch (rows / columns n .. 16T-1 of the last tile row): the
+// scratch is zeroed once per solve and k_schur_block rewrites every real element each trial;
+// the factorization leaves the padding invariant (its W rows are zero).
+__global__ void k_t16_pad(const WinDesc* __restrict__ wins, double* __restrict__ Ts) {
+    const WinDesc W = wins[blockIdx.x];
+    const int T = (W.n + 15) >> 4;
+    for (int R = W.n + (int)threadIdx.x; R < 16 * T; R += blockDim.x) t16_put(Ts + blockIdx_win_tiles(blockIdx.x), W.n, R, R, 1.0);
 }
 
 // x_l = Dinv (b_l - Hpl^T x_p) (block_solver.hpp:456-481) and the trial point estimate.
@@ -1110,7 +1425,7 @@ struct slam_lba {
     unsigned char* harena = nullptr;  // pinned
     size_t harena_cap = 0;
     DevBuf arena, cnt;
-    DevBuf poses, pts, err, rho, lin, Hll, bl, Hpp, bp, tr, xp, xl, Hs;
+    DevBuf poses, pts, err, rho, lin, Hll, bl, Hpp, bp, tr, xp, xl, Hs, Ts;
     DevBuf kf_out, pt_out, outl;
 };
 
@@ -1512,7 +1827,11 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     SLAM_HIP_TRY(s->Hpp.ensure(sizeof(double) * 24 * nps));
     SLAM_HIP_TRY(s->bp.ensure(sizeof(double) * 8 * nps));
     SLAM_HIP_TRY(s->xp.ensure(sizeof(double) * 6 * nps));
+    // tile LDL^T (k_ldlt_t16) when every window fits 18 tile rows (SLAMHOT_LDLT=panel: old kernel)
+    const char* ldlt_env = std::getenv("SLAMHOT_LDLT");
+    const bool use_t16 = Z.max_n <= 16 * kT16Max && !(ldlt_env && !std::strcmp(ldlt_env, "panel"));
     SLAM_HIP_TRY(s->Hs.ensure(sizeof(double) * std::max<long long>(Z.hs_total, 1)));
+    if (use_t16) SLAM_HIP_TRY(s->Ts.ensure((size_t)t16_tiles_bytes() * nw));
     SLAM_HIP_TRY(s->kf_out.ensure(sizeof(float) * 16 * std::max(H.nkf, 1)));
     SLAM_HIP_TRY(s->pt_out.ensure(sizeof(float) * 3 * npt));
     SLAM_HIP_TRY(s->outl.ensure(ne));
@@ -1553,6 +1872,11 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     k_init_state<<<blocks(H.nkf + H.npt, T), T, 0, S>>>(H.nkf, H.npt, DP.kf_in, DP.pt_in,
                                                          poses, pts);
     k_ldlt_pad<<<nw, 64, 0, S>>>(dW, as<double>(s->Hs));
+    double* tiles = use_t16 ? as<double>(s->Ts) : nullptr;
+    if (use_t16) {
+        SLAM_HIP_TRY(hipMemsetAsync(s->Ts.p, 0, (size_t)t16_tiles_bytes() * nw, S));
+        k_t16_pad<<<nw, 64, 0, S>>>(dW, tiles);
+    }
     const size_t lds_bytes = ldlt_lds_bytes(Z.max_n);
     bool stopped = false;
     const int iters_of[2] = {opt->iters_first, opt->iters_second};
@@ -1581,13 +1905,17 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
                     k_schur_block<kSchurDiagLanes><<<blocks(H.npose, 256 / kSchurDiagLanes), 256, 0, S>>>(
                         H.npose, DP.blk_order, DP.blk_pose, DP.blk_win, DP.ct_off, DP.ct, dW,
                         dC, as<double>(s->Hpp), as<double>(s->bp), DP.pe_off, DP.pe,
-                        as<double>(s->lin), as<double>(s->tr), as<double>(s->Hs));
+                        as<double>(s->lin), as<double>(s->tr), as<double>(s->Hs), tiles);
                 if (H.nblk > H.npose)
                     k_schur_block<kSchurLanes><<<blocks(H.nblk - H.npose, 256 / kSchurLanes), 256, 0, S>>>(
                         H.nblk - H.npose, DP.blk_order + H.npose, DP.blk_pose, DP.blk_win, DP.ct_off, DP.ct, dW,
                         dC, as<double>(s->Hpp), as<double>(s->bp), DP.pe_off, DP.pe,
-                        as<double>(s->lin), as<double>(s->tr), as<double>(s->Hs));
-                k_ldlt<<<nw, 512, lds_bytes, S>>>(dW, dC, as<double>(s->Hs), as<double>(s->xp));
+                        as<double>(s->lin), as<double>(s->tr), as<double>(s->Hs), tiles);
+                if (use_t16)
+                    k_ldlt_t16<<<nw, kT16Waves * 64, 0, S>>>(dW, dC, as<double>(s->Hs), as<double>(s->Ts),
+                                                             as<double>(s->xp));
+                else
+                    k_ldlt<<<nw, 512, lds_bytes, S>>>(dW, dC, as<double>(s->Hs), as<double>(s->xp));
                 k_backsub<<<blocks(H.npt, T), T, 0, S>>>(H.npt, DP.spe_off, DP.spe, dE,
                                                           DP.pt_win, dC, as<double>(s->bl),
                                                           as<double>(s->Hll), as<double>(s->lin), as<double>(s->xp),

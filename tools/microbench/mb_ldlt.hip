@@ -6,6 +6,17 @@
 #include <cstdio>
 #include <random>
 
+// row-major lower triangle (identity-padded) -> the tile-major scratch k_ldlt_t16 reads
+__global__ void k_fill_tiles(const double* A, int n, int ld, double* Ts) {
+    const int T = (n + 15) >> 4;
+    for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < (long long)(16 * T) * (16 * T);
+         e += (long long)gridDim.x * blockDim.x) {
+        const int R = (int)(e / (16 * T)), C = (int)(e % (16 * T));
+        if (C > R) continue;
+        t16_put(Ts, n, R, C, R < n ? A[(long long)R * ld + C] : (R == C ? 1.0 : 0.0));
+    }
+}
+
 int main(int argc, char** argv) {
     const int n = argc > 1 ? atoi(argv[1]) : 288;
     const int reps = argc > 2 ? atoi(argv[2]) : 20;
@@ -69,6 +80,35 @@ int main(int argc, char** argv) {
         nb = std::max(nb, std::fabs(b[i]));
     }
     const double us = 1e3 * total / reps;
+    // the tile kernel on the same system (tile scratch, x)
+    double* dT;
+    hipMalloc(&dT, (size_t)t16_tiles_bytes());
+    float total16 = 0;
+    for (int r = 0; r < reps + 1; r++) {
+        if (r == 1) hipMemcpyToSymbol(HIP_SYMBOL(g_t16_phase), zero, sizeof(zero));
+        k_fill_tiles<<<256, 256>>>(dA0, n, ld, dT);
+        hipEventRecord(e0);
+        k_ldlt_t16<<<1, kT16Waves * 64>>>(dW, dC, dA0, dT, dx);
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+        float ms;
+        hipEventElapsedTime(&ms, e0, e1);
+        if (r) total16 += ms;
+    }
+    unsigned long long p16[8];
+    hipMemcpyFromSymbol(p16, HIP_SYMBOL(g_t16_phase), sizeof(p16));
+    std::vector<double> x16(n);
+    hipMemcpy(x16.data(), dx, sizeof(double) * n, hipMemcpyDeviceToHost);
+    double r16 = 0;
+    for (int i = 0; i < n; i++) {
+        double s = 0;
+        for (int j = 0; j < n; j++) s += (j <= i ? A[(size_t)i * ld + j] : A[(size_t)j * ld + i]) * x16[j];
+        r16 = std::max(r16, std::fabs(s - b[i]));
+    }
+    if (n <= 16 * kT16Max)
+        printf("n=%d t16 %.1f us  residual %.3e  phases(us): diag0 %.1f panel %.1f trailing+diag %.1f backsolve %.1f [w0: update %.1f diag %.1f]\n",
+               n, 1e3 * total16 / reps, r16 / (nb > 0 ? nb : 1), p16[1] / 100.0 / reps,
+               p16[3] / 100.0 / reps, p16[4] / 100.0 / reps, p16[5] / 100.0 / reps, p16[6] / 100.0 / reps, p16[7] / 100.0 / reps);
     // wall_clock64 runs at 100 MHz on gfx9
     printf("n=%d ldlt %.1f us  residual %.3e  phases(us): diag %.1f [load %.1f steps %.1f] rows %.1f  trailing %.1f  "
            "backsolve %.1f\n", n, us, res / nb, (ph[1] + ph[5] + ph[6]) / 100.0 / reps, ph[5] / 100.0 / reps,
