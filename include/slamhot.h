@@ -332,12 +332,16 @@ typedef struct slam_lba_problem {
     const float* edge_obs;      /* n_edge x 3: kpUn.pt.x, kpUn.pt.y, mvuRight (< 0 -> mono) */
     const float* edge_inv_sigma2; /* mvInvLevelSigma2[kpUn.octave] */
     slam_camera cam;
+    double user_lambda_init;    /* this window's pMap: > 0 sets the initial LM lambda (100 when
+                                   pMap->IsInertial(), Optimizer.cc:1726-1727); 0 -> the options value */
 } slam_lba_problem;
 
 typedef struct slam_lba_options {
     int32_t iters_first;        /* 5  (Optimizer.cc:1926) */
     int32_t iters_second;       /* 10 (Optimizer.cc:1986) */
     double user_lambda_init;    /* 0 -> tau * max diag(H); 100 if pMap->IsInertial() (:1726) */
+    const volatile uint8_t* stop_flag_bool; /* optional: the caller's `bool* pbStopFlag` itself (a C++
+                                   bool is one byte), polled live like the int32 stop_flag */
 } slam_lba_options;
 
 typedef struct slam_lba_result {
@@ -357,9 +361,14 @@ typedef struct slam_lba slam_lba;
 /* A solver handle keeps device buffers sized for the largest batch seen (grown on demand). */
 slam_status slamhot_lba_create(int device, slam_lba** out);
 void slamhot_lba_destroy(slam_lba* s);
-/* Solve n_prob independent windows.  stop_flag (may be NULL) is the pbStopFlag: it is read
- * between LM trials and, when non-zero, ends every window's optimize() as
- * SparseOptimizer::terminate() does (sparse_optimizer.h:188, Optimizer.cc:1929-1934). */
+/* Solve n_prob independent windows.  stop_flag (may be NULL; or options->stop_flag_bool) is the
+ * pbStopFlag, and it is LIVE: the calling thread polls it while the device works and mirrors it
+ * into pinned memory that the LM control kernel reads at the end of every trial, so a flag set
+ * by another thread during the solve (LocalMapping.cc:300 mbAbortBA) ends every window's
+ * optimize() at its next trial, as SparseOptimizer::terminate() does (sparse_optimizer.h:188,
+ * sparse_optimizer.cpp:376, optimization_algorithm_levenberg.cpp:149); a flag set before the call
+ * returns at once with nothing written back but the copied inputs (Optimizer.cc:1921-1923), and one
+ * set during the first optimize(5) skips the second (Optimizer.cc:1933-1935). */
 slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* probs,
                               const slam_lba_options* opt, const volatile int32_t* stop_flag,
                               slam_lba_result* results);

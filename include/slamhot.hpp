@@ -277,6 +277,7 @@ class LocalBundleAdjuster {
             p.edge_obs = w.edge_obs.data();
             p.edge_inv_sigma2 = w.edge_inv_sigma2.data();
             p.cam = w.cam;
+            p.user_lambda_init = w.inertial ? 100.0 : 0.0;  // this window's pMap->IsInertial() (:1726)
             out[i].kf_Tcw.resize(w.kf_Tcw.size());
             out[i].pt_pos.resize(w.pt_pos.size());
             out[i].edge_outlier.resize(w.edge_pt.size());
@@ -288,14 +289,12 @@ class LocalBundleAdjuster {
         slam_lba_options opt{};
         opt.iters_first = 5;
         opt.iters_second = 10;
-        opt.user_lambda_init = (n > 0 && ws[0].inertial) ? 100.0 : 0.0;
-        volatile int32_t stop = 0;
-        // the reference polls *pbStopFlag between trials; the ABI polls an int32 the same way
+        opt.user_lambda_init = 0.0;  // per window below
+        // the reference's `bool* pbStopFlag` itself: the solver reads it live (a C++ bool is one
+        // byte), so LocalMapping setting mbAbortBA mid-solve stops the LM loop as in g2o
+        static_assert(sizeof(bool) == 1, "slam_lba_options::stop_flag_bool expects a one-byte bool");
+        opt.stop_flag_bool = reinterpret_cast<const volatile uint8_t*>(pbStopFlag);
         const volatile int32_t* sf = nullptr;
-        if (pbStopFlag) {
-            stop = *pbStopFlag ? 1 : 0;
-            sf = &stop;
-        }
         check(slamhot_lba_solve(s_, n, probs.data(), &opt, sf, res.data()), "LocalBundleAdjustment");
         for (int i = 0; i < n; i++) {
             out[i].iterations[0] = res[i].iterations[0];

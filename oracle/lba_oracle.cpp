@@ -510,9 +510,10 @@ int oracle_lba_solve(const slam_lba_problem* P, const slam_lba_options* opt, int
         return 0;
     }
     double cf = 0;
+    const double ul = P->user_lambda_init > 0 ? P->user_lambda_init : opt->user_lambda_init;
     // an empty graph makes initializeOptimization / optimize fail (sparse_optimizer.cpp:282-285)
-    if (ne > 0) R->iterations[0] = S.optimize(opt->iters_first, opt->user_lambda_init, &R->chi2_initial, &cf);
-    if (!S.stop && ne > 0) R->iterations[1] = S.optimize(opt->iters_second, opt->user_lambda_init, nullptr, &cf);
+    if (ne > 0) R->iterations[0] = S.optimize(opt->iters_first, ul, &R->chi2_initial, &cf);
+    if (!S.stop && ne > 0) R->iterations[1] = S.optimize(opt->iters_second, ul, nullptr, &cf);
     R->chi2_final = cf;
     R->lambda_final = S.lambda;
     R->trials = S.trials;

@@ -76,7 +76,7 @@ struct WinDesc {
 
 struct WinCtl {
     double lambda, ni, cur_chi, ini_chi, chi2_initial, chi2_final, user_lambda, tmp_chi;
-    int sel, active, need_trial, ok2;
+    int sel, active, need_trial, ok2, need_lin;
     int qmax, nbad, it, iters;
     int trials, opt, result, n_outlier;
     int iters_run[2];
@@ -201,16 +201,15 @@ __device__ inline void edge_jacobians(bool stereo, const Cam& cam, const double*
 // its edges in insertion order.  Per edge: computeError (error, robust rho) and the
 // pose-landmark block Hpl = B^T W A (constructQuadraticForm's transposed-block write,
 // base_binary_edge.hpp:88-112); per point: Hll = sum A^T W A and b_l = sum A^T (-rho' Omega e).
-__global__ void __launch_bounds__(128) k_lin_points(int npt_total, const int* __restrict__ pt_off, const int* __restrict__ pt_win,
+__device__ __forceinline__ void lin_points_body(int p, int npt_total, const int* __restrict__ pt_off, const int* __restrict__ pt_win,
                              const EdgeS* __restrict__ E, const WinCtl* __restrict__ ctl,
                              const double* __restrict__ poses, const double* __restrict__ pts,
                              long long pose_stride, long long pt_stride, Cam cam, Huber hk,
                              double* __restrict__ err_out, double* __restrict__ rho_out,
                              double* __restrict__ Hpl_out, double* __restrict__ Hll, double* __restrict__ bl) {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= npt_total) return;
     const WinCtl& C = ctl[pt_win[p]];
-    if (!C.active) return;
+    if (!C.need_lin) return;
     const double* Xw = pts + C.sel * pt_stride + 4 * (long long)p;
     const double X[3] = {Xw[0], Xw[1], Xw[2]};
     double h[6] = {0, 0, 0, 0, 0, 0}, bb[3] = {0, 0, 0};
@@ -275,16 +274,15 @@ __device__ inline double wave_sum(double v) {
 // Pose side of buildSystem: one wave per free KeyFrame, lanes stride over its edges and
 // recompute error, robust weight and the pose Jacobian B; Hpp = sum B^T W B,
 // b_p = sum B^T (-rho' Omega e), then a butterfly reduction of the 27 sums.
-__global__ void __launch_bounds__(256) k_lin_poses(int npose_total, const int* __restrict__ pe_off,
+__device__ __forceinline__ void lin_poses_body(int pose, int lane, int npose_total, const int* __restrict__ pe_off,
                                                    const int* __restrict__ pe, const int* __restrict__ pose_win,
                                                    const EdgeS* __restrict__ E, const WinCtl* __restrict__ ctl,
                                                    const double* __restrict__ poses, const double* __restrict__ pts,
                                                    long long pose_stride, long long pt_stride, Cam cam, Huber hk,
                                                    double* __restrict__ Hpp, double* __restrict__ bp) {
-    const int pose = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (pose >= npose_total) return;
     const WinCtl& C = ctl[pose_win[pose]];
-    if (!C.active) return;
+    if (!C.need_lin) return;
     double acc[27];
 #pragma unroll
     for (int k = 0; k < 27; k++) acc[k] = 0.0;
@@ -330,6 +328,29 @@ __global__ void __launch_bounds__(256) k_lin_poses(int npose_total, const int* _
         Hpp[24 * (long long)pose + lane] = mine;
     else if (lane < 27)
         bp[8 * (long long)pose + (lane - 21)] = mine;
+}
+
+// buildSystem in one launch: the first nb_pose blocks take the pose side (a wave per free KF,
+// two per block; the long per-KF edge loops start first), the rest the point side.
+constexpr int kLinThreads = 128;
+__global__ void __launch_bounds__(kLinThreads) k_linearize(int nb_pose, int npose_total, const int* __restrict__ pe_off,
+                                                           const int* __restrict__ pe, const int* __restrict__ pose_win,
+                                                           int npt_total, const int* __restrict__ pt_off,
+                                                           const int* __restrict__ pt_win, const EdgeS* __restrict__ E,
+                                                           const WinCtl* __restrict__ ctl, const double* __restrict__ poses,
+                                                           const double* __restrict__ pts, long long pose_stride,
+                                                           long long pt_stride, Cam cam, Huber hk,
+                                                           double* __restrict__ err_out, double* __restrict__ rho_out,
+                                                           double* __restrict__ Hpl_out, double* __restrict__ Hll,
+                                                           double* __restrict__ bl, double* __restrict__ Hpp,
+                                                           double* __restrict__ bp) {
+    const int b = blockIdx.x;
+    if (b < nb_pose)
+        lin_poses_body(b * (kLinThreads / 64) + (threadIdx.x >> 6), threadIdx.x & 63, npose_total, pe_off, pe,
+                       pose_win, E, ctl, poses, pts, pose_stride, pt_stride, cam, hk, Hpp, bp);
+    else
+        lin_points_body((b - nb_pose) * kLinThreads + threadIdx.x, npt_total, pt_off, pt_win, E, ctl, poses, pts,
+                        pose_stride, pt_stride, cam, hk, err_out, rho_out, Hpl_out, Hll, bl);
 }
 
 // deterministic block sum / max: wave butterflies, then the wave partials in wave order
@@ -379,11 +400,12 @@ __global__ void __launch_bounds__(kCtlThreads) k_iter_begin(const WinDesc* __res
                                                             WinCtl* __restrict__ ctl,
                                                             const double* __restrict__ rho,
                                                             const double* __restrict__ Hpp,
-                                                            const double* __restrict__ Hll) {
+                                                            const double* __restrict__ Hll,
+                                                            const volatile int* __restrict__ stop_dev) {
     __shared__ double sh[kCtlThreads / 64];
     const WinDesc W = wins[blockIdx.x];
     WinCtl& C = ctl[blockIdx.x];
-    if (!C.active) return;
+    if (!C.need_lin) return;
     const double chi = block_sum(strided_sum(rho + W.e0, W.ne), sh);
     double m = 0;
     if (C.it == 0) {
@@ -394,6 +416,13 @@ __global__ void __launch_bounds__(kCtlThreads) k_iter_begin(const WinDesc* __res
         m = block_max(m, sh);
     }
     if (threadIdx.x == 0) {
+        C.need_lin = 0;
+        // SparseOptimizer::optimize: no iteration once terminate() (sparse_optimizer.cpp:376).
+        // One lane reads the pinned host word (a PCIe read per block, not per thread).
+        if (*stop_dev) {
+            C.active = 0;
+            return;
+        }
         C.cur_chi = chi;
         C.ini_chi = chi;
         if (C.opt == 0 && C.it == 0) C.chi2_initial = chi;
@@ -508,7 +537,7 @@ __device__ __forceinline__ void t16_put(double* Tw, int n, int R, int Cc, double
 }
 
 template <int NL>
-__global__ void __launch_bounds__(256) k_schur_block(int nlist, const int* __restrict__ order,
+__device__ __forceinline__ void schur_block_body(int wg, int nlist, const int* __restrict__ order,
                                                      const int2* __restrict__ blk_pose,
                                                      const int* __restrict__ blk_win, const int* __restrict__ ct_off,
                                                      const int2* __restrict__ ct, const WinDesc* __restrict__ wins,
@@ -517,7 +546,6 @@ __global__ void __launch_bounds__(256) k_schur_block(int nlist, const int* __res
                                                      const int* __restrict__ pe, const double* __restrict__ lin,
                                                      const double* __restrict__ tr, double* __restrict__ Hs,
                                                      double* __restrict__ Ts) {
-    const int wg = xcd_swizzle((int)blockIdx.x, (int)gridDim.x);
     const int idx = wg * (256 / NL) + threadIdx.x / NL, lane = threadIdx.x % NL;
     const bool live = idx < nlist;
     const int b = order[live ? idx : 0];
@@ -599,6 +627,31 @@ __global__ void __launch_bounds__(256) k_schur_block(int nlist, const int* __res
         for (int r = 0; r < 6; r++)
             if (r == lane) s6 = sb[r];
         H[(long long)ldlt_npad(W.n) * W.ld + 6 * i1 + lane] = bp[8 * (long long)gp + lane] - s6;
+    }
+}
+
+// Both Schur block lists in one launch: blocks [0, nb_diag) take the npose diagonal blocks
+// (kSchurDiagLanes lanes each), the rest the off-diagonal ones; nb_diag is a multiple of 8 so
+// each part keeps its XCD-contiguous mapping.
+__global__ void __launch_bounds__(256) k_schur_blocks(int nb_diag, int nblk, int npose, const int* __restrict__ order,
+                                                      const int2* __restrict__ blk_pose,
+                                                      const int* __restrict__ blk_win, const int* __restrict__ ct_off,
+                                                      const int2* __restrict__ ct, const WinDesc* __restrict__ wins,
+                                                      const WinCtl* __restrict__ ctl, const double* __restrict__ Hpp,
+                                                      const double* __restrict__ bp, const int* __restrict__ pe_off,
+                                                      const int* __restrict__ pe, const double* __restrict__ lin,
+                                                      const double* __restrict__ tr, double* __restrict__ Hs,
+                                                      double* __restrict__ Ts) {
+    const int b = blockIdx.x;
+    if (b < nb_diag) {
+        const int wg = xcd_swizzle(b, nb_diag);
+        if (wg * (256 / kSchurDiagLanes) >= npose) return;  // padding blocks (whole block)
+        schur_block_body<kSchurDiagLanes>(wg, npose, order, blk_pose, blk_win, ct_off, ct, wins, ctl, Hpp, bp,
+                                          pe_off, pe, lin, tr, Hs, Ts);
+    } else {
+        schur_block_body<kSchurLanes>(xcd_swizzle(b - nb_diag, (int)gridDim.x - nb_diag), nblk - npose,
+                                      order + npose, blk_pose, blk_win, ct_off, ct, wins, ctl, Hpp, bp, pe_off, pe,
+                                      lin, tr, Hs, Ts);
     }
 }
 
@@ -1125,13 +1178,12 @@ __global__ void k_t16_pad(const WinDesc* __restrict__ wins, double* __restrict__
 }
 
 // x_l = Dinv (b_l - Hpl^T x_p) (block_solver.hpp:456-481) and the trial point estimate.
-__global__ void k_backsub(int npt_total, const int* __restrict__ spe_off, const int* __restrict__ spe,
+__device__ __forceinline__ void backsub_body(int p, int npt_total, const int* __restrict__ spe_off, const int* __restrict__ spe,
                           const EdgeS* __restrict__ E, const int* __restrict__ pt_win,
                           const WinCtl* __restrict__ ctl, const double* __restrict__ bl,
                           const double* __restrict__ Hll, const double* __restrict__ lin,
                           const double* __restrict__ xp, double* __restrict__ xl, double* __restrict__ pts,
                           long long pt_stride) {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= npt_total) return;
     const WinCtl& C = ctl[pt_win[p]];
     if (!C.need_trial) return;
@@ -1159,10 +1211,9 @@ __global__ void k_backsub(int npt_total, const int* __restrict__ spe_off, const 
 }
 
 // VertexSE3Expmap::oplusImpl: T <- exp(x) * T  (types_six_dof_expmap.h:71-74, se3quat.h:223-257)
-__global__ void k_pose_update(int nkf_total, const int* __restrict__ kf_hp, const int* __restrict__ kf_win,
+__device__ __forceinline__ void pose_update_body(int k, int nkf_total, const int* __restrict__ kf_hp, const int* __restrict__ kf_win,
                               const WinCtl* __restrict__ ctl, const double* __restrict__ xp,
                               double* __restrict__ poses, long long pose_stride) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= nkf_total) return;
     const WinCtl& C = ctl[kf_win[k]];
     if (!C.need_trial) return;
@@ -1175,6 +1226,25 @@ __global__ void k_pose_update(int nkf_total, const int* __restrict__ kf_hp, cons
         return;
     }
     se3_exp_mul(xp + 6 * (long long)h, cur, nxt);
+}
+
+// the update half of a trial in one launch: blocks [0, nb_kf) apply oplus to the KeyFrames,
+// the rest back-substitute and move the MapPoints (block_solver.hpp:434-466)
+__global__ void __launch_bounds__(256) k_update(int nb_kf, int nkf_total, const int* __restrict__ kf_hp,
+                                                const int* __restrict__ kf_win, int npt_total,
+                                                const int* __restrict__ spe_off, const int* __restrict__ spe,
+                                                const EdgeS* __restrict__ E, const int* __restrict__ pt_win,
+                                                const WinCtl* __restrict__ ctl, const double* __restrict__ bl,
+                                                const double* __restrict__ Hll, const double* __restrict__ lin,
+                                                const double* __restrict__ xp, double* __restrict__ xl,
+                                                double* __restrict__ poses, long long pose_stride,
+                                                double* __restrict__ pts, long long pt_stride) {
+    const int b = blockIdx.x;
+    if (b < nb_kf)
+        pose_update_body(b * 256 + threadIdx.x, nkf_total, kf_hp, kf_win, ctl, xp, poses, pose_stride);
+    else
+        backsub_body((b - nb_kf) * 256 + threadIdx.x, npt_total, spe_off, spe, E, pt_win, ctl, bl, Hll, lin, xp, xl,
+                     pts, pt_stride);
 }
 
 __global__ void k_trial_error(int ne_total, const EdgeS* __restrict__ E, const WinCtl* __restrict__ ctl,
@@ -1199,6 +1269,25 @@ __global__ void k_trial_error(int ne_total, const EdgeS* __restrict__ E, const W
     rho_out[ei] = rho0;
 }
 
+// Per-step counters for the host: every control block adds its window's (need_trial, active)
+// and takes a ticket; the last block publishes the totals straight into the pinned host slot
+// the host polls (no copy, no counting kernel) and rearms the tally for the next step.
+__device__ __forceinline__ void tally_publish(int* __restrict__ tally, int need, int act, int nblocks,
+                                              Counters* __restrict__ host_slot) {
+    if (need) atomicAdd(&tally[0], need);
+    if (act) atomicAdd(&tally[1], act);
+    __threadfence();
+    if (atomicAdd(&tally[2], 1) == nblocks - 1) {
+        __threadfence();
+        const int n = atomicExch(&tally[0], 0), a = atomicExch(&tally[1], 0);
+        atomicExch(&tally[2], 0);
+        volatile Counters* h = host_slot;
+        h->need_trial = n;
+        h->active = a;
+        __threadfence_system();
+    }
+}
+
 // The trial-loop body after the error pass (optimization_algorithm_levenberg.cpp:117-166).
 __global__ void __launch_bounds__(kCtlThreads) k_trial_control(const WinDesc* __restrict__ wins,
                                                                WinCtl* __restrict__ ctl,
@@ -1206,11 +1295,17 @@ __global__ void __launch_bounds__(kCtlThreads) k_trial_control(const WinDesc* __
                                                                const double* __restrict__ xp,
                                                                const double* __restrict__ xl,
                                                                const double* __restrict__ bp,
-                                                               const double* __restrict__ bl, int stop) {
+                                                               const double* __restrict__ bl,
+                                                               const volatile int* __restrict__ stop_dev,
+                                                               int* __restrict__ tally,
+                                                               Counters* __restrict__ host_slot) {
     __shared__ double sh[kCtlThreads / 64];
     const WinDesc W = wins[blockIdx.x];
     WinCtl& C = ctl[blockIdx.x];
-    if (!C.need_trial) return;
+    if (!C.need_trial) {  // idle window: active == 0 here (k_iter_begin put every active one in a trial)
+        if (threadIdx.x == 0) tally_publish(tally, 0, 0, gridDim.x, host_slot);
+        return;
+    }
     double tmpChi = block_sum(strided_sum(rho + W.e0, W.ne), sh);
     const double lam = C.lambda;
     double sc = 0;
@@ -1225,6 +1320,7 @@ __global__ void __launch_bounds__(kCtlThreads) k_trial_control(const WinDesc* __
     }
     double scale = block_sum(sc, sh);
     if (threadIdx.x != 0) return;
+    const int stop = *stop_dev;  // terminate(), read live at the end of the trial
     if (!C.ok2) tmpChi = __DBL_MAX__;
     double rho_ = C.cur_chi - tmpChi;
     scale += 1e-3;
@@ -1247,6 +1343,7 @@ __global__ void __launch_bounds__(kCtlThreads) k_trial_control(const WinDesc* __
     const bool again = rho_ < 0 && C.qmax < 10 && !stop;
     if (again) {
         C.need_trial = 1;
+        tally_publish(tally, 1, C.active, gridDim.x, host_slot);
         return;
     }
     C.need_trial = 0;
@@ -1264,25 +1361,8 @@ __global__ void __launch_bounds__(kCtlThreads) k_trial_control(const WinDesc* __
     C.it++;
     C.chi2_final = C.cur_chi;
     C.active = (result == 0) && C.it < C.iters && !stop;
-}
-
-// windows still in the trial loop / still iterating (read back by the host once per trial)
-__global__ void k_count(int nwin, const WinCtl* __restrict__ ctl, Counters* __restrict__ cnt) {
-    __shared__ int need, act;
-    if (threadIdx.x == 0) need = act = 0;
-    __syncthreads();
-    int a = 0, b = 0;
-    for (int w = threadIdx.x; w < nwin; w += blockDim.x) {
-        a += ctl[w].need_trial;
-        b += ctl[w].active;
-    }
-    atomicAdd(&need, a);
-    atomicAdd(&act, b);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        cnt->need_trial = need;
-        cnt->active = act;
-    }
+    C.need_lin = C.active;  // the next step linearizes again
+    tally_publish(tally, 0, C.active, gridDim.x, host_slot);
 }
 
 // start of SparseOptimizer::optimize(iters) for every window
@@ -1296,6 +1376,7 @@ __global__ void k_opt_begin(int nwin, const WinDesc* __restrict__ wins, WinCtl* 
     C.iters = iters;
     C.active = iters > 0 && wins[w].ne > 0;  // no edges: initializeOptimization fails
     C.need_trial = 0;
+    C.need_lin = C.active;
 }
 
 // final outlier classification (Optimizer.cc:1995-2038) and float write-back (:2041-2077)
@@ -1415,11 +1496,17 @@ struct Plan {
     float *kf_in, *pt_in;
 };
 
+constexpr int kRing = 4;  // LM steps whose counters are in flight (host-side ring)
+
 struct slam_lba {
     int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    Counters* h_cnt = nullptr;  // pinned
+    Counters* h_cnt = nullptr;  // pinned, mapped: kRing slots, one per step in flight
+    Counters* d_hcnt = nullptr; // device view of h_cnt (written by k_trial_control's last block)
+    int* h_stop = nullptr;      // pinned, device-visible: the mirrored stop flag
+    int* d_stop = nullptr;      // its device address
+    hipEvent_t ring_ev[4] = {nullptr, nullptr, nullptr, nullptr};
     double last_ms = 0, last_plan_ms = 0;
     int last_syncs = 0;
     unsigned char* harena = nullptr;  // pinned
@@ -1587,7 +1674,7 @@ slam_status plan_fill(int n_prob, const slam_lba_problem* probs, const std::vect
         hs += (long long)(ldlt_npad(D.n) + 1) * D.ld;
         P.wins[w] = D;
         WinCtl c{};
-        c.user_lambda = opt->user_lambda_init;
+        c.user_lambda = Q.user_lambda_init > 0 ? Q.user_lambda_init : opt->user_lambda_init;
         c.lambda = -1;
         c.ni = 2;
         P.ctl[w] = c;
@@ -1716,10 +1803,18 @@ slam_status slamhot_lba_create(int device, slam_lba** out) {
     s->device = device;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&s->ev0) != hipSuccess || hipEventCreate(&s->ev1) != hipSuccess ||
-        hipHostMalloc((void**)&s->h_cnt, sizeof(Counters), hipHostMallocDefault) != hipSuccess) {
+        hipHostMalloc((void**)&s->h_cnt, sizeof(Counters) * kRing, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&s->d_hcnt, s->h_cnt, 0) != hipSuccess ||
+        hipHostMalloc((void**)&s->h_stop, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&s->d_stop, s->h_stop, 0) != hipSuccess) {
         slamhot_lba_destroy(s);
         return SLAM_EHIP;
     }
+    for (int i = 0; i < kRing; i++)
+        if (hipEventCreateWithFlags(&s->ring_ev[i], hipEventDisableTiming) != hipSuccess) {
+            slamhot_lba_destroy(s);
+            return SLAM_EHIP;
+        }
     if (hipFuncSetAttribute((const void*)k_ldlt, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)ldlt_lds_bytes(kMaxN)) != hipSuccess) {
         slamhot_lba_destroy(s);
@@ -1734,6 +1829,9 @@ void slamhot_lba_destroy(slam_lba* s) {
     (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     if (s->h_cnt) (void)hipHostFree(s->h_cnt);
+    if (s->h_stop) (void)hipHostFree(s->h_stop);
+    for (int i = 0; i < kRing; i++)
+        if (s->ring_ev[i]) (void)hipEventDestroy(s->ring_ev[i]);
     if (s->harena) (void)hipHostFree(s->harena);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
@@ -1759,12 +1857,14 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
             (probs[w].n_edge && !results[w].edge_outlier))
             return SLAM_EINVAL;
     if (n_prob == 0) return SLAM_OK;
+    const volatile uint8_t* stop_b = opt->stop_flag_bool;
+    auto user_stop = [&]() -> bool { return (stop_flag && *stop_flag) || (stop_b && *stop_b); };
     const auto t_plan0 = std::chrono::steady_clock::now();
     PlanSizes Z;
     std::vector<int> hidx_all, np_of;
     slam_status st = plan_sizes(n_prob, probs, Z, hidx_all, np_of);
     if (st != SLAM_OK) return st;
-    const bool stop0 = stop_flag && *stop_flag;
+    const bool stop0 = user_stop();
     for (int w = 0; w < n_prob; w++) {
         slam_lba_result& R = results[w];
         R.iterations[0] = R.iterations[1] = 0;
@@ -1813,7 +1913,7 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
         int nkf, npt, ne, npose, nblk;
     } H{Z.nkf, Z.npt, Z.ne, Z.npose, Z.nblk};
     const long long pose_stride = 8LL * std::max(H.nkf, 1), pt_stride = 4LL * std::max(H.npt, 1);
-    SLAM_HIP_TRY(s->cnt.ensure(sizeof(Counters)));
+    SLAM_HIP_TRY(s->cnt.ensure(sizeof(int) * 4));  // k_trial_control's tally (need, active, ticket)
     const size_t ne = std::max(H.ne, 1), npt = std::max(H.npt, 1), nps = std::max(H.npose, 1);
     SLAM_HIP_TRY(s->poses.ensure(sizeof(double) * 2 * pose_stride));
     SLAM_HIP_TRY(s->pts.ensure(sizeof(double) * 2 * pt_stride));
@@ -1863,11 +1963,11 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     EdgeS* dE = DP.edges;
     WinDesc* dW = DP.wins;
     WinCtl* dC = DP.ctl;
-    Counters* dCnt = as<Counters>(s->cnt);
+    int* dTally = as<int>(s->cnt);
+    SLAM_HIP_TRY(hipMemsetAsync(dTally, 0, sizeof(int) * 4, S));
     double* poses = as<double>(s->poses);
     double* pts = as<double>(s->pts);
     const int T = 256;
-    int syncs = 0;
     SLAM_HIP_TRY(hipEventRecord(s->ev0, S));
     k_init_state<<<blocks(H.nkf + H.npt, T), T, 0, S>>>(H.nkf, H.npt, DP.kf_in, DP.pt_in,
                                                          poses, pts);
@@ -1878,67 +1978,87 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
         k_t16_pad<<<nw, 64, 0, S>>>(dW, tiles);
     }
     const size_t lds_bytes = ldlt_lds_bytes(Z.max_n);
+    // LM as device-driven steps: a step linearizes the windows that start an iteration
+    // (need_lin) and runs one trial for those in the trial loop (need_trial); every kernel skips
+    // the other windows, so the host queues steps without waiting for any decision and reads
+    // the per-step counters asynchronously (a ring of kRing steps in flight).  While it waits it
+    // mirrors the caller's stop flag into pinned memory the control kernels read.
+    *s->h_stop = user_stop() ? 1 : 0;
     bool stopped = false;
+    int syncs = 0;
     const int iters_of[2] = {opt->iters_first, opt->iters_second};
-    for (int o = 0; o < 2 && !stopped; o++) {
-        k_opt_begin<<<blocks(nw, 64), 64, 0, S>>>(nw, dW, dC, o, iters_of[o]);
-        for (int it = 0; it < iters_of[o]; it++) {
-            if (stop_flag && *stop_flag) {
-                stopped = true;
-                break;
-            }
-            k_lin_points<<<blocks(H.npt, 128), 128, 0, S>>>(H.npt, DP.pt_off, DP.pt_win, dE, dC, poses, pts, pose_stride,
-                                                              pt_stride, cam, hk, as<double>(s->err),
-                                                              as<double>(s->rho), as<double>(s->lin),
-                                                              as<double>(s->Hll), as<double>(s->bl));
-            k_lin_poses<<<blocks(H.npose, 4), 256, 0, S>>>(H.npose, DP.pe_off, DP.pe, DP.pose_win, dE, dC, poses, pts,
-                                                            pose_stride, pt_stride, cam, hk, as<double>(s->Hpp),
-                                                            as<double>(s->bp));
-            k_iter_begin<<<nw, kCtlThreads, 0, S>>>(dW, dC, as<double>(s->rho), as<double>(s->Hpp),
-                                                    as<double>(s->Hll));
-            bool any_active = false;
-            for (int t = 0; t < 10; t++) {
-                k_schur_edges<<<blocks(Z.nspe, T), T, 0, S>>>(Z.nspe, DP.spe, dE, dC, as<double>(s->Hll),
-                                                               as<double>(s->bl), as<double>(s->lin),
-                                                               as<double>(s->tr));
-                if (H.npose)
-                    k_schur_block<kSchurDiagLanes><<<blocks(H.npose, 256 / kSchurDiagLanes), 256, 0, S>>>(
-                        H.npose, DP.blk_order, DP.blk_pose, DP.blk_win, DP.ct_off, DP.ct, dW,
-                        dC, as<double>(s->Hpp), as<double>(s->bp), DP.pe_off, DP.pe,
-                        as<double>(s->lin), as<double>(s->tr), as<double>(s->Hs), tiles);
-                if (H.nblk > H.npose)
-                    k_schur_block<kSchurLanes><<<blocks(H.nblk - H.npose, 256 / kSchurLanes), 256, 0, S>>>(
-                        H.nblk - H.npose, DP.blk_order + H.npose, DP.blk_pose, DP.blk_win, DP.ct_off, DP.ct, dW,
-                        dC, as<double>(s->Hpp), as<double>(s->bp), DP.pe_off, DP.pe,
-                        as<double>(s->lin), as<double>(s->tr), as<double>(s->Hs), tiles);
-                if (use_t16)
-                    k_ldlt_t16<<<nw, kT16Waves * 64, 0, S>>>(dW, dC, as<double>(s->Hs), as<double>(s->Ts),
-                                                             as<double>(s->xp));
-                else
-                    k_ldlt<<<nw, 512, lds_bytes, S>>>(dW, dC, as<double>(s->Hs), as<double>(s->xp));
-                k_backsub<<<blocks(H.npt, T), T, 0, S>>>(H.npt, DP.spe_off, DP.spe, dE,
-                                                          DP.pt_win, dC, as<double>(s->bl),
-                                                          as<double>(s->Hll), as<double>(s->lin), as<double>(s->xp),
-                                                          as<double>(s->xl), pts, pt_stride);
-                k_pose_update<<<blocks(H.nkf, T), T, 0, S>>>(H.nkf, DP.kf_hp, DP.kf_win, dC,
-                                                              as<double>(s->xp), poses, pose_stride);
-                k_trial_error<<<blocks(H.ne, T), T, 0, S>>>(H.ne, dE, dC, poses, pts, pose_stride, pt_stride, cam, hk,
-                                                             as<double>(s->err), as<double>(s->rho));
-                const int stop_now = (stop_flag && *stop_flag) ? 1 : 0;
-                k_trial_control<<<nw, kCtlThreads, 0, S>>>(dW, dC, as<double>(s->rho), as<double>(s->xp),
-                                                           as<double>(s->xl), as<double>(s->bp), as<double>(s->bl),
-                                                           stop_now);
-                k_count<<<1, 256, 0, S>>>(nw, dC, dCnt);
-                SLAM_HIP_TRY(hipGetLastError());
-                SLAM_HIP_TRY(hipMemcpyAsync(s->h_cnt, dCnt, sizeof(Counters), hipMemcpyDeviceToHost, S));
-                SLAM_HIP_TRY(hipStreamSynchronize(S));
-                syncs++;
-                if (stop_now) stopped = true;
-                any_active = s->h_cnt->active > 0;
-                if (s->h_cnt->need_trial == 0) break;
-            }
-            if (!any_active || stopped) break;
+    auto wait_event = [&](hipEvent_t ev) -> hipError_t {
+        for (;;) {
+            const hipError_t e = hipEventQuery(ev);
+            if (e != hipErrorNotReady) return e;
+            if (!*s->h_stop && user_stop()) *s->h_stop = 1;
+            std::this_thread::yield();
         }
+    };
+    // grid partitions of the fused launches
+    const int nb_lin_pose = (H.npose + kLinThreads / 64 - 1) / (kLinThreads / 64);
+    const int nb_lin = nb_lin_pose + (H.npt + kLinThreads - 1) / kLinThreads;
+    const int nb_sdiag = ((H.npose + 256 / kSchurDiagLanes - 1) / (256 / kSchurDiagLanes) + 7) & ~7;
+    const int nb_schur = nb_sdiag + (H.nblk - H.npose + 256 / kSchurLanes - 1) / (256 / kSchurLanes);
+    const int nb_kf = (H.nkf + 255) / 256;
+    const int nb_upd = nb_kf + (H.npt + 255) / 256;
+    auto launch_step = [&](int slot) -> hipError_t {
+        if (nb_lin)
+            k_linearize<<<nb_lin, kLinThreads, 0, S>>>(nb_lin_pose, H.npose, DP.pe_off, DP.pe, DP.pose_win, H.npt,
+                                                       DP.pt_off, DP.pt_win, dE, dC, poses, pts, pose_stride,
+                                                       pt_stride, cam, hk, as<double>(s->err), as<double>(s->rho),
+                                                       as<double>(s->lin), as<double>(s->Hll), as<double>(s->bl),
+                                                       as<double>(s->Hpp), as<double>(s->bp));
+        k_iter_begin<<<nw, kCtlThreads, 0, S>>>(dW, dC, as<double>(s->rho), as<double>(s->Hpp),
+                                                as<double>(s->Hll), s->d_stop);
+        if (Z.nspe)
+            k_schur_edges<<<blocks(Z.nspe, T), T, 0, S>>>(Z.nspe, DP.spe, dE, dC, as<double>(s->Hll),
+                                                           as<double>(s->bl), as<double>(s->lin),
+                                                           as<double>(s->tr));
+        if (H.nblk)
+            k_schur_blocks<<<nb_schur, 256, 0, S>>>(nb_sdiag, H.nblk, H.npose, DP.blk_order, DP.blk_pose, DP.blk_win,
+                                                    DP.ct_off, DP.ct, dW, dC, as<double>(s->Hpp), as<double>(s->bp),
+                                                    DP.pe_off, DP.pe, as<double>(s->lin), as<double>(s->tr),
+                                                    as<double>(s->Hs), tiles);
+        if (use_t16)
+            k_ldlt_t16<<<nw, kT16Waves * 64, 0, S>>>(dW, dC, as<double>(s->Hs), as<double>(s->Ts), as<double>(s->xp));
+        else
+            k_ldlt<<<nw, 512, lds_bytes, S>>>(dW, dC, as<double>(s->Hs), as<double>(s->xp));
+        if (nb_upd)
+            k_update<<<nb_upd, 256, 0, S>>>(nb_kf, H.nkf, DP.kf_hp, DP.kf_win, H.npt, DP.spe_off, DP.spe, dE,
+                                            DP.pt_win, dC, as<double>(s->bl), as<double>(s->Hll), as<double>(s->lin),
+                                            as<double>(s->xp), as<double>(s->xl), poses, pose_stride, pts, pt_stride);
+        if (H.ne)
+            k_trial_error<<<blocks(H.ne, T), T, 0, S>>>(H.ne, dE, dC, poses, pts, pose_stride, pt_stride, cam, hk,
+                                                         as<double>(s->err), as<double>(s->rho));
+        k_trial_control<<<nw, kCtlThreads, 0, S>>>(dW, dC, as<double>(s->rho), as<double>(s->xp),
+                                                   as<double>(s->xl), as<double>(s->bp), as<double>(s->bl),
+                                                   s->d_stop, dTally, s->d_hcnt + slot);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        return hipEventRecord(s->ring_ev[slot], S);
+    };
+    for (int o = 0; o < 2; o++) {
+        if (o == 1 && (stopped || user_stop())) break;  // bDoMore = false (Optimizer.cc:1933-1935)
+        k_opt_begin<<<blocks(nw, 64), 64, 0, S>>>(nw, dW, dC, o, iters_of[o]);
+        if (iters_of[o] <= 0) continue;
+        long long launched = 0, checked = 0;
+        bool done = false;
+        while (!done) {
+            if (launched - checked < kRing - 1) {  // keep the device fed
+                SLAM_HIP_TRY(launch_step((int)(launched % kRing)));
+                launched++;
+                if (launched - checked < 2) continue;  // two steps queued before the first wait
+            }
+            const int slot = (int)(checked % kRing);
+            SLAM_HIP_TRY(wait_event(s->ring_ev[slot]));
+            syncs++;
+            checked++;
+            const Counters c = s->h_cnt[slot];
+            done = c.active == 0 && c.need_trial == 0;
+        }
+        SLAM_HIP_TRY(wait_event(s->ring_ev[(launched - 1) % kRing]));  // the queued no-op steps
+        if (*s->h_stop) stopped = true;
     }
     k_finalize_edges<<<blocks(H.ne, T), T, 0, S>>>(H.ne, dE, dC, poses, pts, pose_stride, pt_stride,
                                                     as<double>(s->err), as<uint8_t>(s->outl));

@@ -496,11 +496,13 @@ class Camera(C.Structure):
 class LbaProblem(C.Structure):
     _fields_ = [("n_kf", C.c_int32), ("kf_Tcw", C.c_void_p), ("kf_fixed", C.c_void_p), ("n_pt", C.c_int32),
                 ("pt_pos", C.c_void_p), ("n_edge", C.c_int32), ("edge_pt", C.c_void_p), ("edge_kf", C.c_void_p),
-                ("edge_obs", C.c_void_p), ("edge_inv_sigma2", C.c_void_p), ("cam", Camera)]
+                ("edge_obs", C.c_void_p), ("edge_inv_sigma2", C.c_void_p), ("cam", Camera),
+                ("user_lambda_init", C.c_double)]
 
 
 class LbaOptions(C.Structure):
-    _fields_ = [("iters_first", C.c_int32), ("iters_second", C.c_int32), ("user_lambda_init", C.c_double)]
+    _fields_ = [("iters_first", C.c_int32), ("iters_second", C.c_int32), ("user_lambda_init", C.c_double),
+                ("stop_flag_bool", C.c_void_p)]
 
 
 class LbaResult(C.Structure):
@@ -520,7 +522,8 @@ def make_lba_problem(w: dict):
     n_kf, n_pt, n_e = len(arrs["kf_fixed"]), len(arrs["pt_pos"]), len(arrs["edge_pt"])
     p = LbaProblem(n_kf, arrs["kf_Tcw"].ctypes.data, arrs["kf_fixed"].ctypes.data, n_pt,
                    arrs["pt_pos"].ctypes.data, n_e, arrs["edge_pt"].ctypes.data, arrs["edge_kf"].ctypes.data,
-                   arrs["edge_obs"].ctypes.data, arrs["edge_inv_sigma2"].ctypes.data, Camera(*w["cam"]))
+                   arrs["edge_obs"].ctypes.data, arrs["edge_inv_sigma2"].ctypes.data, Camera(*w["cam"]),
+                   float(w.get("user_lambda_init", 0.0)))
     p._keep = arrs
     out = dict(kf_Tcw=np.zeros((n_kf, 16), np.float32), pt_pos=np.zeros((n_pt, 3), np.float32),
                edge_outlier=np.zeros(n_e, np.uint8))
@@ -560,6 +563,9 @@ class LocalBundleAdjustment:
             pass
 
     def solve(self, windows, iters_first=5, iters_second=10, user_lambda_init=0.0, stop_flag=None):
+        """``stop_flag``: None, a truthy/falsy value (read once), or a live ``ctypes.c_int32`` /
+        ``ctypes.c_bool`` that another thread may set while the call runs (``pbStopFlag``); the
+        device LM loop reads it at every iteration start and trial end, as g2o's terminate()."""
         single = isinstance(windows, dict)
         ws = [windows] if single else list(windows)
         probs = (LbaProblem * len(ws))()
@@ -571,14 +577,21 @@ class LocalBundleAdjustment:
             ress[i] = r
             outs.append((p, r, o))
         opt = LbaOptions(iters_first, iters_second, user_lambda_init)
-        stop = None if stop_flag is None else C.byref(C.c_int32(int(stop_flag)))
+        stop = None
+        if isinstance(stop_flag, C.c_int32):      # live flag another thread may set mid-solve
+            stop = C.byref(stop_flag)
+        elif isinstance(stop_flag, (C.c_bool, C.c_uint8)):  # the reference's bool* pbStopFlag
+            opt.stop_flag_bool = C.addressof(stop_flag)
+        elif stop_flag is not None:
+            stop = C.byref(C.c_int32(int(stop_flag)))
         check(lib().slamhot_lba_solve(self._h, len(ws), probs, C.byref(opt), stop, ress), "lba_solve")
         res = [lba_result_dict(ress[i], outs[i][2]) for i in range(len(ws))]
         return res[0] if single else res
 
-    def prepare(self, windows, iters_first=5, iters_second=10, user_lambda_init=0.0):
+    def prepare(self, windows, iters_first=5, iters_second=10, user_lambda_init=0.0, stop_flag=None):
         """Flatten windows into C structs once (what a C++ caller already holds); returns a
-        callable that runs slamhot_lba_solve on them and returns the LM iteration total."""
+        callable that runs slamhot_lba_solve on them and returns the LM iteration total
+        (``run.results()`` gives the result dicts).  ``stop_flag``: a live ``ctypes.c_bool``."""
         ws = list(windows)
         probs = (LbaProblem * len(ws))()
         ress = (LbaResult * len(ws))()
@@ -589,6 +602,8 @@ class LocalBundleAdjustment:
             ress[i] = r
             keep.append((p, r, o))
         opt = LbaOptions(iters_first, iters_second, user_lambda_init)
+        if stop_flag is not None:
+            opt.stop_flag_bool = C.addressof(stop_flag)
         h = self._h
         fn = lib().slamhot_lba_solve
 
@@ -596,7 +611,8 @@ class LocalBundleAdjustment:
             check(fn(h, len(ws), probs, C.byref(opt), None, ress), "lba_solve")
             return sum(ress[i].iterations[0] + ress[i].iterations[1] for i in range(len(ws)))
 
-        run.keep = (probs, ress, keep, opt)
+        run.keep = (probs, ress, keep, opt, stop_flag)
+        run.results = lambda: [lba_result_dict(ress[i], keep[i][2]) for i in range(len(ws))]
         return run
 
     def last_stats(self):

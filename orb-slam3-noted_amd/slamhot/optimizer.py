@@ -9,6 +9,8 @@ reference line by line (cited below).  This is the logic a C++ shim keeps around
 """
 from __future__ import annotations
 
+import ctypes as C
+
 import numpy as np
 
 
@@ -237,7 +239,8 @@ def LocalBundleAdjustment(pKF: KeyFrame, stop_flag, pMap: Map, solver):
     counts = (num_fixed, len(local), len(local_mps), len(edge_refs))
     if stop_flag:                                                  # :1921-1923
         return counts
-    res = solver.solve(W, user_lambda_init=100.0 if pMap.IsInertial() else 0.0)
+    live = stop_flag if isinstance(stop_flag, (C.c_bool, C.c_uint8, C.c_int32)) else None  # optimizer.setForceStopFlag
+    res = solver.solve(W, user_lambda_init=100.0 if pMap.IsInertial() else 0.0, stop_flag=live)
     for e, bad in enumerate(res["edge_outlier"]):                  # :2043-2052
         if bad:
             k, mp = edge_refs[e]

@@ -115,3 +115,59 @@ def test_lba_deterministic(solver):
     W = synth.lba_window(34)
     a, b = solver.solve(W), solver.solve(W)
     assert np.array_equal(a["kf_Tcw"], b["kf_Tcw"]) and np.array_equal(a["pt_pos"], b["pt_pos"])
+
+
+def test_lba_stop_flag_bool_before_start(solver):
+    """The reference's bool* pbStopFlag passed as is (slam_lba_options.stop_flag_bool)."""
+    import ctypes as C
+    W = synth.lba_window(33, n_kf=12, n_pt=200, obs_per_pt=4)
+    g = solver.solve(W, stop_flag=C.c_bool(True))
+    _check(g, ob.lba_solve(W, stop=1))
+    _check(solver.solve(W, stop_flag=C.c_bool(False)), ob.lba_solve(W))
+
+
+def test_lba_per_window_lambda(solver):
+    """Batched windows of different maps: each window's pMap->IsInertial() sets its own lambda0."""
+    Ws = [dict(synth.lba_window(40 + i, n_kf=10 + 3 * i, n_pt=250, obs_per_pt=5), user_lambda_init=100.0 * (i % 2))
+          for i in range(4)]
+    for W, g in zip(Ws, solver.solve(Ws)):
+        _check(g, ob.lba_solve(W))
+    g1 = solver.solve(Ws[1])
+    _check(g1, ob.lba_solve(Ws[1], user_lambda_init=100.0))
+
+
+def test_lba_stop_flag_mid_solve(solver):
+    """mbAbortBA set by another thread while the device LM loop runs: the solve stops early (g2o
+    checks terminate() per iteration and per trial), every window's trajectory is a prefix of the
+    unstopped one, and outputs stay finite.  The flag is the caller's live bool; it is set at a
+    sweep of delays across the call so that at least one lands inside the LM loop."""
+    import ctypes as C
+    import threading
+    import time
+    Ws = [synth.lba_window(200 + i, n_kf=30, n_pt=1200, obs_per_pt=6) for i in range(96)]
+    flag = C.c_bool(False)
+    run = solver.prepare(Ws, stop_flag=flag)
+    n_full = run()
+    full = run.results()
+    t0 = time.perf_counter()
+    run()
+    t_call = time.perf_counter() - t0
+    dev_ms, plan_ms, _ = solver.last_stats()
+    partial = []
+    for frac in np.linspace(0.3, 0.98, 12):
+        flag.value = False
+        timer = threading.Timer(frac * t_call, lambda: setattr(flag, "value", True))
+        timer.start()
+        n_part = run()
+        timer.join()
+        part = run.results()
+        assert n_part <= n_full
+        for f, p in zip(full, part):
+            assert p["iterations"][0] <= f["iterations"][0] and p["iterations"][1] <= f["iterations"][1]
+            assert np.isfinite(p["kf_Tcw"]).all() and np.isfinite(p["pt_pos"]).all()
+            if p["iterations"] == f["iterations"] and p["trials"] == f["trials"]:
+                assert np.array_equal(p["kf_Tcw"], f["kf_Tcw"]) and np.array_equal(p["pt_pos"], f["pt_pos"])
+        partial.append(n_part)
+    flag.value = False
+    assert run() == n_full  # the flag is re-read per call
+    assert any(0 < n < n_full for n in partial), (partial, n_full, t_call, dev_ms, plan_ms)
