@@ -28,6 +28,8 @@
 #include <cmath>
 #include <cstring>
 #include <thread>
+
+#include <immintrin.h>
 #include <vector>
 
 #include "common.hpp"
@@ -83,7 +85,7 @@ struct WinCtl {
 };
 
 struct Counters {
-    int need_trial, active;
+    int need_trial, active, seq, pad;
 };
 
 struct Cam {
@@ -417,8 +419,8 @@ __global__ void __launch_bounds__(kCtlThreads) k_iter_begin(const WinDesc* __res
     }
     if (threadIdx.x == 0) {
         C.need_lin = 0;
-        // SparseOptimizer::optimize: no iteration once terminate() (sparse_optimizer.cpp:376).
-        // One lane reads the pinned host word (a PCIe read per block, not per thread).
+        // SparseOptimizer::optimize: no iteration once terminate() (sparse_optimizer.cpp:376);
+        // stop_dev is the device copy k_trial_control refreshes from the host word every step
         if (*stop_dev) {
             C.active = 0;
             return;
@@ -1273,7 +1275,7 @@ __global__ void k_trial_error(int ne_total, const EdgeS* __restrict__ E, const W
 // and takes a ticket; the last block publishes the totals straight into the pinned host slot
 // the host polls (no copy, no counting kernel) and rearms the tally for the next step.
 __device__ __forceinline__ void tally_publish(int* __restrict__ tally, int need, int act, int nblocks,
-                                              Counters* __restrict__ host_slot) {
+                                              Counters* __restrict__ host_slot, int seq) {
     if (need) atomicAdd(&tally[0], need);
     if (act) atomicAdd(&tally[1], act);
     __threadfence();
@@ -1284,6 +1286,8 @@ __device__ __forceinline__ void tally_publish(int* __restrict__ tally, int need,
         volatile Counters* h = host_slot;
         h->need_trial = n;
         h->active = a;
+        __threadfence_system();
+        h->seq = seq;  // published last: the host spins on it
         __threadfence_system();
     }
 }
@@ -1296,14 +1300,23 @@ __global__ void __launch_bounds__(kCtlThreads) k_trial_control(const WinDesc* __
                                                                const double* __restrict__ xl,
                                                                const double* __restrict__ bp,
                                                                const double* __restrict__ bl,
-                                                               const volatile int* __restrict__ stop_dev,
+                                                               const volatile int* __restrict__ stop_host,
                                                                int* __restrict__ tally,
-                                                               Counters* __restrict__ host_slot) {
+                                                               Counters* __restrict__ host_slot, int seq) {
     __shared__ double sh[kCtlThreads / 64];
     const WinDesc W = wins[blockIdx.x];
     WinCtl& C = ctl[blockIdx.x];
+    // terminate(): block 0 samples the pinned host word (one PCIe read per step, issued early so
+    // it overlaps the reductions) into tally[3]; the decisions read tally[3], i.e. the flag as
+    // sampled during the previous step -- a stop the host saw a step later, which is all the
+    // reference guarantees between threads anyway
+    int stop_fresh = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) stop_fresh = *stop_host;
     if (!C.need_trial) {  // idle window: active == 0 here (k_iter_begin put every active one in a trial)
-        if (threadIdx.x == 0) tally_publish(tally, 0, 0, gridDim.x, host_slot);
+        if (threadIdx.x == 0) {
+            if (blockIdx.x == 0) atomicExch(&tally[3], stop_fresh);
+            tally_publish(tally, 0, 0, gridDim.x, host_slot, seq);
+        }
         return;
     }
     double tmpChi = block_sum(strided_sum(rho + W.e0, W.ne), sh);
@@ -1320,7 +1333,8 @@ __global__ void __launch_bounds__(kCtlThreads) k_trial_control(const WinDesc* __
     }
     double scale = block_sum(sc, sh);
     if (threadIdx.x != 0) return;
-    const int stop = *stop_dev;  // terminate(), read live at the end of the trial
+    const int stop = ((volatile int*)tally)[3];  // terminate() at the end of the trial
+    if (blockIdx.x == 0) atomicExch(&tally[3], stop_fresh);
     if (!C.ok2) tmpChi = __DBL_MAX__;
     double rho_ = C.cur_chi - tmpChi;
     scale += 1e-3;
@@ -1343,7 +1357,7 @@ __global__ void __launch_bounds__(kCtlThreads) k_trial_control(const WinDesc* __
     const bool again = rho_ < 0 && C.qmax < 10 && !stop;
     if (again) {
         C.need_trial = 1;
-        tally_publish(tally, 1, C.active, gridDim.x, host_slot);
+        tally_publish(tally, 1, C.active, gridDim.x, host_slot, seq);
         return;
     }
     C.need_trial = 0;
@@ -1362,7 +1376,7 @@ __global__ void __launch_bounds__(kCtlThreads) k_trial_control(const WinDesc* __
     C.chi2_final = C.cur_chi;
     C.active = (result == 0) && C.it < C.iters && !stop;
     C.need_lin = C.active;  // the next step linearizes again
-    tally_publish(tally, 0, C.active, gridDim.x, host_slot);
+    tally_publish(tally, 0, C.active, gridDim.x, host_slot, seq);
 }
 
 // start of SparseOptimizer::optimize(iters) for every window
@@ -1506,7 +1520,7 @@ struct slam_lba {
     Counters* d_hcnt = nullptr; // device view of h_cnt (written by k_trial_control's last block)
     int* h_stop = nullptr;      // pinned, device-visible: the mirrored stop flag
     int* d_stop = nullptr;      // its device address
-    hipEvent_t ring_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    unsigned step_seq = 0;      // sequence number of the last LM step queued (never reused)
     double last_ms = 0, last_plan_ms = 0;
     int last_syncs = 0;
     unsigned char* harena = nullptr;  // pinned
@@ -1810,11 +1824,7 @@ slam_status slamhot_lba_create(int device, slam_lba** out) {
         slamhot_lba_destroy(s);
         return SLAM_EHIP;
     }
-    for (int i = 0; i < kRing; i++)
-        if (hipEventCreateWithFlags(&s->ring_ev[i], hipEventDisableTiming) != hipSuccess) {
-            slamhot_lba_destroy(s);
-            return SLAM_EHIP;
-        }
+    std::memset(s->h_cnt, 0, sizeof(Counters) * kRing);
     if (hipFuncSetAttribute((const void*)k_ldlt, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)ldlt_lds_bytes(kMaxN)) != hipSuccess) {
         slamhot_lba_destroy(s);
@@ -1830,8 +1840,6 @@ void slamhot_lba_destroy(slam_lba* s) {
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     if (s->h_cnt) (void)hipHostFree(s->h_cnt);
     if (s->h_stop) (void)hipHostFree(s->h_stop);
-    for (int i = 0; i < kRing; i++)
-        if (s->ring_ev[i]) (void)hipEventDestroy(s->ring_ev[i]);
     if (s->harena) (void)hipHostFree(s->harena);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
@@ -1984,15 +1992,25 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     // the per-step counters asynchronously (a ring of kRing steps in flight).  While it waits it
     // mirrors the caller's stop flag into pinned memory the control kernels read.
     *s->h_stop = user_stop() ? 1 : 0;
+    SLAM_HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(dTally + 3), *s->h_stop, 1, S));  // the device's copy
     bool stopped = false;
     int syncs = 0;
     const int iters_of[2] = {opt->iters_first, opt->iters_second};
-    auto wait_event = [&](hipEvent_t ev) -> hipError_t {
-        for (;;) {
-            const hipError_t e = hipEventQuery(ev);
-            if (e != hipErrorNotReady) return e;
+    // Wait for a step's counters: the last k_trial_control block stores the step's sequence
+    // number into the mapped slot after the counts.  The host spins on that word (mirroring the
+    // caller's stop flag meanwhile) and asks the stream for errors now and then, so a faulted
+    // kernel ends the wait instead of hanging it.
+    auto wait_step = [&](int slot, int seq) -> hipError_t {
+        volatile Counters* c = s->h_cnt + slot;
+        for (unsigned spin = 1;; spin++) {
+            if (c->seq == seq) return hipSuccess;
             if (!*s->h_stop && user_stop()) *s->h_stop = 1;
-            std::this_thread::yield();
+            if ((spin & 1023) == 0) {
+                const hipError_t e = hipStreamQuery(S);
+                if (e == hipSuccess && c->seq != seq) return hipErrorUnknown;  // drained without publishing
+                if (e != hipSuccess && e != hipErrorNotReady) return e;
+            }
+            _mm_pause();
         }
     };
     // grid partitions of the fused launches
@@ -2002,7 +2020,7 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     const int nb_schur = nb_sdiag + (H.nblk - H.npose + 256 / kSchurLanes - 1) / (256 / kSchurLanes);
     const int nb_kf = (H.nkf + 255) / 256;
     const int nb_upd = nb_kf + (H.npt + 255) / 256;
-    auto launch_step = [&](int slot) -> hipError_t {
+    auto launch_step = [&](int slot, int seq) -> hipError_t {
         if (nb_lin)
             k_linearize<<<nb_lin, kLinThreads, 0, S>>>(nb_lin_pose, H.npose, DP.pe_off, DP.pe, DP.pose_win, H.npt,
                                                        DP.pt_off, DP.pt_win, dE, dC, poses, pts, pose_stride,
@@ -2010,7 +2028,7 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
                                                        as<double>(s->lin), as<double>(s->Hll), as<double>(s->bl),
                                                        as<double>(s->Hpp), as<double>(s->bp));
         k_iter_begin<<<nw, kCtlThreads, 0, S>>>(dW, dC, as<double>(s->rho), as<double>(s->Hpp),
-                                                as<double>(s->Hll), s->d_stop);
+                                                as<double>(s->Hll), dTally + 3);
         if (Z.nspe)
             k_schur_edges<<<blocks(Z.nspe, T), T, 0, S>>>(Z.nspe, DP.spe, dE, dC, as<double>(s->Hll),
                                                            as<double>(s->bl), as<double>(s->lin),
@@ -2033,31 +2051,33 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
                                                          as<double>(s->err), as<double>(s->rho));
         k_trial_control<<<nw, kCtlThreads, 0, S>>>(dW, dC, as<double>(s->rho), as<double>(s->xp),
                                                    as<double>(s->xl), as<double>(s->bp), as<double>(s->bl),
-                                                   s->d_stop, dTally, s->d_hcnt + slot);
-        const hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-        return hipEventRecord(s->ring_ev[slot], S);
+                                                   s->d_stop, dTally, s->d_hcnt + slot, seq);
+        return hipGetLastError();
     };
     for (int o = 0; o < 2; o++) {
         if (o == 1 && (stopped || user_stop())) break;  // bDoMore = false (Optimizer.cc:1933-1935)
         k_opt_begin<<<blocks(nw, 64), 64, 0, S>>>(nw, dW, dC, o, iters_of[o]);
         if (iters_of[o] <= 0) continue;
         long long launched = 0, checked = 0;
+        int seqs[kRing] = {0, 0, 0, 0};
         bool done = false;
         while (!done) {
             if (launched - checked < kRing - 1) {  // keep the device fed
-                SLAM_HIP_TRY(launch_step((int)(launched % kRing)));
+                const int slot = (int)(launched % kRing);
+                seqs[slot] = (int)(++s->step_seq & 0x7fffffff);
+                SLAM_HIP_TRY(launch_step(slot, seqs[slot]));
                 launched++;
                 if (launched - checked < 2) continue;  // two steps queued before the first wait
             }
             const int slot = (int)(checked % kRing);
-            SLAM_HIP_TRY(wait_event(s->ring_ev[slot]));
+            SLAM_HIP_TRY(wait_step(slot, seqs[slot]));
             syncs++;
             checked++;
             const Counters c = s->h_cnt[slot];
             done = c.active == 0 && c.need_trial == 0;
         }
-        SLAM_HIP_TRY(wait_event(s->ring_ev[(launched - 1) % kRing]));  // the queued no-op steps
+        const int last = (int)((launched - 1) % kRing);
+        SLAM_HIP_TRY(wait_step(last, seqs[last]));  // the queued no-op steps
         if (*s->h_stop) stopped = true;
     }
     k_finalize_edges<<<blocks(H.ne, T), T, 0, S>>>(H.ne, dE, dC, poses, pts, pose_stride, pt_stride,
