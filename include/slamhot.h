@@ -274,14 +274,16 @@ slam_status slamhot_search_by_projection_last(slam_matcher* m, const slam_frame_
  * FeatureVector.cpp:31-45).  pairs (host, 2 x npairs): (keyframe index, frame index).
  * d_valid (nframes x cap u8, may be NULL = all valid) marks keyframe features with a usable
  * MapPoint.  Outputs (device, cap per pair): d_a2b, d_b2a (-1 = none), d_nmatches (npairs).
- * Asynchronous on hip_stream (NULL = the matcher's stream); slamhot_bow_match_batch_status
- * synchronises and reports pairs the kernel could not hold (skipped, outputs undefined). */
+ * cap <= 8192.  Asynchronous on hip_stream (NULL = the matcher's stream).  Every pair's outputs
+ * are defined: a pair outside the fast kernel's tiles (a side over 8192 features or 4096 nodes,
+ * or a frame node over 256 candidates) runs through an unbounded kernel with the same results;
+ * slamhot_bow_match_batch_status synchronises and reports how many pairs took that path. */
 slam_status slamhot_bow_match_batch_device(slam_matcher* m, slam_vocab* v, int nframes, const void* d_kps,
                                            const void* d_desc, int cap, const void* d_n, const void* d_valid,
                                            int npairs, const int32_t* pairs, float nnratio, int check_ori,
                                            int strict, int levelsup, void* d_a2b, void* d_b2a,
                                            void* d_nmatches, void* hip_stream);
-slam_status slamhot_bow_match_batch_status(slam_matcher* m, void* hip_stream, int* skipped_pairs);
+slam_status slamhot_bow_match_batch_status(slam_matcher* m, void* hip_stream, int* general_pairs);
 
 /* Per KeyFrame feature for SearchByProjection(Frame&, KeyFrame*, const set<MapPoint*>&
  * sAlreadyFound, float th, int ORBdist) (ORBmatcher.cc:2391-2513). */

@@ -118,6 +118,9 @@ struct DevBowPair {
     int32_t* a2b;
     int32_t* b2a;
     int32_t* nmatches;
+    int general;       // outside k_bow_match's tiles: k_bow_match_any handles the pair
+    int8_t* bins;      // k_bow_match_any scratch: rotation bin per A feature (A.n)
+    uint8_t* taken;    // k_bow_match_any scratch: B feature already matched (B.n)
 };
 
 constexpr int kBowCap = 8192;        // features per side held in LDS
@@ -133,6 +136,33 @@ __device__ __forceinline__ int rot_bin(float a, float b) {
     return bin;
 }
 
+// ComputeThreeMaxima (ORBmatcher.cc:2515-2556) over the 30 rotation bins
+__device__ inline void three_maxima(const int* hist, int* keep) {
+    int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+    for (int i = 0; i < 30; i++) {
+        const int s = hist[i];
+        if (s > max1) {
+            max3 = max2; max2 = max1; max1 = s;
+            ind3 = ind2; ind2 = ind1; ind1 = i;
+        } else if (s > max2) {
+            max3 = max2; max2 = s;
+            ind3 = ind2; ind2 = i;
+        } else if (s > max3) {
+            max3 = s;
+            ind3 = i;
+        }
+    }
+    if (max2 < 0.1f * (float)max1) {
+        ind2 = -1;
+        ind3 = -1;
+    } else if (max3 < 0.1f * (float)max1) {
+        ind3 = -1;
+    }
+    keep[0] = ind1;
+    keep[1] = ind2;
+    keep[2] = ind3;
+}
+
 __global__ void __launch_bounds__(512) k_bow_match(const DevBowPair* pairs, float nnratio,
                                                    int check_ori, int strict) {
     __shared__ int16_t matchA[kBowCap];   // B index matched by A feature, -1 none
@@ -141,6 +171,7 @@ __global__ void __launch_bounds__(512) k_bow_match(const DevBowPair* pairs, floa
     __shared__ int hist[32];
     __shared__ int s_ncommon, s_keep[3], s_count;
     const DevBowPair pr = pairs[blockIdx.x];
+    if (pr.general) return;  // k_bow_match_any's pair
     const DevBowSide& A = pr.A;
     const DevBowSide& B = pr.B;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;
@@ -234,32 +265,7 @@ __global__ void __launch_bounds__(512) k_bow_match(const DevBowPair* pairs, floa
         for (int i = tid; i < A.n; i += blockDim.x)
             if (matchA[i] >= 0) atomicAdd(&hist[binA[i]], 1);
         __syncthreads();
-        if (tid == 0) {
-            // ComputeThreeMaxima (ORBmatcher.cc:2515-2556)
-            int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
-            for (int i = 0; i < 30; i++) {
-                const int s = hist[i];
-                if (s > max1) {
-                    max3 = max2; max2 = max1; max1 = s;
-                    ind3 = ind2; ind2 = ind1; ind1 = i;
-                } else if (s > max2) {
-                    max3 = max2; max2 = s;
-                    ind3 = ind2; ind2 = i;
-                } else if (s > max3) {
-                    max3 = s;
-                    ind3 = i;
-                }
-            }
-            if (max2 < 0.1f * (float)max1) {
-                ind2 = -1;
-                ind3 = -1;
-            } else if (max3 < 0.1f * (float)max1) {
-                ind3 = -1;
-            }
-            s_keep[0] = ind1;
-            s_keep[1] = ind2;
-            s_keep[2] = ind3;
-        }
+        if (tid == 0) three_maxima(hist, s_keep);
         __syncthreads();
     }
     if (tid == 0) s_count = 0;
@@ -270,6 +276,112 @@ __global__ void __launch_bounds__(512) k_bow_match(const DevBowPair* pairs, floa
         int m = matchA[i];
         if (m >= 0 && check_ori) {
             const int bn = binA[i];
+            if (bn != s_keep[0] && bn != s_keep[1] && bn != s_keep[2]) m = -1;
+        }
+        pr.a2b[i] = m;
+        if (m >= 0) {
+            pr.b2a[m] = i;
+            cnt++;
+        }
+    }
+    atomicAdd(&s_count, cnt);
+    __syncthreads();
+    if (tid == 0) *pr.nmatches = s_count;
+}
+
+// SearchByBoW for pairs outside k_bow_match's tiles (a side over kBowCap features, over 4096
+// nodes, or a node of B over 4 x 64 candidates): the same algorithm with its state in global
+// memory.  A wave per common node (nodes are independent: a B feature lives in one node),
+// the A features of the node in order, the node's B candidates swept in chunks of 64 twice
+// (best, then the second best over the other positions), the taken flag per B feature in
+// pr.taken, the tentative match in pr.a2b and its rotation bin in pr.bins.
+__global__ void __launch_bounds__(512) k_bow_match_any(const DevBowPair* pairs, float nnratio,
+                                                       int check_ori, int strict) {
+    __shared__ int hist[32];
+    __shared__ int s_keep[3], s_count;
+    const DevBowPair pr = pairs[blockIdx.x];
+    if (!pr.general) return;
+    const DevBowSide& A = pr.A;
+    const DevBowSide& B = pr.B;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;
+    for (int i = tid; i < A.n; i += blockDim.x) {
+        pr.a2b[i] = -1;
+        pr.bins[i] = -1;
+    }
+    for (int i = tid; i < B.n; i += blockDim.x) pr.taken[i] = 0;
+    if (tid < 32) hist[tid] = 0;
+    __syncthreads();
+    for (int ia = wave; ia < A.n_nodes; ia += nwaves) {
+        const uint32_t id = A.node_id[ia];
+        int lo = 0, hi = B.n_nodes;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (B.node_id[mid] < id) lo = mid + 1; else hi = mid;
+        }
+        if (lo >= B.n_nodes || B.node_id[lo] != id) continue;  // wave-uniform
+        const int a0 = A.node_off[ia], a1 = A.node_off[ia + 1];
+        const int b0 = B.node_off[lo], nbn = B.node_off[lo + 1] - b0;
+        for (int pa = a0; pa < a1; pa++) {
+            const int idxA = (int)A.node_feat[pa];
+            if (A.valid && !A.valid[idxA]) continue;
+            const uint4* da = reinterpret_cast<const uint4*>(A.desc + (size_t)idxA * 32);
+            const uint4 q0 = da[0], q1 = da[1];
+            auto dist_at = [&](int p, int& bidx) -> int {  // 1024: not a candidate
+                bidx = (int)B.node_feat[b0 + p];
+                if ((B.valid && !B.valid[bidx]) || pr.taken[bidx]) return 1024;
+                const uint4* d = reinterpret_cast<const uint4*>(B.desc + (size_t)bidx * 32);
+                return hamming32(q0, q1, d[0], d[1]);
+            };
+            uint64_t best = ~0ull;
+            for (int c = 0; c < nbn; c += 64) {
+                const int p = c + lane;
+                int bidx;
+                const int d = p < nbn ? dist_at(p, bidx) : 1024;
+                if (d < 1024) best = min(best, ((uint64_t)d << 32) | (uint64_t)p);
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                const uint64_t x = __shfl_xor(best, o, 64);
+                best = min(best, x);
+            }
+            if (best == ~0ull) continue;
+            const int best1 = (int)(best >> 32), bpos = (int)(best & 0xffffffffu);
+            int sec = 256;
+            for (int c = 0; c < nbn; c += 64) {
+                const int p = c + lane;
+                int bidx;
+                const int d = (p < nbn && p != bpos) ? dist_at(p, bidx) : 1024;
+                if (d < 1024) sec = min(sec, d);
+            }
+            sec = (int)wave_min_u32((uint32_t)sec);
+            const bool pass = (strict ? best1 < 50 : best1 <= 50) && ((float)best1 < nnratio * (float)sec);
+            if (pass && lane == 0) {
+                const int bidx = (int)B.node_feat[b0 + bpos];
+                pr.taken[bidx] = 1;
+                pr.a2b[idxA] = bidx;
+                if (check_ori)
+                    pr.bins[idxA] = (int8_t)rot_bin(A.angle[(size_t)idxA * A.angle_stride],
+                                                     B.angle[(size_t)bidx * B.angle_stride]);
+            }
+            __threadfence_block();  // the taken flag is read by the whole wave next
+        }
+    }
+    __syncthreads();
+    if (check_ori) {
+        for (int i = tid; i < A.n; i += blockDim.x)
+            if (pr.a2b[i] >= 0) atomicAdd(&hist[pr.bins[i]], 1);
+        __syncthreads();
+        if (tid == 0) three_maxima(hist, s_keep);
+        __syncthreads();
+    }
+    if (tid == 0) s_count = 0;
+    for (int i = tid; i < B.n; i += blockDim.x) pr.b2a[i] = -1;
+    __syncthreads();
+    int cnt = 0;
+    for (int i = tid; i < A.n; i += blockDim.x) {
+        int m = pr.a2b[i];
+        if (m >= 0 && check_ori) {
+            const int bn = pr.bins[i];
             if (bn != s_keep[0] && bn != s_keep[1] && bn != s_keep[2]) m = -1;
         }
         pr.a2b[i] = m;
@@ -300,7 +412,7 @@ namespace {
 // features whose word weight is <= 0 are skipped (TemplatedVocabulary.h:1169), std::map
 // keeps nodes ascending: a bitonic sort of (node << 16 | i) gives exactly that CSR.
 // ---------------------------------------------------------------------------------------
-constexpr int kFvMax = 4096;
+constexpr int kFvMax = 8192;  // features per frame (LDS sort keys: 64 KB)
 
 __global__ void __launch_bounds__(1024) k_featvec(int cap, const int32_t* __restrict__ n_per_frame,
                                                   const int32_t* __restrict__ node, const double* __restrict__ weight,
@@ -369,15 +481,16 @@ __global__ void __launch_bounds__(1024) k_featvec(int cap, const int32_t* __rest
     }
 }
 
-// Pair table for k_bow_match from per-frame counts (device side).  Pairs the kernel cannot
-// hold (side > kBowCap features, > 4096 nodes, or a Frame node over 4 x 64 candidates) are
-// skipped and counted in *status.
+// Pair table for k_bow_match from per-frame counts (device side).  Pairs its tiles cannot
+// hold (side > kBowCap features, > 4096 nodes, or a Frame node over 4 x 64 candidates) go to
+// k_bow_match_any instead and are counted in *status.
 __global__ void k_make_pairs(int npairs, const int2* __restrict__ pairs, int cap, const uint8_t* __restrict__ kps,
                              const uint8_t* __restrict__ desc, const int32_t* __restrict__ n_per_frame,
                              const uint8_t* __restrict__ valid, const uint32_t* __restrict__ fv_id,
                              const int32_t* __restrict__ fv_off, const uint32_t* __restrict__ fv_feat,
                              const int32_t* __restrict__ fv_n, int32_t* __restrict__ a2b, int32_t* __restrict__ b2a,
-                             int32_t* __restrict__ nmatch, DevBowPair* __restrict__ out, int* __restrict__ status) {
+                             int32_t* __restrict__ nmatch, DevBowPair* __restrict__ out, int* __restrict__ status,
+                             uint8_t* __restrict__ scratch) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= npairs) return;
     const int2 ab = pairs[p];
@@ -400,15 +513,13 @@ __global__ void k_make_pairs(int npairs, const int2* __restrict__ pairs, int cap
     pr.a2b = a2b + (size_t)p * cap;
     pr.b2a = b2a + (size_t)p * cap;
     pr.nmatches = nmatch + p;
+    pr.bins = reinterpret_cast<int8_t*>(scratch + (size_t)p * 2 * cap);
+    pr.taken = scratch + (size_t)p * 2 * cap + cap;
     bool ok = pr.A.n <= kBowCap && pr.B.n <= kBowCap && pr.A.n_nodes <= 4096 && pr.B.n_nodes <= 4096;
     for (int i = 0; ok && i < pr.B.n_nodes; i++)
         if (pr.B.node_off[i + 1] - pr.B.node_off[i] > 64 * kBowNodeChunks) ok = false;
-    if (!ok) {
-        atomicAdd(status, 1);
-        pr.A.n = 0;
-        pr.A.n_nodes = 0;
-        pr.B.n_nodes = 0;
-    }
+    pr.general = !ok;
+    if (!ok) atomicAdd(status, 1);
     out[p] = pr;
 }
 
@@ -467,7 +578,7 @@ struct slam_matcher {
     hipStream_t stream = nullptr;
     Buf d_pair, d_a, d_b, d_out;
     // batched device path (slamhot_bow_match_batch_device)
-    Buf b_word, b_weight, b_node, b_fv_id, b_fv_off, b_fv_feat, b_fv_n, b_pairs, b_devpairs, b_status;
+    Buf b_word, b_weight, b_node, b_fv_id, b_fv_off, b_fv_feat, b_fv_n, b_pairs, b_devpairs, b_status, b_scratch;
     std::mutex mu;
 };
 
@@ -640,7 +751,7 @@ void slamhot_matcher_destroy(slam_matcher* m) {
     m->d_b.release();
     m->d_out.release();
     for (Buf* b : {&m->b_word, &m->b_weight, &m->b_node, &m->b_fv_id, &m->b_fv_off, &m->b_fv_feat, &m->b_fv_n,
-                   &m->b_pairs, &m->b_devpairs, &m->b_status})
+                   &m->b_pairs, &m->b_devpairs, &m->b_status, &m->b_scratch})
         b->release();
     if (m->stream) (void)hipStreamDestroy(m->stream);
     delete m;
@@ -688,7 +799,7 @@ slam_status upload_bow_side(const slam_bow_side* S, uint8_t* base, DevBowSide& D
 }
 
 bool bow_side_ok(const slam_bow_side* S) {
-    if (!S || S->n < 0 || S->n > kBowCap || S->n_nodes < 0 || S->n_nodes > 4096) return false;
+    if (!S || S->n < 0 || S->n >= (1 << 24) || S->n_nodes < 0) return false;
     if (S->n > 0 && (!S->desc || !S->angle)) return false;
     if (!S->node_off || (S->n_nodes > 0 && (!S->node_id || !S->node_feat))) return false;
     if (S->node_off[0] != 0) return false;
@@ -707,16 +818,17 @@ extern "C" slam_status slamhot_search_by_bow(slam_matcher* m, const slam_bow_sid
                                              float nnratio, int check_ori, int strict, int32_t* a2b,
                                              int32_t* b2a, int* nmatches) {
     if (!m || !bow_side_ok(A) || !bow_side_ok(B) || !a2b || !b2a || !nmatches) return SLAM_EINVAL;
-    // every node of B must be representable in the register tile of k_bow_match
-    for (int i = 0; i < B->n_nodes; i++)
-        if (B->node_off[i + 1] - B->node_off[i] > 64 * kBowNodeChunks) return SLAM_EINVAL;
+    // k_bow_match's LDS / register tiles, else the unbounded k_bow_match_any
+    bool fits = A->n <= kBowCap && B->n <= kBowCap && A->n_nodes <= 4096 && B->n_nodes <= 4096;
+    for (int i = 0; fits && i < B->n_nodes; i++)
+        if (B->node_off[i + 1] - B->node_off[i] > 64 * kBowNodeChunks) fits = false;
     std::lock_guard<std::mutex> g(m->mu);
     SLAM_HIP_TRY(hipSetDevice(m->device));
     slam_status st;
     const size_t ba = bow_side_bytes(A), bb = bow_side_bytes(B);
     const size_t nout = ((size_t)A->n + B->n + 1) * 4;
     if ((st = m->d_a.ensure(ba)) || (st = m->d_b.ensure(bb)) || (st = m->d_out.ensure(nout)) ||
-        (st = m->d_pair.ensure(sizeof(DevBowPair))))
+        (st = m->d_pair.ensure(sizeof(DevBowPair))) || (!fits && (st = m->b_scratch.ensure((size_t)A->n + B->n + 8))))
         return st;
     DevBowPair pr{};
     if ((st = upload_bow_side(A, m->d_a.as<uint8_t>(), pr.A, m->stream)) ||
@@ -725,9 +837,18 @@ extern "C" slam_status slamhot_search_by_bow(slam_matcher* m, const slam_bow_sid
     pr.a2b = m->d_out.as<int32_t>();
     pr.b2a = pr.a2b + A->n;
     pr.nmatches = pr.b2a + B->n;
+    pr.general = !fits;
+    if (!fits) {
+        pr.bins = m->b_scratch.as<int8_t>();
+        pr.taken = m->b_scratch.as<uint8_t>() + A->n;
+    }
     SLAM_HIP_TRY(hipMemcpyAsync(m->d_pair.p, &pr, sizeof(pr), hipMemcpyHostToDevice, m->stream));
-    hipLaunchKernelGGL(k_bow_match, dim3(1), dim3(512), 0, m->stream, m->d_pair.as<DevBowPair>(), nnratio,
-                       check_ori, strict);
+    if (fits)
+        hipLaunchKernelGGL(k_bow_match, dim3(1), dim3(512), 0, m->stream, m->d_pair.as<DevBowPair>(), nnratio,
+                           check_ori, strict);
+    else
+        hipLaunchKernelGGL(k_bow_match_any, dim3(1), dim3(512), 0, m->stream, m->d_pair.as<DevBowPair>(), nnratio,
+                           check_ori, strict);
     SLAM_HIP_TRY(hipGetLastError());
     std::vector<int32_t> out((size_t)A->n + B->n + 1);
     SLAM_HIP_TRY(hipMemcpyAsync(out.data(), m->d_out.p, nout, hipMemcpyDeviceToHost, m->stream));
@@ -757,7 +878,7 @@ extern "C" slam_status slamhot_bow_match_batch_device(slam_matcher* m, slam_voca
         (st = m->b_fv_id.ensure(nf * 4)) || (st = m->b_fv_off.ensure((size_t)nframes * (cap + 1) * 4)) ||
         (st = m->b_fv_feat.ensure(nf * 4)) || (st = m->b_fv_n.ensure((size_t)nframes * 4 + 4)) ||
         (st = m->b_pairs.ensure((size_t)npairs * 8 + 8)) || (st = m->b_devpairs.ensure((size_t)npairs * sizeof(DevBowPair) + 8)) ||
-        (st = m->b_status.ensure(4)))
+        (st = m->b_status.ensure(4)) || (st = m->b_scratch.ensure((size_t)npairs * 2 * cap + 8)))
         return st;
     if (nframes == 0) return SLAM_OK;
     // Frame::ComputeBoW (Frame.cc:721-728): transform every descriptor slot of every frame
@@ -775,8 +896,10 @@ extern "C" slam_status slamhot_bow_match_batch_device(slam_matcher* m, slam_voca
                        (const uint8_t*)d_kps, (const uint8_t*)d_desc, (const int32_t*)d_n, (const uint8_t*)d_valid,
                        m->b_fv_id.as<uint32_t>(), m->b_fv_off.as<int32_t>(), m->b_fv_feat.as<uint32_t>(),
                        m->b_fv_n.as<int32_t>(), (int32_t*)d_a2b, (int32_t*)d_b2a, (int32_t*)d_nmatches,
-                       m->b_devpairs.as<DevBowPair>(), m->b_status.as<int>());
+                       m->b_devpairs.as<DevBowPair>(), m->b_status.as<int>(), m->b_scratch.as<uint8_t>());
     hipLaunchKernelGGL(k_bow_match, dim3(npairs), dim3(512), 0, s, m->b_devpairs.as<DevBowPair>(), nnratio,
+                       check_ori, strict);
+    hipLaunchKernelGGL(k_bow_match_any, dim3(npairs), dim3(512), 0, s, m->b_devpairs.as<DevBowPair>(), nnratio,
                        check_ori, strict);
     SLAM_HIP_TRY(hipGetLastError());
     return SLAM_OK;
@@ -870,6 +993,7 @@ struct DevProjCall {
     int cand_cap;
     int32_t* f_match;       // F.n
     int32_t* out;           // [0] nmatches, [1] status (1 = candidate overflow), [2] iterations
+    int32_t* gstate;        // resolution state in global memory when it exceeds the LDS (else null)
 };
 
 __device__ __forceinline__ void gemm_rx_t(const float* T, const float* X, float* o) {
@@ -1039,7 +1163,7 @@ __global__ void __launch_bounds__(1024) k_search_by_projection(DevProjCall C) {
     // ---- 3. Jacobi resolution of the sequential greedy (state in LDS: owner per
     //         feature, two assignment buffers per query, final match per feature)
     extern __shared__ __attribute__((aligned(16))) int32_t proj_smem[];
-    int32_t* owner = proj_smem;
+    int32_t* owner = C.gstate ? C.gstate : proj_smem;  // one workgroup either way
     int32_t* fm = owner + F.n;
     int32_t* cur = fm + F.n;
     int32_t* nxt = cur + nq;
@@ -1275,6 +1399,8 @@ bool frame_ok(const slam_frame_view* F) {
            F->nlevels <= 16 && F->scale;
 }
 
+constexpr size_t kProjLdsMax = 150 * 1024;
+
 slam_status run_projection(slam_matcher* m, const slam_frame_view* F, DevProjCall& Cc, int nq,
                            const std::vector<ProjQuery>* host_queries, const uint8_t* qdesc,
                            int32_t* f_match, int* nmatches,
@@ -1287,7 +1413,7 @@ slam_status run_projection(slam_matcher* m, const slam_frame_view* F, DevProjCal
     for (int attempt = 0; attempt < 2; attempt++) {
         const size_t need = (size_t)F->n * (sizeof(slam_keypoint) + 4 + 32 + 1 + 4 * 2) + start.size() * 4 +
                             feat.size() * 4 + (size_t)nq * (sizeof(ProjQuery) + 32 + 4 * 3 + 2 * sizeof(slam_mp_track) + sizeof(slam_mp_geom) + 64) +
-                            (size_t)cap * 4 + 64 * 1024;
+                            (size_t)cap * 4 + 64 * 1024 + (size_t)4 * (2 * (size_t)F->n + 2 * (size_t)nq) + 512;
         slam_status st;
         if ((st = m->d_a.ensure(need * 2))) return st;
         Blob B{m->d_a.as<uint8_t>(), 0, m->stream};
@@ -1310,8 +1436,12 @@ slam_status run_projection(slam_matcher* m, const slam_frame_view* F, DevProjCal
         C.f_match = B.take<int32_t>(std::max(1, F->n));
         C.out = B.take<int32_t>(4);
         SLAM_HIP_TRY(hipMemsetAsync(C.out, 0, 16, m->stream));
-        const size_t lds = (size_t)4 * (2 * (size_t)F->n + 2 * (size_t)nq);
-        if (lds > 150 * 1024) return SLAM_EINVAL;
+        size_t lds = (size_t)4 * (2 * (size_t)F->n + 2 * (size_t)nq);
+        C.gstate = nullptr;
+        if (lds > kProjLdsMax) {  // large local map: the owner / match / assignment arrays in HBM
+            C.gstate = B.take<int32_t>(2 * (size_t)F->n + 2 * (size_t)nq);
+            lds = 0;
+        }
         SLAM_HIP_TRY(hipFuncSetAttribute((const void*)k_search_by_projection,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds + 16));
         hipLaunchKernelGGL(k_search_by_projection, dim3(1), dim3(1024), lds, m->stream, C);

@@ -157,3 +157,115 @@ def test_bow_match_batch_device(gpu_vocab, vocab_arrays):
     assert total > 100
     m.close()
     ex.close()
+
+
+def _clustered_desc(rng, n, centres, flips=1):
+    """n descriptors drawn around a few centres (a few random bit flips each): most land in one
+    vocabulary node, so nodes far above k_bow_match's 256-candidate tile appear."""
+    d = centres[rng.integers(0, len(centres), n)].copy()
+    for i in range(n):
+        for b in rng.integers(0, 256, flips):
+            d[i, b >> 3] ^= np.uint8(1 << (b & 7))
+    return d
+
+
+def _kps(rng, n):
+    k = np.zeros(n, ob.KP_DTYPE)
+    k["angle"] = rng.uniform(0, 360, n).astype(np.float32)
+    return k
+
+
+@pytest.mark.parametrize("strict", [False, True])
+def test_search_by_bow_general_path_big_nodes(gpu_vocab, strict):
+    """A node of B over 4 x 64 candidates: the unbounded kernel gives the oracle's matches."""
+    import slamhot
+    rng = np.random.default_rng(40)
+    centres = rng.integers(0, 256, (2, 32), dtype=np.uint8)
+    d0, d1 = _clustered_desc(rng, 900, centres), _clustered_desc(rng, 800, centres)
+    k0, k1 = _kps(rng, len(d0)), _kps(rng, len(d1))
+    valid = (rng.random(len(d0)) < 0.9).astype(np.uint8)
+    A = _side(gpu_vocab, k0, d0, valid)
+    B = _side(gpu_vocab, k1, d1, None)
+    assert np.diff(B[4]).max() > 256  # the general path is exercised
+    m = slamhot.ORBmatcher(0.9, True)
+    if strict:
+        ng, a2b_g = m.SearchByBoW_KF_KF(A, B)
+        no, a2b_o, _ = ob.search_by_bow(A, B, 0.9, True, True)
+        assert np.array_equal(a2b_g, a2b_o)
+    else:
+        ng, b2a_g = m.SearchByBoW_KF_F(A, B)
+        no, _, b2a_o = ob.search_by_bow(A, B, 0.9, True, False)
+        assert np.array_equal(b2a_g, b2a_o)
+    assert ng == no and no > 0
+    m.close()
+
+
+def test_search_by_bow_general_path_large_sides(gpu_vocab):
+    """Sides over k_bow_match's 8192-feature LDS tile."""
+    import slamhot
+    rng = np.random.default_rng(41)
+    base = rng.integers(0, 256, (9000, 32), dtype=np.uint8)
+    d0 = base.copy()
+    d1 = base[rng.permutation(len(base))[:8500]].copy()
+    for d in (d0, d1):
+        for i in range(len(d)):
+            b = rng.integers(0, 256)
+            d[i, b >> 3] ^= np.uint8(1 << (b & 7))
+    k0, k1 = _kps(rng, len(d0)), _kps(rng, len(d1))
+    A = _side(gpu_vocab, k0, d0, None)
+    B = _side(gpu_vocab, k1, d1, None)
+    m = slamhot.ORBmatcher(0.75, False)
+    ng, b2a_g = m.SearchByBoW_KF_F(A, B)
+    no, _, b2a_o = ob.search_by_bow(A, B, 0.75, False, False)
+    assert ng == no and no > 1000
+    assert np.array_equal(b2a_g, b2a_o)
+    m.close()
+
+
+def test_bow_match_batch_general_pairs(gpu_vocab, vocab_arrays):
+    """Batched path: pairs whose frame has a node over 256 candidates take the unbounded
+    kernel (reported by the status call) and every pair's outputs equal the oracle's."""
+    import torch
+
+    import slamhot
+    par, leaf, dn, wn = vocab_arrays
+    rng = np.random.default_rng(42)
+    centres = rng.integers(0, 256, (2, 32), dtype=np.uint8)
+    F, cap = 4, 1200
+    ns = [1100, 1000, 1200, 900]
+    kps = np.zeros((F, cap), ob.KP_DTYPE)
+    desc = np.zeros((F, cap, 32), np.uint8)
+    for f in range(F):
+        n = ns[f]
+        d = _clustered_desc(rng, n, centres) if f in (1, 3) else rng.integers(0, 256, (n, 32), dtype=np.uint8)
+        if f == 2:  # near-copies of frame 1 so that its pairs match
+            d = desc[1, :n].copy()
+            d[:, 0] ^= np.uint8(1)
+        desc[f, :n] = d
+        kps[f, :n] = _kps(rng, n)
+    dev = torch.device("cuda", 0)
+    d_kps = torch.from_numpy(kps.view(np.uint8).reshape(F, cap, 28).copy()).to(dev)
+    d_desc = torch.from_numpy(desc).to(dev)
+    d_n = torch.tensor(ns, dtype=torch.int32, device=dev)
+    pairs = [(0, 1), (2, 1), (1, 3), (0, 2), (3, 3)]
+    d_a2b = torch.zeros((len(pairs), cap), dtype=torch.int32, device=dev)
+    d_b2a = torch.zeros((len(pairs), cap), dtype=torch.int32, device=dev)
+    d_nm = torch.zeros(len(pairs), dtype=torch.int32, device=dev)
+    m = slamhot.ORBmatcher(0.9, True)
+    m.bow_match_batch_device(gpu_vocab, F, d_kps.data_ptr(), d_desc.data_ptr(), cap, d_n.data_ptr(), pairs,
+                             d_a2b.data_ptr(), d_b2a.data_ptr(), d_nm.data_ptr())
+    n_general = m.bow_match_batch_status()
+    a2b, b2a, nm = d_a2b.cpu().numpy(), d_b2a.cpu().numpy(), d_nm.cpu().numpy()
+    expect_general = 0
+    for p, (a, b) in enumerate(pairs):
+        _, wta, nia = ob.vocab_transform(par, leaf, dn, wn, 6, desc[a, : ns[a]], 4)
+        _, wtb, nib = ob.vocab_transform(par, leaf, dn, wn, 6, desc[b, : ns[b]], 4)
+        A = (desc[a, : ns[a]], kps[a, : ns[a]]["angle"], None) + synth.feature_vector(nia, wta)
+        B = (desc[b, : ns[b]], kps[b, : ns[b]]["angle"], None) + synth.feature_vector(nib, wtb)
+        expect_general += int(np.diff(B[4]).max() > 256)
+        no, a2b_o, b2a_o = ob.search_by_bow(A, B, 0.9, True, False)
+        assert nm[p] == no
+        assert np.array_equal(a2b[p, : ns[a]], a2b_o)
+        assert np.array_equal(b2a[p, : ns[b]], b2a_o)
+    assert n_general == expect_general and n_general >= 2
+    m.close()

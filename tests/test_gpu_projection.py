@@ -78,3 +78,19 @@ def test_search_local_points(seed, th, far):
     no, fo = ob.search_by_projection_local(fv, tro, desc, 0.8, th, far, 20.0)
     assert ng == no and no > 50
     assert np.array_equal(fg, fo)
+
+
+def test_local_map_above_lds_cap():
+    """A local map whose resolution state (4 (2N + 2 nMP) bytes) exceeds the 150 KB LDS budget:
+    the state moves to HBM and the matches stay the oracle's (the reference has no such limit)."""
+    import slamhot
+    S = scenes.scene(10)
+    fv, keep = scenes.frame_view(S, with_pose=False)
+    mps, desc = scenes.local_map(S, n_extra=20000)
+    assert 4 * (2 * fv.n + 2 * len(mps)) > 150 * 1024
+    m = slamhot.ORBmatcher(0.8)
+    ng, fg = m.SearchByProjection_local(fv, mps, desc, 3.0, False, 20.0)
+    no, fo = ob.search_by_projection_local(fv, mps, desc, 0.8, 3.0, False, 20.0)
+    m.close()
+    assert ng == no and ng > 50
+    assert np.array_equal(fg, fo)
