@@ -1,22 +1,30 @@
 #!/usr/bin/env python3
 """bench.py — MI355X throughput of the ORB-SLAM3 hot path (BASELINE.json configs).
 
-Headline (N=1 default): BASELINE.json configs[1] — synthetic 640x480, 8-level pyramid,
-1000 features/frame, ORBextractor only.  One step = one pass of the extractor over a batch
-of B synthetic frames already resident in HBM.  value = frames/s of the whole job.
+Headline (`value`): BASELINE.json's metric "ORB extract+match frames/s" on the configuration it
+names for it, configs[2] — EuRoC-shaped stereo (752x480, 1200 features/frame, EuRoC
+calibration): one step takes P raw stereo frames already resident in HBM through
+  cv::remap x2 (stereo_euroc.cc:168-169) -> ORBextractor x2 (Frame.cc:119-122) ->
+  Frame::ComputeStereoMatches -> Frame::ComputeBoW -> ORBmatcher::SearchByBoW(KF, F) against
+  the previous frame of its sequence (Tracking::TrackReferenceKeyFrame, Tracking.cc:2800-2830)
+with everything device-resident.  The images are synthetic renders of a textured room along
+smooth camera paths (slamhot/synth.py: stereo_sequence), pushed back through the EuRoC
+calibration to raw camera images; the vocabulary is a synthetic k=10 L=6 tree (no ORBvoc.txt
+in this image).  value = stereo frames/s of the whole job.
 
-Multi-GPU: one process per GPU (torch.distributed.run); each rank extracts its own batch
-(frames are independent: weak scaling, no collective on the data path).  Timing is
-barrier + synchronize on both sides of exactly K steps; the max over ranks is reported.
+Also reported, each with its own roofline / CPU baseline where it has one:
+  extract  configs[1]: ORBextractor-only, synthetic 640x480 8-level pyramid, 1000 features,
+           plus the drop-in path's host-image -> host-keypoints rate and single-frame latency
+  lba      configs[3]: Optimizer::LocalBundleAdjustment LM/Schur on 50 KF x 2000 pt x 8 obs
+           windows (LM iterations/s, FP64 FLOP/s vs peak, ATE vs ground truth and vs the oracle)
+  pose     Optimizer::PoseOptimization frames/s
+  track    configs[4] per GPU: the per-sequence stereo tracking chain (slamhot_tracker_*)
 
-Also reported: the dominant kernel's roofline (HIP events around every stage during the
-timed steps), and the CPU baseline (the oracle restatement, rank 0 at N=1 only).
-
-Second leg ("lba", BASELINE.json configs[3]): Optimizer::LocalBundleAdjustment's LM/Schur
-solve on synthetic 50 KF x 2000 point x 8 observation windows (2% outliers, 48 free KFs),
-a batch of independent windows per GPU per call (windows shard across ranks like frames).
-Reported as LM iterations/s (one OptimizationAlgorithmLevenberg::solve incl. its trials),
-whole job, plus LBA calls/s, the single-window latency and the oracle's single-core rate.
+Multi-GPU: one process per GPU (torch.distributed.run), every rank runs its own frames /
+windows / sequences (independent units: weak scaling, no collective on the data path).
+Timing is barrier + synchronize on both sides of exactly K steps; the max over ranks is
+reported.  CPU baselines (the oracle restatement on the host cores, rank 0 at N=1 only) run
+after the timed regions.
 """
 from __future__ import annotations
 
@@ -25,6 +33,7 @@ import json
 import os
 import sys
 import time
+from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path
 
 import numpy as np
@@ -32,7 +41,11 @@ import numpy as np
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "orb-slam3-noted_amd"))
 
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E (MI355X_MICROARCH.md, chip-level parameters)
+VALU_PEAK_WAVE_INSTR = 256 * 4 * 2.4e9 / 2  # 256 CUs x 4 SIMDs, one wave64 VALU instr / 2 cycles, 2.4 GHz
+FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector / matrix (spec)
+LBA_FLOP_PER_ITER = 31.85e6    # one LM iteration of a config-4 window, one trial
+LBA_FLOP_PER_EXTRA_TRIAL = 27.05e6  # Schur 17.59 + Cholesky 8.13 + back-substitution 0.61 + errors 0.72
 
 
 def level_sizes(w, h, nlevels=8, scale=1.2):
@@ -48,7 +61,7 @@ def level_sizes(w, h, nlevels=8, scale=1.2):
 
 
 def algorithmic_bytes(w, h, kps_per_frame):
-    """Per-frame algorithmic HBM bytes of each stage."""
+    """Per-frame algorithmic HBM bytes of each extractor stage."""
     sz = level_sizes(w, h)
     P = [a * b for a, b in sz]
     out = {
@@ -62,26 +75,108 @@ def algorithmic_bytes(w, h, kps_per_frame):
     return out, pipeline
 
 
+def host_cores():
+    """CPU threads for the CPU baselines: this process's affinity, capped at the GPU box's CPU
+    share per GPU (16; the box's nproc shows the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(n, 16))
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def timed_region(dist, device, fn, steps):
+    """barrier + synchronize, K calls of fn(i), synchronize + barrier; seconds."""
+    import torch
+    torch.cuda.synchronize(device)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        fn(i)
+    torch.cuda.synchronize(device)
+    if dist:
+        dist.barrier()
+    return time.perf_counter() - t0
+
+
+def roofline_from_stages(stages, calls, frames_per_call, W, H, kps_per_frame):
+    """Dominant extractor kernel vs the HBM peak (+ its VALU issue rate when a PMC summary of the
+    same kernel and shape is committed under profiles/)."""
+    alg, _ = algorithmic_bytes(W, H, kps_per_frame)
+    dom = max(stages, key=lambda k: stages[k][0])
+    dom_ms, launches = stages[dom]
+    avg_s = dom_ms / 1000.0 / max(launches, 1)
+    frames_per_launch = frames_per_call * calls / max(launches, 1)
+    dom_bytes = alg.get(dom, 0) * frames_per_launch
+    achieved = dom_bytes / avg_s / 1e9 if avg_s > 0 else 0.0
+    traffic, valu = None, None
+    tf = ROOT / "profiles" / "traffic_latest.json"
+    if tf.exists():
+        try:
+            tj = json.loads(tf.read_text())
+            if tj.get("kernel") == dom and tj.get("batch") == frames_per_launch and tj.get("width") == W:
+                traffic = tj.get("bytes_per_launch")
+                if tj.get("valu_instr_per_launch"):
+                    vi = float(tj["valu_instr_per_launch"])
+                    valu = {"achieved": round(vi / avg_s / 1e12, 4), "peak": round(VALU_PEAK_WAVE_INSTR / 1e12, 4),
+                            "unit": "T wave64 VALU instr/s", "frac": round(vi / avg_s / VALU_PEAK_WAVE_INSTR, 4),
+                            "valu_instr_per_launch": int(vi), "source": "SQ_INSTS_VALU, profiles/traffic_latest.json"}
+        except Exception:
+            traffic = None
+    roof = {
+        "bound": "hbm",
+        "kernel": dom,
+        "achieved": round(achieved, 2),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 5),
+        "traffic": traffic,
+        "algorithmic_bytes_per_launch": int(dom_bytes),
+        "frames_per_launch": frames_per_launch,
+        "measured": "HIP events on the launch stream, isolated pass after the timed region (1 batch in flight)",
+        "avg_launch_ms": round(avg_s * 1000.0, 5),
+    }
+    if valu:
+        roof["valu_ceiling"] = valu
+    return roof
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=256, help="frames per GPU per step")
+    ap.add_argument("--legs", default="headline,extract,lba,pose,track",
+                    help="comma list of legs to run (headline = configs[2] extract+match)")
+    ap.add_argument("--pairs", type=int, default=128, help="headline: stereo frames per GPU per step")
+    ap.add_argument("--inflight", type=int, default=3, help="batches in flight (handles / streams) per leg")
+    ap.add_argument("--batch", type=int, default=256, help="extract leg: frames per GPU per step")
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--nfeatures", type=int, default=1000)
-    ap.add_argument("--unique", type=int, default=256, help="distinct synthetic frames per rank")
+    ap.add_argument("--unique", type=int, default=256, help="extract leg: distinct synthetic frames per rank")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=384)
-    ap.add_argument("--lba-windows", type=int, default=64, help="LBA windows per GPU per call (0 = skip)")
+    ap.add_argument("--lba-windows", type=int, default=64, help="LBA windows per GPU per call")
     ap.add_argument("--lba-calls", type=int, default=3)
     ap.add_argument("--lba-inflight", type=int, default=3, help="LBA solver handles driven concurrently")
-    ap.add_argument("--match-pairs", type=int, default=128, help="(keyframe, frame) pairs per GPU per step (0 = skip)")
-    ap.add_argument("--pose-frames", type=int, default=512, help="PoseOptimization frames per GPU per call (0 = skip)")
-    ap.add_argument("--stereo-pairs", type=int, default=128, help="stereo frames per GPU per step (0 = skip)")
-    ap.add_argument("--inflight", type=int, default=3, help="extraction batches in flight (handles / streams)")
+    ap.add_argument("--pose-frames", type=int, default=512, help="PoseOptimization frames per GPU per call")
+    ap.add_argument("--track-seqs", type=int, default=64, help="track leg: sequences per GPU (lock-step)")
+    ap.add_argument("--track-frames", type=int, default=24, help="track leg: frames per sequence")
     args = ap.parse_args()
+    legs = set(x.strip() for x in args.legs.split(",") if x.strip())
 
     import torch
 
@@ -96,21 +191,266 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     device = torch.device("cuda", local_rank)
     torch.cuda.set_device(device)
+    ctx = dict(args=args, rank=rank, world=world, local_rank=local_rank, dist=dist, device=device,
+               cpu=(rank == 0 and world == 1 and not args.no_cpu_baseline))
+
+    result = {
+        "metric": "ORB extract+match frames/s and LocalBA iters/s per GPU; ATE vs reference",
+        "value": None, "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": None, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (rendered textured-room stereo sequences / procedural frames, slamhot/synth.py)",
+    }
+    if "headline" in legs:
+        h = headline_leg(ctx)
+        for k in ("value", "ms_per_step", "config", "roofline", "cpu_baseline"):
+            if k in h:
+                result[k] = h.pop(k)
+        result["headline_detail"] = h
+    if "extract" in legs:
+        result["extract"] = extract_leg(ctx)
+        if result["value"] is None:  # headline off (profiling runs): the extract leg's line
+            e = result["extract"]
+            result.update(value=e["value"], ms_per_step=e["ms_per_step"], config=e["config"],
+                          roofline=e["roofline"])
+    if "lba" in legs and args.lba_windows > 0:
+        result["lba"] = lba_leg(ctx)
+    if "pose" in legs and args.pose_frames > 0:
+        result["pose"] = pose_leg(ctx)
+    if "track" in legs and args.track_seqs > 0:
+        result["track"] = track_leg(ctx)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+# ------------------------------------------------------------------------------------------
+# headline: configs[2] stereo extract + match
+# ------------------------------------------------------------------------------------------
+SEQ_LEN = 8      # consecutive frames per synthetic sequence chunk
+N_SEQ = 2        # distinct sequences per rank
+
+
+def euroc_maps():
+    from slamhot import euroc
+    calib = {k: np.array(v) if isinstance(v, list) else v
+             for k, v in json.loads((ROOT / "tests" / "golden" / "euroc_stereo_calib.json").read_text()).items()}
+    return [euroc.init_undistort_rectify_map(calib[f"{sd}.K"], calib[f"{sd}.D"], calib[f"{sd}.R"], calib[f"{sd}.P"],
+                                             (752, 480)) for sd in ("LEFT", "RIGHT")]
+
+
+def stereo_chunks(rank, maps):
+    """N_SEQ rendered sequences of SEQ_LEN raw stereo frames for this rank: (raw L, raw R)."""
+    from slamhot import synth
+    Ls, Rs = [], []
+    for s in range(N_SEQ):
+        L, R, _ = synth.stereo_sequence(101 + 17 * rank + s, SEQ_LEN)
+        Ls += [synth.unrectify(im, *maps[0]) for im in L]
+        Rs += [synth.unrectify(im, *maps[1]) for im in R]
+    return np.stack(Ls), np.stack(Rs)
+
+
+def kf_of(i):
+    """Reference keyframe of batch frame i: the previous frame of its sequence chunk (the chunk's
+    first frame takes its last one)."""
+    return i - 1 if i % SEQ_LEN else i + SEQ_LEN - 1
+
+
+def headline_leg(ctx):
+    import torch
+
+    import slamhot
+    from slamhot import dist as sdist
+    from slamhot import euroc, synth
+    args, device, dist, lr = ctx["args"], ctx["device"], ctx["dist"], ctx["local_rank"]
+    W, H, NF = 752, 480, 1200
+    P = max(SEQ_LEN, args.pairs // SEQ_LEN * SEQ_LEN)
+    maps = euroc_maps()
+    raw_l, raw_r = stereo_chunks(ctx["rank"], maps)
+    nu = len(raw_l)
+    il = np.stack([raw_l[i % nu] for i in range(P)])
+    ir = np.stack([raw_r[i % nu] for i in range(P)])
+    pairs = [(kf_of(i), i) for i in range(P)]
+    mbf = synth.EUROC_STEREO["bf"]
+    mb = mbf / synth.EUROC_STEREO["fx"]
+    voc_arrays = sdist.broadcast_arrays(dist, device, synth.vocab(10, 6, 0) if ctx["rank"] == 0 else None)
+    voc = slamhot.Vocabulary(*voc_arrays, k=10, L=6, device=lr)
+    d_raw_l, d_raw_r = torch.from_numpy(il).to(device), torch.from_numpy(ir).to(device)
+    NS = max(1, args.inflight)
+
+    class Slot:
+        pass
+
+    slots = []
+    for _ in range(NS):
+        s = Slot()
+        s.rect = [euroc.Rectifier(*mp, device=lr) for mp in maps]
+        s.exl = slamhot.ORBextractor(nfeatures=NF, device=lr, max_size=(W, H), max_batch=P)
+        s.exr = slamhot.ORBextractor(nfeatures=NF, device=lr, max_size=(W, H), max_batch=P)
+        s.sm = slamhot.StereoMatcher(device=lr)
+        s.m = slamhot.ORBmatcher(0.7, True, device=lr)
+        cap = s.exl.cap
+        s.img = [torch.empty_like(d_raw_l), torch.empty_like(d_raw_r)]
+        s.out = [(torch.zeros((P, cap, 28), dtype=torch.uint8, device=device),
+                  torch.zeros((P, cap, 32), dtype=torch.uint8, device=device),
+                  torch.zeros(P, dtype=torch.int32, device=device), torch.zeros(P, dtype=torch.int32, device=device))
+                 for _ in range(2)]
+        s.ur = torch.empty((P, cap), dtype=torch.float32, device=device)
+        s.dep = torch.empty((P, cap), dtype=torch.float32, device=device)
+        s.a2b = torch.zeros((P, cap), dtype=torch.int32, device=device)
+        s.b2a = torch.zeros((P, cap), dtype=torch.int32, device=device)
+        s.nm = torch.zeros(P, dtype=torch.int32, device=device)
+        s.stream = torch.cuda.Stream(device)
+        slots.append(s)
+    cap = slots[0].exl.cap
+    ev = {"rectify": [], "extract": [], "stereo": [], "bow": []}
+
+    def step(i, timed=False):
+        s = slots[i % NS]
+        st = s.stream.cuda_stream
+        marks = []
+
+        def mark():
+            if timed:
+                e = torch.cuda.Event(enable_timing=True)
+                e.record(s.stream)
+                marks.append(e)
+        mark()
+        for rc, raw, out in ((s.rect[0], d_raw_l, s.img[0]), (s.rect[1], d_raw_r, s.img[1])):
+            rc.rectify_batch_device(P, raw.data_ptr(), W, W * H, out.data_ptr(), W, W * H, stream=st)
+        mark()
+        for ex, img, (k, d, n, m) in ((s.exl, s.img[0], s.out[0]), (s.exr, s.img[1], s.out[1])):
+            ex.extract_batch_device(img.data_ptr(), P, W, H, k.data_ptr(), d.data_ptr(), cap, n.data_ptr(),
+                                    m.data_ptr(), stream=st)
+        mark()
+        (kl, dl, nl, _), (kr, dr, nr, _) = s.out
+        s.sm.match_batch_device(s.exl, s.exr, P, kl.data_ptr(), dl.data_ptr(), nl.data_ptr(), kr.data_ptr(),
+                                dr.data_ptr(), nr.data_ptr(), cap, mbf, mb, s.ur.data_ptr(), s.dep.data_ptr(),
+                                stream=st)
+        mark()
+        s.m.bow_match_batch_device(voc, P, kl.data_ptr(), dl.data_ptr(), cap, nl.data_ptr(), pairs, s.a2b.data_ptr(),
+                                   s.b2a.data_ptr(), s.nm.data_ptr(), stream=st)
+        mark()
+        if timed:
+            for k_, a, b in zip(("rectify", "extract", "stereo", "bow"), marks[:-1], marks[1:]):
+                ev[k_].append((a, b))
+
+    for i in range(max(args.warmup, 1)):
+        step(i)
+    elapsed = timed_region(dist, device, step, args.steps)
+    # isolated pass: one batch in flight, per-stage HIP events (extractor stages on the left
+    # handle; `rocprofv3 ... bench.py --legs headline --inflight 1` reproduces the kernel times)
+    s0 = slots[0]
+    s0.exl.stage_stats(reset=True)
+    s0.exl.set_profiling(True)
+    nprof = max(10, min(args.steps, 50))
+    for _ in range(nprof):
+        step(0, timed=True)
+    torch.cuda.synchronize(device)
+    s0.exl.set_profiling(False)
+    stages = s0.exl.stage_stats(reset=True)
+    stage_ms = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in ev.items()}
+
+    nl_h = s0.out[0][2].cpu().numpy()
+    nm_h = s0.nm.cpu().numpy()
+    ur_h = s0.ur.cpu().numpy()
+    skipped = s0.m.bow_match_batch_status(s0.stream.cuda_stream)
+    kps_per_frame = float(nl_h.mean())
+    dig = sdist.digest(s0.out[0][1][:, :64].cpu().numpy(), s0.a2b[:, :64].cpu().numpy())
+    el, frames_all = sdist.reduce_run(dist, device, elapsed, float(P * args.steps))
+    digs = sdist.gather_digests(dist, device, ctx["world"], int(nm_h.sum()), dig)
+    out = {
+        "value": round(frames_all / el, 2),
+        "ms_per_step": round(el / args.steps * 1e3, 4),
+        "config": {
+            "workload": f"configs[2] shape: stereo {W}x{H} raw pairs (EuRoC calibration) -> remap x2 -> "
+                        f"ORBextractor x2 ({NF} feat, 8 levels, 1.2, 20/7) -> ComputeStereoMatches -> ComputeBoW "
+                        f"-> SearchByBoW(previous frame as KF, F) (nnratio 0.7, checkOri); synthetic k=10 L=6 "
+                        f"vocabulary",
+            "stereo_frames_per_gpu_per_step": P, "parallelism": f"frame-sharded x{ctx['world']}",
+            "batches_in_flight": NS, "keypoints_per_frame": round(kps_per_frame, 1),
+        },
+        "roofline": roofline_from_stages(stages, nprof, P, W, H, kps_per_frame),
+        "stage_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},
+        "extractor_stage_ms_per_launch": {k: round(v[0] / max(v[1], 1), 5) for k, v in stages.items()},
+        "matches_per_pair": round(float(nm_h.mean()), 1),
+        "stereo_matches_per_frame": round(float(np.mean([(ur_h[f, :nl_h[f]] >= 0).sum() for f in range(P)])), 1),
+        "bow_general_pairs": skipped,
+        "rank_digests": [d for _, d in digs],
+    }
+    if ctx["cpu"]:
+        out["cpu_baseline"] = headline_cpu(raw_l, raw_r, maps, voc_arrays, mbf, mb, NF)
+    for s in slots:
+        for rc in s.rect:
+            rc.close()
+        s.exl.close()
+        s.exr.close()
+        s.sm.close()
+        s.m.close()
+    voc.close()
+    return out
+
+
+def headline_cpu(raw_l, raw_r, maps, voc_arrays, mbf, mb, NF):
+    """The oracle chain (restated reference CPU path) on the host cores: one sequence chunk per
+    thread, frames in order (KF = previous frame), each frame remap x2 + extract x2 +
+    ComputeStereoMatches + vocabulary transform + FeatureVector + SearchByBoW."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_bind as ob
+    from slamhot import synth
+    par, leaf, dn, wn = voc_arrays
+    p = ob.params(nfeatures=NF)
+    sc, isc, _, _, _ = ob.levels(p)
+
+    def chunk(c):
+        prev = None
+        base = (c % N_SEQ) * SEQ_LEN
+        for j in range(SEQ_LEN):
+            l_img = ob.remap_linear(raw_l[base + j], *maps[0])
+            r_img = ob.remap_linear(raw_r[base + j], *maps[1])
+            kl, dl, _ = ob.extract(l_img, p)
+            kr, dr, _ = ob.extract(r_img, p)
+            ob.stereo_matches(kl, dl, kr, dr, ob.pyramid(l_img, p), ob.pyramid(r_img, p), sc, isc, mbf, mb)
+            _, wt, nid = ob.vocab_transform(par, leaf, dn, wn, 6, dl, 4)
+            side = (dl, kl["angle"], None) + synth.feature_vector(nid, wt)
+            if prev is not None:
+                ob.search_by_bow(prev, side, 0.7, True, False)
+            prev = side
+        return SEQ_LEN
+
+    cores = host_cores()
+    nchunks = 2 * cores
+    chunk(0)  # warm-up
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(cores) as pool:
+        frames = sum(pool.map(chunk, range(nchunks)))
+    dt = time.perf_counter() - t0
+    return {"value": round(frames / dt, 2), "unit": "frames/s", "cores": cores, "kind": "port",
+            "cpu": cpu_model(),
+            "sample": f"{nchunks} sequence chunks x {SEQ_LEN} stereo frames, one chunk per thread on {cores} "
+                      f"threads: oracle remap x2 + extract x2 (+ the stereo pyramids) + stereo_oracle + vocabulary "
+                      f"transform + FeatureVector + SearchByBoW; oracle -O3"}
+
+
+# ------------------------------------------------------------------------------------------
+# extract: configs[1] ORBextractor-only + the drop-in host path
+# ------------------------------------------------------------------------------------------
+def extract_leg(ctx):
+    import torch
 
     import slamhot
     from slamhot import dist as sdist
     from slamhot import synth
-
+    args, device, dist, rank = ctx["args"], ctx["device"], ctx["dist"], ctx["rank"]
     W, H, B = args.width, args.height, args.batch
     nuniq = min(args.unique, B)
     base = synth.frames(range(rank * 100000, rank * 100000 + nuniq), W, H)
     frames_np = np.concatenate([base] * ((B + nuniq - 1) // nuniq))[:B]
     d_imgs = torch.from_numpy(frames_np).to(device)
     # `inflight` batches in flight: each slot has its own extractor handle (scratch), output
-    # buffers and stream, so consecutive batches overlap the way a serving loop keeps several
-    # requests on the GPU; every frame of every step is still processed inside the timed region
+    # buffers and stream; every frame of every step is still processed inside the timed region
     NS = max(1, args.inflight)
-    exs = [slamhot.ORBextractor(nfeatures=args.nfeatures, device=local_rank, max_size=(W, H), max_batch=B)
+    exs = [slamhot.ORBextractor(nfeatures=args.nfeatures, device=ctx["local_rank"], max_size=(W, H), max_batch=B)
            for _ in range(NS)]
     ex = exs[0]
     cap = ex.cap
@@ -118,238 +458,103 @@ def main():
              torch.zeros((B, cap, 32), dtype=torch.uint8, device=device),
              torch.zeros(B, dtype=torch.int32, device=device), torch.zeros(B, dtype=torch.int32, device=device))
             for _ in range(NS)]
-    d_kps, d_desc, d_n, d_mono = outs[0]
-    stream_objs = [torch.cuda.Stream(device) for _ in range(NS)]
-    calls = [0] * NS
+    streams = [torch.cuda.Stream(device) for _ in range(NS)]
 
     def step(i):
         k_, d_, n_, m_ = outs[i % NS]
         exs[i % NS].extract_batch_device(d_imgs.data_ptr(), B, W, H, k_.data_ptr(), d_.data_ptr(), cap, n_.data_ptr(),
-                                         m_.data_ptr(), lap=(0, 0), stream=stream_objs[i % NS].cuda_stream)
-        calls[i % NS] += 1
+                                         m_.data_ptr(), lap=(0, 0), stream=streams[i % NS].cuda_stream)
 
     for i in range(args.warmup):
         step(i)
-    torch.cuda.synchronize(device)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(device)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i)
-    torch.cuda.synchronize(device)
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    # per-stage HIP-event timing in a second, isolated pass: K batches through handle 0 alone
-    # (one batch in flight), so each stage's launch duration is the kernel's own, not shared
-    # with concurrent batches; `rocprofv3 ... bench.py --inflight 1` reproduces it
+    elapsed = timed_region(dist, device, step, args.steps)
     ex.stage_stats(reset=True)
     ex.set_profiling(True)
-    calls[0] = 0
-    for i in range(args.steps):
+    for _ in range(args.steps):
         step(0)
     torch.cuda.synchronize(device)
     ex.set_profiling(False)
     stages = ex.stage_stats(reset=True)
-    prof_calls = calls[0]
-
-    n_host = d_n.cpu().numpy()
+    n_host = outs[0][2].cpu().numpy()
     kps_per_frame = float(n_host.mean())
-    dig = sdist.digest(d_desc[:, :64].cpu().numpy())
-    elapsed, _ = sdist.reduce_run(dist, device, elapsed, B * args.steps)
-    total_kps = sum(c for c, _ in sdist.gather_digests(dist, device, world, int(n_host.sum()), dig))
+    el, frames_all = sdist.reduce_run(dist, device, elapsed, float(B * args.steps))
+    _, pipe_bytes = algorithmic_bytes(W, H, kps_per_frame)
+    ms_per_step = el / args.steps * 1000.0
 
-    frames_total = B * args.steps * world
-    value = frames_total / elapsed
-    ms_per_step = elapsed / args.steps * 1000.0
-
-    # dominant kernel roofline (HIP events around each stage, on the launch stream)
-    alg, pipe_bytes = algorithmic_bytes(W, H, kps_per_frame)
-    dom = max(stages, key=lambda k: stages[k][0])
-    dom_ms, dom_launches = stages[dom]
-    dom_avg_s = dom_ms / 1000.0 / max(dom_launches, 1)
-    # the extractor splits a batch into frame ranges on concurrent streams: one launch of a
-    # stage covers B * steps / launches frames
-    frames_per_launch = B * prof_calls / max(dom_launches, 1)
-    dom_bytes = alg.get(dom, 0) * frames_per_launch
-    achieved = dom_bytes / dom_avg_s / 1e9 if dom_avg_s > 0 else 0.0
-    stage_avg_ms = {k: v[0] / max(prof_calls, 1) for k, v in stages.items()}  # per batch, summed over ranges
-    traffic = None
-    tf = ROOT / "profiles" / "traffic_latest.json"
-    if tf.exists():
-        try:
-            tj = json.loads(tf.read_text())
-            if tj.get("kernel") == dom and tj.get("batch") == B and tj.get("width") == W:
-                traffic = tj.get("bytes_per_launch")
-        except Exception:
-            traffic = None
-
-    result = {
-        "metric": "ORB extract+match frames/s and LocalBA iters/s per GPU; ATE vs reference",
-        "value": round(value, 2),
+    # the drop-in path as Tracking calls it: host image in, host keypoints / descriptors out
+    # (slamhot_extract_batch / slamhot_extract: H2D + extraction + D2H, synchronous)
+    hb = 32
+    ex.extract_batch(frames_np[:hb])
+    t0 = time.perf_counter()
+    reps = 5
+    for _ in range(reps):
+        ex.extract_batch(frames_np[:hb])
+    host_batch_fps = hb * reps / (time.perf_counter() - t0)
+    lat = []
+    for i in range(60):
+        t1 = time.perf_counter()
+        ex(frames_np[i % nuniq])
+        lat.append(time.perf_counter() - t1)
+    lat = np.array(lat[10:]) * 1e3
+    out = {
+        "metric": "ORBextractor frames/s",
+        "value": round(frames_all / el, 2),
         "unit": "frames/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u8",
-        "data": "synthetic (seeded procedural textures, slamhot/synth.py)",
-        "config": {
-            "workload": f"ORBextractor-only, synthetic {W}x{H} 8-level pyramid, {args.nfeatures} feat/frame "
-                        f"(BASELINE.json configs[1])",
-            "frames_per_gpu_per_step": B,
-            "nfeatures": args.nfeatures,
-            "levels": 8,
-            "scale_factor": 1.2,
-            "fast_thresholds": [20, 7],
-            "parallelism": f"frame-sharded x{world}",
-            "batches_in_flight": NS,
-            "keypoints_per_frame": round(kps_per_frame, 1),
-            "total_keypoints": total_kps,
-        },
-        "roofline": {
-            "bound": "hbm",
-            "kernel": dom,
-            "achieved": round(achieved, 2),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 5),
-            "traffic": traffic,
-            "algorithmic_bytes_per_launch": int(dom_bytes),
-            "frames_per_launch": frames_per_launch,
-            "measured": "HIP events, isolated pass after the timed region (1 batch in flight, stages serialized)",
-            "avg_launch_ms": round(dom_avg_s * 1000.0, 5),
-        },
-        "stages_ms_per_step": {k: round(v, 5) for k, v in stage_avg_ms.items()},
-        "pipeline_roofline": {
-            "bytes_per_frame": int(pipe_bytes),
-            "achieved_GBps": round(pipe_bytes * B / (ms_per_step / 1000.0) / 1e9, 2),
+        "config": {"workload": f"ORBextractor-only, synthetic {W}x{H} 8-level pyramid, {args.nfeatures} feat/frame "
+                               f"(BASELINE.json configs[1])",
+                   "frames_per_gpu_per_step": B, "nfeatures": args.nfeatures, "levels": 8, "scale_factor": 1.2,
+                   "fast_thresholds": [20, 7], "parallelism": f"frame-sharded x{ctx['world']}",
+                   "batches_in_flight": NS, "keypoints_per_frame": round(kps_per_frame, 1)},
+        "roofline": roofline_from_stages(stages, args.steps, B, W, H, kps_per_frame),
+        "stages_ms_per_step": {k: round(v[0] / max(args.steps, 1), 5) for k, v in stages.items()},
+        "pipeline_roofline": {"bytes_per_frame": int(pipe_bytes),
+                              "achieved_GBps": round(pipe_bytes * B / (ms_per_step / 1000.0) / 1e9, 2)},
+        "host_path": {
+            "batch_frames_per_s": round(host_batch_fps, 1),
+            "batch": hb,
+            "single_frame_latency_ms": {"median": round(float(np.median(lat)), 3),
+                                        "p90": round(float(np.percentile(lat, 90)), 3)},
+            "note": "slamhot_extract_batch / slamhot_extract with host buffers (H2D image + extraction + D2H "
+                    "keypoints and descriptors, synchronous) — the call Frame.cc:119-122 makes",
         },
     }
-
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args, W, H)
-
-    if args.match_pairs > 0:
-        result["match"] = match_leg(args, rank, world, local_rank, dist, device)
-    if args.lba_windows > 0:
-        result["lba"] = lba_leg(args, rank, world, local_rank, dist, device)
-    if args.pose_frames > 0:
-        result["pose"] = pose_leg(args, rank, world, local_rank, dist, device)
-    if args.stereo_pairs > 0:
-        result["stereo"] = stereo_leg(args, rank, world, local_rank, dist, device)
-
-    if rank == 0:
-        print(json.dumps(result), flush=True)
+    if ctx["cpu"]:
+        out["cpu_baseline"] = extract_cpu(args, W, H)
     for e in exs:
         e.close()
-    if dist:
-        dist.destroy_process_group()
-
-
-def match_leg(args, rank, world, local_rank, dist, device):
-    """Extract + ComputeBoW + SearchByBoW(KF, Frame) frames/s (BASELINE.json configs[2] shape on
-    synthetic data: no EuRoC images here).  A step extracts 2P frames (P keyframes and P frames
-    that are shifted / rotated copies of them), builds every FeatureVector on the device and
-    matches the P pairs; everything stays in HBM."""
-    import torch
-
-    import slamhot
-    from slamhot import dist as sdist
-    from slamhot import synth
-    Pn, W, H = args.match_pairs, args.width, args.height
-    nuniq = min(16, Pn)
-    seeds = sdist.shard(nuniq * world, rank, world)
-    kfs = [synth.frame(20000 + s, W, H) for s in seeds]
-    rng = np.random.default_rng(rank)
-    pairs_img = []
-    for i in range(nuniq):
-        dx, dy, a = rng.uniform(-8, 8), rng.uniform(-6, 6), rng.uniform(-10, 10)
-        pairs_img.append((kfs[i], synth.shifted(kfs[i], dx, dy, a, 40000 + seeds[i])))
-    imgs = np.stack([im for i in range(Pn) for im in pairs_img[i % nuniq]])
-    F = len(imgs)
-    # the vocabulary is built (or, with ORBvoc.txt, loaded) once and replicated from rank 0
-    par, leaf, dn, wn = sdist.broadcast_arrays(dist, device, synth.vocab(10, 6, 0) if rank == 0 else None)
-    voc = slamhot.Vocabulary(par, leaf, dn, wn, k=10, L=6, device=local_rank)
-    m = slamhot.ORBmatcher(0.7, True, device=local_rank)
-    ex = slamhot.ORBextractor(nfeatures=args.nfeatures, device=local_rank, max_size=(W, H), max_batch=F)
-    cap = ex.cap
-    d_img = torch.from_numpy(imgs).to(device)
-    d_kps = torch.zeros((F, cap, 28), dtype=torch.uint8, device=device)
-    d_desc = torch.zeros((F, cap, 32), dtype=torch.uint8, device=device)
-    d_n = torch.zeros(F, dtype=torch.int32, device=device)
-    d_mono = torch.zeros(F, dtype=torch.int32, device=device)
-    pairs = [(2 * i, 2 * i + 1) for i in range(Pn)]
-    d_a2b = torch.zeros((Pn, cap), dtype=torch.int32, device=device)
-    d_b2a = torch.zeros((Pn, cap), dtype=torch.int32, device=device)
-    d_nm = torch.zeros(Pn, dtype=torch.int32, device=device)
-    # one real stream orders extraction before matching (NULL would mean each handle's own stream)
-    stream_obj = torch.cuda.Stream(device)
-    stream = stream_obj.cuda_stream
-
-    def step():
-        ex.extract_batch_device(d_img.data_ptr(), F, W, H, d_kps.data_ptr(), d_desc.data_ptr(), cap,
-                                d_n.data_ptr(), d_mono.data_ptr(), stream=stream)
-        m.bow_match_batch_device(voc, F, d_kps.data_ptr(), d_desc.data_ptr(), cap, d_n.data_ptr(), pairs,
-                                 d_a2b.data_ptr(), d_b2a.data_ptr(), d_nm.data_ptr(), stream=stream)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(device)
-    if dist:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(device)
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    skipped = m.bow_match_batch_status(stream)
-    nm = d_nm.cpu().numpy()
-    elapsed, frames_all = sdist.reduce_run(dist, device, elapsed, float(F * args.steps))
-    out = {
-        "metric": "ORB extract + ComputeBoW + SearchByBoW frames/s",
-        "value": round(frames_all / elapsed, 2),
-        "unit": "frames/s",
-        "dtype": "u8",
-        "config": {"workload": f"synthetic {W}x{H}, {args.nfeatures} feat/frame, {Pn} (keyframe, frame) pairs "
-                               f"per GPU per step, synthetic k=10 L=6 vocabulary, levelsup 4, nnratio 0.7, "
-                               f"checkOri (BASELINE.json configs[2] shape)",
-                   "parallelism": f"pair-sharded x{world}"},
-        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-        "matches_per_pair": round(float(nm.mean()), 1),
-        "skipped_pairs": skipped,
-    }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        sys.path.insert(0, str(ROOT / "tests"))
-        import oracle_bind as ob
-        p = ob.params(nfeatures=args.nfeatures)
-        t0 = time.perf_counter()
-        done = 0
-        while done < min(8, nuniq) and time.perf_counter() - t0 < 10.0:
-            sides = []
-            for im in pairs_img[done]:
-                k, d, _ = ob.extract(im, p)
-                _, wt, nid = ob.vocab_transform(par, leaf, dn, wn, 6, d, 4)
-                sides.append((d, k["angle"], None) + synth.feature_vector(nid, wt))
-            ob.search_by_bow(sides[0], sides[1], 0.7, True, False)
-            done += 1
-        dt = time.perf_counter() - t0
-        out["cpu_baseline"] = {"value": round(2 * done / dt, 2), "unit": "frames/s", "cores": 1, "kind": "port",
-                               "sample": f"{done} pairs ({2 * done} frames) one at a time on one core: oracle "
-                                         f"extract + vocabulary transform + FeatureVector + SearchByBoW"}
-    ex.close()
-    m.close()
-    voc.close()
     return out
 
 
-def pose_leg(args, rank, world, local_rank, dist, device):
+def extract_cpu(args, W, H):
+    """The oracle (restated reference CPU path, oracle/orb_oracle.cpp) on the host cores:
+    one frame per std::thread at a time, as Frame.cc:119-122 runs extraction."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_bind as ob
+    from slamhot import synth
+    cores = host_cores()
+    nuniq = 32
+    imgs = synth.frames(range(5000, 5000 + nuniq), W, H)
+    imgs = np.concatenate([imgs] * ((args.cpu_frames + nuniq - 1) // nuniq))[: args.cpu_frames]
+    p = ob.params(nfeatures=args.nfeatures)
+    ob.extract_many(imgs[:cores], p, nthreads=cores)  # warm-up
+    t0 = time.perf_counter()
+    ob.extract_many(imgs, p, nthreads=cores)
+    dt = time.perf_counter() - t0
+    t1 = time.perf_counter()
+    single = 16
+    ob.extract_many(imgs[:single], p, nthreads=1)
+    dt1 = time.perf_counter() - t1
+    return {"value": round(len(imgs) / dt, 2), "unit": "frames/s", "cores": cores, "kind": "port", "cpu": cpu_model(),
+            "sample": f"{len(imgs)} synthetic {W}x{H} frames, {args.nfeatures} feat, {cores} threads "
+                      f"(one frame per thread); oracle/orb_oracle.cpp -O3",
+            "per_core_frames_per_s": round(single / dt1, 2)}
+
+
+# ------------------------------------------------------------------------------------------
+# pose: Optimizer::PoseOptimization
+# ------------------------------------------------------------------------------------------
+def pose_leg(ctx):
     """Optimizer::PoseOptimization frames/s: batches of synthetic frames (1000 keypoints, 80%
     with MapPoints, 10% outliers, EuRoC intrinsics), one workgroup per frame."""
     import torch
@@ -357,209 +562,79 @@ def pose_leg(args, rank, world, local_rank, dist, device):
     import slamhot
     from slamhot import dist as sdist
     from slamhot import synth
+    args, device, dist = ctx["args"], ctx["device"], ctx["dist"]
     nf = args.pose_frames
-    pool = [synth.pose_frame(s) for s in sdist.shard(16 * world, rank, world)]
+    pool = [synth.pose_frame(s) for s in sdist.shard(16 * ctx["world"], ctx["rank"], ctx["world"])]
     frames = [pool[i % len(pool)] for i in range(nf)]
-    S = slamhot.PoseOptimizer(device=local_rank)
+    S = slamhot.PoseOptimizer(device=ctx["local_rank"])
     S.solve(frames[:8])
-    if dist:
-        dist.barrier()
     calls = 3
-    t0 = time.perf_counter()
-    for _ in range(calls):
-        res = S.solve(frames)
-    torch.cuda.synchronize(device)
-    if dist:
-        dist.barrier()
-    elapsed, total = sdist.reduce_run(dist, device, time.perf_counter() - t0, float(nf * calls))
+    res = []
+    elapsed = timed_region(dist, device, lambda i: res.append(S.solve(frames)), calls)
+    el, total = sdist.reduce_run(dist, device, elapsed, float(nf * calls))
     out = {
         "metric": "Optimizer::PoseOptimization frames/s",
-        "value": round(total / elapsed, 1),
+        "value": round(total / el, 1),
         "unit": "frames/s",
         "dtype": "f64",
         "config": {"workload": "synthetic frames, 1000 keypoints, ~800 MapPoint observations, 10% outliers, "
                                "4 x optimize(10)", "frames_per_gpu_per_call": nf,
-                   "parallelism": f"frame-sharded x{world}"},
-        "ms_per_call": round(elapsed / calls * 1e3, 3),
-        "mean_inliers": round(float(np.mean([r["n_inliers"] for r in res])), 1),
+                   "parallelism": f"frame-sharded x{ctx['world']}"},
+        "ms_per_call": round(el / calls * 1e3, 3),
+        "mean_inliers": round(float(np.mean([r["n_inliers"] for r in res[-1]])), 1),
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if ctx["cpu"]:
         sys.path.insert(0, str(ROOT / "tests"))
         import oracle_bind as ob
+        cores = host_cores()
+        work = [pool[i % len(pool)] for i in range(64 * cores)]
         t0 = time.perf_counter()
-        k = 0
-        while k < len(pool) and time.perf_counter() - t0 < 3.0:
-            ob.pose_optimization(pool[k])
-            k += 1
-        out["cpu_baseline"] = {"value": round(k / (time.perf_counter() - t0), 2), "unit": "frames/s", "cores": 1,
-                               "kind": "port", "sample": f"{k} frames one at a time on one core; "
-                                                         f"oracle/pose_oracle.cpp -O3"}
+        with ThreadPoolExecutor(cores) as ex:
+            list(ex.map(ob.pose_optimization, work))
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(len(work) / dt, 2), "unit": "frames/s", "cores": cores, "kind": "port",
+                               "cpu": cpu_model(),
+                               "sample": f"{len(work)} frames on {cores} threads (one frame per task); "
+                                         f"oracle/pose_oracle.cpp -O3"}
     S.close()
     return out
 
 
-def stereo_leg(args, rank, world, local_rank, dist, device):
-    """Stereo Frame construction frames/s (EuRoC stereo shape, BASELINE.json configs[3]:
-    752x480, 1200 features): a step rectifies P raw left and P raw right images with the
-    EuRoC calibration (cv::remap, stereo_euroc.cc:168-169), extracts both and runs
-    ComputeStereoMatches on the P pairs, all device-resident.  rectify_ms / stereo_ms isolate
-    the remap and matching kernels (torch events on the launch stream)."""
-    import torch
-
-    import slamhot
-    from slamhot import dist as sdist
-    from slamhot import synth
-    P, W, H, NF = args.stereo_pairs, 752, 480, 1200
-    from slamhot import euroc
-    calib = {k: np.array(v) if isinstance(v, list) else v
-             for k, v in json.loads((ROOT / "tests" / "golden" / "euroc_stereo_calib.json").read_text()).items()}
-    maps = [euroc.init_undistort_rectify_map(calib[f"{sd}.K"], calib[f"{sd}.D"], calib[f"{sd}.R"], calib[f"{sd}.P"],
-                                             (W, H)) for sd in ("LEFT", "RIGHT")]
-    # raw camera images: synthetic rectified pairs pushed back through the calibration
-    seeds = sdist.shard(8 * world, rank, world)
-    prs = []
-    for s_ in seeds:
-        lr = synth.stereo_pair(int(s_) + 500, W, H)
-        prs.append(tuple(synth.unrectify(im, *mp) for im, mp in zip(lr, maps)))
-    il = np.stack([prs[i % len(prs)][0] for i in range(P)])
-    ir = np.stack([prs[i % len(prs)][1] for i in range(P)])
-    mbf = synth.EUROC_STEREO["bf"]
-    mb = mbf / synth.EUROC_STEREO["fx"]
-    left = slamhot.ORBextractor(nfeatures=NF, device=local_rank, max_size=(W, H), max_batch=P)
-    right = slamhot.ORBextractor(nfeatures=NF, device=local_rank, max_size=(W, H), max_batch=P)
-    sm = slamhot.StereoMatcher(device=local_rank)
-    rect = [euroc.Rectifier(*mp, device=local_rank) for mp in maps]
-    cap = left.cap
-    d_raw_l, d_raw_r = torch.from_numpy(il).to(device), torch.from_numpy(ir).to(device)
-    d_il, d_ir = torch.empty_like(d_raw_l), torch.empty_like(d_raw_r)
-    bufs = [(torch.zeros((P, cap, 28), dtype=torch.uint8, device=device),
-             torch.zeros((P, cap, 32), dtype=torch.uint8, device=device),
-             torch.zeros(P, dtype=torch.int32, device=device), torch.zeros(P, dtype=torch.int32, device=device))
-            for _ in range(2)]
-    d_ur = torch.empty((P, cap), dtype=torch.float32, device=device)
-    d_dep = torch.empty((P, cap), dtype=torch.float32, device=device)
-    stream = torch.cuda.Stream(device)  # a real stream: NULL would mean each handle's own stream
-    ev = []
-    ev_rect = []
-
-    def step(timed=False):
-        if timed:
-            r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            r0.record(stream)
-        for rc, raw, out in ((rect[0], d_raw_l, d_il), (rect[1], d_raw_r, d_ir)):
-            rc.rectify_batch_device(P, raw.data_ptr(), W, W * H, out.data_ptr(), W, W * H, stream=stream.cuda_stream)
-        if timed:
-            r1.record(stream)
-            ev_rect.append((r0, r1))
-        for ex, img, (k, d, n, m) in ((left, d_il, bufs[0]), (right, d_ir, bufs[1])):
-            ex.extract_batch_device(img.data_ptr(), P, W, H, k.data_ptr(), d.data_ptr(), cap, n.data_ptr(),
-                                    m.data_ptr(), stream=stream.cuda_stream)
-        (kl, dl, nl, _), (kr, dr, nr, _) = bufs
-        if timed:
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record(stream)
-        sm.match_batch_device(left, right, P, kl.data_ptr(), dl.data_ptr(), nl.data_ptr(), kr.data_ptr(),
-                              dr.data_ptr(), nr.data_ptr(), cap, mbf, mb, d_ur.data_ptr(), d_dep.data_ptr(),
-                              stream=stream.cuda_stream)
-        if timed:
-            b.record(stream)
-            ev.append((a, b))
-
-    for _ in range(max(args.warmup, 1)):
-        step()
-    torch.cuda.synchronize(device)
-    if dist:
-        dist.barrier()
-    steps = max(args.steps // 2, 3)
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        step(timed=True)
-    torch.cuda.synchronize(device)
-    if dist:
-        dist.barrier()
-    elapsed, total = sdist.reduce_run(dist, device, time.perf_counter() - t0, float(P * steps))
-    stereo_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    rect_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_rect]))
-    nl_h = bufs[0][2].cpu().numpy()
-    ur = d_ur.cpu().numpy()
-    matched = float(np.mean([(ur[f, : nl_h[f]] >= 0).sum() for f in range(P)]))
-    out = {
-        "metric": "stereo Frame (2x remap + 2x ORB extract + ComputeStereoMatches) frames/s",
-        "value": round(total / elapsed, 1),
-        "unit": "frames/s",
-        "dtype": "u8",
-        "config": {"workload": f"synthetic raw stereo pairs {W}x{H} (EuRoC calibration), {NF} features, EuRoC bf",
-                   "pairs_per_gpu_per_step": P, "parallelism": f"frame-sharded x{world}"},
-        "ms_per_step": round(elapsed / steps * 1e3, 3),
-        "stereo_match_ms_per_step": round(stereo_ms, 4),
-        "rectify_ms_per_step": round(rect_ms, 4),
-        "rectify_GBps": round(2 * P * W * H * 2 / (rect_ms / 1e3) / 1e9, 1),
-        "stereo_match_frames_per_s": round(P / (stereo_ms / 1e3), 1),
-        "mean_stereo_matches": round(matched, 1),
-    }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        sys.path.insert(0, str(ROOT / "tests"))
-        import oracle_bind as ob
-        p = ob.params(nfeatures=NF)
-        sc, isc, _, _, _ = ob.levels(p)
-        t_ex = t_st = 0.0
-        k = 0
-        while k < len(prs) and t_ex + t_st < 10.0:
-            t1 = time.perf_counter()
-            l_img = ob.remap_linear(prs[k][0], rect[0].map_x, rect[0].map_y)
-            r_img = ob.remap_linear(prs[k][1], rect[1].map_x, rect[1].map_y)
-            kl, dl, _ = ob.extract(l_img, p)
-            kr, dr, _ = ob.extract(r_img, p)
-            t_ex += time.perf_counter() - t1
-            pl, pr = ob.pyramid(l_img, p), ob.pyramid(r_img, p)  # built inside extract too; untimed
-            t2 = time.perf_counter()
-            ob.stereo_matches(kl, dl, kr, dr, pl, pr, sc, isc, mbf, mb)
-            t_st += time.perf_counter() - t2
-            k += 1
-        out["cpu_baseline"] = {"value": round(k / (t_ex + t_st), 2), "unit": "frames/s", "cores": 1, "kind": "port",
-                               "sample": f"{k} stereo frames on one core (oracle remap x2 + extract x2 + "
-                                         f"oracle/stereo_oracle.cpp, -O3)",
-                               "stereo_match_only_frames_per_s": round(k / t_st, 1)}
-    for rc in rect:
-        rc.close()
-    left.close()
-    right.close()
-    sm.close()
-    return out
-
-
-def sdist_shard_seeds(rank, world, n):
-    from slamhot import dist as sdist
-    return sdist.shard(n * world, rank, world)
-
-
-def lba_leg(args, rank, world, local_rank, dist, device):
+# ------------------------------------------------------------------------------------------
+# lba: configs[3] Optimizer::LocalBundleAdjustment
+# ------------------------------------------------------------------------------------------
+def lba_leg(ctx):
     """LM iterations/s of the device LBA solver on config-4 windows (BASELINE.json configs[3])."""
+    import threading
+
     import torch
 
     import slamhot
+    from slamhot import dist as sdist
     from slamhot import synth
+    args, device, dist, lr = ctx["args"], ctx["device"], ctx["dist"], ctx["local_rank"]
     nwin = args.lba_windows
     # windows are sharded by rank: rank r solves its own seeds (independent units)
-    pool = [synth.lba_window(s) for s in sdist_shard_seeds(rank, world, 8)]
+    pool = [synth.lba_window(s) for s in sdist.shard(8 * ctx["world"], ctx["rank"], ctx["world"])]
     windows = [pool[i % len(pool)] for i in range(nwin)]
-    S = slamhot.LocalBundleAdjustment(device=local_rank)
+    S = slamhot.LocalBundleAdjustment(device=lr)
     S.solve(windows[: min(4, nwin)])  # warm-up
     single = S.solve(pool[0])
     dev1, plan1, _ = S.last_stats()
-    # accuracy: ATE of the solved KeyFrame centres against the windows' ground truth
     ate_dev = [window_ate(w, r["kf_Tcw"]) for w, r in zip(pool, S.solve(pool))]
     ate_init = [window_ate(w, w["kf_Tcw"]) for w in pool]
     it1 = single["iterations"][0] + single["iterations"][1]
     # `lba_inflight` solver handles driven from host threads (the C call releases the GIL), each
     # on its own window set: one call's host planning overlaps another's device LM loop.  The
     # windows are flattened to C structs before the timed region, as a C++ caller holds them.
-    import threading
     NL = max(1, args.lba_inflight)
-    solvers = [S] + [slamhot.LocalBundleAdjustment(device=local_rank) for _ in range(NL - 1)]
+    solvers = [S] + [slamhot.LocalBundleAdjustment(device=lr) for _ in range(NL - 1)]
     runs = [sv.prepare(windows) for sv in solvers]
     for r_ in runs:
         r_()
+    res0 = runs[0].results()
+    trials_per_call = sum(r["trials"] for r in res0)
+    iters_per_call = sum(r["iterations"][0] + r["iterations"][1] for r in res0)
     stats = [[0, 0.0, 0.0] for _ in range(NL)]
 
     def worker(t):
@@ -569,38 +644,41 @@ def lba_leg(args, rank, world, local_rank, dist, device):
             stats[t][1] += d
             stats[t][2] += pl
 
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(device)
-    t0 = time.perf_counter()
-    ths = [threading.Thread(target=worker, args=(t,)) for t in range(1, NL)]
-    for th in ths:
-        th.start()
-    worker(0)
-    for th in ths:
-        th.join()
-    torch.cuda.synchronize(device)
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    def run_all(_):
+        ths = [threading.Thread(target=worker, args=(t,)) for t in range(1, NL)]
+        for th in ths:
+            th.start()
+        worker(0)
+        for th in ths:
+            th.join()
+
+    elapsed = timed_region(dist, device, run_all, 1)
     iters = sum(x[0] for x in stats)
     dev_ms = sum(x[1] for x in stats) / NL
     plan_ms = sum(x[2] for x in stats) / NL
-    from slamhot import dist as sdist
     dev_max, _ = sdist.reduce_run(dist, device, dev_ms, 0.0)
-    elapsed, iters_all = sdist.reduce_run(dist, device, elapsed, float(iters))
+    el, iters_all = sdist.reduce_run(dist, device, elapsed, float(iters))
+    rate = iters_all / el
+    extra = max(trials_per_call - iters_per_call, 0) / max(iters_per_call, 1)
+    flop_per_iter = LBA_FLOP_PER_ITER + extra * LBA_FLOP_PER_EXTRA_TRIAL
+    tf = rate * flop_per_iter / 1e12
     out = {
         "metric": "LocalBundleAdjustment LM iterations/s",
-        "value": round(iters_all / elapsed, 1),
+        "value": round(rate, 1),
         "unit": "LM iterations/s",
         "dtype": "f64",
         "config": {"workload": "synthetic LocalBA 50 KF x 2000 pts x 8 obs, 2% outliers, 48 free KFs, "
                                "schedule 5 + 10 (BASELINE.json configs[3])",
                    "windows_per_gpu_per_call": nwin, "calls": args.lba_calls,
-                   "parallelism": f"window-sharded x{world}"},
-        "lba_calls_per_s": round(nwin * args.lba_calls * NL * world / elapsed, 2),
+                   "parallelism": f"window-sharded x{ctx['world']}"},
+        "roofline": {"bound": "fp64", "achieved": round(tf, 4), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(tf / FP64_PEAK_TFLOPS, 5),
+                     "flop_per_lm_iteration": round(flop_per_iter), "trials_per_iteration": round(1 + extra, 3),
+                     "note": "algorithmic FLOP (SURVEY.md §8d: 31.85 MFLOP per iteration + 27.05 per extra trial) x "
+                             "whole-job LM iterations/s; MFMA-busy cycles per kernel in profiles/"},
+        "lba_calls_per_s": round(nwin * args.lba_calls * NL * ctx["world"] / el, 2),
         "solves_in_flight": NL,
-        "ms_per_call": round(elapsed / args.lba_calls * 1e3, 3),  # NL calls run concurrently
+        "ms_per_call": round(el / args.lba_calls * 1e3, 3),  # NL calls run concurrently
         "device_lm_iters_per_s_one_solver": round(iters_all / NL / (dev_max / 1e3), 1) if dev_max > 0 else None,
         "host_plan_ms_per_call": round(plan_ms / args.lba_calls, 3),
         "single_window": {"lm_iterations": it1, "device_ms": round(dev1, 3),
@@ -610,9 +688,11 @@ def lba_leg(args, rank, world, local_rank, dist, device):
                 "unit": "m", "windows": len(pool),
                 "initial": round(float(np.mean(ate_init)), 7), "device": round(float(np.mean(ate_dev)), 7)},
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if ctx["cpu"]:
         sys.path.insert(0, str(ROOT / "tests"))
         import oracle_bind as ob
+        cores = host_cores()
+        # single core: the drop-in comparison (LocalMapping solves one window at a time)
         reps, cpu_iters, ate_cpu = 0, 0, []
         t0 = time.perf_counter()
         while time.perf_counter() - t0 < 3.0 and reps < len(pool):
@@ -620,14 +700,22 @@ def lba_leg(args, rank, world, local_rank, dist, device):
             cpu_iters += r["iterations"][0] + r["iterations"][1]
             ate_cpu.append(window_ate(pool[reps], r["kf_Tcw"]))
             reps += 1
-        dt = time.perf_counter() - t0
-        # matched accuracy: the oracle (restated reference solver) on the same windows
+        dt1 = time.perf_counter() - t0
+        # every host core: independent windows, one per thread
+        work = [pool[i % len(pool)] for i in range(2 * cores)]
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(cores) as ex:
+            its = list(ex.map(lambda w: sum(ob.lba_solve(w)["iterations"]), work))
+        dtn = time.perf_counter() - t0
         out["ate"]["oracle_same_windows"] = round(float(np.mean(ate_cpu)), 7)
         out["ate"]["device_same_windows"] = round(float(np.mean(ate_dev[:reps])), 7)
         out["cpu_baseline"] = {
-            "value": round(cpu_iters / dt, 2), "unit": "LM iterations/s", "cores": 1, "kind": "port",
-            "sample": f"{reps} config-4 windows, one at a time on one core; oracle/lba_oracle.cpp "
-                      f"(g2o LM/Schur restatement, dense LDL^T) -O3 -march=x86-64-v3",
+            "value": round(sum(its) / dtn, 2), "unit": "LM iterations/s", "cores": cores, "kind": "port",
+            "cpu": cpu_model(),
+            "sample": f"{len(work)} config-4 windows on {cores} threads (one window per task); oracle/lba_oracle.cpp "
+                      f"(g2o LM/Schur restatement, dense LDL^T) -O3",
+            "one_core": {"value": round(cpu_iters / dt1, 2), "windows": reps,
+                         "ms_per_lm_iteration": round(dt1 * 1e3 / max(cpu_iters, 1), 3)},
         }
     for sv in solvers:
         sv.close()
@@ -646,38 +734,20 @@ def window_ate(w, kf_Tcw):
     return float(np.sqrt(np.mean(err * err)))
 
 
-def cpu_baseline(args, W, H):
-    """The oracle (restated reference CPU path, oracle/orb_oracle.cpp) on the host cores:
-    one frame per std::thread at a time, as Frame.cc:119-122 runs extraction."""
-    sys.path.insert(0, str(ROOT / "tests"))
-    import oracle_bind as ob
-    from slamhot import synth
+# ------------------------------------------------------------------------------------------
+# track: configs[4] — the per-sequence stereo tracking chain
+# ------------------------------------------------------------------------------------------
+def track_leg(ctx):
     try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, 16))
-    nuniq = 32
-    imgs = synth.frames(range(5000, 5000 + nuniq), W, H)
-    imgs = np.concatenate([imgs] * ((args.cpu_frames + nuniq - 1) // nuniq))[: args.cpu_frames]
-    p = ob.params(nfeatures=args.nfeatures)
-    ob.extract_many(imgs[:cores], p, nthreads=cores)  # warm-up
-    t0 = time.perf_counter()
-    ob.extract_many(imgs, p, nthreads=cores)
-    dt = time.perf_counter() - t0
-    t1 = time.perf_counter()
-    single = 16
-    ob.extract_many(imgs[:single], p, nthreads=1)
-    dt1 = time.perf_counter() - t1
-    return {
-        "value": round(len(imgs) / dt, 2),
-        "unit": "frames/s",
-        "cores": cores,
-        "kind": "port",
-        "sample": f"{len(imgs)} synthetic {W}x{H} frames, {args.nfeatures} feat, {cores} threads "
-                  f"(one frame per thread); oracle/orb_oracle.cpp -O3 -march=x86-64-v3",
-        "per_core_frames_per_s": round(single / dt1, 2),
-    }
+        from slamhot import tracker  # noqa: F401
+    except ImportError:
+        return {"skipped": "tracker not built"}
+    return tracker_bench(ctx)
+
+
+def tracker_bench(ctx):
+    from slamhot import tracker
+    return tracker.bench(ctx, ROOT)
 
 
 if __name__ == "__main__":

@@ -355,3 +355,102 @@ def unrectify(rect: np.ndarray, map_x: np.ndarray, map_y: np.ndarray) -> np.ndar
         out = np.where(holes & np.isfinite(fill), fill, out)
     out = np.nan_to_num(out, nan=128.0)
     return np.ascontiguousarray(np.clip(np.rint(out), 0, 255).astype(np.uint8))
+
+
+# --------------------------------------------------------------------------------------------
+# Rendered sequences: a textured box room seen by a moving (stereo) pinhole camera, so frame
+# poses, stereo disparities and feature tracks are geometrically consistent (tracking chain,
+# config-3 / config-5 legs).  Camera convention as the reference: Tcw maps world -> camera,
+# x right, y down, z forward; the right camera sits at +b along the left camera's x axis.
+# --------------------------------------------------------------------------------------------
+ROOM = (-4.0, 4.0, -1.8, 1.8, -3.0, 6.0)  # x0, x1, y0, y1, z0, z1 (m)
+_TEX_PER_M = 110.0
+
+
+def _wall_textures(seed: int):
+    """Six wall textures (T x T float) from the procedural frame generator."""
+    return [frame(seed * 16 + k, 1024, 1024).astype(np.float64) for k in range(6)]
+
+
+def _sample(tex, a, b):
+    """Bilinear texture lookup at texel coordinates (a, b), wrapped."""
+    T = tex.shape[0]
+    a0 = np.floor(a)
+    b0 = np.floor(b)
+    fa, fb = a - a0, b - b0
+    a0 = a0.astype(np.int64) % T
+    b0 = b0.astype(np.int64) % T
+    a1, b1 = (a0 + 1) % T, (b0 + 1) % T
+    return ((tex[b0, a0] * (1 - fa) + tex[b0, a1] * fa) * (1 - fb) +
+            (tex[b1, a0] * (1 - fa) + tex[b1, a1] * fa) * fb)
+
+
+def render_view(textures, Tcw, cam=EUROC_CAM, width=None, height=None, noise_seed=None):
+    """Ray-cast the textured room from camera pose Tcw (4x4 world -> camera); returns
+    (image u8, depth float64 z along the optical axis)."""
+    W = width or cam["w"]
+    H = height or cam["h"]
+    R, t = Tcw[:3, :3], Tcw[:3, 3]
+    C = -R.T @ t
+    yy, xx = np.mgrid[0:H, 0:W].astype(np.float64)
+    dc = np.stack([(xx - cam["cx"]) / cam["fx"], (yy - cam["cy"]) / cam["fy"], np.ones_like(xx)], -1)
+    dw = dc @ R  # R^T d per pixel (row vectors)
+    best = np.full((H, W), np.inf)
+    img = np.zeros((H, W))
+    x0, x1, y0, y1, z0, z1 = ROOM
+    planes = [(0, x0, (2, 1)), (0, x1, (2, 1)), (1, y0, (0, 2)), (1, y1, (0, 2)), (2, z0, (0, 1)), (2, z1, (0, 1))]
+    for k, (ax, val, (ua, va)) in enumerate(planes):
+        with np.errstate(divide="ignore", invalid="ignore"):
+            s = (val - C[ax]) / dw[..., ax]
+        ok = (s > 1e-6) & (s < best)
+        if not ok.any():
+            continue
+        P = C[None, None, :] + s[..., None] * dw
+        a = P[..., ua] * _TEX_PER_M
+        b = P[..., va] * _TEX_PER_M
+        v = _sample(textures[k], a, b)
+        img = np.where(ok, v, img)
+        best = np.where(ok, s, best)
+    depth = best  # dc has z = 1, so the ray parameter is the camera-frame depth
+    if noise_seed is not None:
+        img = img + np.random.default_rng(noise_seed).normal(0.0, 1.5, size=img.shape)
+    return np.ascontiguousarray(np.clip(np.rint(img), 0, 255).astype(np.uint8)), depth
+
+
+def sequence_poses(seed: int, n: int, step_m: float = 0.03, yaw_deg: float = 0.6):
+    """Ground-truth Tcw of a smooth walk through the room (looking roughly along +z)."""
+    rng = np.random.default_rng(seed)
+    c = np.array([rng.uniform(-1.0, 1.0), rng.uniform(-0.3, 0.3), rng.uniform(-1.5, 0.0)])
+    yaw, pitch = rng.uniform(-0.3, 0.3), rng.uniform(-0.1, 0.1)
+    dyaw = np.deg2rad(yaw_deg) * rng.choice([-1.0, 1.0])
+    out = []
+    for i in range(n):
+        cy_, sy_ = np.cos(yaw), np.sin(yaw)
+        cp, sp = np.cos(pitch), np.sin(pitch)
+        Ry = np.array([[cy_, 0, sy_], [0, 1, 0], [-sy_, 0, cy_]])
+        Rx = np.array([[1, 0, 0], [0, cp, -sp], [0, sp, cp]])
+        Rwc = Ry @ Rx
+        T = np.eye(4)
+        T[:3, :3] = Rwc.T
+        T[:3, 3] = -Rwc.T @ c
+        out.append(T)
+        fwd = Rwc[:, 2]
+        c = c + step_m * (0.7 * fwd + 0.3 * np.array([np.cos(0.1 * i), 0.2 * np.sin(0.07 * i), 0.0]))
+        yaw += dyaw * (1.0 + 0.5 * np.sin(0.05 * i))
+        pitch = 0.1 * np.sin(0.03 * i + seed)
+    return out
+
+
+def stereo_sequence(seed: int, n: int, cam=EUROC_CAM, step_m: float = 0.03):
+    """n rectified stereo frames of the room: (lefts (n,H,W) u8, rights, gt Tcw list).
+    The right camera is the left one shifted by b = bf / fx along its x axis."""
+    tex = _wall_textures(seed)
+    b = cam["bf"] / cam["fx"]
+    Ls, Rs, Ts = [], [], []
+    for i, T in enumerate(sequence_poses(seed, n, step_m)):
+        Tr = T.copy()
+        Tr[0, 3] -= b  # X_right = X_left - (b, 0, 0)
+        Ls.append(render_view(tex, T, cam, noise_seed=seed * 1000 + 2 * i)[0])
+        Rs.append(render_view(tex, Tr, cam, noise_seed=seed * 1000 + 2 * i + 1)[0])
+        Ts.append(T)
+    return np.stack(Ls), np.stack(Rs), Ts

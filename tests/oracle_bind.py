@@ -197,12 +197,26 @@ def vocab_children(parent):
     return ptr, order.astype(np.int32)
 
 
+_vocab_tables = {}
+
+
+def _vocab_prepared(parent, is_leaf):
+    """Children CSR, leaf flags and word ids of a node table (built once per table)."""
+    key = (id(parent), id(is_leaf), len(parent))
+    t = _vocab_tables.get(key)
+    if t is None or t[0] is not parent:
+        ptr, idx = vocab_children(parent)
+        leaf = np.ascontiguousarray(is_leaf, np.uint8).copy()
+        leaf[ptr[1:] == ptr[:-1]] = 1
+        word = np.full(len(parent), -1, np.int32)
+        word[np.nonzero(is_leaf)[0]] = np.arange(int(np.count_nonzero(is_leaf)), dtype=np.int32)
+        t = (parent, ptr, idx, leaf, word)
+        _vocab_tables[key] = t
+    return t[1:]
+
+
 def vocab_transform(parent, is_leaf, desc_nodes, weight_nodes, L, desc, levelsup=4):
-    ptr, idx = vocab_children(parent)
-    leaf = np.ascontiguousarray(is_leaf, np.uint8).copy()
-    leaf[ptr[1:] == ptr[:-1]] = 1
-    word = np.full(len(parent), -1, np.int32)
-    word[np.nonzero(is_leaf)[0]] = np.arange(int(np.count_nonzero(is_leaf)), dtype=np.int32)
+    ptr, idx, leaf, word = _vocab_prepared(parent, is_leaf)
     desc = np.ascontiguousarray(desc, np.uint8)
     n = len(desc)
     w = np.zeros(n, np.int32)

@@ -27,10 +27,18 @@ def main():
             d[c] = sum(per.values()) / max(len(per), 1)
         summary[k] = d
     (out / "summary.json").write_text(json.dumps(summary, indent=1, sort_keys=True))
+    # FETCH_SIZE -> bytes: the factor measured by tools/microbench/mb_fetch for the load width
+    # the kernel stages with (profiles/fetch_calibration.json; 2.0 = the guide's 16 B/lane value)
+    fac = {"k_fast_wave": "4"}
+    cal = {}
+    cf = Path("profiles/fetch_calibration.json")
+    if cf.exists():
+        cal = json.loads(cf.read_text()).get("factor_by_lane_bytes", {})
     traffic = {}
     for k, d in summary.items():
         if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
-            traffic[k] = (2 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024
+            f = float(cal.get(fac.get(k, "16"), 2.0))
+            traffic[k] = (f * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024
     for k, d in sorted(summary.items()):
         print(k, {c: round(v, 1) for c, v in sorted(d.items())})
     print("traffic bytes/launch:", {k: int(v) for k, v in traffic.items()})
@@ -38,10 +46,15 @@ def main():
     if len(sys.argv) > 2 and sys.argv[2] in traffic:
         # bench.py reads this for roofline.traffic: kernel, shape of the run, HBM bytes / launch
         k = sys.argv[2]
+        f = float(cal.get(fac.get(k, "16"), 2.0))
+        d = summary[k]
         meta = dict(kernel=k, batch=int(sys.argv[3]), width=int(sys.argv[4]), bytes_per_launch=int(traffic[k]),
-                    fetch_size_kib=summary[k]["FETCH_SIZE"], write_size_kib=summary[k]["WRITE_SIZE"],
-                    note="2 x FETCH_SIZE + WRITE_SIZE per MI355X_MICROARCH.md HBM section (the x2 is calibrated "
-                         "there for 16 B/lane streaming reads; this kernel stages with 4 B/lane loads)")
+                    fetch_size_kib=d["FETCH_SIZE"], write_size_kib=d["WRITE_SIZE"], fetch_factor=f,
+                    valu_instr_per_launch=d.get("SQ_INSTS_VALU"),
+                    lds_bank_conflict_per_lds_active=(d["SQ_LDS_BANK_CONFLICT"] / d["SQ_ACTIVE_INST_LDS"]
+                                                      if d.get("SQ_ACTIVE_INST_LDS") else None),
+                    note=f"{f:g} x FETCH_SIZE + WRITE_SIZE; the FETCH_SIZE factor is measured for this kernel's "
+                         f"{fac.get(k, '16')} B/lane loads by tools/microbench/mb_fetch (profiles/fetch_calibration.json)")
         Path("profiles/traffic_latest.json").write_text(json.dumps(meta, indent=1))
 
 
