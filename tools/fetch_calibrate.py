@@ -8,7 +8,6 @@ from collections import defaultdict
 from pathlib import Path
 
 BYTES = 1 << 30
-WIDTH = {"unsigned int": "4", "HIP_vector_type<unsigned int, 2u>": "8", "HIP_vector_type<unsigned int, 4u>": "16"}
 
 
 def main():
@@ -19,9 +18,7 @@ def main():
             name = r.get("Kernel_Name", "")
             if "k_read" not in name:
                 continue
-            w = next((v for k, v in WIDTH.items() if f"k_read<{k}>" in name), None)
-            if w is None:
-                w = "16" if "uint4" in name else "8" if "uint2" in name else "4"
+            w = "16" if "unsigned int, 4u" in name else "8" if "unsigned int, 2u" in name else "4"
             per[w][int(r.get("Dispatch_Id", 0))] += float(r["Counter_Value"])
     res = {}
     for w, disp in per.items():
