@@ -336,6 +336,14 @@ typedef struct slam_lba_problem {
     slam_camera cam;
     double user_lambda_init;    /* this window's pMap: > 0 sets the initial LM lambda (100 when
                                    pMap->IsInertial(), Optimizer.cc:1726-1727); 0 -> the options value */
+    /* Right-camera observations of KeyFrames with a second camera (pKFi->mpCamera2, pinhole
+     * here): EdgeSE3ProjectXYZToBody (OptimizableTypes.h:117-144, OptimizableTypes.cpp:192-215),
+     * inserted by Optimizer.cc:1883-1914 right after the KeyFrame's left edge.  NULL = none. */
+    const uint8_t* edge_body;   /* n_edge: 1 = body edge (edge_obs = mvKeysRight[..].pt, [2] unused;
+                                   inv_sigma2 of that keypoint's octave; Huber / chi2 as mono) */
+    const float* kf_Trl;        /* n_kf x 16 row-major KeyFrame::mTrl (right <- left), read for KFs
+                                   with body edges (Converter::toSE3Quat) */
+    slam_camera cam2;           /* mpCamera2 parameters fx, fy, cx, cy (bf unused) */
 } slam_lba_problem;
 
 typedef struct slam_lba_options {

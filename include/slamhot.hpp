@@ -237,6 +237,10 @@ struct LocalBAWindow {
     std::vector<float> edge_obs;      // n_edge x 3 (u, v, uRight < 0 -> mono)
     std::vector<float> edge_inv_sigma2;
     slam_camera cam{};
+    // right-camera observations (EdgeSE3ProjectXYZToBody, Optimizer.cc:1883-1914): empty = none
+    std::vector<uint8_t> edge_body;   // n_edge, 1 = body edge (edge_obs = right keypoint)
+    std::vector<float> kf_Trl;        // n_kf x 16, KeyFrame::mTrl
+    slam_camera cam2{};               // mpCamera2 parameters
     bool inertial = false;            // pMap->IsInertial(): lambda0 = 100 (Optimizer.cc:1726)
     int n_kf() const { return (int)kf_fixed.size(); }
     int n_pt() const { return (int)pt_pos.size() / 3; }
@@ -277,6 +281,11 @@ class LocalBundleAdjuster {
             p.edge_obs = w.edge_obs.data();
             p.edge_inv_sigma2 = w.edge_inv_sigma2.data();
             p.cam = w.cam;
+            if (!w.edge_body.empty()) {
+                p.edge_body = w.edge_body.data();
+                p.kf_Trl = w.kf_Trl.data();
+                p.cam2 = w.cam2;
+            }
             p.user_lambda_init = w.inertial ? 100.0 : 0.0;  // this window's pMap->IsInertial() (:1726)
             out[i].kf_Tcw.resize(w.kf_Tcw.size());
             out[i].pt_pos.resize(w.pt_pos.size());

@@ -28,6 +28,7 @@ using namespace g2o_oracle;
 struct Edge {
     int pt, kf;
     bool stereo;
+    bool body;              // EdgeSE3ProjectXYZToBody (right camera, mTrl)
     double obs[3];
     double info;            // invSigma2 (float) promoted: Information = I * invSigma2
     double err[3];          // _error of the last computeActiveErrors
@@ -39,6 +40,8 @@ struct Edge {
 struct Solver {
     const slam_lba_problem* P;
     double fx, fy, cx, cy, bf;  // float parameters promoted
+    double fx2, fy2, cx2, cy2;  // mpCamera2 (pinhole) parameters
+    std::vector<SE3> trl;       // per KF: Converter::toSE3Quat(pKFi->mTrl)
     double delta_mono, delta_stereo;
     float dsqr_mono, dsqr_stereo;  // RobustKernelHuber::dsqr is float (robust_kernel_impl.h:84)
     std::vector<SE3> pose, pose_bak;
@@ -65,6 +68,14 @@ struct Solver {
     // (types_six_dof_expmap.h:157-162, types_six_dof_expmap.cpp:190-197).
     void compute_error(Edge& e) {
         double Xc[3];
+        if (e.body) {
+            // EdgeSE3ProjectXYZToBody::computeError (OptimizableTypes.h:127-132):
+            // obs - pCamera->project((mTrl * T_lw).map(X_w)), the composed SE3Quat mapping
+            se3_map(se3_mul(trl[e.kf], pose[e.kf]), &pt[3 * e.pt], Xc);
+            e.err[0] = e.obs[0] - (fx2 * Xc[0] / Xc[2] + cx2);
+            e.err[1] = e.obs[1] - (fy2 * Xc[1] / Xc[2] + cy2);
+            return;
+        }
         se3_map(pose[e.kf], &pt[3 * e.pt], Xc);
         if (!e.stereo) {
             const double u = fx * Xc[0] / Xc[2] + cx;
@@ -106,7 +117,10 @@ struct Solver {
 
     bool depth_positive(const Edge& e) const {
         double Xc[3];
-        se3_map(pose[e.kf], &pt[3 * e.pt], Xc);
+        if (e.body)  // OptimizableTypes.h:134-138
+            se3_map(se3_mul(trl[e.kf], pose[e.kf]), &pt[3 * e.pt], Xc);
+        else
+            se3_map(pose[e.kf], &pt[3 * e.pt], Xc);
         return Xc[2] > 0.0;
     }
 
@@ -125,6 +139,10 @@ struct Solver {
     // EdgeSE3ProjectXYZ::linearizeOplus (OptimizableTypes.cpp:139-160) + Pinhole::projectJac
     // (Pinhole.cpp:88-97); EdgeStereoSE3ProjectXYZ::linearizeOplus (types_six_dof_expmap.cpp:228-275)
     void linearize(Edge& e) {
+        if (e.body) {
+            linearize_body(e);
+            return;
+        }
         const SE3& T = pose[e.kf];
         double R[9], Xc[3];
         se3_map(T, &pt[3 * e.pt], Xc);
@@ -179,6 +197,38 @@ struct Solver {
         }
     }
 
+    // EdgeSE3ProjectXYZToBody::linearizeOplus (OptimizableTypes.cpp:192-215):
+    //   Xi = -projectJac(X_r) * (mTrl * T_lw).rotation().toRotationMatrix()
+    //   Xj = -projectJac(X_r) * mTrl.rotation().toRotationMatrix() * SE3deriv(X_l)
+    // with X_l = T_lw.map(X_w), X_r = mTrl.map(X_l); products left to right (Eigen evaluates
+    // the inner 2x3 product first).
+    void linearize_body(Edge& e) {
+        const SE3& T = pose[e.kf];
+        const SE3& Trl = trl[e.kf];
+        double Xl[3], Xr[3], Rrw[9], Rrl[9];
+        se3_map(T, &pt[3 * e.pt], Xl);
+        se3_map(Trl, Xl, Xr);
+        rot_matrix(se3_mul(Trl, T).r, Rrw);
+        rot_matrix(Trl.r, Rrl);
+        const double x = Xr[0], y = Xr[1], z = Xr[2];
+        const double pj[6] = {-(fx2 / z), -0.0, -((-fx2) * x / (z * z)),
+                              -0.0, -(fy2 / z), -((-fy2) * y / (z * z))};
+        for (int r = 0; r < 2; r++)
+            for (int c = 0; c < 3; c++)
+                e.A[3 * r + c] = pj[3 * r + 0] * Rrw[0 + c] + pj[3 * r + 1] * Rrw[3 + c] + pj[3 * r + 2] * Rrw[6 + c];
+        double M[6];
+        for (int r = 0; r < 2; r++)
+            for (int c = 0; c < 3; c++)
+                M[3 * r + c] = pj[3 * r + 0] * Rrl[0 + c] + pj[3 * r + 1] * Rrl[3 + c] + pj[3 * r + 2] * Rrl[6 + c];
+        const double xl = Xl[0], yl = Xl[1], zl = Xl[2];
+        const double S[18] = {0.0, zl, -yl, 1.0, 0.0, 0.0,
+                              -zl, 0.0, xl, 0.0, 1.0, 0.0,
+                              yl, -xl, 0.0, 0.0, 0.0, 1.0};
+        for (int r = 0; r < 2; r++)
+            for (int c = 0; c < 6; c++)
+                e.B[6 * r + c] = M[3 * r + 0] * S[0 + c] + M[3 * r + 1] * S[6 + c] + M[3 * r + 2] * S[12 + c];
+    }
+
     // BaseBinaryEdge::constructQuadraticForm, robust branch (base_binary_edge.hpp:55-120),
     // robustInformation (base_edge.h:96-102): W = rho' * Omega.
     void quadratic_form(Edge& e) {
@@ -223,14 +273,20 @@ struct Solver {
             }
     }
 
-    // BlockSolver::buildSystem (block_solver.hpp:501-560)
+    // BlockSolver::buildSystem (block_solver.hpp:501-560).  Two edges between the same pose and
+    // point (a KeyFrame's left and right observation, Optimizer.cc:1818-1914) write one shared
+    // Hpl block: the follower's product is added to the leader's, in edge order.
+    std::vector<int> lead;  // per edge: the edge whose Hpl block it accumulates into (itself = own)
     void build_system() {
         std::fill(Hpp.begin(), Hpp.end(), 0.0);
         std::fill(Hll.begin(), Hll.end(), 0.0);
         std::fill(b.begin(), b.end(), 0.0);
-        for (Edge& e : E) {
+        for (size_t i = 0; i < E.size(); i++) {
+            Edge& e = E[i];
             linearize(e);
             quadratic_form(e);
+            if (lead[i] != (int)i && hidx[e.kf] >= 0)
+                for (int k = 0; k < 18; k++) E[lead[i]].Hpl[k] += e.Hpl[k];
         }
     }
 
@@ -457,6 +513,10 @@ int oracle_lba_solve(const slam_lba_problem* P, const slam_lba_options* opt, int
     S.cx = P->cam.cx;
     S.cy = P->cam.cy;
     S.bf = P->cam.bf;
+    S.fx2 = P->cam2.fx;
+    S.fy2 = P->cam2.fy;
+    S.cx2 = P->cam2.cx;
+    S.cy2 = P->cam2.cy;
     const float thMono = std::sqrt(5.991), thStereo = std::sqrt(7.815);  // Optimizer.cc:1794-1795
     S.delta_mono = thMono;
     S.delta_stereo = thStereo;
@@ -468,8 +528,10 @@ int oracle_lba_solve(const slam_lba_problem* P, const slam_lba_options* opt, int
     // vertices without edges are not active (sparse_optimizer.cpp:262-300)
     std::vector<int> kf_edges(nk, 0);
     for (int i = 0; i < ne; i++) kf_edges[P->edge_kf[i]]++;
+    S.trl.assign(nk, SE3{{0, 0, 0, 1}, {0, 0, 0}});
     for (int k = 0; k < nk; k++) {
         S.pose[k] = se3_from_cv(P->kf_Tcw + 16 * k);
+        if (P->edge_body && P->kf_Trl) S.trl[k] = se3_from_cv(P->kf_Trl + 16 * k);
         if (P->kf_fixed[k] == 0 && kf_edges[k] > 0) S.hidx[k] = S.np++;
     }
     S.pt.resize(3 * (size_t)npt);
@@ -480,11 +542,20 @@ int oracle_lba_solve(const slam_lba_problem* P, const slam_lba_options* opt, int
         Edge& e = S.E[i];
         e.pt = P->edge_pt[i];
         e.kf = P->edge_kf[i];
-        e.stereo = P->edge_obs[3 * i + 2] >= 0;  // mvuRight < 0 -> mono (Optimizer.cc:1822, 1852)
+        e.body = P->edge_body && P->edge_body[i];
+        e.stereo = !e.body && P->edge_obs[3 * i + 2] >= 0;  // mvuRight < 0 -> mono (Optimizer.cc:1822, 1852)
         for (int c = 0; c < 3; c++) e.obs[c] = P->edge_obs[3 * i + c];
         e.info = P->edge_inv_sigma2[i];
         e.err[0] = e.err[1] = e.err[2] = 0;
-        if (S.hidx[e.kf] >= 0) S.pt_edges[e.pt].push_back(i);
+    }
+    // one Hpl block per (pose, point): an edge right after one on the same point and KeyFrame
+    // (the body edge after the left edge) shares that edge's block
+    S.lead.resize(ne);
+    for (int i = 0; i < ne; i++) {
+        const Edge& e = S.E[i];
+        const bool follows = i > 0 && S.E[i - 1].pt == e.pt && S.E[i - 1].kf == e.kf;
+        S.lead[i] = follows ? S.lead[i - 1] : i;
+        if (S.hidx[e.kf] >= 0 && !follows) S.pt_edges[e.pt].push_back(i);
     }
     // HplCCS columns are sorted by pose row (block_solver.hpp:247, fillSparseBlockMatrixCCS)
     for (auto& col : S.pt_edges) {

@@ -66,9 +66,13 @@ __host__ __device__ constexpr int sym3(int r, int c) { return r * 3 - (r * (r - 
 
 struct EdgeS {
     int pt, kf, hp, win;   // global point, global KF, global free-pose index (-1 fixed), window
-    float obs[3];          // u, v, ur (ur < 0 -> mono)
+    float obs[3];          // u, v, ur (ur = -1 -> mono, kBodyTag -> EdgeSE3ProjectXYZToBody)
     float info;            // invSigma2
 };
+// obs[2] of a right-camera (EdgeSE3ProjectXYZToBody) observation; the host writes mono edges'
+// negative mvuRight as -1, so the tag never collides
+constexpr float kBodyTag = -2.0f;
+__device__ __forceinline__ bool is_body(const EdgeS& e) { return e.obs[2] == kBodyTag; }
 
 struct WinDesc {
     int kf0, nk, pt0, npt, e0, ne, pose0, np;
@@ -91,12 +95,43 @@ struct Counters {
 struct Cam {
     double fx, fy, cx, cy, bf;
     float bff;
+    double fx2, fy2, cx2, cy2;  // mpCamera2 (body edges)
+    const double* trl;          // per global KF: mTrl as a pose record (NULL without body edges)
 };
+
+// (mTrl * T_lw) as a pose record: SE3Quat::operator* (se3quat.h:104-110)
+__device__ inline void body_pose(const double* Trl, const double* P, double* Q) {
+    double rt[3];
+    quat_rotate(load_q(Trl), P + 4, rt);
+    Quat a = load_q(Trl), b = load_q(P);
+    Quat r;
+    r.w = a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z;
+    r.x = a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y;
+    r.y = a.w * b.y + a.y * b.w + a.z * b.x - a.x * b.z;
+    r.z = a.w * b.z + a.z * b.w + a.x * b.y - a.y * b.x;
+    normalize_rotation(r);
+    Q[0] = r.x;
+    Q[1] = r.y;
+    Q[2] = r.z;
+    Q[3] = r.w;
+    for (int i = 0; i < 3; i++) Q[4 + i] = Trl[4 + i] + rt[i];
+    Q[7] = 0.0;
+}
 
 // ---------------------------------------------------------------- edge math
 __device__ inline void edge_error(const EdgeS& e, const Cam& cam, const double* P, const double* X,
                                   double* err) {
     double Xc[3];
+    if (is_body(e)) {
+        // EdgeSE3ProjectXYZToBody::computeError (OptimizableTypes.h:127-132)
+        double Q[8];
+        body_pose(cam.trl + 8 * (long long)e.kf, P, Q);
+        se3_map(Q, X, Xc);
+        err[0] = (double)e.obs[0] - (cam.fx2 * Xc[0] / Xc[2] + cam.cx2);
+        err[1] = (double)e.obs[1] - (cam.fy2 * Xc[1] / Xc[2] + cam.cy2);
+        err[2] = 0.0;
+        return;
+    }
     se3_map(P, X, Xc);
     if (e.obs[2] < 0.f) {
         const double u = cam.fx * Xc[0] / Xc[2] + cam.cx;
@@ -143,6 +178,40 @@ __device__ inline void robustify(const Huber& hk, bool stereo, double c, double&
 // ---------------------------------------------------------------- iteration kernels
 // Jacobians of one edge at estimate (P, X): A = d e / d X (D x 3), B = d e / d pose (D x 6),
 // OptimizableTypes.cpp:139-160 (mono) and types_six_dof_expmap.cpp:228-275 (stereo).
+// EdgeSE3ProjectXYZToBody::linearizeOplus (OptimizableTypes.cpp:192-215): with X_l = T.map(X),
+// X_r = mTrl.map(X_l): A = -J(X_r) R(mTrl*T), B = (-J(X_r) R(mTrl)) SE3deriv(X_l), left to right.
+__device__ inline void body_jacobians(const EdgeS& e, const Cam& cam, const double* P, const double* X, double* A,
+                                      double* B) {
+    const double* Trl = cam.trl + 8 * (long long)e.kf;
+    double Xl[3], Xr[3], Q[8], Rrw[9], Rrl[9];
+    se3_map(P, X, Xl);
+    se3_map(Trl, Xl, Xr);
+    body_pose(Trl, P, Q);
+    rot_matrix(load_q(Q), Rrw);
+    rot_matrix(load_q(Trl), Rrl);
+    const double x = Xr[0], y = Xr[1], z = Xr[2];
+    const double pj[6] = {-(cam.fx2 / z), -0.0, -((-cam.fx2) * x / (z * z)),
+                          -0.0, -(cam.fy2 / z), -((-cam.fy2) * y / (z * z))};
+    double M[6];
+#pragma unroll
+    for (int r = 0; r < 2; r++)
+#pragma unroll
+        for (int cc = 0; cc < 3; cc++) {
+            A[3 * r + cc] = pj[3 * r + 0] * Rrw[0 + cc] + pj[3 * r + 1] * Rrw[3 + cc] + pj[3 * r + 2] * Rrw[6 + cc];
+            M[3 * r + cc] = pj[3 * r + 0] * Rrl[0 + cc] + pj[3 * r + 1] * Rrl[3 + cc] + pj[3 * r + 2] * Rrl[6 + cc];
+        }
+    const double xl = Xl[0], yl = Xl[1], zl = Xl[2];
+    const double S[18] = {0.0, zl, -yl, 1.0, 0.0, 0.0, -zl, 0.0, xl, 0.0, 1.0, 0.0, yl, -xl, 0.0, 0.0, 0.0, 1.0};
+#pragma unroll
+    for (int r = 0; r < 2; r++)
+#pragma unroll
+        for (int cc = 0; cc < 6; cc++)
+            B[6 * r + cc] = M[3 * r + 0] * S[0 + cc] + M[3 * r + 1] * S[6 + cc] + M[3 * r + 2] * S[12 + cc];
+    A[6] = A[7] = A[8] = 0;
+#pragma unroll
+    for (int cc = 0; cc < 6; cc++) B[12 + cc] = 0;
+}
+
 __device__ inline void edge_jacobians(bool stereo, const Cam& cam, const double* P, const double* X, double* A,
                                       double* B) {
     double R[9], Xc[3];
@@ -215,6 +284,9 @@ __device__ __forceinline__ void lin_points_body(int p, int npt_total, const int*
     const double* Xw = pts + C.sel * pt_stride + 4 * (long long)p;
     const double X[3] = {Xw[0], Xw[1], Xw[2]};
     double h[6] = {0, 0, 0, 0, 0, 0}, bb[3] = {0, 0, 0};
+    // an edge right after one on the same KeyFrame (its body edge) shares that edge's Hpl block:
+    // its product is added to the block in edge order, as g2o's shared Hessian block
+    int lead = -1, lead_kf = -1;
     for (int ei = pt_off[p]; ei < pt_off[p + 1]; ei++) {
         const EdgeS e = E[ei];
         const double* P = poses + C.sel * pose_stride + 8 * (long long)e.kf;
@@ -226,7 +298,10 @@ __device__ __forceinline__ void lin_points_body(int p, int npt_total, const int*
         robustify(hk, stereo, edge_chi2(e, err), rho0, rho1);
         rho_out[ei] = rho0;
         double A[9], B[18];
-        edge_jacobians(stereo, cam, P, X, A, B);
+        if (is_body(e))
+            body_jacobians(e, cam, P, X, A, B);
+        else
+            edge_jacobians(stereo, cam, P, X, A, B);
         const double info = e.info;
         const double w = rho1 * info;
         double om_r[3];
@@ -256,6 +331,17 @@ __device__ __forceinline__ void lin_points_body(int p, int npt_total, const int*
                 for (int k = 0; k < 3; k++) sacc += (B[6 * k + r] * w) * A[3 * k + cc];  // mono: row 2 is zero
                 hpl[3 * r + cc] = sacc;
             }
+        if (e.kf == lead_kf) {
+            double* out = Hpl_out + (long long)kHplStride * lead;
+#pragma unroll
+            for (int k = 0; k < 18; k += 2) {
+                const double2 o = *(double2*)(out + k);
+                *(double2*)(out + k) = double2{o.x + hpl[k], o.y + hpl[k + 1]};
+            }
+            continue;
+        }
+        lead = ei;
+        lead_kf = e.kf;
         double* out = Hpl_out + (long long)kHplStride * ei;
 #pragma unroll
         for (int k = 0; k < 18; k += 2) *(double2*)(out + k) = double2{hpl[k], hpl[k + 1]};
@@ -299,7 +385,10 @@ __device__ __forceinline__ void lin_poses_body(int pose, int lane, int npose_tot
         double rho0, rho1;
         robustify(hk, stereo, edge_chi2(e, err), rho0, rho1);
         double A[9], B[18];
-        edge_jacobians(stereo, cam, P, X, A, B);
+        if (is_body(e))
+            body_jacobians(e, cam, P, X, A, B);
+        else
+            edge_jacobians(stereo, cam, P, X, A, B);
         const double info = e.info;
         const double w = rho1 * info;
         double om_r[3];
@@ -1397,7 +1486,7 @@ __global__ void k_opt_begin(int nwin, const WinDesc* __restrict__ wins, WinCtl* 
 __global__ void k_finalize_edges(int ne_total, const EdgeS* __restrict__ E, const WinCtl* __restrict__ ctl,
                                  const double* __restrict__ poses, const double* __restrict__ pts,
                                  long long pose_stride, long long pt_stride, const double* __restrict__ err,
-                                 uint8_t* __restrict__ outlier) {
+                                 const double* __restrict__ trl, uint8_t* __restrict__ outlier) {
     const int ei = blockIdx.x * blockDim.x + threadIdx.x;
     if (ei >= ne_total) return;
     const EdgeS e = E[ei];
@@ -1406,7 +1495,13 @@ __global__ void k_finalize_edges(int ne_total, const EdgeS* __restrict__ E, cons
     const double* Xw = pts + C.sel * pt_stride + 4 * (long long)e.pt;
     const double X[3] = {Xw[0], Xw[1], Xw[2]};
     double Xc[3];
-    se3_map(P, X, Xc);
+    if (is_body(e)) {  // isDepthPositive in the right camera (OptimizableTypes.h:134-138)
+        double Q[8];
+        body_pose(trl + 8 * (long long)e.kf, P, Q);
+        se3_map(Q, X, Xc);
+    } else {
+        se3_map(P, X, Xc);
+    }
     const double ev[3] = {err[4 * (long long)ei], err[4 * (long long)ei + 1], err[4 * (long long)ei + 2]};
     const bool stereo = e.obs[2] >= 0.f;
     const double c = edge_chi2(e, ev);
@@ -1508,6 +1603,7 @@ struct Plan {
     int *pt_off, *pt_win, *spe_off, *spe, *pe_off, *pe, *pose_win, *kf_hp, *kf_win, *blk_win, *ct_off, *blk_order;
     int2 *blk_pose, *ct;
     float *kf_in, *pt_in;
+    double* kf_trl;  // per KF: mTrl as a pose record (body edges)
 };
 
 constexpr int kRing = 4;  // LM steps whose counters are in flight (host-side ring)
@@ -1533,21 +1629,22 @@ struct slam_lba {
 namespace {
 
 struct WinStart {
-    int kf0, pt0, e0, pose0, blk0, spe0;
+    int kf0, pt0, e0, pose0, blk0, spe0, pe0;
     long long ct0, hs0;
     size_t h0;
 };
 
 struct PlanSizes {
     std::vector<WinStart> starts;
-    int nkf = 0, npt = 0, ne = 0, npose = 0, nblk = 0, nspe = 0, nw = 0;
+    int nkf = 0, npt = 0, ne = 0, npose = 0, nblk = 0, nspe = 0, npe = 0, nw = 0;
     long long nct = 0, hs_total = 0;
     int max_n = 0;
+    bool any_body = false;
 };
 
 struct Layout {
     size_t edges, wins, ctl, pt_off, pt_win, spe_off, spe, pe_off, pe, pose_win, kf_hp, kf_win, blk_win, ct_off,
-        blk_order, blk_pose, ct, kf_in, pt_in, total;
+        blk_order, blk_pose, ct, kf_in, pt_in, kf_trl, total;
 };
 
 Layout make_layout(const PlanSizes& z) {
@@ -1566,7 +1663,7 @@ Layout make_layout(const PlanSizes& z) {
     L.spe_off = take(sizeof(int) * (z.npt + 1));
     L.spe = take(sizeof(int) * z.nspe);
     L.pe_off = take(sizeof(int) * (z.npose + 1));
-    L.pe = take(sizeof(int) * z.nspe);
+    L.pe = take(sizeof(int) * z.npe);
     L.pose_win = take(sizeof(int) * z.npose);
     L.kf_hp = take(sizeof(int) * z.nkf);
     L.kf_win = take(sizeof(int) * z.nkf);
@@ -1577,6 +1674,7 @@ Layout make_layout(const PlanSizes& z) {
     L.ct = take(sizeof(int2) * z.nct);
     L.kf_in = take(sizeof(float) * 16 * z.nkf);
     L.pt_in = take(sizeof(float) * 3 * z.npt);
+    L.kf_trl = take(z.any_body ? sizeof(double) * 8 * z.nkf : 0);
     L.total = off;
     return L;
 }
@@ -1602,6 +1700,7 @@ Plan bind(unsigned char* base, const Layout& L) {
     P.ct = (int2*)(base + L.ct);
     P.kf_in = (float*)(base + L.kf_in);
     P.pt_in = (float*)(base + L.pt_in);
+    P.kf_trl = (double*)(base + L.kf_trl);
     return P;
 }
 
@@ -1615,10 +1714,16 @@ slam_status plan_sizes(int n_prob, const slam_lba_problem* probs, PlanSizes& z, 
     for (int w = 0; w < n_prob; w++) {
         const slam_lba_problem& P = probs[w];
         if (P.n_kf < 0 || P.n_pt < 0 || P.n_edge < 0) return SLAM_EINVAL;
-        z.starts[w] = WinStart{z.nkf, z.npt, z.ne, z.npose, z.nblk, z.nspe, z.nct, z.hs_total, hidx_all.size()};
+        z.starts[w] = WinStart{z.nkf, z.npt, z.ne, z.npose, z.nblk, z.nspe, z.npe, z.nct, z.hs_total, hidx_all.size()};
         if ((P.n_kf && (!P.kf_Tcw || !P.kf_fixed)) || (P.n_pt && !P.pt_pos) ||
             (P.n_edge && (!P.edge_pt || !P.edge_kf || !P.edge_obs || !P.edge_inv_sigma2)))
             return SLAM_EINVAL;
+        if (P.edge_body && P.n_edge) {
+            bool has = false;
+            for (int i = 0; i < P.n_edge && !has; i++) has = P.edge_body[i] != 0;
+            if (has && !P.kf_Trl) return SLAM_EINVAL;  // body edges need each KeyFrame's mTrl
+            z.any_body = z.any_body || has;
+        }
         cnt.assign(P.n_kf, 0);
         for (int i = 0; i < P.n_edge; i++) {
             const int p = P.edge_pt[i], k = P.edge_kf[i];
@@ -1643,8 +1748,12 @@ slam_status plan_sizes(int n_prob, const slam_lba_problem* probs, PlanSizes& z, 
                 prev = p;
             }
             if (i < P.n_edge && hidx_all[h0 + P.edge_kf[i]] >= 0) {
-                run++;
-                z.nspe++;
+                z.npe++;
+                // an edge right after one on the same KeyFrame shares its Hpl block
+                if (!(i > 0 && P.edge_pt[i - 1] == p && P.edge_kf[i - 1] == P.edge_kf[i])) {
+                    run++;
+                    z.nspe++;
+                }
             }
         }
         z.nkf += P.n_kf;
@@ -1697,6 +1806,30 @@ slam_status plan_fill(int n_prob, const slam_lba_problem* probs, const std::vect
             P.kf_win[nkf + k] = w;
         }
         std::memcpy(P.kf_in + 16 * (size_t)nkf, Q.kf_Tcw, sizeof(float) * 16 * Q.n_kf);
+        if (Z.any_body) {  // Converter::toSE3Quat(pKFi->mTrl) -> SE3Quat(R, t) (se3quat.h:56-58)
+            for (int k = 0; k < Q.n_kf; k++) {
+                double* rec = P.kf_trl + 8 * (size_t)(nkf + k);
+                if (!Q.edge_body || !Q.kf_Trl) {
+                    const double id[8] = {0, 0, 0, 1, 0, 0, 0, 0};
+                    std::memcpy(rec, id, sizeof(id));
+                    continue;
+                }
+                const float* T = Q.kf_Trl + 16 * (size_t)k;
+                double R[9];
+                for (int a = 0; a < 3; a++)
+                    for (int b = 0; b < 3; b++) R[3 * a + b] = T[4 * a + b];
+                Quat q = quat_from_R(R);
+                normalize_rotation(q);
+                rec[0] = q.x;
+                rec[1] = q.y;
+                rec[2] = q.z;
+                rec[3] = q.w;
+                rec[4] = T[3];
+                rec[5] = T[7];
+                rec[6] = T[11];
+                rec[7] = 0.0;
+            }
+        }
         std::memcpy(P.pt_in + 3 * (size_t)npt, Q.pt_pos, sizeof(float) * 3 * Q.n_pt);
         for (int i = 0; i < Q.n_edge; i++) {
             EdgeS& e = P.edges[ne + i];
@@ -1707,12 +1840,14 @@ slam_status plan_fill(int n_prob, const slam_lba_problem* probs, const std::vect
             e.win = w;
             e.obs[0] = Q.edge_obs[3 * i];
             e.obs[1] = Q.edge_obs[3 * i + 1];
-            e.obs[2] = Q.edge_obs[3 * i + 2];
+            const bool body = Q.edge_body && Q.edge_body[i];
+            const float ur = Q.edge_obs[3 * i + 2];
+            e.obs[2] = body ? kBodyTag : (ur < 0.f ? -1.0f : ur);
             e.info = Q.edge_inv_sigma2[i];
         }
         // point CSR + per-point free-pose edges sorted by pose (HplCCS column order) + Schur
         // contribution counts per block (i1 <= i2: blk = i2 (i2 + 1) / 2 + i1)
-        const int spe_start = nspe;
+        const int pe_start = ws.pe0;
         bcnt.assign(D.nblk + 1, 0);
         pcnt.assign(np + 1, 0);
         int i = 0;
@@ -1721,16 +1856,18 @@ slam_status plan_fill(int n_prob, const slam_lba_problem* probs, const std::vect
             P.pt_win[npt + p] = w;
             P.spe_off[npt + p] = nspe;
             col.clear();
-            for (; i < Q.n_edge && Q.edge_pt[i] == p; i++)
-                if (hidx[Q.edge_kf[i]] >= 0) col.push_back(i);
+            for (; i < Q.n_edge && Q.edge_pt[i] == p; i++) {
+                // the edge right after one on the same KeyFrame (body edge) shares its Hpl block
+                const bool follows = i > 0 && Q.edge_pt[i - 1] == p && Q.edge_kf[i - 1] == Q.edge_kf[i];
+                if (hidx[Q.edge_kf[i]] >= 0 && !follows) col.push_back(i);
+            }
             for (size_t x = 1; x < col.size(); x++)  // stable insertion sort by pose
                 for (size_t y = x; y > 0 && hidx[Q.edge_kf[col[y - 1]]] > hidx[Q.edge_kf[col[y]]]; y--)
                     std::swap(col[y - 1], col[y]);
             for (size_t x = 0; x < col.size(); x++) {
                 const int i1 = hidx[Q.edge_kf[col[x]]];
-                if (x && i1 == hidx[Q.edge_kf[col[x - 1]]]) return SLAM_EINVAL;  // 2 obs of 1 point in 1 KF
+                if (x && i1 == hidx[Q.edge_kf[col[x - 1]]]) return SLAM_EINVAL;  // non-adjacent edges of 1 point in 1 KF
                 P.spe[nspe++] = ne + col[x];
-                pcnt[i1 + 1]++;
                 for (size_t y = x; y < col.size(); y++) {
                     const int i2 = hidx[Q.edge_kf[col[y]]];
                     bcnt[i2 * (i2 + 1) / 2 + i1 + 1]++;
@@ -1759,15 +1896,19 @@ slam_status plan_fill(int n_prob, const slam_lba_problem* probs, const std::vect
                 }
             }
         }
-        // edges of every free pose, in insertion order (shares the index space of spe)
+        // edges of every free pose (followers included: each adds its own Hpp), insertion order
+        for (int e = 0; e < Q.n_edge; e++) {
+            const int h = hidx[Q.edge_kf[e]];
+            if (h >= 0) pcnt[h + 1]++;
+        }
         for (int k = 0; k < np; k++) pcnt[k + 1] += pcnt[k];
         for (int k = 0; k < np; k++) {
-            P.pe_off[npose + k] = spe_start + pcnt[k];
+            P.pe_off[npose + k] = pe_start + pcnt[k];
             P.pose_win[npose + k] = w;
         }
         for (int e = 0; e < Q.n_edge; e++) {
             const int h = hidx[Q.edge_kf[e]];
-            if (h >= 0) P.pe[spe_start + pcnt[h]++] = ne + e;
+            if (h >= 0) P.pe[pe_start + pcnt[h]++] = ne + e;
         }
         (void)wct;
         (void)nkf;
@@ -1795,7 +1936,7 @@ slam_status plan_fill(int n_prob, const slam_lba_problem* probs, const std::vect
         if (r != SLAM_OK) return r;
     P.pt_off[Z.npt] = Z.ne;
     P.spe_off[Z.npt] = Z.nspe;
-    P.pe_off[Z.npose] = Z.nspe;
+    P.pe_off[Z.npose] = Z.npe;
     P.ct_off[Z.nblk] = (int)Z.nct;
     return SLAM_OK;
 }
@@ -1946,6 +2087,9 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     SLAM_HIP_TRY(hipMemsetAsync(s->xp.p, 0, sizeof(double) * 6 * nps, S));
     SLAM_HIP_TRY(hipMemsetAsync(s->xl.p, 0, sizeof(double) * 4 * npt, S));
     SLAM_HIP_TRY(hipMemsetAsync(s->err.p, 0, sizeof(double) * 4 * ne, S));
+    // body edges that share their KeyFrame's Hpl block have no Schur entry of their own: their
+    // B db slot stays zero, so k_schur_blocks' sum over a pose's edges adds 0 for them
+    if (Z.any_body) SLAM_HIP_TRY(hipMemsetAsync(s->tr.p, 0, sizeof(double) * kTrStride * ne, S));
     s->last_plan_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_plan0).count();
 
     Cam cam;
@@ -1961,6 +2105,21 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     cam.cy = c0.cy;
     cam.bf = c0.bf;
     cam.bff = c0.bf;
+    cam.trl = Z.any_body ? DP.kf_trl : nullptr;
+    cam.fx2 = cam.fy2 = cam.cx2 = cam.cy2 = 0.0;
+    if (Z.any_body) {  // one second camera per batch, among the windows that have body edges
+        const slam_camera* c2 = nullptr;
+        for (int w = 0; w < nw; w++) {
+            if (!probs[w].edge_body || !probs[w].kf_Trl) continue;
+            const slam_camera& c = probs[w].cam2;
+            if (c2 && (c.fx != c2->fx || c.fy != c2->fy || c.cx != c2->cx || c.cy != c2->cy)) return SLAM_EINVAL;
+            c2 = &c;
+        }
+        cam.fx2 = c2->fx;
+        cam.fy2 = c2->fy;
+        cam.cx2 = c2->cx;
+        cam.cy2 = c2->cy;
+    }
     Huber hk;
     const float thMono = std::sqrt(5.991), thStereo = std::sqrt(7.815);  // Optimizer.cc:1794-1795
     hk.delta_mono = thMono;
@@ -2081,7 +2240,7 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
         if (*s->h_stop) stopped = true;
     }
     k_finalize_edges<<<blocks(H.ne, T), T, 0, S>>>(H.ne, dE, dC, poses, pts, pose_stride, pt_stride,
-                                                    as<double>(s->err), as<uint8_t>(s->outl));
+                                                    as<double>(s->err), cam.trl, as<uint8_t>(s->outl));
     k_finalize_state<<<blocks(H.nkf + H.npt, T), T, 0, S>>>(H.nkf, H.npt, DP.kf_win, DP.pt_win, dC,
                                                              poses, pts, pose_stride, pt_stride,
                                                              as<float>(s->kf_out), as<float>(s->pt_out));

@@ -12,7 +12,7 @@ struct Quat {
     double x, y, z, w;
 };
 
-__device__ inline Quat quat_from_R(const double* R) {
+__host__ __device__ inline Quat quat_from_R(const double* R) {
     Quat q;
     double t = R[0] + R[4] + R[8];
     if (t > 0.0) {
@@ -41,7 +41,7 @@ __device__ inline Quat quat_from_R(const double* R) {
     return q;
 }
 
-__device__ inline void normalize_rotation(Quat& q) {
+__host__ __device__ inline void normalize_rotation(Quat& q) {
     if (q.w < 0) {
         q.x = -q.x;
         q.y = -q.y;
@@ -55,7 +55,7 @@ __device__ inline void normalize_rotation(Quat& q) {
     q.w /= n;
 }
 
-__device__ inline void rot_matrix(const Quat& q, double* R) {
+__host__ __device__ inline void rot_matrix(const Quat& q, double* R) {
     const double tx = 2.0 * q.x, ty = 2.0 * q.y, tz = 2.0 * q.z;
     const double twx = tx * q.w, twy = ty * q.w, twz = tz * q.w;
     const double txx = tx * q.x, txy = ty * q.x, txz = tz * q.x;
@@ -71,7 +71,7 @@ __device__ inline void rot_matrix(const Quat& q, double* R) {
     R[8] = 1.0 - (txx + tyy);
 }
 
-__device__ inline void quat_rotate(const Quat& q, const double* p, double* out) {
+__host__ __device__ inline void quat_rotate(const Quat& q, const double* p, double* out) {
     double uv[3] = {q.y * p[2] - q.z * p[1], q.z * p[0] - q.x * p[2], q.x * p[1] - q.y * p[0]};
     uv[0] += uv[0];
     uv[1] += uv[1];

@@ -497,7 +497,8 @@ class LbaProblem(C.Structure):
     _fields_ = [("n_kf", C.c_int32), ("kf_Tcw", C.c_void_p), ("kf_fixed", C.c_void_p), ("n_pt", C.c_int32),
                 ("pt_pos", C.c_void_p), ("n_edge", C.c_int32), ("edge_pt", C.c_void_p), ("edge_kf", C.c_void_p),
                 ("edge_obs", C.c_void_p), ("edge_inv_sigma2", C.c_void_p), ("cam", Camera),
-                ("user_lambda_init", C.c_double)]
+                ("user_lambda_init", C.c_double), ("edge_body", C.c_void_p), ("kf_Trl", C.c_void_p),
+                ("cam2", Camera)]
 
 
 class LbaOptions(C.Structure):
@@ -524,6 +525,12 @@ def make_lba_problem(w: dict):
                    arrs["pt_pos"].ctypes.data, n_e, arrs["edge_pt"].ctypes.data, arrs["edge_kf"].ctypes.data,
                    arrs["edge_obs"].ctypes.data, arrs["edge_inv_sigma2"].ctypes.data, Camera(*w["cam"]),
                    float(w.get("user_lambda_init", 0.0)))
+    if w.get("edge_body") is not None:  # EdgeSE3ProjectXYZToBody observations (mpCamera2)
+        arrs["edge_body"] = np.ascontiguousarray(w["edge_body"], np.uint8)
+        arrs["kf_Trl"] = np.ascontiguousarray(w["kf_Trl"], np.float32)
+        p.edge_body = arrs["edge_body"].ctypes.data
+        p.kf_Trl = arrs["kf_Trl"].ctypes.data
+        p.cam2 = Camera(*w["cam2"])
     p._keep = arrs
     out = dict(kf_Tcw=np.zeros((n_kf, 16), np.float32), pt_pos=np.zeros((n_pt, 3), np.float32),
                edge_outlier=np.zeros(n_e, np.uint8))

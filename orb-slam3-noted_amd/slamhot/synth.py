@@ -152,7 +152,7 @@ def _level_tables(nfeatures=1000, scale_factor=1.2, nlevels=8):
 
 def lba_window(seed: int, n_kf: int = 50, n_pt: int = 2000, obs_per_pt: int = 8,
                stereo_frac: float = 0.0, outlier_frac: float = 0.02, arc_deg: float = 80.0,
-               radius: float = 3.0, noise: float = 1.0):
+               radius: float = 3.0, noise: float = 1.0, body_frac: float = 0.0):
     """A seeded local-BA window in the layout of slam_lba_problem.
 
     50 KeyFrames on a ``radius`` arc facing a 4 x 2 x 4 m box of points; every point is seen
@@ -161,7 +161,10 @@ def lba_window(seed: int, n_kf: int = 50, n_pt: int = 2000, obs_per_pt: int = 8,
     N(0, 1.2^l); ``outlier_frac`` observations replaced by uniform in-image points;
     KF poses perturbed by 0.5 deg / 2 cm and points by 3 cm.  KF 0 is the map-init KF
     (fixed, written back) and KF 1 is the fallback fixed camera (kf_fixed = 2), so 48 KFs
-    are free.  Edges are point-major, KFs in id order."""
+    are free.  Edges are point-major, KFs in id order.
+    ``body_frac`` > 0 gives every KeyFrame a second (pinhole) camera: that fraction of the left
+    observations is followed by a right-camera observation, an EdgeSE3ProjectXYZToBody
+    (Optimizer.cc:1883-1914), with the rig's mTrl and the second camera's intrinsics."""
     rng = np.random.default_rng(seed)
     cam = EUROC_CAM
     scale, inv_sigma2, nf = _level_tables()
@@ -197,7 +200,10 @@ def lba_window(seed: int, n_kf: int = 50, n_pt: int = 2000, obs_per_pt: int = 8,
         pts[i] = X
         obs_kf.append(np.sort(rng.choice(cand, obs_per_pt, replace=False)))
         i += 1
-    edge_pt, edge_kf, obs, isig = [], [], [], []
+    edge_pt, edge_kf, obs, isig, body = [], [], [], [], []
+    cam2 = dict(fx=431.9, fy=432.4, cx=371.3, cy=249.8)
+    R_rl = _axis_angle(np.array([0.2, 1.0, 0.1]), np.deg2rad(0.6))
+    t_rl = np.array([-0.110, 0.0012, 0.0021])
     for p in range(n_pt):
         for k in obs_kf[p]:
             Xc = Rs[k] @ pts[p] + ts[k]
@@ -220,6 +226,21 @@ def lba_window(seed: int, n_kf: int = 50, n_pt: int = 2000, obs_per_pt: int = 8,
             edge_kf.append(k)
             obs.append((u, v, ur))
             isig.append(inv_sigma2[lvl])
+            body.append(0)
+            if body_frac > 0 and rng.random() < body_frac:
+                Xr = R_rl @ Xc + t_rl
+                if Xr[2] > 0.3:
+                    lv2 = rng.choice(len(p_level), p=p_level)
+                    s2 = float(scale[lv2])
+                    u2 = cam2["fx"] * Xr[0] / Xr[2] + cam2["cx"] + noise * rng.normal(0, s2)
+                    v2 = cam2["fy"] * Xr[1] / Xr[2] + cam2["cy"] + noise * rng.normal(0, s2)
+                    if rng.random() < outlier_frac:
+                        u2, v2 = rng.uniform(0, cam["w"]), rng.uniform(0, cam["h"])
+                    edge_pt.append(p)
+                    edge_kf.append(k)
+                    obs.append((u2, v2, -1.0))
+                    isig.append(inv_sigma2[lv2])
+                    body.append(1)
     # perturbed initial estimates
     T0 = np.zeros((n_kf, 16), np.float32)
     for k in range(n_kf):
@@ -242,7 +263,16 @@ def lba_window(seed: int, n_kf: int = 50, n_pt: int = 2000, obs_per_pt: int = 8,
     gt_T[:, :3, :3] = Rs
     gt_T[:, :3, 3] = ts
     gt_T[:, 3, 3] = 1
+    extra = {}
+    if body_frac > 0:
+        Trl = np.eye(4)
+        Trl[:3, :3] = R_rl
+        Trl[:3, 3] = t_rl
+        extra = dict(edge_body=np.array(body, np.uint8),
+                     kf_Trl=np.tile(Trl.reshape(1, 16), (n_kf, 1)).astype(np.float32),
+                     cam2=tuple(np.float32(cam2[k]) for k in ("fx", "fy", "cx", "cy")) + (np.float32(0),))
     return dict(
+        **extra,
         kf_Tcw=T0, kf_fixed=fixed, pt_pos=P0,
         edge_pt=np.array(edge_pt, np.int32), edge_kf=np.array(edge_kf, np.int32),
         edge_obs=np.array(obs, np.float32), edge_inv_sigma2=np.array(isig, np.float32),

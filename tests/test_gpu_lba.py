@@ -55,6 +55,26 @@ def test_lba_full_window_stereo(solver, seed):
     _check(g, o)
 
 
+@pytest.mark.parametrize("seed,stereo", [(50, 0.0), (51, 0.3)])
+def test_lba_full_window_body_edges(solver, seed, stereo):
+    """EdgeSE3ProjectXYZToBody (C4): KeyFrames with a second pinhole camera, 40% of the left
+    observations followed by a right-camera observation through mTrl."""
+    W = synth.lba_window(seed, stereo_frac=stereo, body_frac=0.4)
+    assert W["edge_body"].sum() > 1000
+    g = solver.solve(W)
+    o = ob.lba_solve(W)
+    _check(g, o)
+    assert g["chi2_final"] < g["chi2_initial"]
+
+
+def test_lba_batch_mixed_body_and_plain(solver):
+    """A batch mixing rig windows (body edges) and single-camera windows."""
+    Ws = [synth.lba_window(60 + i, n_kf=10 + 3 * i, n_pt=200 + 50 * i, obs_per_pt=5,
+                           body_frac=0.5 if i % 2 == 0 else 0.0, stereo_frac=0.2 * (i % 3)) for i in range(5)]
+    for W, g in zip(Ws, solver.solve(Ws)):
+        _check(g, ob.lba_solve(W))
+
+
 def test_lba_small_windows(solver):
     for seed in range(5, 11):
         W = synth.lba_window(seed, n_kf=8 + seed, n_pt=150 + 20 * seed, obs_per_pt=4, stereo_frac=0.2 * (seed % 2))

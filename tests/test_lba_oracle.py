@@ -114,3 +114,66 @@ def test_fixed_camera_poses_pass_through():
     assert np.array_equal(T[fixed2], W["kf_Tcw"][fixed2])
     # the init KF (fixed, written back) only round-trips through SE3Quat
     assert np.abs(T[0] - W["kf_Tcw"][0]).max() < 1e-6
+
+
+def _qmul(a, b):
+    ax, ay, az, aw = a
+    bx, by, bz, bw = b
+    return np.array([aw * bx + ax * bw + ay * bz - az * by, aw * by + ay * bw + az * bx - ax * bz,
+                     aw * bz + az * bw + ax * by - ay * bx, aw * bw - ax * bx - ay * by - az * bz])
+
+
+def test_body_edge_initial_chi2_matches_numpy():
+    """EdgeSE3ProjectXYZToBody (OptimizableTypes.h:117-144): obs - project2((mTrl * T_lw).map(X)),
+    Huber as mono; checked against numpy on the composed SE3Quat."""
+    W = synth.lba_window(45, n_kf=12, n_pt=200, obs_per_pt=5, body_frac=0.6)
+    body = W["edge_body"].astype(bool)
+    assert body.any()
+    T = W["kf_Tcw"].reshape(-1, 4, 4).astype(np.float64)
+    Trl = W["kf_Trl"].reshape(-1, 4, 4).astype(np.float64)
+    fx2, fy2, cx2, cy2 = [float(c) for c in W["cam2"][:4]]
+    chi = []
+    for i in np.flatnonzero(body):
+        k = W["edge_kf"][i]
+        q1, q2 = _quat_from_R(Trl[k, :3, :3]), _quat_from_R(T[k, :3, :3])
+        q = _qmul(q1, q2)
+        q = (-q if q[3] < 0 else q) / np.linalg.norm(q)
+        t = Trl[k, :3, 3] + _rot(q1) @ T[k, :3, 3]
+        Xr = _rot(q) @ W["pt_pos"][W["edge_pt"][i]].astype(np.float64) + t
+        e = W["edge_obs"][i, :2] - np.array([fx2 * Xr[0] / Xr[2] + cx2, fy2 * Xr[1] / Xr[2] + cy2])
+        chi.append(float(e @ e) * float(W["edge_inv_sigma2"][i]))
+    chi = np.array(chi)
+    dm = float(f32(np.sqrt(5.991)))
+    dsqr = float(f32(dm * dm))
+    rob_body = np.where(chi <= dsqr, chi, 2 * np.sqrt(chi) * dm - dsqr).sum()
+    Wm = {k: v for k, v in W.items() if k not in ("edge_body", "kf_Trl", "cam2")}
+    for k in ("edge_pt", "edge_kf", "edge_obs", "edge_inv_sigma2"):
+        Wm[k] = W[k][~body]
+    r = ob.lba_solve(W, iters_first=1, iters_second=0)
+    np.testing.assert_allclose(r["chi2_initial"], numpy_robust_chi2(Wm) + rob_body, rtol=1e-9)
+
+
+def test_body_edge_identity_rig_equals_duplicate_mono_edge():
+    """With mTrl = identity and camera2 = camera, a body edge is the same residual and Jacobian as
+    a second mono edge on the left camera: both windows solve to the same estimate."""
+    W = synth.lba_window(46, n_kf=10, n_pt=150, obs_per_pt=4, body_frac=0.5)
+    Wb = dict(W)
+    Wb["kf_Trl"] = np.tile(np.eye(4, dtype=np.float32).reshape(1, 16), (len(W["kf_fixed"]), 1))
+    Wb["cam2"] = W["cam"]
+    Wm = {k: v for k, v in Wb.items() if k not in ("edge_body", "kf_Trl", "cam2")}
+    rb, rm = ob.lba_solve(Wb), ob.lba_solve(Wm)
+    assert rb["iterations"] == rm["iterations"] and rb["trials"] == rm["trials"]
+    assert np.array_equal(rb["edge_outlier"], rm["edge_outlier"])
+    np.testing.assert_allclose(rb["chi2_final"], rm["chi2_final"], rtol=1e-9)
+    assert np.abs(rb["kf_Tcw"] - rm["kf_Tcw"]).max() < 1e-6
+    assert np.abs(rb["pt_pos"] - rm["pt_pos"]).max() < 1e-6
+
+
+def test_body_edge_noise_free_window_converges():
+    """Residual and Jacobians of the body edge agree with each other: a noise-free rig window
+    converges to the ground truth."""
+    W = synth.lba_window(47, n_kf=15, n_pt=400, obs_per_pt=6, outlier_frac=0.0, noise=0.0, body_frac=0.7)
+    r = ob.lba_solve(W)
+    assert r["chi2_final"] < 1e-6 * r["chi2_initial"]
+    assert r["n_outlier"] == 0
+    assert np.abs(r["pt_pos"] - W["gt_pts"]).max() < 1e-3
