@@ -8,10 +8,14 @@ HIPFLAGS ?= --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off \
 SRCS := $(CSRC)/extractor.hip $(CSRC)/matcher.hip $(CSRC)/lba.hip $(CSRC)/pose.hip $(CSRC)/stereo.hip $(CSRC)/mapping.hip $(CSRC)/rectify.hip
 HDRS := $(wildcard $(CSRC)/*.hpp) $(CSRC)/orb_pattern.inc include/slamhot.h
 
-all: $(LIBDIR)/libslamhot.so oracle tests/cpp/host_driver
+all: $(LIBDIR)/libslamhot.so oracle tests/cpp/host_driver tests/cpp/shim_driver
 
 # C++ host layer (include/slamhot.hpp) driven by tests/test_gpu_cpp_host.py (test infra)
 tests/cpp/host_driver: tests/cpp/host_driver.cpp include/slamhot.hpp include/slamhot.h $(LIBDIR)/libslamhot.so
+	g++ -O2 -std=c++17 -Wall -Wextra -Iinclude -o $@ $< -L$(LIBDIR) -lslamhot -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)'
+
+# the drop-in shim bodies (include/slamhot_orbslam3.hpp) on ORB-SLAM3 stand-ins (test infra)
+tests/cpp/shim_driver: tests/cpp/shim_driver.cpp tests/cpp/orbslam3_standins.hpp include/slamhot_orbslam3.hpp include/slamhot.hpp include/slamhot.h $(LIBDIR)/libslamhot.so
 	g++ -O2 -std=c++17 -Wall -Wextra -Iinclude -o $@ $< -L$(LIBDIR) -lslamhot -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)'
 
 $(LIBDIR)/libslamhot.so: $(SRCS) $(HDRS)
@@ -22,6 +26,6 @@ oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -rf $(LIBDIR) oracle/build tests/cpp/host_driver
+	rm -rf $(LIBDIR) oracle/build tests/cpp/host_driver tests/cpp/shim_driver
 
 .PHONY: all oracle clean

@@ -443,6 +443,15 @@ slam_status slamhot_stereo_match_batch_device(slam_stereo* st, slam_extractor* l
                                               float mbf, float mb, void* d_uright, void* d_depth, void* d_sad,
                                               void* hip_stream);
 
+/* void Frame::ComputeStereoMatches() (Frame.cc:794-964) for one stereo Frame whose two images
+ * were just extracted by `left` and `right` (slamhot_extract on each: their pyramids are still on
+ * the device) — the host-buffer form the Frame constructor calls: the keypoints / descriptors
+ * the two extractions returned in, mvuRight / mvDepth (n_left each, -1 where unmatched) out. */
+slam_status slamhot_compute_stereo_matches(slam_stereo* st, slam_extractor* left, slam_extractor* right, int n_left,
+                                           const slam_keypoint* kps_left, const uint8_t* desc_left, int n_right,
+                                           const slam_keypoint* kps_right, const uint8_t* desc_right, float mbf,
+                                           float mb, float* uright, float* depth);
+
 /* ------------------------------------------------------------------ LocalMapping matchers
  * The Hamming-heavy work LocalMapping runs around local BA. */
 typedef struct slam_mapper slam_mapper;

@@ -216,6 +216,62 @@ class ORBmatcher {
         return n;
     }
 
+    /* int SearchByProjection(Frame& F, const vector<MapPoint*>& vpMapPoints, const float th,
+     * const bool bFarPoints, const float thFarPoints) (ORBmatcher.cc:44-214): vpMapPoints as the
+     * tracking records Frame::isInFrustum left (slam_mp_track) + their descriptors (32 B each);
+     * f_match[i] = the MapPoint index F's feature i took (-1 = untouched).  Returns nmatches. */
+    int SearchByProjection(const slam_frame_view& F, const std::vector<slam_mp_track>& vpMapPoints,
+                           const uint8_t* mp_desc, float th, bool bFarPoints, float thFarPoints,
+                           std::vector<int>& f_match) {
+        f_match.assign(F.n, -1);
+        int n = 0;
+        check(slamhot_search_by_projection_local(m_, &F, (int)vpMapPoints.size(), vpMapPoints.data(), mp_desc,
+                                                 nnratio_, th, bFarPoints, thFarPoints, f_match.data(), &n),
+              "SearchByProjection(F, vpMapPoints)");
+        return n;
+    }
+
+    /* int SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, const float th,
+     * const bool bMono) (ORBmatcher.cc:2173-2389). */
+    int SearchByProjection(const slam_frame_view& CurrentFrame, const slam_last_frame& LastFrame, float th, bool bMono,
+                           std::vector<int>& f_match) {
+        f_match.assign(CurrentFrame.n, -1);
+        int n = 0;
+        check(slamhot_search_by_projection_last(m_, &CurrentFrame, &LastFrame, nnratio_, check_ori_, th, bMono,
+                                                f_match.data(), &n),
+              "SearchByProjection(F, LastFrame)");
+        return n;
+    }
+
+    /* int SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const set<MapPoint*>&
+     * sAlreadyFound, const float th, const int ORBdist) (ORBmatcher.cc:2391-2513): the KeyFrame's
+     * MapPoints with sAlreadyFound folded into slam_kf_points::use. */
+    int SearchByProjection(const slam_frame_view& CurrentFrame, const slam_kf_points& KF, float th, int ORBdist,
+                           std::vector<int>& f_match) {
+        f_match.assign(CurrentFrame.n, -1);
+        int n = 0;
+        check(slamhot_search_by_projection_kf(m_, &CurrentFrame, &KF, nnratio_, check_ori_, th, ORBdist,
+                                              f_match.data(), &n),
+              "SearchByProjection(F, KF, sAlreadyFound)");
+        return n;
+    }
+
+    /* Tracking::SearchLocalPoints' projection half (Tracking.cc:3213-3258): Frame::isInFrustum
+     * for every local MapPoint and SearchByProjection on the ones in view, one device call.
+     * track (n_mp) receives the isInFrustum records; returns nmatches, *nToMatch as the reference. */
+    int SearchLocalPoints(const slam_frame_view& F, const std::vector<slam_mp_geom>& vpLocalMapPoints,
+                          const uint8_t* mp_desc, float viewCosLimit, float th, bool bFarPoints, float thFarPoints,
+                          std::vector<slam_mp_track>& track, int& nToMatch, std::vector<int>& f_match) {
+        f_match.assign(F.n, -1);
+        track.resize(vpLocalMapPoints.size());
+        int n = 0;
+        check(slamhot_search_local_points(m_, &F, (int)vpLocalMapPoints.size(), vpLocalMapPoints.data(), mp_desc,
+                                          viewCosLimit, nnratio_, th, bFarPoints, thFarPoints, track.data(),
+                                          &nToMatch, f_match.data(), &n),
+              "SearchLocalPoints");
+        return n;
+    }
+
     slam_matcher* handle() { return m_; }
 
    private:
@@ -321,7 +377,116 @@ class LocalBundleAdjuster {
     slam_lba* s_ = nullptr;
 };
 
+/* ------------------------------------------------------------------------------------
+ * Motion-only BA: Optimizer::PoseOptimization (Optimizer.h:52, Optimizer.cc:824-1118).
+ * ---------------------------------------------------------------------------------- */
+class PoseOptimizer {
+   public:
+    explicit PoseOptimizer(int device = 0) { check(slamhot_pose_opt_create(device, &h_), "PoseOptimizer"); }
+    ~PoseOptimizer() { slamhot_pose_opt_destroy(h_); }
+    PoseOptimizer(const PoseOptimizer&) = delete;
+    PoseOptimizer& operator=(const PoseOptimizer&) = delete;
+    /* frames.size() Frames in one launch; results[i].outlier must point at frames[i].n bytes */
+    void Solve(const std::vector<slam_pose_frame>& frames, std::vector<slam_pose_result>& results) {
+        check(slamhot_pose_optimization(h_, (int)frames.size(), frames.data(), results.data()), "PoseOptimization");
+    }
+    slam_pose_opt* handle() { return h_; }
+
+   private:
+    slam_pose_opt* h_ = nullptr;
+};
+
+/* ------------------------------------------------------------------------------------
+ * Frame::ComputeStereoMatches (Frame.h:112, Frame.cc:794-964) on the pyramids the two
+ * extractors hold from their last call.
+ * ---------------------------------------------------------------------------------- */
+class StereoMatcher {
+   public:
+    explicit StereoMatcher(int device = 0) { check(slamhot_stereo_create(device, &h_), "StereoMatcher"); }
+    ~StereoMatcher() { slamhot_stereo_destroy(h_); }
+    StereoMatcher(const StereoMatcher&) = delete;
+    StereoMatcher& operator=(const StereoMatcher&) = delete;
+    void ComputeStereoMatches(ORBextractor& left, ORBextractor& right, const std::vector<KeyPoint>& mvKeys,
+                              const Mat8U& descLeft, const std::vector<KeyPoint>& mvKeysRight, const Mat8U& descRight,
+                              float mbf, float mb, std::vector<float>& mvuRight, std::vector<float>& mvDepth) {
+        mvuRight.assign(mvKeys.size(), -1.f);
+        mvDepth.assign(mvKeys.size(), -1.f);
+        check(slamhot_compute_stereo_matches(h_, left.handle(), right.handle(), (int)mvKeys.size(), mvKeys.data(),
+                                             descLeft.data.data(), (int)mvKeysRight.size(), mvKeysRight.data(),
+                                             descRight.data.data(), mbf, mb, mvuRight.data(), mvDepth.data()),
+              "ComputeStereoMatches");
+    }
+    slam_stereo* handle() { return h_; }
+
+   private:
+    slam_stereo* h_ = nullptr;
+};
+
+/* ------------------------------------------------------------------------------------
+ * LocalMapping's matchers: MapPoint::ComputeDistinctiveDescriptors,
+ * ORBmatcher::SearchForTriangulation_, the search half of ORBmatcher::Fuse.
+ * ---------------------------------------------------------------------------------- */
+class LocalMapper {
+   public:
+    explicit LocalMapper(int device = 0) { check(slamhot_mapper_create(device, &h_), "LocalMapper"); }
+    ~LocalMapper() { slamhot_mapper_destroy(h_); }
+    LocalMapper(const LocalMapper&) = delete;
+    LocalMapper& operator=(const LocalMapper&) = delete;
+
+    /* MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:349-423) for off.size()-1 MapPoints */
+    void ComputeDistinctiveDescriptors(const std::vector<int32_t>& off, const uint8_t* desc, std::vector<int32_t>& best) {
+        const int n = (int)off.size() - 1;
+        best.assign(std::max(n, 0), -1);
+        if (n > 0) check(slamhot_distinctive_descriptors(h_, n, off.data(), desc, best.data()), "ComputeDistinctiveDescriptors");
+    }
+
+    /* ORBmatcher::SearchForTriangulation_ (ORBmatcher.cc:1208-1433) for every pair at once;
+     * vMatchedPairs[p] = (idx1, idx2) in idx1 order, returns the per-pair counts. */
+    std::vector<int32_t> SearchForTriangulation(const std::vector<slam_tri_kf>& kfs, const std::vector<slam_tri_pair>& pairs,
+                                                bool bCheckOri,
+                                                std::vector<std::vector<std::pair<size_t, size_t>>>& vMatchedPairs) {
+        int cap = 1;
+        for (const slam_tri_kf& k : kfs) cap = std::max(cap, k.n);
+        std::vector<int32_t> m12((size_t)pairs.size() * cap), nm(pairs.size(), 0);
+        if (!pairs.empty())
+            check(slamhot_search_for_triangulation(h_, (int)kfs.size(), kfs.data(), (int)pairs.size(), pairs.data(),
+                                                   bCheckOri, cap, m12.data(), nm.data()),
+                  "SearchForTriangulation_");
+        vMatchedPairs.assign(pairs.size(), {});
+        for (size_t p = 0; p < pairs.size(); p++)
+            for (int i = 0; i < kfs[pairs[p].kf1].n; i++)
+                if (m12[p * cap + i] >= 0) vMatchedPairs[p].emplace_back((size_t)i, (size_t)m12[p * cap + i]);
+        return nm;
+    }
+
+    /* search half of int ORBmatcher::Fuse(KeyFrame*, const vector<MapPoint*>&, th, bRight=false)
+     * (ORBmatcher.cc:1629-1788); the caller applies the update half in list order */
+    void FuseSearch(const slam_frame_view& KF, const float* mvInvLevelSigma2, const std::vector<slam_mp_geom>& mps,
+                    const uint8_t* mp_desc, float th, std::vector<int32_t>& best_idx, std::vector<int32_t>& best_dist) {
+        best_idx.assign(mps.size(), -1);
+        best_dist.assign(mps.size(), 256);
+        if (!mps.empty())
+            check(slamhot_fuse_search(h_, &KF, mvInvLevelSigma2, (int)mps.size(), mps.data(), mp_desc, th,
+                                      best_idx.data(), best_dist.data()),
+                  "Fuse");
+    }
+    slam_mapper* handle() { return h_; }
+
+   private:
+    slam_mapper* h_ = nullptr;
+};
+
 namespace Optimizer {
+/* int Optimizer::PoseOptimization(Frame* pFrame): returns nInitialCorrespondences - nBad
+ * (0 below 3 correspondences); pose and mvbOutlier land in `out` (out.outlier -> n bytes). */
+inline int PoseOptimization(PoseOptimizer& solver, const slam_pose_frame& F, slam_pose_result& out) {
+    std::vector<slam_pose_frame> fs{F};
+    std::vector<slam_pose_result> rs{out};
+    solver.Solve(fs, rs);
+    out = rs[0];
+    return out.n_inliers;
+}
+
 /* static void Optimizer::LocalBundleAdjustment(KeyFrame* pKF, bool* pbStopFlag, Map* pMap,
  *     int& num_fixedKF, int& num_OptKF, int& num_MPs, int& num_edges)
  * on a flattened window: the four counters as the reference reports them (:1714-1718,

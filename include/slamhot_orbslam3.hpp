@@ -1,0 +1,549 @@
+/* slamhot_orbslam3.hpp — the drop-in shim bodies, written against the reference's own types.
+ *
+ * Include AFTER OpenCV and the reference's headers (KeyFrame.h, MapPoint.h, Frame.h, Map.h):
+ * every function here is a template over those classes, so the same text is the body of the
+ * replaced reference function (the shims of INTEGRATION.md call these) and compiles in this
+ * repo's tests against minimal stand-ins (tests/cpp/orbslam3_standins.hpp) that carry exactly
+ * the members used here.  Each shim keeps the reference's control flow and map bookkeeping on
+ * the host and hands the data-parallel work to libslamhot.so through include/slamhot.hpp.
+ *
+ *   ORBextractorCall          ORBextractor::operator()                 ORBextractor.cc:1068-1150
+ *   SearchByBoW               ORBmatcher::SearchByBoW(KeyFrame*, Frame&) ORBmatcher.cc:269-471
+ *   SearchLocalPoints         Tracking::SearchLocalPoints (2nd half)     Tracking.cc:3213-3258
+ *   PoseOptimization          Optimizer::PoseOptimization(Frame*)      Optimizer.cc:824-1118
+ *   ComputeStereoMatches      Frame::ComputeStereoMatches              Frame.cc:794-964
+ *   BuildLocalWindow          Optimizer::LocalBundleAdjustment window  Optimizer.cc:1613-1718
+ *   FlattenLocalWindow        its vertex / edge setup                  Optimizer.cc:1737-1918
+ *   LocalBundleAdjustment     the whole function incl. write-back      Optimizer.cc:1611-2078
+ *   Fuse                      ORBmatcher::Fuse(KeyFrame*, vector<MapPoint*>, th, false)  ORBmatcher.cc:1629-1818
+ *
+ * One header addition on the reference side: MapPoint gains the getters GetMinDistance() /
+ * GetMaxDistance() (mfMinDistance / mfMaxDistance under mMutexPos).  The kernels need the raw
+ * values (PredictScale divides mfMaxDistance, MapPoint.cc:551-566); the reference only exposes
+ * them multiplied by 0.8f / 1.2f, which cannot be undone exactly in float.
+ */
+#ifndef SLAMHOT_ORBSLAM3_HPP
+#define SLAMHOT_ORBSLAM3_HPP
+
+#include <cmath>
+#include <list>
+#include <map>
+#include <mutex>
+#include <set>
+#include <tuple>
+#include <utility>
+#include <vector>
+
+#include "slamhot.hpp"
+
+namespace slamhot {
+namespace orbslam3 {
+
+static_assert(sizeof(cv::KeyPoint) == sizeof(slam_keypoint), "cv::KeyPoint is the 28-byte slam_keypoint");
+
+inline const slam_keypoint* kp_ptr(const std::vector<cv::KeyPoint>& v) {
+    return reinterpret_cast<const slam_keypoint*>(v.data());
+}
+
+inline void mat4(const cv::Mat& T, float* out) {  // a 4x4 CV_32F pose, row-major
+    for (int r = 0; r < 4; r++)
+        for (int c = 0; c < 4; c++) out[4 * r + c] = T.template at<float>(r, c);
+}
+
+inline cv::Mat mat_from(const float* p, int rows, int cols) {
+    cv::Mat m(rows, cols, CV_32F);
+    for (int r = 0; r < rows; r++)
+        for (int c = 0; c < cols; c++) m.template at<float>(r, c) = p[r * cols + c];
+    return m;
+}
+
+/* ------------------------------------------------------------------ ORBextractor::operator()
+ * int operator()(InputArray image, InputArray mask, vector<KeyPoint>& keypoints,
+ *                OutputArray descriptors, vector<int>& vLappingArea)   (ORBextractor.cc:1068-1150)
+ * `hot` is the slamhot extractor the reference ORBextractor owns; mvImagePyramid is refreshed
+ * when the caller reads it (stereo matching on the device does not need it). */
+inline int ORBextractorCall(ORBextractor& hot, const cv::Mat& image, std::vector<cv::KeyPoint>& keypoints,
+                            cv::Mat& descriptors, const std::vector<int>& vLappingArea,
+                            std::vector<cv::Mat>* mvImagePyramid = nullptr) {
+    if (image.empty()) return -1;  // ORBextractor.cc:1072-1073
+    GrayImage g;
+    g.data = image.data;
+    g.cols = image.cols;
+    g.rows = image.rows;
+    g.step = image.step;
+    std::vector<KeyPoint> kps;
+    Mat8U desc;
+    const int mono = hot(g, kps, desc, vLappingArea);
+    keypoints.resize(kps.size());
+    std::memcpy(static_cast<void*>(keypoints.data()), kps.data(), kps.size() * sizeof(slam_keypoint));
+    descriptors.create((int)kps.size(), 32, CV_8U);
+    if (!kps.empty()) std::memcpy(descriptors.data, desc.data.data(), desc.data.size());
+    if (mvImagePyramid) {
+        const std::vector<Mat8U> pyr = hot.mvImagePyramid();
+        mvImagePyramid->resize(pyr.size());
+        for (size_t l = 0; l < pyr.size(); l++) {
+            (*mvImagePyramid)[l].create(pyr[l].rows, pyr[l].cols, CV_8U);
+            std::memcpy((*mvImagePyramid)[l].data, pyr[l].data.data(), pyr[l].data.size());
+        }
+    }
+    return mono;
+}
+
+/* DBoW2::FeatureVector (std::map<NodeId, vector<unsigned>>, ascending node id) as the CSR of
+ * slam_bow_side; the arrays live in `store`. */
+struct BowStore {
+    std::vector<uint32_t> node_id, node_feat;
+    std::vector<int32_t> node_off;
+    std::vector<float> angle;
+    std::vector<uint8_t> valid;
+};
+
+template <class FeatVec>
+slam_bow_side bow_side(const FeatVec& fv, const cv::Mat& desc, const std::vector<cv::KeyPoint>& kps, BowStore& st) {
+    st.node_id.clear();
+    st.node_feat.clear();
+    st.node_off.assign(1, 0);
+    for (const auto& kv : fv) {
+        st.node_id.push_back((uint32_t)kv.first);
+        for (unsigned f : kv.second) st.node_feat.push_back(f);
+        st.node_off.push_back((int32_t)st.node_feat.size());
+    }
+    st.angle.resize(kps.size());
+    for (size_t i = 0; i < kps.size(); i++) st.angle[i] = kps[i].angle;
+    slam_bow_side s{};
+    s.n = (int32_t)kps.size();
+    s.desc = desc.data;
+    s.angle = st.angle.data();
+    s.valid = nullptr;
+    s.n_nodes = (int32_t)st.node_id.size();
+    s.node_id = st.node_id.data();
+    s.node_off = st.node_off.data();
+    s.node_feat = st.node_feat.data();
+    return s;
+}
+
+/* ------------------------------------------------------------------ ORBmatcher::SearchByBoW
+ * int SearchByBoW(KeyFrame* pKF, Frame& F, vector<MapPoint*>& vpMapPointMatches)
+ * (ORBmatcher.cc:269-471) */
+template <class KeyFrame, class Frame, class MapPoint>
+int SearchByBoW(slamhot::ORBmatcher& hot, KeyFrame* pKF, Frame& F, std::vector<MapPoint*>& vpMapPointMatches) {
+    const std::vector<MapPoint*> vpMapPointsKF = pKF->GetMapPointMatches();
+    vpMapPointMatches = std::vector<MapPoint*>(F.N, static_cast<MapPoint*>(nullptr));
+    BowStore sa, sb;
+    KeyFrameBow A;
+    FrameBow B;
+    static_cast<slam_bow_side&>(A) = bow_side(pKF->mFeatVec, pKF->mDescriptors, pKF->mvKeysUn, sa);
+    static_cast<slam_bow_side&>(B) = bow_side(F.mFeatVec, F.mDescriptors, F.mvKeysUn, sb);
+    sa.valid.resize(vpMapPointsKF.size());
+    for (size_t i = 0; i < vpMapPointsKF.size(); i++)  // pMP && !pMP->isBad() (:321-327)
+        sa.valid[i] = vpMapPointsKF[i] && !vpMapPointsKF[i]->isBad();
+    A.valid = sa.valid.data();
+    std::vector<int> idx;
+    const int n = hot.SearchByBoW(A, B, idx);
+    for (int j = 0; j < F.N; j++)
+        if (idx[j] >= 0) vpMapPointMatches[j] = vpMapPointsKF[idx[j]];
+    return n;
+}
+
+/* The matcher-facing view of a Frame (grid bounds and scale tables are Frame statics / members). */
+template <class Frame>
+slam_frame_view frame_view(Frame& F, std::vector<int8_t>& mp_state, float* Tcw16) {
+    slam_frame_view v{};
+    v.n = F.N;
+    v.kps_un = kp_ptr(F.mvKeysUn);
+    v.uright = F.mvuRight.data();
+    v.desc = F.mDescriptors.data;
+    mp_state.assign(F.N, -1);
+    for (int i = 0; i < F.N; i++)
+        if (F.mvpMapPoints[i]) mp_state[i] = F.mvpMapPoints[i]->Observations() > 0 ? 1 : 0;
+    v.mp_state = mp_state.data();
+    v.min_x = Frame::mnMinX;
+    v.min_y = Frame::mnMinY;
+    v.max_x = Frame::mnMaxX;
+    v.max_y = Frame::mnMaxY;
+    v.grid_inv_w = Frame::mfGridElementWidthInv;
+    v.grid_inv_h = Frame::mfGridElementHeightInv;
+    v.nlevels = F.mnScaleLevels;
+    v.scale = F.mvScaleFactors.data();
+    v.log_scale = F.mfLogScaleFactor;
+    v.fx = F.fx;
+    v.fy = F.fy;
+    v.cx = F.cx;
+    v.cy = F.cy;
+    v.bf = F.mbf;
+    v.b = F.mb;
+    mat4(F.mTcw, Tcw16);
+    v.Tcw = Tcw16;
+    return v;
+}
+
+/* ------------------------------------------------------------------ Tracking::SearchLocalPoints
+ * The projection half (Tracking.cc:3213-3258) for a Frame with Nleft == -1: isInFrustum of every
+ * local MapPoint not already seen by this frame and SearchByProjection(F, vpLocalMapPoints, th,
+ * bFarPoints, thFarPoints), one device call; the tracking fields isInFrustum leaves are written
+ * back into the MapPoints and the matches into F.mvpMapPoints.  Returns nToMatch. */
+template <class Frame, class MapPoint>
+int SearchLocalPoints(slamhot::ORBmatcher& hot, Frame& F, std::vector<MapPoint*>& vpLocalMapPoints, float th,
+                      bool bFarPoints, float thFarPoints, int* nmatches = nullptr) {
+    std::vector<slam_mp_geom> G(vpLocalMapPoints.size());
+    std::vector<uint8_t> D(32 * G.size());
+    for (size_t i = 0; i < G.size(); i++) {
+        MapPoint* pMP = vpLocalMapPoints[i];
+        slam_mp_geom& g = G[i];
+        g.seen = pMP->mnLastFrameSeen == F.mnId;
+        g.is_bad = pMP->isBad();
+        g.has_obs = pMP->Observations() > 0;
+        const cv::Mat P = pMP->GetWorldPos(), nrm = pMP->GetNormal(), d = pMP->GetDescriptor();
+        for (int k = 0; k < 3; k++) {
+            g.pos[k] = P.template at<float>(k);
+            g.normal[k] = nrm.template at<float>(k);
+        }
+        g.min_dist = pMP->GetMinDistance();  // raw mfMinDistance / mfMaxDistance: the kernels apply the
+        g.max_dist = pMP->GetMaxDistance();  // 0.8f / 1.2f invariance factors and PredictScale themselves
+        std::memcpy(&D[32 * i], d.data, 32);
+    }
+    std::vector<int8_t> st;
+    float T[16];
+    slam_frame_view v = frame_view(F, st, T);
+    std::vector<slam_mp_track> track;
+    std::vector<int> f_match;
+    int nToMatch = 0;
+    const int n = hot.SearchLocalPoints(v, G, D.data(), 0.5f, th, bFarPoints, thFarPoints, track, nToMatch, f_match);
+    for (size_t i = 0; i < G.size(); i++) {
+        MapPoint* pMP = vpLocalMapPoints[i];
+        if (G[i].seen || G[i].is_bad) continue;
+        const slam_mp_track& t = track[i];
+        pMP->mbTrackInView = t.in_view;
+        if (t.in_view) {
+            pMP->IncreaseVisible();
+            pMP->mTrackProjX = t.proj_x;
+            pMP->mTrackProjY = t.proj_y;
+            pMP->mTrackProjXR = t.proj_xr;
+            pMP->mnTrackScaleLevel = t.scale_level;
+            pMP->mTrackViewCos = t.view_cos;
+            pMP->mTrackDepth = t.depth;
+        }
+    }
+    for (int i = 0; i < F.N; i++)
+        if (f_match[i] >= 0) F.mvpMapPoints[i] = vpLocalMapPoints[f_match[i]];
+    if (nmatches) *nmatches = n;
+    return nToMatch;
+}
+
+/* ------------------------------------------------------------------ Optimizer::PoseOptimization
+ * int PoseOptimization(Frame* pFrame) (Optimizer.cc:824-1118), pinhole. */
+template <class Frame>
+int PoseOptimization(slamhot::PoseOptimizer& hot, Frame* pFrame) {
+    const int N = pFrame->N;
+    std::vector<uint8_t> has_mp(N), outl(N, 0);
+    std::vector<float> mp_pos(3 * (size_t)N, 0.f);
+    for (int i = 0; i < N; i++) {  // under MapPoint::mGlobalMutex in the reference (:861)
+        auto* pMP = pFrame->mvpMapPoints[i];
+        has_mp[i] = pMP != nullptr;
+        if (pMP) {
+            const cv::Mat X = pMP->GetWorldPos();
+            for (int k = 0; k < 3; k++) mp_pos[3 * i + k] = X.template at<float>(k);
+        }
+    }
+    slam_pose_frame F{};
+    mat4(pFrame->mTcw, F.Tcw);
+    F.n = N;
+    F.kps_un = kp_ptr(pFrame->mvKeysUn);
+    F.uright = pFrame->mvuRight.data();
+    F.has_mp = has_mp.data();
+    F.mp_pos = mp_pos.data();
+    F.inv_sigma2 = pFrame->mvInvLevelSigma2.data();
+    F.nlevels = (int)pFrame->mvInvLevelSigma2.size();
+    F.cam = slam_camera{pFrame->fx, pFrame->fy, pFrame->cx, pFrame->cy, pFrame->mbf};
+    slam_pose_result R{};
+    R.outlier = outl.data();
+    const int n = slamhot::Optimizer::PoseOptimization(hot, F, R);
+    if (R.n_initial < 3) return 0;  // Optimizer.cc:1012-1013: pose and flags untouched
+    for (int i = 0; i < N; i++)
+        if (has_mp[i]) pFrame->mvbOutlier[i] = outl[i] != 0;
+    pFrame->SetPose(mat_from(R.Tcw, 4, 4));
+    return n;
+}
+
+/* ------------------------------------------------------------------ Frame::ComputeStereoMatches
+ * (Frame.cc:794-964) right after the stereo Frame constructor's two extractions. */
+template <class Frame>
+void ComputeStereoMatches(slamhot::StereoMatcher& hot, ORBextractor& left, ORBextractor& right, Frame& F) {
+    Mat8U dl, dr;
+    dl.rows = F.mDescriptors.rows;
+    dl.cols = 32;
+    dl.data.assign(F.mDescriptors.data, F.mDescriptors.data + (size_t)dl.rows * 32);
+    dr.rows = F.mDescriptorsRight.rows;
+    dr.cols = 32;
+    dr.data.assign(F.mDescriptorsRight.data, F.mDescriptorsRight.data + (size_t)dr.rows * 32);
+    std::vector<KeyPoint> kl(F.mvKeys.size()), kr(F.mvKeysRight.size());
+    std::memcpy(kl.data(), F.mvKeys.data(), kl.size() * sizeof(slam_keypoint));
+    std::memcpy(kr.data(), F.mvKeysRight.data(), kr.size() * sizeof(slam_keypoint));
+    hot.ComputeStereoMatches(left, right, kl, dl, kr, dr, F.mbf, F.mb, F.mvuRight, F.mvDepth);
+}
+
+/* ------------------------------------------------------------------ Optimizer::LocalBundleAdjustment */
+template <class KeyFrame, class MapPoint>
+struct LocalWindow {
+    std::list<KeyFrame*> lLocalKeyFrames, lFixedCameras;
+    std::list<MapPoint*> lLocalMapPoints;
+    int num_fixedKF = 0;
+};
+
+/* Optimizer.cc:1613-1718.  Returns false where the reference returns (no fixed KeyFrame).  One
+ * deviation: the "< 2 fixed" fallback pushes the reference's uninitialised pLowerKf /
+ * pSecondLowerKF when no candidate exists (undefined behaviour); here they are skipped. */
+template <class KeyFrame, class MapPoint, class Map>
+bool BuildLocalWindow(KeyFrame* pKF, Map* pMap, LocalWindow<KeyFrame, MapPoint>& W) {
+    W.lLocalKeyFrames.push_back(pKF);
+    pKF->mnBALocalForKF = pKF->mnId;
+    Map* pCurrentMap = pKF->GetMap();
+    const std::vector<KeyFrame*> vNeighKFs = pKF->GetVectorCovisibleKeyFrames();
+    for (KeyFrame* pKFi : vNeighKFs) {
+        pKFi->mnBALocalForKF = pKF->mnId;
+        if (!pKFi->isBad() && pKFi->GetMap() == pCurrentMap) W.lLocalKeyFrames.push_back(pKFi);
+    }
+    W.num_fixedKF = 0;
+    for (KeyFrame* pKFi : W.lLocalKeyFrames) {
+        if (pKFi->mnId == pMap->GetInitKFid()) W.num_fixedKF = 1;
+        for (MapPoint* pMP : pKFi->GetMapPointMatches())
+            if (pMP && !pMP->isBad() && pMP->GetMap() == pCurrentMap && pMP->mnBALocalForKF != pKF->mnId) {
+                W.lLocalMapPoints.push_back(pMP);
+                pMP->mnBALocalForKF = pKF->mnId;
+            }
+    }
+    for (MapPoint* pMP : W.lLocalMapPoints) {
+        const auto observations = pMP->GetObservations();
+        for (const auto& ob : observations) {
+            KeyFrame* pKFi = ob.first;
+            if (pKFi->mnBALocalForKF != pKF->mnId && pKFi->mnBAFixedForKF != pKF->mnId) {
+                pKFi->mnBAFixedForKF = pKF->mnId;
+                if (!pKFi->isBad() && pKFi->GetMap() == pCurrentMap) W.lFixedCameras.push_back(pKFi);
+            }
+        }
+    }
+    W.num_fixedKF += (int)W.lFixedCameras.size();
+    if (W.num_fixedKF < 2) {
+        long lowerId = (long)pKF->mnId, secondLowerId = (long)pKF->mnId;
+        KeyFrame *pLowerKf = nullptr, *pSecondLowerKF = nullptr;
+        for (KeyFrame* pKFi : W.lLocalKeyFrames) {
+            if (pKFi == pKF || pKFi->mnId == pMap->GetInitKFid()) continue;
+            if ((long)pKFi->mnId < lowerId) {
+                lowerId = (long)pKFi->mnId;
+                pLowerKf = pKFi;
+            } else if ((long)pKFi->mnId < secondLowerId) {
+                secondLowerId = (long)pKFi->mnId;
+                pSecondLowerKF = pKFi;
+            }
+        }
+        if (pLowerKf) {
+            W.lFixedCameras.push_back(pLowerKf);
+            W.lLocalKeyFrames.remove(pLowerKf);
+            W.num_fixedKF++;
+        }
+        if (W.num_fixedKF < 2 && pSecondLowerKF) {
+            W.lFixedCameras.push_back(pSecondLowerKF);
+            W.lLocalKeyFrames.remove(pSecondLowerKF);
+            W.num_fixedKF++;
+        }
+    }
+    return W.num_fixedKF != 0;
+}
+
+/* The vertex / edge setup (Optimizer.cc:1737-1918) as slam_lba_problem arrays: KeyFrames in
+ * vertex-id (mnId) order, MapPoints in lLocalMapPoints order, per MapPoint its observations in
+ * the observation map's order — the left (mono / stereo) edge, then the right-camera body edge
+ * for KeyFrames with mpCamera2.  edge_refs[e] = the (KeyFrame, MapPoint) vToErase would name. */
+template <class KeyFrame, class MapPoint, class Map>
+void FlattenLocalWindow(const LocalWindow<KeyFrame, MapPoint>& W, Map* pMap, LocalBAWindow& out,
+                        std::vector<KeyFrame*>& kfs, std::vector<std::pair<KeyFrame*, MapPoint*>>& edge_refs) {
+    kfs.assign(W.lLocalKeyFrames.begin(), W.lLocalKeyFrames.end());
+    kfs.insert(kfs.end(), W.lFixedCameras.begin(), W.lFixedCameras.end());
+    std::stable_sort(kfs.begin(), kfs.end(), [](KeyFrame* a, KeyFrame* b) { return a->mnId < b->mnId; });
+    std::map<KeyFrame*, int> index;
+    const std::set<KeyFrame*> fixed(W.lFixedCameras.begin(), W.lFixedCameras.end());
+    out = LocalBAWindow{};
+    bool rig = false;
+    for (size_t k = 0; k < kfs.size(); k++) {
+        KeyFrame* pKFi = kfs[k];
+        index[pKFi] = (int)k;
+        float T[16];
+        mat4(pKFi->GetPose(), T);
+        out.kf_Tcw.insert(out.kf_Tcw.end(), T, T + 16);
+        out.kf_fixed.push_back(fixed.count(pKFi) ? 2 : (pKFi->mnId == pMap->GetInitKFid() ? 1 : 0));  // :1741-1744
+        rig = rig || pKFi->mpCamera2 != nullptr;
+    }
+    if (rig) {
+        for (KeyFrame* pKFi : kfs) {
+            float T[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+            if (pKFi->mpCamera2) mat4(pKFi->mTrl, T);
+            out.kf_Trl.insert(out.kf_Trl.end(), T, T + 16);
+        }
+    }
+    Map* pCurrentMap = W.lLocalKeyFrames.empty() ? nullptr : W.lLocalKeyFrames.front()->GetMap();
+    int pi = 0;
+    for (MapPoint* pMP : W.lLocalMapPoints) {
+        const cv::Mat P = pMP->GetWorldPos();
+        for (int c = 0; c < 3; c++) out.pt_pos.push_back(P.template at<float>(c));
+        const auto observations = pMP->GetObservations();
+        for (const auto& ob : observations) {
+            KeyFrame* pKFi = ob.first;
+            if (pKFi->isBad() || pKFi->GetMap() != pCurrentMap) continue;
+            auto it = index.find(pKFi);
+            if (it == index.end()) continue;
+            const int leftIndex = std::get<0>(ob.second);
+            if (leftIndex != -1) {  // mono (:1819-1849) or stereo (:1850-1880)
+                const cv::KeyPoint& kpUn = pKFi->mvKeysUn[leftIndex];
+                const float ur = pKFi->mvuRight[leftIndex];
+                out.edge_pt.push_back(pi);
+                out.edge_kf.push_back(it->second);
+                out.edge_obs.push_back(kpUn.pt.x);
+                out.edge_obs.push_back(kpUn.pt.y);
+                out.edge_obs.push_back(ur < 0 ? -1.f : ur);
+                out.edge_inv_sigma2.push_back(pKFi->mvInvLevelSigma2[kpUn.octave]);
+                if (rig) out.edge_body.push_back(0);
+                edge_refs.emplace_back(pKFi, pMP);
+            }
+            if (pKFi->mpCamera2) {  // EdgeSE3ProjectXYZToBody (:1883-1914)
+                int rightIndex = std::get<1>(ob.second);
+                if (rightIndex != -1) {
+                    rightIndex -= pKFi->NLeft;
+                    const cv::KeyPoint& kp = pKFi->mvKeysRight[rightIndex];
+                    out.edge_pt.push_back(pi);
+                    out.edge_kf.push_back(it->second);
+                    out.edge_obs.push_back(kp.pt.x);
+                    out.edge_obs.push_back(kp.pt.y);
+                    out.edge_obs.push_back(-1.f);
+                    out.edge_inv_sigma2.push_back(pKFi->mvInvLevelSigma2[kp.octave]);
+                    out.edge_body.push_back(1);
+                    edge_refs.emplace_back(pKFi, pMP);
+                }
+            }
+        }
+        pi++;
+    }
+    KeyFrame* k0 = kfs.front();
+    out.cam = slam_camera{k0->fx, k0->fy, k0->cx, k0->cy, k0->mbf};
+    for (KeyFrame* pKFi : kfs)
+        if (pKFi->mpCamera2) {
+            auto* c2 = pKFi->mpCamera2;  // GeometricCamera::getParameter (GeometricCamera.h:70)
+            out.cam2 = slam_camera{c2->getParameter(0), c2->getParameter(1), c2->getParameter(2), c2->getParameter(3),
+                                   0.f};
+            break;
+        }
+    out.inertial = pMap->IsInertial();
+}
+
+/* static void Optimizer::LocalBundleAdjustment(KeyFrame* pKF, bool* pbStopFlag, Map* pMap,
+ *     int& num_fixedKF, int& num_OptKF, int& num_MPs, int& num_edges)  (Optimizer.cc:1611-2078) */
+template <class KeyFrame, class MapPoint, class Map>
+void LocalBundleAdjustment(LocalBundleAdjuster& hot, KeyFrame* pKF, bool* pbStopFlag, Map* pMap, int& num_fixedKF,
+                           int& num_OptKF, int& num_MPs, int& num_edges) {
+    LocalWindow<KeyFrame, MapPoint> W;
+    const bool ok = BuildLocalWindow(pKF, pMap, W);
+    num_fixedKF = W.num_fixedKF;
+    num_MPs = (int)W.lLocalMapPoints.size();
+    if (!ok) return;  // :1714-1718
+    num_OptKF = (int)W.lLocalKeyFrames.size();
+    LocalBAWindow flat;
+    std::vector<KeyFrame*> kfs;
+    std::vector<std::pair<KeyFrame*, MapPoint*>> edge_refs;
+    FlattenLocalWindow(W, pMap, flat, kfs, edge_refs);
+    num_edges = flat.n_edge();
+    if (pbStopFlag && *pbStopFlag) return;  // :1921-1923
+    std::vector<LocalBAResult> res;
+    hot.Solve({flat}, pbStopFlag, res);  // optimize(5), stop check, optimize(10), outlier scan
+    const LocalBAResult& R = res[0];
+    std::unique_lock<std::mutex> lock(pMap->mMutexMapUpdate);  // :2040
+    for (size_t e = 0; e < edge_refs.size(); e++)           // vToErase (:2043-2052)
+        if (R.edge_outlier[e] && !edge_refs[e].second->isBad()) {
+            edge_refs[e].first->EraseMapPointMatch(edge_refs[e].second);
+            edge_refs[e].second->EraseObservation(edge_refs[e].first);
+        }
+    const std::set<KeyFrame*> local(W.lLocalKeyFrames.begin(), W.lLocalKeyFrames.end());
+    for (size_t k = 0; k < kfs.size(); k++)                 // :2056-2063
+        if (local.count(kfs[k])) kfs[k]->SetPose(mat_from(&R.kf_Tcw[16 * k], 4, 4));
+    int i = 0;
+    for (MapPoint* pMP : W.lLocalMapPoints) {               // :2066-2074
+        pMP->SetWorldPos(mat_from(&R.pt_pos[3 * (size_t)i++], 3, 1));
+        pMP->UpdateNormalAndDepth();
+    }
+    pMap->IncreaseChangeIndex();
+}
+
+/* ------------------------------------------------------------------ ORBmatcher::Fuse
+ * int Fuse(KeyFrame* pKF, const vector<MapPoint*>& vpMapPoints, const float th, const bool bRight)
+ * for bRight == false (ORBmatcher.cc:1629-1818): the search half on the device, the update half
+ * here in list order (its skip checks are re-evaluated: earlier updates can change them). */
+template <class KeyFrame, class MapPoint>
+int Fuse(LocalMapper& hot, KeyFrame* pKF, const std::vector<MapPoint*>& vpMapPoints, float th) {
+    const int n = (int)vpMapPoints.size();
+    std::vector<slam_mp_geom> G(n);
+    std::vector<uint8_t> D(32 * (size_t)n, 0);
+    for (int i = 0; i < n; i++) {
+        MapPoint* pMP = vpMapPoints[i];
+        slam_mp_geom& g = G[i];
+        g.is_bad = !pMP || pMP->isBad();
+        g.seen = pMP && pMP->IsInKeyFrame(pKF);
+        if (!pMP) continue;
+        const cv::Mat P = pMP->GetWorldPos(), nrm = pMP->GetNormal(), d = pMP->GetDescriptor();
+        for (int k = 0; k < 3; k++) {
+            g.pos[k] = P.template at<float>(k);
+            g.normal[k] = nrm.template at<float>(k);
+        }
+        g.min_dist = pMP->GetMinDistance();  // raw mfMinDistance / mfMaxDistance: the kernels apply the
+        g.max_dist = pMP->GetMaxDistance();  // 0.8f / 1.2f invariance factors and PredictScale themselves
+        g.has_obs = pMP->Observations() > 0;
+        std::memcpy(&D[32 * (size_t)i], d.data, 32);
+    }
+    slam_frame_view v{};
+    v.n = pKF->N;
+    v.kps_un = kp_ptr(pKF->mvKeysUn);
+    v.uright = pKF->mvuRight.data();
+    v.desc = pKF->mDescriptors.data;
+    v.min_x = (float)pKF->mnMinX;
+    v.min_y = (float)pKF->mnMinY;
+    v.max_x = (float)pKF->mnMaxX;
+    v.max_y = (float)pKF->mnMaxY;
+    v.grid_inv_w = pKF->mfGridElementWidthInv;
+    v.grid_inv_h = pKF->mfGridElementHeightInv;
+    v.nlevels = pKF->mnScaleLevels;
+    v.scale = pKF->mvScaleFactors.data();
+    v.log_scale = pKF->mfLogScaleFactor;
+    v.fx = pKF->fx;
+    v.fy = pKF->fy;
+    v.cx = pKF->cx;
+    v.cy = pKF->cy;
+    v.bf = pKF->mbf;
+    v.b = pKF->mb;
+    float T[16];
+    mat4(pKF->GetPose(), T);
+    v.Tcw = T;
+    std::vector<int32_t> bi, bd;
+    hot.FuseSearch(v, pKF->mvInvLevelSigma2.data(), G, D.data(), th, bi, bd);
+    int nFused = 0;
+    for (int i = 0; i < n; i++) {  // :1789-1816
+        MapPoint* pMP = vpMapPoints[i];
+        if (!pMP || pMP->isBad() || pMP->IsInKeyFrame(pKF)) continue;
+        if (bd[i] > ORBmatcher::TH_LOW) continue;
+        MapPoint* pMPinKF = pKF->GetMapPoint(bi[i]);
+        if (pMPinKF) {
+            if (!pMPinKF->isBad()) {
+                if (pMPinKF->Observations() > pMP->Observations())
+                    pMP->Replace(pMPinKF);
+                else
+                    pMPinKF->Replace(pMP);
+            }
+        } else {
+            pMP->AddObservation(pKF, bi[i]);
+            pKF->AddMapPoint(pMP, bi[i]);
+        }
+        nFused++;
+    }
+    return nFused;
+}
+
+}  // namespace orbslam3
+}  // namespace slamhot
+
+#endif  // SLAMHOT_ORBSLAM3_HPP

@@ -264,8 +264,8 @@ using namespace slamhot;
 struct slam_stereo {
     int device = 0;
     hipStream_t stream = nullptr;
-    void *d_rowoff = nullptr, *d_ent = nullptr, *d_sad = nullptr;
-    size_t cap_rowoff = 0, cap_ent = 0, cap_sad = 0;
+    void *d_rowoff = nullptr, *d_ent = nullptr, *d_sad = nullptr, *d_io = nullptr;
+    size_t cap_rowoff = 0, cap_ent = 0, cap_sad = 0, cap_io = 0;
 };
 
 namespace {
@@ -303,7 +303,7 @@ void slamhot_stereo_destroy(slam_stereo* st) {
     if (!st) return;
     (void)hipSetDevice(st->device);
     if (st->stream) (void)hipStreamSynchronize(st->stream);
-    for (void* p : {st->d_rowoff, st->d_ent, st->d_sad})
+    for (void* p : {st->d_rowoff, st->d_ent, st->d_sad, st->d_io})
         if (p) (void)hipFree(p);
     if (st->stream) (void)hipStreamDestroy(st->stream);
     delete st;
@@ -383,6 +383,43 @@ slam_status slamhot_stereo_match_batch_device(slam_stereo* st, slam_extractor* l
     hipLaunchKernelGGL(k_stereo_median, dim3(nframes), dim3(kMedianThreads), 0, strm, cap,
                        (const int32_t*)d_n_left, (const int32_t*)sad, (float*)d_uright, (float*)d_depth);
     SLAM_HIP_TRY(hipGetLastError());
+    return SLAM_OK;
+}
+
+slam_status slamhot_compute_stereo_matches(slam_stereo* st, slam_extractor* left, slam_extractor* right, int n_left,
+                                           const slam_keypoint* kps_left, const uint8_t* desc_left, int n_right,
+                                           const slam_keypoint* kps_right, const uint8_t* desc_right, float mbf,
+                                           float mb, float* uright, float* depth) {
+    if (!st || !left || !right || n_left < 0 || n_right < 0 || (n_left && (!kps_left || !desc_left || !uright ||
+                                                                             !depth)) ||
+        (n_right && (!kps_right || !desc_right)))
+        return SLAM_EINVAL;
+    if (n_left == 0) return SLAM_OK;
+    const int cap = std::max(std::max(n_left, n_right), 1);
+    if (cap > kStMaxSort) return SLAM_EINVAL;
+    // one upload: [n_l, n_r | kps L | kps R | desc L | desc R | uright | depth], cap rows each
+    const size_t kb = (size_t)cap * sizeof(slam_keypoint), db = (size_t)cap * 32, fb = (size_t)cap * 4;
+    const size_t o_kl = 256, o_kr = o_kl + kb, o_dl = o_kr + kb, o_dr = o_dl + db, o_ur = o_dr + db, o_dp = o_ur + fb;
+    (void)hipSetDevice(st->device);
+    slam_status s;
+    if ((s = grow(&st->d_io, &st->cap_io, o_dp + fb))) return s;
+    uint8_t* b = (uint8_t*)st->d_io;
+    const int32_t ns[2] = {n_left, n_right};
+    hipStream_t S = st->stream;
+    SLAM_HIP_TRY(hipMemcpyAsync(b, ns, sizeof(ns), hipMemcpyHostToDevice, S));
+    SLAM_HIP_TRY(hipMemcpyAsync(b + o_kl, kps_left, (size_t)n_left * sizeof(slam_keypoint), hipMemcpyHostToDevice, S));
+    SLAM_HIP_TRY(hipMemcpyAsync(b + o_dl, desc_left, (size_t)n_left * 32, hipMemcpyHostToDevice, S));
+    if (n_right) {
+        SLAM_HIP_TRY(hipMemcpyAsync(b + o_kr, kps_right, (size_t)n_right * sizeof(slam_keypoint), hipMemcpyHostToDevice,
+                                    S));
+        SLAM_HIP_TRY(hipMemcpyAsync(b + o_dr, desc_right, (size_t)n_right * 32, hipMemcpyHostToDevice, S));
+    }
+    s = slamhot_stereo_match_batch_device(st, left, right, 1, b + o_kl, b + o_dl, b, b + o_kr, b + o_dr, b + 4, cap,
+                                          mbf, mb, b + o_ur, b + o_dp, nullptr, S);
+    if (s != SLAM_OK) return s;
+    SLAM_HIP_TRY(hipMemcpyAsync(uright, b + o_ur, (size_t)n_left * 4, hipMemcpyDeviceToHost, S));
+    SLAM_HIP_TRY(hipMemcpyAsync(depth, b + o_dp, (size_t)n_left * 4, hipMemcpyDeviceToHost, S));
+    SLAM_HIP_TRY(hipStreamSynchronize(S));
     return SLAM_OK;
 }
 

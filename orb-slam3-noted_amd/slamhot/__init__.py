@@ -758,6 +758,24 @@ class StereoMatcher:
                                                      P(stream) if stream else None)
         check(st, "slamhot_stereo_match_batch_device")
 
+    def compute(self, left: ORBextractor, right: ORBextractor, kps_l, desc_l, kps_r, desc_r, mbf: float, mb: float):
+        """Frame::ComputeStereoMatches on host arrays after one host extraction on each handle
+        (slamhot_compute_stereo_matches): returns (mvuRight, mvDepth)."""
+        L = lib()
+        if not getattr(L, "_stereo_host_ready", False):
+            L.slamhot_compute_stereo_matches.argtypes = [P, P, P, I, P, P, I, P, P, C.c_float, C.c_float, P, P]
+            L._stereo_host_ready = True
+        kl = np.ascontiguousarray(kps_l, KP_DTYPE)
+        kr = np.ascontiguousarray(kps_r, KP_DTYPE)
+        dl = np.ascontiguousarray(desc_l, np.uint8)
+        dr = np.ascontiguousarray(desc_r, np.uint8)
+        ur = np.full(len(kl), -1.0, np.float32)
+        dep = np.full(len(kl), -1.0, np.float32)
+        check(L.slamhot_compute_stereo_matches(self._h, left._h, right._h, len(kl), _ptr(kl), _ptr(dl), len(kr),
+                                               _ptr(kr), _ptr(dr), mbf, mb, _ptr(ur), _ptr(dep)),
+              "slamhot_compute_stereo_matches")
+        return ur, dep
+
 
 def ComputeStereoMatches(left: ORBextractor, right: ORBextractor, images_left, images_right, mbf: float, mb: float,
                          matcher: StereoMatcher | None = None):

@@ -112,6 +112,18 @@ class KeyFrame:
         self.covisible: list = []            # GetVectorCovisibleKeyFrames order
         self.mnBALocalForKF = -1
         self.mnBAFixedForKF = -1
+        # second camera (mpCamera2): right keypoints indexed from NLeft, mTrl, its parameters
+        self.mpCamera2 = None
+        self.mvKeysRight = None
+        self.NLeft = -1
+        self.mTrl = None
+
+    def set_rig(self, keys_right, Trl, cam2):
+        self.mvKeysRight = keys_right
+        self.NLeft = len(self.mvKeysUn)
+        self.mTrl = np.asarray(Trl, np.float32).reshape(4, 4)
+        self.mpCamera2 = tuple(np.float32(c) for c in cam2[:4])
+        self.mvpMapPoints = self.mvpMapPoints + [None] * len(keys_right)
 
     def isBad(self):
         return self.bad
@@ -204,20 +216,29 @@ def flatten_window(local, fixed, local_mps, pMap: Map):
     kf_fixed = np.array([2 if id(k) in fixed_ids else (1 if k.mnId == pMap.GetInitKFid() else 0) for k in kfs],
                         np.uint8)
     cur_map = local[0].GetMap() if local else None
-    edge_pt, edge_kf, obs, isig, edge_refs = [], [], [], [], []
+    rig = any(k.mpCamera2 is not None for k in kfs)
+    edge_pt, edge_kf, obs, isig, edge_refs, body = [], [], [], [], [], []
     for pi, mp in enumerate(local_mps):
         for k, (li, ri) in mp.GetObservations().items():
             if k.isBad() or k.GetMap() is not cur_map or id(k) not in kf_index:
                 continue
-            if li == -1:
-                continue
-            kp = k.mvKeysUn[li]
-            ur = float(k.mvuRight[li])
-            edge_pt.append(pi)
-            edge_kf.append(kf_index[id(k)])
-            obs.append((kp["x"], kp["y"], ur if ur >= 0 else -1.0))
-            isig.append(k.mvInvLevelSigma2[kp["octave"]])
-            edge_refs.append((k, mp))
+            if li != -1:                                          # mono / stereo (:1819-1880)
+                kp = k.mvKeysUn[li]
+                ur = float(k.mvuRight[li])
+                edge_pt.append(pi)
+                edge_kf.append(kf_index[id(k)])
+                obs.append((kp["x"], kp["y"], ur if ur >= 0 else -1.0))
+                isig.append(k.mvInvLevelSigma2[kp["octave"]])
+                edge_refs.append((k, mp))
+                body.append(0)
+            if k.mpCamera2 is not None and ri != -1:              # EdgeSE3ProjectXYZToBody (:1883-1914)
+                kp = k.mvKeysRight[ri - k.NLeft]
+                edge_pt.append(pi)
+                edge_kf.append(kf_index[id(k)])
+                obs.append((kp["x"], kp["y"], -1.0))
+                isig.append(k.mvInvLevelSigma2[kp["octave"]])
+                edge_refs.append((k, mp))
+                body.append(1)
     k0 = kfs[0]
     W = dict(kf_Tcw=np.stack([k.GetPose().reshape(-1) for k in kfs]).astype(np.float32), kf_fixed=kf_fixed,
              pt_pos=np.stack([mp.GetWorldPos() for mp in local_mps]).astype(np.float32) if local_mps
@@ -225,6 +246,12 @@ def flatten_window(local, fixed, local_mps, pMap: Map):
              edge_pt=np.array(edge_pt, np.int32), edge_kf=np.array(edge_kf, np.int32),
              edge_obs=np.array(obs, np.float32).reshape(-1, 3), edge_inv_sigma2=np.array(isig, np.float32),
              cam=(k0.fx, k0.fy, k0.cx, k0.cy, k0.mbf))
+    if rig:
+        eye = np.eye(4, dtype=np.float32)
+        W["edge_body"] = np.array(body, np.uint8)
+        W["kf_Trl"] = np.stack([(k.mTrl if k.mpCamera2 is not None else eye).reshape(-1) for k in kfs])
+        c2 = next(k.mpCamera2 for k in kfs if k.mpCamera2 is not None)
+        W["cam2"] = tuple(c2) + (np.float32(0),)
     return W, kfs, edge_refs
 
 
@@ -260,13 +287,15 @@ def LocalBundleAdjustment(pKF: KeyFrame, stop_flag, pMap: Map, solver):
 def map_from_window(W: dict, covis_order=None):
     """Build the map model of a synthetic window (slamhot.synth.lba_window): every KF observes
     its points, KeyFrame 0 is the map-init KF, the last KF is the current one and sees all the
-    others as covisible."""
+    others as covisible.  Body edges (a rig window) become right-camera keypoints."""
     pmap = Map(init_kf_id=0)
     nk = len(W["kf_fixed"])
     cam = W["cam"]
+    body = W.get("edge_body")
     per_kf = [[] for _ in range(nk)]
+    per_kf_r = [[] for _ in range(nk)]
     for e in range(len(W["edge_pt"])):
-        per_kf[W["edge_kf"][e]].append(e)
+        (per_kf_r if body is not None and body[e] else per_kf)[W["edge_kf"][e]].append(e)
     from .synth import _level_tables
     _, inv_sigma2, _ = _level_tables()
     kfs = []
@@ -279,13 +308,26 @@ def map_from_window(W: dict, covis_order=None):
             lvl = int(np.argmin(np.abs(inv_sigma2 - W["edge_inv_sigma2"][e])))
             keys["octave"][j] = lvl
             ur[j] = W["edge_obs"][e][2]
-        kfs.append(KeyFrame(k, W["kf_Tcw"][k].reshape(4, 4), keys, ur, inv_sigma2, cam, pmap))
+        kf = KeyFrame(k, W["kf_Tcw"][k].reshape(4, 4), keys, ur, inv_sigma2, cam, pmap)
+        if body is not None:
+            kr = np.zeros(len(per_kf_r[k]), dtype=keys.dtype)
+            for j, e in enumerate(per_kf_r[k]):
+                kr["x"][j], kr["y"][j] = W["edge_obs"][e][:2]
+                kr["octave"][j] = int(np.argmin(np.abs(inv_sigma2 - W["edge_inv_sigma2"][e])))
+            kf.set_rig(kr, W["kf_Trl"][k], W["cam2"])
+        kfs.append(kf)
     mps = [MapPoint(i, W["pt_pos"][i], pmap) for i in range(len(W["pt_pos"]))]
     for k in range(nk):
         for j, e in enumerate(per_kf[k]):
             mp = mps[W["edge_pt"][e]]
             kfs[k].mvpMapPoints[j] = mp
             mp.AddObservation(kfs[k], j)
+        for j, e in enumerate(per_kf_r[k]):
+            mp = mps[W["edge_pt"][e]]
+            jr = kfs[k].NLeft + j
+            kfs[k].mvpMapPoints[jr] = mp
+            li, _ = mp.observations.get(kfs[k], (-1, -1))
+            mp.AddObservation(kfs[k], li, jr)
     cur = kfs[-1]
     cur.covisible = covis_order if covis_order is not None else [kfs[i] for i in range(nk - 2, -1, -1)]
     return pmap, kfs, mps

@@ -172,3 +172,20 @@ def test_stereo_stream_ordered_batch():
     sm.close()
     left.close()
     right.close()
+
+
+def test_stereo_host_buffer_form():
+    """slamhot_compute_stereo_matches: the Frame constructor's host path (two host extractions,
+    then ComputeStereoMatches on host keypoints) equals the oracle."""
+    import slamhot
+    il, ir = _pairs([(7, 4.0, 40.0, 2.0)])
+    left = slamhot.ORBextractor(nfeatures=1200, max_size=(752, 480))
+    right = slamhot.ORBextractor(nfeatures=1200, max_size=(752, 480))
+    kl, dl, _ = left(il[0])
+    kr, dr, _ = right(ir[0])
+    sm = slamhot.StereoMatcher()
+    ur, dep = sm.compute(left, right, kl, dl, kr, dr, MBF, MB)
+    assert _check(left, right, [(kl, dl, kr, dr, ur, dep)], 1200) > 300
+    sm.close()
+    left.close()
+    right.close()
