@@ -129,6 +129,25 @@ slam_status slamhot_extractor_stage_stats(slam_extractor* ex, double* total_ms, 
                                           int reset);
 
 /* ---------------------------------------------------------------------------------
+ * Frame construction after extraction (monocular / RGB-D / unrectified cameras)
+ * ------------------------------------------------------------------------------- */
+/* void Frame::UndistortKeyPoints() (Frame.cc:730-763): mvKeysUn = cv::undistortPoints(mvKeys,
+ * K, mDistCoef, R = I, P = mK) with OpenCV 4.2.0's default 5 iterations.  K = (fx, fy, cx, cy)
+ * of the Pinhole camera (toK() and mK are the same matrix), dist = mDistCoef (k1, k2, p1, p2
+ * [, k3]), ndist 4 or 5 (0, or dist[0] == 0: mvKeysUn = mvKeys).  Every keypoint field but pt
+ * is copied.  Host buffers, synchronous. */
+slam_status slamhot_undistort_keypoints(int device, const float* K, const float* dist, int ndist, int n,
+                                        const slam_keypoint* kps, slam_keypoint* kps_un);
+/* The same for nframes frames left in HBM by slamhot_extract_batch_device (d_kps cap per frame,
+ * d_n per frame) into d_kps_un (cap per frame); asynchronous on hip_stream. */
+slam_status slamhot_undistort_keypoints_batch_device(const float* K, const float* dist, int ndist, int nframes,
+                                                     const void* d_kps, const void* d_n, int cap, void* d_kps_un,
+                                                     void* hip_stream);
+/* void Frame::ComputeImageBounds(const cv::Mat&) (Frame.cc:765-792): bounds = (mnMinX, mnMaxX,
+ * mnMinY, mnMaxY) from the undistorted image corners (the image size without distortion). */
+slam_status slamhot_image_bounds(const float* K, const float* dist, int ndist, int cols, int rows, float* bounds);
+
+/* ---------------------------------------------------------------------------------
  * Vocabulary (DBoW2 TemplatedVocabulary<FORB>, ORBVocabulary.h:29-30)
  * ------------------------------------------------------------------------------- */
 typedef struct slam_vocab slam_vocab;

@@ -161,6 +161,31 @@ class ORBextractor {
 };
 
 /* ------------------------------------------------------------------------------------
+ * Frame construction after extraction (Frame.cc:730-792) for a Pinhole camera with OpenCV
+ * distortion mDistCoef = (k1, k2, p1, p2[, k3]).
+ * ---------------------------------------------------------------------------------- */
+struct PinholeCalib {
+    float K[4] = {0, 0, 0, 0};  // fx, fy, cx, cy (Pinhole::toK() and mK)
+    std::vector<float> dist;    // mDistCoef
+};
+
+/* void Frame::UndistortKeyPoints() (Frame.cc:730-763) */
+inline void UndistortKeyPoints(const PinholeCalib& c, const std::vector<KeyPoint>& mvKeys, std::vector<KeyPoint>& mvKeysUn,
+                               int device = 0) {
+    mvKeysUn.resize(mvKeys.size());
+    check(slamhot_undistort_keypoints(device, c.K, c.dist.data(), (int)c.dist.size(), (int)mvKeys.size(),
+                                      mvKeys.data(), mvKeysUn.data()),
+          "UndistortKeyPoints");
+}
+
+/* void Frame::ComputeImageBounds(const cv::Mat&) (Frame.cc:765-792): {mnMinX, mnMaxX, mnMinY, mnMaxY} */
+inline std::vector<float> ComputeImageBounds(const PinholeCalib& c, int cols, int rows) {
+    std::vector<float> b(4);
+    check(slamhot_image_bounds(c.K, c.dist.data(), (int)c.dist.size(), cols, rows, b.data()), "ComputeImageBounds");
+    return b;
+}
+
+/* ------------------------------------------------------------------------------------
  * ORBmatcher (ORBmatcher.h:36-110).  The KeyFrame / Frame arguments arrive as their
  * matcher-relevant views; the MapPoint* outputs as indices into the other side (-1 = NULL).
  * ---------------------------------------------------------------------------------- */

@@ -950,3 +950,48 @@ class Mapper:
         check(lib().slamhot_fuse_search(self._h, C.byref(kf_view), _ptr(isig), len(mps), _ptr(mps), _ptr(mp_desc), th,
                                         _ptr(bi), _ptr(bd)), "fuse_search")
         return bi, bd
+
+
+# ------------------------------------------------------------------------------------------
+# Frame construction: Frame::UndistortKeyPoints / ComputeImageBounds (Frame.cc:730-792)
+# ------------------------------------------------------------------------------------------
+def _bind_frame(L):
+    if getattr(L, "_frame_ready", False):
+        return
+    L.slamhot_undistort_keypoints.argtypes = [I, P, P, I, I, P, P]
+    L.slamhot_undistort_keypoints_batch_device.argtypes = [P, P, I, I, P, P, I, P, P]
+    L.slamhot_image_bounds.argtypes = [P, P, I, I, I, P]
+    L._frame_ready = True
+
+
+def UndistortKeyPoints(kps, K, dist, device: int = 0):
+    """mvKeysUn of mvKeys for a Pinhole camera K = (fx, fy, cx, cy) with mDistCoef = dist."""
+    L = lib()
+    _bind_frame(L)
+    kps = np.ascontiguousarray(kps, KP_DTYPE)
+    Kf = np.ascontiguousarray(K, np.float32)
+    D = np.ascontiguousarray(dist, np.float32)
+    out = np.zeros_like(kps)
+    check(L.slamhot_undistort_keypoints(device, _ptr(Kf), _ptr(D), len(D), len(kps), _ptr(kps), _ptr(out)),
+          "undistort_keypoints")
+    return out
+
+
+def undistort_keypoints_batch_device(K, dist, nframes, d_kps, d_n, cap, d_kps_un, stream=None):
+    L = lib()
+    _bind_frame(L)
+    Kf = np.ascontiguousarray(K, np.float32)
+    D = np.ascontiguousarray(dist, np.float32)
+    check(L.slamhot_undistort_keypoints_batch_device(_ptr(Kf), _ptr(D), len(D), nframes, P(d_kps), P(d_n), cap,
+                                                     P(d_kps_un), P(stream) if stream else None),
+          "undistort_keypoints_batch_device")
+
+
+def ComputeImageBounds(K, dist, cols, rows):
+    L = lib()
+    _bind_frame(L)
+    Kf = np.ascontiguousarray(K, np.float32)
+    D = np.ascontiguousarray(dist, np.float32)
+    b = np.zeros(4, np.float32)
+    check(L.slamhot_image_bounds(_ptr(Kf), _ptr(D), len(D), cols, rows, _ptr(b)), "image_bounds")
+    return b

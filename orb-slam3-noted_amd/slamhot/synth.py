@@ -415,15 +415,42 @@ def _sample(tex, a, b):
             (tex[b1, a0] * (1 - fa) + tex[b1, a1] * fa) * fb)
 
 
+EUROC_MONO_CAM = dict(fx=458.654, fy=457.296, cx=367.215, cy=248.375, w=752, h=480,
+                      dist=(-0.28340811, 0.07395907, 0.00019359, 1.76187114e-05))  # Monocular/EuRoC.yaml
+
+
+def _undistort_normalized(xx, yy, cam):
+    """Normalised undistorted coordinates of raw pixels (the radial-tangential model inverted by
+    fixed-point iteration, as cv::undistortPoints; 20 iterations for rendering)."""
+    k1, k2, p1, p2 = cam["dist"][:4]
+    k3 = cam["dist"][4] if len(cam["dist"]) > 4 else 0.0
+    x0 = (xx - cam["cx"]) / cam["fx"]
+    y0 = (yy - cam["cy"]) / cam["fy"]
+    x, y = x0.copy(), y0.copy()
+    for _ in range(20):
+        r2 = x * x + y * y
+        icd = 1.0 / (1 + ((k3 * r2 + k2) * r2 + k1) * r2)
+        dx = 2 * p1 * x * y + p2 * (r2 + 2 * x * x)
+        dy = p1 * (r2 + 2 * y * y) + 2 * p2 * x * y
+        x = (x0 - dx) * icd
+        y = (y0 - dy) * icd
+    return x, y
+
+
 def render_view(textures, Tcw, cam=EUROC_CAM, width=None, height=None, noise_seed=None):
     """Ray-cast the textured room from camera pose Tcw (4x4 world -> camera); returns
-    (image u8, depth float64 z along the optical axis)."""
+    (image u8, depth float64 z along the optical axis).  A ``dist`` entry in ``cam`` renders
+    the raw (distorted) image of that camera."""
     W = width or cam["w"]
     H = height or cam["h"]
     R, t = Tcw[:3, :3], Tcw[:3, 3]
     C = -R.T @ t
     yy, xx = np.mgrid[0:H, 0:W].astype(np.float64)
-    dc = np.stack([(xx - cam["cx"]) / cam["fx"], (yy - cam["cy"]) / cam["fy"], np.ones_like(xx)], -1)
+    if cam.get("dist") is not None:
+        nx, ny = _undistort_normalized(xx, yy, cam)
+        dc = np.stack([nx, ny, np.ones_like(xx)], -1)
+    else:
+        dc = np.stack([(xx - cam["cx"]) / cam["fx"], (yy - cam["cy"]) / cam["fy"], np.ones_like(xx)], -1)
     dw = dc @ R  # R^T d per pixel (row vectors)
     best = np.full((H, W), np.inf)
     img = np.zeros((H, W))
@@ -484,3 +511,14 @@ def stereo_sequence(seed: int, n: int, cam=EUROC_CAM, step_m: float = 0.03):
         Rs.append(render_view(tex, Tr, cam, noise_seed=seed * 1000 + 2 * i + 1)[0])
         Ts.append(T)
     return np.stack(Ls), np.stack(Rs), Ts
+
+
+def mono_sequence(seed: int, n: int, cam=EUROC_MONO_CAM, step_m: float = 0.03):
+    """n raw monocular frames of the room through a distorting pinhole camera (EuRoC MH01-like,
+    Examples/Monocular/EuRoC.yaml): (images (n,H,W) u8, gt Tcw list)."""
+    tex = _wall_textures(seed)
+    imgs, Ts = [], []
+    for i, T in enumerate(sequence_poses(seed, n, step_m)):
+        imgs.append(render_view(tex, T, cam, noise_seed=seed * 1000 + i)[0])
+        Ts.append(T)
+    return np.stack(imgs), Ts

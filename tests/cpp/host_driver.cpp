@@ -10,6 +10,9 @@
 //       ORBmatcher(nnratio, true).SearchByBoW(A, B, matches) -> int32 n, int32 matches[]
 //   host_driver lba <window.bin> <out.bin>
 //       Optimizer::LocalBundleAdjustment(window) -> counters, poses, points, outliers, stats
+//   host_driver mono <W> <H> <nframes> <n_init> <nfeatures> <images.u8> <calib.bin> <out.bin>
+//       monocular Frame construction over a sequence: init / tracking extractors, lap (0, 1000),
+//       UndistortKeyPoints, ComputeImageBounds
 //
 // Exit codes: 0 ok, 2 usage / file error, 3 slamhot::Error (message on stderr).
 #include <cstdio>
@@ -205,6 +208,43 @@ int run_lba(char** a) {
     return 0;
 }
 
+// Monocular Frame construction over a sequence (Tracking.cc:1335-1346, Frame.cc:262-330):
+// frames < n_init go through the 5*nFeatures initialisation extractor (mpIniORBextractor),
+// the rest through mpORBextractorLeft; ExtractORB(0, im, 0, 1000) (Frame.cc:306), then
+// UndistortKeyPoints, plus ComputeImageBounds once.
+// calib file: 4 f32 K | int32 nd | nd f32 dist.  Output: f32 bounds[4], then per frame
+// int32 n, int32 mono, n x 28 B mvKeys, n x 28 B mvKeysUn, n x 32 B descriptors.
+int run_mono(char** a) {
+    const int W = std::atoi(a[0]), H = std::atoi(a[1]), nframes = std::atoi(a[2]), n_init = std::atoi(a[3]);
+    const int nfeat = std::atoi(a[4]);
+    const std::vector<uint8_t> imgs = read_file(a[5]);
+    const std::vector<uint8_t> cb = read_file(a[6]);
+    if (imgs.size() != (size_t)W * H * nframes) throw std::runtime_error("image size mismatch");
+    Reader r{cb};
+    slamhot::PinholeCalib calib;
+    for (int i = 0; i < 4; i++) calib.K[i] = r.get<float>();
+    calib.dist = r.vec<float>(r.get<int32_t>());
+    slamhot::ORBextractor ini(5 * nfeat, 1.2f, 8, 20, 7), left(nfeat, 1.2f, 8, 20, 7);  // Tracking.cc: 5*nFeatures
+    Writer o;
+    for (float v : slamhot::ComputeImageBounds(calib, W, H)) o.put<float>(v);
+    const std::vector<int> lap = {0, 1000};
+    for (int f = 0; f < nframes; f++) {
+        slamhot::ORBextractor& ex = f < n_init ? ini : left;
+        std::vector<slamhot::KeyPoint> kps, kun;
+        slamhot::Mat8U desc;
+        slamhot::GrayImage gi{imgs.data() + (size_t)f * W * H, W, H, (size_t)W};
+        const int mono = ex(gi, kps, desc, lap);
+        slamhot::UndistortKeyPoints(calib, kps, kun);
+        o.put<int32_t>((int32_t)kps.size());
+        o.put<int32_t>(mono);
+        o.vec(kps);
+        o.vec(kun);
+        o.vec(desc.data);
+    }
+    write_file(a[7], o.b.data(), o.b.size());
+    return 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -217,6 +257,7 @@ int main(int argc, char** argv) {
         if (mode == "extract" && argc == 9) return run_extract(argv + 2);
         if (mode == "bow" && argc == 7) return run_bow(argv + 2);
         if (mode == "lba" && argc == 4) return run_lba(argv + 2);
+        if (mode == "mono" && argc == 10) return run_mono(argv + 2);
         std::fprintf(stderr, "bad arguments for %s\n", mode.c_str());
         return 2;
     } catch (const slamhot::Error& e) {

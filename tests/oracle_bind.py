@@ -439,3 +439,29 @@ def remap_linear(src, map_x, map_y):
     dst = np.zeros((dh, dw), np.uint8)
     L.oracle_remap_linear(_ptr(src), sw, sh, sw, _ptr(mx), _ptr(my), dw, dh, _ptr(dst), dw)
     return dst
+
+
+# ---- Frame construction (oracle/frame_oracle.cpp)
+def undistort_keypoints(kps, K, dist):
+    L = lib()
+    if not hasattr(L, "_frame_ready"):
+        L.oracle_undistort_keypoints.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
+        L.oracle_undistort_keypoints.restype = None
+        L.oracle_image_bounds.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
+        L.oracle_image_bounds.restype = None
+        L._frame_ready = True
+    kps = np.ascontiguousarray(kps, KP_DTYPE)
+    Kf = np.ascontiguousarray(K, np.float32)
+    D = np.ascontiguousarray(dist, np.float32)
+    out = np.zeros_like(kps)
+    L.oracle_undistort_keypoints(len(kps), _ptr(kps), _ptr(Kf), _ptr(D), len(D), _ptr(out))
+    return out
+
+
+def image_bounds(K, dist, cols, rows):
+    undistort_keypoints(np.zeros(0, KP_DTYPE), K, dist)  # binds
+    Kf = np.ascontiguousarray(K, np.float32)
+    D = np.ascontiguousarray(dist, np.float32)
+    b = np.zeros(4, np.float32)
+    lib().oracle_image_bounds(_ptr(Kf), _ptr(D), len(D), cols, rows, _ptr(b))
+    return b
