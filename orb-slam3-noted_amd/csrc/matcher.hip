@@ -26,6 +26,8 @@
 #include "common.hpp"
 #include "gate_fp.hpp"
 
+#include "projection.hpp"  // DevProjFrame / ProjQuery / DevProjCall / FrustumCall
+
 namespace slamhot {
 
 // ----------------------------------------------------------------------------- vocab
@@ -938,64 +940,6 @@ extern "C" slam_status slamhot_bow_match_batch_status(slam_matcher* m, void* hip
 // =======================================================================================
 namespace slamhot {
 
-constexpr int kGridCols = 64, kGridRows = 48;  // Frame.h:37-38
-
-struct DevProjFrame {
-    int n;
-    const slam_keypoint* kps;
-    const float* uright;
-    const uint8_t* desc;
-    const int8_t* state;          // entry mvpMapPoints state
-    const int32_t* cell_start;    // kGridCols*kGridRows + 1
-    const int32_t* cell_feat;
-    float min_x, min_y, max_x, max_y, inv_w, inv_h;
-    float fx, fy, cx, cy, bf, b;
-    float T[16];
-    float scale[16];
-    int nlevels;
-};
-
-struct ProjQuery {
-    float u, v, r;      // window centre and half size
-    float ur, er;       // stereo gate: skip candidates with uright > 0 && |ur - uright| > er (er < 0: off)
-    int16_t min_level, max_level;
-    int32_t valid;
-    float angle;        // for the rotation histogram
-    int32_t blocking;   // a match by this query occupies the feature for later queries
-};
-
-enum { kProjLocal = 0, kProjLast = 1, kProjKF = 2 };
-
-struct DevProjCall {
-    DevProjFrame F;
-    int mode, nq;
-    // local-map inputs
-    const slam_mp_track* mps;
-    float th, th_far, nnratio;
-    int far_points;
-    // last-frame inputs
-    const slam_keypoint* lf_kps;
-    const slam_keypoint* lf_kps_un;
-    const uint8_t* lf_has_mp;
-    const uint8_t* lf_outlier;
-    const float* lf_pos;
-    const uint8_t* lf_has_obs;
-    float LT[16];
-    int mono;
-    // prepared queries (KF variant) or scratch for computed ones
-    ProjQuery* queries;
-    const uint8_t* qdesc;   // nq x 32 query descriptors
-    int th_dist;            // acceptance threshold (TH_HIGH or ORBdist)
-    int check_ori;
-    // scratch / outputs
-    int32_t* cand_off;      // nq + 1
-    uint32_t* cand;         // (feature << 12) | dist   (capacity cand_cap)
-    int cand_cap;
-    int32_t* f_match;       // F.n
-    int32_t* out;           // [0] nmatches, [1] status (1 = candidate overflow), [2] iterations
-    int32_t* gstate;        // resolution state in global memory when it exceeds the LDS (else null)
-};
-
 __device__ __forceinline__ void gemm_rx_t(const float* T, const float* X, float* o) {
     for (int i = 0; i < 3; i++) {
         const double acc = (double)T[4 * i] * (double)X[0] + (double)T[4 * i + 1] * (double)X[1] +
@@ -1052,7 +996,8 @@ __device__ __forceinline__ void for_candidates(const DevProjFrame& F, const Proj
     }
 }
 
-__global__ void __launch_bounds__(1024) k_search_by_projection(DevProjCall C) {
+__global__ void __launch_bounds__(1024) k_search_by_projection(const DevProjCall* __restrict__ calls) {
+    const DevProjCall& C = calls[blockIdx.x];
     __shared__ int scratch[20];
     __shared__ int s_flag, s_hist[32], s_keep[3], s_count;
     const DevProjFrame& F = C.F;
@@ -1286,17 +1231,8 @@ __global__ void __launch_bounds__(1024) k_search_by_projection(DevProjCall C) {
 // MapPoint::PredictScale's ceil(logf(ratio) / mfLogScaleFactor) uses the correctly rounded
 // logf ((float)log((double)r)); its ceil equals glibc logf's for every ratio in [1e-3, 1e3]
 // (exhaustive check, tests/test_projection_oracle.py).
-struct FrustumCall {
-    float R[9], t[3], Ow[3];
-    float min_x, max_x, min_y, max_y, fx, fy, cx, cy, bf;
-    float log_scale, view_cos_limit;
-    int nlevels, n;
-    const slam_mp_geom* mps;
-    slam_mp_track* track;
-    int32_t* n_in_view;
-};
-
-__global__ void __launch_bounds__(256) k_is_in_frustum(FrustumCall C) {
+__global__ void __launch_bounds__(256) k_is_in_frustum(const FrustumCall* __restrict__ calls) {
+    const FrustumCall& C = calls[blockIdx.y];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= C.n) return;
     const slam_mp_geom g = C.mps[i];
@@ -1350,6 +1286,29 @@ __global__ void __launch_bounds__(256) k_is_in_frustum(FrustumCall C) {
     C.track[i] = tr;
 }
 
+
+constexpr size_t kProjLdsMax = 150 * 1024;
+
+size_t projection_lds_bytes(int n_features, int n_queries) {
+    const size_t lds = (size_t)4 * (2 * (size_t)n_features + 2 * (size_t)n_queries);
+    return lds > kProjLdsMax ? 0 : lds;
+}
+
+hipError_t launch_search_by_projection(const DevProjCall* calls, int ncalls, size_t lds, hipStream_t s) {
+    if (ncalls <= 0) return hipSuccess;
+    hipError_t e = hipFuncSetAttribute((const void*)k_search_by_projection, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds + 16);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_search_by_projection, dim3(ncalls), dim3(1024), lds, s, calls);
+    return hipGetLastError();
+}
+
+hipError_t launch_is_in_frustum(const FrustumCall* calls, int ncalls, int max_n, hipStream_t s) {
+    if (ncalls <= 0 || max_n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_is_in_frustum, dim3((max_n + 255) / 256, ncalls), dim3(256), 0, s, calls);
+    return hipGetLastError();
+}
+
 }  // namespace slamhot
 
 namespace {
@@ -1399,8 +1358,6 @@ bool frame_ok(const slam_frame_view* F) {
            F->nlevels <= 16 && F->scale;
 }
 
-constexpr size_t kProjLdsMax = 150 * 1024;
-
 slam_status run_projection(slam_matcher* m, const slam_frame_view* F, DevProjCall& Cc, int nq,
                            const std::vector<ProjQuery>* host_queries, const uint8_t* qdesc,
                            int32_t* f_match, int* nmatches,
@@ -1436,16 +1393,12 @@ slam_status run_projection(slam_matcher* m, const slam_frame_view* F, DevProjCal
         C.f_match = B.take<int32_t>(std::max(1, F->n));
         C.out = B.take<int32_t>(4);
         SLAM_HIP_TRY(hipMemsetAsync(C.out, 0, 16, m->stream));
-        size_t lds = (size_t)4 * (2 * (size_t)F->n + 2 * (size_t)nq);
+        const size_t lds = projection_lds_bytes(F->n, nq);
         C.gstate = nullptr;
-        if (lds > kProjLdsMax) {  // large local map: the owner / match / assignment arrays in HBM
+        if (!lds)  // large local map: the owner / match / assignment arrays in HBM
             C.gstate = B.take<int32_t>(2 * (size_t)F->n + 2 * (size_t)nq);
-            lds = 0;
-        }
-        SLAM_HIP_TRY(hipFuncSetAttribute((const void*)k_search_by_projection,
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds + 16));
-        hipLaunchKernelGGL(k_search_by_projection, dim3(1), dim3(1024), lds, m->stream, C);
-        SLAM_HIP_TRY(hipGetLastError());
+        const DevProjCall* dC = B.put(&C, 1);
+        SLAM_HIP_TRY(launch_search_by_projection(dC, 1, lds, m->stream));
         int32_t out[4];
         SLAM_HIP_TRY(hipMemcpyAsync(out, C.out, 16, hipMemcpyDeviceToHost, m->stream));
         if (F->n) SLAM_HIP_TRY(hipMemcpyAsync(f_match, C.f_match, (size_t)F->n * 4, hipMemcpyDeviceToHost, m->stream));
@@ -1547,9 +1500,7 @@ extern "C" slam_status slamhot_search_local_points(slam_matcher* m, const slam_f
                                         Fc.track = B.take<slam_mp_track>(std::max(1, n_mp));
                                         Fc.n_in_view = B.take<int32_t>(1);
                                         (void)hipMemsetAsync(Fc.n_in_view, 0, 4, B.s);
-                                        if (n_mp)
-                                            hipLaunchKernelGGL(k_is_in_frustum, dim3((n_mp + 255) / 256), dim3(256),
-                                                               0, B.s, Fc);
+                                        (void)launch_is_in_frustum(B.put(&Fc, 1), 1, n_mp, B.s);
                                         c.mps = Fc.track;
                                     });
     if (st != SLAM_OK) return st;

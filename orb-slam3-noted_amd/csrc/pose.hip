@@ -16,6 +16,7 @@
 
 #include "common.hpp"
 #include "se3_device.hpp"
+#include "pose_types.hpp"
 
 namespace slamhot {
 namespace pose {
@@ -25,25 +26,6 @@ using lba::Quat;
 constexpr int kThreads = 256;
 
 __host__ __device__ constexpr int sym6(int r, int c) { return r * 6 - (r * (r - 1)) / 2 + (c - r); }
-
-struct PEdge {
-    float obs[3];     // u, v, ur
-    float info;       // invSigma2
-    float Xw[3];
-    int idx;          // feature index; bit 31 = stereo
-};
-
-struct PFrame {
-    float Tcw[16];
-    float fx, fy, cx, cy, bf;
-    int e0, ne;       // edge range
-};
-
-struct POut {
-    float Tcw[16];
-    int n_inliers;
-    int pad[3];
-};
 
 __device__ inline bool is_stereo(const PEdge& e) { return e.idx < 0; }
 
@@ -423,6 +405,23 @@ __global__ void __launch_bounds__(kThreads) k_pose_opt(const PFrame* __restrict_
     }
 }
 
+Hub pose_hub() {
+    Hub hub;
+    const float deltaMono = std::sqrt(5.991), deltaStereo = std::sqrt(7.815);  // Optimizer.cc:852-853
+    hub.delta_mono = deltaMono;
+    hub.delta_stereo = deltaStereo;
+    hub.dsqr_mono = (float)(hub.delta_mono * hub.delta_mono);
+    hub.dsqr_stereo = (float)(hub.delta_stereo * hub.delta_stereo);
+    return hub;
+}
+
+hipError_t launch_pose_opt(const PFrame* frames, const PEdge* edges, double* errs, uint8_t* level, uint8_t* outlier,
+                           POut* out, int nframes, hipStream_t s) {
+    if (nframes <= 0) return hipSuccess;
+    k_pose_opt<<<nframes, kThreads, 0, s>>>(frames, edges, errs, level, outlier, out, pose_hub());
+    return hipGetLastError();
+}
+
 }  // namespace pose
 }  // namespace slamhot
 
@@ -531,16 +530,8 @@ slam_status slamhot_pose_optimization(slam_pose_opt* h, int nframes, const slam_
     SLAM_HIP_TRY(hipMemcpyAsync(h->d_frames, pf.data(), nframes * sizeof(PFrame), hipMemcpyHostToDevice, S));
     if (!pe.empty())
         SLAM_HIP_TRY(hipMemcpyAsync(h->d_edges, pe.data(), pe.size() * sizeof(PEdge), hipMemcpyHostToDevice, S));
-    Hub hub;
-    const float deltaMono = std::sqrt(5.991), deltaStereo = std::sqrt(7.815);  // Optimizer.cc:852-853
-    hub.delta_mono = deltaMono;
-    hub.delta_stereo = deltaStereo;
-    hub.dsqr_mono = (float)(hub.delta_mono * hub.delta_mono);
-    hub.dsqr_stereo = (float)(hub.delta_stereo * hub.delta_stereo);
-    k_pose_opt<<<nframes, kThreads, 0, S>>>((const PFrame*)h->d_frames, (const PEdge*)h->d_edges,
-                                            (double*)h->d_errs, (uint8_t*)h->d_level, (uint8_t*)h->d_outl,
-                                            (POut*)h->d_out, hub);
-    SLAM_HIP_TRY(hipGetLastError());
+    SLAM_HIP_TRY(launch_pose_opt((const PFrame*)h->d_frames, (const PEdge*)h->d_edges, (double*)h->d_errs,
+                                 (uint8_t*)h->d_level, (uint8_t*)h->d_outl, (POut*)h->d_out, nframes, S));
     std::vector<POut> po(nframes);
     std::vector<uint8_t> outl(pe.size());
     SLAM_HIP_TRY(hipMemcpyAsync(po.data(), h->d_out, nframes * sizeof(POut), hipMemcpyDeviceToHost, S));
