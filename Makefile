@@ -5,7 +5,7 @@ CSRC := $(PKG)/csrc
 LIBDIR := $(PKG)/lib
 HIPFLAGS ?= --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off \
             -fhip-fp32-correctly-rounded-divide-sqrt -Wall -Wno-unused-result
-SRCS := $(CSRC)/extractor.hip $(CSRC)/matcher.hip $(CSRC)/lba.hip $(CSRC)/pose.hip $(CSRC)/stereo.hip $(CSRC)/mapping.hip $(CSRC)/rectify.hip $(CSRC)/frame.hip
+SRCS := $(CSRC)/extractor.hip $(CSRC)/matcher.hip $(CSRC)/lba.hip $(CSRC)/pose.hip $(CSRC)/stereo.hip $(CSRC)/mapping.hip $(CSRC)/rectify.hip $(CSRC)/frame.hip $(CSRC)/track.hip
 HDRS := $(wildcard $(CSRC)/*.hpp) $(CSRC)/orb_pattern.inc include/slamhot.h
 
 all: $(LIBDIR)/libslamhot.so oracle tests/cpp/host_driver tests/cpp/shim_driver

@@ -562,6 +562,62 @@ slam_status slamhot_rectify_batch_device(slam_rectifier* r, int nframes, const v
                                          int64_t src_stride, void* d_dst, int dst_pitch, int64_t dst_stride,
                                          void* hip_stream);
 
+/* ------------------------------------------------------------------ per-sequence tracking
+ * The stereo tracking chain of Tracking::Track for rectified stereo (BASELINE.json configs[4]),
+ * device-resident: per frame cv::remap x2 -> ORBextractor x2 -> Frame::ComputeStereoMatches ->
+ * ComputeBoW + SearchByBoW(reference KF, F) -> PoseOptimization -> SearchLocalPoints ->
+ * PoseOptimization -> NeedNewKeyFrame / CreateNewKeyFrame (Tracking.cc:1256-3330), with every
+ * decision taken on the device.  nseq sequences advance in lock-step (one frame each per step);
+ * the map is the reference KeyFrame of each sequence (DESIGN.md §4g states what LocalMapping-side
+ * bookkeeping is left out). */
+typedef struct slam_tracker slam_tracker;
+
+typedef struct slam_tracker_config {
+    int32_t nseq, width, height;
+    slam_orb_params orb;          /* both extractors (EuRoC: 1200, 1.2, 8, 20, 7) */
+    slam_camera cam;              /* rectified Camera.fx, fy, cx, cy, bf */
+    float th_depth;               /* ThDepth in baselines (35): mThDepth = bf * ThDepth / fx */
+    const float* map_lx;          /* initUndistortRectifyMap maps (width x height, float), or NULL */
+    const float* map_ly;          /* when the inputs are already rectified */
+    const float* map_rx;
+    const float* map_ry;
+} slam_tracker_config;
+
+typedef struct slam_track_record {   /* one step of one sequence */
+    float Tcw[16];                   /* mCurrentFrame.mTcw after the step */
+    int32_t n, n_stereo;             /* N, features with mvDepth > 0 */
+    int32_t n_bow;                   /* SearchByBoW(mpReferenceKF, F) */
+    int32_t n_inl_ref;               /* TrackReferenceKeyFrame's nmatchesMap */
+    int32_t n_local;                 /* SearchByProjection matches of SearchLocalPoints */
+    int32_t n_inl;                   /* TrackLocalMap's mnMatchesInliers */
+    int32_t is_keyframe, lost, initialized, pad[3];
+} slam_track_record;
+
+typedef struct slam_track_keyframe { /* the reference KeyFrame of one sequence (read back) */
+    float Tcw[16];                   /* the sequence's current pose */
+    int32_t initialized, n_ref, n, cap;  /* cap: capacity of the arrays below (in) */
+    slam_keypoint* kps;
+    uint8_t* desc;                   /* n x 32 */
+    uint8_t* mp_valid;
+    float* mp_pos;                   /* n x 3 */
+    float* mp_normal;                /* n x 3 */
+    float* mp_min_dist;
+    float* mp_max_dist;
+    uint8_t* mp_desc;                /* n x 32 */
+} slam_track_keyframe;
+
+/* voc stays owned by the caller and must outlive the tracker. */
+slam_status slamhot_tracker_create(int device, const slam_tracker_config* cfg, slam_vocab* voc, slam_tracker** out);
+void slamhot_tracker_destroy(slam_tracker* t);
+/* One frame of every sequence: nseq left and nseq right u8 images in device memory (raw when the
+ * tracker holds rectification maps).  Asynchronous: nothing waits on the host. */
+slam_status slamhot_tracker_step_device(slam_tracker* t, const void* d_left, int left_pitch, int64_t left_stride,
+                                        const void* d_right, int right_pitch, int64_t right_stride);
+/* The last step's records (nseq), synchronising; SLAM_ECAP if a sequence's SearchByProjection
+ * candidates overflowed (its matches would be incomplete). */
+slam_status slamhot_tracker_records(slam_tracker* t, slam_track_record* out);
+slam_status slamhot_tracker_keyframe(slam_tracker* t, int seq, slam_track_keyframe* kf);
+
 #ifdef __cplusplus
 }
 #endif

@@ -995,3 +995,91 @@ def ComputeImageBounds(K, dist, cols, rows):
     b = np.zeros(4, np.float32)
     check(L.slamhot_image_bounds(_ptr(Kf), _ptr(D), len(D), cols, rows, _ptr(b)), "image_bounds")
     return b
+
+
+# ------------------------------------------------------------------------------------------
+# Per-sequence stereo tracking chain (slamhot_tracker_*, csrc/track.hip; BASELINE configs[4])
+# ------------------------------------------------------------------------------------------
+class TrackerConfig(C.Structure):
+    _fields_ = [("nseq", C.c_int32), ("width", C.c_int32), ("height", C.c_int32), ("orb", OrbParams),
+                ("cam", Camera), ("th_depth", C.c_float), ("map_lx", C.c_void_p), ("map_ly", C.c_void_p),
+                ("map_rx", C.c_void_p), ("map_ry", C.c_void_p)]
+
+
+class TrackRecord(C.Structure):
+    _fields_ = [("Tcw", C.c_float * 16), ("n", C.c_int32), ("n_stereo", C.c_int32), ("n_bow", C.c_int32),
+                ("n_inl_ref", C.c_int32), ("n_local", C.c_int32), ("n_inl", C.c_int32), ("is_keyframe", C.c_int32),
+                ("lost", C.c_int32), ("initialized", C.c_int32), ("pad", C.c_int32 * 3)]
+
+
+class TrackKeyFrame(C.Structure):
+    _fields_ = [("Tcw", C.c_float * 16), ("initialized", C.c_int32), ("n_ref", C.c_int32), ("n", C.c_int32),
+                ("cap", C.c_int32), ("kps", C.c_void_p), ("desc", C.c_void_p), ("mp_valid", C.c_void_p),
+                ("mp_pos", C.c_void_p), ("mp_normal", C.c_void_p), ("mp_min_dist", C.c_void_p),
+                ("mp_max_dist", C.c_void_p), ("mp_desc", C.c_void_p)]
+
+
+class Tracker:
+    """nseq stereo sequences tracked in lock-step on one device (Tracking::Track, stereo)."""
+
+    def __init__(self, vocab: Vocabulary, nseq: int, cam, maps=None, width: int = 752, height: int = 480,
+                 nfeatures: int = 1200, th_depth: float = 35.0, device: int = 0):
+        L = lib()
+        if not getattr(L, "_track_ready", False):
+            L.slamhot_tracker_create.argtypes = [I, C.POINTER(TrackerConfig), P, C.POINTER(P)]
+            L.slamhot_tracker_destroy.argtypes = [P]
+            L.slamhot_tracker_destroy.restype = None
+            L.slamhot_tracker_step_device.argtypes = [P, P, I, C.c_int64, P, I, C.c_int64]
+            L.slamhot_tracker_records.argtypes = [P, P]
+            L.slamhot_tracker_keyframe.argtypes = [P, I, C.POINTER(TrackKeyFrame)]
+            L._track_ready = True
+        self.nseq, self.W, self.H, self.cap = nseq, width, height, 2 * nfeatures + 64
+        self._maps = None
+        cfg = TrackerConfig(nseq, width, height, OrbParams(nfeatures, 1.2, 8, 20, 7), Camera(*cam), th_depth)
+        if maps is not None:
+            self._maps = [np.ascontiguousarray(m, np.float32) for pair in maps for m in pair]
+            cfg.map_lx, cfg.map_ly, cfg.map_rx, cfg.map_ry = [m.ctypes.data for m in self._maps]
+        self._voc = vocab
+        h = P()
+        check(L.slamhot_tracker_create(device, C.byref(cfg), vocab._h, C.byref(h)), "tracker_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().slamhot_tracker_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def step_device(self, d_left: int, d_right: int, pitch=None, stride=None):
+        pitch = pitch or self.W
+        stride = stride or self.W * self.H
+        check(lib().slamhot_tracker_step_device(self._h, P(d_left), pitch, stride, P(d_right), pitch, stride),
+              "tracker_step")
+
+    def records(self):
+        recs = (TrackRecord * self.nseq)()
+        check(lib().slamhot_tracker_records(self._h, recs), "tracker_records")
+        return [dict(Tcw=np.array(r.Tcw[:], np.float32).reshape(4, 4), n=r.n, n_stereo=r.n_stereo, n_bow=r.n_bow,
+                     n_inl_ref=r.n_inl_ref, n_local=r.n_local, n_inl=r.n_inl, is_keyframe=r.is_keyframe,
+                     lost=r.lost, initialized=r.initialized) for r in recs]
+
+    def keyframe(self, seq: int):
+        cap = self.cap
+        out = dict(kps=np.zeros(cap, KP_DTYPE), desc=np.zeros((cap, 32), np.uint8), mp_valid=np.zeros(cap, np.uint8),
+                   mp_pos=np.zeros((cap, 3), np.float32), mp_normal=np.zeros((cap, 3), np.float32),
+                   mp_min_dist=np.zeros(cap, np.float32), mp_max_dist=np.zeros(cap, np.float32),
+                   mp_desc=np.zeros((cap, 32), np.uint8))
+        kf = TrackKeyFrame()
+        kf.cap = cap
+        for k, a in out.items():
+            setattr(kf, k, a.ctypes.data)
+        check(lib().slamhot_tracker_keyframe(self._h, seq, C.byref(kf)), "tracker_keyframe")
+        n = kf.n
+        res = {k: v[:n].copy() for k, v in out.items()}
+        res.update(Tcw=np.array(kf.Tcw[:], np.float32).reshape(4, 4), initialized=kf.initialized, n_ref=kf.n_ref, n=n)
+        return res

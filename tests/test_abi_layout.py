@@ -15,7 +15,8 @@ PAIRS = {"OrbParams": "slam_orb_params", "BowSide": "slam_bow_side", "FrameView"
          "LastFrameView": "slam_last_frame", "KFPointsView": "slam_kf_points", "Camera": "slam_camera",
          "LbaProblem": "slam_lba_problem", "LbaOptions": "slam_lba_options", "LbaResult": "slam_lba_result",
          "PoseFrame": "slam_pose_frame", "PoseResult": "slam_pose_result", "TriKF": "slam_tri_kf",
-         "TriPair": "slam_tri_pair"}
+         "TriPair": "slam_tri_pair", "TrackerConfig": "slam_tracker_config", "TrackRecord": "slam_track_record",
+         "TrackKeyFrame": "slam_track_keyframe"}
 
 
 @pytest.fixture(scope="module")
