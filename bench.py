@@ -174,7 +174,7 @@ def main():
     ap.add_argument("--lba-inflight", type=int, default=3, help="LBA solver handles driven concurrently")
     ap.add_argument("--pose-frames", type=int, default=512, help="PoseOptimization frames per GPU per call")
     ap.add_argument("--track-seqs", type=int, default=64, help="track leg: sequences per GPU (lock-step)")
-    ap.add_argument("--track-frames", type=int, default=24, help="track leg: frames per sequence")
+    ap.add_argument("--track-frames", type=int, default=56, help="track leg: steps (frames per sequence)")
     args = ap.parse_args()
     legs = set(x.strip() for x in args.legs.split(",") if x.strip())
 
@@ -267,6 +267,7 @@ def headline_leg(ctx):
     P = max(SEQ_LEN, args.pairs // SEQ_LEN * SEQ_LEN)
     maps = euroc_maps()
     raw_l, raw_r = stereo_chunks(ctx["rank"], maps)
+    ctx["chunks"] = (raw_l, raw_r)
     nu = len(raw_l)
     il = np.stack([raw_l[i % nu] for i in range(P)])
     ir = np.stack([raw_r[i % nu] for i in range(P)])
@@ -737,17 +738,128 @@ def window_ate(w, kf_Tcw):
 # ------------------------------------------------------------------------------------------
 # track: configs[4] — the per-sequence stereo tracking chain
 # ------------------------------------------------------------------------------------------
+def pingpong(n, steps):
+    """Frame index of step k walking 0..n-1..0.. (a continuous path over n rendered frames)."""
+    period = 2 * (n - 1)
+    return [k % period if k % period < n else period - k % period for k in range(steps)]
+
+
 def track_leg(ctx):
-    try:
-        from slamhot import tracker  # noqa: F401
-    except ImportError:
-        return {"skipped": "tracker not built"}
-    return tracker_bench(ctx)
+    """configs[4]: per-sequence stereo tracking (slamhot_tracker_*): S sequences per GPU advance in
+    lock-step, one raw stereo frame each per step, through the whole device-resident chain
+    (remap x2, extract x2, stereo, BoW + SearchByBoW vs the reference KF, PoseOptimization,
+    SearchLocalPoints, PoseOptimization, keyframe insertion).  Sequence s replays rendered chunk
+    s % N_SEQ back and forth (a continuous path).  value = sequence-frames/s of the whole job."""
+    import torch
+
+    import slamhot
+    from slamhot import ate
+    from slamhot import dist as sdist
+    from slamhot import synth
+    args, device, dist, lr = ctx["args"], ctx["device"], ctx["dist"], ctx["local_rank"]
+    S, K = args.track_seqs, args.track_frames
+    W, H = 752, 480
+    maps = euroc_maps()
+    raw_l, raw_r = ctx.get("chunks") or stereo_chunks(ctx["rank"], maps)
+    voc_arrays = sdist.broadcast_arrays(dist, device, synth.vocab(10, 6, 0) if ctx["rank"] == 0 else None)
+    voc = slamhot.Vocabulary(*voc_arrays, k=10, L=6, device=lr)
+    cam = (np.float32(synth.EUROC_STEREO["fx"]), np.float32(synth.EUROC_STEREO["fx"]), np.float32(367.4517211914062),
+           np.float32(252.2008514404297), np.float32(synth.EUROC_STEREO["bf"]))
+    # device frames: d_l[f] holds frame f of every sequence
+    d_l, d_r = [], []
+    for f in range(SEQ_LEN):
+        idx = [(s % N_SEQ) * SEQ_LEN + f for s in range(S)]
+        d_l.append(torch.from_numpy(np.ascontiguousarray(raw_l[idx])).to(device))
+        d_r.append(torch.from_numpy(np.ascontiguousarray(raw_r[idx])).to(device))
+    order = pingpong(SEQ_LEN, K)
+    warm = slamhot.Tracker(voc, S, cam, maps=maps, device=lr)
+    for f in order[: min(K, 2 * SEQ_LEN)]:
+        warm.step_device(d_l[f].data_ptr(), d_r[f].data_ptr())
+    warm.records()
+    warm.close()
+    T = slamhot.Tracker(voc, S, cam, maps=maps, device=lr)
+    recs = []
+
+    def step(k):
+        f = order[k]
+        T.step_device(d_l[f].data_ptr(), d_r[f].data_ptr())
+
+    elapsed = timed_region(dist, device, step, K)
+    # a second pass for the per-step records (same inputs, fresh tracker): lost / keyframe counts,
+    # inliers and the trajectory of sequence 0 for the ATE
+    T2 = slamhot.Tracker(voc, S, cam, maps=maps, device=lr)
+    for k in range(K):
+        f = order[k]
+        T2.step_device(d_l[f].data_ptr(), d_r[f].data_ptr())
+        recs.append(T2.records())
+    T2.close()
+    T.close()
+    # configs[4] literally: ONE sequence on the GPU (its frame latency bounds a live camera)
+    T1 = slamhot.Tracker(voc, 1, cam, maps=maps, device=lr)
+    for k in range(min(K, 4)):
+        T1.step_device(d_l[order[k]][:1].data_ptr(), d_r[order[k]][:1].data_ptr())
+    T1.records()
+    T1.close()
+    T1 = slamhot.Tracker(voc, 1, cam, maps=maps, device=lr)
+    el1 = timed_region(None, device, lambda k: T1.step_device(d_l[order[k]][:1].data_ptr(),
+                                                              d_r[order[k]][:1].data_ptr()), K)
+    T1.close()
+    voc.close()
+    el, units = sdist.reduce_run(dist, device, elapsed, float(S * K))
+    lost = sum(r["lost"] for rr in recs[1:] for r in rr)
+    kfs = sum(r["is_keyframe"] for rr in recs for r in rr)
+    inl = float(np.mean([r["n_inl"] for rr in recs[1:] for r in rr]))
+    # ATE of sequence 0 (chunk 0): centres of the tracked poses vs ground truth (SE3 + scale
+    # alignment of evaluate_ate_scale.py); the tracker starts at the identity, GT at its frame 0
+    gt = synth.sequence_poses(101 + 17 * ctx["rank"], SEQ_LEN)
+    est_c = np.stack([-(r[0]["Tcw"][:3, :3].T.astype(np.float64) @ r[0]["Tcw"][:3, 3]) for r in recs])
+    gt_c = np.stack([-(gt[f][:3, :3].T @ gt[f][:3, 3]) for f in order])
+    _, _, _, _, err, _ = ate.align(est_c.T, gt_c.T)
+    out = {
+        "metric": "stereo tracking sequence-frames/s (configs[4] per GPU)",
+        "value": round(units / el, 2),
+        "unit": "sequence-frames/s",
+        "dtype": "u8 / f64",
+        "config": {"workload": f"{S} stereo sequences per GPU in lock-step, {K} raw 752x480 frames each (rendered room, "
+                               f"EuRoC calibration): remap x2, ORBextractor x2 (1200), ComputeStereoMatches, ComputeBoW + "
+                               f"SearchByBoW vs reference KF, PoseOptimization, SearchLocalPoints, PoseOptimization, "
+                               f"NeedNewKeyFrame / CreateNewKeyFrame — all device-resident",
+                   "parallelism": f"sequence-sharded x{ctx['world']}"},
+        "ms_per_step": round(el / K * 1e3, 3),
+        "per_sequence_frames_per_s": round(K / el, 1),
+        "single_sequence": {"frames_per_s": round(K / el1, 1), "ms_per_frame": round(el1 / K * 1e3, 3),
+                            "note": "one sequence alone on the GPU (nseq = 1), same frames"},
+        "lost_frames": int(lost), "keyframes": int(kfs), "mean_inliers": round(inl, 1),
+        "ate_seq0_m": round(float(np.sqrt(np.mean(err * err))), 5),
+    }
+    if ctx["cpu"]:
+        out["cpu_baseline"] = track_cpu(raw_l, raw_r, maps, voc_arrays, order[: 2 * SEQ_LEN])
+    return out
 
 
-def tracker_bench(ctx):
-    from slamhot import tracker
-    return tracker.bench(ctx, ROOT)
+def track_cpu(raw_l, raw_r, maps, voc_arrays, order):
+    """The oracle chain (tests/track_oracle.py) on the host cores, one sequence per thread."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import track_oracle as to
+    P = to.params()
+    cores = host_cores()
+
+    def run(c):
+        st = to.SeqState()
+        base = (c % N_SEQ) * SEQ_LEN
+        for f in order:
+            to.step(P, voc_arrays, maps, st, raw_l[base + f], raw_r[base + f])
+        return len(order)
+
+    run(0)  # warm-up
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(cores) as pool:
+        frames = sum(pool.map(run, range(cores)))
+    dt = time.perf_counter() - t0
+    return {"value": round(frames / dt, 2), "unit": "sequence-frames/s", "cores": cores, "kind": "port",
+            "cpu": cpu_model(),
+            "sample": f"{cores} sequences x {len(order)} stereo frames, one sequence per thread: the oracle chain "
+                      f"tests/track_oracle.py (oracle remap, extract, stereo, BoW, PoseOptimization, SearchLocalPoints)"}
 
 
 if __name__ == "__main__":

@@ -102,3 +102,64 @@ def test_two_rank_gloo_matches_single_process():
     for o in out:  # rank 1 received exactly rank 0's tables
         assert o[7] == sdist.digest(*ref)
         assert o[8] == [(np.asarray(a).dtype.str, np.asarray(a).shape) for a in ref]
+
+
+# ---- configs[4]: whole stereo sequences sharded across ranks (bench.py track leg)
+N_SEQS, SEQ_FRAMES = 3, 3
+
+
+def _identity_maps(w=752, h=480):
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float32)
+    return [(xx, yy), (xx, yy)]
+
+
+def _sequence_digest(idx):
+    """The oracle tracking chain (tests/track_oracle.py) over sequences `idx`: per frame the
+    counts and the pose, folded into (frames, digest)."""
+    import track_oracle as to
+    P = to.params()
+    voc = synth.vocab(4, 3, 7)
+    maps = _identity_maps()
+    recs, frames = [], 0
+    for s in idx:
+        L, R, _ = synth.stereo_sequence(401 + s, SEQ_FRAMES)
+        st = to.SeqState()
+        for f in range(SEQ_FRAMES):
+            r = to.step(P, voc, maps, st, L[f], R[f])
+            recs.append(np.array([r["n"], r["stereo"], r["nbow"], r["ninl1"], r["nlocal"], r["ninl2"], r["is_kf"],
+                                  r["lost"]], np.int32))
+            recs.append(r["Tcw"].astype(np.float32))
+            frames += 1
+    return frames, sdist.digest(*recs) if recs else 0
+
+
+def _seq_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sidx = sdist.shard(N_SEQS, rank, world)
+    frames, dig = _sequence_digest(sidx)
+    _, units = sdist.reduce_run(dist, "cpu", 1.0, float(frames))
+    g = sdist.gather_digests(dist, "cpu", world, frames, dig)
+    q.put((rank, units, g))
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_sequence_sharding():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_seq_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=600) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for o in out:
+        assert o[1] == N_SEQS * SEQ_FRAMES and o[2] == out[0][2]
+    frames, dig = _sequence_digest(range(N_SEQS))
+    g = out[0][2]
+    assert sum(c for c, _ in g) == frames
+    assert np.bitwise_xor.reduce(np.array([d for _, d in g], np.int64)) == dig
