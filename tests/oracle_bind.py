@@ -7,7 +7,26 @@ from pathlib import Path
 import numpy as np
 
 ROOT = Path(__file__).resolve().parents[1]
-LIB_PATH = ROOT / "oracle" / "build" / "liboracle.so"
+
+
+def _lib_path():
+    """The AVX-512 build (-march=x86-64-v4, what -march=native gives on the GPU box's EPYC) where
+    the CPU has it, else the x86-64-v3 build; SLAMHOT_ORACLE_LIB overrides."""
+    import os
+    env = os.environ.get("SLAMHOT_ORACLE_LIB")
+    if env:
+        return Path(env)
+    v4 = ROOT / "oracle" / "build" / "liboracle_v4.so"
+    try:
+        flags = open("/proc/cpuinfo").read()
+        if v4.exists() and " avx512f " in flags and " avx512bw " in flags and " avx512vl " in flags:
+            return v4
+    except OSError:
+        pass
+    return ROOT / "oracle" / "build" / "liboracle.so"
+
+
+LIB_PATH = _lib_path()
 
 
 class KeyPoint(C.Structure):

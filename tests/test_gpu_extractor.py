@@ -112,3 +112,33 @@ def test_low_contrast_minth_retry(gpu_extractor_factory):
     ko, do, mo = ob.extract(img)
     assert len(ko) > 500
     _compare(kg, dg, mg, ko, do, mo)
+
+
+def test_kitti_stereo_settings(gpu_extractor_factory):
+    """Examples/Stereo/KITTI04-12.yaml:21-54: 1241 x 376, 2000 features, iniThFAST 12, minThFAST 7."""
+    ex = gpu_extractor_factory(nfeatures=2000, scaleFactor=1.2, nlevels=8, iniThFAST=12, minThFAST=7,
+                               max_size=(1241, 376))
+    for seed in (3, 4):
+        img = synth.frame(300 + seed, 1241, 376)
+        kg, dg, mg = ex(img)
+        ko, do, mo = ob.extract(img, ob.params(nfeatures=2000, ini=12, mn=7))
+        _compare(kg, dg, mg, ko, do, mo)
+        assert len(kg) > 1800
+
+
+@pytest.mark.parametrize("scale,levels,nf", [(1.3, 6, 1000), (1.15, 10, 1500), (2.0, 3, 800), (1.2, 1, 500)])
+def test_non_default_pyramid(gpu_extractor_factory, scale, levels, nf):
+    """Other ORBextractor.scaleFactor / nLevels: the level geometry, per-level feature split and
+    the scale tables follow the parameters (ORBextractor.cc:408-468, 1152-1177)."""
+    ex = gpu_extractor_factory(nfeatures=nf, scaleFactor=scale, nlevels=levels, max_size=(752, 480))
+    img = synth.frame(410 + levels, 752, 480)
+    kg, dg, mg = ex(img)
+    p = ob.params(nfeatures=nf, scale=scale, nlevels=levels)
+    ko, do, mo = ob.extract(img, p)
+    _compare(kg, dg, mg, ko, do, mo)
+    sc, isc, s2, is2, nfl = ob.levels(p)
+    assert np.array_equal(ex.GetScaleFactors(), sc) and np.array_equal(ex.GetInverseScaleSigmaSquares(), is2)
+    assert np.array_equal(ex.GetFeaturesPerLevel(), nfl)
+    ref = ob.pyramid(img, p)
+    for l in range(levels):
+        assert np.array_equal(ex.pyramid_level(l), ref[l]), l

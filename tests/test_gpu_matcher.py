@@ -269,3 +269,42 @@ def test_bow_match_batch_general_pairs(gpu_vocab, vocab_arrays):
         assert np.array_equal(b2a[p, : ns[b]], b2a_o)
     assert n_general == expect_general and n_general >= 2
     m.close()
+
+
+def _write_vocab_text(path, parent, is_leaf, desc, weight, k, L, header=None):
+    """ORBvoc.txt layout (TemplatedVocabulary.h:1350-1436): "k L scoring weighting", then one line
+    per node after the root: parent, isLeaf, the 32 descriptor bytes (FORB::toString), weight."""
+    lines = [header or f"{k} {L} 0 0"]
+    for i in range(1, len(parent)):
+        lines.append(f"{int(parent[i])} {int(is_leaf[i])} " + " ".join(str(int(b)) for b in desc[i]) +
+                     f" {float(weight[i])!r}")
+    path.write_text("\n".join(lines) + "\n")  # ORBvoc.txt ends with a newline
+
+
+def test_vocab_load_text_equals_tables(tmp_path):
+    """slamhot_vocab_load_text on a synthetic vocabulary written in the ORBvoc.txt format gives the
+    same tree as the tables it was written from: identical transform (word, weight, node) for
+    extracted descriptors; a malformed header is rejected like the reference (k > 20)."""
+    import slamhot
+    par, leaf, dn, wn = synth.vocab(10, 4, 3)
+    p = tmp_path / "voc.txt"
+    _write_vocab_text(p, par, leaf, dn, wn, 10, 4)
+    vt = slamhot.Vocabulary(path=str(p))
+    va = slamhot.Vocabulary(par, leaf, dn, wn, k=10, L=4)
+    assert (vt.k, vt.L, vt.n_nodes, vt.n_words) == (va.k, va.L, va.n_nodes, va.n_words)
+    _, d, _ = ob.extract(synth.frame(77, 640, 480))
+    for lv in (0, 2, 4):
+        a = vt.transform(d, lv)
+        b = va.transform(d, lv)
+        for x, y in zip(a, b):
+            assert np.array_equal(x, y)
+    # and both equal the oracle's transform of the same tree
+    w, wt, nid = ob.vocab_transform(par, leaf, dn, wn, 4, d, 2)
+    a = vt.transform(d, 2)
+    assert np.array_equal(a[0], w) and np.array_equal(a[1], wt) and np.array_equal(a[2], nid)
+    vt.close()
+    va.close()
+    bad = tmp_path / "bad.txt"
+    _write_vocab_text(bad, par, leaf, dn, wn, 10, 4, header="21 4 0 0")
+    with pytest.raises(slamhot.SlamError):
+        slamhot.Vocabulary(path=str(bad))
