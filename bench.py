@@ -158,7 +158,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--legs", default="headline,extract,lba,pose,track",
+    ap.add_argument("--legs", default="headline,extract,lba,pose,track,localmap",
                     help="comma list of legs to run (headline = configs[2] extract+match)")
     ap.add_argument("--pairs", type=int, default=128, help="headline: stereo frames per GPU per step")
     ap.add_argument("--inflight", type=int, default=3, help="batches in flight (handles / streams) per leg")
@@ -173,6 +173,7 @@ def main():
     ap.add_argument("--lba-calls", type=int, default=3)
     ap.add_argument("--lba-inflight", type=int, default=3, help="LBA solver handles driven concurrently")
     ap.add_argument("--pose-frames", type=int, default=512, help="PoseOptimization frames per GPU per call")
+    ap.add_argument("--localmap-frames", type=int, default=256, help="localmap leg: frames per call")
     ap.add_argument("--track-seqs", type=int, default=64, help="track leg: sequences per GPU (lock-step)")
     ap.add_argument("--track-frames", type=int, default=56, help="track leg: steps (frames per sequence)")
     args = ap.parse_args()
@@ -218,6 +219,8 @@ def main():
         result["pose"] = pose_leg(ctx)
     if "track" in legs and args.track_seqs > 0:
         result["track"] = track_leg(ctx)
+    if "localmap" in legs and args.localmap_frames > 0:
+        result["localmap"] = localmap_leg(ctx)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:
@@ -598,6 +601,71 @@ def pose_leg(ctx):
                                "sample": f"{len(work)} frames on {cores} threads (one frame per task); "
                                          f"oracle/pose_oracle.cpp -O3"}
     S.close()
+    return out
+
+
+# ------------------------------------------------------------------------------------------
+# localmap: batched Tracking::SearchLocalPoints (isInFrustum + SearchByProjection)
+# ------------------------------------------------------------------------------------------
+def localmap_leg(ctx):
+    """Tracking::SearchLocalPoints frames/s through slamhot_search_local_points_batch: P frames per
+    call (1200 features, ~1200 local MapPoints each: back-projected features plus points behind,
+    outside, too near / far, at grazing angles, already seen or bad), host buffers in and out —
+    the drop-in call, PCIe included."""
+    import torch
+
+    import slamhot
+    from slamhot import dist as sdist
+    sys.path.insert(0, str(ROOT / "tests"))
+    import scenes
+    args, device, dist = ctx["args"], ctx["device"], ctx["dist"]
+    P = args.localmap_frames
+    uniq = []
+    for seed in sdist.shard(16 * ctx["world"], ctx["rank"], ctx["world"]):
+        S = scenes.scene(1000 + seed)
+        fv, keep = scenes.frame_view(S)
+        geom, desc = scenes.local_map_geom(S)
+        uniq.append((fv, keep, geom, desc))
+    views = [uniq[i % len(uniq)][0] for i in range(P)]
+    geoms = [uniq[i % len(uniq)][2] for i in range(P)]
+    descs = [uniq[i % len(uniq)][3] for i in range(P)]
+    m = slamhot.ORBmatcher(0.8, device=ctx["local_rank"])
+    m.SearchLocalPoints_batch(views, geoms, descs)
+    calls = 5
+    res = []
+    elapsed = timed_region(dist, device, lambda i: res.append(m.SearchLocalPoints_batch(views, geoms, descs)), calls)
+    el, total = sdist.reduce_run(dist, device, elapsed, float(P * calls))
+    out = {
+        "metric": "Tracking::SearchLocalPoints frames/s (batched, host buffers)",
+        "value": round(total / el, 1),
+        "unit": "frames/s",
+        "dtype": "f32 / u8",
+        "config": {"workload": f"{P} frames per call, 1200 features and ~{int(np.mean([len(g) for g in geoms]))} local "
+                               f"MapPoints each, th 1, nnratio 0.8 (slamhot_search_local_points_batch)",
+                   "parallelism": f"frame-sharded x{ctx['world']}"},
+        "ms_per_call": round(el / calls * 1e3, 3),
+        "mean_matches": round(float(np.mean([r[0] for r in res[-1]])), 1),
+    }
+    if ctx["cpu"]:
+        import oracle_bind as ob
+        cores = host_cores()
+
+        def one(i):
+            fv, _, g, d = uniq[i % len(uniq)]
+            _, tr = ob.is_in_frustum(fv, g, 0.5)
+            ob.search_by_projection_local(fv, tr, d, 0.8, 1.0, False, 50.0)
+            return 1
+
+        work = list(range(64 * cores))
+        one(0)
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(cores) as pool:
+            n = sum(pool.map(one, work))
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(n / dt, 1), "unit": "frames/s", "cores": cores, "kind": "port",
+                               "cpu": cpu_model(),
+                               "sample": f"{n} frames on {cores} threads: oracle isInFrustum + SearchByProjection"}
+    m.close()
     return out
 
 

@@ -266,6 +266,16 @@ slam_status slamhot_search_local_points(slam_matcher* m, const slam_frame_view* 
                                         float nnratio, float th, int far_points, float th_far,
                                         slam_mp_track* track, int* n_to_match, int32_t* f_match, int* nmatches);
 
+/* Batched form of slamhot_search_local_points: nframes independent (Frame, local map) problems
+ * (frames[f] with n_mp[f] MapPoints mps[f] / mp_desc[f]) in one upload and two launches (one
+ * isInFrustum grid row and one SearchByProjection workgroup per frame).  Outputs per frame:
+ * f_match[f] (frames[f].n entries), n_to_match[f], nmatches[f]; identical to nframes single calls. */
+slam_status slamhot_search_local_points_batch(slam_matcher* m, int nframes, const slam_frame_view* frames,
+                                              const int32_t* n_mp, const slam_mp_geom* const* mps,
+                                              const uint8_t* const* mp_desc, float view_cos_limit, float nnratio,
+                                              float th, int far_points, float th_far, int32_t* const* f_match,
+                                              int32_t* n_to_match, int32_t* nmatches);
+
 /* The previous Frame for SearchByProjection(Frame&, const Frame& LastFrame, th, bMono)
  * (ORBmatcher.cc:2173-2389): per last-frame feature its MapPoint (has_mp, outlier flag,
  * world position, descriptor, Observations()>0) and keypoint octave/angle. */

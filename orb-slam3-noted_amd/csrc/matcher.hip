@@ -581,7 +581,18 @@ struct slam_matcher {
     Buf d_pair, d_a, d_b, d_out;
     // batched device path (slamhot_bow_match_batch_device)
     Buf b_word, b_weight, b_node, b_fv_id, b_fv_off, b_fv_feat, b_fv_n, b_pairs, b_devpairs, b_status, b_scratch;
+    uint8_t* h_stage = nullptr;  // pinned staging of the batched host-buffer calls
+    size_t h_cap = 0;
     std::mutex mu;
+    slam_status stage(size_t bytes) {
+        if (bytes <= h_cap) return SLAM_OK;
+        if (h_stage) (void)hipHostFree(h_stage);
+        h_stage = nullptr;
+        h_cap = 0;
+        if (hipHostMalloc((void**)&h_stage, bytes, hipHostMallocDefault) != hipSuccess) return SLAM_ENOMEM;
+        h_cap = bytes;
+        return SLAM_OK;
+    }
 };
 
 extern "C" {
@@ -755,6 +766,7 @@ void slamhot_matcher_destroy(slam_matcher* m) {
     for (Buf* b : {&m->b_word, &m->b_weight, &m->b_node, &m->b_fv_id, &m->b_fv_off, &m->b_fv_feat, &m->b_fv_n,
                    &m->b_pairs, &m->b_devpairs, &m->b_status, &m->b_scratch})
         b->release();
+    if (m->h_stage) (void)hipHostFree(m->h_stage);
     if (m->stream) (void)hipStreamDestroy(m->stream);
     delete m;
 }
@@ -1508,6 +1520,191 @@ extern "C" slam_status slamhot_search_local_points(slam_matcher* m, const slam_f
     SLAM_HIP_TRY(hipMemcpy(n_to_match, Fc.n_in_view, 4, hipMemcpyDeviceToHost));
     if (track && n_mp) SLAM_HIP_TRY(hipMemcpy(track, Fc.track, sizeof(slam_mp_track) * n_mp, hipMemcpyDeviceToHost));
     return SLAM_OK;
+}
+
+// Batched Tracking::SearchLocalPoints: nframes independent (Frame, local map) problems, every
+// frame's inputs staged into one host image and uploaded with one copy, one isInFrustum launch
+// (grid row per frame) and one SearchByProjection launch (workgroup per frame).
+extern "C" slam_status slamhot_search_local_points_batch(slam_matcher* m, int nframes, const slam_frame_view* frames,
+                                                         const int32_t* n_mp, const slam_mp_geom* const* mps,
+                                                         const uint8_t* const* mp_desc, float view_cos_limit,
+                                                         float nnratio, float th, int far_points, float th_far,
+                                                         int32_t* const* f_match, int32_t* n_to_match,
+                                                         int32_t* nmatches) {
+    if (!m || nframes < 0 || (nframes && (!frames || !n_mp || !mps || !mp_desc || !f_match || !n_to_match || !nmatches)))
+        return SLAM_EINVAL;
+    for (int f = 0; f < nframes; f++)
+        if (!frame_ok(&frames[f]) || !frames[f].Tcw || n_mp[f] < 0 || (n_mp[f] && (!mps[f] || !mp_desc[f])) ||
+            (frames[f].n && !f_match[f]))
+            return SLAM_EINVAL;
+    if (nframes == 0) return SLAM_OK;
+    // host image: per frame kps | uright | desc | state | grid | mps | mp_desc, then device-only
+    // scratch (track, queries, cand_off, cand, f_match, out, n_in_view, gstate)
+    struct Off {
+        size_t kps, ur, desc, st, cs, cf, mps, md, tr, q, co, cand, fm, out, niv, gs;
+        int cand_cap;
+        bool gstate;
+    };
+    std::vector<Off> O(nframes);
+    std::vector<std::vector<int32_t>> starts(nframes), feats(nframes);
+    size_t off = 0, lds = 0;
+    auto take = [&](size_t bytes) {
+        const size_t o = off;
+        off += (bytes + 255) & ~(size_t)255;
+        return o;
+    };
+    for (int f = 0; f < nframes; f++) {
+        const slam_frame_view& F = frames[f];
+        const int nq = n_mp[f];
+        build_grid_csr(&F, starts[f], feats[f]);
+        Off& o = O[f];
+        o.kps = take(sizeof(slam_keypoint) * F.n);
+        o.ur = take(F.uright ? 4 * (size_t)F.n : 0);
+        o.desc = take(32 * (size_t)F.n);
+        o.st = take(F.mp_state ? (size_t)F.n : 0);
+        o.cs = take(4 * starts[f].size());
+        o.cf = take(4 * feats[f].size());
+        o.mps = take(sizeof(slam_mp_geom) * nq);
+        o.md = take(32 * (size_t)nq);
+    }
+    const size_t calls_off = take(sizeof(DevProjCall) * nframes), fc_off = take(sizeof(FrustumCall) * nframes);
+    const size_t in_bytes = off;  // the host image: inputs and call records
+    for (int f = 0; f < nframes; f++) {  // device-only scratch
+        const int nq = n_mp[f];
+        Off& o = O[f];
+        o.tr = take(sizeof(slam_mp_track) * std::max(1, nq));
+        o.q = take(sizeof(ProjQuery) * std::max(1, nq));
+        o.co = take(4 * (size_t)(nq + 1));
+        o.cand_cap = std::max(4096, nq * 64);
+        o.cand = take(4 * (size_t)o.cand_cap);
+        const size_t need = projection_lds_bytes(frames[f].n, nq);
+        o.gstate = need == 0;
+        o.gs = take(o.gstate ? 4 * (2 * (size_t)frames[f].n + 2 * (size_t)nq) : 0);
+        if (!o.gstate) lds = std::max(lds, need);
+    }
+    // the outputs of every frame in one contiguous tail: one copy back
+    const size_t res_off = off;
+    for (int f = 0; f < nframes; f++) {
+        O[f].fm = take(4 * (size_t)std::max(1, frames[f].n));
+        O[f].out = take(16);
+        O[f].niv = take(4);
+    }
+    const size_t total = off;
+    std::lock_guard<std::mutex> g(m->mu);
+    SLAM_HIP_TRY(hipSetDevice(m->device));
+    slam_status st;
+    if ((st = m->d_a.ensure(total))) return st;
+    uint8_t* D = m->d_a.as<uint8_t>();
+    // inputs and results through one pinned staging buffer: [inputs | results]
+    if ((st = m->stage(in_bytes + (total - res_off)))) return st;
+    uint8_t* Hs = m->h_stage;
+    uint8_t* Rs = m->h_stage + in_bytes;
+    struct View {
+        uint8_t* p;
+        uint8_t* data() { return p; }
+    } H{Hs}, R{Rs};
+    for (int f = 0; f < nframes; f++) {
+        const slam_frame_view& F = frames[f];
+        const Off& o = O[f];
+        const int nq = n_mp[f];
+        auto put = [&](size_t at, const void* src, size_t bytes) {
+            if (src && bytes) std::memcpy(H.data() + at, src, bytes);
+        };
+        put(o.kps, F.kps_un, sizeof(slam_keypoint) * F.n);
+        put(o.ur, F.uright, F.uright ? 4 * (size_t)F.n : 0);
+        put(o.desc, F.desc, 32 * (size_t)F.n);
+        put(o.st, F.mp_state, F.mp_state ? (size_t)F.n : 0);
+        put(o.cs, starts[f].data(), 4 * starts[f].size());
+        put(o.cf, feats[f].data(), 4 * feats[f].size());
+        put(o.mps, mps[f], sizeof(slam_mp_geom) * nq);
+        put(o.md, mp_desc[f], 32 * (size_t)nq);
+        DevProjCall C{};
+        fill_frame(C, &F);
+        C.F.n = F.n;
+        C.F.kps = (const slam_keypoint*)(D + o.kps);
+        C.F.uright = F.uright ? (const float*)(D + o.ur) : nullptr;
+        C.F.desc = D + o.desc;
+        C.F.state = F.mp_state ? (const int8_t*)(D + o.st) : nullptr;
+        C.F.cell_start = (const int32_t*)(D + o.cs);
+        C.F.cell_feat = (const int32_t*)(D + o.cf);
+        C.mode = kProjLocal;
+        C.nq = nq;
+        C.mps = (const slam_mp_track*)(D + o.tr);
+        C.th = th;
+        C.th_far = th_far;
+        C.far_points = far_points;
+        C.nnratio = nnratio;
+        C.th_dist = 100;
+        C.check_ori = 0;
+        C.queries = (ProjQuery*)(D + o.q);
+        C.qdesc = D + o.md;
+        C.cand_off = (int32_t*)(D + o.co);
+        C.cand = (uint32_t*)(D + o.cand);
+        C.cand_cap = o.cand_cap;
+        C.f_match = (int32_t*)(D + o.fm);
+        C.out = (int32_t*)(D + o.out);
+        C.gstate = o.gstate ? (int32_t*)(D + o.gs) : nullptr;
+        std::memcpy(H.data() + calls_off + sizeof(DevProjCall) * f, &C, sizeof(C));
+        FrustumCall Fc{};
+        const float* T = F.Tcw;
+        for (int r = 0; r < 3; r++) {
+            for (int c = 0; c < 3; c++) Fc.R[3 * r + c] = T[4 * r + c];
+            Fc.t[r] = T[4 * r + 3];
+            const double acc = (double)T[r] * T[3] + (double)T[4 + r] * T[7] + (double)T[8 + r] * T[11];
+            Fc.Ow[r] = (float)(-1.0 * acc);
+        }
+        Fc.min_x = F.min_x;
+        Fc.max_x = F.max_x;
+        Fc.min_y = F.min_y;
+        Fc.max_y = F.max_y;
+        Fc.fx = F.fx;
+        Fc.fy = F.fy;
+        Fc.cx = F.cx;
+        Fc.cy = F.cy;
+        Fc.bf = F.bf;
+        Fc.log_scale = F.log_scale;
+        Fc.view_cos_limit = view_cos_limit;
+        Fc.nlevels = F.nlevels;
+        Fc.n = nq;
+        Fc.mps = (const slam_mp_geom*)(D + o.mps);
+        Fc.track = (slam_mp_track*)(D + o.tr);
+        Fc.n_in_view = (int32_t*)(D + o.niv);
+        std::memcpy(H.data() + fc_off + sizeof(FrustumCall) * f, &Fc, sizeof(Fc));
+    }
+    int max_nq = 1;
+    for (int f = 0; f < nframes; f++) max_nq = std::max(max_nq, n_mp[f]);
+    hipStream_t S = m->stream;
+    SLAM_HIP_TRY(hipMemcpyAsync(D, H.data(), in_bytes, hipMemcpyHostToDevice, S));
+    SLAM_HIP_TRY(hipMemsetAsync(D + res_off, 0, total - res_off, S));  // out[] and n_in_view start at 0
+    SLAM_HIP_TRY(launch_is_in_frustum((const FrustumCall*)(D + fc_off), nframes, max_nq, S));
+    SLAM_HIP_TRY(launch_search_by_projection((const DevProjCall*)(D + calls_off), nframes, lds, S));
+    // results: per frame f_match, out[4], n_in_view (one copy of the whole image back)
+    SLAM_HIP_TRY(hipMemcpyAsync(R.data(), D + res_off, total - res_off, hipMemcpyDeviceToHost, S));
+    SLAM_HIP_TRY(hipStreamSynchronize(S));
+    std::vector<int> redo;
+    for (int f = 0; f < nframes; f++) {
+        const Off& o = O[f];
+        const int32_t* out = (const int32_t*)(R.data() + (o.out - res_off));
+        if (out[1] == 1) {  // candidate overflow: this frame again through the single-call path
+            redo.push_back(f);
+            continue;
+        }
+        nmatches[f] = out[0];
+        n_to_match[f] = *(const int32_t*)(R.data() + (o.niv - res_off));
+        if (frames[f].n) std::memcpy(f_match[f], R.data() + (o.fm - res_off), 4 * (size_t)frames[f].n);
+    }
+    m->mu.unlock();
+    slam_status rs = SLAM_OK;
+    for (int f : redo) {
+        int n = 0, ntm = 0;
+        rs = slamhot_search_local_points(m, &frames[f], n_mp[f], mps[f], mp_desc[f], view_cos_limit, nnratio, th,
+                                         far_points, th_far, nullptr, &ntm, f_match[f], &n);
+        if (rs != SLAM_OK) break;
+        nmatches[f] = n;
+        n_to_match[f] = ntm;
+    }
+    m->mu.lock();  // the guard unlocks on return
+    return rs;
 }
 
 extern "C" slam_status slamhot_search_by_projection_last(slam_matcher* m, const slam_frame_view* F,

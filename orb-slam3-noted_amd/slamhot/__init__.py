@@ -435,6 +435,31 @@ def _matcher_methods():
                                             _ptr(tr), C.byref(nt), _ptr(fm), C.byref(nm)), "search_local_points")
         return nm.value, fm, nt.value, tr
 
+    def SearchLocalPoints_batch(self, frame_views, mps_list, desc_list, th=1.0, bFarPoints=False, thFarPoints=50.0,
+                                viewingCosLimit=0.5):
+        """Batched Tracking::SearchLocalPoints (slamhot_search_local_points_batch): lists of frame
+        views / MP_GEOM arrays / descriptors.  Returns [(nmatches, f_match, nToMatch)] per frame."""
+        L = lib()
+        if not getattr(L, "_slpb_ready", False):
+            L.slamhot_search_local_points_batch.argtypes = [P, I, P, P, P, P, C.c_float, C.c_float, C.c_float, I,
+                                                            C.c_float, P, P, P]
+            L._slpb_ready = True
+        nf = len(frame_views)
+        fv = (FrameView * nf)(*frame_views)
+        mps = [np.ascontiguousarray(m, MP_GEOM_DTYPE) for m in mps_list]
+        dsc = [np.ascontiguousarray(d, np.uint8) for d in desc_list]
+        fms = [np.full(v.n, -1, np.int32) for v in frame_views]
+        nmp = np.array([len(m) for m in mps], np.int32)
+        pm = (P * nf)(*[m.ctypes.data for m in mps])
+        pd = (P * nf)(*[d.ctypes.data for d in dsc])
+        pf = (P * nf)(*[f.ctypes.data for f in fms])
+        nt = np.zeros(nf, np.int32)
+        nm = np.zeros(nf, np.int32)
+        check(L.slamhot_search_local_points_batch(self._h, nf, fv, _ptr(nmp), pm, pd, viewingCosLimit, self.mfNNratio,
+                                                  th, int(bFarPoints), thFarPoints, pf, _ptr(nt), _ptr(nm)),
+              "search_local_points_batch")
+        return [(int(nm[i]), fms[i], int(nt[i])) for i in range(nf)]
+
     def SearchByProjection_last(self, frame_view, last_view, th, bMono):
         """int SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, th, bMono)."""
         fm = np.full(frame_view.n, -1, np.int32)
@@ -479,6 +504,7 @@ def _matcher_methods():
     ORBmatcher.bow_match_batch_status = bow_match_batch_status
     ORBmatcher.SearchByProjection_local = SearchByProjection_local
     ORBmatcher.SearchLocalPoints = SearchLocalPoints
+    ORBmatcher.SearchLocalPoints_batch = SearchLocalPoints_batch
     ORBmatcher.SearchByProjection_last = SearchByProjection_last
     ORBmatcher.SearchByProjection_kf = SearchByProjection_kf
 

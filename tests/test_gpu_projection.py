@@ -94,3 +94,27 @@ def test_local_map_above_lds_cap():
     m.close()
     assert ng == no and ng > 50
     assert np.array_equal(fg, fo)
+
+
+def test_search_local_points_batch():
+    """slamhot_search_local_points_batch: many (Frame, local map) problems in one upload and two
+    launches equal the single calls and the oracle, including a local map above the LDS budget."""
+    import slamhot
+    views, keeps, geoms, descs = [], [], [], []
+    for seed in range(20, 28):
+        S = scenes.scene(seed)
+        fv, keep = scenes.frame_view(S)
+        geom, desc = scenes.local_map_geom(S, n_extra=300 if seed != 25 else 12000)
+        views.append(fv)
+        keeps.append((S, keep))
+        geoms.append(geom)
+        descs.append(desc)
+    m = slamhot.ORBmatcher(0.8)
+    out = m.SearchLocalPoints_batch(views, geoms, descs, 1.0, False, 20.0)
+    for i, (nm, fm, nt) in enumerate(out):
+        ns, fs, nts, _ = m.SearchLocalPoints(views[i], geoms[i], descs[i], 1.0, False, 20.0)
+        assert (nm, nt) == (ns, nts) and np.array_equal(fm, fs), i
+        nto, tro = ob.is_in_frustum(views[i], geoms[i], 0.5)
+        no, fo = ob.search_by_projection_local(views[i], tro, descs[i], 0.8, 1.0, False, 20.0)
+        assert nt == nto and nm == no and np.array_equal(fm, fo), i
+    m.close()
