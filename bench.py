@@ -169,9 +169,9 @@ def main():
     ap.add_argument("--unique", type=int, default=256, help="extract leg: distinct synthetic frames per rank")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=384)
-    ap.add_argument("--lba-windows", type=int, default=64, help="LBA windows per GPU per call")
+    ap.add_argument("--lba-windows", type=int, default=128, help="LBA windows per GPU per call")
     ap.add_argument("--lba-calls", type=int, default=3)
-    ap.add_argument("--lba-inflight", type=int, default=3, help="LBA solver handles driven concurrently")
+    ap.add_argument("--lba-inflight", type=int, default=4, help="LBA solver handles driven concurrently")
     ap.add_argument("--pose-frames", type=int, default=512, help="PoseOptimization frames per GPU per call")
     ap.add_argument("--localmap-frames", type=int, default=256, help="localmap leg: frames per call")
     ap.add_argument("--track-seqs", type=int, default=64, help="track leg: sequences per GPU (lock-step)")
@@ -185,13 +185,22 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # one GPU per rank; SLAMHOT_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share
+    # cuda:(local_rank mod device_count), collectives on host copies) — the driver's runs use nccl
+    backend = os.environ.get("SLAMHOT_BENCH_BACKEND", "nccl")
+    ndev = max(torch.cuda.device_count(), 1)
+    gpu = local_rank % ndev if backend == "gloo" else local_rank
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    device = torch.device("cuda", local_rank)
+        torch.cuda.set_device(gpu)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group("gloo")
+    device = torch.device("cuda", gpu)
     torch.cuda.set_device(device)
+    local_rank = gpu
     ctx = dict(args=args, rank=rank, world=world, local_rank=local_rank, dist=dist, device=device,
                cpu=(rank == 0 and world == 1 and not args.no_cpu_baseline))
 

@@ -27,11 +27,20 @@ def digest(*arrays) -> int:
     return int(acc & np.uint64((1 << 62) - 1))
 
 
+def _coll_device(dist, device):
+    """Collectives run on `device` under nccl, on the host under gloo (bench rehearsals)."""
+    try:
+        return "cpu" if dist.get_backend() == "gloo" else device
+    except Exception:
+        return device
+
+
 def reduce_run(dist, device, elapsed_s: float, units: float):
     """(max elapsed over ranks, total units over ranks)."""
     import torch
     if dist is None:
         return elapsed_s, units
+    device = _coll_device(dist, device)
     t = torch.tensor([elapsed_s], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     u = torch.tensor([units], dtype=torch.float64, device=device)
@@ -44,6 +53,7 @@ def gather_digests(dist, device, world: int, count: int, dig: int):
     import torch
     if dist is None:
         return [(count, dig)]
+    device = _coll_device(dist, device)
     g = [torch.zeros(2, dtype=torch.int64, device=device) for _ in range(world)]
     dist.all_gather(g, torch.tensor([count, dig], dtype=torch.int64, device=device))
     return [(int(x[0].item()), int(x[1].item())) for x in g]
@@ -56,6 +66,7 @@ def broadcast_arrays(dist, device, arrays):
     import torch
     if dist is None:
         return [np.asarray(a) for a in arrays]
+    device = _coll_device(dist, device)
     rank = dist.get_rank()
     codes = ["u1", "i1", "u2", "i2", "u4", "i4", "u8", "i8", "f4", "f8", "b1"]
     if rank == 0:
