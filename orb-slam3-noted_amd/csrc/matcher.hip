@@ -301,8 +301,8 @@ __global__ void __launch_bounds__(512) k_bow_match_any(const DevBowPair* pairs, 
                                                        int check_ori, int strict) {
     __shared__ int hist[32];
     __shared__ int s_keep[3], s_count;
+    if (!pairs[blockIdx.x].general) return;  // one flag read before the whole record
     const DevBowPair pr = pairs[blockIdx.x];
-    if (!pr.general) return;
     const DevBowSide& A = pr.A;
     const DevBowSide& B = pr.B;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <new>
 
 #include "common.hpp"
@@ -87,6 +88,126 @@ __global__ void __launch_bounds__(kRemapThreads) k_remap(const MapEntry* map, in
     }
 }
 
+// ---- LDS-tiled form: a workgroup owns a 64 x 16 destination tile.  A rectification map is
+// near-identity, so the tile reads a small source box (its bounding box over the tile's map
+// entries, +1 for the bilinear taps): the box is staged into LDS with row-contiguous loads
+// (out-of-image cells as the border value 0 — exactly remap_px's `at`), then each thread makes
+// 4 pixels from LDS.  Boxes are computed once per map (k_tile_boxes); a tile whose box exceeds
+// kBoxMax bytes keeps the per-pixel gather path.
+constexpr int kTileW = 64, kTileH = 16, kBoxMax = 12 * 1024;
+
+__global__ void __launch_bounds__(256) k_tile_boxes(const MapEntry* map, int dw, int dh, int tiles_x, int4* boxes) {
+    const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
+    int x0 = 1 << 30, y0 = 1 << 30, x1 = -(1 << 30), y1 = -(1 << 30);
+    for (int i = threadIdx.x; i < kTileW * kTileH; i += blockDim.x) {
+        const int x = tx * kTileW + (i % kTileW), y = ty * kTileH + i / kTileW;
+        if (x >= dw || y >= dh) continue;
+        const MapEntry e = map[(size_t)y * dw + x];
+        x0 = min(x0, (int)e.sx);
+        y0 = min(y0, (int)e.sy);
+        x1 = max(x1, (int)e.sx + 1);
+        y1 = max(y1, (int)e.sy + 1);
+    }
+    __shared__ int red[4][256];
+    red[0][threadIdx.x] = x0;
+    red[1][threadIdx.x] = y0;
+    red[2][threadIdx.x] = -x1;
+    red[3][threadIdx.x] = -y1;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o)
+            for (int k = 0; k < 4; k++) red[k][threadIdx.x] = min(red[k][threadIdx.x], red[k][threadIdx.x + o]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const int bx0 = red[0][0], by0 = red[1][0], bx1 = -red[2][0], by1 = -red[3][0];
+        const long long bw = (long long)bx1 - bx0 + 1, bh = (long long)by1 - by0 + 1;
+        const bool ok = bw > 0 && bh > 0 && (bw + 6) * bh <= kBoxMax && bw + 6 <= 4 * 256;
+        boxes[blockIdx.x] = ok ? make_int4(bx0, by0, (int)bw, (int)bh) : make_int4(0, 0, 0, 0);  // w = 0: gather
+    }
+}
+
+__global__ void __launch_bounds__(256) k_remap_tiled(const MapEntry* map, const int4* boxes, int tiles_x, int dw,
+                                                     int dh, int sw, int sh, int nframes, const uint8_t* src, int sp,
+                                                     int64_t sstride, uint8_t* dst, int dp, int64_t dstride) {
+    __shared__ __attribute__((aligned(16))) uint8_t box[kBoxMax];
+    constexpr int kPer = 4;  // box dwords per thread (register double buffer across frames)
+    const int tile = blockIdx.x, tx = tile % tiles_x, ty = tile / tiles_x;
+    const int4 B = boxes[tile];
+    const int lx = (threadIdx.x & 15) * 4, ly = threadIdx.x >> 4;  // 16 threads x 4 px per row, 16 rows
+    const int x0 = tx * kTileW + lx, y = ty * kTileH + ly;
+    const bool live = x0 < dw && y < dh;
+    const int nx = live ? min(4, dw - x0) : 0;
+    MapEntry e[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) e[k] = live ? map[(size_t)y * dw + min(x0 + k, dw - 1)] : MapEntry{0, 0, 0};
+    const int f0 = blockIdx.y * kFramesPerBlock, f1 = min(nframes, f0 + kFramesPerBlock);
+    const bool aligned = nx == 4 && ((dp | (int)(dstride & 3)) & 3) == 0;
+    const bool aligned_src = ((sp | (int)(sstride & 3) | (int)((uintptr_t)src & 3)) & 3) == 0;
+    // box rows start at the 4-byte-aligned column ax <= B.x; thread (qr, qc) owns dword qc of rows
+    // qr, qr + rpp, ... (at most kPer of them, else the tile takes the gather path)
+    const int ax = B.x & ~3, q = B.z > 0 ? (B.x - ax + B.z + 3) >> 2 : 1, bw = q * 4;
+    const int qr = (int)threadIdx.x / q, qc = (int)threadIdx.x - qr * q, rpp = (int)blockDim.x / q;
+    const bool tiled = B.z > 0 && (B.w + rpp - 1) / rpp <= kPer;
+    uint32_t nxt[kPer];
+    auto load = [&](const uint8_t* S) {
+#pragma unroll
+        for (int j = 0; j < kPer; j++) {
+            const int r = qr + j * rpp;
+            uint32_t w = 0;
+            if (qr < rpp && r < B.w) {
+                const int sy = B.y + r, sx = ax + 4 * qc;
+                if ((unsigned)sy < (unsigned)sh) {
+                    const uint8_t* row = S + (size_t)sy * sp;
+                    if (sx >= 0 && sx + 3 < sw && aligned_src) {
+                        w = *reinterpret_cast<const uint32_t*>(row + sx);
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < 4; k++)
+                            if ((unsigned)(sx + k) < (unsigned)sw) w |= (uint32_t)row[sx + k] << (8 * k);
+                    }
+                }
+            }
+            nxt[j] = w;
+        }
+    };
+    if (tiled && f0 < f1) load(src + f0 * sstride);
+    uint32_t* box32 = reinterpret_cast<uint32_t*>(box);
+    for (int f = f0; f < f1; f++) {
+        const uint8_t* S = src + f * sstride;
+        int v[4];
+        if (tiled) {
+            __syncthreads();  // the previous frame's box reads are done
+#pragma unroll
+            for (int j = 0; j < kPer; j++) {
+                const int r = qr + j * rpp;
+                if (qr < rpp && r < B.w) box32[r * q + qc] = nxt[j];
+            }
+            __syncthreads();
+            if (f + 1 < f1) load(S + sstride);  // next frame's box in flight during this one's math
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int fx = e[k].frac & 31, fy = e[k].frac >> 5;
+                const int w00 = (32 - fx) * (32 - fy), w01 = fx * (32 - fy), w10 = (32 - fx) * fy, w11 = fx * fy;
+                const uint8_t* qq = box + (e[k].sy - B.y) * bw + (e[k].sx - ax);
+                const int s = (qq[0] * w00 + qq[1] * w01 + qq[bw] * w10 + qq[bw + 1] * w11) * 32;
+                v[k] = min(max((s + (1 << 14)) >> 15, 0), 255);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; k++) v[k] = live ? remap_px(S, sw, sh, sp, e[k]) : 0;
+        }
+        if (!live) continue;
+        uint8_t* D = dst + f * dstride + (size_t)y * dp + x0;
+        if (aligned) {
+            *reinterpret_cast<uint32_t*>(D) = (uint32_t)v[0] | ((uint32_t)v[1] << 8) | ((uint32_t)v[2] << 16) |
+                                              ((uint32_t)v[3] << 24);
+        } else {
+            for (int k = 0; k < nx; k++) D[k] = (uint8_t)v[k];
+        }
+    }
+}
+
 }  // namespace
 }  // namespace slamhot
 
@@ -95,8 +216,9 @@ using namespace slamhot;
 struct slam_rectifier {
     int device = 0;
     hipStream_t stream = nullptr;
-    int sw = 0, sh = 0, dw = 0, dh = 0;
+    int sw = 0, sh = 0, dw = 0, dh = 0, tiles_x = 0, ntiles = 0;
     MapEntry* d_map = nullptr;
+    int4* d_boxes = nullptr;
 };
 
 extern "C" {
@@ -132,6 +254,14 @@ slam_status slamhot_rectifier_create(int device, int src_w, int src_h, int dst_w
                            d_f + np, r->d_map);
         e = hipGetLastError();
     }
+    r->tiles_x = (dst_w + kTileW - 1) / kTileW;
+    r->ntiles = r->tiles_x * ((dst_h + kTileH - 1) / kTileH);
+    if (e == hipSuccess) e = hipMalloc(&r->d_boxes, sizeof(int4) * r->ntiles);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_tile_boxes, dim3(r->ntiles), dim3(256), 0, r->stream, r->d_map, dst_w, dst_h, r->tiles_x,
+                           r->d_boxes);
+        e = hipGetLastError();
+    }
     if (e == hipSuccess) e = hipStreamSynchronize(r->stream);
     (void)hipFree(d_f);
     if (e != hipSuccess) {
@@ -147,6 +277,7 @@ void slamhot_rectifier_destroy(slam_rectifier* r) {
     (void)hipSetDevice(r->device);
     if (r->stream) (void)hipStreamSynchronize(r->stream);
     if (r->d_map) (void)hipFree(r->d_map);
+    if (r->d_boxes) (void)hipFree(r->d_boxes);
     if (r->stream) (void)hipStreamDestroy(r->stream);
     delete r;
 }
@@ -160,11 +291,19 @@ slam_status slamhot_rectify_batch_device(slam_rectifier* r, int nframes, const v
     if (nframes == 0) return SLAM_OK;
     SLAM_HIP_TRY(hipSetDevice(r->device));
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : r->stream;
-    const int qw = (r->dw + 3) >> 2;
-    const dim3 grid((unsigned)((qw * r->dh + kRemapThreads - 1) / kRemapThreads),
-                    (unsigned)((nframes + kFramesPerBlock - 1) / kFramesPerBlock));
-    hipLaunchKernelGGL(k_remap, grid, dim3(kRemapThreads), 0, s, r->d_map, r->dw, r->dh, r->sw, r->sh, nframes,
-                       (const uint8_t*)d_src, src_pitch, src_stride, (uint8_t*)d_dst, dst_pitch, dst_stride);
+    const char* env = std::getenv("SLAMHOT_REMAP");  // "gather": the per-pixel kernel (A/B runs)
+    if (env && env[0] == 'g') {
+        const int qw = (r->dw + 3) >> 2;
+        const dim3 grid((unsigned)((qw * r->dh + kRemapThreads - 1) / kRemapThreads),
+                        (unsigned)((nframes + kFramesPerBlock - 1) / kFramesPerBlock));
+        hipLaunchKernelGGL(k_remap, grid, dim3(kRemapThreads), 0, s, r->d_map, r->dw, r->dh, r->sw, r->sh, nframes,
+                           (const uint8_t*)d_src, src_pitch, src_stride, (uint8_t*)d_dst, dst_pitch, dst_stride);
+    } else {
+        const dim3 grid((unsigned)r->ntiles, (unsigned)((nframes + kFramesPerBlock - 1) / kFramesPerBlock));
+        hipLaunchKernelGGL(k_remap_tiled, grid, dim3(256), 0, s, r->d_map, r->d_boxes, r->tiles_x, r->dw, r->dh, r->sw,
+                           r->sh, nframes, (const uint8_t*)d_src, src_pitch, src_stride, (uint8_t*)d_dst, dst_pitch,
+                           dst_stride);
+    }
     SLAM_HIP_TRY(hipGetLastError());
     return SLAM_OK;
 }
