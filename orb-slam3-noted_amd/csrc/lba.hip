@@ -12,7 +12,7 @@
 //   k_lin_poses      wave / pose    : Hpp (6x6) and b_p over the pose's edges
 //   k_iter_begin     block / window : chi2 = sum rho, lambda init (iteration 0)
 // per LM trial:
-//   k_schur_edges    thread / edge  : Dinv = (Hll + lambda I)^-1, B_e Dinv, B_e Dinv b_l
+//   k_point_prep     thread / point : Dinv = (Hll + lambda I)^-1, db = Dinv b_l
 //   k_schur_block    wave / 6x6 block of the Schur complement (lower triangle + rhs row)
 //   k_ldlt           block / window : dense LDL^T of the (n+1) x (n+1) augmented system
 //   k_backsub        thread / point : x_l = Dinv (b_l - Hpl^T x_p), trial point
@@ -41,7 +41,6 @@ namespace lba {
 constexpr int kNB = 32;           // LDL^T panel width
 constexpr int kMaxN = 480;        // 80 free KeyFrames per window
 constexpr int kHplStride = 18;    // doubles per edge: pose-landmark block Hpl = B^T W A (6 x 3)
-constexpr int kTrStride = 24;     // doubles per edge of Schur trial output: B Dinv (18), B db (6)
 constexpr int kCtlThreads = 1024;
 // k_ldlt_t16 geometry
 constexpr int kT16Max = 18;                                  // tile rows (n <= 288)
@@ -78,6 +77,9 @@ struct WinDesc {
     int kf0, nk, pt0, npt, e0, ne, pose0, np;
     int n, ld, blk0, nblk;
     long long hs_off;      // doubles
+    int spe0, nwd;         // first free-pose edge (spe) of the window; 64-point words per pose bitmap
+    long long bm0;         // first word of the window's pose bitmaps (np x nwd)
+    long long ct0;         // first Schur contribution of the window
 };
 
 struct WinCtl {
@@ -535,34 +537,25 @@ __device__ inline void point_dinv(const double* __restrict__ Hll, long long p, d
     inverse3(D, Di);
 }
 
-// Schur per landmark (block_solver.hpp:381-432), one thread per (landmark, free-pose edge):
-// Dinv = (Hll + lambda I)^-1 of the edge's point (Eigen cofactor inverse, recomputed per edge),
-// db = Dinv b_l, then B Dinv and B db for the edge.
-__global__ void k_schur_edges(int nspe_total, const int* __restrict__ spe, const EdgeS* __restrict__ E,
-                              const WinCtl* __restrict__ ctl, const double* __restrict__ Hll,
-                              const double* __restrict__ bl, const double* __restrict__ lin,
-                              double* __restrict__ tr) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nspe_total) return;
-    const int e = spe[i];
-    const EdgeS ed = E[e];
-    const WinCtl& C = ctl[ed.win];
+// Schur per landmark (block_solver.hpp:381-432), the per-point half: Dinv = (Hll + lambda I)^-1
+// (Eigen cofactor inverse) and db = Dinv b_l, one thread per point, kPdStride doubles each.  The
+// per-edge products B Dinv and B db are formed where they are used (k_schur_blocks), so no
+// per-edge record goes through HBM.
+constexpr int kPdStride = 12;  // Dinv (9, row-major), db (3)
+__global__ void k_point_prep(int npt_total, const int* __restrict__ pt_win, const WinCtl* __restrict__ ctl,
+                             const double* __restrict__ Hll, const double* __restrict__ bl, double* __restrict__ pd) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npt_total) return;
+    const WinCtl& C = ctl[pt_win[p]];
     if (!C.need_trial) return;
     double Di[9];
-    point_dinv(Hll, ed.pt, C.lambda, Di);
-    const double* b = bl + 4 * (long long)ed.pt;
-    double db[3];
+    point_dinv(Hll, p, C.lambda, Di);
+    const double* b = bl + 4 * (long long)p;
+    double* o = pd + (long long)kPdStride * p;
 #pragma unroll
-    for (int r = 0; r < 3; r++) db[r] = Di[3 * r] * b[0] + Di[3 * r + 1] * b[1] + Di[3 * r + 2] * b[2];
-    const double* H = lin + (long long)kHplStride * e;
-    double* T = tr + (long long)kTrStride * e;
+    for (int k = 0; k < 9; k++) o[k] = Di[k];
 #pragma unroll
-    for (int r = 0; r < 6; r++) {
-        const double h0 = H[3 * r], h1 = H[3 * r + 1], h2 = H[3 * r + 2];
-#pragma unroll
-        for (int c = 0; c < 3; c++) T[3 * r + c] = h0 * Di[c] + h1 * Di[3 + c] + h2 * Di[6 + c];
-        T[18 + r] = h0 * db[0] + h1 * db[1] + h2 * db[2];
-    }
+    for (int r = 0; r < 3; r++) o[9 + r] = Di[3 * r] * b[0] + Di[3 * r + 1] * b[1] + Di[3 * r + 2] * b[2];
 }
 
 // value of lane j (compile-time) within each 32-lane half: ds_swizzle bit mode, and_mask 0,
@@ -627,15 +620,159 @@ __device__ __forceinline__ void t16_put(double* Tw, int n, int R, int Cc, double
     if (I == J && r != c) Tw[256LL * t + 4 * (c + 16 * (r & 3)) + (r >> 2)] = v;
 }
 
+// ---------------------------------------------------------------- Schur contribution lists
+// The Schur contributions of block (i1, i2) are the MapPoints observed by both poses (one
+// free-pose edge each: block_solver.hpp:403-430 walks them per landmark), in point order.  They
+// are built once per solve on the device instead of on the host (8 B per pair: ~74 MB per 128
+// config-4 windows through PCIe, and most of the host plan time): every pose gets a bitmap over
+// its window's points and the list of its edges in point order; a block's list is the AND of the
+// two bitmaps with each common point ranked inside both pose lists.
+//   bm  [W.bm0 + i * nwd + wd]   bit q <-> local point 64 wd + q observed by local pose i
+//   bmp [same index]             set bits of pose i before word wd
+//   pls [W.spe0 + pbase[i] + r]  r-th free-pose edge (edge id) of pose i in point order
+__global__ void k_bm_set(int nspe_total, const int* __restrict__ spe, const EdgeS* __restrict__ E,
+                         const WinDesc* __restrict__ wins, unsigned long long* __restrict__ bm) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nspe_total) return;
+    const EdgeS e = E[spe[s]];
+    const WinDesc& W = wins[e.win];
+    const int lp = e.pt - W.pt0, i = e.hp - W.pose0;
+    atomicOr(bm + W.bm0 + (long long)i * W.nwd + (lp >> 6), 1ull << (lp & 63));
+}
+
+// one thread per pose of the window: word prefix counts, then the pose list bases in pose order
+__global__ void k_bm_scan(const WinDesc* __restrict__ wins, const unsigned long long* __restrict__ bm,
+                          int* __restrict__ bmp, int* __restrict__ pbase) {
+    __shared__ int cnt[kMaxN / 6 + 1];
+    const WinDesc W = wins[blockIdx.x];
+    for (int i = threadIdx.x; i < W.np; i += blockDim.x) {
+        const long long o = W.bm0 + (long long)i * W.nwd;
+        int run = 0;
+        for (int wd = 0; wd < W.nwd; wd++) {
+            bmp[o + wd] = run;
+            run += __popcll(bm[o + wd]);
+        }
+        cnt[i] = run;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int run = 0;
+        for (int i = 0; i < W.np; i++) {
+            pbase[W.pose0 + i] = run;
+            run += cnt[i];
+        }
+    }
+}
+
+__global__ void k_bm_list(int nspe_total, const int* __restrict__ spe, const EdgeS* __restrict__ E,
+                          const WinDesc* __restrict__ wins, const unsigned long long* __restrict__ bm,
+                          const int* __restrict__ bmp, const int* __restrict__ pbase, int* __restrict__ pls) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nspe_total) return;
+    const EdgeS e = E[spe[s]];
+    const WinDesc& W = wins[e.win];
+    const int lp = e.pt - W.pt0, i = e.hp - W.pose0;
+    const long long o = W.bm0 + (long long)i * W.nwd + (lp >> 6);
+    const int r = bmp[o] + __popcll(bm[o] & ((1ull << (lp & 63)) - 1));
+    pls[W.spe0 + pbase[e.hp] + r] = spe[s];
+}
+
+__device__ __forceinline__ int ct_words(const WinDesc& W, const unsigned long long* __restrict__ bm, int i1, int i2,
+                                        int wd, unsigned long long* w1, unsigned long long* w2) {
+    *w1 = bm[W.bm0 + (long long)i1 * W.nwd + wd];
+    *w2 = bm[W.bm0 + (long long)i2 * W.nwd + wd];
+    return __popcll(*w1 & *w2);
+}
+
+// thread per block: its number of contributions
+__global__ void k_ct_count(int nblk_total, const int2* __restrict__ blk_pose, const int* __restrict__ blk_win,
+                           const WinDesc* __restrict__ wins, const unsigned long long* __restrict__ bm,
+                           int* __restrict__ cnt) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nblk_total) return;
+    const WinDesc& W = wins[blk_win[b]];
+    const int2 ij = blk_pose[b];
+    int c = 0;
+    unsigned long long w1, w2;
+    for (int wd = 0; wd < W.nwd; wd++) c += ct_words(W, bm, ij.x, ij.y, wd, &w1, &w2);
+    cnt[b] = c;
+}
+
+// workgroup per window: ct_off over the window's blocks (exclusive scan from W.ct0)
+constexpr int kCtScanThreads = 1024;
+__global__ void __launch_bounds__(kCtScanThreads) k_ct_scan(const WinDesc* __restrict__ wins,
+                                                            const int* __restrict__ cnt, int* __restrict__ ct_off) {
+    __shared__ int part[kCtScanThreads];
+    const WinDesc W = wins[blockIdx.x];
+    const int per = (W.nblk + kCtScanThreads - 1) / kCtScanThreads;
+    const int b0 = min(W.nblk, (int)threadIdx.x * per), b1 = min(W.nblk, b0 + per);
+    int sum = 0;
+    for (int b = b0; b < b1; b++) sum += cnt[W.blk0 + b];
+    part[threadIdx.x] = sum;
+    __syncthreads();
+    for (int o = 1; o < kCtScanThreads; o <<= 1) {  // Hillis-Steele inclusive scan
+        const int v = threadIdx.x >= (unsigned)o ? part[threadIdx.x - o] : 0;
+        __syncthreads();
+        part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    long long run = W.ct0 + part[threadIdx.x] - sum;
+    for (int b = b0; b < b1; b++) {
+        ct_off[W.blk0 + b] = (int)run;
+        run += cnt[W.blk0 + b];
+    }
+    if (threadIdx.x == kCtScanThreads - 1) ct_off[W.blk0 + W.nblk] = (int)(W.ct0 + part[threadIdx.x]);
+}
+
+// wave per block: lane = 64-point word (word-prefix by wave scan), each lane writes the pairs of
+// its word's common points in point order
+__global__ void __launch_bounds__(256) k_ct_fill(int nblk_total, const int2* __restrict__ blk_pose,
+                                                 const int* __restrict__ blk_win, const WinDesc* __restrict__ wins,
+                                                 const unsigned long long* __restrict__ bm,
+                                                 const int* __restrict__ bmp, const int* __restrict__ pbase,
+                                                 const int* __restrict__ pls, const int* __restrict__ ct_off,
+                                                 int4* __restrict__ ct) {
+    const int b = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (b >= nblk_total) return;
+    const WinDesc& W = wins[blk_win[b]];
+    const int2 ij = blk_pose[b];
+    const int* l1 = pls + W.spe0 + pbase[W.pose0 + ij.x];
+    const int* l2 = pls + W.spe0 + pbase[W.pose0 + ij.y];
+    int pos = ct_off[b];
+    for (int wd0 = 0; wd0 < W.nwd; wd0 += 64) {
+        const int wd = wd0 + lane;
+        unsigned long long w1 = 0, w2 = 0;
+        const int c = wd < W.nwd ? ct_words(W, bm, ij.x, ij.y, wd, &w1, &w2) : 0;
+        int incl = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += v;
+        }
+        int k = pos + incl - c;
+        if (c) {
+            const long long o1 = W.bm0 + (long long)ij.x * W.nwd + wd, o2 = W.bm0 + (long long)ij.y * W.nwd + wd;
+            const int r1 = bmp[o1], r2 = bmp[o2];
+            unsigned long long m = w1 & w2;
+            while (m) {
+                const int q = __builtin_ctzll(m);
+                const unsigned long long below = (1ull << q) - 1ull;
+                m &= m - 1ull;
+                ct[k++] = int4{l1[r1 + __popcll(w1 & below)], l2[r2 + __popcll(w2 & below)], W.pt0 + 64 * wd + q, 0};
+            }
+        }
+        pos += __shfl(incl, 63, 64);
+    }
+}
+
 template <int NL>
 __device__ __forceinline__ void schur_block_body(int wg, int nlist, const int* __restrict__ order,
                                                      const int2* __restrict__ blk_pose,
                                                      const int* __restrict__ blk_win, const int* __restrict__ ct_off,
-                                                     const int2* __restrict__ ct, const WinDesc* __restrict__ wins,
+                                                     const int4* __restrict__ ct, const WinDesc* __restrict__ wins,
                                                      const WinCtl* __restrict__ ctl, const double* __restrict__ Hpp,
-                                                     const double* __restrict__ bp, const int* __restrict__ pe_off,
-                                                     const int* __restrict__ pe, const double* __restrict__ lin,
-                                                     const double* __restrict__ tr, double* __restrict__ Hs,
+                                                     const double* __restrict__ bp, const double* __restrict__ lin,
+                                                     const double* __restrict__ pd, double* __restrict__ Hs,
                                                      double* __restrict__ Ts) {
     const int idx = wg * (256 / NL) + threadIdx.x / NL, lane = threadIdx.x % NL;
     const bool live = idx < nlist;
@@ -646,47 +783,58 @@ __device__ __forceinline__ void schur_block_body(int wg, int nlist, const int* _
     const WinDesc W = wins[win];
     const int2 ij = blk_pose[b];  // local free-pose indices i1 <= i2
     const int i1 = ij.x, i2 = ij.y;
-    // lane = (row half h, contribution stream j): rows 3h..3h+2 of the 6x6 over every 8th
-    // contribution; 18 accumulators instead of 36 keep the kernel at 4 waves per SIMD
+    // lane = (row half h, contribution stream j): rows 3h..3h+2 of the 6x6 over every
+    // kStreams-th contribution; 18 accumulators keep the kernel at 4 waves per SIMD.  Per
+    // contribution (edges a of pose i1 and b of pose i2 on point p) the lane forms its rows of
+    // B_a Dinv_p (the products k_schur_edges used to store per edge, same expression) and
+    // multiplies by Hpl_b^T; a diagonal block also sums its rows of B_a db_p (the rhs).
     const int h = lane & 1, j = lane >> 1;
     constexpr int kStreams = NL / 2;
     double acc[18];
 #pragma unroll
     for (int k = 0; k < 18; k++) acc[k] = 0.0;
+    double sb[3] = {0, 0, 0};
     if (act) {
         for (int k = ct_off[b] + j; k < ct_off[b + 1]; k += kStreams) {
-            const int2 ab = ct[k];
-            const double* BD = tr + (long long)kTrStride * ab.x + 9 * h;
+            const int4 ab = ct[k];
+            const double* Ba = lin + (long long)kHplStride * ab.x + 9 * h;
             const double* Bj = lin + (long long)kHplStride * ab.y;
-            double bd[9], bj[18];
+            const double* Dp = pd + (long long)kPdStride * ab.z;
+            double ba[9], di[12], bj[18], bd[9];
 #pragma unroll
-            for (int t = 0; t < 9; t++) bd[t] = BD[t];
+            for (int t = 0; t < 9; t++) ba[t] = Ba[t];
+#pragma unroll
+            for (int t = 0; t < 12; t++) di[t] = Dp[t];
 #pragma unroll
             for (int t = 0; t < 18; t++) bj[t] = Bj[t];
 #pragma unroll
             for (int r = 0; r < 3; r++)
 #pragma unroll
+                for (int c = 0; c < 3; c++)
+                    bd[3 * r + c] = ba[3 * r] * di[c] + ba[3 * r + 1] * di[3 + c] + ba[3 * r + 2] * di[6 + c];
+#pragma unroll
+            for (int r = 0; r < 3; r++)
+#pragma unroll
                 for (int c = 0; c < 6; c++)
                     acc[6 * r + c] += bd[3 * r] * bj[3 * c] + bd[3 * r + 1] * bj[3 * c + 1] + bd[3 * r + 2] * bj[3 * c + 2];
+            if (i1 == i2) {
+#pragma unroll
+                for (int r = 0; r < 3; r++) sb[r] += ba[3 * r] * di[9] + ba[3 * r + 1] * di[10] + ba[3 * r + 2] * di[11];
+            }
         }
     }
-    // butterfly over the 8 streams of the same half (lane bits 1..3)
+    // butterfly over the streams of the same half (lane bits 1..)
 #pragma unroll
     for (int k = 0; k < 18; k++) {
 #pragma unroll
         for (int o = 2; o < NL; o <<= 1) acc[k] += __shfl_xor(acc[k], o, NL);
     }
-    double sb[6] = {0, 0, 0, 0, 0, 0};
-    const int gp = W.pose0 + i1;
-    if (act && i1 == i2) {
-        for (int k = pe_off[gp] + lane; k < pe_off[gp + 1]; k += NL) {
-            const double* T = tr + (long long)kTrStride * pe[k] + 18;
 #pragma unroll
-            for (int r = 0; r < 6; r++) sb[r] += T[r];
-        }
+    for (int r = 0; r < 3; r++) {
+#pragma unroll
+        for (int o = 2; o < NL; o <<= 1) sb[r] += __shfl_xor(sb[r], o, NL);
     }
-#pragma unroll
-    for (int r = 0; r < 6; r++) sb[r] = group_sum<NL>(sb[r]);
+    const int gp = W.pose0 + i1;
     if (!act) return;
     double* H = Hs + W.hs_off;
     // every lane of a half holds that half's sums: stream j writes its elements j, j+8, j+16
@@ -712,12 +860,10 @@ __device__ __forceinline__ void schur_block_body(int wg, int nlist, const int* _
             else H[(long long)(6 * i2 + c) * W.ld + 6 * i1 + r] = v;
         }
     }
-    if (i1 == i2 && lane < 6) {
-        double s6 = 0.0;
+    if (i1 == i2 && j == 0) {  // lanes 0 / 1: rhs rows 0..2 / 3..5
 #pragma unroll
-        for (int r = 0; r < 6; r++)
-            if (r == lane) s6 = sb[r];
-        H[(long long)ldlt_npad(W.n) * W.ld + 6 * i1 + lane] = bp[8 * (long long)gp + lane] - s6;
+        for (int r = 0; r < 3; r++)
+            H[(long long)ldlt_npad(W.n) * W.ld + 6 * i1 + 3 * h + r] = bp[8 * (long long)gp + 3 * h + r] - sb[r];
     }
 }
 
@@ -727,22 +873,21 @@ __device__ __forceinline__ void schur_block_body(int wg, int nlist, const int* _
 __global__ void __launch_bounds__(256) k_schur_blocks(int nb_diag, int nblk, int npose, const int* __restrict__ order,
                                                       const int2* __restrict__ blk_pose,
                                                       const int* __restrict__ blk_win, const int* __restrict__ ct_off,
-                                                      const int2* __restrict__ ct, const WinDesc* __restrict__ wins,
+                                                      const int4* __restrict__ ct, const WinDesc* __restrict__ wins,
                                                       const WinCtl* __restrict__ ctl, const double* __restrict__ Hpp,
-                                                      const double* __restrict__ bp, const int* __restrict__ pe_off,
-                                                      const int* __restrict__ pe, const double* __restrict__ lin,
-                                                      const double* __restrict__ tr, double* __restrict__ Hs,
+                                                      const double* __restrict__ bp, const double* __restrict__ lin,
+                                                      const double* __restrict__ pd, double* __restrict__ Hs,
                                                       double* __restrict__ Ts) {
     const int b = blockIdx.x;
     if (b < nb_diag) {
         const int wg = xcd_swizzle(b, nb_diag);
         if (wg * (256 / kSchurDiagLanes) >= npose) return;  // padding blocks (whole block)
-        schur_block_body<kSchurDiagLanes>(wg, npose, order, blk_pose, blk_win, ct_off, ct, wins, ctl, Hpp, bp,
-                                          pe_off, pe, lin, tr, Hs, Ts);
+        schur_block_body<kSchurDiagLanes>(wg, npose, order, blk_pose, blk_win, ct_off, ct, wins, ctl, Hpp, bp, lin,
+                                          pd, Hs, Ts);
     } else {
         schur_block_body<kSchurLanes>(xcd_swizzle(b - nb_diag, (int)gridDim.x - nb_diag), nblk - npose,
-                                      order + npose, blk_pose, blk_win, ct_off, ct, wins, ctl, Hpp, bp, pe_off, pe,
-                                      lin, tr, Hs, Ts);
+                                      order + npose, blk_pose, blk_win, ct_off, ct, wins, ctl, Hpp, bp, lin, pd, Hs,
+                                      Ts);
     }
 }
 
@@ -1272,7 +1417,7 @@ __global__ void k_t16_pad(const WinDesc* __restrict__ wins, double* __restrict__
 __device__ __forceinline__ void backsub_body(int p, int npt_total, const int* __restrict__ spe_off, const int* __restrict__ spe,
                           const EdgeS* __restrict__ E, const int* __restrict__ pt_win,
                           const WinCtl* __restrict__ ctl, const double* __restrict__ bl,
-                          const double* __restrict__ Hll, const double* __restrict__ lin,
+                          const double* __restrict__ pd, const double* __restrict__ lin,
                           const double* __restrict__ xp, double* __restrict__ xl, double* __restrict__ pts,
                           long long pt_stride) {
     if (p >= npt_total) return;
@@ -1290,8 +1435,7 @@ __device__ __forceinline__ void backsub_body(int p, int npt_total, const int* __
 #pragma unroll
                 for (int r = 0; r < 6; r++) cl[c] += H[3 * r + c] * (-xpp[r]);
         }
-        double Di[9];
-        point_dinv(Hll, p, C.lambda, Di);
+        const double* Di = pd + (long long)kPdStride * p;  // k_point_prep's Dinv of this trial
 #pragma unroll
         for (int r = 0; r < 3; r++) x[r] = Di[3 * r] * cl[0] + Di[3 * r + 1] * cl[1] + Di[3 * r + 2] * cl[2];
     }
@@ -1326,7 +1470,7 @@ __global__ void __launch_bounds__(256) k_update(int nb_kf, int nkf_total, const 
                                                 const int* __restrict__ spe_off, const int* __restrict__ spe,
                                                 const EdgeS* __restrict__ E, const int* __restrict__ pt_win,
                                                 const WinCtl* __restrict__ ctl, const double* __restrict__ bl,
-                                                const double* __restrict__ Hll, const double* __restrict__ lin,
+                                                const double* __restrict__ pd, const double* __restrict__ lin,
                                                 const double* __restrict__ xp, double* __restrict__ xl,
                                                 double* __restrict__ poses, long long pose_stride,
                                                 double* __restrict__ pts, long long pt_stride) {
@@ -1334,7 +1478,7 @@ __global__ void __launch_bounds__(256) k_update(int nb_kf, int nkf_total, const 
     if (b < nb_kf)
         pose_update_body(b * 256 + threadIdx.x, nkf_total, kf_hp, kf_win, ctl, xp, poses, pose_stride);
     else
-        backsub_body((b - nb_kf) * 256 + threadIdx.x, npt_total, spe_off, spe, E, pt_win, ctl, bl, Hll, lin, xp, xl,
+        backsub_body((b - nb_kf) * 256 + threadIdx.x, npt_total, spe_off, spe, E, pt_win, ctl, bl, pd, lin, xp, xl,
                      pts, pt_stride);
 }
 
@@ -1600,8 +1744,8 @@ struct Plan {
     EdgeS* edges;
     WinDesc* wins;
     WinCtl* ctl;
-    int *pt_off, *pt_win, *spe_off, *spe, *pe_off, *pe, *pose_win, *kf_hp, *kf_win, *blk_win, *ct_off, *blk_order;
-    int2 *blk_pose, *ct;
+    int *pt_off, *pt_win, *spe_off, *spe, *pe_off, *pe, *pose_win, *kf_hp, *kf_win, *blk_win, *blk_order;
+    int2* blk_pose;
     float *kf_in, *pt_in;
     double* kf_trl;  // per KF: mTrl as a pose record (body edges)
 };
@@ -1622,7 +1766,9 @@ struct slam_lba {
     unsigned char* harena = nullptr;  // pinned
     size_t harena_cap = 0;
     DevBuf arena, cnt;
-    DevBuf poses, pts, err, rho, lin, Hll, bl, Hpp, bp, tr, xp, xl, Hs, Ts;
+    DevBuf poses, pts, err, rho, lin, Hll, bl, Hpp, bp, pd, xp, xl, Hs, Ts;
+    DevBuf bm, bmp, pbase, pls;  // pose bitmaps, their word prefixes, pose list bases, pose edge lists
+    DevBuf ct, ct_off, ct_cnt;   // Schur contribution lists (built on the device)
     DevBuf kf_out, pt_out, outl;
 };
 
@@ -1630,21 +1776,21 @@ namespace {
 
 struct WinStart {
     int kf0, pt0, e0, pose0, blk0, spe0, pe0;
-    long long ct0, hs0;
+    long long bm0, ct0, hs0;
     size_t h0;
 };
 
 struct PlanSizes {
     std::vector<WinStart> starts;
     int nkf = 0, npt = 0, ne = 0, npose = 0, nblk = 0, nspe = 0, npe = 0, nw = 0;
-    long long nct = 0, hs_total = 0;
+    long long nbm = 0, nct = 0, hs_total = 0;
     int max_n = 0;
     bool any_body = false;
 };
 
 struct Layout {
-    size_t edges, wins, ctl, pt_off, pt_win, spe_off, spe, pe_off, pe, pose_win, kf_hp, kf_win, blk_win, ct_off,
-        blk_order, blk_pose, ct, kf_in, pt_in, kf_trl, total;
+    size_t edges, wins, ctl, pt_off, pt_win, spe_off, spe, pe_off, pe, pose_win, kf_hp, kf_win, blk_win,
+        blk_order, blk_pose, kf_in, pt_in, kf_trl, total;
 };
 
 Layout make_layout(const PlanSizes& z) {
@@ -1668,10 +1814,8 @@ Layout make_layout(const PlanSizes& z) {
     L.kf_hp = take(sizeof(int) * z.nkf);
     L.kf_win = take(sizeof(int) * z.nkf);
     L.blk_win = take(sizeof(int) * z.nblk);
-    L.ct_off = take(sizeof(int) * (z.nblk + 1));
     L.blk_order = take(sizeof(int) * z.nblk);
     L.blk_pose = take(sizeof(int2) * z.nblk);
-    L.ct = take(sizeof(int2) * z.nct);
     L.kf_in = take(sizeof(float) * 16 * z.nkf);
     L.pt_in = take(sizeof(float) * 3 * z.npt);
     L.kf_trl = take(z.any_body ? sizeof(double) * 8 * z.nkf : 0);
@@ -1695,9 +1839,7 @@ Plan bind(unsigned char* base, const Layout& L) {
     P.kf_win = (int*)(base + L.kf_win);
     P.blk_win = (int*)(base + L.blk_win);
     P.blk_order = (int*)(base + L.blk_order);
-    P.ct_off = (int*)(base + L.ct_off);
     P.blk_pose = (int2*)(base + L.blk_pose);
-    P.ct = (int2*)(base + L.ct);
     P.kf_in = (float*)(base + L.kf_in);
     P.pt_in = (float*)(base + L.pt_in);
     P.kf_trl = (double*)(base + L.kf_trl);
@@ -1714,7 +1856,7 @@ slam_status plan_sizes(int n_prob, const slam_lba_problem* probs, PlanSizes& z, 
     for (int w = 0; w < n_prob; w++) {
         const slam_lba_problem& P = probs[w];
         if (P.n_kf < 0 || P.n_pt < 0 || P.n_edge < 0) return SLAM_EINVAL;
-        z.starts[w] = WinStart{z.nkf, z.npt, z.ne, z.npose, z.nblk, z.nspe, z.npe, z.nct, z.hs_total, hidx_all.size()};
+        z.starts[w] = WinStart{z.nkf, z.npt, z.ne, z.npose, z.nblk, z.nspe, z.npe, z.nbm, z.nct, z.hs_total, hidx_all.size()};
         if ((P.n_kf && (!P.kf_Tcw || !P.kf_fixed)) || (P.n_pt && !P.pt_pos) ||
             (P.n_edge && (!P.edge_pt || !P.edge_kf || !P.edge_obs || !P.edge_inv_sigma2)))
             return SLAM_EINVAL;
@@ -1738,24 +1880,23 @@ slam_status plan_sizes(int n_prob, const slam_lba_problem* probs, PlanSizes& z, 
         for (int k = 0; k < P.n_kf; k++) hidx_all.push_back(P.kf_fixed[k] == 0 && cnt[k] > 0 ? np++ : -1);
         np_of[w] = np;
         if (6 * np > kMaxN) return SLAM_ECAP;
-        // free-pose edges per point -> Schur contributions k(k+1)/2
-        int run = 0, prev = -1;
+        // free-pose edges; an edge right after one of the same point on the same KeyFrame (body
+        // edge) shares its Hpl block and has no Schur entry of its own.  A point with k such
+        // edges adds k (k + 1) / 2 Schur contributions.
+        int run = 0;
         for (int i = 0; i <= P.n_edge; i++) {
-            const int p = i < P.n_edge ? P.edge_pt[i] : -2;
-            if (p != prev) {
+            if (i == P.n_edge || (i > 0 && P.edge_pt[i] != P.edge_pt[i - 1])) {
                 z.nct += (long long)run * (run + 1) / 2;
                 run = 0;
-                prev = p;
             }
-            if (i < P.n_edge && hidx_all[h0 + P.edge_kf[i]] >= 0) {
-                z.npe++;
-                // an edge right after one on the same KeyFrame shares its Hpl block
-                if (!(i > 0 && P.edge_pt[i - 1] == p && P.edge_kf[i - 1] == P.edge_kf[i])) {
-                    run++;
-                    z.nspe++;
-                }
+            if (i == P.n_edge || hidx_all[h0 + P.edge_kf[i]] < 0) continue;
+            z.npe++;
+            if (!(i > 0 && P.edge_pt[i - 1] == P.edge_pt[i] && P.edge_kf[i - 1] == P.edge_kf[i])) {
+                z.nspe++;
+                run++;
             }
         }
+        z.nbm += (long long)np * ((P.n_pt + 63) / 64);
         z.nkf += P.n_kf;
         z.npt += P.n_pt;
         z.ne += P.n_edge;
@@ -1772,11 +1913,10 @@ slam_status plan_fill(int n_prob, const slam_lba_problem* probs, const std::vect
                       const std::vector<int>& np_of, const slam_lba_options* opt, const PlanSizes& Z,
                       const Plan& P) {
     // windows are independent given their start offsets: fill them on host threads
-    auto fill_one = [&](int w, std::vector<int>& col, std::vector<int>& bcnt,
-                        std::vector<int>& pcnt) -> slam_status {
+    auto fill_one = [&](int w, std::vector<int>& col, std::vector<int>& pcnt) -> slam_status {
         const WinStart& ws = Z.starts[w];
         int nkf = ws.kf0, npt = ws.pt0, ne = ws.e0, npose = ws.pose0, nblk = ws.blk0, nspe = ws.spe0;
-        long long nct = ws.ct0, hs = ws.hs0;
+        long long hs = ws.hs0;
         const slam_lba_problem& Q = probs[w];
         const int* hidx = &hidx_all[ws.h0];
         const int np = np_of[w];
@@ -1794,6 +1934,10 @@ slam_status plan_fill(int n_prob, const slam_lba_problem* probs, const std::vect
         D.blk0 = nblk;
         D.nblk = np * (np + 1) / 2;
         D.hs_off = hs;
+        D.spe0 = ws.spe0;
+        D.nwd = (Q.n_pt + 63) / 64;
+        D.bm0 = ws.bm0;
+        D.ct0 = ws.ct0;
         hs += (long long)(ldlt_npad(D.n) + 1) * D.ld;
         P.wins[w] = D;
         WinCtl c{};
@@ -1845,10 +1989,8 @@ slam_status plan_fill(int n_prob, const slam_lba_problem* probs, const std::vect
             e.obs[2] = body ? kBodyTag : (ur < 0.f ? -1.0f : ur);
             e.info = Q.edge_inv_sigma2[i];
         }
-        // point CSR + per-point free-pose edges sorted by pose (HplCCS column order) + Schur
-        // contribution counts per block (i1 <= i2: blk = i2 (i2 + 1) / 2 + i1)
+        // point CSR + per-point free-pose edges sorted by pose (HplCCS column order)
         const int pe_start = ws.pe0;
-        bcnt.assign(D.nblk + 1, 0);
         pcnt.assign(np + 1, 0);
         int i = 0;
         for (int p = 0; p < Q.n_pt; p++) {
@@ -1868,34 +2010,18 @@ slam_status plan_fill(int n_prob, const slam_lba_problem* probs, const std::vect
                 const int i1 = hidx[Q.edge_kf[col[x]]];
                 if (x && i1 == hidx[Q.edge_kf[col[x - 1]]]) return SLAM_EINVAL;  // non-adjacent edges of 1 point in 1 KF
                 P.spe[nspe++] = ne + col[x];
-                for (size_t y = x; y < col.size(); y++) {
-                    const int i2 = hidx[Q.edge_kf[col[y]]];
-                    bcnt[i2 * (i2 + 1) / 2 + i1 + 1]++;
-                }
             }
         }
-        // blocks and their contribution lists, filled in point order
-        for (int b = 0; b < D.nblk; b++) bcnt[b + 1] += bcnt[b];
-        const long long wct = bcnt[D.nblk];
+        // Schur blocks (i1 <= i2: blk = i2 (i2 + 1) / 2 + i1); their contributions come from the
+        // pose bitmaps built on the device (k_bm_*)
         for (int i2 = 0, b = 0; i2 < np; i2++)
             for (int i1 = 0; i1 <= i2; i1++, b++) {
                 P.blk_pose[nblk + b] = int2{i1, i2};
                 P.blk_win[nblk + b] = w;
-                P.ct_off[nblk + b] = (int)(nct + bcnt[b]);
                 // diagonal blocks of all windows first, then the off-diagonal ones
                 if (i1 == i2) P.blk_order[npose + i2] = nblk + b;
                 else P.blk_order[Z.npose + (nblk - npose) + (b - i2)] = nblk + b;
             }
-        for (int p = 0; p < Q.n_pt; p++) {
-            const int s0 = P.spe_off[npt + p], s1 = p + 1 < Q.n_pt ? P.spe_off[npt + p + 1] : nspe;
-            for (int x = s0; x < s1; x++) {
-                const int i1 = P.edges[P.spe[x]].hp - npose;
-                for (int y = x; y < s1; y++) {
-                    const int i2 = P.edges[P.spe[y]].hp - npose;
-                    P.ct[nct + bcnt[i2 * (i2 + 1) / 2 + i1]++] = int2{P.spe[x], P.spe[y]};
-                }
-            }
-        }
         // edges of every free pose (followers included: each adds its own Hpp), insertion order
         for (int e = 0; e < Q.n_edge; e++) {
             const int h = hidx[Q.edge_kf[e]];
@@ -1910,7 +2036,6 @@ slam_status plan_fill(int n_prob, const slam_lba_problem* probs, const std::vect
             const int h = hidx[Q.edge_kf[e]];
             if (h >= 0) P.pe[pe_start + pcnt[h]++] = ne + e;
         }
-        (void)wct;
         (void)nkf;
         return SLAM_OK;
     };
@@ -1918,9 +2043,9 @@ slam_status plan_fill(int n_prob, const slam_lba_problem* probs, const std::vect
     const int nth = std::min(hw, n_prob);
     std::vector<slam_status> rs(nth, SLAM_OK);
     auto run = [&](int t) {
-        std::vector<int> col, bcnt, pcnt;
+        std::vector<int> col, pcnt;
         for (int w = t; w < n_prob; w += nth) {
-            const slam_status r = fill_one(w, col, bcnt, pcnt);
+            const slam_status r = fill_one(w, col, pcnt);
             if (r != SLAM_OK) rs[t] = r;
         }
     };
@@ -1937,7 +2062,6 @@ slam_status plan_fill(int n_prob, const slam_lba_problem* probs, const std::vect
     P.pt_off[Z.npt] = Z.ne;
     P.spe_off[Z.npt] = Z.nspe;
     P.pe_off[Z.npose] = Z.npe;
-    P.ct_off[Z.nblk] = (int)Z.nct;
     return SLAM_OK;
 }
 
@@ -2069,13 +2193,22 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     SLAM_HIP_TRY(s->err.ensure(sizeof(double) * 4 * ne));
     SLAM_HIP_TRY(s->rho.ensure(sizeof(double) * ne));
     SLAM_HIP_TRY(s->lin.ensure(sizeof(double) * kHplStride * ne));
-    SLAM_HIP_TRY(s->tr.ensure(sizeof(double) * kTrStride * ne));
+    SLAM_HIP_TRY(s->pd.ensure(sizeof(double) * kPdStride * npt));
     SLAM_HIP_TRY(s->Hll.ensure(sizeof(double) * 8 * npt));
     SLAM_HIP_TRY(s->bl.ensure(sizeof(double) * 4 * npt));
     SLAM_HIP_TRY(s->xl.ensure(sizeof(double) * 4 * npt));
     SLAM_HIP_TRY(s->Hpp.ensure(sizeof(double) * 24 * nps));
     SLAM_HIP_TRY(s->bp.ensure(sizeof(double) * 8 * nps));
     SLAM_HIP_TRY(s->xp.ensure(sizeof(double) * 6 * nps));
+    SLAM_HIP_TRY(s->bm.ensure(sizeof(unsigned long long) * std::max<long long>(Z.nbm, 1)));
+    SLAM_HIP_TRY(s->bmp.ensure(sizeof(int) * std::max<long long>(Z.nbm, 1)));
+    SLAM_HIP_TRY(s->pbase.ensure(sizeof(int) * nps));
+    SLAM_HIP_TRY(s->pls.ensure(sizeof(int) * std::max(Z.nspe, 1)));
+    SLAM_HIP_TRY(s->ct.ensure(sizeof(int4) * std::max<long long>(Z.nct, 1)));
+    SLAM_HIP_TRY(s->ct_off.ensure(sizeof(int) * (Z.nblk + 1)));
+    SLAM_HIP_TRY(s->ct_cnt.ensure(sizeof(int) * std::max(Z.nblk, 1)));
+    if (Z.nct >= (1LL << 31)) return SLAM_ECAP;  // int offsets
+    SLAM_HIP_TRY(hipMemsetAsync(s->bm.p, 0, sizeof(unsigned long long) * std::max<long long>(Z.nbm, 1), S));
     // tile LDL^T (k_ldlt_t16) when every window fits 18 tile rows (SLAMHOT_LDLT=panel: old kernel)
     const char* ldlt_env = std::getenv("SLAMHOT_LDLT");
     const bool use_t16 = Z.max_n <= 16 * kT16Max && !(ldlt_env && !std::strcmp(ldlt_env, "panel"));
@@ -2087,9 +2220,6 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     SLAM_HIP_TRY(hipMemsetAsync(s->xp.p, 0, sizeof(double) * 6 * nps, S));
     SLAM_HIP_TRY(hipMemsetAsync(s->xl.p, 0, sizeof(double) * 4 * npt, S));
     SLAM_HIP_TRY(hipMemsetAsync(s->err.p, 0, sizeof(double) * 4 * ne, S));
-    // body edges that share their KeyFrame's Hpl block have no Schur entry of their own: their
-    // B db slot stays zero, so k_schur_blocks' sum over a pose's edges adds 0 for them
-    if (Z.any_body) SLAM_HIP_TRY(hipMemsetAsync(s->tr.p, 0, sizeof(double) * kTrStride * ne, S));
     s->last_plan_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_plan0).count();
 
     Cam cam;
@@ -2139,6 +2269,20 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     k_init_state<<<blocks(H.nkf + H.npt, T), T, 0, S>>>(H.nkf, H.npt, DP.kf_in, DP.pt_in,
                                                          poses, pts);
     k_ldlt_pad<<<nw, 64, 0, S>>>(dW, as<double>(s->Hs));
+    if (Z.nspe) {  // the Schur contribution structure, once per solve
+        k_bm_set<<<blocks(Z.nspe, T), T, 0, S>>>(Z.nspe, DP.spe, DP.edges, DP.wins, as<unsigned long long>(s->bm));
+        k_bm_scan<<<nw, 64, 0, S>>>(DP.wins, as<unsigned long long>(s->bm), as<int>(s->bmp), as<int>(s->pbase));
+        k_bm_list<<<blocks(Z.nspe, T), T, 0, S>>>(Z.nspe, DP.spe, DP.edges, DP.wins, as<unsigned long long>(s->bm),
+                                                   as<int>(s->bmp), as<int>(s->pbase), as<int>(s->pls));
+    }
+    if (H.nblk) {
+        k_ct_count<<<blocks(H.nblk, T), T, 0, S>>>(H.nblk, DP.blk_pose, DP.blk_win, DP.wins,
+                                                    as<unsigned long long>(s->bm), as<int>(s->ct_cnt));
+        k_ct_scan<<<nw, kCtScanThreads, 0, S>>>(DP.wins, as<int>(s->ct_cnt), as<int>(s->ct_off));
+        k_ct_fill<<<blocks(H.nblk, 4), 256, 0, S>>>(H.nblk, DP.blk_pose, DP.blk_win, DP.wins,
+                                                     as<unsigned long long>(s->bm), as<int>(s->bmp), as<int>(s->pbase),
+                                                     as<int>(s->pls), as<int>(s->ct_off), as<int4>(s->ct));
+    }
     double* tiles = use_t16 ? as<double>(s->Ts) : nullptr;
     if (use_t16) {
         SLAM_HIP_TRY(hipMemsetAsync(s->Ts.p, 0, (size_t)t16_tiles_bytes() * nw, S));
@@ -2188,14 +2332,13 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
                                                        as<double>(s->Hpp), as<double>(s->bp));
         k_iter_begin<<<nw, kCtlThreads, 0, S>>>(dW, dC, as<double>(s->rho), as<double>(s->Hpp),
                                                 as<double>(s->Hll), dTally + 3);
-        if (Z.nspe)
-            k_schur_edges<<<blocks(Z.nspe, T), T, 0, S>>>(Z.nspe, DP.spe, dE, dC, as<double>(s->Hll),
-                                                           as<double>(s->bl), as<double>(s->lin),
-                                                           as<double>(s->tr));
+        if (H.npt)
+            k_point_prep<<<blocks(H.npt, T), T, 0, S>>>(H.npt, DP.pt_win, dC, as<double>(s->Hll), as<double>(s->bl),
+                                                         as<double>(s->pd));
         if (H.nblk)
             k_schur_blocks<<<nb_schur, 256, 0, S>>>(nb_sdiag, H.nblk, H.npose, DP.blk_order, DP.blk_pose, DP.blk_win,
-                                                    DP.ct_off, DP.ct, dW, dC, as<double>(s->Hpp), as<double>(s->bp),
-                                                    DP.pe_off, DP.pe, as<double>(s->lin), as<double>(s->tr),
+                                                    as<int>(s->ct_off), as<int4>(s->ct), dW, dC, as<double>(s->Hpp),
+                                                    as<double>(s->bp), as<double>(s->lin), as<double>(s->pd),
                                                     as<double>(s->Hs), tiles);
         if (use_t16)
             k_ldlt_t16<<<nw, kT16Waves * 64, 0, S>>>(dW, dC, as<double>(s->Hs), as<double>(s->Ts), as<double>(s->xp));
@@ -2203,7 +2346,7 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
             k_ldlt<<<nw, 512, lds_bytes, S>>>(dW, dC, as<double>(s->Hs), as<double>(s->xp));
         if (nb_upd)
             k_update<<<nb_upd, 256, 0, S>>>(nb_kf, H.nkf, DP.kf_hp, DP.kf_win, H.npt, DP.spe_off, DP.spe, dE,
-                                            DP.pt_win, dC, as<double>(s->bl), as<double>(s->Hll), as<double>(s->lin),
+                                            DP.pt_win, dC, as<double>(s->bl), as<double>(s->pd), as<double>(s->lin),
                                             as<double>(s->xp), as<double>(s->xl), poses, pose_stride, pts, pt_stride);
         if (H.ne)
             k_trial_error<<<blocks(H.ne, T), T, 0, S>>>(H.ne, dE, dC, poses, pts, pose_stride, pt_stride, cam, hk,
