@@ -30,6 +30,7 @@
 #include <thread>
 
 #include <immintrin.h>
+#include <type_traits>
 #include <vector>
 
 #include "common.hpp"
@@ -309,30 +310,40 @@ __device__ __forceinline__ void lin_points_body(int p, int npt_total, const int*
         double om_r[3];
 #pragma unroll
         for (int k = 0; k < 3; k++) om_r[k] = (-(info * err[k])) * rho1;
+        // 2-D edges (mono, body): row 2 of A and B is zero, and a sum that starts at +0 is
+        // unchanged by those +-0 products, so they are skipped (bit-identical: each sum keeps
+        // the ((0 + p0) + p1) + p2 order of the full form)
+        double sb3[3], sh6[6], hpl[18];
 #pragma unroll
-        for (int cc = 0; cc < 3; cc++) {
-            double sacc = 0;
-            for (int k = 0; k < 3; k++) sacc += A[3 * k + cc] * om_r[k];  // mono: row 2 is zero
-            bb[cc] += sacc;
-        }
+        for (int cc = 0; cc < 3; cc++) sb3[cc] = (0.0 + A[cc] * om_r[0]) + A[3 + cc] * om_r[1];
 #pragma unroll
         for (int r = 0; r < 3; r++)
 #pragma unroll
-            for (int cc = r; cc < 3; cc++) {
-                double sacc = 0;
-                for (int k = 0; k < 3; k++) sacc += (A[3 * k + r] * w) * A[3 * k + cc];  // mono: row 2 is zero
-                h[sym3(r, cc)] += sacc;
-            }
+            for (int cc = r; cc < 3; cc++)
+                sh6[sym3(r, cc)] = (0.0 + (A[r] * w) * A[cc]) + (A[3 + r] * w) * A[3 + cc];
+        if (stereo) {
+#pragma unroll
+            for (int cc = 0; cc < 3; cc++) sb3[cc] += A[6 + cc] * om_r[2];
+#pragma unroll
+            for (int r = 0; r < 3; r++)
+#pragma unroll
+                for (int cc = r; cc < 3; cc++) sh6[sym3(r, cc)] += (A[6 + r] * w) * A[6 + cc];
+        }
+#pragma unroll
+        for (int k = 0; k < 3; k++) bb[k] += sb3[k];
+#pragma unroll
+        for (int k = 0; k < 6; k++) h[k] += sh6[k];
         if (e.hp < 0) continue;
-        double hpl[18];
 #pragma unroll
         for (int r = 0; r < 6; r++)
 #pragma unroll
-            for (int cc = 0; cc < 3; cc++) {
-                double sacc = 0;
-                for (int k = 0; k < 3; k++) sacc += (B[6 * k + r] * w) * A[3 * k + cc];  // mono: row 2 is zero
-                hpl[3 * r + cc] = sacc;
-            }
+            for (int cc = 0; cc < 3; cc++) hpl[3 * r + cc] = (0.0 + (B[r] * w) * A[cc]) + (B[6 + r] * w) * A[3 + cc];
+        if (stereo) {
+#pragma unroll
+            for (int r = 0; r < 6; r++)
+#pragma unroll
+                for (int cc = 0; cc < 3; cc++) hpl[3 * r + cc] += (B[12 + r] * w) * A[6 + cc];
+        }
         if (e.kf == lead_kf) {
             double* out = Hpl_out + (long long)kHplStride * lead;
 #pragma unroll
@@ -396,20 +407,24 @@ __device__ __forceinline__ void lin_poses_body(int pose, int lane, int npose_tot
         double om_r[3];
 #pragma unroll
         for (int k = 0; k < 3; k++) om_r[k] = (-(info * err[k])) * rho1;
+        // 2-D edges: zero row 2 skipped (bit-identical, as on the point side)
+        double s27[27];
 #pragma unroll
         for (int r = 0; r < 6; r++)
 #pragma unroll
-            for (int cc = r; cc < 6; cc++) {
-                double sacc = 0;
-                for (int k = 0; k < 3; k++) sacc += (B[6 * k + r] * w) * B[6 * k + cc];  // mono: row 2 is zero
-                acc[sym6(r, cc)] += sacc;
-            }
+            for (int cc = r; cc < 6; cc++) s27[sym6(r, cc)] = (0.0 + (B[r] * w) * B[cc]) + (B[6 + r] * w) * B[6 + cc];
 #pragma unroll
-        for (int cc = 0; cc < 6; cc++) {
-            double sacc = 0;
-            for (int k = 0; k < 3; k++) sacc += B[6 * k + cc] * om_r[k];  // mono: row 2 is zero
-            acc[21 + cc] += sacc;
+        for (int cc = 0; cc < 6; cc++) s27[21 + cc] = (0.0 + B[cc] * om_r[0]) + B[6 + cc] * om_r[1];
+        if (stereo) {
+#pragma unroll
+            for (int r = 0; r < 6; r++)
+#pragma unroll
+                for (int cc = r; cc < 6; cc++) s27[sym6(r, cc)] += (B[12 + r] * w) * B[12 + cc];
+#pragma unroll
+            for (int cc = 0; cc < 6; cc++) s27[21 + cc] += B[12 + cc] * om_r[2];
         }
+#pragma unroll
+        for (int k = 0; k < 27; k++) acc[k] += s27[k];
     }
     double mine = 0.0;
 #pragma unroll
@@ -541,7 +556,16 @@ __device__ inline void point_dinv(const double* __restrict__ Hll, long long p, d
 // (Eigen cofactor inverse) and db = Dinv b_l, one thread per point, kPdStride doubles each.  The
 // per-edge products B Dinv and B db are formed where they are used (k_schur_blocks), so no
 // per-edge record goes through HBM.
-constexpr int kPdStride = 12;  // Dinv (9, row-major), db (3)
+constexpr int kPdStride = 12;  // Dinv upper triangle (D00 D01 D02 D11 D12 D22), db (3), pad
+// Eigen's cofactor inverse of a symmetric 3x3 is symmetric bit for bit (every cofactor pairs
+// the same two products in the same order), so the upper triangle holds all of Dinv.
+__device__ __forceinline__ void pd_load(const double* __restrict__ o, double* Di, double* db) {
+    const double d00 = o[0], d01 = o[1], d02 = o[2], d11 = o[3], d12 = o[4], d22 = o[5];
+    Di[0] = d00; Di[1] = d01; Di[2] = d02;
+    Di[3] = d01; Di[4] = d11; Di[5] = d12;
+    Di[6] = d02; Di[7] = d12; Di[8] = d22;
+    db[0] = o[6]; db[1] = o[7]; db[2] = o[8];
+}
 __global__ void k_point_prep(int npt_total, const int* __restrict__ pt_win, const WinCtl* __restrict__ ctl,
                              const double* __restrict__ Hll, const double* __restrict__ bl, double* __restrict__ pd) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -552,10 +576,18 @@ __global__ void k_point_prep(int npt_total, const int* __restrict__ pt_win, cons
     point_dinv(Hll, p, C.lambda, Di);
     const double* b = bl + 4 * (long long)p;
     double* o = pd + (long long)kPdStride * p;
+    o[0] = Di[0]; o[1] = Di[1]; o[2] = Di[2]; o[3] = Di[4]; o[4] = Di[5]; o[5] = Di[8];
 #pragma unroll
-    for (int k = 0; k < 9; k++) o[k] = Di[k];
-#pragma unroll
-    for (int r = 0; r < 3; r++) o[9 + r] = Di[3 * r] * b[0] + Di[3 * r + 1] * b[1] + Di[3 * r + 2] * b[2];
+    for (int r = 0; r < 3; r++) o[6 + r] = Di[3 * r] * b[0] + Di[3 * r + 1] * b[1] + Di[3 * r + 2] * b[2];
+    o[9] = o[10] = o[11] = 0.0;
+}
+
+// 64-bit value of the partner lane (lane ^ 1): DPP quad_perm [1,0,3,2] on both halves
+__device__ __forceinline__ double swap_pair(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)b, 0xB1, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), 0xB1, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
 // value of lane j (compile-time) within each 32-lane half: ds_swizzle bit mode, and_mask 0,
@@ -794,33 +826,44 @@ __device__ __forceinline__ void schur_block_body(int wg, int nlist, const int* _
 #pragma unroll
     for (int k = 0; k < 18; k++) acc[k] = 0.0;
     double sb[3] = {0, 0, 0};
+    // The two lanes of a contribution load one half of Hpl_b each and trade halves by DPP; the
+    // next contribution's record is fetched while this one is computed.
     if (act) {
-        for (int k = ct_off[b] + j; k < ct_off[b + 1]; k += kStreams) {
-            const int4 ab = ct[k];
+        int k = ct_off[b] + j;
+        const int kend = ct_off[b + 1];
+        int4 nxt = k < kend ? ct[k] : int4{0, 0, 0, 0};
+        while (k < kend) {
+            const int4 ab = nxt;
+            k += kStreams;
+            if (k < kend) nxt = ct[k];
             const double* Ba = lin + (long long)kHplStride * ab.x + 9 * h;
-            const double* Bj = lin + (long long)kHplStride * ab.y;
-            const double* Dp = pd + (long long)kPdStride * ab.z;
-            double ba[9], di[12], bj[18], bd[9];
+            const double* Bo = lin + (long long)kHplStride * ab.y + 9 * h;
+            double ba[9], bo[9], di[9], db[3], bd[9], bj[18];
 #pragma unroll
             for (int t = 0; t < 9; t++) ba[t] = Ba[t];
 #pragma unroll
-            for (int t = 0; t < 12; t++) di[t] = Dp[t];
+            for (int t = 0; t < 9; t++) bo[t] = Bo[t];
+            pd_load(pd + (long long)kPdStride * ab.z, di, db);
 #pragma unroll
-            for (int t = 0; t < 18; t++) bj[t] = Bj[t];
+            for (int t = 0; t < 9; t++) {
+                const double other = swap_pair(bo[t]);
+                bj[t] = h ? other : bo[t];
+                bj[9 + t] = h ? bo[t] : other;
+            }
 #pragma unroll
             for (int r = 0; r < 3; r++)
 #pragma unroll
                 for (int c = 0; c < 3; c++)
                     bd[3 * r + c] = ba[3 * r] * di[c] + ba[3 * r + 1] * di[3 + c] + ba[3 * r + 2] * di[6 + c];
+            if (i1 == i2) {
+#pragma unroll
+                for (int r = 0; r < 3; r++) sb[r] += ba[3 * r] * db[0] + ba[3 * r + 1] * db[1] + ba[3 * r + 2] * db[2];
+            }
 #pragma unroll
             for (int r = 0; r < 3; r++)
 #pragma unroll
                 for (int c = 0; c < 6; c++)
                     acc[6 * r + c] += bd[3 * r] * bj[3 * c] + bd[3 * r + 1] * bj[3 * c + 1] + bd[3 * r + 2] * bj[3 * c + 2];
-            if (i1 == i2) {
-#pragma unroll
-                for (int r = 0; r < 3; r++) sb[r] += ba[3 * r] * di[9] + ba[3 * r + 1] * di[10] + ba[3 * r + 2] * di[11];
-            }
         }
     }
     // butterfly over the streams of the same half (lane bits 1..)
@@ -1435,7 +1478,8 @@ __device__ __forceinline__ void backsub_body(int p, int npt_total, const int* __
 #pragma unroll
                 for (int r = 0; r < 6; r++) cl[c] += H[3 * r + c] * (-xpp[r]);
         }
-        const double* Di = pd + (long long)kPdStride * p;  // k_point_prep's Dinv of this trial
+        double Di[9], db[3];
+        pd_load(pd + (long long)kPdStride * p, Di, db);  // k_point_prep's Dinv of this trial
 #pragma unroll
         for (int r = 0; r < 3; r++) x[r] = Di[3 * r] * cl[0] + Di[3 * r + 1] * cl[1] + Di[3 * r + 2] * cl[2];
     }
