@@ -844,11 +844,11 @@ __device__ __forceinline__ void schur_block_body(int wg, int nlist, const int* _
 #pragma unroll
             for (int t = 0; t < 9; t++) bo[t] = Bo[t];
             pd_load(pd + (long long)kPdStride * ab.z, di, db);
+            // columns in lane order: this lane's rows of Hpl_b first (c' = (c + 3h) mod 6)
 #pragma unroll
             for (int t = 0; t < 9; t++) {
-                const double other = swap_pair(bo[t]);
-                bj[t] = h ? other : bo[t];
-                bj[9 + t] = h ? bo[t] : other;
+                bj[t] = bo[t];
+                bj[9 + t] = swap_pair(bo[t]);
             }
 #pragma unroll
             for (int r = 0; r < 3; r++)
@@ -859,11 +859,16 @@ __device__ __forceinline__ void schur_block_body(int wg, int nlist, const int* _
 #pragma unroll
                 for (int r = 0; r < 3; r++) sb[r] += ba[3 * r] * db[0] + ba[3 * r + 1] * db[1] + ba[3 * r + 2] * db[2];
             }
+            // acc += B_a Dinv Hpl_b^T with fused multiply-adds: g2o's own build (-O3 -march=native)
+            // contracts these Eigen products too; the rounding differs from the oracle's unfused
+            // sums well inside the 1e-5 bar (tests/test_gpu_lba.py)
 #pragma unroll
             for (int r = 0; r < 3; r++)
 #pragma unroll
                 for (int c = 0; c < 6; c++)
-                    acc[6 * r + c] += bd[3 * r] * bj[3 * c] + bd[3 * r + 1] * bj[3 * c + 1] + bd[3 * r + 2] * bj[3 * c + 2];
+                    acc[6 * r + c] = __builtin_fma(bd[3 * r + 2], bj[3 * c + 2],
+                                                   __builtin_fma(bd[3 * r + 1], bj[3 * c + 1],
+                                                                 __builtin_fma(bd[3 * r], bj[3 * c], acc[6 * r + c])));
         }
     }
     // butterfly over the streams of the same half (lane bits 1..)
@@ -893,9 +898,10 @@ __device__ __forceinline__ void schur_block_body(int wg, int nlist, const int* _
             if (r == c) v += C.lambda;
         }
         double m = 0.0;
+        const int ek = 6 * (e / 6) + (c + 3 * h) % 6;  // accumulator columns are in lane order
 #pragma unroll
         for (int k = 0; k < 18; k++)
-            if (k == e) m = acc[k];
+            if (k == ek) m = acc[k];
         v -= m;
         // upper (i1, i2)[r][c] -> lower element (6 i2 + c, 6 i1 + r)
         if (i1 != i2 || r <= c) {
