@@ -191,3 +191,14 @@ def test_lba_stop_flag_mid_solve(solver):
     flag.value = False
     assert run() == n_full  # the flag is re-read per call
     assert any(0 < n < n_full for n in partial), (partial, n_full, t_call, dev_ms, plan_ms)
+
+
+def test_lba_large_window_and_mixed_batch(solver):
+    """5000 points: the per-pose point bitmaps span 79 words, so the device-built Schur
+    contribution lists (k_ct_fill) take more than one 64-word pass; batched with a config-4
+    window and a small one (different word counts per window)."""
+    big = synth.lba_window(60, n_pt=5000)
+    ws = [synth.lba_window(61, n_kf=12, n_pt=300, obs_per_pt=4), big, synth.lba_window(62)]
+    gs = solver.solve(ws)
+    for W, g in zip(ws, gs):
+        _check(g, ob.lba_solve(W))
