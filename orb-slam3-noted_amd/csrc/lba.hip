@@ -663,10 +663,12 @@ __device__ __forceinline__ void t16_put(double* Tw, int n, int R, int Cc, double
 //   bmp [same index]             set bits of pose i before word wd
 //   pls [W.spe0 + pbase[i] + r]  r-th free-pose edge (edge id) of pose i in point order
 __global__ void k_bm_set(int nspe_total, const int* __restrict__ spe, const EdgeS* __restrict__ E,
-                         const WinDesc* __restrict__ wins, unsigned long long* __restrict__ bm) {
+                         const WinDesc* __restrict__ wins, unsigned long long* __restrict__ bm,
+                         int* __restrict__ spe_hp) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= nspe_total) return;
     const EdgeS e = E[spe[s]];
+    spe_hp[s] = e.hp;  // free-pose index per spe entry (the back-substitution's xp row)
     const WinDesc& W = wins[e.win];
     const int lp = e.pt - W.pt0, i = e.hp - W.pose0;
     atomicOr(bm + W.bm0 + (long long)i * W.nwd + (lp >> 6), 1ull << (lp & 63));
@@ -1464,7 +1466,7 @@ __global__ void k_t16_pad(const WinDesc* __restrict__ wins, double* __restrict__
 
 // x_l = Dinv (b_l - Hpl^T x_p) (block_solver.hpp:456-481) and the trial point estimate.
 __device__ __forceinline__ void backsub_body(int p, int npt_total, const int* __restrict__ spe_off, const int* __restrict__ spe,
-                          const EdgeS* __restrict__ E, const int* __restrict__ pt_win,
+                          const int* __restrict__ spe_hp, const int* __restrict__ pt_win,
                           const WinCtl* __restrict__ ctl, const double* __restrict__ bl,
                           const double* __restrict__ pd, const double* __restrict__ lin,
                           const double* __restrict__ xp, double* __restrict__ xl, double* __restrict__ pts,
@@ -1475,14 +1477,34 @@ __device__ __forceinline__ void backsub_body(int p, int npt_total, const int* __
     double* x = xl + 4 * (long long)p;
     if (C.ok2) {  // a failed factorization leaves x untouched (block_solver.hpp:451-452)
         double cl[3] = {bl[4 * (long long)p], bl[4 * (long long)p + 1], bl[4 * (long long)p + 2]};
-        for (int i = spe_off[p]; i < spe_off[p + 1]; i++) {
-            const int e = spe[i];
-            const double* H = lin + (long long)kHplStride * e;
-            const double* xpp = xp + 6 * (long long)E[e].hp;
+        // two edges per step: both edges' Hpl and x_p rows are in flight together (same
+        // accumulation order as one edge at a time)
+        const int i1 = spe_off[p + 1];
+        for (int i = spe_off[p]; i < i1; i += 2) {
+            const bool two = i + 1 < i1;
+            const double* H0 = lin + (long long)kHplStride * spe[i];
+            const double* x0 = xp + 6 * (long long)spe_hp[i];
+            const double* H1 = lin + (long long)kHplStride * spe[two ? i + 1 : i];
+            const double* x1 = xp + 6 * (long long)spe_hp[two ? i + 1 : i];
+            double h0[18], v0[6], h1[18], v1[6];
+#pragma unroll
+            for (int k = 0; k < 18; k++) h0[k] = H0[k];
+#pragma unroll
+            for (int k = 0; k < 6; k++) v0[k] = x0[k];
+#pragma unroll
+            for (int k = 0; k < 18; k++) h1[k] = H1[k];
+#pragma unroll
+            for (int k = 0; k < 6; k++) v1[k] = x1[k];
 #pragma unroll
             for (int c = 0; c < 3; c++)
 #pragma unroll
-                for (int r = 0; r < 6; r++) cl[c] += H[3 * r + c] * (-xpp[r]);
+                for (int r = 0; r < 6; r++) cl[c] += h0[3 * r + c] * (-v0[r]);
+            if (two) {
+#pragma unroll
+                for (int c = 0; c < 3; c++)
+#pragma unroll
+                    for (int r = 0; r < 6; r++) cl[c] += h1[3 * r + c] * (-v1[r]);
+            }
         }
         double Di[9], db[3];
         pd_load(pd + (long long)kPdStride * p, Di, db);  // k_point_prep's Dinv of this trial
@@ -1518,7 +1540,7 @@ __device__ __forceinline__ void pose_update_body(int k, int nkf_total, const int
 __global__ void __launch_bounds__(256) k_update(int nb_kf, int nkf_total, const int* __restrict__ kf_hp,
                                                 const int* __restrict__ kf_win, int npt_total,
                                                 const int* __restrict__ spe_off, const int* __restrict__ spe,
-                                                const EdgeS* __restrict__ E, const int* __restrict__ pt_win,
+                                                const int* __restrict__ spe_hp, const int* __restrict__ pt_win,
                                                 const WinCtl* __restrict__ ctl, const double* __restrict__ bl,
                                                 const double* __restrict__ pd, const double* __restrict__ lin,
                                                 const double* __restrict__ xp, double* __restrict__ xl,
@@ -1528,7 +1550,7 @@ __global__ void __launch_bounds__(256) k_update(int nb_kf, int nkf_total, const 
     if (b < nb_kf)
         pose_update_body(b * 256 + threadIdx.x, nkf_total, kf_hp, kf_win, ctl, xp, poses, pose_stride);
     else
-        backsub_body((b - nb_kf) * 256 + threadIdx.x, npt_total, spe_off, spe, E, pt_win, ctl, bl, pd, lin, xp, xl,
+        backsub_body((b - nb_kf) * 256 + threadIdx.x, npt_total, spe_off, spe, spe_hp, pt_win, ctl, bl, pd, lin, xp, xl,
                      pts, pt_stride);
 }
 
@@ -1818,6 +1840,7 @@ struct slam_lba {
     DevBuf arena, cnt;
     DevBuf poses, pts, err, rho, lin, Hll, bl, Hpp, bp, pd, xp, xl, Hs, Ts;
     DevBuf bm, bmp, pbase, pls;  // pose bitmaps, their word prefixes, pose list bases, pose edge lists
+    DevBuf spe_hp;               // free-pose index of every spe entry
     DevBuf ct, ct_off, ct_cnt;   // Schur contribution lists (built on the device)
     DevBuf kf_out, pt_out, outl;
 };
@@ -2254,6 +2277,7 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     SLAM_HIP_TRY(s->bmp.ensure(sizeof(int) * std::max<long long>(Z.nbm, 1)));
     SLAM_HIP_TRY(s->pbase.ensure(sizeof(int) * nps));
     SLAM_HIP_TRY(s->pls.ensure(sizeof(int) * std::max(Z.nspe, 1)));
+    SLAM_HIP_TRY(s->spe_hp.ensure(sizeof(int) * std::max(Z.nspe, 1)));
     SLAM_HIP_TRY(s->ct.ensure(sizeof(int4) * std::max<long long>(Z.nct, 1)));
     SLAM_HIP_TRY(s->ct_off.ensure(sizeof(int) * (Z.nblk + 1)));
     SLAM_HIP_TRY(s->ct_cnt.ensure(sizeof(int) * std::max(Z.nblk, 1)));
@@ -2320,7 +2344,8 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
                                                          poses, pts);
     k_ldlt_pad<<<nw, 64, 0, S>>>(dW, as<double>(s->Hs));
     if (Z.nspe) {  // the Schur contribution structure, once per solve
-        k_bm_set<<<blocks(Z.nspe, T), T, 0, S>>>(Z.nspe, DP.spe, DP.edges, DP.wins, as<unsigned long long>(s->bm));
+        k_bm_set<<<blocks(Z.nspe, T), T, 0, S>>>(Z.nspe, DP.spe, DP.edges, DP.wins, as<unsigned long long>(s->bm),
+                                                  as<int>(s->spe_hp));
         k_bm_scan<<<nw, 64, 0, S>>>(DP.wins, as<unsigned long long>(s->bm), as<int>(s->bmp), as<int>(s->pbase));
         k_bm_list<<<blocks(Z.nspe, T), T, 0, S>>>(Z.nspe, DP.spe, DP.edges, DP.wins, as<unsigned long long>(s->bm),
                                                    as<int>(s->bmp), as<int>(s->pbase), as<int>(s->pls));
@@ -2395,7 +2420,7 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
         else
             k_ldlt<<<nw, 512, lds_bytes, S>>>(dW, dC, as<double>(s->Hs), as<double>(s->xp));
         if (nb_upd)
-            k_update<<<nb_upd, 256, 0, S>>>(nb_kf, H.nkf, DP.kf_hp, DP.kf_win, H.npt, DP.spe_off, DP.spe, dE,
+            k_update<<<nb_upd, 256, 0, S>>>(nb_kf, H.nkf, DP.kf_hp, DP.kf_win, H.npt, DP.spe_off, DP.spe, as<int>(s->spe_hp),
                                             DP.pt_win, dC, as<double>(s->bl), as<double>(s->pd), as<double>(s->lin),
                                             as<double>(s->xp), as<double>(s->xl), poses, pose_stride, pts, pt_stride);
         if (H.ne)
