@@ -26,6 +26,14 @@ oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -rf $(LIBDIR) oracle/build tests/cpp/host_driver tests/cpp/shim_driver
+	rm -rf $(LIBDIR) oracle/build tests/cpp/host_driver tests/cpp/shim_driver tests/cpp/*_asan
 
-.PHONY: all oracle clean
+# host-side sanitizer builds (test infrastructure; GPU code is never instrumented): the oracle
+# with ASan + UBSan, and the C++ host-layer / shim drivers with ASan + UBSan (tools/sanitize.sh)
+SAN := -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -fno-sanitize-recover=undefined
+sanitize: $(LIBDIR)/libslamhot.so
+	cd oracle && g++ $(SAN) -march=x86-64-v3 -ffp-contract=off -fPIC -std=c++17 -shared -o build/liboracle_asan.so *.cpp -lpthread
+	g++ $(SAN) -std=c++17 -Iinclude -o tests/cpp/host_driver_asan tests/cpp/host_driver.cpp -L$(LIBDIR) -lslamhot -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)'
+	g++ $(SAN) -std=c++17 -Iinclude -o tests/cpp/shim_driver_asan tests/cpp/shim_driver.cpp -L$(LIBDIR) -lslamhot -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)'
+
+.PHONY: all oracle clean sanitize

@@ -3,6 +3,7 @@ include/slamhot_orbslam3.hpp on ORB-SLAM3 stand-ins).  The map written here is t
 Python mirror (slamhot.optimizer) holds, so both sides start from identical objects."""
 from __future__ import annotations
 
+import os
 import struct
 import subprocess
 from pathlib import Path
@@ -10,7 +11,7 @@ from pathlib import Path
 import numpy as np
 
 ROOT = Path(__file__).resolve().parents[1]
-DRIVER = ROOT / "tests" / "cpp" / "shim_driver"
+DRIVER = Path(os.environ.get("SLAMHOT_SHIM_DRIVER", str(ROOT / "tests" / "cpp" / "shim_driver")))  # sanitizer builds: tools/sanitize.sh
 
 
 def write_map(path, pmap, kfs, mps, cur_index=-1):

@@ -5,6 +5,7 @@ bit-exact keypoints / descriptors / pyramid / match indices, LBA within 1e-5.
 
 The not-gpu test checks the other half of the contract: without a gfx950 device the C++
 layer raises slamhot::Error(SLAM_ENODEV) (exit code 3) instead of computing anything."""
+import os
 import subprocess
 from pathlib import Path
 
@@ -15,7 +16,7 @@ import oracle_bind as ob
 from slamhot import synth
 
 ROOT = Path(__file__).resolve().parents[1]
-DRIVER = ROOT / "tests" / "cpp" / "host_driver"
+DRIVER = Path(os.environ.get("SLAMHOT_HOST_DRIVER", str(ROOT / "tests" / "cpp" / "host_driver")))  # sanitizer builds: tools/sanitize.sh
 
 
 def _run(*args, check=True):
