@@ -1162,7 +1162,10 @@ __device__ __forceinline__ int refl101(int i, int n) {
 constexpr int kO3R = 43, kO3Pairs = 22, kO3RawS = 13, kO3HS = 40, kO3BlS = 40;
 
 __global__ void __launch_bounds__(256) k_orb3(Bufs b) {
-    __shared__ __attribute__((aligned(16))) uint32_t raw_all[4][2 * kO3Pairs * kO3RawS];
+    // 43 staged rows (the horizontal pass also reads a 44th, whose sums are discarded: for the
+    // last wave that read lands in hp_all, still inside this workgroup's LDS).  43 rows instead
+    // of 44 keep the workgroup at 23,024 B: 7 workgroups (28 waves) per CU instead of 6.
+    __shared__ __attribute__((aligned(16))) uint32_t raw_all[4][kO3R * kO3RawS];
     __shared__ __attribute__((aligned(16))) uint32_t hp_all[4][kO3Pairs * kO3HS];
     const DevPlan& P = *b.plan;
     const int f = blockIdx.y;
