@@ -4,19 +4,20 @@
 // + BlockSolver<6,3> + LinearSolverEigen (SimplicialLDLT).  Here one call solves a batch of
 // independent windows; every window's state (poses, points, Hessian blocks, the dense Schur
 // complement, the LM scalars) lives in HBM for the whole solve, and each LM decision is taken
-// on the device by a per-window control kernel.  The host only launches kernels and reads
-// back two counters per trial (windows still trying / still iterating) plus the stop flag.
+// on the device by a per-window control kernel.  The host queues LM steps (every kernel below
+// skips the windows a step does not concern) and polls a step counter the last control block
+// publishes into mapped memory, mirroring the caller's stop flag meanwhile.
 //
-// Kernels (per LM iteration, all windows of the batch in one launch each):
-//   k_lin_points     thread / point : errors, Huber rho, Hpl = B^T W A per edge, Hll and b_l
-//   k_lin_poses      wave / pose    : Hpp (6x6) and b_p over the pose's edges
-//   k_iter_begin     block / window : chi2 = sum rho, lambda init (iteration 0)
-// per LM trial:
+// Once per solve: k_bm_set / k_bm_scan / k_bm_list (per-pose point bitmaps and point-ordered
+// edge lists) and k_ct_count / k_ct_scan / k_ct_fill (each Schur block's contribution list).
+// Per LM step (all windows of the batch in one launch each):
+//   k_linearize      wave / free pose (Hpp, b_p) + thread / point (errors, Huber rho, Hpl, Hll, b_l)
+//   k_iter_begin     block / window : chi2 = sum rho, lambda init (iteration 0), stop flag
 //   k_point_prep     thread / point : Dinv = (Hll + lambda I)^-1, db = Dinv b_l
-//   k_schur_block    wave / 6x6 block of the Schur complement (lower triangle + rhs row)
-//   k_ldlt           block / window : dense LDL^T of the (n+1) x (n+1) augmented system
-//   k_backsub        thread / point : x_l = Dinv (b_l - Hpl^T x_p), trial point
-//   k_pose_update    thread / KF    : trial pose = exp(x_p) * pose
+//   k_schur_blocks   lanes / 6x6 block of the Schur complement (B Dinv Hpl^T per contribution,
+//                    rhs row), written into the tile-major LDL^T scratch
+//   k_ldlt_t16       block / window : tile LDL^T on v_mfma_f64_16x16x4f64 (k_ldlt above 288)
+//   k_update         thread / KF (exp(x_p) * pose) + thread / point (x_l = Dinv (b_l - Hpl^T x_p))
 //   k_trial_error    thread / edge  : error + rho at the trial state
 //   k_trial_control  block / window : rho, accept (swap state) or reject, lambda, stop rules
 // FP64 throughout, with the reference's float quirks (see oracle/lba_oracle.cpp).
