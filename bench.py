@@ -145,7 +145,9 @@ def roofline_from_stages(stages, calls, frames_per_call, W, H, kps_per_frame):
         "traffic": traffic,
         "algorithmic_bytes_per_launch": int(dom_bytes),
         "frames_per_launch": frames_per_launch,
-        "measured": "HIP events on the launch stream, isolated pass after the timed region (1 batch in flight)",
+        "measured": "HIP events on the launch stream around the kernel's stage of one batch, isolated pass after "
+                    "the timed region (1 batch in flight); k_fast_wave's stage is two dispatches (cell classes B then "
+                    "A, DESIGN.md §2): rocprof's per-dispatch average is about half of avg_launch_ms",
         "avg_launch_ms": round(avg_s * 1000.0, 5),
     }
     if valu:

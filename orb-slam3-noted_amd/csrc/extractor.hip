@@ -1456,7 +1456,8 @@ struct slam_extractor {
     Plan plan;
     DevBuf d_plan, d_xtab, d_ytab, d_cells, d_wave_cells, d_wide_cells;
     int n_wave_cells = 0, n_wide_cells = 0;
-    FastWaveLds fw_lay{};
+    FastWaveLds fw_lay{}, fw_lay_b{};  // layouts of the two wave-cell classes (see below)
+    int n_wave_a = 0;                  // d_wave_cells: class A cells first, then class B
     // per-batch buffers
     DevBuf d_img, d_pyr, d_cell_keys, d_cell_cnt, d_keys_g, d_knode_g, d_okp, d_ocnt,
         d_oidx, d_err, d_kps, d_desc, d_n, d_mono;
@@ -1548,30 +1549,63 @@ static slam_status ensure_plan(slam_extractor* ex, int W, int H) {
         // cells whose tested region fits one wave (<= 64 columns, <= kRoiRows rows) take the
         // wave-per-cell kernel; the rest (tiny levels of small images) the workgroup kernel
         std::vector<int32_t> wave, wide;
-        int ch_max = 0, th_max = 0, tw_max = 0, cw_max = 0;
+        std::vector<const CellDesc*> wc;
         for (const CellDesc& c : P.cells) {
-            if (c.cw - 6 <= 64 && c.ch <= kRoiRows && c.cw + 3 <= kRoiStride) {
-                wave.push_back(c.slot);
+            if (c.cw - 6 <= 64 && c.ch <= kRoiRows && c.cw + 3 <= kRoiStride) wc.push_back(&c);
+            else wide.push_back(c.slot);
+        }
+        // Two classes, each with an LDS layout sized to its own largest cell: class A = the
+        // cells that fit the most common cell's box (the full cells of the fine levels), class
+        // B = the rest (clipped or coarse-level cells up to ~46 x 57).  One layout for all
+        // would size every wave for the largest cell (EuRoC: 9.4 KB, 4 workgroups per CU); class
+        // A needs 6.5 KB (6 per CU) and holds ~3/4 of the cells.
+        int box_w = 0, box_h = 0;
+        {
+            std::vector<std::pair<int, int>> dims;
+            for (const CellDesc* c : wc) dims.emplace_back(c->cw, c->ch);
+            std::sort(dims.begin(), dims.end());
+            int best = 0;
+            for (size_t i = 0; i < dims.size();) {
+                size_t j = i;
+                while (j < dims.size() && dims[j] == dims[i]) j++;
+                if ((int)(j - i) > best) {
+                    best = (int)(j - i);
+                    box_w = dims[i].first;
+                    box_h = dims[i].second;
+                }
+                i = j;
+            }
+        }
+        if (std::getenv("SLAMHOT_FAST_ONE_CLASS")) box_w = box_h = 1 << 20;
+        std::vector<int32_t> wave_b;
+        for (const CellDesc* c : wc) (c->cw <= box_w && c->ch <= box_h ? wave : wave_b).push_back(c->slot);
+        auto r16 = [](int v) { return (v + 15) & ~15; };
+        auto layout_of = [&](const std::vector<int32_t>& list) {
+            int ch_max = 0, th_max = 0, tw_max = 0, cw_max = 0;
+            for (int32_t sl : list) {
+                const CellDesc& c = P.cells[sl];
                 ch_max = std::max(ch_max, (int)c.ch);
                 th_max = std::max(th_max, c.ch - 6);
                 tw_max = std::max(tw_max, c.cw - 6);
                 cw_max = std::max(cw_max, (int)c.cw);
-            } else {
-                wide.push_back(c.slot);
             }
-        }
-        auto r16 = [](int v) { return (v + 15) & ~15; };
-        FastWaveLds lay;
-        // ROI rows: staged dwords reach byte sh + cw + 3 and pass A reads one dword past its
-        // last group, so cw + 8 bytes (rounded to dwords) cover every access
-        lay.rs = std::min(kRoiStride, (cw_max + 8 + 3) & ~3);
-        lay.ms = tw_max + 2;
-        lay.roi = 0;
-        lay.map = r16(ch_max * lay.rs);
-        lay.lst = lay.map + r16((th_max + 2) * lay.ms);
-        lay.total = lay.lst + r16(std::max(1, tw_max * th_max) * 2);
+            FastWaveLds lay;
+            // ROI rows: staged dwords reach byte sh + cw + 3 and pass A reads one dword past its
+            // last group, so cw + 8 bytes (rounded to dwords) cover every access
+            lay.rs = std::min(kRoiStride, (cw_max + 8 + 3) & ~3);
+            lay.ms = tw_max + 2;
+            lay.roi = 0;
+            lay.map = r16(ch_max * lay.rs);
+            lay.lst = lay.map + r16((th_max + 2) * lay.ms);
+            lay.total = lay.lst + r16(std::max(1, tw_max * th_max) * 2);
+            return lay;
+        };
+        FastWaveLds lay = layout_of(wave);
+        ex->fw_lay_b = layout_of(wave_b);
+        ex->n_wave_a = (int)wave.size();
+        wave.insert(wave.end(), wave_b.begin(), wave_b.end());
         ex->fw_lay = lay;
-        if (4 * lay.total > 160 * 1024) return SLAM_EINVAL;
+        if (4 * lay.total > 160 * 1024 || 4 * ex->fw_lay_b.total > 160 * 1024) return SLAM_EINVAL;
         SLAM_HIP_TRY(hipFuncSetAttribute((const void*)k_fast_wave, hipFuncAttributeMaxDynamicSharedMemorySize,
                                          160 * 1024));
         if ((st = ex->d_wave_cells.ensure(std::max<size_t>(4, wave.size() * 4))) ||
@@ -1701,10 +1735,15 @@ static slam_status launch_range(slam_extractor* ex, int f0, int nframes, const u
     // orb then overlap the next range's FAST
     if (fast_after) SLAM_HIP_TRY(hipStreamWaitEvent(s, fast_after, 0));
     begin(kStFast);
-    if (ex->n_wave_cells && !SKIP(kStFast))
-        hipLaunchKernelGGL(k_fast_wave, dim3((ex->n_wave_cells + 3) / 4, nframes), dim3(256),
-                           4 * ex->fw_lay.total + fast_pad, s, b, ex->d_wave_cells.as<int32_t>(), ex->n_wave_cells,
-                           ex->fw_lay);
+    if (!SKIP(kStFast)) {  // class B cells (larger LDS layout, fewer), then class A
+        const int na = ex->n_wave_a, nb = ex->n_wave_cells - ex->n_wave_a;
+        if (nb)
+            hipLaunchKernelGGL(k_fast_wave, dim3((nb + 3) / 4, nframes), dim3(256), 4 * ex->fw_lay_b.total + fast_pad,
+                               s, b, ex->d_wave_cells.as<int32_t>() + na, nb, ex->fw_lay_b);
+        if (na)
+            hipLaunchKernelGGL(k_fast_wave, dim3((na + 3) / 4, nframes), dim3(256), 4 * ex->fw_lay.total + fast_pad, s,
+                               b, ex->d_wave_cells.as<int32_t>(), na, ex->fw_lay);
+    }
     if (ex->n_wide_cells)
         hipLaunchKernelGGL(k_fast_cells, dim3(ex->n_wide_cells, nframes), dim3(256), 0, s, b,
                            ex->d_wide_cells.as<int32_t>());

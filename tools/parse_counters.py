@@ -48,12 +48,16 @@ def main():
         k = sys.argv[2]
         f = float(cal.get(fac.get(k, "16"), 2.0))
         d = summary[k]
-        meta = dict(kernel=k, batch=int(sys.argv[3]), width=int(sys.argv[4]), bytes_per_launch=int(traffic[k]),
-                    fetch_size_kib=d["FETCH_SIZE"], write_size_kib=d["WRITE_SIZE"], fetch_factor=f,
-                    valu_instr_per_launch=d.get("SQ_INSTS_VALU"),
+        # dispatches of the kernel per batch (k_fast_wave: one per cell class):
+        # the per-dispatch means times this are the batch's figures, what bench.py's roofline uses
+        nd = int(sys.argv[5]) if len(sys.argv) > 5 else 1
+        meta = dict(kernel=k, batch=int(sys.argv[3]), width=int(sys.argv[4]), dispatches_per_batch=nd,
+                    bytes_per_launch=int(nd * traffic[k]),
+                    fetch_size_kib=nd * d["FETCH_SIZE"], write_size_kib=nd * d["WRITE_SIZE"], fetch_factor=f,
+                    valu_instr_per_launch=nd * d["SQ_INSTS_VALU"] if d.get("SQ_INSTS_VALU") else None,
                     lds_bank_conflict_per_lds_active=(d["SQ_LDS_BANK_CONFLICT"] / d["SQ_ACTIVE_INST_LDS"]
                                                       if d.get("SQ_ACTIVE_INST_LDS") else None),
-                    note=f"{f:g} x FETCH_SIZE + WRITE_SIZE; the FETCH_SIZE factor is measured for this kernel's "
+                    note=f"({f:g} x FETCH_SIZE + WRITE_SIZE) x {nd} dispatches per batch; the FETCH_SIZE factor is measured for this kernel's "
                          f"{fac.get(k, '16')} B/lane loads by tools/microbench/mb_fetch (profiles/fetch_calibration.json)")
         Path("profiles/traffic_latest.json").write_text(json.dumps(meta, indent=1))
 
