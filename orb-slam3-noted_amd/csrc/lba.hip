@@ -2279,10 +2279,10 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     SLAM_HIP_TRY(s->pbase.ensure(sizeof(int) * nps));
     SLAM_HIP_TRY(s->pls.ensure(sizeof(int) * std::max(Z.nspe, 1)));
     SLAM_HIP_TRY(s->spe_hp.ensure(sizeof(int) * std::max(Z.nspe, 1)));
+    if (Z.nct >= (1LL << 31)) return SLAM_ECAP;  // int contribution offsets
     SLAM_HIP_TRY(s->ct.ensure(sizeof(int4) * std::max<long long>(Z.nct, 1)));
     SLAM_HIP_TRY(s->ct_off.ensure(sizeof(int) * (Z.nblk + 1)));
     SLAM_HIP_TRY(s->ct_cnt.ensure(sizeof(int) * std::max(Z.nblk, 1)));
-    if (Z.nct >= (1LL << 31)) return SLAM_ECAP;  // int offsets
     SLAM_HIP_TRY(hipMemsetAsync(s->bm.p, 0, sizeof(unsigned long long) * std::max<long long>(Z.nbm, 1), S));
     // tile LDL^T (k_ldlt_t16) when every window fits 18 tile rows (SLAMHOT_LDLT=panel: old kernel)
     const char* ldlt_env = std::getenv("SLAMHOT_LDLT");
