@@ -1237,38 +1237,37 @@ __global__ void __launch_bounds__(256) k_orb3(Bufs b) {
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     ORB_MARK();
-    const uint8_t* rawb = reinterpret_cast<const uint8_t*>(raw);
 
     // ---- orientation (IC_Angle, ORBextractor.cc:75-102) on the raw centre 31x31
+    // Lane = (disc row v, half): the row's bytes as staged dwords (row 21 + v, dwords 1..5 for
+    // half 0, 6..10 for half 1: bytes 4..39 hold every column kx-15..kx+15 for any sh), the
+    // disc's byte range |u| <= umax[|v|] as a per-dword byte mask, and two v_dot4 per dword:
+    // the row sum (weights 1) and the byte-offset moment (weights = byte offset b), so
+    // sum u I = moment - (sh + 21) sum.  Exact integers, like the reference's loops.
     int m01 = 0, m10 = 0;
     {
-        const int cl = lane & 31, half = lane >> 5;
-        const int u = cl - kHalfPatch;
-        const int au = u < 0 ? -u : u;
-        // umax is non-increasing in v: column u is inside the disc for |v| < nv
-        int nv = 0;
+        const int row = lane >> 1, half = lane & 1;
+        const int v = row - kHalfPatch;
+        const int d = __shfl(um, v < 0 ? -v : v, 64);  // umax[|v|]
+        if (row < 2 * kHalfPatch + 1) {
+            const int c0 = sh + 21;                    // byte offset of column u = 0
+            const int lo = c0 - d, hi = c0 + d;        // byte range of the disc row
+            const uint32_t* rp = raw + (21 + v) * kO3RawS;
+            const int k0 = half ? 6 : 1;  // five dwords per lane (dword 10 lies past hi: masked out)
+            uint32_t s0 = 0, s1 = 0;
 #pragma unroll
-        for (int v = 0; v <= kHalfPatch; v++) nv += (int)(au <= __builtin_amdgcn_readlane(um, v));
-        if (cl < 2 * kHalfPatch + 1) {
-            const uint8_t* colp = rawb + 21 * (4 * kO3RawS) + sh + 21 + u;
-            int s0 = 0, s1 = 0;
-            if (half == 0) {
-#pragma unroll
-                for (int v = -kHalfPatch; v <= 0; v++) {
-                    const int val = colp[v * (4 * kO3RawS)] & -(int)(-v < nv);
-                    s0 += val;
-                    s1 += v * val;
-                }
-            } else {
-#pragma unroll
-                for (int v = 1; v <= kHalfPatch; v++) {
-                    const int val = colp[v * (4 * kO3RawS)] & -(int)(v < nv);
-                    s0 += val;
-                    s1 += v * val;
-                }
+            for (int i = 0; i < 5; i++) {
+                const int k = k0 + i;
+                const int a0 = min(max(lo - 4 * k, 0), 4), e0 = min(max(hi + 1 - 4 * k, 0), 4);
+                const uint32_t mhi = e0 >= 4 ? 0xFFFFFFFFu : ((1u << (8 * e0)) - 1u);
+                const uint32_t mlo = a0 >= 4 ? 0xFFFFFFFFu : ((1u << (8 * a0)) - 1u);
+                const uint32_t x = rp[k] & mhi & ~mlo;
+                const uint32_t wk = (uint32_t)(4 * k) * 0x01010101u + 0x03020100u;  // bytes 4k .. 4k+3
+                s0 = __builtin_amdgcn_udot4(x, 0x01010101u, s0, false);
+                s1 = __builtin_amdgcn_udot4(x, wk, s1, false);
             }
-            m10 = u * s0;
-            m01 = s1;
+            m10 = (int)s1 - c0 * (int)s0;
+            m01 = v * (int)s0;
         }
     }
     m10 = wave_sum_dpp(m10);
