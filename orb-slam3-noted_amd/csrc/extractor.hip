@@ -1174,6 +1174,34 @@ __device__ __forceinline__ int refl101(int i, int n) {
 // ---------------------------------------------------------------------------------------
 constexpr int kO3R = 43, kO3Pairs = 22, kO3RawS = 13, kO3HS = 40, kO3BlS = 40;
 
+// Horizontal-pass items (row pair p, 4-column group q) that a sampled pixel can depend on.  A
+// pattern point of radius r lands, rotated and rounded to the pixel grid, within r + sqrt(2)/2
+// of the keypoint; the largest r is 13 sqrt(2) = 18.385, so every sampled offset (dy, dx) has
+// dy^2 + dx^2 <= 364 (19.092^2 = 364.5).  Blurred pixel (y, x) reads row sums y .. y+6 of column x.
+// 189 of the 22 x 10 items qualify; the corner items' row sums stay unwritten and only feed
+// blurred corner pixels no sample reads.
+struct HItems {
+    uint8_t v[kO3Pairs * 10];
+    int n;
+};
+constexpr HItems make_hitems() {
+    bool need[kO3Pairs][10] = {};
+    for (int dy = -18; dy <= 18; dy++)
+        for (int dx = -18; dx <= 18; dx++) {
+            if (dy * dy + dx * dx > 364) continue;
+            for (int hr = dy + 18; hr <= dy + 24; hr++) need[hr / 2][(dx + 18) / 4] = true;
+        }
+    HItems h{};
+    for (int p = 0; p < kO3Pairs; p++)
+        for (int q = 0; q < 10; q++)
+            if (need[p][q]) h.v[h.n++] = (uint8_t)(p * 10 + q);  // item index of the full 22 x 10 grid
+    return h;
+}
+constexpr HItems kHItemsTable = make_hitems();
+constexpr int kHItems = kHItemsTable.n;
+static_assert(kHItems <= 192, "horizontal pass items must fit three wave passes");
+__constant__ HItems c_hitems = kHItemsTable;
+
 __global__ void __launch_bounds__(256) k_orb3(Bufs b) {
     // 43 staged rows (the horizontal pass also reads a 44th, whose sums are discarded: for the
     // last wave that read lands in hp_all, still inside this workgroup's LDS).  43 rows instead
@@ -1308,8 +1336,8 @@ __global__ void __launch_bounds__(256) k_orb3(Bufs b) {
         h[3] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(E2, E1, 3), KB,
                                       __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(E1, E0, 3), KA, 0u, false), false);
     };
-    for (int it = lane; it < kO3Pairs * 10; it += 64) {
-        const int p = it / 10, q = it - p * 10;
+    for (int it = lane; it < kHItems; it += 64) {  // 3 passes of the wave instead of 4
+        const int pq = c_hitems.v[it], p = pq / 10, q = pq - p * 10;
         uint32_t h0[4], h1[4];
         hrow4(raw + (2 * p) * kO3RawS + q, h0);
         hrow4(raw + (2 * p + 1) * kO3RawS + q, h1);
