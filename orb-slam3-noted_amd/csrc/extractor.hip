@@ -1167,12 +1167,12 @@ __device__ __forceinline__ int refl101(int i, int n) {
 // integer arithmetic as the OpenCV 8U fixed-point path (Q8 taps, exact row sums, rounded
 // (acc + 2^15) >> 16, BORDER_REFLECT_101 at the level bounds), so the bits are those of the
 // whole-level blur; the blurred level is never written to HBM.
-//   raw: 43 (+1) rows x 13 dwords (staged byte j <-> level column xs + j, xs = (kx-21) & ~3)
+//   raw: 43 rows x 12 dwords (staged byte j <-> level column xs + j, xs = (kx-21) & ~3)
 //   hp : 22 row pairs x 40 dwords of exact horizontal sums, rows 2p | 2p+1 << 16 (column
 //        c <-> kx - 18 + c)
 //   bl : 37 rows x 40 bytes, aliased onto raw once the horizontal pass has read it
 // ---------------------------------------------------------------------------------------
-constexpr int kO3R = 43, kO3Pairs = 22, kO3RawS = 13, kO3HS = 40, kO3BlS = 40;
+constexpr int kO3R = 43, kO3Pairs = 22, kO3RawS = 12, kO3HS = 40, kO3BlS = 40;
 
 // Horizontal-pass items (row pair p, 4-column group q) that a sampled pixel can depend on.  A
 // pattern point of radius r lands, rotated and rounded to the pixel grid, within r + sqrt(2)/2
@@ -1203,9 +1203,9 @@ static_assert(kHItems <= 192, "horizontal pass items must fit three wave passes"
 __constant__ HItems c_hitems = kHItemsTable;
 
 __global__ void __launch_bounds__(256) k_orb3(Bufs b) {
-    // 43 staged rows (the horizontal pass also reads a 44th, whose sums are discarded: for the
-    // last wave that read lands in hp_all, still inside this workgroup's LDS).  43 rows instead
-    // of 44 keep the workgroup at 23,024 B: 7 workgroups (28 waves) per CU instead of 6.
+    // 43 staged rows of 48 B (the horizontal pass also reads a 44th, whose sums are discarded:
+    // for the last wave that read lands in hp_all, still inside this workgroup's LDS): 22,336 B
+    // per workgroup, 7 workgroups (28 waves) per CU.
     __shared__ __attribute__((aligned(16))) uint32_t raw_all[4][kO3R * kO3RawS];
     __shared__ __attribute__((aligned(16))) uint32_t hp_all[4][kO3Pairs * kO3HS];
     const DevPlan& P = *b.plan;
@@ -1268,11 +1268,7 @@ __global__ void __launch_bounds__(256) k_orb3(Bufs b) {
             const int e = lane + 64 * k;
             if (e < kO3R * 3) {
                 const int r = e / 3, part = e - 3 * r;
-                uint32_t* d = raw + r * kO3RawS + 4 * part;
-                d[0] = v[k].x;
-                d[1] = v[k].y;
-                d[2] = v[k].z;
-                d[3] = v[k].w;
+                *reinterpret_cast<uint4*>(raw + r * kO3RawS + 4 * part) = v[k];  // 16-byte aligned (48-byte rows)
             }
         }
     }
