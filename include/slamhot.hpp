@@ -17,8 +17,10 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <memory>
 #include <stdexcept>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "slamhot.h"
@@ -192,17 +194,44 @@ inline std::vector<float> ComputeImageBounds(const PinholeCalib& c, int cols, in
 struct KeyFrameBow : slam_bow_side {};  // pKF: descriptors, angles, MapPoint validity, mFeatVec
 struct FrameBow : slam_bow_side {};     // F: descriptors, angles, mFeatVec (valid ignored)
 
+/* The device half of a matcher: one slam_matcher handle (device scratch + a private stream).
+ * The reference builds ORBmatcher(nnratio, checkOri) on the stack at every call site, with a
+ * different ratio per site on the same thread (Tracking.cc:2566 0.7, :2700 0.9, :3475 0.75,
+ * :3218 0.8), so the handle lives once per (thread, device) and every ORBmatcher is a light view
+ * over it carrying its own nnratio / checkOri.  A slam_matcher is not shared between threads. */
+class MatcherDevice {
+   public:
+    explicit MatcherDevice(int device) { check(slamhot_matcher_create(device, &m_), "ORBmatcher"); }
+    ~MatcherDevice() { slamhot_matcher_destroy(m_); }
+    MatcherDevice(const MatcherDevice&) = delete;
+    MatcherDevice& operator=(const MatcherDevice&) = delete;
+    slam_matcher* handle() const { return m_; }
+
+    /* this thread's handle on `device`, created on first use, destroyed at thread exit */
+    static slam_matcher* ForThisThread(int device) {
+        static thread_local std::vector<std::pair<int, std::unique_ptr<MatcherDevice>>> per_device;
+        for (auto& d : per_device)
+            if (d.first == device) return d.second->handle();
+        per_device.emplace_back(device, std::unique_ptr<MatcherDevice>(new MatcherDevice(device)));
+        return per_device.back().second->handle();
+    }
+
+   private:
+    slam_matcher* m_ = nullptr;
+};
+
 class ORBmatcher {
    public:
     static constexpr int TH_LOW = 50, TH_HIGH = 100, HISTO_LENGTH = 30;  // ORBmatcher.h:90-92
 
+    /* ORBmatcher(float nnratio, bool checkOri) (ORBmatcher.cc:36-39): cheap to construct per call,
+     * as the reference does; the device handle is the calling thread's (MatcherDevice). */
     explicit ORBmatcher(float nnratio = 0.6f, bool checkOri = true, int device = 0)
-        : nnratio_(nnratio), check_ori_(checkOri) {
-        check(slamhot_matcher_create(device, &m_), "ORBmatcher");
-    }
-    ~ORBmatcher() { slamhot_matcher_destroy(m_); }
+        : nnratio_(nnratio), check_ori_(checkOri), m_(MatcherDevice::ForThisThread(device)) {}
     ORBmatcher(const ORBmatcher&) = delete;
     ORBmatcher& operator=(const ORBmatcher&) = delete;
+    float NNratio() const { return nnratio_; }
+    bool CheckOrientation() const { return check_ori_; }
 
     /* static int DescriptorDistance(const cv::Mat& a, const cv::Mat& b) (ORBmatcher.cc:
      * 2561-2577): bit-set count of a XOR b over 8 x 32 bits.  A host utility in the

@@ -258,7 +258,11 @@ int PoseOptimization(slamhot::PoseOptimizer& hot, Frame* pFrame) {
     slam_pose_result R{};
     R.outlier = outl.data();
     const int n = slamhot::Optimizer::PoseOptimization(hot, F, R);
-    if (R.n_initial < 3) return 0;  // Optimizer.cc:1012-1013: pose and flags untouched
+    if (R.n_initial < 3) {  // Optimizer.cc:1012-1013: pose untouched, but the edge set-up loop
+        for (int i = 0; i < N; i++)  // (:864-1005) has already cleared mvbOutlier of every MapPoint
+            if (has_mp[i]) pFrame->mvbOutlier[i] = false;
+        return 0;
+    }
     for (int i = 0; i < N; i++)
         if (has_mp[i]) pFrame->mvbOutlier[i] = outl[i] != 0;
     pFrame->SetPose(mat_from(R.Tcw, 4, 4));

@@ -6,6 +6,9 @@
 //   shim_driver lba MAP OUT       the whole LocalBundleAdjustment shim on the device -> counts,
 //                                 KeyFrame poses, MapPoint positions, surviving observations
 //   shim_driver pose FRAME OUT    the PoseOptimization shim on one Frame
+//   shim_driver bow PAIR OUT      ORB_SLAM3::ORBmatcher(nnratio, checkOri).SearchByBoW(pKF, F, ...)
+//                                 through the reference-side binding of INTEGRATION.md, once per
+//                                 (nnratio, checkOri) listed in PAIR, all on this one thread
 //
 // MAP / FRAME are little-endian binaries written by tests/shim_io.py.
 #include <cstdio>
@@ -222,7 +225,7 @@ int run_pose(const char* in, const char* out) {
     F.mvKeysUn.resize(F.N);
     F.mvuRight.resize(F.N);
     F.mvpMapPoints.assign(F.N, nullptr);
-    F.mvbOutlier.assign(F.N, false);
+    F.mvbOutlier.assign(F.N, true);  // stale flags from an earlier optimisation of this Frame
     std::vector<MapPoint> mps(F.N);
     for (int i = 0; i < F.N; i++) {
         F.mvKeysUn[i].pt.x = R.get<float>();
@@ -251,6 +254,83 @@ int run_pose(const char* in, const char* out) {
     return 0;
 }
 
+}  // namespace
+
+// The reference's ORBmatcher (ORBmatcher.h:36-110, stateful only in its two members), with the
+// SearchByBoW body exactly as INTEGRATION.md tells a maintainer to write it.
+namespace ORB_SLAM3 {
+class ORBmatcher {
+   public:
+    ORBmatcher(float nnratio = 0.6, bool checkOri = true) : mfNNratio(nnratio), mbCheckOrientation(checkOri) {}
+    int SearchByBoW(KeyFrame* pKF, Frame& F, std::vector<MapPoint*>& vpMapPointMatches);
+
+   protected:
+    float mfNNratio;
+    bool mbCheckOrientation;
+};
+
+int ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, std::vector<MapPoint*>& vpMapPointMatches) {
+    slamhot::ORBmatcher hot(mfNNratio, mbCheckOrientation);  // this thread's device handle, this call's ratio
+    return slamhot::orbslam3::SearchByBoW(hot, pKF, F, vpMapPointMatches);
+}
+}  // namespace ORB_SLAM3
+
+namespace {
+
+// one side of SearchByBoW: N, descriptors, keypoint angles, [MapPoint validity], FeatureVector CSR
+template <class Side>
+void read_bow_side(Reader& R, Side& S, bool with_valid, std::vector<MapPoint>& mps) {
+    const int n = R.get<int32_t>();
+    S.N = n;
+    S.mDescriptors.create(n, 32, CV_8U);
+    if (n) R.get(S.mDescriptors.data, (size_t)n * 32);
+    S.mvKeysUn.resize(n);
+    for (int i = 0; i < n; i++) S.mvKeysUn[i].angle = R.get<float>();
+    if (with_valid) {
+        mps.resize(n);
+        S.mvpMapPoints.assign(n, nullptr);
+        for (int i = 0; i < n; i++) {
+            mps[i].mnId = (unsigned long)i;
+            if (R.get<uint8_t>()) S.mvpMapPoints[i] = &mps[i];
+        }
+    }
+    const int nn = R.get<int32_t>();
+    std::vector<uint32_t> id(nn);
+    std::vector<int32_t> off(nn + 1);
+    R.get(id.data(), nn);
+    R.get(off.data(), nn + 1);
+    std::vector<uint32_t> feat(off[nn]);
+    R.get(feat.data(), feat.size());
+    for (int k = 0; k < nn; k++) S.mFeatVec[id[k]].assign(feat.begin() + off[k], feat.begin() + off[k + 1]);
+}
+
+int run_bow(const char* in, const char* out) {
+    Reader R(in);
+    const int ncalls = R.get<int32_t>();
+    std::vector<std::pair<float, bool>> calls;
+    for (int c = 0; c < ncalls; c++) {
+        const float r = R.get<float>();
+        calls.emplace_back(r, R.get<int32_t>() != 0);
+    }
+    KeyFrame kf;
+    Frame F;
+    std::vector<MapPoint> mps, unused;
+    read_bow_side(R, kf, true, mps);
+    read_bow_side(R, F, false, unused);
+    Writer O(out);
+    for (const auto& c : calls) {  // Tracking.cc:2566 then :3475 on the Tracking thread
+        ORB_SLAM3::ORBmatcher matcher(c.first, c.second);
+        std::vector<MapPoint*> vpMapPointMatches;
+        const int n = matcher.SearchByBoW(&kf, F, vpMapPointMatches);
+        std::vector<int32_t> idx(F.N, -1);
+        for (int i = 0; i < F.N; i++)
+            if (vpMapPointMatches[i]) idx[i] = (int32_t)vpMapPointMatches[i]->mnId;
+        O.put<int32_t>(n);
+        O.put(idx);
+    }
+    return 0;
+}
+
 // Instantiations of the shims this driver does not run (they must compile against the
 // reference-shaped types; their device paths are exercised through include/slamhot.hpp).
 [[maybe_unused]] void instantiate_all(slamhot::ORBmatcher& m, slamhot::LocalMapper& lm, slamhot::StereoMatcher& sm,
@@ -272,7 +352,7 @@ int run_pose(const char* in, const char* out) {
 
 int main(int argc, char** argv) {
     if (argc < 4) {
-        std::fprintf(stderr, "usage: shim_driver flatten|lba|pose IN OUT\n");
+        std::fprintf(stderr, "usage: shim_driver flatten|lba|pose|bow IN OUT\n");
         return 2;
     }
     const std::string mode = argv[1];
@@ -280,6 +360,7 @@ int main(int argc, char** argv) {
         if (mode == "flatten") return run_flatten(argv[2], argv[3]);
         if (mode == "lba") return run_lba(argv[2], argv[3]);
         if (mode == "pose") return run_pose(argv[2], argv[3]);
+        if (mode == "bow") return run_bow(argv[2], argv[3]);
     } catch (const slamhot::Error& e) {
         std::fprintf(stderr, "slamhot error: %s\n", e.what());
         return 3;
