@@ -18,15 +18,23 @@ tests/cpp/host_driver: tests/cpp/host_driver.cpp include/slamhot.hpp include/sla
 tests/cpp/shim_driver: tests/cpp/shim_driver.cpp tests/cpp/orbslam3_standins.hpp include/slamhot_orbslam3.hpp include/slamhot.hpp include/slamhot.h $(LIBDIR)/libslamhot.so
 	g++ -O2 -std=c++17 -Wall -Wextra -Iinclude -o $@ $< -L$(LIBDIR) -lslamhot -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)'
 
-$(LIBDIR)/libslamhot.so: $(SRCS) $(HDRS)
+OBJDIR := build/obj
+OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(SRCS))
+
+# one object per kernel file (parallel make), linked into the one library
+$(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(LIBDIR)/libslamhot.so: $(OBJS)
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJS)
 
 oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -rf $(LIBDIR) oracle/build tests/cpp/host_driver tests/cpp/shim_driver tests/cpp/*_asan
+	rm -rf $(LIBDIR) build oracle/build tests/cpp/host_driver tests/cpp/shim_driver tests/cpp/*_asan
 
 # host-side sanitizer builds (test infrastructure; GPU code is never instrumented): the oracle
 # with ASan + UBSan, and the C++ host-layer / shim drivers with ASan + UBSan (tools/sanitize.sh)

@@ -373,6 +373,13 @@ typedef struct slam_lba_problem {
     const float* kf_Trl;        /* n_kf x 16 row-major KeyFrame::mTrl (right <- left), read for KFs
                                    with body edges (Converter::toSE3Quat) */
     slam_camera cam2;           /* mpCamera2 parameters fx, fy, cx, cy (bf unused) */
+    /* A camera per KeyFrame: the reference binds every edge to its own KeyFrame's calibration
+     * (mono e->pCamera = pKFi->mpCamera, Optimizer.cc:1840; stereo e->fx..bf = pKFi->fx..mbf,
+     * :1869-1873; body e->pCamera = pKFi->mpCamera2, :1906), so one window (an Atlas map built
+     * from several cameras) and one batch may mix calibrations.  NULL = cam / cam2 for every
+     * KeyFrame of this window. */
+    const slam_camera* kf_cam;  /* n_kf: pKFi->fx, fy, cx, cy, mbf */
+    const slam_camera* kf_cam2; /* n_kf: pKFi->mpCamera2 fx, fy, cx, cy (read for KFs with body edges) */
 } slam_lba_problem;
 
 typedef struct slam_lba_options {
@@ -381,6 +388,11 @@ typedef struct slam_lba_options {
     double user_lambda_init;    /* 0 -> tau * max diag(H); 100 if pMap->IsInertial() (:1726) */
     const volatile uint8_t* stop_flag_bool; /* optional: the caller's `bool* pbStopFlag` itself (a C++
                                    bool is one byte), polled live like the int32 stop_flag */
+    /* optional diagnostic hook (NULL = none): called on the calling thread each time the host has
+     * seen the counters of an LM step, with the step's number (0-based over the whole call).  A
+     * hook that sets the stop flag stops the solve at a chosen step, independent of timing. */
+    void (*step_hook)(void* ctx, int32_t step);
+    void* step_hook_ctx;
 } slam_lba_options;
 
 typedef struct slam_lba_result {
@@ -393,6 +405,8 @@ typedef struct slam_lba_result {
     double chi2_initial;        /* activeRobustChi2 at the first iteration */
     double chi2_final;          /* activeRobustChi2 after the last accepted step */
     double lambda_final;
+    int32_t ran;                /* 0: the stop flag was already set on entry, nothing was optimized
+                                   and nothing is to be written back (Optimizer.cc:1921-1923) */
 } slam_lba_result;
 
 typedef struct slam_lba slam_lba;

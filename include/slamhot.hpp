@@ -351,6 +351,9 @@ struct LocalBAWindow {
     std::vector<uint8_t> edge_body;   // n_edge, 1 = body edge (edge_obs = right keypoint)
     std::vector<float> kf_Trl;        // n_kf x 16, KeyFrame::mTrl
     slam_camera cam2{};               // mpCamera2 parameters
+    // a camera per KeyFrame (pKFi->fx..mbf / mpCamera2, Optimizer.cc:1840, 1869-1873, 1906):
+    // empty = cam / cam2 for every KeyFrame
+    std::vector<slam_camera> kf_cam, kf_cam2;
     bool inertial = false;            // pMap->IsInertial(): lambda0 = 100 (Optimizer.cc:1726)
     int n_kf() const { return (int)kf_fixed.size(); }
     int n_pt() const { return (int)pt_pos.size() / 3; }
@@ -362,6 +365,7 @@ struct LocalBAResult {
     std::vector<uint8_t> edge_outlier;  // vToErase (Optimizer.cc:1995-2038)
     int iterations[2] = {0, 0}, trials = 0, n_outlier = 0;
     double chi2_initial = 0, chi2_final = 0;
+    bool ran = false;  // false: *pbStopFlag was set on entry, nothing to write back (Optimizer.cc:1921-1923)
 };
 
 class LocalBundleAdjuster {
@@ -396,6 +400,8 @@ class LocalBundleAdjuster {
                 p.kf_Trl = w.kf_Trl.data();
                 p.cam2 = w.cam2;
             }
+            if (!w.kf_cam.empty()) p.kf_cam = w.kf_cam.data();
+            if (!w.kf_cam2.empty()) p.kf_cam2 = w.kf_cam2.data();
             p.user_lambda_init = w.inertial ? 100.0 : 0.0;  // this window's pMap->IsInertial() (:1726)
             out[i].kf_Tcw.resize(w.kf_Tcw.size());
             out[i].pt_pos.resize(w.pt_pos.size());
@@ -422,6 +428,7 @@ class LocalBundleAdjuster {
             out[i].n_outlier = res[i].n_outlier;
             out[i].chi2_initial = res[i].chi2_initial;
             out[i].chi2_final = res[i].chi2_final;
+            out[i].ran = res[i].ran != 0;
         }
     }
 

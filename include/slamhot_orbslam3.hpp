@@ -426,15 +426,32 @@ void FlattenLocalWindow(const LocalWindow<KeyFrame, MapPoint>& W, Map* pMap, Loc
         }
         pi++;
     }
+    // every edge uses its own KeyFrame's camera: mono e->pCamera = pKFi->mpCamera (:1840), stereo
+    // e->fx..bf = pKFi->fx..mbf (:1869-1873), body e->pCamera = pKFi->mpCamera2 (:1906)
+    auto cam2_of = [](KeyFrame* k) {  // GeometricCamera::getParameter (GeometricCamera.h:70)
+        if (!k->mpCamera2) return slam_camera{};
+        auto* c2 = k->mpCamera2;
+        return slam_camera{c2->getParameter(0), c2->getParameter(1), c2->getParameter(2), c2->getParameter(3), 0.f};
+    };
     KeyFrame* k0 = kfs.front();
     out.cam = slam_camera{k0->fx, k0->fy, k0->cx, k0->cy, k0->mbf};
     for (KeyFrame* pKFi : kfs)
         if (pKFi->mpCamera2) {
-            auto* c2 = pKFi->mpCamera2;  // GeometricCamera::getParameter (GeometricCamera.h:70)
-            out.cam2 = slam_camera{c2->getParameter(0), c2->getParameter(1), c2->getParameter(2), c2->getParameter(3),
-                                   0.f};
+            out.cam2 = cam2_of(pKFi);
             break;
         }
+    bool mixed = false;
+    for (KeyFrame* pKFi : kfs) {
+        const slam_camera c{pKFi->fx, pKFi->fy, pKFi->cx, pKFi->cy, pKFi->mbf}, c2 = cam2_of(pKFi);
+        out.kf_cam.push_back(c);
+        out.kf_cam2.push_back(c2);
+        mixed = mixed || std::memcmp(&c, &out.cam, sizeof(c)) != 0 ||
+                (pKFi->mpCamera2 && std::memcmp(&c2, &out.cam2, sizeof(c2)) != 0);
+    }
+    if (!mixed) {  // one calibration: cam / cam2 stand for every KeyFrame
+        out.kf_cam.clear();
+        out.kf_cam2.clear();
+    }
     out.inertial = pMap->IsInertial();
 }
 
@@ -458,6 +475,7 @@ void LocalBundleAdjustment(LocalBundleAdjuster& hot, KeyFrame* pKF, bool* pbStop
     std::vector<LocalBAResult> res;
     hot.Solve({flat}, pbStopFlag, res);  // optimize(5), stop check, optimize(10), outlier scan
     const LocalBAResult& R = res[0];
+    if (!R.ran) return;  // the flag flipped between the check above and the solver's own: :1921-1923
     std::unique_lock<std::mutex> lock(pMap->mMutexMapUpdate);  // :2040
     for (size_t e = 0; e < edge_refs.size(); e++)           // vToErase (:2043-2052)
         if (R.edge_outlier[e] && !edge_refs[e].second->isBad()) {

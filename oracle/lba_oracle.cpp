@@ -37,10 +37,16 @@ struct Edge {
     double Hpl[18];         // pose-landmark block B^T W A, 6 x 3 row-major
 };
 
+// One KeyFrame's pinhole parameters (float, promoted): the edge's camera.
+struct KCam {
+    double fx, fy, cx, cy, bf;
+};
+
 struct Solver {
     const slam_lba_problem* P;
-    double fx, fy, cx, cy, bf;  // float parameters promoted
-    double fx2, fy2, cx2, cy2;  // mpCamera2 (pinhole) parameters
+    // per KeyFrame: its own camera (e->pCamera = pKFi->mpCamera, e->fx..bf = pKFi->fx..mbf,
+    // Optimizer.cc:1840, 1869-1873) and its mpCamera2 (body edges, :1906)
+    std::vector<KCam> kc, kc2;
     std::vector<SE3> trl;       // per KF: Converter::toSE3Quat(pKFi->mTrl)
     double delta_mono, delta_stereo;
     float dsqr_mono, dsqr_stereo;  // RobustKernelHuber::dsqr is float (robust_kernel_impl.h:84)
@@ -71,11 +77,13 @@ struct Solver {
         if (e.body) {
             // EdgeSE3ProjectXYZToBody::computeError (OptimizableTypes.h:127-132):
             // obs - pCamera->project((mTrl * T_lw).map(X_w)), the composed SE3Quat mapping
+            const KCam& K2 = kc2[e.kf];
             se3_map(se3_mul(trl[e.kf], pose[e.kf]), &pt[3 * e.pt], Xc);
-            e.err[0] = e.obs[0] - (fx2 * Xc[0] / Xc[2] + cx2);
-            e.err[1] = e.obs[1] - (fy2 * Xc[1] / Xc[2] + cy2);
+            e.err[0] = e.obs[0] - (K2.fx * Xc[0] / Xc[2] + K2.cx);
+            e.err[1] = e.obs[1] - (K2.fy * Xc[1] / Xc[2] + K2.cy);
             return;
         }
+        const double fx = kc[e.kf].fx, fy = kc[e.kf].fy, cx = kc[e.kf].cx, cy = kc[e.kf].cy, bf = kc[e.kf].bf;
         se3_map(pose[e.kf], &pt[3 * e.pt], Xc);
         if (!e.stereo) {
             const double u = fx * Xc[0] / Xc[2] + cx;
@@ -144,6 +152,7 @@ struct Solver {
             return;
         }
         const SE3& T = pose[e.kf];
+        const double fx = kc[e.kf].fx, fy = kc[e.kf].fy, bf = kc[e.kf].bf;
         double R[9], Xc[3];
         se3_map(T, &pt[3 * e.pt], Xc);
         rot_matrix(T.r, R);
@@ -205,6 +214,7 @@ struct Solver {
     void linearize_body(Edge& e) {
         const SE3& T = pose[e.kf];
         const SE3& Trl = trl[e.kf];
+        const double fx2 = kc2[e.kf].fx, fy2 = kc2[e.kf].fy;
         double Xl[3], Xr[3], Rrw[9], Rrl[9];
         se3_map(T, &pt[3 * e.pt], Xl);
         se3_map(Trl, Xl, Xr);
@@ -508,15 +518,6 @@ int oracle_lba_solve(const slam_lba_problem* P, const slam_lba_options* opt, int
     Solver S;
     S.P = P;
     S.stop = stop;
-    S.fx = P->cam.fx;
-    S.fy = P->cam.fy;
-    S.cx = P->cam.cx;
-    S.cy = P->cam.cy;
-    S.bf = P->cam.bf;
-    S.fx2 = P->cam2.fx;
-    S.fy2 = P->cam2.fy;
-    S.cx2 = P->cam2.cx;
-    S.cy2 = P->cam2.cy;
     const float thMono = std::sqrt(5.991), thStereo = std::sqrt(7.815);  // Optimizer.cc:1794-1795
     S.delta_mono = thMono;
     S.delta_stereo = thStereo;
@@ -529,7 +530,13 @@ int oracle_lba_solve(const slam_lba_problem* P, const slam_lba_options* opt, int
     std::vector<int> kf_edges(nk, 0);
     for (int i = 0; i < ne; i++) kf_edges[P->edge_kf[i]]++;
     S.trl.assign(nk, SE3{{0, 0, 0, 1}, {0, 0, 0}});
+    S.kc.resize(nk);
+    S.kc2.resize(nk);
     for (int k = 0; k < nk; k++) {
+        const slam_camera& c = P->kf_cam ? P->kf_cam[k] : P->cam;
+        const slam_camera& c2 = P->kf_cam2 ? P->kf_cam2[k] : P->cam2;
+        S.kc[k] = KCam{c.fx, c.fy, c.cx, c.cy, c.bf};
+        S.kc2[k] = KCam{c2.fx, c2.fy, c2.cx, c2.cy, 0.0};
         S.pose[k] = se3_from_cv(P->kf_Tcw + 16 * k);
         if (P->edge_body && P->kf_Trl) S.trl[k] = se3_from_cv(P->kf_Trl + 16 * k);
         if (P->kf_fixed[k] == 0 && kf_edges[k] > 0) S.hidx[k] = S.np++;
@@ -574,6 +581,7 @@ int oracle_lba_solve(const slam_lba_problem* P, const slam_lba_options* opt, int
     R->chi2_final = 0;
     R->lambda_final = 0;
     R->n_outlier = 0;
+    R->ran = stop ? 0 : 1;
     if (stop) {  // Optimizer.cc:1921-1923: return before optimizing, nothing written back
         std::memcpy(R->kf_Tcw, P->kf_Tcw, sizeof(float) * 16 * nk);
         std::memcpy(R->pt_pos, P->pt_pos, sizeof(float) * 3 * npt);

@@ -101,7 +101,28 @@ struct Cam {
     float bff;
     double fx2, fy2, cx2, cy2;  // mpCamera2 (body edges)
     const double* trl;          // per global KF: mTrl as a pose record (NULL without body edges)
+    // per global KF: its own camera as 8 floats {fx, fy, cx, cy, fx2, fy2, cx2, cy2} and its bf
+    // (Optimizer.cc:1840, 1869-1873, 1906); NULL when the whole batch shares the scalars above
+    const float4* kcam;
+    const float* kbf;
 };
+
+// the edge's camera (float parameters promoted, as the reference's edges hold them)
+struct Intr {
+    double fx, fy, cx, cy, bf;
+    float bff;
+};
+__device__ __forceinline__ Intr left_cam(const Cam& c, int kf) {
+    if (!c.kcam) return Intr{c.fx, c.fy, c.cx, c.cy, c.bf, c.bff};
+    const float4 a = c.kcam[2 * (long long)kf];
+    const float bf = c.kbf[kf];
+    return Intr{a.x, a.y, a.z, a.w, bf, bf};
+}
+__device__ __forceinline__ Intr right_cam(const Cam& c, int kf) {
+    if (!c.kcam) return Intr{c.fx2, c.fy2, c.cx2, c.cy2, 0.0, 0.f};
+    const float4 a = c.kcam[2 * (long long)kf + 1];
+    return Intr{a.x, a.y, a.z, a.w, 0.0, 0.f};
+}
 
 // (mTrl * T_lw) as a pose record: SE3Quat::operator* (se3quat.h:104-110)
 __device__ inline void body_pose(const double* Trl, const double* P, double* Q) {
@@ -129,25 +150,27 @@ __device__ inline void edge_error(const EdgeS& e, const Cam& cam, const double* 
     if (is_body(e)) {
         // EdgeSE3ProjectXYZToBody::computeError (OptimizableTypes.h:127-132)
         double Q[8];
+        const Intr K2 = right_cam(cam, e.kf);
         body_pose(cam.trl + 8 * (long long)e.kf, P, Q);
         se3_map(Q, X, Xc);
-        err[0] = (double)e.obs[0] - (cam.fx2 * Xc[0] / Xc[2] + cam.cx2);
-        err[1] = (double)e.obs[1] - (cam.fy2 * Xc[1] / Xc[2] + cam.cy2);
+        err[0] = (double)e.obs[0] - (K2.fx * Xc[0] / Xc[2] + K2.cx);
+        err[1] = (double)e.obs[1] - (K2.fy * Xc[1] / Xc[2] + K2.cy);
         err[2] = 0.0;
         return;
     }
+    const Intr K = left_cam(cam, e.kf);
     se3_map(P, X, Xc);
     if (e.obs[2] < 0.f) {
-        const double u = cam.fx * Xc[0] / Xc[2] + cam.cx;
-        const double v = cam.fy * Xc[1] / Xc[2] + cam.cy;
+        const double u = K.fx * Xc[0] / Xc[2] + K.cx;
+        const double v = K.fy * Xc[1] / Xc[2] + K.cy;
         err[0] = (double)e.obs[0] - u;
         err[1] = (double)e.obs[1] - v;
         err[2] = 0.0;
     } else {
         const float invz = (float)(1.0 / Xc[2]);
-        const double u = Xc[0] * (double)invz * cam.fx + cam.cx;
-        const double v = Xc[1] * (double)invz * cam.fy + cam.cy;
-        const double ur = u - (double)(cam.bff * invz);
+        const double u = Xc[0] * (double)invz * K.fx + K.cx;
+        const double v = Xc[1] * (double)invz * K.fy + K.cy;
+        const double ur = u - (double)(K.bff * invz);
         err[0] = (double)e.obs[0] - u;
         err[1] = (double)e.obs[1] - v;
         err[2] = (double)e.obs[2] - ur;
@@ -187,6 +210,7 @@ __device__ inline void robustify(const Huber& hk, bool stereo, double c, double&
 __device__ inline void body_jacobians(const EdgeS& e, const Cam& cam, const double* P, const double* X, double* A,
                                       double* B) {
     const double* Trl = cam.trl + 8 * (long long)e.kf;
+    const Intr K2 = right_cam(cam, e.kf);
     double Xl[3], Xr[3], Q[8], Rrw[9], Rrl[9];
     se3_map(P, X, Xl);
     se3_map(Trl, Xl, Xr);
@@ -194,8 +218,8 @@ __device__ inline void body_jacobians(const EdgeS& e, const Cam& cam, const doub
     rot_matrix(load_q(Q), Rrw);
     rot_matrix(load_q(Trl), Rrl);
     const double x = Xr[0], y = Xr[1], z = Xr[2];
-    const double pj[6] = {-(cam.fx2 / z), -0.0, -((-cam.fx2) * x / (z * z)),
-                          -0.0, -(cam.fy2 / z), -((-cam.fy2) * y / (z * z))};
+    const double pj[6] = {-(K2.fx / z), -0.0, -((-K2.fx) * x / (z * z)),
+                          -0.0, -(K2.fy / z), -((-K2.fy) * y / (z * z))};
     double M[6];
 #pragma unroll
     for (int r = 0; r < 2; r++)
@@ -216,7 +240,7 @@ __device__ inline void body_jacobians(const EdgeS& e, const Cam& cam, const doub
     for (int cc = 0; cc < 6; cc++) B[12 + cc] = 0;
 }
 
-__device__ inline void edge_jacobians(bool stereo, const Cam& cam, const double* P, const double* X, double* A,
+__device__ inline void edge_jacobians(bool stereo, const Intr& cam, const double* P, const double* X, double* A,
                                       double* B) {
     double R[9], Xc[3];
     se3_map(P, X, Xc);
@@ -305,7 +329,7 @@ __device__ __forceinline__ void lin_points_body(int p, int npt_total, const int*
         if (is_body(e))
             body_jacobians(e, cam, P, X, A, B);
         else
-            edge_jacobians(stereo, cam, P, X, A, B);
+            edge_jacobians(stereo, left_cam(cam, e.kf), P, X, A, B);
         const double info = e.info;
         const double w = rho1 * info;
         double om_r[3];
@@ -402,7 +426,7 @@ __device__ __forceinline__ void lin_poses_body(int pose, int lane, int npose_tot
         if (is_body(e))
             body_jacobians(e, cam, P, X, A, B);
         else
-            edge_jacobians(stereo, cam, P, X, A, B);
+            edge_jacobians(stereo, left_cam(cam, e.kf), P, X, A, B);
         const double info = e.info;
         const double w = rho1 * info;
         double om_r[3];
@@ -510,7 +534,7 @@ __global__ void __launch_bounds__(kCtlThreads) k_iter_begin(const WinDesc* __res
                                                             const double* __restrict__ rho,
                                                             const double* __restrict__ Hpp,
                                                             const double* __restrict__ Hll,
-                                                            const volatile int* __restrict__ stop_dev) {
+                                                            const volatile int* __restrict__ stop_dev, int seq) {
     __shared__ double sh[kCtlThreads / 64];
     const WinDesc W = wins[blockIdx.x];
     WinCtl& C = ctl[blockIdx.x];
@@ -527,8 +551,9 @@ __global__ void __launch_bounds__(kCtlThreads) k_iter_begin(const WinDesc* __res
     if (threadIdx.x == 0) {
         C.need_lin = 0;
         // SparseOptimizer::optimize: no iteration once terminate() (sparse_optimizer.cpp:376);
-        // stop_dev is the device copy k_trial_control refreshes from the host word every step
-        if (*stop_dev) {
+        // stop_dev[seq & 1]: this step's sample of the host word (k_trial_control of the previous
+        // step wrote it; the same value this step's k_trial_control decides on)
+        if (stop_dev[seq & 1]) {
             C.active = 0;
             return;
         }
@@ -1613,14 +1638,16 @@ __global__ void __launch_bounds__(kCtlThreads) k_trial_control(const WinDesc* __
     const WinDesc W = wins[blockIdx.x];
     WinCtl& C = ctl[blockIdx.x];
     // terminate(): block 0 samples the pinned host word (one PCIe read per step, issued early so
-    // it overlaps the reductions) into tally[3]; the decisions read tally[3], i.e. the flag as
-    // sampled during the previous step -- a stop the host saw a step later, which is all the
-    // reference guarantees between threads anyway
+    // it overlaps the reductions) into the sample slot of the NEXT step, tally[4 + ((seq + 1) & 1)];
+    // every block of this step decides on tally[4 + (seq & 1)], written during the previous step
+    // and not touched during this one, so all windows of a step see one value -- a stop the host
+    // saw a step later, which is all the reference guarantees between threads anyway
     int stop_fresh = 0;
     if (blockIdx.x == 0 && threadIdx.x == 0) stop_fresh = *stop_host;
+    int* const stop_next = &tally[4 + ((seq + 1) & 1)];
     if (!C.need_trial) {  // idle window: active == 0 here (k_iter_begin put every active one in a trial)
         if (threadIdx.x == 0) {
-            if (blockIdx.x == 0) atomicExch(&tally[3], stop_fresh);
+            if (blockIdx.x == 0) atomicExch(stop_next, stop_fresh);
             tally_publish(tally, 0, 0, gridDim.x, host_slot, seq);
         }
         return;
@@ -1639,8 +1666,8 @@ __global__ void __launch_bounds__(kCtlThreads) k_trial_control(const WinDesc* __
     }
     double scale = block_sum(sc, sh);
     if (threadIdx.x != 0) return;
-    const int stop = ((volatile int*)tally)[3];  // terminate() at the end of the trial
-    if (blockIdx.x == 0) atomicExch(&tally[3], stop_fresh);
+    const int stop = ((volatile int*)tally)[4 + (seq & 1)];  // terminate() at the end of the trial
+    if (blockIdx.x == 0) atomicExch(stop_next, stop_fresh);
     if (!C.ok2) tmpChi = __DBL_MAX__;
     double rho_ = C.cur_chi - tmpChi;
     scale += 1e-3;
@@ -1821,6 +1848,8 @@ struct Plan {
     int2* blk_pose;
     float *kf_in, *pt_in;
     double* kf_trl;  // per KF: mTrl as a pose record (body edges)
+    float4* kcam;    // per KF: {fx, fy, cx, cy}, {fx2, fy2, cx2, cy2} (batches of mixed calibrations)
+    float* kbf;      // per KF: mbf
 };
 
 constexpr int kRing = 4;  // LM steps whose counters are in flight (host-side ring)
@@ -1860,11 +1889,13 @@ struct PlanSizes {
     long long nbm = 0, nct = 0, hs_total = 0;
     int max_n = 0;
     bool any_body = false;
+    bool per_kf_cam = false;           // the KeyFrames of the batch do not share one calibration
+    slam_camera cam{}, cam2{};         // the shared calibration otherwise
 };
 
 struct Layout {
     size_t edges, wins, ctl, pt_off, pt_win, spe_off, spe, pe_off, pe, pose_win, kf_hp, kf_win, blk_win,
-        blk_order, blk_pose, kf_in, pt_in, kf_trl, total;
+        blk_order, blk_pose, kf_in, pt_in, kf_trl, kcam, kbf, total;
 };
 
 Layout make_layout(const PlanSizes& z) {
@@ -1893,6 +1924,8 @@ Layout make_layout(const PlanSizes& z) {
     L.kf_in = take(sizeof(float) * 16 * z.nkf);
     L.pt_in = take(sizeof(float) * 3 * z.npt);
     L.kf_trl = take(z.any_body ? sizeof(double) * 8 * z.nkf : 0);
+    L.kcam = take(z.per_kf_cam ? sizeof(float4) * 2 * z.nkf : 0);
+    L.kbf = take(z.per_kf_cam ? sizeof(float) * z.nkf : 0);
     L.total = off;
     return L;
 }
@@ -1917,6 +1950,8 @@ Plan bind(unsigned char* base, const Layout& L) {
     P.kf_in = (float*)(base + L.kf_in);
     P.pt_in = (float*)(base + L.pt_in);
     P.kf_trl = (double*)(base + L.kf_trl);
+    P.kcam = (float4*)(base + L.kcam);
+    P.kbf = (float*)(base + L.kbf);
     return P;
 }
 
@@ -1979,6 +2014,23 @@ slam_status plan_sizes(int n_prob, const slam_lba_problem* probs, PlanSizes& z, 
         z.hs_total += (long long)(ldlt_npad(6 * np) + 1) * ldlt_ld(6 * np);
         z.max_n = std::max(z.max_n, 6 * np);
     }
+    // one calibration for the whole batch (the usual case: the scalars go in the kernel
+    // arguments), else a camera record per KeyFrame (Optimizer.cc:1840, 1869-1873, 1906)
+    bool have = false, have2 = false;
+    for (int w = 0; w < n_prob && !z.per_kf_cam; w++) {
+        const slam_lba_problem& P = probs[w];
+        bool body = false;
+        for (int i = 0; P.edge_body && i < P.n_edge && !body; i++) body = P.edge_body[i] != 0;
+        for (int k = 0; k < P.n_kf && !z.per_kf_cam; k++) {
+            const slam_camera& c = P.kf_cam ? P.kf_cam[k] : P.cam;
+            if (!have) z.cam = c, have = true;
+            else if (std::memcmp(&c, &z.cam, sizeof(slam_camera)) != 0) z.per_kf_cam = true;
+            if (!body) continue;
+            const slam_camera& c2 = P.kf_cam2 ? P.kf_cam2[k] : P.cam2;  // bf unused
+            if (!have2) z.cam2 = c2, have2 = true;
+            else if (std::memcmp(&c2, &z.cam2, 4 * sizeof(float)) != 0) z.per_kf_cam = true;
+        }
+    }
     return SLAM_OK;
 }
 
@@ -2024,6 +2076,14 @@ slam_status plan_fill(int n_prob, const slam_lba_problem* probs, const std::vect
             P.kf_win[nkf + k] = w;
         }
         std::memcpy(P.kf_in + 16 * (size_t)nkf, Q.kf_Tcw, sizeof(float) * 16 * Q.n_kf);
+        if (Z.per_kf_cam)
+            for (int k = 0; k < Q.n_kf; k++) {
+                const slam_camera& c = Q.kf_cam ? Q.kf_cam[k] : Q.cam;
+                const slam_camera& c2 = Q.kf_cam2 ? Q.kf_cam2[k] : Q.cam2;
+                P.kcam[2 * (size_t)(nkf + k)] = float4{c.fx, c.fy, c.cx, c.cy};
+                P.kcam[2 * (size_t)(nkf + k) + 1] = float4{c2.fx, c2.fy, c2.cx, c2.cy};
+                P.kbf[nkf + k] = c.bf;
+            }
         if (Z.any_body) {  // Converter::toSE3Quat(pKFi->mTrl) -> SE3Quat(R, t) (se3quat.h:56-58)
             for (int k = 0; k < Q.n_kf; k++) {
                 double* rec = P.kf_trl + 8 * (size_t)(nkf + k);
@@ -2218,6 +2278,7 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
         R.trials = 0;
         R.n_outlier = 0;
         R.chi2_initial = R.chi2_final = R.lambda_final = 0;
+        R.ran = stop0 ? 0 : 1;
     }
     if (stop0) {  // Optimizer.cc:1921-1923: nothing optimized, nothing written back
         for (int w = 0; w < n_prob; w++) {
@@ -2260,7 +2321,7 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
         int nkf, npt, ne, npose, nblk;
     } H{Z.nkf, Z.npt, Z.ne, Z.npose, Z.nblk};
     const long long pose_stride = 8LL * std::max(H.nkf, 1), pt_stride = 4LL * std::max(H.npt, 1);
-    SLAM_HIP_TRY(s->cnt.ensure(sizeof(int) * 4));  // k_trial_control's tally (need, active, ticket)
+    SLAM_HIP_TRY(s->cnt.ensure(sizeof(int) * 8));  // k_trial_control's tally (need, active, ticket, -, stop x 2)
     const size_t ne = std::max(H.ne, 1), npt = std::max(H.npt, 1), nps = std::max(H.npose, 1);
     SLAM_HIP_TRY(s->poses.ensure(sizeof(double) * 2 * pose_stride));
     SLAM_HIP_TRY(s->pts.ensure(sizeof(double) * 2 * pt_stride));
@@ -2297,34 +2358,20 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     SLAM_HIP_TRY(hipMemsetAsync(s->err.p, 0, sizeof(double) * 4 * ne, S));
     s->last_plan_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_plan0).count();
 
-    Cam cam;
-    const slam_camera& c0 = probs[0].cam;
-    for (int w = 1; w < nw; w++) {
-        const slam_camera& c = probs[w].cam;
-        if (c.fx != c0.fx || c.fy != c0.fy || c.cx != c0.cx || c.cy != c0.cy || c.bf != c0.bf)
-            return SLAM_EINVAL;  // one camera per batch
-    }
-    cam.fx = c0.fx;
-    cam.fy = c0.fy;
-    cam.cx = c0.cx;
-    cam.cy = c0.cy;
-    cam.bf = c0.bf;
-    cam.bff = c0.bf;
+    Cam cam;  // the batch's one calibration, or per-KeyFrame records (PlanSizes::per_kf_cam)
+    cam.fx = Z.cam.fx;
+    cam.fy = Z.cam.fy;
+    cam.cx = Z.cam.cx;
+    cam.cy = Z.cam.cy;
+    cam.bf = Z.cam.bf;
+    cam.bff = Z.cam.bf;
     cam.trl = Z.any_body ? DP.kf_trl : nullptr;
-    cam.fx2 = cam.fy2 = cam.cx2 = cam.cy2 = 0.0;
-    if (Z.any_body) {  // one second camera per batch, among the windows that have body edges
-        const slam_camera* c2 = nullptr;
-        for (int w = 0; w < nw; w++) {
-            if (!probs[w].edge_body || !probs[w].kf_Trl) continue;
-            const slam_camera& c = probs[w].cam2;
-            if (c2 && (c.fx != c2->fx || c.fy != c2->fy || c.cx != c2->cx || c.cy != c2->cy)) return SLAM_EINVAL;
-            c2 = &c;
-        }
-        cam.fx2 = c2->fx;
-        cam.fy2 = c2->fy;
-        cam.cx2 = c2->cx;
-        cam.cy2 = c2->cy;
-    }
+    cam.fx2 = Z.cam2.fx;
+    cam.fy2 = Z.cam2.fy;
+    cam.cx2 = Z.cam2.cx;
+    cam.cy2 = Z.cam2.cy;
+    cam.kcam = Z.per_kf_cam ? DP.kcam : nullptr;
+    cam.kbf = Z.per_kf_cam ? DP.kbf : nullptr;
     Huber hk;
     const float thMono = std::sqrt(5.991), thStereo = std::sqrt(7.815);  // Optimizer.cc:1794-1795
     hk.delta_mono = thMono;
@@ -2336,7 +2383,7 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     WinDesc* dW = DP.wins;
     WinCtl* dC = DP.ctl;
     int* dTally = as<int>(s->cnt);
-    SLAM_HIP_TRY(hipMemsetAsync(dTally, 0, sizeof(int) * 4, S));
+    SLAM_HIP_TRY(hipMemsetAsync(dTally, 0, sizeof(int) * 8, S));
     double* poses = as<double>(s->poses);
     double* pts = as<double>(s->pts);
     const int T = 256;
@@ -2371,9 +2418,9 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     // the per-step counters asynchronously (a ring of kRing steps in flight).  While it waits it
     // mirrors the caller's stop flag into pinned memory the control kernels read.
     *s->h_stop = user_stop() ? 1 : 0;
-    SLAM_HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(dTally + 3), *s->h_stop, 1, S));  // the device's copy
+    SLAM_HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(dTally + 4), *s->h_stop, 2, S));  // the device's samples
     bool stopped = false;
-    int syncs = 0;
+    int syncs = 0, step_no = 0;
     const int iters_of[2] = {opt->iters_first, opt->iters_second};
     // Wait for a step's counters: the last k_trial_control block stores the step's sequence
     // number into the mapped slot after the counts.  The host spins on that word (mirroring the
@@ -2407,7 +2454,7 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
                                                        as<double>(s->lin), as<double>(s->Hll), as<double>(s->bl),
                                                        as<double>(s->Hpp), as<double>(s->bp));
         k_iter_begin<<<nw, kCtlThreads, 0, S>>>(dW, dC, as<double>(s->rho), as<double>(s->Hpp),
-                                                as<double>(s->Hll), dTally + 3);
+                                                as<double>(s->Hll), dTally + 4, seq);
         if (H.npt)
             k_point_prep<<<blocks(H.npt, T), T, 0, S>>>(H.npt, DP.pt_win, dC, as<double>(s->Hll), as<double>(s->bl),
                                                          as<double>(s->pd));
@@ -2451,6 +2498,11 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
             SLAM_HIP_TRY(wait_step(slot, seqs[slot]));
             syncs++;
             checked++;
+            if (opt->step_hook) {  // diagnostic hook (slam_lba_options): may set the caller's flag
+                opt->step_hook(opt->step_hook_ctx, step_no);
+                if (!*s->h_stop && user_stop()) *s->h_stop = 1;
+            }
+            step_no++;
             const Counters c = s->h_cnt[slot];
             done = c.active == 0 && c.need_trial == 0;
         }

@@ -524,18 +524,19 @@ class LbaProblem(C.Structure):
                 ("pt_pos", C.c_void_p), ("n_edge", C.c_int32), ("edge_pt", C.c_void_p), ("edge_kf", C.c_void_p),
                 ("edge_obs", C.c_void_p), ("edge_inv_sigma2", C.c_void_p), ("cam", Camera),
                 ("user_lambda_init", C.c_double), ("edge_body", C.c_void_p), ("kf_Trl", C.c_void_p),
-                ("cam2", Camera)]
+                ("cam2", Camera), ("kf_cam", C.c_void_p), ("kf_cam2", C.c_void_p)]
 
 
 class LbaOptions(C.Structure):
     _fields_ = [("iters_first", C.c_int32), ("iters_second", C.c_int32), ("user_lambda_init", C.c_double),
-                ("stop_flag_bool", C.c_void_p)]
+                ("stop_flag_bool", C.c_void_p), ("step_hook", C.c_void_p), ("step_hook_ctx", C.c_void_p)]
 
 
 class LbaResult(C.Structure):
     _fields_ = [("kf_Tcw", C.c_void_p), ("pt_pos", C.c_void_p), ("edge_outlier", C.c_void_p),
                 ("iterations", C.c_int32 * 2), ("trials", C.c_int32), ("n_outlier", C.c_int32),
-                ("chi2_initial", C.c_double), ("chi2_final", C.c_double), ("lambda_final", C.c_double)]
+                ("chi2_initial", C.c_double), ("chi2_final", C.c_double), ("lambda_final", C.c_double),
+                ("ran", C.c_int32)]
 
 
 _LBA_KEYS = {"kf_Tcw": np.float32, "kf_fixed": np.uint8, "pt_pos": np.float32, "edge_pt": np.int32,
@@ -557,6 +558,13 @@ def make_lba_problem(w: dict):
         p.edge_body = arrs["edge_body"].ctypes.data
         p.kf_Trl = arrs["kf_Trl"].ctypes.data
         p.cam2 = Camera(*w["cam2"])
+    for key in ("kf_cam", "kf_cam2"):  # a camera per KeyFrame (n_kf x 5: fx, fy, cx, cy, bf)
+        if w.get(key) is not None:
+            c = np.zeros((n_kf, 5), np.float32)
+            v = np.asarray(w[key], np.float32).reshape(n_kf, -1)
+            c[:, :v.shape[1]] = v
+            arrs[key] = c
+            setattr(p, key, c.ctypes.data)
     p._keep = arrs
     out = dict(kf_Tcw=np.zeros((n_kf, 16), np.float32), pt_pos=np.zeros((n_pt, 3), np.float32),
                edge_outlier=np.zeros(n_e, np.uint8))
@@ -568,7 +576,7 @@ def make_lba_problem(w: dict):
 def lba_result_dict(r: LbaResult, out: dict) -> dict:
     d = dict(out)
     d.update(iterations=tuple(r.iterations), trials=r.trials, n_outlier=r.n_outlier,
-             chi2_initial=r.chi2_initial, chi2_final=r.chi2_final, lambda_final=r.lambda_final)
+             chi2_initial=r.chi2_initial, chi2_final=r.chi2_final, lambda_final=r.lambda_final, ran=r.ran)
     return d
 
 
@@ -624,7 +632,9 @@ class LocalBundleAdjustment:
     def prepare(self, windows, iters_first=5, iters_second=10, user_lambda_init=0.0, stop_flag=None):
         """Flatten windows into C structs once (what a C++ caller already holds); returns a
         callable that runs slamhot_lba_solve on them and returns the LM iteration total
-        (``run.results()`` gives the result dicts).  ``stop_flag``: a live ``ctypes.c_bool``."""
+        (``run.results()`` gives the result dicts).  ``stop_flag``: a live ``ctypes.c_bool``;
+        ``run(stop_at_step=k)`` sets it from the solver's step hook once step k's counters are
+        in (slam_lba_options.step_hook), a deterministic stand-in for another thread's abort."""
         ws = list(windows)
         probs = (LbaProblem * len(ws))()
         ress = (LbaResult * len(ws))()
@@ -640,11 +650,23 @@ class LocalBundleAdjustment:
         h = self._h
         fn = lib().slamhot_lba_solve
 
-        def run():
+        state = dict(stop_at=-1, steps=0)
+
+        def hook(_ctx, step):
+            state["steps"] = step + 1
+            if step == state["stop_at"]:
+                stop_flag.value = True
+
+        hook_c = _STEP_HOOK(hook)
+
+        def run(stop_at_step=None):
+            state["stop_at"] = -1 if stop_at_step is None else int(stop_at_step)
+            opt.step_hook = C.cast(hook_c, C.c_void_p) if stop_at_step is not None or stop_flag is not None else None
             check(fn(h, len(ws), probs, C.byref(opt), None, ress), "lba_solve")
             return sum(ress[i].iterations[0] + ress[i].iterations[1] for i in range(len(ws)))
 
-        run.keep = (probs, ress, keep, opt, stop_flag)
+        run.keep = (probs, ress, keep, opt, stop_flag, hook_c)
+        run.steps = lambda: state["steps"]  # LM steps the host saw in the last call
         run.results = lambda: [lba_result_dict(ress[i], keep[i][2]) for i in range(len(ws))]
         return run
 
@@ -653,6 +675,9 @@ class LocalBundleAdjustment:
         ms, plan, syncs = C.c_double(0), C.c_double(0), I(0)
         check(lib().slamhot_lba_last_stats(self._h, C.byref(ms), C.byref(plan), C.byref(syncs)), "lba_last_stats")
         return ms.value, plan.value, syncs.value
+
+
+_STEP_HOOK = C.CFUNCTYPE(None, C.c_void_p, C.c_int32)
 
 
 def _bind_lba(L):

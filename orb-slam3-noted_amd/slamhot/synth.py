@@ -152,7 +152,7 @@ def _level_tables(nfeatures=1000, scale_factor=1.2, nlevels=8):
 
 def lba_window(seed: int, n_kf: int = 50, n_pt: int = 2000, obs_per_pt: int = 8,
                stereo_frac: float = 0.0, outlier_frac: float = 0.02, arc_deg: float = 80.0,
-               radius: float = 3.0, noise: float = 1.0, body_frac: float = 0.0):
+               radius: float = 3.0, noise: float = 1.0, body_frac: float = 0.0, mixed_cams: bool = False):
     """A seeded local-BA window in the layout of slam_lba_problem.
 
     50 KeyFrames on a ``radius`` arc facing a 4 x 2 x 4 m box of points; every point is seen
@@ -164,9 +164,20 @@ def lba_window(seed: int, n_kf: int = 50, n_pt: int = 2000, obs_per_pt: int = 8,
     are free.  Edges are point-major, KFs in id order.
     ``body_frac`` > 0 gives every KeyFrame a second (pinhole) camera: that fraction of the left
     observations is followed by a right-camera observation, an EdgeSE3ProjectXYZToBody
-    (Optimizer.cc:1883-1914), with the rig's mTrl and the second camera's intrinsics."""
+    (Optimizer.cc:1883-1914), with the rig's mTrl and the second camera's intrinsics.
+    ``mixed_cams``: odd KeyFrames carry a second calibration (an Atlas map merged from two
+    cameras): the window then has ``kf_cam`` (and ``kf_cam2``), one camera per KeyFrame, as the
+    reference binds every edge to its own KeyFrame's camera (Optimizer.cc:1840, 1869-1873, 1906).
+    ``mixed_cams="all"``: every KeyFrame uses the second calibration (window-level ``cam``)."""
     rng = np.random.default_rng(seed)
     cam = EUROC_CAM
+    cam_b = dict(fx=458.654, fy=457.296, cx=367.215 - 7.5, cy=248.375 + 3.25, bf=52.103, w=752, h=480)
+    alt_all = mixed_cams == "all"
+    kcam = [cam_b if (alt_all or (mixed_cams and k % 2)) else cam for k in range(n_kf)]
+    kfx = np.array([c["fx"] for c in kcam], np.float64)
+    kfy = np.array([c["fy"] for c in kcam], np.float64)
+    kcx = np.array([c["cx"] for c in kcam], np.float64)
+    kcy = np.array([c["cy"] for c in kcam], np.float64)
     scale, inv_sigma2, nf = _level_tables()
     p_level = nf / nf.sum()
     # ground-truth poses Tcw
@@ -191,8 +202,8 @@ def lba_window(seed: int, n_kf: int = 50, n_pt: int = 2000, obs_per_pt: int = 8,
         Xc = np.einsum("kij,j->ki", Rs, X) + ts
         z = Xc[:, 2]
         with np.errstate(divide="ignore", invalid="ignore"):
-            u = cam["fx"] * Xc[:, 0] / z + cam["cx"]
-            v = cam["fy"] * Xc[:, 1] / z + cam["cy"]
+            u = kfx * Xc[:, 0] / z + kcx
+            v = kfy * Xc[:, 1] / z + kcy
         ok = (z > 0.3) & (u >= 0) & (u < cam["w"]) & (v >= 0) & (v < cam["h"])
         cand = np.flatnonzero(ok)
         if len(cand) < obs_per_pt:
@@ -202,19 +213,22 @@ def lba_window(seed: int, n_kf: int = 50, n_pt: int = 2000, obs_per_pt: int = 8,
         i += 1
     edge_pt, edge_kf, obs, isig, body = [], [], [], [], []
     cam2 = dict(fx=431.9, fy=432.4, cx=371.3, cy=249.8)
+    cam2_b = dict(fx=455.1, fy=454.7, cx=362.9, cy=251.4)
+    kcam2 = [cam2_b if (alt_all or (mixed_cams and k % 2)) else cam2 for k in range(n_kf)]
     R_rl = _axis_angle(np.array([0.2, 1.0, 0.1]), np.deg2rad(0.6))
     t_rl = np.array([-0.110, 0.0012, 0.0021])
     for p in range(n_pt):
         for k in obs_kf[p]:
             Xc = Rs[k] @ pts[p] + ts[k]
+            ck = kcam[k]
             lvl = rng.choice(len(p_level), p=p_level)
             s = float(scale[lvl])
-            u = cam["fx"] * Xc[0] / Xc[2] + cam["cx"] + noise * rng.normal(0, s)
-            v = cam["fy"] * Xc[1] / Xc[2] + cam["cy"] + noise * rng.normal(0, s)
+            u = ck["fx"] * Xc[0] / Xc[2] + ck["cx"] + noise * rng.normal(0, s)
+            v = ck["fy"] * Xc[1] / Xc[2] + ck["cy"] + noise * rng.normal(0, s)
             ur = -1.0
             stereo = rng.random() < stereo_frac
             if stereo:
-                ur = u - cam["bf"] / Xc[2] + noise * rng.normal(0, s)
+                ur = u - ck["bf"] / Xc[2] + noise * rng.normal(0, s)
             if rng.random() < outlier_frac:
                 u = rng.uniform(0, cam["w"])
                 v = rng.uniform(0, cam["h"])
@@ -232,8 +246,9 @@ def lba_window(seed: int, n_kf: int = 50, n_pt: int = 2000, obs_per_pt: int = 8,
                 if Xr[2] > 0.3:
                     lv2 = rng.choice(len(p_level), p=p_level)
                     s2 = float(scale[lv2])
-                    u2 = cam2["fx"] * Xr[0] / Xr[2] + cam2["cx"] + noise * rng.normal(0, s2)
-                    v2 = cam2["fy"] * Xr[1] / Xr[2] + cam2["cy"] + noise * rng.normal(0, s2)
+                    c2 = kcam2[k]
+                    u2 = c2["fx"] * Xr[0] / Xr[2] + c2["cx"] + noise * rng.normal(0, s2)
+                    v2 = c2["fy"] * Xr[1] / Xr[2] + c2["cy"] + noise * rng.normal(0, s2)
                     if rng.random() < outlier_frac:
                         u2, v2 = rng.uniform(0, cam["w"]), rng.uniform(0, cam["h"])
                     edge_pt.append(p)
@@ -271,6 +286,14 @@ def lba_window(seed: int, n_kf: int = 50, n_pt: int = 2000, obs_per_pt: int = 8,
         extra = dict(edge_body=np.array(body, np.uint8),
                      kf_Trl=np.tile(Trl.reshape(1, 16), (n_kf, 1)).astype(np.float32),
                      cam2=tuple(np.float32(cam2[k]) for k in ("fx", "fy", "cx", "cy")) + (np.float32(0),))
+    if alt_all:
+        cam = cam_b
+        if body_frac > 0:
+            extra["cam2"] = tuple(np.float32(cam2_b[k]) for k in ("fx", "fy", "cx", "cy")) + (np.float32(0),)
+    elif mixed_cams:
+        extra["kf_cam"] = np.array([[c[k] for k in ("fx", "fy", "cx", "cy", "bf")] for c in kcam], np.float32)
+        if body_frac > 0:
+            extra["kf_cam2"] = np.array([[c[k] for k in ("fx", "fy", "cx", "cy")] + [0.0] for c in kcam2], np.float32)
     return dict(
         **extra,
         kf_Tcw=T0, kf_fixed=fixed, pt_pos=P0,

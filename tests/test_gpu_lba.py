@@ -101,8 +101,9 @@ def test_lba_stop_flag_before_start(solver):
     g = solver.solve(W, stop_flag=1)
     assert np.array_equal(g["kf_Tcw"], W["kf_Tcw"])
     assert np.array_equal(g["pt_pos"], W["pt_pos"])
-    assert g["n_outlier"] == 0 and g["iterations"] == (0, 0)
+    assert g["n_outlier"] == 0 and g["iterations"] == (0, 0) and g["ran"] == 0
     _check(g, ob.lba_solve(W, stop=1))
+    assert solver.solve(W)["ran"] == 1
 
 
 def test_lba_degenerate_windows(solver):
@@ -157,40 +158,63 @@ def test_lba_per_window_lambda(solver):
 
 
 def test_lba_stop_flag_mid_solve(solver):
-    """mbAbortBA set by another thread while the device LM loop runs: the solve stops early (g2o
-    checks terminate() per iteration and per trial), every window's trajectory is a prefix of the
-    unstopped one, and outputs stay finite.  The flag is the caller's live bool; it is set at a
-    sweep of delays across the call so that at least one lands inside the LM loop."""
+    """mbAbortBA set while the device LM loop runs: the solve stops early (g2o checks terminate()
+    per iteration and per trial), every window's trajectory is a prefix of the unstopped one,
+    outputs stay finite, and a stop inside optimize(5) skips optimize(10) (Optimizer.cc:
+    1933-1935).  Deterministic: the caller's live bool is set by the solver's step hook
+    (slam_lba_options.step_hook) once LM step k's counters are in, a fixed point of the loop
+    instead of a wall-clock time; the solver then reads it like any other thread's write."""
     import ctypes as C
-    import threading
-    import time
-    Ws = [synth.lba_window(200 + i, n_kf=30, n_pt=1200, obs_per_pt=6) for i in range(96)]
+    Ws = [synth.lba_window(200 + i, n_kf=20, n_pt=500, obs_per_pt=6, stereo_frac=0.2 * (i % 2)) for i in range(8)]
     flag = C.c_bool(False)
     run = solver.prepare(Ws, stop_flag=flag)
     n_full = run()
     full = run.results()
-    t0 = time.perf_counter()
-    run()
-    t_call = time.perf_counter() - t0
-    dev_ms, plan_ms, _ = solver.last_stats()
-    partial = []
-    for frac in np.linspace(0.3, 0.98, 12):
+    steps = run.steps()
+    assert steps >= 14 and not flag.value, steps
+    for k in (0, 2, steps // 2, steps - 9):
         flag.value = False
-        timer = threading.Timer(frac * t_call, lambda: setattr(flag, "value", True))
-        timer.start()
-        n_part = run()
-        timer.join()
+        n_part = run(stop_at_step=k)
         part = run.results()
-        assert n_part <= n_full
+        assert flag.value and 0 < n_part < n_full, (k, n_part, n_full, steps)
+        assert run.steps() <= k + 6, (k, run.steps())  # at most the ring of queued steps after the stop
         for f, p in zip(full, part):
+            assert p["ran"] == 1
             assert p["iterations"][0] <= f["iterations"][0] and p["iterations"][1] <= f["iterations"][1]
             assert np.isfinite(p["kf_Tcw"]).all() and np.isfinite(p["pt_pos"]).all()
+            if k <= 2:
+                assert p["iterations"][1] == 0  # stopped inside optimize(5): optimize(10) skipped
             if p["iterations"] == f["iterations"] and p["trials"] == f["trials"]:
                 assert np.array_equal(p["kf_Tcw"], f["kf_Tcw"]) and np.array_equal(p["pt_pos"], f["pt_pos"])
-        partial.append(n_part)
     flag.value = False
     assert run() == n_full  # the flag is re-read per call
-    assert any(0 < n < n_full for n in partial), (partial, n_full, t_call, dev_ms, plan_ms)
+    assert all(np.array_equal(a["kf_Tcw"], b["kf_Tcw"]) for a, b in zip(run.results(), full))
+
+
+@pytest.mark.parametrize("kw", [dict(stereo_frac=0.3), dict(body_frac=0.4, stereo_frac=0.2), dict()])
+def test_lba_camera_per_keyframe(solver, kw):
+    """Every edge uses its own KeyFrame's camera (Optimizer.cc:1840, 1869-1873, 1906): a window
+    whose odd KeyFrames carry a second calibration (kf_cam / kf_cam2) vs the oracle."""
+    W = synth.lba_window(70, n_kf=24, n_pt=800, obs_per_pt=6, mixed_cams=True, **kw)
+    assert len(np.unique(W["kf_cam"][:, 0])) == 2
+    g = solver.solve(W)
+    _check(g, ob.lba_solve(W))
+    assert g["chi2_final"] < g["chi2_initial"]
+    # the per-KeyFrame cameras matter: one camera for all would have been a different problem
+    wrong = ob.lba_solve({k: v for k, v in W.items() if k not in ("kf_cam", "kf_cam2")})
+    assert wrong["n_outlier"] > g["n_outlier"]
+
+
+def test_lba_batch_of_different_calibrations(solver):
+    """One batch holding windows of two different calibrations and a mixed one (configs[4]
+    sequences of different cameras batched together; round 2 rejected such batches)."""
+    Ws = [synth.lba_window(71, n_kf=14, n_pt=300, obs_per_pt=5),
+          synth.lba_window(72, n_kf=14, n_pt=300, obs_per_pt=5, mixed_cams="all", stereo_frac=0.3),
+          synth.lba_window(73, n_kf=16, n_pt=400, obs_per_pt=5, mixed_cams=True, body_frac=0.4),
+          synth.lba_window(74, n_kf=12, n_pt=250, obs_per_pt=5, mixed_cams="all", body_frac=0.3)]
+    assert Ws[1]["cam"][0] != Ws[0]["cam"][0]
+    for W, g in zip(Ws, solver.solve(Ws)):
+        _check(g, ob.lba_solve(W))
 
 
 def test_lba_large_window_and_mixed_batch(solver):
