@@ -371,9 +371,17 @@ def headline_leg(ctx):
     ur_h = s0.ur.cpu().numpy()
     skipped = s0.m.bow_match_batch_status(s0.stream.cuda_stream)
     kps_per_frame = float(nl_h.mean())
-    dig = sdist.digest(s0.out[0][1][:, :64].cpu().numpy(), s0.a2b[:, :64].cpu().numpy())
+    # parity digest over this rank's UNIQUE frames (the batch repeats them P / nu times): per
+    # frame a hash of its keypoints, descriptors, stereo uR and both match directions, mixed with
+    # the frame's global index (rank * nu + i), summed (slamhot.dist.unit_hash / combine)
+    kk, dd = s0.out[0][0].cpu().numpy(), s0.out[0][1].cpu().numpy()
+    a2b_h, b2a_h = s0.a2b.cpu().numpy(), s0.b2a.cpu().numpy()
+    nuniq = min(nu, P)
+    dig = sdist.combine(sdist.unit_hash(ctx["rank"] * nu + i, kk[i, :nl_h[i]], dd[i, :nl_h[i]], ur_h[i, :nl_h[i]],
+                                        a2b_h[i, :nl_h[kf_of(i)]], b2a_h[i, :nl_h[i]], nm_h[i:i + 1])
+                        for i in range(nuniq))
     el, frames_all = sdist.reduce_run(dist, device, elapsed, float(P * args.steps))
-    digs = sdist.gather_digests(dist, device, ctx["world"], int(nm_h.sum()), dig)
+    digs = sdist.gather_digests(dist, device, ctx["world"], int(nm_h[:nuniq].sum()), dig)
     out = {
         "value": round(frames_all / el, 2),
         "ms_per_step": round(el / args.steps * 1e3, 4),
@@ -392,6 +400,9 @@ def headline_leg(ctx):
         "stereo_matches_per_frame": round(float(np.mean([(ur_h[f, :nl_h[f]] >= 0).sum() for f in range(P)])), 1),
         "bow_general_pairs": skipped,
         "rank_digests": [d for _, d in digs],
+        "digest": {"units_per_rank": nuniq, "job": sdist.combine(d for _, d in digs),
+                   "what": "sum over unique frames of BLAKE2b(global frame index, keypoints, descriptors, "
+                           "mvuRight, SearchByBoW a2b / b2a, nmatches) mod 2^62"},
     }
     if ctx["cpu"]:
         out["cpu_baseline"] = headline_cpu(raw_l, raw_r, maps, voc_arrays, mbf, mb, NF)

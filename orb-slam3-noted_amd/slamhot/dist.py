@@ -1,10 +1,12 @@
 """Multi-GPU plumbing of the batched path: one process per GPU, independent
 units (frames, BA windows) sharded by rank, no collective on the data path.  The only
 collectives are the timing reduction (max over ranks), the unit count (sum) and an all-gather
-of per-rank parity digests at the end, plus one setup broadcast of the replicated tables (the
+of per-rank parity digests at the end (each the sum of position-mixed unit hashes), plus one setup broadcast of the replicated tables (the
 vocabulary) from rank 0.  Backend-agnostic: "nccl" (RCCL over xGMI) with
 device tensors in bench.py, "gloo" with CPU tensors in the tests."""
 from __future__ import annotations
+
+import hashlib
 
 import numpy as np
 
@@ -14,17 +16,41 @@ def shard(n_units: int, rank: int, world: int) -> list[int]:
     return list(range(rank, n_units, world))
 
 
-def digest(*arrays) -> int:
-    """64-bit XOR-fold of byte arrays (order-independent across ranks, 62-bit so it fits int64)."""
-    acc = np.uint64(0)
+MASK62 = (1 << 62) - 1
+
+
+def _update(h, arrays):
     for a in arrays:
-        b = np.ascontiguousarray(a).view(np.uint8).ravel()
-        pad = (-len(b)) % 8
-        if pad:
-            b = np.concatenate([b, np.zeros(pad, np.uint8)])
-        if len(b):
-            acc ^= np.bitwise_xor.reduce(b.view(np.uint64))
-    return int(acc & np.uint64((1 << 62) - 1))
+        a = np.ascontiguousarray(a)
+        h.update(f"{a.dtype.str}{a.shape}".encode())
+        h.update(a.view(np.uint8).tobytes())
+
+
+def digest(*arrays) -> int:
+    """62-bit content hash (BLAKE2b) of byte arrays, dtype and shape included (fits int64)."""
+    h = hashlib.blake2b(digest_size=8)
+    _update(h, arrays)
+    return int.from_bytes(h.digest(), "little") & MASK62
+
+
+def unit_hash(index: int, *arrays) -> int:
+    """Hash of one unit of work (a frame, a BA window, a sequence) mixed with its GLOBAL index, so
+    equal outputs of different units never cancel and a unit computed on the wrong rank or in
+    the wrong slot changes the result."""
+    h = hashlib.blake2b(digest_size=8)
+    h.update(int(index).to_bytes(8, "little", signed=True))
+    _update(h, arrays)
+    return int.from_bytes(h.digest(), "little") & MASK62
+
+
+def combine(hashes) -> int:
+    """Order-independent combination of unit hashes (sum mod 2^62): a rank combines its units,
+    the gathered rank values combine the same way into the job's digest, which therefore equals
+    a single-process run over all units whatever the sharding."""
+    acc = 0
+    for x in hashes:
+        acc = (acc + int(x)) & MASK62
+    return acc
 
 
 def _coll_device(dist, device):

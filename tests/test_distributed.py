@@ -24,24 +24,29 @@ def _free_port():
     return port
 
 
-def _frame_digest(idx):
-    descs, count = [], 0
+def _frame_digest(idx, flip=None):
+    """(keypoints, combined unit hashes) of frames idx; flip = frame whose first descriptor
+    bit is flipped (a one-bit parity break on one rank)."""
+    hs, count = [], 0
     for i in idx:
         img = synth.frame(700 + i, 320, 240)
         kps, desc, _ = ob.extract(img)
-        descs.append(desc)
+        if i == flip:
+            desc = desc.copy()
+            desc[0, 0] ^= 1
+        hs.append(sdist.unit_hash(i, kps, desc))
         count += len(kps)
-    return count, sdist.digest(*descs) if descs else 0
+    return count, sdist.combine(hs)
 
 
 def _lba_digest(idx):
-    outs, iters = [], 0
+    hs, iters = [], 0
     for i in idx:
         w = synth.lba_window(900 + i, n_kf=8, n_pt=60, obs_per_pt=3)
         r = ob.lba_solve(w)
-        outs += [r["kf_Tcw"], r["pt_pos"], r["edge_outlier"]]
+        hs.append(sdist.unit_hash(i, r["kf_Tcw"], r["pt_pos"], r["edge_outlier"]))
         iters += r["iterations"][0] + r["iterations"][1]
-    return iters, sdist.digest(*outs) if outs else 0
+    return iters, sdist.combine(hs)
 
 
 def _worker(rank, world, port, q):
@@ -61,10 +66,26 @@ def _worker(rank, world, port, q):
     _, wunits = sdist.reduce_run(dist, "cpu", elapsed, float(len(widx)))
     kg = sdist.gather_digests(dist, "cpu", world, kcount, kdig)
     lg = sdist.gather_digests(dist, "cpu", world, lit, ldig)
+    # the same gather with one descriptor bit flipped in one frame of rank 1
+    _, fdig = _frame_digest(fidx, flip=fidx[0] if rank == 1 else None)
+    fg = sdist.gather_digests(dist, "cpu", world, kcount, fdig)
     # setup broadcast of the replicated vocabulary tables (bench.py match leg)
     voc = sdist.broadcast_arrays(dist, "cpu", synth.vocab(4, 3, 7) if rank == 0 else None)
-    q.put((rank, elapsed, el_max, units, wunits, kg, lg, sdist.digest(*voc), [(a.dtype.str, a.shape) for a in voc]))
+    q.put((rank, elapsed, el_max, units, wunits, kg, lg, sdist.digest(*voc), [(a.dtype.str, a.shape) for a in voc], fg))
     dist.destroy_process_group()
+
+
+def test_unit_hashes_do_not_cancel():
+    """Repeated content (the headline batch repeats its unique frames) must not cancel: the old
+    XOR fold gave 0 for any even repetition; position-mixed unit hashes do not."""
+    d = np.random.default_rng(0).integers(0, 256, (100, 32), dtype=np.uint8)
+    hs = [sdist.unit_hash(i, d) for i in range(8)]
+    assert len(set(hs)) == 8 and sdist.combine(hs) != 0
+    assert sdist.combine(hs) == sdist.combine(hs[::-1])  # order-independent across ranks
+    d2 = d.copy()
+    d2[5, 3] ^= 0x10
+    assert sdist.unit_hash(3, d2) != hs[3]
+    assert sdist.unit_hash(3, d) != sdist.unit_hash(4, d)
 
 
 def test_shard_partitions_units():
@@ -94,10 +115,12 @@ def test_two_rank_gloo_matches_single_process():
     kg, lg = out[0][5], out[0][6]
     kc, kd = _frame_digest(range(N_FRAMES))
     assert sum(c for c, _ in kg) == kc
-    assert np.bitwise_xor.reduce(np.array([d for _, d in kg], np.int64)) == kd
+    assert sdist.combine(d for _, d in kg) == kd != 0
     li, ld = _lba_digest(range(N_WIN))
     assert sum(c for c, _ in lg) == li
-    assert np.bitwise_xor.reduce(np.array([d for _, d in lg], np.int64)) == ld
+    assert sdist.combine(d for _, d in lg) == ld != 0
+    # one flipped descriptor bit on one rank changes the gathered job digest
+    assert sdist.combine(d for _, d in out[0][9]) != kd
     ref = synth.vocab(4, 3, 7)
     for o in out:  # rank 1 received exactly rank 0's tables
         assert o[7] == sdist.digest(*ref)
@@ -126,11 +149,11 @@ def _sequence_digest(idx):
         st = to.SeqState()
         for f in range(SEQ_FRAMES):
             r = to.step(P, voc, maps, st, L[f], R[f])
-            recs.append(np.array([r["n"], r["stereo"], r["nbow"], r["ninl1"], r["nlocal"], r["ninl2"], r["is_kf"],
-                                  r["lost"]], np.int32))
-            recs.append(r["Tcw"].astype(np.float32))
+            recs.append(sdist.unit_hash(1000 * s + f, np.array([r["n"], r["stereo"], r["nbow"], r["ninl1"],
+                                                                 r["nlocal"], r["ninl2"], r["is_kf"], r["lost"]],
+                                                                np.int32), r["Tcw"].astype(np.float32)))
             frames += 1
-    return frames, sdist.digest(*recs) if recs else 0
+    return frames, sdist.combine(recs)
 
 
 def _seq_worker(rank, world, port, q):
@@ -162,4 +185,4 @@ def test_two_rank_gloo_sequence_sharding():
     frames, dig = _sequence_digest(range(N_SEQS))
     g = out[0][2]
     assert sum(c for c, _ in g) == frames
-    assert np.bitwise_xor.reduce(np.array([d for _, d in g], np.int64)) == dig
+    assert sdist.combine(d for _, d in g) == dig != 0
