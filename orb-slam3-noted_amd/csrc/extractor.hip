@@ -99,6 +99,24 @@ __device__ __forceinline__ int level_pitch(const DevPlan& P, int l) {
 
 // packed u16 pairs (v_pk_*_u16) for the SWAR FAST pre-test
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+// XCD-aware workgroup order (MI355X_MICROARCH.md, Workgroup dispatch / XCD placement; guide T1):
+// the dispatcher deals workgroups round-robin over the 8 XCDs, each with its own L2, so
+// consecutive workgroups -- neighbouring cells / keypoints of one frame, whose windows overlap --
+// land on 8 different L2s and each fetches the shared rows from HBM.  This bijective remap of the
+// (x, y) grid gives every XCD one contiguous run of it (a few whole frames), so the overlapping
+// windows of a frame are fetched once into one L2.  Speed only: any placement is correct.
+#ifndef SLAMHOT_NO_XCD_REMAP
+__device__ __forceinline__ int2 xcd_block() {
+    const int gx = gridDim.x, nwg = gridDim.x * gridDim.y;
+    const int orig = blockIdx.x + gx * blockIdx.y;
+    const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+    const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+    return int2{wg % gx, wg / gx};
+}
+#else
+__device__ __forceinline__ int2 xcd_block() { return int2{(int)blockIdx.x, (int)blockIdx.y}; }
+#endif
+
 __device__ __forceinline__ us2 as_us2(uint32_t x) { return __builtin_bit_cast(us2, x); }
 __device__ __forceinline__ uint32_t as_u32(us2 x) { return __builtin_bit_cast(uint32_t, x); }
 
@@ -474,10 +492,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))
                                                    FastWaveLds lay) {
     extern __shared__ __attribute__((aligned(16))) uint8_t fw_smem[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int idx = blockIdx.x * 4 + wave;
+    const int2 blk = xcd_block();
+    const int idx = blk.x * 4 + wave;
     if (idx >= nlist) return;
     const DevPlan& P = *b.plan;
-    const int f = blockIdx.y;
+    const int f = blk.y;
     const CellDesc cd = b.cells[list[idx]];
     const int l = cd.level;
     const uint8_t* img = level_ptr(b, P, f, l);
@@ -1209,9 +1228,10 @@ __global__ void __launch_bounds__(256) k_orb3(Bufs b) {
     __shared__ __attribute__((aligned(16))) uint32_t raw_all[4][kO3R * kO3RawS];
     __shared__ __attribute__((aligned(16))) uint32_t hp_all[4][kO3Pairs * kO3HS];
     const DevPlan& P = *b.plan;
-    const int f = blockIdx.y;
+    const int2 blk = xcd_block();
+    const int f = blk.y;
     const int wave = threadIdx.x >> 6;
-    const int slot = blockIdx.x * 4 + wave;
+    const int slot = blk.x * 4 + wave;
     const int lane = threadIdx.x & 63;
     if (slot >= P.kslots) return;
     int l = 0;
