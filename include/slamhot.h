@@ -330,6 +330,23 @@ slam_status slamhot_search_by_projection_kf(slam_matcher* m, const slam_frame_vi
                                             const slam_kf_points* KF, float nnratio, int check_ori,
                                             float th, int orb_dist, int32_t* f_match, int* nmatches);
 
+/* Batched forms of the two projection matchers above: nframes independent problems staged into
+ * one pinned host image, one upload, one k_search_by_projection launch (a workgroup per frame),
+ * one copy back; results identical to nframes single calls.  f_match[f] holds frames[f].n
+ * entries, nmatches[f] the count.
+ *   _last_batch: SearchByProjection(Frame&, const Frame& LastFrame, th, bMono), the matcher of
+ *     Tracking::TrackWithMotionModel, which every steady-state frame runs (Tracking.cc:2683-2760,
+ *     ORBmatcher.cc:2173-2389); frame f against last[f].
+ *   _kf_batch: SearchByProjection(Frame&, KeyFrame*, const set<MapPoint*>&, th, ORBdist)
+ *     (Tracking::Relocalization, Tracking.cc:3455-3590; ORBmatcher.cc:2391-2513); frame f
+ *     against kfs[f]. */
+slam_status slamhot_search_by_projection_last_batch(slam_matcher* m, int nframes, const slam_frame_view* frames,
+                                                    const slam_last_frame* last, float nnratio, int check_ori,
+                                                    float th, int mono, int32_t* const* f_match, int32_t* nmatches);
+slam_status slamhot_search_by_projection_kf_batch(slam_matcher* m, int nframes, const slam_frame_view* frames,
+                                                  const slam_kf_points* kfs, float nnratio, int check_ori,
+                                                  float th, int orb_dist, int32_t* const* f_match, int32_t* nmatches);
+
 /* ------------------------------------------------------------------------------------------
  * Local bundle adjustment: the g2o LM/Schur solve inside
  *   static void Optimizer::LocalBundleAdjustment(KeyFrame* pKF, bool* pbStopFlag, Map* pMap,
@@ -589,8 +606,10 @@ slam_status slamhot_rectify_batch_device(slam_rectifier* r, int nframes, const v
 /* ------------------------------------------------------------------ per-sequence tracking
  * The stereo tracking chain of Tracking::Track for rectified stereo (BASELINE.json configs[4]),
  * device-resident: per frame cv::remap x2 -> ORBextractor x2 -> Frame::ComputeStereoMatches ->
- * ComputeBoW + SearchByBoW(reference KF, F) -> PoseOptimization -> SearchLocalPoints ->
- * PoseOptimization -> NeedNewKeyFrame / CreateNewKeyFrame (Tracking.cc:1256-3330), with every
+ * TrackWithMotionModel (SearchByProjection(F, LastFrame) + PoseOptimization) when a velocity
+ * exists, else / on its failure ComputeBoW + SearchByBoW(reference KF, F) + PoseOptimization ->
+ * SearchLocalPoints -> PoseOptimization -> NeedNewKeyFrame / CreateNewKeyFrame
+ * (Tracking.cc:1256-3330), with every
  * decision taken on the device.  nseq sequences advance in lock-step (one frame each per step);
  * the map is the reference KeyFrame of each sequence (DESIGN.md §4g states what LocalMapping-side
  * bookkeeping is left out). */
@@ -614,8 +633,33 @@ typedef struct slam_track_record {   /* one step of one sequence */
     int32_t n_inl_ref;               /* TrackReferenceKeyFrame's nmatchesMap */
     int32_t n_local;                 /* SearchByProjection matches of SearchLocalPoints */
     int32_t n_inl;                   /* TrackLocalMap's mnMatchesInliers */
-    int32_t is_keyframe, lost, initialized, pad[3];
+    int32_t is_keyframe, lost, initialized;
+    int32_t n_motion;                /* TrackWithMotionModel's SearchByProjection(F, LastFrame) matches
+                                        (after the 2 th retry; 0 = not tried: no velocity) */
+    int32_t motion;                  /* 1: the first pose came from the motion model (n_bow = 0, the
+                                        reference never ran TrackReferenceKeyFrame) */
+    int32_t status;                  /* 0 ok; 1 a SearchByProjection candidate overflow voided the step:
+                                        the sequence kept its previous state (lost = 1) */
 } slam_track_record;
+
+typedef struct slam_track_state {    /* a sequence's tracking state between steps (read back) */
+    float V[16];                     /* mVelocity, valid when has_vel */
+    float Tlr[16];                   /* mlRelativeFramePoses.back(): last frame w.r.t. its reference KF */
+    float Tref[16];                  /* the reference KeyFrame's pose */
+    int32_t has_vel, nkf;            /* KeyFrames created in the sequence (KeyFramesInMap) */
+    int32_t last_n, cap;             /* mLastFrame.N; cap: capacity of the arrays below (in) */
+    slam_keypoint* last_kps;         /* mLastFrame.mvKeysUn */
+    int32_t* last_mp;                /* mLastFrame.mvpMapPoints as reference-KeyFrame MapPoint slots, -1 = NULL */
+} slam_track_state;
+
+typedef struct slam_track_frame {    /* the last step's per-feature results of one sequence */
+    int32_t n, cap;                  /* N; cap: capacity of the arrays (in) */
+    float* uright;                   /* mvuRight (ComputeStereoMatches) */
+    int32_t* bow_match;              /* SearchByBoW(refKF, F): the KF feature (= MapPoint slot) per feature */
+    int32_t* motion_match;           /* SearchByProjection(F, LastFrame): MapPoint slot per feature */
+    int32_t* local_match;            /* SearchLocalPoints' SearchByProjection: MapPoint slot per feature */
+    int32_t* mappoints;              /* mvpMapPoints at the end of the step (outliers removed) */
+} slam_track_frame;
 
 typedef struct slam_track_keyframe { /* the reference KeyFrame of one sequence (read back) */
     float Tcw[16];                   /* the sequence's current pose */
@@ -641,6 +685,10 @@ slam_status slamhot_tracker_step_device(slam_tracker* t, const void* d_left, int
  * candidates overflowed (its matches would be incomplete). */
 slam_status slamhot_tracker_records(slam_tracker* t, slam_track_record* out);
 slam_status slamhot_tracker_keyframe(slam_tracker* t, int seq, slam_track_keyframe* kf);
+/* The motion-model state and last frame of sequence seq (synchronising). */
+slam_status slamhot_tracker_state(slam_tracker* t, int seq, slam_track_state* st);
+/* The last step's per-feature match arrays of sequence seq (synchronising; NULL arrays skipped). */
+slam_status slamhot_tracker_frame(slam_tracker* t, int seq, slam_track_frame* fr);
 
 #ifdef __cplusplus
 }

@@ -1370,6 +1370,17 @@ bool frame_ok(const slam_frame_view* F) {
            F->nlevels <= 16 && F->scale;
 }
 
+bool last_ok(const slam_last_frame* LF) {
+    return LF && LF->Tcw && LF->n >= 0 &&
+           (LF->n == 0 || (LF->kps && LF->kps_un && LF->has_mp && LF->outlier && LF->mp_pos && LF->mp_desc &&
+                           LF->mp_has_obs));
+}
+
+bool kf_ok(const slam_kf_points* KF) {
+    return KF && KF->n >= 0 &&
+           (KF->n == 0 || (KF->kps_un && KF->use && KF->mp_pos && KF->max_dist && KF->min_dist && KF->mp_desc));
+}
+
 slam_status run_projection(slam_matcher* m, const slam_frame_view* F, DevProjCall& Cc, int nq,
                            const std::vector<ProjQuery>* host_queries, const uint8_t* qdesc,
                            int32_t* f_match, int* nmatches,
@@ -1710,10 +1721,7 @@ extern "C" slam_status slamhot_search_local_points_batch(slam_matcher* m, int nf
 extern "C" slam_status slamhot_search_by_projection_last(slam_matcher* m, const slam_frame_view* F,
                                                          const slam_last_frame* LF, float nnratio, int check_ori,
                                                          float th, int mono, int32_t* f_match, int* nmatches) {
-    if (!m || !frame_ok(F) || !F->Tcw || !LF || !LF->Tcw || LF->n < 0 || !f_match || !nmatches) return SLAM_EINVAL;
-    if (LF->n && (!LF->kps || !LF->kps_un || !LF->has_mp || !LF->outlier || !LF->mp_pos || !LF->mp_desc ||
-                  !LF->mp_has_obs))
-        return SLAM_EINVAL;
+    if (!m || !frame_ok(F) || !F->Tcw || !last_ok(LF) || !f_match || !nmatches) return SLAM_EINVAL;
     DevProjCall C{};
     fill_frame(C, F);
     C.mode = kProjLast;
@@ -1736,20 +1744,15 @@ extern "C" slam_status slamhot_search_by_projection_last(slam_matcher* m, const 
 // The KeyFrame variant's per-MapPoint geometry (projection, distance gate and
 // MapPoint::PredictScale with glibc logf, MapPoint.cc:551-566) runs here on the host, in
 // the reference's arithmetic; candidate search and resolution run on the device.
-extern "C" slam_status slamhot_search_by_projection_kf(slam_matcher* m, const slam_frame_view* F,
-                                                       const slam_kf_points* KF, float nnratio, int check_ori,
-                                                       float th, int orb_dist, int32_t* f_match, int* nmatches) {
-    if (!m || !frame_ok(F) || !F->Tcw || !KF || KF->n < 0 || !f_match || !nmatches) return SLAM_EINVAL;
-    if (KF->n && (!KF->kps_un || !KF->use || !KF->mp_pos || !KF->max_dist || !KF->min_dist || !KF->mp_desc))
-        return SLAM_EINVAL;
-    (void)nnratio;
+namespace {
+void kf_queries(const slam_frame_view* F, const slam_kf_points* KF, float th, std::vector<ProjQuery>& qs) {
     const float* T = F->Tcw;
     float Ow[3];
     for (int i = 0; i < 3; i++) {
         const double acc = (double)T[i] * T[3] + (double)T[4 + i] * T[7] + (double)T[8 + i] * T[11];
         Ow[i] = (float)(-1.0 * acc);
     }
-    std::vector<ProjQuery> qs(KF->n);
+    qs.assign(KF->n, ProjQuery{});
     for (int i = 0; i < KF->n; i++) {
         ProjQuery& Q = qs[i];
         Q.valid = 0;
@@ -1780,10 +1783,200 @@ extern "C" slam_status slamhot_search_by_projection_kf(slam_matcher* m, const sl
         Q.min_level = (int16_t)(level - 1);
         Q.max_level = (int16_t)(level + 1);
     }
+}
+
+// Bump layout over one pinned host image and its device copy: a sizing pass (host == nullptr)
+// fixes every offset, the filling pass repeats the same puts with the buffers in place.
+struct Stager {
+    uint8_t* host = nullptr;
+    uint8_t* dev = nullptr;
+    size_t off = 0;
+    template <class T>
+    const T* put(const T* src, size_t count) {
+        if (!src || !count) return nullptr;
+        const size_t o = off;
+        off += (count * sizeof(T) + 255) & ~(size_t)255;
+        if (host) std::memcpy(host + o, src, count * sizeof(T));
+        return reinterpret_cast<const T*>(dev + o);
+    }
+    template <class T>
+    T* take(size_t count) {
+        const size_t o = off;
+        off += (count * sizeof(T) + 255) & ~(size_t)255;
+        return reinterpret_cast<T*>(dev + o);
+    }
+};
+
+// Batched SearchByProjection over nframes independent problems of one mode (last frame /
+// KeyFrame): every frame's inputs, grid and call record staged into one pinned host image and
+// uploaded with one copy, one k_search_by_projection launch (a workgroup per frame), every
+// frame's f_match / counters back with one copy.  `inputs(f, S, C)` puts the mode's per-frame
+// inputs and returns the query count; a frame whose candidates overflow the preset capacity
+// goes again through `single(f)`.
+slam_status run_projection_batch(slam_matcher* m, int nframes, const slam_frame_view* frames, const DevProjCall& proto,
+                                 const std::function<int(int, Stager&, DevProjCall&)>& inputs,
+                                 int32_t* const* f_match, int32_t* nmatches,
+                                 const std::function<slam_status(int, int*)>& single) {
+    std::vector<std::vector<int32_t>> starts(nframes), feats(nframes);
+    for (int f = 0; f < nframes; f++) build_grid_csr(&frames[f], starts[f], feats[f]);
+    std::vector<DevProjCall> calls(nframes);
+    std::vector<size_t> fm_off(nframes), out_off(nframes);
+    size_t in_bytes = 0, res_off = 0, total = 0, lds = 0, calls_off = 0;
+    std::lock_guard<std::mutex> g(m->mu);
+    SLAM_HIP_TRY(hipSetDevice(m->device));
+    for (int pass = 0; pass < 2; pass++) {
+        Stager S;
+        if (pass == 1) {
+            slam_status st;
+            if ((st = m->d_a.ensure(total)) || (st = m->stage(in_bytes + (total - res_off)))) return st;
+            S.host = m->h_stage;
+            S.dev = m->d_a.as<uint8_t>();
+        }
+        for (int f = 0; f < nframes; f++) {
+            const slam_frame_view& F = frames[f];
+            DevProjCall C = proto;
+            fill_frame(C, &F);
+            C.F.n = F.n;
+            C.F.kps = S.put(F.kps_un, F.n);
+            C.F.uright = S.put(F.uright, F.n);
+            C.F.desc = S.put(F.desc, (size_t)F.n * 32);
+            C.F.state = S.put(F.mp_state, F.n);
+            C.F.cell_start = S.put(starts[f].data(), starts[f].size());
+            C.F.cell_feat = S.put(feats[f].data(), feats[f].size());
+            C.nq = inputs(f, S, C);
+            calls[f] = C;
+        }
+        calls_off = S.off;
+        S.off += (sizeof(DevProjCall) * nframes + 255) & ~(size_t)255;
+        in_bytes = S.off;
+        for (int f = 0; f < nframes; f++) {  // device-only scratch
+            DevProjCall& C = calls[f];
+            const int nq = C.nq;
+            if (!C.queries) C.queries = S.take<ProjQuery>(std::max(1, nq));
+            C.cand_off = S.take<int32_t>(nq + 1);
+            C.cand_cap = std::max(4096, nq * 64);
+            C.cand = S.take<uint32_t>(C.cand_cap);
+            const size_t need = projection_lds_bytes(frames[f].n, nq);
+            C.gstate = need ? nullptr : S.take<int32_t>(2 * (size_t)frames[f].n + 2 * (size_t)nq);
+            if (need) lds = std::max(lds, need);
+        }
+        res_off = S.off;  // results of every frame in one tail: one copy back
+        for (int f = 0; f < nframes; f++) {
+            fm_off[f] = S.off;
+            calls[f].f_match = S.take<int32_t>(std::max(1, frames[f].n));
+            out_off[f] = S.off;
+            calls[f].out = S.take<int32_t>(4);
+        }
+        total = S.off;
+        if (pass == 1) std::memcpy(S.host + calls_off, calls.data(), sizeof(DevProjCall) * nframes);
+    }
+    uint8_t* D = m->d_a.as<uint8_t>();
+    uint8_t* R = m->h_stage + in_bytes;
+    hipStream_t st = m->stream;
+    SLAM_HIP_TRY(hipMemcpyAsync(D, m->h_stage, in_bytes, hipMemcpyHostToDevice, st));
+    SLAM_HIP_TRY(hipMemsetAsync(D + res_off, 0, total - res_off, st));
+    SLAM_HIP_TRY(launch_search_by_projection((const DevProjCall*)(D + calls_off), nframes, lds, st));
+    SLAM_HIP_TRY(hipMemcpyAsync(R, D + res_off, total - res_off, hipMemcpyDeviceToHost, st));
+    SLAM_HIP_TRY(hipStreamSynchronize(st));
+    std::vector<int> redo;
+    for (int f = 0; f < nframes; f++) {
+        const int32_t* out = (const int32_t*)(R + (out_off[f] - res_off));
+        if (out[1] == 1) {
+            redo.push_back(f);
+            continue;
+        }
+        nmatches[f] = out[0];
+        if (frames[f].n) std::memcpy(f_match[f], R + (fm_off[f] - res_off), 4 * (size_t)frames[f].n);
+    }
+    m->mu.unlock();
+    slam_status rs = SLAM_OK;
+    for (int f : redo) {
+        int n = 0;
+        if ((rs = single(f, &n)) != SLAM_OK) break;
+        nmatches[f] = n;
+    }
+    m->mu.lock();  // the guard unlocks on return
+    return rs;
+}
+}  // namespace
+
+extern "C" slam_status slamhot_search_by_projection_kf(slam_matcher* m, const slam_frame_view* F,
+                                                       const slam_kf_points* KF, float nnratio, int check_ori,
+                                                       float th, int orb_dist, int32_t* f_match, int* nmatches) {
+    if (!m || !frame_ok(F) || !F->Tcw || !kf_ok(KF) || !f_match || !nmatches) return SLAM_EINVAL;
+    (void)nnratio;
+    std::vector<ProjQuery> qs;
+    kf_queries(F, KF, th, qs);
     DevProjCall C{};
     fill_frame(C, F);
     C.mode = kProjKF;
     C.th_dist = orb_dist;
     C.check_ori = check_ori;
     return run_projection(m, F, C, KF->n, &qs, KF->mp_desc, f_match, nmatches, [](Blob&, DevProjCall&) {});
+}
+
+extern "C" slam_status slamhot_search_by_projection_last_batch(slam_matcher* m, int nframes,
+                                                               const slam_frame_view* frames,
+                                                               const slam_last_frame* last, float nnratio,
+                                                               int check_ori, float th, int mono,
+                                                               int32_t* const* f_match, int32_t* nmatches) {
+    if (!m || nframes < 0 || (nframes && (!frames || !last || !f_match || !nmatches))) return SLAM_EINVAL;
+    for (int f = 0; f < nframes; f++)
+        if (!frame_ok(&frames[f]) || !frames[f].Tcw || !last_ok(&last[f]) || (frames[f].n && !f_match[f]))
+            return SLAM_EINVAL;
+    if (nframes == 0) return SLAM_OK;
+    DevProjCall proto{};
+    proto.mode = kProjLast;
+    proto.th = th;
+    proto.mono = mono;
+    proto.nnratio = nnratio;
+    proto.th_dist = 100;
+    proto.check_ori = check_ori;
+    return run_projection_batch(
+        m, nframes, frames, proto,
+        [&](int f, Stager& S, DevProjCall& c) {
+            const slam_last_frame& LF = last[f];
+            for (int i = 0; i < 16; i++) c.LT[i] = LF.Tcw[i];
+            c.lf_kps = S.put(LF.kps, LF.n);
+            c.lf_kps_un = S.put(LF.kps_un, LF.n);
+            c.lf_has_mp = S.put(LF.has_mp, LF.n);
+            c.lf_outlier = S.put(LF.outlier, LF.n);
+            c.lf_pos = S.put(LF.mp_pos, (size_t)LF.n * 3);
+            c.lf_has_obs = S.put(LF.mp_has_obs, LF.n);
+            c.qdesc = S.put(LF.mp_desc, (size_t)LF.n * 32);
+            c.queries = nullptr;
+            return LF.n;
+        },
+        f_match, nmatches,
+        [&](int f, int* n) {
+            return slamhot_search_by_projection_last(m, &frames[f], &last[f], nnratio, check_ori, th, mono, f_match[f], n);
+        });
+}
+
+extern "C" slam_status slamhot_search_by_projection_kf_batch(slam_matcher* m, int nframes, const slam_frame_view* frames,
+                                                             const slam_kf_points* kfs, float nnratio, int check_ori,
+                                                             float th, int orb_dist, int32_t* const* f_match,
+                                                             int32_t* nmatches) {
+    if (!m || nframes < 0 || (nframes && (!frames || !kfs || !f_match || !nmatches))) return SLAM_EINVAL;
+    for (int f = 0; f < nframes; f++)
+        if (!frame_ok(&frames[f]) || !frames[f].Tcw || !kf_ok(&kfs[f]) || (frames[f].n && !f_match[f]))
+            return SLAM_EINVAL;
+    if (nframes == 0) return SLAM_OK;
+    std::vector<std::vector<ProjQuery>> qs(nframes);
+    for (int f = 0; f < nframes; f++) kf_queries(&frames[f], &kfs[f], th, qs[f]);
+    DevProjCall proto{};
+    proto.mode = kProjKF;
+    proto.th_dist = orb_dist;
+    proto.check_ori = check_ori;
+    return run_projection_batch(
+        m, nframes, frames, proto,
+        [&](int f, Stager& S, DevProjCall& c) {
+            c.queries = const_cast<ProjQuery*>(S.put(qs[f].data(), qs[f].size()));
+            c.qdesc = S.put(kfs[f].mp_desc, (size_t)kfs[f].n * 32);
+            return kfs[f].n;
+        },
+        f_match, nmatches,
+        [&](int f, int* n) {
+            return slamhot_search_by_projection_kf(m, &frames[f], &kfs[f], nnratio, check_ori, th, orb_dist, f_match[f], n);
+        });
 }

@@ -2,10 +2,13 @@
 // one sequence per GPU; here S sequences advance in lock-step on one GPU so the batched case
 // fills the chip).  One step = one stereo frame per sequence:
 //
-//   cv::remap x2 -> ORBextractor x2 -> Frame::ComputeStereoMatches -> ComputeBoW +
-//   SearchByBoW(reference KF, F) -> PoseOptimization -> SearchLocalPoints (isInFrustum +
-//   SearchByProjection over the reference KeyFrame's MapPoints) -> PoseOptimization ->
-//   NeedNewKeyFrame / CreateNewKeyFrame   (Tracking.cc:1256-3330; tests/track_oracle.py)
+//   cv::remap x2 -> ORBextractor x2 -> Frame::ComputeStereoMatches ->
+//   TrackWithMotionModel when a velocity exists (UpdateLastFrame, SearchByProjection(F,
+//   LastFrame, 7), retry at 14 below 20 matches, PoseOptimization, >= 10 inliers), else or on
+//   its failure TrackReferenceKeyFrame (ComputeBoW + SearchByBoW(reference KF, F),
+//   PoseOptimization) -> SearchLocalPoints (isInFrustum + SearchByProjection over the reference
+//   KeyFrame's MapPoints) -> PoseOptimization -> motion model update -> NeedNewKeyFrame /
+//   CreateNewKeyFrame   (Tracking.cc:1256-3330; tests/track_oracle.py)
 //
 // Every decision (initialisation, lost, keyframe insertion) is taken on the device: the host
 // only enqueues the same launches every step and never waits, so a sequence advances at the
@@ -19,6 +22,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -41,14 +45,21 @@ struct Params {
 };
 
 struct Seq {  // per-sequence state, device resident
-    float Tcw[16];
-    float T1[16];       // pose after TrackReferenceKeyFrame
+    float Tcw[16];      // mLastFrame.mTcw (the last tracked frame's pose)
+    float T1[16];       // pose after TrackWithMotionModel / TrackReferenceKeyFrame
+    float V[16];        // mVelocity (valid when has_vel)
+    float Tlr[16];      // mlRelativeFramePoses.back(): the last frame relative to its reference KF
+    float Tref[16];     // the reference KeyFrame's pose (KeyFrame::GetPose)
+    float Tlast[16];    // mLastFrame.mTcw as this step uses it (UpdateLastFrame: Tlr * Tref)
+    float Tpred[16];    // mVelocity * mLastFrame.mTcw
     int initialized, cur, n_ref, active;
+    int has_vel, nkf, mode, last_n;  // mode 1: this step's first pose came from the motion model
+    int motion_try, motion_n, fail, pad;
 };
 
 struct Rec {  // what one step reports per sequence (slam_track_record)
     float Tcw[16];
-    int n, n_stereo, n_bow, n_inl_ref, n_local, n_inl, is_kf, lost, initialized, pad[3];
+    int n, n_stereo, n_bow, n_inl_ref, n_local, n_inl, is_kf, lost, initialized, n_motion, motion, status;
 };
 
 struct MapPts {  // the reference KeyFrame's MapPoint slots, one per KF feature (x2: double buffer)
@@ -90,6 +101,19 @@ struct Bufs {
     int cand_cap;
     int32_t* fmatch;      // S x cap
     int32_t* pout;        // S x 4
+    // TrackWithMotionModel: the last frame, its SearchByProjection query arrays, two attempts
+    slam_keypoint* lf_kps;  // S x cap: mLastFrame.mvKeysUn
+    int32_t* lf_fmp;        // S x cap: mLastFrame.mvpMapPoints as MapPoint slots of the current map
+    uint8_t* lf_has;        // S x cap
+    uint8_t* lf_zero;       // S x cap, 0: mvbOutlier (outliers left the frame, Tracking.cc:2105-2109)
+    uint8_t* lf_one;        // S x cap, 1: Observations() > 0
+    float* lf_pos;          // S x cap x 3
+    uint8_t* lf_desc;       // S x cap x 32
+    const int8_t* fclear;   // S x cap, -1: mvpMapPoints cleared before the search (Tracking.cc:2704)
+    DevProjCall* mcalls;    // 2S: th = 7, then 2 th for the sequences below 20 matches
+    int32_t* mmatch;        // 2 x S x cap
+    int32_t* mout;          // 2 x S x 4
+    int32_t* motm;          // S x cap: the motion model's matches (MapPoint slot per feature)
 };
 
 __device__ inline size_t slot(const Params& P, int s) { return (size_t)s * P.cap; }
@@ -100,6 +124,32 @@ __device__ inline void camera_center(const float* T, float* Ow) {
         const double acc = (double)T[i] * (double)T[3] + (double)T[4 + i] * (double)T[7] + (double)T[8 + i] * (double)T[11];
         Ow[i] = (float)(-1.0 * acc);
     }
+}
+
+// 4x4 float cv::Mat product (cv::gemm on CV_32F accumulates in double, one rounding per entry,
+// DESIGN.md §1 deviation 3): C = A * B, row-major
+__device__ inline void gemm4(const float* A, const float* B, float* C) {
+    float o[16];
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++) {
+            double acc = 0.0;
+            for (int k = 0; k < 4; k++) acc += (double)A[4 * i + k] * (double)B[4 * k + j];
+            o[4 * i + j] = (float)acc;
+        }
+    for (int k = 0; k < 16; k++) C[k] = o[k];
+}
+
+// the inverse pose Twc as Frame::UpdatePoseMatrices / KeyFrame::SetPose form it: Rwc = Rcw^T,
+// Ow = -Rcw^T tcw, last row (0, 0, 0, 1)
+__device__ inline void pose_inverse(const float* T, float* Twc) {
+    float Ow[3];
+    camera_center(T, Ow);
+    for (int r = 0; r < 3; r++) {
+        for (int c = 0; c < 3; c++) Twc[4 * r + c] = T[4 * c + r];
+        Twc[4 * r + 3] = Ow[r];
+    }
+    Twc[12] = Twc[13] = Twc[14] = 0.f;
+    Twc[15] = 1.f;
 }
 
 // order-preserving compaction helper: exclusive prefix of `flag` over the block (chunked)
@@ -167,30 +217,6 @@ __device__ int drop_outliers(const Bufs& B, int s, int* scratch) {
     return block_reduce_sum(cnt, scratch);
 }
 
-// ---------------------------------------------------------------- step kernels
-// after extraction + stereo + BoW: TrackReferenceKeyFrame's matches -> PoseOptimization input
-__global__ void __launch_bounds__(kT) k_ref_edges(Bufs B) {
-    __shared__ int scratch[20];
-    const int s = blockIdx.x;
-    const Params& P = B.P;
-    const size_t o = slot(P, s);
-    Seq& Q = B.seq[s];
-    const bool active = Q.initialized && B.nbow[s] >= 15;  // Tracking.cc:2571-2575
-    for (int i = threadIdx.x; i < B.n[s]; i += kT) B.fmp[o + i] = active ? B.b2a[o + i] : -1;
-    __syncthreads();
-    pack_edges(B, s, Q.Tcw, active, scratch);
-    if (threadIdx.x == 0) {
-        Q.active = active;
-        Rec& R = B.rec[s];
-        R.n = B.n[s];
-        R.n_bow = Q.initialized ? B.nbow[s] : 0;
-        R.n_inl_ref = R.n_local = R.n_inl = 0;
-        R.is_kf = 0;
-        R.lost = Q.initialized && !active;
-        R.initialized = Q.initialized;
-    }
-}
-
 // Frame::AssignFeaturesToGrid (Frame.cc:380-411) as CSR over cells [ix][iy]: (cell, index) keys
 // sorted in LDS (keys are unique, so the order inside a cell is the insertion order)
 __device__ void build_grid(const Bufs& B, int s, uint32_t* keys) {
@@ -242,20 +268,196 @@ __device__ void build_grid(const Bufs& B, int s, uint32_t* keys) {
     __syncthreads();
 }
 
-// after the first PoseOptimization: outliers out (TrackReferenceKeyFrame, :2586-2616); the
-// SearchLocalPoints inputs (Tracking.cc:3179-3258): MapPoint records, grid, call records
-__global__ void __launch_bounds__(kT) k_local_setup(Bufs B) {
-    __shared__ int scratch[20];
+// ---------------------------------------------------------------- step kernels
+// TrackWithMotionModel setup (Tracking.cc:2683-2718), after extraction + stereo + BoW: the frame
+// grid, UpdateLastFrame (mLastFrame.SetPose(Tlr * pRef->GetPose()), :2619-2627), the predicted
+// pose mVelocity * mLastFrame.mTcw, the last frame's MapPoints as SearchByProjection queries and
+// the call records of both attempts (th = 7 stereo, ORBmatcher(0.9, true)).
+__global__ void __launch_bounds__(kT) k_motion_setup(Bufs B) {
     __shared__ uint32_t keys[kMaxCap];
     const int s = blockIdx.x;
     const Params& P = B.P;
     const size_t o = slot(P, s);
     Seq& Q = B.seq[s];
+    if (Q.initialized) build_grid(B, s, keys);  // Frame::AssignFeaturesToGrid of the current frame
+    const bool try_m = Q.initialized && Q.has_vel;
+    const int nq = try_m ? Q.last_n : 0;
+    const MapPts& M = B.mp[Q.cur];
+    for (int i = threadIdx.x; i < nq; i += kT) {
+        const int j = B.lf_fmp[o + i];
+        const float4 X = j >= 0 ? M.pos[o + j] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const bool has = j >= 0 && X.w != 0.f;
+        B.lf_has[o + i] = has;
+        B.lf_pos[3 * (o + i)] = X.x;
+        B.lf_pos[3 * (o + i) + 1] = X.y;
+        B.lf_pos[3 * (o + i) + 2] = X.z;
+        uint4* d = reinterpret_cast<uint4*>(B.lf_desc + (o + i) * 32);
+        if (has) {
+            const uint4* ms = reinterpret_cast<const uint4*>(M.desc + (o + j) * 32);
+            d[0] = ms[0];
+            d[1] = ms[1];
+        }
+    }
+    if (threadIdx.x != 0) return;
+    if (try_m) {
+        gemm4(Q.Tlr, Q.Tref, Q.Tlast);   // UpdateLastFrame
+        gemm4(Q.V, Q.Tlast, Q.Tpred);    // mCurrentFrame.SetPose(mVelocity * mLastFrame.mTcw)
+    } else {
+        for (int k = 0; k < 16; k++) Q.Tlast[k] = Q.Tcw[k];
+    }
+    Q.motion_try = try_m;
+    Q.motion_n = 0;
+    Q.mode = 0;
+    Q.fail = 0;
+    for (int a = 0; a < 2; a++) {
+        DevProjCall C{};
+        DevProjFrame& F = C.F;
+        F.n = B.n[s];
+        F.kps = B.kps + o;
+        F.uright = B.ur + o;
+        F.desc = B.desc + o * 32;
+        F.state = B.fclear + o;
+        F.cell_start = B.cell_start + (size_t)s * (kGridCells + 1);
+        F.cell_feat = B.cell_feat + o;
+        F.min_x = P.min_x;
+        F.min_y = P.min_y;
+        F.max_x = P.max_x;
+        F.max_y = P.max_y;
+        F.inv_w = P.grid_inv_w;
+        F.inv_h = P.grid_inv_h;
+        F.fx = P.fx;
+        F.fy = P.fy;
+        F.cx = P.cx;
+        F.cy = P.cy;
+        F.bf = P.bf;
+        F.b = P.b;
+        for (int k = 0; k < 16; k++) {
+            F.T[k] = Q.Tpred[k];
+            C.LT[k] = Q.Tlast[k];
+            F.scale[k] = k < P.nlevels ? P.scale[k] : 1.f;
+        }
+        F.nlevels = P.nlevels;
+        C.mode = kProjLast;
+        C.nq = a == 0 ? nq : 0;  // the retry's count is set by k_motion_retry
+        C.th = a == 0 ? 7.0f : 14.0f;  // Tracking.cc:2710-2714, 2722
+        C.mono = 0;
+        C.nnratio = 0.9f;
+        C.th_dist = 100;  // TH_HIGH
+        C.check_ori = 1;
+        C.lf_kps = B.lf_kps + o;
+        C.lf_kps_un = B.lf_kps + o;  // rectified stereo: mvKeysUn == mvKeys
+        C.lf_has_mp = B.lf_has + o;
+        C.lf_outlier = B.lf_zero + o;
+        C.lf_pos = B.lf_pos + 3 * o;
+        C.lf_has_obs = B.lf_one + o;
+        C.queries = B.queries + o;
+        C.qdesc = B.lf_desc + o * 32;
+        C.cand_off = B.cand_off + (size_t)s * (P.cap + 1);
+        C.cand = B.cand + (size_t)s * B.cand_cap;
+        C.cand_cap = B.cand_cap;
+        C.f_match = B.mmatch + (size_t)a * P.S * P.cap + o;
+        C.out = B.mout + 4 * ((size_t)a * P.S + s);
+        C.gstate = nullptr;
+        for (int k = 0; k < 4; k++) C.out[k] = 0;
+        B.mcalls[(size_t)a * P.S + s] = C;
+    }
+}
+
+// "If few matches, uses a wider window search" (Tracking.cc:2718-2724): the second attempt runs
+// for the sequences whose first one found fewer than 20 matches
+__global__ void k_motion_retry(Bufs B) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= B.P.S) return;
+    const Seq& Q = B.seq[s];
+    const int32_t* out = B.mout + 4 * s;
+    B.mcalls[B.P.S + s].nq = (Q.motion_try && out[1] == 0 && out[0] < 20) ? Q.last_n : 0;
+}
+
+// the motion model's matches join the frame (MapPoint of the matched last-frame feature) and the
+// PoseOptimization input from the predicted pose (Tracking.cc:2726-2735)
+__global__ void __launch_bounds__(kT) k_motion_edges(Bufs B) {
+    __shared__ int scratch[20];
+    const int s = blockIdx.x;
+    const Params& P = B.P;
+    const size_t o = slot(P, s);
+    Seq& Q = B.seq[s];
+    const int32_t* o0 = B.mout + 4 * s;
+    const int32_t* o1 = B.mout + 4 * ((size_t)P.S + s);
+    const bool retry = Q.motion_try && o0[1] == 0 && o0[0] < 20;
+    const bool overflow = Q.motion_try && (o0[1] == 1 || (retry && o1[1] == 1));
+    const int nm = !Q.motion_try ? 0 : retry ? o1[0] : o0[0];
+    const bool use = Q.motion_try && !overflow && nm >= 20;
+    const int32_t* fm = B.mmatch + (retry ? (size_t)P.S * P.cap : 0) + o;
+    for (int i = threadIdx.x; i < B.n[s]; i += kT) {
+        const int q = use ? fm[i] : -1;
+        const int j = q >= 0 ? B.lf_fmp[o + q] : -1;
+        B.fmp[o + i] = j;
+        B.motm[o + i] = Q.motion_try ? j : -1;
+    }
+    __syncthreads();
+    pack_edges(B, s, Q.Tpred, use, scratch);
+    if (threadIdx.x == 0) {
+        Q.motion_n = nm;
+        if (overflow) Q.fail = 1;
+    }
+}
+
+// TrackWithMotionModel's end (outliers out, nmatchesMap >= 10, Tracking.cc:2736-2775); where it
+// was not tried or failed, TrackReferenceKeyFrame (Tracking.cc:2559-2616): SearchByBoW's matches
+// (< 15: lost) -> PoseOptimization input from mLastFrame.mTcw
+__global__ void __launch_bounds__(kT) k_ref_edges(Bufs B) {
+    __shared__ int scratch[20];
+    __shared__ int s_ok;
+    const int s = blockIdx.x;
+    const Params& P = B.P;
+    const size_t o = slot(P, s);
+    Seq& Q = B.seq[s];
+    const bool tried = Q.motion_try && Q.motion_n >= 20 && !Q.fail;
+    int kept = 0;
+    if (tried) kept = drop_outliers(B, s, scratch);  // the motion model's PoseOptimization
+    if (threadIdx.x == 0) {
+        s_ok = tried && kept >= 10;
+        if (s_ok)
+            for (int k = 0; k < 16; k++) Q.T1[k] = B.po[s].Tcw[k];
+    }
+    __syncthreads();
+    const bool motion_ok = s_ok;
+    const bool active = motion_ok || (Q.initialized && B.nbow[s] >= 15);  // Tracking.cc:2571-2575
+    if (!motion_ok)
+        for (int i = threadIdx.x; i < B.n[s]; i += kT) B.fmp[o + i] = active ? B.b2a[o + i] : -1;
+    __syncthreads();
+    pack_edges(B, s, Q.Tlast, active && !motion_ok, scratch);  // mCurrentFrame.SetPose(mLastFrame.mTcw)
+    if (threadIdx.x == 0) {
+        Q.active = active;
+        Q.mode = motion_ok;
+        Rec& R = B.rec[s];
+        R.n = B.n[s];
+        R.n_bow = Q.initialized && !motion_ok ? B.nbow[s] : 0;
+        R.n_motion = Q.motion_n;
+        R.motion = motion_ok;
+        R.n_inl_ref = motion_ok ? kept : 0;
+        R.n_local = R.n_inl = 0;
+        R.is_kf = 0;
+        R.lost = Q.initialized && !active;
+        R.initialized = Q.initialized;
+        R.status = 0;
+    }
+}
+
+// after the first PoseOptimization: outliers out (TrackReferenceKeyFrame, :2586-2616); the
+// SearchLocalPoints inputs (Tracking.cc:3179-3258): MapPoint records, grid, call records
+__global__ void __launch_bounds__(kT) k_local_setup(Bufs B) {
+    __shared__ int scratch[20];
+    const int s = blockIdx.x;
+    const Params& P = B.P;
+    const size_t o = slot(P, s);
+    Seq& Q = B.seq[s];
     bool active = Q.active;
-    const int kept = drop_outliers(B, s, scratch);
-    if (active && kept < 10) active = false;  // nmatchesMap >= 10 (:2616)
+    const bool motion = Q.mode == 1;  // the motion model's pose and inliers stand (k_ref_edges)
+    const int kept = drop_outliers(B, s, scratch);  // TrackReferenceKeyFrame's PoseOptimization
+    if (active && !motion && kept < 10) active = false;  // nmatchesMap >= 10 (:2616)
     const pose::POut& po = B.po[s];
-    if (threadIdx.x < 16) Q.T1[threadIdx.x] = active ? po.Tcw[threadIdx.x] : Q.Tcw[threadIdx.x];
+    if (threadIdx.x < 16 && !motion) Q.T1[threadIdx.x] = active ? po.Tcw[threadIdx.x] : Q.Tcw[threadIdx.x];
     const int kfn = active ? B.n[P.S + s] : 0;
     const MapPts& M = B.mp[Q.cur];
     // local MapPoint records: the reference KeyFrame's slots; "seen" = already in the frame
@@ -283,8 +485,8 @@ __global__ void __launch_bounds__(kT) k_local_setup(Bufs B) {
         const int j = B.fmp[o + i];
         B.fstate[o + i] = j >= 0 ? 1 : -1;
         if (j >= 0) B.geom[o + j].seen = 1;
+        if (!active) B.fmatch[o + i] = -1;  // no SearchLocalPoints this step (the launch covers F.n = 0)
     }
-    if (active) build_grid(B, s, keys);
     if (threadIdx.x == 0) {
         Q.active = active;
         B.rec[s].n_inl_ref = active ? kept : 0;
@@ -377,7 +579,10 @@ __global__ void __launch_bounds__(kT) k_local_edges(Bufs B) {
         }
     __syncthreads();
     pack_edges(B, s, Q.T1, active, scratch);
-    if (threadIdx.x == 0) B.rec[s].n_local = active ? B.pout[4 * s] : 0;
+    if (threadIdx.x == 0) {
+        B.rec[s].n_local = active ? B.pout[4 * s] : 0;
+        if (active && B.pout[4 * s + 1] == 1) Q.fail = 1;  // candidate overflow: matches incomplete
+    }
 }
 
 // Frame::UnprojectStereo (Frame.cc:1006-1022): mRwc * x3Dc + mOw as one cv::gemm with beta
@@ -508,6 +713,29 @@ __device__ void make_keyframe(const Bufs& B, int s, const float* T, bool initial
 
 // after the second PoseOptimization: TrackLocalMap's inliers (stereo outliers leave the frame),
 // the pose, NeedNewKeyFrame / CreateNewKeyFrame; uninitialised sequences try StereoInitialization
+// the current frame becomes mLastFrame (Tracking.cc:2140): its keypoints and MapPoints (after a
+// new KeyFrame, every valid slot of it: CreateNewKeyFrame gives the frame its new MapPoints,
+// Tracking.cc:3290-3300) and mlRelativeFramePoses' Tcr = Tcw * Tref^-1 (:2149)
+__device__ void set_last_frame(const Bufs& B, int s, bool new_kf) {
+    const Params& P = B.P;
+    const size_t o = slot(P, s), okf = slot(P, P.S + s);
+    Seq& Q = B.seq[s];
+    const int n = B.n[s];
+    for (int i = threadIdx.x; i < n; i += kT) {
+        B.lf_kps[o + i] = B.kps[o + i];
+        B.lf_fmp[o + i] = new_kf ? (B.valid[okf + i] ? i : -1) : B.fmp[o + i];
+    }
+    if (threadIdx.x == 0) {
+        float Twr[16];
+        pose_inverse(Q.Tref, Twr);  // KeyFrame::GetPoseInverse
+        gemm4(Q.Tcw, Twr, Q.Tlr);
+        Q.last_n = n;
+    }
+}
+
+// after the second PoseOptimization: TrackLocalMap's inliers (stereo outliers leave the frame),
+// the pose, the motion model, NeedNewKeyFrame / CreateNewKeyFrame, the last frame;
+// uninitialised sequences try StereoInitialization
 __global__ void __launch_bounds__(kT) k_finish(Bufs B) {
     __shared__ int scratch[20];
     __shared__ uint64_t keys[kMaxCap];
@@ -522,20 +750,33 @@ __global__ void __launch_bounds__(kT) k_finish(Bufs B) {
     int ns = 0;
     for (int i = threadIdx.x; i < n; i += kT) ns += B.depth[o + i] > 0;
     ns = block_reduce_sum(ns, scratch);
+    if (Q.fail) {  // a SearchByProjection candidate overflow left this step's matches incomplete:
+        // the step is void (status 1, reported lost) and the sequence keeps its previous state
+        if (threadIdx.x == 0) {
+            for (int k = 0; k < 16; k++) R.Tcw[k] = Q.Tcw[k];
+            R.status = 1;
+            R.lost = 1;
+            R.is_kf = 0;
+            R.n_stereo = ns;
+        }
+        return;
+    }
     if (!Q.initialized) {  // Tracking::StereoInitialization (Tracking.cc:2366-2429)
         const bool init = n > 500;
-        if (init) {
-            float I[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
-            make_keyframe(B, s, I, true, keys, scratch);
-        }
+        const float I[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+        if (init) make_keyframe(B, s, I, true, keys, scratch);
         if (threadIdx.x == 0) {
-            for (int k = 0; k < 16; k++) Q.Tcw[k] = (k % 5 == 0) ? 1.f : 0.f;
+            for (int k = 0; k < 16; k++) Q.Tcw[k] = Q.Tref[k] = I[k];
             Q.initialized = init;
+            Q.nkf = init;
+            Q.has_vel = 0;  // mLastFrame has no pose yet: mVelocity stays empty
             for (int k = 0; k < 16; k++) R.Tcw[k] = Q.Tcw[k];
             R.is_kf = init;
             R.initialized = init;
             R.n_stereo = ns;
         }
+        __syncthreads();
+        if (init) set_last_frame(B, s, true);
         return;
     }
     const bool active = Q.active;
@@ -560,17 +801,33 @@ __global__ void __launch_bounds__(kT) k_finish(Bufs B) {
     ntc = block_reduce_sum(ntc, scratch);
     if (threadIdx.x == 0) {
         const bool close = tc < 100 && ntc > 70;
-        s_need = ok && (((float)ninl < (float)Q.n_ref * 0.75f || close) && ninl > 15);
+        const float thRefRatio = Q.nkf < 2 ? 0.4f : 0.75f;  // KeyFramesInMap() < 2 (:2990-2992)
+        s_need = ok && (((float)ninl < (float)Q.n_ref * thRefRatio || close) && ninl > 15);
         for (int k = 0; k < 16; k++) R.Tcw[k] = Q.Tcw[k];
         R.n_inl = active ? ninl : 0;
         R.lost = !ok;
         R.n_stereo = ns;
+        // motion model (Tracking.cc:2058-2068): mVelocity = mTcw * LastTwc, LastTwc from
+        // mLastFrame's GetRotationInverse / GetCameraCenter; a lost frame drops it
+        if (ok) {
+            float Twl[16];
+            pose_inverse(Q.Tlast, Twl);
+            gemm4(Q.Tcw, Twl, Q.V);
+        }
+        Q.has_vel = ok;
     }
     __syncthreads();
-    if (s_need) {
+    const bool need = s_need;
+    if (need) {
         make_keyframe(B, s, Q.Tcw, false, keys, scratch);
-        if (threadIdx.x == 0) R.is_kf = 1;
+        if (threadIdx.x == 0) {
+            R.is_kf = 1;
+            Q.nkf++;
+            for (int k = 0; k < 16; k++) Q.Tref[k] = Q.Tcw[k];  // mpReferenceKF = pKF (:3075)
+        }
     }
+    __syncthreads();
+    if (ok) set_last_frame(B, s, need);
 }
 
 }  // namespace track
@@ -595,6 +852,7 @@ struct slam_tracker {
     slam_keypoint* d_kps_r = nullptr;
     uint8_t* d_desc_r = nullptr;
     int32_t *d_n_r = nullptr, *d_mono = nullptr, *d_a2b = nullptr, *d_b2a = nullptr, *d_nbow = nullptr;
+    int8_t* d_fclear = nullptr;
     float *d_ur = nullptr, *d_depth = nullptr;
     double* d_errs = nullptr;
     uint8_t *d_level = nullptr, *d_outl = nullptr;
@@ -697,6 +955,7 @@ slam_status slamhot_tracker_create(int device, const slam_tracker_config* cfg, s
     P.cap = cap;
     P.S = S;
     t->cand_cap = cap * 96;
+    if (const char* e = std::getenv("SLAMHOT_TRACK_CAND_CAP")) t->cand_cap = std::max(16, std::atoi(e));  // tests: force overflow
     Bufs& B = t->B;
     B.P = P;
     B.cand_cap = t->cand_cap;
@@ -714,8 +973,14 @@ slam_status slamhot_tracker_create(int device, const slam_tracker_config* cfg, s
         (st = alloc(t, &B.cand, (size_t)S * t->cand_cap)) || (st = alloc(t, &B.fmatch, SC)) ||
         (st = alloc(t, &B.pout, (size_t)S * 4)) || (st = alloc(t, &t->d_kps_r, SC)) ||
         (st = alloc(t, &t->d_desc_r, SC * 32)) || (st = alloc(t, &t->d_n_r, S)) || (st = alloc(t, &t->d_mono, S)) ||
-        (st = alloc(t, &t->d_rect_l, (size_t)S * W * H)) || (st = alloc(t, &t->d_rect_r, (size_t)S * W * H)))
+        (st = alloc(t, &t->d_rect_l, (size_t)S * W * H)) || (st = alloc(t, &t->d_rect_r, (size_t)S * W * H)) ||
+        (st = alloc(t, &B.lf_kps, SC)) || (st = alloc(t, &B.lf_fmp, SC)) || (st = alloc(t, &B.lf_has, SC)) ||
+        (st = alloc(t, &B.lf_zero, SC)) || (st = alloc(t, &B.lf_one, SC)) || (st = alloc(t, &B.lf_pos, SC * 3)) ||
+        (st = alloc(t, &B.lf_desc, SC * 32)) || (st = alloc(t, &t->d_fclear, SC)) || (st = alloc(t, &B.mcalls, 2 * (size_t)S)) ||
+        (st = alloc(t, &B.mmatch, 2 * SC)) || (st = alloc(t, &B.mout, 8 * (size_t)S)) || (st = alloc(t, &B.motm, SC)))
         return fail(st);
+    if (hipMemset(B.lf_one, 1, SC) != hipSuccess || hipMemset(t->d_fclear, 0xFF, SC) != hipSuccess) return fail(SLAM_EHIP);
+    B.fclear = t->d_fclear;
     for (int k = 0; k < 2; k++)
         if ((st = alloc(t, &B.mp[k].pos, SC)) || (st = alloc(t, &B.mp[k].normal, SC)) ||
             (st = alloc(t, &B.mp[k].dist, SC)) || (st = alloc(t, &B.mp[k].desc, SC * 32)))
@@ -770,11 +1035,20 @@ slam_status slamhot_tracker_step_device(slam_tracker* t, const void* d_left, int
         (st = slamhot_bow_match_batch_device(t->m, t->voc, 2 * S, B.kps, B.desc, cap, B.n, B.valid, S, t->pairs.data(),
                                              0.7f, 1, 0, 4, t->d_a2b, t->d_b2a, t->d_nbow, s)))
         return st;
+    // TrackWithMotionModel (sequences with a velocity), then TrackReferenceKeyFrame where it was
+    // not tried or failed; both run as launches over all sequences, the device picks per sequence
+    const size_t plds = projection_lds_bytes(cap, cap);
+    hipLaunchKernelGGL(k_motion_setup, dim3(S), dim3(kT), 0, s, B);
+    SLAM_HIP_TRY(launch_search_by_projection(B.mcalls, S, plds, s));
+    hipLaunchKernelGGL(k_motion_retry, dim3((S + 63) / 64), dim3(64), 0, s, B);
+    SLAM_HIP_TRY(launch_search_by_projection(B.mcalls + S, S, plds, s));
+    hipLaunchKernelGGL(k_motion_edges, dim3(S), dim3(kT), 0, s, B);
+    SLAM_HIP_TRY(pose::launch_pose_opt(B.pf, B.pe, t->d_errs, t->d_level, t->d_outl, t->d_po, S, s));
     hipLaunchKernelGGL(k_ref_edges, dim3(S), dim3(kT), 0, s, B);
     SLAM_HIP_TRY(pose::launch_pose_opt(B.pf, B.pe, t->d_errs, t->d_level, t->d_outl, t->d_po, S, s));
     hipLaunchKernelGGL(k_local_setup, dim3(S), dim3(kT), 0, s, B);
     SLAM_HIP_TRY(launch_is_in_frustum(B.fcalls, S, cap, s));
-    SLAM_HIP_TRY(launch_search_by_projection(B.pcalls, S, projection_lds_bytes(cap, cap), s));
+    SLAM_HIP_TRY(launch_search_by_projection(B.pcalls, S, plds, s));
     hipLaunchKernelGGL(k_local_edges, dim3(S), dim3(kT), 0, s, B);
     SLAM_HIP_TRY(pose::launch_pose_opt(B.pf, B.pe, t->d_errs, t->d_level, t->d_outl, t->d_po, S, s));
     hipLaunchKernelGGL(k_finish, dim3(S), dim3(kT), 0, s, B);
@@ -789,11 +1063,10 @@ slam_status slamhot_tracker_records(slam_tracker* t, slam_track_record* out) {
     SLAM_HIP_TRY(hipSetDevice(t->device));
     SLAM_HIP_TRY(hipMemcpyAsync(out, t->B.rec, sizeof(Rec) * t->S, hipMemcpyDeviceToHost, t->stream));
     SLAM_HIP_TRY(hipStreamSynchronize(t->stream));
-    // a SearchByProjection candidate overflow would have left a sequence's matches incomplete
-    std::vector<int32_t> po((size_t)t->S * 4);
-    SLAM_HIP_TRY(hipMemcpy(po.data(), t->B.pout, po.size() * 4, hipMemcpyDeviceToHost));
+    // a SearchByProjection candidate overflow voided a sequence's step on the device (status 1:
+    // its state was kept as before the step); report it
     for (int s = 0; s < t->S; s++)
-        if (po[4 * s + 1] == 1) return SLAM_ECAP;
+        if (out[s].status == 1) return SLAM_ECAP;
     return SLAM_OK;
 }
 
@@ -833,6 +1106,47 @@ slam_status slamhot_tracker_keyframe(slam_tracker* t, int seq, slam_track_keyfra
         kf->mp_min_dist[i] = d[i].x;
         kf->mp_max_dist[i] = d[i].y;
     }
+    return SLAM_OK;
+}
+
+slam_status slamhot_tracker_state(slam_tracker* t, int seq, slam_track_state* st) {
+    if (!t || !st || seq < 0 || seq >= t->S) return SLAM_EINVAL;
+    SLAM_HIP_TRY(hipSetDevice(t->device));
+    SLAM_HIP_TRY(hipStreamSynchronize(t->stream));
+    Seq q;
+    SLAM_HIP_TRY(hipMemcpy(&q, t->B.seq + seq, sizeof(Seq), hipMemcpyDeviceToHost));
+    std::memcpy(st->V, q.V, sizeof(st->V));
+    std::memcpy(st->Tlr, q.Tlr, sizeof(st->Tlr));
+    std::memcpy(st->Tref, q.Tref, sizeof(st->Tref));
+    st->has_vel = q.initialized && q.has_vel;
+    st->nkf = q.nkf;
+    st->last_n = q.initialized ? q.last_n : 0;
+    if (st->cap < st->last_n) return SLAM_ECAP;
+    const size_t o = (size_t)seq * t->cap;
+    if (st->last_n && st->last_kps)
+        SLAM_HIP_TRY(hipMemcpy(st->last_kps, t->B.lf_kps + o, sizeof(slam_keypoint) * st->last_n, hipMemcpyDeviceToHost));
+    if (st->last_n && st->last_mp)
+        SLAM_HIP_TRY(hipMemcpy(st->last_mp, t->B.lf_fmp + o, 4 * (size_t)st->last_n, hipMemcpyDeviceToHost));
+    return SLAM_OK;
+}
+
+slam_status slamhot_tracker_frame(slam_tracker* t, int seq, slam_track_frame* fr) {
+    if (!t || !fr || seq < 0 || seq >= t->S) return SLAM_EINVAL;
+    SLAM_HIP_TRY(hipSetDevice(t->device));
+    SLAM_HIP_TRY(hipStreamSynchronize(t->stream));
+    int32_t n = 0;
+    SLAM_HIP_TRY(hipMemcpy(&n, t->B.n + seq, 4, hipMemcpyDeviceToHost));
+    fr->n = n;
+    if (fr->cap < n) return SLAM_ECAP;
+    const size_t o = (size_t)seq * t->cap;
+    auto get = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
+        return dst && bytes ? hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) : hipSuccess;
+    };
+    SLAM_HIP_TRY(get(fr->uright, t->d_ur + o, 4 * (size_t)n));
+    SLAM_HIP_TRY(get(fr->bow_match, t->d_b2a + o, 4 * (size_t)n));
+    SLAM_HIP_TRY(get(fr->motion_match, t->B.motm + o, 4 * (size_t)n));
+    SLAM_HIP_TRY(get(fr->local_match, t->B.fmatch + o, 4 * (size_t)n));
+    SLAM_HIP_TRY(get(fr->mappoints, t->B.fmp + o, 4 * (size_t)n));
     return SLAM_OK;
 }
 

@@ -478,6 +478,33 @@ def _matcher_methods():
                                                     C.byref(nm)), "search_by_projection_kf")
         return nm.value, fm
 
+    def _proj_batch(self, fn_name, frame_views, others, other_cls, *args):
+        L = lib()
+        fn = getattr(L, fn_name)
+        if not getattr(fn, "_ready", False):
+            fn.argtypes = [P, I, P, P, C.c_float, I, C.c_float, I, P, P]
+            fn._ready = True
+        nf = len(frame_views)
+        fv = (FrameView * nf)(*frame_views)
+        ov = (other_cls * nf)(*others)
+        fms = [np.full(v.n, -1, np.int32) for v in frame_views]
+        pf = (P * nf)(*[f.ctypes.data for f in fms])
+        nm = np.zeros(nf, np.int32)
+        check(fn(self._h, nf, fv, ov, self.mfNNratio, int(self.mbCheckOrientation), *args, pf, _ptr(nm)), fn_name)
+        return [(int(nm[i]), fms[i]) for i in range(nf)]
+
+    def SearchByProjection_last_batch(self, frame_views, last_views, th, bMono):
+        """Batched SearchByProjection(Frame&, const Frame& LastFrame, th, bMono)
+        (slamhot_search_by_projection_last_batch): [(nmatches, f_match)] per frame."""
+        return self._proj_batch("slamhot_search_by_projection_last_batch", frame_views, last_views, LastFrameView,
+                                float(th), int(bMono))
+
+    def SearchByProjection_kf_batch(self, frame_views, kf_views, th, ORBdist):
+        """Batched SearchByProjection(Frame&, KeyFrame*, set, th, ORBdist)
+        (slamhot_search_by_projection_kf_batch): [(nmatches, f_match)] per frame."""
+        return self._proj_batch("slamhot_search_by_projection_kf_batch", frame_views, kf_views, KFPointsView,
+                                float(th), int(ORBdist))
+
     def bow_match_batch_device(self, vocab, nframes, d_kps, d_desc, cap, d_n, pairs, d_a2b, d_b2a, d_nmatches,
                                d_valid=None, levelsup=4, strict=False, stream=None):
         """Device-resident Frame::ComputeBoW + SearchByBoW over (keyframe, frame) index pairs
@@ -507,6 +534,9 @@ def _matcher_methods():
     ORBmatcher.SearchLocalPoints_batch = SearchLocalPoints_batch
     ORBmatcher.SearchByProjection_last = SearchByProjection_last
     ORBmatcher.SearchByProjection_kf = SearchByProjection_kf
+    ORBmatcher._proj_batch = _proj_batch
+    ORBmatcher.SearchByProjection_last_batch = SearchByProjection_last_batch
+    ORBmatcher.SearchByProjection_kf_batch = SearchByProjection_kf_batch
 
 
 _matcher_methods()
@@ -1060,7 +1090,19 @@ class TrackerConfig(C.Structure):
 class TrackRecord(C.Structure):
     _fields_ = [("Tcw", C.c_float * 16), ("n", C.c_int32), ("n_stereo", C.c_int32), ("n_bow", C.c_int32),
                 ("n_inl_ref", C.c_int32), ("n_local", C.c_int32), ("n_inl", C.c_int32), ("is_keyframe", C.c_int32),
-                ("lost", C.c_int32), ("initialized", C.c_int32), ("pad", C.c_int32 * 3)]
+                ("lost", C.c_int32), ("initialized", C.c_int32), ("n_motion", C.c_int32), ("motion", C.c_int32),
+                ("status", C.c_int32)]
+
+
+class TrackState(C.Structure):
+    _fields_ = [("V", C.c_float * 16), ("Tlr", C.c_float * 16), ("Tref", C.c_float * 16), ("has_vel", C.c_int32),
+                ("nkf", C.c_int32), ("last_n", C.c_int32), ("cap", C.c_int32), ("last_kps", C.c_void_p),
+                ("last_mp", C.c_void_p)]
+
+
+class TrackFrame(C.Structure):
+    _fields_ = [("n", C.c_int32), ("cap", C.c_int32), ("uright", C.c_void_p), ("bow_match", C.c_void_p),
+                ("motion_match", C.c_void_p), ("local_match", C.c_void_p), ("mappoints", C.c_void_p)]
 
 
 class TrackKeyFrame(C.Structure):
@@ -1083,6 +1125,8 @@ class Tracker:
             L.slamhot_tracker_step_device.argtypes = [P, P, I, C.c_int64, P, I, C.c_int64]
             L.slamhot_tracker_records.argtypes = [P, P]
             L.slamhot_tracker_keyframe.argtypes = [P, I, C.POINTER(TrackKeyFrame)]
+            L.slamhot_tracker_state.argtypes = [P, I, C.POINTER(TrackState)]
+            L.slamhot_tracker_frame.argtypes = [P, I, C.POINTER(TrackFrame)]
             L._track_ready = True
         self.nseq, self.W, self.H, self.cap = nseq, width, height, 2 * nfeatures + 64
         self._maps = None
@@ -1117,7 +1161,41 @@ class Tracker:
         check(lib().slamhot_tracker_records(self._h, recs), "tracker_records")
         return [dict(Tcw=np.array(r.Tcw[:], np.float32).reshape(4, 4), n=r.n, n_stereo=r.n_stereo, n_bow=r.n_bow,
                      n_inl_ref=r.n_inl_ref, n_local=r.n_local, n_inl=r.n_inl, is_keyframe=r.is_keyframe,
-                     lost=r.lost, initialized=r.initialized) for r in recs]
+                     lost=r.lost, initialized=r.initialized, n_motion=r.n_motion, motion=r.motion,
+                     status=r.status) for r in recs]
+
+    def records_status(self):
+        """(slam_status of slamhot_tracker_records, records) without raising on SLAM_ECAP."""
+        recs = (TrackRecord * self.nseq)()
+        st = lib().slamhot_tracker_records(self._h, recs)
+        return st, [dict(status=r.status, lost=r.lost, is_keyframe=r.is_keyframe,
+                         Tcw=np.array(r.Tcw[:], np.float32).reshape(4, 4)) for r in recs]
+
+    def state(self, seq: int):
+        """The motion-model state and last frame of sequence seq (slamhot_tracker_state)."""
+        cap = self.cap
+        kps, mp = np.zeros(cap, KP_DTYPE), np.zeros(cap, np.int32)
+        st = TrackState()
+        st.cap, st.last_kps, st.last_mp = cap, kps.ctypes.data, mp.ctypes.data
+        check(lib().slamhot_tracker_state(self._h, seq, C.byref(st)), "tracker_state")
+        n = st.last_n
+        return dict(V=np.array(st.V[:], np.float32).reshape(4, 4), Tlr=np.array(st.Tlr[:], np.float32).reshape(4, 4),
+                    Tref=np.array(st.Tref[:], np.float32).reshape(4, 4), has_vel=st.has_vel, nkf=st.nkf,
+                    last_kps=kps[:n].copy(), last_mp=mp[:n].copy())
+
+    def frame(self, seq: int):
+        """The last step's per-feature arrays of sequence seq (slamhot_tracker_frame): uright,
+        bow_match, motion_match, local_match, mappoints."""
+        cap = self.cap
+        out = dict(uright=np.zeros(cap, np.float32), bow_match=np.zeros(cap, np.int32),
+                   motion_match=np.zeros(cap, np.int32), local_match=np.zeros(cap, np.int32),
+                   mappoints=np.zeros(cap, np.int32))
+        fr = TrackFrame()
+        fr.cap = cap
+        for k, a in out.items():
+            setattr(fr, k, a.ctypes.data)
+        check(lib().slamhot_tracker_frame(self._h, seq, C.byref(fr)), "tracker_frame")
+        return {k: v[:fr.n].copy() for k, v in out.items()}
 
     def keyframe(self, seq: int):
         cap = self.cap

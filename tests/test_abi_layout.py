@@ -16,7 +16,8 @@ PAIRS = {"OrbParams": "slam_orb_params", "BowSide": "slam_bow_side", "FrameView"
          "LbaProblem": "slam_lba_problem", "LbaOptions": "slam_lba_options", "LbaResult": "slam_lba_result",
          "PoseFrame": "slam_pose_frame", "PoseResult": "slam_pose_result", "TriKF": "slam_tri_kf",
          "TriPair": "slam_tri_pair", "TrackerConfig": "slam_tracker_config", "TrackRecord": "slam_track_record",
-         "TrackKeyFrame": "slam_track_keyframe"}
+         "TrackKeyFrame": "slam_track_keyframe", "TrackState": "slam_track_state",
+         "TrackFrame": "slam_track_frame"}
 
 
 @pytest.fixture(scope="module")

@@ -118,3 +118,67 @@ def test_search_local_points_batch():
         no, fo = ob.search_by_projection_local(views[i], tro, descs[i], 0.8, 1.0, False, 20.0)
         assert nt == nto and nm == no and np.array_equal(fm, fo), i
     m.close()
+
+
+def test_search_by_projection_last_batch():
+    """slamhot_search_by_projection_last_batch (TrackWithMotionModel's matcher over many frames in
+    one launch) equals the single calls and the oracle, at th 7 and its 2th retry, mono and stereo,
+    with and without the rotation check."""
+    import slamhot
+    views, lfs, keeps = [], [], []
+    for seed in range(40, 52):
+        S = scenes.scene(seed)
+        fv, keep = scenes.frame_view(S)
+        lf, lkeep = scenes.last_frame(S, mono=False, motion=(0.02, 0.2, 0.6)[seed % 3])
+        views.append(fv)
+        lfs.append(lf)
+        keeps.append((S, keep, lkeep))
+    for th, mono, ori in [(7.0, False, True), (14.0, False, True), (15.0, True, False)]:
+        m = slamhot.ORBmatcher(0.9, ori)
+        out = m.SearchByProjection_last_batch(views, lfs, th, mono)
+        assert len(out) == len(views)
+        for i, (nm, fm) in enumerate(out):
+            ns, fs = m.SearchByProjection_last(views[i], lfs[i], th, mono)
+            no, fo = ob.search_by_projection_last(views[i], lfs[i], 0.9, ori, th, mono)
+            assert nm == ns == no and np.array_equal(fm, fs) and np.array_equal(fm, fo), (th, mono, ori, i)
+        assert sum(nm for nm, _ in out) > 20 * len(out)
+        m.close()
+
+
+def test_search_by_projection_kf_batch():
+    """slamhot_search_by_projection_kf_batch (Relocalization's projection matcher, batched) equals
+    the single calls and the oracle at both of the reference's (th, ORBdist) settings."""
+    import slamhot
+    views, kfs, keeps = [], [], []
+    for seed in range(60, 70):
+        S = scenes.scene(seed)
+        fv, keep = scenes.frame_view(S)
+        kf, kkeep = scenes.kf_points(S)
+        views.append(fv)
+        kfs.append(kf)
+        keeps.append((S, keep, kkeep))
+    m = slamhot.ORBmatcher(0.75, True)
+    for th, orb_dist in [(10.0, 100), (3.0, 64)]:  # Tracking.cc:3538, :3563
+        out = m.SearchByProjection_kf_batch(views, kfs, th, orb_dist)
+        for i, (nm, fm) in enumerate(out):
+            ns, fs = m.SearchByProjection_kf(views[i], kfs[i], th, orb_dist)
+            no, fo = ob.search_by_projection_kf(views[i], kfs[i], 0.75, True, th, orb_dist)
+            assert nm == ns == no and np.array_equal(fm, fs) and np.array_equal(fm, fo), (th, orb_dist, i)
+    m.close()
+
+
+def test_projection_batches_empty_and_degenerate():
+    """Empty batch, a frame with no last-frame MapPoints and a KeyFrame with nothing usable."""
+    import slamhot
+    m = slamhot.ORBmatcher(0.9, True)
+    assert m.SearchByProjection_last_batch([], [], 7.0, False) == []
+    S = scenes.scene(80)
+    fv, keep = scenes.frame_view(S)
+    lf, lkeep = scenes.last_frame(S)
+    lkeep[3][:] = 0  # has_mp: no MapPoints at all
+    kf, kkeep = scenes.kf_points(S)
+    kkeep[1][:] = 0  # use
+    (n1, f1), = m.SearchByProjection_last_batch([fv], [lf], 7.0, False)
+    (n2, f2), = m.SearchByProjection_kf_batch([fv], [kf], 10.0, 100)
+    assert n1 == 0 and n2 == 0 and (f1 == -1).all() and (f2 == -1).all()
+    m.close()
