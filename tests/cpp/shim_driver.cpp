@@ -6,11 +6,14 @@
 //   shim_driver lba MAP OUT       the whole LocalBundleAdjustment shim on the device -> counts,
 //                                 KeyFrame poses, MapPoint positions, surviving observations
 //   shim_driver pose FRAME OUT    the PoseOptimization shim on one Frame
+//   shim_driver lbatime MAP OUT [N]  wall-clock per call of the LocalBundleAdjustment shim (N calls,
+//                                 each on a freshly loaded map)
 //   shim_driver bow PAIR OUT      ORB_SLAM3::ORBmatcher(nnratio, checkOri).SearchByBoW(pKF, F, ...)
 //                                 through the reference-side binding of INTEGRATION.md, once per
 //                                 (nnratio, checkOri) listed in PAIR, all on this one thread
 //
 // MAP / FRAME are little-endian binaries written by tests/shim_io.py.
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
@@ -207,6 +210,34 @@ int run_lba(const char* in, const char* out) {
     return 0;
 }
 
+// wall-clock of the drop-in call: the LocalBundleAdjustment shim (window build, flatten, plan,
+// upload, device solve, download, vToErase, write-back) on a freshly loaded map, `reps` times
+int run_lba_time(const char* in, const char* out, int reps) {
+    slamhot::LocalBundleAdjuster solver(0);
+    std::vector<double> ms;
+    int nf = 0, no = 0, nm = 0, ne = 0;
+    for (int r = 0; r < reps; r++) {
+        World W;
+        load_map(in, W);
+        bool stop = false;
+        const auto t0 = std::chrono::steady_clock::now();
+        slamhot::orbslam3::LocalBundleAdjustment<KeyFrame, MapPoint, Map>(solver, &W.kfs[W.cur], &stop, &W.map, nf, no,
+                                                                           nm, ne);
+        ms.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    }
+    double dev = 0, plan = 0;
+    int syncs = 0;
+    slamhot::check(slamhot_lba_last_stats(solver.handle(), &dev, &plan, &syncs), "lba_last_stats");
+    Writer O(out);
+    O.put<int32_t>(nf);
+    O.put<int32_t>(no);
+    O.put<int32_t>(nm);
+    O.put<int32_t>(ne);
+    O.put(ms);
+    O.put(std::vector<double>{dev, plan, (double)syncs});
+    return 0;
+}
+
 int run_pose(const char* in, const char* out) {
     Reader R(in);
     Frame F;
@@ -361,6 +392,7 @@ int main(int argc, char** argv) {
         if (mode == "lba") return run_lba(argv[2], argv[3]);
         if (mode == "pose") return run_pose(argv[2], argv[3]);
         if (mode == "bow") return run_bow(argv[2], argv[3]);
+        if (mode == "lbatime") return run_lba_time(argv[2], argv[3], argc > 4 ? std::atoi(argv[4]) : 5);
     } catch (const slamhot::Error& e) {
         std::fprintf(stderr, "slamhot error: %s\n", e.what());
         return 3;
