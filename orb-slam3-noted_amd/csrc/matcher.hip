@@ -63,12 +63,16 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
                min((uint32_t)__builtin_amdgcn_readlane((int)x, 32), (uint32_t)__builtin_amdgcn_readlane((int)x, 48)));
 }
 
+// n_per_frame (optional): the descriptors are frames of `cap` slots and only the first
+// n_per_frame[f] slots of frame f hold features; the empty slots' groups exit at once
 __global__ void __launch_bounds__(256) k_vocab_transform(DevVocab V, int n, const uint8_t* desc,
                                                          int desc_stride, int levelsup,
                                                          int32_t* word_id, double* weight,
-                                                         int32_t* node_id) {
+                                                         int32_t* node_id, const int32_t* __restrict__ n_per_frame,
+                                                         int cap) {
     const int g = (blockIdx.x * blockDim.x + threadIdx.x) >> 4;  // feature
     const int j = threadIdx.x & 15;                                // child slot
+    if (n_per_frame && g < n && (g % cap) >= n_per_frame[g / cap]) return;  // whole 16-lane group
     const bool live = g < n;
     const int gi = live ? g : 0;
     const uint4* f = reinterpret_cast<const uint4*>(desc + (size_t)gi * desc_stride);
@@ -126,6 +130,10 @@ struct DevBowPair {
 };
 
 constexpr int kBowCap = 8192;        // features per side held in LDS
+#ifndef SLAMHOT_BOW_THREADS
+#define SLAMHOT_BOW_THREADS 1024
+#endif
+constexpr int kBowThreads = SLAMHOT_BOW_THREADS;  // 16 waves per pair: a wave per common node in turn
 constexpr int kBowNodeChunks = 4;    // B candidates per node held in registers: 4 x 64
 
 __device__ __forceinline__ int rot_bin(float a, float b) {
@@ -165,7 +173,7 @@ __device__ inline void three_maxima(const int* hist, int* keep) {
     keep[2] = ind3;
 }
 
-__global__ void __launch_bounds__(512) k_bow_match(const DevBowPair* pairs, float nnratio,
+__global__ void __launch_bounds__(kBowThreads) k_bow_match(const DevBowPair* pairs, float nnratio,
                                                    int check_ori, int strict) {
     __shared__ int16_t matchA[kBowCap];   // B index matched by A feature, -1 none
     __shared__ int8_t binA[kBowCap];
@@ -225,11 +233,27 @@ __global__ void __launch_bounds__(512) k_bow_match(const DevBowPair* pairs, floa
                 bd1[k] = d[1];
             }
         }
-        for (int pa = a0; pa < a1; pa++) {
-            const int idxA = (int)A.node_feat[pa];
-            if (A.valid && !A.valid[idxA]) continue;
-            const uint4* da = reinterpret_cast<const uint4*>(A.desc + (size_t)idxA * 32);
-            const uint4 q0 = da[0], q1 = da[1];
+        // the node's A features, 64 at a time, loaded lane-distributed (index, validity and
+        // descriptor in parallel) and taken in node order by v_readlane: the sequential greedy
+        // loop then waits on no memory
+        for (int pc = a0; pc < a1; pc += 64) {
+          const int cnt = min(64, a1 - pc);
+          int my_idx = 0, my_ok = 0;
+          uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
+          if (lane < cnt) {
+              my_idx = (int)A.node_feat[pc + lane];
+              my_ok = !A.valid || A.valid[my_idx];
+              const uint4* dm = reinterpret_cast<const uint4*>(A.desc + (size_t)my_idx * 32);
+              m0 = dm[0];
+              m1 = dm[1];
+          }
+          for (int t = 0; t < cnt; t++) {
+            if (!__builtin_amdgcn_readlane(my_ok, t)) continue;
+            const int idxA = __builtin_amdgcn_readlane(my_idx, t);
+            const uint4 q0 = make_uint4(__builtin_amdgcn_readlane(m0.x, t), __builtin_amdgcn_readlane(m0.y, t),
+                                        __builtin_amdgcn_readlane(m0.z, t), __builtin_amdgcn_readlane(m0.w, t));
+            const uint4 q1 = make_uint4(__builtin_amdgcn_readlane(m1.x, t), __builtin_amdgcn_readlane(m1.y, t),
+                                        __builtin_amdgcn_readlane(m1.z, t), __builtin_amdgcn_readlane(m1.w, t));
             int dist[kBowNodeChunks];
             uint32_t bestkey = 0xFFFFFFFFu;
 #pragma unroll
@@ -260,6 +284,7 @@ __global__ void __launch_bounds__(512) k_bow_match(const DevBowPair* pairs, floa
                     }
                 }
             }
+          }
         }
     }
     __syncthreads();
@@ -483,17 +508,20 @@ __global__ void __launch_bounds__(1024) k_featvec(int cap, const int32_t* __rest
     }
 }
 
-// Pair table for k_bow_match from per-frame counts (device side).  Pairs its tiles cannot
-// hold (side > kBowCap features, > 4096 nodes, or a Frame node over 4 x 64 candidates) go to
-// k_bow_match_any instead and are counted in *status.
-__global__ void k_make_pairs(int npairs, const int2* __restrict__ pairs, int cap, const uint8_t* __restrict__ kps,
-                             const uint8_t* __restrict__ desc, const int32_t* __restrict__ n_per_frame,
-                             const uint8_t* __restrict__ valid, const uint32_t* __restrict__ fv_id,
-                             const int32_t* __restrict__ fv_off, const uint32_t* __restrict__ fv_feat,
-                             const int32_t* __restrict__ fv_n, int32_t* __restrict__ a2b, int32_t* __restrict__ b2a,
-                             int32_t* __restrict__ nmatch, DevBowPair* __restrict__ out, int* __restrict__ status,
-                             uint8_t* __restrict__ scratch) {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+// Pair table for k_bow_match from per-frame counts (device side), a wave per pair (lanes scan
+// the Frame's nodes for the largest).  Pairs its tiles cannot hold (side > kBowCap features,
+// > 4096 nodes, or a Frame node over 4 x 64 candidates) go to k_bow_match_any instead and are
+// counted in *status.
+__global__ void __launch_bounds__(64) k_make_pairs(int npairs, const int2* __restrict__ pairs, int cap,
+                                                   const uint8_t* __restrict__ kps, const uint8_t* __restrict__ desc,
+                                                   const int32_t* __restrict__ n_per_frame,
+                                                   const uint8_t* __restrict__ valid, const uint32_t* __restrict__ fv_id,
+                                                   const int32_t* __restrict__ fv_off,
+                                                   const uint32_t* __restrict__ fv_feat, const int32_t* __restrict__ fv_n,
+                                                   int32_t* __restrict__ a2b, int32_t* __restrict__ b2a,
+                                                   int32_t* __restrict__ nmatch, DevBowPair* __restrict__ out,
+                                                   int* __restrict__ status, uint8_t* __restrict__ scratch) {
+    const int p = blockIdx.x, lane = threadIdx.x;
     if (p >= npairs) return;
     const int2 ab = pairs[p];
     auto side = [&](int f, bool use_valid) {
@@ -512,14 +540,16 @@ __global__ void k_make_pairs(int npairs, const int2* __restrict__ pairs, int cap
     DevBowPair pr;
     pr.A = side(ab.x, true);
     pr.B = side(ab.y, false);
+    int big = 0;
+    for (int i = lane; i < pr.B.n_nodes; i += 64) big |= pr.B.node_off[i + 1] - pr.B.node_off[i] > 64 * kBowNodeChunks;
+    big = __any(big);
+    if (lane != 0) return;
     pr.a2b = a2b + (size_t)p * cap;
     pr.b2a = b2a + (size_t)p * cap;
     pr.nmatches = nmatch + p;
     pr.bins = reinterpret_cast<int8_t*>(scratch + (size_t)p * 2 * cap);
     pr.taken = scratch + (size_t)p * 2 * cap + cap;
-    bool ok = pr.A.n <= kBowCap && pr.B.n <= kBowCap && pr.A.n_nodes <= 4096 && pr.B.n_nodes <= 4096;
-    for (int i = 0; ok && i < pr.B.n_nodes; i++)
-        if (pr.B.node_off[i + 1] - pr.B.node_off[i] > 64 * kBowNodeChunks) ok = false;
+    const bool ok = pr.A.n <= kBowCap && pr.B.n <= kBowCap && pr.A.n_nodes <= 4096 && pr.B.n_nodes <= 4096 && !big;
     pr.general = !ok;
     if (!ok) atomicAdd(status, 1);
     out[p] = pr;
@@ -715,10 +745,24 @@ slam_status slamhot_vocab_transform_device(slam_vocab* v, int n, const void* d_d
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : v->stream;
     const int blocks = (int)(((size_t)n * 16 + 255) / 256);
     hipLaunchKernelGGL(k_vocab_transform, dim3(blocks), dim3(256), 0, s, v->dev(), n, (const uint8_t*)d_desc,
-                       desc_stride, levelsup, (int32_t*)d_word_id, (double*)d_weight, (int32_t*)d_node_id);
+                       desc_stride, levelsup, (int32_t*)d_word_id, (double*)d_weight, (int32_t*)d_node_id,
+                       (const int32_t*)nullptr, 1);
     SLAM_HIP_TRY(hipGetLastError());
     return SLAM_OK;
 }
+
+namespace {
+// the batched path's transform: nframes x cap slots, only each frame's first n slots
+slam_status vocab_transform_frames(slam_vocab* v, int nframes, int cap, const void* d_desc, const int32_t* d_n,
+                                   int levelsup, void* d_word_id, void* d_weight, void* d_node_id, hipStream_t s) {
+    const size_t n = (size_t)nframes * cap;
+    const int blocks = (int)((n * 16 + 255) / 256);
+    hipLaunchKernelGGL(k_vocab_transform, dim3(blocks), dim3(256), 0, s, v->dev(), (int)n, (const uint8_t*)d_desc, 32,
+                       levelsup, (int32_t*)d_word_id, (double*)d_weight, (int32_t*)d_node_id, d_n, cap);
+    SLAM_HIP_TRY(hipGetLastError());
+    return SLAM_OK;
+}
+}  // namespace
 
 slam_status slamhot_vocab_transform(slam_vocab* v, int n, const uint8_t* desc, int levelsup,
                                     int32_t* word_id, double* weight, int32_t* node_id) {
@@ -858,7 +902,7 @@ extern "C" slam_status slamhot_search_by_bow(slam_matcher* m, const slam_bow_sid
     }
     SLAM_HIP_TRY(hipMemcpyAsync(m->d_pair.p, &pr, sizeof(pr), hipMemcpyHostToDevice, m->stream));
     if (fits)
-        hipLaunchKernelGGL(k_bow_match, dim3(1), dim3(512), 0, m->stream, m->d_pair.as<DevBowPair>(), nnratio,
+        hipLaunchKernelGGL(k_bow_match, dim3(1), dim3(kBowThreads), 0, m->stream, m->d_pair.as<DevBowPair>(), nnratio,
                            check_ori, strict);
     else
         hipLaunchKernelGGL(k_bow_match_any, dim3(1), dim3(512), 0, m->stream, m->d_pair.as<DevBowPair>(), nnratio,
@@ -896,8 +940,8 @@ extern "C" slam_status slamhot_bow_match_batch_device(slam_matcher* m, slam_voca
         return st;
     if (nframes == 0) return SLAM_OK;
     // Frame::ComputeBoW (Frame.cc:721-728): transform every descriptor slot of every frame
-    if ((st = slamhot_vocab_transform_device(v, (int)nf, d_desc, 32, levelsup, m->b_word.p, m->b_weight.p,
-                                             m->b_node.p, s)))
+    if ((st = vocab_transform_frames(v, nframes, cap, d_desc, (const int32_t*)d_n, levelsup, m->b_word.p,
+                                     m->b_weight.p, m->b_node.p, s)))
         return st;
     hipLaunchKernelGGL(k_featvec, dim3(nframes), dim3(1024), 0, s, cap, (const int32_t*)d_n,
                        m->b_node.as<int32_t>(), m->b_weight.as<double>(), m->b_fv_id.as<uint32_t>(),
@@ -906,12 +950,12 @@ extern "C" slam_status slamhot_bow_match_batch_device(slam_matcher* m, slam_voca
     if (npairs == 0) return SLAM_OK;
     SLAM_HIP_TRY(hipMemcpyAsync(m->b_pairs.p, pairs, (size_t)npairs * 8, hipMemcpyHostToDevice, s));
     SLAM_HIP_TRY(hipMemsetAsync(m->b_status.p, 0, 4, s));
-    hipLaunchKernelGGL(k_make_pairs, dim3((npairs + 127) / 128), dim3(128), 0, s, npairs, m->b_pairs.as<int2>(), cap,
+    hipLaunchKernelGGL(k_make_pairs, dim3(npairs), dim3(64), 0, s, npairs, m->b_pairs.as<int2>(), cap,
                        (const uint8_t*)d_kps, (const uint8_t*)d_desc, (const int32_t*)d_n, (const uint8_t*)d_valid,
                        m->b_fv_id.as<uint32_t>(), m->b_fv_off.as<int32_t>(), m->b_fv_feat.as<uint32_t>(),
                        m->b_fv_n.as<int32_t>(), (int32_t*)d_a2b, (int32_t*)d_b2a, (int32_t*)d_nmatches,
                        m->b_devpairs.as<DevBowPair>(), m->b_status.as<int>(), m->b_scratch.as<uint8_t>());
-    hipLaunchKernelGGL(k_bow_match, dim3(npairs), dim3(512), 0, s, m->b_devpairs.as<DevBowPair>(), nnratio,
+    hipLaunchKernelGGL(k_bow_match, dim3(npairs), dim3(kBowThreads), 0, s, m->b_devpairs.as<DevBowPair>(), nnratio,
                        check_ori, strict);
     hipLaunchKernelGGL(k_bow_match_any, dim3(npairs), dim3(512), 0, s, m->b_devpairs.as<DevBowPair>(), nnratio,
                        check_ori, strict);
