@@ -119,19 +119,38 @@ __global__ void __launch_bounds__(kMatchThreads) k_stereo_match(StereoGeom G, co
             const uint8_t* DR = desc_r + (size_t)f * G.cap * 32;
             const uint16_t* E = ent + (size_t)f * G.ent_cap;
             const int c0 = off[row], c1 = off[row + 1];
-            for (int c = c0; c < c1; c++) {
-                const int iR = E[c];
-                const int oct = KR[iR].octave;
-                if (oct < levelL - 1 || oct > levelL + 1) continue;
-                const float uR = KR[iR].x;
-                if (uR >= minU && uR <= maxU) {
-                    const uint4* dr = reinterpret_cast<const uint4*>(DR + (size_t)iR * 32);
-                    const int d = ham32(a0, a1, dr[0], dr[1]);
-                    if (d < bestDist || (d == bestDist && d < 100 && iR < bestIdxR)) {
-                        bestDist = d;
-                        bestIdxR = iR;
+            // candidates four at a time: their indices, then keypoints, then descriptors are
+            // loaded together (three dependent rounds per four candidates instead of per one)
+            for (int c = c0; c < c1; c += 4) {
+                int iR[4];
+                bool ok[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) iR[q] = c + q < c1 ? (int)E[c + q] : -1;
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    ok[q] = false;
+                    if (iR[q] >= 0) {
+                        const slam_keypoint k = KR[iR[q]];
+                        ok[q] = !(k.octave < levelL - 1 || k.octave > levelL + 1) && k.x >= minU && k.x <= maxU;
                     }
                 }
+                uint4 d0[4], d1[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    if (ok[q]) {
+                        const uint4* dr = reinterpret_cast<const uint4*>(DR + (size_t)iR[q] * 32);
+                        d0[q] = dr[0];
+                        d1[q] = dr[1];
+                    }
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    if (ok[q]) {
+                        const int d = ham32(a0, a1, d0[q], d1[q]);
+                        if (d < bestDist || (d == bestDist && d < 100 && iR[q] < bestIdxR)) {
+                            bestDist = d;
+                            bestIdxR = iR[q];
+                        }
+                    }
             }
         }
         if (bestDist < 75) {  // thOrbDist = (TH_HIGH + TH_LOW) / 2
@@ -154,16 +173,52 @@ __global__ void __launch_bounds__(kMatchThreads) k_stereo_match(StereoGeom G, co
                 int acc[2 * L + 1];
 #pragma unroll
                 for (int k = 0; k < 2 * L + 1; k++) acc[k] = 0;
-                for (int yy = 0; yy < 2 * w + 1; yy++) {
-                    uint8_t a[2 * w + 1], b[2 * w + 2 * L + 1];
+                // packed form: each row's 11 left and 21 right bytes as aligned dword loads, the
+                // eleven window offsets by v_alignbyte, the 11-byte row sums by three v_sad_u8
+                // (the 12th byte zeroed on both sides); used when the dword reads stay inside
+                // the rows (3 bytes of slack before the pitch), else the byte form
+                const bool packed = ux0 + 2 * w + 4 <= pl && ur0 + L + w + 4 <= pr;
+                if (packed) {
+                    for (int yy = 0; yy < 2 * w + 1; yy++) {
+                        const uint8_t* ra = PL + (size_t)yy * pl;
+                        const uint8_t* rb = PR + (size_t)yy * pr;
+                        const uint32_t* da = reinterpret_cast<const uint32_t*>((uintptr_t)ra & ~(uintptr_t)3);
+                        const uint32_t* db = reinterpret_cast<const uint32_t*>((uintptr_t)rb & ~(uintptr_t)3);
+                        const int sa = (int)((uintptr_t)ra & 3), sb = (int)((uintptr_t)rb & 3);
+                        uint32_t wa[4], wb[7];
 #pragma unroll
-                    for (int x = 0; x < 2 * w + 1; x++) a[x] = PL[(size_t)yy * pl + x];
+                        for (int q = 0; q < 4; q++) wa[q] = q * 4 < sa + 2 * w + 1 ? da[q] : 0u;
 #pragma unroll
-                    for (int x = 0; x < 2 * w + 2 * L + 1; x++) b[x] = PR[(size_t)yy * pr + x];
+                        for (int q = 0; q < 7; q++) wb[q] = q * 4 < sb + 2 * w + 2 * L + 1 ? db[q] : 0u;
+                        const uint32_t A0 = __builtin_amdgcn_alignbyte(wa[1], wa[0], sa);
+                        const uint32_t A1 = __builtin_amdgcn_alignbyte(wa[2], wa[1], sa);
+                        const uint32_t A2 = __builtin_amdgcn_alignbyte(wa[3], wa[2], sa) & 0x00FFFFFFu;
+                        uint32_t Bn[6];  // right bytes 0..23 of the row, dword aligned
 #pragma unroll
-                    for (int k = 0; k < 2 * L + 1; k++)
+                        for (int q = 0; q < 6; q++) Bn[q] = __builtin_amdgcn_alignbyte(wb[q + 1], wb[q], sb);
 #pragma unroll
-                        for (int x = 0; x < 2 * w + 1; x++) acc[k] += abs((int)a[x] - (int)b[k + x]);
+                        for (int k = 0; k < 2 * L + 1; k++) {
+                            const int qd = k >> 2, sh = k & 3;
+                            const uint32_t B0 = __builtin_amdgcn_alignbyte(Bn[qd + 1], Bn[qd], sh);
+                            const uint32_t B1 = __builtin_amdgcn_alignbyte(Bn[qd + 2], Bn[qd + 1], sh);
+                            const uint32_t B2 = __builtin_amdgcn_alignbyte(Bn[qd + 3], Bn[qd + 2], sh) & 0x00FFFFFFu;
+                            acc[k] = (int)__builtin_amdgcn_sad_u8(A2, B2,
+                                                                 __builtin_amdgcn_sad_u8(A1, B1,
+                                                                                         __builtin_amdgcn_sad_u8(A0, B0, (uint32_t)acc[k])));
+                        }
+                    }
+                } else {
+                    for (int yy = 0; yy < 2 * w + 1; yy++) {
+                        uint8_t a[2 * w + 1], b[2 * w + 2 * L + 1];
+#pragma unroll
+                        for (int x = 0; x < 2 * w + 1; x++) a[x] = PL[(size_t)yy * pl + x];
+#pragma unroll
+                        for (int x = 0; x < 2 * w + 2 * L + 1; x++) b[x] = PR[(size_t)yy * pr + x];
+#pragma unroll
+                        for (int k = 0; k < 2 * L + 1; k++)
+#pragma unroll
+                            for (int x = 0; x < 2 * w + 1; x++) acc[k] += abs((int)a[x] - (int)b[k + x]);
+                    }
                 }
                 int bestDist2 = INT_MAX, bestk = 0;
                 float vd[2 * L + 1];
