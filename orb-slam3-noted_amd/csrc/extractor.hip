@@ -1189,9 +1189,12 @@ __device__ __forceinline__ int refl101(int i, int n) {
 //   raw: 43 rows x 12 dwords (staged byte j <-> level column xs + j, xs = (kx-21) & ~3)
 //   hp : 22 row pairs x 40 dwords of exact horizontal sums, rows 2p | 2p+1 << 16 (column
 //        c <-> kx - 18 + c)
-//   bl : 37 rows x 40 bytes, aliased onto raw once the horizontal pass has read it
+// The vertical pass runs only at the sampled pixels (the descriptor stage reads hp directly).
+// One 3,520-byte region per wave holds both: hp from byte 0, raw from byte kO3RawOff
+// (checked below: each of the horizontal pass's three wave passes writes hp rows that lie
+// below every raw byte the later passes read).
 // ---------------------------------------------------------------------------------------
-constexpr int kO3R = 43, kO3Pairs = 22, kO3RawS = 12, kO3HS = 40, kO3BlS = 40;
+constexpr int kO3R = 43, kO3Pairs = 22, kO3RawS = 12, kO3HS = 40;
 
 // Horizontal-pass items (row pair p, 4-column group q) that a sampled pixel can depend on.  A
 // pattern point of radius r lands, rotated and rounded to the pixel grid, within r + sqrt(2)/2
@@ -1221,12 +1224,37 @@ constexpr int kHItems = kHItemsTable.n;
 static_assert(kHItems <= 192, "horizontal pass items must fit three wave passes");
 __constant__ HItems c_hitems = kHItemsTable;
 
+// Smallest 16-byte aligned raw offset such that the hp bytes written by wave pass k (items
+// 64k .. 64k+63, 16 B at p*160 + q*16) all lie below the lowest raw byte any later pass reads
+// (rows 2p and 2p+1 from dword q: 96p + 4q onwards).
+constexpr int hp_raw_offset() {
+    for (int x = 0;; x += 16) {
+        bool ok = true;
+        for (int k = 0; 64 * (k + 1) < kHItems; k++) {
+            int we = 0, rs = 1 << 30;
+            for (int it = 64 * k; it < 64 * (k + 1); it++) {
+                const int p = kHItemsTable.v[it] / 10, q = kHItemsTable.v[it] % 10;
+                we = we > p * 160 + q * 16 + 16 ? we : p * 160 + q * 16 + 16;
+            }
+            for (int it = 64 * (k + 1); it < kHItems; it++) {
+                const int p = kHItemsTable.v[it] / 10, q = kHItemsTable.v[it] % 10;
+                rs = rs < x + 96 * p + 4 * q ? rs : x + 96 * p + 4 * q;
+            }
+            if (we > rs) ok = false;
+        }
+        if (ok) return x;
+    }
+}
+constexpr int kO3RawOff = hp_raw_offset();
+// bytes per wave: hp (22 x 160) or raw incl. the discarded 44th row read (16 B past dword 9)
+constexpr int kO3WaveBytes = (kO3Pairs * kO3HS * 4 > kO3RawOff + (kO3R + 1) * kO3RawS * 4 + 4)
+                                 ? kO3Pairs * kO3HS * 4
+                                 : ((kO3RawOff + (kO3R + 1) * kO3RawS * 4 + 4 + 15) & ~15);
+static_assert(kO3RawOff % 16 == 0 && kO3WaveBytes % 16 == 0, "16-byte aligned staging");
+
 __global__ void __launch_bounds__(256) k_orb3(Bufs b) {
-    // 43 staged rows of 48 B (the horizontal pass also reads a 44th, whose sums are discarded:
-    // for the last wave that read lands in hp_all, still inside this workgroup's LDS): 22,336 B
-    // per workgroup, 7 workgroups (28 waves) per CU.
-    __shared__ __attribute__((aligned(16))) uint32_t raw_all[4][kO3R * kO3RawS];
-    __shared__ __attribute__((aligned(16))) uint32_t hp_all[4][kO3Pairs * kO3HS];
+    // hp, raw and bl share one region per wave (14,080 B per workgroup)
+    __shared__ __attribute__((aligned(16))) uint32_t buf_all[4][kO3WaveBytes / 4];
     const DevPlan& P = *b.plan;
     const int2 blk = xcd_block();
     const int f = blk.y;
@@ -1245,8 +1273,8 @@ __global__ void __launch_bounds__(256) k_orb3(Bufs b) {
     const int kx = kp_x(key), ky = kp_y(key);
     const uint8_t* img = level_ptr(b, P, f, l);
     const int pitch = level_pitch(P, l);
-    uint32_t* raw = raw_all[wave];
-    uint32_t* hp = hp_all[wave];
+    uint32_t* hp = buf_all[wave];
+    uint32_t* raw = buf_all[wave] + kO3RawOff / 4;
     const int xs = (kx - 21) & ~3, sh = (kx - 21) - xs;
     const int um = lane <= kHalfPatch ? P.umax[lane] : 0;  // umax[v] in lane v (read once)
 #ifdef SLAMHOT_ORB_TRACE
@@ -1259,28 +1287,23 @@ __global__ void __launch_bounds__(256) k_orb3(Bufs b) {
 #endif
     ORB_MARK();
     // ---- stage the raw window (rows ky-21..ky+21 reflected, 12 dwords per row) as three
-    // 16-byte pieces per row: 129 pieces, <= 3 per lane; pieces that leave the level go
-    // byte by byte through BORDER_REFLECT_101
+    // 16-byte pieces per row: 129 pieces, <= 3 per lane, loaded together; pieces that leave
+    // the level go byte by byte through BORDER_REFLECT_101 afterwards, one at a time
     {
         const int wfull = (pitch & 3) ? 0 : (L.w & ~3);
         uint4 v[3];
+        uint32_t slow = 0;
 #pragma unroll
         for (int k = 0; k < 3; k++) {
             const int e = lane + 64 * k;
             v[k] = make_uint4(0, 0, 0, 0);
             if (e < kO3R * 3) {
                 const int r = e / 3, part = e - 3 * r;
-                const int yy = refl101(ky - 21 + r, L.h);
-                const uint8_t* rowp = img + (size_t)yy * pitch;
                 const int x = xs + 16 * part;
-                if (x >= 0 && x + 16 <= wfull) {
-                    v[k] = *reinterpret_cast<const uint4*>(rowp + x);
-                } else {
-                    uint32_t w[4] = {0, 0, 0, 0};
-#pragma unroll
-                    for (int q = 0; q < 16; q++) w[q >> 2] |= (uint32_t)rowp[refl101(min(x + q, L.w + 3), L.w)] << (8 * (q & 3));
-                    v[k] = make_uint4(w[0], w[1], w[2], w[3]);
-                }
+                if (x >= 0 && x + 16 <= wfull)
+                    v[k] = *reinterpret_cast<const uint4*>(img + (size_t)refl101(ky - 21 + r, L.h) * pitch + x);
+                else
+                    slow |= 1u << k;
             }
         }
 #pragma unroll
@@ -1288,8 +1311,19 @@ __global__ void __launch_bounds__(256) k_orb3(Bufs b) {
             const int e = lane + 64 * k;
             if (e < kO3R * 3) {
                 const int r = e / 3, part = e - 3 * r;
-                *reinterpret_cast<uint4*>(raw + r * kO3RawS + 4 * part) = v[k];  // 16-byte aligned (48-byte rows)
+                if (!(slow >> k & 1)) *reinterpret_cast<uint4*>(raw + r * kO3RawS + 4 * part) = v[k];  // 16-byte aligned
             }
+        }
+        for (int k = 0; k < 3; k++) {
+            if (!(slow >> k & 1)) continue;
+            const int e = lane + 64 * k;
+            const int r = e / 3, part = e - 3 * r;
+            const uint8_t* rowp = img + (size_t)refl101(ky - 21 + r, L.h) * pitch;
+            const int x = xs + 16 * part;
+            uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int q = 0; q < 16; q++) w[q >> 2] |= (uint32_t)rowp[refl101(min(x + q, L.w + 3), L.w)] << (8 * (q & 3));
+            *reinterpret_cast<uint4*>(raw + r * kO3RawS + 4 * part) = make_uint4(w[0], w[1], w[2], w[3]);
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1362,65 +1396,28 @@ __global__ void __launch_bounds__(256) k_orb3(Bufs b) {
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     ORB_MARK();
-    // ---- vertical pass: lane -> 8 columns (g) x 4 output rows 4rb..4rb+3 (rb); 5 x 10 = 50
-    // lanes.  Output row y sums hs rows y..y+6: for even y the pairs y/2 .. y/2+3 with taps
-    // (k0,k1)(k2,k3)(k4,k5)(k6,0), for odd y the pairs (y-1)/2 .. with (0,k0)(k1,k2)(k3,k4)(k5,k6).
-    // acc starts at 2^15 (the rounding term); taps sum to 256, so acc >> 16 <= 255.
-    uint8_t* bl = reinterpret_cast<uint8_t*>(raw);  // raw is dead from here on
-    if (lane < 50) {
-        const int g = lane % 5, rb = lane / 5;
-        const us2 KE[4] = {us2{18, 34}, us2{48, 56}, us2{48, 34}, us2{18, 0}};
-        const us2 KO[4] = {us2{0, 18}, us2{34, 48}, us2{56, 48}, us2{34, 18}};
-        uint32_t acc[4][8];
-#pragma unroll
-        for (int o = 0; o < 4; o++)
-#pragma unroll
-            for (int e = 0; e < 8; e++) acc[o][e] = 1u << 15;
-#pragma unroll
-        for (int j = 0; j < 5; j++) {
-            const int pr = 2 * rb + j;
-            if (pr < kO3Pairs) {
-                const uint4 u0 = *reinterpret_cast<const uint4*>(&hp[pr * kO3HS + 8 * g]);
-                const uint4 u1 = *reinterpret_cast<const uint4*>(&hp[pr * kO3HS + 8 * g + 4]);
-                const uint32_t hv[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
-#pragma unroll
-                for (int e = 0; e < 8; e++) {
-                    const us2 v = as_us2(hv[e]);
-                    if (j < 4) {  // rows 4rb (even) and 4rb+1 (odd) use pairs 2rb .. 2rb+3
-                        acc[0][e] = __builtin_amdgcn_udot2(v, KE[j], acc[0][e], false);
-                        acc[1][e] = __builtin_amdgcn_udot2(v, KO[j], acc[1][e], false);
-                    }
-                    if (j >= 1) {  // rows 4rb+2 and 4rb+3 use pairs 2rb+1 .. 2rb+4
-                        acc[2][e] = __builtin_amdgcn_udot2(v, KE[j - 1], acc[2][e], false);
-                        acc[3][e] = __builtin_amdgcn_udot2(v, KO[j - 1], acc[3][e], false);
-                    }
-                }
-            }
-        }
-#pragma unroll
-        for (int o = 0; o < 4; o++) {
-            const int y = 4 * rb + o;
-            if (y < 37) {
-                uint32_t w0 = 0, w1 = 0;
-#pragma unroll
-                for (int e = 0; e < 4; e++) {
-                    w0 |= (acc[o][e] >> 16) << (8 * e);
-                    w1 |= (acc[o][e + 4] >> 16) << (8 * e);
-                }
-                *reinterpret_cast<uint2*>(&bl[y * kO3BlS + 8 * g]) = make_uint2(w0, w1);
-            }
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    ORB_MARK();
-
-    // ---- descriptor (computeOrbDescriptor, ORBextractor.cc:106-145)
+    // ---- descriptor (computeOrbDescriptor, ORBextractor.cc:106-145), with the vertical pass
+    // of the blur evaluated only at the 512 sampled pixels: blurred pixel (y, x) of the 37x37
+    // window sums hs rows y..y+6 of column x = the row pairs y>>1 .. (y>>1)+3 with taps
+    // (k0,k1)(k2,k3)(k4,k5)(k6,0) for even y and (0,k0)(k1,k2)(k3,k4)(k5,k6) for odd y (the
+    // high half of the last even-y pair is row y+7, tap 0).  acc starts at 2^15 (the rounding
+    // term); taps sum to 256, so acc >> 16 <= 255: the bits of the whole-level blur.
     const float factor_pi = (float)(3.14159265358979323846 / 180.f);
     float sn, cs;
     glibc_sincosf(angle * factor_pi, &sn, &cs);
     const float a = cs, bb = sn;
     ORB_MARK();
-    const uint8_t* center = bl + 18 * kO3BlS + 18;
+    auto blurred = [&](int r, int c) -> int {  // r, c: rounded offsets from the keypoint
+        const int y = r + 18;
+        const uint32_t* q = hp + (y >> 1) * kO3HS + (c + 18);
+        const bool odd = y & 1;
+        uint32_t acc = 1u << 15;
+        acc = __builtin_amdgcn_udot2(as_us2(q[0]), odd ? us2{0, 18} : us2{18, 34}, acc, false);
+        acc = __builtin_amdgcn_udot2(as_us2(q[kO3HS]), odd ? us2{34, 48} : us2{48, 56}, acc, false);
+        acc = __builtin_amdgcn_udot2(as_us2(q[2 * kO3HS]), odd ? us2{56, 48} : us2{48, 34}, acc, false);
+        acc = __builtin_amdgcn_udot2(as_us2(q[3 * kO3HS]), odd ? us2{34, 18} : us2{18, 0}, acc, false);
+        return (int)(acc >> 16);
+    };
     int t0[4], t1[4];
 #pragma unroll
     for (int w = 0; w < 4; w++) {
@@ -1430,8 +1427,8 @@ __global__ void __launch_bounds__(256) k_orb3(Bufs b) {
         const float x1 = (float)(int8_t)((pw >> 16) & 0xFF), y1 = (float)(int8_t)(pw >> 24);
         const int r0 = cv_round(fmaf(x0, bb, y0 * a)), c0 = cv_round(fmaf(x0, a, -(y0 * bb)));
         const int r1 = cv_round(fmaf(x1, bb, y1 * a)), c1 = cv_round(fmaf(x1, a, -(y1 * bb)));
-        t0[w] = center[r0 * kO3BlS + c0];
-        t1[w] = center[r1 * kO3BlS + c1];
+        t0[w] = blurred(r0, c0);
+        t1[w] = blurred(r1, c1);
     }
     uint64_t m[4];
 #pragma unroll
@@ -1452,8 +1449,8 @@ __global__ void __launch_bounds__(256) k_orb3(Bufs b) {
 #ifdef SLAMHOT_ORB_TRACE
     ORB_MARK();
     if (otrace)
-        printf("ORB slot=%d l=%d stage %lld ic %lld horiz %lld vert %lld sincos %lld desc %lld\n", slot, l, otr[1] - otr[0],
-               otr[2] - otr[1], otr[3] - otr[2], otr[4] - otr[3], otr[5] - otr[4], otr[6] - otr[5]);
+        printf("ORB slot=%d l=%d stage %lld ic %lld horiz %lld sincos %lld desc %lld\n", slot, l, otr[1] - otr[0],
+               otr[2] - otr[1], otr[3] - otr[2], otr[4] - otr[3], otr[5] - otr[4]);
 #endif
 }
 
