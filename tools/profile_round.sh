@@ -10,9 +10,11 @@ set -e
 export TMPDIR=/tmp
 cd "${GRAFT_REPO_ROOT:-.}"
 TAG=${1:-r02}
+if [ -z "$SKIP_CAL" ]; then  # SKIP_CAL=1: keep the committed profiles/fetch_calibration.json
 timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run \
   -- tools/microbench/mb_fetch > gpurun_out/pmc_fetch.log 2>&1
 python3 tools/fetch_calibrate.py gpurun_out/pmc_fetch
+fi
 timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_default -o run \
   -- python3 bench.py > gpurun_out/prof_default.json 2> gpurun_out/prof_default.err
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_inflight1 -o run \
