@@ -488,12 +488,16 @@ struct FastWaveLds {
     int rs, ms;                       // ROI / M-map row strides (bytes), sized to the geometry
 };
 
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) k_fast_wave(Bufs b, const int32_t* list, int nlist,
+#ifndef SLAMHOT_FAST_WPG
+#define SLAMHOT_FAST_WPG 4
+#endif
+constexpr int kFastWpg = SLAMHOT_FAST_WPG;  // waves (cells) per workgroup
+__global__ void __launch_bounds__(64 * kFastWpg) __attribute__((amdgpu_waves_per_eu(6, 8))) k_fast_wave(Bufs b, const int32_t* list, int nlist,
                                                    FastWaveLds lay) {
     extern __shared__ __attribute__((aligned(16))) uint8_t fw_smem[];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = kFastWpg == 1 ? 0 : threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int2 blk = xcd_block();
-    const int idx = blk.x * 4 + wave;
+    const int idx = blk.x * kFastWpg + wave;
     if (idx >= nlist) return;
     const DevPlan& P = *b.plan;
     const int f = blk.y;
@@ -1178,7 +1182,7 @@ __device__ __forceinline__ int refl101(int i, int n) {
 
 
 // ---------------------------------------------------------------------------------------
-// k_orb3: IC angle + GaussianBlur + rBRIEF fused, one wave per keypoint, 4 per workgroup.
+// k_orb3: IC angle + GaussianBlur + rBRIEF fused, one wave per keypoint (one per workgroup).
 // The reference blurs a clone of every level (ORBextractor.cc:1113-1115) only to sample it
 // at the 512 pattern points of each keypoint; here each wave blurs just the 37x37 window the
 // rotated pattern can reach (radius 18.38 -> rounded offsets within +-18), from one 43x43
@@ -1252,14 +1256,22 @@ constexpr int kO3WaveBytes = (kO3Pairs * kO3HS * 4 > kO3RawOff + (kO3R + 1) * kO
                                  : ((kO3RawOff + (kO3R + 1) * kO3RawS * 4 + 4 + 15) & ~15);
 static_assert(kO3RawOff % 16 == 0 && kO3WaveBytes % 16 == 0, "16-byte aligned staging");
 
-__global__ void __launch_bounds__(256) k_orb3(Bufs b) {
-    // hp, raw and bl share one region per wave (14,080 B per workgroup)
-    __shared__ __attribute__((aligned(16))) uint32_t buf_all[4][kO3WaveBytes / 4];
+// One wave (keypoint) per workgroup: each wave frees its LDS and slot the moment it is done
+// (keypoint waves finish at different times, and slots past a level's count exit at once).
+// 4 per workgroup measured 0.190 ms per 128 EuRoC frames, 1 per workgroup 0.165 ms (headline
+// 95.9k -> 101.0k stereo frames/s, interleaved A/B); 2 per workgroup 0.188 ms.
+#ifndef SLAMHOT_ORB_WPG
+#define SLAMHOT_ORB_WPG 1
+#endif
+constexpr int kOrbWpg = SLAMHOT_ORB_WPG;  // waves (keypoints) per workgroup
+__global__ void __launch_bounds__(64 * kOrbWpg) k_orb3(Bufs b) {
+    // hp, raw and bl share one region per wave (3,520 B per wave)
+    __shared__ __attribute__((aligned(16))) uint32_t buf_all[kOrbWpg][kO3WaveBytes / 4];
     const DevPlan& P = *b.plan;
     const int2 blk = xcd_block();
     const int f = blk.y;
-    const int wave = threadIdx.x >> 6;
-    const int slot = blk.x * 4 + wave;
+    const int wave = kOrbWpg == 1 ? 0 : threadIdx.x >> 6;
+    const int slot = blk.x * kOrbWpg + wave;
     const int lane = threadIdx.x & 63;
     if (slot >= P.kslots) return;
     int l = 0;
@@ -1791,12 +1803,14 @@ static slam_status launch_range(slam_extractor* ex, int f0, int nframes, const u
     begin(kStFast);
     if (!SKIP(kStFast)) {  // class B cells (larger LDS layout, fewer), then class A
         const int na = ex->n_wave_a, nb = ex->n_wave_cells - ex->n_wave_a;
+        constexpr int G = kFastWpg;
         if (nb)
-            hipLaunchKernelGGL(k_fast_wave, dim3((nb + 3) / 4, nframes), dim3(256), 4 * ex->fw_lay_b.total + fast_pad,
-                               s, b, ex->d_wave_cells.as<int32_t>() + na, nb, ex->fw_lay_b);
+            hipLaunchKernelGGL(k_fast_wave, dim3((nb + G - 1) / G, nframes), dim3(64 * G),
+                               G * ex->fw_lay_b.total + fast_pad, s, b, ex->d_wave_cells.as<int32_t>() + na, nb,
+                               ex->fw_lay_b);
         if (na)
-            hipLaunchKernelGGL(k_fast_wave, dim3((na + 3) / 4, nframes), dim3(256), 4 * ex->fw_lay.total + fast_pad, s,
-                               b, ex->d_wave_cells.as<int32_t>(), na, ex->fw_lay);
+            hipLaunchKernelGGL(k_fast_wave, dim3((na + G - 1) / G, nframes), dim3(64 * G),
+                               G * ex->fw_lay.total + fast_pad, s, b, ex->d_wave_cells.as<int32_t>(), na, ex->fw_lay);
     }
     if (ex->n_wide_cells)
         hipLaunchKernelGGL(k_fast_cells, dim3(ex->n_wide_cells, nframes), dim3(256), 0, s, b,
@@ -1814,7 +1828,7 @@ static slam_status launch_range(slam_extractor* ex, int f0, int nframes, const u
     hipLaunchKernelGGL(k_layout, dim3(nframes), dim3(256), 0, s, b);
     end(kStLayout);
     begin(kStOrb);
-    if (!SKIP(kStOrb)) hipLaunchKernelGGL(k_orb3, dim3((P.kslots + 3) / 4, nframes), dim3(256), 0, s, b);
+    if (!SKIP(kStOrb)) hipLaunchKernelGGL(k_orb3, dim3((P.kslots + kOrbWpg - 1) / kOrbWpg, nframes), dim3(64 * kOrbWpg), 0, s, b);
     end(kStOrb);
     SLAM_HIP_TRY(hipGetLastError());
 #undef SKIP

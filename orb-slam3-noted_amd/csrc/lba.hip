@@ -702,7 +702,7 @@ __global__ void k_bm_set(int nspe_total, const int* __restrict__ spe, const Edge
 
 // one thread per pose of the window: word prefix counts, then the pose list bases in pose order
 __global__ void k_bm_scan(const WinDesc* __restrict__ wins, const unsigned long long* __restrict__ bm,
-                          int* __restrict__ bmp, int* __restrict__ pbase) {
+                          int* __restrict__ bmp, int* __restrict__ pbase, int* __restrict__ pcnt) {
     __shared__ int cnt[kMaxN / 6 + 1];
     const WinDesc W = wins[blockIdx.x];
     for (int i = threadIdx.x; i < W.np; i += blockDim.x) {
@@ -713,6 +713,7 @@ __global__ void k_bm_scan(const WinDesc* __restrict__ wins, const unsigned long 
             run += __popcll(bm[o + wd]);
         }
         cnt[i] = run;
+        pcnt[W.pose0 + i] = run;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -726,7 +727,8 @@ __global__ void k_bm_scan(const WinDesc* __restrict__ wins, const unsigned long 
 
 __global__ void k_bm_list(int nspe_total, const int* __restrict__ spe, const EdgeS* __restrict__ E,
                           const WinDesc* __restrict__ wins, const unsigned long long* __restrict__ bm,
-                          const int* __restrict__ bmp, const int* __restrict__ pbase, int* __restrict__ pls) {
+                          const int* __restrict__ bmp, const int* __restrict__ pbase, int* __restrict__ pls,
+                          int* __restrict__ ppt) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= nspe_total) return;
     const EdgeS e = E[spe[s]];
@@ -735,6 +737,7 @@ __global__ void k_bm_list(int nspe_total, const int* __restrict__ spe, const Edg
     const long long o = W.bm0 + (long long)i * W.nwd + (lp >> 6);
     const int r = bmp[o] + __popcll(bm[o] & ((1ull << (lp & 63)) - 1));
     pls[W.spe0 + pbase[e.hp] + r] = spe[s];
+    ppt[W.spe0 + pbase[e.hp] + r] = e.pt;  // its point (k_schur_rows' Dinv)
 }
 
 __device__ __forceinline__ int ct_words(const WinDesc& W, const unsigned long long* __restrict__ bm, int i1, int i2,
@@ -818,7 +821,9 @@ __global__ void __launch_bounds__(256) k_ct_fill(int nblk_total, const int2* __r
                 const int q = __builtin_ctzll(m);
                 const unsigned long long below = (1ull << q) - 1ull;
                 m &= m - 1ull;
-                ct[k++] = int4{l1[r1 + __popcll(w1 & below)], l2[r2 + __popcll(w2 & below)], W.pt0 + 64 * wd + q, 0};
+                // record {edge a, point, edge b, rank of edge a in pose i1's list = k_schur_rows' W row}
+                const int ra = r1 + __popcll(w1 & below);
+                ct[k++] = int4{l1[ra], W.pt0 + 64 * wd + q, l2[r2 + __popcll(w2 & below)], ra};
             }
         }
         pos += __shfl(incl, 63, 64);
@@ -865,13 +870,13 @@ __device__ __forceinline__ void schur_block_body(int wg, int nlist, const int* _
             k += kStreams;
             if (k < kend) nxt = ct[k];
             const double* Ba = lin + (long long)kHplStride * ab.x + 9 * h;
-            const double* Bo = lin + (long long)kHplStride * ab.y + 9 * h;
+            const double* Bo = lin + (long long)kHplStride * ab.z + 9 * h;
             double ba[9], bo[9], di[9], db[3], bd[9], bj[18];
 #pragma unroll
             for (int t = 0; t < 9; t++) ba[t] = Ba[t];
 #pragma unroll
             for (int t = 0; t < 9; t++) bo[t] = Bo[t];
-            pd_load(pd + (long long)kPdStride * ab.z, di, db);
+            pd_load(pd + (long long)kPdStride * ab.y, di, db);
             // columns in lane order: this lane's rows of Hpl_b first (c' = (c + 3h) mod 6)
 #pragma unroll
             for (int t = 0; t < 9; t++) {
@@ -965,6 +970,270 @@ __global__ void __launch_bounds__(256) k_schur_blocks(int nb_diag, int nblk, int
         schur_block_body<kSchurLanes>(xcd_swizzle(b - nb_diag, (int)gridDim.x - nb_diag), nblk - npose,
                                       order + npose, blk_pose, blk_win, ct_off, ct, wins, ctl, Hpp, bp, lin, pd, Hs,
                                       Ts);
+    }
+}
+
+// ---------------------------------------------------------------- Schur by block row (round 3)
+// k_schur_rows: one workgroup per free pose i1 = one block row (i1, i1..np-1) of the Schur
+// complement.  The row's W_a = Hpl_a Dinv_p (6x3, one per edge a of pose i1, in point order) is
+// formed once into LDS, so a contribution of a block (i1, i2) loads only the other side's Hpl_b
+// and its list record and does no B Dinv product (k_schur_blocks, kept as SLAMHOT_SCHUR=blocks,
+// re-formed B_a Dinv for every block and read Hpl_a and Dinv each time).
+//   W pass: lane pair (rows 3h..3h+2) per edge a: W_a into LDS, its edge id, and the rhs sums
+//     Hpl_a db_p;
+//   diagonal block: lane quad per edge a, sum W_a Hpl_a^T, reduced over the workgroup in a fixed
+//     order (wave butterflies, then the waves in order);
+//   off-diagonal rounds: 32 lanes (8 contribution streams x a quad) per block (i1, i2); the
+//     record {edge b, rank of edge a} gives Hpl_b and the W row in LDS; per-block butterfly.
+// A lane quad (h, v) takes the 3x3 sub-block rows 3h.., columns 3v.. of a 6x6 product: W rows
+// from LDS (equal h: one broadcast address), Hpl_b rows 3v.. (equal v: the same bytes in one
+// load instruction), nine accumulators.
+// Rows with more than kSrChunk edges take W chunk by chunk (recomputed per round): the records of
+// a block are in point order, so each stream's chunk boundary is where its ranks pass the chunk.
+// Same per-contribution expressions as k_schur_blocks (B Dinv, then an FMA chain per element);
+// only the order in which contributions are summed differs.
+// 512 threads and a 384-edge W chunk (55 KB): two workgroups per CU at <= 128 VGPRs.  Measured
+// and rejected: 768 / 1024 threads at 80 / 64 VGPRs (spills: 366 / 570 us vs 310 us per 128
+// config-4 windows).
+constexpr int kSrThreads = 512, kSrGroups = kSrThreads / 32, kSrChunk = 384;
+
+// W rows [r0, r1) of pose i1's list into LDS (lane pair per edge, rows 3h..3h+2), and with kSb
+// the rhs sums Hpl_a db_p.  A pair takes at most kSrWIt edges of a chunk; all their loads are
+// issued before the first product.
+constexpr int kSrWIt = (kSrChunk + kSrThreads / 2 - 1) / (kSrThreads / 2);
+template <bool kSb>
+__device__ __forceinline__ void sr_w(int r0, int r1, const int* __restrict__ lst, const int* __restrict__ lpt,
+                                     const double* __restrict__ lin, const double* __restrict__ pd, double* Wl,
+                                     int* We, double (&sb)[3]) {
+    const int q = threadIdx.x >> 1, h = threadIdx.x & 1;
+    int e[kSrWIt], pt[kSrWIt];
+#pragma unroll
+    for (int m = 0; m < kSrWIt; m++) {
+        const int r = r0 + q + m * (kSrThreads / 2);
+        e[m] = r < r1 ? lst[r] : -1;
+        pt[m] = r < r1 ? lpt[r] : 0;
+    }
+    double ba[kSrWIt][9], di[kSrWIt][9], db[kSrWIt][3];
+#pragma unroll
+    for (int m = 0; m < kSrWIt; m++) {
+        if (e[m] < 0) continue;
+        const double* Ba = lin + (long long)kHplStride * e[m] + 9 * h;
+#pragma unroll
+        for (int t = 0; t < 9; t++) ba[m][t] = Ba[t];
+        pd_load(pd + (long long)kPdStride * pt[m], di[m], db[m]);
+    }
+#pragma unroll
+    for (int m = 0; m < kSrWIt; m++) {
+        if (e[m] < 0) continue;
+        double* o = Wl + 18 * (q + m * (kSrThreads / 2)) + 9 * h;
+        if (h == 0) We[q + m * (kSrThreads / 2)] = e[m];
+#pragma unroll
+        for (int rr = 0; rr < 3; rr++)
+#pragma unroll
+            for (int c = 0; c < 3; c++)
+                o[3 * rr + c] = ba[m][3 * rr] * di[m][c] + ba[m][3 * rr + 1] * di[m][3 + c] + ba[m][3 * rr + 2] * di[m][6 + c];
+        if constexpr (kSb) {
+#pragma unroll
+            for (int rr = 0; rr < 3; rr++)
+                sb[rr] += ba[m][3 * rr] * db[m][0] + ba[m][3 * rr + 1] * db[m][1] + ba[m][3 * rr + 2] * db[m][2];
+        }
+    }
+}
+
+// Products: a contribution W_a Hpl_b^T (6x6) is taken by a lane quad, lane (h, v) the 3x3
+// sub-block rows 3h.., columns 3v..: its W rows from LDS (lanes of equal h read the same
+// address: a broadcast) and Hpl_b rows 3v.. (lanes of equal v load the same bytes in one
+// instruction), nine accumulators, no cross-lane traffic until the final reduction.
+__device__ __forceinline__ void sr_fma(const double* Wa, const double* __restrict__ Bo, double (&acc)[9]) {
+    double bo[9];
+#pragma unroll
+    for (int t = 0; t < 9; t++) bo[t] = Bo[t];
+#pragma unroll
+    for (int rr = 0; rr < 3; rr++) {
+        const double w0 = Wa[3 * rr], w1 = Wa[3 * rr + 1], w2 = Wa[3 * rr + 2];
+#pragma unroll
+        for (int cc = 0; cc < 3; cc++)
+            acc[3 * rr + cc] = __builtin_fma(w2, bo[3 * cc + 2], __builtin_fma(w1, bo[3 * cc + 1],
+                                                                            __builtin_fma(w0, bo[3 * cc], acc[3 * rr + cc])));
+    }
+}
+
+// two contributions, loads first; the second one only when `two`
+__device__ __forceinline__ void sr_fma2(const double* Wa, const double* __restrict__ Bo, const double* Wa2,
+                                        const double* __restrict__ Bo2, bool two, double (&acc)[9]) {
+    double w[9], bo[9], w2[9], bo2[9];
+#pragma unroll
+    for (int t = 0; t < 9; t++) bo[t] = Bo[t];
+#pragma unroll
+    for (int t = 0; t < 9; t++) bo2[t] = Bo2[t];
+#pragma unroll
+    for (int t = 0; t < 9; t++) w[t] = Wa[t];
+#pragma unroll
+    for (int t = 0; t < 9; t++) w2[t] = Wa2[t];
+#pragma unroll
+    for (int rr = 0; rr < 3; rr++)
+#pragma unroll
+        for (int cc = 0; cc < 3; cc++)
+            acc[3 * rr + cc] = __builtin_fma(w[3 * rr + 2], bo[3 * cc + 2],
+                                             __builtin_fma(w[3 * rr + 1], bo[3 * cc + 1],
+                                                           __builtin_fma(w[3 * rr], bo[3 * cc], acc[3 * rr + cc])));
+    if (two) {
+#pragma unroll
+        for (int rr = 0; rr < 3; rr++)
+#pragma unroll
+            for (int cc = 0; cc < 3; cc++)
+                acc[3 * rr + cc] = __builtin_fma(w2[3 * rr + 2], bo2[3 * cc + 2],
+                                                 __builtin_fma(w2[3 * rr + 1], bo2[3 * cc + 1],
+                                                               __builtin_fma(w2[3 * rr], bo2[3 * cc], acc[3 * rr + cc])));
+    }
+}
+
+__global__ void __launch_bounds__(kSrThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) k_schur_rows(int npose, const int* __restrict__ pose_win,
+                                                           const WinDesc* __restrict__ wins,
+                                                           const WinCtl* __restrict__ ctl, const int* __restrict__ pls,
+                                                           const int* __restrict__ ppt, const int* __restrict__ pbase,
+                                                           const int* __restrict__ pcnt,
+                                                           const EdgeS* __restrict__ E, const int* __restrict__ ct_off,
+                                                           const int4* __restrict__ ct, const double* __restrict__ Hpp,
+                                                           const double* __restrict__ bp, const double* __restrict__ lin,
+                                                           const double* __restrict__ pd, double* __restrict__ Hs,
+                                                           double* __restrict__ Ts) {
+    __shared__ double Wl[kSrChunk * 18];
+    __shared__ int We[kSrChunk];  // edge id of each W row
+    __shared__ double red[kSrThreads / 64][4][9];
+    __shared__ double red_sb[kSrThreads / 64][2][3];
+    const int gp = xcd_swizzle(blockIdx.x, gridDim.x);  // a window's rows run on one XCD
+    if (gp >= npose) return;
+    const int win = pose_win[gp];
+    const WinCtl& C = ctl[win];
+    if (!C.need_trial) return;
+    const WinDesc W = wins[win];
+    const int i1 = gp - W.pose0;
+    const int* lst = pls + W.spe0 + pbase[gp];
+    const int* lpt = ppt + W.spe0 + pbase[gp];
+    const int cnt = pcnt[gp];
+    const int nch = max(1, (cnt + kSrChunk - 1) / kSrChunk);
+    double* H = Hs + W.hs_off;
+    double* Tw = Ts ? Ts + blockIdx_win_tiles(win) : nullptr;
+    auto put = [&](int R, int Cc, double v) {  // lower element (R, Cc) of the Schur system
+        if (Tw) t16_put(Tw, W.n, R, Cc, v);
+        else H[(long long)R * W.ld + Cc] = v;
+    };
+    const int quad = threadIdx.x & 3, h = quad & 1, v = quad >> 1;  // sub-block rows 3h.., columns 3v..
+
+    // ---- diagonal block (i1, i1) = sum_a W_a Hpl_a^T (lane quad per edge a) and the rhs rows
+    {
+        double acc[9], sb[3] = {0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 9; k++) acc[k] = 0.0;
+        const int e4 = threadIdx.x >> 2;  // lane quad per edge
+        for (int c = 0; c < nch; c++) {
+            const int r0 = c * kSrChunk, r1 = min(cnt, r0 + kSrChunk);
+            if (c) __syncthreads();
+            sr_w<true>(r0, r1, lst, lpt, lin, pd, Wl, We, sb);
+            __syncthreads();
+            // edge ids from LDS (the W pass left them there)
+            for (int r = r0 + e4; r < r1; r += kSrThreads / 4)
+                sr_fma(Wl + 18 * (r - r0) + 9 * h, lin + (long long)kHplStride * We[r - r0] + 9 * v, acc);
+        }
+        // butterflies over the wave (quads: lane bits 2..5; sb pairs: bits 1..5), then the waves
+#pragma unroll
+        for (int k = 0; k < 9; k++)
+#pragma unroll
+            for (int o = 4; o < 64; o <<= 1) acc[k] += __shfl_xor(acc[k], o, 64);
+#pragma unroll
+        for (int k = 0; k < 3; k++)
+#pragma unroll
+            for (int o = 2; o < 64; o <<= 1) sb[k] += __shfl_xor(sb[k], o, 64);
+        const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+        if (ln < 4) {
+#pragma unroll
+            for (int k = 0; k < 9; k++) red[wv][ln][k] = acc[k];
+        }
+        if (ln < 2) {
+#pragma unroll
+            for (int k = 0; k < 3; k++) red_sb[wv][ln][k] = sb[k];
+        }
+        __syncthreads();
+        const int t = threadIdx.x;
+        if (t < 36) {  // element (r, c), r <= c, of the upper block -> lower (6 i1 + c, 6 i1 + r)
+            const int r = t / 6, c = t % 6;
+            if (r <= c) {
+                const int qd = r / 3 + 2 * (c / 3), el = 3 * (r % 3) + c % 3;
+                double m = 0.0;
+                for (int w = 0; w < kSrThreads / 64; w++) m += red[w][qd][el];
+                double val = Hpp[24 * (long long)gp + sym6(r, c)];
+                if (r == c) val += C.lambda;
+                put(6 * i1 + c, 6 * i1 + r, val - m);
+            }
+        } else if (t < 42) {
+            const int r = t - 36;
+            double m = 0.0;
+            for (int w = 0; w < kSrThreads / 64; w++) m += red_sb[w][r / 3][r % 3];
+            H[(long long)ldlt_npad(W.n) * W.ld + 6 * i1 + r] = bp[8 * (long long)gp + r] - m;
+        }
+    }
+
+    // ---- off-diagonal blocks (i1, i2 > i1): 32 lanes (8 contribution streams x a quad) per block
+    const int g = threadIdx.x >> 5, j = (threadIdx.x & 31) >> 2;
+    const int nboff = W.np - 1 - i1;
+    for (int rd = 0; rd * kSrGroups < nboff; rd++) {
+        const int i2 = i1 + 1 + g + kSrGroups * rd;
+        const bool live = i2 < W.np;
+        const int b = W.blk0 + (live ? i2 * (i2 + 1) / 2 + i1 : 0);
+        int k = live ? ct_off[b] + j : 0;
+        const int kend = live ? ct_off[b + 1] : 0;
+        double acc[9];
+#pragma unroll
+        for (int t = 0; t < 9; t++) acc[t] = 0.0;
+        for (int c = 0; c < nch; c++) {
+            if (nch > 1) {  // this chunk's W (a single chunk's W stays from the diagonal pass)
+                __syncthreads();
+                double s_[3];
+                sr_w<false>(c * kSrChunk, min(cnt, (c + 1) * kSrChunk), lst, lpt, lin, pd, Wl, We, s_);
+                __syncthreads();
+            }
+            const int rbase = c * kSrChunk, rend = rbase + kSrChunk;
+            // record = {edge b, rank of edge a}; the next one is fetched while this one is computed
+            auto rec_at = [&](int kk) {
+                return kk < kend ? *reinterpret_cast<const int2*>(reinterpret_cast<const int*>(ct + kk) + 2)
+                                 : int2{0, 1 << 30};
+            };
+            // ranks grow along a block's list, so an entry past the chunk ends the stream's chunk
+            // two of the stream's entries per step (their Hpl_b loads issued together), in order
+            int2 ra = rec_at(k), rb = rec_at(k + 8);
+            while (ra.y < rend) {
+                const int2 na = rec_at(k + 16), nb = rec_at(k + 24);
+                const bool two = rb.y < rend;
+                sr_fma2(Wl + 18 * (ra.y - rbase) + 9 * h, lin + (long long)kHplStride * ra.x + 9 * v,
+                        Wl + 18 * ((two ? rb.y : ra.y) - rbase) + 9 * h,
+                        lin + (long long)kHplStride * (two ? rb.x : ra.x) + 9 * v, two, acc);
+                if (!two) {
+                    k += 8;
+                    break;
+                }
+                k += 16;
+                ra = na;
+                rb = nb;
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < 9; t++)
+#pragma unroll
+            for (int o = 4; o < 32; o <<= 1) acc[t] += __shfl_xor(acc[t], o, 32);
+        if (live) {
+            // every stream of a quad lane holds the sums: stream j writes element j (and 0 also 8)
+#pragma unroll
+            for (int qq = 0; qq < 2; qq++) {
+                const int e = j + 8 * qq;
+                if (e >= 9) break;
+                double m = 0.0;
+#pragma unroll
+                for (int kk = 0; kk < 9; kk++)
+                    if (kk == e) m = acc[kk];
+                put(6 * i2 + 3 * v + e % 3, 6 * i1 + 3 * h + e / 3, 0.0 - m);
+            }
+        }
     }
 }
 
@@ -1870,6 +2139,8 @@ struct slam_lba {
     DevBuf arena, cnt;
     DevBuf poses, pts, err, rho, lin, Hll, bl, Hpp, bp, pd, xp, xl, Hs, Ts;
     DevBuf bm, bmp, pbase, pls;  // pose bitmaps, their word prefixes, pose list bases, pose edge lists
+    DevBuf ppt;                  // the point of every pose-list entry
+    DevBuf pcnt;                 // free-pose edges per pose (pose list lengths)
     DevBuf spe_hp;               // free-pose index of every spe entry
     DevBuf ct, ct_off, ct_cnt;   // Schur contribution lists (built on the device)
     DevBuf kf_out, pt_out, outl;
@@ -2338,7 +2609,9 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     SLAM_HIP_TRY(s->bm.ensure(sizeof(unsigned long long) * std::max<long long>(Z.nbm, 1)));
     SLAM_HIP_TRY(s->bmp.ensure(sizeof(int) * std::max<long long>(Z.nbm, 1)));
     SLAM_HIP_TRY(s->pbase.ensure(sizeof(int) * nps));
+    SLAM_HIP_TRY(s->pcnt.ensure(sizeof(int) * nps));
     SLAM_HIP_TRY(s->pls.ensure(sizeof(int) * std::max(Z.nspe, 1)));
+    SLAM_HIP_TRY(s->ppt.ensure(sizeof(int) * std::max(Z.nspe, 1)));
     SLAM_HIP_TRY(s->spe_hp.ensure(sizeof(int) * std::max(Z.nspe, 1)));
     if (Z.nct >= (1LL << 31)) return SLAM_ECAP;  // int contribution offsets
     SLAM_HIP_TRY(s->ct.ensure(sizeof(int4) * std::max<long long>(Z.nct, 1)));
@@ -2391,12 +2664,16 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     k_init_state<<<blocks(H.nkf + H.npt, T), T, 0, S>>>(H.nkf, H.npt, DP.kf_in, DP.pt_in,
                                                          poses, pts);
     k_ldlt_pad<<<nw, 64, 0, S>>>(dW, as<double>(s->Hs));
-    if (Z.nspe) {  // the Schur contribution structure, once per solve
+    // the Schur contribution structure, once per solve (pose list bases / lengths even without edges)
+    if (Z.nspe)
         k_bm_set<<<blocks(Z.nspe, T), T, 0, S>>>(Z.nspe, DP.spe, DP.edges, DP.wins, as<unsigned long long>(s->bm),
                                                   as<int>(s->spe_hp));
-        k_bm_scan<<<nw, 64, 0, S>>>(DP.wins, as<unsigned long long>(s->bm), as<int>(s->bmp), as<int>(s->pbase));
+    k_bm_scan<<<nw, 64, 0, S>>>(DP.wins, as<unsigned long long>(s->bm), as<int>(s->bmp), as<int>(s->pbase),
+                                as<int>(s->pcnt));
+    if (Z.nspe) {
         k_bm_list<<<blocks(Z.nspe, T), T, 0, S>>>(Z.nspe, DP.spe, DP.edges, DP.wins, as<unsigned long long>(s->bm),
-                                                   as<int>(s->bmp), as<int>(s->pbase), as<int>(s->pls));
+                                                   as<int>(s->bmp), as<int>(s->pbase), as<int>(s->pls),
+                                                   as<int>(s->ppt));
     }
     if (H.nblk) {
         k_ct_count<<<blocks(H.nblk, T), T, 0, S>>>(H.nblk, DP.blk_pose, DP.blk_win, DP.wins,
@@ -2412,6 +2689,12 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
         k_t16_pad<<<nw, 64, 0, S>>>(dW, tiles);
     }
     const size_t lds_bytes = ldlt_lds_bytes(Z.max_n);
+    // Schur complement by block row (k_schur_rows: a workgroup per free pose) for batches with
+    // enough rows to fill the chip; a few windows (LocalMapping's one-window call) keep the
+    // per-block kernel, whose smaller work items finish a lone window sooner (0.214 vs 0.220 ms
+    // per LM iteration).  SLAMHOT_SCHUR=rows / blocks forces one.
+    const char* schur_env = std::getenv("SLAMHOT_SCHUR");
+    const bool schur_rows = schur_env ? std::strcmp(schur_env, "blocks") != 0 : H.npose >= 256;
     // LM as device-driven steps: a step linearizes the windows that start an iteration
     // (need_lin) and runs one trial for those in the trial loop (need_trial); every kernel skips
     // the other windows, so the host queues steps without waiting for any decision and reads
@@ -2458,7 +2741,13 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
         if (H.npt)
             k_point_prep<<<blocks(H.npt, T), T, 0, S>>>(H.npt, DP.pt_win, dC, as<double>(s->Hll), as<double>(s->bl),
                                                          as<double>(s->pd));
-        if (H.nblk)
+        if (H.nblk && schur_rows)
+            k_schur_rows<<<H.npose, kSrThreads, 0, S>>>(H.npose, DP.pose_win, dW, dC, as<int>(s->pls), as<int>(s->ppt),
+                                                        as<int>(s->pbase),
+                                                        as<int>(s->pcnt), dE, as<int>(s->ct_off), as<int4>(s->ct),
+                                                        as<double>(s->Hpp), as<double>(s->bp), as<double>(s->lin),
+                                                        as<double>(s->pd), as<double>(s->Hs), tiles);
+        else if (H.nblk)
             k_schur_blocks<<<nb_schur, 256, 0, S>>>(nb_sdiag, H.nblk, H.npose, DP.blk_order, DP.blk_pose, DP.blk_win,
                                                     as<int>(s->ct_off), as<int4>(s->ct), dW, dC, as<double>(s->Hpp),
                                                     as<double>(s->bp), as<double>(s->lin), as<double>(s->pd),

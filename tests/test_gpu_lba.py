@@ -226,3 +226,19 @@ def test_lba_large_window_and_mixed_batch(solver):
     gs = solver.solve(ws)
     for W, g in zip(ws, gs):
         _check(g, ob.lba_solve(W))
+
+
+@pytest.mark.parametrize("kernel", ["rows", "blocks"])
+def test_lba_schur_kernels(solver, monkeypatch, kernel):
+    """Both Schur-complement kernels on one batch, forced through SLAMHOT_SCHUR: k_schur_rows
+    (a workgroup per block row; the default from 256 free poses up) and k_schur_blocks (the default
+    for a few windows).  The batch holds mono, stereo and rig (body-edge) config-4 windows, a
+    5000-point window whose poses have ~830 edges each (W formed in three 384-edge chunks,
+    recomputed per round), per-KeyFrame cameras and a small window."""
+    monkeypatch.setenv("SLAMHOT_SCHUR", kernel)
+    Ws = [synth.lba_window(0), synth.lba_window(3, stereo_frac=0.3),
+          synth.lba_window(51, stereo_frac=0.3, body_frac=0.4), synth.lba_window(60, n_pt=5000),
+          synth.lba_window(70, n_kf=24, n_pt=800, obs_per_pt=6, mixed_cams=True),
+          synth.lba_window(61, n_kf=12, n_pt=300, obs_per_pt=4)]
+    for W, g in zip(Ws, solver.solve(Ws)):
+        _check(g, ob.lba_solve(W))

@@ -1,0 +1,10 @@
+export TMPDIR=/tmp
+for E in SLAMHOT_SCHUR=rows SLAMHOT_SCHUR=blocks; do
+  export $E
+  timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_iso/${E#*=} -o run -- python3 bench.py --legs lba --no-cpu-baseline --lba-inflight 1 --lba-calls 1 --steps 3 --warmup 1 > gpurun_out/iso_${E#*=}.json 2>/dev/null || exit 1
+  f=$(find gpurun_out/prof_iso/${E#*=} -name "*kernel_stats.csv" | head -1)
+  echo "== $E"; python3 -c "
+import csv
+rows=list(csv.DictReader(open('$f')))
+for r in sorted(rows,key=lambda r:-float(r['TotalDurationNs']))[:6]: print(r['Name'][:40].ljust(40), r['Calls'], round(float(r['AverageNs'])/1e3,1))"
+done
