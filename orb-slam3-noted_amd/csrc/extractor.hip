@@ -492,6 +492,11 @@ struct FastWaveLds {
 #define SLAMHOT_FAST_WPG 4
 #endif
 constexpr int kFastWpg = SLAMHOT_FAST_WPG;  // waves (cells) per workgroup
+#ifdef SLAMHOT_FAST_TRACE  // experiment builds: per-pass s_memtime of sampled cells, printed
+#define FW_MARK() do { if (ftrace) ftr[nftr++] = (long long)__builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define FW_MARK() do {} while (0)
+#endif
 __global__ void __launch_bounds__(64 * kFastWpg) __attribute__((amdgpu_waves_per_eu(6, 8))) k_fast_wave(Bufs b, const int32_t* list, int nlist,
                                                    FastWaveLds lay) {
     extern __shared__ __attribute__((aligned(16))) uint8_t fw_smem[];
@@ -513,6 +518,12 @@ __global__ void __launch_bounds__(64 * kFastWpg) __attribute__((amdgpu_waves_per
     uint16_t* lst = reinterpret_cast<uint16_t*>(base_ptr + lay.lst);
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     const int ti = min(max(P.ini_th, 0), 255), tm = min(max(P.min_th, 0), 255);
+#ifdef SLAMHOT_FAST_TRACE
+    long long ftr[12];
+    int nftr = 0, ftr_n[6] = {0, 0, 0, 0, 0, 0};
+    const bool ftrace = f == 100 && (idx % 53) == 7 && lane == 0;
+#endif
+    FW_MARK();
 
     // stage the ROI with independent 32-bit loads (row start aligned down to 4 bytes; the
     // ROI origin inside LDS is then `sh` bytes into each row), zero the M map.  Lane =
@@ -546,6 +557,7 @@ __global__ void __launch_bounds__(64 * kFastWpg) __attribute__((amdgpu_waves_per
         }
     }
     roi += sh;
+    FW_MARK();
     {
         uint32_t* m32 = reinterpret_cast<uint32_t*>(map);
         const int nw = ((th + 2) * lay.ms + 3) >> 2;
@@ -622,6 +634,10 @@ __global__ void __launch_bounds__(64 * kFastWpg) __attribute__((amdgpu_waves_per
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        FW_MARK();
+#ifdef SLAMHOT_FAST_TRACE
+        ftr_n[3 * attempt] = na;
+#endif
 
         // pass B1: the eight-pair pre-test on the compass survivors (in-place compaction)
         {
@@ -640,6 +656,10 @@ __global__ void __launch_bounds__(64 * kFastWpg) __attribute__((amdgpu_waves_per
             na = n1;
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        FW_MARK();
+#ifdef SLAMHOT_FAST_TRACE
+        ftr_n[3 * attempt + 1] = na;
+#endif
 
         // pass B (compacts the list in place: writes never pass the chunk being read)
         int nb = 0;
@@ -658,6 +678,10 @@ __global__ void __launch_bounds__(64 * kFastWpg) __attribute__((amdgpu_waves_per
             nb += __popcll(m);
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        FW_MARK();
+#ifdef SLAMHOT_FAST_TRACE
+        ftr_n[3 * attempt + 2] = nb;
+#endif
 
         // pass C: cell-local 3x3 NMS at t; count, then emit in list (row-major) order
         int cnt = 0;
@@ -677,6 +701,16 @@ __global__ void __launch_bounds__(64 * kFastWpg) __attribute__((amdgpu_waves_per
             base += __popcll(m);
         }
         if (lane == 0) b.cell_cnt[(size_t)f * P.ncells + cd.slot] = base;
+        FW_MARK();
+#ifdef SLAMHOT_FAST_TRACE
+        if (ftrace) {
+            long long d[10];
+            for (int q = 0; q < 10; q++) d[q] = q + 1 < nftr ? ftr[q + 1] - ftr[q] : 0;
+            printf("FAST cell=%d l=%d %dx%d att=%d d %lld %lld %lld %lld %lld %lld %lld %lld %lld n %d %d %d %d %d %d kept %d\n",
+                   idx, l, cw, ch, attempt, d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7], d[8], ftr_n[0], ftr_n[1],
+                   ftr_n[2], ftr_n[3], ftr_n[4], ftr_n[5], base);
+        }
+#endif
         return;
     }
 }

@@ -18,6 +18,7 @@ out = {"lib": sys.argv[1].split("/")[-1]}
 if "value" in d:
     out["headline"] = d["value"]; hd = d.get("headline_detail", {})
     out["ext_stages"] = hd.get("extractor_stage_ms_per_launch")
+    out["stages"] = hd.get("stage_ms_per_step")
 for k in ("extract", "lba", "track", "projection", "localmap", "pose"):
     if k in d: out[k] = d[k]["value"]
 if "extract" in d: out["extract_stages"] = d["extract"].get("stages_ms_per_step")
