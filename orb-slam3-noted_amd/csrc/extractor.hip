@@ -492,72 +492,17 @@ struct FastWaveLds {
 #define SLAMHOT_FAST_WPG 4
 #endif
 constexpr int kFastWpg = SLAMHOT_FAST_WPG;  // waves (cells) per workgroup
-#ifdef SLAMHOT_FAST_TRACE  // experiment builds: per-pass s_memtime of sampled cells, printed
-#define FW_MARK() do { if (ftrace) ftr[nftr++] = (long long)__builtin_amdgcn_s_memtime(); } while (0)
-#else
-#define FW_MARK() do {} while (0)
-#endif
-__global__ void __launch_bounds__(64 * kFastWpg) __attribute__((amdgpu_waves_per_eu(6, 8))) k_fast_wave(Bufs b, const int32_t* list, int nlist,
-                                                   FastWaveLds lay) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t fw_smem[];
-    const int wave = kFastWpg == 1 ? 0 : threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int2 blk = xcd_block();
-    const int idx = blk.x * kFastWpg + wave;
-    if (idx >= nlist) return;
-    const DevPlan& P = *b.plan;
-    const int f = blk.y;
-    const CellDesc cd = b.cells[list[idx]];
-    const int l = cd.level;
-    const uint8_t* img = level_ptr(b, P, f, l);
-    const int pitch = level_pitch(P, l);
+
+// One cell after its ROI is in LDS (roi = the ROI origin, `sh` bytes into each staged row): the
+// M map zeroed, passes A / B1 / B / C at iniThFAST, again at minThFAST for an empty cell, the
+// kept corners emitted to the cell's slot in row-major order.
+__device__ __forceinline__ void fast_cell(const Bufs& b, const DevPlan& P, const CellDesc& cd, int f, int sh,
+                                          const uint8_t* roi, const uint32_t* roi32, uint8_t* map, uint16_t* lst,
+                                          const FastWaveLds& lay, int lane) {
     const int cw = cd.cw, ch = cd.ch;
     const int th = ch - 6;
-    uint8_t* base_ptr = fw_smem + wave * lay.total;
-    uint8_t* roi = base_ptr + lay.roi;
-    uint8_t* map = base_ptr + lay.map;
-    uint16_t* lst = reinterpret_cast<uint16_t*>(base_ptr + lay.lst);
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     const int ti = min(max(P.ini_th, 0), 255), tm = min(max(P.min_th, 0), 255);
-#ifdef SLAMHOT_FAST_TRACE
-    long long ftr[12];
-    int nftr = 0, ftr_n[6] = {0, 0, 0, 0, 0, 0};
-    const bool ftrace = f == 100 && (idx % 53) == 7 && lane == 0;
-#endif
-    FW_MARK();
-
-    // stage the ROI with independent 32-bit loads (row start aligned down to 4 bytes; the
-    // ROI origin inside LDS is then `sh` bytes into each row), zero the M map.  Lane =
-    // (row offset, dword column), fixed for the wave; 8 rows per lane in flight.
-    const int sh = (pitch & 3) ? 0 : (cd.iniX & 3);
-    uint32_t* roi32 = reinterpret_cast<uint32_t*>(roi);
-    {
-        const uint8_t* src = img + (size_t)cd.iniY * pitch + (cd.iniX - sh);
-        if ((pitch & 3) == 0) {
-            const int wd = (sh + cw + 3) >> 2;  // <= kRoiStride / 4
-            const int rp = 64 / wd;
-            const int lr = lane / wd, lc = lane - lr * wd;
-            if (lr < rp) {
-                for (int r0 = lr; r0 < ch; r0 += 8 * rp) {
-                    uint32_t v[8];
-#pragma unroll
-                    for (int k = 0; k < 8; k++) {
-                        const int r = r0 + k * rp;
-                        if (r < ch) v[k] = *reinterpret_cast<const uint32_t*>(src + (size_t)r * pitch + 4 * lc);
-                    }
-#pragma unroll
-                    for (int k = 0; k < 8; k++) {
-                        const int r = r0 + k * rp;
-                        if (r < ch) roi32[r * (lay.rs >> 2) + lc] = v[k];
-                    }
-                }
-            }
-        } else {
-            for (int r = 0; r < ch; r++)
-                for (int c = lane; c < cw; c += 64) roi[r * lay.rs + c] = src[(size_t)r * pitch + c];
-        }
-    }
-    roi += sh;
-    FW_MARK();
     {
         uint32_t* m32 = reinterpret_cast<uint32_t*>(map);
         const int nw = ((th + 2) * lay.ms + 3) >> 2;
@@ -634,10 +579,6 @@ __global__ void __launch_bounds__(64 * kFastWpg) __attribute__((amdgpu_waves_per
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        FW_MARK();
-#ifdef SLAMHOT_FAST_TRACE
-        ftr_n[3 * attempt] = na;
-#endif
 
         // pass B1: the eight-pair pre-test on the compass survivors (in-place compaction)
         {
@@ -656,10 +597,6 @@ __global__ void __launch_bounds__(64 * kFastWpg) __attribute__((amdgpu_waves_per
             na = n1;
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        FW_MARK();
-#ifdef SLAMHOT_FAST_TRACE
-        ftr_n[3 * attempt + 1] = na;
-#endif
 
         // pass B (compacts the list in place: writes never pass the chunk being read)
         int nb = 0;
@@ -678,10 +615,6 @@ __global__ void __launch_bounds__(64 * kFastWpg) __attribute__((amdgpu_waves_per
             nb += __popcll(m);
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        FW_MARK();
-#ifdef SLAMHOT_FAST_TRACE
-        ftr_n[3 * attempt + 2] = nb;
-#endif
 
         // pass C: cell-local 3x3 NMS at t; count, then emit in list (row-major) order
         int cnt = 0;
@@ -701,18 +634,78 @@ __global__ void __launch_bounds__(64 * kFastWpg) __attribute__((amdgpu_waves_per
             base += __popcll(m);
         }
         if (lane == 0) b.cell_cnt[(size_t)f * P.ncells + cd.slot] = base;
-        FW_MARK();
-#ifdef SLAMHOT_FAST_TRACE
-        if (ftrace) {
-            long long d[10];
-            for (int q = 0; q < 10; q++) d[q] = q + 1 < nftr ? ftr[q + 1] - ftr[q] : 0;
-            printf("FAST cell=%d l=%d %dx%d att=%d d %lld %lld %lld %lld %lld %lld %lld %lld %lld n %d %d %d %d %d %d kept %d\n",
-                   idx, l, cw, ch, attempt, d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7], d[8], ftr_n[0], ftr_n[1],
-                   ftr_n[2], ftr_n[3], ftr_n[4], ftr_n[5], base);
-        }
-#endif
         return;
     }
+}
+
+// Stage a cell's ROI rows with independent 32-bit loads (row start aligned down to 4 bytes, so
+// the ROI origin inside LDS is `sh` bytes into each row).  Lane = (row offset, dword column),
+// fixed for the wave: rows lr, lr + rp, ... ; kPf of them held in registers at once.
+struct RoiGeo {
+    const uint8_t* src;
+    int pitch, sh, ch, cw, lr, lc, rp;
+    bool dw;  // dword path (pitch % 4 == 0); else byte copies
+};
+__device__ __forceinline__ RoiGeo roi_geo(const Bufs& b, const DevPlan& P, const CellDesc& cd, int f, int lane) {
+    RoiGeo g;
+    const int l = cd.level;
+    g.pitch = level_pitch(P, l);
+    g.dw = (g.pitch & 3) == 0;
+    g.sh = g.dw ? (cd.iniX & 3) : 0;
+    g.src = level_ptr(b, P, f, l) + (size_t)cd.iniY * g.pitch + (cd.iniX - g.sh);
+    g.ch = cd.ch;
+    g.cw = cd.cw;
+    const int wd = (g.sh + g.cw + 3) >> 2;  // <= kRoiStride / 4
+    g.rp = 64 / wd;
+    g.lr = lane / wd;
+    g.lc = lane - g.lr * wd;
+    return g;
+}
+__device__ __forceinline__ void stage_roi(const RoiGeo& g, uint8_t* roi, int rs, int lane) {
+    uint32_t* roi32 = reinterpret_cast<uint32_t*>(roi);
+    if (g.dw) {
+        if (g.lr < g.rp) {
+            for (int r0 = g.lr; r0 < g.ch; r0 += 8 * g.rp) {
+                uint32_t v[8];
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const int r = r0 + k * g.rp;
+                    if (r < g.ch) v[k] = *reinterpret_cast<const uint32_t*>(g.src + (size_t)r * g.pitch + 4 * g.lc);
+                }
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const int r = r0 + k * g.rp;
+                    if (r < g.ch) roi32[r * (rs >> 2) + g.lc] = v[k];
+                }
+            }
+        }
+    } else {
+        for (int r = 0; r < g.ch; r++)
+            for (int c = lane; c < g.cw; c += 64) roi[r * rs + c] = g.src[(size_t)r * g.pitch + c];
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// k_fast_wave: one WAVE per cell whose tested region is <= 64 columns wide (all cells of
+// the standard geometries); see fast_cell for the passes.
+// LDS per wave (host-sized to the widest cell of the class): ROI ch x rs | M map (th+2) x ms |
+// list.
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(64 * kFastWpg) __attribute__((amdgpu_waves_per_eu(6, 8))) k_fast_wave(Bufs b, const int32_t* list, int nlist,
+                                                   FastWaveLds lay) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t fw_smem[];
+    const int wave = kFastWpg == 1 ? 0 : threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int2 blk = xcd_block();
+    const int idx = blk.x * kFastWpg + wave;
+    if (idx >= nlist) return;
+    const DevPlan& P = *b.plan;
+    const int f = blk.y;
+    const CellDesc cd = b.cells[list[idx]];
+    uint8_t* base_ptr = fw_smem + wave * lay.total;
+    const RoiGeo g = roi_geo(b, P, cd, f, lane);
+    stage_roi(g, base_ptr + lay.roi, lay.rs, lane);
+    fast_cell(b, P, cd, f, g.sh, base_ptr + lay.roi + g.sh, reinterpret_cast<const uint32_t*>(base_ptr + lay.roi),
+              base_ptr + lay.map, reinterpret_cast<uint16_t*>(base_ptr + lay.lst), lay, lane);
 }
 
 // ---------------------------------------------------------------------------------------
