@@ -226,10 +226,21 @@ def main():
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(gpu)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
-        else:
-            dist.init_process_group("gloo")
+        # the process-group libraries may print to fd 1 (gloo's "[Gloo] Rank 0 is connected ...");
+        # stdout carries only the JSON line, so fd 1 points at stderr while they initialise
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+            else:
+                dist.init_process_group("gloo")
+            dist.barrier()
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
     device = torch.device("cuda", gpu)
     torch.cuda.set_device(device)
     local_rank = gpu

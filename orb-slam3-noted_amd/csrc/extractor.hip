@@ -1556,6 +1556,17 @@ struct slam_extractor {
         d_oidx, d_err, d_kps, d_desc, d_n, d_mono;
     int last_frames = 0;
     const uint8_t* last_img = nullptr;  // level-0 pointer of the last run (for pyramid_level)
+    // host-buffer path (slamhot_extract / _batch, the call Frame.cc:119-122 makes per image):
+    // pinned staging in and out, one device output block, and the whole call (H2D, pipeline,
+    // D2H) captured once per shape as a HIP graph and replayed (host_graph below)
+    void* h_in = nullptr;
+    size_t h_in_bytes = 0;
+    void* h_out = nullptr;
+    size_t h_out_bytes = 0;
+    DevBuf d_out;
+    hipGraphExec_t hg_exec = nullptr;
+    std::vector<uintptr_t> hg_key;
+    bool hg_off = false;  // a capture failed, or SLAMHOT_EXTRACT_GRAPH=0: plain stream calls
     // k_octree launch groups: {first level, levels, keys held in LDS, dynamic LDS bytes}
     struct OctGroup { int l0, nl, keycap; size_t lds; };
     OctGroup oct[2] = {};
@@ -1895,6 +1906,105 @@ static slam_status launch_pipeline(slam_extractor* ex, int nframes, const uint8_
     return SLAM_OK;
 }
 
+// ---- host-buffer path as a HIP graph.  A per-image call is ~16 kernel launches, a memset and
+// six small copies: launch and copy latency, not the GPU, set its time (0.37 ms for a VGA frame).
+// The call is captured once per shape (frames, size, lapping area, capacity, buffer addresses) and
+// replayed: the image goes through pinned memory (one host memcpy, one DMA), the outputs come
+// back as one block (counts, error flags, keypoints, descriptors) into pinned memory.
+constexpr int kHostGraphFrames = 8;  // larger batches keep the sub-stream pipeline
+constexpr slam_status SLAM_ENOTSUP = (slam_status)-100;  // internal: fall back to stream calls
+
+static bool pinned_ensure(void*& p, size_t& have, size_t need) {
+    if (need <= have) return true;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    have = 0;
+    if (hipHostMalloc(&p, need, hipHostMallocDefault) != hipSuccess) return false;
+    have = need;
+    return true;
+}
+
+static slam_status host_graph_extract(slam_extractor* ex, int nframes, const uint8_t* imgs, int width, int height,
+                                      size_t stride, int lap0, int lap1, slam_keypoint* kps, uint8_t* desc, int cap,
+                                      int* n, int* mono_index) {
+    const size_t F = (size_t)nframes, fb = (size_t)width * height, dcap = (size_t)std::max(cap, 1);
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t o_n = 0, o_mono = 4 * F, o_err = 8 * F, o_kps = al(12 * F);
+    const size_t o_desc = al(o_kps + F * dcap * sizeof(slam_keypoint)), out_bytes = o_desc + F * dcap * 32;
+    slam_status st;
+    if ((st = ex->d_img.ensure(F * fb)) || (st = ex->d_out.ensure(out_bytes))) return st;
+    if (!pinned_ensure(ex->h_in, ex->h_in_bytes, F * fb) || !pinned_ensure(ex->h_out, ex->h_out_bytes, out_bytes))
+        return SLAM_ENOMEM;
+    hipStream_t s = ex->stream;
+    uint8_t* dout = ex->d_out.as<uint8_t>();
+    const std::vector<uintptr_t> key = {
+        (uintptr_t)nframes, (uintptr_t)width, (uintptr_t)height, (uintptr_t)(intptr_t)lap0, (uintptr_t)(intptr_t)lap1,
+        (uintptr_t)cap, (uintptr_t)ex->h_in, (uintptr_t)ex->h_out, (uintptr_t)ex->d_img.p, (uintptr_t)ex->d_out.p,
+        (uintptr_t)ex->d_plan.p, (uintptr_t)ex->d_xtab.p, (uintptr_t)ex->d_ytab.p, (uintptr_t)ex->d_cells.p,
+        (uintptr_t)ex->d_wave_cells.p, (uintptr_t)ex->d_wide_cells.p, (uintptr_t)ex->d_pyr.p,
+        (uintptr_t)ex->d_cell_keys.p, (uintptr_t)ex->d_cell_cnt.p, (uintptr_t)ex->d_keys_g.p,
+        (uintptr_t)ex->d_knode_g.p, (uintptr_t)ex->d_okp.p, (uintptr_t)ex->d_ocnt.p, (uintptr_t)ex->d_oidx.p,
+        (uintptr_t)ex->d_err.p};
+    if (!ex->hg_exec || key != ex->hg_key) {
+        if (ex->hg_exec) (void)hipGraphExecDestroy(ex->hg_exec);
+        ex->hg_exec = nullptr;
+        ex->hg_key.clear();
+        if (hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+            ex->hg_off = true;
+            return SLAM_ENOTSUP;
+        }
+        bool ok = hipMemcpyAsync(ex->d_img.p, ex->h_in, F * fb, hipMemcpyHostToDevice, s) == hipSuccess;
+        ok = ok && launch_pipeline(ex, nframes, ex->d_img.as<uint8_t>(), lap0, lap1,
+                                   reinterpret_cast<slam_keypoint*>(dout + o_kps), dout + o_desc, cap,
+                                   reinterpret_cast<int32_t*>(dout + o_n), reinterpret_cast<int32_t*>(dout + o_mono),
+                                   s) == SLAM_OK;
+        ok = ok && hipMemcpyAsync(dout + o_err, ex->d_err.p, 4 * F, hipMemcpyDeviceToDevice, s) == hipSuccess;
+        ok = ok && hipMemcpyAsync(ex->h_out, dout, out_bytes, hipMemcpyDeviceToHost, s) == hipSuccess;
+        hipGraph_t graph = nullptr;
+        const bool ended = hipStreamEndCapture(s, &graph) == hipSuccess && graph;
+        ok = ok && ended && hipGraphInstantiate(&ex->hg_exec, graph, nullptr, nullptr, 0) == hipSuccess;
+        if (graph) (void)hipGraphDestroy(graph);
+        (void)hipGetLastError();
+        if (!ok) {
+            if (ex->hg_exec) (void)hipGraphExecDestroy(ex->hg_exec);
+            ex->hg_exec = nullptr;
+            ex->hg_off = true;
+            return SLAM_ENOTSUP;
+        }
+        ex->hg_key = key;
+    }
+    uint8_t* hin = static_cast<uint8_t*>(ex->h_in);
+    for (int f = 0; f < nframes; f++) {
+        if (stride == (size_t)width) {
+            std::memcpy(hin + f * fb, imgs + f * fb, fb);
+        } else {
+            for (int y = 0; y < height; y++)
+                std::memcpy(hin + f * fb + (size_t)y * width, imgs + ((size_t)f * height + y) * stride, width);
+        }
+    }
+    SLAM_HIP_TRY(hipGraphLaunch(ex->hg_exec, s));
+    SLAM_HIP_TRY(hipStreamSynchronize(s));
+    ex->last_frames = nframes;
+    ex->last_img = ex->d_img.as<uint8_t>();
+    const uint8_t* hout = static_cast<const uint8_t*>(ex->h_out);
+    std::memcpy(n, hout + o_n, 4 * F);
+    std::memcpy(mono_index, hout + o_mono, 4 * F);
+    const int32_t* err = reinterpret_cast<const int32_t*>(hout + o_err);
+    if (cap > 0) {
+        std::memcpy(kps, hout + o_kps, F * cap * sizeof(slam_keypoint));
+        std::memcpy(desc, hout + o_desc, F * cap * 32);
+    }
+    slam_status res = SLAM_OK;
+    for (int f = 0; f < nframes; f++) {
+        if (err[f] & ~kErrCap) {
+            std::fprintf(stderr, "slamhot: extractor internal error flags 0x%x on frame %d\n", err[f], f);
+            return SLAM_EINVAL;
+        }
+        if (n[f] > cap) res = SLAM_ECAP;
+    }
+    return res;
+}
+
 extern "C" {
 
 const char* slamhot_version(void) { return "slamhot 0.1 (gfx950)"; }
@@ -1952,6 +2062,8 @@ slam_status slamhot_extractor_create(const slam_orb_params* params, int device, 
         if (e) ex->nsub = std::max(1, std::min(slam_extractor::kMaxSub, std::atoi(e)));
         const char* c = std::getenv("SLAMHOT_CHAIN_FAST");
         ex->chain_fast = c && c[0] == '1';
+        const char* g = std::getenv("SLAMHOT_EXTRACT_GRAPH");
+        ex->hg_off = g && g[0] == '0';
     }
     for (int k = 0; k < slam_extractor::kMaxSub; k++)
         if (hipStreamCreateWithFlags(&ex->sub[k], hipStreamNonBlocking) != hipSuccess ||
@@ -1974,6 +2086,10 @@ void slamhot_extractor_destroy(slam_extractor* ex) {
                       &ex->d_okp, &ex->d_ocnt, &ex->d_oidx, &ex->d_err, &ex->d_kps, &ex->d_desc,
                       &ex->d_n, &ex->d_mono};
     for (DevBuf* b : bufs) b->release();
+    ex->d_out.release();
+    if (ex->hg_exec) (void)hipGraphExecDestroy(ex->hg_exec);
+    if (ex->h_in) (void)hipHostFree(ex->h_in);
+    if (ex->h_out) (void)hipHostFree(ex->h_out);
     for (auto& m : ex->marks) { ex->pool.push_back(m.a); ex->pool.push_back(m.b); }
     for (hipEvent_t e : ex->pool) (void)hipEventDestroy(e);
     for (int k = 0; k < slam_extractor::kMaxSub; k++) {
@@ -2035,6 +2151,10 @@ slam_status slamhot_extract_batch(slam_extractor* ex, int nframes, const uint8_t
     SLAM_HIP_TRY(hipSetDevice(ex->device));
     slam_status st;
     if ((st = ensure_plan(ex, width, height)) || (st = ensure_batch(ex, nframes, cap))) return st;
+    if (nframes <= kHostGraphFrames && !ex->profiling && !ex->hg_off) {
+        st = host_graph_extract(ex, nframes, imgs, width, height, stride, lap0, lap1, kps, desc, cap, n, mono_index);
+        if (st != SLAM_ENOTSUP) return st;  // else: the capture failed, plain stream calls below
+    }
     const size_t F = (size_t)nframes, fb = (size_t)width * height;
     const int dcap = std::max(cap, 1);
     if ((st = ex->d_img.ensure(F * fb)) || (st = ex->d_kps.ensure(F * dcap * sizeof(slam_keypoint))) ||
