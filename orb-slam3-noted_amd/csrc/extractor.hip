@@ -1529,6 +1529,8 @@ static const char* kStageNames[kNumStages] = {"k_resize", "k_fast_wave", "k_octr
 
 using namespace slamhot;
 
+constexpr int kSmallBatch = 8;  // batches up to this size: the small-batch octree launch
+
 struct slam_extractor {
     slam_orb_params prm{};
     int device = 0;
@@ -1550,6 +1552,7 @@ struct slam_extractor {
     DevBuf d_plan, d_xtab, d_ytab, d_cells, d_wave_cells, d_wide_cells;
     int n_wave_cells = 0, n_wide_cells = 0;
     FastWaveLds fw_lay{}, fw_lay_b{};  // layouts of the two wave-cell classes (see below)
+    FastWaveLds fw_lay_all{};          // one layout for every wave cell (small batches: one dispatch)
     int n_wave_a = 0;                  // d_wave_cells: class A cells first, then class B
     // per-batch buffers
     DevBuf d_img, d_pyr, d_cell_keys, d_cell_cnt, d_keys_g, d_knode_g, d_okp, d_ocnt,
@@ -1571,6 +1574,11 @@ struct slam_extractor {
     struct OctGroup { int l0, nl, keycap; size_t lds; };
     OctGroup oct[2] = {};
     int n_oct = 0;
+    // small batches (the per-image call): every level in one launch with its keys in LDS; the
+    // two-group split above is for the concurrent batch pipeline, where the octree's LDS is
+    // taken from other batches' FAST / orb and level 0 keeps its keys in L2 (one VGA frame:
+    // level 0 115 us + levels 1-7 49 us as two launches)
+    OctGroup oct_small{};
     int octree_max_cells = 1;
     // per-stage HIP-event timing (slamhot_extractor_set_profiling)
     bool profiling = false;
@@ -1709,6 +1717,7 @@ static slam_status ensure_plan(slam_extractor* ex, int W, int H) {
         ex->n_wave_a = (int)wave.size();
         wave.insert(wave.end(), wave_b.begin(), wave_b.end());
         ex->fw_lay = lay;
+        ex->fw_lay_all = layout_of(wave);  // wave now holds both classes
         if (4 * lay.total > 160 * 1024 || 4 * ex->fw_lay_b.total > 160 * 1024) return SLAM_EINVAL;
         SLAM_HIP_TRY(hipFuncSetAttribute((const void*)k_fast_wave, hipFuncAttributeMaxDynamicSharedMemorySize,
                                          160 * 1024));
@@ -1751,6 +1760,11 @@ static slam_status ensure_plan(slam_extractor* ex, int W, int H) {
         G.lds = octree_lds_bytes(P.max_nodes, G.keycap, max_cells);
         lds_attr = std::max(lds_attr, G.lds);
     }
+    ex->oct_small.l0 = 0;
+    ex->oct_small.nl = P.nlevels;
+    ex->oct_small.keycap = keycap_for(96 * 1024);
+    ex->oct_small.lds = octree_lds_bytes(P.max_nodes, ex->oct_small.keycap, max_cells);
+    lds_attr = std::max(lds_attr, ex->oct_small.lds);
     SLAM_HIP_TRY(hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds_attr));
     return SLAM_OK;
@@ -1842,6 +1856,13 @@ static slam_status launch_range(slam_extractor* ex, int f0, int nframes, const u
     if (!SKIP(kStFast)) {  // class B cells (larger LDS layout, fewer), then class A
         const int na = ex->n_wave_a, nb = ex->n_wave_cells - ex->n_wave_a;
         constexpr int G = kFastWpg;
+        if (nframes <= kSmallBatch && na && nb && kFastWpg * ex->fw_lay_all.total <= 160 * 1024) {
+            // a small batch fills a fraction of the chip: one dispatch over both classes at the
+            // union layout saves the second launch on the per-image critical path
+            hipLaunchKernelGGL(k_fast_wave, dim3((na + nb + G - 1) / G, nframes), dim3(64 * G),
+                               G * ex->fw_lay_all.total + fast_pad, s, b, ex->d_wave_cells.as<int32_t>(), na + nb,
+                               ex->fw_lay_all);
+        } else {
         if (nb)
             hipLaunchKernelGGL(k_fast_wave, dim3((nb + G - 1) / G, nframes), dim3(64 * G),
                                G * ex->fw_lay_b.total + fast_pad, s, b, ex->d_wave_cells.as<int32_t>() + na, nb,
@@ -1849,6 +1870,7 @@ static slam_status launch_range(slam_extractor* ex, int f0, int nframes, const u
         if (na)
             hipLaunchKernelGGL(k_fast_wave, dim3((na + G - 1) / G, nframes), dim3(64 * G),
                                G * ex->fw_lay.total + fast_pad, s, b, ex->d_wave_cells.as<int32_t>(), na, ex->fw_lay);
+        }
     }
     if (ex->n_wide_cells)
         hipLaunchKernelGGL(k_fast_cells, dim3(ex->n_wide_cells, nframes), dim3(256), 0, s, b,
@@ -1856,8 +1878,9 @@ static slam_status launch_range(slam_extractor* ex, int f0, int nframes, const u
     end(kStFast);
     if (fast_done) SLAM_HIP_TRY(hipEventRecord(fast_done, s));
     begin(kStOctree);
-    for (int g = 0; g < ex->n_oct && !SKIP(kStOctree); g++) {
-        const slam_extractor::OctGroup& G = ex->oct[g];
+    const bool small = nframes <= kSmallBatch;
+    for (int g = 0; g < (small ? 1 : ex->n_oct) && !SKIP(kStOctree); g++) {
+        const slam_extractor::OctGroup& G = small ? ex->oct_small : ex->oct[g];
         hipLaunchKernelGGL(k_octree, dim3(G.nl, nframes), dim3(64), G.lds, s, b, G.l0, G.keycap,
                            ex->octree_max_cells);
     }
@@ -1911,7 +1934,7 @@ static slam_status launch_pipeline(slam_extractor* ex, int nframes, const uint8_
 // The call is captured once per shape (frames, size, lapping area, capacity, buffer addresses) and
 // replayed: the image goes through pinned memory (one host memcpy, one DMA), the outputs come
 // back as one block (counts, error flags, keypoints, descriptors) into pinned memory.
-constexpr int kHostGraphFrames = 8;  // larger batches keep the sub-stream pipeline
+constexpr int kHostGraphFrames = kSmallBatch;  // larger batches keep the sub-stream pipeline
 constexpr slam_status SLAM_ENOTSUP = (slam_status)-100;  // internal: fall back to stream calls
 
 static bool pinned_ensure(void*& p, size_t& have, size_t need) {
