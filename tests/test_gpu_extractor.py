@@ -142,3 +142,27 @@ def test_non_default_pyramid(gpu_extractor_factory, scale, levels, nf):
     ref = ob.pyramid(img, p)
     for l in range(levels):
         assert np.array_equal(ex.pyramid_level(l), ref[l]), l
+
+
+@pytest.mark.parametrize("graph", ["1", "0"])
+def test_host_call_graph_and_stream_paths(gpu_extractor_factory, monkeypatch, graph):
+    """The per-image host-buffer call is captured as a HIP graph per shape (frame size, lapping
+    area, batch size, capacity) and replayed; SLAMHOT_EXTRACT_GRAPH=0 keeps plain stream calls.
+    One handle alternates shapes (re-capture) and repeats them (replay); a 5-frame batch takes the
+    small-batch launches (one FAST dispatch, one octree launch); a 12-frame batch the batch
+    pipeline.  Every result bit-exact against the oracle."""
+    monkeypatch.setenv("SLAMHOT_EXTRACT_GRAPH", graph)
+    ex = gpu_extractor_factory(nfeatures=1000, max_size=(752, 480), max_batch=12)
+    calls = [((640, 480), (0, 0), 40), ((752, 480), (0, 1000), 41), ((640, 480), (0, 0), 42),
+             ((640, 480), (100, 400), 43), ((752, 480), (0, 1000), 44)]
+    for (w, h), lap, seed in calls:
+        img = synth.frame(seed, w, h)
+        kg, dg, mg = ex(img, lap)
+        ko, do, mo = ob.extract(img, ob.params(), lap=lap)
+        _compare(kg, dg, mg, ko, do, mo)
+    for nb in (5, 12):
+        imgs = synth.frames(range(60, 60 + nb))
+        kps, desc, n, mono = ex.extract_batch(imgs)
+        for f in range(nb):
+            ko, do, mo = ob.extract(imgs[f])
+            _compare(kps[f][: n[f]], desc[f][: n[f]], mono[f], ko, do, mo)
