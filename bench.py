@@ -202,6 +202,8 @@ def main():
     ap.add_argument("--lba-windows", type=int, default=128, help="LBA windows per GPU per call")
     ap.add_argument("--lba-calls", type=int, default=3)
     ap.add_argument("--lba-inflight", type=int, default=4, help="LBA solver handles driven concurrently")
+    ap.add_argument("--lba-stagger-ms", type=float, default=0.0,
+                    help="LBA: solver t starts t x this many ms late (host planning out of phase)")
     ap.add_argument("--pose-frames", type=int, default=512, help="PoseOptimization frames per GPU per call")
     ap.add_argument("--localmap-frames", type=int, default=256, help="localmap leg: frames per call")
     ap.add_argument("--projection-frames", type=int, default=256,
@@ -846,6 +848,8 @@ def lba_leg(ctx):
     stats = [[0, 0.0, 0.0] for _ in range(NL)]
 
     def worker(t):
+        if args.lba_stagger_ms > 0:
+            time.sleep(t * args.lba_stagger_ms / 1e3)
         for _ in range(args.lba_calls):
             stats[t][0] += runs[t]()
             d, pl, _ = solvers[t].last_stats()

@@ -29,7 +29,9 @@ constexpr int kStMaxLevels = 16;
 constexpr int kStMaxRows = 4096;      // level-0 image height limit (extractor limit 4095)
 constexpr int kStMaxSort = 8192;      // keypoints per frame for the median sort (LDS)
 constexpr int kRowsThreads = 1024;
-constexpr int kMatchThreads = 128;
+// one wave per workgroup (keypoints' band searches finish at different times): stereo stage
+// 0.125 -> 0.120 ms per 128 pairs, headline +0.6% against 128 threads (interleaved A/B)
+constexpr int kMatchThreads = 64;
 constexpr int kMedianThreads = 1024;
 
 struct StereoGeom {
