@@ -200,10 +200,12 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=384)
     ap.add_argument("--lba-windows", type=int, default=128, help="LBA windows per GPU per call")
-    ap.add_argument("--lba-calls", type=int, default=3)
+    ap.add_argument("--lba-calls", type=int, default=6)
     ap.add_argument("--lba-inflight", type=int, default=4, help="LBA solver handles driven concurrently")
-    ap.add_argument("--lba-stagger-ms", type=float, default=0.0,
-                    help="LBA: solver t starts t x this many ms late (host planning out of phase)")
+    ap.add_argument("--lba-stagger-ms", type=float, default=6.0,
+                    help="LBA: solver t starts t x this many ms late, so the solvers' host planning phases "
+                         "(~5 ms per 128-window call) fall between the others' device phases instead of "
+                         "all at once (independent LocalMapping clients arrive out of phase)")
     ap.add_argument("--pose-frames", type=int, default=512, help="PoseOptimization frames per GPU per call")
     ap.add_argument("--localmap-frames", type=int, default=256, help="localmap leg: frames per call")
     ap.add_argument("--projection-frames", type=int, default=256,
@@ -890,6 +892,7 @@ def lba_leg(ctx):
                              "whole-job LM iterations/s; MFMA-busy cycles per kernel in profiles/"},
         "lba_calls_per_s": round(nwin * args.lba_calls * NL * ctx["world"] / el, 2),
         "solves_in_flight": NL,
+        "solver_start_stagger_ms": args.lba_stagger_ms,
         "ms_per_call": round(el / args.lba_calls * 1e3, 3),  # NL calls run concurrently
         "device_lm_iters_per_s_one_solver": round(iters_all / NL / (dev_max / 1e3), 1) if dev_max > 0 else None,
         "host_plan_ms_per_call": round(plan_ms / args.lba_calls, 3),
