@@ -1,8 +1,9 @@
 // matcher.hip — MI355X (gfx950) DBoW2 vocabulary descent and ORBmatcher::SearchByBoW.
 //
 //   k_vocab_transform  TemplatedVocabulary::transform (TemplatedVocabulary.h:1229-1271):
-//                      16 lanes per descriptor; at each level lane j scores child j (two
-//                      16-byte loads + 8 popcounts), (distance, child position) wave-min.
+//                      kVocG lanes per descriptor; at each level lane j scores child slots
+//                      j, j + kVocG, .. (two 16-byte loads + 8 popcounts each) together with
+//                      the child's next-level record, (distance, child position) group-min.
 //   k_bow_match        SearchByBoW (ORBmatcher.cc:269-471 and 823-963): one workgroup per
 //                      (A, B) pair.  Common FeatureVector nodes are independent (every
 //                      feature lives in exactly one node), so waves take nodes round-robin;
@@ -38,6 +39,9 @@ struct DevVocab {
     const uint8_t* is_leaf;
     const int32_t* word;        // word id per node (-1 for inner nodes)
     const double* weight;
+    const uint8_t* child_desc;  // n_nodes - 1 child slots x 32: desc of child_idx[c]
+    const int4* child_next;     // per child slot: {its child range begin, end, node id | leaf << 31, 0}
+    int root_c0, root_c1;       // the root's child range
     int L;
 };
 
@@ -63,43 +67,89 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
                min((uint32_t)__builtin_amdgcn_readlane((int)x, 32), (uint32_t)__builtin_amdgcn_readlane((int)x, 48)));
 }
 
+// Lanes per descriptor: lane j scores children j, j + kVocG, ... of the current node (the first
+// 16 child slots from registers, further ones -- vocabularies with k > 16 -- in a second loop).
+#ifndef SLAMHOT_VOC_G
+#define SLAMHOT_VOC_G 8
+#endif
+constexpr int kVocG = SLAMHOT_VOC_G;
+constexpr int kVocS = 16 / kVocG;  // child slots per lane held in registers
+static_assert(kVocG == 4 || kVocG == 8 || kVocG == 16, "lanes per descriptor");
+
+// min over the kVocG-lane group (DPP inside rows of 16), in every lane of the group
+__device__ __forceinline__ uint32_t group_min_u32(uint32_t x) {
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false));  // quad_perm [1,0,3,2]
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false));  // quad_perm [2,3,0,1]
+    if constexpr (kVocG >= 8) x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xF, 0xF, false));
+    if constexpr (kVocG >= 16) x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x140, 0xF, 0xF, false));
+    return x;
+}
+
 // n_per_frame (optional): the descriptors are frames of `cap` slots and only the first
-// n_per_frame[f] slots of frame f hold features; the empty slots' groups exit at once
+// n_per_frame[f] slots of frame f hold features; the empty slots' groups exit at once.
+// One global round trip per level: the children's descriptors are stored contiguously per
+// parent (child_desc[c] for child slot c) next to each child's own child range, node id and
+// leaf flag (child_next[c]), both loaded together; the winner's record then comes from its
+// lane by ds_bpermute instead of three dependent loads (child_idx, child_ptr, is_leaf).
 constexpr int kVocThreads = 256;  // 64 measured 0.9% slower in the headline
 __global__ void __launch_bounds__(kVocThreads) k_vocab_transform(DevVocab V, int n, const uint8_t* desc,
                                                          int desc_stride, int levelsup,
                                                          int32_t* word_id, double* weight,
                                                          int32_t* node_id, const int32_t* __restrict__ n_per_frame,
                                                          int cap) {
-    const int g = (blockIdx.x * blockDim.x + threadIdx.x) >> 4;  // feature
-    const int j = threadIdx.x & 15;                                // child slot
-    if (n_per_frame && g < n && (g % cap) >= n_per_frame[g / cap]) return;  // whole 16-lane group
+    const int g = (blockIdx.x * blockDim.x + threadIdx.x) / kVocG;  // feature
+    const int lane = threadIdx.x & 63, j = lane & (kVocG - 1);        // child slot
+    if (n_per_frame && g < n && (g % cap) >= n_per_frame[g / cap]) return;  // whole lane group
     const bool live = g < n;
     const int gi = live ? g : 0;
     const uint4* f = reinterpret_cast<const uint4*>(desc + (size_t)gi * desc_stride);
     const uint4 f0 = f[0], f1 = f[1];
     const int nid_level = V.L - levelsup;
     int final_id = 0, level = 0, nid = 0;
-    bool leaf = false;
-    // every lane of a 16-lane group follows the same path; bounded by the tree depth
-    for (int it = 0; it < 64 && !leaf; it++) {
+    int c0 = V.root_c0, c1 = V.root_c1;
+    // every lane of a group follows the same path; bounded by the tree depth
+    for (int it = 0; it < 64; it++) {
         ++level;
-        const int c0 = V.child_ptr[final_id], c1 = V.child_ptr[final_id + 1];
         uint32_t bestkey = 0xFFFFFFFFu;
-        for (int cb = c0; cb < c1; cb += 16) {
-            const int c = cb + j;
-            uint32_t key = 0xFFFFFFFFu;
+        int4 inf[kVocS];
+#pragma unroll
+        for (int sl = 0; sl < kVocS; sl++) {
+            const int c = c0 + j + sl * kVocG;
+            inf[sl] = make_int4(0, 0, 0, 0);
             if (c < c1) {
-                const int id = V.child_idx[c];
-                const uint4* d = reinterpret_cast<const uint4*>(V.desc + (size_t)id * 32);
-                key = ((uint32_t)hamming32(f0, f1, d[0], d[1]) << 20) | (uint32_t)(c - c0);
+                const uint4* d = reinterpret_cast<const uint4*>(V.child_desc + (size_t)c * 32);
+                inf[sl] = V.child_next[c];
+                bestkey = min(bestkey, ((uint32_t)hamming32(f0, f1, d[0], d[1]) << 20) | (uint32_t)(c - c0));
             }
-            bestkey = min(bestkey, row16_min_u32(key));  // the 16-lane group is one DPP row
         }
+        for (int cb = c0 + 16; cb < c1; cb += kVocG) {  // k > 16
+            const int c = cb + j;
+            if (c < c1) {
+                const uint4* d = reinterpret_cast<const uint4*>(V.child_desc + (size_t)c * 32);
+                bestkey = min(bestkey, ((uint32_t)hamming32(f0, f1, d[0], d[1]) << 20) | (uint32_t)(c - c0));
+            }
+        }
+        bestkey = group_min_u32(bestkey);
         if (bestkey == 0xFFFFFFFFu) break;  // malformed tree (inner node without children)
-        final_id = V.child_idx[c0 + (int)(bestkey & 0xFFFFF)];
+        const int pos = (int)(bestkey & 0xFFFFF);
+        int4 nx;
+        if (pos < 16) {
+            const int slot = pos / kVocG, src = (lane & ~(kVocG - 1)) | (pos & (kVocG - 1));
+            int4 sel = inf[0];
+#pragma unroll
+            for (int sl = 1; sl < kVocS; sl++)
+                if (slot == sl) sel = inf[sl];
+            nx.x = __shfl(sel.x, src, 64);
+            nx.y = __shfl(sel.y, src, 64);
+            nx.z = __shfl(sel.z, src, 64);
+        } else {
+            nx = V.child_next[c0 + pos];
+        }
+        final_id = nx.z & 0x7FFFFFFF;
         if (level == nid_level) nid = final_id;
-        leaf = V.is_leaf[final_id] != 0;
+        if (nx.z < 0) break;  // leaf
+        c0 = nx.x;
+        c1 = nx.y;
     }
     if (live && j == 0) {
         word_id[g] = V.word[final_id];
@@ -590,7 +640,8 @@ struct slam_vocab {
     int device = 0;
     int k = 0, L = 0, scoring = 0, weighting = 0, n_nodes = 0, n_words = 0;
     hipStream_t stream = nullptr;
-    Buf d_desc, d_child_ptr, d_child_idx, d_leaf, d_word, d_weight;
+    Buf d_desc, d_child_ptr, d_child_idx, d_leaf, d_word, d_weight, d_child_desc, d_child_next;
+    int root_c0 = 0, root_c1 = 0;
     Buf d_in, d_word_out, d_weight_out, d_node_out;
     std::mutex mu;
     DevVocab dev() const {
@@ -601,6 +652,10 @@ struct slam_vocab {
         V.is_leaf = d_leaf.as<uint8_t>();
         V.word = d_word.as<int32_t>();
         V.weight = d_weight.as<double>();
+        V.child_desc = d_child_desc.as<uint8_t>();
+        V.child_next = d_child_next.as<int4>();
+        V.root_c0 = root_c0;
+        V.root_c1 = root_c1;
         V.L = L;
         return V;
     }
@@ -650,8 +705,21 @@ slam_status slamhot_vocab_create(int device, int k, int L, int scoring, int weig
     std::vector<uint8_t> leaf(is_leaf, is_leaf + n_nodes);
     for (int i = 0; i < n_nodes; i++)
         if (cnt[i] == 0) leaf[i] = 1;  // a childless node ends the descent
+    // per child slot: the child's descriptor and {its child range, node id | leaf << 31}
+    const size_t nslots = idx.size();
+    std::vector<uint8_t> cdesc(nslots * 32, 0);
+    std::vector<int32_t> cnext(nslots * 4, 0);
+    for (int c = 0; c < ptr[n_nodes]; c++) {
+        const int id = idx[c];
+        std::memcpy(&cdesc[(size_t)c * 32], desc + (size_t)id * 32, 32);
+        cnext[4 * (size_t)c] = ptr[id];
+        cnext[4 * (size_t)c + 1] = ptr[id + 1];
+        cnext[4 * (size_t)c + 2] = id | (leaf[id] ? (int32_t)0x80000000u : 0);
+    }
     slam_vocab* v = new slam_vocab();
     v->device = device;
+    v->root_c0 = ptr[0];
+    v->root_c1 = ptr[1];
     v->k = k;
     v->L = L;
     v->scoring = scoring;
@@ -664,14 +732,17 @@ slam_status slamhot_vocab_create(int device, int k, int L, int scoring, int weig
     slam_status st;
     if ((st = v->d_desc.ensure((size_t)n_nodes * 32)) || (st = v->d_child_ptr.ensure(ptr.size() * 4)) ||
         (st = v->d_child_idx.ensure(idx.size() * 4)) || (st = v->d_leaf.ensure(n_nodes)) ||
-        (st = v->d_word.ensure((size_t)n_nodes * 4)) || (st = v->d_weight.ensure((size_t)n_nodes * 8)))
+        (st = v->d_word.ensure((size_t)n_nodes * 4)) || (st = v->d_weight.ensure((size_t)n_nodes * 8)) ||
+        (st = v->d_child_desc.ensure(cdesc.size())) || (st = v->d_child_next.ensure(cnext.size() * 4)))
         return fail(st);
     if (hipMemcpy(v->d_desc.p, desc, (size_t)n_nodes * 32, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(v->d_child_ptr.p, ptr.data(), ptr.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(v->d_child_idx.p, idx.data(), idx.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(v->d_leaf.p, leaf.data(), n_nodes, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(v->d_word.p, word.data(), (size_t)n_nodes * 4, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(v->d_weight.p, weight, (size_t)n_nodes * 8, hipMemcpyHostToDevice) != hipSuccess)
+        hipMemcpy(v->d_weight.p, weight, (size_t)n_nodes * 8, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(v->d_child_desc.p, cdesc.data(), cdesc.size(), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(v->d_child_next.p, cnext.data(), cnext.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
         return fail(SLAM_EHIP);
     *out = v;
     return SLAM_OK;
@@ -720,7 +791,7 @@ void slamhot_vocab_destroy(slam_vocab* v) {
     (void)hipSetDevice(v->device);
     if (v->stream) (void)hipStreamSynchronize(v->stream);
     Buf* bufs[] = {&v->d_desc, &v->d_child_ptr, &v->d_child_idx, &v->d_leaf, &v->d_word, &v->d_weight,
-                   &v->d_in, &v->d_word_out, &v->d_weight_out, &v->d_node_out};
+                   &v->d_child_desc, &v->d_child_next, &v->d_in, &v->d_word_out, &v->d_weight_out, &v->d_node_out};
     for (Buf* b : bufs) b->release();
     if (v->stream) (void)hipStreamDestroy(v->stream);
     delete v;
@@ -744,7 +815,7 @@ slam_status slamhot_vocab_transform_device(slam_vocab* v, int n, const void* d_d
     if (n == 0) return SLAM_OK;
     SLAM_HIP_TRY(hipSetDevice(v->device));
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : v->stream;
-    const int blocks = (int)(((size_t)n * 16 + kVocThreads - 1) / kVocThreads);
+    const int blocks = (int)(((size_t)n * kVocG + kVocThreads - 1) / kVocThreads);
     hipLaunchKernelGGL(k_vocab_transform, dim3(blocks), dim3(kVocThreads), 0, s, v->dev(), n, (const uint8_t*)d_desc,
                        desc_stride, levelsup, (int32_t*)d_word_id, (double*)d_weight, (int32_t*)d_node_id,
                        (const int32_t*)nullptr, 1);
@@ -757,7 +828,7 @@ namespace {
 slam_status vocab_transform_frames(slam_vocab* v, int nframes, int cap, const void* d_desc, const int32_t* d_n,
                                    int levelsup, void* d_word_id, void* d_weight, void* d_node_id, hipStream_t s) {
     const size_t n = (size_t)nframes * cap;
-    const int blocks = (int)((n * 16 + kVocThreads - 1) / kVocThreads);
+    const int blocks = (int)((n * kVocG + kVocThreads - 1) / kVocThreads);
     hipLaunchKernelGGL(k_vocab_transform, dim3(blocks), dim3(kVocThreads), 0, s, v->dev(), (int)n, (const uint8_t*)d_desc, 32,
                        levelsup, (int32_t*)d_word_id, (double*)d_weight, (int32_t*)d_node_id, d_n, cap);
     SLAM_HIP_TRY(hipGetLastError());

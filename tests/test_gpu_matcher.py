@@ -44,6 +44,24 @@ def test_vocab_transform_bitexact(gpu_vocab, vocab_arrays, frames):
             assert np.array_equal(ng, no)
 
 
+@pytest.mark.parametrize("k,L", [(20, 3), (17, 3), (16, 4), (3, 6), (5, 1)])
+def test_vocab_transform_branching(k, L):
+    """Branching factors around the kernel's register-held child slots (16 per node): k > 16
+    takes the spill loop and reads the winner's record from memory, k <= 16 gets it from the
+    winning lane; L = 1 stops at the root's children.  Same words / weights / nodes as the
+    oracle descent (TemplatedVocabulary.h:1229-1271) at every levelsup."""
+    import slamhot
+    par, leaf, d, w = synth.vocab(k, L, 5)
+    v = slamhot.Vocabulary(par, leaf, d, w, k=k, L=L)
+    _, desc, _ = ob.extract(synth.frame(78, 640, 480))
+    for levelsup in sorted({0, 1, L}):
+        got = v.transform(desc, levelsup)
+        ref = ob.vocab_transform(par, leaf, d, w, L, desc, levelsup)
+        for x, y in zip(got, ref):
+            assert np.array_equal(x, y), (k, L, levelsup)
+    v.close()
+
+
 def _side(gpu_vocab, k, desc, valid):
     _, wt, nid = gpu_vocab.transform(desc, 4)
     return (desc, k["angle"], valid) + synth.feature_vector(nid, wt)
