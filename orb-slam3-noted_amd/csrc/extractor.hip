@@ -788,18 +788,34 @@ __host__ __device__ inline size_t octree_lds_bytes(int maxn, int keycap, int max
 
 constexpr int kKU = 8;  // keys per lane in flight in the octree key loops
 
-__global__ void __launch_bounds__(64) k_octree(Bufs b, int level0, int key_lds_cap, int max_cells) {
+#ifndef SLAMHOT_OCT_WAVES
+#define SLAMHOT_OCT_WAVES 4
+#endif
+constexpr int kOctWaves = SLAMHOT_OCT_WAVES;  // waves per (frame, level) of the multi-wave form
+
+// W waves per (frame, level): the key loops (gather, root / quadrant counts, key remap, best
+// key) are spread over all W waves; the node-list steps (prefix sums over at most a few hundred
+// nodes) stay on wave 0, whose results the others read from LDS after a barrier.  W = 1 is the
+// wave-only form (no workgroup barriers).
+template <int W>
+__global__ void __launch_bounds__(64 * W) k_octree(Bufs b, int level0, int key_lds_cap, int max_cells) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ int bc[8];  // scalars wave 0 hands to the other waves (W > 1)
+    constexpr int NT = 64 * W;
     const DevPlan& P = *b.plan;
     const int l = level0 + blockIdx.x, f = blockIdx.y;
     const DevLevel& L = P.lv[l];
     const int MAXN = P.max_nodes;
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = W == 1 ? 0 : tid >> 6;
+    auto sync = [&]() {
+        if constexpr (W == 1) wave_fence();
+        else __syncthreads();
+    };
 #ifdef SLAMHOT_OCTREE_TRACE
     // experiment builds only: phase timestamps of a few waves
     long long tr[24];
     int ntr = 0;
-    const bool trace = (f == 100 || f == 101) && lane == 0;
+    const bool trace = (f == 0 || f == 100 || f == 101) && tid == 0;
 #define OCT_MARK() do { if (trace && ntr < 24) tr[ntr++] = (long long)__builtin_amdgcn_s_memtime(); } while (0)
 #else
 #define OCT_MARK() do {} while (0)
@@ -834,15 +850,21 @@ __global__ void __launch_bounds__(64) k_octree(Bufs b, int level0, int key_lds_c
     const int cb = L.cell_begin, ncl = L.cell_end - L.cell_begin;
     const int32_t* ccount = b.cell_cnt + (size_t)f * P.ncells;
     int nk = 0;
-    for (int base = 0; base < ncl; base += 64) {
-        const int i = base + lane;
-        const int v = i < ncl ? ccount[cb + i] : 0;
-        int tot;
-        const int ex = wave_scan_excl(v, &tot);
-        if (i < ncl) coff[i] = nk + ex;
-        nk += tot;
+    if (wave == 0) {
+        for (int base = 0; base < ncl; base += 64) {
+            const int i = base + lane;
+            const int v = i < ncl ? ccount[cb + i] : 0;
+            int tot;
+            const int ex = wave_scan_excl(v, &tot);
+            if (i < ncl) coff[i] = nk + ex;
+            nk += tot;
+        }
+        if constexpr (W > 1) {
+            if (lane == 0) bc[0] = nk;
+        }
     }
-    wave_fence();
+    sync();
+    if constexpr (W > 1) nk = bc[0];
     const bool in_lds = nk <= key_lds_cap;
     uint32_t* keys = in_lds ? keys_l : b.keys_g + (size_t)f * P.key_slots + L.key_base;
     uint16_t* knode = in_lds ? knode_l : b.knode_g + (size_t)f * P.key_slots + L.key_base;
@@ -850,7 +872,7 @@ __global__ void __launch_bounds__(64) k_octree(Bufs b, int level0, int key_lds_c
         const uint32_t* src = b.cell_keys + ((size_t)f * P.ncells + cb) * P.slot_cap;
         const int steps = ncl > 1 ? 32 - __clz(ncl - 1) : 0;  // ceil(log2(ncl))
         constexpr int U = 8;
-        for (int k0 = lane; k0 < nk; k0 += U * 64) {
+        for (int k0 = tid; k0 < nk; k0 += U * NT) {
             // largest c with coff[c] <= k (a non-empty cell); extra steps keep lo == hi
             int lo[U], hi[U];
 #pragma unroll
@@ -858,7 +880,7 @@ __global__ void __launch_bounds__(64) k_octree(Bufs b, int level0, int key_lds_c
             for (int st = 0; st < steps; st++) {
 #pragma unroll
                 for (int u = 0; u < U; u++) {
-                    const int k = min(k0 + u * 64, nk - 1);
+                    const int k = min(k0 + u * NT, nk - 1);
                     const int mid = (lo[u] + hi[u] + 1) >> 1;
                     if (coff[mid] <= k) lo[u] = mid; else hi[u] = mid - 1;
                 }
@@ -866,36 +888,35 @@ __global__ void __launch_bounds__(64) k_octree(Bufs b, int level0, int key_lds_c
             uint32_t v[U];
 #pragma unroll
             for (int u = 0; u < U; u++) {
-                const int k = min(k0 + u * 64, nk - 1);
+                const int k = min(k0 + u * NT, nk - 1);
                 v[u] = src[(size_t)lo[u] * P.slot_cap + (k - coff[lo[u]])];
             }
 #pragma unroll
             for (int u = 0; u < U; u++) {
-                const int k = k0 + u * 64;
+                const int k = k0 + u * NT;
                 if (k < nk) keys[k] = pack_kp(kp_x(v[u]) - L.minBX, kp_y(v[u]) - L.minBY, kp_s(v[u]));
             }
         }
     }
-    wave_fence();
     OCT_MARK();
     const int N = L.nfeat;
     int32_t* out_cnt = b.ocnt + (size_t)f * P.nlevels + l;
     uint32_t* okp = b.okp + (size_t)f * P.kslots + L.kbase;
     if (nk == 0) {
-        if (lane == 0) *out_cnt = 0;
+        if (tid == 0) *out_cnt = 0;
         return;
     }
 
     // ---- roots (:541-583): key -> root (int)(x / hX); empty roots erased
-    if (lane < L.nIni) best[lane] = 0;
-    wave_fence();
-    for (int k0 = lane; k0 < nk; k0 += kKU * 64) {
+    if (tid < L.nIni) best[tid] = 0;
+    sync();
+    for (int k0 = tid; k0 < nk; k0 += kKU * NT) {
         uint32_t key[kKU];
 #pragma unroll
-        for (int u = 0; u < kKU; u++) key[u] = keys[min(k0 + 64 * u, nk - 1)];
+        for (int u = 0; u < kKU; u++) key[u] = keys[min(k0 + NT * u, nk - 1)];
 #pragma unroll
         for (int u = 0; u < kKU; u++) {
-            const int k = k0 + 64 * u;
+            const int k = k0 + NT * u;
             const int x = kp_x(key[u]);
             int r = 0;
             for (int i = 1; i < L.nIni; i++) r += x >= L.root_first_x[i];
@@ -905,9 +926,9 @@ __global__ void __launch_bounds__(64) k_octree(Bufs b, int level0, int key_lds_c
             }
         }
     }
-    wave_fence();
+    sync();
     int n = 0;
-    {
+    if (wave == 0) {
         const bool ne = lane < L.nIni && best[lane] > 0;
         const uint64_t m = __ballot(ne);
         if (ne) {
@@ -920,19 +941,20 @@ __global__ void __launch_bounds__(64) k_octree(Bufs b, int level0, int key_lds_c
         }
         n = __popcll(m);
     }
-    wave_fence();
-    for (int k0 = lane; k0 < nk; k0 += kKU * 64) {
+    sync();
+    if constexpr (W > 1) n = __popcll(__ballot(lane < L.nIni && best[lane] > 0));  // every wave: the same count
+    for (int k0 = tid; k0 < nk; k0 += kKU * NT) {
         int nd[kKU];
 #pragma unroll
-        for (int u = 0; u < kKU; u++) nd[u] = knode[min(k0 + 64 * u, nk - 1)];
+        for (int u = 0; u < kKU; u++) nd[u] = knode[min(k0 + NT * u, nk - 1)];
         uint16_t cm[kKU];
 #pragma unroll
         for (int u = 0; u < kKU; u++) cm[u] = cmap[nd[u]];
 #pragma unroll
         for (int u = 0; u < kKU; u++)
-            if (k0 + 64 * u < nk) knode[k0 + 64 * u] = cm[u];
+            if (k0 + NT * u < nk) knode[k0 + NT * u] = cm[u];
     }
-    wave_fence();
+    sync();
     OCT_MARK();
     int seq_next = L.nIni;
     int tprev = 0;  // children region [0, tprev) of the last pass
@@ -944,18 +966,18 @@ __global__ void __launch_bounds__(64) k_octree(Bufs b, int level0, int key_lds_c
         if (iter >= 512) { err |= kErrOctreeIters; break; }
         const int prev = n;
         // -- candidate set and quadrant counts
-        for (int i = lane; i < n; i += 64) {
+        for (int i = tid; i < n; i += NT) {
             cc[i] = make_uint4(0, 0, 0, 0);
             rnk[i] = -1;
         }
-        wave_fence();
-        // four keys per lane per step: their node loads overlap, then the four atomics
-        for (int k0 = lane; k0 < nk; k0 += kKU * 64) {
+        sync();
+        // kKU keys per lane per step: their node loads overlap, then the atomics
+        for (int k0 = tid; k0 < nk; k0 += kKU * NT) {
             int nd[kKU];
             uint32_t key[kKU];
 #pragma unroll
             for (int u = 0; u < kKU; u++) {
-                const int k = min(k0 + 64 * u, nk - 1);
+                const int k = min(k0 + NT * u, nk - 1);
                 nd[u] = knode[k];
                 key[u] = keys[k];
             }
@@ -965,125 +987,146 @@ __global__ void __launch_bounds__(64) k_octree(Bufs b, int level0, int key_lds_c
             for (int u = 0; u < kKU; u++) { c[u] = A.cnt[nd[u]]; xb[u] = A.xb[nd[u]]; yb[u] = A.yb[nd[u]]; }
 #pragma unroll
             for (int u = 0; u < kKU; u++)
-                if (k0 + 64 * u < nk && c[u] > 1 && (!careful || nd[u] < tprev))
+                if (k0 + NT * u < nk && c[u] > 1 && (!careful || nd[u] < tprev))
                     atomicAdd(&ccu[nd[u] * 4 + quadrant_of(key[u], xb[u], yb[u])], 1u);
         }
-        wave_fence();
+        sync();
         auto nonempty = [&](int nd) -> int {
             const uint4 q = cc[nd];
             return (q.x > 0) + (q.y > 0) + (q.z > 0) + (q.w > 0);
         };
-        int nsplit = 0;
-        if (!careful) {
-            // phase A: split every node with >1 key, push order = list order
-            for (int base = 0; base < n; base += 64) {
-                const int i = base + lane;
-                const bool c = i < n && A.cnt[i] > 1;
-                const uint64_t m = __ballot(c);
-                if (c) {
-                    const int ex = nsplit + mbcnt64(m, 0);
-                    rnk[i] = (int16_t)ex;
-                    ord[ex] = (uint16_t)i;
-                }
-                nsplit += __popcll(m);
-            }
-        } else {
-            // careful phase: E = children of the last pass with >1 key, ordered by
-            // (size desc, sequence desc) = (cnt desc, position asc) inside [0, tprev)
-            int ne = 0;
-            for (int ib = 0; ib < tprev; ib += 64) {
-                const int i = ib + lane;
-                const int ci = i < tprev ? A.cnt[i] : 0;
-                const uint64_t mi = __ballot(ci > 1);
-                ne += __popcll(mi);
-                int r = 0;
-                for (int jb = 0; jb < tprev; jb += 64) {
-                    const int cj = jb + lane < tprev ? A.cnt[jb + lane] : 0;
-                    const int jn = min(64, tprev - jb);
-                    for (int t = 0; t < jn; t++) {
-                        const int c = __builtin_amdgcn_readlane(cj, t);
-                        r += (c > 1) & ((c > ci) | ((c == ci) & (jb + t < i)));
+        // -- node-list steps on wave 0: split set, children offsets, the new list in B
+        int T = 0, U = 0, n_to_expand = 0;
+        bool overflow = false;
+        if (wave == 0) {
+            int nsplit = 0;
+            if (!careful) {
+                // phase A: split every node with >1 key, push order = list order
+                for (int base = 0; base < n; base += 64) {
+                    const int i = base + lane;
+                    const bool c = i < n && A.cnt[i] > 1;
+                    const uint64_t m = __ballot(c);
+                    if (c) {
+                        const int ex = nsplit + mbcnt64(m, 0);
+                        rnk[i] = (int16_t)ex;
+                        ord[ex] = (uint16_t)i;
                     }
+                    nsplit += __popcll(m);
                 }
-                if (ci > 1) ord[r] = (uint16_t)i;
+            } else {
+                // careful phase: E = children of the last pass with >1 key, ordered by
+                // (size desc, sequence desc) = (cnt desc, position asc) inside [0, tprev)
+                int ne = 0;
+                for (int ib = 0; ib < tprev; ib += 64) {
+                    const int i = ib + lane;
+                    const int ci = i < tprev ? A.cnt[i] : 0;
+                    const uint64_t mi = __ballot(ci > 1);
+                    ne += __popcll(mi);
+                    int r = 0;
+                    for (int jb = 0; jb < tprev; jb += 64) {
+                        const int cj = jb + lane < tprev ? A.cnt[jb + lane] : 0;
+                        const int jn = min(64, tprev - jb);
+                        for (int t = 0; t < jn; t++) {
+                            const int c = __builtin_amdgcn_readlane(cj, t);
+                            r += (c > 1) & ((c > ci) | ((c == ci) & (jb + t < i)));
+                        }
+                    }
+                    if (ci > 1) ord[r] = (uint16_t)i;
+                }
+                wave_fence();
+                // cut: first rank r with n + sum_{r'<=r}(nonempty-1) >= N (:728-729)
+                int firstcut = ne - 1, carry = 0;
+                for (int base = 0; base < ne; base += 64) {
+                    const int r = base + lane;
+                    const int v = r < ne ? nonempty(ord[r]) - 1 : 0;
+                    int tot;
+                    const int incl = carry + wave_scan_excl(v, &tot) + v;
+                    const uint64_t m = __ballot(r < ne && n + incl >= N);
+                    if (m) { firstcut = base + __ffsll((long long)m) - 1; break; }
+                    carry += tot;
+                }
+                nsplit = firstcut + 1;
+                for (int r = lane; r < nsplit; r += 64) rnk[ord[r]] = (int16_t)r;
             }
             wave_fence();
-            // cut: first rank r with n + sum_{r'<=r}(nonempty-1) >= N (:728-729)
-            int firstcut = ne - 1, carry = 0;
-            for (int base = 0; base < ne; base += 64) {
+            // -- children offsets in push order
+            for (int base = 0; base < nsplit; base += 64) {
                 const int r = base + lane;
-                const int v = r < ne ? nonempty(ord[r]) - 1 : 0;
+                const int v = r < nsplit ? nonempty(ord[r]) : 0;
                 int tot;
-                const int incl = carry + wave_scan_excl(v, &tot) + v;
-                const uint64_t m = __ballot(r < ne && n + incl >= N);
-                if (m) { firstcut = base + __ffsll((long long)m) - 1; break; }
-                carry += tot;
+                const int ex = wave_scan_excl(v, &tot);
+                if (r < nsplit) oarr[r] = T + ex;
+                T += tot;
             }
-            nsplit = firstcut + 1;
-            for (int r = lane; r < nsplit; r += 64) rnk[ord[r]] = (int16_t)r;
-        }
-        wave_fence();
-        // -- children offsets in push order
-        int T = 0;
-        for (int base = 0; base < nsplit; base += 64) {
-            const int r = base + lane;
-            const int v = r < nsplit ? nonempty(ord[r]) : 0;
-            int tot;
-            const int ex = wave_scan_excl(v, &tot);
-            if (r < nsplit) oarr[r] = T + ex;
-            T += tot;
-        }
-        if (T + (n - nsplit) > MAXN) { err |= kErrOctreeNodes; break; }
-        wave_fence();
-        // -- write the new list into B
-        int U = 0, nexp_local = 0;
-        for (int base = 0; base < n; base += 64) {
-            const int i = base + lane;
-            const bool valid = i < n;
-            const int r = valid ? rnk[i] : 0;
-            const bool uns = valid && r < 0;
-            const uint64_t m = __ballot(uns);
-            if (uns) {
-                const int pos = T + U + mbcnt64(m, 0);
-                B.xb[pos] = A.xb[i]; B.yb[pos] = A.yb[i];
-                B.cnt[pos] = A.cnt[i]; B.seq[pos] = A.seq[i];
-                cmap[i * 4] = (uint16_t)pos;
-            } else if (valid) {
-                const int o = oarr[r];
-                const uint32_t xb = A.xb[i], yb = A.yb[i];
-                const int x0 = (int)(xb & 0xFFFF), x1 = (int)(xb >> 16), y0 = (int)(yb & 0xFFFF), y1 = (int)(yb >> 16);
-                const int xm = x0 + ((x1 - x0 + 1) >> 1), ym = y0 + ((y1 - y0 + 1) >> 1);
-                const uint4 q4 = cc[i];
-                const uint32_t cq[4] = {q4.x, q4.y, q4.z, q4.w};
-                int kk = 0;
+            overflow = T + (n - nsplit) > MAXN;
+            if (!overflow) {
+                wave_fence();
+                // -- write the new list into B
+                int nexp_local = 0;
+                for (int base = 0; base < n; base += 64) {
+                    const int i = base + lane;
+                    const bool valid = i < n;
+                    const int r = valid ? rnk[i] : 0;
+                    const bool uns = valid && r < 0;
+                    const uint64_t m = __ballot(uns);
+                    if (uns) {
+                        const int pos = T + U + mbcnt64(m, 0);
+                        B.xb[pos] = A.xb[i]; B.yb[pos] = A.yb[i];
+                        B.cnt[pos] = A.cnt[i]; B.seq[pos] = A.seq[i];
+                        cmap[i * 4] = (uint16_t)pos;
+                    } else if (valid) {
+                        const int o = oarr[r];
+                        const uint32_t xb = A.xb[i], yb = A.yb[i];
+                        const int x0 = (int)(xb & 0xFFFF), x1 = (int)(xb >> 16), y0 = (int)(yb & 0xFFFF), y1 = (int)(yb >> 16);
+                        const int xm = x0 + ((x1 - x0 + 1) >> 1), ym = y0 + ((y1 - y0 + 1) >> 1);
+                        const uint4 q4 = cc[i];
+                        const uint32_t cq[4] = {q4.x, q4.y, q4.z, q4.w};
+                        int kk = 0;
 #pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    const int c = (int)cq[q];
-                    if (c > 0) {
-                        const int pos = T - 1 - (o + kk);
-                        const int nx0 = (q & 1) ? xm : x0, nx1 = (q & 1) ? x1 : xm;
-                        const int ny0 = (q & 2) ? ym : y0, ny1 = (q & 2) ? y1 : ym;
-                        B.xb[pos] = (uint32_t)nx0 | ((uint32_t)nx1 << 16);
-                        B.yb[pos] = (uint32_t)ny0 | ((uint32_t)ny1 << 16);
-                        B.cnt[pos] = c;
-                        B.seq[pos] = seq_next + o + kk;
-                        cmap[i * 4 + q] = (uint16_t)pos;
-                        nexp_local += c > 1;
-                        kk++;
+                        for (int q = 0; q < 4; q++) {
+                            const int c = (int)cq[q];
+                            if (c > 0) {
+                                const int pos = T - 1 - (o + kk);
+                                const int nx0 = (q & 1) ? xm : x0, nx1 = (q & 1) ? x1 : xm;
+                                const int ny0 = (q & 2) ? ym : y0, ny1 = (q & 2) ? y1 : ym;
+                                B.xb[pos] = (uint32_t)nx0 | ((uint32_t)nx1 << 16);
+                                B.yb[pos] = (uint32_t)ny0 | ((uint32_t)ny1 << 16);
+                                B.cnt[pos] = c;
+                                B.seq[pos] = seq_next + o + kk;
+                                cmap[i * 4 + q] = (uint16_t)pos;
+                                nexp_local += c > 1;
+                                kk++;
+                            }
+                        }
                     }
+                    U += __popcll(m);
+                }
+                n_to_expand = wave_sum(nexp_local);
+            }
+            if constexpr (W > 1) {
+                if (lane == 0) {
+                    bc[1] = T;
+                    bc[2] = U;
+                    bc[3] = n_to_expand;
+                    bc[4] = overflow;
                 }
             }
-            U += __popcll(m);
         }
-        const int n_to_expand = wave_sum(nexp_local);
-        wave_fence();
+        sync();
+        if constexpr (W > 1) {
+            T = bc[1];
+            U = bc[2];
+            n_to_expand = bc[3];
+            overflow = bc[4] != 0;
+        }
+        if (overflow) { err |= kErrOctreeNodes; break; }
         // -- remap keys
-        for (int k0 = lane; k0 < nk; k0 += kKU * 64) {
+        for (int k0 = tid; k0 < nk; k0 += kKU * NT) {
             int nd[kKU];
             uint32_t key[kKU];
 #pragma unroll
             for (int u = 0; u < kKU; u++) {
-                const int k = min(k0 + 64 * u, nk - 1);
+                const int k = min(k0 + NT * u, nk - 1);
                 nd[u] = knode[k];
                 key[u] = keys[k];
             }
@@ -1096,9 +1139,9 @@ __global__ void __launch_bounds__(64) k_octree(Bufs b, int level0, int key_lds_c
             for (int u = 0; u < kKU; u++) cm[u] = cmap[nd[u] * 4 + (r[u] >= 0 ? quadrant_of(key[u], xb[u], yb[u]) : 0)];
 #pragma unroll
             for (int u = 0; u < kKU; u++)
-                if (k0 + 64 * u < nk) knode[k0 + 64 * u] = cm[u];
+                if (k0 + NT * u < nk) knode[k0 + NT * u] = cm[u];
         }
-        wave_fence();
+        sync();
         { NodeArr t = A; A = B; B = t; }
         n = T + U;
         seq_next += T;
@@ -1113,32 +1156,32 @@ __global__ void __launch_bounds__(64) k_octree(Bufs b, int level0, int key_lds_c
     }
 
     // ---- retain the best key of each node (:740-758)
-    for (int i = lane; i < n; i += 64) best[i] = 0;
-    wave_fence();
-    for (int k0 = lane; k0 < nk; k0 += kKU * 64) {
+    for (int i = tid; i < n; i += NT) best[i] = 0;
+    sync();
+    for (int k0 = tid; k0 < nk; k0 += kKU * NT) {
         uint32_t key[kKU];
         int nd[kKU];
 #pragma unroll
         for (int u = 0; u < kKU; u++) {
-            const int k = min(k0 + 64 * u, nk - 1);
+            const int k = min(k0 + NT * u, nk - 1);
             key[u] = keys[k];
             nd[u] = knode[k];
         }
 #pragma unroll
         for (int u = 0; u < kKU; u++) {
-            const int k = k0 + 64 * u;
+            const int k = k0 + NT * u;
             if (k < nk) atomicMax(&best[nd[u]], ((uint32_t)kp_s(key[u]) << 24) | (uint32_t)(0xFFFFFF - k));
         }
     }
-    wave_fence();
+    sync();
     const int nout = min(n, L.kcap);
-    for (int i = lane; i < nout; i += 64) {
+    for (int i = tid; i < nout; i += NT) {
         const int k = 0xFFFFFF - (int)(best[i] & 0xFFFFFF);
         const uint32_t key = keys[k];
         okp[i] = pack_kp(kp_x(key) + L.minBX, kp_y(key) + L.minBY, kp_s(key));
     }
     if (n > L.kcap) err |= kErrOctreeNodes;
-    if (lane == 0) {
+    if (tid == 0) {
         *out_cnt = nout;
         if (err) atomicOr(&b.err[f], err);
     }
@@ -1147,8 +1190,8 @@ __global__ void __launch_bounds__(64) k_octree(Bufs b, int level0, int key_lds_c
     if (trace) {
         long long d[10] = {};
         for (int i = 1; i < ntr && i <= 10; i++) d[i - 1] = tr[i] - tr[i - 1];
-        printf("OCT f=%d l=%d nk=%d n=%d marks=%d: %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld tot=%lld\n", f, l, nk, n,
-               ntr, d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7], d[8], d[9], tr[ntr - 1] - tr[0]);
+        printf("OCT W=%d f=%d l=%d nk=%d n=%d marks=%d: %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld tot=%lld\n", W, f, l,
+               nk, n, ntr, d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7], d[8], d[9], tr[ntr - 1] - tr[0]);
     }
 #endif
 }
@@ -1765,7 +1808,9 @@ static slam_status ensure_plan(slam_extractor* ex, int W, int H) {
     ex->oct_small.keycap = keycap_for(96 * 1024);
     ex->oct_small.lds = octree_lds_bytes(P.max_nodes, ex->oct_small.keycap, max_cells);
     lds_attr = std::max(lds_attr, ex->oct_small.lds);
-    SLAM_HIP_TRY(hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize,
+    SLAM_HIP_TRY(hipFuncSetAttribute((const void*)k_octree<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds_attr));
+    SLAM_HIP_TRY(hipFuncSetAttribute((const void*)k_octree<kOctWaves>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds_attr));
     return SLAM_OK;
 }
@@ -1784,6 +1829,12 @@ static slam_status ensure_batch(slam_extractor* ex, int nframes, int cap) {
         return st;
     (void)cap;
     return SLAM_OK;
+}
+
+// "1" / "0" from the environment (A/B switches), else the default
+static bool env_flag(const char* name, bool dflt) {
+    const char* e = std::getenv(name);
+    return e ? std::strcmp(e, "0") != 0 : dflt;
 }
 
 // One frame range [f0, f0 + nframes) of a batch: every per-frame buffer is frame-major, so
@@ -1818,6 +1869,9 @@ static slam_status launch_range(slam_extractor* ex, int f0, int nframes, const u
     b.lap0 = lap0;
     b.lap1 = lap1;
     SLAM_HIP_TRY(hipMemsetAsync(b.err, 0, (size_t)nframes * 4, s));
+    // A/B switches: SLAMHOT_OCT_SMALL / SLAMHOT_OCT_L0 = 1 | 0 (multi-wave octree on / off)
+    static const bool oct_multi_small = env_flag("SLAMHOT_OCT_SMALL", true);
+    static const bool oct_multi_l0 = env_flag("SLAMHOT_OCT_L0", false);
     hipEvent_t e0 = nullptr;
     auto begin = [&](int, hipStream_t st_ = nullptr) {
         if (ex->profiling) { e0 = ex->ev(); (void)hipEventRecord(e0, st_ ? st_ : s); }
@@ -1881,8 +1935,14 @@ static slam_status launch_range(slam_extractor* ex, int f0, int nframes, const u
     const bool small = nframes <= kSmallBatch;
     for (int g = 0; g < (small ? 1 : ex->n_oct) && !SKIP(kStOctree); g++) {
         const slam_extractor::OctGroup& G = small ? ex->oct_small : ex->oct[g];
-        hipLaunchKernelGGL(k_octree, dim3(G.nl, nframes), dim3(64), G.lds, s, b, G.l0, G.keycap,
-                           ex->octree_max_cells);
+        // the per-image call (small batches) and, for large batches, level 0 run the multi-wave
+        // form; levels 1-7 of large batches one wave per (frame, level)
+        if (small ? oct_multi_small : (G.l0 == 0 && oct_multi_l0))
+            hipLaunchKernelGGL(k_octree<kOctWaves>, dim3(G.nl, nframes), dim3(64 * kOctWaves), G.lds, s, b, G.l0,
+                               G.keycap, ex->octree_max_cells);
+        else
+            hipLaunchKernelGGL(k_octree<1>, dim3(G.nl, nframes), dim3(64), G.lds, s, b, G.l0, G.keycap,
+                               ex->octree_max_cells);
     }
     end(kStOctree);
     begin(kStLayout);
