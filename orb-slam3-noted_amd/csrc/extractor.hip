@@ -1200,43 +1200,57 @@ __global__ void __launch_bounds__(64 * W) k_octree(Bufs b, int level0, int key_l
 // k_layout: output order of operator() (ORBextractor.cc:1100-1146), one workgroup per
 // frame.  Keypoints are visited level-major in octree order; those whose scaled x lies in
 // [lap0, lap1] are written from the back, the rest from the front; returns monoIndex.
+// The level-major order is the order of the keypoint slots (level l at kbase_l, its first
+// ocnt_l slots used), so each thread takes a run of consecutive slots and one block scan of
+// its (lapping, front) counts, packed in one int, places all of them.
 // ---------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_layout(Bufs b) {
     __shared__ int scratch[20];
     const DevPlan& P = *b.plan;
     const int f = blockIdx.x, tid = threadIdx.x, NT = blockDim.x;
     const int32_t* ocnt = b.ocnt + (size_t)f * P.nlevels;
-    int total = 0;
-    for (int l = 0; l < P.nlevels; l++) total += ocnt[l];
+    const int K = P.kslots, per = (K + NT - 1) / NT, s0 = min(tid * per, K), s1 = min(s0 + per, K);
     const float lap0 = (float)b.lap0, lap1 = (float)b.lap1;
-    int mono_carry = 0, stereo_carry = 0;
-    for (int l = 0; l < P.nlevels; l++) {
-        const DevLevel& L = P.lv[l];
-        const int n = ocnt[l];
-        const uint32_t* okp = b.okp + (size_t)f * P.kslots + L.kbase;
-        int32_t* oidx = b.oidx + (size_t)f * P.kslots + L.kbase;
-        for (int base = 0; base < n; base += NT) {
-            const int i = base + tid;
-            bool lap = false;
-            if (i < n) {
-                float x = (float)kp_x(okp[i]);
-                if (l != 0) x = x * L.scale;  // keypoint->pt *= scale (:1131-1133)
-                lap = x >= lap0 && x <= lap1;
-            }
-            int tot;
-            const int incl = block_scan_incl(lap ? 1 : 0, scratch, &tot);
-            if (i < n) {
-                const int ls = stereo_carry + incl - 1;          // laps before me (incl. me) - 1
-                const int lm = mono_carry + (i - base + 1) - incl;  // monos before me (incl. me)
-                oidx[i] = lap ? (total - 1 - ls) : (lm - 1);
-            }
-            stereo_carry += tot;
-            mono_carry += min(NT, n - base) - tot;
+    const uint32_t* okp = b.okp + (size_t)f * P.kslots;
+    int32_t* oidx = b.oidx + (size_t)f * P.kslots;
+    int total = 0, l = 0;
+    for (int i = 0; i < P.nlevels; i++) {
+        total += ocnt[i];
+        if (i > 0 && P.lv[i].kbase <= s0) l = i;  // level of this thread's first slot
+    }
+    // slot s: 0 unused, 1 front, 2 lapping
+    auto kind = [&](int s, int& lv) -> int {
+        while (lv + 1 < P.nlevels && s >= P.lv[lv + 1].kbase) lv++;
+        const DevLevel& L = P.lv[lv];
+        if (s - L.kbase >= ocnt[lv]) return 0;
+        float x = (float)kp_x(okp[s]);
+        if (lv != 0) x = x * L.scale;  // keypoint->pt *= scale (:1131-1133)
+        return x >= lap0 && x <= lap1 ? 2 : 1;
+    };
+    int nlap = 0, nfront = 0;
+    {
+        int lv = l;
+        for (int s = s0; s < s1; s++) {
+            const int k = kind(s, lv);
+            nlap += k == 2;
+            nfront += k == 1;
+        }
+    }
+    int tot;
+    const int packed = (nlap << 16) | nfront;  // both counts < 2^16 (slots per frame)
+    const int excl = block_scan_incl(packed, scratch, &tot) - packed;
+    int ls = excl >> 16, lm = excl & 0xFFFF;  // lapping / front keypoints before this run
+    {
+        int lv = l;
+        for (int s = s0; s < s1; s++) {
+            const int k = kind(s, lv);
+            if (k == 2) oidx[s] = total - 1 - ls++;
+            else if (k == 1) oidx[s] = lm++;
         }
     }
     if (tid == 0) {
         b.out_n[f] = total;
-        b.out_mono[f] = mono_carry;
+        b.out_mono[f] = tot & 0xFFFF;
         if (total > b.cap) atomicOr(&b.err[f], kErrCap);
     }
 }
