@@ -1883,9 +1883,10 @@ static slam_status launch_range(slam_extractor* ex, int f0, int nframes, const u
     b.lap0 = lap0;
     b.lap1 = lap1;
     SLAM_HIP_TRY(hipMemsetAsync(b.err, 0, (size_t)nframes * 4, s));
-    // A/B switches: SLAMHOT_OCT_SMALL / SLAMHOT_OCT_L0 = 1 | 0 (multi-wave octree on / off)
-    static const bool oct_multi_small = env_flag("SLAMHOT_OCT_SMALL", true);
-    static const bool oct_multi_l0 = env_flag("SLAMHOT_OCT_L0", false);
+    // A/B switches: SLAMHOT_OCT_SMALL / SLAMHOT_OCT_L0 = 1 | 0 (multi-wave octree on / off),
+    // read per call (a handle's captured graphs keep the setting they were captured with)
+    const bool oct_multi_small = env_flag("SLAMHOT_OCT_SMALL", true);
+    const bool oct_multi_l0 = env_flag("SLAMHOT_OCT_L0", false);
     hipEvent_t e0 = nullptr;
     auto begin = [&](int, hipStream_t st_ = nullptr) {
         if (ex->profiling) { e0 = ex->ev(); (void)hipEventRecord(e0, st_ ? st_ : s); }

@@ -144,6 +144,28 @@ def test_non_default_pyramid(gpu_extractor_factory, scale, levels, nf):
         assert np.array_equal(ex.pyramid_level(l), ref[l]), l
 
 
+@pytest.mark.parametrize("small,l0", [("1", "1"), ("0", "0")])
+def test_octree_wave_forms(gpu_extractor_factory, monkeypatch, small, l0):
+    """k_octree<4> (key loops over four waves, node-list scans on wave 0) and k_octree<1> give the
+    same keypoints: the per-image call (all levels in one launch) and a 10-frame batch (level 0 in
+    its own launch) with each form, bit-exact against the oracle.  Textured VGA frames put ~3.6k
+    candidates on level 0 (several key-loop rounds per wave) and reach the careful phase."""
+    monkeypatch.setenv("SLAMHOT_OCT_SMALL", small)
+    monkeypatch.setenv("SLAMHOT_OCT_L0", l0)
+    ex = gpu_extractor_factory(nfeatures=1000, max_size=(640, 480), max_batch=10)
+    for seed in (3, 91):
+        img = synth.frame(seed)
+        _compare(*ex(img), *ob.extract(img))
+    imgs = synth.frames(range(70, 80))
+    kps, desc, n, mono = ex.extract_batch(imgs)
+    for f in range(10):
+        ko, do, mo = ob.extract(imgs[f])
+        _compare(kps[f][: n[f]], desc[f][: n[f]], mono[f], ko, do, mo)
+    ex2 = gpu_extractor_factory(nfeatures=5000, max_size=(752, 480))  # Tracking's 5x init extractor
+    img = synth.frame(92, 752, 480)
+    _compare(*ex2(img), *ob.extract(img, ob.params(nfeatures=5000)))
+
+
 @pytest.mark.parametrize("graph", ["1", "0"])
 def test_host_call_graph_and_stream_paths(gpu_extractor_factory, monkeypatch, graph):
     """The per-image host-buffer call is captured as a HIP graph per shape (frame size, lapping
