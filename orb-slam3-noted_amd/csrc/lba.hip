@@ -995,6 +995,21 @@ __global__ void __launch_bounds__(256) k_schur_blocks(int nb_diag, int nblk, int
 // 512 threads and a 384-edge W chunk (55 KB): two workgroups per CU at <= 128 VGPRs.  Measured
 // and rejected: 768 / 1024 threads at 80 / 64 VGPRs (spills: 366 / 570 us vs 310 us per 128
 // config-4 windows).
+template <int R>
+__device__ __forceinline__ double row_ror(double v) {  // DPP row_ror:R on both halves of a double
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x120 + R, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x120 + R, 0xf, 0xf, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+// Sum over the lanes l, l^4, l^8, l^12 of a 16-lane DPP row (every lane): two row rotations
+// (VALU) instead of two ds_bpermute round trips per double (the sums of k_schur_rows' eight
+// contribution streams / lane quads; SLAMHOT_SR_SHFL keeps the __shfl_xor butterflies).
+__device__ __forceinline__ double sum_quads16(double v) {
+    v += row_ror<4>(v);
+    v += row_ror<8>(v);
+    return v;
+}
 constexpr int kSrThreads = 512, kSrGroups = kSrThreads / 32, kSrChunk = 384;
 
 // W rows [r0, r1) of pose i1's list into LDS (lane pair per edge, rows 3h..3h+2), and with kSb
@@ -1137,6 +1152,7 @@ __global__ void __launch_bounds__(kSrThreads) __attribute__((amdgpu_waves_per_eu
                 sr_fma(Wl + 18 * (r - r0) + 9 * h, lin + (long long)kHplStride * We[r - r0] + 9 * v, acc);
         }
         // butterflies over the wave (quads: lane bits 2..5; sb pairs: bits 1..5), then the waves
+#ifdef SLAMHOT_SR_SHFL
 #pragma unroll
         for (int k = 0; k < 9; k++)
 #pragma unroll
@@ -1145,6 +1161,21 @@ __global__ void __launch_bounds__(kSrThreads) __attribute__((amdgpu_waves_per_eu
         for (int k = 0; k < 3; k++)
 #pragma unroll
             for (int o = 2; o < 64; o <<= 1) sb[k] += __shfl_xor(sb[k], o, 64);
+#else
+#pragma unroll
+        for (int k = 0; k < 9; k++) {
+            acc[k] = sum_quads16(acc[k]);
+            acc[k] += __shfl_xor(acc[k], 16, 64);
+            acc[k] += __shfl_xor(acc[k], 32, 64);
+        }
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            sb[k] += row_ror<2>(sb[k]);  // pairs: lanes l, l^2 (same h) ...
+            sb[k] = sum_quads16(sb[k]);
+            sb[k] += __shfl_xor(sb[k], 16, 64);
+            sb[k] += __shfl_xor(sb[k], 32, 64);
+        }
+#endif
         const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
         if (ln < 4) {
 #pragma unroll
@@ -1217,10 +1248,18 @@ __global__ void __launch_bounds__(kSrThreads) __attribute__((amdgpu_waves_per_eu
                 rb = nb;
             }
         }
+#ifdef SLAMHOT_SR_SHFL
 #pragma unroll
         for (int t = 0; t < 9; t++)
 #pragma unroll
             for (int o = 4; o < 32; o <<= 1) acc[t] += __shfl_xor(acc[t], o, 32);
+#else
+#pragma unroll
+        for (int t = 0; t < 9; t++) {
+            acc[t] = sum_quads16(acc[t]);
+            acc[t] += __shfl_xor(acc[t], 16, 32);
+        }
+#endif
         if (live) {
             // every stream of a quad lane holds the sums: stream j writes element j (and 0 also 8)
 #pragma unroll
@@ -1487,13 +1526,6 @@ struct T16Lds {
 };
 __host__ __device__ constexpr long long t16_tiles_bytes() { return (long long)kT16Tiles * 256 * sizeof(double); }
 
-template <int R>
-__device__ __forceinline__ double row_ror(double v) {  // DPP row_ror:R on both halves of a double
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x120 + R, 0xf, 0xf, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x120 + R, 0xf, 0xf, false);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
 __device__ __forceinline__ double t16_sum16(double v) {  // sum over the 16 lanes of a DPP row (every lane)
     v += row_ror<8>(v);
     v += row_ror<4>(v);
