@@ -116,11 +116,36 @@ __device__ inline void pjac(const PEdge& e, const double* P, const PFrame& F, do
     }
 }
 
+#ifndef SLAMHOT_POSE_SHFL
+// wave sum by DPP (VALU; every lane of the wave active): row sums by row_ror 8 / 4 / 2 / 1, the
+// rows combined by row_bcast:15 and row_bcast:31 into lane 63, read back as a uniform value.
+// Fixed order ((r2 + r3) + (r0 + r1)); replaces six ds_bpermute round trips per double (the
+// 28-value reduction of every LM step).  SLAMHOT_POSE_SHFL keeps the xor butterfly.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_d(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, ROWS, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROWS, 0xf, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ inline double wsum(double v) {
+    v += dpp_d<0x128, 0xf>(v);  // row_ror:8
+    v += dpp_d<0x124, 0xf>(v);  // row_ror:4
+    v += dpp_d<0x122, 0xf>(v);  // row_ror:2
+    v += dpp_d<0x121, 0xf>(v);  // row_ror:1
+    v += dpp_d<0x142, 0xa>(v);  // row_bcast:15 -> rows 1, 3
+    v += dpp_d<0x143, 0xc>(v);  // row_bcast:31 -> rows 2, 3
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, 63), hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+#else
 __device__ inline double wsum(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
+#endif
 
 // unpivoted LDL^T of a 6x6 SPD matrix; fails on a negative pivot (Eigen LDLT::isPositive)
 __device__ inline bool solve6(const double* M, const double* rhs, double* out) {
