@@ -390,12 +390,37 @@ __device__ __forceinline__ void lin_points_body(int p, int npt_total, const int*
     *(double4_t*)(bl + 4 * (long long)p) = double4_t{bb[0], bb[1], bb[2], 0.0};
 }
 
-// wave-wide sum by xor butterfly (fixed order: every lane ends with the same total)
+// wave-wide sum in a fixed order, every lane ends with the same total (every lane of the wave
+// must be active).  DPP form: row sums by row_ror 8 / 4 / 2 / 1, rows combined by row_bcast:15 /
+// row_bcast:31 into lane 63 ((r2 + r3) + (r0 + r1)), read back uniform: VALU instead of six
+// ds_bpermute round trips per double (k_linearize's 27 pose sums per KeyFrame, the chi2 sums).
+// SLAMHOT_LBA_SHFL keeps the xor butterfly.
+#ifndef SLAMHOT_LBA_SHFL
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_d(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, ROWS, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROWS, 0xf, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ inline double wave_sum(double v) {
+    v += dpp_d<0x128, 0xf>(v);  // row_ror:8
+    v += dpp_d<0x124, 0xf>(v);  // row_ror:4
+    v += dpp_d<0x122, 0xf>(v);  // row_ror:2
+    v += dpp_d<0x121, 0xf>(v);  // row_ror:1
+    v += dpp_d<0x142, 0xa>(v);  // row_bcast:15 -> rows 1, 3
+    v += dpp_d<0x143, 0xc>(v);  // row_bcast:31 -> rows 2, 3
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, 63), hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+#else
 __device__ inline double wave_sum(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
+#endif
 
 // Pose side of buildSystem: one wave per free KeyFrame, lanes stride over its edges and
 // recompute error, robust weight and the pose Jacobian B; Hpp = sum B^T W B,
