@@ -2501,7 +2501,12 @@ slam_status plan_fill(int n_prob, const slam_lba_problem* probs, const std::vect
         (void)nkf;
         return SLAM_OK;
     };
-    const int hw = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    // a few threads per call: callers run several solvers at once (the bench's LBA leg: 4), and
+    // 16 planning threads per call oversubscribed the GPU box's 16-thread CPU share, delaying
+    // the solver threads that launch the next LM step (SLAMHOT_LBA_PLAN_THREADS overrides)
+    static const int cap_env = std::getenv("SLAMHOT_LBA_PLAN_THREADS") ? std::atoi(std::getenv("SLAMHOT_LBA_PLAN_THREADS")) : 0;
+    const int cap = cap_env > 0 ? cap_env : 4;
+    const int hw = (int)std::max(1u, std::min((unsigned)cap, std::thread::hardware_concurrency()));
     const int nth = std::min(hw, n_prob);
     std::vector<slam_status> rs(nth, SLAM_OK);
     auto run = [&](int t) {
