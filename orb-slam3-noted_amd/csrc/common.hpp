@@ -33,23 +33,25 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 // Inclusive block-wide scan of one int per thread (blockDim.x multiple of 64, <= 1024).
 // `scratch` needs blockDim.x/64 + 1 ints of LDS.  Returns the inclusive prefix; *total
 // receives the block sum.
+// Inclusive scan of one int per lane over a full wave by DPP (row_shr 1/2/4/8 Kogge-Stone inside
+// each 16-lane row, then row_bcast:15 / row_bcast:31 across rows): VALU, no ds_bpermute.
+__device__ __forceinline__ int wave_scan_incl_dpp(int x) {
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, true);   // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, true);   // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, true);   // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, true);   // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+    return x;
+}
+
 __device__ __forceinline__ int block_scan_incl(int v, int* scratch, int* total) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    int x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        int y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
+    const int x = wave_scan_incl_dpp(v);
     if (lane == 63) scratch[wid] = x;
     __syncthreads();
     if (wid == 0) {
-        int s = lane < nw ? scratch[lane] : 0;
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-            int y = __shfl_up(s, o, 64);
-            if (lane >= o) s += y;
-        }
+        const int s = wave_scan_incl_dpp(lane < nw ? scratch[lane] : 0);
         if (lane < nw) scratch[lane] = s;
     }
     __syncthreads();
