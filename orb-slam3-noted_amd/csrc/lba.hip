@@ -98,7 +98,10 @@ struct Counters {
 
 struct Cam {
     double fx, fy, cx, cy, bf;
-    float bff;
+    // mbf as the float the reference multiplies with, held as a double: a float field here was
+    // merged with the per-KeyFrame kbf[kf] load into a load through a selected pointer, which put
+    // this by-value kernel argument in scratch (a private segment in every kernel taking a Cam)
+    double bff;
     double fx2, fy2, cx2, cy2;  // mpCamera2 (body edges)
     const double* trl;          // per global KF: mTrl as a pose record (NULL without body edges)
     // per global KF: its own camera as 8 floats {fx, fy, cx, cy, fx2, fy2, cx2, cy2} and its bf
@@ -113,7 +116,7 @@ struct Intr {
     float bff;
 };
 __device__ __forceinline__ Intr left_cam(const Cam& c, int kf) {
-    if (!c.kcam) return Intr{c.fx, c.fy, c.cx, c.cy, c.bf, c.bff};
+    if (!c.kcam) return Intr{c.fx, c.fy, c.cx, c.cy, c.bf, (float)c.bff};
     const float4 a = c.kcam[2 * (long long)kf];
     const float bf = c.kbf[kf];
     return Intr{a.x, a.y, a.z, a.w, bf, bf};
@@ -2699,7 +2702,7 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     cam.cx = Z.cam.cx;
     cam.cy = Z.cam.cy;
     cam.bf = Z.cam.bf;
-    cam.bff = Z.cam.bf;
+    cam.bff = (double)(float)Z.cam.bf;
     cam.trl = Z.any_body ? DP.kf_trl : nullptr;
     cam.fx2 = Z.cam2.fx;
     cam.fy2 = Z.cam2.fy;

@@ -214,7 +214,7 @@ __global__ void __launch_bounds__(kThreads) k_pose_opt(const PFrame* __restrict_
                                                        uint8_t* __restrict__ level, uint8_t* __restrict__ outlier,
                                                        POut* __restrict__ out, Hub hub) {
     __shared__ Shared sh;
-    const PFrame F = frames[blockIdx.x];
+    const PFrame& F = frames[blockIdx.x];  // by reference: F.Tcw[tid] below would put a copy in scratch
     const int tid = threadIdx.x;
     const int e0 = F.e0, ne = F.ne;
     if (tid == 0) {

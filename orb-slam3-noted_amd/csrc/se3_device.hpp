@@ -12,6 +12,26 @@ struct Quat {
     double x, y, z, w;
 };
 
+// Eigen's Quaternion(Matrix3) off the positive-trace branch, with the largest diagonal index I as
+// a template argument: constant indices keep R and c in registers (a runtime i put a 3x3 array in
+// scratch, giving every kernel that converts a rotation a private segment)
+template <int I>
+__host__ __device__ inline Quat quat_from_R_diag(const double* R) {
+    constexpr int J = (I + 1) % 3, K = (J + 1) % 3;
+    Quat q;
+    double c[3];
+    double t = sqrt(R[4 * I] - R[4 * J] - R[4 * K] + 1.0);
+    c[I] = 0.5 * t;
+    t = 0.5 / t;
+    q.w = (R[3 * K + J] - R[3 * J + K]) * t;
+    c[J] = (R[3 * J + I] + R[3 * I + J]) * t;
+    c[K] = (R[3 * K + I] + R[3 * I + K]) * t;
+    q.x = c[0];
+    q.y = c[1];
+    q.z = c[2];
+    return q;
+}
+
 __host__ __device__ inline Quat quat_from_R(const double* R) {
     Quat q;
     double t = R[0] + R[4] + R[8];
@@ -27,18 +47,7 @@ __host__ __device__ inline Quat quat_from_R(const double* R) {
     int i = 0;
     if (R[4] > R[0]) i = 1;
     if (R[8] > R[4 * i]) i = 2;
-    const int j = (i + 1) % 3, k = (j + 1) % 3;
-    double c[3];
-    t = sqrt(R[4 * i] - R[4 * j] - R[4 * k] + 1.0);
-    c[i] = 0.5 * t;
-    t = 0.5 / t;
-    q.w = (R[3 * k + j] - R[3 * j + k]) * t;
-    c[j] = (R[3 * j + i] + R[3 * i + j]) * t;
-    c[k] = (R[3 * k + i] + R[3 * i + k]) * t;
-    q.x = c[0];
-    q.y = c[1];
-    q.z = c[2];
-    return q;
+    return i == 0 ? quat_from_R_diag<0>(R) : i == 1 ? quat_from_R_diag<1>(R) : quat_from_R_diag<2>(R);
 }
 
 __host__ __device__ inline void normalize_rotation(Quat& q) {
