@@ -1762,6 +1762,8 @@ static slam_status ensure_plan(slam_extractor* ex, int W, int H) {
             // ROI rows: staged dwords reach byte sh + cw + 3 and pass A reads one dword past its
             // last group, so cw + 8 bytes (rounded to dwords) cover every access
             lay.rs = std::min(kRoiStride, (cw_max + 8 + 3) & ~3);
+            // SLAMHOT_FAST_RS_PAD=<dwords>: extra ROI row stride (LDS bank-spread probe)
+            if (const char* e = std::getenv("SLAMHOT_FAST_RS_PAD")) lay.rs += 4 * std::max(0, std::atoi(e));
             lay.ms = tw_max + 2;
             lay.roi = 0;
             lay.map = r16(ch_max * lay.rs);
