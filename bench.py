@@ -289,8 +289,8 @@ def main():
 # ------------------------------------------------------------------------------------------
 # headline: configs[2] stereo extract + match
 # ------------------------------------------------------------------------------------------
-SEQ_LEN = 8      # consecutive frames per synthetic sequence chunk
-N_SEQ = 2        # distinct sequences per rank
+SEQ_LEN = 8      # consecutive frames per synthetic sequence chunk (frame j's KF is frame j - 1)
+SEQ_RENDER = 64  # frames per rendered sequence (one textured room per sequence)
 
 
 def euroc_maps():
@@ -301,15 +301,27 @@ def euroc_maps():
                                              (752, 480)) for sd in ("LEFT", "RIGHT")]
 
 
-def stereo_chunks(rank, maps):
-    """N_SEQ rendered sequences of SEQ_LEN raw stereo frames for this rank: (raw L, raw R)."""
+def stereo_chunks(rank, maps, nframes):
+    """nframes distinct raw stereo frames for this rank (raw L, raw R): rendered sequences of up
+    to SEQ_RENDER frames, cut into chunks of SEQ_LEN consecutive frames; rendered and unrectified
+    on the host threads before the timed region."""
+    from concurrent.futures import ThreadPoolExecutor
+
     from slamhot import synth
+    th = host_cores()
     Ls, Rs = [], []
-    for s in range(N_SEQ):
-        L, R, _ = synth.stereo_sequence(101 + 17 * rank + s, SEQ_LEN)
-        Ls += [synth.unrectify(im, *maps[0]) for im in L]
-        Rs += [synth.unrectify(im, *maps[1]) for im in R]
-    return np.stack(Ls), np.stack(Rs)
+    nseq = (nframes + SEQ_RENDER - 1) // SEQ_RENDER
+    for s in range(nseq):
+        n = min(SEQ_RENDER, nframes - s * SEQ_RENDER)
+        # sequence seeds follow the global frame order (rank r holds global sequences r * nseq + s), so
+        # one process rendering world x nframes frames (a multiple of SEQ_RENDER) sees the same frames
+        L, R, _ = synth.stereo_sequence(101 + rank * nseq + s, n, threads=th)
+        Ls += list(L)
+        Rs += list(R)
+    with ThreadPoolExecutor(th) as pool:
+        rl = list(pool.map(lambda im: synth.unrectify(im, *maps[0]), Ls))
+        rr = list(pool.map(lambda im: synth.unrectify(im, *maps[1]), Rs))
+    return np.stack(rl), np.stack(rr)
 
 
 def kf_of(i):
@@ -328,11 +340,10 @@ def headline_leg(ctx):
     W, H, NF = 752, 480, 1200
     P = max(SEQ_LEN, args.pairs // SEQ_LEN * SEQ_LEN)
     maps = euroc_maps()
-    raw_l, raw_r = stereo_chunks(ctx["rank"], maps)
+    raw_l, raw_r = stereo_chunks(ctx["rank"], maps, P)
     ctx["chunks"] = (raw_l, raw_r)
-    nu = len(raw_l)
-    il = np.stack([raw_l[i % nu] for i in range(P)])
-    ir = np.stack([raw_r[i % nu] for i in range(P)])
+    nu = len(raw_l)  # every frame of the batch is distinct
+    il, ir = raw_l, raw_r
     pairs = [(kf_of(i), i) for i in range(P)]
     mbf = synth.EUROC_STEREO["bf"]
     mb = mbf / synth.EUROC_STEREO["fx"]
@@ -419,9 +430,9 @@ def headline_leg(ctx):
     ur_h = s0.ur.cpu().numpy()
     skipped = s0.m.bow_match_batch_status(s0.stream.cuda_stream)
     kps_per_frame = float(nl_h.mean())
-    # parity digest over this rank's UNIQUE frames (the batch repeats them P / nu times): per
-    # frame a hash of its keypoints, descriptors, stereo uR and both match directions, mixed with
-    # the frame's global index (rank * nu + i), summed (slamhot.dist.unit_hash / combine)
+    # parity digest over this rank's frames (all distinct): per frame a hash of its keypoints,
+    # descriptors, stereo uR and both match directions, mixed with the frame's global index
+    # (rank * nu + i), summed (slamhot.dist.unit_hash / combine)
     kk, dd = s0.out[0][0].cpu().numpy(), s0.out[0][1].cpu().numpy()
     a2b_h, b2a_h = s0.a2b.cpu().numpy(), s0.b2a.cpu().numpy()
     nuniq = min(nu, P)
@@ -438,7 +449,8 @@ def headline_leg(ctx):
                         f"ORBextractor x2 ({NF} feat, 8 levels, 1.2, 20/7) -> ComputeStereoMatches -> ComputeBoW "
                         f"-> SearchByBoW(previous frame as KF, F) (nnratio 0.7, checkOri); synthetic k=10 L=6 "
                         f"vocabulary",
-            "stereo_frames_per_gpu_per_step": P, "parallelism": f"frame-sharded x{ctx['world']}",
+            "stereo_frames_per_gpu_per_step": P, "distinct_frames_per_gpu": nu,
+            "parallelism": f"frame-sharded x{ctx['world']}",
             "batches_in_flight": NS, "keypoints_per_frame": round(kps_per_frame, 1),
         },
         "roofline": roofline_from_stages(stages, nprof, P, W, H, kps_per_frame),
@@ -449,7 +461,9 @@ def headline_leg(ctx):
         "bow_general_pairs": skipped,
         "rank_digests": [d for _, d in digs],
         "digest": {"units_per_rank": nuniq, "job": sdist.combine(d for _, d in digs),
-                   "what": "sum over unique frames of BLAKE2b(global frame index, keypoints, descriptors, "
+                   "what": "rank_digests: per rank, reproducible run to run; job: their sum, equal to one process's "
+                           "digest over world x frames since frame content follows the global frame index; each term "
+                           "= sum over frames of BLAKE2b(global frame index, keypoints, descriptors, "
                            "mvuRight, SearchByBoW a2b / b2a, nmatches) mod 2^62"},
     }
     if ctx["cpu"]:
@@ -476,15 +490,19 @@ def headline_cpu(raw_l, raw_r, maps, voc_arrays, mbf, mb, NF):
     p = ob.params(nfeatures=NF)
     sc, isc, _, _, _ = ob.levels(p)
 
+    nch = len(raw_l) // SEQ_LEN
+
     def chunk(c):
         prev = None
-        base = (c % N_SEQ) * SEQ_LEN
+        base = (c % nch) * SEQ_LEN
         for j in range(SEQ_LEN):
             l_img = ob.remap_linear(raw_l[base + j], *maps[0])
             r_img = ob.remap_linear(raw_r[base + j], *maps[1])
-            kl, dl, _ = ob.extract(l_img, p)
-            kr, dr, _ = ob.extract(r_img, p)
-            ob.stereo_matches(kl, dl, kr, dr, ob.pyramid(l_img, p), ob.pyramid(r_img, p), sc, isc, mbf, mb)
+            # the stereo matcher reads the pyramids the two extractions built (mvImagePyramid,
+            # Frame.cc:801, 891), as the reference does
+            kl, dl, _, pl = ob.extract_with_pyramid(l_img, p)
+            kr, dr, _, pr = ob.extract_with_pyramid(r_img, p)
+            ob.stereo_matches(kl, dl, kr, dr, pl, pr, sc, isc, mbf, mb)
             _, wt, nid = ob.vocab_transform(par, leaf, dn, wn, 6, dl, 4)
             side = (dl, kl["angle"], None) + synth.feature_vector(nid, wt)
             if prev is not None:
@@ -501,9 +519,10 @@ def headline_cpu(raw_l, raw_r, maps, voc_arrays, mbf, mb, NF):
     dt = time.perf_counter() - t0
     return {"value": round(frames / dt, 2), "unit": "frames/s", "cores": cores, "kind": "port",
             "cpu": cpu_model(),
-            "sample": f"{nchunks} sequence chunks x {SEQ_LEN} stereo frames, one chunk per thread on {cores} "
-                      f"threads: oracle remap x2 + extract x2 (+ the stereo pyramids) + stereo_oracle + vocabulary "
-                      f"transform + FeatureVector + SearchByBoW; oracle -O3"}
+            "sample": f"{nchunks} sequence chunks x {SEQ_LEN} stereo frames (the headline's distinct frames), one "
+                      f"chunk per thread on {cores} threads: oracle remap x2 + extract x2 (each leaving its "
+                      f"mvImagePyramid) + stereo_oracle on those pyramids + vocabulary transform + FeatureVector + "
+                      f"SearchByBoW; oracle -O3"}
 
 
 # ------------------------------------------------------------------------------------------
@@ -996,7 +1015,7 @@ def track_leg(ctx):
     lock-step, one raw stereo frame each per step, through the whole device-resident chain
     (remap x2, extract x2, stereo, BoW + SearchByBoW vs the reference KF, PoseOptimization,
     SearchLocalPoints, PoseOptimization, keyframe insertion).  Sequence s replays rendered chunk
-    s % N_SEQ back and forth (a continuous path).  value = sequence-frames/s of the whole job."""
+    s % (number of chunks) back and forth (a continuous path).  value = sequence-frames/s of the whole job."""
     import torch
 
     import slamhot
@@ -1007,7 +1026,8 @@ def track_leg(ctx):
     S, K = args.track_seqs, args.track_frames
     W, H = 752, 480
     maps = euroc_maps()
-    raw_l, raw_r = ctx.get("chunks") or stereo_chunks(ctx["rank"], maps)
+    raw_l, raw_r = ctx.get("chunks") or stereo_chunks(ctx["rank"], maps, 2 * SEQ_LEN)
+    nch = len(raw_l) // SEQ_LEN
     voc_arrays = sdist.broadcast_arrays(dist, device, synth.vocab(10, 6, 0) if ctx["rank"] == 0 else None)
     voc = slamhot.Vocabulary(*voc_arrays, k=10, L=6, device=lr)
     cam = (np.float32(synth.EUROC_STEREO["fx"]), np.float32(synth.EUROC_STEREO["fx"]), np.float32(367.4517211914062),
@@ -1015,7 +1035,7 @@ def track_leg(ctx):
     # device frames: d_l[f] holds frame f of every sequence
     d_l, d_r = [], []
     for f in range(SEQ_LEN):
-        idx = [(s % N_SEQ) * SEQ_LEN + f for s in range(S)]
+        idx = [(s % nch) * SEQ_LEN + f for s in range(S)]
         d_l.append(torch.from_numpy(np.ascontiguousarray(raw_l[idx])).to(device))
         d_r.append(torch.from_numpy(np.ascontiguousarray(raw_r[idx])).to(device))
     order = pingpong(SEQ_LEN, K)
@@ -1091,9 +1111,11 @@ def track_cpu(raw_l, raw_r, maps, voc_arrays, order):
     P = to.params()
     cores = host_cores()
 
+    nch = len(raw_l) // SEQ_LEN
+
     def run(c):
         st = to.SeqState()
-        base = (c % N_SEQ) * SEQ_LEN
+        base = (c % nch) * SEQ_LEN
         for f in order:
             to.step(P, voc_arrays, maps, st, raw_l[base + f], raw_r[base + f])
         return len(order)

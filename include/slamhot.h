@@ -169,6 +169,21 @@ slam_status slamhot_vocab_info(const slam_vocab* v, int* k, int* L, int* n_nodes
  * (features with weight <= 0 are dropped, :1169). */
 slam_status slamhot_vocab_transform(slam_vocab* v, int n, const uint8_t* desc, int levelsup,
                                     int32_t* word_id, double* weight, int32_t* node_id);
+/* void TemplatedVocabulary::transform(const vector<TDescriptor>& features, BowVector& v,
+ * FeatureVector& fv, int levelsup) (TemplatedVocabulary.h:1139-1206), the whole body of
+ * Frame::ComputeBoW / KeyFrame::ComputeBoW (Frame.cc:721-728, KeyFrame.cc:105-114): the descent of
+ * every descriptor on the device, then DBoW2's BowVector and FeatureVector on the host exactly as
+ * the reference builds them — features whose word weight is <= 0 dropped (:1169); TF_IDF / TF:
+ * BowVector::addWeight (sum in feature order), divided by the word count when the scoring does not
+ * normalise (:1174-1180); IDF / BINARY: addIfNotExist (first weight, :1195); then the scoring's
+ * L1 / L2 normalisation (BowVector.cpp:62-84; L1 for L1 / chi-square / KL / Bhattacharyya, none for
+ * dot product).  Outputs, caller-owned with room for n entries (n + 1 for fv_off):
+ *   BowVector:     *n_words pairs (bow_word ascending, bow_value)
+ *   FeatureVector: *n_nodes nodes (fv_node ascending), node j's features fv_feat[fv_off[j] ..
+ *                  fv_off[j+1]) ascending (FeatureVector::addFeature, FeatureVector.cpp:31-45). */
+slam_status slamhot_compute_bow(slam_vocab* v, int n, const uint8_t* desc, int levelsup, int* n_words,
+                                uint32_t* bow_word, double* bow_value, int* n_nodes, uint32_t* fv_node,
+                                int32_t* fv_off, uint32_t* fv_feat);
 /* Device-resident form: d_desc n x 32 (row stride desc_stride bytes), outputs on device. */
 slam_status slamhot_vocab_transform_device(slam_vocab* v, int n, const void* d_desc,
                                            int desc_stride, int levelsup, void* d_word_id,
@@ -291,6 +306,11 @@ typedef struct slam_last_frame {
     const uint8_t* mp_has_obs;
 } slam_last_frame;
 
+/* f_match[i] (F->n entries) for this and slamhot_search_by_projection_kf: the LastFrame / KeyFrame
+ * feature whose MapPoint this call wrote into CurrentFrame.mvpMapPoints[i] (the last assignment
+ * wins), -1 if the call left entry i untouched, -2 if it assigned entry i and the rotation check
+ * then set it to NULL (ORBmatcher.cc:2366-2386, 2491-2510: that NULL overwrites whatever the entry
+ * held before the call). */
 slam_status slamhot_search_by_projection_last(slam_matcher* m, const slam_frame_view* F,
                                               const slam_last_frame* LF, float nnratio, int check_ori,
                                               float th, int mono, int32_t* f_match, int* nmatches);
@@ -407,7 +427,9 @@ typedef struct slam_lba_options {
                                    bool is one byte), polled live like the int32 stop_flag */
     /* optional diagnostic hook (NULL = none): called on the calling thread each time the host has
      * seen the counters of an LM step, with the step's number (0-based over the whole call).  A
-     * hook that sets the stop flag stops the solve at a chosen step, independent of timing. */
+     * hook that sets the stop flag at step k stops the solve within the steps already queued
+     * behind k (at most 3 more: the host keeps a ring of 4 steps in flight), the same bound
+     * g2o's asynchronous terminate() check has; the step it lands on depends on timing. */
     void (*step_hook)(void* ctx, int32_t step);
     void* step_hook_ctx;
 } slam_lba_options;

@@ -188,6 +188,52 @@ inline std::vector<float> ComputeImageBounds(const PinholeCalib& c, int cols, in
 }
 
 /* ------------------------------------------------------------------------------------
+ * ORBVocabulary = DBoW2::TemplatedVocabulary<FORB::TDescriptor, FORB> (ORBVocabulary.h:29-30),
+ * resident on one device.  DBoW2::BowVector / FeatureVector come back as sorted pairs, the order
+ * their std::maps iterate in.
+ * ---------------------------------------------------------------------------------- */
+using BowVector = std::vector<std::pair<uint32_t, double>>;                   // (WordId, WordValue)
+using FeatureVector = std::vector<std::pair<uint32_t, std::vector<uint32_t>>>;  // (NodeId, features)
+
+class Vocabulary {
+   public:
+    /* bool loadFromTextFile(const std::string&) (TemplatedVocabulary.h:1350-1436): ORBvoc.txt */
+    explicit Vocabulary(const std::string& path, int device = 0) {
+        check(slamhot_vocab_load_text(device, path.c_str(), &v_), "ORBVocabulary::loadFromTextFile");
+    }
+    /* a node table in DBoW2 order (slamhot_vocab_create) */
+    Vocabulary(int device, int k, int L, int scoring, int weighting, int n_nodes, const int32_t* parent,
+               const uint8_t* is_leaf, const uint8_t* desc, const double* weight) {
+        check(slamhot_vocab_create(device, k, L, scoring, weighting, n_nodes, parent, is_leaf, desc, weight, &v_),
+              "ORBVocabulary");
+    }
+    ~Vocabulary() { slamhot_vocab_destroy(v_); }
+    Vocabulary(const Vocabulary&) = delete;
+    Vocabulary& operator=(const Vocabulary&) = delete;
+
+    /* void transform(const vector<TDescriptor>& features, BowVector& v, FeatureVector& fv,
+     * int levelsup) (TemplatedVocabulary.h:1139-1206) over n descriptors of 32 bytes, row-contiguous */
+    void transform(const uint8_t* desc, int n, BowVector& v, FeatureVector& fv, int levelsup) {
+        std::vector<uint32_t> word(n), node(n), feat(n);
+        std::vector<double> value(n);
+        std::vector<int32_t> off(n + 1);
+        int nw = 0, nn = 0;
+        check(slamhot_compute_bow(v_, n, desc, levelsup, &nw, word.data(), value.data(), &nn, node.data(), off.data(),
+                                  feat.data()),
+              "ORBVocabulary::transform");
+        v.resize(nw);
+        for (int j = 0; j < nw; j++) v[j] = {word[j], value[j]};
+        fv.resize(nn);
+        for (int j = 0; j < nn; j++) fv[j] = {node[j], std::vector<uint32_t>(feat.begin() + off[j], feat.begin() + off[j + 1])};
+    }
+
+    slam_vocab* handle() { return v_; }
+
+   private:
+    slam_vocab* v_ = nullptr;
+};
+
+/* ------------------------------------------------------------------------------------
  * ORBmatcher (ORBmatcher.h:36-110).  The KeyFrame / Frame arguments arrive as their
  * matcher-relevant views; the MapPoint* outputs as indices into the other side (-1 = NULL).
  * ---------------------------------------------------------------------------------- */
@@ -286,7 +332,9 @@ class ORBmatcher {
     }
 
     /* int SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, const float th,
-     * const bool bMono) (ORBmatcher.cc:2173-2389). */
+     * const bool bMono) (ORBmatcher.cc:2173-2389).  f_match[i]: the LastFrame feature whose MapPoint
+     * CurrentFrame.mvpMapPoints[i] now holds, -1 untouched, -2 set to NULL by the rotation check
+     * (the same convention for the KeyFrame variant below). */
     int SearchByProjection(const slam_frame_view& CurrentFrame, const slam_last_frame& LastFrame, float th, bool bMono,
                            std::vector<int>& f_match) {
         f_match.assign(CurrentFrame.n, -1);

@@ -9,7 +9,13 @@
  *
  *   ORBextractorCall          ORBextractor::operator()                 ORBextractor.cc:1068-1150
  *   SearchByBoW               ORBmatcher::SearchByBoW(KeyFrame*, Frame&) ORBmatcher.cc:269-471
- *   SearchLocalPoints         Tracking::SearchLocalPoints (2nd half)     Tracking.cc:3213-3258
+ *   SearchByBoW               ORBmatcher::SearchByBoW(KeyFrame*, KeyFrame*) ORBmatcher.cc:823-963
+ *   SearchByProjection        ORBmatcher::SearchByProjection(Frame&, const Frame&, th, bMono)
+ *                                                                        ORBmatcher.cc:2173-2389
+ *   SearchByProjection        ORBmatcher::SearchByProjection(Frame&, KeyFrame*, set<MapPoint*>, th, ORBdist)
+ *                                                                        ORBmatcher.cc:2391-2513
+ *   ComputeBoW                Frame::ComputeBoW / KeyFrame::ComputeBoW   Frame.cc:721-728, KeyFrame.cc:105-114
+ *   SearchLocalPoints         Tracking::SearchLocalPoints               Tracking.cc:3187-3258
  *   PoseOptimization          Optimizer::PoseOptimization(Frame*)      Optimizer.cc:824-1118
  *   ComputeStereoMatches      Frame::ComputeStereoMatches              Frame.cc:794-964
  *   BuildLocalWindow          Optimizer::LocalBundleAdjustment window  Optimizer.cc:1613-1718
@@ -31,6 +37,7 @@
 #include <mutex>
 #include <set>
 #include <tuple>
+#include <type_traits>
 #include <utility>
 #include <vector>
 
@@ -105,7 +112,8 @@ slam_bow_side bow_side(const FeatVec& fv, const cv::Mat& desc, const std::vector
     st.node_off.assign(1, 0);
     for (const auto& kv : fv) {
         st.node_id.push_back((uint32_t)kv.first);
-        for (unsigned f : kv.second) st.node_feat.push_back(f);
+        for (unsigned f : kv.second)  // features past mvKeysUn (a second camera's) are skipped, :858, :878
+            if (f < kps.size()) st.node_feat.push_back(f);
         st.node_off.push_back((int32_t)st.node_feat.size());
     }
     st.angle.resize(kps.size());
@@ -125,7 +133,7 @@ slam_bow_side bow_side(const FeatVec& fv, const cv::Mat& desc, const std::vector
 /* ------------------------------------------------------------------ ORBmatcher::SearchByBoW
  * int SearchByBoW(KeyFrame* pKF, Frame& F, vector<MapPoint*>& vpMapPointMatches)
  * (ORBmatcher.cc:269-471) */
-template <class KeyFrame, class Frame, class MapPoint>
+template <class KeyFrame, class Frame, class MapPoint, class = typename std::enable_if<!std::is_pointer<Frame>::value>::type>
 int SearchByBoW(slamhot::ORBmatcher& hot, KeyFrame* pKF, Frame& F, std::vector<MapPoint*>& vpMapPointMatches) {
     const std::vector<MapPoint*> vpMapPointsKF = pKF->GetMapPointMatches();
     vpMapPointMatches = std::vector<MapPoint*>(F.N, static_cast<MapPoint*>(nullptr));
@@ -143,6 +151,59 @@ int SearchByBoW(slamhot::ORBmatcher& hot, KeyFrame* pKF, Frame& F, std::vector<M
     for (int j = 0; j < F.N; j++)
         if (idx[j] >= 0) vpMapPointMatches[j] = vpMapPointsKF[idx[j]];
     return n;
+}
+
+/* ------------------------------------------------------------------ ORBmatcher::SearchByBoW
+ * int SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*>& vpMatches12)
+ * (ORBmatcher.cc:823-963): both sides need a MapPoint that is not bad (:862-866, :882-888);
+ * vpMatches12[i] = the MapPoint of the KF2 feature KF1 feature i matched. */
+template <class KeyFrame, class MapPoint>
+int SearchByBoW(slamhot::ORBmatcher& hot, KeyFrame* pKF1, KeyFrame* pKF2, std::vector<MapPoint*>& vpMatches12) {
+    const std::vector<MapPoint*> vpMapPoints1 = pKF1->GetMapPointMatches();
+    const std::vector<MapPoint*> vpMapPoints2 = pKF2->GetMapPointMatches();
+    vpMatches12 = std::vector<MapPoint*>(vpMapPoints1.size(), static_cast<MapPoint*>(nullptr));
+    BowStore s1, s2;
+    KeyFrameBow A, B;
+    static_cast<slam_bow_side&>(A) = bow_side(pKF1->mFeatVec, pKF1->mDescriptors, pKF1->mvKeysUn, s1);
+    static_cast<slam_bow_side&>(B) = bow_side(pKF2->mFeatVec, pKF2->mDescriptors, pKF2->mvKeysUn, s2);
+    s1.valid.assign(A.n, 0);
+    s2.valid.assign(B.n, 0);
+    for (int i = 0; i < A.n && i < (int)vpMapPoints1.size(); i++)
+        s1.valid[i] = vpMapPoints1[i] && !vpMapPoints1[i]->isBad();
+    for (int i = 0; i < B.n && i < (int)vpMapPoints2.size(); i++)
+        s2.valid[i] = vpMapPoints2[i] && !vpMapPoints2[i]->isBad();
+    A.valid = s1.valid.data();
+    B.valid = s2.valid.data();
+    std::vector<int> idx;
+    const int n = hot.SearchByBoW(A, B, idx);
+    for (int i = 0; i < A.n; i++)
+        if (idx[i] >= 0) vpMatches12[i] = vpMapPoints2[idx[i]];
+    return n;
+}
+
+/* ------------------------------------------------------------------ Frame / KeyFrame::ComputeBoW
+ * void Frame::ComputeBoW() (Frame.cc:721-728) and KeyFrame::ComputeBoW() (KeyFrame.cc:105-114):
+ * mpORBvocabulary->transform(toDescriptorVector(mDescriptors), mBowVec, mFeatVec, 4) with the device
+ * descent; mBowVec (DBoW2::BowVector) and mFeatVec (DBoW2::FeatureVector) are filled in key order.
+ * `hot` is the process's device copy of mpORBvocabulary (one per vocabulary, shareable between
+ * threads: the handle serialises its calls).  mDescriptors is N x 32 and row-contiguous, as
+ * ORBextractor creates it. */
+template <class Frame>
+void ComputeBoW(Vocabulary& hot, Frame& F) {
+    if (!F.mBowVec.empty()) return;  // :723
+    BowVector v;
+    FeatureVector fv;
+    hot.transform(F.mDescriptors.data, F.mDescriptors.rows, v, fv, 4);
+    F.mBowVec.clear();
+    F.mFeatVec.clear();
+    for (const auto& w : v) F.mBowVec.emplace_hint(F.mBowVec.end(), w.first, w.second);
+    for (auto& nd : fv) F.mFeatVec.emplace_hint(F.mFeatVec.end(), nd.first, std::move(nd.second));
+}
+template <class KeyFrame>
+void KeyFrameComputeBoW(Vocabulary& hot, KeyFrame* pKF) {
+    if (!pKF->mBowVec.empty() && !pKF->mFeatVec.empty()) return;  // KeyFrame.cc:107
+    pKF->mBowVec.clear();
+    ComputeBoW(hot, *pKF);
 }
 
 /* The matcher-facing view of a Frame (grid bounds and scale tables are Frame statics / members). */
@@ -177,14 +238,115 @@ slam_frame_view frame_view(Frame& F, std::vector<int8_t>& mp_state, float* Tcw16
     return v;
 }
 
+/* ------------------------------------------------------------------ ORBmatcher::SearchByProjection
+ * int SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, const float th, const bool bMono)
+ * (ORBmatcher.cc:2173-2389), Nleft == -1: TrackWithMotionModel's matcher (Tracking.cc:2683-2760).
+ * Only the last frame's MapPoints that are set and not flagged mvbOutlier are read (:2196-2201); a
+ * current feature is a candidate unless it holds a MapPoint with observations (:2248-2250).  The
+ * matches land in CurrentFrame.mvpMapPoints, and so do the NULLs of the rotation check (:2366-2386). */
+template <class Frame>
+int SearchByProjection(slamhot::ORBmatcher& hot, Frame& CurrentFrame, const Frame& LastFrame, float th, bool bMono) {
+    const int n = LastFrame.N;
+    std::vector<uint8_t> has_mp(n, 0), outlier(n, 0), has_obs(n, 0), desc(32 * (size_t)n, 0);
+    std::vector<float> pos(3 * (size_t)n, 0.f);
+    for (int i = 0; i < n; i++) {
+        auto* pMP = LastFrame.mvpMapPoints[i];
+        if (!pMP) continue;
+        has_mp[i] = 1;
+        outlier[i] = LastFrame.mvbOutlier[i] ? 1 : 0;
+        if (outlier[i]) continue;
+        const cv::Mat X = pMP->GetWorldPos(), d = pMP->GetDescriptor();
+        for (int k = 0; k < 3; k++) pos[3 * (size_t)i + k] = X.template at<float>(k);
+        std::memcpy(&desc[32 * (size_t)i], d.data, 32);
+        has_obs[i] = pMP->Observations() > 0;  // a match makes the candidate blocking (:2248-2250)
+    }
+    float Tl[16];
+    mat4(LastFrame.mTcw, Tl);
+    slam_last_frame L{};
+    L.n = n;
+    L.Tcw = Tl;
+    L.kps = kp_ptr(LastFrame.mvKeys);      // octave (:2221)
+    L.kps_un = kp_ptr(LastFrame.mvKeysUn); // angle (:2278)
+    L.has_mp = has_mp.data();
+    L.outlier = outlier.data();
+    L.mp_pos = pos.data();
+    L.mp_desc = desc.data();
+    L.mp_has_obs = has_obs.data();
+    std::vector<int8_t> st;
+    float T[16];
+    const slam_frame_view v = frame_view(CurrentFrame, st, T);
+    std::vector<int> fm;
+    const int nmatches = hot.SearchByProjection(v, L, th, bMono, fm);
+    for (int i = 0; i < CurrentFrame.N; i++) {
+        if (fm[i] >= 0) CurrentFrame.mvpMapPoints[i] = LastFrame.mvpMapPoints[fm[i]];
+        else if (fm[i] == -2) CurrentFrame.mvpMapPoints[i] = nullptr;
+    }
+    return nmatches;
+}
+
+/* int SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const set<MapPoint*>& sAlreadyFound,
+ * const float th, const int ORBdist) (ORBmatcher.cc:2391-2513): Relocalization's matcher
+ * (Tracking.cc:3455-3590).  The KeyFrame's MapPoints that are set, not bad and not in sAlreadyFound
+ * (:2409-2413); a current feature holding any MapPoint is no candidate (:2455-2456). */
+template <class Frame, class KeyFrame, class MapPoint>
+int SearchByProjection(slamhot::ORBmatcher& hot, Frame& CurrentFrame, KeyFrame* pKF,
+                       const std::set<MapPoint*>& sAlreadyFound, float th, int ORBdist) {
+    const std::vector<MapPoint*> vpMPs = pKF->GetMapPointMatches();
+    const int n = (int)vpMPs.size();
+    std::vector<uint8_t> use(n, 0), desc(32 * (size_t)n, 0);
+    std::vector<float> pos(3 * (size_t)n, 0.f), max_d(n, 0.f), min_d(n, 0.f);
+    for (int i = 0; i < n; i++) {
+        MapPoint* pMP = vpMPs[i];
+        if (!pMP || pMP->isBad() || sAlreadyFound.count(pMP)) continue;
+        use[i] = 1;
+        const cv::Mat X = pMP->GetWorldPos(), d = pMP->GetDescriptor();
+        for (int k = 0; k < 3; k++) pos[3 * (size_t)i + k] = X.template at<float>(k);
+        std::memcpy(&desc[32 * (size_t)i], d.data, 32);
+        max_d[i] = pMP->GetMaxDistance();  // raw: the kernel applies 1.2f / 0.8f and PredictScale (:2430-2437)
+        min_d[i] = pMP->GetMinDistance();
+    }
+    slam_kf_points K{};
+    K.n = n;
+    K.kps_un = kp_ptr(pKF->mvKeysUn);  // angle (:2476)
+    K.use = use.data();
+    K.mp_pos = pos.data();
+    K.max_dist = max_d.data();
+    K.min_dist = min_d.data();
+    K.mp_desc = desc.data();
+    std::vector<int8_t> st;
+    float T[16];
+    const slam_frame_view v = frame_view(CurrentFrame, st, T);
+    std::vector<int> fm;
+    const int nmatches = hot.SearchByProjection(v, K, th, ORBdist, fm);
+    for (int i = 0; i < CurrentFrame.N; i++) {
+        if (fm[i] >= 0) CurrentFrame.mvpMapPoints[i] = vpMPs[fm[i]];
+        else if (fm[i] == -2) CurrentFrame.mvpMapPoints[i] = nullptr;
+    }
+    return nmatches;
+}
+
 /* ------------------------------------------------------------------ Tracking::SearchLocalPoints
- * The projection half (Tracking.cc:3213-3258) for a Frame with Nleft == -1: isInFrustum of every
- * local MapPoint not already seen by this frame and SearchByProjection(F, vpLocalMapPoints, th,
- * bFarPoints, thFarPoints), one device call; the tracking fields isInFrustum leaves are written
- * back into the MapPoints and the matches into F.mvpMapPoints.  Returns nToMatch. */
+ * void Tracking::SearchLocalPoints() (Tracking.cc:3187-3258) for a Frame with Nleft == -1: the
+ * frame's own MapPoints are marked seen (bad ones dropped, :3190-3206); then Frame::isInFrustum of
+ * every local MapPoint not seen / not bad and SearchByProjection(F, vpLocalMapPoints, th, bFarPoints,
+ * thFarPoints) on the ones in view, one device call; the fields isInFrustum leaves (Frame.cc:497-554)
+ * and IncreaseVisible are written back into the MapPoints, mmProjectPoints into the Frame
+ * (:3227-3230), the matches into F.mvpMapPoints.  `th` is the caller's choice of :3234-3253
+ * (sensor, IMU and relocalisation state of the Tracking thread).  Returns nToMatch. */
 template <class Frame, class MapPoint>
-int SearchLocalPoints(slamhot::ORBmatcher& hot, Frame& F, std::vector<MapPoint*>& vpLocalMapPoints, float th,
+int SearchLocalPoints(slamhot::ORBmatcher& hot, Frame& F, const std::vector<MapPoint*>& vpLocalMapPoints, float th,
                       bool bFarPoints, float thFarPoints, int* nmatches = nullptr) {
+    for (auto& pMP : F.mvpMapPoints) {  // :3190-3206
+        if (!pMP) continue;
+        if (pMP->isBad()) {
+            pMP = nullptr;
+        } else {
+            pMP->IncreaseVisible();
+            pMP->mnLastFrameSeen = F.mnId;
+            pMP->mbTrackInView = false;
+            pMP->mbTrackInViewR = false;
+        }
+    }
     std::vector<slam_mp_geom> G(vpLocalMapPoints.size());
     std::vector<uint8_t> D(32 * G.size());
     for (size_t i = 0; i < G.size(); i++) {
@@ -211,17 +373,18 @@ int SearchLocalPoints(slamhot::ORBmatcher& hot, Frame& F, std::vector<MapPoint*>
     const int n = hot.SearchLocalPoints(v, G, D.data(), 0.5f, th, bFarPoints, thFarPoints, track, nToMatch, f_match);
     for (size_t i = 0; i < G.size(); i++) {
         MapPoint* pMP = vpLocalMapPoints[i];
-        if (G[i].seen || G[i].is_bad) continue;
+        if (G[i].seen || G[i].is_bad) continue;  // :3217-3220
         const slam_mp_track& t = track[i];
-        pMP->mbTrackInView = t.in_view;
+        pMP->mbTrackInView = t.in_view;          // isInFrustum, Frame.cc:497-554
+        pMP->mTrackProjX = t.proj_x;             // -1, or the projection once it lies in the image
+        pMP->mTrackProjY = t.proj_y;
         if (t.in_view) {
             pMP->IncreaseVisible();
-            pMP->mTrackProjX = t.proj_x;
-            pMP->mTrackProjY = t.proj_y;
             pMP->mTrackProjXR = t.proj_xr;
             pMP->mnTrackScaleLevel = t.scale_level;
             pMP->mTrackViewCos = t.view_cos;
             pMP->mTrackDepth = t.depth;
+            F.mmProjectPoints[pMP->mnId] = cv::Point2f(pMP->mTrackProjX, pMP->mTrackProjY);  // :3227-3230
         }
     }
     for (int i = 0; i < F.N; i++)

@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <map>
 #include <vector>
 
 #include "matcher_oracle.h"
@@ -119,6 +120,62 @@ void oracle_vocab_transform(int L, const int32_t* child_ptr, const int32_t* chil
         weight[i] = weight_of_node[final_id];
         node_id[i] = nid;
     }
+}
+
+// TemplatedVocabulary::transform(features, BowVector&, FeatureVector&, levelsup)'s map building
+// (TemplatedVocabulary.h:1139-1206) over the per-feature descent results of oracle_vocab_transform,
+// with DBoW2's containers: BowVector::addWeight / addIfNotExist / normalize (BowVector.cpp:34-84),
+// FeatureVector::addFeature (FeatureVector.cpp:31-45).  weighting: TF_IDF 0, TF 1, IDF 2, BINARY 3;
+// scoring: L1_NORM 0, L2_NORM 1, CHI_SQUARE 2, KL 3, BHATTACHARYYA 4, DOT_PRODUCT 5
+// (ScoringObject.h:74-89: all but DOT_PRODUCT normalise, L2 only for L2_NORM).
+void oracle_bow_vectors(int n, const int32_t* word_id, const double* weight, const int32_t* node_id,
+                        int scoring, int weighting, int* n_words, uint32_t* bow_word, double* bow_value,
+                        int* n_nodes, uint32_t* fv_node, int32_t* fv_off, uint32_t* fv_feat) {
+    std::map<unsigned int, double> v;
+    std::map<unsigned int, std::vector<unsigned int>> fv;
+    const bool must = scoring != 5;
+    for (int i = 0; i < n; i++) {
+        const double w = weight[i];
+        if (!(w > 0)) continue;
+        const unsigned int id = (unsigned int)word_id[i];
+        auto vit = v.lower_bound(id);
+        if (weighting == 0 || weighting == 1) {
+            if (vit != v.end() && !(id < vit->first)) vit->second += w;
+            else v.insert(vit, std::make_pair(id, w));
+        } else if (vit == v.end() || id < vit->first) {
+            v.insert(vit, std::make_pair(id, w));
+        }
+        fv[(unsigned int)node_id[i]].push_back((unsigned int)i);
+    }
+    if ((weighting == 0 || weighting == 1) && !v.empty() && !must) {
+        const double nd = v.size();
+        for (auto& kv : v) kv.second /= nd;
+    }
+    if (must) {
+        double norm = 0.0;
+        if (scoring == 1) {
+            for (auto& kv : v) norm += kv.second * kv.second;
+            norm = std::sqrt(norm);
+        } else {
+            for (auto& kv : v) norm += std::fabs(kv.second);
+        }
+        if (norm > 0.0)
+            for (auto& kv : v) kv.second /= norm;
+    }
+    int j = 0;
+    for (auto& kv : v) {
+        bow_word[j] = kv.first;
+        bow_value[j++] = kv.second;
+    }
+    *n_words = j;
+    int k = 0, f = 0;
+    fv_off[0] = 0;
+    for (auto& kv : fv) {
+        fv_node[k] = kv.first;
+        for (unsigned int i : kv.second) fv_feat[f++] = i;
+        fv_off[++k] = f;
+    }
+    *n_nodes = k;
 }
 
 // SearchByBoW, both variants (ORBmatcher.cc:269-471 KF-Frame, 823-963 KF-KF), pinhole

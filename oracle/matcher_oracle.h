@@ -16,6 +16,9 @@ void oracle_vocab_transform(int L, const int32_t* child_ptr, const int32_t* chil
                             const int32_t* word_of_node, const double* weight_of_node, int n,
                             const uint8_t* desc, int levelsup, int32_t* word_id, double* weight,
                             int32_t* node_id);
+void oracle_bow_vectors(int n, const int32_t* word_id, const double* weight, const int32_t* node_id,
+                        int scoring, int weighting, int* n_words, uint32_t* bow_word, double* bow_value,
+                        int* n_nodes, uint32_t* fv_node, int32_t* fv_off, uint32_t* fv_feat);
 int oracle_search_by_bow(const slam_bow_side* A, const slam_bow_side* B, float nnratio,
                          int check_ori, int strict, int32_t* a2b, int32_t* b2a);
 #ifdef __cplusplus

@@ -648,6 +648,27 @@ int oracle_extract(const slam_orb_params* p, const uint8_t* img, int w, int h, s
     return ex.run(img, w, h, stride, lap0, lap1, kps, desc, cap, n, mono_index);
 }
 
+/* operator() and the mvImagePyramid it leaves (ORBextractor.h:83), which Frame::ComputeStereoMatches
+ * reads (Frame.cc:801, 891): the levels land in `pyr` as oracle_pyramid lays them out. */
+int oracle_extract_pyr(const slam_orb_params* p, const uint8_t* img, int w, int h, size_t stride, int lap0,
+                       int lap1, slam_keypoint* kps, uint8_t* desc, int cap, int* n, int* mono_index, uint8_t* pyr,
+                       size_t pyr_cap, int* lw, int* lh, size_t* offsets) {
+    Extractor ex(*p);
+    const int st = ex.run(img, w, h, stride, lap0, lap1, kps, desc, cap, n, mono_index);
+    if (st != SLAM_OK) return st;
+    size_t off = 0;
+    for (int l = 0; l < ex.t.nlevels; l++) {
+        const Image& L = ex.pyr[l];
+        lw[l] = L.w;
+        lh[l] = L.h;
+        offsets[l] = off;
+        if (off + L.px.size() > pyr_cap) return SLAM_ECAP;
+        std::memcpy(pyr + off, L.px.data(), L.px.size());
+        off += L.px.size();
+    }
+    return SLAM_OK;
+}
+
 void oracle_levels(const slam_orb_params* p, float* scale, float* inv_scale, float* sigma2,
                    float* inv_sigma2, int32_t* nfeat) {
     Tables t = make_tables(*p);

@@ -233,7 +233,7 @@ int oracle_search_by_projection_last(const slam_frame_view* F, const slam_last_f
         for (int b = 0; b < HISTO_LENGTH; b++) {
             if (b == i1 || b == i2 || b == i3) continue;
             for (int idx : rotHist[b]) {
-                f_match[idx] = -1;
+                f_match[idx] = -2;  // CurrentFrame.mvpMapPoints[idx] = NULL
                 nmatches--;
             }
         }
@@ -298,7 +298,7 @@ int oracle_search_by_projection_kf(const slam_frame_view* F, const slam_kf_point
         for (int b = 0; b < HISTO_LENGTH; b++) {
             if (b == i1 || b == i2 || b == i3) continue;
             for (int idx : rotHist[b]) {
-                f_match[idx] = -1;
+                f_match[idx] = -2;  // CurrentFrame.mvpMapPoints[idx] = NULL
                 nmatches--;
             }
         }

@@ -857,6 +857,82 @@ slam_status slamhot_vocab_transform(slam_vocab* v, int n, const uint8_t* desc, i
     return SLAM_OK;
 }
 
+// TemplatedVocabulary::transform(features, BowVector&, FeatureVector&, levelsup)
+// (TemplatedVocabulary.h:1139-1206): the descent on the device (slamhot_vocab_transform), the two
+// maps on the host in DBoW2's own order of operations (DBoW2 enums: weighting TF_IDF 0, TF 1, IDF 2,
+// BINARY 3; scoring L1_NORM 0, L2_NORM 1, CHI_SQUARE 2, KL 3, BHATTACHARYYA 4, DOT_PRODUCT 5).
+slam_status slamhot_compute_bow(slam_vocab* v, int n, const uint8_t* desc, int levelsup, int* n_words,
+                                uint32_t* bow_word, double* bow_value, int* n_nodes, uint32_t* fv_node,
+                                int32_t* fv_off, uint32_t* fv_feat) {
+    if (!v || n < 0 || !n_words || !n_nodes || (n > 0 && (!desc || !bow_word || !bow_value || !fv_node || !fv_feat)) ||
+        !fv_off)
+        return SLAM_EINVAL;
+    *n_words = 0;
+    *n_nodes = 0;
+    fv_off[0] = 0;
+    if (n == 0) return SLAM_OK;
+    std::vector<int32_t> word(n), node(n);
+    std::vector<double> weight(n);
+    slam_status st = slamhot_vocab_transform(v, n, desc, levelsup, word.data(), weight.data(), node.data());
+    if (st) return st;
+    // features not stopped (w > 0, :1169), in feature order
+    std::vector<uint32_t> kept;
+    kept.reserve(n);
+    for (int i = 0; i < n; i++)
+        if (weight[i] > 0) kept.push_back((uint32_t)i);
+    // BowVector: stable sort by word keeps feature order inside a word = addWeight's summation order
+    std::vector<uint32_t> by_word(kept);
+    std::stable_sort(by_word.begin(), by_word.end(),
+                     [&](uint32_t a, uint32_t b) { return (uint32_t)word[a] < (uint32_t)word[b]; });
+    const bool sum_weights = v->weighting == 0 || v->weighting == 1;  // TF_IDF, TF: addWeight; else addIfNotExist
+    int nw = 0;
+    for (size_t j = 0; j < by_word.size();) {
+        const uint32_t w = (uint32_t)word[by_word[j]];
+        double val = weight[by_word[j]];
+        size_t k = j + 1;
+        for (; k < by_word.size() && (uint32_t)word[by_word[k]] == w; k++)
+            if (sum_weights) val += weight[by_word[k]];
+        bow_word[nw] = w;
+        bow_value[nw] = val;
+        nw++;
+        j = k;
+    }
+    const bool must = v->scoring != 5;  // every ScoringObject but DotProductScoring normalises (ScoringObject.h:74-89)
+    if (sum_weights && nw > 0 && !must) {
+        const double nd = (double)nw;  // :1174-1180
+        for (int j = 0; j < nw; j++) bow_value[j] /= nd;
+    }
+    if (must) {  // BowVector::normalize (BowVector.cpp:62-84): L2 for L2_NORM, L1 otherwise
+        double norm = 0.0;
+        if (v->scoring == 1) {
+            for (int j = 0; j < nw; j++) norm += bow_value[j] * bow_value[j];
+            norm = std::sqrt(norm);
+        } else {
+            for (int j = 0; j < nw; j++) norm += std::fabs(bow_value[j]);
+        }
+        if (norm > 0.0)
+            for (int j = 0; j < nw; j++) bow_value[j] /= norm;
+    }
+    *n_words = nw;
+    // FeatureVector: node ascending, features ascending inside a node (addFeature appends in order)
+    std::vector<uint32_t> by_node(kept);
+    std::stable_sort(by_node.begin(), by_node.end(),
+                     [&](uint32_t a, uint32_t b) { return (uint32_t)node[a] < (uint32_t)node[b]; });
+    int nn = 0;
+    for (size_t j = 0; j < by_node.size(); j++) {
+        const uint32_t id = (uint32_t)node[by_node[j]];
+        if (nn == 0 || fv_node[nn - 1] != id) {
+            fv_node[nn] = id;
+            fv_off[nn] = (int32_t)j;
+            nn++;
+        }
+        fv_feat[j] = by_node[j];
+    }
+    fv_off[nn] = (int32_t)by_node.size();
+    *n_nodes = nn;
+    return SLAM_OK;
+}
+
 slam_status slamhot_matcher_create(int device, slam_matcher** out) {
     if (!out) return SLAM_EINVAL;
     *out = nullptr;
@@ -1338,7 +1414,7 @@ __global__ void __launch_bounds__(1024) k_search_by_projection(const DevProjCall
             if (a >= 0) {
                 const int bin = rot_bin(C.queries[q].angle, F.kps[a].angle);
                 if (bin != s_keep[0] && bin != s_keep[1] && bin != s_keep[2]) {
-                    fm[a] = -1;  // nulled after all assignments (ORBmatcher.cc:2371-2386)
+                    fm[a] = -2;  // set to NULL after all assignments (ORBmatcher.cc:2371-2386, 2491-2510)
                     drop++;
                 }
             }
@@ -1717,7 +1793,7 @@ extern "C" slam_status slamhot_search_local_points_batch(slam_matcher* m, int nf
         O[f].niv = take(4);
     }
     const size_t total = off;
-    std::lock_guard<std::mutex> g(m->mu);
+    std::unique_lock<std::mutex> g(m->mu);
     SLAM_HIP_TRY(hipSetDevice(m->device));
     slam_status st;
     if ((st = m->d_a.ensure(total))) return st;
@@ -1820,7 +1896,7 @@ extern "C" slam_status slamhot_search_local_points_batch(slam_matcher* m, int nf
         n_to_match[f] = *(const int32_t*)(R.data() + (o.niv - res_off));
         if (frames[f].n) std::memcpy(f_match[f], R.data() + (o.fm - res_off), 4 * (size_t)frames[f].n);
     }
-    m->mu.unlock();
+    g.unlock();  // the single-call path takes the handle's lock itself
     slam_status rs = SLAM_OK;
     for (int f : redo) {
         int n = 0, ntm = 0;
@@ -1830,7 +1906,6 @@ extern "C" slam_status slamhot_search_local_points_batch(slam_matcher* m, int nf
         nmatches[f] = n;
         n_to_match[f] = ntm;
     }
-    m->mu.lock();  // the guard unlocks on return
     return rs;
 }
 
@@ -1938,7 +2013,7 @@ slam_status run_projection_batch(slam_matcher* m, int nframes, const slam_frame_
     std::vector<DevProjCall> calls(nframes);
     std::vector<size_t> fm_off(nframes), out_off(nframes);
     size_t in_bytes = 0, res_off = 0, total = 0, lds = 0, calls_off = 0;
-    std::lock_guard<std::mutex> g(m->mu);
+    std::unique_lock<std::mutex> g(m->mu);
     SLAM_HIP_TRY(hipSetDevice(m->device));
     for (int pass = 0; pass < 2; pass++) {
         Stager S;
@@ -2004,14 +2079,13 @@ slam_status run_projection_batch(slam_matcher* m, int nframes, const slam_frame_
         nmatches[f] = out[0];
         if (frames[f].n) std::memcpy(f_match[f], R + (fm_off[f] - res_off), 4 * (size_t)frames[f].n);
     }
-    m->mu.unlock();
+    g.unlock();  // the single-call path takes the handle's lock itself
     slam_status rs = SLAM_OK;
     for (int f : redo) {
         int n = 0;
         if ((rs = single(f, &n)) != SLAM_OK) break;
         nmatches[f] = n;
     }
-    m->mu.lock();  // the guard unlocks on return
     return rs;
 }
 }  // namespace

@@ -663,8 +663,9 @@ class LocalBundleAdjustment:
         """Flatten windows into C structs once (what a C++ caller already holds); returns a
         callable that runs slamhot_lba_solve on them and returns the LM iteration total
         (``run.results()`` gives the result dicts).  ``stop_flag``: a live ``ctypes.c_bool``;
-        ``run(stop_at_step=k)`` sets it from the solver's step hook once step k's counters are
-        in (slam_lba_options.step_hook), a deterministic stand-in for another thread's abort."""
+        ``run(stop_at_step=k)`` clears it, then sets it from the solver's step hook once step k's
+        counters are in (slam_lba_options.step_hook): another thread's abort at a known point; the
+        solve stops within the steps already queued behind k (at most 3)."""
         ws = list(windows)
         probs = (LbaProblem * len(ws))()
         ress = (LbaResult * len(ws))()
@@ -690,6 +691,10 @@ class LocalBundleAdjustment:
         hook_c = _STEP_HOOK(hook)
 
         def run(stop_at_step=None):
+            if stop_at_step is not None and stop_flag is None:
+                raise ValueError("run(stop_at_step=...) needs prepare(..., stop_flag=ctypes.c_bool())")
+            if stop_flag is not None and stop_at_step is not None:
+                stop_flag.value = False  # a flag left set by the last run would stop this one on entry
             state["stop_at"] = -1 if stop_at_step is None else int(stop_at_step)
             opt.step_hook = C.cast(hook_c, C.c_void_p) if stop_at_step is not None or stop_flag is not None else None
             check(fn(h, len(ws), probs, C.byref(opt), None, ress), "lba_solve")

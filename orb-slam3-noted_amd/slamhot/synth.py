@@ -393,19 +393,30 @@ def unrectify(rect: np.ndarray, map_x: np.ndarray, map_y: np.ndarray) -> np.ndar
     for dy, dx, wt in ((0, 0, (1 - fx) * (1 - fy)), (0, 1, fx * (1 - fy)), (1, 0, (1 - fx) * fy), (1, 1, fx * fy)):
         xi, yi = x0 + dx + 1, y0 + dy + 1
         ok = (xi >= 0) & (xi < w + 2) & (yi >= 0) & (yi < h + 2)
-        np.add.at(acc, (yi[ok], xi[ok]), (val * wt)[ok])
-        np.add.at(wsum, (yi[ok], xi[ok]), wt[ok])
+        flat = (yi[ok] * (w + 2) + xi[ok]).ravel()
+        # bincount accumulates in input order, as np.add.at does (same sums, ~20x faster)
+        acc += np.bincount(flat, (val * wt)[ok].ravel(), minlength=acc.size).reshape(acc.shape)
+        wsum += np.bincount(flat, wt[ok].ravel(), minlength=acc.size).reshape(acc.shape)
     acc, wsum = acc[1:-1, 1:-1], wsum[1:-1, 1:-1]
     out = np.where(wsum > 1e-6, acc / np.maximum(wsum, 1e-6), np.nan)
+    # fill holes from their 4-neighbours, Jacobi passes (each pass reads the previous one); only
+    # the hole pixels are visited, the neighbour sum in the order np.nansum over the stacked
+    # (up, down, left, right) planes takes
     for _ in range(32):
-        holes = np.isnan(out)
-        if not holes.any():
+        ys, xs = np.nonzero(np.isnan(out))
+        if len(ys) == 0:
             break
         pad = np.pad(out, 1, constant_values=np.nan)
-        nb = np.stack([pad[:-2, 1:-1], pad[2:, 1:-1], pad[1:-1, :-2], pad[1:-1, 2:]])
-        cnt = np.isfinite(nb).sum(0)
-        fill = np.where(cnt > 0, np.nansum(nb, axis=0) / np.maximum(cnt, 1), np.nan)
-        out = np.where(holes & np.isfinite(fill), fill, out)
+        acc_n = np.zeros(len(ys))
+        cnt = np.zeros(len(ys), np.int64)
+        for v in (pad[ys, xs + 1], pad[ys + 2, xs + 1], pad[ys + 1, xs], pad[ys + 1, xs + 2]):
+            ok = np.isfinite(v)
+            acc_n = acc_n + np.where(ok, v, 0.0)
+            cnt += ok
+        new = cnt > 0
+        if not new.any():  # nothing reachable is left: later passes would change nothing
+            break
+        out[ys[new], xs[new]] = acc_n[new] / cnt[new]
     out = np.nan_to_num(out, nan=128.0)
     return np.ascontiguousarray(np.clip(np.rint(out), 0, 255).astype(np.uint8))
 
@@ -521,19 +532,28 @@ def sequence_poses(seed: int, n: int, step_m: float = 0.03, yaw_deg: float = 0.6
     return out
 
 
-def stereo_sequence(seed: int, n: int, cam=EUROC_CAM, step_m: float = 0.03):
+def stereo_sequence(seed: int, n: int, cam=EUROC_CAM, step_m: float = 0.03, threads: int = 1):
     """n rectified stereo frames of the room: (lefts (n,H,W) u8, rights, gt Tcw list).
-    The right camera is the left one shifted by b = bf / fx along its x axis."""
+    The right camera is the left one shifted by b = bf / fx along its x axis.  threads > 1
+    renders the views concurrently (numpy releases the GIL; same images)."""
     tex = _wall_textures(seed)
     b = cam["bf"] / cam["fx"]
-    Ls, Rs, Ts = [], [], []
-    for i, T in enumerate(sequence_poses(seed, n, step_m)):
-        Tr = T.copy()
-        Tr[0, 3] -= b  # X_right = X_left - (b, 0, 0)
-        Ls.append(render_view(tex, T, cam, noise_seed=seed * 1000 + 2 * i)[0])
-        Rs.append(render_view(tex, Tr, cam, noise_seed=seed * 1000 + 2 * i + 1)[0])
-        Ts.append(T)
-    return np.stack(Ls), np.stack(Rs), Ts
+    Ts = sequence_poses(seed, n, step_m)
+
+    def view(j):
+        i, right = divmod(j, 2)
+        T = Ts[i].copy()
+        if right:
+            T[0, 3] -= b  # X_right = X_left - (b, 0, 0)
+        return render_view(tex, T, cam, noise_seed=seed * 1000 + j)[0]
+
+    if threads > 1:
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(threads) as pool:
+            V = list(pool.map(view, range(2 * n)))
+    else:
+        V = [view(j) for j in range(2 * n)]
+    return np.stack(V[0::2]), np.stack(V[1::2]), Ts
 
 
 def mono_sequence(seed: int, n: int, cam=EUROC_MONO_CAM, step_m: float = 0.03):

@@ -18,6 +18,8 @@
 namespace cv {
 struct Point2f {
     float x = 0, y = 0;
+    Point2f() = default;
+    Point2f(float x_, float y_) : x(x_), y(y_) {}
 };
 struct KeyPoint {  // OpenCV 4.x layout: pt, size, angle, response, octave, class_id
     Point2f pt;
@@ -95,7 +97,7 @@ class MapPoint {
     long unsigned int mnId = 0;
     long unsigned int mnBALocalForKF = (unsigned long)-1;
     long unsigned int mnLastFrameSeen = (unsigned long)-1;
-    bool mbTrackInView = false;
+    bool mbTrackInView = false, mbTrackInViewR = false;
     float mTrackProjX = -1, mTrackProjY = -1, mTrackProjXR = -1, mTrackDepth = -1, mTrackViewCos = 0;
     int mnTrackScaleLevel = -1, mnVisible = 1, mnNormalUpdates = 0;
     cv::Mat mWorldPos{3, 1, CV_32F}, mNormalVector{3, 1, CV_32F}, mDescriptor{1, 32, CV_8U};
@@ -115,7 +117,7 @@ class MapPoint {
     float GetMinDistanceInvariance() { return 0.8f * mfMinDistance; }
     float GetMaxDistanceInvariance() { return 1.2f * mfMaxDistance; }
     std::map<KeyFrame*, std::tuple<int, int>> GetObservations() { return mObservations; }
-    int Observations() { return (int)mObservations.size(); }
+    int Observations();  // nObs: 2 per stereo observation of a one-camera KeyFrame (MapPoint.cc:161-186)
     bool IsInKeyFrame(KeyFrame* pKF) { return mObservations.count(pKF) > 0; }
     void AddObservation(KeyFrame* pKF, int idx) { mObservations[pKF] = std::make_tuple(idx, -1); }
     void EraseObservation(KeyFrame* pKF) { mObservations.erase(pKF); }
@@ -134,6 +136,7 @@ class KeyFrame {
     std::vector<float> mvuRight, mvInvLevelSigma2, mvScaleFactors;
     cv::Mat mDescriptors, mTcw{4, 4, CV_32F}, mTrl;
     std::map<unsigned int, std::vector<unsigned int>> mFeatVec;  // DBoW2::FeatureVector
+    std::map<unsigned int, double> mBowVec;                       // DBoW2::BowVector
     int mnScaleLevels = 8, mnMinX = 0, mnMinY = 0, mnMaxX = 752, mnMaxY = 480;
     float mfLogScaleFactor = 0, mfGridElementWidthInv = 0, mfGridElementHeightInv = 0;
     GeometricCamera* mpCamera2 = nullptr;
@@ -155,6 +158,16 @@ class KeyFrame {
             if (m == pMP) m = nullptr;
     }
 };
+
+inline int MapPoint::Observations() {
+    int n = 0;
+    for (const auto& o : mObservations) {
+        const int li = std::get<0>(o.second), ri = std::get<1>(o.second);
+        if (li != -1) n += (!o.first->mpCamera2 && o.first->mvuRight[li] >= 0) ? 2 : 1;
+        if (ri != -1) n += 1;
+    }
+    return n;
+}
 
 inline void MapPoint::Replace(MapPoint* pMP) {  // MapPoint.cc:238-290 (observation transfer)
     if (pMP->mnId == mnId) return;
@@ -185,8 +198,10 @@ class Frame {
     std::vector<float> mvuRight, mvDepth, mvInvLevelSigma2, mvScaleFactors;
     cv::Mat mDescriptors, mDescriptorsRight, mTcw{4, 4, CV_32F};
     std::map<unsigned int, std::vector<unsigned int>> mFeatVec;
+    std::map<unsigned int, double> mBowVec;
     std::vector<MapPoint*> mvpMapPoints;
     std::vector<bool> mvbOutlier;
+    std::map<long unsigned int, cv::Point2f> mmProjectPoints;
     void SetPose(cv::Mat Tcw) { mTcw = Tcw.clone(); }
 };
 inline float Frame::mnMinX = 0, Frame::mnMinY = 0, Frame::mnMaxX = 752, Frame::mnMaxY = 480,

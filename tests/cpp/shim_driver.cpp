@@ -11,12 +11,22 @@
 //   shim_driver bow PAIR OUT      ORB_SLAM3::ORBmatcher(nnratio, checkOri).SearchByBoW(pKF, F, ...)
 //                                 through the reference-side binding of INTEGRATION.md, once per
 //                                 (nnratio, checkOri) listed in PAIR, all on this one thread
+//   shim_driver bowkk PAIR OUT    SearchByBoW(pKF1, pKF2, vpMatches12) per (nnratio, checkOri)
+//   shim_driver projlast IN OUT   SearchByProjection(CurrentFrame, LastFrame, th, bMono) per call
+//   shim_driver projkf IN OUT     SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist)
+//   shim_driver computebow IN OUT Frame::ComputeBoW and KeyFrame::ComputeBoW per vocabulary
+//   shim_driver extract IN OUT    ORBextractor::operator() incl. mvImagePyramid, per image
+//   shim_driver stereo IN OUT     the stereo Frame's two extractions + ComputeStereoMatches
+//   shim_driver localpoints IN OUT  Tracking::SearchLocalPoints (both halves)
+//   shim_driver fuse IN OUT       ORBmatcher::Fuse(pKF, vpMapPoints, th) incl. its map updates
 //
 // MAP / FRAME are little-endian binaries written by tests/shim_io.py.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
+#include <memory>
+#include <set>
 #include <string>
 
 #include "orbslam3_standins.hpp"
@@ -228,6 +238,27 @@ int run_lba_time(const char* in, const char* out, int reps) {
     double dev = 0, plan = 0;
     int syncs = 0;
     slamhot::check(slamhot_lba_last_stats(solver.handle(), &dev, &plan, &syncs), "lba_last_stats");
+    // where the wall time goes: window build + flattening alone, the solve alone (host wall), on
+    // fresh maps; the rest of a call is vToErase and the write-back
+    std::vector<double> build_ms, solve_ms;
+    for (int r = 0; r < reps; r++) {
+        World W;
+        load_map(in, W);
+        const auto t0 = std::chrono::steady_clock::now();
+        slamhot::orbslam3::LocalWindow<KeyFrame, MapPoint> L;
+        slamhot::orbslam3::BuildLocalWindow(&W.kfs[W.cur], &W.map, L);
+        slamhot::LocalBAWindow F;
+        std::vector<KeyFrame*> kfs;
+        std::vector<std::pair<KeyFrame*, MapPoint*>> refs;
+        slamhot::orbslam3::FlattenLocalWindow(L, &W.map, F, kfs, refs);
+        const auto t1 = std::chrono::steady_clock::now();
+        std::vector<slamhot::LocalBAResult> res;
+        bool stop = false;
+        solver.Solve({F}, &stop, res);
+        const auto t2 = std::chrono::steady_clock::now();
+        build_ms.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count());
+        solve_ms.push_back(std::chrono::duration<double, std::milli>(t2 - t1).count());
+    }
     Writer O(out);
     O.put<int32_t>(nf);
     O.put<int32_t>(no);
@@ -235,6 +266,8 @@ int run_lba_time(const char* in, const char* out, int reps) {
     O.put<int32_t>(ne);
     O.put(ms);
     O.put(std::vector<double>{dev, plan, (double)syncs});
+    O.put(build_ms);
+    O.put(solve_ms);
     return 0;
 }
 
@@ -288,12 +321,16 @@ int run_pose(const char* in, const char* out) {
 }  // namespace
 
 // The reference's ORBmatcher (ORBmatcher.h:36-110, stateful only in its two members), with the
-// SearchByBoW body exactly as INTEGRATION.md tells a maintainer to write it.
+// bodies exactly as INTEGRATION.md tells a maintainer to write them.
 namespace ORB_SLAM3 {
 class ORBmatcher {
    public:
     ORBmatcher(float nnratio = 0.6, bool checkOri = true) : mfNNratio(nnratio), mbCheckOrientation(checkOri) {}
     int SearchByBoW(KeyFrame* pKF, Frame& F, std::vector<MapPoint*>& vpMapPointMatches);
+    int SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, std::vector<MapPoint*>& vpMatches12);
+    int SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, const float th, const bool bMono);
+    int SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const std::set<MapPoint*>& sAlreadyFound,
+                           const float th, const int ORBdist);
 
    protected:
     float mfNNratio;
@@ -303,6 +340,19 @@ class ORBmatcher {
 int ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, std::vector<MapPoint*>& vpMapPointMatches) {
     slamhot::ORBmatcher hot(mfNNratio, mbCheckOrientation);  // this thread's device handle, this call's ratio
     return slamhot::orbslam3::SearchByBoW(hot, pKF, F, vpMapPointMatches);
+}
+int ORBmatcher::SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, std::vector<MapPoint*>& vpMatches12) {
+    slamhot::ORBmatcher hot(mfNNratio, mbCheckOrientation);
+    return slamhot::orbslam3::SearchByBoW(hot, pKF1, pKF2, vpMatches12);
+}
+int ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, const float th, const bool bMono) {
+    slamhot::ORBmatcher hot(mfNNratio, mbCheckOrientation);
+    return slamhot::orbslam3::SearchByProjection(hot, CurrentFrame, LastFrame, th, bMono);
+}
+int ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const std::set<MapPoint*>& sAlreadyFound,
+                                   const float th, const int ORBdist) {
+    slamhot::ORBmatcher hot(mfNNratio, mbCheckOrientation);
+    return slamhot::orbslam3::SearchByProjection(hot, CurrentFrame, pKF, sAlreadyFound, th, ORBdist);
 }
 }  // namespace ORB_SLAM3
 
@@ -362,28 +412,506 @@ int run_bow(const char* in, const char* out) {
     return 0;
 }
 
-// Instantiations of the shims this driver does not run (they must compile against the
-// reference-shaped types; their device paths are exercised through include/slamhot.hpp).
-[[maybe_unused]] void instantiate_all(slamhot::ORBmatcher& m, slamhot::LocalMapper& lm, slamhot::StereoMatcher& sm,
-                                      slamhot::ORBextractor& exl, slamhot::ORBextractor& exr) {
-    KeyFrame kf;
+
+// ---------------------------------------------------------------- the remaining shims
+// A Frame as the matchers see it (tests/shim_io.py write_frame): pose, camera, Frame statics,
+// scale tables and per feature mvKeysUn, mvKeys, mvuRight, descriptor and the MapPoint it holds
+// on entry (-1 none, 0 one without observations, 1 one with observations; bad flag).  The
+// pre-existing MapPoints are `own` (mnId 1000000 + feature index).
+struct FrameIn {
     Frame F;
-    std::vector<MapPoint*> out, local;
-    slamhot::orbslam3::SearchByBoW(m, &kf, F, out);
-    slamhot::orbslam3::SearchLocalPoints(m, F, local, 1.f, false, 50.f);
-    slamhot::orbslam3::Fuse(lm, &kf, local, 3.f);
-    slamhot::orbslam3::ComputeStereoMatches(sm, exl, exr, F);
-    std::vector<cv::KeyPoint> kps;
-    cv::Mat img(480, 752, CV_8U), desc;
-    std::vector<int> lap{0, 0};
-    slamhot::orbslam3::ORBextractorCall(exl, img, kps, desc, lap);
+    std::vector<MapPoint> own;
+    std::vector<MapPoint*> initial;  // F.mvpMapPoints on entry
+    KeyFrame obs_kf;                 // the one KeyFrame every "observed" MapPoint is seen in
+};
+
+void add_obs(MapPoint& m, KeyFrame& k, int idx) { m.mObservations[&k] = std::make_tuple(idx, -1); }
+
+void read_frame(Reader& R, FrameIn& in) {
+    Frame& F = in.F;
+    F.N = R.get<int32_t>();
+    F.mnId = (unsigned long)R.get<int32_t>();
+    float T[16];
+    R.get(T, 16);
+    F.mTcw = mat(T, 4, 4);
+    F.fx = R.get<float>();
+    F.fy = R.get<float>();
+    F.cx = R.get<float>();
+    F.cy = R.get<float>();
+    F.mbf = R.get<float>();
+    F.mb = R.get<float>();
+    Frame::mnMinX = R.get<float>();
+    Frame::mnMinY = R.get<float>();
+    Frame::mnMaxX = R.get<float>();
+    Frame::mnMaxY = R.get<float>();
+    Frame::mfGridElementWidthInv = R.get<float>();
+    Frame::mfGridElementHeightInv = R.get<float>();
+    F.mnScaleLevels = R.get<int32_t>();
+    F.mvScaleFactors.resize(F.mnScaleLevels);
+    R.get(F.mvScaleFactors.data(), F.mnScaleLevels);
+    F.mfLogScaleFactor = R.get<float>();
+    F.mvInvLevelSigma2.resize(F.mnScaleLevels);
+    R.get(F.mvInvLevelSigma2.data(), F.mnScaleLevels);
+    const int n = F.N;
+    F.mvKeysUn.resize(n);
+    F.mvKeys.resize(n);
+    F.mvuRight.resize(n);
+    F.mDescriptors.create(n, 32, CV_8U);
+    F.mvpMapPoints.assign(n, nullptr);
+    F.mvbOutlier.assign(n, false);
+    in.own.resize(n);
+    in.obs_kf.mvuRight.assign(1, -1.f);
+    for (int i = 0; i < n; i++) {
+        R.get(&F.mvKeysUn[i], 1);
+        R.get(&F.mvKeys[i], 1);
+        F.mvuRight[i] = R.get<float>();
+        R.get(F.mDescriptors.data + 32 * (size_t)i, 32);
+        const int st = R.get<int8_t>();
+        const int bad = R.get<uint8_t>();
+        MapPoint& m = in.own[i];
+        m.mnId = 1000000ul + (unsigned long)i;
+        m.mbBad = bad != 0;
+        if (st >= 0) F.mvpMapPoints[i] = &m;
+        if (st == 1) add_obs(m, in.obs_kf, 0);
+    }
+    in.initial = F.mvpMapPoints;
+}
+
+template <class V>
+std::vector<int32_t> ids_of(const V& mps) {
+    std::vector<int32_t> out;
+    for (auto* m : mps) out.push_back(m ? (int32_t)m->mnId : -1);
+    return out;
+}
+
+// SearchByProjection(CurrentFrame, LastFrame, th, bMono) through ORB_SLAM3::ORBmatcher
+int run_projlast(const char* in, const char* out) {
+    Reader R(in);
+    FrameIn cur;
+    read_frame(R, cur);
+    Frame last;
+    last.N = R.get<int32_t>();
+    float T[16];
+    R.get(T, 16);
+    last.mTcw = mat(T, 4, 4);
+    const int n = last.N;
+    last.mvKeys.resize(n);
+    last.mvKeysUn.resize(n);
+    last.mvpMapPoints.assign(n, nullptr);
+    last.mvbOutlier.assign(n, false);
+    std::vector<MapPoint> mps(n);
+    KeyFrame obs_kf;
+    obs_kf.mvuRight.assign(1, -1.f);
+    for (int i = 0; i < n; i++) {
+        R.get(&last.mvKeys[i], 1);
+        R.get(&last.mvKeysUn[i], 1);
+        const int has = R.get<uint8_t>(), outl = R.get<uint8_t>(), obs = R.get<uint8_t>();
+        float X[3];
+        R.get(X, 3);
+        MapPoint& m = mps[i];
+        m.mnId = (unsigned long)i;
+        m.mWorldPos = mat(X, 3, 1);
+        R.get(m.mDescriptor.data, 32);
+        if (obs) add_obs(m, obs_kf, 0);
+        if (has) last.mvpMapPoints[i] = &m;
+        last.mvbOutlier[i] = outl != 0;
+    }
+    const int ncalls = R.get<int32_t>();
+    Writer O(out);
+    for (int c = 0; c < ncalls; c++) {
+        const float th = R.get<float>();
+        const int mono = R.get<int32_t>();
+        const float ratio = R.get<float>();
+        const int ori = R.get<int32_t>();
+        cur.F.mvpMapPoints = cur.initial;
+        ORB_SLAM3::ORBmatcher matcher(ratio, ori != 0);
+        const int nm = matcher.SearchByProjection(cur.F, last, th, mono != 0);
+        O.put<int32_t>(nm);
+        O.put(ids_of(cur.F.mvpMapPoints));
+    }
+    return 0;
+}
+
+// SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist) through ORB_SLAM3::ORBmatcher
+int run_projkf(const char* in, const char* out) {
+    Reader R(in);
+    FrameIn cur;
+    read_frame(R, cur);
+    KeyFrame kf;
+    kf.N = R.get<int32_t>();
+    const int n = kf.N;
+    kf.mvKeysUn.resize(n);
+    kf.mvpMapPoints.assign(n, nullptr);
+    std::vector<MapPoint> mps(n);
+    std::set<MapPoint*> found;
+    for (int i = 0; i < n; i++) {
+        R.get(&kf.mvKeysUn[i], 1);
+        const int has = R.get<uint8_t>(), bad = R.get<uint8_t>(), fnd = R.get<uint8_t>();
+        float X[3];
+        R.get(X, 3);
+        MapPoint& m = mps[i];
+        m.mnId = 2000000ul + (unsigned long)i;
+        m.mWorldPos = mat(X, 3, 1);
+        m.mfMaxDistance = R.get<float>();
+        m.mfMinDistance = R.get<float>();
+        R.get(m.mDescriptor.data, 32);
+        m.mbBad = bad != 0;
+        if (has) kf.mvpMapPoints[i] = &m;
+        if (has && fnd) found.insert(&m);
+    }
+    const int ncalls = R.get<int32_t>();
+    Writer O(out);
+    for (int c = 0; c < ncalls; c++) {
+        const float th = R.get<float>();
+        const int orb_dist = R.get<int32_t>();
+        const float ratio = R.get<float>();
+        const int ori = R.get<int32_t>();
+        cur.F.mvpMapPoints = cur.initial;
+        ORB_SLAM3::ORBmatcher matcher(ratio, ori != 0);
+        const int nm = matcher.SearchByProjection(cur.F, &kf, found, th, orb_dist);
+        O.put<int32_t>(nm);
+        O.put(ids_of(cur.F.mvpMapPoints));
+    }
+    return 0;
+}
+
+// one KeyFrame side of SearchByBoW(KF1, KF2): MapPoints present (has) and bad flags, ids base + i
+void read_kf_side(Reader& R, KeyFrame& K, std::vector<MapPoint>& mps, unsigned long base) {
+    const int n = R.get<int32_t>();
+    K.N = n;
+    K.mDescriptors.create(n, 32, CV_8U);
+    if (n) R.get(K.mDescriptors.data, (size_t)n * 32);
+    K.mvKeysUn.resize(n);
+    for (int i = 0; i < n; i++) K.mvKeysUn[i].angle = R.get<float>();
+    mps.resize(n);
+    K.mvpMapPoints.assign(n, nullptr);
+    for (int i = 0; i < n; i++) {
+        mps[i].mnId = base + (unsigned long)i;
+        if (R.get<uint8_t>()) K.mvpMapPoints[i] = &mps[i];
+    }
+    for (int i = 0; i < n; i++) mps[i].mbBad = R.get<uint8_t>() != 0;
+    const int nn = R.get<int32_t>();
+    std::vector<uint32_t> id(nn);
+    std::vector<int32_t> off(nn + 1);
+    R.get(id.data(), nn);
+    R.get(off.data(), nn + 1);
+    std::vector<uint32_t> feat(off[nn]);
+    R.get(feat.data(), feat.size());
+    for (int k = 0; k < nn; k++) K.mFeatVec[id[k]].assign(feat.begin() + off[k], feat.begin() + off[k + 1]);
+}
+
+int run_bowkk(const char* in, const char* out) {
+    Reader R(in);
+    const int ncalls = R.get<int32_t>();
+    std::vector<std::pair<float, bool>> calls;
+    for (int c = 0; c < ncalls; c++) {
+        const float r = R.get<float>();
+        calls.emplace_back(r, R.get<int32_t>() != 0);
+    }
+    KeyFrame k1, k2;
+    std::vector<MapPoint> m1, m2;
+    read_kf_side(R, k1, m1, 3000000ul);
+    read_kf_side(R, k2, m2, 0ul);
+    Writer O(out);
+    for (const auto& c : calls) {  // LoopClosing / LocalMapping build ORBmatcher(0.75, true) etc.
+        ORB_SLAM3::ORBmatcher matcher(c.first, c.second);
+        std::vector<MapPoint*> v12;
+        const int n = matcher.SearchByBoW(&k1, &k2, v12);
+        O.put<int32_t>(n);
+        O.put(ids_of(v12));
+    }
+    return 0;
+}
+
+// Frame::ComputeBoW and KeyFrame::ComputeBoW over one vocabulary per case
+int run_computebow(const char* in, const char* out) {
+    Reader R(in);
+    const int ncases = R.get<int32_t>();
+    Writer O(out);
+    for (int c = 0; c < ncases; c++) {
+        const int k = R.get<int32_t>(), L = R.get<int32_t>(), scoring = R.get<int32_t>(),
+                  weighting = R.get<int32_t>(), nn = R.get<int32_t>();
+        std::vector<int32_t> parent(nn);
+        std::vector<uint8_t> leaf(nn), ndesc(32 * (size_t)nn);
+        std::vector<double> weight(nn);
+        R.get(parent.data(), nn);
+        R.get(leaf.data(), nn);
+        R.get(ndesc.data(), ndesc.size());
+        R.get(weight.data(), nn);
+        const int nd = R.get<int32_t>();
+        Frame F;
+        F.mDescriptors.create(nd, 32, CV_8U);
+        R.get(F.mDescriptors.data, 32 * (size_t)nd);
+        KeyFrame K;
+        K.mDescriptors = F.mDescriptors.clone();
+        slamhot::Vocabulary voc(0, k, L, scoring, weighting, nn, parent.data(), leaf.data(), ndesc.data(), weight.data());
+        slamhot::orbslam3::ComputeBoW(voc, F);
+        std::memset(F.mDescriptors.data, 0, 32 * (size_t)nd);  // computed once: a second call keeps the vectors
+        slamhot::orbslam3::ComputeBoW(voc, F);
+        slamhot::orbslam3::KeyFrameComputeBoW(voc, &K);
+        for (int side = 0; side < 2; side++) {
+            const auto& bv = side ? K.mBowVec : F.mBowVec;
+            const auto& fv = side ? K.mFeatVec : F.mFeatVec;
+            std::vector<uint32_t> w, node, feat;
+            std::vector<double> val;
+            std::vector<int32_t> off{0};
+            for (const auto& kv : bv) {
+                w.push_back(kv.first);
+                val.push_back(kv.second);
+            }
+            for (const auto& kv : fv) {
+                node.push_back(kv.first);
+                feat.insert(feat.end(), kv.second.begin(), kv.second.end());
+                off.push_back((int32_t)feat.size());
+            }
+            O.put(w);
+            O.put(val);
+            O.put(node);
+            O.put(off);
+            O.put(feat);
+        }
+    }
+    return 0;
+}
+
+// ORBextractor::operator() through the shim, incl. the mvImagePyramid refresh, one extractor
+// (one camera) over several images
+int run_extract(const char* in, const char* out) {
+    Reader R(in);
+    const int nfeat = R.get<int32_t>(), nlevels = R.get<int32_t>(), ini = R.get<int32_t>(), mn = R.get<int32_t>();
+    const float scale = R.get<float>();
+    slamhot::ORBextractor ex(nfeat, scale, nlevels, ini, mn);
+    const int nimg = R.get<int32_t>();
+    Writer O(out);
+    std::vector<cv::Mat> mvImagePyramid;
+    for (int i = 0; i < nimg; i++) {
+        const int w = R.get<int32_t>(), h = R.get<int32_t>(), lap0 = R.get<int32_t>(), lap1 = R.get<int32_t>();
+        cv::Mat img;
+        if (w > 0 && h > 0) {
+            img.create(h, w, CV_8U);
+            R.get(img.data, (size_t)w * h);
+        }
+        std::vector<cv::KeyPoint> kps;
+        cv::Mat desc;
+        const std::vector<int> lap{lap0, lap1};
+        const int mono = slamhot::orbslam3::ORBextractorCall(ex, img, kps, desc, lap, &mvImagePyramid);
+        O.put<int32_t>(mono);
+        O.put(kps);
+        std::vector<uint8_t> d(desc.data, desc.data + (size_t)desc.rows * 32);
+        O.put(d);
+        O.put<int32_t>((int32_t)mvImagePyramid.size());
+        for (const cv::Mat& m : mvImagePyramid) {
+            O.put<int32_t>(m.rows);
+            O.put<int32_t>(m.cols);
+            O.put(std::vector<uint8_t>(m.data, m.data + (size_t)m.rows * m.cols));
+        }
+    }
+    return 0;
+}
+
+// the stereo Frame constructor's host path (Frame.cc:98-152): two extractions, then
+// ComputeStereoMatches
+int run_stereo(const char* in, const char* out) {
+    Reader R(in);
+    const int nfeat = R.get<int32_t>(), nlevels = R.get<int32_t>(), ini = R.get<int32_t>(), mn = R.get<int32_t>();
+    const float scale = R.get<float>();
+    Frame F;
+    F.mbf = R.get<float>();
+    F.mb = R.get<float>();
+    const int w = R.get<int32_t>(), h = R.get<int32_t>();
+    cv::Mat l(h, w, CV_8U), r(h, w, CV_8U);
+    R.get(l.data, (size_t)w * h);
+    R.get(r.data, (size_t)w * h);
+    slamhot::ORBextractor left(nfeat, scale, nlevels, ini, mn), right(nfeat, scale, nlevels, ini, mn);
+    const std::vector<int> lap{0, 0};
+    slamhot::orbslam3::ORBextractorCall(left, l, F.mvKeys, F.mDescriptors, lap);
+    slamhot::orbslam3::ORBextractorCall(right, r, F.mvKeysRight, F.mDescriptorsRight, lap);
+    slamhot::StereoMatcher sm(0);
+    slamhot::orbslam3::ComputeStereoMatches(sm, left, right, F);
+    Writer O(out);
+    O.put(F.mvKeys);
+    O.put(std::vector<uint8_t>(F.mDescriptors.data, F.mDescriptors.data + (size_t)F.mDescriptors.rows * 32));
+    O.put(F.mvKeysRight);
+    O.put(std::vector<uint8_t>(F.mDescriptorsRight.data, F.mDescriptorsRight.data + (size_t)F.mDescriptorsRight.rows * 32));
+    O.put(F.mvuRight);
+    O.put(F.mvDepth);
+    return 0;
+}
+
+// Tracking::SearchLocalPoints: the frame's own MapPoints may also sit in the local map
+// (frame_ref >= 0), the others are local-map objects (mnId 3000000 + j)
+int run_localpoints(const char* in, const char* out) {
+    Reader R(in);
+    FrameIn cur;
+    read_frame(R, cur);
+    Frame& F = cur.F;
+    const int nmp = R.get<int32_t>();
+    std::vector<MapPoint> local(nmp);
+    std::vector<MapPoint*> vpLocal(nmp);
+    KeyFrame obs_kf;
+    obs_kf.mvuRight.assign(1, -1.f);
+    for (int j = 0; j < nmp; j++) {
+        const int ref = R.get<int32_t>();
+        MapPoint* m = ref >= 0 ? &cur.own[ref] : &local[j];
+        if (ref < 0) m->mnId = 3000000ul + (unsigned long)j;
+        float X[3], N[3];
+        R.get(X, 3);
+        R.get(N, 3);
+        m->mWorldPos = mat(X, 3, 1);
+        m->mNormalVector = mat(N, 3, 1);
+        m->mfMinDistance = R.get<float>();
+        m->mfMaxDistance = R.get<float>();
+        const int seen = R.get<uint8_t>(), bad = R.get<uint8_t>(), obs = R.get<uint8_t>();
+        R.get(m->mDescriptor.data, 32);
+        if (ref < 0) {
+            m->mbBad = bad != 0;
+            if (seen) m->mnLastFrameSeen = F.mnId;
+            if (obs) add_obs(*m, obs_kf, 0);
+        }
+        vpLocal[j] = m;
+    }
+    const float th = R.get<float>();
+    const int far = R.get<int32_t>();
+    const float th_far = R.get<float>();
+    slamhot::ORBmatcher hot(0.8f);  // ORBmatcher matcher(0.8) (Tracking.cc:3234)
+    int nmatches = 0;
+    const int nToMatch = slamhot::orbslam3::SearchLocalPoints(hot, F, vpLocal, th, far != 0, th_far, &nmatches);
+    Writer O(out);
+    O.put<int32_t>(nToMatch);
+    O.put<int32_t>(nmatches);
+    O.put(ids_of(F.mvpMapPoints));
+    std::vector<uint8_t> inview;
+    std::vector<float> fl;
+    std::vector<int32_t> iv;
+    for (MapPoint* m : vpLocal) {
+        inview.push_back(m->mbTrackInView);
+        for (float v : {m->mTrackProjX, m->mTrackProjY, m->mTrackProjXR, m->mTrackDepth, m->mTrackViewCos}) fl.push_back(v);
+        iv.push_back(m->mnTrackScaleLevel);
+        iv.push_back(m->mnVisible);
+        iv.push_back(m->mnLastFrameSeen == F.mnId);
+    }
+    O.put(inview);
+    O.put(fl);
+    O.put(iv);
+    std::vector<int32_t> own_vis;
+    for (const MapPoint& m : cur.own) own_vis.push_back(m.mnVisible);
+    O.put(own_vis);
+    std::vector<int32_t> pid;
+    std::vector<float> pxy;
+    for (const auto& kv : F.mmProjectPoints) {
+        pid.push_back((int32_t)kv.first);
+        pxy.push_back(kv.second.x);
+        pxy.push_back(kv.second.y);
+    }
+    O.put(pid);
+    O.put(pxy);
+    return 0;
+}
+
+// ORBmatcher::Fuse(pKF, vpMapPoints, th) with the update half applied to the stand-in map:
+// pKF is KeyFrame 0, the other observations sit in KeyFrames 1..D (slot = MapPoint index)
+int run_fuse(const char* in, const char* out) {
+    Reader R(in);
+    KeyFrame kf;
+    kf.mnId = 0;
+    kf.N = R.get<int32_t>();
+    float T[16];
+    R.get(T, 16);
+    kf.mTcw = mat(T, 4, 4);
+    kf.fx = R.get<float>();
+    kf.fy = R.get<float>();
+    kf.cx = R.get<float>();
+    kf.cy = R.get<float>();
+    kf.mbf = R.get<float>();
+    kf.mb = R.get<float>();
+    kf.mnMinX = R.get<int32_t>();
+    kf.mnMinY = R.get<int32_t>();
+    kf.mnMaxX = R.get<int32_t>();
+    kf.mnMaxY = R.get<int32_t>();
+    kf.mfGridElementWidthInv = R.get<float>();
+    kf.mfGridElementHeightInv = R.get<float>();
+    kf.mnScaleLevels = R.get<int32_t>();
+    kf.mvScaleFactors.resize(kf.mnScaleLevels);
+    R.get(kf.mvScaleFactors.data(), kf.mnScaleLevels);
+    kf.mfLogScaleFactor = R.get<float>();
+    kf.mvInvLevelSigma2.resize(kf.mnScaleLevels);
+    R.get(kf.mvInvLevelSigma2.data(), kf.mnScaleLevels);
+    const int n = kf.N;
+    kf.mvKeysUn.resize(n);
+    kf.mvuRight.resize(n);
+    kf.mDescriptors.create(n, 32, CV_8U);
+    kf.mvpMapPoints.assign(n, nullptr);
+    for (int i = 0; i < n; i++) {
+        R.get(&kf.mvKeysUn[i], 1);
+        kf.mvuRight[i] = R.get<float>();
+        R.get(kf.mDescriptors.data + 32 * (size_t)i, 32);
+    }
+    const int nmp = R.get<int32_t>(), ndummy = R.get<int32_t>();
+    std::vector<KeyFrame> others(ndummy);
+    for (int d = 0; d < ndummy; d++) {
+        others[d].mnId = (unsigned long)(1 + d);
+        others[d].mvuRight.assign(nmp, -1.f);
+        others[d].mvpMapPoints.assign(nmp, nullptr);
+    }
+    std::vector<MapPoint> mps(nmp);
+    for (int j = 0; j < nmp; j++) {
+        MapPoint& m = mps[j];
+        m.mnId = (unsigned long)j;
+        float X[3], N[3];
+        R.get(X, 3);
+        R.get(N, 3);
+        m.mWorldPos = mat(X, 3, 1);
+        m.mNormalVector = mat(N, 3, 1);
+        m.mfMinDistance = R.get<float>();
+        m.mfMaxDistance = R.get<float>();
+        m.mbBad = R.get<uint8_t>() != 0;
+        R.get(m.mDescriptor.data, 32);
+        const int kf_idx = R.get<int32_t>(), nother = R.get<int32_t>();
+        if (kf_idx >= 0) {
+            m.mObservations[&kf] = std::make_tuple(kf_idx, -1);
+            kf.mvpMapPoints[kf_idx] = &m;
+        }
+        for (int o = 0; o < nother; o++) {
+            KeyFrame& K = others[R.get<int32_t>()];
+            m.mObservations[&K] = std::make_tuple(j, -1);
+            K.mvpMapPoints[j] = &m;
+        }
+    }
+    const int nlist = R.get<int32_t>();
+    std::vector<MapPoint*> list(nlist);
+    for (int i = 0; i < nlist; i++) {
+        const int j = R.get<int32_t>();
+        list[i] = j >= 0 ? &mps[j] : nullptr;
+    }
+    const float th = R.get<float>();
+    slamhot::LocalMapper hot(0);
+    const int nfused = slamhot::orbslam3::Fuse(hot, &kf, list, th);
+    Writer O(out);
+    O.put<int32_t>(nfused);
+    O.put(ids_of(kf.mvpMapPoints));
+    std::vector<int32_t> st, obs;
+    for (MapPoint& m : mps) {
+        st.push_back(m.mbBad);
+        st.push_back(m.Observations());
+        std::vector<std::pair<int, int>> o;
+        for (const auto& kv : m.mObservations) o.emplace_back((int)kv.first->mnId, std::get<0>(kv.second));
+        std::sort(o.begin(), o.end());
+        obs.push_back((int32_t)o.size());
+        for (const auto& p : o) {
+            obs.push_back(p.first);
+            obs.push_back(p.second);
+        }
+    }
+    O.put(st);
+    O.put(obs);
+    return 0;
 }
 
 }  // namespace
 
 int main(int argc, char** argv) {
     if (argc < 4) {
-        std::fprintf(stderr, "usage: shim_driver flatten|lba|pose|bow IN OUT\n");
+        std::fprintf(stderr, "usage: shim_driver MODE IN OUT (modes: see the header comment)\n");
         return 2;
     }
     const std::string mode = argv[1];
@@ -393,6 +921,14 @@ int main(int argc, char** argv) {
         if (mode == "pose") return run_pose(argv[2], argv[3]);
         if (mode == "bow") return run_bow(argv[2], argv[3]);
         if (mode == "lbatime") return run_lba_time(argv[2], argv[3], argc > 4 ? std::atoi(argv[4]) : 5);
+        if (mode == "bowkk") return run_bowkk(argv[2], argv[3]);
+        if (mode == "projlast") return run_projlast(argv[2], argv[3]);
+        if (mode == "projkf") return run_projkf(argv[2], argv[3]);
+        if (mode == "computebow") return run_computebow(argv[2], argv[3]);
+        if (mode == "extract") return run_extract(argv[2], argv[3]);
+        if (mode == "stereo") return run_stereo(argv[2], argv[3]);
+        if (mode == "localpoints") return run_localpoints(argv[2], argv[3]);
+        if (mode == "fuse") return run_fuse(argv[2], argv[3]);
     } catch (const slamhot::Error& e) {
         std::fprintf(stderr, "slamhot error: %s\n", e.what());
         return 3;

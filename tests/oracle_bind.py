@@ -102,6 +102,35 @@ def extract(img: np.ndarray, p: OrbParams | None = None, lap=(0, 0)):
     return kps[:n.value].copy(), desc[:n.value].copy(), mono.value
 
 
+def extract_with_pyramid(img: np.ndarray, p: OrbParams | None = None, lap=(0, 0)):
+    """ORBextractor::operator() and its mvImagePyramid from one run: (kps, desc, mono, levels)."""
+    p = p or params()
+    L = lib()
+    if not hasattr(L, "_xp_ready"):
+        P = C.c_void_p
+        L.oracle_extract_pyr.argtypes = [C.POINTER(OrbParams), P, C.c_int, C.c_int, C.c_size_t, C.c_int, C.c_int, P,
+                                         P, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), P, C.c_size_t, P, P, P]
+        L.oracle_extract_pyr.restype = C.c_int
+        L._xp_ready = True
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    cap = p.nfeatures * 2 + 64
+    kps = np.zeros(cap, KP_DTYPE)
+    desc = np.zeros((cap, 32), np.uint8)
+    n, mono = C.c_int(0), C.c_int(0)
+    pcap = w * h * 4
+    out = np.zeros(pcap, np.uint8)
+    lw = np.zeros(p.nlevels, np.int32)
+    lh = np.zeros(p.nlevels, np.int32)
+    off = np.zeros(p.nlevels, np.uint64)
+    st = L.oracle_extract_pyr(C.byref(p), _ptr(img), w, h, w, lap[0], lap[1], _ptr(kps), _ptr(desc), cap, C.byref(n),
+                              C.byref(mono), _ptr(out), pcap, _ptr(lw), _ptr(lh), _ptr(off))
+    if st != 0:
+        raise RuntimeError(f"oracle_extract_pyr status {st}")
+    pyr = [out[int(off[l]): int(off[l]) + lw[l] * lh[l]].reshape(lh[l], lw[l]) for l in range(p.nlevels)]
+    return kps[:n.value].copy(), desc[:n.value].copy(), mono.value, pyr
+
+
 def levels(p: OrbParams | None = None):
     p = p or params()
     L = p.nlevels
@@ -246,6 +275,30 @@ def vocab_transform(parent, is_leaf, desc_nodes, weight_nodes, L, desc, levelsup
     _mlib().oracle_vocab_transform(L, _ptr(ptr), _ptr(idx), _ptr(dn), _ptr(leaf), _ptr(word), _ptr(wn), n,
                                    _ptr(desc), levelsup, _ptr(w), _ptr(wt), _ptr(nid))
     return w, wt, nid
+
+
+def bow_vectors(word, weight, node, scoring=0, weighting=0):
+    """TemplatedVocabulary::transform's BowVector / FeatureVector from the per-feature descent
+    (oracle/matcher_oracle.cpp oracle_bow_vectors): (words, values, nodes, offsets, features)."""
+    L = _mlib()
+    if not hasattr(L, "_bv_ready"):
+        P = C.c_void_p
+        L.oracle_bow_vectors.argtypes = [C.c_int, P, P, P, C.c_int, C.c_int, P, P, P, P, P, P, P]
+        L.oracle_bow_vectors.restype = None
+        L._bv_ready = True
+    word = np.ascontiguousarray(word, np.int32)
+    weight = np.ascontiguousarray(weight, np.float64)
+    node = np.ascontiguousarray(node, np.int32)
+    n = len(word)
+    nw, nn = C.c_int(0), C.c_int(0)
+    bw = np.zeros(max(n, 1), np.uint32)
+    bv = np.zeros(max(n, 1), np.float64)
+    fn = np.zeros(max(n, 1), np.uint32)
+    fo = np.zeros(n + 1, np.int32)
+    ff = np.zeros(max(n, 1), np.uint32)
+    L.oracle_bow_vectors(n, _ptr(word), _ptr(weight), _ptr(node), scoring, weighting, C.byref(nw), _ptr(bw), _ptr(bv),
+                         C.byref(nn), _ptr(fn), _ptr(fo), _ptr(ff))
+    return bw[:nw.value], bv[:nw.value], fn[:nn.value], fo[:nn.value + 1], ff[:fo[nn.value]]
 
 
 def search_by_bow(A, B, nnratio, check_ori, strict):

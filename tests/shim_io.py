@@ -80,3 +80,62 @@ def read_flatten(b: Blob):
                   ("edge_obs", "<f4"), ("edge_inv_sigma2", "<f4"), ("edge_body", "u1"), ("kf_Trl", "<f4")):
         out[k] = b.vec(dt)
     return out
+
+
+class Out:
+    """Little-endian writer for the shim_driver input files."""
+
+    def __init__(self):
+        self.b = bytearray()
+
+    def i32(self, *v):
+        self.b += struct.pack(f"<{len(v)}i", *[int(x) for x in v])
+        return self
+
+    def f32(self, *v):
+        self.b += struct.pack(f"<{len(v)}f", *[float(x) for x in v])
+        return self
+
+    def raw(self, a, dt=None):
+        a = np.ascontiguousarray(a if dt is None else np.asarray(a, dt))
+        self.b += a.tobytes()
+        return self
+
+    def save(self, path):
+        Path(path).write_bytes(bytes(self.b))
+        return path
+
+
+def level_tables(nlevels=8, scale_factor=1.2):
+    """mvScaleFactors / mvInvLevelSigma2 / mfLogScaleFactor as ORBextractor / Frame compute them
+    (ORBextractor.cc:413-425, Frame.cc:107-113): the oracle's own tables."""
+    import oracle_bind as ob
+    sc, isc, s2, is2, _ = ob.levels(ob.params(nlevels=nlevels, scale=scale_factor))
+    lsf = np.float32(np.log(np.float64(np.float32(scale_factor))))
+    return sc, is2, lsf
+
+
+def write_frame(o: Out, fv, kps_un, kps, uright, desc, state, bad, Tcw, mnId=7):
+    """A stand-in Frame for shim_driver (read_frame): fv is the slam_frame_view the oracle is given
+    for the same Frame (its bounds, grid, camera and scale tables are written from it)."""
+    import ctypes as C
+    n = len(kps_un)
+    o.i32(n, mnId).raw(Tcw, np.float32)
+    o.f32(fv.fx, fv.fy, fv.cx, fv.cy, fv.bf, fv.b)
+    o.f32(fv.min_x, fv.min_y, fv.max_x, fv.max_y, fv.grid_inv_w, fv.grid_inv_h)
+    sc = np.ctypeslib.as_array(C.cast(fv.scale, C.POINTER(C.c_float)), (fv.nlevels,)).copy()
+    _, is2, _ = level_tables(fv.nlevels)
+    o.i32(fv.nlevels).raw(sc, np.float32).f32(fv.log_scale).raw(is2, np.float32)
+    rec = np.zeros(n, np.dtype([("ku", "V28"), ("k", "V28"), ("ur", "<f4"), ("d", "u1", 32), ("st", "i1"), ("bad", "u1")]))
+    rec["ku"] = np.ascontiguousarray(kps_un).view("V28")
+    rec["k"] = np.ascontiguousarray(kps).view("V28")
+    rec["ur"] = uright
+    rec["d"] = desc
+    rec["st"] = state
+    rec["bad"] = bad
+    o.raw(rec)
+    return o
+
+
+def run_any(mode, out: Out, tmp_path, name="in.bin"):
+    return run(mode, out.save(Path(tmp_path) / name), Path(tmp_path) / (name + ".out"))

@@ -161,9 +161,11 @@ def test_lba_stop_flag_mid_solve(solver):
     """mbAbortBA set while the device LM loop runs: the solve stops early (g2o checks terminate()
     per iteration and per trial), every window's trajectory is a prefix of the unstopped one,
     outputs stay finite, and a stop inside optimize(5) skips optimize(10) (Optimizer.cc:
-    1933-1935).  Deterministic: the caller's live bool is set by the solver's step hook
-    (slam_lba_options.step_hook) once LM step k's counters are in, a fixed point of the loop
-    instead of a wall-clock time; the solver then reads it like any other thread's write."""
+    1933-1935).  The caller's live bool is set by the solver's step hook
+    (slam_lba_options.step_hook) once LM step k's counters are in, a known point of the loop
+    instead of a wall-clock time; the solver then reads it like any other thread's write, so the
+    stop lands within the steps already queued behind k (the host's ring, at most 3 more) — the
+    bound is what is asserted, not an exact step."""
     import ctypes as C
     Ws = [synth.lba_window(200 + i, n_kf=20, n_pt=500, obs_per_pt=6, stereo_frac=0.2 * (i % 2)) for i in range(8)]
     flag = C.c_bool(False)
