@@ -464,6 +464,11 @@ void slamhot_lba_destroy(slam_lba* s);
 slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* probs,
                               const slam_lba_options* opt, const volatile int32_t* stop_flag,
                               slam_lba_result* results);
+/* Warm a handle for windows of about n_kf KeyFrames x n_pt MapPoints x obs_per_pt observations:
+ * one synthetic window of that size is solved, which loads every kernel of the single-window path
+ * and sizes the device buffers and the pinned staging arena, so LocalMapping's first
+ * LocalBundleAdjustment (LocalMapping.cc:161) costs what every later one does. */
+slam_status slamhot_lba_warmup(slam_lba* s, int n_kf, int n_pt, int obs_per_pt);
 /* Last solve: device time (ms, kernels + copies), host plan time (ms: graph structure build
  * and upload, buildStructure in g2o), and the number of host<->device round trips. */
 slam_status slamhot_lba_last_stats(const slam_lba* s, double* device_ms, double* plan_ms, int* syncs);

@@ -418,7 +418,20 @@ struct LocalBAResult {
 
 class LocalBundleAdjuster {
    public:
-    explicit LocalBundleAdjuster(int device = 0) { check(slamhot_lba_create(device, &s_), "LocalBundleAdjuster"); }
+    /* warm: solve one synthetic window of warm_kf x warm_pt x warm_obs at construction
+     * (slamhot_lba_warmup) so the first LocalBundleAdjustment is not the one that loads kernels and
+     * allocates; the default is the config-4 window (50 KeyFrames, 2000 MapPoints, 8 observations) */
+    explicit LocalBundleAdjuster(int device = 0, bool warm = true, int warm_kf = 50, int warm_pt = 2000,
+                                 int warm_obs = 8) {
+        check(slamhot_lba_create(device, &s_), "LocalBundleAdjuster");
+        if (warm) {
+            const slam_status st = slamhot_lba_warmup(s_, warm_kf, warm_pt, warm_obs);
+            if (st != SLAM_OK) {
+                slamhot_lba_destroy(s_);
+                throw Error(st, "LocalBundleAdjuster warm-up");
+            }
+        }
+    }
     ~LocalBundleAdjuster() { slamhot_lba_destroy(s_); }
     LocalBundleAdjuster(const LocalBundleAdjuster&) = delete;
     LocalBundleAdjuster& operator=(const LocalBundleAdjuster&) = delete;

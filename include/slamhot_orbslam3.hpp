@@ -31,7 +31,9 @@
 #ifndef SLAMHOT_ORBSLAM3_HPP
 #define SLAMHOT_ORBSLAM3_HPP
 
+#include <algorithm>
 #include <cmath>
+#include <cstring>
 #include <list>
 #include <map>
 #include <mutex>
@@ -452,8 +454,13 @@ void ComputeStereoMatches(slamhot::StereoMatcher& hot, ORBextractor& left, ORBex
 /* ------------------------------------------------------------------ Optimizer::LocalBundleAdjustment */
 template <class KeyFrame, class MapPoint>
 struct LocalWindow {
-    std::list<KeyFrame*> lLocalKeyFrames, lFixedCameras;
-    std::list<MapPoint*> lLocalMapPoints;
+    using Observations = decltype(std::declval<MapPoint&>().GetObservations());
+    std::vector<KeyFrame*> lLocalKeyFrames, lFixedCameras;  // the reference's std::lists, same order
+    std::vector<MapPoint*> lLocalMapPoints;
+    // GetObservations() of every local MapPoint, in lLocalMapPoints order: read once for the fixed
+    // cameras (Optimizer.cc:1655-1672) and reused by the edge setup (:1815), which the reference
+    // fetches a second time from the unchanged map
+    std::vector<Observations> observations;
     int num_fixedKF = 0;
 };
 
@@ -479,9 +486,11 @@ bool BuildLocalWindow(KeyFrame* pKF, Map* pMap, LocalWindow<KeyFrame, MapPoint>&
                 pMP->mnBALocalForKF = pKF->mnId;
             }
     }
+    W.observations.clear();
+    W.observations.reserve(W.lLocalMapPoints.size());
     for (MapPoint* pMP : W.lLocalMapPoints) {
-        const auto observations = pMP->GetObservations();
-        for (const auto& ob : observations) {
+        W.observations.push_back(pMP->GetObservations());
+        for (const auto& ob : W.observations.back()) {
             KeyFrame* pKFi = ob.first;
             if (pKFi->mnBALocalForKF != pKF->mnId && pKFi->mnBAFixedForKF != pKF->mnId) {
                 pKFi->mnBAFixedForKF = pKF->mnId;
@@ -503,14 +512,18 @@ bool BuildLocalWindow(KeyFrame* pKF, Map* pMap, LocalWindow<KeyFrame, MapPoint>&
                 pSecondLowerKF = pKFi;
             }
         }
+        auto remove = [&](KeyFrame* k) {  // std::list::remove
+            W.lLocalKeyFrames.erase(std::remove(W.lLocalKeyFrames.begin(), W.lLocalKeyFrames.end(), k),
+                                    W.lLocalKeyFrames.end());
+        };
         if (pLowerKf) {
             W.lFixedCameras.push_back(pLowerKf);
-            W.lLocalKeyFrames.remove(pLowerKf);
+            remove(pLowerKf);
             W.num_fixedKF++;
         }
         if (W.num_fixedKF < 2 && pSecondLowerKF) {
             W.lFixedCameras.push_back(pSecondLowerKF);
-            W.lLocalKeyFrames.remove(pSecondLowerKF);
+            remove(pSecondLowerKF);
             W.num_fixedKF++;
         }
     }
@@ -527,17 +540,34 @@ void FlattenLocalWindow(const LocalWindow<KeyFrame, MapPoint>& W, Map* pMap, Loc
     kfs.assign(W.lLocalKeyFrames.begin(), W.lLocalKeyFrames.end());
     kfs.insert(kfs.end(), W.lFixedCameras.begin(), W.lFixedCameras.end());
     std::stable_sort(kfs.begin(), kfs.end(), [](KeyFrame* a, KeyFrame* b) { return a->mnId < b->mnId; });
-    std::map<KeyFrame*, int> index;
-    const std::set<KeyFrame*> fixed(W.lFixedCameras.begin(), W.lFixedCameras.end());
+    // vertex index of a KeyFrame: a pointer-sorted table (a few dozen entries, binary search)
+    std::vector<std::pair<KeyFrame*, int>> index(kfs.size());
+    for (size_t k = 0; k < kfs.size(); k++) index[k] = {kfs[k], (int)k};
+    std::sort(index.begin(), index.end());
+    auto vertex_of = [&](KeyFrame* k) -> int {
+        auto it = std::lower_bound(index.begin(), index.end(), std::make_pair(k, -1));
+        return it != index.end() && it->first == k ? it->second : -1;
+    };
+    std::vector<KeyFrame*> fixed(W.lFixedCameras.begin(), W.lFixedCameras.end());
+    std::sort(fixed.begin(), fixed.end());
     out = LocalBAWindow{};
+    size_t nobs = 0;
+    for (const auto& o : W.observations) nobs += o.size();
+    out.kf_Tcw.reserve(16 * kfs.size());
+    out.pt_pos.reserve(3 * W.lLocalMapPoints.size());
+    out.edge_pt.reserve(nobs);
+    out.edge_kf.reserve(nobs);
+    out.edge_obs.reserve(3 * nobs);
+    out.edge_inv_sigma2.reserve(nobs);
+    edge_refs.reserve(edge_refs.size() + nobs);
     bool rig = false;
     for (size_t k = 0; k < kfs.size(); k++) {
         KeyFrame* pKFi = kfs[k];
-        index[pKFi] = (int)k;
         float T[16];
         mat4(pKFi->GetPose(), T);
         out.kf_Tcw.insert(out.kf_Tcw.end(), T, T + 16);
-        out.kf_fixed.push_back(fixed.count(pKFi) ? 2 : (pKFi->mnId == pMap->GetInitKFid() ? 1 : 0));  // :1741-1744
+        const bool is_fixed = std::binary_search(fixed.begin(), fixed.end(), pKFi);
+        out.kf_fixed.push_back(is_fixed ? 2 : (pKFi->mnId == pMap->GetInitKFid() ? 1 : 0));  // :1741-1744
         rig = rig || pKFi->mpCamera2 != nullptr;
     }
     if (rig) {
@@ -552,18 +582,17 @@ void FlattenLocalWindow(const LocalWindow<KeyFrame, MapPoint>& W, Map* pMap, Loc
     for (MapPoint* pMP : W.lLocalMapPoints) {
         const cv::Mat P = pMP->GetWorldPos();
         for (int c = 0; c < 3; c++) out.pt_pos.push_back(P.template at<float>(c));
-        const auto observations = pMP->GetObservations();
-        for (const auto& ob : observations) {
+        for (const auto& ob : W.observations[pi]) {
             KeyFrame* pKFi = ob.first;
             if (pKFi->isBad() || pKFi->GetMap() != pCurrentMap) continue;
-            auto it = index.find(pKFi);
-            if (it == index.end()) continue;
+            const int vk = vertex_of(pKFi);
+            if (vk < 0) continue;
             const int leftIndex = std::get<0>(ob.second);
             if (leftIndex != -1) {  // mono (:1819-1849) or stereo (:1850-1880)
                 const cv::KeyPoint& kpUn = pKFi->mvKeysUn[leftIndex];
                 const float ur = pKFi->mvuRight[leftIndex];
                 out.edge_pt.push_back(pi);
-                out.edge_kf.push_back(it->second);
+                out.edge_kf.push_back(vk);
                 out.edge_obs.push_back(kpUn.pt.x);
                 out.edge_obs.push_back(kpUn.pt.y);
                 out.edge_obs.push_back(ur < 0 ? -1.f : ur);
@@ -577,7 +606,7 @@ void FlattenLocalWindow(const LocalWindow<KeyFrame, MapPoint>& W, Map* pMap, Loc
                     rightIndex -= pKFi->NLeft;
                     const cv::KeyPoint& kp = pKFi->mvKeysRight[rightIndex];
                     out.edge_pt.push_back(pi);
-                    out.edge_kf.push_back(it->second);
+                    out.edge_kf.push_back(vk);
                     out.edge_obs.push_back(kp.pt.x);
                     out.edge_obs.push_back(kp.pt.y);
                     out.edge_obs.push_back(-1.f);
@@ -645,12 +674,16 @@ void LocalBundleAdjustment(LocalBundleAdjuster& hot, KeyFrame* pKF, bool* pbStop
             edge_refs[e].first->EraseMapPointMatch(edge_refs[e].second);
             edge_refs[e].second->EraseObservation(edge_refs[e].first);
         }
-    const std::set<KeyFrame*> local(W.lLocalKeyFrames.begin(), W.lLocalKeyFrames.end());
-    for (size_t k = 0; k < kfs.size(); k++)                 // :2056-2063
-        if (local.count(kfs[k])) kfs[k]->SetPose(mat_from(&R.kf_Tcw[16 * k], 4, 4));
+    cv::Mat Tcw(4, 4, CV_32F), Pos(3, 1, CV_32F);           // SetPose / SetWorldPos copy their argument
+    for (size_t k = 0; k < kfs.size(); k++) {               // :2056-2063
+        if (flat.kf_fixed[k] == 2) continue;                 // lFixedCameras are not written back
+        std::memcpy(Tcw.data, &R.kf_Tcw[16 * k], 16 * sizeof(float));
+        kfs[k]->SetPose(Tcw);
+    }
     int i = 0;
     for (MapPoint* pMP : W.lLocalMapPoints) {               // :2066-2074
-        pMP->SetWorldPos(mat_from(&R.pt_pos[3 * (size_t)i++], 3, 1));
+        std::memcpy(Pos.data, &R.pt_pos[3 * (size_t)i++], 3 * sizeof(float));
+        pMP->SetWorldPos(Pos);
         pMP->UpdateNormalAndDepth();
     }
     pMap->IncreaseChangeIndex();

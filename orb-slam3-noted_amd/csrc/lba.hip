@@ -2105,6 +2105,27 @@ __global__ void k_finalize_state(int nkf_total, int npt_total, const int* __rest
     }
 }
 
+// The per-solve clears (pose bitmaps, increments, errors, tile scratch, the control tally) in one
+// launch instead of one fill per buffer
+struct ClearRange {
+    unsigned long long* p;
+    long long n;             // 8-byte words
+    unsigned long long v;    // fill value
+};
+constexpr int kClearMax = 12;
+struct ClearList {
+    ClearRange r[kClearMax];
+    int n;
+};
+__global__ void k_clear(ClearList L) {
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (int i = 0; i < L.n; i++) {
+        unsigned long long* p = L.r[i].p;
+        const unsigned long long v = L.r[i].v;
+        for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < L.r[i].n; e += stride) p[e] = v;
+    }
+}
+
 // Converter::toSE3Quat on the device for the initial estimates
 __global__ void k_init_state(int nkf_total, int npt_total, const float* __restrict__ kf_in,
                              const float* __restrict__ pt_in, double* __restrict__ poses,
@@ -2582,6 +2603,71 @@ void slamhot_lba_destroy(slam_lba* s) {
     delete s;
 }
 
+// A synthetic window of the given size solved once: loads every kernel of the single-window path
+// and sizes the device buffers and the pinned arena, so the caller's first real solve pays none of
+// that.  KeyFrames along a line looking down +z (the first two fixed), points in front of them,
+// each seen by obs_per_pt consecutive KeyFrames (noise-free projections, every fourth stereo).
+slam_status slamhot_lba_warmup(slam_lba* s, int n_kf, int n_pt, int obs_per_pt) {
+    if (!s || n_kf < 3 || n_pt < 1 || obs_per_pt < 2 || obs_per_pt > n_kf) return SLAM_EINVAL;
+    const slam_camera cam{435.2f, 435.2f, 367.45f, 252.2f, 47.9f};
+    std::vector<float> Tcw(16 * (size_t)n_kf, 0.f), pts(3 * (size_t)n_pt), obs, isig;
+    std::vector<uint8_t> fixed(n_kf, 0);
+    std::vector<int32_t> ept, ekf;
+    fixed[0] = 1;
+    fixed[1] = 2;
+    for (int k = 0; k < n_kf; k++) {
+        float* T = &Tcw[16 * (size_t)k];
+        T[0] = T[5] = T[10] = T[15] = 1.f;
+        T[3] = -(0.05f * (float)k - 0.025f * (float)n_kf);  // t = -C, C = (x_k, 0, 0)
+    }
+    uint32_t lcg = 12345u;
+    auto uni = [&]() {
+        lcg = lcg * 1664525u + 1013904223u;
+        return (float)(lcg >> 8) * (1.0f / 16777216.0f);
+    };
+    for (int p = 0; p < n_pt; p++) {
+        float* X = &pts[3 * (size_t)p];
+        X[0] = 3.f * uni() - 1.5f;
+        X[1] = 2.f * uni() - 1.f;
+        X[2] = 3.f + 5.f * uni();
+        const int k0 = p % (n_kf - obs_per_pt + 1);
+        for (int j = 0; j < obs_per_pt; j++) {
+            const int k = k0 + j;
+            const float xc = X[0] + Tcw[16 * (size_t)k + 3], z = X[2];
+            const float u = cam.fx * xc / z + cam.cx + 0.3f * (uni() - 0.5f);
+            const float v = cam.fy * X[1] / z + cam.cy + 0.3f * (uni() - 0.5f);
+            ept.push_back(p);
+            ekf.push_back(k);
+            obs.push_back(u);
+            obs.push_back(v);
+            obs.push_back((ept.size() & 3) == 0 ? u - cam.bf / z : -1.f);
+            isig.push_back(1.f);
+        }
+    }
+    slam_lba_problem P{};
+    P.n_kf = n_kf;
+    P.kf_Tcw = Tcw.data();
+    P.kf_fixed = fixed.data();
+    P.n_pt = n_pt;
+    P.pt_pos = pts.data();
+    P.n_edge = (int32_t)ept.size();
+    P.edge_pt = ept.data();
+    P.edge_kf = ekf.data();
+    P.edge_obs = obs.data();
+    P.edge_inv_sigma2 = isig.data();
+    P.cam = cam;
+    std::vector<float> kf_out(Tcw.size()), pt_out(pts.size());
+    std::vector<uint8_t> outl(ept.size());
+    slam_lba_result R{};
+    R.kf_Tcw = kf_out.data();
+    R.pt_pos = pt_out.data();
+    R.edge_outlier = outl.data();
+    slam_lba_options opt{};
+    opt.iters_first = 5;
+    opt.iters_second = 10;
+    return slamhot_lba_solve(s, 1, &P, &opt, nullptr, &R);
+}
+
 slam_status slamhot_lba_last_stats(const slam_lba* s, double* device_ms, double* plan_ms, int* syncs) {
     if (!s) return SLAM_EINVAL;
     if (device_ms) *device_ms = s->last_ms;
@@ -2682,7 +2768,6 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     SLAM_HIP_TRY(s->ct.ensure(sizeof(int4) * std::max<long long>(Z.nct, 1)));
     SLAM_HIP_TRY(s->ct_off.ensure(sizeof(int) * (Z.nblk + 1)));
     SLAM_HIP_TRY(s->ct_cnt.ensure(sizeof(int) * std::max(Z.nblk, 1)));
-    SLAM_HIP_TRY(hipMemsetAsync(s->bm.p, 0, sizeof(unsigned long long) * std::max<long long>(Z.nbm, 1), S));
     // tile LDL^T (k_ldlt_t16) when every window fits 18 tile rows (SLAMHOT_LDLT=panel: old kernel)
     const char* ldlt_env = std::getenv("SLAMHOT_LDLT");
     const bool use_t16 = Z.max_n <= 16 * kT16Max && !(ldlt_env && !std::strcmp(ldlt_env, "panel"));
@@ -2691,9 +2776,6 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     SLAM_HIP_TRY(s->kf_out.ensure(sizeof(float) * 16 * std::max(H.nkf, 1)));
     SLAM_HIP_TRY(s->pt_out.ensure(sizeof(float) * 3 * npt));
     SLAM_HIP_TRY(s->outl.ensure(ne));
-    SLAM_HIP_TRY(hipMemsetAsync(s->xp.p, 0, sizeof(double) * 6 * nps, S));
-    SLAM_HIP_TRY(hipMemsetAsync(s->xl.p, 0, sizeof(double) * 4 * npt, S));
-    SLAM_HIP_TRY(hipMemsetAsync(s->err.p, 0, sizeof(double) * 4 * ne, S));
     s->last_plan_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_plan0).count();
 
     Cam cam;  // the batch's one calibration, or per-KeyFrame records (PlanSizes::per_kf_cam)
@@ -2721,11 +2803,34 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     WinDesc* dW = DP.wins;
     WinCtl* dC = DP.ctl;
     int* dTally = as<int>(s->cnt);
-    SLAM_HIP_TRY(hipMemsetAsync(dTally, 0, sizeof(int) * 8, S));
     double* poses = as<double>(s->poses);
     double* pts = as<double>(s->pts);
     const int T = 256;
+    // the caller's stop flag as the device sees it at the start (k_trial_control's samples, tally
+    // words 4 and 5)
+    *s->h_stop = user_stop() ? 1 : 0;
     SLAM_HIP_TRY(hipEventRecord(s->ev0, S));
+    {
+        ClearList CL{};
+        long long most = 0;
+        auto add = [&](void* p, long long words, unsigned long long v) {
+            if (CL.n >= kClearMax) return;  // sized for the ranges below (static_assert-like guard)
+            CL.r[CL.n++] = ClearRange{(unsigned long long*)p, words, v};
+            most = std::max(most, words);
+        };
+        add(s->bm.p, std::max<long long>(Z.nbm, 1), 0ull);
+        add(s->xp.p, 6 * (long long)nps, 0ull);
+        add(s->xl.p, 4 * (long long)npt, 0ull);
+        add(s->err.p, 4 * (long long)ne, 0ull);
+        const unsigned long long st2 = (unsigned long long)(unsigned)*s->h_stop;
+        add(dTally, 1, 0ull);                                         // need, active
+        add(dTally + 2, 1, 0ull);                                     // ticket, -
+        add(dTally + 4, 1, st2 | (st2 << 32));                        // stop samples x 2
+        add(dTally + 6, 1, 0ull);
+        if (use_t16) add(s->Ts.p, t16_tiles_bytes() * nw / 8, 0ull);  // tile scratch (padding by k_t16_pad)
+        if (CL.n != (use_t16 ? 9 : 8)) return SLAM_EINVAL;  // every range above made it into the list
+        k_clear<<<(unsigned)std::min<long long>(1024, (most + 255) / 256), 256, 0, S>>>(CL);
+    }
     k_init_state<<<blocks(H.nkf + H.npt, T), T, 0, S>>>(H.nkf, H.npt, DP.kf_in, DP.pt_in,
                                                          poses, pts);
     k_ldlt_pad<<<nw, 64, 0, S>>>(dW, as<double>(s->Hs));
@@ -2749,10 +2854,7 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
                                                      as<int>(s->pls), as<int>(s->ct_off), as<int4>(s->ct));
     }
     double* tiles = use_t16 ? as<double>(s->Ts) : nullptr;
-    if (use_t16) {
-        SLAM_HIP_TRY(hipMemsetAsync(s->Ts.p, 0, (size_t)t16_tiles_bytes() * nw, S));
-        k_t16_pad<<<nw, 64, 0, S>>>(dW, tiles);
-    }
+    if (use_t16) k_t16_pad<<<nw, 64, 0, S>>>(dW, tiles);
     const size_t lds_bytes = ldlt_lds_bytes(Z.max_n);
     // Schur complement by block row (k_schur_rows: a workgroup per free pose) for batches with
     // enough rows to fill the chip; a few windows (LocalMapping's one-window call) keep the
@@ -2765,8 +2867,6 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     // the other windows, so the host queues steps without waiting for any decision and reads
     // the per-step counters asynchronously (a ring of kRing steps in flight).  While it waits it
     // mirrors the caller's stop flag into pinned memory the control kernels read.
-    *s->h_stop = user_stop() ? 1 : 0;
-    SLAM_HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(dTally + 4), *s->h_stop, 2, S));  // the device's samples
     bool stopped = false;
     int syncs = 0, step_no = 0;
     const int iters_of[2] = {opt->iters_first, opt->iters_second};

@@ -22,6 +22,7 @@
 #include <mutex>
 #include <sstream>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "common.hpp"
@@ -1998,51 +1999,122 @@ struct Stager {
     }
 };
 
+// Frame::AssignFeaturesToGrid (Frame.cc:380-411) + PosInGrid (:708-718) for the batched calls,
+// workgroup per frame: (cell << 16 | index) keys sorted in LDS (the keys are unique, so the order
+// inside a cell is the insertion order), cell starts by binary search.  Frames above
+// kGridSortMax features keep the host-built grid.
+constexpr int kGridSortMax = 4096;
+__global__ void __launch_bounds__(1024) k_frame_grid(const DevProjCall* __restrict__ calls) {
+    __shared__ uint32_t keys[kGridSortMax];
+    const DevProjCall& C = calls[blockIdx.x];
+    const int n = C.F.n;
+    if (n > kGridSortMax || !C.grid_on_device) return;
+    const float min_x = C.F.min_x, min_y = C.F.min_y, inv_w = C.F.inv_w, inv_h = C.F.inv_h;
+    int npad = 1;
+    while (npad < n) npad <<= 1;
+    for (int i = threadIdx.x; i < npad; i += blockDim.x) {
+        uint32_t k = 0xFFFFFFFFu;
+        if (i < n) {
+            const slam_keypoint kp = C.F.kps[i];
+            const int px = (int)roundf((kp.x - min_x) * inv_w);
+            const int py = (int)roundf((kp.y - min_y) * inv_h);
+            if (px >= 0 && px < kGridCols && py >= 0 && py < kGridRows)
+                k = ((uint32_t)(px * kGridRows + py) << 16) | (uint32_t)i;
+        }
+        keys[i] = k;
+    }
+    __syncthreads();
+    for (int kk = 2; kk <= npad; kk <<= 1)
+        for (int j = kk >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < npad; i += blockDim.x) {
+                const int l = i ^ j;
+                if (l > i) {
+                    const uint32_t a = keys[i], b = keys[l];
+                    if ((a > b) == ((i & kk) == 0)) {
+                        keys[i] = b;
+                        keys[l] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    int32_t* cs = const_cast<int32_t*>(C.F.cell_start);
+    int32_t* cf = const_cast<int32_t*>(C.F.cell_feat);
+    for (int c = threadIdx.x; c <= kGridCols * kGridRows; c += blockDim.x) {  // lower_bound(c << 16)
+        int lo = 0, hi = npad;
+        const uint32_t key = (uint32_t)c << 16;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (keys[mid] < key) lo = mid + 1;
+            else hi = mid;
+        }
+        cs[c] = lo;
+    }
+    for (int i = threadIdx.x; i < n; i += blockDim.x)
+        if (keys[i] != 0xFFFFFFFFu) cf[i] = (int32_t)(keys[i] & 0xFFFFu);
+}
+
+// f(i) for i in [0, n) on up to `cap` host threads (the caller's thread included)
+void parallel_for(int n, int cap, const std::function<void(int)>& f) {
+    const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
+    const int nth = std::max(1, std::min({cap, hw, n / 8}));
+    if (nth <= 1) {
+        for (int i = 0; i < n; i++) f(i);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int t = 1; t < nth; t++)
+        th.emplace_back([&, t] {
+            for (int i = t; i < n; i += nth) f(i);
+        });
+    for (int i = 0; i < n; i += nth) f(i);
+    for (auto& x : th) x.join();
+}
+
 // Batched SearchByProjection over nframes independent problems of one mode (last frame /
-// KeyFrame): every frame's inputs, grid and call record staged into one pinned host image and
-// uploaded with one copy, one k_search_by_projection launch (a workgroup per frame), every
-// frame's f_match / counters back with one copy.  `inputs(f, S, C)` puts the mode's per-frame
-// inputs and returns the query count; a frame whose candidates overflow the preset capacity
-// goes again through `single(f)`.
+// KeyFrame): every frame's inputs and call record staged into one pinned host image (a sizing
+// pass fixes every frame's offset, then the frames are copied in on several host threads) and
+// uploaded with one copy; the Frame grids built on the device (k_frame_grid); one
+// k_search_by_projection launch (a workgroup per frame); every frame's f_match / counters back
+// with one copy.  `inputs(f, S, C)` puts the mode's per-frame inputs and returns the query count;
+// a frame whose candidates overflow the preset capacity goes again through `single(f)`.
 slam_status run_projection_batch(slam_matcher* m, int nframes, const slam_frame_view* frames, const DevProjCall& proto,
                                  const std::function<int(int, Stager&, DevProjCall&)>& inputs,
                                  int32_t* const* f_match, int32_t* nmatches,
                                  const std::function<slam_status(int, int*)>& single) {
+    constexpr int kStageThreads = 8;
+    const int ncell = kGridCols * kGridRows;
     std::vector<std::vector<int32_t>> starts(nframes), feats(nframes);
-    for (int f = 0; f < nframes; f++) build_grid_csr(&frames[f], starts[f], feats[f]);
+    for (int f = 0; f < nframes; f++)
+        if (frames[f].n > kGridSortMax) build_grid_csr(&frames[f], starts[f], feats[f]);
     std::vector<DevProjCall> calls(nframes);
-    std::vector<size_t> fm_off(nframes), out_off(nframes);
+    std::vector<size_t> frame_off(nframes), fm_off(nframes), out_off(nframes);
     size_t in_bytes = 0, res_off = 0, total = 0, lds = 0, calls_off = 0;
-    std::unique_lock<std::mutex> g(m->mu);
-    SLAM_HIP_TRY(hipSetDevice(m->device));
-    for (int pass = 0; pass < 2; pass++) {
-        Stager S;
-        if (pass == 1) {
-            slam_status st;
-            if ((st = m->d_a.ensure(total)) || (st = m->stage(in_bytes + (total - res_off)))) return st;
-            S.host = m->h_stage;
-            S.dev = m->d_a.as<uint8_t>();
-        }
-        for (int f = 0; f < nframes; f++) {
-            const slam_frame_view& F = frames[f];
-            DevProjCall C = proto;
-            fill_frame(C, &F);
-            C.F.n = F.n;
-            C.F.kps = S.put(F.kps_un, F.n);
-            C.F.uright = S.put(F.uright, F.n);
-            C.F.desc = S.put(F.desc, (size_t)F.n * 32);
-            C.F.state = S.put(F.mp_state, F.n);
+    auto stage_frame = [&](int f, Stager& S) {
+        const slam_frame_view& F = frames[f];
+        DevProjCall C = proto;
+        fill_frame(C, &F);
+        C.F.n = F.n;
+        C.F.kps = S.put(F.kps_un, F.n);
+        C.F.uright = S.put(F.uright, F.n);
+        C.F.desc = S.put(F.desc, (size_t)F.n * 32);
+        C.F.state = S.put(F.mp_state, F.n);
+        C.grid_on_device = F.n <= kGridSortMax;
+        if (!C.grid_on_device) {
             C.F.cell_start = S.put(starts[f].data(), starts[f].size());
             C.F.cell_feat = S.put(feats[f].data(), feats[f].size());
-            C.nq = inputs(f, S, C);
-            calls[f] = C;
         }
-        calls_off = S.off;
-        S.off += (sizeof(DevProjCall) * nframes + 255) & ~(size_t)255;
-        in_bytes = S.off;
-        for (int f = 0; f < nframes; f++) {  // device-only scratch
+        C.nq = inputs(f, S, C);
+        calls[f] = C;
+    };
+    auto scratch = [&](Stager& S) {  // device-only: grids, queries, candidates, results
+        for (int f = 0; f < nframes; f++) {
             DevProjCall& C = calls[f];
             const int nq = C.nq;
+            if (C.grid_on_device) {
+                C.F.cell_start = S.take<int32_t>(ncell + 1);
+                C.F.cell_feat = S.take<int32_t>(std::max(1, frames[f].n));
+            }
             if (!C.queries) C.queries = S.take<ProjQuery>(std::max(1, nq));
             C.cand_off = S.take<int32_t>(nq + 1);
             C.cand_cap = std::max(4096, nq * 64);
@@ -2059,13 +2131,47 @@ slam_status run_projection_batch(slam_matcher* m, int nframes, const slam_frame_
             calls[f].out = S.take<int32_t>(4);
         }
         total = S.off;
-        if (pass == 1) std::memcpy(S.host + calls_off, calls.data(), sizeof(DevProjCall) * nframes);
+    };
+    // sizing pass: offsets only
+    {
+        Stager S;
+        for (int f = 0; f < nframes; f++) {
+            frame_off[f] = S.off;
+            stage_frame(f, S);
+        }
+        calls_off = S.off;
+        S.off += (sizeof(DevProjCall) * nframes + 255) & ~(size_t)255;
+        in_bytes = S.off;
+        scratch(S);
+    }
+    std::unique_lock<std::mutex> g(m->mu);
+    SLAM_HIP_TRY(hipSetDevice(m->device));
+    {
+        slam_status st;
+        if ((st = m->d_a.ensure(total)) || (st = m->stage(in_bytes + (total - res_off)))) return st;
     }
     uint8_t* D = m->d_a.as<uint8_t>();
+    // filling pass: frames copied into the pinned image on several threads
+    parallel_for(nframes, kStageThreads, [&](int f) {
+        Stager S;
+        S.host = m->h_stage;
+        S.dev = D;
+        S.off = frame_off[f];
+        stage_frame(f, S);
+    });
+    {
+        Stager S;
+        S.dev = D;
+        S.off = in_bytes;
+        scratch(S);
+        std::memcpy(m->h_stage + calls_off, calls.data(), sizeof(DevProjCall) * nframes);
+    }
     uint8_t* R = m->h_stage + in_bytes;
     hipStream_t st = m->stream;
     SLAM_HIP_TRY(hipMemcpyAsync(D, m->h_stage, in_bytes, hipMemcpyHostToDevice, st));
     SLAM_HIP_TRY(hipMemsetAsync(D + res_off, 0, total - res_off, st));
+    hipLaunchKernelGGL(k_frame_grid, dim3(nframes), dim3(1024), 0, st, (const DevProjCall*)(D + calls_off));
+    SLAM_HIP_TRY(hipGetLastError());
     SLAM_HIP_TRY(launch_search_by_projection((const DevProjCall*)(D + calls_off), nframes, lds, st));
     SLAM_HIP_TRY(hipMemcpyAsync(R, D + res_off, total - res_off, hipMemcpyDeviceToHost, st));
     SLAM_HIP_TRY(hipStreamSynchronize(st));
@@ -2153,7 +2259,7 @@ extern "C" slam_status slamhot_search_by_projection_kf_batch(slam_matcher* m, in
             return SLAM_EINVAL;
     if (nframes == 0) return SLAM_OK;
     std::vector<std::vector<ProjQuery>> qs(nframes);
-    for (int f = 0; f < nframes; f++) kf_queries(&frames[f], &kfs[f], th, qs[f]);
+    parallel_for(nframes, 8, [&](int f) { kf_queries(&frames[f], &kfs[f], th, qs[f]); });
     DevProjCall proto{};
     proto.mode = kProjKF;
     proto.th_dist = orb_dist;

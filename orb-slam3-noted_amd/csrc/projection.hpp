@@ -65,6 +65,7 @@ struct DevProjCall {
     int32_t* f_match;       // F.n
     int32_t* out;           // [0] nmatches, [1] status (1 = candidate overflow), [2] iterations
     int32_t* gstate;        // resolution state in global memory when it exceeds the LDS (else null)
+    int grid_on_device;     // batched calls: F.cell_start / cell_feat are built by k_frame_grid
 };
 
 struct FrustumCall {

@@ -705,6 +705,10 @@ class LocalBundleAdjustment:
         run.results = lambda: [lba_result_dict(ress[i], keep[i][2]) for i in range(len(ws))]
         return run
 
+    def warmup(self, n_kf=50, n_pt=2000, obs_per_pt=8):
+        """slamhot_lba_warmup: one synthetic window of that size (kernels loaded, buffers sized)."""
+        check(lib().slamhot_lba_warmup(self._h, n_kf, n_pt, obs_per_pt), "lba_warmup")
+
     def last_stats(self):
         """(device_ms, plan_ms, syncs) of the last solve."""
         ms, plan, syncs = C.c_double(0), C.c_double(0), I(0)
@@ -723,6 +727,7 @@ def _bind_lba(L):
     L.slamhot_lba_destroy.restype = None
     L.slamhot_lba_solve.argtypes = [P, I, C.POINTER(LbaProblem), C.POINTER(LbaOptions), P, C.POINTER(LbaResult)]
     L.slamhot_lba_last_stats.argtypes = [P, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(I)]
+    L.slamhot_lba_warmup.argtypes = [P, I, I, I]
     L._lba_ready = True
 
 

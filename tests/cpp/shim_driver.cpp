@@ -271,6 +271,26 @@ int run_lba_time(const char* in, const char* out, int reps) {
     return 0;
 }
 
+// host-only: wall-clock of the window build + flattening on fresh maps (no device)
+int run_flat_time(const char* in, const char* out, int reps) {
+    std::vector<double> ms;
+    for (int r = 0; r < reps; r++) {
+        World W;
+        load_map(in, W);
+        const auto t0 = std::chrono::steady_clock::now();
+        slamhot::orbslam3::LocalWindow<KeyFrame, MapPoint> L;
+        slamhot::orbslam3::BuildLocalWindow(&W.kfs[W.cur], &W.map, L);
+        slamhot::LocalBAWindow F;
+        std::vector<KeyFrame*> kfs;
+        std::vector<std::pair<KeyFrame*, MapPoint*>> refs;
+        slamhot::orbslam3::FlattenLocalWindow(L, &W.map, F, kfs, refs);
+        ms.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    }
+    Writer O(out);
+    O.put(ms);
+    return 0;
+}
+
 int run_pose(const char* in, const char* out) {
     Reader R(in);
     Frame F;
@@ -921,6 +941,7 @@ int main(int argc, char** argv) {
         if (mode == "pose") return run_pose(argv[2], argv[3]);
         if (mode == "bow") return run_bow(argv[2], argv[3]);
         if (mode == "lbatime") return run_lba_time(argv[2], argv[3], argc > 4 ? std::atoi(argv[4]) : 5);
+        if (mode == "flattime") return run_flat_time(argv[2], argv[3], argc > 4 ? std::atoi(argv[4]) : 20);
         if (mode == "bowkk") return run_bowkk(argv[2], argv[3]);
         if (mode == "projlast") return run_projlast(argv[2], argv[3]);
         if (mode == "projkf") return run_projkf(argv[2], argv[3]);

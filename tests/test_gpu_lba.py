@@ -244,3 +244,25 @@ def test_lba_schur_kernels(solver, monkeypatch, kernel):
           synth.lba_window(61, n_kf=12, n_pt=300, obs_per_pt=4)]
     for W, g in zip(Ws, solver.solve(Ws)):
         _check(g, ob.lba_solve(W))
+
+
+def test_lba_warmup_then_solve():
+    """slamhot_lba_warmup (what slamhot::LocalBundleAdjuster runs at construction) leaves a handle
+    whose next solve equals a fresh handle's and the oracle's (no state leaks from the synthetic
+    window), and a smaller window after a larger one reuses the sized buffers."""
+    import slamhot
+    W = synth.lba_window(3, stereo_frac=0.3)
+    fresh = slamhot.LocalBundleAdjustment()
+    g0 = fresh.solve(W)
+    fresh.close()
+    warm = slamhot.LocalBundleAdjustment()
+    warm.warmup(50, 2000, 8)
+    g1 = warm.solve(W)
+    small = synth.lba_window(4, n_kf=12, n_pt=300, obs_per_pt=5)
+    g2 = warm.solve(small)
+    warm.close()
+    for k in ("kf_Tcw", "pt_pos", "edge_outlier"):
+        assert np.array_equal(g0[k], g1[k]), k
+    assert g0["iterations"] == g1["iterations"] and g0["trials"] == g1["trials"]
+    _check(g1, ob.lba_solve(W))
+    _check(g2, ob.lba_solve(small))
