@@ -1545,6 +1545,8 @@ struct T16Lds {
     double M[kT16Max][256];                // M_k = L_kk^-T per panel (row-major)
     double dinv[kT16Max][16];              // 1 / d per panel
     double P[kT16Max][16 * kPStride];      // W_ik of the current panel, row-major with stride 17
+    double NP[kT16Max][256];               // tiles (i, k + 1) as phase (4) of panel k leaves them,
+                                           // lane-major: phase (3) of panel k + 1 reads them here
     double y[kT16Max * 16];                // b_s, then z, then the back-substitution right-hand side
     double wb[16];                         // M_k^T y_k of the current panel
     double xk[16];
@@ -1586,7 +1588,8 @@ __device__ __forceinline__ void t16_store(double* tile, int lane, double4_t v) {
 // lane J of every 16-lane DPP row, to the whole row (v_mov_b64 DPP row_newbcast, gfx90a+)
 template <int J>
 __device__ __forceinline__ double row_bcast(double v) {  // DPP row_newbcast (64-bit DPP, gfx90a+)
-    return __longlong_as_double(__builtin_amdgcn_update_dpp(0LL, __double_as_longlong(v), 0x150 + J, 0xf, 0xf, false));
+    // bound_ctrl with full masks: every lane reads a valid source, the old value is never used
+    return __longlong_as_double(__builtin_amdgcn_update_dpp(0LL, __double_as_longlong(v), 0x150 + J, 0xf, 0xf, true));
 }
 // 1/d: v_rcp_f64 and two Newton steps (the pivot reciprocal is on the serial chain; within
 // the LBA tolerance it equals the divided value)
@@ -1604,20 +1607,35 @@ __device__ __forceinline__ double rcp_nr(double d) {
 // are zero), so only rows r <= J need masking, through a zero multiplier.  Measured 2.3 us per
 // tile (tools/microbench/mb_diag).
 template <int J>
-__device__ __forceinline__ void t16_pivot(double (&row)[8], int r, int g, int lane, bool& bad, double* dinv) {
-    constexpr int gs = J >> 3, e = J & 7;      // the group / element holding column J of A
-    const double dj = readlane_d(row[e], 16 * gs + J);
+__device__ __forceinline__ void t16_pivot(double (&row)[8], int r, int g, int lane, bool& bad, double dj, double arj) {
+    // dj = pivot J (row J's column J), arj = A[r][J] of this lane's row: both read by the previous
+    // step right after it updated column J
     if (dj == 0.0) bad = true;
-    const double inv = rcp_nr(dj);
-    const double a = row[e];                    // A[r][J] in group gs
-    // A[r][J] from group gs to all four groups of row r: one ds_bpermute (all lanes active; it
-    // measured 2.3 us per diagonal tile against 3.4 us for v_permlane16/32_swap chains)
-    const double arj = __shfl(a, 16 * gs + r);
-    const double m = r > J ? arj * inv : 0.0;
+    // the pivot row's broadcasts do not depend on the multiplier: issued while the reciprocal
+    // and the bpermute are in flight
+    double pr[8];
 #pragma unroll
-    for (int c = 0; c < 8; c++) row[c] = __builtin_fma(-m, row_bcast<J>(row[c]), row[c]);
-    if (lane == J) dinv[J] = inv;
-    if constexpr (J + 1 < 16) t16_pivot<J + 1>(row, r, g, lane, bad, dinv);
+    for (int c = 0; c < 8; c++) pr[c] = row_bcast<J>(row[c]);
+    const double inv = rcp_nr(dj);
+    const double m = r > J ? arj * inv : 0.0;
+    if constexpr (J + 1 < 16) {
+        // column J + 1 first, then the next pivot and A[r][J + 1] leave at once (readlane; one
+        // ds_bpermute from group gs to the row's four groups: all lanes active, 2.3 us per tile
+        // measured against 3.4 us for v_permlane16/32_swap chains); the scheduling barrier keeps
+        // them ahead of the other seven columns' updates
+        constexpr int en = (J + 1) & 7, gn = (J + 1) >> 3;
+        row[en] = __builtin_fma(-m, pr[en], row[en]);
+        const double dn = readlane_d(row[en], 16 * gn + J + 1);
+        const double an = __shfl(row[en], 16 * gn + r);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int c = 0; c < 8; c++)
+            if (c != en) row[c] = __builtin_fma(-m, pr[c], row[c]);
+        t16_pivot<J + 1>(row, r, g, lane, bad, dn, an);
+    } else {
+#pragma unroll
+        for (int c = 0; c < 8; c++) row[c] = __builtin_fma(-m, pr[c], row[c]);
+    }
 }
 
 // The diagonal tile of panel k (held by wave 0 in the transposed accumulator layout, which for
@@ -1639,8 +1657,16 @@ __device__ __forceinline__ void t16_diag(Lds& L, int k, double4_t dt, int lane) 
         row[c] = g < 2 ? L.D[r * 16 + col] : (col == r ? 1.0 : 0.0);
     }
     bool bad = false;
-    t16_pivot<0>(row, r, g, lane, bad, L.dinv[k]);
+    t16_pivot<0>(row, r, g, lane, bad, readlane_d(row[0], 0), __shfl(row[0], r));
     if (bad && lane == 0) L.fail = 1;
+    // 1 / d_r off the chain: pivot r's row is final once it has been eliminated, so the diagonal
+    // of the A half is d_r, and rcp_nr gives the same value the chain used
+    if (g == (r >> 3)) {
+        double dr = row[0];
+#pragma unroll
+        for (int c = 1; c < 8; c++) dr = (r & 7) == c ? row[c] : dr;
+        L.dinv[k][r] = rcp_nr(dr);
+    }
     if (g >= 2) {
 #pragma unroll
         for (int c = 0; c < 8; c++) L.M[k][(8 * (g & 1) + c) * 16 + r] = row[c];  // M_k[col][r] = L^-1[r][col]
@@ -1701,7 +1727,7 @@ __global__ void __launch_bounds__(kT16Waves * 64) k_ldlt_t16(const WinDesc* __re
         // (3) panel tiles (i, k), i > k
         for (int t = L.col0[k] + 1 + wid; t < L.col0[k + 1]; t += kT16Waves) {
             const int i = L.tij[t] >> 8;
-            const double4_t a = t16_load(Tw + 256 * t, lane);
+            const double4_t a = k == 0 ? t16_load(Tw + 256 * t, lane) : t16_load(L.NP[i], lane);
             double4_t acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
             for (int u = 0; u < 4; u++)
@@ -1736,7 +1762,8 @@ __global__ void __launch_bounds__(kT16Waves * 64) k_ldlt_t16(const WinDesc* __re
                 acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
             }
             const double4_t v = cur - acc;
-            t16_store(Tw + 256 * t, lane, v);
+            if (j == k + 1) t16_store(L.NP[i], lane, v);  // the next panel's tile: it stays in the LDS
+            else t16_store(Tw + 256 * t, lane, v);
             return v;
         };
         const int t0 = L.col0[k + 1];

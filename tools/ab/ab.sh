@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B the extraction bench line between experiment libraries in one box session, interleaved.
-# Usage: tools/ab.sh LIB_A LIB_B [rounds]
+# Usage: tools/ab/ab.sh LIB_A LIB_B [rounds]
 export TMPDIR=/tmp
 A=$1; B=$2; R=${3:-3}
 for i in $(seq $R); do

@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of runtime switches (environment assignments) on the in-tree build: TESTS once per
 # setting, LEGS interleaved three times, then one rocprofv3 kernel-stats pass of PROF_LEGS per
-# setting.  Usage: tools/ab_env.sh TAG "TESTS" LEGS "VAR=a" "VAR=b" ...   ("-" = no assignment)
+# setting.  Usage: tools/ab/ab_env.sh TAG "TESTS" LEGS "VAR=a" "VAR=b" ...   ("-" = no assignment)
 export TMPDIR=/tmp
 TAG=$1; TESTS=$2; LEGS=$3; shift 3
 PROF_LEGS=${PROF_LEGS:-$LEGS}

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Generic A/B of experiment libraries: GPU tests (TESTS, space-separated, in-tree build), then
 # interleaved bench runs of each library (LEGS), then one rocprofv3 kernel-stats pass per library
-# (headline leg, one batch in flight).  Usage: tools/ab_libs.sh TAG "TESTS" LEGS LIB...
+# (headline leg, one batch in flight).  Usage: tools/ab/ab_libs.sh TAG "TESTS" LEGS LIB...
 export TMPDIR=/tmp
 TAG=$1; TESTS=$2; LEGS=$3; shift 3
 timeout -k 10 400 python -u -m pytest $TESTS -x -q --timeout 120 --timeout-method thread > gpurun_out/ab_tests_$TAG.log 2>&1

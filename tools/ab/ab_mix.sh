@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of (library, environment) pairs: TESTS once per entry, then LEGS interleaved three times.
-# Entry = LIB or LIB@VAR=value.  Usage: tools/ab_mix.sh TAG "TESTS" LEGS ENTRY...
+# Entry = LIB or LIB@VAR=value.  Usage: tools/ab/ab_mix.sh TAG "TESTS" LEGS ENTRY...
 export TMPDIR=/tmp
 TAG=$1; TESTS=$2; LEGS=$3; shift 3
 run() {  # entry, command...

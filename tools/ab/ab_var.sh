@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of experiment libraries with per-library parity: TESTS run against every library
-# (SLAMHOT_LIB), then LEGS interleaved twice.  Usage: tools/ab_var.sh TAG "TESTS" LEGS LIB...
+# (SLAMHOT_LIB), then LEGS interleaved twice.  Usage: tools/ab/ab_var.sh TAG "TESTS" LEGS LIB...
 export TMPDIR=/tmp
 TAG=$1; TESTS=$2; LEGS=$3; shift 3
 for L in "$@"; do

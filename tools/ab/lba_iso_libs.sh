@@ -1,6 +1,6 @@
 #!/bin/bash
 # k_schur_rows and the other LBA kernels in isolation (one solver, one call) per library, then the
-# LBA leg interleaved N times.  Usage: tools/lba_iso_libs.sh N LIB...
+# LBA leg interleaved N times.  Usage: tools/ab/lba_iso_libs.sh N LIB...
 export TMPDIR=/tmp
 N=$1; shift
 for L in "$@"; do

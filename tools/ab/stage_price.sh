@@ -1,7 +1,7 @@
 #!/bin/bash
 # Price each extractor stage inside the concurrent (3 batches in flight) pipeline: the bench
 # value with that stage left out (experiment build, SLAMHOT_SKIP bitmask; results invalid).
-# Stages: 0 resize, 1 fast, 2 octree, 3 layout, 4 orb.  Usage: tools/stage_price.sh LIB
+# Stages: 0 resize, 1 fast, 2 octree, 3 layout, 4 orb.  Usage: tools/ab/stage_price.sh LIB
 export TMPDIR=/tmp
 LIB=${1:-tools/libslamhot_exp.so}
 for m in 0 1 2 4 16 22 21 19; do
