@@ -439,11 +439,25 @@ class LocalBundleAdjuster {
     /* Many independent windows in one call (batched mode); pbStopFlag as the reference's. */
     void Solve(const std::vector<LocalBAWindow>& ws, const bool* pbStopFlag, std::vector<LocalBAResult>& out) {
         const int n = (int)ws.size();
+        out.assign(n, LocalBAResult{});
+        std::vector<const LocalBAWindow*> wp(n);
+        for (int i = 0; i < n; i++) wp[i] = &ws[i];
+        solve(wp.data(), out.data(), n, pbStopFlag);
+    }
+    /* One window (LocalMapping's call), without copying it. */
+    void Solve(const LocalBAWindow& w, const bool* pbStopFlag, LocalBAResult& out) {
+        const LocalBAWindow* wp = &w;
+        out = LocalBAResult{};
+        solve(&wp, &out, 1, pbStopFlag);
+    }
+
+    slam_lba* handle() { return s_; }
+   private:
+    void solve(const LocalBAWindow* const* ws, LocalBAResult* out, int n, const bool* pbStopFlag) {
         std::vector<slam_lba_problem> probs(n);
         std::vector<slam_lba_result> res(n);
-        out.assign(n, LocalBAResult{});
         for (int i = 0; i < n; i++) {
-            const LocalBAWindow& w = ws[i];
+            const LocalBAWindow& w = *ws[i];
             slam_lba_problem& p = probs[i];
             p.n_kf = w.n_kf();
             p.kf_Tcw = w.kf_Tcw.data();
@@ -493,9 +507,6 @@ class LocalBundleAdjuster {
         }
     }
 
-    slam_lba* handle() { return s_; }
-
-   private:
     slam_lba* s_ = nullptr;
 };
 
@@ -625,9 +636,7 @@ inline void LocalBundleAdjustment(LocalBundleAdjuster& solver, const LocalBAWind
     num_MPs = w.n_pt();
     num_edges = w.n_edge();
     if (num_fixedKF == 0) return;  // Optimizer.cc:1714-1718
-    std::vector<LocalBAResult> res;
-    solver.Solve({w}, pbStopFlag, res);
-    out = std::move(res[0]);
+    solver.Solve(w, pbStopFlag, out);
 }
 }  // namespace Optimizer
 

@@ -540,13 +540,27 @@ void FlattenLocalWindow(const LocalWindow<KeyFrame, MapPoint>& W, Map* pMap, Loc
     kfs.assign(W.lLocalKeyFrames.begin(), W.lLocalKeyFrames.end());
     kfs.insert(kfs.end(), W.lFixedCameras.begin(), W.lFixedCameras.end());
     std::stable_sort(kfs.begin(), kfs.end(), [](KeyFrame* a, KeyFrame* b) { return a->mnId < b->mnId; });
-    // vertex index of a KeyFrame: a pointer-sorted table (a few dozen entries, binary search)
-    std::vector<std::pair<KeyFrame*, int>> index(kfs.size());
-    for (size_t k = 0; k < kfs.size(); k++) index[k] = {kfs[k], (int)k};
-    std::sort(index.begin(), index.end());
+    // the vertex of an observing KeyFrame, or -1 when the edge is skipped (not a window KeyFrame, or
+    // bad / another map: :1817, evaluated once per KeyFrame instead of once per edge): an
+    // open-addressing table on the pointer (a few dozen entries, one probe per edge)
+    Map* pCurrentMap = W.lLocalKeyFrames.empty() ? nullptr : W.lLocalKeyFrames.front()->GetMap();
+    size_t tsize = 16;
+    while (tsize < 4 * kfs.size()) tsize *= 2;
+    std::vector<std::pair<KeyFrame*, int>> table(tsize, {nullptr, -1});
+    auto slot_of = [&](KeyFrame* k) {
+        return (size_t)(((uintptr_t)k >> 4) * 0x9E3779B97F4A7C15ull >> 40) & (tsize - 1);
+    };
+    for (size_t k = 0; k < kfs.size(); k++) {
+        size_t h = slot_of(kfs[k]);
+        while (table[h].first) h = (h + 1) & (tsize - 1);
+        const bool usable = !kfs[k]->isBad() && kfs[k]->GetMap() == pCurrentMap;
+        table[h] = {kfs[k], usable ? (int)k : -1};
+    }
     auto vertex_of = [&](KeyFrame* k) -> int {
-        auto it = std::lower_bound(index.begin(), index.end(), std::make_pair(k, -1));
-        return it != index.end() && it->first == k ? it->second : -1;
+        for (size_t h = slot_of(k);; h = (h + 1) & (tsize - 1)) {
+            if (table[h].first == k) return table[h].second;
+            if (!table[h].first) return -1;
+        }
     };
     std::vector<KeyFrame*> fixed(W.lFixedCameras.begin(), W.lFixedCameras.end());
     std::sort(fixed.begin(), fixed.end());
@@ -577,14 +591,12 @@ void FlattenLocalWindow(const LocalWindow<KeyFrame, MapPoint>& W, Map* pMap, Loc
             out.kf_Trl.insert(out.kf_Trl.end(), T, T + 16);
         }
     }
-    Map* pCurrentMap = W.lLocalKeyFrames.empty() ? nullptr : W.lLocalKeyFrames.front()->GetMap();
     int pi = 0;
     for (MapPoint* pMP : W.lLocalMapPoints) {
         const cv::Mat P = pMP->GetWorldPos();
         for (int c = 0; c < 3; c++) out.pt_pos.push_back(P.template at<float>(c));
         for (const auto& ob : W.observations[pi]) {
             KeyFrame* pKFi = ob.first;
-            if (pKFi->isBad() || pKFi->GetMap() != pCurrentMap) continue;
             const int vk = vertex_of(pKFi);
             if (vk < 0) continue;
             const int leftIndex = std::get<0>(ob.second);
@@ -648,10 +660,11 @@ void FlattenLocalWindow(const LocalWindow<KeyFrame, MapPoint>& W, Map* pMap, Loc
 }
 
 /* static void Optimizer::LocalBundleAdjustment(KeyFrame* pKF, bool* pbStopFlag, Map* pMap,
- *     int& num_fixedKF, int& num_OptKF, int& num_MPs, int& num_edges)  (Optimizer.cc:1611-2078) */
-template <class KeyFrame, class MapPoint, class Map>
-void LocalBundleAdjustment(LocalBundleAdjuster& hot, KeyFrame* pKF, bool* pbStopFlag, Map* pMap, int& num_fixedKF,
-                           int& num_OptKF, int& num_MPs, int& num_edges) {
+ *     int& num_fixedKF, int& num_OptKF, int& num_MPs, int& num_edges)  (Optimizer.cc:1611-2078)
+ * `hot`: slamhot::LocalBundleAdjuster (or anything with its Solve(window, stop, result)). */
+template <class KeyFrame, class MapPoint, class Map, class Hot>
+void LocalBundleAdjustment(Hot& hot, KeyFrame* pKF, bool* pbStopFlag, Map* pMap, int& num_fixedKF, int& num_OptKF,
+                           int& num_MPs, int& num_edges) {
     LocalWindow<KeyFrame, MapPoint> W;
     const bool ok = BuildLocalWindow(pKF, pMap, W);
     num_fixedKF = W.num_fixedKF;
@@ -664,9 +677,8 @@ void LocalBundleAdjustment(LocalBundleAdjuster& hot, KeyFrame* pKF, bool* pbStop
     FlattenLocalWindow(W, pMap, flat, kfs, edge_refs);
     num_edges = flat.n_edge();
     if (pbStopFlag && *pbStopFlag) return;  // :1921-1923
-    std::vector<LocalBAResult> res;
-    hot.Solve({flat}, pbStopFlag, res);  // optimize(5), stop check, optimize(10), outlier scan
-    const LocalBAResult& R = res[0];
+    LocalBAResult R;
+    hot.Solve(flat, pbStopFlag, R);  // optimize(5), stop check, optimize(10), outlier scan
     if (!R.ran) return;  // the flag flipped between the check above and the solver's own: :1921-1923
     std::unique_lock<std::mutex> lock(pMap->mMutexMapUpdate);  // :2040
     for (size_t e = 0; e < edge_refs.size(); e++)           // vToErase (:2043-2052)

@@ -508,6 +508,11 @@ struct Solver {
 
 }  // namespace
 
+// LocalBundleAdjustment's Huber deltas (Optimizer.cc:1794-1795: float sqrt, widened by setDelta)
+// and outlier thresholds (:2002, :2024: double constants)
+const float kThHuberMono = std::sqrt(5.991), kThHuberStereo = std::sqrt(7.815);
+constexpr double kChi2Mono = 5.991, kChi2Stereo = 7.815;
+
 extern "C" {
 
 /* Optimizer::LocalBundleAdjustment from the vertex/edge setup on (Optimizer.cc:1722-2077).
@@ -518,7 +523,7 @@ int oracle_lba_solve(const slam_lba_problem* P, const slam_lba_options* opt, int
     Solver S;
     S.P = P;
     S.stop = stop;
-    const float thMono = std::sqrt(5.991), thStereo = std::sqrt(7.815);  // Optimizer.cc:1794-1795
+    const float thMono = kThHuberMono, thStereo = kThHuberStereo;  // Optimizer.cc:1794-1795
     S.delta_mono = thMono;
     S.delta_stereo = thStereo;
     S.dsqr_mono = (float)(S.delta_mono * S.delta_mono);  // RobustKernelHuber::setDelta
@@ -599,7 +604,7 @@ int oracle_lba_solve(const slam_lba_problem* P, const slam_lba_options* opt, int
     int nout = 0;
     for (int i = 0; i < ne; i++) {
         const Edge& e = S.E[i];
-        const double th = e.stereo ? 7.815 : 5.991;
+        const double th = e.stereo ? kChi2Stereo : kChi2Mono;
         const bool bad = S.chi2(e) > th || !S.depth_positive(e);
         R->edge_outlier[i] = bad;
         nout += bad;
@@ -613,6 +618,14 @@ int oracle_lba_solve(const slam_lba_problem* P, const slam_lba_options* opt, int
     }
     for (int i = 0; i < 3 * npt; i++) R->pt_pos[i] = (float)S.pt[i];
     return 0;
+}
+
+/* {Huber delta mono, stereo (as setDelta receives them), chi2 mono, stereo} for test_fp_sites.py */
+void oracle_fp_lba_consts(double* out) {
+    out[0] = (double)kThHuberMono;
+    out[1] = (double)kThHuberStereo;
+    out[2] = kChi2Mono;
+    out[3] = kChi2Stereo;
 }
 
 }  // extern "C"

@@ -243,4 +243,7 @@ int oracle_search_by_bow(const slam_bow_side* A, const slam_bow_side* B, float n
     return nmatches;
 }
 
+/* SearchByBoW's rotation bin (ORBmatcher.cc:391-396) for tests/test_fp_sites.py */
+int oracle_fp_rot_bin_bow(float a, float b) { return rot_bin(a, b); }
+
 }  // extern "C"

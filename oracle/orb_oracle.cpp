@@ -56,6 +56,19 @@ struct Tables {
     int umax[kHalfPatch + 1];
 };
 
+// ComputePyramid's level size (ORBextractor.cc:1157): cvRound((float)cols * scale) per side
+inline void level_size(int w, int h, float inv_scale, int& lw, int& lh) {
+    lw = cv_round((float)w * inv_scale);
+    lh = cv_round((float)h * inv_scale);
+}
+
+// operator()'s keypoint scaling to level-0 coordinates (ORBextractor.cc:1131-1133: pt *= scale)
+template <class K>
+inline void scale_kp(K& k, float scale) {
+    k.x *= scale;
+    k.y *= scale;
+}
+
 Tables make_tables(const slam_orb_params& p) {
     Tables t;
     const int L = p.nlevels;
@@ -528,8 +541,7 @@ struct Extractor {
         for (int l = 0; l < t.nlevels; ++l) {
             const float s = t.inv_scale[l];
             Image& L = pyr[l];
-            L.w = cv_round((float)w * s);
-            L.h = cv_round((float)h * s);
+            level_size(w, h, s, L.w, L.h);
             L.px.resize((size_t)L.w * L.h);
             if (l == 0) {
                 for (int y = 0; y < h; y++) std::memcpy(L.px.data() + (size_t)y * w, img + y * stride, w);
@@ -622,7 +634,7 @@ struct Extractor {
             const float scale = t.scale[level];
             for (Kp& k : kps) {
                 orb_descriptor(blurred, k, d.data());
-                if (level != 0) { k.x *= scale; k.y *= scale; }
+                if (level != 0) scale_kp(k, scale);
                 int dst;
                 if (k.x >= lap0 && k.x <= lap1) dst = stereo--;
                 else dst = mono++;
@@ -786,6 +798,25 @@ long oracle_extract_many(const slam_orb_params* p, int nframes, const uint8_t* i
 }
 
 }  // extern "C"
+
+// single float sites of the extractor for tests/test_fp_sites.py (vs the reference objects)
+extern "C" void oracle_fp_umax(int* out) {  // umax[0..15] of the circular patch
+    slam_orb_params p{};
+    p.nfeatures = 1000;
+    p.scale_factor = 1.2f;
+    p.nlevels = 8;
+    p.ini_th_fast = 20;
+    p.min_th_fast = 7;
+    const Tables t = make_tables(p);
+    for (int v = 0; v <= kHalfPatch; v++) out[v] = t.umax[v];
+}
+extern "C" void oracle_fp_level_size(int w, int h, float inv_scale, int* out) { level_size(w, h, inv_scale, out[0], out[1]); }
+extern "C" void oracle_fp_kp_scale(float x, float y, float scale, float* out) {
+    struct P { float x, y; } k{x, y};
+    scale_kp(k, scale);
+    out[0] = k.x;
+    out[1] = k.y;
+}
 
 // Exhaustive check of the device sincosf restatement (device_math.hpp, compiled for the host
 // here) against this host's glibc sincosf over every float in [lo, hi).  Returns mismatches.

@@ -48,6 +48,20 @@ int rot_bin(float a, float b) {
     return bin;
 }
 
+// Frame::PosInGrid (Frame.cc:708-718): round((x - mnMinX) * mfGridElementWidthInv)
+inline void pos_in_grid(float x, float y, float min_x, float min_y, float inv_w, float inv_h, int& px, int& py) {
+    px = (int)std::round((x - min_x) * inv_w);
+    py = (int)std::round((y - min_y) * inv_h);
+}
+
+// Frame::GetFeaturesInArea's cell range (Frame.cc:645-659): floor / ceil of the scaled box
+inline void area_cells(float x, float y, float r, float min_x, float min_y, float inv_w, float inv_h, int* c) {
+    c[0] = (int)std::floor((x - min_x - r) * inv_w);
+    c[1] = (int)std::ceil((x - min_x + r) * inv_w);
+    c[2] = (int)std::floor((y - min_y - r) * inv_h);
+    c[3] = (int)std::ceil((y - min_y + r) * inv_h);
+}
+
 struct Grid {
     std::vector<std::vector<int>> cells;  // [ix * GRID_ROWS + iy]
 };
@@ -58,8 +72,8 @@ Grid build_grid(const slam_frame_view* F) {
     g.cells.assign(GRID_COLS * GRID_ROWS, {});
     for (int i = 0; i < F->n; i++) {
         const slam_keypoint& kp = F->kps_un[i];
-        const int px = (int)std::round((kp.x - F->min_x) * F->grid_inv_w);
-        const int py = (int)std::round((kp.y - F->min_y) * F->grid_inv_h);
+        int px, py;
+        pos_in_grid(kp.x, kp.y, F->min_x, F->min_y, F->grid_inv_w, F->grid_inv_h, px, py);
         if (px < 0 || px >= GRID_COLS || py < 0 || py >= GRID_ROWS) continue;
         g.cells[px * GRID_ROWS + py].push_back(i);
     }
@@ -70,13 +84,15 @@ Grid build_grid(const slam_frame_view* F) {
 std::vector<int> features_in_area(const slam_frame_view* F, const Grid& g, float x, float y, float r,
                                   int minLevel, int maxLevel) {
     std::vector<int> out;
-    const int nMinCellX = std::max(0, (int)std::floor((x - F->min_x - r) * F->grid_inv_w));
+    int cb[4];
+    area_cells(x, y, r, F->min_x, F->min_y, F->grid_inv_w, F->grid_inv_h, cb);
+    const int nMinCellX = std::max(0, cb[0]);
     if (nMinCellX >= GRID_COLS) return out;
-    const int nMaxCellX = std::min(GRID_COLS - 1, (int)std::ceil((x - F->min_x + r) * F->grid_inv_w));
+    const int nMaxCellX = std::min(GRID_COLS - 1, cb[1]);
     if (nMaxCellX < 0) return out;
-    const int nMinCellY = std::max(0, (int)std::floor((y - F->min_y - r) * F->grid_inv_h));
+    const int nMinCellY = std::max(0, cb[2]);
     if (nMinCellY >= GRID_ROWS) return out;
-    const int nMaxCellY = std::min(GRID_ROWS - 1, (int)std::ceil((y - F->min_y + r) * F->grid_inv_h));
+    const int nMaxCellY = std::min(GRID_ROWS - 1, cb[3]);
     if (nMaxCellY < 0) return out;
     const bool check = (minLevel > 0) || (maxLevel >= 0);
     for (int ix = nMinCellX; ix <= nMaxCellX; ix++)
@@ -106,6 +122,9 @@ void neg_rt_t(const float* T, float* out) {  // -R^T * t
         out[i] = (float)(-1.0 * acc);
     }
 }
+
+// SearchByProjection(F, LastF)'s window (ORBmatcher.cc:2221): th * mvScaleFactors[nLastOctave]
+inline float search_radius(float th, float scale) { return th * scale; }
 
 float radius_by_viewing_cos(float c) { return c > 0.998 ? 2.5f : 4.0f; }  // ORBmatcher.cc:216-222
 
@@ -200,7 +219,7 @@ int oracle_search_by_projection_last(const slam_frame_view* F, const slam_last_f
         if (u < F->min_x || u > F->max_x) continue;
         if (v < F->min_y || v > F->max_y) continue;
         const int nLastOctave = LF->kps[i].octave;
-        const float radius = th * F->scale[nLastOctave];
+        const float radius = search_radius(th, F->scale[nLastOctave]);
         std::vector<int> idxs;
         if (bForward) idxs = features_in_area(F, g, u, v, radius, nLastOctave, -1);
         else if (bBackward) idxs = features_in_area(F, g, u, v, radius, 0, nLastOctave);
@@ -380,5 +399,15 @@ long oracle_check_predict_scale(float lo, float hi, float log_scale) {
     }
     return bad;
 }
+
+/* single float sites for tests/test_fp_sites.py (vs the reference objects) */
+int oracle_fp_rot_bin_proj(float a, float b) { return rot_bin(a, b); }
+void oracle_fp_pos_in_grid(float x, float y, float min_x, float min_y, float inv_w, float inv_h, int* out) {
+    pos_in_grid(x, y, min_x, min_y, inv_w, inv_h, out[0], out[1]);
+}
+void oracle_fp_area_cells(float x, float y, float r, float min_x, float min_y, float inv_w, float inv_h, int* out) {
+    area_cells(x, y, r, min_x, min_y, inv_w, inv_h, out);
+}
+float oracle_fp_search_radius(float th, float scale) { return search_radius(th, scale); }
 
 }  // extern "C"

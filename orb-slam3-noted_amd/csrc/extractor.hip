@@ -1348,9 +1348,18 @@ static_assert(kO3RawOff % 16 == 0 && kO3WaveBytes % 16 == 0, "16-byte aligned st
 #define SLAMHOT_ORB_WPG 1
 #endif
 constexpr int kOrbWpg = SLAMHOT_ORB_WPG;  // waves (keypoints) per workgroup
+// SLAMHOT_ORB_BLURWIN (experiment): the vertical blur pass over the whole 37x37 window (a lane per
+// column, sliding over the row pairs, conflict-free), the blurred bytes column-major in LDS
+// (kO3BS bytes per column, odd dword stride), and the descriptor samples as one byte read each
+// instead of four random hp dword reads
+#ifndef SLAMHOT_ORB_BLURWIN
+#define SLAMHOT_ORB_BLURWIN 0
+#endif
+constexpr int kO3BS = 44, kO3W = 37;
+constexpr int kO3BlurBytes = SLAMHOT_ORB_BLURWIN ? ((kO3W * kO3BS + 15) & ~15) : 0;
 __global__ void __launch_bounds__(64 * kOrbWpg) k_orb3(Bufs b) {
     // hp, raw and bl share one region per wave (3,520 B per wave)
-    __shared__ __attribute__((aligned(16))) uint32_t buf_all[kOrbWpg][kO3WaveBytes / 4];
+    __shared__ __attribute__((aligned(16))) uint32_t buf_all[kOrbWpg][(kO3WaveBytes + kO3BlurBytes) / 4];
     const DevPlan& P = *b.plan;
     const int2 blk = xcd_block();
     const int f = blk.y;
@@ -1503,6 +1512,37 @@ __global__ void __launch_bounds__(64 * kOrbWpg) k_orb3(Bufs b) {
     glibc_sincosf(angle * factor_pi, &sn, &cs);
     const float a = cs, bb = sn;
     ORB_MARK();
+#if SLAMHOT_ORB_BLURWIN
+    uint8_t* bw = reinterpret_cast<uint8_t*>(buf_all[wave]) + kO3WaveBytes;
+    if (lane < kO3W) {  // column x = lane: blurred rows 0..36, two per row pair step
+        const uint32_t* hc = hp + lane;
+        uint32_t q0 = hc[0], q1 = hc[kO3HS], q2 = hc[2 * kO3HS];
+        uint32_t* bcol = reinterpret_cast<uint32_t*>(bw + lane * kO3BS);
+        uint32_t word = 0;
+#pragma unroll
+        for (int P = 0; P < 19; P++) {
+            const uint32_t q3 = hc[(P + 3) * kO3HS];
+            uint32_t ev = 1u << 15, od = 1u << 15;
+            ev = __builtin_amdgcn_udot2(as_us2(q0), us2{18, 34}, ev, false);
+            ev = __builtin_amdgcn_udot2(as_us2(q1), us2{48, 56}, ev, false);
+            ev = __builtin_amdgcn_udot2(as_us2(q2), us2{48, 34}, ev, false);
+            ev = __builtin_amdgcn_udot2(as_us2(q3), us2{18, 0}, ev, false);
+            od = __builtin_amdgcn_udot2(as_us2(q0), us2{0, 18}, od, false);
+            od = __builtin_amdgcn_udot2(as_us2(q1), us2{34, 48}, od, false);
+            od = __builtin_amdgcn_udot2(as_us2(q2), us2{56, 48}, od, false);
+            od = __builtin_amdgcn_udot2(as_us2(q3), us2{34, 18}, od, false);
+            // rows 2P, 2P+1 -> bytes (2P) & 3, (2P+1) & 3 of dword P >> 1
+            const uint32_t two = ((ev >> 16) & 0xFF) | (((od >> 16) & 0xFF) << 8);
+            word = (P & 1) ? (word | (two << 16)) : two;
+            if ((P & 1) || P == 18) bcol[P >> 1] = word;
+            q0 = q1;
+            q1 = q2;
+            q2 = q3;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    auto blurred = [&](int r, int c) -> int { return bw[(c + 18) * kO3BS + (r + 18)]; };
+#else
     auto blurred = [&](int r, int c) -> int {  // r, c: rounded offsets from the keypoint
         const int y = r + 18;
         const uint32_t* q = hp + (y >> 1) * kO3HS + (c + 18);
@@ -1514,6 +1554,7 @@ __global__ void __launch_bounds__(64 * kOrbWpg) k_orb3(Bufs b) {
         acc = __builtin_amdgcn_udot2(as_us2(q[3 * kO3HS]), odd ? us2{34, 18} : us2{18, 0}, acc, false);
         return (int)(acc >> 16);
     };
+#endif
     int t0[4], t1[4];
 #pragma unroll
     for (int w = 0; w < 4; w++) {

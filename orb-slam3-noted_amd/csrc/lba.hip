@@ -1682,6 +1682,82 @@ __device__ __forceinline__ void t16_diag(Lds& L, int k, double4_t dt, int lane) 
     }
 }
 
+// t16_diag, second form (SLAMHOT_T16_DIAG=1 selects the first): every 16-lane group holds the
+// whole A row (16 values) of row lane & 15 and four I columns (4g .. 4g+3), so the multiplier
+// A[r][J] / d_J is lane-local in every group and the pivot row reaches each group through its own
+// DPP row broadcast: the chain per pivot is readlane(d_J) -> 1/d -> m -> column J+1, with no
+// cross-group shuffle.  Only the columns right of the pivot are updated (compile-time J).
+template <int J>
+__device__ __forceinline__ void t16_pivot2(double (&a)[16], double (&iq)[4], int r, bool& bad, double dj) {
+    if (dj == 0.0) bad = true;
+    double pr[16], pi[4];
+#pragma unroll
+    for (int c = J + 1; c < 16; c++) pr[c] = row_bcast<J>(a[c]);
+#pragma unroll
+    for (int k = 0; k < 4; k++) pi[k] = row_bcast<J>(iq[k]);
+    const double inv = rcp_nr(dj);
+    const double m = r > J ? a[J] * inv : 0.0;
+    if constexpr (J + 1 < 16) {
+        a[J + 1] = __builtin_fma(-m, pr[J + 1], a[J + 1]);
+        const double dn = readlane_d(a[J + 1], J + 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int c = J + 2; c < 16; c++) a[c] = __builtin_fma(-m, pr[c], a[c]);
+#pragma unroll
+        for (int k = 0; k < 4; k++) iq[k] = __builtin_fma(-m, pi[k], iq[k]);
+        t16_pivot2<J + 1>(a, iq, r, bad, dn);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; k++) iq[k] = __builtin_fma(-m, pi[k], iq[k]);
+    }
+}
+
+template <class Lds>
+__device__ __forceinline__ void t16_diag2(Lds& L, int k, double4_t dt, int lane) {
+    const int lr = lane & 15, lq = lane >> 4;
+#pragma unroll
+    for (int u = 0; u < 4; u++) L.D[lr * 16 + lq + 4 * u] = dt[u];
+    wave_sync();
+    const int r = lane & 15, g = lane >> 4;
+    double a[16], iq[4];
+#pragma unroll
+    for (int c = 0; c < 16; c++) a[c] = L.D[r * 16 + c];
+#pragma unroll
+    for (int q = 0; q < 4; q++) iq[q] = (4 * g + q == r) ? 1.0 : 0.0;
+    bool bad = false;
+    t16_pivot2<0>(a, iq, r, bad, readlane_d(a[0], 0));
+    if (bad && lane == 0) L.fail = 1;
+    if (g == 0) {  // 1 / d_r off the chain (the A half's diagonal is d_r once row r is eliminated)
+        double dr = a[0];
+#pragma unroll
+        for (int c = 1; c < 16; c++) dr = r == c ? a[c] : dr;
+        L.dinv[k][r] = rcp_nr(dr);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) L.M[k][(4 * g + q) * 16 + r] = iq[q];  // M_k[col][r] = L^-1[r][col]
+    wave_sync();
+    if (lane < 16) {
+        const int c = lane;
+        double wb = 0.0;
+#pragma unroll
+        for (int rr = 0; rr < 16; rr++) wb = __builtin_fma(L.M[k][rr * 16 + c], L.y[16 * k + rr], wb);
+        L.wb[c] = wb;
+        L.y[16 * k + c] = wb * L.dinv[k][c];
+    }
+}
+
+#ifndef SLAMHOT_T16_DIAG
+#define SLAMHOT_T16_DIAG 1
+#endif
+template <class Lds>
+__device__ __forceinline__ void t16_diag_sel(Lds& L, int k, double4_t dt, int lane) {
+#if SLAMHOT_T16_DIAG == 1
+    t16_diag(L, k, dt, lane);
+#else
+    t16_diag2(L, k, dt, lane);
+#endif
+}
+
 __global__ void __launch_bounds__(kT16Waves * 64) k_ldlt_t16(const WinDesc* __restrict__ wins, WinCtl* __restrict__ ctl,
                                                              const double* __restrict__ Hs, double* __restrict__ Ts,
                                                              double* __restrict__ xp_out) {
@@ -1714,7 +1790,7 @@ __global__ void __launch_bounds__(kT16Waves * 64) k_ldlt_t16(const WinDesc* __re
     // the tiles were written by k_schur_block (t16_put); padding by k_t16_pad
     double4_t d0 = {0.0, 0.0, 0.0, 0.0};
     if (wid == 0) d0 = t16_load(Tw, lane);
-    if (wid == 0) t16_diag(L, 0, d0, lane);
+    if (wid == 0) t16_diag_sel(L, 0, d0, lane);
     __syncthreads();
     T16_MARK(1);
     for (int k = 0; k < T; k++) {
@@ -1773,7 +1849,7 @@ __global__ void __launch_bounds__(kT16Waves * 64) k_ldlt_t16(const WinDesc* __re
                 __builtin_amdgcn_s_setprio(3);  // the critical path: ahead of the trailing MFMA waves
                 const double4_t dn = update(t0, diag_next);
                 T16_MARK(6);
-                t16_diag(L, k + 1, dn, lane);
+                t16_diag_sel(L, k + 1, dn, lane);
                 __builtin_amdgcn_s_setprio(0);
                 T16_MARK(7);
             } else {
@@ -2251,7 +2327,10 @@ struct slam_lba {
     DevBuf pcnt;                 // free-pose edges per pose (pose list lengths)
     DevBuf spe_hp;               // free-pose index of every spe entry
     DevBuf ct, ct_off, ct_cnt;   // Schur contribution lists (built on the device)
-    DevBuf kf_out, pt_out, outl;
+    DevBuf outb;                 // one region for everything read back: KF poses, points, control
+                                 // records, outlier flags (one D2H into hout)
+    unsigned char* hout = nullptr;  // pinned
+    size_t hout_cap = 0;
 };
 
 namespace {
@@ -2624,6 +2703,7 @@ void slamhot_lba_destroy(slam_lba* s) {
     if (s->h_cnt) (void)hipHostFree(s->h_cnt);
     if (s->h_stop) (void)hipHostFree(s->h_stop);
     if (s->harena) (void)hipHostFree(s->harena);
+    if (s->hout) (void)hipHostFree(s->hout);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
     if (s->stream) (void)hipStreamDestroy(s->stream);
@@ -2716,6 +2796,13 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     const volatile uint8_t* stop_b = opt->stop_flag_bool;
     auto user_stop = [&]() -> bool { return (stop_flag && *stop_flag) || (stop_b && *stop_b); };
     const auto t_plan0 = std::chrono::steady_clock::now();
+    // SLAMHOT_LBA_TRACE: host timestamps of the call's phases to stderr (latency study)
+    const bool trace = std::getenv("SLAMHOT_LBA_TRACE") != nullptr;
+    std::chrono::steady_clock::time_point tp[8];
+    int ntp = 0;
+    auto mark = [&]() {
+        if (trace && ntp < 8) tp[ntp++] = std::chrono::steady_clock::now();
+    };
     PlanSizes Z;
     std::vector<int> hidx_all, np_of;
     slam_status st = plan_sizes(n_prob, probs, Z, hidx_all, np_of);
@@ -2800,10 +2887,24 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     const bool use_t16 = Z.max_n <= 16 * kT16Max && !(ldlt_env && !std::strcmp(ldlt_env, "panel"));
     SLAM_HIP_TRY(s->Hs.ensure(sizeof(double) * std::max<long long>(Z.hs_total, 1)));
     if (use_t16) SLAM_HIP_TRY(s->Ts.ensure((size_t)t16_tiles_bytes() * nw));
-    SLAM_HIP_TRY(s->kf_out.ensure(sizeof(float) * 16 * std::max(H.nkf, 1)));
-    SLAM_HIP_TRY(s->pt_out.ensure(sizeof(float) * 3 * npt));
-    SLAM_HIP_TRY(s->outl.ensure(ne));
+    // read-back region: [KF poses | points | control records | outlier flags], 256-byte sections
+    auto up256 = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t o_pt = up256(sizeof(float) * 16 * std::max(H.nkf, 1));
+    const size_t o_ctl = o_pt + up256(sizeof(float) * 3 * npt);
+    const size_t o_outl = o_ctl + up256(sizeof(WinCtl) * nw);
+    const size_t out_bytes = o_outl + up256(ne);
+    SLAM_HIP_TRY(s->outb.ensure(out_bytes));
+    if (out_bytes > s->hout_cap) {
+        SLAM_HIP_TRY(hipStreamSynchronize(S));
+        if (s->hout) (void)hipHostFree(s->hout);
+        s->hout = nullptr;
+        s->hout_cap = 0;
+        SLAM_HIP_TRY(hipHostMalloc((void**)&s->hout, out_bytes, hipHostMallocDefault));
+        s->hout_cap = out_bytes;
+    }
+    unsigned char* dout = (unsigned char*)s->outb.p;
     s->last_plan_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_plan0).count();
+    mark();  // 0: planned, arena copy queued, buffers sized
 
     Cam cam;  // the batch's one calibration, or per-KeyFrame records (PlanSizes::per_kf_cam)
     cam.fx = Z.cam.fx;
@@ -2960,6 +3061,7 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
                                                    s->d_stop, dTally, s->d_hcnt + slot, seq);
         return hipGetLastError();
     };
+    mark();  // 1: setup kernels launched
     for (int o = 0; o < 2; o++) {
         if (o == 1 && (stopped || user_stop())) break;  // bDoMore = false (Optimizer.cc:1933-1935)
         k_opt_begin<<<blocks(nw, 64), 64, 0, S>>>(nw, dW, dC, o, iters_of[o]);
@@ -2977,6 +3079,7 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
             }
             const int slot = (int)(checked % kRing);
             SLAM_HIP_TRY(wait_step(slot, seqs[slot]));
+            if (syncs == 0) mark();  // 2: the first step's counters are in
             syncs++;
             checked++;
             if (opt->step_hook) {  // diagnostic hook (slam_lba_options): may set the caller's flag
@@ -2991,21 +3094,24 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
         SLAM_HIP_TRY(wait_step(last, seqs[last]));  // the queued no-op steps
         if (*s->h_stop) stopped = true;
     }
+    mark();  // 3: LM loop done
     k_finalize_edges<<<blocks(H.ne, T), T, 0, S>>>(H.ne, dE, dC, poses, pts, pose_stride, pt_stride,
-                                                    as<double>(s->err), cam.trl, as<uint8_t>(s->outl));
+                                                    as<double>(s->err), cam.trl, dout + o_outl);
     k_finalize_state<<<blocks(H.nkf + H.npt, T), T, 0, S>>>(H.nkf, H.npt, DP.kf_win, DP.pt_win, dC,
                                                              poses, pts, pose_stride, pt_stride,
-                                                             as<float>(s->kf_out), as<float>(s->pt_out));
+                                                             (float*)dout, (float*)(dout + o_pt));
     SLAM_HIP_TRY(hipGetLastError());
     SLAM_HIP_TRY(hipEventRecord(s->ev1, S));
-    std::vector<float> kf_out(16 * (size_t)H.nkf), pt_out(3 * (size_t)H.npt);
-    std::vector<uint8_t> outl(H.ne);
-    std::vector<WinCtl> ctl1(nw);
-    if (H.nkf) SLAM_HIP_TRY(hipMemcpyAsync(kf_out.data(), s->kf_out.p, sizeof(float) * kf_out.size(), hipMemcpyDeviceToHost, S));
-    if (H.npt) SLAM_HIP_TRY(hipMemcpyAsync(pt_out.data(), s->pt_out.p, sizeof(float) * pt_out.size(), hipMemcpyDeviceToHost, S));
-    if (H.ne) SLAM_HIP_TRY(hipMemcpyAsync(outl.data(), s->outl.p, outl.size(), hipMemcpyDeviceToHost, S));
-    SLAM_HIP_TRY(hipMemcpyAsync(ctl1.data(), DP.ctl, sizeof(WinCtl) * nw, hipMemcpyDeviceToHost, S));
+    // one pinned read-back (pageable copies are synchronous, ~40 us each)
+    SLAM_HIP_TRY(hipMemcpyAsync(dout + o_ctl, DP.ctl, sizeof(WinCtl) * nw, hipMemcpyDeviceToDevice, S));
+    SLAM_HIP_TRY(hipMemcpyAsync(s->hout, dout, out_bytes, hipMemcpyDeviceToHost, S));
+    mark();  // 4: finalize + copies queued
     SLAM_HIP_TRY(hipStreamSynchronize(S));
+    mark();  // 5: results on the host
+    const float* kf_out = (const float*)s->hout;
+    const float* pt_out = (const float*)(s->hout + o_pt);
+    const WinCtl* ctl1 = (const WinCtl*)(s->hout + o_ctl);
+    const uint8_t* outl = s->hout + o_outl;
     float ms = 0;
     SLAM_HIP_TRY(hipEventElapsedTime(&ms, s->ev0, s->ev1));
     s->last_ms = ms;
@@ -3032,6 +3138,12 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
         R.chi2_initial = C.chi2_initial;
         R.chi2_final = C.chi2_final;
         R.lambda_final = C.lambda;
+    }
+    mark();  // 6: results copied out
+    if (trace) {
+        auto ms_of = [&](int i) { return std::chrono::duration<double, std::milli>(tp[i] - t_plan0).count(); };
+        std::fprintf(stderr, "lba trace ms: plan %.3f setup %.3f first_step %.3f loop %.3f queued %.3f synced %.3f out %.3f device %.3f steps %d\n",
+                     ms_of(0), ms_of(1), ms_of(2), ms_of(3), ms_of(4), ms_of(5), ms_of(6), s->last_ms, syncs);
     }
     return SLAM_OK;
 }

@@ -252,9 +252,9 @@ int run_lba_time(const char* in, const char* out, int reps) {
         std::vector<std::pair<KeyFrame*, MapPoint*>> refs;
         slamhot::orbslam3::FlattenLocalWindow(L, &W.map, F, kfs, refs);
         const auto t1 = std::chrono::steady_clock::now();
-        std::vector<slamhot::LocalBAResult> res;
+        slamhot::LocalBAResult res;
         bool stop = false;
-        solver.Solve({F}, &stop, res);
+        solver.Solve(F, &stop, res);
         const auto t2 = std::chrono::steady_clock::now();
         build_ms.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count());
         solve_ms.push_back(std::chrono::duration<double, std::milli>(t2 - t1).count());
@@ -268,6 +268,37 @@ int run_lba_time(const char* in, const char* out, int reps) {
     O.put(std::vector<double>{dev, plan, (double)syncs});
     O.put(build_ms);
     O.put(solve_ms);
+    return 0;
+}
+
+// host-only: the whole LocalBundleAdjustment shim with a stand-in for the device solve (results =
+// inputs, every 50th edge an outlier), wall clock per call on fresh maps
+struct HostOnlyLBA {
+    void Solve(const slamhot::LocalBAWindow& f, const bool*, slamhot::LocalBAResult& r) {
+        r = slamhot::LocalBAResult{};
+        r.kf_Tcw = f.kf_Tcw;
+        r.pt_pos = f.pt_pos;
+        r.edge_outlier.assign(f.edge_pt.size(), 0);
+        for (size_t e = 0; e < r.edge_outlier.size(); e += 50) r.edge_outlier[e] = 1;
+        r.ran = true;
+    }
+};
+
+int run_lba_host_time(const char* in, const char* out, int reps) {
+    HostOnlyLBA hot;
+    std::vector<double> ms;
+    int nf = 0, no = 0, nm = 0, ne = 0;
+    for (int r = 0; r < reps; r++) {
+        World W;
+        load_map(in, W);
+        bool stop = false;
+        const auto t0 = std::chrono::steady_clock::now();
+        slamhot::orbslam3::LocalBundleAdjustment<KeyFrame, MapPoint, Map>(hot, &W.kfs[W.cur], &stop, &W.map, nf, no, nm,
+                                                                           ne);
+        ms.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    }
+    Writer O(out);
+    O.put(ms);
     return 0;
 }
 
@@ -941,6 +972,7 @@ int main(int argc, char** argv) {
         if (mode == "pose") return run_pose(argv[2], argv[3]);
         if (mode == "bow") return run_bow(argv[2], argv[3]);
         if (mode == "lbatime") return run_lba_time(argv[2], argv[3], argc > 4 ? std::atoi(argv[4]) : 5);
+        if (mode == "lbahost") return run_lba_host_time(argv[2], argv[3], argc > 4 ? std::atoi(argv[4]) : 20);
         if (mode == "flattime") return run_flat_time(argv[2], argv[3], argc > 4 ? std::atoi(argv[4]) : 20);
         if (mode == "bowkk") return run_bowkk(argv[2], argv[3]);
         if (mode == "projlast") return run_projlast(argv[2], argv[3]);

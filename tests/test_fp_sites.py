@@ -11,6 +11,7 @@ elsewhere; the device kernels are then held to the oracle by the -m gpu parity t
 from __future__ import annotations
 
 import ctypes as C
+import math
 import subprocess
 import sys
 from pathlib import Path
@@ -66,6 +67,41 @@ SITES = {
     # computeOrbDescriptor's rotated sample (ORBextractor.cc:110-118): a = cos, b = sin (sincosf)
     "orb_rc": ("ORBextractor.cc.o", ["0x6a63:0x6adf"],
                ["arg_rbp-0x408", "arg_rbp-0x404", "int (%rbx)", "int 0x4(%rbx)"], [("int#2", 0), ("int#3", 0)]),
+    # ORBextractor ctor: mvScaleFactor[i] = mvScaleFactor[i-1] * scaleFactor (a double member) and
+    # mvLevelSigma2[i] = mvScaleFactor[i]^2 (ORBextractor.cc:417-423)
+    "ctor_scale": ("ORBextractor.cc.o", ["0x345e:0x348f"], ["arg_rbx+0x38", "-0x4(%rdx,%rax,4)"],
+                   [("store:(%rdx,%rax,4)", 0), ("live:%xmm0", 0)]),
+    # ctor feature split: factor = 1/scaleFactor, nDesiredFeaturesPerScale (ORBextractor.cc:433-435)
+    "ctor_nfeat": ("ORBextractor.cc.o", ["0x315a:0x31b7"],
+                   ["arg_rbx+0x38", "int 0x30(%rbx)", "arg_rbp-0x34", "pow#1.xmm0d"],
+                   [("store:arg_rbp-0x3c", 0), ("live:%xmm0", 0)]),
+    # ctor umax[0..vmax] = cvRound(sqrt(hp2 - v*v)), folded to constants by the compiler (:452-457)
+    "umax": ("ORBextractor.cc.o", ["0x3279:0x3303"], [], [("int#%d" % k, 0) for k in range(12)]),
+    # ComputePyramid level size cvRound((float)rows|cols * mvInvScaleFactor[level]) (:1157)
+    "pyr_size": ("ORBextractor.cc.o", ["0x4d0:0x515"], ["int 0x8(%r14)", "int 0xc(%r14)", "(%rax,%r12,4)"],
+                 [("int#0", 0), ("int#1", 0)]),
+    # operator(): keypoint->pt *= scale (:1131-1133)
+    "kp_scale": ("ORBextractor.cc.o", ["0x6ec0:0x6ee0"], ["arg_rbx+0x0", "arg_rbx+0x4", "arg_rbp-0x470"],
+                 [("store:arg_rbx+0x0", 0), ("store:arg_rbx+0x4", 0)]),
+    # Frame::PosInGrid: round((pt - mnMin) * mfGridElement*Inv) (Frame.cc:708-718)
+    "pos_in_grid": ("Frame.cc.o", ["0x6d30:0x6d8a"],
+                    ["arg_rsi+0x0", "arg_rsi+0x4", "got:ORB_SLAM3::Frame::mnMinX-0x4+0x0",
+                     "got:ORB_SLAM3::Frame::mfGridElementWidthInv-0x4+0x0", "got:ORB_SLAM3::Frame::mnMinY-0x4+0x0",
+                     "got:ORB_SLAM3::Frame::mfGridElementHeightInv-0x4+0x0"],
+                    [("int#0", 0), ("int#1", 0)]),
+    # Frame::GetFeaturesInArea's cell range: floor / ceil of (x - mnMinX -+ r) * inv (Frame.cc:645-659)
+    "area_cells": ("Frame.cc.o", ["0x67c0:0x6899"],
+                   ["*(rsp+0x8)+0x0", "*(rsp+0x20)+0x0", "arg_r8+0x0", "got:ORB_SLAM3::Frame::mnMinX-0x4+0x0",
+                    "got:ORB_SLAM3::Frame::mnMinY-0x4+0x0", "got:ORB_SLAM3::Frame::mfGridElementWidthInv-0x4+0x0",
+                    "got:ORB_SLAM3::Frame::mfGridElementHeightInv-0x4+0x0"],
+                   [("int#%d" % k, 0) for k in range(4)]),
+    # SearchByBoW(KF, F) rotation bin: roundf(rot * (1/30)), rot < 0 path (+360) and rot >= 0 path
+    # (ORBmatcher.cc:391-396)
+    "rot_neg": ("ORBmatcher.cc.o", ["0x36e4:0x3711"], ["arg_rdx+0xc", "arg_rax+0xc"], [("int#0", 0)]),
+    "rot_pos": ("ORBmatcher.cc.o", ["0x36e4:0x36f8", "0x3700:0x3711"], ["arg_rdx+0xc", "arg_rax+0xc"],
+                [("int#0", 0)]),
+    # SearchByProjection(F, LastF) window: radius = th * mvScaleFactors[nLastOctave] (ORBmatcher.cc:2225)
+    "sbp_radius": ("ORBmatcher.cc.o", ["0x8cc3:0x8cc9"], ["(%rdx,%rax,4)", "%xmm7"], [("live:%xmm0", 0)]),
     # Fuse stereo reprojection chi2 (ORBmatcher.cc:1697, 1735-1745)
     "fuse_e2": ("ORBmatcher.cc.o", ["0x1bc8:0x1c25", "0x1c60:0x1cca"],
                 ["rsp+0xa0", "rsp+0xbc", "arg_rdx+0x0", "arg_rdx+0x4", "(%rdi,%rax,4)", "rsp+0x8c", "rsp+0xa8",
@@ -225,3 +261,154 @@ def test_orb_descriptor_rotation(ref_lib, orc):
         ref = call_site(ref_lib, "orb_rc", [a, b, x, y], 2)
         orc.oracle_orb_sample_rc(float(x), float(y), float(a), float(b), C.byref(r), C.byref(c))
         assert list(ref) == [r.value, c.value], (ref, r.value, c.value)
+
+
+# ---- round 4: the remaining float sites of the path (second part)
+
+def test_ctor_scale_tables(ref_lib):
+    """ORBextractor ctor tables (ORBextractor.cc:408-468): mvScaleFactor / mvLevelSigma2 through the
+    object's own step (float -> double product -> float), their inverses, and the per-level
+    feature split (factor = (float)(1 / (double)scaleFactor), pow in double, cvRound per level)."""
+    import oracle_bind as ob
+    rng = np.random.default_rng(11)
+    for _ in range(400):
+        sf = np.float32(rng.uniform(1.05, 2.2))
+        L = int(rng.integers(1, 13))
+        nf = int(rng.integers(100, 6000))
+        sc_, inv_, sig_, isig_, nfeat_ = ob.levels(ob.params(nfeatures=nf, scale=float(sf), nlevels=L))
+        t = dict(scale=sc_, inv_scale=inv_, sigma2=sig_, inv_sigma2=isig_, nfeat=nfeat_)
+        scale, sig = [np.float32(1)], [np.float32(1)]
+        for i in range(1, L):
+            r = call_site(ref_lib, "ctor_scale", [float(sf), float(scale[-1])], 2)
+            scale.append(np.float32(r[0]))
+            sig.append(np.float32(r[1]))
+        assert same(t["scale"], scale) and same(t["sigma2"], sig), (sf, L)
+        assert same(t["inv_scale"], np.float32(1) / np.array(scale, np.float32))
+        assert same(t["inv_sigma2"], np.float32(1) / np.array(sig, np.float32))
+        factor = np.float32(call_site(ref_lib, "ctor_nfeat", [float(sf), nf, 1.0, 0.0], 2)[0])
+        per = np.float32(call_site(ref_lib, "ctor_nfeat", [float(sf), nf, 1.0, math.pow(float(factor), L)], 2)[1])
+        want, total = [], 0
+        for _l in range(L - 1):  # :436-441: vcvtss2si (round half even), then per *= factor
+            want.append(int(np.rint(per)))
+            total += want[-1]
+            per = np.float32(per * factor)
+        want.append(max(nf - total, 0))
+        assert list(t["nfeat"]) == want, (sf, L, nf)
+
+
+def test_umax_constants(ref_lib, orc):
+    """umax[0..11] are constants the compiler folded (cvRound of sqrt(225 - v^2)); the rest follow
+    the reference's symmetric integer loop (ORBextractor.cc:452-467)."""
+    ref = [int(v) for v in call_site(ref_lib, "umax", [], 12)]
+    out = (C.c_int * 16)()
+    orc.oracle_fp_umax(out)
+    assert list(out[:12]) == ref, (list(out), ref)
+    um = ref + [0] * 4
+    v0 = 0
+    for v in range(15, 10, -1):  # vmin = cvCeil(15 * sqrt(2) / 2) = 11
+        while um[v0] == um[v0 + 1]:
+            v0 += 1
+        um[v] = v0
+        v0 += 1
+    assert list(out) == um
+
+
+def test_pyramid_level_sizes(ref_lib, orc):
+    import oracle_bind as ob
+    out = (C.c_int * 2)()
+    rng = np.random.default_rng(12)
+    for _ in range(N):
+        w, h = int(rng.integers(16, 4096)), int(rng.integers(16, 4096))
+        inv = np.float32(1) / np.float32(np.float32(rng.uniform(1.05, 2.2)) ** int(rng.integers(0, 12)))
+        r = call_site(ref_lib, "pyr_size", [h, w, inv], 2)  # cv::Mat rows at +0x8, cols at +0xc
+        orc.oracle_fp_level_size(w, h, C.c_float(inv), out)
+        assert [out[1], out[0]] == [int(r[0]), int(r[1])], (w, h, inv, list(out), r)
+    for sf in (1.2, 1.5, 2.0):  # the standard geometries through the whole table
+        inv_scales = ob.levels(ob.params(scale=sf))[1]
+        for w, h in ((752, 480), (640, 480), (1241, 376), (1280, 720)):
+            for inv in inv_scales:
+                r = call_site(ref_lib, "pyr_size", [h, w, float(inv)], 2)
+                orc.oracle_fp_level_size(w, h, C.c_float(inv), out)
+                assert [out[1], out[0]] == [int(r[0]), int(r[1])]
+
+
+def test_keypoint_scaling(ref_lib, orc):
+    rng = np.random.default_rng(13)
+    out = (C.c_float * 2)()
+    for _ in range(N):
+        x, y = rng.uniform(0, 800, 2).astype(np.float32)
+        s = np.float32(np.float32(1.2) ** int(rng.integers(1, 8)))
+        r = call_site(ref_lib, "kp_scale", [x, y, s], 2)
+        orc.oracle_fp_kp_scale(C.c_float(x), C.c_float(y), C.c_float(s), out)
+        assert same(r, out[:2])
+
+
+def test_pos_in_grid_and_area_cells(ref_lib, orc):
+    """Frame::PosInGrid (roundf, then truncation) and GetFeaturesInArea's cell range (floorf /
+    ceilf of the scaled box), incl. values on the .5 rounding boundaries."""
+    rng = np.random.default_rng(14)
+    pg, ac = (C.c_int * 2)(), (C.c_int * 4)()
+    for i in range(N * 2):
+        minx, miny = np.float32(rng.uniform(-5, 5, 2).astype(np.float32))
+        maxx, maxy = np.float32(minx + rng.uniform(600, 1300)), np.float32(miny + rng.uniform(400, 800))
+        iw = np.float32(np.float32(64) / np.float32(maxx - minx))
+        ih = np.float32(np.float32(48) / np.float32(maxy - miny))
+        if i % 4 == 0:  # exactly on a half cell
+            x = np.float32(minx + (np.float32(rng.integers(0, 64)) + np.float32(0.5)) / iw)
+            y = np.float32(miny + (np.float32(rng.integers(0, 48)) + np.float32(0.5)) / ih)
+        else:
+            x = np.float32(rng.uniform(minx - 20, maxx + 20))
+            y = np.float32(rng.uniform(miny - 20, maxy + 20))
+        r = call_site(ref_lib, "pos_in_grid", [x, y, minx, iw, miny, ih], 2)
+        orc.oracle_fp_pos_in_grid(*(C.c_float(v) for v in (x, y, minx, miny, iw, ih)), pg)
+        assert list(pg) == [int(v) for v in r], (x, y, list(pg), r)
+        rad = np.float32(rng.uniform(1, 100))
+        r = call_site(ref_lib, "area_cells", [x, y, rad, minx, miny, iw, ih], 4)
+        orc.oracle_fp_area_cells(*(C.c_float(v) for v in (x, y, rad, minx, miny, iw, ih)), ac)
+        assert list(ac) == [int(v) for v in r], (x, y, rad, list(ac), r)
+
+
+def test_rotation_bins(ref_lib, orc):
+    """rotHist bin of a match: roundf((a - b [+360]) * (1/30)), 30 -> 0 (ORBmatcher.cc:391-396), for
+    both oracle copies (SearchByBoW's and the projection matchers'), incl. angles that land on
+    bin edges."""
+    orc.oracle_fp_rot_bin_bow.argtypes = [C.c_float] * 2
+    orc.oracle_fp_rot_bin_proj.argtypes = [C.c_float] * 2
+    rng = np.random.default_rng(15)
+    for i in range(N * 4):
+        a = np.float32(rng.uniform(0, 360))
+        b = np.float32(a - np.float32(15 * rng.integers(-24, 24) + (0 if i % 3 else rng.uniform(-1e-3, 1e-3))))
+        if i % 2:
+            b = np.float32(rng.uniform(0, 360))
+        rot = np.float32(a - b)
+        r = int(call_site(ref_lib, "rot_neg" if rot < 0 else "rot_pos", [a, b], 1)[0])
+        r = 0 if r == 30 else r
+        assert orc.oracle_fp_rot_bin_bow(a, b) == r and orc.oracle_fp_rot_bin_proj(a, b) == r, (a, b, r)
+
+
+def test_search_radius(ref_lib, orc):
+    orc.oracle_fp_search_radius.restype = C.c_float
+    orc.oracle_fp_search_radius.argtypes = [C.c_float] * 2
+    rng = np.random.default_rng(16)
+    for _ in range(N):
+        th = np.float32(rng.choice([7, 14, 15, 3, 1, 10, rng.uniform(0.5, 30)]))
+        s = np.float32(np.float32(rng.uniform(1.05, 2.2)) ** int(rng.integers(0, 8)))
+        r = call_site(ref_lib, "sbp_radius", [s, th], 1)
+        assert same(r, [orc.oracle_fp_search_radius(th, s)])
+
+
+def test_lba_robust_constants(orc):
+    """LocalBundleAdjustment's Huber deltas as setDelta receives them (float sqrt widened to double:
+    Optimizer.cc.o .LC116 at 0x1b005 / 0x1b799 mono, .LC101 at 0x1b580 stereo) and the outlier
+    thresholds it compares chi2 with (.LC105 5.991 at 0x1b2ca, .LC106 7.815 at 0x1ba6c)."""
+    import struct
+    import fptrace
+    obj = str(OBJ / "Optimizer.cc.o")
+    tr = fptrace.Tracer(obj, {})
+    rel = {a: r for a, _i, _o, r in fptrace.read_range(obj, None, "0x1a270", "0x1d800")}
+    val = lambda addr: struct.unpack("<d", tr.const_bytes(rel[addr], 8))[0]  # noqa: E731
+    ref = [val(0x1b005), val(0x1b580), val(0x1b2ca), val(0x1ba6c)]
+    assert val(0x1b799) == ref[0]
+    out = (C.c_double * 4)()
+    orc.oracle_fp_lba_consts(out)
+    assert list(out) == ref, (list(out), ref)

@@ -334,7 +334,7 @@ class Tracer:
             return
         if ins in ("vcvttss2si", "vcvtss2si", "vcvttsd2si", "vcvtsd2si"):
             s, d = ops
-            v = self.reg(R(s))[0]
+            v = self.reg(R(s))[0] if X(s) else self.load_scalar(s, reloc, "f64" if "sd2" in ins else "f32")
             op = "trunc" if "tt" in ins else "rint"
             n = self.mk(op, [v], "i32")
             self.gpr[R32.get(R(d), R(d))] = ("ival", n)
@@ -406,6 +406,13 @@ class Tracer:
             callee = (reloc or " ".join(ops)).split("(")[0].replace("-0x4", "").split("::")[-1]
             tag = f"{callee}#{self.ncall}"
             self.event("call", extra=tag)
+            if callee in ("roundf", "round", "floorf", "ceilf"):  # pure libm: its value, not an input
+                x = self.reg("xmm0")[0]
+                res = self.mk(callee, [x], "f32" if callee.endswith("f") else "f64")
+                for k in range(32):
+                    self.regs.pop(f"xmm{k}", None)
+                self.regs["xmm0"] = [res] + [None] * 7
+                return
             for k in range(32):
                 self.regs.pop(f"xmm{k}", None)
             dret = any(k in callee for k in ("normL2Sqr", "sqrt", "pow", "log", "exp"))
@@ -582,6 +589,8 @@ def emit_c(tr: Tracer, fname: str, inputs: list[str], outputs: list[tuple[str, i
             e = f"{'fabsf' if n.ty == 'f32' else 'fabs'}({a[0]})"
         elif n.op in ("ceil", "floor", "trunc", "rint"):
             e = f"{n.op}{'f' if n.ty == 'f32' else ''}({a[0]})"
+        elif n.op in ("roundf", "round", "floorf", "ceilf"):
+            e = f"{n.op}({a[0]})"
         elif n.op == "i2f":
             e = f"({t}){a[0]}"
         else:
