@@ -696,6 +696,17 @@ def pose_leg(ctx):
 # ------------------------------------------------------------------------------------------
 # localmap: batched Tracking::SearchLocalPoints (isInFrustum + SearchByProjection)
 # ------------------------------------------------------------------------------------------
+def call_split(m, wall_ms):
+    """Where a batched host-buffer matcher call's time goes (last timed call, events on its
+    stream): its kernels, its device-side span (first upload .. read-back done), and the share of
+    the host wall clock per call that the kernels take."""
+    k, span = m.last_batch_stats()
+    return {"kernel_ms": round(k, 4), "device_span_ms": round(span, 4), "wall_ms": round(wall_ms, 4),
+            "kernel_share": round(k / wall_ms, 4) if wall_ms > 0 else None,
+            "what": "kernel_ms: grid + (isInFrustum) + SearchByProjection kernels; device_span_ms: first H2D "
+                    "chunk queued .. read-back done (staging runs on host threads and overlaps the chunked uploads)"}
+
+
 def localmap_leg(ctx):
     """Tracking::SearchLocalPoints frames/s through slamhot_search_local_points_batch: P frames per
     call (1200 features, ~1200 local MapPoints each: back-projected features plus points behind,
@@ -734,6 +745,7 @@ def localmap_leg(ctx):
                    "parallelism": f"frame-sharded x{ctx['world']}"},
         "ms_per_call": round(el / calls * 1e3, 3),
         "mean_matches": round(float(np.mean([r[0] for r in res[-1]])), 1),
+        "call_split": call_split(m, el / calls * 1e3),
     }
     if ctx["cpu"]:
         import oracle_bind as ob
@@ -787,6 +799,7 @@ def projection_leg(ctx):
     elapsed = timed_region(dist, device, lambda i: res.append(m.SearchByProjection_last_batch(views, lfs, 7.0, False)),
                            calls)
     el, total = sdist.reduce_run(dist, device, elapsed, float(P * calls))
+    split = call_split(m, el / calls * 1e3)
     mk = slamhot.ORBmatcher(0.75, True, device=ctx["local_rank"])
     mk.SearchByProjection_kf_batch(views, kfs, 10.0, 100)
     resk = []
@@ -804,9 +817,11 @@ def projection_leg(ctx):
                    "parallelism": f"frame-sharded x{ctx['world']}"},
         "ms_per_call": round(el / calls * 1e3, 3),
         "mean_matches": round(float(np.mean([r[0] for r in res[-1]])), 1),
+        "call_split": split,
         "keyframe_variant": {"metric": "SearchByProjection(F, KF, set, th 10, ORBdist 100) frames/s (batched)",
                              "value": round(totk / elk, 1), "ms_per_call": round(elk / calls * 1e3, 3),
-                             "mean_matches": round(float(np.mean([r[0] for r in resk[-1]])), 1)},
+                             "mean_matches": round(float(np.mean([r[0] for r in resk[-1]])), 1),
+                             "call_split": call_split(mk, elk / calls * 1e3)},
     }
     if ctx["cpu"]:
         import oracle_bind as ob

@@ -196,6 +196,10 @@ typedef struct slam_matcher slam_matcher;
 
 slam_status slamhot_matcher_create(int device, slam_matcher** out);
 void slamhot_matcher_destroy(slam_matcher* m);
+/* Timing of the handle's last batched host-buffer call (slamhot_search_local_points_batch,
+ * slamhot_search_by_projection_{last,kf}_batch), from events on its stream: kernel_ms = the
+ * call's kernels, span_ms = first upload to the end of the read-back (device side). */
+slam_status slamhot_matcher_last_batch_stats(const slam_matcher* m, float* kernel_ms, float* span_ms);
 
 /* One side of SearchByBoW: descriptors, keypoint angles, MapPoint validity
  * (pMP != NULL && !pMP->isBad(); NULL = all valid) and the DBoW2 FeatureVector as CSR

@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -445,15 +446,20 @@ class LocalBundleAdjuster {
         solve(wp.data(), out.data(), n, pbStopFlag);
     }
     /* One window (LocalMapping's call), without copying it. */
-    void Solve(const LocalBAWindow& w, const bool* pbStopFlag, LocalBAResult& out) {
+    /* One window (LocalMapping's call), without copying it.  `overlap` (optional) runs once on
+     * this thread while the device works on the first LM steps (after the window has been
+     * uploaded): host work of the caller that does not need the result, e.g. releasing scratch. */
+    void Solve(const LocalBAWindow& w, const bool* pbStopFlag, LocalBAResult& out,
+               const std::function<void()>& overlap = nullptr) {
         const LocalBAWindow* wp = &w;
         out = LocalBAResult{};
-        solve(&wp, &out, 1, pbStopFlag);
+        solve(&wp, &out, 1, pbStopFlag, overlap);
     }
 
     slam_lba* handle() { return s_; }
    private:
-    void solve(const LocalBAWindow* const* ws, LocalBAResult* out, int n, const bool* pbStopFlag) {
+    void solve(const LocalBAWindow* const* ws, LocalBAResult* out, int n, const bool* pbStopFlag,
+               const std::function<void()>& overlap = nullptr) {
         std::vector<slam_lba_problem> probs(n);
         std::vector<slam_lba_result> res(n);
         for (int i = 0; i < n; i++) {
@@ -495,7 +501,24 @@ class LocalBundleAdjuster {
         static_assert(sizeof(bool) == 1, "slam_lba_options::stop_flag_bool expects a one-byte bool");
         opt.stop_flag_bool = reinterpret_cast<const volatile uint8_t*>(pbStopFlag);
         const volatile int32_t* sf = nullptr;
+        // the step hook runs on this thread each time the host has a step's counters, with the
+        // next steps already queued on the device: the first call runs `overlap`
+        struct Hook {
+            const std::function<void()>* fn;
+            bool ran;
+        } hk{&overlap, false};
+        if (overlap) {
+            opt.step_hook = [](void* ctx, int32_t) {
+                Hook* h = static_cast<Hook*>(ctx);
+                if (!h->ran) {
+                    h->ran = true;
+                    (*h->fn)();
+                }
+            };
+            opt.step_hook_ctx = &hk;
+        }
         check(slamhot_lba_solve(s_, n, probs.data(), &opt, sf, res.data()), "LocalBundleAdjustment");
+        if (overlap && !hk.ran) overlap();  // nothing ran on the device (stop flag set on entry)
         for (int i = 0; i < n; i++) {
             out[i].iterations[0] = res[i].iterations[0];
             out[i].iterations[1] = res[i].iterations[1];

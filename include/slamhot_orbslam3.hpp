@@ -661,7 +661,7 @@ void FlattenLocalWindow(const LocalWindow<KeyFrame, MapPoint>& W, Map* pMap, Loc
 
 /* static void Optimizer::LocalBundleAdjustment(KeyFrame* pKF, bool* pbStopFlag, Map* pMap,
  *     int& num_fixedKF, int& num_OptKF, int& num_MPs, int& num_edges)  (Optimizer.cc:1611-2078)
- * `hot`: slamhot::LocalBundleAdjuster (or anything with its Solve(window, stop, result)). */
+ * `hot`: slamhot::LocalBundleAdjuster (or anything with its Solve(window, stop, result, overlap)). */
 template <class KeyFrame, class MapPoint, class Map, class Hot>
 void LocalBundleAdjustment(Hot& hot, KeyFrame* pKF, bool* pbStopFlag, Map* pMap, int& num_fixedKF, int& num_OptKF,
                            int& num_MPs, int& num_edges) {
@@ -678,7 +678,9 @@ void LocalBundleAdjustment(Hot& hot, KeyFrame* pKF, bool* pbStopFlag, Map* pMap,
     num_edges = flat.n_edge();
     if (pbStopFlag && *pbStopFlag) return;  // :1921-1923
     LocalBAResult R;
-    hot.Solve(flat, pbStopFlag, R);  // optimize(5), stop check, optimize(10), outlier scan
+    // optimize(5), stop check, optimize(10), outlier scan; the observation copies (no longer
+    // needed) are released while the device runs the first LM steps
+    hot.Solve(flat, pbStopFlag, R, [&W] { decltype(W.observations)().swap(W.observations); });
     if (!R.ran) return;  // the flag flipped between the check above and the solver's own: :1921-1923
     std::unique_lock<std::mutex> lock(pMap->mMutexMapUpdate);  // :2040
     for (size_t e = 0; e < edge_refs.size(); e++)           // vToErase (:2043-2052)

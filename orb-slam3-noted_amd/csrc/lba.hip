@@ -1682,82 +1682,6 @@ __device__ __forceinline__ void t16_diag(Lds& L, int k, double4_t dt, int lane) 
     }
 }
 
-// t16_diag, second form (SLAMHOT_T16_DIAG=1 selects the first): every 16-lane group holds the
-// whole A row (16 values) of row lane & 15 and four I columns (4g .. 4g+3), so the multiplier
-// A[r][J] / d_J is lane-local in every group and the pivot row reaches each group through its own
-// DPP row broadcast: the chain per pivot is readlane(d_J) -> 1/d -> m -> column J+1, with no
-// cross-group shuffle.  Only the columns right of the pivot are updated (compile-time J).
-template <int J>
-__device__ __forceinline__ void t16_pivot2(double (&a)[16], double (&iq)[4], int r, bool& bad, double dj) {
-    if (dj == 0.0) bad = true;
-    double pr[16], pi[4];
-#pragma unroll
-    for (int c = J + 1; c < 16; c++) pr[c] = row_bcast<J>(a[c]);
-#pragma unroll
-    for (int k = 0; k < 4; k++) pi[k] = row_bcast<J>(iq[k]);
-    const double inv = rcp_nr(dj);
-    const double m = r > J ? a[J] * inv : 0.0;
-    if constexpr (J + 1 < 16) {
-        a[J + 1] = __builtin_fma(-m, pr[J + 1], a[J + 1]);
-        const double dn = readlane_d(a[J + 1], J + 1);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int c = J + 2; c < 16; c++) a[c] = __builtin_fma(-m, pr[c], a[c]);
-#pragma unroll
-        for (int k = 0; k < 4; k++) iq[k] = __builtin_fma(-m, pi[k], iq[k]);
-        t16_pivot2<J + 1>(a, iq, r, bad, dn);
-    } else {
-#pragma unroll
-        for (int k = 0; k < 4; k++) iq[k] = __builtin_fma(-m, pi[k], iq[k]);
-    }
-}
-
-template <class Lds>
-__device__ __forceinline__ void t16_diag2(Lds& L, int k, double4_t dt, int lane) {
-    const int lr = lane & 15, lq = lane >> 4;
-#pragma unroll
-    for (int u = 0; u < 4; u++) L.D[lr * 16 + lq + 4 * u] = dt[u];
-    wave_sync();
-    const int r = lane & 15, g = lane >> 4;
-    double a[16], iq[4];
-#pragma unroll
-    for (int c = 0; c < 16; c++) a[c] = L.D[r * 16 + c];
-#pragma unroll
-    for (int q = 0; q < 4; q++) iq[q] = (4 * g + q == r) ? 1.0 : 0.0;
-    bool bad = false;
-    t16_pivot2<0>(a, iq, r, bad, readlane_d(a[0], 0));
-    if (bad && lane == 0) L.fail = 1;
-    if (g == 0) {  // 1 / d_r off the chain (the A half's diagonal is d_r once row r is eliminated)
-        double dr = a[0];
-#pragma unroll
-        for (int c = 1; c < 16; c++) dr = r == c ? a[c] : dr;
-        L.dinv[k][r] = rcp_nr(dr);
-    }
-#pragma unroll
-    for (int q = 0; q < 4; q++) L.M[k][(4 * g + q) * 16 + r] = iq[q];  // M_k[col][r] = L^-1[r][col]
-    wave_sync();
-    if (lane < 16) {
-        const int c = lane;
-        double wb = 0.0;
-#pragma unroll
-        for (int rr = 0; rr < 16; rr++) wb = __builtin_fma(L.M[k][rr * 16 + c], L.y[16 * k + rr], wb);
-        L.wb[c] = wb;
-        L.y[16 * k + c] = wb * L.dinv[k][c];
-    }
-}
-
-#ifndef SLAMHOT_T16_DIAG
-#define SLAMHOT_T16_DIAG 1
-#endif
-template <class Lds>
-__device__ __forceinline__ void t16_diag_sel(Lds& L, int k, double4_t dt, int lane) {
-#if SLAMHOT_T16_DIAG == 1
-    t16_diag(L, k, dt, lane);
-#else
-    t16_diag2(L, k, dt, lane);
-#endif
-}
-
 __global__ void __launch_bounds__(kT16Waves * 64) k_ldlt_t16(const WinDesc* __restrict__ wins, WinCtl* __restrict__ ctl,
                                                              const double* __restrict__ Hs, double* __restrict__ Ts,
                                                              double* __restrict__ xp_out) {
@@ -1790,7 +1714,7 @@ __global__ void __launch_bounds__(kT16Waves * 64) k_ldlt_t16(const WinDesc* __re
     // the tiles were written by k_schur_block (t16_put); padding by k_t16_pad
     double4_t d0 = {0.0, 0.0, 0.0, 0.0};
     if (wid == 0) d0 = t16_load(Tw, lane);
-    if (wid == 0) t16_diag_sel(L, 0, d0, lane);
+    if (wid == 0) t16_diag(L, 0, d0, lane);
     __syncthreads();
     T16_MARK(1);
     for (int k = 0; k < T; k++) {
@@ -1849,7 +1773,7 @@ __global__ void __launch_bounds__(kT16Waves * 64) k_ldlt_t16(const WinDesc* __re
                 __builtin_amdgcn_s_setprio(3);  // the critical path: ahead of the trailing MFMA waves
                 const double4_t dn = update(t0, diag_next);
                 T16_MARK(6);
-                t16_diag_sel(L, k + 1, dn, lane);
+                t16_diag(L, k + 1, dn, lane);
                 __builtin_amdgcn_s_setprio(0);
                 T16_MARK(7);
             } else {

@@ -14,14 +14,17 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <sstream>
 #include <string>
+#include <thread>
 #include <thread>
 #include <vector>
 
@@ -671,6 +674,15 @@ struct slam_matcher {
     uint8_t* h_stage = nullptr;  // pinned staging of the batched host-buffer calls
     size_t h_cap = 0;
     std::mutex mu;
+    // the last batched host-buffer call on the stream: [0] before the first upload, [1] before the
+    // first kernel, [2] after the last kernel, [3] after the read-back (slamhot_matcher_last_batch_stats)
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    float last_kernel_ms = 0, last_span_ms = 0;
+    void batch_stats() {
+        if (!ev[0] || hipEventElapsedTime(&last_kernel_ms, ev[1], ev[2]) != hipSuccess ||
+            hipEventElapsedTime(&last_span_ms, ev[0], ev[3]) != hipSuccess)
+            last_kernel_ms = last_span_ms = 0;
+    }
     slam_status stage(size_t bytes) {
         if (bytes <= h_cap) return SLAM_OK;
         if (h_stage) (void)hipHostFree(h_stage);
@@ -944,7 +956,19 @@ slam_status slamhot_matcher_create(int device, slam_matcher** out) {
         delete m;
         return SLAM_EHIP;
     }
+    for (hipEvent_t& e : m->ev)
+        if (hipEventCreate(&e) != hipSuccess) {
+            slamhot_matcher_destroy(m);
+            return SLAM_EHIP;
+        }
     *out = m;
+    return SLAM_OK;
+}
+
+slam_status slamhot_matcher_last_batch_stats(const slam_matcher* m, float* kernel_ms, float* span_ms) {
+    if (!m) return SLAM_EINVAL;
+    if (kernel_ms) *kernel_ms = m->last_kernel_ms;
+    if (span_ms) *span_ms = m->last_span_ms;
     return SLAM_OK;
 }
 
@@ -960,6 +984,8 @@ void slamhot_matcher_destroy(slam_matcher* m) {
                    &m->b_pairs, &m->b_devpairs, &m->b_status, &m->b_scratch})
         b->release();
     if (m->h_stage) (void)hipHostFree(m->h_stage);
+    for (hipEvent_t e : m->ev)
+        if (e) (void)hipEventDestroy(e);
     if (m->stream) (void)hipStreamDestroy(m->stream);
     delete m;
 }
@@ -1726,9 +1752,18 @@ extern "C" slam_status slamhot_search_local_points(slam_matcher* m, const slam_f
     return SLAM_OK;
 }
 
-// Batched Tracking::SearchLocalPoints: nframes independent (Frame, local map) problems, every
-// frame's inputs staged into one host image and uploaded with one copy, one isInFrustum launch
-// (grid row per frame) and one SearchByProjection launch (workgroup per frame).
+namespace {
+constexpr int kGridSortMax = 4096;  // frames above this many features keep the host-built grid
+__global__ void k_frame_grid(const DevProjCall* __restrict__ calls);
+slam_status staged_upload(int nframes, const std::vector<size_t>& off, uint8_t* host, uint8_t* dev, hipStream_t st,
+                          int threads, const std::function<void(int)>& stage);
+}  // namespace
+
+// Batched Tracking::SearchLocalPoints: nframes independent (Frame, local map) problems.  Every
+// frame's inputs are staged into one pinned host image on several host threads and uploaded in
+// chunks as they complete; the Frame grids are built on the device (k_frame_grid); one
+// isInFrustum launch (grid row per frame) and one SearchByProjection launch (workgroup per
+// frame); every frame's results back with one copy.
 extern "C" slam_status slamhot_search_local_points_batch(slam_matcher* m, int nframes, const slam_frame_view* frames,
                                                          const int32_t* n_mp, const slam_mp_geom* const* mps,
                                                          const uint8_t* const* mp_desc, float view_cos_limit,
@@ -1742,15 +1777,19 @@ extern "C" slam_status slamhot_search_local_points_batch(slam_matcher* m, int nf
             (frames[f].n && !f_match[f]))
             return SLAM_EINVAL;
     if (nframes == 0) return SLAM_OK;
-    // host image: per frame kps | uright | desc | state | grid | mps | mp_desc, then device-only
-    // scratch (track, queries, cand_off, cand, f_match, out, n_in_view, gstate)
+    constexpr int kStageThreads = 8;
+    const int ncell = kGridCols * kGridRows;
+    // host image: per frame kps | uright | desc | state | (host grid) | mps | mp_desc, the call
+    // records; then device-only scratch (device grid, track, queries, cand_off, cand, gstate) and
+    // the results (f_match, out, n_in_view)
     struct Off {
         size_t kps, ur, desc, st, cs, cf, mps, md, tr, q, co, cand, fm, out, niv, gs;
         int cand_cap;
-        bool gstate;
+        bool gstate, dgrid;
     };
     std::vector<Off> O(nframes);
     std::vector<std::vector<int32_t>> starts(nframes), feats(nframes);
+    std::vector<size_t> frame_off(nframes + 1);
     size_t off = 0, lds = 0;
     auto take = [&](size_t bytes) {
         const size_t o = off;
@@ -1760,22 +1799,29 @@ extern "C" slam_status slamhot_search_local_points_batch(slam_matcher* m, int nf
     for (int f = 0; f < nframes; f++) {
         const slam_frame_view& F = frames[f];
         const int nq = n_mp[f];
-        build_grid_csr(&F, starts[f], feats[f]);
         Off& o = O[f];
+        o.dgrid = F.n <= kGridSortMax;
+        if (!o.dgrid) build_grid_csr(&F, starts[f], feats[f]);
+        frame_off[f] = off;
         o.kps = take(sizeof(slam_keypoint) * F.n);
         o.ur = take(F.uright ? 4 * (size_t)F.n : 0);
         o.desc = take(32 * (size_t)F.n);
         o.st = take(F.mp_state ? (size_t)F.n : 0);
-        o.cs = take(4 * starts[f].size());
-        o.cf = take(4 * feats[f].size());
+        o.cs = o.dgrid ? 0 : take(4 * starts[f].size());
+        o.cf = o.dgrid ? 0 : take(4 * feats[f].size());
         o.mps = take(sizeof(slam_mp_geom) * nq);
         o.md = take(32 * (size_t)nq);
     }
     const size_t calls_off = take(sizeof(DevProjCall) * nframes), fc_off = take(sizeof(FrustumCall) * nframes);
+    frame_off[nframes] = calls_off;
     const size_t in_bytes = off;  // the host image: inputs and call records
     for (int f = 0; f < nframes; f++) {  // device-only scratch
         const int nq = n_mp[f];
         Off& o = O[f];
+        if (o.dgrid) {
+            o.cs = take(4 * (size_t)(ncell + 1));
+            o.cf = take(4 * (size_t)std::max(1, frames[f].n));
+        }
         o.tr = take(sizeof(slam_mp_track) * std::max(1, nq));
         o.q = take(sizeof(ProjQuery) * std::max(1, nq));
         o.co = take(4 * (size_t)(nq + 1));
@@ -1801,25 +1847,24 @@ extern "C" slam_status slamhot_search_local_points_batch(slam_matcher* m, int nf
     uint8_t* D = m->d_a.as<uint8_t>();
     // inputs and results through one pinned staging buffer: [inputs | results]
     if ((st = m->stage(in_bytes + (total - res_off)))) return st;
-    uint8_t* Hs = m->h_stage;
-    uint8_t* Rs = m->h_stage + in_bytes;
-    struct View {
-        uint8_t* p;
-        uint8_t* data() { return p; }
-    } H{Hs}, R{Rs};
-    for (int f = 0; f < nframes; f++) {
+    uint8_t* H = m->h_stage;
+    uint8_t* R = m->h_stage + in_bytes;
+    hipStream_t S = m->stream;
+    auto stage_frame = [&](int f) {
         const slam_frame_view& F = frames[f];
         const Off& o = O[f];
         const int nq = n_mp[f];
         auto put = [&](size_t at, const void* src, size_t bytes) {
-            if (src && bytes) std::memcpy(H.data() + at, src, bytes);
+            if (src && bytes) std::memcpy(H + at, src, bytes);
         };
         put(o.kps, F.kps_un, sizeof(slam_keypoint) * F.n);
         put(o.ur, F.uright, F.uright ? 4 * (size_t)F.n : 0);
         put(o.desc, F.desc, 32 * (size_t)F.n);
         put(o.st, F.mp_state, F.mp_state ? (size_t)F.n : 0);
-        put(o.cs, starts[f].data(), 4 * starts[f].size());
-        put(o.cf, feats[f].data(), 4 * feats[f].size());
+        if (!o.dgrid) {
+            put(o.cs, starts[f].data(), 4 * starts[f].size());
+            put(o.cf, feats[f].data(), 4 * feats[f].size());
+        }
         put(o.mps, mps[f], sizeof(slam_mp_geom) * nq);
         put(o.md, mp_desc[f], 32 * (size_t)nq);
         DevProjCall C{};
@@ -1831,6 +1876,7 @@ extern "C" slam_status slamhot_search_local_points_batch(slam_matcher* m, int nf
         C.F.state = F.mp_state ? (const int8_t*)(D + o.st) : nullptr;
         C.F.cell_start = (const int32_t*)(D + o.cs);
         C.F.cell_feat = (const int32_t*)(D + o.cf);
+        C.grid_on_device = o.dgrid;
         C.mode = kProjLocal;
         C.nq = nq;
         C.mps = (const slam_mp_track*)(D + o.tr);
@@ -1848,7 +1894,7 @@ extern "C" slam_status slamhot_search_local_points_batch(slam_matcher* m, int nf
         C.f_match = (int32_t*)(D + o.fm);
         C.out = (int32_t*)(D + o.out);
         C.gstate = o.gstate ? (int32_t*)(D + o.gs) : nullptr;
-        std::memcpy(H.data() + calls_off + sizeof(DevProjCall) * f, &C, sizeof(C));
+        std::memcpy(H + calls_off + sizeof(DevProjCall) * f, &C, sizeof(C));
         FrustumCall Fc{};
         const float* T = F.Tcw;
         for (int r = 0; r < 3; r++) {
@@ -1873,29 +1919,36 @@ extern "C" slam_status slamhot_search_local_points_batch(slam_matcher* m, int nf
         Fc.mps = (const slam_mp_geom*)(D + o.mps);
         Fc.track = (slam_mp_track*)(D + o.tr);
         Fc.n_in_view = (int32_t*)(D + o.niv);
-        std::memcpy(H.data() + fc_off + sizeof(FrustumCall) * f, &Fc, sizeof(Fc));
-    }
+        std::memcpy(H + fc_off + sizeof(FrustumCall) * f, &Fc, sizeof(Fc));
+    };
+    SLAM_HIP_TRY(hipEventRecord(m->ev[0], S));
+    if ((st = staged_upload(nframes, frame_off, H, D, S, kStageThreads, stage_frame))) return st;
     int max_nq = 1;
     for (int f = 0; f < nframes; f++) max_nq = std::max(max_nq, n_mp[f]);
-    hipStream_t S = m->stream;
-    SLAM_HIP_TRY(hipMemcpyAsync(D, H.data(), in_bytes, hipMemcpyHostToDevice, S));
+    SLAM_HIP_TRY(hipMemcpyAsync(D + calls_off, H + calls_off, in_bytes - calls_off, hipMemcpyHostToDevice, S));
     SLAM_HIP_TRY(hipMemsetAsync(D + res_off, 0, total - res_off, S));  // out[] and n_in_view start at 0
+    SLAM_HIP_TRY(hipEventRecord(m->ev[1], S));
+    hipLaunchKernelGGL(k_frame_grid, dim3(nframes), dim3(1024), 0, S, (const DevProjCall*)(D + calls_off));
+    SLAM_HIP_TRY(hipGetLastError());
     SLAM_HIP_TRY(launch_is_in_frustum((const FrustumCall*)(D + fc_off), nframes, max_nq, S));
     SLAM_HIP_TRY(launch_search_by_projection((const DevProjCall*)(D + calls_off), nframes, lds, S));
-    // results: per frame f_match, out[4], n_in_view (one copy of the whole image back)
-    SLAM_HIP_TRY(hipMemcpyAsync(R.data(), D + res_off, total - res_off, hipMemcpyDeviceToHost, S));
+    SLAM_HIP_TRY(hipEventRecord(m->ev[2], S));
+    // results: per frame f_match, out[4], n_in_view (one copy of the whole tail back)
+    SLAM_HIP_TRY(hipMemcpyAsync(R, D + res_off, total - res_off, hipMemcpyDeviceToHost, S));
+    SLAM_HIP_TRY(hipEventRecord(m->ev[3], S));
     SLAM_HIP_TRY(hipStreamSynchronize(S));
+    m->batch_stats();
     std::vector<int> redo;
     for (int f = 0; f < nframes; f++) {
         const Off& o = O[f];
-        const int32_t* out = (const int32_t*)(R.data() + (o.out - res_off));
+        const int32_t* out = (const int32_t*)(R + (o.out - res_off));
         if (out[1] == 1) {  // candidate overflow: this frame again through the single-call path
             redo.push_back(f);
             continue;
         }
         nmatches[f] = out[0];
-        n_to_match[f] = *(const int32_t*)(R.data() + (o.niv - res_off));
-        if (frames[f].n) std::memcpy(f_match[f], R.data() + (o.fm - res_off), 4 * (size_t)frames[f].n);
+        n_to_match[f] = *(const int32_t*)(R + (o.niv - res_off));
+        if (frames[f].n) std::memcpy(f_match[f], R + (o.fm - res_off), 4 * (size_t)frames[f].n);
     }
     g.unlock();  // the single-call path takes the handle's lock itself
     slam_status rs = SLAM_OK;
@@ -2003,7 +2056,6 @@ struct Stager {
 // workgroup per frame: (cell << 16 | index) keys sorted in LDS (the keys are unique, so the order
 // inside a cell is the insertion order), cell starts by binary search.  Frames above
 // kGridSortMax features keep the host-built grid.
-constexpr int kGridSortMax = 4096;
 __global__ void __launch_bounds__(1024) k_frame_grid(const DevProjCall* __restrict__ calls) {
     __shared__ uint32_t keys[kGridSortMax];
     const DevProjCall& C = calls[blockIdx.x];
@@ -2069,6 +2121,54 @@ void parallel_for(int n, int cap, const std::function<void(int)>& f) {
         });
     for (int i = 0; i < n; i += nth) f(i);
     for (auto& x : th) x.join();
+}
+
+// Stage nframes frames into the pinned host image and upload them in chunks: host threads copy
+// the frames in index order (frame f's bytes at [off[f], off[f + 1])), and the calling thread
+// sends each chunk of frames to the device as soon as all its frames are in, while the threads
+// fill the next one -- the staging copies and the PCIe transfer overlap instead of following one
+// another.  Stream operations are issued from the calling thread only.
+slam_status staged_upload(int nframes, const std::vector<size_t>& off, uint8_t* host, uint8_t* dev, hipStream_t st,
+                          int threads, const std::function<void(int)>& stage) {
+    if (nframes <= 0) return SLAM_OK;
+    const int nchunk = std::max(1, std::min(nframes, 8));
+    auto lo = [&](int c) { return (int)((long long)nframes * c / nchunk); };
+    std::vector<int> chunk_of(nframes);
+    for (int c = 0; c < nchunk; c++)
+        for (int f = lo(c); f < lo(c + 1); f++) chunk_of[f] = c;
+    std::unique_ptr<std::atomic<int>[]> done(new std::atomic<int>[nchunk]);
+    for (int c = 0; c < nchunk; c++) done[c].store(0);
+    std::atomic<int> next{0};
+    auto one = [&](int f) {
+        stage(f);
+        done[chunk_of[f]].fetch_add(1, std::memory_order_release);
+    };
+    const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
+    const int nth = std::max(1, std::min({threads, hw, nframes / 8}));
+    std::vector<std::thread> th;
+    for (int t = 1; t < nth; t++)
+        th.emplace_back([&] {
+            for (int f; (f = next.fetch_add(1)) < nframes;) one(f);
+        });
+    int c = 0;
+    hipError_t err = hipSuccess;
+    auto flush = [&] {
+        while (c < nchunk && done[c].load(std::memory_order_acquire) == lo(c + 1) - lo(c)) {
+            const size_t a = off[lo(c)], b = off[lo(c + 1)];
+            if (b > a && err == hipSuccess) err = hipMemcpyAsync(dev + a, host + a, b - a, hipMemcpyHostToDevice, st);
+            c++;
+        }
+    };
+    for (int f; (f = next.fetch_add(1)) < nframes;) {
+        one(f);
+        flush();
+    }
+    while (c < nchunk) {
+        flush();
+        if (c < nchunk) std::this_thread::yield();
+    }
+    for (auto& x : th) x.join();
+    return err == hipSuccess ? SLAM_OK : SLAM_EHIP;
 }
 
 // Batched SearchByProjection over nframes independent problems of one mode (last frame /
@@ -2151,14 +2251,22 @@ slam_status run_projection_batch(slam_matcher* m, int nframes, const slam_frame_
         if ((st = m->d_a.ensure(total)) || (st = m->stage(in_bytes + (total - res_off)))) return st;
     }
     uint8_t* D = m->d_a.as<uint8_t>();
-    // filling pass: frames copied into the pinned image on several threads
-    parallel_for(nframes, kStageThreads, [&](int f) {
-        Stager S;
-        S.host = m->h_stage;
-        S.dev = D;
-        S.off = frame_off[f];
-        stage_frame(f, S);
-    });
+    hipStream_t st = m->stream;
+    // filling pass: frames copied into the pinned image on several threads, uploaded in chunks
+    // as they complete
+    {
+        std::vector<size_t> offs(frame_off);
+        offs.push_back(calls_off);
+        SLAM_HIP_TRY(hipEventRecord(m->ev[0], st));
+        slam_status ss = staged_upload(nframes, offs, m->h_stage, D, st, kStageThreads, [&](int f) {
+            Stager S;
+            S.host = m->h_stage;
+            S.dev = D;
+            S.off = frame_off[f];
+            stage_frame(f, S);
+        });
+        if (ss != SLAM_OK) return ss;
+    }
     {
         Stager S;
         S.dev = D;
@@ -2167,14 +2275,17 @@ slam_status run_projection_batch(slam_matcher* m, int nframes, const slam_frame_
         std::memcpy(m->h_stage + calls_off, calls.data(), sizeof(DevProjCall) * nframes);
     }
     uint8_t* R = m->h_stage + in_bytes;
-    hipStream_t st = m->stream;
-    SLAM_HIP_TRY(hipMemcpyAsync(D, m->h_stage, in_bytes, hipMemcpyHostToDevice, st));
+    SLAM_HIP_TRY(hipMemcpyAsync(D + calls_off, m->h_stage + calls_off, in_bytes - calls_off, hipMemcpyHostToDevice, st));
     SLAM_HIP_TRY(hipMemsetAsync(D + res_off, 0, total - res_off, st));
+    SLAM_HIP_TRY(hipEventRecord(m->ev[1], st));
     hipLaunchKernelGGL(k_frame_grid, dim3(nframes), dim3(1024), 0, st, (const DevProjCall*)(D + calls_off));
     SLAM_HIP_TRY(hipGetLastError());
     SLAM_HIP_TRY(launch_search_by_projection((const DevProjCall*)(D + calls_off), nframes, lds, st));
+    SLAM_HIP_TRY(hipEventRecord(m->ev[2], st));
     SLAM_HIP_TRY(hipMemcpyAsync(R, D + res_off, total - res_off, hipMemcpyDeviceToHost, st));
+    SLAM_HIP_TRY(hipEventRecord(m->ev[3], st));
     SLAM_HIP_TRY(hipStreamSynchronize(st));
+    m->batch_stats();
     std::vector<int> redo;
     for (int f = 0; f < nframes; f++) {
         const int32_t* out = (const int32_t*)(R + (out_off[f] - res_off));

@@ -173,6 +173,7 @@ def lib() -> C.CDLL:
     L.slamhot_matcher_create.argtypes = [I, C.POINTER(P)]
     L.slamhot_matcher_destroy.argtypes = [P]
     L.slamhot_matcher_destroy.restype = None
+    L.slamhot_matcher_last_batch_stats.argtypes = [P, P, P]
     L.slamhot_search_by_bow.argtypes = [P, C.POINTER(BowSide), C.POINTER(BowSide), C.c_float, I, I, P, P,
                                         C.POINTER(I)]
     L.slamhot_search_by_projection_local.argtypes = [P, C.POINTER(FrameView), I, P, P, C.c_float, C.c_float, I,
@@ -378,6 +379,12 @@ class ORBmatcher:
             self.close()
         except Exception:
             pass
+
+    def last_batch_stats(self):
+        """(kernel_ms, span_ms) of the last batched host-buffer call (slamhot_matcher_last_batch_stats)."""
+        k, sp = C.c_float(0), C.c_float(0)
+        check(lib().slamhot_matcher_last_batch_stats(self._h, C.byref(k), C.byref(sp)), "matcher_last_batch_stats")
+        return k.value, sp.value
 
     def _bow(self, A, B, strict):
         sa, ka = make_bow_side(*A)

@@ -274,7 +274,9 @@ int run_lba_time(const char* in, const char* out, int reps) {
 // host-only: the whole LocalBundleAdjustment shim with a stand-in for the device solve (results =
 // inputs, every 50th edge an outlier), wall clock per call on fresh maps
 struct HostOnlyLBA {
-    void Solve(const slamhot::LocalBAWindow& f, const bool*, slamhot::LocalBAResult& r) {
+    void Solve(const slamhot::LocalBAWindow& f, const bool*, slamhot::LocalBAResult& r,
+               const std::function<void()>& overlap = nullptr) {
+        if (overlap) overlap();
         r = slamhot::LocalBAResult{};
         r.kf_Tcw = f.kf_Tcw;
         r.pt_pos = f.pt_pos;
