@@ -1549,7 +1549,7 @@ struct T16Lds {
                                            // lane-major: phase (3) of panel k + 1 reads them here
     double y[kT16Max * 16];                // b_s, then z, then the back-substitution right-hand side
     double wb[16];                         // M_k^T y_k of the current panel
-    double xk[16];
+    double xb[2][16];                      // x_k of the back-solve, double-buffered by parity
     unsigned short tij[kT16Tiles];         // tile list, column-major: (i << 8) | j
     unsigned short col0[kT16Max + 1];      // first tile of column j
     int fail;
@@ -1795,31 +1795,52 @@ __global__ void __launch_bounds__(kT16Waves * 64) k_ldlt_t16(const WinDesc* __re
         if (tid == 0) C.ok2 = 0;
         return;
     }
-    // L^T x = z, right-looking from the last tile column; wave w handles tiles (k, w) (and
-    // (k, w + 16) when k > 16), the next step's tile loaded before the barrier
-    double4_t nxt = wid < T - 1 ? t16_load(Tw + 256 * (L.col0[wid] + (T - 1) - wid), lane) : double4_t{0.0, 0.0, 0.0, 0.0};
-    for (int k = T - 1; k >= 0; k--) {
-        if (wid == 0 && lane < 16) {
-            const double* Mk = L.M[k];
-            double x = 0.0;
+    // L^T x = z, right-looking from the last tile column, one barrier per step: wave 0 owns the
+    // tiles (k, k-1) next to the diagonal, so right after applying x_k to y_{k-1} it forms
+    // x_{k-1} = M_{k-1} y_{k-1} (every other tile of column k-1 was applied in earlier steps), while
+    // waves 1.. apply x_k to the tiles (k, j < k-1); x_k is double-buffered by parity
+    {
+        auto put_x = [&](int k) {  // wave 0: x_k from the final y_k
+            if (lane < 16) {
+                const double* Mk = L.M[k];
+                double x = 0.0;
 #pragma unroll
-            for (int r = 0; r < 16; r++) x = __builtin_fma(Mk[lane * 16 + r], L.y[16 * k + r], x);
-            L.xk[lane] = x;
-            if (16 * k + lane < n) xp_out[6 * (long long)W.pose0 + 16 * k + lane] = x;
-        }
-        const double4_t cur = nxt;
-        if (k >= 1 && wid < k - 1) nxt = t16_load(Tw + 256 * (L.col0[wid] + (k - 1) - wid), lane);
-        __syncthreads();
-        for (int j = wid; j < k; j += kT16Waves) {  // tile (k, j) holds L_kj
-            const double4_t l = j == wid ? cur : t16_load(Tw + 256 * (L.col0[j] + k - j), lane);
-            const double xr = L.xk[lr];
+                for (int r = 0; r < 16; r++) x = __builtin_fma(Mk[lane * 16 + r], L.y[16 * k + r], x);
+                L.xb[k & 1][lane] = x;
+                if (16 * k + lane < n) xp_out[6 * (long long)W.pose0 + 16 * k + lane] = x;
+            }
+        };
+        auto apply = [&](const double4_t& l, int k, int j) {  // y_j -= L_kj^T x_k
+            const double xr = L.xb[k & 1][lr];
 #pragma unroll
             for (int u = 0; u < 4; u++) {
                 const double sum = t16_sum16(l[u] * xr);
                 if (lr == 0) L.y[16 * j + lq + 4 * u] -= sum;
             }
+        };
+        auto tile = [&](int k, int j) { return t16_load(Tw + 256 * (L.col0[j] + k - j), lane); };
+        const double4_t zero = {0.0, 0.0, 0.0, 0.0};
+        // wave 0: the (k, k-1) tile of the coming step; waves w >= 1: their first tile (k, w-1)
+        double4_t nxt = zero;
+        if (wid == 0) {
+            put_x(T - 1);
+            if (T >= 2) nxt = tile(T - 1, T - 2);
+        } else if (wid - 1 < T - 2) {
+            nxt = tile(T - 1, wid - 1);
         }
-        __syncthreads();
+        for (int k = T - 1; k >= 1; k--) {
+            __syncthreads();  // x_k and every earlier update of y visible
+            const double4_t cur = nxt;
+            if (wid == 0) {
+                if (k >= 2) nxt = tile(k - 1, k - 2);
+                apply(cur, k, k - 1);
+                wave_sync();
+                put_x(k - 1);
+            } else {
+                if (wid - 1 < k - 2) nxt = tile(k - 1, wid - 1);
+                for (int j = wid - 1; j < k - 1; j += kT16Waves - 1) apply(j == wid - 1 ? cur : tile(k, j), k, j);
+            }
+        }
     }
     T16_MARK(5);
     if (tid == 0) C.ok2 = 1;

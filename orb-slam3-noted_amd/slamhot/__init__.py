@@ -500,6 +500,54 @@ def _matcher_methods():
         check(fn(self._h, nf, fv, ov, self.mfNNratio, int(self.mbCheckOrientation), *args, pf, _ptr(nm)), fn_name)
         return [(int(nm[i]), fms[i]) for i in range(nf)]
 
+    def prepare_batch(self, kind, frame_views, others, *args):
+        """The batched host-buffer call with its arguments marshalled once (what a C++ caller
+        already holds): returns run() -> total matches, which makes only the C call;
+        run.results() gives [(nmatches, f_match[, nToMatch])].  kind: "last" (others = last-frame
+        views, args = th, bMono), "kf" (KeyFrame views, th, ORBdist) or "local" (others = (MP_GEOM
+        arrays, descriptor arrays), args = th, bFarPoints, thFarPoints, viewingCosLimit)."""
+        L = lib()
+        nf = len(frame_views)
+        fv = (FrameView * nf)(*frame_views)
+        fms = [np.full(v.n, -1, np.int32) for v in frame_views]
+        pf = (P * nf)(*[f.ctypes.data for f in fms])
+        nm = np.zeros(nf, np.int32)
+        h = self._h
+        if kind == "local":
+            self.SearchLocalPoints_batch(frame_views[:1], others[0][:1], others[1][:1])  # binds argtypes
+            mps = [np.ascontiguousarray(m, MP_GEOM_DTYPE) for m in others[0]]
+            dsc = [np.ascontiguousarray(d, np.uint8) for d in others[1]]
+            nmp = np.array([len(m) for m in mps], np.int32)
+            pm = (P * nf)(*[m.ctypes.data for m in mps])
+            pd = (P * nf)(*[d.ctypes.data for d in dsc])
+            nt = np.zeros(nf, np.int32)
+            th, far, thf, vc = (list(args) + [1.0, False, 50.0, 0.5][len(args):])[:4]
+            fn = L.slamhot_search_local_points_batch
+            call = lambda: fn(h, nf, fv, _ptr(nmp), pm, pd, vc, self.mfNNratio, th, int(far), thf, pf, _ptr(nt),  # noqa: E731
+                              _ptr(nm))
+            keep = (mps, dsc, nmp, pm, pd, nt)
+            results = lambda: [(int(nm[i]), fms[i], int(nt[i])) for i in range(nf)]  # noqa: E731
+        else:
+            fn_name, cls = (("slamhot_search_by_projection_last_batch", LastFrameView) if kind == "last" else
+                            ("slamhot_search_by_projection_kf_batch", KFPointsView))
+            fn = getattr(L, fn_name)
+            if not getattr(fn, "_ready", False):
+                fn.argtypes = [P, I, P, P, C.c_float, I, C.c_float, I, P, P]
+                fn._ready = True
+            ov = (cls * nf)(*others)
+            a0, a1 = float(args[0]), int(args[1])
+            call = lambda: fn(h, nf, fv, ov, self.mfNNratio, int(self.mbCheckOrientation), a0, a1, pf, _ptr(nm))  # noqa: E731
+            keep = (ov,)
+            results = lambda: [(int(nm[i]), fms[i]) for i in range(nf)]  # noqa: E731
+
+        def run():
+            check(call(), "matcher batch")
+            return int(nm.sum())
+
+        run.keep = (fv, fms, pf, nm, keep)
+        run.results = results
+        return run
+
     def SearchByProjection_last_batch(self, frame_views, last_views, th, bMono):
         """Batched SearchByProjection(Frame&, const Frame& LastFrame, th, bMono)
         (slamhot_search_by_projection_last_batch): [(nmatches, f_match)] per frame."""
@@ -540,6 +588,7 @@ def _matcher_methods():
     ORBmatcher.SearchLocalPoints = SearchLocalPoints
     ORBmatcher.SearchLocalPoints_batch = SearchLocalPoints_batch
     ORBmatcher.SearchByProjection_last = SearchByProjection_last
+    ORBmatcher.prepare_batch = prepare_batch
     ORBmatcher.SearchByProjection_kf = SearchByProjection_kf
     ORBmatcher._proj_batch = _proj_batch
     ORBmatcher.SearchByProjection_last_batch = SearchByProjection_last_batch
