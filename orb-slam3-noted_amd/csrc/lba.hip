@@ -3007,6 +3007,11 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
         return hipGetLastError();
     };
     mark();  // 1: setup kernels launched
+    // steps queued ahead of the one the host waits on: a few windows (a step of ~0.17 ms against
+    // ~30 us to queue the next) need one, which leaves one no-op step after the last instead of
+    // two; big batches keep more in flight.  SLAMHOT_LBA_DEPTH overrides (A/B)
+    const char* depth_env = std::getenv("SLAMHOT_LBA_DEPTH");
+    const int depth = depth_env ? std::max(2, std::min(kRing - 1, std::atoi(depth_env))) : (nw <= 8 ? 2 : kRing - 1);
     for (int o = 0; o < 2; o++) {
         if (o == 1 && (stopped || user_stop())) break;  // bDoMore = false (Optimizer.cc:1933-1935)
         k_opt_begin<<<blocks(nw, 64), 64, 0, S>>>(nw, dW, dC, o, iters_of[o]);
@@ -3015,7 +3020,7 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
         int seqs[kRing] = {0, 0, 0, 0};
         bool done = false;
         while (!done) {
-            if (launched - checked < kRing - 1) {  // keep the device fed
+            if (launched - checked < depth) {  // keep the device fed
                 const int slot = (int)(launched % kRing);
                 seqs[slot] = (int)(++s->step_seq & 0x7fffffff);
                 SLAM_HIP_TRY(launch_step(slot, seqs[slot]));

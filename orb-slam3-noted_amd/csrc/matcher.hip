@@ -1990,14 +1990,14 @@ extern "C" slam_status slamhot_search_by_projection_last(slam_matcher* m, const 
 // MapPoint::PredictScale with glibc logf, MapPoint.cc:551-566) runs here on the host, in
 // the reference's arithmetic; candidate search and resolution run on the device.
 namespace {
-void kf_queries(const slam_frame_view* F, const slam_kf_points* KF, float th, std::vector<ProjQuery>& qs) {
+void kf_queries(const slam_frame_view* F, const slam_kf_points* KF, float th, ProjQuery* qs) {
     const float* T = F->Tcw;
     float Ow[3];
     for (int i = 0; i < 3; i++) {
         const double acc = (double)T[i] * T[3] + (double)T[4 + i] * T[7] + (double)T[8 + i] * T[11];
         Ow[i] = (float)(-1.0 * acc);
     }
-    qs.assign(KF->n, ProjQuery{});
+    for (int i = 0; i < KF->n; i++) qs[i] = ProjQuery{};
     for (int i = 0; i < KF->n; i++) {
         ProjQuery& Q = qs[i];
         Q.valid = 0;
@@ -2043,6 +2043,14 @@ struct Stager {
         off += (count * sizeof(T) + 255) & ~(size_t)255;
         if (host) std::memcpy(host + o, src, count * sizeof(T));
         return reinterpret_cast<const T*>(dev + o);
+    }
+    // a region the caller fills in place on the host (nullptr in the sizing pass); device address
+    template <class T>
+    T* fill(size_t count, T** host_at) {
+        const size_t o = off;
+        off += (count * sizeof(T) + 255) & ~(size_t)255;
+        *host_at = host && count ? reinterpret_cast<T*>(host + o) : nullptr;
+        return count ? reinterpret_cast<T*>(dev + o) : nullptr;
     }
     template <class T>
     T* take(size_t count) {
@@ -2106,22 +2114,6 @@ __global__ void __launch_bounds__(1024) k_frame_grid(const DevProjCall* __restri
         if (keys[i] != 0xFFFFFFFFu) cf[i] = (int32_t)(keys[i] & 0xFFFFu);
 }
 
-// f(i) for i in [0, n) on up to `cap` host threads (the caller's thread included)
-void parallel_for(int n, int cap, const std::function<void(int)>& f) {
-    const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
-    const int nth = std::max(1, std::min({cap, hw, n / 8}));
-    if (nth <= 1) {
-        for (int i = 0; i < n; i++) f(i);
-        return;
-    }
-    std::vector<std::thread> th;
-    for (int t = 1; t < nth; t++)
-        th.emplace_back([&, t] {
-            for (int i = t; i < n; i += nth) f(i);
-        });
-    for (int i = 0; i < n; i += nth) f(i);
-    for (auto& x : th) x.join();
-}
 
 // Stage nframes frames into the pinned host image and upload them in chunks: host threads copy
 // the frames in index order (frame f's bytes at [off[f], off[f + 1])), and the calling thread
@@ -2312,8 +2304,8 @@ extern "C" slam_status slamhot_search_by_projection_kf(slam_matcher* m, const sl
                                                        float th, int orb_dist, int32_t* f_match, int* nmatches) {
     if (!m || !frame_ok(F) || !F->Tcw || !kf_ok(KF) || !f_match || !nmatches) return SLAM_EINVAL;
     (void)nnratio;
-    std::vector<ProjQuery> qs;
-    kf_queries(F, KF, th, qs);
+    std::vector<ProjQuery> qs(KF->n);
+    kf_queries(F, KF, th, qs.data());
     DevProjCall C{};
     fill_frame(C, F);
     C.mode = kProjKF;
@@ -2369,16 +2361,18 @@ extern "C" slam_status slamhot_search_by_projection_kf_batch(slam_matcher* m, in
         if (!frame_ok(&frames[f]) || !frames[f].Tcw || !kf_ok(&kfs[f]) || (frames[f].n && !f_match[f]))
             return SLAM_EINVAL;
     if (nframes == 0) return SLAM_OK;
-    std::vector<std::vector<ProjQuery>> qs(nframes);
-    parallel_for(nframes, 8, [&](int f) { kf_queries(&frames[f], &kfs[f], th, qs[f]); });
     DevProjCall proto{};
     proto.mode = kProjKF;
     proto.th_dist = orb_dist;
     proto.check_ori = check_ori;
+    // the per-MapPoint queries (the reference's host arithmetic) are computed straight into the
+    // pinned image by the staging threads, overlapping the uploads of earlier frames
     return run_projection_batch(
         m, nframes, frames, proto,
         [&](int f, Stager& S, DevProjCall& c) {
-            c.queries = const_cast<ProjQuery*>(S.put(qs[f].data(), qs[f].size()));
+            ProjQuery* hq = nullptr;
+            c.queries = S.fill<ProjQuery>(kfs[f].n, &hq);
+            if (hq) kf_queries(&frames[f], &kfs[f], th, hq);
             c.qdesc = S.put(kfs[f].mp_desc, (size_t)kfs[f].n * 32);
             return kfs[f].n;
         },
