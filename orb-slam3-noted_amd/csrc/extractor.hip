@@ -408,55 +408,11 @@ __global__ void __launch_bounds__(256) k_fast_cells(Bufs b, const int32_t* list)
     if (threadIdx.x == 0) b.cell_cnt[(size_t)f * P.ncells + cd.slot] = tot2;
 }
 
-// SLAMHOT_FAST_RING32 (experiment): the 16 circle pixels and the centre of a survivor read as
-// three dwords per row (rows -3..+3, columns -3..+3 from the aligned dword at or below c - 3) and
-// cut out with v_alignbyte / bit-field extracts, instead of 17 ds_read_u8
-#ifndef SLAMHOT_FAST_RING32
-#define SLAMHOT_FAST_RING32 0
-#endif
-__device__ __forceinline__ void fast_ring32(const uint8_t* c, int stride, int& v, int (&p)[16]) {
-    const uint8_t* b = c - 3;
-    const int sh = (int)((uintptr_t)b & 3);
-    const uint8_t* a = b - sh;
-    uint32_t w0[7], w1[7];
-#pragma unroll
-    for (int k = 0; k < 7; k++) {
-        const uint32_t* q = reinterpret_cast<const uint32_t*>(a + (k - 3) * stride);
-        const uint32_t d0 = q[0], d1 = q[1], d2 = q[2];
-        w0[k] = __builtin_amdgcn_alignbyte(d1, d0, sh);  // columns c-3 .. c
-        w1[k] = __builtin_amdgcn_alignbyte(d2, d1, sh);  // columns c+1 .. c+4
-    }
-    auto by = [](uint32_t w, int i) { return (int)((w >> (8 * i)) & 0xFFu); };
-    v = by(w0[3], 3);
-    p[0] = by(w0[6], 3);
-    p[1] = by(w1[6], 0);
-    p[2] = by(w1[5], 1);
-    p[3] = by(w1[4], 2);
-    p[4] = by(w1[3], 2);
-    p[5] = by(w1[2], 2);
-    p[6] = by(w1[1], 1);
-    p[7] = by(w1[0], 0);
-    p[8] = by(w0[0], 3);
-    p[9] = by(w0[0], 2);
-    p[10] = by(w0[1], 1);
-    p[11] = by(w0[2], 0);
-    p[12] = by(w0[3], 0);
-    p[13] = by(w0[4], 0);
-    p[14] = by(w0[5], 1);
-    p[15] = by(w0[6], 2);
-}
-
 // ---------------------------------------------------------------------------------------
 // Exact FAST measure without a threshold: M = max(max_s min d[s..s+8], -min_s max d[s..s+8])
 // with d_k = v - p_k over the 16-pixel Bresenham circle (windows by min3/max3 doubling).
 // ---------------------------------------------------------------------------------------
 __device__ __forceinline__ int fast_M(const uint8_t* c, int stride) {
-#if SLAMHOT_FAST_RING32
-    int v, pr[16], d[16];
-    fast_ring32(c, stride, v, pr);
-#pragma unroll
-    for (int k = 0; k < 16; k++) d[k] = v - pr[k];
-#else
     const int v = c[0];
     int d[16];
     d[0] = v - c[3 * stride];
@@ -475,7 +431,6 @@ __device__ __forceinline__ int fast_M(const uint8_t* c, int stride) {
     d[13] = v - c[stride - 3];
     d[14] = v - c[2 * stride - 2];
     d[15] = v - c[3 * stride - 1];
-#endif
     int mn3[16], mx3[16];
 #pragma unroll
     for (int k = 0; k < 16; k++) {
@@ -499,16 +454,11 @@ __device__ __forceinline__ int fast_M(const uint8_t* c, int stride) {
 // and a dark one max(p_k, p_k+8) > v + t for all eight pairs.  Passes ~7% of the pixels of
 // textured frames at t = 7 (the compass pre-test of pass A, two pairs, passes ~24%).
 __device__ __forceinline__ bool fast_pairs8(const uint8_t* c, int stride, int t) {
-#if SLAMHOT_FAST_RING32
-    int v, p[16];
-    fast_ring32(c, stride, v, p);
-#else
     const int v = c[0];
     const int p[16] = {c[3 * stride],      c[3 * stride + 1],  c[2 * stride + 2],  c[stride + 3],
                        c[3],               c[-stride + 3],     c[-2 * stride + 2], c[-3 * stride + 1],
                        c[-3 * stride],     c[-3 * stride - 1], c[-2 * stride - 2], c[-stride - 3],
                        c[-3],              c[stride - 3],      c[2 * stride - 2],  c[3 * stride - 1]};
-#endif
     int lo = min(p[0], p[8]), hi = max(p[0], p[8]);
 #pragma unroll
     for (int k = 1; k < 8; k++) {
