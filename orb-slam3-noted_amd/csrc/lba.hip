@@ -90,6 +90,7 @@ struct WinCtl {
     int qmax, nbad, it, iters;
     int trials, opt, result, n_outlier;
     int iters_run[2];
+    int iters2;  // iterations of the second optimize() (0: none); k_trial_control moves on to it
 };
 
 struct Counters {
@@ -2085,19 +2086,30 @@ __global__ void __launch_bounds__(kCtlThreads) k_trial_control(const WinDesc* __
     C.it++;
     C.chi2_final = C.cur_chi;
     C.active = (result == 0) && C.it < C.iters && !stop;
+    if (!C.active && C.opt == 0 && C.iters2 > 0 && !stop) {
+        // optimize(5) is over and no stop was seen: bDoMore, initializeOptimization(0) on the same
+        // graph and optimize(10) (Optimizer.cc:1931-1986), started here so the next queued step runs
+        // its first iteration (a stop set meanwhile is caught by that step's k_iter_begin, so no
+        // iteration of optimize(10) runs, as when the reference skips it)
+        C.opt = 1;
+        C.it = 0;
+        C.iters = C.iters2;
+        C.active = 1;
+    }
     C.need_lin = C.active;  // the next step linearizes again
     tally_publish(tally, 0, C.active, gridDim.x, host_slot, seq);
 }
 
 // start of SparseOptimizer::optimize(iters) for every window
 __global__ void k_opt_begin(int nwin, const WinDesc* __restrict__ wins, WinCtl* __restrict__ ctl, int opt,
-                            int iters) {
+                            int iters, int iters2) {
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= nwin) return;
     WinCtl& C = ctl[w];
     C.opt = opt;
     C.it = 0;
     C.iters = iters;
+    C.iters2 = iters2;
     C.active = iters > 0 && wins[w].ne > 0;  // no edges: initializeOptimization fails
     C.need_trial = 0;
     C.need_lin = C.active;
@@ -2940,7 +2952,6 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     // the other windows, so the host queues steps without waiting for any decision and reads
     // the per-step counters asynchronously (a ring of kRing steps in flight).  While it waits it
     // mirrors the caller's stop flag into pinned memory the control kernels read.
-    bool stopped = false;
     int syncs = 0, step_no = 0;
     const int iters_of[2] = {opt->iters_first, opt->iters_second};
     // Wait for a step's counters: the last k_trial_control block stores the step's sequence
@@ -3012,13 +3023,15 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     // two; big batches keep more in flight.  SLAMHOT_LBA_DEPTH overrides (A/B)
     const char* depth_env = std::getenv("SLAMHOT_LBA_DEPTH");
     const int depth = depth_env ? std::max(2, std::min(kRing - 1, std::atoi(depth_env))) : (nw <= 8 ? 2 : kRing - 1);
-    for (int o = 0; o < 2; o++) {
-        if (o == 1 && (stopped || user_stop())) break;  // bDoMore = false (Optimizer.cc:1933-1935)
-        k_opt_begin<<<blocks(nw, 64), 64, 0, S>>>(nw, dW, dC, o, iters_of[o]);
-        if (iters_of[o] <= 0) continue;
+    // optimize(5) and optimize(10) as one stream of steps: each window's control block moves on to
+    // its second optimize() when the first ends without a stop (k_trial_control), so the host
+    // neither waits at the boundary nor drains queued steps there
+    {
+        const int o0 = iters_of[0] > 0 ? 0 : 1;
+        k_opt_begin<<<blocks(nw, 64), 64, 0, S>>>(nw, dW, dC, o0, iters_of[o0], o0 == 0 ? iters_of[1] : 0);
         long long launched = 0, checked = 0;
         int seqs[kRing] = {0, 0, 0, 0};
-        bool done = false;
+        bool done = iters_of[o0] <= 0;
         while (!done) {
             if (launched - checked < depth) {  // keep the device fed
                 const int slot = (int)(launched % kRing);
@@ -3040,9 +3053,7 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
             const Counters c = s->h_cnt[slot];
             done = c.active == 0 && c.need_trial == 0;
         }
-        const int last = (int)((launched - 1) % kRing);
-        SLAM_HIP_TRY(wait_step(last, seqs[last]));  // the queued no-op steps
-        if (*s->h_stop) stopped = true;
+        // the steps still queued are no-ops; the finalize kernels follow them in stream order
     }
     mark();  // 3: LM loop done
     k_finalize_edges<<<blocks(H.ne, T), T, 0, S>>>(H.ne, dE, dC, poses, pts, pose_stride, pt_stride,
