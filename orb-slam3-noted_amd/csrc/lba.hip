@@ -717,10 +717,9 @@ __device__ __forceinline__ void t16_put(double* Tw, int n, int R, int Cc, double
 //   bm  [W.bm0 + i * nwd + wd]   bit q <-> local point 64 wd + q observed by local pose i
 //   bmp [same index]             set bits of pose i before word wd
 //   pls [W.spe0 + pbase[i] + r]  r-th free-pose edge (edge id) of pose i in point order
-__global__ void k_bm_set(int nspe_total, const int* __restrict__ spe, const EdgeS* __restrict__ E,
-                         const WinDesc* __restrict__ wins, unsigned long long* __restrict__ bm,
-                         int* __restrict__ spe_hp) {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void bm_set_body(int s, int nspe_total, const int* __restrict__ spe,
+                                            const EdgeS* __restrict__ E, const WinDesc* __restrict__ wins,
+                                            unsigned long long* __restrict__ bm, int* __restrict__ spe_hp) {
     if (s >= nspe_total) return;
     const EdgeS e = E[spe[s]];
     spe_hp[s] = e.hp;  // free-pose index per spe entry (the back-substitution's xp row)
@@ -730,10 +729,11 @@ __global__ void k_bm_set(int nspe_total, const int* __restrict__ spe, const Edge
 }
 
 // one thread per pose of the window: word prefix counts, then the pose list bases in pose order
-__global__ void k_bm_scan(const WinDesc* __restrict__ wins, const unsigned long long* __restrict__ bm,
-                          int* __restrict__ bmp, int* __restrict__ pbase, int* __restrict__ pcnt) {
+__device__ __forceinline__ void bm_scan_body(int w, const WinDesc* __restrict__ wins,
+                                             const unsigned long long* __restrict__ bm, int* __restrict__ bmp,
+                                             int* __restrict__ pbase, int* __restrict__ pcnt) {
     __shared__ int cnt[kMaxN / 6 + 1];
-    const WinDesc W = wins[blockIdx.x];
+    const WinDesc W = wins[w];
     for (int i = threadIdx.x; i < W.np; i += blockDim.x) {
         const long long o = W.bm0 + (long long)i * W.nwd;
         int run = 0;
@@ -754,11 +754,11 @@ __global__ void k_bm_scan(const WinDesc* __restrict__ wins, const unsigned long 
     }
 }
 
-__global__ void k_bm_list(int nspe_total, const int* __restrict__ spe, const EdgeS* __restrict__ E,
-                          const WinDesc* __restrict__ wins, const unsigned long long* __restrict__ bm,
-                          const int* __restrict__ bmp, const int* __restrict__ pbase, int* __restrict__ pls,
-                          int* __restrict__ ppt) {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void bm_list_body(int s, int nspe_total, const int* __restrict__ spe,
+                                             const EdgeS* __restrict__ E, const WinDesc* __restrict__ wins,
+                                             const unsigned long long* __restrict__ bm, const int* __restrict__ bmp,
+                                             const int* __restrict__ pbase, int* __restrict__ pls,
+                                             int* __restrict__ ppt) {
     if (s >= nspe_total) return;
     const EdgeS e = E[spe[s]];
     const WinDesc& W = wins[e.win];
@@ -777,10 +777,9 @@ __device__ __forceinline__ int ct_words(const WinDesc& W, const unsigned long lo
 }
 
 // thread per block: its number of contributions
-__global__ void k_ct_count(int nblk_total, const int2* __restrict__ blk_pose, const int* __restrict__ blk_win,
-                           const WinDesc* __restrict__ wins, const unsigned long long* __restrict__ bm,
-                           int* __restrict__ cnt) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void ct_count_body(int b, int nblk_total, const int2* __restrict__ blk_pose,
+                                              const int* __restrict__ blk_win, const WinDesc* __restrict__ wins,
+                                              const unsigned long long* __restrict__ bm, int* __restrict__ cnt) {
     if (b >= nblk_total) return;
     const WinDesc& W = wins[blk_win[b]];
     const int2 ij = blk_pose[b];
@@ -792,10 +791,10 @@ __global__ void k_ct_count(int nblk_total, const int2* __restrict__ blk_pose, co
 
 // workgroup per window: ct_off over the window's blocks (exclusive scan from W.ct0)
 constexpr int kCtScanThreads = 1024;
-__global__ void __launch_bounds__(kCtScanThreads) k_ct_scan(const WinDesc* __restrict__ wins,
-                                                            const int* __restrict__ cnt, int* __restrict__ ct_off) {
+__device__ __forceinline__ void ct_scan_body(int w, const WinDesc* __restrict__ wins, const int* __restrict__ cnt,
+                                             int* __restrict__ ct_off) {
     __shared__ int part[kCtScanThreads];
-    const WinDesc W = wins[blockIdx.x];
+    const WinDesc W = wins[w];
     const int per = (W.nblk + kCtScanThreads - 1) / kCtScanThreads;
     const int b0 = min(W.nblk, (int)threadIdx.x * per), b1 = min(W.nblk, b0 + per);
     int sum = 0;
@@ -1639,6 +1638,43 @@ __device__ __forceinline__ void t16_pivot(double (&row)[8], int r, int g, int la
     }
 }
 
+// Two-row form of the same elimination: lane r of DPP row 0 holds row r of A (register c =
+// column c), lane r of DPP row 1 the same row of I (rows 2 / 3 repeat 0 / 1).  One instruction
+// updates register c in both halves with the pivot row's register c broadcast inside each DPP
+// row, so the multiplier a_rJ / d_J is local to the A half (no cross-group shuffle on the chain)
+// and reaches the I half by one v_permlane16_swap off the chain.  A column c <= J and an I column
+// c > J of the pivot row are leftovers / zeros, so updating both halves of every register is
+// harmless (a zero pivot-row entry leaves the I column unchanged).
+__device__ __forceinline__ double row0_to_row1(double v) {  // lanes of DPP row 1 (3) get row 0's (2's) value
+    const long long b = __double_as_longlong(v);
+    const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)b, (unsigned)b, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
+    return __longlong_as_double(((long long)hi[0] << 32) | (unsigned int)lo[0]);
+}
+template <int J>
+__device__ __forceinline__ void t16_pivot2(double (&row)[16], int r, bool& bad, double dj) {
+    if (dj == 0.0) bad = true;
+    const double inv = rcp_nr(dj);
+    double pr[16];
+#pragma unroll
+    for (int c = 0; c < 16; c++) pr[c] = row_bcast<J>(row[c]);
+    const double m = r > J ? row[J] * inv : 0.0;  // I half: a finite leftover, times a zero pr
+    if constexpr (J + 1 < 16) {
+        row[J + 1] = __builtin_fma(-m, pr[J + 1], row[J + 1]);
+        const double dn = readlane_d(row[J + 1], J + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        const double mm = row0_to_row1(m);
+#pragma unroll
+        for (int c = 0; c < 16; c++)
+            if (c != J + 1) row[c] = __builtin_fma(-mm, pr[c], row[c]);
+        t16_pivot2<J + 1>(row, r, bad, dn);
+    } else {
+        const double mm = row0_to_row1(m);
+#pragma unroll
+        for (int c = 0; c < 16; c++) row[c] = __builtin_fma(-mm, pr[c], row[c]);
+    }
+}
+
 // The diagonal tile of panel k (held by wave 0 in the transposed accumulator layout, which for
 // a symmetric tile is the tile itself): Gauss elimination of [A_kk | I] without pivoting, the
 // four 16-lane groups of wave 0 holding A columns 0-7, 8-15 and I columns 0-7, 8-15 of row
@@ -1650,6 +1686,27 @@ __device__ __forceinline__ void t16_diag(Lds& L, int k, double4_t dt, int lane) 
 #pragma unroll
     for (int u = 0; u < 4; u++) L.D[lr * 16 + lq + 4 * u] = dt[u];
     wave_sync();
+#ifdef SLAMHOT_T16_DIAG2
+    {
+        const int r = lane & 15;
+        const bool ih = (lane >> 4) & 1;
+        double row[16];
+#pragma unroll
+        for (int c = 0; c < 16; c++) row[c] = ih ? (c == r ? 1.0 : 0.0) : L.D[r * 16 + c];
+        bool bad = false;
+        t16_pivot2<0>(row, r, bad, readlane_d(row[0], 0));
+        if (bad && lane == 0) L.fail = 1;
+        if (lane < 16) {
+            double dr = row[0];
+#pragma unroll
+            for (int c = 1; c < 16; c++) dr = r == c ? row[c] : dr;
+            L.dinv[k][r] = rcp_nr(dr);
+        } else if (lane < 32) {
+#pragma unroll
+            for (int c = 0; c < 16; c++) L.M[k][c * 16 + r] = row[c];  // M_k[col][r] = L^-1[r][col]
+        }
+    }
+#else
     const int r = lane & 15, g = lane >> 4;
     double row[8];
 #pragma unroll
@@ -1672,6 +1729,7 @@ __device__ __forceinline__ void t16_diag(Lds& L, int k, double4_t dt, int lane) 
 #pragma unroll
         for (int c = 0; c < 8; c++) L.M[k][(8 * (g & 1) + c) * 16 + r] = row[c];  // M_k[col][r] = L^-1[r][col]
     }
+#endif
     wave_sync();
     if (lane < 16) {
         const int c = lane;
@@ -1778,6 +1836,8 @@ __global__ void __launch_bounds__(kT16Waves * 64) k_ldlt_t16(const WinDesc* __re
                 __builtin_amdgcn_s_setprio(0);
                 T16_MARK(7);
             } else {
+                // one tile ahead: deeper prefetch (2-4 tiles in flight) measured slower, 114 -> 116-118 us
+                // in mb_ldlt and -10% on the batched LBA leg (profiles/r04e_t16_prefetch.txt)
                 int t = t0 + wid;
                 double4_t cur = t < ntiles ? t16_load(Tw + 256 * t, lane) : double4_t{0.0, 0.0, 0.0, 0.0};
                 while (t < ntiles) {
@@ -1849,8 +1909,8 @@ __global__ void __launch_bounds__(kT16Waves * 64) k_ldlt_t16(const WinDesc* __re
 
 // Identity padding of the dense systems (rows/cols n..npad-1) and a zero rhs tail; the
 // factorization keeps it invariant, so it is written once per solve.
-__global__ void k_ldlt_pad(const WinDesc* __restrict__ wins, double* __restrict__ Hs) {
-    const WinDesc W = wins[blockIdx.x];
+__device__ __forceinline__ void ldlt_pad_body(int w, const WinDesc* __restrict__ wins, double* __restrict__ Hs) {
+    const WinDesc W = wins[w];
     const int n = W.n, npad = ldlt_npad(n), ld = W.ld;
     double* A = Hs + W.hs_off;
     for (int i = n + threadIdx.x; i < npad; i += blockDim.x) {
@@ -1862,10 +1922,10 @@ __global__ void k_ldlt_pad(const WinDesc* __restrict__ wins, double* __restrict_
 // Identity padding of the tile scratch (rows / columns n .. 16T-1 of the last tile row): the
 // scratch is zeroed once per solve and k_schur_block rewrites every real element each trial;
 // the factorization leaves the padding invariant (its W rows are zero).
-__global__ void k_t16_pad(const WinDesc* __restrict__ wins, double* __restrict__ Ts) {
-    const WinDesc W = wins[blockIdx.x];
+__device__ __forceinline__ void t16_pad_body(int w, const WinDesc* __restrict__ wins, double* __restrict__ Ts) {
+    const WinDesc W = wins[w];
     const int T = (W.n + 15) >> 4;
-    for (int R = W.n + (int)threadIdx.x; R < 16 * T; R += blockDim.x) t16_put(Ts + blockIdx_win_tiles(blockIdx.x), W.n, R, R, 1.0);
+    for (int R = W.n + (int)threadIdx.x; R < 16 * T; R += blockDim.x) t16_put(Ts + blockIdx_win_tiles(w), W.n, R, R, 1.0);
 }
 
 // x_l = Dinv (b_l - Hpl^T x_p) (block_solver.hpp:456-481) and the trial point estimate.
@@ -2101,9 +2161,8 @@ __global__ void __launch_bounds__(kCtlThreads) k_trial_control(const WinDesc* __
 }
 
 // start of SparseOptimizer::optimize(iters) for every window
-__global__ void k_opt_begin(int nwin, const WinDesc* __restrict__ wins, WinCtl* __restrict__ ctl, int opt,
-                            int iters, int iters2) {
-    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void opt_begin_body(int w, int nwin, const WinDesc* __restrict__ wins,
+                                               WinCtl* __restrict__ ctl, int opt, int iters, int iters2) {
     if (w >= nwin) return;
     WinCtl& C = ctl[w];
     C.opt = opt;
@@ -2116,11 +2175,11 @@ __global__ void k_opt_begin(int nwin, const WinDesc* __restrict__ wins, WinCtl* 
 }
 
 // final outlier classification (Optimizer.cc:1995-2038) and float write-back (:2041-2077)
-__global__ void k_finalize_edges(int ne_total, const EdgeS* __restrict__ E, const WinCtl* __restrict__ ctl,
-                                 const double* __restrict__ poses, const double* __restrict__ pts,
-                                 long long pose_stride, long long pt_stride, const double* __restrict__ err,
-                                 const double* __restrict__ trl, uint8_t* __restrict__ outlier) {
-    const int ei = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void finalize_edge_body(int ei, int ne_total, const EdgeS* __restrict__ E,
+                                                   const WinCtl* __restrict__ ctl, const double* __restrict__ poses,
+                                                   const double* __restrict__ pts, long long pose_stride,
+                                                   long long pt_stride, const double* __restrict__ err,
+                                                   const double* __restrict__ trl, uint8_t* __restrict__ outlier) {
     if (ei >= ne_total) return;
     const EdgeS e = E[ei];
     const WinCtl& C = ctl[e.win];
@@ -2141,12 +2200,11 @@ __global__ void k_finalize_edges(int ne_total, const EdgeS* __restrict__ E, cons
     outlier[ei] = (c > (stereo ? 7.815 : 5.991) || !(Xc[2] > 0.0)) ? 1 : 0;
 }
 
-__global__ void k_finalize_state(int nkf_total, int npt_total, const int* __restrict__ kf_win,
-                                 const int* __restrict__ pt_win, const WinCtl* __restrict__ ctl,
-                                 const double* __restrict__ poses, const double* __restrict__ pts,
-                                 long long pose_stride, long long pt_stride, float* __restrict__ kf_out,
-                                 float* __restrict__ pt_out) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void finalize_state_body(int t, int nkf_total, int npt_total, const int* __restrict__ kf_win,
+                                                    const int* __restrict__ pt_win, const WinCtl* __restrict__ ctl,
+                                                    const double* __restrict__ poses, const double* __restrict__ pts,
+                                                    long long pose_stride, long long pt_stride,
+                                                    float* __restrict__ kf_out, float* __restrict__ pt_out) {
     if (t < nkf_total) {
         const double* P = poses + ctl[kf_win[t]].sel * pose_stride + 8 * (long long)t;
         double R[9];
@@ -2165,6 +2223,37 @@ __global__ void k_finalize_state(int nkf_total, int npt_total, const int* __rest
     }
 }
 
+// one launch after the LM loop: outlier flags per edge | float estimates | the control blocks
+// into the read-back region (was two kernels and a device copy)
+struct FinalArgs {
+    int ne, nkf, npt, nw, nb_edges, nb_state;
+    const EdgeS* E;
+    const WinCtl* ctl;
+    const double* poses;
+    const double* pts;
+    long long pose_stride, pt_stride;
+    const double* err;
+    const double* trl;
+    const int* kf_win;
+    const int* pt_win;
+    uint8_t* outlier;
+    float* kf_out;
+    float* pt_out;
+    int* ctl_out;
+};
+__global__ void __launch_bounds__(256) k_finalize(FinalArgs a) {
+    int b = blockIdx.x;
+    if (b < a.nb_edges)
+        return finalize_edge_body(b * 256 + threadIdx.x, a.ne, a.E, a.ctl, a.poses, a.pts, a.pose_stride, a.pt_stride,
+                                  a.err, a.trl, a.outlier);
+    b -= a.nb_edges;
+    if (b < a.nb_state)
+        return finalize_state_body(b * 256 + threadIdx.x, a.nkf, a.npt, a.kf_win, a.pt_win, a.ctl, a.poses, a.pts,
+                                   a.pose_stride, a.pt_stride, a.kf_out, a.pt_out);
+    const int words = (int)(sizeof(WinCtl) / sizeof(int)) * a.nw;
+    for (int i = threadIdx.x; i < words; i += blockDim.x) a.ctl_out[i] = ((const int*)a.ctl)[i];
+}
+
 // The per-solve clears (pose bitmaps, increments, errors, tile scratch, the control tally) in one
 // launch instead of one fill per buffer
 struct ClearRange {
@@ -2177,20 +2266,19 @@ struct ClearList {
     ClearRange r[kClearMax];
     int n;
 };
-__global__ void k_clear(ClearList L) {
-    const long long stride = (long long)gridDim.x * blockDim.x;
+__device__ __forceinline__ void clear_body(const ClearList& L, int b, int nb) {
+    const long long stride = (long long)nb * blockDim.x;
     for (int i = 0; i < L.n; i++) {
         unsigned long long* p = L.r[i].p;
         const unsigned long long v = L.r[i].v;
-        for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < L.r[i].n; e += stride) p[e] = v;
+        for (long long e = b * (long long)blockDim.x + threadIdx.x; e < L.r[i].n; e += stride) p[e] = v;
     }
 }
 
 // Converter::toSE3Quat on the device for the initial estimates
-__global__ void k_init_state(int nkf_total, int npt_total, const float* __restrict__ kf_in,
-                             const float* __restrict__ pt_in, double* __restrict__ poses,
-                             double* __restrict__ pts) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void init_state_body(int t, int nkf_total, int npt_total, const float* __restrict__ kf_in,
+                                                const float* __restrict__ pt_in, double* __restrict__ poses,
+                                                double* __restrict__ pts) {
     if (t < nkf_total) {
         const float* T = kf_in + 16 * (long long)t;
         double R[9];
@@ -2213,6 +2301,69 @@ __global__ void k_init_state(int nkf_total, int npt_total, const float* __restri
         for (int k = 0; k < 3; k++) X[k] = pt_in[3 * (long long)p + k];
         X[3] = 0.0;
     }
+}
+
+// The per-solve setup in four launches, each the union of independent steps (a block range
+// apiece, so every branch is block-uniform).  A lone window pays one dispatch per launch (~5 us
+// each in profiles/r04d_dropin_kernels.txt), and eleven launches became four plus k_ct_fill.
+struct SetupArgs {
+    ClearList clear;
+    int nb_clear, nb_init, nb_spe, nb_blk, nb_list, nw_scan;
+    int nw, nkf, npt, nspe, nblk;
+    const WinDesc* wins;
+    WinCtl* ctl;
+    int opt, iters, iters2;
+    const float* kf_in;
+    const float* pt_in;
+    double* poses;
+    double* pts;
+    double* Hs;
+    double* Ts;  // tile scratch (k_ldlt_t16) or null
+    const int* spe;
+    const EdgeS* E;
+    unsigned long long* bm;
+    int* spe_hp;
+    int* bmp;
+    int* pbase;
+    int* pcnt;
+    int* pls;
+    int* ppt;
+    const int2* blk_pose;
+    const int* blk_win;
+    int* ct_cnt;
+    int* ct_off;
+};
+// clears | initial estimates | dense padding | optimize() start
+__global__ void __launch_bounds__(256) k_setup_a(SetupArgs a) {
+    int b = blockIdx.x;
+    if (b < a.nb_clear) return clear_body(a.clear, b, a.nb_clear);
+    b -= a.nb_clear;
+    if (b < a.nb_init) return init_state_body(b * 256 + threadIdx.x, a.nkf, a.npt, a.kf_in, a.pt_in, a.poses, a.pts);
+    b -= a.nb_init;
+    if (b < a.nw) return ldlt_pad_body(b, a.wins, a.Hs);
+    b -= a.nw;
+    opt_begin_body(b * 256 + threadIdx.x, a.nw, a.wins, a.ctl, a.opt, a.iters, a.iters2);
+}
+// pose bitmaps | tile padding (both after the clears)
+__global__ void __launch_bounds__(256) k_setup_b(SetupArgs a) {
+    int b = blockIdx.x;
+    if (b < a.nb_spe) return bm_set_body(b * 256 + threadIdx.x, a.nspe, a.spe, a.E, a.wins, a.bm, a.spe_hp);
+    b -= a.nb_spe;
+    t16_pad_body(b, a.wins, a.Ts);
+}
+// bitmap word prefixes and pose list bases | contribution counts per block
+__global__ void __launch_bounds__(256) k_setup_c(SetupArgs a) {
+    int b = blockIdx.x;
+    if (b < a.nw) return bm_scan_body(b, a.wins, a.bm, a.bmp, a.pbase, a.pcnt);
+    b -= a.nw;
+    ct_count_body(b * 256 + threadIdx.x, a.nblk, a.blk_pose, a.blk_win, a.wins, a.bm, a.ct_cnt);
+}
+// contribution offsets | pose edge lists
+__global__ void __launch_bounds__(kCtScanThreads) k_setup_d(SetupArgs a) {
+    int b = blockIdx.x;
+    if (b < a.nw_scan) return ct_scan_body(b, a.wins, a.ct_cnt, a.ct_off);
+    b -= a.nw_scan;
+    bm_list_body(b * kCtScanThreads + threadIdx.x, a.nspe, a.spe, a.E, a.wins, a.bm, a.bmp, a.pbase, a.pls, a.ppt);
 }
 
 }  // namespace lba
@@ -2895,6 +3046,7 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     // words 4 and 5)
     *s->h_stop = user_stop() ? 1 : 0;
     SLAM_HIP_TRY(hipEventRecord(s->ev0, S));
+    SetupArgs SA{};
     {
         ClearList CL{};
         long long most = 0;
@@ -2914,32 +3066,66 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
         add(dTally + 6, 1, 0ull);
         if (use_t16) add(s->Ts.p, t16_tiles_bytes() * nw / 8, 0ull);  // tile scratch (padding by k_t16_pad)
         if (CL.n != (use_t16 ? 9 : 8)) return SLAM_EINVAL;  // every range above made it into the list
-        k_clear<<<(unsigned)std::min<long long>(1024, (most + 255) / 256), 256, 0, S>>>(CL);
-    }
-    k_init_state<<<blocks(H.nkf + H.npt, T), T, 0, S>>>(H.nkf, H.npt, DP.kf_in, DP.pt_in,
-                                                         poses, pts);
-    k_ldlt_pad<<<nw, 64, 0, S>>>(dW, as<double>(s->Hs));
-    // the Schur contribution structure, once per solve (pose list bases / lengths even without edges)
-    if (Z.nspe)
-        k_bm_set<<<blocks(Z.nspe, T), T, 0, S>>>(Z.nspe, DP.spe, DP.edges, DP.wins, as<unsigned long long>(s->bm),
-                                                  as<int>(s->spe_hp));
-    k_bm_scan<<<nw, 64, 0, S>>>(DP.wins, as<unsigned long long>(s->bm), as<int>(s->bmp), as<int>(s->pbase),
-                                as<int>(s->pcnt));
-    if (Z.nspe) {
-        k_bm_list<<<blocks(Z.nspe, T), T, 0, S>>>(Z.nspe, DP.spe, DP.edges, DP.wins, as<unsigned long long>(s->bm),
-                                                   as<int>(s->bmp), as<int>(s->pbase), as<int>(s->pls),
-                                                   as<int>(s->ppt));
-    }
-    if (H.nblk) {
-        k_ct_count<<<blocks(H.nblk, T), T, 0, S>>>(H.nblk, DP.blk_pose, DP.blk_win, DP.wins,
-                                                    as<unsigned long long>(s->bm), as<int>(s->ct_cnt));
-        k_ct_scan<<<nw, kCtScanThreads, 0, S>>>(DP.wins, as<int>(s->ct_cnt), as<int>(s->ct_off));
-        k_ct_fill<<<blocks(H.nblk, 4), 256, 0, S>>>(H.nblk, DP.blk_pose, DP.blk_win, DP.wins,
-                                                     as<unsigned long long>(s->bm), as<int>(s->bmp), as<int>(s->pbase),
-                                                     as<int>(s->pls), as<int>(s->ct_off), as<int4>(s->ct));
+        SA.clear = CL;
+        SA.nb_clear = (int)std::min<long long>(1024, (most + 255) / 256);
     }
     double* tiles = use_t16 ? as<double>(s->Ts) : nullptr;
-    if (use_t16) k_t16_pad<<<nw, 64, 0, S>>>(dW, tiles);
+    // optimize(5) and optimize(10) as one stream of steps: each window's control block moves on to
+    // its second optimize() when the first ends without a stop (k_trial_control), so the host
+    // neither waits at the boundary nor drains queued steps there
+    const int iters_of[2] = {opt->iters_first, opt->iters_second};
+    const int o0 = iters_of[0] > 0 ? 0 : 1;
+    {
+        auto cdiv = [](long long n, int t) { return (int)((n + t - 1) / t); };
+        SA.nb_init = cdiv(H.nkf + H.npt, 256);
+        SA.nb_spe = cdiv(Z.nspe, 256);
+        SA.nb_blk = cdiv(H.nblk, 256);
+        SA.nb_list = cdiv(Z.nspe, kCtScanThreads);
+        SA.nw_scan = H.nblk ? nw : 0;
+        SA.nw = nw;
+        SA.nkf = H.nkf;
+        SA.npt = H.npt;
+        SA.nspe = Z.nspe;
+        SA.nblk = H.nblk;
+        SA.wins = dW;
+        SA.ctl = dC;
+        SA.opt = o0;
+        SA.iters = iters_of[o0];
+        SA.iters2 = o0 == 0 ? iters_of[1] : 0;
+        SA.kf_in = DP.kf_in;
+        SA.pt_in = DP.pt_in;
+        SA.poses = poses;
+        SA.pts = pts;
+        SA.Hs = as<double>(s->Hs);
+        SA.Ts = tiles;
+        SA.spe = DP.spe;
+        SA.E = DP.edges;
+        SA.bm = as<unsigned long long>(s->bm);
+        SA.spe_hp = as<int>(s->spe_hp);
+        SA.bmp = as<int>(s->bmp);
+        SA.pbase = as<int>(s->pbase);
+        SA.pcnt = as<int>(s->pcnt);
+        SA.pls = as<int>(s->pls);
+        SA.ppt = as<int>(s->ppt);
+        SA.blk_pose = DP.blk_pose;
+        SA.blk_win = DP.blk_win;
+        SA.ct_cnt = as<int>(s->ct_cnt);
+        SA.ct_off = as<int>(s->ct_off);
+        // (a) clears, initial estimates, dense padding, optimize() start; (b) pose bitmaps and tile
+        // padding; (c) bitmap prefixes / pose list bases (pose list lengths even without edges) and
+        // contribution counts; (d) contribution offsets and pose edge lists; then the lists
+        k_setup_a<<<SA.nb_clear + SA.nb_init + nw + cdiv(nw, 256), 256, 0, S>>>(SA);
+        const int nb_b = SA.nb_spe + (use_t16 ? nw : 0);
+        if (nb_b) k_setup_b<<<nb_b, 256, 0, S>>>(SA);
+        k_setup_c<<<nw + SA.nb_blk, 256, 0, S>>>(SA);
+        const int nb_d = SA.nw_scan + SA.nb_list;
+        if (nb_d) k_setup_d<<<nb_d, kCtScanThreads, 0, S>>>(SA);
+        if (H.nblk)
+            k_ct_fill<<<blocks(H.nblk, 4), 256, 0, S>>>(H.nblk, DP.blk_pose, DP.blk_win, DP.wins,
+                                                         as<unsigned long long>(s->bm), as<int>(s->bmp),
+                                                         as<int>(s->pbase), as<int>(s->pls), as<int>(s->ct_off),
+                                                         as<int4>(s->ct));
+    }
     const size_t lds_bytes = ldlt_lds_bytes(Z.max_n);
     // Schur complement by block row (k_schur_rows: a workgroup per free pose) for batches with
     // enough rows to fill the chip; a few windows (LocalMapping's one-window call) keep the
@@ -2953,7 +3139,6 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     // the per-step counters asynchronously (a ring of kRing steps in flight).  While it waits it
     // mirrors the caller's stop flag into pinned memory the control kernels read.
     int syncs = 0, step_no = 0;
-    const int iters_of[2] = {opt->iters_first, opt->iters_second};
     // Wait for a step's counters: the last k_trial_control block stores the step's sequence
     // number into the mapped slot after the counts.  The host spins on that word (mirroring the
     // caller's stop flag meanwhile) and asks the stream for errors now and then, so a faulted
@@ -3023,12 +3208,7 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     // two; big batches keep more in flight.  SLAMHOT_LBA_DEPTH overrides (A/B)
     const char* depth_env = std::getenv("SLAMHOT_LBA_DEPTH");
     const int depth = depth_env ? std::max(2, std::min(kRing - 1, std::atoi(depth_env))) : (nw <= 8 ? 2 : kRing - 1);
-    // optimize(5) and optimize(10) as one stream of steps: each window's control block moves on to
-    // its second optimize() when the first ends without a stop (k_trial_control), so the host
-    // neither waits at the boundary nor drains queued steps there
     {
-        const int o0 = iters_of[0] > 0 ? 0 : 1;
-        k_opt_begin<<<blocks(nw, 64), 64, 0, S>>>(nw, dW, dC, o0, iters_of[o0], o0 == 0 ? iters_of[1] : 0);
         long long launched = 0, checked = 0;
         int seqs[kRing] = {0, 0, 0, 0};
         bool done = iters_of[o0] <= 0;
@@ -3056,15 +3236,34 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
         // the steps still queued are no-ops; the finalize kernels follow them in stream order
     }
     mark();  // 3: LM loop done
-    k_finalize_edges<<<blocks(H.ne, T), T, 0, S>>>(H.ne, dE, dC, poses, pts, pose_stride, pt_stride,
-                                                    as<double>(s->err), cam.trl, dout + o_outl);
-    k_finalize_state<<<blocks(H.nkf + H.npt, T), T, 0, S>>>(H.nkf, H.npt, DP.kf_win, DP.pt_win, dC,
-                                                             poses, pts, pose_stride, pt_stride,
-                                                             (float*)dout, (float*)(dout + o_pt));
+    {
+        static_assert(sizeof(WinCtl) % sizeof(int) == 0, "k_finalize copies the control blocks as ints");
+        FinalArgs FA{};
+        FA.ne = H.ne;
+        FA.nkf = H.nkf;
+        FA.npt = H.npt;
+        FA.nw = nw;
+        FA.nb_edges = (H.ne + T - 1) / T;
+        FA.nb_state = (H.nkf + H.npt + T - 1) / T;
+        FA.E = dE;
+        FA.ctl = dC;
+        FA.poses = poses;
+        FA.pts = pts;
+        FA.pose_stride = pose_stride;
+        FA.pt_stride = pt_stride;
+        FA.err = as<double>(s->err);
+        FA.trl = cam.trl;
+        FA.kf_win = DP.kf_win;
+        FA.pt_win = DP.pt_win;
+        FA.outlier = dout + o_outl;
+        FA.kf_out = (float*)dout;
+        FA.pt_out = (float*)(dout + o_pt);
+        FA.ctl_out = (int*)(dout + o_ctl);
+        k_finalize<<<FA.nb_edges + FA.nb_state + 1, T, 0, S>>>(FA);
+    }
     SLAM_HIP_TRY(hipGetLastError());
     SLAM_HIP_TRY(hipEventRecord(s->ev1, S));
     // one pinned read-back (pageable copies are synchronous, ~40 us each)
-    SLAM_HIP_TRY(hipMemcpyAsync(dout + o_ctl, DP.ctl, sizeof(WinCtl) * nw, hipMemcpyDeviceToDevice, S));
     SLAM_HIP_TRY(hipMemcpyAsync(s->hout, dout, out_bytes, hipMemcpyDeviceToHost, S));
     mark();  // 4: finalize + copies queued
     SLAM_HIP_TRY(hipStreamSynchronize(S));
