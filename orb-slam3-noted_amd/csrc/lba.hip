@@ -1638,43 +1638,6 @@ __device__ __forceinline__ void t16_pivot(double (&row)[8], int r, int g, int la
     }
 }
 
-// Two-row form of the same elimination: lane r of DPP row 0 holds row r of A (register c =
-// column c), lane r of DPP row 1 the same row of I (rows 2 / 3 repeat 0 / 1).  One instruction
-// updates register c in both halves with the pivot row's register c broadcast inside each DPP
-// row, so the multiplier a_rJ / d_J is local to the A half (no cross-group shuffle on the chain)
-// and reaches the I half by one v_permlane16_swap off the chain.  A column c <= J and an I column
-// c > J of the pivot row are leftovers / zeros, so updating both halves of every register is
-// harmless (a zero pivot-row entry leaves the I column unchanged).
-__device__ __forceinline__ double row0_to_row1(double v) {  // lanes of DPP row 1 (3) get row 0's (2's) value
-    const long long b = __double_as_longlong(v);
-    const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)b, (unsigned)b, false, false);
-    const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
-    return __longlong_as_double(((long long)hi[0] << 32) | (unsigned int)lo[0]);
-}
-template <int J>
-__device__ __forceinline__ void t16_pivot2(double (&row)[16], int r, bool& bad, double dj) {
-    if (dj == 0.0) bad = true;
-    const double inv = rcp_nr(dj);
-    double pr[16];
-#pragma unroll
-    for (int c = 0; c < 16; c++) pr[c] = row_bcast<J>(row[c]);
-    const double m = r > J ? row[J] * inv : 0.0;  // I half: a finite leftover, times a zero pr
-    if constexpr (J + 1 < 16) {
-        row[J + 1] = __builtin_fma(-m, pr[J + 1], row[J + 1]);
-        const double dn = readlane_d(row[J + 1], J + 1);
-        __builtin_amdgcn_sched_barrier(0);
-        const double mm = row0_to_row1(m);
-#pragma unroll
-        for (int c = 0; c < 16; c++)
-            if (c != J + 1) row[c] = __builtin_fma(-mm, pr[c], row[c]);
-        t16_pivot2<J + 1>(row, r, bad, dn);
-    } else {
-        const double mm = row0_to_row1(m);
-#pragma unroll
-        for (int c = 0; c < 16; c++) row[c] = __builtin_fma(-mm, pr[c], row[c]);
-    }
-}
-
 // The diagonal tile of panel k (held by wave 0 in the transposed accumulator layout, which for
 // a symmetric tile is the tile itself): Gauss elimination of [A_kk | I] without pivoting, the
 // four 16-lane groups of wave 0 holding A columns 0-7, 8-15 and I columns 0-7, 8-15 of row
@@ -1686,27 +1649,6 @@ __device__ __forceinline__ void t16_diag(Lds& L, int k, double4_t dt, int lane) 
 #pragma unroll
     for (int u = 0; u < 4; u++) L.D[lr * 16 + lq + 4 * u] = dt[u];
     wave_sync();
-#ifdef SLAMHOT_T16_DIAG2
-    {
-        const int r = lane & 15;
-        const bool ih = (lane >> 4) & 1;
-        double row[16];
-#pragma unroll
-        for (int c = 0; c < 16; c++) row[c] = ih ? (c == r ? 1.0 : 0.0) : L.D[r * 16 + c];
-        bool bad = false;
-        t16_pivot2<0>(row, r, bad, readlane_d(row[0], 0));
-        if (bad && lane == 0) L.fail = 1;
-        if (lane < 16) {
-            double dr = row[0];
-#pragma unroll
-            for (int c = 1; c < 16; c++) dr = r == c ? row[c] : dr;
-            L.dinv[k][r] = rcp_nr(dr);
-        } else if (lane < 32) {
-#pragma unroll
-            for (int c = 0; c < 16; c++) L.M[k][c * 16 + r] = row[c];  // M_k[col][r] = L^-1[r][col]
-        }
-    }
-#else
     const int r = lane & 15, g = lane >> 4;
     double row[8];
 #pragma unroll
@@ -1729,7 +1671,6 @@ __device__ __forceinline__ void t16_diag(Lds& L, int k, double4_t dt, int lane) 
 #pragma unroll
         for (int c = 0; c < 8; c++) L.M[k][(8 * (g & 1) + c) * 16 + r] = row[c];  // M_k[col][r] = L^-1[r][col]
     }
-#endif
     wave_sync();
     if (lane < 16) {
         const int c = lane;
