@@ -568,6 +568,16 @@ __global__ void __launch_bounds__(kCtlThreads) k_iter_begin(const WinDesc* __res
     const WinDesc W = wins[blockIdx.x];
     WinCtl& C = ctl[blockIdx.x];
     if (!C.need_lin) return;
+    // thread 0: the control block and the stop sample load while the sums run
+    WinCtl c;
+    int stop = 0;
+    if (threadIdx.x == 0) {
+        c = C;
+        // SparseOptimizer::optimize: no iteration once terminate() (sparse_optimizer.cpp:376);
+        // stop_dev[seq & 1]: this step's sample of the host word (k_trial_control of the previous
+        // step wrote it; the same value this step's k_trial_control decides on)
+        stop = stop_dev[seq & 1];
+    }
     const double chi = block_sum(strided_sum(rho + W.e0, W.ne), sh);
     double m = 0;
     if (C.it == 0) {
@@ -578,24 +588,22 @@ __global__ void __launch_bounds__(kCtlThreads) k_iter_begin(const WinDesc* __res
         m = block_max(m, sh);
     }
     if (threadIdx.x == 0) {
-        C.need_lin = 0;
-        // SparseOptimizer::optimize: no iteration once terminate() (sparse_optimizer.cpp:376);
-        // stop_dev[seq & 1]: this step's sample of the host word (k_trial_control of the previous
-        // step wrote it; the same value this step's k_trial_control decides on)
-        if (stop_dev[seq & 1]) {
-            C.active = 0;
-            return;
+        c.need_lin = 0;
+        if (stop) {
+            c.active = 0;
+        } else {
+            c.cur_chi = chi;
+            c.ini_chi = chi;
+            if (c.opt == 0 && c.it == 0) c.chi2_initial = chi;
+            if (c.it == 0) {
+                c.lambda = c.user_lambda > 0 ? c.user_lambda : 1e-5 * m;
+                c.ni = 2;
+                c.nbad = 0;
+            }
+            c.qmax = 0;
+            c.need_trial = 1;
         }
-        C.cur_chi = chi;
-        C.ini_chi = chi;
-        if (C.opt == 0 && C.it == 0) C.chi2_initial = chi;
-        if (C.it == 0) {
-            C.lambda = C.user_lambda > 0 ? C.user_lambda : 1e-5 * m;
-            C.ni = 2;
-            C.nbad = 0;
-        }
-        C.qmax = 0;
-        C.need_trial = 1;
+        C = c;
     }
 }
 
@@ -1984,21 +1992,25 @@ __global__ void k_trial_error(int ne_total, const EdgeS* __restrict__ E, const W
 // Per-step counters for the host: every control block adds its window's (need_trial, active)
 // and takes a ticket; the last block publishes the totals straight into the pinned host slot
 // the host polls (no copy, no counting kernel) and rearms the tally for the next step.
+// The three counts share one 64-bit word (need bits 0-20, active 21-41, tickets 42-62), so a
+// block's contribution and its ticket are one returning atomic; the last block rearms the word
+// with a plain store (the next step's kernels start after this one ends).
+constexpr int kTallyBits = 21;
 __device__ __forceinline__ void tally_publish(int* __restrict__ tally, int need, int act, int nblocks,
                                               Counters* __restrict__ host_slot, int seq) {
-    if (need) atomicAdd(&tally[0], need);
-    if (act) atomicAdd(&tally[1], act);
-    __threadfence();
-    if (atomicAdd(&tally[2], 1) == nblocks - 1) {
-        __threadfence();
-        const int n = atomicExch(&tally[0], 0), a = atomicExch(&tally[1], 0);
-        atomicExch(&tally[2], 0);
-        volatile Counters* h = host_slot;
-        h->need_trial = n;
-        h->active = a;
+    constexpr unsigned long long field = (1ull << kTallyBits) - 1;
+    unsigned long long* word = reinterpret_cast<unsigned long long*>(tally);
+    const unsigned long long mine =
+        (unsigned long long)need | ((unsigned long long)act << kTallyBits) | (1ull << (2 * kTallyBits));
+    const unsigned long long old = atomicAdd(word, mine);
+    if ((long long)(old >> (2 * kTallyBits)) == nblocks - 1) {
+        const unsigned long long tot = old + mine;
+        *word = 0ull;
+        // need_trial and active in one store, then the sequence number the host spins on
+        *reinterpret_cast<volatile unsigned long long*>(host_slot) =
+            (tot & field) | (((tot >> kTallyBits) & field) << 32);
         __threadfence_system();
-        h->seq = seq;  // published last: the host spins on it
-        __threadfence_system();
+        reinterpret_cast<volatile Counters*>(host_slot)->seq = seq;
     }
 }
 
@@ -2031,6 +2043,14 @@ __global__ void __launch_bounds__(kCtlThreads) k_trial_control(const WinDesc* __
         }
         return;
     }
+    // thread 0 takes the control block and this step's stop sample into registers now: their
+    // loads overlap the sums instead of following them on the step's critical path
+    WinCtl c;
+    int stop = 0;
+    if (threadIdx.x == 0) {
+        c = C;
+        stop = ((volatile int*)tally)[4 + (seq & 1)];  // terminate() at the end of the trial
+    }
     double tmpChi = block_sum(strided_sum(rho + W.e0, W.ne), sh);
     const double lam = C.lambda;
     double sc = 0;
@@ -2045,60 +2065,61 @@ __global__ void __launch_bounds__(kCtlThreads) k_trial_control(const WinDesc* __
     }
     double scale = block_sum(sc, sh);
     if (threadIdx.x != 0) return;
-    const int stop = ((volatile int*)tally)[4 + (seq & 1)];  // terminate() at the end of the trial
     if (blockIdx.x == 0) atomicExch(stop_next, stop_fresh);
-    if (!C.ok2) tmpChi = __DBL_MAX__;
-    double rho_ = C.cur_chi - tmpChi;
+    if (!c.ok2) tmpChi = __DBL_MAX__;
+    double rho_ = c.cur_chi - tmpChi;
     scale += 1e-3;
     rho_ /= scale;
-    C.tmp_chi = tmpChi;
+    c.tmp_chi = tmpChi;
     if (rho_ > 0 && isfinite(tmpChi)) {
         double alpha = 1. - pow((2 * rho_ - 1), 3);
         alpha = fmin(alpha, 2. / 3.);
         const double f = fmax(1. / 3., alpha);
-        C.lambda = lam * f;
-        C.ni = 2;
-        C.cur_chi = tmpChi;
-        C.sel = 1 - C.sel;  // discardTop: the trial state becomes the estimate
+        c.lambda = lam * f;
+        c.ni = 2;
+        c.cur_chi = tmpChi;
+        c.sel = 1 - c.sel;  // discardTop: the trial state becomes the estimate
     } else {
-        C.lambda = lam * C.ni;
-        C.ni *= 2;           // pop: keep the previous estimate
+        c.lambda = lam * c.ni;
+        c.ni *= 2;           // pop: keep the previous estimate
     }
-    C.qmax++;
-    C.trials++;
-    const bool again = rho_ < 0 && C.qmax < 10 && !stop;
+    c.qmax++;
+    c.trials++;
+    const bool again = rho_ < 0 && c.qmax < 10 && !stop;
     if (again) {
-        C.need_trial = 1;
-        tally_publish(tally, 1, C.active, gridDim.x, host_slot, seq);
+        c.need_trial = 1;
+        C = c;
+        tally_publish(tally, 1, c.active, gridDim.x, host_slot, seq);
         return;
     }
-    C.need_trial = 0;
+    c.need_trial = 0;
     int result = 0;  // OK
-    if (C.qmax == 10 || rho_ == 0) {
+    if (c.qmax == 10 || rho_ == 0) {
         result = 1;  // Terminate
     } else {
-        if ((C.ini_chi - C.cur_chi) * 1e3 < C.ini_chi)
-            C.nbad++;
+        if ((c.ini_chi - c.cur_chi) * 1e3 < c.ini_chi)
+            c.nbad++;
         else
-            C.nbad = 0;
-        if (C.nbad >= 3) result = 1;
+            c.nbad = 0;
+        if (c.nbad >= 3) result = 1;
     }
-    C.iters_run[C.opt]++;
-    C.it++;
-    C.chi2_final = C.cur_chi;
-    C.active = (result == 0) && C.it < C.iters && !stop;
-    if (!C.active && C.opt == 0 && C.iters2 > 0 && !stop) {
+    c.iters_run[c.opt]++;
+    c.it++;
+    c.chi2_final = c.cur_chi;
+    c.active = (result == 0) && c.it < c.iters && !stop;
+    if (!c.active && c.opt == 0 && c.iters2 > 0 && !stop) {
         // optimize(5) is over and no stop was seen: bDoMore, initializeOptimization(0) on the same
         // graph and optimize(10) (Optimizer.cc:1931-1986), started here so the next queued step runs
         // its first iteration (a stop set meanwhile is caught by that step's k_iter_begin, so no
         // iteration of optimize(10) runs, as when the reference skips it)
-        C.opt = 1;
-        C.it = 0;
-        C.iters = C.iters2;
-        C.active = 1;
+        c.opt = 1;
+        c.it = 0;
+        c.iters = c.iters2;
+        c.active = 1;
     }
-    C.need_lin = C.active;  // the next step linearizes again
-    tally_publish(tally, 0, C.active, gridDim.x, host_slot, seq);
+    c.need_lin = c.active;  // the next step linearizes again
+    C = c;
+    tally_publish(tally, 0, c.active, gridDim.x, host_slot, seq);
 }
 
 // start of SparseOptimizer::optimize(iters) for every window
@@ -2880,6 +2901,7 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     SLAM_HIP_TRY(hipSetDevice(s->device));
     hipStream_t S = s->stream;
     const int nw = n_prob;
+    if (nw >= (1 << kTallyBits)) return SLAM_EINVAL;  // the step tally's 21-bit fields
     const Layout LY = make_layout(Z);
     if (LY.total > s->harena_cap) {
         SLAM_HIP_TRY(hipStreamSynchronize(S));
