@@ -44,4 +44,18 @@ sanitize: $(LIBDIR)/libslamhot.so
 	g++ $(SAN) -std=c++17 -Iinclude -o tests/cpp/host_driver_asan tests/cpp/host_driver.cpp -L$(LIBDIR) -lslamhot -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)'
 	g++ $(SAN) -std=c++17 -Iinclude -o tests/cpp/shim_driver_asan tests/cpp/shim_driver.cpp -L$(LIBDIR) -lslamhot -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)'
 
-.PHONY: all oracle clean sanitize
+# the library's C++ host side under ASan + UBSan (GPU code not instrumented; clang's runtime, which
+# the clang++-built drivers load first, so no preload is needed): tools/ab/asan_gpu.sh runs the
+# C++ host-layer and shim GPU tests through them
+CLANGRT := $(dir $(firstword $(wildcard /opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so)))
+HIPSAN := --offload-arch=gfx950 -O1 -g -std=c++17 -fPIC -ffp-contract=off \
+          -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined
+sanitize-hip:
+	@mkdir -p build/asan $(LIBDIR)/asan
+	for f in $(SRCS); do $(HIPCC) $(HIPSAN) -c -o build/asan/$$(basename $$f .hip).o $$f || exit 1; done
+	$(HIPCC) $(HIPSAN) -shared -shared-libasan -o $(LIBDIR)/asan/libslamhot.so build/asan/*.o -Wl,-rpath,$(CLANGRT)
+	for d in host_driver shim_driver; do /opt/rocm/lib/llvm/bin/clang++ -std=c++17 -O1 -g -fno-omit-frame-pointer \
+	  -fsanitize=address,undefined -shared-libasan -Iinclude -o tests/cpp/$${d}_casan tests/cpp/$$d.cpp \
+	  -L$(LIBDIR)/asan -lslamhot -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)/asan' -Wl,-rpath,$(CLANGRT) || exit 1; done
+
+.PHONY: all oracle clean sanitize sanitize-hip
