@@ -191,7 +191,7 @@ def main():
     ap.add_argument("--legs", default="headline,extract,lba,pose,track,localmap,projection",
                     help="comma list of legs to run (headline = configs[2] extract+match)")
     ap.add_argument("--pairs", type=int, default=128, help="headline: stereo frames per GPU per step")
-    ap.add_argument("--inflight", type=int, default=3, help="batches in flight (handles / streams) per leg")
+    ap.add_argument("--inflight", type=int, default=4, help="batches in flight (handles / streams) per leg (3 / 4 / 5: headline 103.0k / 105.6k / 95.8k, profiles/r04h_inflight.txt)")
     ap.add_argument("--batch", type=int, default=256, help="extract leg: frames per GPU per step")
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
