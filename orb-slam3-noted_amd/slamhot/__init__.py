@@ -863,6 +863,28 @@ class PoseOptimizer:
         res = [pose_result_dict(rs[i], keep[i][2]) for i in range(len(fs))]
         return res[0] if single else res
 
+    def prepare(self, frames):
+        """Marshal `frames` into the C structs once, as a C++ Tracking caller holds them: returns
+        run() doing only the slamhot_pose_optimization call (host buffers in and out), with
+        run.results() -> the result dicts of the last run."""
+        fs = list(frames)
+        pfs = (PoseFrame * len(fs))()
+        rs = (PoseResult * len(fs))()
+        keep = []
+        for i, f in enumerate(fs):
+            pf, r, out = make_pose_frame(f)
+            pfs[i] = pf
+            rs[i] = r
+            keep.append((pf, r, out))
+        h = self._h
+
+        def run():
+            check(lib().slamhot_pose_optimization(h, len(fs), pfs, rs), "pose_optimization")
+
+        run.results = lambda: [pose_result_dict(rs[i], keep[i][2]) for i in range(len(fs))]
+        run._keep = (pfs, rs, keep)
+        return run
+
 
 # ------------------------------------------------------------------ stereo matching
 class StereoMatcher:

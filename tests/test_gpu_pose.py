@@ -50,3 +50,14 @@ def test_pose_batch_and_small_frames(popt):
 def test_pose_large_initial_error(popt):
     f = synth.pose_frame(20, rot_deg=5.0, trans_m=0.3, outlier_frac=0.3)
     _check(popt.solve(f), ob.pose_optimization(f))
+
+
+def test_pose_prepared_run_repeats(popt):
+    """prepare(): the bench's C call on pre-marshalled frames gives solve()'s results, call after call."""
+    frames = [synth.pose_frame(30 + i, stereo_frac=0.5 * (i % 2)) for i in range(5)]
+    run = popt.prepare(frames)
+    for _ in range(2):
+        run()
+        for f, g, s in zip(frames, run.results(), popt.solve(frames)):
+            assert np.array_equal(g["Tcw"], s["Tcw"]) and np.array_equal(g["outlier"], s["outlier"])
+            _check(g, ob.pose_optimization(f))
