@@ -212,6 +212,8 @@ def main():
                     help="projection leg: frames per batched SearchByProjection(F, LastFrame) call")
     ap.add_argument("--track-seqs", type=int, default=64, help="track leg: sequences per GPU (lock-step)")
     ap.add_argument("--track-frames", type=int, default=56, help="track leg: steps (frames per sequence)")
+    ap.add_argument("--track-inflight", type=int, default=1,
+                    help="track leg: tracker handles the sequences are split over (each its own stream)")
     args = ap.parse_args()
     legs = set(x.strip() for x in args.legs.split(",") if x.strip())
 
@@ -1069,17 +1071,27 @@ def track_leg(ctx):
         d_l.append(torch.from_numpy(np.ascontiguousarray(raw_l[idx])).to(device))
         d_r.append(torch.from_numpy(np.ascontiguousarray(raw_r[idx])).to(device))
     order = pingpong(SEQ_LEN, K)
-    warm = slamhot.Tracker(voc, S, cam, maps=maps, device=lr)
+    # the S sequences split over G tracker handles (each its own stream; sequences are
+    # independent, so the split changes no result), stepped in turn from this thread
+    G = max(1, min(args.track_inflight, S))
+    sizes = [S // G + (1 if g < S % G else 0) for g in range(G)]
+    offs = [sum(sizes[:g]) * W * H for g in range(G)]
+
+    def step_all(Ts, f):
+        for g, Tg in enumerate(Ts):
+            Tg.step_device(d_l[f].data_ptr() + offs[g], d_r[f].data_ptr() + offs[g])
+
+    warm = [slamhot.Tracker(voc, n, cam, maps=maps, device=lr) for n in sizes]
     for f in order[: min(K, 2 * SEQ_LEN)]:
-        warm.step_device(d_l[f].data_ptr(), d_r[f].data_ptr())
-    warm.records()
-    warm.close()
-    T = slamhot.Tracker(voc, S, cam, maps=maps, device=lr)
+        step_all(warm, f)
+    for w_ in warm:
+        w_.records()
+        w_.close()
+    Ts = [slamhot.Tracker(voc, n, cam, maps=maps, device=lr) for n in sizes]
     recs = []
 
     def step(k):
-        f = order[k]
-        T.step_device(d_l[f].data_ptr(), d_r[f].data_ptr())
+        step_all(Ts, order[k])
 
     elapsed = timed_region(dist, device, step, K)
     # a second pass for the per-step records (same inputs, fresh tracker): lost / keyframe counts,
@@ -1090,7 +1102,8 @@ def track_leg(ctx):
         T2.step_device(d_l[f].data_ptr(), d_r[f].data_ptr())
         recs.append(T2.records())
     T2.close()
-    T.close()
+    for Tg in Ts:
+        Tg.close()
     # configs[4] literally: ONE sequence on the GPU (its frame latency bounds a live camera)
     T1 = slamhot.Tracker(voc, 1, cam, maps=maps, device=lr)
     for k in range(min(K, 4)):
@@ -1121,7 +1134,7 @@ def track_leg(ctx):
                                f"EuRoC calibration): remap x2, ORBextractor x2 (1200), ComputeStereoMatches, ComputeBoW + "
                                f"SearchByBoW vs reference KF, PoseOptimization, SearchLocalPoints, PoseOptimization, "
                                f"NeedNewKeyFrame / CreateNewKeyFrame — all device-resident",
-                   "parallelism": f"sequence-sharded x{ctx['world']}"},
+                   "parallelism": f"sequence-sharded x{ctx['world']}", "tracker_handles": G},
         "ms_per_step": round(el / K * 1e3, 3),
         "per_sequence_frames_per_s": round(K / el, 1),
         "single_sequence": {"frames_per_s": round(K / el1, 1), "ms_per_frame": round(el1 / K * 1e3, 3),
