@@ -48,6 +48,11 @@ constexpr int kCtlThreads = 1024;
 constexpr int kT16Max = 18;                                  // tile rows (n <= 288)
 constexpr int kT16Waves = 16;
 constexpr int kT16Tiles = kT16Max * (kT16Max + 1) / 2;
+#ifndef T16_SPARE_TILES
+#define T16_SPARE_TILES 48
+#endif
+// panels with at most this many trailing tiles leave wave 0's SIMD to wave 0 (k_ldlt_t16)
+constexpr int kT16SpareTiles = T16_SPARE_TILES;
 constexpr int kPStride = 17;                                 // panel row stride (doubles): odd, no bank conflicts
 
 typedef double double4_t __attribute__((ext_vector_type(4)));
@@ -1784,13 +1789,19 @@ __global__ void __launch_bounds__(kT16Waves * 64) k_ldlt_t16(const WinDesc* __re
                 t16_diag(L, k + 1, dn, lane);
                 __builtin_amdgcn_s_setprio(0);
                 T16_MARK(7);
-            } else {
+            } else if (!(ntiles - t0 - 1 <= kT16SpareTiles && (wid & 3) == 0)) {
+                // Late panels (few trailing tiles): the three waves that share wave 0's SIMD (wave w
+                // runs on SIMD w % 4) stay off the MFMA pipe while wave 0 updates and factors the
+                // next diagonal tile; the other twelve take the tiles.
+                const bool spare = ntiles - t0 - 1 <= kT16SpareTiles;
+                const int nwk = spare ? kT16Waves - kT16Waves / 4 : kT16Waves - 1;
+                const int widx = spare ? wid - (wid >> 2) - 1 : wid - 1;
                 // one tile ahead: deeper prefetch (2-4 tiles in flight) measured slower, 114 -> 116-118 us
                 // in mb_ldlt and -10% on the batched LBA leg (profiles/r04e_t16_prefetch.txt)
-                int t = t0 + wid;
+                int t = t0 + 1 + widx;
                 double4_t cur = t < ntiles ? t16_load(Tw + 256 * t, lane) : double4_t{0.0, 0.0, 0.0, 0.0};
                 while (t < ntiles) {
-                    const int tn = t + kT16Waves - 1;
+                    const int tn = t + nwk;
                     const double4_t nxt = tn < ntiles ? t16_load(Tw + 256 * tn, lane) : double4_t{0.0, 0.0, 0.0, 0.0};
                     update(t, cur);
                     cur = nxt;
