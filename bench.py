@@ -126,17 +126,97 @@ def cpu_model():
 def timed_region(dist, device, fn, steps):
     """barrier + synchronize, K calls of fn(i), synchronize + barrier; seconds."""
     import torch
-    torch.cuda.synchronize(device)
+    sync = torch.cuda.synchronize if device.type == "cuda" else (lambda d: None)
+    sync(device)
     if dist:
         dist.barrier()
-    torch.cuda.synchronize(device)
+    sync(device)
     t0 = time.perf_counter()
     for i in range(steps):
         fn(i)
-    torch.cuda.synchronize(device)
+    sync(device)
     if dist:
         dist.barrier()
     return time.perf_counter() - t0
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv, timeout_s):
+    """`bench.py --gpus N` without WORLD_SIZE in the environment: start N rank processes of this
+    script (RANK = LOCAL_RANK = r, WORLD_SIZE = N, MASTER_ADDR 127.0.0.1, a free MASTER_PORT; rank r
+    drives cuda:r over nccl), relay rank 0's JSON line and return the job's exit status.  This
+    process never touches the GPU (no torch import) and never execs: the ranks are children.  A rank
+    that fails ends the job (the others are terminated, its status returned); a job still running
+    after `timeout_s` is killed (status 124)."""
+    import signal
+    import subprocess
+    import threading
+    env = dict(os.environ)
+    env.update(WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    procs = []
+    for r in range(n):
+        e = dict(env, RANK=str(r), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n))
+        procs.append(subprocess.Popen([sys.executable, "-u", str(Path(__file__).resolve())] + argv, env=e,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr, stderr=None))
+    lines = []
+
+    def relay():  # rank 0's stdout: the JSON line to our stdout, anything else to stderr
+        for raw in procs[0].stdout:
+            s = raw.decode(errors="replace")
+            if s.lstrip().startswith("{"):
+                lines.append(s)
+            else:
+                sys.stderr.write(s)
+    t = threading.Thread(target=relay, daemon=True)
+    t.start()
+
+    def stop_all():
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+        t_end = time.monotonic() + 10
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, t_end - time.monotonic()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+
+    deadline = time.monotonic() + timeout_s
+    status = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad:
+            status = bad[0] if bad[0] > 0 else 128 - bad[0]
+            sys.stderr.write(f"bench.py launcher: a rank exited with {bad[0]}; stopping the job\n")
+            stop_all()
+            break
+        if all(c == 0 for c in codes):
+            break
+        if time.monotonic() > deadline:
+            sys.stderr.write(f"bench.py launcher: job still running after {timeout_s:.0f} s; killing it\n")
+            stop_all()
+            status = 124
+            break
+        time.sleep(0.2)
+    t.join(timeout=10)
+    if status == 0:
+        if len(lines) != 1:
+            sys.stderr.write(f"bench.py launcher: rank 0 printed {len(lines)} JSON lines, expected 1\n")
+            return 1
+        sys.stdout.write(lines[0])
+        sys.stdout.flush()
+    return status
 
 
 def roofline_from_stages(stages, calls, frames_per_call, W, H, kps_per_frame):
@@ -214,24 +294,35 @@ def main():
     ap.add_argument("--track-frames", type=int, default=56, help="track leg: steps (frames per sequence)")
     ap.add_argument("--track-inflight", type=int, default=1,
                     help="track leg: tracker handles the sequences are split over (each its own stream)")
+    ap.add_argument("--launch-timeout", type=float, default=3000.0,
+                    help="--gpus N > 1 started without WORLD_SIZE: seconds before the rank processes are killed")
     args = ap.parse_args()
     legs = set(x.strip() for x in args.legs.split(",") if x.strip())
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # the driver's `python bench.py --gpus N`: one child process per GPU, before any GPU call
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], args.launch_timeout))
 
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        sys.stderr.write(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; one rank per GPU, n_gpus = {world}\n")
     dist = None
+    # `--legs dry` is the GPU-free rehearsal of the launcher and the collectives (host only, gloo)
+    dry = legs == {"dry"}
     # one GPU per rank; SLAMHOT_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share
     # cuda:(local_rank mod device_count), collectives on host copies) — the driver's runs use nccl
-    backend = os.environ.get("SLAMHOT_BENCH_BACKEND", "nccl")
+    backend = "gloo" if dry else os.environ.get("SLAMHOT_BENCH_BACKEND", "nccl")
     ndev = max(torch.cuda.device_count(), 1)
     gpu = local_rank % ndev if backend == "gloo" else local_rank
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(gpu)
+        if not dry:
+            torch.cuda.set_device(gpu)
         # the process-group libraries may print to fd 1 (gloo's "[Gloo] Rank 0 is connected ...");
         # stdout carries only the JSON line, so fd 1 points at stderr while they initialise
         sys.stdout.flush()
@@ -247,8 +338,11 @@ def main():
             sys.stdout.flush()
             os.dup2(saved, 1)
             os.close(saved)
-    device = torch.device("cuda", gpu)
-    torch.cuda.set_device(device)
+    if dry:
+        device = torch.device("cpu")
+    else:
+        device = torch.device("cuda", gpu)
+        torch.cuda.set_device(device)
     local_rank = gpu
     ctx = dict(args=args, rank=rank, world=world, local_rank=local_rank, dist=dist, device=device,
                cpu=(rank == 0 and world == 1 and not args.no_cpu_baseline))
@@ -259,6 +353,8 @@ def main():
         "ms_per_step": None, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (rendered textured-room stereo sequences / procedural frames, slamhot/synth.py)",
     }
+    if dry:
+        result.update(dry_leg(ctx))
     if "headline" in legs:
         h = headline_leg(ctx)
         for k in ("value", "ms_per_step", "config", "roofline", "cpu_baseline"):
@@ -286,6 +382,36 @@ def main():
         print(json.dumps(result), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def dry_leg(ctx):
+    """GPU-free rehearsal of the multi-rank plumbing (`--legs dry`, gloo): every rank renders its
+    shard of synthetic 320x240 frames (global frame index = rank x frames-per-rank + i) and hashes
+    them, K steps inside the same barrier-bracketed timed region, then the same max-time / unit-sum
+    reductions and digest gather as the real legs.  Nothing is measured here; it is what
+    `tests/test_bench_launch.py` runs through the `--gpus N` launcher."""
+    from slamhot import dist as sdist
+    from slamhot import synth
+    args, dist, device, rank = ctx["args"], ctx["dist"], ctx["device"], ctx["rank"]
+    n = max(1, args.pairs // 32)
+    idx = [rank * n + i for i in range(n)]
+    state = {}
+    if os.environ.get("SLAMHOT_DRY_FAIL_RANK") == str(rank):  # the launcher's failure path, under test
+        sys.stderr.write(f"dry leg: rank {rank} failing on request\n")
+        sys.exit(3)
+
+    def step(_):
+        state["dig"] = sdist.combine(sdist.unit_hash(g, synth.frame(g, 320, 240)) for g in idx)
+    step(0)
+    elapsed = timed_region(dist, device, step, args.steps)
+    el, units = sdist.reduce_run(dist, device, elapsed, float(n * args.steps))
+    digs = sdist.gather_digests(dist, device, ctx["world"], n, state["dig"])
+    return {"value": round(units / el, 2), "ms_per_step": round(el / args.steps * 1e3, 4), "dtype": "u8",
+            "data": "synthetic frames (slamhot/synth.py), host only", "scaling": "weak",
+            "config": {"workload": "dry: launcher / collective rehearsal, no GPU work", "frames_per_rank": n,
+                       "parallelism": f"frame-sharded x{ctx['world']}"},
+            "rank_digests": [d for _, d in digs],
+            "digest": {"units_per_rank": n, "job": sdist.combine(d for _, d in digs)}}
 
 
 # ------------------------------------------------------------------------------------------
