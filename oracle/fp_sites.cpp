@@ -81,3 +81,54 @@ double oracle_fp_fuse_e2(float u, float v, float kpx, float kpy, float kpr, floa
 }
 
 }  // extern "C"
+
+/* Round 5: the FP64 edge / chi2 / Huber sites of LocalBundleAdjustment and PoseOptimization as
+ * the oracle computes them (g2o_sites.hpp), for tests/test_fp64_sites.py.  q = (x, y, z, w),
+ * t = translation; matrices row-major. */
+#include "g2o_sites.hpp"
+
+namespace {
+g2o_oracle::SE3 se3_of(const double* q, const double* t) {
+    g2o_oracle::SE3 T;
+    T.r = {q[0], q[1], q[2], q[3]};
+    for (int i = 0; i < 3; i++) T.t[i] = t[i];
+    return T;
+}
+}  // namespace
+
+extern "C" {
+
+void oracle_fp64_tv(const double* q, const double* v, double* out) {
+    g2o_oracle::tv_cc({q[0], q[1], q[2], q[3]}, v, out);
+}
+void oracle_fp64_map(const double* q, const double* t, const double* X, double* out) {
+    g2o_oracle::map_cc(se3_of(q, t), X, out);
+}
+void oracle_fp64_project(const double* K, const double* X, double* uv) { g2o_oracle::project_cc(K, X, uv); }
+void oracle_fp64_neg_project_jac(const float* Kf, const double* X, double* n) { g2o_oracle::neg_project_jac_cc(Kf, X, n); }
+void oracle_fp64_rot(const double* q, double* R) { g2o_oracle::rot_cc({q[0], q[1], q[2], q[3]}, R); }
+void oracle_fp64_lin_mono(const double* q, const double* t, const double* X, const float* Kf, double* A, double* B) {
+    g2o_oracle::lin_mono_cc(se3_of(q, t), X, Kf, A, B);
+}
+void oracle_fp64_lin_pose_mono(const double* q, const double* t, const double* X, const float* Kf, double* B) {
+    g2o_oracle::lin_pose_mono_cc(se3_of(q, t), X, Kf, B);
+}
+void oracle_fp64_lin_stereo(const double* q, const double* t, const double* X, double fx, double fy, double bf,
+                            double* A, double* B) {
+    g2o_oracle::lin_stereo_cc(se3_of(q, t), X, fx, fy, bf, A, B);
+}
+void oracle_fp64_lin_pose_stereo(const double* q, const double* t, const double* X, double fx, double fy, double bf,
+                                 double* A) {
+    g2o_oracle::lin_pose_stereo_cc(se3_of(q, t), X, fx, fy, bf, A);
+}
+void oracle_fp64_cam_stereo(const double* X, double fx, double fy, double cx, double cy, float bf, double* out) {
+    g2o_oracle::cam_project_stereo_cc(X, fx, fy, cx, cy, bf, out);
+}
+void oracle_fp64_cam_pose_stereo(const double* X, double fx, double fy, double cx, double cy, double bf, double* out) {
+    g2o_oracle::cam_project_pose_stereo_cc(X, fx, fy, cx, cy, bf, out);
+}
+double oracle_fp64_chi2_2(const double* e, double info) { return g2o_oracle::chi2_2_cc(e, info); }
+double oracle_fp64_chi2_3(const double* e, double info) { return g2o_oracle::chi2_3_cc(e, info); }
+void oracle_fp64_huber(double e, double delta, float dsqr, double* rho) { g2o_oracle::huber_cc(e, delta, dsqr, rho); }
+
+}  // extern "C"

@@ -20,6 +20,7 @@
 
 #include "../include/slamhot.h"
 #include "g2o_math.hpp"
+#include "g2o_sites.hpp"
 
 namespace {
 
@@ -71,64 +72,52 @@ struct Solver {
 
     // EdgeSE3ProjectXYZ::computeError (OptimizableTypes.h:97-102) + Pinhole::project
     // (Pinhole.cpp:42-48); EdgeStereoSE3ProjectXYZ::computeError / cam_project
-    // (types_six_dof_expmap.h:157-162, types_six_dof_expmap.cpp:190-197).
+    // (types_six_dof_expmap.h:157-162, types_six_dof_expmap.cpp:190-197).  Round 5: the mapping,
+    // the stereo projection, chi2 and the Huber kernel as the reference's objects compute them
+    // (g2o_sites.hpp, tests/test_fp64_sites.py).
     void compute_error(Edge& e) {
         double Xc[3];
         if (e.body) {
             // EdgeSE3ProjectXYZToBody::computeError (OptimizableTypes.h:127-132):
             // obs - pCamera->project((mTrl * T_lw).map(X_w)), the composed SE3Quat mapping
+            // (not pinned to the objects: the inlined SE3Quat product)
             const KCam& K2 = kc2[e.kf];
             se3_map(se3_mul(trl[e.kf], pose[e.kf]), &pt[3 * e.pt], Xc);
             e.err[0] = e.obs[0] - (K2.fx * Xc[0] / Xc[2] + K2.cx);
             e.err[1] = e.obs[1] - (K2.fy * Xc[1] / Xc[2] + K2.cy);
             return;
         }
-        const double fx = kc[e.kf].fx, fy = kc[e.kf].fy, cx = kc[e.kf].cx, cy = kc[e.kf].cy, bf = kc[e.kf].bf;
-        se3_map(pose[e.kf], &pt[3 * e.pt], Xc);
+        const KCam& K = kc[e.kf];
+        map_cc(pose[e.kf], &pt[3 * e.pt], Xc);
         if (!e.stereo) {
-            const double u = fx * Xc[0] / Xc[2] + cx;
-            const double v = fy * Xc[1] / Xc[2] + cy;
-            e.err[0] = e.obs[0] - u;
-            e.err[1] = e.obs[1] - v;
+            const double Kd[4] = {K.fx, K.fy, K.cx, K.cy};
+            double uv[2];
+            project_cc(Kd, Xc, uv);
+            e.err[0] = e.obs[0] - uv[0];
+            e.err[1] = e.obs[1] - uv[1];
         } else {
-            const float invz = (float)(1.0 / Xc[2]);
-            const float bff = (float)bf;
-            const double u = Xc[0] * (double)invz * fx + cx;
-            const double v = Xc[1] * (double)invz * fy + cy;
-            const double ur = u - (double)(bff * invz);
-            e.err[0] = e.obs[0] - u;
-            e.err[1] = e.obs[1] - v;
-            e.err[2] = e.obs[2] - ur;
+            double p[3];
+            cam_project_stereo_cc(Xc, K.fx, K.fy, K.cx, K.cy, (float)K.bf, p);
+            e.err[0] = e.obs[0] - p[0];
+            e.err[1] = e.obs[1] - p[1];
+            e.err[2] = e.obs[2] - p[2];
         }
     }
 
-    // BaseEdge::chi2 (base_edge.h:58-61) with Information = invSigma2 * I
-    double chi2(const Edge& e) const {
-        double s = e.err[0] * (e.info * e.err[0]) + e.err[1] * (e.info * e.err[1]);
-        if (e.stereo) s += e.err[2] * (e.info * e.err[2]);
-        return s;
-    }
+    // BaseEdge::chi2 (base_edge.h:58-61) with Information = invSigma2 * I, as compiled
+    double chi2(const Edge& e) const { return e.stereo ? chi2_3_cc(e.err, e.info) : chi2_2_cc(e.err, e.info); }
 
-    // RobustKernelHuber::robustify (robust_kernel_impl.cpp:79-91)
+    // RobustKernelHuber::robustify (robust_kernel_impl.cpp:79-91), as compiled
     void robustify(const Edge& e, double c, double* rho) const {
-        const double delta = e.stereo ? delta_stereo : delta_mono;
-        const float dsqr = e.stereo ? dsqr_stereo : dsqr_mono;
-        if (c <= dsqr) {
-            rho[0] = c;
-            rho[1] = 1.;
-        } else {
-            const double sqrte = std::sqrt(c);
-            rho[0] = 2 * sqrte * delta - dsqr;
-            rho[1] = delta / sqrte;
-        }
+        huber_cc(c, e.stereo ? delta_stereo : delta_mono, e.stereo ? dsqr_stereo : dsqr_mono, rho);
     }
 
     bool depth_positive(const Edge& e) const {
         double Xc[3];
         if (e.body)  // OptimizableTypes.h:134-138
             se3_map(se3_mul(trl[e.kf], pose[e.kf]), &pt[3 * e.pt], Xc);
-        else
-            se3_map(pose[e.kf], &pt[3 * e.pt], Xc);
+        else  // isDepthPositive: _transformVector + t, z > 0 (Optimizer.cc.o final scan)
+            map_cc(pose[e.kf], &pt[3 * e.pt], Xc);
         return Xc[2] > 0.0;
     }
 
@@ -153,57 +142,12 @@ struct Solver {
         }
         const SE3& T = pose[e.kf];
         const double fx = kc[e.kf].fx, fy = kc[e.kf].fy, bf = kc[e.kf].bf;
-        double R[9], Xc[3];
-        se3_map(T, &pt[3 * e.pt], Xc);
-        rot_matrix(T.r, R);
-        const double x = Xc[0], y = Xc[1], z = Xc[2];
-        if (!e.stereo) {
-            // projectJac = -Jac, Jac(0,2) = -fx * x / (z*z) with fx float
-            const double pj[6] = {-(fx / z), -0.0, -((-fx) * x / (z * z)),
-                                  -0.0, -(fy / z), -((-fy) * y / (z * z))};
-            for (int r = 0; r < 2; r++)
-                for (int c = 0; c < 3; c++)
-                    e.A[3 * r + c] = pj[3 * r + 0] * R[0 + c] + pj[3 * r + 1] * R[3 + c] +
-                                     pj[3 * r + 2] * R[6 + c];
-            const double S[18] = {0.0, z, -y, 1.0, 0.0, 0.0,
-                                  -z, 0.0, x, 0.0, 1.0, 0.0,
-                                  y, -x, 0.0, 0.0, 0.0, 1.0};
-            for (int r = 0; r < 2; r++)
-                for (int c = 0; c < 6; c++)
-                    e.B[6 * r + c] = pj[3 * r + 0] * S[0 + c] + pj[3 * r + 1] * S[6 + c] +
-                                     pj[3 * r + 2] * S[12 + c];
-        } else {
-            const double z_2 = z * z;
-            double* A = e.A;
-            A[0] = -fx * R[0] / z + fx * x * R[6] / z_2;
-            A[1] = -fx * R[1] / z + fx * x * R[7] / z_2;
-            A[2] = -fx * R[2] / z + fx * x * R[8] / z_2;
-            A[3] = -fy * R[3] / z + fy * y * R[6] / z_2;
-            A[4] = -fy * R[4] / z + fy * y * R[7] / z_2;
-            A[5] = -fy * R[5] / z + fy * y * R[8] / z_2;
-            A[6] = A[0] - bf * R[6] / z_2;
-            A[7] = A[1] - bf * R[7] / z_2;
-            A[8] = A[2] - bf * R[8] / z_2;
-            double* B = e.B;
-            B[0] = x * y / z_2 * fx;
-            B[1] = -(1 + (x * x / z_2)) * fx;
-            B[2] = y / z * fx;
-            B[3] = -1. / z * fx;
-            B[4] = 0;
-            B[5] = x / z_2 * fx;
-            B[6] = (1 + y * y / z_2) * fy;
-            B[7] = -x * y / z_2 * fy;
-            B[8] = -x / z * fy;
-            B[9] = 0;
-            B[10] = -1. / z * fy;
-            B[11] = y / z_2 * fy;
-            B[12] = B[0] - bf * y / z_2;
-            B[13] = B[1] + bf * x / z_2;
-            B[14] = B[2];
-            B[15] = B[3];
-            B[16] = 0;
-            B[17] = B[5] - bf / z_2;
+        if (!e.stereo) {  // OptimizableTypes.cpp.o @0x1840, as compiled
+            const float Kf[2] = {(float)fx, (float)fy};
+            lin_mono_cc(T, &pt[3 * e.pt], Kf, e.A, e.B);
+            return;
         }
+        lin_stereo_cc(T, &pt[3 * e.pt], fx, fy, bf, e.A, e.B);  // types_six_dof_expmap.cpp.o @0xcf0
     }
 
     // EdgeSE3ProjectXYZToBody::linearizeOplus (OptimizableTypes.cpp:192-215):

@@ -15,6 +15,7 @@
 
 #include "../include/slamhot.h"
 #include "g2o_math.hpp"
+#include "g2o_sites.hpp"
 
 namespace {
 
@@ -41,41 +42,33 @@ struct PoseSolver {
     double lambda = 0, ni = 2;
     int nBad = 0;
 
+    // EdgeSE3ProjectXYZOnlyPose::computeError (OptimizableTypes.h:44-49 + Pinhole::project) and
+    // EdgeStereoSE3ProjectXYZOnlyPose::computeError / cam_project (types_six_dof_expmap.cpp:
+    // 377-386), chi2 and the Huber kernel as the reference's objects compute them (round 5,
+    // g2o_sites.hpp, tests/test_fp64_sites.py)
     void compute_error(PEdge& e) const {
         double Xc[3];
-        se3_map(est, e.Xw, Xc);
+        map_cc(est, e.Xw, Xc);
         if (!e.stereo) {
-            e.err[0] = e.obs[0] - (fx * Xc[0] / Xc[2] + cx);
-            e.err[1] = e.obs[1] - (fy * Xc[1] / Xc[2] + cy);
+            const double K[4] = {fx, fy, cx, cy};
+            double uv[2];
+            project_cc(K, Xc, uv);
+            e.err[0] = e.obs[0] - uv[0];
+            e.err[1] = e.obs[1] - uv[1];
             e.err[2] = 0;
         } else {
-            // EdgeStereoSE3ProjectXYZOnlyPose::cam_project: float invz, bf a double member
-            const float invz = (float)(1.0 / Xc[2]);
-            const double u = Xc[0] * (double)invz * fx + cx;
-            const double v = Xc[1] * (double)invz * fy + cy;
-            e.err[0] = e.obs[0] - u;
-            e.err[1] = e.obs[1] - v;
-            e.err[2] = e.obs[2] - (u - bf * (double)invz);
+            double p[3];
+            cam_project_pose_stereo_cc(Xc, fx, fy, cx, cy, bf, p);
+            e.err[0] = e.obs[0] - p[0];
+            e.err[1] = e.obs[1] - p[1];
+            e.err[2] = e.obs[2] - p[2];
         }
     }
 
-    static double chi2(const PEdge& e) {
-        double s = e.err[0] * (e.info * e.err[0]) + e.err[1] * (e.info * e.err[1]);
-        if (e.stereo) s += e.err[2] * (e.info * e.err[2]);
-        return s;
-    }
+    static double chi2(const PEdge& e) { return e.stereo ? chi2_3_cc(e.err, e.info) : chi2_2_cc(e.err, e.info); }
 
     void robustify(const PEdge& e, double c, double* rho) const {
-        const double delta = e.stereo ? delta_stereo : delta_mono;
-        const float dsqr = e.stereo ? dsqr_stereo : dsqr_mono;
-        if (c <= dsqr) {
-            rho[0] = c;
-            rho[1] = 1.;
-        } else {
-            const double sqrte = std::sqrt(c);
-            rho[0] = 2 * sqrte * delta - dsqr;
-            rho[1] = delta / sqrte;
-        }
+        huber_cc(c, e.stereo ? delta_stereo : delta_mono, e.stereo ? dsqr_stereo : dsqr_mono, rho);
     }
 
     double active_errors() {
@@ -95,37 +88,15 @@ struct PoseSolver {
         return chi;
     }
 
+    // OptimizableTypes.cpp.o @0x1630 (mono) and types_six_dof_expmap.cpp.o @0x1280 (stereo), as
+    // compiled; A row-major 3x6 (row 2 zero for mono)
     void jacobian(const PEdge& e, double* A) const {
-        double Xc[3];
-        se3_map(est, e.Xw, Xc);
-        const double x = Xc[0], y = Xc[1], z = Xc[2];
         if (!e.stereo) {
-            const double pj[6] = {-(fx / z), -0.0, -((-fx) * x / (z * z)), -0.0, -(fy / z), -((-fy) * y / (z * z))};
-            const double S[18] = {0.0, z, -y, 1.0, 0.0, 0.0, -z, 0.0, x, 0.0, 1.0, 0.0, y, -x, 0.0, 0.0, 0.0, 1.0};
-            for (int r = 0; r < 2; r++)
-                for (int c = 0; c < 6; c++)
-                    A[6 * r + c] = pj[3 * r] * S[c] + pj[3 * r + 1] * S[6 + c] + pj[3 * r + 2] * S[12 + c];
+            const float Kf[2] = {(float)fx, (float)fy};
+            lin_pose_mono_cc(est, e.Xw, Kf, A);
             for (int c = 0; c < 6; c++) A[12 + c] = 0;
         } else {
-            const double invz = 1.0 / z, invz_2 = invz * invz;
-            A[0] = x * y * invz_2 * fx;
-            A[1] = -(1 + (x * x * invz_2)) * fx;
-            A[2] = y * invz * fx;
-            A[3] = -invz * fx;
-            A[4] = 0;
-            A[5] = x * invz_2 * fx;
-            A[6] = (1 + y * y * invz_2) * fy;
-            A[7] = -x * y * invz_2 * fy;
-            A[8] = -x * invz * fy;
-            A[9] = 0;
-            A[10] = -invz * fy;
-            A[11] = y * invz_2 * fy;
-            A[12] = A[0] - bf * y * invz_2;
-            A[13] = A[1] + bf * x * invz_2;
-            A[14] = A[2];
-            A[15] = A[3];
-            A[16] = 0;
-            A[17] = A[5] - bf * invz_2;
+            lin_pose_stereo_cc(est, e.Xw, fx, fy, bf, A);
         }
     }
 

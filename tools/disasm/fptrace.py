@@ -42,8 +42,10 @@ class Node:
 
 
 class Tracer:
-    def __init__(self, obj, names):
+    def __init__(self, obj, names, packed=False):
         self.obj = obj
+        self.packed = packed    # round 5: packed-double instructions and untyped vector moves
+        self.sret_slots = {"_transformVector": 6, "cam_project": 6, "*0x50": 12} if packed else {}
         self.nodes = []
         self.memo = {}
         self.regs = {}          # xmmN -> [lane0..lane3] (lane0 of a double holds the f64 node)
@@ -136,7 +138,168 @@ class Tracer:
         if v is None:
             v = self.inp(self.where(a), ty)
             self.mem[key] = v
+        elif v.ty == "raw" and ty != "raw":
+            v = self.inp(v.name, ty)
         return v
+
+    # ---- untyped 4-byte slots (round 5: packed doubles) ----
+    # Vector moves copy memory without saying what it holds: a slot never written is read as a
+    # "raw" node named by its address, typed when an instruction consumes it (f32: the slot, f64:
+    # the slot pair whose low half it is).  A double lives in slot 2k of a register (slot 2k + 1 is
+    # its high half, None).
+    def raw(self, a):
+        key = (a[0], a[1])
+        v = self.mem.get(key)
+        if v is None:
+            v = self.mk("in", [], "raw", self.names.get(self.where(a), self.where(a)))
+            self.mem[key] = v
+        return v
+
+    def as_f64(self, lanes, k):
+        lo = lanes[2 * k]
+        if lo is None:
+            raise ValueError("f64 lane %d empty" % k)
+        if lo.ty == "raw":
+            return self.inp(lo.name, "f64")
+        if lo.ty == "f32" and lo.op == "const":  # a constant moved as f32 slots, consumed as f64
+            hi = lanes[2 * k + 1]
+            lo_b = struct.pack("<f", float(lo.name))
+            hi_b = struct.pack("<f", float(hi.name)) if hi is not None and hi.op == "const" else b"\0\0\0\0"
+            return self.const(struct.unpack("<d", lo_b + hi_b)[0], "f64")
+        if lo.ty != "f64":
+            raise ValueError("f64 use of %s" % lo.ty)
+        return lo
+
+    def sv(self, n, ty):
+        """A scalar operand of type ty (a raw slot typed on use)."""
+        if n is not None and n.ty == "raw":
+            return self.inp(n.name, ty)
+        return n
+
+    def as_f32(self, n):
+        if n is not None and n.ty == "raw":
+            return self.inp(n.name, "f32")
+        return n
+
+    def load_pd(self, s, reloc, w):
+        """w doubles from memory (or a RIP-relative constant) as register slots."""
+        a = self.addr(s, reloc)
+        lanes = [None] * 8
+        if a[0] == "const":
+            b = self.const_bytes(reloc, 8 * w)
+            for k in range(w):
+                lanes[2 * k] = self.const(struct.unpack("<d", b[8 * k:8 * k + 8])[0], "f64")
+            return lanes
+        for k in range(w):
+            v = self.mem.get((a[0], a[1] + 8 * k))
+            if v is None or v.ty == "raw":
+                v = self.inp(v.name if v is not None else self.where((a[0], a[1] + 8 * k)), "f64")
+                self.mem[(a[0], a[1] + 8 * k)] = v
+            lanes[2 * k] = v
+        return lanes
+
+    def pd_operand(self, o, reloc, w):
+        if o[:4] in ("%xmm", "%ymm", "%zmm"):
+            lanes = self.reg("xmm" + o[4:])
+            return [self.as_f64(lanes, k) if lanes[2 * k] is not None else None for k in range(w)]
+        lanes = self.load_pd(o, reloc, w)
+        return [lanes[2 * k] for k in range(w)]
+
+    def set_pd(self, d, vals):
+        lanes = [None] * 8
+        for k, v in enumerate(vals):
+            lanes[2 * k] = v
+        self.regs["xmm" + d[4:]] = lanes
+
+    def step_pd(self, ins, ops, reloc):
+        """Packed-double instructions (Eigen's vectorised 2x3 / 3x3 products).  Returns True when
+        handled."""
+        X = lambda o: o[:4] in ("%xmm", "%ymm", "%zmm")
+        wid = lambda o: 4 if o.startswith("%ymm") else 2
+        binop = {"vaddpd": "+", "vsubpd": "-", "vmulpd": "*", "vdivpd": "/"}
+        if ins in binop:
+            s2, s1, d = ops
+            w = wid(d)
+            b = self.pd_operand(s2, reloc, w)
+            a = self.pd_operand(s1, reloc, w)
+            self.set_pd(d, [self.mk(binop[ins], [x, y], "f64") if x is not None and y is not None else None
+                            for x, y in zip(a, b)])
+            return True
+        m = re.match(r"^v(fn?m)(add|sub)(132|213|231)pd$", ins)
+        if m:
+            neg, sub, form = m.group(1) == "fnm", m.group(2) == "sub", m.group(3)
+            o1, o2, d = ops
+            w = wid(d)
+            v1 = self.pd_operand(o1, reloc, w)
+            v2 = self.pd_operand(o2, reloc, w)
+            vd = self.pd_operand(d, reloc, w)
+            out = []
+            for k in range(w):
+                if form == "132":
+                    p, q, c = vd[k], v1[k], v2[k]
+                elif form == "213":
+                    p, q, c = v2[k], vd[k], v1[k]
+                else:
+                    p, q, c = v2[k], v1[k], vd[k]
+                if p is None or q is None or c is None:
+                    out.append(None)
+                    continue
+                if neg:
+                    p = self.mk("neg", [p], "f64")
+                if sub:
+                    c = self.mk("neg", [c], "f64")
+                out.append(self.mk("fma", [p, q, c], "f64"))
+            self.set_pd(d, out)
+            return True
+        if ins == "vmovddup":
+            s, d = ops
+            v = self.pd_operand(s, reloc, 1)[0] if not X(s) else self.as_f64(self.reg("xmm" + s[4:]), 0)
+            self.set_pd(d, [v, v] if wid(d) == 2 else [v, v, v, v])
+            return True
+        if ins in ("vunpckhpd", "vunpcklpd"):
+            s2, s1, d = ops
+            a = self.pd_operand(s1, reloc, 2)
+            b = self.pd_operand(s2, reloc, 2)
+            k = 1 if ins == "vunpckhpd" else 0
+            self.set_pd(d, [a[k], b[k]])
+            return True
+        if ins == "vpermilpd":
+            imm, s, d = ops
+            imm = int(imm[1:], 16)
+            w = wid(d)
+            a = self.pd_operand(s, reloc, w)
+            out = [a[(imm >> 0) & 1], a[(imm >> 1) & 1]]
+            if w == 4:
+                out += [a[2 + ((imm >> 2) & 1)], a[2 + ((imm >> 3) & 1)]]
+            self.set_pd(d, out)
+            return True
+        if ins == "vxorpd" and ops[0] != ops[1]:
+            s2, s1, d = ops
+            w = wid(d)
+            a = self.pd_operand(s1, reloc, w)
+            b = self.pd_operand(s2, reloc, w)
+            out = []
+            for x, y in zip(a, b):
+                if x is None or y is None:
+                    out.append(None)
+                    continue
+                # one operand is the sign-mask constant (-0.0: negate) or +0.0 (no-op)
+                mask, val = (x, y) if x.op == "const" else (y, x)
+                if mask.op != "const" or float(mask.name) != 0.0:
+                    raise ValueError("vxorpd without a sign-mask operand")
+                neg = struct.pack("<d", float(mask.name)) == struct.pack("<d", -0.0)
+                out.append(self.mk("neg", [val], "f64") if neg else val)
+            self.set_pd(d, out)
+            return True
+        if ins in ("vmovapd", "vmovupd") and X(ops[1]) and not X(ops[0]):
+            w = wid(ops[1])
+            self.regs["xmm" + ops[1][4:]] = self.load_pd(ops[0], reloc, w)
+            return True
+        if ins == "vmovq" and "%rip" in ops[0] and X(ops[1]):
+            b = self.const_bytes(reloc, 8)
+            self.set_pd(ops[1], [self.const(struct.unpack("<d", b)[0], "f64"), self.const(0.0, "f64")])
+            return True
+        return False
 
     def load_scalar(self, s, reloc, ty):
         a = self.addr(s, reloc)
@@ -147,6 +310,8 @@ class Tracer:
             v = self.mem.get((a[0], a[1]))
             if v is not None and v.ty == "f64":
                 return v
+            if v is not None and v.ty == "raw":
+                return self.inp(v.name, "f64")
             if v is None:
                 v = self.inp(self.where(a), "f64")
                 self.mem[(a[0], a[1])] = v
@@ -180,6 +345,8 @@ class Tracer:
         binop = {"vaddss": "+", "vsubss": "-", "vmulss": "*", "vdivss": "/",
                  "vaddsd": "+", "vsubsd": "-", "vmulsd": "*", "vdivsd": "/",
                  "vminss": "min", "vmaxss": "max", "vminsd": "min", "vmaxsd": "max"}
+        if self.packed and self.step_pd(ins, ops, reloc):
+            return
         if ins in ("vmovss", "vmovsd"):
             ty = "f32" if ins == "vmovss" else "f64"
             if len(ops) == 2 and X(ops[1]) and not X(ops[0]):
@@ -211,6 +378,8 @@ class Tracer:
                 if a[0] == "const":
                     cb = self.const_bytes(reloc, 4 * w)
                     self.regs[R(dst)] = [self.const(struct.unpack("<f", cb[4 * k:4 * k + 4])[0], "f32") for k in range(w)] + [None] * (8 - w)
+                elif self.packed:
+                    self.regs[R(dst)] = [self.raw((a[0], a[1] + 4 * k)) for k in range(w)] + [None] * (8 - w)
                 else:
                     self.regs[R(dst)] = [self.load32((a[0], a[1] + 4 * k)) for k in range(w)] + [None] * (8 - w)
             else:
@@ -277,10 +446,10 @@ class Tracer:
         if ins in binop:
             s2, s1, d = ops
             ty = "f32" if ins.endswith("ss") else "f64"
-            b = self.reg(R(s2))[0] if X(s2) else self.load_scalar(s2, reloc, ty)
+            b = self.sv(self.reg(R(s2))[0], ty) if X(s2) else self.load_scalar(s2, reloc, ty)
             a = self.reg(R(s1))
             lanes = list(a)
-            lanes[0] = self.mk(binop[ins], [a[0], b], ty)
+            lanes[0] = self.mk(binop[ins], [self.sv(a[0], ty), b], ty)
             self.regs[R(d)] = lanes
             return
         if ins in ("vsqrtss", "vsqrtsd"):
@@ -298,9 +467,9 @@ class Tracer:
             form = m.group(3)
             ty = "f32" if m.group(4) == "s" else "f64"
             o1, o2, d = ops
-            v1 = self.reg(R(o1))[0] if X(o1) else self.load_scalar(o1, reloc, ty)
-            v2 = self.reg(R(o2))[0]
-            vd = self.reg(R(d))[0]
+            v1 = self.sv(self.reg(R(o1))[0], ty) if X(o1) else self.load_scalar(o1, reloc, ty)
+            v2 = self.sv(self.reg(R(o2))[0], ty)
+            vd = self.sv(self.reg(R(d))[0], ty)
             if form == "132":  # AT&T operand order: (op1, op2, dst)
                 p, q, c = vd, v1, v2
             elif form == "213":
@@ -318,7 +487,7 @@ class Tracer:
         if ins in ("vcvtss2sd", "vcvtsd2ss"):
             s, o, d = ops
             src_ty, ty = ("f32", "f64") if ins == "vcvtss2sd" else ("f64", "f32")
-            v = self.reg(R(s))[0] if X(s) else self.load_scalar(s, reloc, src_ty)
+            v = self.sv(self.reg(R(s))[0], src_ty) if X(s) else self.load_scalar(s, reloc, src_ty)
             lanes = list(self.reg(R(o)))
             lanes[0] = self.mk("cvt", [v], ty)
             self.regs[R(d)] = lanes
@@ -424,8 +593,12 @@ class Tracer:
             # (Matx33f, Point2f); normL2Sqr only reads its rdi argument
             sret = "normL2Sqr" not in callee
             if sret and rdi and isinstance(rdi[1], int) and rdi[0] in ("rsp", "arg_rbp", "rbp"):
-                for k in range(16):
-                    self.mem[(rdi[0], rdi[1] + 4 * k)] = self.inp(f"{tag}.out[{k}]", "f32")
+                # slots the callee writes: the Eigen Vector3d / 2x3 results of the FP64 sites are
+                # smaller than 16 slots, and the caller keeps its own stack data right above them
+                nslots = next((v for k, v in self.sret_slots.items() if k in callee), 16)
+                for k in range(nslots):
+                    self.mem[(rdi[0], rdi[1] + 4 * k)] = self.mk("in", [], "raw", f"{tag}.out[{k}]") if self.packed \
+                        else self.inp(f"{tag}.out[{k}]", "f32")
             return
         if ins in ("ret", "retq"):
             self.event("ret", *(x for x in [self.regs.get("xmm0", [None])[0]] if x is not None))
@@ -475,8 +648,8 @@ class Tracer:
         return n.id
 
 
-def read_range(obj, func, start, end):
-    out = subprocess.run(["objdump", "-d", "-C", "-r", "--no-show-raw-insn", "-j", ".text",
+def read_range(obj, func, start, end, section=".text"):
+    out = subprocess.run(["objdump", "-d", "-C", "-r", "--no-show-raw-insn", "-j", section,
                           f"--start-address={start}", f"--stop-address={end}", obj],
                          capture_output=True, text=True, check=True).stdout
     res = []
@@ -498,12 +671,18 @@ def read_range(obj, func, start, end):
     return res
 
 
-def trace(obj, ranges, names=None):
-    """Walk the address ranges ["0xA:0xB", ...] of obj in order; returns the Tracer."""
-    t = Tracer(obj, names or {})
+def trace(obj, ranges, names=None, packed=False, f64_regs=()):
+    """Walk the address ranges ["0xA:0xB", ...] of obj in order; returns the Tracer.  packed=True
+    (the FP64 sites, round 5) follows packed-double instructions and types vector-moved slots on
+    use; the float sites of rounds 2-4 are traced without it, exactly as before."""
+    t = Tracer(obj, names or {}, packed)
+    for r in f64_regs:  # registers holding double arguments at entry (%xmm0 = "%xmm0" input)
+        t.regs[r] = [t.inp("%" + r, "f64")] + [None] * 7
     for r in ranges:
+        # "0xA:0xB" in .text, or "0xA:0xB@SECTION" (a COMDAT function: inline members, Eigen)
+        r, _, sec = r.partition("@")
         a, b = r.split(":")
-        t.run(read_range(obj, None, a, b))
+        t.run(read_range(obj, None, a, b, sec or ".text"))
     for k in range(32):
         lanes = t.regs.get(f"xmm{k}")
         if lanes and lanes[0] is not None and lanes[0].op not in ("in", "const"):
@@ -534,11 +713,11 @@ if __name__ == "__main__":
 def emit_c(tr: Tracer, fname: str, inputs: list[str], outputs: list[tuple[str, int]]) -> str:
     byname = {}
     for n in tr.nodes:
-        if n.op == "in":
+        if n.op == "in" and n.ty != "raw":  # a raw slot is typed on use: its typed node is the input
             byname.setdefault(n.name, n)
     sel = []
     for kind_key, idx in outputs:
-        # kind_key: "store:LOC", "cmp#K", "live:%xmmN", "ret", "int#K"
+        # kind_key: "store:LOC", "laststore:LOC", "cmp#K", "live:%xmmN", "ret", "int#K"
         found = None
         if kind_key.startswith("cmp#") or kind_key.startswith("int#"):
             kind, k = kind_key.split("#")
@@ -546,10 +725,13 @@ def emit_c(tr: Tracer, fname: str, inputs: list[str], outputs: list[tuple[str, i
             found = evs[int(k)][1][idx]
         else:
             kind, _, loc = kind_key.partition(":")
+            last = kind == "laststore"  # the final value stored at LOC (a stack slot reused)
+            kind = "store" if last else kind
             for e in tr.events:
                 if e[0] == kind and (not loc or e[2] == loc):
                     found = e[1][idx]
-                    break
+                    if not last:
+                        break
         if found is None:
             raise KeyError(kind_key)
         sel.append(found)
