@@ -168,17 +168,19 @@ __device__ inline void edge_error(const EdgeS& e, const Cam& cam, const double* 
         return;
     }
     const Intr K = left_cam(cam, e.kf);
-    se3_map(P, X, Xc);
+    map_cc(P, X, Xc);  // the compiled reference's arithmetic from here on (se3_device.hpp, round 5)
     if (e.obs[2] < 0.f) {
-        const double u = K.fx * Xc[0] / Xc[2] + K.cx;
+        const double u = K.fx * Xc[0] / Xc[2] + K.cx;  // Pinhole::project(Vector3d): no contraction
         const double v = K.fy * Xc[1] / Xc[2] + K.cy;
         err[0] = (double)e.obs[0] - u;
         err[1] = (double)e.obs[1] - v;
         err[2] = 0.0;
     } else {
+        // g2o::EdgeStereoSE3ProjectXYZ::cam_project as compiled (types_six_dof_expmap.cpp.o @0xb90)
         const float invz = (float)(1.0 / Xc[2]);
-        const double u = Xc[0] * (double)invz * K.fx + K.cx;
-        const double v = Xc[1] * (double)invz * K.fy + K.cy;
+        const double iz = (double)invz;
+        const double u = __builtin_fma(iz * Xc[0], K.fx, K.cx);
+        const double v = __builtin_fma(iz * Xc[1], K.fy, K.cy);
         const double ur = u - (double)(K.bff * invz);
         err[0] = (double)e.obs[0] - u;
         err[1] = (double)e.obs[1] - v;
@@ -186,11 +188,12 @@ __device__ inline void edge_error(const EdgeS& e, const Cam& cam, const double* 
     }
 }
 
+// BaseEdge::chi2 as compiled (Optimizer.cc.o COMDATs): the 2-D form is the plain sum, the 3-D
+// form fuses its third term
 __device__ inline double edge_chi2(const EdgeS& e, const double* err) {
     const double info = e.info;
-    double s = err[0] * (info * err[0]) + err[1] * (info * err[1]);
-    if (e.obs[2] >= 0.f) s += err[2] * (info * err[2]);
-    return s;
+    if (e.obs[2] >= 0.f) return chi2_3_cc(err, info);
+    return err[0] * (info * err[0]) + err[1] * (info * err[1]);
 }
 
 struct Huber {
@@ -199,16 +202,7 @@ struct Huber {
 };
 
 __device__ inline void robustify(const Huber& hk, bool stereo, double c, double& rho0, double& rho1) {
-    const double delta = stereo ? hk.delta_stereo : hk.delta_mono;
-    const float dsqr = stereo ? hk.dsqr_stereo : hk.dsqr_mono;
-    if (c <= dsqr) {
-        rho0 = c;
-        rho1 = 1.;
-    } else {
-        const double sqrte = sqrt(c);
-        rho0 = 2 * sqrte * delta - dsqr;
-        rho1 = delta / sqrte;
-    }
+    huber_cc(c, stereo ? hk.delta_stereo : hk.delta_mono, stereo ? hk.dsqr_stereo : hk.dsqr_mono, rho0, rho1);
 }
 
 // ---------------------------------------------------------------- iteration kernels
@@ -251,24 +245,19 @@ __device__ inline void body_jacobians(const EdgeS& e, const Cam& cam, const doub
 
 __device__ inline void edge_jacobians(bool stereo, const Intr& cam, const double* P, const double* X, double* A,
                                       double* B) {
+    // mapping, R and the mono products as the reference's objects compute them (OptimizableTypes.cpp.o
+    // @0x1840, types_six_dof_expmap.cpp.o @0xcf0; se3_device.hpp)
     double R[9], Xc[3];
-    se3_map(P, X, Xc);
-    rot_matrix(load_q(P), R);
+    map_cc(P, X, Xc);
+    rot_cc(load_q(P), R);
     const double x = Xc[0], y = Xc[1], z = Xc[2];
     if (!stereo) {
-        const double pj[6] = {-(cam.fx / z), -0.0, -((-cam.fx) * x / (z * z)),
-                              -0.0, -(cam.fy / z), -((-cam.fy) * y / (z * z))};
-#pragma unroll
-        for (int r = 0; r < 2; r++)
-#pragma unroll
-            for (int cc = 0; cc < 3; cc++)
-                A[3 * r + cc] = pj[3 * r + 0] * R[0 + cc] + pj[3 * r + 1] * R[3 + cc] + pj[3 * r + 2] * R[6 + cc];
+        // -projectJac with fx, fy the camera's floats (the edge's doubles are their exact values)
+        const double n[6] = {-(cam.fx / z), -0.0, -((double)(-(float)cam.fx) * x / (z * z)),
+                             -0.0, -(cam.fy / z), -((double)(-(float)cam.fy) * y / (z * z))};
+        mul23_cc<3>(n, R, A);
         const double S[18] = {0.0, z, -y, 1.0, 0.0, 0.0, -z, 0.0, x, 0.0, 1.0, 0.0, y, -x, 0.0, 0.0, 0.0, 1.0};
-#pragma unroll
-        for (int r = 0; r < 2; r++)
-#pragma unroll
-            for (int cc = 0; cc < 6; cc++)
-                B[6 * r + cc] = pj[3 * r + 0] * S[0 + cc] + pj[3 * r + 1] * S[6 + cc] + pj[3 * r + 2] * S[12 + cc];
+        mul23_cc<6>(n, S, B);
         A[6] = A[7] = A[8] = 0;
 #pragma unroll
         for (int cc = 0; cc < 6; cc++) B[12 + cc] = 0;
@@ -2165,7 +2154,7 @@ __device__ __forceinline__ void finalize_edge_body(int ei, int ne_total, const E
         body_pose(trl + 8 * (long long)e.kf, P, Q);
         se3_map(Q, X, Xc);
     } else {
-        se3_map(P, X, Xc);
+        map_cc(P, X, Xc);  // isDepthPositive: _transformVector + t (Optimizer.cc.o final scan)
     }
     const double ev[3] = {err[4 * (long long)ei], err[4 * (long long)ei + 1], err[4 * (long long)ei + 2]};
     const bool stereo = e.obs[2] >= 0.f;

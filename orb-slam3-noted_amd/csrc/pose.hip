@@ -36,83 +36,72 @@ struct Hub {
 
 // computeError of EdgeSE3ProjectXYZOnlyPose (OptimizableTypes.h:41-45) /
 // EdgeStereoSE3ProjectXYZOnlyPose (types_six_dof_expmap.h:218-222, .cpp:339-346: float invz,
-// bf a double member)
+// bf a double member), chi2, the Huber kernel and linearizeOplus as the reference's objects compute
+// them (round 5: lba::map_cc / chi2_3_cc / huber_cc / mul23_cc, se3_device.hpp)
 __device__ inline void perr(const PEdge& e, const double* P, const PFrame& F, double* err) {
     const double X[3] = {e.Xw[0], e.Xw[1], e.Xw[2]};
     double Xc[3];
-    lba::se3_map(P, X, Xc);
+    lba::map_cc(P, X, Xc);
     const double fx = F.fx, fy = F.fy, cx = F.cx, cy = F.cy;
     if (!is_stereo(e)) {
         err[0] = (double)e.obs[0] - (fx * Xc[0] / Xc[2] + cx);
         err[1] = (double)e.obs[1] - (fy * Xc[1] / Xc[2] + cy);
         err[2] = 0.0;
     } else {
-        const float invz = (float)(1.0 / Xc[2]);
-        const double u = Xc[0] * (double)invz * fx + cx;
-        const double v = Xc[1] * (double)invz * fy + cy;
+        // cam_project as compiled (types_six_dof_expmap.cpp.o @0xc90)
+        const double iz = (double)(float)(1.0 / Xc[2]);
+        const double u = __builtin_fma(iz * Xc[0], fx, cx);
+        const double v = __builtin_fma(iz * Xc[1], fy, cy);
         err[0] = (double)e.obs[0] - u;
         err[1] = (double)e.obs[1] - v;
-        err[2] = (double)e.obs[2] - (u - (double)F.bf * (double)invz);
+        err[2] = (double)e.obs[2] - __builtin_fma(-iz, (double)F.bf, u);
     }
 }
 
 __device__ inline double pchi2(const PEdge& e, const double* err) {
     const double info = e.info;
-    double s = err[0] * (info * err[0]) + err[1] * (info * err[1]);
-    if (is_stereo(e)) s += err[2] * (info * err[2]);
-    return s;
+    if (is_stereo(e)) return lba::chi2_3_cc(err, info);
+    return err[0] * (info * err[0]) + err[1] * (info * err[1]);
 }
 
 __device__ inline void prob(const Hub& h, bool stereo, double c, double& r0, double& r1) {
-    const double delta = stereo ? h.delta_stereo : h.delta_mono;
-    const float dsqr = stereo ? h.dsqr_stereo : h.dsqr_mono;
-    if (c <= dsqr) {
-        r0 = c;
-        r1 = 1.;
-    } else {
-        const double sqrte = sqrt(c);
-        r0 = 2 * sqrte * delta - dsqr;
-        r1 = delta / sqrte;
-    }
+    lba::huber_cc(c, stereo ? h.delta_stereo : h.delta_mono, stereo ? h.dsqr_stereo : h.dsqr_mono, r0, r1);
 }
 
-// linearizeOplus (OptimizableTypes.cpp:49-63; types_six_dof_expmap.cpp:375-404)
+// linearizeOplus (OptimizableTypes.cpp:49-63 @0x1630; types_six_dof_expmap.cpp:388-423 @0x1280)
 __device__ inline void pjac(const PEdge& e, const double* P, const PFrame& F, double* A) {
     const double X[3] = {e.Xw[0], e.Xw[1], e.Xw[2]};
     double Xc[3];
-    lba::se3_map(P, X, Xc);
+    lba::map_cc(P, X, Xc);
     const double x = Xc[0], y = Xc[1], z = Xc[2];
     const double fx = F.fx, fy = F.fy, bf = F.bf;
     if (!is_stereo(e)) {
-        const double pj[6] = {-(fx / z), -0.0, -((-fx) * x / (z * z)), -0.0, -(fy / z), -((-fy) * y / (z * z))};
+        const double n[6] = {-(fx / z), -0.0, -((double)(-(float)fx) * x / (z * z)),
+                             -0.0, -(fy / z), -((double)(-(float)fy) * y / (z * z))};
         const double S[18] = {0.0, z, -y, 1.0, 0.0, 0.0, -z, 0.0, x, 0.0, 1.0, 0.0, y, -x, 0.0, 0.0, 0.0, 1.0};
-#pragma unroll
-        for (int r = 0; r < 2; r++)
-#pragma unroll
-            for (int c = 0; c < 6; c++)
-                A[6 * r + c] = pj[3 * r] * S[c] + pj[3 * r + 1] * S[6 + c] + pj[3 * r + 2] * S[12 + c];
+        lba::mul23_cc<6>(n, S, A);
 #pragma unroll
         for (int c = 0; c < 6; c++) A[12 + c] = 0;
     } else {
         const double invz = 1.0 / z, invz_2 = invz * invz;
-        A[0] = x * y * invz_2 * fx;
-        A[1] = -(1 + (x * x * invz_2)) * fx;
+        A[0] = y * x * invz_2 * fx;
+        A[1] = -__builtin_fma(x * x, invz_2, 1.0) * fx;
         A[2] = y * invz * fx;
         A[3] = -invz * fx;
         A[4] = 0;
-        A[5] = x * invz_2 * fx;
-        A[6] = (1 + y * y * invz_2) * fy;
+        A[5] = invz_2 * x * fx;
+        A[6] = __builtin_fma(y * y, invz_2, 1.0) * fy;
         A[7] = -x * y * invz_2 * fy;
         A[8] = -x * invz * fy;
         A[9] = 0;
         A[10] = -invz * fy;
         A[11] = y * invz_2 * fy;
-        A[12] = A[0] - bf * y * invz_2;
-        A[13] = A[1] + bf * x * invz_2;
+        A[12] = __builtin_fma(-(y * bf), invz_2, A[0]);
+        A[13] = __builtin_fma(x * bf, invz_2, A[1]);
         A[14] = A[2];
         A[15] = A[3];
         A[16] = 0;
-        A[17] = A[5] - bf * invz_2;
+        A[17] = __builtin_fma(-invz_2, bf, A[5]);
     }
 }
 

@@ -102,6 +102,73 @@ __device__ inline void se3_map(const double* P, const double* X, double* out) {
     out[2] += P[6];
 }
 
+// ---- the optimizer edges' FP64 sites as the reference's objects compute them (round 5; DESIGN.md
+// §1, pinned by tests/test_fp64_sites.py through the oracle's oracle/g2o_sites.hpp).  The edge
+// bodies call Eigen's _transformVector out of line (OptimizableTypes.cpp.o COMDAT): each cross
+// product component is fma(first product, -(second)), w * uv is fused with v.
+__device__ inline void tv_cc(const Quat& q, const double* v, double* o) {
+    const double uv0 = __builtin_fma(v[2], q.y, -(v[1] * q.z));
+    const double uv1 = __builtin_fma(v[0], q.z, -(q.x * v[2]));
+    const double uv2 = __builtin_fma(q.x, v[1], -(q.y * v[0]));
+    const double u0 = uv0 + uv0, u1 = uv1 + uv1, u2 = uv2 + uv2;
+    const double c0 = __builtin_fma(q.y, u2, -(q.z * u1));
+    const double c1 = __builtin_fma(q.z, u0, -(u2 * q.x));
+    const double c2 = __builtin_fma(q.x, u1, -(q.y * u0));
+    o[0] = __builtin_fma(q.w, u0, v[0]) + c0;
+    o[1] = __builtin_fma(q.w, u1, v[1]) + c1;
+    o[2] = c2 + __builtin_fma(q.w, u2, v[2]);
+}
+
+// SE3Quat::map inside computeError / linearizeOplus / isDepthPositive: _transformVector, then + t
+__device__ inline void map_cc(const double* P, const double* X, double* o) {
+    tv_cc(load_q(P), X, o);
+    o[0] = P[4] + o[0];
+    o[1] = P[5] + o[1];
+    o[2] = o[2] + P[6];
+}
+
+// Quaternion::toRotationMatrix as inlined into the linearizeOplus bodies (row-major)
+__device__ inline void rot_cc(const Quat& q, double* R) {
+    const double tx = q.x + q.x, ty = q.y + q.y, tz = q.z + q.z;
+    const double tyy = q.y * ty, tzz = q.z * tz, txy = q.x * ty, txz = q.x * tz, tyz = q.y * tz;
+    R[0] = 1.0 - (tyy + tzz);
+    R[1] = __builtin_fma(-tz, q.w, txy);
+    R[2] = __builtin_fma(ty, q.w, txz);
+    R[3] = __builtin_fma(tz, q.w, txy);
+    R[4] = 1.0 - __builtin_fma(q.x, tx, tzz);
+    R[5] = __builtin_fma(-tx, q.w, tyz);
+    R[6] = __builtin_fma(-ty, q.w, txz);
+    R[7] = __builtin_fma(tx, q.w, tyz);
+    R[8] = 1.0 - __builtin_fma(q.x, tx, tyy);
+}
+
+// Eigen's lazy (2x3) * (3xC) product as compiled: fma(P(r,2), M(2,c), fma(P(r,1), M(1,c), P(r,0) M(0,c)))
+template <int C>
+__device__ inline void mul23_cc(const double* P, const double* M, double* out) {
+#pragma unroll
+    for (int r = 0; r < 2; r++)
+#pragma unroll
+        for (int c = 0; c < C; c++)
+            out[C * r + c] = __builtin_fma(P[3 * r + 2], M[2 * C + c], __builtin_fma(P[3 * r + 1], M[C + c], P[3 * r] * M[c]));
+}
+
+// BaseEdge<3>::chi2 with Information = I / s^2 as compiled: the third term fused
+__device__ inline double chi2_3_cc(const double* e, double info) {
+    return __builtin_fma(info * e[2], e[2], e[0] * (info * e[0]) + e[1] * (info * e[1]));
+}
+
+// RobustKernelHuber::robustify as compiled (robust_kernel_impl.cpp.o @0x350)
+__device__ inline void huber_cc(double c, double delta, float dsqr, double& rho0, double& rho1) {
+    if (c <= (double)dsqr) {
+        rho0 = c;
+        rho1 = 1.;
+    } else {
+        const double s = sqrt(c);
+        rho0 = __builtin_fma(s + s, delta, -(double)dsqr);
+        rho1 = delta / s;
+    }
+}
+
 // VertexSE3Expmap::oplusImpl: T <- exp(upd) * T (types_six_dof_expmap.h:71-74, se3quat.h:223-257,
 // including the small-angle branch R = I + W + W^2), on pose records.
 __device__ inline void se3_exp_mul(const double* upd, const double* cur, double* nxt) {
