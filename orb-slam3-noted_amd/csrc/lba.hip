@@ -48,11 +48,6 @@ constexpr int kCtlThreads = 1024;
 constexpr int kT16Max = 18;                                  // tile rows (n <= 288)
 constexpr int kT16Waves = 16;
 constexpr int kT16Tiles = kT16Max * (kT16Max + 1) / 2;
-#ifndef T16_SPARE_TILES
-#define T16_SPARE_TILES 48
-#endif
-// panels with at most this many trailing tiles leave wave 0's SIMD to wave 0 (k_ldlt_t16)
-constexpr int kT16SpareTiles = T16_SPARE_TILES;
 constexpr int kPStride = 17;                                 // panel row stride (doubles): odd, no bank conflicts
 
 typedef double double4_t __attribute__((ext_vector_type(4)));
@@ -1531,30 +1526,46 @@ __global__ void __launch_bounds__(512) k_ldlt(const WinDesc* __restrict__ wins, 
 // (i, j) is held TRANSPOSED in the v_mfma_f64_16x16x4_f64 accumulator layout (lane l, register
 // u = A_ij[l & 15][(l >> 4) + 4u]); in that form register u is directly the operand of k-step u
 // of both products below, so no tile is transposed through LDS.
-// Per 16-column panel k:
-//   (3) tiles (i, k), i > k: W_ik^T = M_k^T A_ik^T (4 MFMAs), W_ik to the LDS panel,
-//       L_ik = W_ik D^-1 back to the scratch, y_i -= L_ik D (M_k^T y_k);
+// Per 16-column panel k (round 5: no barrier per panel; the panel TRSM fused into the trailing
+// update of the previous panel):
 //   (4) tiles (i, j), i >= j > k: A_ij^T -= W_jk D^-1 W_ik^T (4 MFMAs, both operands from the
-//       panel), waves 1..15 round-robin with the next tile's load in flight, while wave 0
-//       updates the next diagonal tile and factors it (look-ahead, t16_diag: Gauss elimination
-//       of [A_kk | I], DPP row broadcasts, giving D, M_{k+1} = L^-T and z_{k+1} = D^-1 L^-1 y).
-// Then L^T x = z right-looking: x_k = M_k z_k by one wave, tile (k, j) owners subtract
-// L_kj^T x_k from z_j (DPP 16-lane sums).  A zero pivot fails the solve, like Eigen's
-// SimplicialLDLT.  The serial 16-pivot diagonal factorization is the critical path
-// (tools/microbench/mb_ldlt, mb_diag).
+//       panel buffer P[k & 1]) by the tile's owner (worker wave 1 + t mod 15, fixed for the whole
+//       factorization), its column-(k+1) tiles first and kept in registers, the others with the
+//       next tile's load in flight; meanwhile wave 0 updates the next diagonal tile (handed over
+//       through the LDS by its owner) and factors it (look-ahead, t16_diag: Gauss elimination of
+//       [A_kk | I], DPP row broadcasts, giving D, M_{k+1} = L^-T and z_{k+1} = D^-1 L^-1 y);
+//   (3) as soon as wave 0 publishes M_{k+1} (polled between trailing tiles) each owner applies
+//       the panel TRSM to its column-(k+1) tiles: W^T = M_{k+1}^T A^T (4 MFMAs) into
+//       P[(k + 1) & 1], L = W D^-1 back to the scratch, y_i -= L D (M^T y_{k+1}).
+// Hand-offs are LDS words with release / acquire (see the panel loop).  Round-4 form: two
+// barriers per panel, every wave waiting for the slowest: 113 -> 109 us at n = 288 (mb_ldlt).
+// Then L^T x = z right-looking: x_k = M_k z_k by wave 0, tile (k, j) owners subtract L_kj^T x_k
+// from z_j (DPP 16-lane sums), synchronised by LDS progress words instead of a barrier per
+// step (wave 0 waits only for the one wave that owns column k - 1).  A zero pivot fails the
+// solve, like Eigen's SimplicialLDLT.  Results are bit-identical to the round-4 form: every tile,
+// y and x sees the same operations in the same order.  (tools/microbench/mb_ldlt, mb_diag)
 struct T16Lds {
     double D[256];                         // diagonal tile of the current panel (row-major)
-    double M[kT16Max][256];                // M_k = L_kk^-T per panel (row-major)
+    double M[kT16Max][16 * kPStride];      // M_k = L_kk^-T per panel (row-major, stride 17: the
+                                           // back-solve's row-per-lane reads hit distinct banks)
     double dinv[kT16Max][16];              // 1 / d per panel
-    double P[kT16Max][16 * kPStride];      // W_ik of the current panel, row-major with stride 17
-    double NP[kT16Max][256];               // tiles (i, k + 1) as phase (4) of panel k leaves them,
-                                           // lane-major: phase (3) of panel k + 1 reads them here
+    double P[2][kT16Max][16 * kPStride];   // W_ik of panels k (read) and k + 1 (written), stride 17
+    double Dn[2][256];                     // diagonal tile (k + 2, k + 2) as panel k leaves it
+                                           // (lane-major): wave 0 reads it at panel k + 1
     double y[kT16Max * 16];                // b_s, then z, then the back-substitution right-hand side
-    double wb[16];                         // M_k^T y_k of the current panel
-    double xb[2][16];                      // x_k of the back-solve, double-buffered by parity
+    double wb[2][16];                      // M_k^T y_k, by panel parity (TRSMs of panel k read it
+                                           // while wave 0 may already form panel k + 1's)
+    double xs[kT16Max * 16];               // x_k of the back-solve, every k (no reuse: waves lag freely)
     unsigned short tij[kT16Tiles];         // tile list, column-major: (i << 8) | j
     unsigned short col0[kT16Max + 1];      // first tile of column j
     int fail;
+    int diag_ready;                        // last panel whose M / dinv / wb / z wave 0 has published
+    int tr_first;                          // last column c whose TRSM of tile (c + 1, c) is done
+    int dn_ready;                          // last panel k whose Dn[k & 1] (tile (k+2, k+2)) is in
+    int trsm_cnt[kT16Max];                 // TRSMs done per column (complete at T - c - 1)
+    int done_cnt[kT16Max];                 // worker waves done with panel k (15 = all)
+    int x_low;                             // lowest k whose x_k wave 0 has published
+    int prog[kT16Waves];                   // back-solve: last step whose updates wave w has applied
 };
 __host__ __device__ constexpr long long t16_tiles_bytes() { return (long long)kT16Tiles * 256 * sizeof(double); }
 
@@ -1671,15 +1682,15 @@ __device__ __forceinline__ void t16_diag(Lds& L, int k, double4_t dt, int lane) 
     }
     if (g >= 2) {
 #pragma unroll
-        for (int c = 0; c < 8; c++) L.M[k][(8 * (g & 1) + c) * 16 + r] = row[c];  // M_k[col][r] = L^-1[r][col]
+        for (int c = 0; c < 8; c++) L.M[k][(8 * (g & 1) + c) * kPStride + r] = row[c];  // M_k[col][r] = L^-1[r][col]
     }
     wave_sync();
     if (lane < 16) {
         const int c = lane;
         double wb = 0.0;
 #pragma unroll
-        for (int rr = 0; rr < 16; rr++) wb = __builtin_fma(L.M[k][rr * 16 + c], L.y[16 * k + rr], wb);
-        L.wb[c] = wb;
+        for (int rr = 0; rr < 16; rr++) wb = __builtin_fma(L.M[k][rr * kPStride + c], L.y[16 * k + rr], wb);
+        L.wb[k & 1][c] = wb;
         L.y[16 * k + c] = wb * L.dinv[k][c];
     }
 }
@@ -1711,147 +1722,241 @@ __global__ void __launch_bounds__(kT16Waves * 64) k_ldlt_t16(const WinDesc* __re
         L.fail = 0;
     }
     for (int c = tid; c < 16 * T; c += blockDim.x) L.y[c] = A[(long long)rhs * ld + c];
+    if (tid == 0) {
+        L.diag_ready = 0;
+        L.tr_first = -1;
+        L.dn_ready = -1;
+        L.x_low = T;
+    }
+    if (tid < kT16Waves) L.prog[tid] = T;
+    if (tid < kT16Max) L.trsm_cnt[tid] = L.done_cnt[tid] = 0;
     __syncthreads();
     T16_MARK(0);
+    // (3) of one panel tile (i, kk) held in registers (transposed accumulator layout): W^T =
+    // M_kk^T A^T into panel buffer Pb, L = W D^-1 back to the scratch tile t, y_i -= L (M^T y_kk)
+    auto trsm = [&](int kk, int i, int t, const double4_t& a, double* Pb) {
+        const double* Mk = L.M[kk];
+        const double* dkk = L.dinv[kk];
+        double4_t acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Mk[(4 * u + lq) * kPStride + lr], a[u], acc, 0, 0, 0);
+        double part = 0.0;  // sum_q L_ik[lr][q] (M_k^T y_k)[q] over this lane's q
+        double4_t l;
+        double* Pi = Pb + i * (16 * kPStride);
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int q = lq + 4 * u;
+            Pi[lr * kPStride + q] = acc[u];
+            l[u] = acc[u] * dkk[q];
+            part = __builtin_fma(l[u], L.wb[kk & 1][q], part);
+        }
+        t16_store(Tw + 256 * t, lane, l);
+        part += __shfl_xor(part, 16);
+        part += __shfl_xor(part, 32);
+        if (lq == 0) L.y[16 * i + lr] -= part;
+        // publish: P / y writes ordered before the counters (release)
+        if (lane == 0) {
+            if (i == kk + 1) __hip_atomic_store(&L.tr_first, kk, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(&L.trsm_cnt[kk], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    };
+    auto wait_at_least = [&](int* w, int v) {
+        while (__hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v) __builtin_amdgcn_s_sleep(1);
+    };
     // the tiles were written by k_schur_block (t16_put); padding by k_t16_pad
-    double4_t d0 = {0.0, 0.0, 0.0, 0.0};
-    if (wid == 0) d0 = t16_load(Tw, lane);
-    if (wid == 0) t16_diag(L, 0, d0, lane);
+    double4_t diag1 = {0.0, 0.0, 0.0, 0.0};  // wave 0: tile (1, 1), untouched before panel 0
+    if (wid == 0) {
+        t16_diag(L, 0, t16_load(Tw, lane), lane);
+        if (T >= 2) diag1 = t16_load(Tw + 256 * L.col0[1], lane);
+    }
+    __syncthreads();
+    for (int t = L.col0[0] + 1 + wid; t < L.col0[1]; t += kT16Waves) trsm(0, L.tij[t] >> 8, t, t16_load(Tw + 256 * t, lane), L.P[0][0]);
     __syncthreads();
     T16_MARK(1);
-    for (int k = 0; k < T; k++) {
-        if (L.fail) break;
-        // wave 0: the next diagonal tile (final since the previous trailing update) in flight
-        double4_t diag_next = {0.0, 0.0, 0.0, 0.0};
-        if (wid == 0 && k + 1 < T) diag_next = t16_load(Tw + 256 * L.col0[k + 1], lane);
-        const double* Mk = L.M[k];
+    // Panels without a barrier: tile t belongs to worker wave 1 + t mod 15 for the whole
+    // factorization (every update of a tile, and its TRSM, in program order on one wave); the
+    // hand-offs between waves are LDS words (release / acquire):
+    //   trsm_cnt[c]  all TRSMs of column c done -> panel c's trailing updates may read P[c & 1]
+    //   diag_ready   M_{k+1}, dinv, wb, z_{k+1} published by wave 0 -> column k+1's TRSMs
+    //   tr_first     TRSM (k+1, k) done -> wave 0 may update tile (k+1, k+1) at panel k
+    //   dn_ready     tile (k+2, k+2) as panel k leaves it, in Dn[k & 1] -> wave 0 at panel k+1
+    //   done_cnt[k]  every worker finished panel k -> P[k & 1] may be rewritten (column k+2)
+    // Wave 0 never stops early (a zero pivot only sets L.fail), so no wave waits for a flag that
+    // is never raised; the chain of waits only points at earlier panels.
+    constexpr int kNw = kT16Waves - 1;
+    for (int k = 0; k + 1 < T; k++) {
         const double* dk = L.dinv[k];
-        // (3) panel tiles (i, k), i > k
-        for (int t = L.col0[k] + 1 + wid; t < L.col0[k + 1]; t += kT16Waves) {
-            const int i = L.tij[t] >> 8;
-            const double4_t a = k == 0 ? t16_load(Tw + 256 * t, lane) : t16_load(L.NP[i], lane);
-            double4_t acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-            for (int u = 0; u < 4; u++)
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Mk[(4 * u + lq) * 16 + lr], a[u], acc, 0, 0, 0);
-            double part = 0.0;  // sum_q L_ik[lr][q] (M_k^T y_k)[q] over this lane's q
-            double4_t l;
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int q = lq + 4 * u;
-                L.P[i][lr * kPStride + q] = acc[u];
-                l[u] = acc[u] * dk[q];
-                part = __builtin_fma(l[u], L.wb[q], part);
-            }
-            t16_store(Tw + 256 * t, lane, l);
-            part += __shfl_xor(part, 16);
-            part += __shfl_xor(part, 32);
-            if (lq == 0) L.y[16 * i + lr] -= part;
-        }
-        __syncthreads();
-        T16_MARK(3);
-        // (4) trailing tiles of columns k+1 .. T-1.  Wave 0 takes the next diagonal tile first and
-        // factors it while the other waves update the rest (look-ahead); they keep the next
-        // tile's load in flight.
-        auto update = [&](int t, double4_t cur) -> double4_t {
+        const double* Pk = L.P[k & 1][0];
+        double* Pn = L.P[(k + 1) & 1][0];
+        // (4) A_ij^T -= W_jk D^-1 W_ik^T for tile t = (i, j)
+        auto update = [&](int t, const double4_t& cur) -> double4_t {
             const int i = L.tij[t] >> 8, j = L.tij[t] & 255;
             double4_t acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
             for (int u = 0; u < 4; u++) {
                 const int q = 4 * u + lq;
-                const double a = L.P[j][lr * kPStride + q] * dk[q];
-                const double b = L.P[i][lr * kPStride + q];
+                const double a = Pk[j * (16 * kPStride) + lr * kPStride + q] * dk[q];
+                const double b = Pk[i * (16 * kPStride) + lr * kPStride + q];
                 acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
             }
-            const double4_t v = cur - acc;
-            if (j == k + 1) t16_store(L.NP[i], lane, v);  // the next panel's tile: it stays in the LDS
-            else t16_store(Tw + 256 * t, lane, v);
-            return v;
+            return cur - acc;
         };
-        const int t0 = L.col0[k + 1];
-        if (k + 1 < T) {
-            if (wid == 0) {
-                T16_MARK(0);
-                __builtin_amdgcn_s_setprio(3);  // the critical path: ahead of the trailing MFMA waves
-                const double4_t dn = update(t0, diag_next);
-                T16_MARK(6);
-                t16_diag(L, k + 1, dn, lane);
-                __builtin_amdgcn_s_setprio(0);
-                T16_MARK(7);
-            } else if (!(ntiles - t0 - 1 <= kT16SpareTiles && (wid & 3) == 0)) {
-                // Late panels (few trailing tiles): the three waves that share wave 0's SIMD (wave w
-                // runs on SIMD w % 4) stay off the MFMA pipe while wave 0 updates and factors the
-                // next diagonal tile; the other twelve take the tiles.
-                const bool spare = ntiles - t0 - 1 <= kT16SpareTiles;
-                const int nwk = spare ? kT16Waves - kT16Waves / 4 : kT16Waves - 1;
-                const int widx = spare ? wid - (wid >> 2) - 1 : wid - 1;
-                // one tile ahead: deeper prefetch (2-4 tiles in flight) measured slower, 114 -> 116-118 us
-                // in mb_ldlt and -10% on the batched LBA leg (profiles/r04e_t16_prefetch.txt)
-                int t = t0 + 1 + widx;
-                double4_t cur = t < ntiles ? t16_load(Tw + 256 * t, lane) : double4_t{0.0, 0.0, 0.0, 0.0};
-                while (t < ntiles) {
-                    const int tn = t + nwk;
-                    const double4_t nxt = tn < ntiles ? t16_load(Tw + 256 * tn, lane) : double4_t{0.0, 0.0, 0.0, 0.0};
-                    update(t, cur);
-                    cur = nxt;
-                    t = tn;
-                }
+        const int t0 = L.col0[k + 1];  // the next diagonal tile (k + 1, k + 1)
+        const int c1 = L.col0[k + 2];  // end of column k + 1
+        if (wid == 0) {
+            T16_MARK(0);
+            // tile (k + 1, k + 1) as panel k - 1 left it (in the LDS, from its owner), W_{k+1,k}
+            if (k > 0) wait_at_least(&L.dn_ready, k - 1);
+            wait_at_least(&L.tr_first, k);
+            const double4_t diag_next = k == 0 ? diag1 : t16_load(L.Dn[(k - 1) & 1], lane);
+            T16_MARK(3);
+            __builtin_amdgcn_s_setprio(3);  // the critical path: ahead of the trailing MFMA waves
+            const double4_t dn = update(t0, diag_next);
+            T16_MARK(6);
+            t16_diag(L, k + 1, dn, lane);
+            __builtin_amdgcn_s_setprio(0);
+            if (lane == 0) __hip_atomic_store(&L.diag_ready, k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            T16_MARK(7);
+        } else {
+            const int widx = wid - 1;
+            // this wave's first tile at or after t: the next t' >= t with t' mod 15 == widx
+            auto first_at = [&](int t) { return t + ((widx - t % kNw) % kNw + kNw) % kNw; };
+            int ta = first_at(t0 + 1);  // column k + 1 tiles (at most two: 16 tiles, 15 waves)
+            const int tb = ta + kNw;
+            double4_t va = {0.0, 0.0, 0.0, 0.0}, vb = {0.0, 0.0, 0.0, 0.0};
+            if (ta < c1) va = t16_load(Tw + 256 * ta, lane);
+            if (tb < c1) vb = t16_load(Tw + 256 * tb, lane);
+            wait_at_least(&L.trsm_cnt[k], T - k - 1);  // W_{., k} complete in P[k & 1]
+            // column k + 1 first (held in registers): its TRSMs are on the critical path, so they
+            // run as soon as M_{k+1} is published (polled between trailing tiles) and no wave still
+            // reads P[(k + 1) & 1] for panel k - 1
+            bool pending = ta < c1;
+            if (pending) {
+                va = update(ta, va);
+                if (tb < c1) vb = update(tb, vb);
             }
+            auto ready = [&]() {
+                return __hip_atomic_load(&L.diag_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= k + 1 &&
+                       (k == 0 || __hip_atomic_load(&L.done_cnt[k - 1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= kNw);
+            };
+            auto flush = [&]() {
+                trsm(k + 1, L.tij[ta] >> 8, ta, va, Pn);
+                if (tb < c1) trsm(k + 1, L.tij[tb] >> 8, tb, vb, Pn);
+                pending = false;
+            };
+            // then columns > k + 1, one tile ahead in flight (deeper prefetch measured slower,
+            // profiles/r04e_t16_prefetch.txt)
+            int t = first_at(c1);
+            double4_t cur = t < ntiles ? t16_load(Tw + 256 * t, lane) : double4_t{0.0, 0.0, 0.0, 0.0};
+            while (t < ntiles) {
+                const int tn = t + kNw;
+                const double4_t nxt = tn < ntiles ? t16_load(Tw + 256 * tn, lane) : double4_t{0.0, 0.0, 0.0, 0.0};
+                const double4_t v = update(t, cur);
+                if (t == c1) {  // the next panel's diagonal tile: to wave 0 through the LDS
+                    t16_store(L.Dn[k & 1], lane, v);
+                    if (lane == 0) __hip_atomic_store(&L.dn_ready, k, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                } else {
+                    t16_store(Tw + 256 * t, lane, v);
+                }
+                if (pending && ready()) flush();
+                cur = nxt;
+                t = tn;
+            }
+            if (pending) {
+                wait_at_least(&L.diag_ready, k + 1);
+                if (k > 0) wait_at_least(&L.done_cnt[k - 1], kNw);
+                flush();
+            }
+            if (lane == 0) __hip_atomic_fetch_add(&L.done_cnt[k], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
-        __syncthreads();
-        T16_MARK(4);
     }
+    __syncthreads();
+    T16_MARK(4);
     if (L.fail) {
         if (tid == 0) C.ok2 = 0;
         return;
     }
-    // L^T x = z, right-looking from the last tile column, one barrier per step: wave 0 owns the
-    // tiles (k, k-1) next to the diagonal, so right after applying x_k to y_{k-1} it forms
-    // x_{k-1} = M_{k-1} y_{k-1} (every other tile of column k-1 was applied in earlier steps), while
-    // waves 1.. apply x_k to the tiles (k, j < k-1); x_k is double-buffered by parity
+    // L^T x = z, right-looking from the last tile column.  Wave 0 owns the tiles (k, k-1) next to
+    // the diagonal: at step k it applies x_k to y_{k-1} and forms x_{k-1} = M_{k-1} y_{k-1}, once
+    // the owner of column k-1 (wave 1 + (k-1) mod 15) has applied every earlier x to it; waves w >= 1
+    // apply x_k to their columns j < k-1 as soon as x_k is published.  No barrier per step, and each
+    // wave's tiles come three steps ahead through a ring of four registers sets, so the L2 latency
+    // of a tile load no longer sits in every step (round 4 loaded one step ahead and waited).
     {
         auto put_x = [&](int k) {  // wave 0: x_k from the final y_k
             if (lane < 16) {
                 const double* Mk = L.M[k];
                 double x = 0.0;
 #pragma unroll
-                for (int r = 0; r < 16; r++) x = __builtin_fma(Mk[lane * 16 + r], L.y[16 * k + r], x);
-                L.xb[k & 1][lane] = x;
+                for (int r = 0; r < 16; r++) x = __builtin_fma(Mk[lane * kPStride + r], L.y[16 * k + r], x);
+                L.xs[16 * k + lane] = x;
                 if (16 * k + lane < n) xp_out[6 * (long long)W.pose0 + 16 * k + lane] = x;
             }
         };
         auto apply = [&](const double4_t& l, int k, int j) {  // y_j -= L_kj^T x_k
-            const double xr = L.xb[k & 1][lr];
+            const double xr = L.xs[16 * k + lr];
+            double sum[4];
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const double sum = t16_sum16(l[u] * xr);
-                if (lr == 0) L.y[16 * j + lq + 4 * u] -= sum;
+            for (int u = 0; u < 4; u++) sum[u] = t16_sum16(l[u] * xr);
+            if (lr == 0) {
+#pragma unroll
+                for (int u = 0; u < 4; u++) L.y[16 * j + lq + 4 * u] -= sum[u];
             }
         };
         auto tile = [&](int k, int j) { return t16_load(Tw + 256 * (L.col0[j] + k - j), lane); };
+        auto wait_ge = [&](int* w, int v) {  // LDS word reaches v (counting down: <=)
+            while (__hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) > v) __builtin_amdgcn_s_sleep(1);
+        };
+        const int nw1 = kT16Waves - 1;
         const double4_t zero = {0.0, 0.0, 0.0, 0.0};
-        // wave 0: the (k, k-1) tile of the coming step; waves w >= 1: their first tile (k, w-1)
-        double4_t nxt = zero;
+        double4_t b0 = zero, b1 = zero, b2 = zero, b3 = zero;
         if (wid == 0) {
             put_x(T - 1);
-            if (T >= 2) nxt = tile(T - 1, T - 2);
-        } else if (wid - 1 < T - 2) {
-            nxt = tile(T - 1, wid - 1);
-        }
-        for (int k = T - 1; k >= 1; k--) {
-            __syncthreads();  // x_k and every earlier update of y visible
-            const double4_t cur = nxt;
-            if (wid == 0) {
-                if (k >= 2) nxt = tile(k - 1, k - 2);
+            if (lane == 0) __hip_atomic_store(&L.x_low, T - 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            // step k uses tile (k, k-1) and loads tile (k-3, k-4) into the set step k+1 used
+            auto step0 = [&](int k, const double4_t& cur, double4_t& ahead) {
+                if (k - 3 >= 1) ahead = tile(k - 3, k - 4);
+                // y_{k-1} final but for tile (k, k-1): its owner has applied steps > k
+                if (k + 1 <= T - 1) wait_ge(&L.prog[1 + (k - 1) % nw1], k + 1);
                 apply(cur, k, k - 1);
                 wave_sync();
                 put_x(k - 1);
-            } else {
-                if (wid - 1 < k - 2) nxt = tile(k - 1, wid - 1);
-                for (int j = wid - 1; j < k - 1; j += kT16Waves - 1) apply(j == wid - 1 ? cur : tile(k, j), k, j);
+                if (lane == 0) __hip_atomic_store(&L.x_low, k - 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            };
+            if (T - 1 >= 1) b0 = tile(T - 1, T - 2);
+            if (T - 2 >= 1) b1 = tile(T - 2, T - 3);
+            if (T - 3 >= 1) b2 = tile(T - 3, T - 4);
+            for (int k = T - 1; k >= 1; k -= 4) {
+                step0(k, b0, b3);
+                if (k - 1 >= 1) step0(k - 1, b1, b0);
+                if (k - 2 >= 1) step0(k - 2, b2, b1);
+                if (k - 3 >= 1) step0(k - 3, b3, b2);
+            }
+        } else {
+            // steps k = T-1 .. 2: columns j = wid-1, wid-1+15, ... below k-1 (the first one three
+            // steps ahead, a second one (wave 1 at n > 240) loaded on the spot)
+            const int j0 = wid - 1;
+            auto stepw = [&](int k, const double4_t& cur, double4_t& ahead) {
+                if (j0 < k - 4) ahead = tile(k - 3, j0);
+                wait_ge(&L.x_low, k);  // x_k published
+                apply(cur, k, j0);
+                for (int j = j0 + nw1; j < k - 1; j += nw1) apply(tile(k, j), k, j);
+                wave_sync();
+                if (lane == 0) __hip_atomic_store(&L.prog[wid], k, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            };
+            if (j0 < T - 2) b0 = tile(T - 1, j0);
+            if (j0 < T - 3) b1 = tile(T - 2, j0);
+            if (j0 < T - 4) b2 = tile(T - 3, j0);
+            for (int k = T - 1; k >= 2 && j0 < k - 1; k -= 4) {
+                stepw(k, b0, b3);
+                if (k - 1 >= 2 && j0 < k - 2) stepw(k - 1, b1, b0);
+                if (k - 2 >= 2 && j0 < k - 3) stepw(k - 2, b2, b1);
+                if (k - 3 >= 2 && j0 < k - 4) stepw(k - 3, b3, b2);
             }
         }
     }
+    __syncthreads();
     T16_MARK(5);
     if (tid == 0) C.ok2 = 1;
 }

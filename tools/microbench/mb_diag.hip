@@ -6,10 +6,10 @@
 
 struct DiagLds {
     double D[256];
-    double M[kT16Max][256];
+    double M[kT16Max][16 * kPStride];
     double dinv[kT16Max][16];
     double y[kT16Max * 16];
-    double wb[16];
+    double wb[2][16];
     int fail;
 };
 
@@ -25,7 +25,7 @@ __global__ void k_bench(const double* A, double* out, long long* cyc, int reps) 
         dt[0] += L.M[r & 1][lane & 15] * 1e-30;  // keep the calls dependent
     }
     const long long t1 = wall_clock64();
-    out[lane] = L.M[0][lane] + L.dinv[0][lane & 15] + L.y[lane & 15];
+    out[lane] = L.M[0][lane] + L.M[0][64 + lane] + L.M[0][128 + lane] + L.M[0][192 + lane] + L.dinv[0][lane & 15] + L.y[lane & 15];
     if (lane == 0) cyc[0] = t1 - t0;
 }
 

@@ -105,6 +105,13 @@ int main(int argc, char** argv) {
         for (int j = 0; j < n; j++) s += (j <= i ? A[(size_t)i * ld + j] : A[(size_t)j * ld + i]) * x16[j];
         r16 = std::max(r16, std::fabs(s - b[i]));
     }
+    if (argc > 3) {  // x of the tile kernel, for bit-for-bit comparisons between builds
+        FILE* f = fopen(argv[3], "wb");
+        if (f) {
+            fwrite(x16.data(), sizeof(double), n, f);
+            fclose(f);
+        }
+    }
     if (n <= 16 * kT16Max)
         printf("n=%d t16 %.1f us  residual %.3e  phases(us): diag0 %.1f panel %.1f trailing+diag %.1f backsolve %.1f [w0: update %.1f diag %.1f]\n",
                n, 1e3 * total16 / reps, r16 / (nb > 0 ? nb : 1), p16[1] / 100.0 / reps,
