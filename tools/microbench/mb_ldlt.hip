@@ -113,9 +113,9 @@ int main(int argc, char** argv) {
         }
     }
     if (n <= 16 * kT16Max)
-        printf("n=%d t16 %.1f us  residual %.3e  phases(us): diag0 %.1f panel %.1f trailing+diag %.1f backsolve %.1f [w0: update %.1f diag %.1f]\n",
+        printf("n=%d t16 %.1f us  residual %.3e  phases(us): diag0 %.1f w0-wait %.1f end-wait %.1f backsolve %.1f [w0: update %.1f diag %.1f trsm %.1f]\n",
                n, 1e3 * total16 / reps, r16 / (nb > 0 ? nb : 1), p16[1] / 100.0 / reps,
-               p16[3] / 100.0 / reps, p16[4] / 100.0 / reps, p16[5] / 100.0 / reps, p16[6] / 100.0 / reps, p16[7] / 100.0 / reps);
+               p16[3] / 100.0 / reps, p16[4] / 100.0 / reps, p16[5] / 100.0 / reps, p16[6] / 100.0 / reps, p16[7] / 100.0 / reps, p16[2] / 100.0 / reps);
     // wall_clock64 runs at 100 MHz on gfx9
     printf("n=%d ldlt %.1f us  residual %.3e  phases(us): diag %.1f [load %.1f steps %.1f] rows %.1f  trailing %.1f  "
            "backsolve %.1f\n", n, us, res / nb, (ph[1] + ph[5] + ph[6]) / 100.0 / reps, ph[5] / 100.0 / reps,
