@@ -421,7 +421,9 @@ class LocalBundleAdjuster {
    public:
     /* warm: solve one synthetic window of warm_kf x warm_pt x warm_obs at construction
      * (slamhot_lba_warmup) so the first LocalBundleAdjustment is not the one that loads kernels and
-     * allocates; the default is the config-4 window (50 KeyFrames, 2000 MapPoints, 8 observations) */
+     * allocates; the default is the config-4 window (50 KeyFrames, 2000 MapPoints, 8 observations).
+     * That costs one solve (~3 ms) per construction and can throw a warm-up error: batched users
+     * and short-lived handles pass warm = false ("LocalBundleAdjuster"). */
     explicit LocalBundleAdjuster(int device = 0, bool warm = true, int warm_kf = 50, int warm_pt = 2000,
                                  int warm_obs = 8) {
         check(slamhot_lba_create(device, &s_), "LocalBundleAdjuster");
@@ -445,7 +447,6 @@ class LocalBundleAdjuster {
         for (int i = 0; i < n; i++) wp[i] = &ws[i];
         solve(wp.data(), out.data(), n, pbStopFlag);
     }
-    /* One window (LocalMapping's call), without copying it. */
     /* One window (LocalMapping's call), without copying it.  `overlap` (optional) runs once on
      * this thread while the device works on the first LM steps (after the window has been
      * uploaded): host work of the caller that does not need the result, e.g. releasing scratch. */

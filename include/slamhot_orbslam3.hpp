@@ -565,8 +565,13 @@ void FlattenLocalWindow(const LocalWindow<KeyFrame, MapPoint>& W, Map* pMap, Loc
     std::vector<KeyFrame*> fixed(W.lFixedCameras.begin(), W.lFixedCameras.end());
     std::sort(fixed.begin(), fixed.end());
     out = LocalBAWindow{};
+    // W.observations is BuildLocalWindow's copy of every MapPoint's observations; a window filled
+    // otherwise (LocalWindow is a public struct), or whose copies were already released, reads
+    // them from the MapPoints as the reference does (:1815)
+    const bool have_obs = W.observations.size() == W.lLocalMapPoints.size();
     size_t nobs = 0;
-    for (const auto& o : W.observations) nobs += o.size();
+    if (have_obs)
+        for (const auto& o : W.observations) nobs += o.size();
     out.kf_Tcw.reserve(16 * kfs.size());
     out.pt_pos.reserve(3 * W.lLocalMapPoints.size());
     out.edge_pt.reserve(nobs);
@@ -592,10 +597,12 @@ void FlattenLocalWindow(const LocalWindow<KeyFrame, MapPoint>& W, Map* pMap, Loc
         }
     }
     int pi = 0;
+    typename LocalWindow<KeyFrame, MapPoint>::Observations fetched;
     for (MapPoint* pMP : W.lLocalMapPoints) {
         const cv::Mat P = pMP->GetWorldPos();
         for (int c = 0; c < 3; c++) out.pt_pos.push_back(P.template at<float>(c));
-        for (const auto& ob : W.observations[pi]) {
+        if (!have_obs) fetched = pMP->GetObservations();
+        for (const auto& ob : have_obs ? W.observations[pi] : fetched) {
             KeyFrame* pKFi = ob.first;
             const int vk = vertex_of(pKFi);
             if (vk < 0) continue;

@@ -2138,10 +2138,16 @@ slam_status staged_upload(int nframes, const std::vector<size_t>& off, uint8_t* 
     const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
     const int nth = std::max(1, std::min({threads, hw, nframes / 8}));
     std::vector<std::thread> th;
-    for (int t = 1; t < nth; t++)
-        th.emplace_back([&] {
-            for (int f; (f = next.fetch_add(1)) < nframes;) one(f);
-        });
+    // helper threads take frames from the shared counter, so the calling thread finishes whatever
+    // they do not: a thread that cannot be created only costs speed (the ones created are joined)
+    try {
+        th.reserve(nth);
+        for (int t = 1; t < nth; t++)
+            th.emplace_back([&] {
+                for (int f; (f = next.fetch_add(1)) < nframes;) one(f);
+            });
+    } catch (...) {
+    }
     int c = 0;
     hipError_t err = hipSuccess;
     auto flush = [&] {
@@ -2160,7 +2166,13 @@ slam_status staged_upload(int nframes, const std::vector<size_t>& off, uint8_t* 
         if (c < nchunk) std::this_thread::yield();
     }
     for (auto& x : th) x.join();
-    return err == hipSuccess ? SLAM_OK : SLAM_EHIP;
+    if (err != hipSuccess) {
+        // copies queued before the failure may still read the pinned image: let them finish
+        // before the caller (or its next call on this handle) reuses it
+        (void)hipStreamSynchronize(st);
+        return SLAM_EHIP;
+    }
+    return SLAM_OK;
 }
 
 // Batched SearchByProjection over nframes independent problems of one mode (last frame /

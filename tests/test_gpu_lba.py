@@ -193,6 +193,44 @@ def test_lba_stop_flag_mid_solve(solver):
     assert all(np.array_equal(a["kf_Tcw"], b["kf_Tcw"]) for a, b in zip(run.results(), full))
 
 
+def test_lba_stop_flag_at_optimize5_boundary_deep_ring(solver):
+    """A stop that lands on optimize(5)'s last step with more than 8 windows (the host keeps three
+    steps in flight instead of two).  The step that ends optimize(5) starts optimize(10) on the
+    device unless it has already seen the stop; the steps queued behind the hook's step before the
+    flag was mirrored (at most depth - 1 = 2) run without seeing it.  Guaranteed: at most two
+    iterations of optimize(10), every trajectory a prefix of the unstopped one, optimize(5)
+    complete; the usual case (the next step's k_trial_control sees the flag) is one at most."""
+    import ctypes as C
+    base = synth.lba_window(300, n_kf=30, n_pt=800, obs_per_pt=6, stereo_frac=0.3)  # oracle: (5, 10) iterations
+    Ws = [base] * 12  # identical windows: the batch moves in lock-step, one boundary step for all
+    flag = C.c_bool(False)
+    run = solver.prepare(Ws, stop_flag=flag)
+    run()
+    full = run.results()
+    it5 = full[0]["iterations"][0]
+    assert it5 == 5 and full[0]["iterations"][1] >= 6
+    # the last step of optimize(5): the first stop step after which optimize(5) is complete
+    kb = None
+    for k in range(0, 40):
+        flag.value = False
+        run(stop_at_step=k)
+        if run.results()[0]["iterations"][0] == it5:
+            kb = k
+            break
+    assert kb is not None and kb >= 1  # optimize(5) completes from a stop a little before its last step (queued steps)
+    for k in (kb, kb + 1):
+        flag.value = False
+        run(stop_at_step=k)
+        for f, p in zip(full, run.results()):
+            assert p["ran"] == 1 and p["iterations"][0] == it5
+            assert p["iterations"][1] <= 2 + (k - kb), (k, kb, p["iterations"])
+            assert p["iterations"][1] <= f["iterations"][1]
+            assert np.isfinite(p["kf_Tcw"]).all() and np.isfinite(p["pt_pos"]).all()
+    flag.value = False
+    run(stop_at_step=kb)
+    assert run.results()[0]["iterations"][1] <= 2
+
+
 @pytest.mark.parametrize("kw", [dict(stereo_frac=0.3), dict(body_frac=0.4, stereo_frac=0.2), dict()])
 def test_lba_camera_per_keyframe(solver, kw):
     """Every edge uses its own KeyFrame's camera (Optimizer.cc:1840, 1869-1873, 1906): a window

@@ -182,3 +182,54 @@ def test_projection_batches_empty_and_degenerate():
     (n2, f2), = m.SearchByProjection_kf_batch([fv], [kf], 10.0, 100)
     assert n1 == 0 and n2 == 0 and (f1 == -1).all() and (f2 == -1).all()
     m.close()
+
+
+@pytest.mark.parametrize("kind", ["last", "kf", "local"])
+def test_projection_batches_threaded_staging(kind):
+    """Batches large enough for the threaded staging (a frame count of at least 16 spreads the
+    pinned-image copies over up to 8 host threads: matcher.hip staged_upload), one frame above
+    kGridSortMax (4096 features: its grid is built on the host while the others' are built on the
+    device): every frame equals the single call and the oracle."""
+    import slamhot
+    nfr = 64
+    views, others, descs = [], [], []
+    for i in range(nfr):
+        S = scenes.scene(100 + i, n_feat=7000 if i == 37 else 1200)
+        fv, keep = scenes.frame_view(S)
+        views.append(fv)
+        if kind == "last":
+            lf, lkeep = scenes.last_frame(S, mono=False, motion=(0.02, 0.2)[i % 2])
+            others.append((lf, lkeep, keep))
+        elif kind == "kf":
+            kf, kkeep = scenes.kf_points(S)
+            others.append((kf, kkeep, keep))
+        else:
+            geom, desc = scenes.local_map_geom(S, n_extra=300)
+            others.append((geom, keep))
+            descs.append(desc)
+    assert views[37].n > 4096
+    if kind == "last":
+        m = slamhot.ORBmatcher(0.9, True)
+        out = m.SearchByProjection_last_batch(views, [o[0] for o in others], 7.0, False)
+        for i, (nm, fm) in enumerate(out):
+            ns, fs = m.SearchByProjection_last(views[i], others[i][0], 7.0, False)
+            no, fo = ob.search_by_projection_last(views[i], others[i][0], 0.9, True, 7.0, False)
+            assert nm == ns == no and np.array_equal(fm, fs) and np.array_equal(fm, fo), i
+    elif kind == "kf":
+        m = slamhot.ORBmatcher(0.75, True)
+        out = m.SearchByProjection_kf_batch(views, [o[0] for o in others], 10.0, 100)
+        for i, (nm, fm) in enumerate(out):
+            ns, fs = m.SearchByProjection_kf(views[i], others[i][0], 10.0, 100)
+            no, fo = ob.search_by_projection_kf(views[i], others[i][0], 0.75, True, 10.0, 100)
+            assert nm == ns == no and np.array_equal(fm, fs) and np.array_equal(fm, fo), i
+    else:
+        m = slamhot.ORBmatcher(0.8)
+        geoms = [o[0] for o in others]
+        out = m.SearchLocalPoints_batch(views, geoms, descs, 1.0, False, 20.0)
+        for i, (nm, fm, nt) in enumerate(out):
+            ns, fs, nts, _ = m.SearchLocalPoints(views[i], geoms[i], descs[i], 1.0, False, 20.0)
+            assert (nm, nt) == (ns, nts) and np.array_equal(fm, fs), i
+            nto, tro = ob.is_in_frustum(views[i], geoms[i], 0.5)
+            no, fo = ob.search_by_projection_local(views[i], tro, descs[i], 0.8, 1.0, False, 20.0)
+            assert nt == nto and nm == no and np.array_equal(fm, fo), i
+    m.close()
