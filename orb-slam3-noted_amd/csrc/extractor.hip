@@ -43,6 +43,19 @@ constexpr Pattern8 make_pattern8() {
     return p;
 }
 __constant__ Pattern8 c_pattern8 = make_pattern8();
+// the pattern's point pairs as floats (x0, y0, x1, y1) of bit i: k_orb3 loads one float4 per
+// bit and rotates with packed f32 math, no int8 unpacking per sample
+struct PatternF {
+    float4 v[256];
+};
+constexpr PatternF make_patternf() {
+    PatternF p{};
+    for (int i = 0; i < 256; i++)
+        p.v[i] = float4{(float)kPattern[4 * i], (float)kPattern[4 * i + 1], (float)kPattern[4 * i + 2],
+                        (float)kPattern[4 * i + 3]};
+    return p;
+}
+__constant__ PatternF c_patternf = make_patternf();
 
 // Device copy of the plan (uploaded once per geometry).
 struct DevLevel {
@@ -57,6 +70,15 @@ struct DevLevel {
     int xtab_off, ytab_off, xmax;
 };
 
+// k_orb3's per-level fields, 48 bytes: lane k of a wave reads level k's in three 16-byte loads
+struct OrbLv {
+    int kbase, w, h, pitch;  // first keypoint slot (INT_MAX past the last level), level geometry
+    int64_t off, fstride;    // level bytes: base (Bufs img for level 0, else pyr) + f * fstride + off
+    float scale, size;
+    int pad[2];
+};
+static_assert(sizeof(OrbLv) == 48, "three 16-byte loads");
+
 struct DevPlan {
     int nlevels, W, H;
     int ncells, slot_cap, kslots, key_slots, max_nodes;
@@ -64,6 +86,11 @@ struct DevPlan {
     int64_t pyr_frame, blur_frame;
     int umax[kHalfPatch + 1];
     DevLevel lv[kMaxLevels];
+    OrbLv orb_lv[kMaxLevels];
+    // k_orb3's IC_Angle weights (see there), per (staging shift sh, |v| (16: no row), half):
+    // [0, 5) the disc-byte masks (1 per byte inside |u| <= umax[|v|]) of the lane's five
+    // staged dwords, [5, 10) the same bytes weighted by their byte offset, [10, 12) zero
+    uint32_t ic_w[4][kHalfPatch + 2][2][12];
 };
 
 // Buffers of one batch launch (device pointers).
@@ -86,6 +113,7 @@ struct Bufs {
     const ResizeY* ytab;
     const CellDesc* cells;
     const DevPlan* plan;
+    int kslots, nlevels;       // = plan->kslots / nlevels, at hand in the kernel arguments
     int nframes, cap, lap0, lap1;
 };
 
@@ -1348,40 +1376,45 @@ static_assert(kO3RawOff % 16 == 0 && kO3WaveBytes % 16 == 0, "16-byte aligned st
 #define SLAMHOT_ORB_WPG 1
 #endif
 constexpr int kOrbWpg = SLAMHOT_ORB_WPG;  // waves (keypoints) per workgroup
-// SLAMHOT_ORB_BLURWIN (experiment): the vertical blur pass over the whole 37x37 window (a lane per
-// column, sliding over the row pairs, conflict-free), the blurred bytes column-major in LDS
-// (kO3BS bytes per column, odd dword stride), and the descriptor samples as one byte read each
-// instead of four random hp dword reads
-#ifndef SLAMHOT_ORB_BLURWIN
-#define SLAMHOT_ORB_BLURWIN 0
-#endif
-constexpr int kO3BS = 44, kO3W = 37;
-constexpr int kO3BlurBytes = SLAMHOT_ORB_BLURWIN ? ((kO3W * kO3BS + 15) & ~15) : 0;
+
+// The 7-tap Gaussian (sigma 2, CV_8U fixed point: taps sum to 256) as byte weights against the
+// staged dwords: hblur_w(o, m) = the taps of an output whose window starts at byte o, over
+// staged dword m (bytes 4m .. 4m+3); zero where the window misses the dword.
+constexpr int kHTap[7] = {18, 34, 48, 56, 48, 34, 18};
+constexpr uint32_t hblur_w(int o, int m) {
+    uint32_t w = 0;
+    for (int j = 0; j < 4; j++) {
+        const int t = 4 * m + j - o;
+        if (t >= 0 && t <= 6) w |= (uint32_t)kHTap[t] << (8 * j);
+    }
+    return w;
+}
+template <int O, int M>
+__device__ __forceinline__ uint32_t hdot(const uint32_t (&D)[4], uint32_t acc) {
+    if constexpr (hblur_w(O, M) != 0) return __builtin_amdgcn_udot4(D[M], hblur_w(O, M), acc, false);
+    else return acc;
+}
+// one staged row, 4 output columns of shift SH: h[c] sums bytes SH+c .. SH+c+6
+template <int SH>
+__device__ __forceinline__ void hrow_sh(const uint32_t* row, uint32_t* h) {
+    const uint32_t D[4] = {row[0], row[1], row[2], SH == 3 ? row[3] : 0u};
+    h[0] = hdot<SH, 2>(D, hdot<SH, 1>(D, hdot<SH, 0>(D, 0u)));
+    h[1] = hdot<SH + 1, 3>(D, hdot<SH + 1, 2>(D, hdot<SH + 1, 1>(D, hdot<SH + 1, 0>(D, 0u))));
+    h[2] = hdot<SH + 2, 3>(D, hdot<SH + 2, 2>(D, hdot<SH + 2, 1>(D, hdot<SH + 2, 0>(D, 0u))));
+    h[3] = hdot<SH + 3, 3>(D, hdot<SH + 3, 2>(D, hdot<SH + 3, 1>(D, hdot<SH + 3, 0>(D, 0u))));
+}
+static_assert(hblur_w(0, 2) == 0 && hblur_w(2, 3) == 0 && hblur_w(5, 3) == 0 && hblur_w(6, 3) == 18,
+              "dword 3 only for windows starting at byte 6; dword 2 not at byte 0");
+
 __global__ void __launch_bounds__(64 * kOrbWpg) k_orb3(Bufs b) {
-    // hp, raw and bl share one region per wave (3,520 B per wave)
-    __shared__ __attribute__((aligned(16))) uint32_t buf_all[kOrbWpg][(kO3WaveBytes + kO3BlurBytes) / 4];
+    // hp and raw share one region per wave (3,520 B per wave)
+    __shared__ __attribute__((aligned(16))) uint32_t buf_all[kOrbWpg][kO3WaveBytes / 4];
     const DevPlan& P = *b.plan;
     const int2 blk = xcd_block();
     const int f = blk.y;
     const int wave = kOrbWpg == 1 ? 0 : threadIdx.x >> 6;
     const int slot = blk.x * kOrbWpg + wave;
     const int lane = threadIdx.x & 63;
-    if (slot >= P.kslots) return;
-    int l = 0;
-    while (l + 1 < P.nlevels && slot >= P.lv[l + 1].kbase) l++;
-    const DevLevel& L = P.lv[l];
-    const int i = slot - L.kbase;
-    if (i >= b.ocnt[(size_t)f * P.nlevels + l]) return;
-    const int oi = b.oidx[(size_t)f * P.kslots + slot];
-    if (oi >= b.cap) return;
-    const uint32_t key = b.okp[(size_t)f * P.kslots + slot];
-    const int kx = kp_x(key), ky = kp_y(key);
-    const uint8_t* img = level_ptr(b, P, f, l);
-    const int pitch = level_pitch(P, l);
-    uint32_t* hp = buf_all[wave];
-    uint32_t* raw = buf_all[wave] + kO3RawOff / 4;
-    const int xs = (kx - 21) & ~3, sh = (kx - 21) - xs;
-    const int um = lane <= kHalfPatch ? P.umax[lane] : 0;  // umax[v] in lane v (read once)
 #ifdef SLAMHOT_ORB_TRACE
     long long otr[8];
     int notr = 0;
@@ -1391,11 +1424,39 @@ __global__ void __launch_bounds__(64 * kOrbWpg) k_orb3(Bufs b) {
 #define ORB_MARK() do {} while (0)
 #endif
     ORB_MARK();
+    // The prologue is a chain of dependent loads every wave waits through, kept to three steps:
+    // (1) the kernel arguments; (2) the keypoint, its output index and the levels' first slots
+    // (lane k: level k, one vector load) together, the level = the ballot of the slot against
+    // those; (3) the level's fields (scalar loads) and its keypoint count.
+    const int nlev = b.nlevels, kslots = b.kslots;
+    if (slot >= kslots) return;
+    const int oi = b.oidx[(size_t)f * kslots + slot];
+    const uint32_t key = b.okp[(size_t)f * kslots + slot];
+    const int kb = P.orb_lv[min(lane, kMaxLevels - 1)].kbase;  // INT_MAX past the last level
+    const int l = __builtin_amdgcn_readfirstlane(__popcll(__ballot(slot >= kb)) - 1);  // kbase[0] = 0
+    const OrbLv& O = P.orb_lv[l];
+    if ((slot - O.kbase >= b.ocnt[(size_t)f * nlev + l]) | (oi >= b.cap)) return;  // one branch
+    const int lw = O.w, lh = O.h, pitch = O.pitch;
+    const uint8_t* img = (l ? (const uint8_t*)b.pyr : b.img) + (size_t)f * O.fstride + O.off;
+    const int kx = kp_x(key), ky = kp_y(key);
+    uint32_t* hp = buf_all[wave];
+    uint32_t* raw = buf_all[wave] + kO3RawOff / 4;
+    const int xs = (kx - 21) & ~3, sh = (kx - 21) - xs;
+    // the orientation's weights (DevPlan::ic_w) for this lane's disc row, loaded with the window
+    const uint4* icw;
+    {
+        const int row = lane >> 1;
+        const int av = row < 2 * kHalfPatch + 1 ? abs(row - kHalfPatch) : kHalfPatch + 1;
+        icw = reinterpret_cast<const uint4*>(P.ic_w[sh][av][lane & 1]);
+    }
+    const uint4 icw0 = icw[0], icw1 = icw[1], icw2 = icw[2];
+    ORB_MARK();
+    // ---- stage the raw window    ORB_MARK();
     // ---- stage the raw window (rows ky-21..ky+21 reflected, 12 dwords per row) as three
     // 16-byte pieces per row: 129 pieces, <= 3 per lane, loaded together; pieces that leave
     // the level go byte by byte through BORDER_REFLECT_101 afterwards, one at a time
     {
-        const int wfull = (pitch & 3) ? 0 : (L.w & ~3);
+        const int wfull = (pitch & 3) ? 0 : (lw & ~3);
         uint4 v[3];
         uint32_t slow = 0;
 #pragma unroll
@@ -1406,7 +1467,7 @@ __global__ void __launch_bounds__(64 * kOrbWpg) k_orb3(Bufs b) {
                 const int r = e / 3, part = e - 3 * r;
                 const int x = xs + 16 * part;
                 if (x >= 0 && x + 16 <= wfull)
-                    v[k] = *reinterpret_cast<const uint4*>(img + (size_t)refl101(ky - 21 + r, L.h) * pitch + x);
+                    v[k] = *reinterpret_cast<const uint4*>(img + (size_t)refl101(ky - 21 + r, lh) * pitch + x);
                 else
                     slow |= 1u << k;
             }
@@ -1423,11 +1484,11 @@ __global__ void __launch_bounds__(64 * kOrbWpg) k_orb3(Bufs b) {
             if (!(slow >> k & 1)) continue;
             const int e = lane + 64 * k;
             const int r = e / 3, part = e - 3 * r;
-            const uint8_t* rowp = img + (size_t)refl101(ky - 21 + r, L.h) * pitch;
+            const uint8_t* rowp = img + (size_t)refl101(ky - 21 + r, lh) * pitch;
             const int x = xs + 16 * part;
             uint32_t w[4] = {0, 0, 0, 0};
 #pragma unroll
-            for (int q = 0; q < 16; q++) w[q >> 2] |= (uint32_t)rowp[refl101(min(x + q, L.w + 3), L.w)] << (8 * (q & 3));
+            for (int q = 0; q < 16; q++) w[q >> 2] |= (uint32_t)rowp[refl101(min(x + q, lw + 3), lw)] << (8 * (q & 3));
             *reinterpret_cast<uint4*>(raw + r * kO3RawS + 4 * part) = make_uint4(w[0], w[1], w[2], w[3]);
         }
     }
@@ -1436,35 +1497,25 @@ __global__ void __launch_bounds__(64 * kOrbWpg) k_orb3(Bufs b) {
 
     // ---- orientation (IC_Angle, ORBextractor.cc:75-102) on the raw centre 31x31
     // Lane = (disc row v, half): the row's bytes as staged dwords (row 21 + v, dwords 1..5 for
-    // half 0, 6..10 for half 1: bytes 4..39 hold every column kx-15..kx+15 for any sh), the
-    // disc's byte range |u| <= umax[|v|] as a per-dword byte mask, and two v_dot4 per dword:
-    // the row sum (weights 1) and the byte-offset moment (weights = byte offset b), so
-    // sum u I = moment - (sh + 21) sum.  Exact integers, like the reference's loops.
-    int m01 = 0, m10 = 0;
+    // half 0, 6..10 for half 1: bytes 4..43 hold every column kx-15..kx+15 for any sh) against two
+    // weight dwords each (DevPlan::ic_w, by sh, |v| and half): the disc's bytes |u| <= umax[|v|]
+    // as 1 (row sum) and as their byte offset b (moment), so sum u I = moment - (sh + 21) sum.
+    // Exact integers, like the reference's loops; row 31 (lanes 62, 63) has zero weights.
+    int m01, m10;
     {
-        const int row = lane >> 1, half = lane & 1;
-        const int v = row - kHalfPatch;
-        const int d = __shfl(um, v < 0 ? -v : v, 64);  // umax[|v|]
-        if (row < 2 * kHalfPatch + 1) {
-            const int c0 = sh + 21;                    // byte offset of column u = 0
-            const int lo = c0 - d, hi = c0 + d;        // byte range of the disc row
-            const uint32_t* rp = raw + (21 + v) * kO3RawS;
-            const int k0 = half ? 6 : 1;  // five dwords per lane (dword 10 lies past hi: masked out)
-            uint32_t s0 = 0, s1 = 0;
+        const int v = (lane >> 1) - kHalfPatch;
+        const uint32_t* rp = raw + (21 + v) * kO3RawS + ((lane & 1) ? 6 : 1);
+        const uint32_t w0[5] = {icw0.x, icw0.y, icw0.z, icw0.w, icw1.x};
+        const uint32_t w1[5] = {icw1.y, icw1.z, icw1.w, icw2.x, icw2.y};
+        uint32_t s0 = 0, s1 = 0;
 #pragma unroll
-            for (int i = 0; i < 5; i++) {
-                const int k = k0 + i;
-                const int a0 = min(max(lo - 4 * k, 0), 4), e0 = min(max(hi + 1 - 4 * k, 0), 4);
-                const uint32_t mhi = e0 >= 4 ? 0xFFFFFFFFu : ((1u << (8 * e0)) - 1u);
-                const uint32_t mlo = a0 >= 4 ? 0xFFFFFFFFu : ((1u << (8 * a0)) - 1u);
-                const uint32_t x = rp[k] & mhi & ~mlo;
-                const uint32_t wk = (uint32_t)(4 * k) * 0x01010101u + 0x03020100u;  // bytes 4k .. 4k+3
-                s0 = __builtin_amdgcn_udot4(x, 0x01010101u, s0, false);
-                s1 = __builtin_amdgcn_udot4(x, wk, s1, false);
-            }
-            m10 = (int)s1 - c0 * (int)s0;
-            m01 = v * (int)s0;
+        for (int i = 0; i < 5; i++) {
+            const uint32_t x = rp[i];
+            s0 = __builtin_amdgcn_udot4(x, w0[i], s0, false);
+            s1 = __builtin_amdgcn_udot4(x, w1[i], s1, false);
         }
+        m10 = (int)s1 - (sh + 21) * (int)s0;
+        m01 = v * (int)s0;
     }
     m10 = wave_sum_dpp(m10);
     m01 = wave_sum_dpp(m01);
@@ -1472,111 +1523,85 @@ __global__ void __launch_bounds__(64 * kOrbWpg) k_orb3(Bufs b) {
     ORB_MARK();
 
     // ---- horizontal pass: 22 row pairs x 10 groups of 4 output columns; output column c
-    // needs staged bytes sh+c .. sh+c+6 (v_alignbyte by the runtime shift, two v_dot4 per
-    // output).  Rows 2p and 2p+1 go to the low / high half of one dword (hp), so the
-    // vertical pass takes two taps per v_dot2_u32_u16.  Row 43 is never staged: its sums
-    // only reach blurred rows >= 37, which are not kept.
-    constexpr uint32_t KA = 18u | (34u << 8) | (48u << 16) | (56u << 24);
-    constexpr uint32_t KB = 48u | (34u << 8) | (18u << 16);
-    auto hrow4 = [&](const uint32_t* row, uint32_t* h) {
-        const uint32_t D0 = row[0], D1 = row[1], D2 = row[2], D3 = row[3];
-        const uint32_t E0 = __builtin_amdgcn_alignbyte(D1, D0, sh);
-        const uint32_t E1 = __builtin_amdgcn_alignbyte(D2, D1, sh);
-        const uint32_t E2 = __builtin_amdgcn_alignbyte(D3, D2, sh);
-        h[0] = __builtin_amdgcn_udot4(E1, KB, __builtin_amdgcn_udot4(E0, KA, 0u, false), false);
-        h[1] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(E2, E1, 1), KB,
-                                      __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(E1, E0, 1), KA, 0u, false), false);
-        h[2] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(E2, E1, 2), KB,
-                                      __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(E1, E0, 2), KA, 0u, false), false);
-        h[3] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(E2, E1, 3), KB,
-                                      __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(E1, E0, 3), KA, 0u, false), false);
+    // needs staged bytes sh+c .. sh+c+6.  sh is wave-uniform: one specialisation per sh, with the
+    // seven taps placed at each output's byte offset against the staged dwords (hblur_w), two or
+    // three v_dot4 per output and no data realignment.  Rows 2p and 2p+1 go to the low / high
+    // half of one dword (hp), so the vertical pass takes two taps per v_dot2_u32_u16.  Row 43 is
+    // never staged: its sums only reach blurred rows >= 37, which are not kept.
+    int hit[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) hit[k] = c_hitems.v[min(lane + 64 * k, kHItems - 1)];
+    auto hpass = [&](auto shc) {
+        constexpr int SH = decltype(shc)::value;
+#pragma unroll
+        for (int k = 0; k < 3; k++) {  // 3 passes of the wave instead of 4
+            if (lane + 64 * k >= kHItems) break;
+            const int pq = hit[k], p = pq / 10, q = pq - p * 10;
+            uint32_t h0[4], h1[4];
+            hrow_sh<SH>(raw + (2 * p) * kO3RawS + q, h0);
+            hrow_sh<SH>(raw + (2 * p + 1) * kO3RawS + q, h1);
+            *reinterpret_cast<uint4*>(&hp[p * kO3HS + 4 * q]) =
+                make_uint4(h0[0] | (h1[0] << 16), h0[1] | (h1[1] << 16), h0[2] | (h1[2] << 16), h0[3] | (h1[3] << 16));
+        }
     };
-    for (int it = lane; it < kHItems; it += 64) {  // 3 passes of the wave instead of 4
-        const int pq = c_hitems.v[it], p = pq / 10, q = pq - p * 10;
-        uint32_t h0[4], h1[4];
-        hrow4(raw + (2 * p) * kO3RawS + q, h0);
-        hrow4(raw + (2 * p + 1) * kO3RawS + q, h1);
-        *reinterpret_cast<uint4*>(&hp[p * kO3HS + 4 * q]) =
-            make_uint4(h0[0] | (h1[0] << 16), h0[1] | (h1[1] << 16), h0[2] | (h1[2] << 16), h0[3] | (h1[3] << 16));
+    switch (sh) {
+        case 0: hpass(std::integral_constant<int, 0>{}); break;
+        case 1: hpass(std::integral_constant<int, 1>{}); break;
+        case 2: hpass(std::integral_constant<int, 2>{}); break;
+        default: hpass(std::integral_constant<int, 3>{}); break;
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     ORB_MARK();
     // ---- descriptor (computeOrbDescriptor, ORBextractor.cc:106-145), with the vertical pass
-    // of the blur evaluated only at the 512 sampled pixels: blurred pixel (y, x) of the 37x37
-    // window sums hs rows y..y+6 of column x = the row pairs y>>1 .. (y>>1)+3 with taps
-    // (k0,k1)(k2,k3)(k4,k5)(k6,0) for even y and (0,k0)(k1,k2)(k3,k4)(k5,k6) for odd y (the
-    // high half of the last even-y pair is row y+7, tap 0).  acc starts at 2^15 (the rounding
-    // term); taps sum to 256, so acc >> 16 <= 255: the bits of the whole-level blur.
+    // of the blur evaluated only at the 512 sampled pixels of the 37x37 window.
     const float factor_pi = (float)(3.14159265358979323846 / 180.f);
     float sn, cs;
     glibc_sincosf(angle * factor_pi, &sn, &cs);
     const float a = cs, bb = sn;
     ORB_MARK();
-#if SLAMHOT_ORB_BLURWIN
-    uint8_t* bw = reinterpret_cast<uint8_t*>(buf_all[wave]) + kO3WaveBytes;
-    if (lane < kO3W) {  // column x = lane: blurred rows 0..36, two per row pair step
-        const uint32_t* hc = hp + lane;
-        uint32_t q0 = hc[0], q1 = hc[kO3HS], q2 = hc[2 * kO3HS];
-        uint32_t* bcol = reinterpret_cast<uint32_t*>(bw + lane * kO3BS);
-        uint32_t word = 0;
-#pragma unroll
-        for (int P = 0; P < 19; P++) {
-            const uint32_t q3 = hc[(P + 3) * kO3HS];
-            uint32_t ev = 1u << 15, od = 1u << 15;
-            ev = __builtin_amdgcn_udot2(as_us2(q0), us2{18, 34}, ev, false);
-            ev = __builtin_amdgcn_udot2(as_us2(q1), us2{48, 56}, ev, false);
-            ev = __builtin_amdgcn_udot2(as_us2(q2), us2{48, 34}, ev, false);
-            ev = __builtin_amdgcn_udot2(as_us2(q3), us2{18, 0}, ev, false);
-            od = __builtin_amdgcn_udot2(as_us2(q0), us2{0, 18}, od, false);
-            od = __builtin_amdgcn_udot2(as_us2(q1), us2{34, 48}, od, false);
-            od = __builtin_amdgcn_udot2(as_us2(q2), us2{56, 48}, od, false);
-            od = __builtin_amdgcn_udot2(as_us2(q3), us2{34, 18}, od, false);
-            // rows 2P, 2P+1 -> bytes (2P) & 3, (2P+1) & 3 of dword P >> 1
-            const uint32_t two = ((ev >> 16) & 0xFF) | (((od >> 16) & 0xFF) << 8);
-            word = (P & 1) ? (word | (two << 16)) : two;
-            if ((P & 1) || P == 18) bcol[P >> 1] = word;
-            q0 = q1;
-            q1 = q2;
-            q2 = q3;
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    auto blurred = [&](int r, int c) -> int { return bw[(c + 18) * kO3BS + (r + 18)]; };
-#else
-    auto blurred = [&](int r, int c) -> int {  // r, c: rounded offsets from the keypoint
-        const int y = r + 18;
-        const uint32_t* q = hp + (y >> 1) * kO3HS + (c + 18);
-        const bool odd = y & 1;
+    // Per pattern point: (r, c) = the rotated offset as a packed pair, rounded to nearest-even
+    // by adding 1.5 * 2^23 + 18 (cv_round's rint, shifted by the window centre 18, exact for
+    // |v| < 2^22): the sum's low bits are r + 18 and c + 18 on top of 0x4B400000.  Blurred pixel
+    // (y, x) sums hs rows y .. y+6 of column x: the row pairs y >> 1 .. (y >> 1) + 3, realigned
+    // by v_alignbit to start at row y (16 bits for odd y), then fixed taps (k0,k1)(k2,k3)(k4,k5)
+    // (k6,-).  acc starts at 2^15 (the rounding term); taps sum to 256, so acc >> 16 <= 255:
+    // the whole-level blur's byte, and (acc0 >> 16) < (acc1 >> 16) <=> acc0 < (acc1 & ~0xFFFF).
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const f2 rot_a = {a, -bb}, rot_b = {bb, a};
+    constexpr float kRound = 12582930.0f;  // 1.5 * 2^23 + 18
+    auto sample = [&](float x, float y) -> uint32_t {
+        // r = fma(x, b, y a), c = fma(x, a, -(y b)) (computeOrbDescriptor's GET_VALUE), y (-b) = -(y b)
+        const f2 yy = f2{y, y} * rot_a;
+        const f2 rc = __builtin_elementwise_fma(f2{x, x}, rot_b, yy);  // {r, c} unrounded
+        const f2 rcr = rc + f2{kRound, kRound};
+        const uint32_t rb = __float_as_uint(rcr.x), cb = __float_as_uint(rcr.y);
+        // (y >> 1) * kO3HS + x from the biased bits: v_mad_u32_u24 reads the low 24 bits of rb >> 1
+        // (0xA00000 + (y >> 1)); the constant bias is taken back out of the index
+        const uint32_t idx = __umul24(rb >> 1, kO3HS) + cb - (0xA00000u * kO3HS + 0x4B400000u);
+        const uint32_t* q = hp + idx;
+        const uint32_t q0 = q[0], q1 = q[kO3HS], q2 = q[2 * kO3HS], q3 = q[3 * kO3HS];
+        const uint32_t sft = rb << 4;  // v_alignbit reads bits [4:0]: 16 for odd y
         uint32_t acc = 1u << 15;
-        acc = __builtin_amdgcn_udot2(as_us2(q[0]), odd ? us2{0, 18} : us2{18, 34}, acc, false);
-        acc = __builtin_amdgcn_udot2(as_us2(q[kO3HS]), odd ? us2{34, 48} : us2{48, 56}, acc, false);
-        acc = __builtin_amdgcn_udot2(as_us2(q[2 * kO3HS]), odd ? us2{56, 48} : us2{48, 34}, acc, false);
-        acc = __builtin_amdgcn_udot2(as_us2(q[3 * kO3HS]), odd ? us2{34, 18} : us2{18, 0}, acc, false);
-        return (int)(acc >> 16);
+        acc = __builtin_amdgcn_udot2(as_us2(__builtin_amdgcn_alignbit(q1, q0, sft)), us2{18, 34}, acc, false);
+        acc = __builtin_amdgcn_udot2(as_us2(__builtin_amdgcn_alignbit(q2, q1, sft)), us2{48, 56}, acc, false);
+        acc = __builtin_amdgcn_udot2(as_us2(__builtin_amdgcn_alignbit(q3, q2, sft)), us2{48, 34}, acc, false);
+        acc = __builtin_amdgcn_udot2(as_us2(__builtin_amdgcn_alignbit(q3, q3, sft)), us2{18, 0}, acc, false);
+        return acc;
     };
-#endif
-    int t0[4], t1[4];
-#pragma unroll
-    for (int w = 0; w < 4; w++) {
-        const int bit = w * 64 + lane;
-        const uint32_t pw = c_pattern8.v[bit];
-        const float x0 = (float)(int8_t)(pw & 0xFF), y0 = (float)(int8_t)((pw >> 8) & 0xFF);
-        const float x1 = (float)(int8_t)((pw >> 16) & 0xFF), y1 = (float)(int8_t)(pw >> 24);
-        const int r0 = cv_round(fmaf(x0, bb, y0 * a)), c0 = cv_round(fmaf(x0, a, -(y0 * bb)));
-        const int r1 = cv_round(fmaf(x1, bb, y1 * a)), c1 = cv_round(fmaf(x1, a, -(y1 * bb)));
-        t0[w] = blurred(r0, c0);
-        t1[w] = blurred(r1, c1);
-    }
     uint64_t m[4];
 #pragma unroll
-    for (int w = 0; w < 4; w++) m[w] = __ballot(t0[w] < t1[w]);
+    for (int w = 0; w < 4; w++) {
+        const float4 pt = c_patternf.v[w * 64 + lane];
+        const uint32_t acc0 = sample(pt.x, pt.y), acc1 = sample(pt.z, pt.w);
+        m[w] = __ballot(acc0 < (acc1 & 0xFFFF0000u));
+    }
     uint8_t* desc = b.out_desc + ((size_t)f * b.cap + oi) * 32;
     if (lane < 4) reinterpret_cast<uint64_t*>(desc)[lane] = lane == 0 ? m[0] : lane == 1 ? m[1] : lane == 2 ? m[2] : m[3];
     if (lane == 4) {
         slam_keypoint kp;
-        kp.x = l ? (float)kx * L.scale : (float)kx;
-        kp.y = l ? (float)ky * L.scale : (float)ky;
-        kp.size = L.size;
+        kp.x = l ? (float)kx * O.scale : (float)kx;
+        kp.y = l ? (float)ky * O.scale : (float)ky;
+        kp.size = O.size;
         kp.angle = angle;
         kp.response = (float)kp_s(key);
         kp.octave = l;
@@ -1586,8 +1611,8 @@ __global__ void __launch_bounds__(64 * kOrbWpg) k_orb3(Bufs b) {
 #ifdef SLAMHOT_ORB_TRACE
     ORB_MARK();
     if (otrace)
-        printf("ORB slot=%d l=%d stage %lld ic %lld horiz %lld sincos %lld desc %lld\n", slot, l, otr[1] - otr[0],
-               otr[2] - otr[1], otr[3] - otr[2], otr[4] - otr[3], otr[5] - otr[4]);
+        printf("ORB slot=%d l=%d pro %lld stage %lld ic %lld horiz %lld sincos %lld desc %lld\n", slot, l, otr[1] - otr[0],
+               otr[2] - otr[1], otr[3] - otr[2], otr[4] - otr[3], otr[5] - otr[4], otr[6] - otr[5]);
 #endif
 }
 
@@ -1727,6 +1752,23 @@ static slam_status ensure_plan(slam_extractor* ex, int W, int H) {
             ++v0;
         }
         for (int v = 0; v <= kHalfPatch; v++) dp.umax[v] = umax[v];
+        // k_orb3's IC_Angle weights: lane (row v, half) holds staged dwords k0 .. k0+4 (k0 = 1 or
+        // 6) of window row 21 + v, whose byte b is column b - (sh + 21) from the keypoint
+        for (int sh = 0; sh < 4; sh++)
+            for (int av = 0; av <= kHalfPatch + 1; av++)
+                for (int half = 0; half < 2; half++) {
+                    uint32_t* w = dp.ic_w[sh][av][half];
+                    const int c0 = sh + 21, d = av <= kHalfPatch ? umax[av] : -1;  // -1: no bytes
+                    for (int i = 0; i < 12; i++) w[i] = 0;
+                    for (int i = 0; i < 5; i++)
+                        for (int j = 0; j < 4; j++) {
+                            const int bo = 4 * ((half ? 6 : 1) + i) + j;
+                            if (d >= 0 && bo >= c0 - d && bo <= c0 + d) {
+                                w[i] |= 1u << (8 * j);
+                                w[5 + i] |= (uint32_t)bo << (8 * j);
+                            }
+                        }
+                }
     }
     for (int l = 0; l < P.nlevels; l++) {
         const LevelPlan& L = P.lv[l];
@@ -1742,7 +1784,13 @@ static slam_status ensure_plan(slam_extractor* ex, int W, int H) {
             D.root_x0[i] = L.root_x0[i]; D.root_x1[i] = L.root_x1[i]; D.root_first_x[i] = L.root_first_x[i];
         }
         D.xtab_off = L.xtab_off; D.ytab_off = L.ytab_off; D.xmax = L.xmax;
+        OrbLv& O = dp.orb_lv[l];
+        O.kbase = L.kbase; O.w = L.w; O.h = L.h; O.pitch = l ? L.pitch : W;
+        O.off = l ? L.pyr_off : 0;
+        O.fstride = l ? P.pyr_frame : (int64_t)W * H;
+        O.scale = L.scale; O.size = L.size;
     }
+    for (int l = P.nlevels; l < kMaxLevels; l++) dp.orb_lv[l].kbase = 0x7FFFFFFF;
     slam_status st;
     if ((st = ex->d_plan.ensure(sizeof(DevPlan))) ||
         (st = ex->d_xtab.ensure(std::max<size_t>(16, P.xtab.size() * sizeof(ResizeX)))) ||
@@ -1921,6 +1969,8 @@ static slam_status launch_range(slam_extractor* ex, int f0, int nframes, const u
     b.ytab = ex->d_ytab.as<ResizeY>();
     b.cells = ex->d_cells.as<CellDesc>();
     b.plan = ex->d_plan.as<DevPlan>();
+    b.kslots = P.kslots;
+    b.nlevels = P.nlevels;
     b.nframes = nframes;
     b.cap = cap;
     b.lap0 = lap0;
