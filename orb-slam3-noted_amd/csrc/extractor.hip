@@ -531,6 +531,18 @@ __device__ __forceinline__ void fast_cell(const Bufs& b, const DevPlan& P, const
     const int th = ch - 6;
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     const int ti = min(max(P.ini_th, 0), 255), tm = min(max(P.min_th, 0), 255);
+#ifdef SLAMHOT_FAST_TRACE
+    // per-pass s_memtime cycles and list sizes of sampled cells (tools/ab/r05_fasttrace.sh)
+    long long ftr[12];
+    int nftr = 0, fcnt[8], nfc = 0;
+    const bool ftrace = f == 5 && (cd.slot % 7) == 3 && lane == 0;
+#define FAST_MARK() do { if (ftrace && nftr < 12) ftr[nftr++] = (long long)__builtin_amdgcn_s_memtime(); } while (0)
+#define FAST_CNT(x) do { if (ftrace && nfc < 8) fcnt[nfc++] = (x); } while (0)
+#else
+#define FAST_MARK() do {} while (0)
+#define FAST_CNT(x) do {} while (0)
+#endif
+    FAST_MARK();
     {
         uint32_t* m32 = reinterpret_cast<uint32_t*>(map);
         const int nw = ((th + 2) * lay.ms + 3) >> 2;
@@ -556,6 +568,7 @@ __device__ __forceinline__ void fast_cell(const Bufs& b, const DevPlan& P, const
     };
     for (int attempt = 0; attempt < 2; attempt++) {
         const int t = attempt == 0 ? ti : tm;
+        FAST_MARK();
         // pass A, four pixels per lane in packed u16 pairs (even / odd bytes of an LDS dword).
         // Lane = (row, dword group) over the dwords covering the tested columns; the compass
         // test per pixel is  min(p0,p8), min(p4,p12) < v - t  (dark) or  max(..) > v + t
@@ -607,6 +620,8 @@ __device__ __forceinline__ void fast_cell(const Bufs& b, const DevPlan& P, const
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        FAST_MARK();
+        FAST_CNT(na);
 
         // pass B1: the eight-pair pre-test on the compass survivors (in-place compaction)
         {
@@ -625,6 +640,8 @@ __device__ __forceinline__ void fast_cell(const Bufs& b, const DevPlan& P, const
             na = n1;
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        FAST_MARK();
+        FAST_CNT(na);
 
         // pass B (compacts the list in place: writes never pass the chunk being read)
         int nb = 0;
@@ -644,6 +661,8 @@ __device__ __forceinline__ void fast_cell(const Bufs& b, const DevPlan& P, const
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 
+        FAST_MARK();
+        FAST_CNT(nb);
         // pass C: cell-local 3x3 NMS at t; count, then emit in list (row-major) order
         int cnt = 0;
         for (int j = 0; j < nb; j += 64) cnt += __popcll(__ballot(j + lane < nb && keep_at(j + lane, t)));
@@ -662,6 +681,23 @@ __device__ __forceinline__ void fast_cell(const Bufs& b, const DevPlan& P, const
             base += __popcll(m);
         }
         if (lane == 0) b.cell_cnt[(size_t)f * P.ncells + cd.slot] = base;
+#ifdef SLAMHOT_FAST_TRACE
+        FAST_MARK();
+        if (ftrace) {
+            // marks: 0 start, per attempt: begin, A, B1, B; then the end (after C and the emit)
+            const int a = attempt;
+            const long long zero = ftr[1] - ftr[0];
+            long long A = 0, B1 = 0, B = 0;
+            for (int k = 0; k <= a; k++) {
+                A += ftr[2 + 4 * k] - ftr[1 + 4 * k];
+                B1 += ftr[3 + 4 * k] - ftr[2 + 4 * k];
+                B += ftr[4 + 4 * k] - ftr[3 + 4 * k];
+            }
+            const long long C = ftr[nftr - 1] - ftr[nftr - 2];
+            printf("FAST lvl=%d cw=%d ch=%d att=%d nA=%d nB1=%d nB=%d kept=%d zero %lld A %lld B1 %lld B %lld C %lld\n",
+                   cd.level, cw, ch, a + 1, fcnt[3 * a], fcnt[3 * a + 1], fcnt[3 * a + 2], base, zero, A, B1, B, C);
+        }
+#endif
         return;
     }
 }
