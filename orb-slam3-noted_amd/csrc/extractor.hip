@@ -521,10 +521,27 @@ struct FastWaveLds {
 #endif
 constexpr int kFastWpg = SLAMHOT_FAST_WPG;  // waves (cells) per workgroup
 
+// One wave cell with everything its wave derives from the geometry precomputed on the host
+// (ensure_plan): one scalar load instead of cell index -> CellDesc -> level plan, and no
+// per-wave integer divisions (lane / d = (lane * m_d) >> 16 with m_d = ceil(2^16 / d), exact for
+// lane < 64, d <= 20).
+// All fields are dwords: scalar loads, no byte extraction (which the compiler does in VALU).
+struct FastWaveCell {
+    int64_t roi_off;        // byte offset of the staged ROI's first dword in the frame's level
+    int64_t fstride;        // frame stride of that level's base (Bufs img for level 0, else pyr)
+    int32_t slot, pitch;    // cell slot; level row pitch
+    int32_t level, iniX, iniY, cw, ch;
+    int32_t sh, wd, rp, ng; // staging shift (bytes), staged dwords per row, rows per staging pass,
+                            // pass-A dword groups
+    int32_t g0, rpi, dw;    // first pass-A group, pass-A rows per iteration, dword staging
+    int32_t m_wd, m_ng;
+};
+static_assert(sizeof(FastWaveCell) == 80, "five 16-byte rows");
+
 // One cell after its ROI is in LDS (roi = the ROI origin, `sh` bytes into each staged row): the
 // M map zeroed, passes A / B1 / B / C at iniThFAST, again at minThFAST for an empty cell, the
 // kept corners emitted to the cell's slot in row-major order.
-__device__ __forceinline__ void fast_cell(const Bufs& b, const DevPlan& P, const CellDesc& cd, int f, int sh,
+__device__ __forceinline__ void fast_cell(const Bufs& b, const DevPlan& P, const FastWaveCell& cd, int f, int sh,
                                           const uint8_t* roi, const uint32_t* roi32, uint8_t* map, uint16_t* lst,
                                           const FastWaveLds& lay, int lane) {
     const int cw = cd.cw, ch = cd.ch;
@@ -555,6 +572,19 @@ __device__ __forceinline__ void fast_cell(const Bufs& b, const DevPlan& P, const
     // current attempt (far fewer survivors at iniTh = 20 than at minTh = 7); only empty cells
     // pay for the second attempt.  M is exact, so the map entries of the first attempt stay
     // valid for the second (NMS reads neighbours as M > t ? M - 1 : 0).
+    // pass A's lane = (row ar, dword group gd) over the ng dwords that cover the tested columns
+    // (ng <= 17, rpi = 64 / ng rows per iteration; host-computed), and the byte mask of its
+    // tested columns
+    const int ng = cd.ng, rpi = cd.rpi;
+    const int ar = (lane * cd.m_ng) >> 16, gd = cd.g0 + (lane - ar * ng);
+    uint32_t cmask = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int x = 4 * gd + k - sh;  // ROI column of byte k
+        if (x >= 3 && x <= cw - 4) cmask |= 0xFFu << (8 * k);
+    }
+    if (ar >= rpi) cmask = 0;
+    const int code0 = (4 * gd - sh - 3) + ar * 64;  // code of byte 0 in row 0
     auto keep_at = [&](int e, int t) -> bool {
         const int code = lst[e];
         const int r = code >> 6, c = code & 63;
@@ -576,18 +606,6 @@ __device__ __forceinline__ void fast_cell(const Bufs& b, const DevPlan& P, const
         // Four ballots (one per byte) + mbcnt give row-major compaction.
         int na = 0;
         {
-            const int g0 = (sh + 3) >> 2, g1 = (sh + cw - 4) >> 2;
-            const int ng = g1 - g0 + 1;  // <= 17
-            const int rpi = 64 / ng;     // tested rows per iteration
-            const int ar = lane / ng, gd = g0 + (lane - ar * ng);
-            uint32_t cmask = 0;
-    #pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const int x = 4 * gd + k - sh;  // ROI column of byte k
-                if (x >= 3 && x <= cw - 4) cmask |= 0xFFu << (8 * k);
-            }
-            if (ar >= rpi) cmask = 0;
-            const int code0 = (4 * gd - sh - 3) + ar * 64;  // code of byte 0 in row 0
             const us2 T = {(unsigned short)t, (unsigned short)t};
             const int RS = lay.rs >> 2;
             for (int rt = 0; rt < th; rt += rpi) {
@@ -702,50 +720,34 @@ __device__ __forceinline__ void fast_cell(const Bufs& b, const DevPlan& P, const
     }
 }
 
-// Stage a cell's ROI rows with independent 32-bit loads (row start aligned down to 4 bytes, so
-// the ROI origin inside LDS is `sh` bytes into each row).  Lane = (row offset, dword column),
-// fixed for the wave: rows lr, lr + rp, ... ; kPf of them held in registers at once.
-struct RoiGeo {
-    const uint8_t* src;
-    int pitch, sh, ch, cw, lr, lc, rp;
-    bool dw;  // dword path (pitch % 4 == 0); else byte copies
-};
-__device__ __forceinline__ RoiGeo roi_geo(const Bufs& b, const DevPlan& P, const CellDesc& cd, int f, int lane) {
-    RoiGeo g;
-    const int l = cd.level;
-    g.pitch = level_pitch(P, l);
-    g.dw = (g.pitch & 3) == 0;
-    g.sh = g.dw ? (cd.iniX & 3) : 0;
-    g.src = level_ptr(b, P, f, l) + (size_t)cd.iniY * g.pitch + (cd.iniX - g.sh);
-    g.ch = cd.ch;
-    g.cw = cd.cw;
-    const int wd = (g.sh + g.cw + 3) >> 2;  // <= kRoiStride / 4
-    g.rp = 64 / wd;
-    g.lr = lane / wd;
-    g.lc = lane - g.lr * wd;
-    return g;
-}
-__device__ __forceinline__ void stage_roi(const RoiGeo& g, uint8_t* roi, int rs, int lane) {
+// Stage a cell's ROI rows with independent 32-bit buffer loads (row start aligned down to 4
+// bytes, so the ROI origin inside LDS is `sh` bytes into each row).  Lane = (row offset lr,
+// dword column lc), fixed for the wave: rows lr, lr + rp, ...; eight rows per lane in flight, each
+// load's row offset an SGPR (soffset), the resource bounded at the ROI's last byte so the rows
+// past it read zero without touching memory.
+__device__ __forceinline__ void stage_roi(const FastWaveCell& c, const uint8_t* src, uint8_t* roi, int rs, int lane) {
     uint32_t* roi32 = reinterpret_cast<uint32_t*>(roi);
-    if (g.dw) {
-        if (g.lr < g.rp) {
-            for (int r0 = g.lr; r0 < g.ch; r0 += 8 * g.rp) {
+    if (c.dw) {
+        const int lr = (lane * c.m_wd) >> 16, lc = lane - lr * c.wd;
+        if (lr < c.rp) {
+            const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)src, (short)0, __builtin_amdgcn_readfirstlane((c.ch - 1) * c.pitch + 4 * c.wd), 0x00020000);
+            const int voff = lr * c.pitch + 4 * lc;
+            uint32_t* dst = roi32 + lr * (rs >> 2) + lc;
+            const int rp = c.rp, step = rp * (rs >> 2);
+            for (int r0 = 0, q0 = 0; r0 < c.ch; r0 += 8 * rp, q0 += 8) {
                 uint32_t v[8];
 #pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    const int r = r0 + k * g.rp;
-                    if (r < g.ch) v[k] = *reinterpret_cast<const uint32_t*>(g.src + (size_t)r * g.pitch + 4 * g.lc);
-                }
+                for (int k = 0; k < 8; k++)
+                    v[k] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, (r0 + k * rp) * c.pitch, 0);
 #pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    const int r = r0 + k * g.rp;
-                    if (r < g.ch) roi32[r * (rs >> 2) + g.lc] = v[k];
-                }
+                for (int k = 0; k < 8; k++)
+                    if (lr + r0 + k * rp < c.ch) dst[(q0 + k) * step] = v[k];
             }
         }
     } else {
-        for (int r = 0; r < g.ch; r++)
-            for (int c = lane; c < g.cw; c += 64) roi[r * rs + c] = g.src[(size_t)r * g.pitch + c];
+        for (int r = 0; r < c.ch; r++)
+            for (int x = lane; x < c.cw; x += 64) roi[r * rs + x] = src[(size_t)r * c.pitch + x];
     }
 }
 
@@ -755,20 +757,22 @@ __device__ __forceinline__ void stage_roi(const RoiGeo& g, uint8_t* roi, int rs,
 // LDS per wave (host-sized to the widest cell of the class): ROI ch x rs | M map (th+2) x ms |
 // list.
 // ---------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(64 * kFastWpg) __attribute__((amdgpu_waves_per_eu(6, 8))) k_fast_wave(Bufs b, const int32_t* list, int nlist,
+__global__ void __launch_bounds__(64 * kFastWpg) __attribute__((amdgpu_waves_per_eu(6, 8))) k_fast_wave(Bufs b, const FastWaveCell* list, int nlist,
                                                    FastWaveLds lay) {
     extern __shared__ __attribute__((aligned(16))) uint8_t fw_smem[];
-    const int wave = kFastWpg == 1 ? 0 : threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // the wave index through v_readfirstlane: known wave-uniform, so the cell record and all the
+    // geometry derived from it live in SGPRs (scalar loads, buffer-load soffsets)
+    const int wave = kFastWpg == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int2 blk = xcd_block();
     const int idx = blk.x * kFastWpg + wave;
     if (idx >= nlist) return;
     const DevPlan& P = *b.plan;
     const int f = blk.y;
-    const CellDesc cd = b.cells[list[idx]];
+    const FastWaveCell cd = list[idx];
     uint8_t* base_ptr = fw_smem + wave * lay.total;
-    const RoiGeo g = roi_geo(b, P, cd, f, lane);
-    stage_roi(g, base_ptr + lay.roi, lay.rs, lane);
-    fast_cell(b, P, cd, f, g.sh, base_ptr + lay.roi + g.sh, reinterpret_cast<const uint32_t*>(base_ptr + lay.roi),
+    const uint8_t* src = (cd.level ? (const uint8_t*)b.pyr : b.img) + (size_t)f * cd.fstride + cd.roi_off;
+    stage_roi(cd, src, base_ptr + lay.roi, lay.rs, lane);
+    fast_cell(b, P, cd, f, cd.sh, base_ptr + lay.roi + cd.sh, reinterpret_cast<const uint32_t*>(base_ptr + lay.roi),
               base_ptr + lay.map, reinterpret_cast<uint16_t*>(base_ptr + lay.lst), lay, lane);
 }
 
@@ -1905,11 +1909,45 @@ static slam_status ensure_plan(slam_extractor* ex, int W, int H) {
         if (4 * lay.total > 160 * 1024 || 4 * ex->fw_lay_b.total > 160 * 1024) return SLAM_EINVAL;
         SLAM_HIP_TRY(hipFuncSetAttribute((const void*)k_fast_wave, hipFuncAttributeMaxDynamicSharedMemorySize,
                                          160 * 1024));
-        if ((st = ex->d_wave_cells.ensure(std::max<size_t>(4, wave.size() * 4))) ||
+        // the wave cells' records (FastWaveCell): staging geometry and pass-A lane map per cell
+        std::vector<FastWaveCell> wcells;
+        wcells.reserve(wave.size());
+        auto magic = [](int d) { return (65536 + d - 1) / d; };
+        for (int d = 1; d <= 20; d++)  // the lane / d identity k_fast_wave relies on
+            for (int x = 0; x < 64; x++)
+                if (((x * magic(d)) >> 16) != x / d) return SLAM_EINVAL;
+        for (int32_t sl : wave) {
+            const CellDesc& c = P.cells[sl];
+            const LevelPlan& L = P.lv[c.level];
+            FastWaveCell w{};
+            w.pitch = c.level ? L.pitch : W;
+            w.dw = (w.pitch & 3) == 0;
+            w.sh = w.dw ? (c.iniX & 3) : 0;
+            w.fstride = c.level ? P.pyr_frame : (int64_t)W * H;
+            w.roi_off = (c.level ? L.pyr_off : 0) + (int64_t)c.iniY * w.pitch + (c.iniX - w.sh);
+            w.slot = c.slot;
+            w.level = c.level;
+            w.iniX = c.iniX;
+            w.iniY = c.iniY;
+            w.cw = c.cw;
+            w.ch = c.ch;
+            const int wd = (w.sh + c.cw + 3) >> 2, g0 = (w.sh + 3) >> 2, g1 = (w.sh + c.cw - 4) >> 2;
+            const int ng = std::max(1, g1 - g0 + 1);  // < 1: no tested column (cw < 7), cmask stays 0
+            if (wd < 1 || wd > 20 || ng > 17) return SLAM_EINVAL;
+            w.wd = wd;
+            w.rp = 64 / wd;
+            w.m_wd = magic(wd);
+            w.g0 = g0;
+            w.ng = ng;
+            w.rpi = 64 / ng;
+            w.m_ng = magic(ng);
+            wcells.push_back(w);
+        }
+        if ((st = ex->d_wave_cells.ensure(std::max<size_t>(sizeof(FastWaveCell), wcells.size() * sizeof(FastWaveCell)))) ||
             (st = ex->d_wide_cells.ensure(std::max<size_t>(4, wide.size() * 4))))
             return st;
-        if (!wave.empty())
-            SLAM_HIP_TRY(hipMemcpy(ex->d_wave_cells.p, wave.data(), wave.size() * 4, hipMemcpyHostToDevice));
+        if (!wcells.empty())
+            SLAM_HIP_TRY(hipMemcpy(ex->d_wave_cells.p, wcells.data(), wcells.size() * sizeof(FastWaveCell), hipMemcpyHostToDevice));
         if (!wide.empty())
             SLAM_HIP_TRY(hipMemcpy(ex->d_wide_cells.p, wide.data(), wide.size() * 4, hipMemcpyHostToDevice));
         ex->n_wave_cells = (int)wave.size();
@@ -2058,16 +2096,16 @@ static slam_status launch_range(slam_extractor* ex, int f0, int nframes, const u
             // a small batch fills a fraction of the chip: one dispatch over both classes at the
             // union layout saves the second launch on the per-image critical path
             hipLaunchKernelGGL(k_fast_wave, dim3((na + nb + G - 1) / G, nframes), dim3(64 * G),
-                               G * ex->fw_lay_all.total + fast_pad, s, b, ex->d_wave_cells.as<int32_t>(), na + nb,
+                               G * ex->fw_lay_all.total + fast_pad, s, b, ex->d_wave_cells.as<FastWaveCell>(), na + nb,
                                ex->fw_lay_all);
         } else {
         if (nb)
             hipLaunchKernelGGL(k_fast_wave, dim3((nb + G - 1) / G, nframes), dim3(64 * G),
-                               G * ex->fw_lay_b.total + fast_pad, s, b, ex->d_wave_cells.as<int32_t>() + na, nb,
+                               G * ex->fw_lay_b.total + fast_pad, s, b, ex->d_wave_cells.as<FastWaveCell>() + na, nb,
                                ex->fw_lay_b);
         if (na)
             hipLaunchKernelGGL(k_fast_wave, dim3((na + G - 1) / G, nframes), dim3(64 * G),
-                               G * ex->fw_lay.total + fast_pad, s, b, ex->d_wave_cells.as<int32_t>(), na, ex->fw_lay);
+                               G * ex->fw_lay.total + fast_pad, s, b, ex->d_wave_cells.as<FastWaveCell>(), na, ex->fw_lay);
         }
     }
     if (ex->n_wide_cells)
