@@ -497,7 +497,8 @@ __global__ void __launch_bounds__(kLinThreads) k_linearize(int nb_pose, int npos
                                                            double* __restrict__ bp) {
     const int b = blockIdx.x;
     if (b < nb_pose)
-        lin_poses_body(b * (kLinThreads / 64) + (threadIdx.x >> 6), threadIdx.x & 63, npose_total, pe_off, pe,
+        lin_poses_body(b * (kLinThreads / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), threadIdx.x & 63,
+                       npose_total, pe_off, pe,
                        pose_win, E, ctl, poses, pts, pose_stride, pt_stride, cam, hk, Hpp, bp);
     else
         lin_points_body((b - nb_pose) * kLinThreads + threadIdx.x, npt_total, pt_off, pt_win, E, ctl, poses, pts,
@@ -820,7 +821,8 @@ __global__ void __launch_bounds__(256) k_ct_fill(int nblk_total, const int2* __r
                                                  const int* __restrict__ bmp, const int* __restrict__ pbase,
                                                  const int* __restrict__ pls, const int* __restrict__ ct_off,
                                                  int4* __restrict__ ct) {
-    const int b = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    // wave index via v_readfirstlane: wave-uniform, so the block's records load into SGPRs
+    const int b = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (b >= nblk_total) return;
     const WinDesc& W = wins[blk_win[b]];
     const int2 ij = blk_pose[b];

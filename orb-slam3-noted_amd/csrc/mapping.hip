@@ -40,7 +40,7 @@ __device__ __forceinline__ int ham(const uint4 a0, const uint4 a1, const uint4 b
 
 __global__ void __launch_bounds__(kDistThreads) k_distinctive(int n_mp, const int32_t* off, const uint8_t* desc,
                                                               int32_t* best) {
-    const int mpi = blockIdx.x * (kDistThreads / 64) + (threadIdx.x >> 6);
+    const int mpi = blockIdx.x * (kDistThreads / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
     const int lane = threadIdx.x & 63;
     if (mpi >= n_mp) return;
     const int o = off[mpi];
