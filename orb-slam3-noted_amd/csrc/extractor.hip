@@ -247,14 +247,49 @@ __global__ void __launch_bounds__(256) k_resize4(Bufs b, int l, double scale_x, 
         a0s[k] = a0;
         a1s[k] = a1;
     }
-    // horizontal pass of one source row (HResizeLinear): D[k] = S[sx]*a0 + S[sx+1]*a1
+    // horizontal pass of one source row (HResizeLinear): D[k] = S[sx]*a0 + S[sx+1]*a1.
+    // Dword form: the thread's eight source bytes sx_k, sx_k + 1 lie in the 12 bytes from
+    // xb = sx_0 & ~3 when sx_3 + 1 - xb <= 11 (scale factors up to ~2.5): three dword buffer loads
+    // per row instead of eight byte loads (the byte loads bound the kernel's memory pipeline), each
+    // pair (S[sx], S[sx+1]) gathered by one v_perm into a u16 pair for one v_dot2 with (a0, a1).
+    // The resource spans the source level of this frame, so the few bytes read past its last row
+    // (weight 0 or unused) come back as zero.  Otherwise (pitch not a multiple of 4, wider
+    // spans) the byte loads.
+    const int xb = sxs[0] & ~3;
+    const bool dw = ((spitch & 3) == 0) && (sxs[3] + 1 - xb <= 11);
+    uint32_t selp[4], hiw[4];
+    us2 coef[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int o = sxs[k] - xb;              // 0 .. 10
+        const int w = o >= 4 ? 1 : 0;           // window {w[w+1], w[w]} holds bytes o, o + 1 (o - 4w <= 6)
+        const int ob = o - 4 * w;
+        selp[k] = 0x0c000c00u | (uint32_t)ob | ((uint32_t)(ob + 1) << 16);  // [S[sx], 0, S[sx+1], 0]
+        hiw[k] = (uint32_t)w;
+        coef[k] = us2{(unsigned short)a0s[k], (unsigned short)a1s[k]};
+    }
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)src, (short)0, __builtin_amdgcn_readfirstlane(S.h * spitch), 0x00020000);
     auto hrow = [&](int y, int* d) {
-        const uint8_t* r = src + (size_t)min(max(y, 0), S.h - 1) * spitch;
-        int p0[4], p1[4];
+        const int yc = min(max(y, 0), S.h - 1);
+        if (dw) {
+            const int off = yc * spitch + xb;
+            const uint32_t w0 = __builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, 0);
+            const uint32_t w1 = __builtin_amdgcn_raw_buffer_load_b32(rsrc, off + 4, 0, 0);
+            const uint32_t w2 = __builtin_amdgcn_raw_buffer_load_b32(rsrc, off + 8, 0, 0);
 #pragma unroll
-        for (int k = 0; k < 4; k++) { p0[k] = r[sxs[k]]; p1[k] = r[sxs[k] + 1]; }
+            for (int k = 0; k < 4; k++) {
+                const uint32_t lo = hiw[k] ? w1 : w0, hi = hiw[k] ? w2 : w1;
+                d[k] = (int)__builtin_amdgcn_udot2(as_us2(__builtin_amdgcn_perm(hi, lo, selp[k])), coef[k], 0u, false);
+            }
+        } else {
+            const uint8_t* r = src + (size_t)yc * spitch;
+            int p0[4], p1[4];
 #pragma unroll
-        for (int k = 0; k < 4; k++) d[k] = __mul24(p0[k], a0s[k]) + __mul24(p1[k], a1s[k]);
+            for (int k = 0; k < 4; k++) { p0[k] = r[sxs[k]]; p1[k] = r[sxs[k] + 1]; }
+#pragma unroll
+            for (int k = 0; k < 4; k++) d[k] = __mul24(p0[k], a0s[k]) + __mul24(p1[k], a1s[k]);
+        }
     };
     uint8_t* dbase = b.pyr + (size_t)f * P.pyr_frame + L.pyr_off + 4 * q;
     int D0[4], D1[4];
