@@ -28,6 +28,7 @@
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
+#include <atomic>
 #include <thread>
 
 #include <immintrin.h>
@@ -2590,25 +2591,75 @@ Plan bind(unsigned char* base, const Layout& L) {
     return P;
 }
 
-// Pass 1: validation and sizes.  hidx: free-pose index of every KF of every window.
+// host threads of one call's planning: callers run several solvers at once (the bench's LBA leg:
+// 4), and 16 planning threads per call oversubscribed the GPU box's 16-thread CPU share, delaying
+// the solver threads that launch the next LM step (SLAMHOT_LBA_PLAN_THREADS overrides)
+int plan_threads(int n_prob) {
+    static const int cap_env = std::getenv("SLAMHOT_LBA_PLAN_THREADS") ? std::atoi(std::getenv("SLAMHOT_LBA_PLAN_THREADS")) : 0;
+    const int cap = cap_env > 0 ? cap_env : 4;
+    const int hw = (int)std::max(1u, std::min((unsigned)cap, std::thread::hardware_concurrency()));
+    return std::max(1, std::min(hw, n_prob));
+}
+
+// run fn(w, scratch) for every window on nth threads (window w on thread w % nth)
+template <class S, class F>
+slam_status for_windows(int n_prob, int nth, F fn) {
+    std::vector<slam_status> rs(nth, SLAM_OK);
+    auto run = [&](int t) {
+        S scratch;
+        for (int w = t; w < n_prob; w += nth) {
+            const slam_status r = fn(w, scratch);
+            if (r != SLAM_OK) rs[t] = r;
+        }
+    };
+    if (nth <= 1) {
+        run(0);
+    } else {
+        std::vector<std::thread> th;
+        try {
+            for (int t = 1; t < nth; t++) th.emplace_back(run, t);
+        } catch (...) {  // thread creation failed: the rest run here
+            for (int t = (int)th.size() + 1; t < nth; t++) run(t);
+        }
+        run(0);
+        for (auto& x : th) x.join();
+    }
+    for (slam_status r : rs)
+        if (r != SLAM_OK) return r;
+    return SLAM_OK;
+}
+
+// Pass 1: validation and sizes, per window on the planning threads, then the windows' start
+// offsets (prefix sums).  hidx: free-pose index of every KF of every window.
 slam_status plan_sizes(int n_prob, const slam_lba_problem* probs, PlanSizes& z, std::vector<int>& hidx_all,
                        std::vector<int>& np_of) {
     z.nw = n_prob;
     np_of.assign(n_prob, 0);
     z.starts.resize(n_prob);
-    std::vector<int> cnt;
+    size_t nkf_all = 0;
     for (int w = 0; w < n_prob; w++) {
+        if (probs[w].n_kf < 0 || probs[w].n_pt < 0 || probs[w].n_edge < 0) return SLAM_EINVAL;
+        z.starts[w].h0 = nkf_all;
+        nkf_all += probs[w].n_kf;
+    }
+    hidx_all.assign(nkf_all, -1);
+    struct WinSz {
+        int npe = 0, nspe = 0;
+        long long nct = 0;
+        bool body = false;
+    };
+    std::vector<WinSz> sz(n_prob);
+    slam_status st = for_windows<std::vector<int>>(n_prob, plan_threads(n_prob), [&](int w, std::vector<int>& cnt) {
         const slam_lba_problem& P = probs[w];
-        if (P.n_kf < 0 || P.n_pt < 0 || P.n_edge < 0) return SLAM_EINVAL;
-        z.starts[w] = WinStart{z.nkf, z.npt, z.ne, z.npose, z.nblk, z.nspe, z.npe, z.nbm, z.nct, z.hs_total, hidx_all.size()};
         if ((P.n_kf && (!P.kf_Tcw || !P.kf_fixed)) || (P.n_pt && !P.pt_pos) ||
             (P.n_edge && (!P.edge_pt || !P.edge_kf || !P.edge_obs || !P.edge_inv_sigma2)))
             return SLAM_EINVAL;
+        WinSz& S = sz[w];
         if (P.edge_body && P.n_edge) {
             bool has = false;
             for (int i = 0; i < P.n_edge && !has; i++) has = P.edge_body[i] != 0;
             if (has && !P.kf_Trl) return SLAM_EINVAL;  // body edges need each KeyFrame's mTrl
-            z.any_body = z.any_body || has;
+            S.body = has;
         }
         cnt.assign(P.n_kf, 0);
         for (int i = 0; i < P.n_edge; i++) {
@@ -2619,9 +2670,9 @@ slam_status plan_sizes(int n_prob, const slam_lba_problem* probs, PlanSizes& z, 
         }
         // a KeyFrame without edges is not an active vertex (sparse_optimizer.cpp:262-300): it
         // stays out of the Hessian and keeps its estimate
-        const size_t h0 = hidx_all.size();
+        int* hidx = &hidx_all[z.starts[w].h0];
         int np = 0;
-        for (int k = 0; k < P.n_kf; k++) hidx_all.push_back(P.kf_fixed[k] == 0 && cnt[k] > 0 ? np++ : -1);
+        for (int k = 0; k < P.n_kf; k++) hidx[k] = P.kf_fixed[k] == 0 && cnt[k] > 0 ? np++ : -1;
         np_of[w] = np;
         if (6 * np > kMaxN) return SLAM_ECAP;
         // free-pose edges; an edge right after one of the same point on the same KeyFrame (body
@@ -2630,16 +2681,27 @@ slam_status plan_sizes(int n_prob, const slam_lba_problem* probs, PlanSizes& z, 
         int run = 0;
         for (int i = 0; i <= P.n_edge; i++) {
             if (i == P.n_edge || (i > 0 && P.edge_pt[i] != P.edge_pt[i - 1])) {
-                z.nct += (long long)run * (run + 1) / 2;
+                S.nct += (long long)run * (run + 1) / 2;
                 run = 0;
             }
-            if (i == P.n_edge || hidx_all[h0 + P.edge_kf[i]] < 0) continue;
-            z.npe++;
+            if (i == P.n_edge || hidx[P.edge_kf[i]] < 0) continue;
+            S.npe++;
             if (!(i > 0 && P.edge_pt[i - 1] == P.edge_pt[i] && P.edge_kf[i - 1] == P.edge_kf[i])) {
-                z.nspe++;
+                S.nspe++;
                 run++;
             }
         }
+        return SLAM_OK;
+    });
+    if (st != SLAM_OK) return st;
+    for (int w = 0; w < n_prob; w++) {
+        const slam_lba_problem& P = probs[w];
+        const int np = np_of[w];
+        z.starts[w] = WinStart{z.nkf, z.npt, z.ne, z.npose, z.nblk, z.nspe, z.npe, z.nbm, z.nct, z.hs_total, z.starts[w].h0};
+        z.any_body = z.any_body || sz[w].body;
+        z.nct += sz[w].nct;
+        z.npe += sz[w].npe;
+        z.nspe += sz[w].nspe;
         z.nbm += (long long)np * ((P.n_pt + 63) / 64);
         z.nkf += P.n_kf;
         z.npt += P.n_pt;
@@ -2654,8 +2716,7 @@ slam_status plan_sizes(int n_prob, const slam_lba_problem* probs, PlanSizes& z, 
     bool have = false, have2 = false;
     for (int w = 0; w < n_prob && !z.per_kf_cam; w++) {
         const slam_lba_problem& P = probs[w];
-        bool body = false;
-        for (int i = 0; P.edge_body && i < P.n_edge && !body; i++) body = P.edge_body[i] != 0;
+        const bool body = sz[w].body;
         for (int k = 0; k < P.n_kf && !z.per_kf_cam; k++) {
             const slam_camera& c = P.kf_cam ? P.kf_cam[k] : P.cam;
             if (!have) z.cam = c, have = true;
@@ -2674,7 +2735,18 @@ slam_status plan_fill(int n_prob, const slam_lba_problem* probs, const std::vect
                       const std::vector<int>& np_of, const slam_lba_options* opt, const PlanSizes& Z,
                       const Plan& P) {
     // windows are independent given their start offsets: fill them on host threads
+#ifdef SLAMHOT_PLAN_BENCH
+    // section cycle counts of plan_fill (rdtsc, summed over windows and threads)
+    static std::atomic<long long> pb_sec[5];
+    for (auto& x : pb_sec) x = 0;
+#define PB_MARK(k) do { const long long t_ = (long long)__rdtsc(); if (k) pb_sec[(k) - 1] += t_ - pb_t; pb_t = t_; } while (0)
+#else
+#define PB_MARK(k) do {} while (0)
+#endif
     auto fill_one = [&](int w, std::vector<int>& col, std::vector<int>& pcnt) -> slam_status {
+#ifdef SLAMHOT_PLAN_BENCH
+        long long pb_t = (long long)__rdtsc();
+#endif
         const WinStart& ws = Z.starts[w];
         int nkf = ws.kf0, npt = ws.pt0, ne = ws.e0, npose = ws.pose0, nblk = ws.blk0, nspe = ws.spe0;
         long long hs = ws.hs0;
@@ -2743,6 +2815,7 @@ slam_status plan_fill(int n_prob, const slam_lba_problem* probs, const std::vect
                 rec[7] = 0.0;
             }
         }
+        PB_MARK(0);
         std::memcpy(P.pt_in + 3 * (size_t)npt, Q.pt_pos, sizeof(float) * 3 * Q.n_pt);
         for (int i = 0; i < Q.n_edge; i++) {
             EdgeS& e = P.edges[ne + i];
@@ -2758,6 +2831,7 @@ slam_status plan_fill(int n_prob, const slam_lba_problem* probs, const std::vect
             e.obs[2] = body ? kBodyTag : (ur < 0.f ? -1.0f : ur);
             e.info = Q.edge_inv_sigma2[i];
         }
+        PB_MARK(1);
         // point CSR + per-point free-pose edges sorted by pose (HplCCS column order)
         const int pe_start = ws.pe0;
         pcnt.assign(np + 1, 0);
@@ -2781,6 +2855,7 @@ slam_status plan_fill(int n_prob, const slam_lba_problem* probs, const std::vect
                 P.spe[nspe++] = ne + col[x];
             }
         }
+        PB_MARK(2);
         // Schur blocks (i1 <= i2: blk = i2 (i2 + 1) / 2 + i1); their contributions come from the
         // pose bitmaps built on the device (k_bm_*)
         for (int i2 = 0, b = 0; i2 < np; i2++)
@@ -2791,6 +2866,7 @@ slam_status plan_fill(int n_prob, const slam_lba_problem* probs, const std::vect
                 if (i1 == i2) P.blk_order[npose + i2] = nblk + b;
                 else P.blk_order[Z.npose + (nblk - npose) + (b - i2)] = nblk + b;
             }
+        PB_MARK(3);
         // edges of every free pose (followers included: each adds its own Hpp), insertion order
         for (int e = 0; e < Q.n_edge; e++) {
             const int h = hidx[Q.edge_kf[e]];
@@ -2805,34 +2881,22 @@ slam_status plan_fill(int n_prob, const slam_lba_problem* probs, const std::vect
             const int h = hidx[Q.edge_kf[e]];
             if (h >= 0) P.pe[pe_start + pcnt[h]++] = ne + e;
         }
+        PB_MARK(4);
         (void)nkf;
         return SLAM_OK;
     };
-    // a few threads per call: callers run several solvers at once (the bench's LBA leg: 4), and
-    // 16 planning threads per call oversubscribed the GPU box's 16-thread CPU share, delaying
-    // the solver threads that launch the next LM step (SLAMHOT_LBA_PLAN_THREADS overrides)
-    static const int cap_env = std::getenv("SLAMHOT_LBA_PLAN_THREADS") ? std::atoi(std::getenv("SLAMHOT_LBA_PLAN_THREADS")) : 0;
-    const int cap = cap_env > 0 ? cap_env : 4;
-    const int hw = (int)std::max(1u, std::min((unsigned)cap, std::thread::hardware_concurrency()));
-    const int nth = std::min(hw, n_prob);
-    std::vector<slam_status> rs(nth, SLAM_OK);
-    auto run = [&](int t) {
+    struct FillScratch {
         std::vector<int> col, pcnt;
-        for (int w = t; w < n_prob; w += nth) {
-            const slam_status r = fill_one(w, col, pcnt);
-            if (r != SLAM_OK) rs[t] = r;
-        }
     };
-    if (nth <= 1) {
-        run(0);
-    } else {
-        std::vector<std::thread> th;
-        for (int t = 1; t < nth; t++) th.emplace_back(run, t);
-        run(0);
-        for (auto& x : th) x.join();
-    }
-    for (slam_status r : rs)
-        if (r != SLAM_OK) return r;
+    const slam_status st = for_windows<FillScratch>(n_prob, plan_threads(n_prob), [&](int w, FillScratch& sc) {
+        return fill_one(w, sc.col, sc.pcnt);
+    });
+    if (st != SLAM_OK) return st;
+#ifdef SLAMHOT_PLAN_BENCH
+    std::fprintf(stderr, "fill sections (Mcycles): header+edges %.1f, csr %.1f, blocks %.1f, pose lists %.1f\n",
+                 pb_sec[0] / 1e6, pb_sec[1] / 1e6, pb_sec[2] / 1e6, pb_sec[3] / 1e6);
+#endif
+#undef PB_MARK
     P.pt_off[Z.npt] = Z.ne;
     P.spe_off[Z.npt] = Z.nspe;
     P.pe_off[Z.npose] = Z.npe;
@@ -3377,5 +3441,31 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     }
     return SLAM_OK;
 }
+
+#ifdef SLAMHOT_PLAN_BENCH
+// Experiment builds only (tools/microbench/lba_plan_bench.py): the host plan of a call, no device
+// work, into ordinary memory; reps repetitions, the last one's phase times returned.
+slam_status slamhot_lba_plan_bench(int n_prob, const slam_lba_problem* probs, const slam_lba_options* opt, int reps,
+                                   double* sizes_ms, double* fill_ms, double* arena_mb) {
+    std::vector<unsigned char> arena;
+    for (int r = 0; r < reps; r++) {
+        const auto t0 = std::chrono::steady_clock::now();
+        PlanSizes Z;
+        std::vector<int> hidx_all, np_of;
+        slam_status st = plan_sizes(n_prob, probs, Z, hidx_all, np_of);
+        if (st != SLAM_OK) return st;
+        const Layout LY = make_layout(Z);
+        if (arena.size() < LY.total) arena.resize(LY.total);
+        const auto t1 = std::chrono::steady_clock::now();
+        st = plan_fill(n_prob, probs, hidx_all, np_of, opt, Z, bind(arena.data(), LY));
+        if (st != SLAM_OK) return st;
+        const auto t2 = std::chrono::steady_clock::now();
+        *sizes_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+        *fill_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
+        *arena_mb = LY.total / 1e6;
+    }
+    return SLAM_OK;
+}
+#endif
 
 }  // extern "C"
