@@ -3,7 +3,7 @@
 # (3 pairs), after the LBA / shim GPU tests on the in-tree library.
 export TMPDIR=/tmp
 TAG=${1:-lbahead}
-A=orb-slam3-noted_amd/lib/libslamhot.so; B=orb-slam3-noted_amd/lib/ab/libslamhot_head.so
+A=orb-slam3-noted_amd/lib/libslamhot.so; B=${HEADLIB:-orb-slam3-noted_amd/lib/ab/libslamhot_head.so}
 timeout -k 10 600 python -u -m pytest tests/test_gpu_lba.py tests/test_gpu_shim.py -x -q --timeout 120 --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1
 rc=$?; echo tests_exit=$rc; tail -2 gpurun_out/${TAG}_tests.log; [ $rc -ne 0 ] && exit $rc
 for i in 1 2 3; do

@@ -4,7 +4,7 @@
 # kernel-stats pass per library (headline, one batch in flight).  Usage: r05_vs_head.sh TAG "TESTS"
 export TMPDIR=/tmp
 TAG=$1; TESTS=$2
-A=orb-slam3-noted_amd/lib/libslamhot.so; B=orb-slam3-noted_amd/lib/ab/libslamhot_head.so
+A=orb-slam3-noted_amd/lib/libslamhot.so; B=${HEADLIB:-orb-slam3-noted_amd/lib/ab/libslamhot_head.so}
 timeout -k 10 500 python -u -m pytest $TESTS -x -q --timeout 120 --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1
 rc=$?; echo tests_exit=$rc; tail -2 gpurun_out/${TAG}_tests.log; [ $rc -ne 0 ] && exit $rc
 for i in 1 2 3; do
