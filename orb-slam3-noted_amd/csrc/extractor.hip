@@ -642,11 +642,15 @@ __device__ __forceinline__ void fast_cell(const Bufs& b, const DevPlan& P, const
         int na = 0;
         {
             const us2 T = {(unsigned short)t, (unsigned short)t};
+            // the lane's row walks down by rpi rows per iteration; rows past the tested region
+            // (m = 0) read the last tested row instead
             const int RS = lay.rs >> 2;
-            for (int rt = 0; rt < th; rt += rpi) {
-                const int r = rt + ar;
-                const uint32_t m = r < th ? cmask : 0u;
-                const uint32_t* row = roi32 + (min(r, th - 1) + 3) * RS + gd;
+            const uint32_t* row_it = roi32 + (ar + 3) * RS + gd;
+            const uint32_t* row_last = roi32 + (th + 2) * RS + gd;
+            for (int rt = 0; rt < th; rt += rpi, row_it += rpi * RS) {
+                const bool in = ar < th - rt;
+                const uint32_t m = in ? cmask : 0u;
+                const uint32_t* row = in ? row_it : row_last;
                 const uint32_t W0 = row[-1], W1 = row[0], W2 = row[1], U = row[-3 * RS], D = row[3 * RS];
                 auto set = [&](uint32_t v, uint32_t p0, uint32_t p8, uint32_t p4, uint32_t p12) -> uint32_t {
                     const us2 V = as_us2(v), a = as_us2(p0), bq = as_us2(p8), c = as_us2(p4), d = as_us2(p12);
@@ -909,7 +913,7 @@ __global__ void __launch_bounds__(64 * W) k_octree(Bufs b, int level0, int key_l
     const int l = level0 + blockIdx.x, f = blockIdx.y;
     const DevLevel& L = P.lv[l];
     const int MAXN = P.max_nodes;
-    const int tid = threadIdx.x, lane = tid & 63, wave = W == 1 ? 0 : tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = W == 1 ? 0 : __builtin_amdgcn_readfirstlane(tid >> 6);
     auto sync = [&]() {
         if constexpr (W == 1) wave_fence();
         else __syncthreads();

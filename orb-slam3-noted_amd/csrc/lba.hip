@@ -416,23 +416,38 @@ __device__ inline double wave_sum(double v) {
 }
 #endif
 
+// per-pose free-pose edge lists built on the device (k_setup_d); pls null: use pe
+struct PoseLists {
+    const int* pls;
+    const int* pbase;
+    const int* pcnt;
+    const WinDesc* wins;
+};
+
 // Pose side of buildSystem: one wave per free KeyFrame, lanes stride over its edges and
 // recompute error, robust weight and the pose Jacobian B; Hpp = sum B^T W B,
 // b_p = sum B^T (-rho' Omega e), then a butterfly reduction of the 27 sums.
+// The pose's edges in edge order: pe[pe_off[pose] ..] when the batch has followers (body edges: a
+// follower adds its own Hpp), else its free-pose edge list pls (k_setup_d: the leader edges in point order
+// = edge order), which is the same sequence and needs no host-built list.
 __device__ __forceinline__ void lin_poses_body(int pose, int lane, int npose_total, const int* __restrict__ pe_off,
-                                                   const int* __restrict__ pe, const int* __restrict__ pose_win,
+                                                   const int* __restrict__ pe, const PoseLists pl, const int* __restrict__ pose_win,
                                                    const EdgeS* __restrict__ E, const WinCtl* __restrict__ ctl,
                                                    const double* __restrict__ poses, const double* __restrict__ pts,
                                                    long long pose_stride, long long pt_stride, Cam cam, Huber hk,
                                                    double* __restrict__ Hpp, double* __restrict__ bp) {
     if (pose >= npose_total) return;
-    const WinCtl& C = ctl[pose_win[pose]];
+    const int win = pose_win[pose];
+    const WinCtl& C = ctl[win];
     if (!C.need_lin) return;
     double acc[27];
 #pragma unroll
     for (int k = 0; k < 27; k++) acc[k] = 0.0;
-    for (int i = pe_off[pose] + lane; i < pe_off[pose + 1]; i += 64) {
-        const EdgeS e = E[pe[i]];
+    const int* list = pl.pls ? pl.pls : pe;
+    const int i0 = pl.pls ? pl.wins[win].spe0 + pl.pbase[pose] : pe_off[pose];
+    const int i1 = pl.pls ? i0 + pl.pcnt[pose] : pe_off[pose + 1];
+    for (int i = i0 + lane; i < i1; i += 64) {
+        const EdgeS e = E[list[i]];
         const double* P = poses + C.sel * pose_stride + 8 * (long long)e.kf;
         const double* Xw = pts + C.sel * pt_stride + 4 * (long long)e.pt;
         const double X[3] = {Xw[0], Xw[1], Xw[2]};
@@ -486,7 +501,7 @@ __device__ __forceinline__ void lin_poses_body(int pose, int lane, int npose_tot
 // two per block; the long per-KF edge loops start first), the rest the point side.
 constexpr int kLinThreads = 128;
 __global__ void __launch_bounds__(kLinThreads) k_linearize(int nb_pose, int npose_total, const int* __restrict__ pe_off,
-                                                           const int* __restrict__ pe, const int* __restrict__ pose_win,
+                                                           const int* __restrict__ pe, PoseLists pl, const int* __restrict__ pose_win,
                                                            int npt_total, const int* __restrict__ pt_off,
                                                            const int* __restrict__ pt_win, const EdgeS* __restrict__ E,
                                                            const WinCtl* __restrict__ ctl, const double* __restrict__ poses,
@@ -499,7 +514,7 @@ __global__ void __launch_bounds__(kLinThreads) k_linearize(int nb_pose, int npos
     const int b = blockIdx.x;
     if (b < nb_pose)
         lin_poses_body(b * (kLinThreads / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), threadIdx.x & 63,
-                       npose_total, pe_off, pe,
+                       npose_total, pe_off, pe, pl,
                        pose_win, E, ctl, poses, pts, pose_stride, pt_stride, cam, hk, Hpp, bp);
     else
         lin_points_body((b - nb_pose) * kLinThreads + threadIdx.x, npt_total, pt_off, pt_win, E, ctl, poses, pts,
@@ -2378,7 +2393,10 @@ __device__ __forceinline__ void init_state_body(int t, int nkf_total, int npt_to
 // each in profiles/r04d_dropin_kernels.txt), and eleven launches became four plus k_ct_fill.
 struct SetupArgs {
     ClearList clear;
-    int nb_clear, nb_init, nb_spe, nb_blk, nb_list, nw_scan;
+    int nb_clear, nb_init, nb_spe, nb_blk, nb_list, nw_scan, nb_pts;
+    const int* pt_off;   // point CSR (edge ranges) and spe offsets, from the host plan
+    const int* spe_off;
+    int* spe_out;        // per-point free-pose edges sorted by pose, written by spe_build_body
     int nw, nkf, npt, nspe, nblk;
     const WinDesc* wins;
     WinCtl* ctl;
@@ -2403,11 +2421,37 @@ struct SetupArgs {
     int* ct_cnt;
     int* ct_off;
 };
-// clears | initial estimates | dense padding | optimize() start
+// thread per point: its free-pose leader edges (hp >= 0, not a body edge's follower: the edge right
+// after one of the same point on the same KeyFrame shares its Hpl block) in pose order, stably
+// (HplCCS column order: block_solver.hpp:381-481), and their free-pose indices
+__device__ __forceinline__ void spe_build_body(int p, int npt_total, const int* __restrict__ pt_off,
+                                               const int* __restrict__ spe_off, const EdgeS* __restrict__ E,
+                                               int* __restrict__ spe, int* __restrict__ spe_hp) {
+    if (p >= npt_total) return;
+    const int e0 = pt_off[p], e1 = pt_off[p + 1], s0 = spe_off[p];
+    int n = 0, prev_kf = -1;
+    for (int i = e0; i < e1; i++) {
+        const int kf = E[i].kf, hp = E[i].hp;
+        const bool follows = i > e0 && kf == prev_kf;
+        prev_kf = kf;
+        if (hp < 0 || follows) continue;
+        int j = n++;
+        for (; j > 0 && spe_hp[s0 + j - 1] > hp; j--) {
+            spe[s0 + j] = spe[s0 + j - 1];
+            spe_hp[s0 + j] = spe_hp[s0 + j - 1];
+        }
+        spe[s0 + j] = i;
+        spe_hp[s0 + j] = hp;
+    }
+}
+
+// clears | per-point pose-sorted edge lists | initial estimates | dense padding | optimize() start
 __global__ void __launch_bounds__(256) k_setup_a(SetupArgs a) {
     int b = blockIdx.x;
     if (b < a.nb_clear) return clear_body(a.clear, b, a.nb_clear);
     b -= a.nb_clear;
+    if (b < a.nb_pts) return spe_build_body(b * 256 + threadIdx.x, a.npt, a.pt_off, a.spe_off, a.E, a.spe_out, a.spe_hp);
+    b -= a.nb_pts;
     if (b < a.nb_init) return init_state_body(b * 256 + threadIdx.x, a.nkf, a.npt, a.kf_in, a.pt_in, a.poses, a.pts);
     b -= a.nb_init;
     if (b < a.nw) return ldlt_pad_body(b, a.wins, a.Hs);
@@ -2525,6 +2569,7 @@ struct PlanSizes {
     long long nbm = 0, nct = 0, hs_total = 0;
     int max_n = 0;
     bool any_body = false;
+    bool any_follow = false;           // some free-pose edge follows one of its point on its KeyFrame
     bool per_kf_cam = false;           // the KeyFrames of the batch do not share one calibration
     slam_camera cam{}, cam2{};         // the shared calibration otherwise
 };
@@ -2532,6 +2577,7 @@ struct PlanSizes {
 struct Layout {
     size_t edges, wins, ctl, pt_off, pt_win, spe_off, spe, pe_off, pe, pose_win, kf_hp, kf_win, blk_win,
         blk_order, blk_pose, kf_in, pt_in, kf_trl, kcam, kbf, total;
+    size_t host_bytes;  // the host-written prefix (the device-built spe lists come last)
 };
 
 Layout make_layout(const PlanSizes& z) {
@@ -2548,7 +2594,6 @@ Layout make_layout(const PlanSizes& z) {
     L.pt_off = take(sizeof(int) * (z.npt + 1));
     L.pt_win = take(sizeof(int) * z.npt);
     L.spe_off = take(sizeof(int) * (z.npt + 1));
-    L.spe = take(sizeof(int) * z.nspe);
     L.pe_off = take(sizeof(int) * (z.npose + 1));
     L.pe = take(sizeof(int) * z.npe);
     L.pose_win = take(sizeof(int) * z.npose);
@@ -2562,6 +2607,8 @@ Layout make_layout(const PlanSizes& z) {
     L.kf_trl = take(z.any_body ? sizeof(double) * 8 * z.nkf : 0);
     L.kcam = take(z.per_kf_cam ? sizeof(float4) * 2 * z.nkf : 0);
     L.kbf = take(z.per_kf_cam ? sizeof(float) * z.nkf : 0);
+    L.host_bytes = off;
+    L.spe = take(sizeof(int) * z.nspe);
     L.total = off;
     return L;
 }
@@ -2649,7 +2696,11 @@ slam_status plan_sizes(int n_prob, const slam_lba_problem* probs, PlanSizes& z, 
         bool body = false;
     };
     std::vector<WinSz> sz(n_prob);
-    slam_status st = for_windows<std::vector<int>>(n_prob, plan_threads(n_prob), [&](int w, std::vector<int>& cnt) {
+    struct SizeScratch {
+        std::vector<int> cnt, stamp;
+    };
+    slam_status st = for_windows<SizeScratch>(n_prob, plan_threads(n_prob), [&](int w, SizeScratch& sc) {
+        std::vector<int>& cnt = sc.cnt;
         const slam_lba_problem& P = probs[w];
         if ((P.n_kf && (!P.kf_Tcw || !P.kf_fixed)) || (P.n_pt && !P.pt_pos) ||
             (P.n_edge && (!P.edge_pt || !P.edge_kf || !P.edge_obs || !P.edge_inv_sigma2)))
@@ -2678,6 +2729,10 @@ slam_status plan_sizes(int n_prob, const slam_lba_problem* probs, PlanSizes& z, 
         // free-pose edges; an edge right after one of the same point on the same KeyFrame (body
         // edge) shares its Hpl block and has no Schur entry of its own.  A point with k such
         // edges adds k (k + 1) / 2 Schur contributions.
+        // Two such edges of one point on one KeyFrame that are not adjacent are refused (a
+        // KeyFrame stamp per point).
+        std::vector<int>& stamp = sc.stamp;
+        stamp.assign(P.n_kf, 0);
         int run = 0;
         for (int i = 0; i <= P.n_edge; i++) {
             if (i == P.n_edge || (i > 0 && P.edge_pt[i] != P.edge_pt[i - 1])) {
@@ -2687,6 +2742,9 @@ slam_status plan_sizes(int n_prob, const slam_lba_problem* probs, PlanSizes& z, 
             if (i == P.n_edge || hidx[P.edge_kf[i]] < 0) continue;
             S.npe++;
             if (!(i > 0 && P.edge_pt[i - 1] == P.edge_pt[i] && P.edge_kf[i - 1] == P.edge_kf[i])) {
+                const int k = P.edge_kf[i];
+                if (stamp[k] == P.edge_pt[i] + 1) return SLAM_EINVAL;  // non-adjacent edges of 1 point in 1 KF
+                stamp[k] = P.edge_pt[i] + 1;
                 S.nspe++;
                 run++;
             }
@@ -2695,12 +2753,15 @@ slam_status plan_sizes(int n_prob, const slam_lba_problem* probs, PlanSizes& z, 
     });
     if (st != SLAM_OK) return st;
     for (int w = 0; w < n_prob; w++) {
+        z.any_body = z.any_body || sz[w].body;
+        z.any_follow = z.any_follow || sz[w].npe != sz[w].nspe;
+    }
+    for (int w = 0; w < n_prob; w++) {
         const slam_lba_problem& P = probs[w];
         const int np = np_of[w];
         z.starts[w] = WinStart{z.nkf, z.npt, z.ne, z.npose, z.nblk, z.nspe, z.npe, z.nbm, z.nct, z.hs_total, z.starts[w].h0};
-        z.any_body = z.any_body || sz[w].body;
         z.nct += sz[w].nct;
-        z.npe += sz[w].npe;
+        if (z.any_follow) z.npe += sz[w].npe;  // pe is built only for batches with followers
         z.nspe += sz[w].nspe;
         z.nbm += (long long)np * ((P.n_pt + 63) / 64);
         z.nkf += P.n_kf;
@@ -2743,7 +2804,7 @@ slam_status plan_fill(int n_prob, const slam_lba_problem* probs, const std::vect
 #else
 #define PB_MARK(k) do {} while (0)
 #endif
-    auto fill_one = [&](int w, std::vector<int>& col, std::vector<int>& pcnt) -> slam_status {
+    auto fill_one = [&](int w, std::vector<int>& pcnt) -> slam_status {
 #ifdef SLAMHOT_PLAN_BENCH
         long long pb_t = (long long)__rdtsc();
 #endif
@@ -2832,27 +2893,18 @@ slam_status plan_fill(int n_prob, const slam_lba_problem* probs, const std::vect
             e.info = Q.edge_inv_sigma2[i];
         }
         PB_MARK(1);
-        // point CSR + per-point free-pose edges sorted by pose (HplCCS column order)
+        // point CSR and the offsets of the per-point free-pose edge lists (the lists themselves,
+        // sorted by pose, are built on the device: spe_build_body)
         const int pe_start = ws.pe0;
-        pcnt.assign(np + 1, 0);
         int i = 0;
         for (int p = 0; p < Q.n_pt; p++) {
             P.pt_off[npt + p] = ne + i;
             P.pt_win[npt + p] = w;
             P.spe_off[npt + p] = nspe;
-            col.clear();
             for (; i < Q.n_edge && Q.edge_pt[i] == p; i++) {
                 // the edge right after one on the same KeyFrame (body edge) shares its Hpl block
                 const bool follows = i > 0 && Q.edge_pt[i - 1] == p && Q.edge_kf[i - 1] == Q.edge_kf[i];
-                if (hidx[Q.edge_kf[i]] >= 0 && !follows) col.push_back(i);
-            }
-            for (size_t x = 1; x < col.size(); x++)  // stable insertion sort by pose
-                for (size_t y = x; y > 0 && hidx[Q.edge_kf[col[y - 1]]] > hidx[Q.edge_kf[col[y]]]; y--)
-                    std::swap(col[y - 1], col[y]);
-            for (size_t x = 0; x < col.size(); x++) {
-                const int i1 = hidx[Q.edge_kf[col[x]]];
-                if (x && i1 == hidx[Q.edge_kf[col[x - 1]]]) return SLAM_EINVAL;  // non-adjacent edges of 1 point in 1 KF
-                P.spe[nspe++] = ne + col[x];
+                nspe += hidx[Q.edge_kf[i]] >= 0 && !follows;
             }
         }
         PB_MARK(2);
@@ -2867,29 +2919,31 @@ slam_status plan_fill(int n_prob, const slam_lba_problem* probs, const std::vect
                 else P.blk_order[Z.npose + (nblk - npose) + (b - i2)] = nblk + b;
             }
         PB_MARK(3);
-        // edges of every free pose (followers included: each adds its own Hpp), insertion order
-        for (int e = 0; e < Q.n_edge; e++) {
-            const int h = hidx[Q.edge_kf[e]];
-            if (h >= 0) pcnt[h + 1]++;
-        }
-        for (int k = 0; k < np; k++) pcnt[k + 1] += pcnt[k];
-        for (int k = 0; k < np; k++) {
-            P.pe_off[npose + k] = pe_start + pcnt[k];
-            P.pose_win[npose + k] = w;
-        }
-        for (int e = 0; e < Q.n_edge; e++) {
-            const int h = hidx[Q.edge_kf[e]];
-            if (h >= 0) P.pe[pe_start + pcnt[h]++] = ne + e;
+        for (int k = 0; k < np; k++) P.pose_win[npose + k] = w;
+        // with followers (body edges): the edges of every free pose (followers included: each adds
+        // its own Hpp), insertion order; otherwise the pose side reads the device-built pose lists
+        if (Z.any_follow) {
+            pcnt.assign(np + 1, 0);
+            for (int e = 0; e < Q.n_edge; e++) {
+                const int h = hidx[Q.edge_kf[e]];
+                if (h >= 0) pcnt[h + 1]++;
+            }
+            for (int k = 0; k < np; k++) pcnt[k + 1] += pcnt[k];
+            for (int k = 0; k < np; k++) P.pe_off[npose + k] = pe_start + pcnt[k];
+            for (int e = 0; e < Q.n_edge; e++) {
+                const int h = hidx[Q.edge_kf[e]];
+                if (h >= 0) P.pe[pe_start + pcnt[h]++] = ne + e;
+            }
         }
         PB_MARK(4);
         (void)nkf;
         return SLAM_OK;
     };
     struct FillScratch {
-        std::vector<int> col, pcnt;
+        std::vector<int> pcnt;
     };
     const slam_status st = for_windows<FillScratch>(n_prob, plan_threads(n_prob), [&](int w, FillScratch& sc) {
-        return fill_one(w, sc.col, sc.pcnt);
+        return fill_one(w, sc.pcnt);
     });
     if (st != SLAM_OK) return st;
 #ifdef SLAMHOT_PLAN_BENCH
@@ -2899,7 +2953,7 @@ slam_status plan_fill(int n_prob, const slam_lba_problem* probs, const std::vect
 #undef PB_MARK
     P.pt_off[Z.npt] = Z.ne;
     P.spe_off[Z.npt] = Z.nspe;
-    P.pe_off[Z.npose] = Z.npe;
+    if (Z.any_follow) P.pe_off[Z.npose] = Z.npe;
     return SLAM_OK;
 }
 
@@ -3093,7 +3147,7 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
                      std::chrono::duration<double, std::milli>(t1 - t_fill0).count(), LY.total / 1e6);
     }
     SLAM_HIP_TRY(s->arena.ensure(LY.total));
-    SLAM_HIP_TRY(hipMemcpyAsync(s->arena.p, s->harena, LY.total, hipMemcpyHostToDevice, S));
+    SLAM_HIP_TRY(hipMemcpyAsync(s->arena.p, s->harena, LY.host_bytes, hipMemcpyHostToDevice, S));
     const Plan DP = bind((unsigned char*)s->arena.p, LY);
     struct {
         int nkf, npt, ne, npose, nblk;
@@ -3212,6 +3266,10 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     {
         auto cdiv = [](long long n, int t) { return (int)((n + t - 1) / t); };
         SA.nb_init = cdiv(H.nkf + H.npt, 256);
+        SA.nb_pts = cdiv(H.npt, 256);
+        SA.pt_off = DP.pt_off;
+        SA.spe_off = DP.spe_off;
+        SA.spe_out = DP.spe;
         SA.nb_spe = cdiv(Z.nspe, 256);
         SA.nb_blk = cdiv(H.nblk, 256);
         SA.nb_list = cdiv(Z.nspe, kCtScanThreads);
@@ -3248,7 +3306,7 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
         // (a) clears, initial estimates, dense padding, optimize() start; (b) pose bitmaps and tile
         // padding; (c) bitmap prefixes / pose list bases (pose list lengths even without edges) and
         // contribution counts; (d) contribution offsets and pose edge lists; then the lists
-        k_setup_a<<<SA.nb_clear + SA.nb_init + nw + cdiv(nw, 256), 256, 0, S>>>(SA);
+        k_setup_a<<<SA.nb_clear + SA.nb_pts + SA.nb_init + nw + cdiv(nw, 256), 256, 0, S>>>(SA);
         const int nb_b = SA.nb_spe + (use_t16 ? nw : 0);
         if (nb_b) k_setup_b<<<nb_b, 256, 0, S>>>(SA);
         k_setup_c<<<nw + SA.nb_blk, 256, 0, S>>>(SA);
@@ -3297,9 +3355,12 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     const int nb_schur = nb_sdiag + (H.nblk - H.npose + 256 / kSchurLanes - 1) / (256 / kSchurLanes);
     const int nb_kf = (H.nkf + 255) / 256;
     const int nb_upd = nb_kf + (H.npt + 255) / 256;
+    // the pose side's edge lists: the device-built pls unless the batch has followers (pe)
+    const PoseLists pose_lists = Z.any_follow ? PoseLists{nullptr, nullptr, nullptr, nullptr}
+                                            : PoseLists{as<int>(s->pls), as<int>(s->pbase), as<int>(s->pcnt), dW};
     auto launch_step = [&](int slot, int seq) -> hipError_t {
         if (nb_lin)
-            k_linearize<<<nb_lin, kLinThreads, 0, S>>>(nb_lin_pose, H.npose, DP.pe_off, DP.pe, DP.pose_win, H.npt,
+            k_linearize<<<nb_lin, kLinThreads, 0, S>>>(nb_lin_pose, H.npose, DP.pe_off, DP.pe, pose_lists, DP.pose_win, H.npt,
                                                        DP.pt_off, DP.pt_win, dE, dC, poses, pts, pose_stride,
                                                        pt_stride, cam, hk, as<double>(s->err), as<double>(s->rho),
                                                        as<double>(s->lin), as<double>(s->Hll), as<double>(s->bl),

@@ -239,7 +239,8 @@ __global__ void __launch_bounds__(kBowThreads) k_bow_match(const DevBowPair* pai
     if (pr.general) return;  // k_bow_match_any's pair
     const DevBowSide& A = pr.A;
     const DevBowSide& B = pr.B;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;
+    // wave index via v_readfirstlane: wave-uniform, so the per-node records load into SGPRs
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), nwaves = blockDim.x >> 6;
     for (int i = tid; i < A.n; i += blockDim.x) {
         matchA[i] = -1;
         binA[i] = -1;
@@ -270,6 +271,9 @@ __global__ void __launch_bounds__(kBowThreads) k_bow_match(const DevBowPair* pai
         const int a0 = A.node_off[ia], a1 = A.node_off[ia + 1];
         const int b0 = B.node_off[ib], b1 = B.node_off[ib + 1];
         const int nbn = min(b1 - b0, 64 * kBowNodeChunks);
+        // chunks holding candidates (wave-uniform): most vocabulary nodes hold a few features, so
+        // the distance sweeps below skip the empty chunks instead of evaluating all four
+        const int nch = __builtin_amdgcn_readfirstlane((nbn + 63) >> 6);
         // this lane's B candidates: descriptor, index, validity, taken flag
         uint4 bd0[kBowNodeChunks], bd1[kBowNodeChunks];
         int bidx[kBowNodeChunks];
@@ -313,6 +317,8 @@ __global__ void __launch_bounds__(kBowThreads) k_bow_match(const DevBowPair* pai
             uint32_t bestkey = 0xFFFFFFFFu;
 #pragma unroll
             for (int k = 0; k < kBowNodeChunks; k++) {
+                dist[k] = 1024;
+                if (k >= nch) continue;
                 dist[k] = bok[k] ? hamming32(q0, q1, bd0[k], bd1[k]) : 1024;
                 const uint32_t key = bok[k] ? (((uint32_t)dist[k] << 16) | (uint32_t)(64 * k + lane)) : 0xFFFFFFFFu;
                 bestkey = min(bestkey, key);
@@ -323,7 +329,7 @@ __global__ void __launch_bounds__(kBowThreads) k_bow_match(const DevBowPair* pai
             int sec = 256;
 #pragma unroll
             for (int k = 0; k < kBowNodeChunks; k++)
-                if (bok[k] && (64 * k + lane) != bpos) sec = min(sec, dist[k]);
+                if (k < nch && bok[k] && (64 * k + lane) != bpos) sec = min(sec, dist[k]);
             sec = (int)wave_min_u32((uint32_t)sec);
             const bool pass = (strict ? best1 < 50 : best1 <= 50) && ((float)best1 < nnratio * (float)sec);
             if (pass) {
@@ -385,7 +391,8 @@ __global__ void __launch_bounds__(512) k_bow_match_any(const DevBowPair* pairs, 
     const DevBowPair pr = pairs[blockIdx.x];
     const DevBowSide& A = pr.A;
     const DevBowSide& B = pr.B;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;
+    // wave index via v_readfirstlane: wave-uniform, so the per-node records load into SGPRs
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), nwaves = blockDim.x >> 6;
     for (int i = tid; i < A.n; i += blockDim.x) {
         pr.a2b[i] = -1;
         pr.bins[i] = -1;

@@ -130,6 +130,23 @@ def test_lba_rejects_bad_input(solver):
     bad = dict(W, edge_kf=np.full_like(W["edge_kf"], 99))
     with pytest.raises(slamhot.SlamError):
         solver.solve(bad)
+    # a point seen twice by one free KeyFrame through non-adjacent edges (g2o would add two
+    # Hessian blocks for one (pose, point) pair): refused by the host plan's KeyFrame stamps
+    ekf = W["edge_kf"].copy()
+    ept = W["edge_pt"]
+    p0 = np.nonzero(np.bincount(ept) >= 3)[0][0]
+    e = np.nonzero(ept == p0)[0]
+    free = np.nonzero(W["kf_fixed"] == 0)[0]
+    k = ekf[e[0]] if W["kf_fixed"][ekf[e[0]]] == 0 else free[0]
+    ekf[e[0]] = ekf[e[2]] = k
+    ekf[e[1]] = next(x for x in range(len(W["kf_fixed"])) if x != k)
+    bad = dict(W, edge_kf=ekf)
+    with pytest.raises(slamhot.SlamError):
+        solver.solve(bad)
+    # the same three edges with the repeated KeyFrame adjacent (a body edge's follower) pass
+    ekf2 = ekf.copy()
+    ekf2[e[1]], ekf2[e[2]] = ekf[e[2]], ekf[e[1]]
+    solver.solve(dict(W, edge_kf=ekf2))
 
 
 def test_lba_deterministic(solver):
