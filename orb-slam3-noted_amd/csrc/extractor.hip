@@ -1122,9 +1122,67 @@ __global__ void __launch_bounds__(64 * W) k_octree(Bufs b, int level0, int key_l
                 }
             } else {
                 // careful phase: E = children of the last pass with >1 key, ordered by
-                // (size desc, sequence desc) = (cnt desc, position asc) inside [0, tprev)
+                // (size desc, sequence desc) = (cnt desc, position asc) inside [0, tprev).
+                // rank(i) = #{j : c_j > c_i} + #{j < i : c_j == c_i}: a counting sort when the
+                // counts are below MAXN -- histogram H (in `best`, free until the end) turned into
+                // suffix sums, E (in `oarr`, free until the children offsets) the count of each
+                // value in earlier blocks, and inside a block one ballot per distinct value --
+                // instead of comparing every pair (tprev^2 / 64 readlane steps, most of this
+                // phase's ~50k cycles at the fine levels)
                 int ne = 0;
+                int maxc = 0;
                 for (int ib = 0; ib < tprev; ib += 64) {
+                    const int i = ib + lane;
+                    const int ci = i < tprev ? A.cnt[i] : 0;
+                    maxc = max(maxc, ci);
+                }
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) maxc = max(maxc, __shfl_xor(maxc, o, 64));
+                const bool counting = maxc < MAXN;
+                if (counting) {
+                    int* H = reinterpret_cast<int*>(best);
+                    int* Ecnt = reinterpret_cast<int*>(oarr);
+                    for (int v = lane; v <= maxc; v += 64) { H[v] = 0; Ecnt[v] = 0; }
+                    wave_fence();
+                    for (int ib = 0; ib < tprev; ib += 64) {
+                        const int i = ib + lane;
+                        const int ci = i < tprev ? A.cnt[i] : 0;
+                        if (ci > 1) atomicAdd(&H[ci], 1);
+                    }
+                    wave_fence();
+                    // H[v] <- #{candidates with count > v}: lane order = descending v
+                    int carry = 0;
+                    for (int base = 0; base <= maxc; base += 64) {
+                        const int v = maxc - (base + lane);
+                        const int h = v >= 0 ? H[v] : 0;
+                        int tot;
+                        const int ex = wave_scan_excl(h, &tot);
+                        wave_fence();
+                        if (v >= 0) H[v] = carry + ex;
+                        carry += tot;
+                    }
+                    wave_fence();
+                    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+                    for (int ib = 0; ib < tprev; ib += 64) {
+                        const int i = ib + lane;
+                        const int ci = i < tprev ? A.cnt[i] : 0;
+                        uint64_t rem = __ballot(ci > 1);
+                        ne += __popcll(rem);
+                        int r = 0;
+                        while (rem) {
+                            const int v = __builtin_amdgcn_readlane(ci, __ffsll((long long)rem) - 1);
+                            const uint64_t m = __ballot(ci == v);
+                            const int before = Ecnt[v];
+                            if ((m >> lane) & 1) r = H[v] + before + __popcll(m & lt);
+                            wave_fence();
+                            if (lane == 0) Ecnt[v] = before + __popcll(m);
+                            wave_fence();
+                            rem &= ~m;
+                        }
+                        if (ci > 1) ord[r] = (uint16_t)i;
+                    }
+                }
+                for (int ib = 0; ib < tprev && !counting; ib += 64) {
                     const int i = ib + lane;
                     const int ci = i < tprev ? A.cnt[i] : 0;
                     const uint64_t mi = __ballot(ci > 1);
@@ -2093,6 +2151,7 @@ static slam_status launch_range(slam_extractor* ex, int f0, int nframes, const u
     // read per call (a handle's captured graphs keep the setting they were captured with)
     const bool oct_multi_small = env_flag("SLAMHOT_OCT_SMALL", true);
     const bool oct_multi_l0 = env_flag("SLAMHOT_OCT_L0", false);
+    const bool oct_multi_rest = env_flag("SLAMHOT_OCT_REST", false);  // levels 1-7 group multi-wave (A/B)
     hipEvent_t e0 = nullptr;
     auto begin = [&](int, hipStream_t st_ = nullptr) {
         if (ex->profiling) { e0 = ex->ev(); (void)hipEventRecord(e0, st_ ? st_ : s); }
@@ -2158,7 +2217,7 @@ static slam_status launch_range(slam_extractor* ex, int f0, int nframes, const u
         const slam_extractor::OctGroup& G = small ? ex->oct_small : ex->oct[g];
         // the per-image call (small batches) and, for large batches, level 0 run the multi-wave
         // form; levels 1-7 of large batches one wave per (frame, level)
-        if (small ? oct_multi_small : (G.l0 == 0 && oct_multi_l0))
+        if (small ? oct_multi_small : (G.l0 == 0 ? oct_multi_l0 : oct_multi_rest))
             hipLaunchKernelGGL(k_octree<kOctWaves>, dim3(G.nl, nframes), dim3(64 * kOctWaves), G.lds, s, b, G.l0,
                                G.keycap, ex->octree_max_cells);
         else
