@@ -1168,18 +1168,19 @@ __global__ void __launch_bounds__(64 * W) k_octree(Bufs b, int level0, int key_l
                         const int ci = i < tprev ? A.cnt[i] : 0;
                         uint64_t rem = __ballot(ci > 1);
                         ne += __popcll(rem);
-                        int r = 0;
+                        // larger counts + equal counts of earlier blocks, then equal counts of
+                        // lower lanes (one ballot per distinct value in the block, no LDS)
+                        int r = ci > 1 ? H[ci] + Ecnt[ci] : 0;
                         while (rem) {
                             const int v = __builtin_amdgcn_readlane(ci, __ffsll((long long)rem) - 1);
                             const uint64_t m = __ballot(ci == v);
-                            const int before = Ecnt[v];
-                            if ((m >> lane) & 1) r = H[v] + before + __popcll(m & lt);
-                            wave_fence();
-                            if (lane == 0) Ecnt[v] = before + __popcll(m);
-                            wave_fence();
+                            if ((m >> lane) & 1) r += __popcll(m & lt);
                             rem &= ~m;
                         }
                         if (ci > 1) ord[r] = (uint16_t)i;
+                        wave_fence();
+                        if (ci > 1) atomicAdd(&Ecnt[ci], 1);
+                        wave_fence();
                     }
                 }
                 for (int ib = 0; ib < tprev && !counting; ib += 64) {
