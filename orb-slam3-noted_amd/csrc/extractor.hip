@@ -210,17 +210,18 @@ __device__ __forceinline__ void stage_u32(uint32_t* dst, int dstride, const uint
 
 
 // ---------------------------------------------------------------------------------------
-// k_resize4: the resize with its coefficients recomputed in the reference's own arithmetic
-// (double (dx+0.5)*scale-0.5 -> float, cvFloor, saturate_cast<short> by round-half-even)
-// instead of gathered from tables: bit-identical to the host plan (table gathers bound an
-// earlier version: microbench 199 -> 74 us at L1).  Thread = 4 output columns x kRzRows
-// output rows: the four column coefficients (the FP64 part) are computed once, and a source
-// row loaded for output row y is reused for row y+1 when its vertical pair starts there
-// (scale 1.2: most rows).  Byte loads: a wave's 64 quads coalesce into row segments.
+// k_resize4: cv::resize INTER_LINEAR (OpenCV 4.2.0 fixed point 2^11) from the host plan's
+// coefficient tables (extractor_plan.hpp build_resize_tables, the reference's own arithmetic).
+// Thread = 4 output columns x kRzRows output rows: its four columns are two 16-byte table loads
+// and each row one (per-level tables padded to a multiple of 4).  An early version gathered the
+// entries one by one per pixel and was bound by it (microbench 199 -> 74 us at L1 when the
+// coefficients were recomputed per thread in FP64 instead); the quad loads replace that
+// per-thread FP64 math (round 5: stage 0.131 -> 0.126 ms per batch).  A source row loaded for
+// output row y is reused for row y+1 when its vertical pair starts there (scale 1.2: most rows).
 // ---------------------------------------------------------------------------------------
 constexpr int kRzRows = 4;
 
-__global__ void __launch_bounds__(256) k_resize4(Bufs b, int l, double scale_x, double scale_y) {
+__global__ void __launch_bounds__(256) k_resize4(Bufs b, int l) {
     const DevPlan& P = *b.plan;
     const DevLevel& L = P.lv[l];
     const DevLevel& S = P.lv[l - 1];
@@ -232,21 +233,23 @@ __global__ void __launch_bounds__(256) k_resize4(Bufs b, int l, double scale_x, 
     const int rb = i / qw, q = i - rb * qw;
     const uint8_t* src = level_ptr(b, P, f, l - 1);
     const int spitch = level_pitch(P, l - 1);
+    // the four columns' (sx, a0, a1) from the level's coefficient table (the host plan's
+    // OpenCV arithmetic, padded per level so a quad is two 16-byte loads; columns past the edge
+    // repeat the last one, as the clamped dx did): no per-thread FP64 coefficient math
     int sxs[4], a0s[4], a1s[4];
+    {
+        const uint4* xq = reinterpret_cast<const uint4*>(b.xtab + L.xtab_off + 4 * q);
+        const uint4 x01 = xq[0], x23 = xq[1];
+        const uint32_t sx4[4] = {x01.x, x01.z, x23.x, x23.z}, aa4[4] = {x01.y, x01.w, x23.y, x23.w};
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int dx = min(4 * q + k, L.w - 1);
-        float fx = (float)((dx + 0.5) * scale_x - 0.5);
-        int sx = (int)floorf(fx);
-        fx -= (float)sx;
-        if (sx < 0) { fx = 0.f; sx = 0; }
-        if (sx >= S.w - 1) { fx = 0.f; sx = S.w - 1; }
-        int a0 = (int)rintf((1.f - fx) * 2048), a1 = (int)rintf(fx * 2048);
-        if (dx >= L.xmax) { a0 = 2048; a1 = 0; }  // HResizeLinear tail: S[sx] * 2048
-        sxs[k] = sx;
-        a0s[k] = a0;
-        a1s[k] = a1;
+        for (int k = 0; k < 4; k++) {
+            sxs[k] = (int)sx4[k];
+            a0s[k] = (int)(aa4[k] & 0xFFFF);
+            a1s[k] = (int)(aa4[k] >> 16);
+        }
     }
+    // the thread's rows: (y0, y1, b0 | b1 << 16) per output row, one 16-byte load each
+    const uint4* yq = reinterpret_cast<const uint4*>(b.ytab + L.ytab_off) + rb * kRzRows;
     // horizontal pass of one source row (HResizeLinear): D[k] = S[sx]*a0 + S[sx+1]*a1.
     // Dword form: the thread's eight source bytes sx_k, sx_k + 1 lie in the 12 bytes from
     // xb = sx_0 & ~3 when sx_3 + 1 - xb <= 11 (scale factors up to ~2.5): three dword buffer loads
@@ -298,12 +301,10 @@ __global__ void __launch_bounds__(256) k_resize4(Bufs b, int l, double scale_x, 
     for (int rr = 0; rr < kRzRows; rr++) {
         const int dy = rb * kRzRows + rr;
         if (dy >= L.h) break;
-        float fy = (float)((dy + 0.5) * scale_y - 0.5);
-        const int sy = (int)floorf(fy);
-        fy -= (float)sy;
-        const int b0 = (int)rintf((1.f - fy) * 2048), b1 = (int)rintf(fy * 2048);
         // rows are clamped (VResizeLinear reads clip(sy+k, 0, h-1)); reuse by clamped index
-        const int y0 = min(max(sy, 0), S.h - 1), y1 = min(max(sy + 1, 0), S.h - 1);
+        const uint4 yt = yq[rr];
+        const int y0 = (int)yt.x, y1 = (int)yt.y;
+        const int b0 = (int)(yt.z & 0xFFFF), b1 = (int)(yt.z >> 16);
         if (have == y0) {
 #pragma unroll
             for (int k = 0; k < 4; k++) D0[k] = D1[k];
@@ -2178,10 +2179,8 @@ static slam_status launch_range(slam_extractor* ex, int f0, int nframes, const u
     begin(kStResize);
     for (int l = 1; l < P.nlevels && !SKIP(kStResize); l++) {
         const int qw = (P.lv[l].w + 3) / 4;
-        const double sxv = 1. / ((double)P.lv[l].w / P.lv[l - 1].w);
-        const double syv = 1. / ((double)P.lv[l].h / P.lv[l - 1].h);
         const int nrb = (P.lv[l].h + kRzRows - 1) / kRzRows;
-        hipLaunchKernelGGL(k_resize4, dim3((qw * nrb + 255) / 256, nframes), dim3(256), 0, s, b, l, sxv, syv);
+        hipLaunchKernelGGL(k_resize4, dim3((qw * nrb + 255) / 256, nframes), dim3(256), 0, s, b, l);
     }
     end(kStResize);
     // ranges run FAST one after another (each fills the chip); a range's octree / layout /
