@@ -19,6 +19,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <type_traits>
 #include <vector>
 
 #include "common.hpp"
@@ -597,9 +598,10 @@ __device__ __forceinline__ void fast_cell(const Bufs& b, const DevPlan& P, const
 #endif
     FAST_MARK();
     {
-        uint32_t* m32 = reinterpret_cast<uint32_t*>(map);
-        const int nw = ((th + 2) * lay.ms + 3) >> 2;
-        for (int i = lane; i < nw; i += 64) m32[i] = 0;
+        // 16-byte stores, rounded up into the list region (r16-aligned, written before it is read)
+        uint4* m128 = reinterpret_cast<uint4*>(map);
+        const int nq = ((th + 2) * lay.ms + 15) >> 4;
+        for (int i = lane; i < nq; i += 64) m128[i] = uint4{0u, 0u, 0u, 0u};
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 
@@ -632,51 +634,91 @@ __device__ __forceinline__ void fast_cell(const Bufs& b, const DevPlan& P, const
         mx = max(mx, max(max(sc(q[1]), sc(q[MS - 1])), max(sc(q[MS]), sc(q[MS + 1]))));
         return (M > t) & (M - 1 > mx);
     };
-    for (int attempt = 0; attempt < 2; attempt++) {
-        const int t = attempt == 0 ? ti : tm;
-        FAST_MARK();
-        // pass A, four pixels per lane in packed u16 pairs (even / odd bytes of an LDS dword).
-        // Lane = (row, dword group) over the dwords covering the tested columns; the compass
-        // test per pixel is  min(p0,p8), min(p4,p12) < v - t  (dark) or  max(..) > v + t
-        // (bright), i.e. saturating (v - t - max of the mins) | (min of the maxes - v - t) != 0.
-        // Four ballots (one per byte) + mbcnt give row-major compaction.
+    // Compass-score cache for the second attempt: attempt 1 keeps each lane's per-pixel compass
+    // scores s = max(v - L, H - v) (the largest t the pixel passes at, one byte each, one dword per
+    // lane and pass-A iteration) at the END of the list region, while its list grows from the start;
+    // attempt 2 (minThFAST, about half the cells) reads them back instead of re-deriving them from
+    // the ROI.  Valid when attempt 1's list stayed below them (2 * na <= s_off, checked before every
+    // store, so a store never lands on the list); attempt 2 checks before each iteration's list
+    // writes that the list stays below the scores it has not read yet, and otherwise runs pass A
+    // again from the ROI.  All the conditions are wave-uniform.
+    const int nit = (th + rpi - 1) / rpi;
+    const int s_off = (lay.total - lay.lst) - nit * 256;  // bytes from lst (multiple of 16), < 0: no room
+    uint32_t* const scache = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(lst) + s_off) + lane;
+    // pass A, four pixels per lane in packed u16 pairs (even / odd bytes of an LDS dword).
+    // Lane = (row, dword group) over the dwords covering the tested columns; the compass
+    // test per pixel is  min(p0,p8), min(p4,p12) < v - t  (dark) or  max(..) > v + t
+    // (bright), i.e. s = max(v - max of the mins, min of the maxes - v) > t (saturating u16).
+    // Four ballots (one per byte) + mbcnt give row-major compaction.  Returns the list length,
+    // or -1 when a cached pass would overwrite scores it has not read yet.
+    auto pass_a = [&](auto from_cache_c, auto keep_s_c, int t) -> int {
+        constexpr bool from_cache = decltype(from_cache_c)::value, keep_s = decltype(keep_s_c)::value;
+        const us2 T = {(unsigned short)t, (unsigned short)t};
+        // the lane's row walks down by rpi rows per iteration; rows past the tested region
+        // (m = 0) read the last tested row instead
+        const int RS = lay.rs >> 2;
+        const uint32_t* row_it = roi32 + (ar + 3) * RS + gd;
+        const uint32_t* row_last = roi32 + (th + 2) * RS + gd;
+        uint32_t* sp = scache;
+        int s_next = s_off + 256;  // where the scores of the iterations after this one start
         int na = 0;
-        {
-            const us2 T = {(unsigned short)t, (unsigned short)t};
-            // the lane's row walks down by rpi rows per iteration; rows past the tested region
-            // (m = 0) read the last tested row instead
-            const int RS = lay.rs >> 2;
-            const uint32_t* row_it = roi32 + (ar + 3) * RS + gd;
-            const uint32_t* row_last = roi32 + (th + 2) * RS + gd;
-            for (int rt = 0; rt < th; rt += rpi, row_it += rpi * RS) {
-                const bool in = ar < th - rt;
-                const uint32_t m = in ? cmask : 0u;
+        for (int rt = 0; rt < th; rt += rpi, row_it += rpi * RS, sp += 64, s_next += 256) {
+            const bool in = ar < th - rt;
+            const uint32_t m = in ? cmask : 0u;
+            us2 se, so;  // compass scores of the even / odd bytes
+            if constexpr (from_cache) {
+                const uint32_t S = *sp;  // byte k = pixel k
+                se = as_us2(__builtin_amdgcn_perm(0u, S, 0x0c020c00u));
+                so = as_us2(__builtin_amdgcn_perm(0u, S, 0x0c030c01u));
+            } else {
                 const uint32_t* row = in ? row_it : row_last;
                 const uint32_t W0 = row[-1], W1 = row[0], W2 = row[1], U = row[-3 * RS], D = row[3 * RS];
-                auto set = [&](uint32_t v, uint32_t p0, uint32_t p8, uint32_t p4, uint32_t p12) -> uint32_t {
+                auto score = [&](uint32_t v, uint32_t p0, uint32_t p8, uint32_t p4, uint32_t p12) -> us2 {
                     const us2 V = as_us2(v), a = as_us2(p0), bq = as_us2(p8), c = as_us2(p4), d = as_us2(p12);
                     const us2 L = __builtin_elementwise_max(__builtin_elementwise_min(a, bq), __builtin_elementwise_min(c, d));
                     const us2 H = __builtin_elementwise_min(__builtin_elementwise_max(a, bq), __builtin_elementwise_max(c, d));
-                    return as_u32(__builtin_elementwise_sub_sat(V, L + T) | __builtin_elementwise_sub_sat(H, V + T));
+                    return __builtin_elementwise_max(__builtin_elementwise_sub_sat(V, L), __builtin_elementwise_sub_sat(H, V));
                 };
-                const uint32_t fe = set(__builtin_amdgcn_perm(0u, W1, 0x0c020c00u), __builtin_amdgcn_perm(0u, D, 0x0c020c00u),
-                                        __builtin_amdgcn_perm(0u, U, 0x0c020c00u), __builtin_amdgcn_perm(W2, W1, 0x0c050c03u),
-                                        __builtin_amdgcn_perm(W1, W0, 0x0c030c01u));
-                const uint32_t fo = set(__builtin_amdgcn_perm(0u, W1, 0x0c030c01u), __builtin_amdgcn_perm(0u, D, 0x0c030c01u),
-                                        __builtin_amdgcn_perm(0u, U, 0x0c030c01u), __builtin_amdgcn_perm(W2, W1, 0x0c060c04u),
-                                        __builtin_amdgcn_perm(W1, W0, 0x0c040c02u));
-                const uint32_t F = (fe | (fo << 8)) & m;  // byte k != 0 <=> pixel k survives
-                const bool f0 = (F & 0xFFu) != 0, f1 = (F & 0xFF00u) != 0, f2 = (F & 0xFF0000u) != 0, f3 = (F >> 24) != 0;
-                const uint64_t b0 = __ballot(f0), b1 = __ballot(f1), b2 = __ballot(f2), b3 = __ballot(f3);
-                int pos = mbcnt64(b3, mbcnt64(b2, mbcnt64(b1, mbcnt64(b0, na))));
-                const int code = code0 + rt * 64;
-                if (f0) lst[pos++] = (uint16_t)code;
-                if (f1) lst[pos++] = (uint16_t)(code + 1);
-                if (f2) lst[pos++] = (uint16_t)(code + 2);
-                if (f3) lst[pos] = (uint16_t)(code + 3);
-                na += __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
+                se = score(__builtin_amdgcn_perm(0u, W1, 0x0c020c00u), __builtin_amdgcn_perm(0u, D, 0x0c020c00u),
+                           __builtin_amdgcn_perm(0u, U, 0x0c020c00u), __builtin_amdgcn_perm(W2, W1, 0x0c050c03u),
+                           __builtin_amdgcn_perm(W1, W0, 0x0c030c01u));
+                so = score(__builtin_amdgcn_perm(0u, W1, 0x0c030c01u), __builtin_amdgcn_perm(0u, D, 0x0c030c01u),
+                           __builtin_amdgcn_perm(0u, U, 0x0c030c01u), __builtin_amdgcn_perm(W2, W1, 0x0c060c04u),
+                           __builtin_amdgcn_perm(W1, W0, 0x0c040c02u));
             }
+            const us2 fe = __builtin_elementwise_sub_sat(se, T), fo = __builtin_elementwise_sub_sat(so, T);
+            const uint32_t F = (as_u32(fe) | (as_u32(fo) << 8)) & m;  // byte k != 0 <=> pixel k survives
+            const bool f0 = (F & 0xFFu) != 0, f1 = (F & 0xFF00u) != 0, f2 = (F & 0xFF0000u) != 0, f3 = (F >> 24) != 0;
+            const uint64_t b0 = __ballot(f0), b1 = __ballot(f1), b2 = __ballot(f2), b3 = __ballot(f3);
+            const int na_next = na + __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
+            if constexpr (from_cache)
+                if (2 * na_next > s_next) return -1;
+            int pos = mbcnt64(b3, mbcnt64(b2, mbcnt64(b1, mbcnt64(b0, na))));
+            const int code = code0 + rt * 64;
+            if (f0) lst[pos++] = (uint16_t)code;
+            if (f1) lst[pos++] = (uint16_t)(code + 1);
+            if (f2) lst[pos++] = (uint16_t)(code + 2);
+            if (f3) lst[pos] = (uint16_t)(code + 3);
+            na = na_next;
+            if constexpr (keep_s)
+                if (2 * na <= s_off) *sp = as_u32(se) | (as_u32(so) << 8);
         }
+        return na;
+    };
+    using yes = std::integral_constant<bool, true>;
+    using no = std::integral_constant<bool, false>;
+    bool cached = false;
+    for (int attempt = 0; attempt < 2; attempt++) {
+        const int t = attempt == 0 ? ti : tm;
+        FAST_MARK();
+        int na;
+        if (attempt == 0) {
+            na = s_off >= 0 ? pass_a(no{}, yes{}, t) : pass_a(no{}, no{}, t);
+        } else {
+            na = cached ? pass_a(yes{}, no{}, t) : -1;
+            if (na < 0) na = pass_a(no{}, no{}, t);
+        }
+        if (attempt == 0) cached = s_off >= 0 && 2 * na <= s_off;
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         FAST_MARK();
         FAST_CNT(na);
@@ -775,14 +817,28 @@ __device__ __forceinline__ void stage_roi(const FastWaveCell& c, const uint8_t* 
             const int voff = lr * c.pitch + 4 * lc;
             uint32_t* dst = roi32 + lr * (rs >> 2) + lc;
             const int rp = c.rp, step = rp * (rs >> 2);
-            for (int r0 = 0, q0 = 0; r0 < c.ch; r0 += 8 * rp, q0 += 8) {
-                uint32_t v[8];
+            if (c.dw == 2) {
+                // rows past the ROI land in this wave's own map / list regions (host-checked:
+                // (ch + 8 rp - 1) rows of rs bytes fit its layout), which are written before they
+                // are read, and read zero (the resource ends at the ROI): no per-row guard
+                for (int r0 = 0, q0 = 0; r0 < c.ch; r0 += 8 * rp, q0 += 8) {
+                    uint32_t v[8];
 #pragma unroll
-                for (int k = 0; k < 8; k++)
-                    v[k] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, (r0 + k * rp) * c.pitch, 0);
+                    for (int k = 0; k < 8; k++)
+                        v[k] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, (r0 + k * rp) * c.pitch, 0);
 #pragma unroll
-                for (int k = 0; k < 8; k++)
-                    if (lr + r0 + k * rp < c.ch) dst[(q0 + k) * step] = v[k];
+                    for (int k = 0; k < 8; k++) dst[(q0 + k) * step] = v[k];
+                }
+            } else {
+                for (int r0 = 0, q0 = 0; r0 < c.ch; r0 += 8 * rp, q0 += 8) {
+                    uint32_t v[8];
+#pragma unroll
+                    for (int k = 0; k < 8; k++)
+                        v[k] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, (r0 + k * rp) * c.pitch, 0);
+#pragma unroll
+                    for (int k = 0; k < 8; k++)
+                        if (lr + r0 + k * rp < c.ch) dst[(q0 + k) * step] = v[k];
+                }
             }
         }
     } else {
@@ -2040,6 +2096,13 @@ static slam_status ensure_plan(slam_extractor* ex, int W, int H) {
             w.ng = ng;
             w.rpi = 64 / ng;
             w.m_ng = magic(ng);
+            // unguarded dword staging when the rows it writes past the ROI stay inside the wave's
+            // region in every layout the cell can run under (its class's and the one-dispatch one)
+            if (w.dw) {
+                const FastWaveLds& lc = (int)wcells.size() < ex->n_wave_a ? ex->fw_lay : ex->fw_lay_b;
+                const int rows = c.ch + 8 * w.rp - 1;
+                if (rows * lc.rs <= lc.total && rows * ex->fw_lay_all.rs <= ex->fw_lay_all.total) w.dw = 2;
+            }
             wcells.push_back(w);
         }
         if ((st = ex->d_wave_cells.ensure(std::max<size_t>(sizeof(FastWaveCell), wcells.size() * sizeof(FastWaveCell)))) ||
