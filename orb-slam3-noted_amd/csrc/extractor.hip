@@ -296,6 +296,42 @@ __global__ void __launch_bounds__(256) k_resize4(Bufs b, int l) {
         }
     };
     uint8_t* dbase = b.pyr + (size_t)f * P.pyr_frame + L.pyr_off + 4 * q;
+    if (dw) {
+        // Every source row of the thread's output rows first: both rows of each output row, 24
+        // independent dword loads in flight (the level tables are padded to whole row blocks, so
+        // rows past the level's last read copies of it), then the products and the stores.  The
+        // store of one output row no longer sits between the loads of the next (the source and the
+        // destination levels share the pyramid allocation, so the compiler could not hoist them).
+        uint4 yt[kRzRows];
+#pragma unroll
+        for (int rr = 0; rr < kRzRows; rr++) yt[rr] = yq[rr];
+        uint32_t w[kRzRows][2][3];
+#pragma unroll
+        for (int rr = 0; rr < kRzRows; rr++)
+#pragma unroll
+            for (int s = 0; s < 2; s++) {
+                const int off = (int)(s ? yt[rr].y : yt[rr].x) * spitch + xb;  // rows clamped by the plan
+#pragma unroll
+                for (int t = 0; t < 3; t++) w[rr][s][t] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, off + 4 * t, 0, 0);
+            }
+        const int nr = min(kRzRows, L.h - rb * kRzRows);
+#pragma unroll
+        for (int rr = 0; rr < kRzRows; rr++) {
+            const int b0 = (int)(yt[rr].z & 0xFFFF), b1 = (int)(yt[rr].z >> 16);
+            uint32_t word = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t lo0 = hiw[k] ? w[rr][0][1] : w[rr][0][0], hi0 = hiw[k] ? w[rr][0][2] : w[rr][0][1];
+                const uint32_t lo1 = hiw[k] ? w[rr][1][1] : w[rr][1][0], hi1 = hiw[k] ? w[rr][1][2] : w[rr][1][1];
+                const int d0 = (int)__builtin_amdgcn_udot2(as_us2(__builtin_amdgcn_perm(hi0, lo0, selp[k])), coef[k], 0u, false);
+                const int d1 = (int)__builtin_amdgcn_udot2(as_us2(__builtin_amdgcn_perm(hi1, lo1, selp[k])), coef[k], 0u, false);
+                const int v = ((__mul24(b0, d0 >> 4) >> 16) + (__mul24(b1, d1 >> 4) >> 16) + 2) >> 2;
+                word |= (uint32_t)(v & 0xFF) << (8 * k);
+            }
+            if (rr < nr) *reinterpret_cast<uint32_t*>(dbase + (size_t)(rb * kRzRows + rr) * L.pitch) = word;
+        }
+        return;
+    }
     int D0[4], D1[4];
     int have = INT_MIN;  // source row currently held in D1 (INT_MIN: none)
 #pragma unroll
