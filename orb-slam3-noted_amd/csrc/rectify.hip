@@ -24,7 +24,10 @@ constexpr int kRemapThreads = 256;
 // 16 frames per workgroup: the map entries are read once per 16 frames (at 8 the map traffic
 // equalled the image traffic); rectify stage 0.122 -> 0.115 ms per 128 pairs, headline +1%
 // (interleaved A/B); 32 was slower (0.133 ms, too few workgroups).
-constexpr int kFramesPerBlock = 16;
+#ifndef SLAMHOT_REMAP_FPB
+#define SLAMHOT_REMAP_FPB 16
+#endif
+constexpr int kFramesPerBlock = SLAMHOT_REMAP_FPB;  // experiment builds: -DSLAMHOT_REMAP_FPB=<n>
 
 struct MapEntry {
     int16_t sx, sy;
