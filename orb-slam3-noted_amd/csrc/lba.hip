@@ -29,6 +29,9 @@
 #include <cmath>
 #include <cstring>
 #include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <thread>
 
 #include <immintrin.h>
@@ -2529,7 +2532,70 @@ struct Plan {
 
 constexpr int kRing = 4;  // LM steps whose counters are in flight (host-side ring)
 
+// The planning threads of one handle, kept between calls (spawning and joining them twice per
+// call cost ~0.1-0.3 ms): run(n, f) calls f(0) on the caller and f(1..n-1) on the workers.
+struct PlanPool {
+    std::vector<std::thread> th;
+    std::mutex m;
+    std::condition_variable cv, done;
+    unsigned long long gen = 0;
+    int busy = 0, n = 0;
+    bool stop = false;
+    const std::function<void(int)>* job = nullptr;
+
+    // false: fewer workers than asked for (thread creation failed); the caller runs the rest
+    int ensure(int want) {
+        while ((int)th.size() < want - 1) {
+            const int t = (int)th.size() + 1;
+            try {
+                th.emplace_back([this, t] { worker(t); });
+            } catch (...) {
+                break;
+            }
+        }
+        return (int)th.size() + 1;
+    }
+    void run(int nt, const std::function<void(int)>& f) {
+        {
+            std::lock_guard<std::mutex> lk(m);
+            job = &f;
+            n = nt;
+            busy = (int)th.size();
+            gen++;
+        }
+        cv.notify_all();
+        f(0);
+        std::unique_lock<std::mutex> lk(m);
+        done.wait(lk, [&] { return busy == 0; });
+        job = nullptr;
+    }
+    void worker(int t) {
+        unsigned long long seen = 0;
+        std::unique_lock<std::mutex> lk(m);
+        for (;;) {
+            cv.wait(lk, [&] { return stop || gen != seen; });
+            if (stop) return;
+            seen = gen;
+            const std::function<void(int)>* f = job;
+            const int nt = n;
+            lk.unlock();
+            if (t < nt) (*f)(t);
+            lk.lock();
+            if (--busy == 0) done.notify_all();
+        }
+    }
+    ~PlanPool() {
+        {
+            std::lock_guard<std::mutex> lk(m);
+            stop = true;
+        }
+        cv.notify_all();
+        for (auto& x : th) x.join();
+    }
+};
+
 struct slam_lba {
+    PlanPool plan_pool;
     int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -2638,19 +2704,21 @@ Plan bind(unsigned char* base, const Layout& L) {
     return P;
 }
 
-// host threads of one call's planning: callers run several solvers at once (the bench's LBA leg:
-// 4), and 16 planning threads per call oversubscribed the GPU box's 16-thread CPU share, delaying
-// the solver threads that launch the next LM step (SLAMHOT_LBA_PLAN_THREADS overrides)
+// host threads of one call's planning (the handle's PlanPool): callers run several solvers at once
+// (the bench's LBA leg: 4), and 16 planning threads per call oversubscribed the GPU box's 16-thread
+// CPU share, delaying the solver threads that launch the next LM step; with the threads kept
+// between calls, 8 measured best (plan 4.0-4.5 -> 2.6-2.8 ms per 128-window call, LBA leg
+// 131-134k -> 139-145k LM it/s, profiles/r05_lba_plan.txt).  SLAMHOT_LBA_PLAN_THREADS overrides.
 int plan_threads(int n_prob) {
     static const int cap_env = std::getenv("SLAMHOT_LBA_PLAN_THREADS") ? std::atoi(std::getenv("SLAMHOT_LBA_PLAN_THREADS")) : 0;
-    const int cap = cap_env > 0 ? cap_env : 4;
+    const int cap = cap_env > 0 ? cap_env : 8;
     const int hw = (int)std::max(1u, std::min((unsigned)cap, std::thread::hardware_concurrency()));
     return std::max(1, std::min(hw, n_prob));
 }
 
 // run fn(w, scratch) for every window on nth threads (window w on thread w % nth)
 template <class S, class F>
-slam_status for_windows(int n_prob, int nth, F fn) {
+slam_status for_windows(int n_prob, int nth, F fn, PlanPool* pool) {
     std::vector<slam_status> rs(nth, SLAM_OK);
     auto run = [&](int t) {
         S scratch;
@@ -2661,6 +2729,12 @@ slam_status for_windows(int n_prob, int nth, F fn) {
     };
     if (nth <= 1) {
         run(0);
+    } else if (pool) {
+        const int have = pool->ensure(nth);
+        const std::function<void(int)> f = [&](int t) {
+            for (int u = t; u < nth; u += have) run(u);  // threads the pool could not start: here
+        };
+        pool->run(std::min(have, nth), f);
     } else {
         std::vector<std::thread> th;
         try {
@@ -2679,7 +2753,7 @@ slam_status for_windows(int n_prob, int nth, F fn) {
 // Pass 1: validation and sizes, per window on the planning threads, then the windows' start
 // offsets (prefix sums).  hidx: free-pose index of every KF of every window.
 slam_status plan_sizes(int n_prob, const slam_lba_problem* probs, PlanSizes& z, std::vector<int>& hidx_all,
-                       std::vector<int>& np_of) {
+                       std::vector<int>& np_of, PlanPool* pool) {
     z.nw = n_prob;
     np_of.assign(n_prob, 0);
     z.starts.resize(n_prob);
@@ -2712,13 +2786,38 @@ slam_status plan_sizes(int n_prob, const slam_lba_problem* probs, PlanSizes& z, 
             if (has && !P.kf_Trl) return SLAM_EINVAL;  // body edges need each KeyFrame's mTrl
             S.body = has;
         }
+        // One pass over the edges: validation, edges per KeyFrame, and the free-pose edge counts.
+        // An edge's KeyFrame has an edge (this one), so it is a free pose iff it is not fixed.
+        // Free-pose edges: an edge right after one of the same point on the same KeyFrame (body
+        // edge) shares its Hpl block and has no Schur entry of its own; a point with k such edges
+        // adds k (k + 1) / 2 Schur contributions.  Two such edges of one point on one KeyFrame
+        // that are not adjacent are refused (a KeyFrame stamp per point).
         cnt.assign(P.n_kf, 0);
+        std::vector<int>& stamp = sc.stamp;
+        stamp.assign(P.n_kf, 0);
+        int run = 0, pprev = -1, kprev = -1;
         for (int i = 0; i < P.n_edge; i++) {
             const int p = P.edge_pt[i], k = P.edge_kf[i];
             if (p < 0 || p >= P.n_pt || k < 0 || k >= P.n_kf) return SLAM_EINVAL;
-            if (i && p < P.edge_pt[i - 1]) return SLAM_EINVAL;  // point-major insertion order
+            if (p < pprev) return SLAM_EINVAL;  // point-major insertion order
             cnt[k]++;
+            if (p != pprev) {
+                S.nct += (long long)run * (run + 1) / 2;
+                run = 0;
+            }
+            const bool follows = p == pprev && k == kprev;
+            pprev = p;
+            kprev = k;
+            if (P.kf_fixed[k] != 0) continue;
+            S.npe++;
+            if (!follows) {
+                if (stamp[k] == p + 1) return SLAM_EINVAL;  // non-adjacent edges of 1 point in 1 KF
+                stamp[k] = p + 1;
+                S.nspe++;
+                run++;
+            }
         }
+        S.nct += (long long)run * (run + 1) / 2;
         // a KeyFrame without edges is not an active vertex (sparse_optimizer.cpp:262-300): it
         // stays out of the Hessian and keeps its estimate
         int* hidx = &hidx_all[z.starts[w].h0];
@@ -2726,31 +2825,8 @@ slam_status plan_sizes(int n_prob, const slam_lba_problem* probs, PlanSizes& z, 
         for (int k = 0; k < P.n_kf; k++) hidx[k] = P.kf_fixed[k] == 0 && cnt[k] > 0 ? np++ : -1;
         np_of[w] = np;
         if (6 * np > kMaxN) return SLAM_ECAP;
-        // free-pose edges; an edge right after one of the same point on the same KeyFrame (body
-        // edge) shares its Hpl block and has no Schur entry of its own.  A point with k such
-        // edges adds k (k + 1) / 2 Schur contributions.
-        // Two such edges of one point on one KeyFrame that are not adjacent are refused (a
-        // KeyFrame stamp per point).
-        std::vector<int>& stamp = sc.stamp;
-        stamp.assign(P.n_kf, 0);
-        int run = 0;
-        for (int i = 0; i <= P.n_edge; i++) {
-            if (i == P.n_edge || (i > 0 && P.edge_pt[i] != P.edge_pt[i - 1])) {
-                S.nct += (long long)run * (run + 1) / 2;
-                run = 0;
-            }
-            if (i == P.n_edge || hidx[P.edge_kf[i]] < 0) continue;
-            S.npe++;
-            if (!(i > 0 && P.edge_pt[i - 1] == P.edge_pt[i] && P.edge_kf[i - 1] == P.edge_kf[i])) {
-                const int k = P.edge_kf[i];
-                if (stamp[k] == P.edge_pt[i] + 1) return SLAM_EINVAL;  // non-adjacent edges of 1 point in 1 KF
-                stamp[k] = P.edge_pt[i] + 1;
-                S.nspe++;
-                run++;
-            }
-        }
         return SLAM_OK;
-    });
+    }, pool);
     if (st != SLAM_OK) return st;
     for (int w = 0; w < n_prob; w++) {
         z.any_body = z.any_body || sz[w].body;
@@ -2794,7 +2870,7 @@ slam_status plan_sizes(int n_prob, const slam_lba_problem* probs, PlanSizes& z, 
 // Pass 2: fill the arena in place.
 slam_status plan_fill(int n_prob, const slam_lba_problem* probs, const std::vector<int>& hidx_all,
                       const std::vector<int>& np_of, const slam_lba_options* opt, const PlanSizes& Z,
-                      const Plan& P) {
+                      const Plan& P, PlanPool* pool) {
     // windows are independent given their start offsets: fill them on host threads
 #ifdef SLAMHOT_PLAN_BENCH
     // section cycle counts of plan_fill (rdtsc, summed over windows and threads)
@@ -2878,10 +2954,23 @@ slam_status plan_fill(int n_prob, const slam_lba_problem* probs, const std::vect
         }
         PB_MARK(0);
         std::memcpy(P.pt_in + 3 * (size_t)npt, Q.pt_pos, sizeof(float) * 3 * Q.n_pt);
+        // edge records, and in the same pass the point CSR and the offsets of the per-point
+        // free-pose edge lists (the lists themselves, sorted by pose, are built on the device:
+        // spe_build_body); a point's entries are written at its first edge (points without
+        // edges: at the next point's, or after the last edge)
+        int p_next = 0;
         for (int i = 0; i < Q.n_edge; i++) {
             EdgeS& e = P.edges[ne + i];
-            const int k = Q.edge_kf[i];
-            e.pt = npt + Q.edge_pt[i];
+            const int k = Q.edge_kf[i], p = Q.edge_pt[i];
+            for (; p_next <= p; p_next++) {
+                P.pt_off[npt + p_next] = ne + i;
+                P.pt_win[npt + p_next] = w;
+                P.spe_off[npt + p_next] = nspe;
+            }
+            // the edge right after one on the same KeyFrame (body edge) shares its Hpl block
+            const bool follows = i > 0 && Q.edge_pt[i - 1] == p && Q.edge_kf[i - 1] == k;
+            nspe += hidx[k] >= 0 && !follows;
+            e.pt = npt + p;
             e.kf = nkf + k;
             e.hp = hidx[k] >= 0 ? npose + hidx[k] : -1;
             e.win = w;
@@ -2892,21 +2981,13 @@ slam_status plan_fill(int n_prob, const slam_lba_problem* probs, const std::vect
             e.obs[2] = body ? kBodyTag : (ur < 0.f ? -1.0f : ur);
             e.info = Q.edge_inv_sigma2[i];
         }
-        PB_MARK(1);
-        // point CSR and the offsets of the per-point free-pose edge lists (the lists themselves,
-        // sorted by pose, are built on the device: spe_build_body)
-        const int pe_start = ws.pe0;
-        int i = 0;
-        for (int p = 0; p < Q.n_pt; p++) {
-            P.pt_off[npt + p] = ne + i;
-            P.pt_win[npt + p] = w;
-            P.spe_off[npt + p] = nspe;
-            for (; i < Q.n_edge && Q.edge_pt[i] == p; i++) {
-                // the edge right after one on the same KeyFrame (body edge) shares its Hpl block
-                const bool follows = i > 0 && Q.edge_pt[i - 1] == p && Q.edge_kf[i - 1] == Q.edge_kf[i];
-                nspe += hidx[Q.edge_kf[i]] >= 0 && !follows;
-            }
+        for (; p_next < Q.n_pt; p_next++) {
+            P.pt_off[npt + p_next] = ne + Q.n_edge;
+            P.pt_win[npt + p_next] = w;
+            P.spe_off[npt + p_next] = nspe;
         }
+        PB_MARK(1);
+        const int pe_start = ws.pe0;
         PB_MARK(2);
         // Schur blocks (i1 <= i2: blk = i2 (i2 + 1) / 2 + i1); their contributions come from the
         // pose bitmaps built on the device (k_bm_*)
@@ -2944,7 +3025,7 @@ slam_status plan_fill(int n_prob, const slam_lba_problem* probs, const std::vect
     };
     const slam_status st = for_windows<FillScratch>(n_prob, plan_threads(n_prob), [&](int w, FillScratch& sc) {
         return fill_one(w, sc.pcnt);
-    });
+    }, pool);
     if (st != SLAM_OK) return st;
 #ifdef SLAMHOT_PLAN_BENCH
     std::fprintf(stderr, "fill sections (Mcycles): header+edges %.1f, csr %.1f, blocks %.1f, pose lists %.1f\n",
@@ -3100,7 +3181,7 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     };
     PlanSizes Z;
     std::vector<int> hidx_all, np_of;
-    slam_status st = plan_sizes(n_prob, probs, Z, hidx_all, np_of);
+    slam_status st = plan_sizes(n_prob, probs, Z, hidx_all, np_of, &s->plan_pool);
     if (st != SLAM_OK) return st;
     const bool stop0 = user_stop();
     for (int w = 0; w < n_prob; w++) {
@@ -3138,7 +3219,7 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     }
     const Plan HP = bind(s->harena, LY);
     const auto t_fill0 = std::chrono::steady_clock::now();
-    st = plan_fill(n_prob, probs, hidx_all, np_of, opt, Z, HP);
+    st = plan_fill(n_prob, probs, hidx_all, np_of, opt, Z, HP, &s->plan_pool);
     if (st != SLAM_OK) return st;
     if (std::getenv("SLAMHOT_LBA_PLAN_TIMING")) {
         const auto t1 = std::chrono::steady_clock::now();
@@ -3513,12 +3594,13 @@ slam_status slamhot_lba_plan_bench(int n_prob, const slam_lba_problem* probs, co
         const auto t0 = std::chrono::steady_clock::now();
         PlanSizes Z;
         std::vector<int> hidx_all, np_of;
-        slam_status st = plan_sizes(n_prob, probs, Z, hidx_all, np_of);
+        static PlanPool bench_pool;
+        slam_status st = plan_sizes(n_prob, probs, Z, hidx_all, np_of, &bench_pool);
         if (st != SLAM_OK) return st;
         const Layout LY = make_layout(Z);
         if (arena.size() < LY.total) arena.resize(LY.total);
         const auto t1 = std::chrono::steady_clock::now();
-        st = plan_fill(n_prob, probs, hidx_all, np_of, opt, Z, bind(arena.data(), LY));
+        st = plan_fill(n_prob, probs, hidx_all, np_of, opt, Z, bind(arena.data(), LY), &bench_pool);
         if (st != SLAM_OK) return st;
         const auto t2 = std::chrono::steady_clock::now();
         *sizes_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
