@@ -114,6 +114,23 @@ def test_low_contrast_minth_retry(gpu_extractor_factory):
     _compare(kg, dg, mg, ko, do, mo)
 
 
+def test_minth_retry_dense_compass(gpu_extractor_factory):
+    """A one-pixel checkerboard of amplitude 12 (100 / 112) on the left half: every pixel passes
+    the compass pre-test at minThFAST 7 and none at iniThFAST 20, and no 9-arc exists at either
+    (12 of the 16 circle pixels have the centre's colour).  Its cells are empty at iniTh, and
+    their minTh attempt grows the pass-A list past the compass scores the first attempt kept at
+    the end of the list region, so k_fast_wave falls back to deriving them from the ROI again.
+    Textured right half."""
+    ex = gpu_extractor_factory(nfeatures=1000, max_size=(640, 480))
+    yy, xx = np.mgrid[0:480, 0:640]
+    img = np.where((xx + yy) & 1, 112, 100).astype(np.uint8)
+    img[:, 320:] = synth.frame(13)[:, 320:]
+    kg, dg, mg = ex(img)
+    ko, do, mo = ob.extract(img)
+    assert len(ko) > 300
+    _compare(kg, dg, mg, ko, do, mo)
+
+
 def test_kitti_stereo_settings(gpu_extractor_factory):
     """Examples/Stereo/KITTI04-12.yaml:21-54: 1241 x 376, 2000 features, iniThFAST 12, minThFAST 7."""
     ex = gpu_extractor_factory(nfeatures=2000, scaleFactor=1.2, nlevels=8, iniThFAST=12, minThFAST=7,
