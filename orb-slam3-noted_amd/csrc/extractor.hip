@@ -513,25 +513,11 @@ __global__ void __launch_bounds__(256) k_fast_cells(Bufs b, const int32_t* list)
 // Exact FAST measure without a threshold: M = max(max_s min d[s..s+8], -min_s max d[s..s+8])
 // with d_k = v - p_k over the 16-pixel Bresenham circle (windows by min3/max3 doubling).
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ int fast_M(const uint8_t* c, int stride) {
-    const int v = c[0];
+// M from the centre v and the circle p[0..15] (p_k in FAST_t<16>'s pixel order)
+__device__ __forceinline__ int fast_M_of(int v, const int (&p)[16]) {
     int d[16];
-    d[0] = v - c[3 * stride];
-    d[1] = v - c[3 * stride + 1];
-    d[2] = v - c[2 * stride + 2];
-    d[3] = v - c[stride + 3];
-    d[4] = v - c[3];
-    d[5] = v - c[-stride + 3];
-    d[6] = v - c[-2 * stride + 2];
-    d[7] = v - c[-3 * stride + 1];
-    d[8] = v - c[-3 * stride];
-    d[9] = v - c[-3 * stride - 1];
-    d[10] = v - c[-2 * stride - 2];
-    d[11] = v - c[-stride - 3];
-    d[12] = v - c[-3];
-    d[13] = v - c[stride - 3];
-    d[14] = v - c[2 * stride - 2];
-    d[15] = v - c[3 * stride - 1];
+#pragma unroll
+    for (int k = 0; k < 16; k++) d[k] = v - p[k];
     int mn3[16], mx3[16];
 #pragma unroll
     for (int k = 0; k < 16; k++) {
@@ -548,6 +534,14 @@ __device__ __forceinline__ int fast_M(const uint8_t* c, int stride) {
     }
     const int M = max(mdark, -mbr);
     return M > 0 ? M : 0;
+}
+
+__device__ __forceinline__ int fast_M(const uint8_t* c, int stride) {
+    const int p[16] = {c[3 * stride],      c[3 * stride + 1],  c[2 * stride + 2],  c[stride + 3],
+                       c[3],               c[-stride + 3],     c[-2 * stride + 2], c[-3 * stride + 1],
+                       c[-3 * stride],     c[-3 * stride - 1], c[-2 * stride - 2], c[-stride - 3],
+                       c[-3],              c[stride - 3],      c[2 * stride - 2],  c[3 * stride - 1]};
+    return fast_M_of(c[0], p);
 }
 
 // Necessary condition for a 9-arc at threshold t: every 9-run of the 16-pixel circle holds
@@ -569,13 +563,32 @@ __device__ __forceinline__ bool fast_pairs8(const uint8_t* c, int stride, int t)
     return (lo < v - t) || (hi > v + t);
 }
 
+// The eight-pair pre-test and, when it passes, the exact measure from the same 17 reads (the
+// single-chunk form of passes B1 + B): 0 when the pre-test fails (then M <= t as well).
+__device__ __forceinline__ int fast_pairs8_M(const uint8_t* c, int stride, int t) {
+    const int v = c[0];
+    const int p[16] = {c[3 * stride],      c[3 * stride + 1],  c[2 * stride + 2],  c[stride + 3],
+                       c[3],               c[-stride + 3],     c[-2 * stride + 2], c[-3 * stride + 1],
+                       c[-3 * stride],     c[-3 * stride - 1], c[-2 * stride - 2], c[-stride - 3],
+                       c[-3],              c[stride - 3],      c[2 * stride - 2],  c[3 * stride - 1]};
+    int lo = min(p[0], p[8]), hi = max(p[0], p[8]);
+#pragma unroll
+    for (int k = 1; k < 8; k++) {
+        lo = max(lo, min(p[k], p[k + 8]));
+        hi = min(hi, max(p[k], p[k + 8]));
+    }
+    if (!((lo < v - t) || (hi > v + t))) return 0;
+    return fast_M_of(v, p);
+}
+
 // ---------------------------------------------------------------------------------------
 // k_fast_wave: one WAVE per cell whose tested region is <= 64 columns wide (all cells of
 // the standard geometries).  Three order-preserving, wave-compacted passes over the cell:
 //   A  compass pre-test on every tested pixel (necessary for a 9-arc at threshold t: it
 //      covers one of each opposite pair 0/8 and 4/12)  -> list of survivors
 //   B1 the eight-pair test, B exact measure M (fast_M) on the survivors; M > t goes to a
-//      zero-padded M map and stays in the (in-place) list
+//      zero-padded M map and stays in the (in-place) list.  When A leaves at most 64 pixels
+//      (one chunk), B1 and B run as one pass on one set of circle reads (fast_pairs8_M)
 //   C  cell-local 3x3 NMS at t on the remaining corners
 // t = iniThFAST, then minThFAST only for cells left empty (ORBextractor.cc:808-841).  Lists
 // keep row-major order, so the survivors are emitted in cv::FAST's order.
@@ -759,41 +772,58 @@ __device__ __forceinline__ void fast_cell(const Bufs& b, const DevPlan& P, const
         FAST_MARK();
         FAST_CNT(na);
 
-        // pass B1: the eight-pair pre-test on the compass survivors (in-place compaction)
-        {
-            int n1 = 0;
+        int nb = 0;
+        if (na <= 64) {
+            // one chunk of compass survivors: B1 and B together, one set of circle reads per pixel
+            const bool valid = lane < na;
+            const int code = valid ? lst[lane] : 0;
+            const int r = code >> 6, c = code & 63;
+            int M = 0;
+            if (valid) M = fast_pairs8_M(roi + (r + 3) * lay.rs + c + 3, lay.rs, t);
+            const bool corner = M > t;
+            if (corner) map[(r + 1) * lay.ms + c + 1] = (uint8_t)M;
+            const uint64_t m = __ballot(corner);
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            if (corner) lst[__popcll(m & lt)] = (uint16_t)code;
+            nb = __popcll(m);
+            FAST_MARK();
+            FAST_CNT(-1);
+        } else {
+            // pass B1: the eight-pair pre-test on the compass survivors (in-place compaction)
+            {
+                int n1 = 0;
+                for (int j = 0; j < na; j += 64) {
+                    const int e = j + lane;
+                    const bool valid = e < na;
+                    const int code = valid ? lst[e] : 0;
+                    const int r = code >> 6, c = code & 63;
+                    const bool keep = valid && fast_pairs8(roi + (r + 3) * lay.rs + c + 3, lay.rs, t);
+                    const uint64_t m = __ballot(keep);
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                    if (keep) lst[n1 + __popcll(m & lt)] = (uint16_t)code;
+                    n1 += __popcll(m);
+                }
+                na = n1;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            FAST_MARK();
+            FAST_CNT(na);
+
+            // pass B (compacts the list in place: writes never pass the chunk being read)
             for (int j = 0; j < na; j += 64) {
                 const int e = j + lane;
                 const bool valid = e < na;
                 const int code = valid ? lst[e] : 0;
                 const int r = code >> 6, c = code & 63;
-                const bool keep = valid && fast_pairs8(roi + (r + 3) * lay.rs + c + 3, lay.rs, t);
-                const uint64_t m = __ballot(keep);
+                int M = 0;
+                if (valid) M = fast_M(roi + (r + 3) * lay.rs + c + 3, lay.rs);
+                const bool corner = M > t;
+                if (corner) map[(r + 1) * lay.ms + c + 1] = (uint8_t)M;
+                const uint64_t m = __ballot(corner);
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                if (keep) lst[n1 + __popcll(m & lt)] = (uint16_t)code;
-                n1 += __popcll(m);
+                if (corner) lst[nb + __popcll(m & lt)] = (uint16_t)code;
+                nb += __popcll(m);
             }
-            na = n1;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        FAST_MARK();
-        FAST_CNT(na);
-
-        // pass B (compacts the list in place: writes never pass the chunk being read)
-        int nb = 0;
-        for (int j = 0; j < na; j += 64) {
-            const int e = j + lane;
-            const bool valid = e < na;
-            const int code = valid ? lst[e] : 0;
-            const int r = code >> 6, c = code & 63;
-            int M = 0;
-            if (valid) M = fast_M(roi + (r + 3) * lay.rs + c + 3, lay.rs);
-            const bool corner = M > t;
-            if (corner) map[(r + 1) * lay.ms + c + 1] = (uint8_t)M;
-            const uint64_t m = __ballot(corner);
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            if (corner) lst[nb + __popcll(m & lt)] = (uint16_t)code;
-            nb += __popcll(m);
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 
