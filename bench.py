@@ -124,20 +124,32 @@ def cpu_model():
 
 
 def timed_region(dist, device, fn, steps):
-    """barrier + synchronize, K calls of fn(i), synchronize + barrier; seconds."""
+    """barrier + synchronize, K calls of fn(i), synchronize + barrier; seconds.  Python's cyclic
+    garbage collector is collected before and paused inside the region: a gen-2 pass over the
+    objects earlier legs left stalls the host threads that queue the device work (the LBA leg read
+    ~10% lower after any other leg), which a C / C++ caller of the library does not have."""
+    import gc
+
     import torch
     sync = torch.cuda.synchronize if device.type == "cuda" else (lambda d: None)
+    gc.collect()
     sync(device)
     if dist:
         dist.barrier()
     sync(device)
-    t0 = time.perf_counter()
-    for i in range(steps):
-        fn(i)
-    sync(device)
-    if dist:
-        dist.barrier()
-    return time.perf_counter() - t0
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        t0 = time.perf_counter()
+        for i in range(steps):
+            fn(i)
+        sync(device)
+        if dist:
+            dist.barrier()
+        return time.perf_counter() - t0
+    finally:
+        if was:
+            gc.enable()
 
 
 def _free_port():
@@ -191,24 +203,34 @@ def launch_ranks(n, argv, timeout_s):
                 p.kill()
                 p.wait()
 
+    # one waiter per rank records when it exited: a rank that fails takes the others down (their
+    # collectives see the connection close), and the job's status is the first failure's
+    exits = {}
+
+    def waiter(r, p):
+        c = p.wait()
+        exits[r] = (time.monotonic(), c)
+    for r, p in enumerate(procs):
+        threading.Thread(target=waiter, args=(r, p), daemon=True).start()
     deadline = time.monotonic() + timeout_s
     status = 0
     while True:
-        codes = [p.poll() for p in procs]
-        bad = [c for c in codes if c not in (None, 0)]
+        done = dict(exits)
+        bad = sorted((tc[0], r, tc[1]) for r, tc in done.items() if tc[1] != 0)
         if bad:
-            status = bad[0] if bad[0] > 0 else 128 - bad[0]
-            sys.stderr.write(f"bench.py launcher: a rank exited with {bad[0]}; stopping the job\n")
+            _, r, c = bad[0]
+            status = c if c > 0 else 128 - c
+            sys.stderr.write(f"bench.py launcher: rank {r} exited with {c}; stopping the job\n")
             stop_all()
             break
-        if all(c == 0 for c in codes):
+        if len(done) == n:
             break
         if time.monotonic() > deadline:
             sys.stderr.write(f"bench.py launcher: job still running after {timeout_s:.0f} s; killing it\n")
             stop_all()
             status = 124
             break
-        time.sleep(0.2)
+        time.sleep(0.05)
     t.join(timeout=10)
     if status == 0:
         if len(lines) != 1:

@@ -43,7 +43,8 @@ def test_gpus_launcher_fails_when_a_rank_fails():
     p = _run(["--gpus", "2", "--legs", "dry", "--steps", "2", "--warmup", "0"], {"SLAMHOT_DRY_FAIL_RANK": "1"})
     assert p.returncode == 3, (p.returncode, p.stderr[-3000:])
     assert p.stdout.strip() == ""
-    assert "a rank exited with 3" in p.stderr
+    # the first rank to fail sets the status (rank 0 then fails too, on the closed connection)
+    assert "rank 1 exited with 3" in p.stderr
 
 
 def test_gpus_launcher_kills_a_hung_job():
