@@ -220,7 +220,11 @@ __device__ __forceinline__ void stage_u32(uint32_t* dst, int dstride, const uint
 // per-thread FP64 math (round 5: stage 0.131 -> 0.126 ms per batch).  A source row loaded for
 // output row y is reused for row y+1 when its vertical pair starts there (scale 1.2: most rows).
 // ---------------------------------------------------------------------------------------
-constexpr int kRzRows = 4;
+#ifndef SLAMHOT_RZ_ROWS
+#define SLAMHOT_RZ_ROWS 4
+#endif
+constexpr int kRzRows = SLAMHOT_RZ_ROWS;  // output rows per thread (the y table is padded to 8)
+static_assert(8 % kRzRows == 0, "the plan pads each level's y table to a multiple of 8 rows");
 
 __global__ void __launch_bounds__(256) k_resize4(Bufs b, int l) {
     const DevPlan& P = *b.plan;

@@ -143,11 +143,11 @@ inline void build_resize_tables(int sw, int sh, int dw, int dh, Plan& P, LevelPl
         e.pad = 0;
         P.ytab.push_back(e);
     }
-    // k_resize4 reads four consecutive entries (a thread's 4 columns / 4 rows) as 16-byte vectors:
-    // each level's tables padded to a multiple of 4 with copies of the last entry (the clamped
-    // column / row the kernel would compute), so the next level's tables stay 4-aligned
+    // k_resize4 reads a thread's 4 columns as two 16-byte vectors and its rows (up to 8) one entry
+    // each: each level's tables padded (x to a multiple of 4, y of 8) with copies of the last entry
+    // (the clamped column / row the kernel would compute), so the next level's tables stay aligned
     while (P.xtab.size() % 4) P.xtab.push_back(P.xtab.back());
-    while (P.ytab.size() % 4) P.ytab.push_back(P.ytab.back());
+    while (P.ytab.size() % 8) P.ytab.push_back(P.ytab.back());
 }
 
 // Everything a W x H extraction needs.  Returns false for unsupported geometry.
