@@ -303,7 +303,9 @@ def main():
     ap.add_argument("--cpu-frames", type=int, default=384)
     ap.add_argument("--lba-windows", type=int, default=128, help="LBA windows per GPU per call")
     ap.add_argument("--lba-calls", type=int, default=6)
-    ap.add_argument("--lba-inflight", type=int, default=4, help="LBA solver handles driven concurrently")
+    # 6 solvers: 138.8-140.6k LM it/s after the extractor legs against 122.7-127.0k with 4 and
+    # 129.3-137.1k with 3 (tools/ab/r05_lba_inflight.sh, profiles/r05_lba_plan.txt)
+    ap.add_argument("--lba-inflight", type=int, default=6, help="LBA solver handles driven concurrently")
     ap.add_argument("--lba-stagger-ms", type=float, default=6.0,
                     help="LBA: solver t starts t x this many ms late, so the solvers' host planning phases "
                          "(~5 ms per 128-window call) fall between the others' device phases instead of "
