@@ -59,3 +59,20 @@ sanitize-hip:
 	  -L$(LIBDIR)/asan -lslamhot -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)/asan' -Wl,-rpath,$(CLANGRT) || exit 1; done
 
 .PHONY: all oracle clean sanitize sanitize-hip
+
+# The LBA host planning path of six solver handles at once, each handle's pool growing between
+# calls (tests/cpp/plan_stress.cpp), under TSan and under ASan + UBSan (host code instrumented, GPU
+# code not; no HIP call is made): tests/test_sanitize_plan.py runs both on the CPU
+PLANSAN_SRC := $(CSRC)/lba.hip $(HDRS) tests/cpp/plan_stress.cpp
+PLANSAN := --offload-arch=gfx950 -O1 -g -std=c++17 -fPIC -ffp-contract=off -DSLAMHOT_PLAN_BENCH
+sanitize-plan: tests/cpp/plan_stress_tsan tests/cpp/plan_stress_asan
+tests/cpp/plan_stress_tsan: $(PLANSAN_SRC)
+	@mkdir -p build/plansan
+	$(HIPCC) $(PLANSAN) -Xarch_host -fsanitize=thread -c -o build/plansan/lba_tsan.o $(CSRC)/lba.hip 2>&1 | grep -v "not currently supported for target" || true
+	/opt/rocm/lib/llvm/bin/clang++ -O1 -g -std=c++17 -fsanitize=thread -Iinclude -c -o build/plansan/stress_tsan.o tests/cpp/plan_stress.cpp
+	$(HIPCC) --hip-link --offload-arch=gfx950 -fsanitize=thread -o $@ build/plansan/stress_tsan.o build/plansan/lba_tsan.o
+tests/cpp/plan_stress_asan: $(PLANSAN_SRC)
+	@mkdir -p build/plansan
+	$(HIPCC) $(PLANSAN) -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -c -o build/plansan/lba_asan.o $(CSRC)/lba.hip 2>&1 | grep -v "not currently supported for target" || true
+	/opt/rocm/lib/llvm/bin/clang++ -O1 -g -std=c++17 -fsanitize=address,undefined -Iinclude -c -o build/plansan/stress_asan.o tests/cpp/plan_stress.cpp
+	$(HIPCC) --hip-link --offload-arch=gfx950 -fsanitize=address,undefined -o $@ build/plansan/stress_asan.o build/plansan/lba_asan.o

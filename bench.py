@@ -123,6 +123,22 @@ def cpu_model():
     return "unknown"
 
 
+PHASE = {"file": None, "rank": 0, "leg": None}
+
+
+def phase(what):
+    """The leg child's current phase, kept in a file its parent reads when the leg fails or times out:
+    a rank stuck in its own work ("compute: ...") is told apart from ranks waiting for it in a
+    collective ("collective: ...").  Rank 0 also logs each phase on stderr."""
+    if PHASE["file"]:
+        try:
+            Path(PHASE["file"]).write_text(what)
+        except OSError:
+            pass
+    if PHASE["rank"] == 0 and PHASE["leg"]:
+        progress(f"  {PHASE['leg']}: {what}")
+
+
 def timed_region(dist, device, fn, steps):
     """barrier + synchronize, K calls of fn(i), synchronize + barrier; seconds.  Python's cyclic
     garbage collector is collected before and paused inside the region: a gen-2 pass over the
@@ -135,18 +151,23 @@ def timed_region(dist, device, fn, steps):
     gc.collect()
     sync(device)
     if dist:
+        phase("collective: barrier before the timed region")
         dist.barrier()
     sync(device)
     was = gc.isenabled()
     gc.disable()
     try:
+        phase(f"compute: timed region ({steps} steps)")
         t0 = time.perf_counter()
         for i in range(steps):
             fn(i)
         sync(device)
         if dist:
+            phase("collective: barrier after the timed region")
             dist.barrier()
-        return time.perf_counter() - t0
+        el = time.perf_counter() - t0
+        phase("compute: after the timed region")
+        return el
     finally:
         if was:
             gc.enable()
@@ -285,7 +306,28 @@ def roofline_from_stages(stages, calls, frames_per_call, W, H, kps_per_frame):
     return roof
 
 
-def main():
+# ------------------------------------------------------------------------------------------
+# orchestration: every leg in a child process of its own, with a deadline
+# ------------------------------------------------------------------------------------------
+LEG_ORDER = ("dry", "dryaux", "headline", "extract", "lba", "pose", "track", "localmap", "projection")
+# seconds a leg may take (child start .. exit, CPU baseline included); the round-4 driver run of
+# every leg took 21 s in one process, so each cap is several times the leg's normal length.  The
+# whole job also has one deadline (--job-deadline) below the driver's 600 s limit: a leg starts
+# only with the time that is left.
+LEG_CAP_S = {"dry": 90, "dryaux": 90, "headline": 150, "extract": 90, "lba": 120, "pose": 60, "track": 120,
+             "localmap": 60, "projection": 60}
+T_START = time.monotonic()
+T0_WALL = float(os.environ.get("SLAMHOT_BENCH_T0", time.time()))  # the rank's start (leg children inherit it)
+
+
+def progress(msg, rank=0):
+    """One flushed stderr line per orchestration event (leg start / phase / done / failure), so a
+    stalled run says where it stopped; seconds since the rank process started."""
+    sys.stderr.write(f"bench[r{rank} {time.time() - T0_WALL:7.1f}s] {msg}\n")
+    sys.stderr.flush()
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
@@ -318,25 +360,286 @@ def main():
     ap.add_argument("--track-frames", type=int, default=56, help="track leg: steps (frames per sequence)")
     ap.add_argument("--track-inflight", type=int, default=1,
                     help="track leg: tracker handles the sequences are split over (each its own stream)")
-    ap.add_argument("--launch-timeout", type=float, default=3000.0,
-                    help="--gpus N > 1 started without WORLD_SIZE: seconds before the rank processes are killed")
-    args = ap.parse_args()
-    legs = set(x.strip() for x in args.legs.split(",") if x.strip())
+    ap.add_argument("--launch-timeout", type=float, default=570.0,
+                    help="--gpus N > 1 started without WORLD_SIZE: seconds before the rank processes are killed "
+                         "(below the driver's 600 s, so the launcher reports first)")
+    ap.add_argument("--job-deadline", type=float, default=540.0,
+                    help="seconds from a rank's start by which every leg must have ended (legs that would "
+                         "start later are skipped and recorded as such)")
+    ap.add_argument("--leg-timeout-scale", type=float, default=1.0, help="multiplies every leg's own cap (LEG_CAP_S)")
+    ap.add_argument("--leg-child", default=None, help=argparse.SUPPRESS)      # internal: run one leg here
+    ap.add_argument("--leg-deadline", type=float, default=0.0, help=argparse.SUPPRESS)
+    return ap.parse_args(argv)
 
+
+def leg_list(args):
+    want = [x.strip() for x in args.legs.split(",") if x.strip()]
+    bad = [x for x in want if x not in LEG_ORDER]
+    if bad:
+        raise SystemExit(f"bench.py: unknown leg(s) {bad}; known: {list(LEG_ORDER)}")
+    skip = {"lba": args.lba_windows <= 0, "pose": args.pose_frames <= 0, "track": args.track_seqs <= 0,
+            "localmap": args.localmap_frames <= 0, "projection": args.projection_frames <= 0}
+    return [x for x in LEG_ORDER if x in want and not skip.get(x, False)]
+
+
+def main():
+    args = parse_args()
+    if args.leg_child:
+        sys.exit(child_main(args))
+    legs = leg_list(args)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # the driver's `python bench.py --gpus N`: one child process per GPU, before any GPU call
         sys.exit(launch_ranks(args.gpus, sys.argv[1:], args.launch_timeout))
+    sys.exit(rank_main(args, legs))
 
+
+class LegCoord:
+    """What the rank processes of a job share about its legs (nothing when world = 1): a gloo group
+    on the host (no GPU call in these processes) for the per-leg rendezvous port and deadline, which
+    rank 0 chooses, and the statuses gathered after each leg; and its store, where a rank whose leg
+    failed says so at once, so the other ranks end their own leg child instead of waiting in a
+    collective until the deadline."""
+
+    def __init__(self, world, rank):
+        self.world, self.rank = world, rank
+        self.dist = self.store = None
+        if world > 1:
+            import torch.distributed as dist
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            sys.stdout.flush()
+            saved = os.dup(1)  # gloo may print to fd 1, which carries only the JSON line
+            os.dup2(2, 1)
+            try:
+                dist.init_process_group("gloo")
+            finally:
+                sys.stdout.flush()
+                os.dup2(saved, 1)
+                os.close(saved)
+            self.dist = dist
+            self.store = dist.distributed_c10d._get_default_store()
+
+    def plan(self, leg, deadline):
+        """(port, deadline) of this leg, the same on every rank (rank 0's)."""
+        obj = [_free_port() if self.rank == 0 else 0, deadline]
+        if self.dist:
+            self.dist.broadcast_object_list(obj, src=0)
+        return int(obj[0]), float(obj[1])
+
+    def fail(self, leg, why):
+        if self.store is not None:
+            self.store.set(f"bench/legfail/{leg}", f"{self.rank}:{why}")
+
+    def peer_failed(self, leg):
+        if self.store is None:
+            return None
+        key = f"bench/legfail/{leg}"
+        if self.store.check([key]):
+            return self.store.get(key).decode()
+        return None
+
+    def gather(self, status):
+        if not self.dist:
+            return [status]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, status)
+        return out
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def run_leg_child(args, leg, deadline, port, coord, scratch):
+    """Run one leg in a fresh child process (`bench.py --leg-child LEG`); returns (status, payload).
+    The child's stderr is ours; its stdout carries rank 0's one JSON line.  A child still running at
+    `deadline` seconds is stopped (SIGTERM, then SIGKILL after 10 s) and the leg is a timeout."""
+    import signal
+    import subprocess
+    import threading
+    rank, world = coord.rank, coord.world
+    env = dict(os.environ)
+    env.pop("TORCHELASTIC_USE_AGENT_STORE", None)  # the child's group has its own store (rank 0's child)
+    env.update(WORLD_SIZE=str(world), RANK=str(rank), LOCAL_RANK=os.environ.get("LOCAL_RANK", str(rank)),
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SLAMHOT_BENCH_SCRATCH=scratch,
+               SLAMHOT_BENCH_T0=repr(T0_WALL))
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    # a library wait on device progress gives up well before the leg's deadline (SLAM_ETIMEDOUT)
+    env.setdefault("SLAMHOT_WAIT_TIMEOUT_S", str(max(5, int(min(60.0, deadline / 3)))))
+    argv = [a for a in sys.argv[1:]]
+    cmd = [sys.executable, "-u", str(Path(__file__).resolve())] + argv + ["--leg-child", leg,
+                                                                           "--leg-deadline", f"{deadline:.1f}"]
+    t0 = time.monotonic()
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=None)
+    lines = []
+
+    def relay():
+        for raw in p.stdout:
+            s = raw.decode(errors="replace")
+            if s.lstrip().startswith("{"):
+                lines.append(s)
+            else:
+                sys.stderr.write(s)
+    th = threading.Thread(target=relay, daemon=True)
+    th.start()
+    status = None
+    while True:
+        rc = p.poll()
+        if rc is not None:
+            status = {"status": "ok" if rc == 0 else "failed", "rc": rc}
+            break
+        if time.monotonic() - t0 > deadline:
+            status = {"status": "timeout", "rc": 124}
+            break
+        peer = coord.peer_failed(leg)
+        if peer is not None:
+            status = {"status": "peer_failed", "rc": 1, "peer": peer}
+            break
+        time.sleep(0.1)
+    if p.poll() is None:
+        p.send_signal(signal.SIGTERM)
+        try:
+            p.wait(timeout=10)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+    th.join(timeout=10)
+    status.update(rank=rank, after_s=round(time.monotonic() - t0, 1))
+    if status["status"] == "failed" and status["after_s"] >= deadline - 6.0:
+        status.update(status="timeout", why="stopped itself at its deadline (stack dump on stderr)")
+    if status["status"] != "ok":
+        try:
+            status["phase"] = (Path(scratch) / f"phase.{leg}").read_text()
+        except OSError:
+            status["phase"] = None
+    if status["status"] in ("failed", "timeout"):
+        coord.fail(leg, status["status"])
+    payload = None
+    if status["status"] == "ok" and rank == 0:
+        if len(lines) != 1:
+            status.update(status="failed", rc=1, why=f"rank 0 printed {len(lines)} JSON lines, expected 1")
+        else:
+            payload = json.loads(lines[0])["result"]
+    return status, payload
+
+
+def merge_leg(result, leg, payload):
+    if leg == "dry":
+        result.update(payload)
+    elif leg == "headline":
+        for k in ("value", "ms_per_step", "config", "roofline", "cpu_baseline"):
+            if k in payload:
+                result[k] = payload.pop(k)
+        result["headline_detail"] = payload
+    elif leg == "extract":
+        result["extract"] = payload
+        if result["value"] is None:  # headline off (profiling runs): the extract leg's line
+            result.update(value=payload["value"], ms_per_step=payload["ms_per_step"], config=payload["config"],
+                          roofline=payload["roofline"])
+    else:
+        result[leg] = payload
+
+
+def rank_main(args, legs):
+    """One rank of the job (the only one at N = 1): runs each leg in a child process of its own
+    (fresh HIP context, its own deadline), merges the legs into the one JSON line (rank 0) and
+    records a leg that failed or timed out as an error entry; the first leg of the list (the
+    headline) is the line's value, so its failure fails the job, naming the leg and the rank."""
+    import tempfile
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world != args.gpus and rank == 0:
+        sys.stderr.write(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; one rank per GPU, n_gpus = {world}\n")
+    if rank == 0:
+        progress(f"bench.py: legs {','.join(legs)}, {world} rank(s), steps {args.steps}, warmup {args.warmup}")
+    # this process never touches the GPU; importing torch here pages the image in once (1-2 min on
+    # a fresh box) outside every leg's deadline
+    import torch  # noqa: F401
+    coord = LegCoord(world, rank)
+    result = {
+        "metric": "ORB extract+match frames/s and LocalBA iters/s per GPU; ATE vs reference",
+        "value": None, "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": None, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (rendered textured-room stereo sequences / procedural frames, slamhot/synth.py)",
+    }
+    legs_info = {}
+    primary_fail = None
+    with tempfile.TemporaryDirectory(prefix="slamhot_bench_") as scratch:
+        for leg in legs:
+            left = args.job_deadline - (time.monotonic() - T_START)
+            want = min(LEG_CAP_S[leg] * args.leg_timeout_scale, left - 5.0)
+            port, deadline = coord.plan(leg, want)
+            if deadline < 5.0:
+                if rank == 0:
+                    progress(f"leg {leg} skipped: {left:.0f} s left of the job deadline")
+                result[leg] = {"error": "skipped", "why": f"job deadline ({args.job_deadline:.0f} s) reached"}
+                if leg == legs[0]:
+                    primary_fail = (leg, {"status": "skipped", "rank": rank, "rc": 124})
+                    break
+                continue
+            if rank == 0:
+                progress(f"leg {leg} start (deadline {deadline:.0f} s)")
+            status, payload = run_leg_child(args, leg, deadline, port, coord, scratch)
+            sts = coord.gather(status)
+            bad = [s_ for s_ in sts if s_["status"] != "ok"]
+            legs_info[leg] = {"s": status["after_s"], "status": "ok" if not bad else "error"}
+            if not bad:
+                if rank == 0:
+                    progress(f"leg {leg} done in {status['after_s']:.1f} s")
+                    merge_leg(result, leg, payload)
+                continue
+            # the rank that failed first (a peer that stopped because of it is not the cause)
+            # and of the ranks that timed out together, one stuck in its own work, not one waiting for
+            # it in a collective
+            def waiting(s_):
+                return (s_.get("phase") or "").startswith("collective")
+            cause = sorted(bad, key=lambda s_: (s_["status"] == "peer_failed", waiting(s_), s_["after_s"]))[0]
+            err = {"error": cause["status"], "rank": cause["rank"], "rc": cause["rc"], "after_s": cause["after_s"],
+                   "deadline_s": round(deadline, 1), "phase": cause.get("phase"),
+                   "ranks": {str(s_["rank"]): f"{s_['status']} ({s_.get('phase')})" for s_ in bad}}
+            if "why" in cause:
+                err["why"] = cause["why"]
+            if rank == 0:
+                progress(f"leg {leg} FAILED: {cause['status']} on rank {cause['rank']} (rc {cause['rc']}) after "
+                         f"{cause['after_s']:.1f} s, in phase: {cause.get('phase')}")
+            if leg == legs[0]:
+                primary_fail = (leg, cause)
+                break
+            result[leg] = err
+    coord.close()
+    if primary_fail:
+        leg, cause = primary_fail
+        sys.stderr.write(f"bench.py: leg {leg} {cause['status']} on rank {cause['rank']} (phase: {cause.get('phase')}); "
+                         f"no line printed\n")
+        rc = int(cause.get("rc") or 1)
+        return rc if 0 < rc < 256 else 1
+    if rank == 0:
+        result["legs"] = {"isolation": "one child process per leg (fresh HIP context), per-leg deadline",
+                          "wall_s": legs_info, "job_wall_s": round(time.monotonic() - T_START, 1)}
+        add_full_socket(result)
+        print(json.dumps(result), flush=True)
+    return 0
+
+
+def child_main(args):
+    """One leg in this process (started by rank_main): the rank's process group on the leg's own
+    port, the leg, rank 0 prints {"leg", "result"}.  A Python stack dump of every thread and exit
+    just before the parent's deadline, so a stall leaves its place on stderr."""
+    import faulthandler
+    leg = args.leg_child
+    PHASE.update(rank=int(os.environ.get("RANK", "0")), leg=leg,
+                 file=os.path.join(os.environ["SLAMHOT_BENCH_SCRATCH"], f"phase.{leg}")
+                 if os.environ.get("SLAMHOT_BENCH_SCRATCH") else None)
+    phase("compute: starting (import torch, process group)")
+    if args.leg_deadline > 0:
+        faulthandler.dump_traceback_later(max(1.0, args.leg_deadline - 5.0), exit=True)
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        sys.stderr.write(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; one rank per GPU, n_gpus = {world}\n")
     dist = None
-    # `--legs dry` is the GPU-free rehearsal of the launcher and the collectives (host only, gloo)
-    dry = legs == {"dry"}
+    # dry legs: the GPU-free rehearsal of the launcher and the collectives (host only, gloo)
+    dry = leg in ("dry", "dryaux")
     # one GPU per rank; SLAMHOT_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share
     # cuda:(local_rank mod device_count), collectives on host copies) — the driver's runs use nccl
     backend = "gloo" if dry else os.environ.get("SLAMHOT_BENCH_BACKEND", "nccl")
@@ -367,45 +670,19 @@ def main():
     else:
         device = torch.device("cuda", gpu)
         torch.cuda.set_device(device)
-    local_rank = gpu
-    ctx = dict(args=args, rank=rank, world=world, local_rank=local_rank, dist=dist, device=device,
+    phase("compute: leg setup")
+    ctx = dict(args=args, rank=rank, world=world, local_rank=gpu, dist=dist, device=device, leg=leg,
                cpu=(rank == 0 and world == 1 and not args.no_cpu_baseline))
-
-    result = {
-        "metric": "ORB extract+match frames/s and LocalBA iters/s per GPU; ATE vs reference",
-        "value": None, "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": None, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-        "data": "synthetic (rendered textured-room stereo sequences / procedural frames, slamhot/synth.py)",
-    }
-    if dry:
-        result.update(dry_leg(ctx))
-    if "headline" in legs:
-        h = headline_leg(ctx)
-        for k in ("value", "ms_per_step", "config", "roofline", "cpu_baseline"):
-            if k in h:
-                result[k] = h.pop(k)
-        result["headline_detail"] = h
-    if "extract" in legs:
-        result["extract"] = extract_leg(ctx)
-        if result["value"] is None:  # headline off (profiling runs): the extract leg's line
-            e = result["extract"]
-            result.update(value=e["value"], ms_per_step=e["ms_per_step"], config=e["config"],
-                          roofline=e["roofline"])
-    if "lba" in legs and args.lba_windows > 0:
-        result["lba"] = lba_leg(ctx)
-    if "pose" in legs and args.pose_frames > 0:
-        result["pose"] = pose_leg(ctx)
-    if "track" in legs and args.track_seqs > 0:
-        result["track"] = track_leg(ctx)
-    if "localmap" in legs and args.localmap_frames > 0:
-        result["localmap"] = localmap_leg(ctx)
-    if "projection" in legs and args.projection_frames > 0:
-        result["projection"] = projection_leg(ctx)
+    fn = {"dry": dry_leg, "dryaux": dry_leg, "headline": headline_leg, "extract": extract_leg, "lba": lba_leg,
+          "pose": pose_leg, "track": track_leg, "localmap": localmap_leg, "projection": projection_leg}[leg]
+    out = fn(ctx)
+    phase("compute: leg done")
     if rank == 0:
-        add_full_socket(result)
-        print(json.dumps(result), flush=True)
+        print(json.dumps({"leg": leg, "result": out}), flush=True)
     if dist:
         dist.destroy_process_group()
+    faulthandler.cancel_dump_traceback_later()
+    return 0
 
 
 def dry_leg(ctx):
@@ -420,9 +697,15 @@ def dry_leg(ctx):
     n = max(1, args.pairs // 32)
     idx = [rank * n + i for i in range(n)]
     state = {}
-    if os.environ.get("SLAMHOT_DRY_FAIL_RANK") == str(rank):  # the launcher's failure path, under test
+    # the failure paths under test (tests/test_bench_launch.py): SLAMHOT_DRY_FAIL_RANK=r fails rank r
+    # of leg "dry"; SLAMHOT_DRY_HANG=leg:r hangs rank r of that leg (a host stall: no progress, no exit)
+    if ctx["leg"] == "dry" and os.environ.get("SLAMHOT_DRY_FAIL_RANK") == str(rank):
         sys.stderr.write(f"dry leg: rank {rank} failing on request\n")
         sys.exit(3)
+    if os.environ.get("SLAMHOT_DRY_HANG") == f"{ctx['leg']}:{rank}":
+        sys.stderr.write(f"{ctx['leg']} leg: rank {rank} hanging on request\n")
+        while True:
+            time.sleep(1)
 
     def step(_):
         state["dig"] = sdist.combine(sdist.unit_hash(g, synth.frame(g, 320, 240)) for g in idx)
@@ -476,6 +759,24 @@ def stereo_chunks(rank, maps, nframes):
     return np.stack(rl), np.stack(rr)
 
 
+def load_chunks(ctx, maps, nframes):
+    """stereo_chunks(rank, maps, nframes), rendered once per rank: the first leg child that needs them
+    renders and leaves them in the rank's scratch directory (SLAMHOT_BENCH_SCRATCH), later ones load
+    them."""
+    d = os.environ.get("SLAMHOT_BENCH_SCRATCH")
+    f = Path(d) / f"chunks_{nframes}.npz" if d else None
+    if f is not None and f.exists():
+        z = np.load(f)
+        return z["l"], z["r"]
+    phase(f"compute: rendering {nframes} stereo frames")
+    raw_l, raw_r = stereo_chunks(ctx["rank"], maps, nframes)
+    if f is not None:
+        tmp = f.with_suffix(".tmp.npz")
+        np.savez(tmp, l=raw_l, r=raw_r)
+        tmp.rename(f)
+    return raw_l, raw_r
+
+
 def kf_of(i):
     """Reference keyframe of batch frame i: the previous frame of its sequence chunk (the chunk's
     first frame takes its last one)."""
@@ -492,8 +793,7 @@ def headline_leg(ctx):
     W, H, NF = 752, 480, 1200
     P = max(SEQ_LEN, args.pairs // SEQ_LEN * SEQ_LEN)
     maps = euroc_maps()
-    raw_l, raw_r = stereo_chunks(ctx["rank"], maps, P)
-    ctx["chunks"] = (raw_l, raw_r)
+    raw_l, raw_r = load_chunks(ctx, maps, P)
     nu = len(raw_l)  # every frame of the batch is distinct
     il, ir = raw_l, raw_r
     pairs = [(kf_of(i), i) for i in range(P)]
@@ -561,6 +861,7 @@ def headline_leg(ctx):
             for k_, a, b in zip(("rectify", "extract", "stereo", "bow"), marks[:-1], marks[1:]):
                 ev[k_].append((a, b))
 
+    phase("compute: warm-up steps")
     for i in range(max(args.warmup, 1)):
         step(i)
     elapsed = timed_region(dist, device, step, args.steps)
@@ -619,6 +920,7 @@ def headline_leg(ctx):
                            "mvuRight, SearchByBoW a2b / b2a, nmatches) mod 2^62"},
     }
     if ctx["cpu"]:
+        phase("compute: CPU baseline (oracle on the host cores)")
         out["cpu_baseline"] = headline_cpu(raw_l, raw_r, maps, voc_arrays, mbf, mb, NF)
     for s in slots:
         for rc in s.rect:
@@ -765,6 +1067,7 @@ def extract_leg(ctx):
         },
     }
     if ctx["cpu"]:
+        phase("compute: CPU baseline (oracle on the host cores)")
         out["cpu_baseline"] = extract_cpu(args, W, H)
     for e in exs:
         e.close()
@@ -835,6 +1138,7 @@ def pose_leg(ctx):
         "mean_inliers": round(float(np.mean([r["n_inliers"] for r in res[-1]])), 1),
     }
     if ctx["cpu"]:
+        phase("compute: CPU baseline (oracle on the host cores)")
         sys.path.insert(0, str(ROOT / "tests"))
         import oracle_bind as ob
         cores = host_cores()
@@ -910,6 +1214,7 @@ def localmap_leg(ctx):
         "call_split": call_split(m, el / calls * 1e3),
     }
     if ctx["cpu"]:
+        phase("compute: CPU baseline (oracle on the host cores)")
         import oracle_bind as ob
         cores = host_cores()
 
@@ -989,6 +1294,7 @@ def projection_leg(ctx):
                              "call_split": call_split(mk, elk / calls * 1e3)},
     }
     if ctx["cpu"]:
+        phase("compute: CPU baseline (oracle on the host cores)")
         import oracle_bind as ob
         cores = host_cores()
 
@@ -1035,6 +1341,8 @@ def lba_leg(ctx):
     ate_dev = [window_ate(w, r["kf_Tcw"]) for w, r in zip(pool, S.solve(pool))]
     ate_init = [window_ate(w, w["kf_Tcw"]) for w in pool]
     it1 = single["iterations"][0] + single["iterations"][1]
+    phase("compute: LBA drop-in call (tests/cpp/shim_driver lbatime)")
+    drop_in = lba_drop_in(pool[0])
     # `lba_inflight` solver handles driven from host threads (the C call releases the GIL), each
     # on its own window set: one call's host planning overlaps another's device LM loop.  The
     # windows are flattened to C structs before the timed region, as a C++ caller holds them.
@@ -1097,13 +1405,14 @@ def lba_leg(ctx):
         "host_plan_ms_per_call": round(plan_ms / args.lba_calls, 3),
         "single_window": {"lm_iterations": it1, "device_ms": round(dev1, 3),
                           "ms_per_lm_iteration": round(dev1 / max(it1, 1), 4),
-                          "drop_in": lba_drop_in(pool[0])},
+                          "drop_in": drop_in},
         "ate": {"metric": "ATE RMSE of the window's KeyFrame centres vs ground truth after LBA "
                           "(SE3 alignment, slamhot.ate = evaluate_ate_scale.py align)",
                 "unit": "m", "windows": len(pool),
                 "initial": round(float(np.mean(ate_init)), 7), "device": round(float(np.mean(ate_dev)), 7)},
     }
     if ctx["cpu"]:
+        phase("compute: CPU baseline (oracle on the host cores)")
         sys.path.insert(0, str(ROOT / "tests"))
         import oracle_bind as ob
         cores = host_cores()
@@ -1208,7 +1517,8 @@ def track_leg(ctx):
     S, K = args.track_seqs, args.track_frames
     W, H = 752, 480
     maps = euroc_maps()
-    raw_l, raw_r = ctx.get("chunks") or stereo_chunks(ctx["rank"], maps, 2 * SEQ_LEN)
+    # the headline's frames (its leg child left them in the rank's scratch directory)
+    raw_l, raw_r = load_chunks(ctx, maps, max(SEQ_LEN, args.pairs // SEQ_LEN * SEQ_LEN))
     nch = len(raw_l) // SEQ_LEN
     voc_arrays = sdist.broadcast_arrays(dist, device, synth.vocab(10, 6, 0) if ctx["rank"] == 0 else None)
     voc = slamhot.Vocabulary(*voc_arrays, k=10, L=6, device=lr)
@@ -1293,6 +1603,7 @@ def track_leg(ctx):
         "ate_seq0_m": round(float(np.sqrt(np.mean(err * err))), 5),
     }
     if ctx["cpu"]:
+        phase("compute: CPU baseline (oracle on the host cores)")
         out["cpu_baseline"] = track_cpu(raw_l, raw_r, maps, voc_arrays, order[: 2 * SEQ_LEN])
     return out
 

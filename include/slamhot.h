@@ -32,7 +32,9 @@ enum {
     SLAM_EHIP = -3,    /* HIP runtime error */
     SLAM_ECAP = -4,    /* output capacity too small (n holds the required size) */
     SLAM_ENODEV = -5,  /* no gfx950 device */
-    SLAM_EEMPTY = -6   /* empty image (reference returns -1, ORBextractor.cc:1072-1073) */
+    SLAM_EEMPTY = -6,  /* empty image (reference returns -1, ORBextractor.cc:1072-1073) */
+    SLAM_ETIMEDOUT = -7 /* a bounded wait expired (host wait on device progress, or a device-side
+                           hand-off wait); the handle's stream state is printed on stderr */
 };
 
 /* cv::KeyPoint memory layout (28 bytes): pt.x, pt.y, size, angle, response, octave, class_id */

@@ -165,7 +165,7 @@ inline void huber_cc(double e, double delta, float dsqr, double* rho) {
     }
 }
 
-// g2o::EdgeStereoSE3ProjectXYZOnlyPose::linearizeOplus (types_six_dof_expmap.cpp:388-423,
+// g2o::EdgeStereoSE3ProjectXYZOnlyPose::linearizeOplus (types_six_dof_expmap.cpp:375-404,
 // @0x1280): 3x6 row-major; the "1 + a invz^2" and the stereo-row corrections are fused.
 inline void lin_pose_stereo_cc(const SE3& T, const double* Xw, double fx, double fy, double bf, double* A) {
     double Xc[3];

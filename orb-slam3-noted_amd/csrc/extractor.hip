@@ -1697,7 +1697,9 @@ __global__ void __launch_bounds__(64 * kOrbWpg) k_orb3(Bufs b) {
     if (slot >= kslots) return;
     const int oi = b.oidx[(size_t)f * kslots + slot];
     const uint32_t key = b.okp[(size_t)f * kslots + slot];
-    const int kb = P.orb_lv[min(lane, kMaxLevels - 1)].kbase;  // INT_MAX past the last level
+    // INT_MAX past the last level: lanes >= kMaxLevels must not repeat level kMaxLevels-1's kbase
+    // (with nlevels == kMaxLevels that would push the ballot count past the table)
+    const int kb = lane < kMaxLevels ? P.orb_lv[lane].kbase : INT_MAX;
     const int l = __builtin_amdgcn_readfirstlane(__popcll(__ballot(slot >= kb)) - 1);  // kbase[0] = 0
     const OrbLv& O = P.orb_lv[l];
     if ((slot - O.kbase >= b.ocnt[(size_t)f * nlev + l]) | (oi >= b.cap)) return;  // one branch
@@ -2514,6 +2516,7 @@ const char* slamhot_status_string(slam_status s) {
         case SLAM_ECAP: return "output capacity too small";
         case SLAM_ENODEV: return "no gfx950 device";
         case SLAM_EEMPTY: return "empty image";
+        case SLAM_ETIMEDOUT: return "wait timed out";
         default: return "unknown status";
     }
 }

@@ -1587,7 +1587,14 @@ struct T16Lds {
     int done_cnt[kT16Max];                 // worker waves done with panel k (15 = all)
     int x_low;                             // lowest k whose x_k wave 0 has published
     int prog[kT16Waves];                   // back-solve: last step whose updates wave w has applied
+    int hang;                              // a hand-off wait ran past kT16SpinCap (bounded waits)
 };
+// Polls of one LDS hand-off word before the wait gives up (each poll sleeps ~64 cycles, so about a
+// quarter of a second; a wait in a healthy factorization lasts well under a microsecond).  A wait
+// that gives up raises L.hang, which ends every other wait at once: the kernel finishes, the trial
+// fails (ok2 = 0) and the launch's error word tells the host (SLAM_ETIMEDOUT), instead of a
+// workgroup spinning forever on a flag that never comes.
+constexpr unsigned kT16SpinCap = 1u << 22;
 __host__ __device__ constexpr long long t16_tiles_bytes() { return (long long)kT16Tiles * 256 * sizeof(double); }
 
 __device__ __forceinline__ double t16_sum16(double v) {  // sum over the 16 lanes of a DPP row (every lane)
@@ -1718,7 +1725,7 @@ __device__ __forceinline__ void t16_diag(Lds& L, int k, double4_t dt, int lane) 
 
 __global__ void __launch_bounds__(kT16Waves * 64) k_ldlt_t16(const WinDesc* __restrict__ wins, WinCtl* __restrict__ ctl,
                                                              const double* __restrict__ Hs, double* __restrict__ Ts,
-                                                             double* __restrict__ xp_out) {
+                                                             double* __restrict__ xp_out, int* __restrict__ err_word) {
     __shared__ T16Lds L;
     const WinDesc W = wins[blockIdx.x];
     WinCtl& C = ctl[blockIdx.x];
@@ -1741,6 +1748,7 @@ __global__ void __launch_bounds__(kT16Waves * 64) k_ldlt_t16(const WinDesc* __re
         }
         L.col0[T] = (unsigned short)t;
         L.fail = 0;
+        L.hang = 0;
     }
     for (int c = tid; c < 16 * T; c += blockDim.x) L.y[c] = A[(long long)rhs * ld + c];
     if (tid == 0) {
@@ -1782,8 +1790,17 @@ __global__ void __launch_bounds__(kT16Waves * 64) k_ldlt_t16(const WinDesc* __re
             __hip_atomic_fetch_add(&L.trsm_cnt[kk], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     };
+    // bounded: gives up after kT16SpinCap polls, or at once when another wave gave up (L.hang)
+    auto give_up = [&](unsigned spin) {
+        if (spin < kT16SpinCap && !__hip_atomic_load(&L.hang, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return false;
+        __hip_atomic_store(&L.hang, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return true;
+    };
     auto wait_at_least = [&](int* w, int v) {
-        while (__hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v) __builtin_amdgcn_s_sleep(1);
+        for (unsigned spin = 0; __hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v; spin++) {
+            if (give_up(spin)) return;
+            __builtin_amdgcn_s_sleep(1);
+        }
     };
     // the tiles were written by k_schur_block (t16_put); padding by k_t16_pad
     double4_t diag1 = {0.0, 0.0, 0.0, 0.0};  // wave 0: tile (1, 1), untouched before panel 0
@@ -1894,8 +1911,11 @@ __global__ void __launch_bounds__(kT16Waves * 64) k_ldlt_t16(const WinDesc* __re
     }
     __syncthreads();
     T16_MARK(4);
-    if (L.fail) {
-        if (tid == 0) C.ok2 = 0;
+    if (L.fail || L.hang) {
+        if (tid == 0) {
+            C.ok2 = 0;
+            if (L.hang) atomicAdd(err_word, 1);
+        }
         return;
     }
     // L^T x = z, right-looking from the last tile column.  Wave 0 owns the tiles (k, k-1) next to
@@ -1926,8 +1946,11 @@ __global__ void __launch_bounds__(kT16Waves * 64) k_ldlt_t16(const WinDesc* __re
             }
         };
         auto tile = [&](int k, int j) { return t16_load(Tw + 256 * (L.col0[j] + k - j), lane); };
-        auto wait_ge = [&](int* w, int v) {  // LDS word reaches v (counting down: <=)
-            while (__hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) > v) __builtin_amdgcn_s_sleep(1);
+        auto wait_ge = [&](int* w, int v) {  // LDS word reaches v (counting down: <=); bounded
+            for (unsigned spin = 0; __hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) > v; spin++) {
+                if (give_up(spin)) return;
+                __builtin_amdgcn_s_sleep(1);
+            }
         };
         const int nw1 = kT16Waves - 1;
         const double4_t zero = {0.0, 0.0, 0.0, 0.0};
@@ -1979,7 +2002,10 @@ __global__ void __launch_bounds__(kT16Waves * 64) k_ldlt_t16(const WinDesc* __re
     }
     __syncthreads();
     T16_MARK(5);
-    if (tid == 0) C.ok2 = 1;
+    if (tid == 0) {
+        C.ok2 = L.hang ? 0 : 1;
+        if (L.hang) atomicAdd(err_word, 1);
+    }
 }
 
 // Identity padding of the dense systems (rows/cols n..npad-1) and a zero rhs tail; the
@@ -2135,6 +2161,9 @@ __device__ __forceinline__ void tally_publish(int* __restrict__ tally, int need,
         // need_trial and active in one store, then the sequence number the host spins on
         *reinterpret_cast<volatile unsigned long long*>(host_slot) =
             (tot & field) | (((tot >> kTallyBits) & field) << 32);
+        // device-side hand-offs that gave up this solve (k_ldlt_t16's bounded waits): the host
+        // ends the call with SLAM_ETIMEDOUT
+        reinterpret_cast<volatile Counters*>(host_slot)->pad = ((volatile int*)tally)[6];
         __threadfence_system();
         reinterpret_cast<volatile Counters*>(host_slot)->seq = seq;
     }
@@ -2534,43 +2563,58 @@ constexpr int kRing = 4;  // LM steps whose counters are in flight (host-side ri
 
 // The planning threads of one handle, kept between calls (spawning and joining them twice per
 // call cost ~0.1-0.3 ms): run(n, f) calls f(0) on the caller and f(1..n-1) on the workers.
+// A worker is created knowing the generation current at its creation (read under the lock), so it
+// waits for the next run() and never acts on an older one (a worker created with 0 after gen had
+// advanced woke on that stale generation and decremented busy below zero).  run() always waits for
+// every worker before it returns, also when a job throws (the job and its captures live on the
+// caller's stack); the first exception of a call is returned, never let across the C ABI.
 struct PlanPool {
     std::vector<std::thread> th;
     std::mutex m;
     std::condition_variable cv, done;
     unsigned long long gen = 0;
     int busy = 0, n = 0;
-    bool stop = false;
+    bool stop = false, failed = false;
     const std::function<void(int)>* job = nullptr;
 
-    // false: fewer workers than asked for (thread creation failed); the caller runs the rest
+    // the number of threads run() can use (workers + the caller); fewer than asked when thread
+    // creation fails, and the caller then runs the rest
     int ensure(int want) {
+        std::lock_guard<std::mutex> lk(m);
         while ((int)th.size() < want - 1) {
             const int t = (int)th.size() + 1;
+            const unsigned long long g = gen;
             try {
-                th.emplace_back([this, t] { worker(t); });
+                th.emplace_back([this, t, g] { worker(t, g); });
             } catch (...) {
                 break;
             }
         }
         return (int)th.size() + 1;
     }
-    void run(int nt, const std::function<void(int)>& f) {
+    // false: a job threw (on the caller or on a worker); every worker has finished either way
+    bool run(int nt, const std::function<void(int)>& f) {
         {
             std::lock_guard<std::mutex> lk(m);
             job = &f;
             n = nt;
             busy = (int)th.size();
+            failed = false;
             gen++;
         }
         cv.notify_all();
-        f(0);
+        bool ok = true;
+        try {
+            f(0);
+        } catch (...) {
+            ok = false;
+        }
         std::unique_lock<std::mutex> lk(m);
         done.wait(lk, [&] { return busy == 0; });
         job = nullptr;
+        return ok && !failed;
     }
-    void worker(int t) {
-        unsigned long long seen = 0;
+    void worker(int t, unsigned long long seen) {
         std::unique_lock<std::mutex> lk(m);
         for (;;) {
             cv.wait(lk, [&] { return stop || gen != seen; });
@@ -2579,8 +2623,16 @@ struct PlanPool {
             const std::function<void(int)>* f = job;
             const int nt = n;
             lk.unlock();
-            if (t < nt) (*f)(t);
+            bool ok = true;
+            if (t < nt && f) {
+                try {
+                    (*f)(t);
+                } catch (...) {
+                    ok = false;
+                }
+            }
             lk.lock();
+            if (!ok) failed = true;
             if (--busy == 0) done.notify_all();
         }
     }
@@ -2709,6 +2761,17 @@ Plan bind(unsigned char* base, const Layout& L) {
 // CPU share, delaying the solver threads that launch the next LM step; with the threads kept
 // between calls, 8 measured best (plan 4.0-4.5 -> 2.6-2.8 ms per 128-window call, LBA leg
 // 131-134k -> 139-145k LM it/s, profiles/r05_lba_plan.txt).  SLAMHOT_LBA_PLAN_THREADS overrides.
+// Seconds a host wait on device progress may last (SLAMHOT_WAIT_TIMEOUT_S, default 60): one LM
+// step of a 128-window batch takes about a millisecond.
+double wait_timeout_s() {
+    static const double v = [] {
+        const char* e = std::getenv("SLAMHOT_WAIT_TIMEOUT_S");
+        const double x = e ? std::atof(e) : 0.0;
+        return x > 0.0 ? x : 60.0;
+    }();
+    return v;
+}
+
 int plan_threads(int n_prob) {
     static const int cap_env = std::getenv("SLAMHOT_LBA_PLAN_THREADS") ? std::atoi(std::getenv("SLAMHOT_LBA_PLAN_THREADS")) : 0;
     const int cap = cap_env > 0 ? cap_env : 8;
@@ -2727,22 +2790,30 @@ slam_status for_windows(int n_prob, int nth, F fn, PlanPool* pool) {
             if (r != SLAM_OK) rs[t] = r;
         }
     };
+    // a scratch allocation that throws (bad_alloc) ends that thread's windows with SLAM_ENOMEM
+    auto run_safe = [&](int t) {
+        try {
+            run(t);
+        } catch (...) {
+            rs[t] = SLAM_ENOMEM;
+        }
+    };
     if (nth <= 1) {
-        run(0);
+        run_safe(0);
     } else if (pool) {
         const int have = pool->ensure(nth);
         const std::function<void(int)> f = [&](int t) {
-            for (int u = t; u < nth; u += have) run(u);  // threads the pool could not start: here
+            for (int u = t; u < nth; u += have) run_safe(u);  // threads the pool could not start: here
         };
-        pool->run(std::min(have, nth), f);
+        if (!pool->run(std::min(have, nth), f)) return SLAM_ENOMEM;
     } else {
         std::vector<std::thread> th;
         try {
-            for (int t = 1; t < nth; t++) th.emplace_back(run, t);
+            for (int t = 1; t < nth; t++) th.emplace_back(run_safe, t);
         } catch (...) {  // thread creation failed: the rest run here
-            for (int t = (int)th.size() + 1; t < nth; t++) run(t);
+            for (int t = (int)th.size() + 1; t < nth; t++) run_safe(t);
         }
-        run(0);
+        run_safe(0);
         for (auto& x : th) x.join();
     }
     for (slam_status r : rs)
@@ -3332,7 +3403,7 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
         add(dTally, 1, 0ull);                                         // need, active
         add(dTally + 2, 1, 0ull);                                     // ticket, -
         add(dTally + 4, 1, st2 | (st2 << 32));                        // stop samples x 2
-        add(dTally + 6, 1, 0ull);
+        add(dTally + 6, 1, 0ull);                                     // device error word, -
         if (use_t16) add(s->Ts.p, t16_tiles_bytes() * nw / 8, 0ull);  // tile scratch (padding by k_t16_pad)
         if (CL.n != (use_t16 ? 9 : 8)) return SLAM_EINVAL;  // every range above made it into the list
         SA.clear = CL;
@@ -3416,15 +3487,45 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     // number into the mapped slot after the counts.  The host spins on that word (mirroring the
     // caller's stop flag meanwhile) and asks the stream for errors now and then, so a faulted
     // kernel ends the wait instead of hanging it.
-    auto wait_step = [&](int slot, int seq) -> hipError_t {
+    // The wait is bounded in wall-clock time (wait_timeout_s(), SLAMHOT_WAIT_TIMEOUT_S): a step
+    // whose counters do not arrive by then ends the call with SLAM_ETIMEDOUT, naming the slot, the
+    // sequence numbers and the stream state on stderr.  After every 1024 polls the thread also
+    // yields its core: several solver threads wait at once beside the planning threads, and a
+    // waiter must not hold a core another thread needs to queue the work it waits for.
+    const auto wait_deadline = std::chrono::duration<double>(wait_timeout_s());
+    auto wait_step = [&](int slot, int seq) -> slam_status {
         volatile Counters* c = s->h_cnt + slot;
+        const auto t0 = std::chrono::steady_clock::now();
         for (unsigned spin = 1;; spin++) {
-            if (c->seq == seq) return hipSuccess;
+            if (c->seq == seq) {
+                if (c->pad != 0) {
+                    std::fprintf(stderr, "slamhot lba: %d device hand-off wait(s) gave up in k_ldlt_t16 (step seq %d)\n",
+                                 (int)c->pad, seq);
+                    return SLAM_ETIMEDOUT;
+                }
+                return SLAM_OK;
+            }
             if (!*s->h_stop && user_stop()) *s->h_stop = 1;
             if ((spin & 1023) == 0) {
                 const hipError_t e = hipStreamQuery(S);
-                if (e == hipSuccess && c->seq != seq) return hipErrorUnknown;  // drained without publishing
-                if (e != hipSuccess && e != hipErrorNotReady) return e;
+                if (e == hipSuccess && c->seq != seq) {  // drained without publishing
+                    std::fprintf(stderr, "slamhot lba: stream drained without step seq %d (slot %d holds %d)\n", seq, slot,
+                                 (int)c->seq);
+                    return SLAM_EHIP;
+                }
+                if (e != hipSuccess && e != hipErrorNotReady) {
+                    std::fprintf(stderr, "slamhot lba: stream error %s waiting for step seq %d\n", hipGetErrorName(e), seq);
+                    return SLAM_EHIP;
+                }
+                if (std::chrono::steady_clock::now() - t0 > wait_deadline) {
+                    std::fprintf(stderr,
+                                 "slamhot lba: no counters for step seq %d after %.0f s (slot %d holds seq %d, stream %s, "
+                                 "%d windows); SLAM_ETIMEDOUT\n",
+                                 seq, wait_deadline.count(), slot, (int)c->seq,
+                                 e == hipErrorNotReady ? "busy" : "idle", nw);
+                    return SLAM_ETIMEDOUT;
+                }
+                std::this_thread::yield();
             }
             _mm_pause();
         }
@@ -3463,7 +3564,8 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
                                                     as<double>(s->bp), as<double>(s->lin), as<double>(s->pd),
                                                     as<double>(s->Hs), tiles);
         if (use_t16)
-            k_ldlt_t16<<<nw, kT16Waves * 64, 0, S>>>(dW, dC, as<double>(s->Hs), as<double>(s->Ts), as<double>(s->xp));
+            k_ldlt_t16<<<nw, kT16Waves * 64, 0, S>>>(dW, dC, as<double>(s->Hs), as<double>(s->Ts), as<double>(s->xp),
+                                                     dTally + 6);
         else
             k_ldlt<<<nw, 512, lds_bytes, S>>>(dW, dC, as<double>(s->Hs), as<double>(s->xp));
         if (nb_upd)
@@ -3497,7 +3599,12 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
                 if (launched - checked < 2) continue;  // two steps queued before the first wait
             }
             const int slot = (int)(checked % kRing);
-            SLAM_HIP_TRY(wait_step(slot, seqs[slot]));
+            {
+                // an error ends the call here; steps still queued stay ordered on the handle's
+                // stream ahead of anything a later call queues
+                const slam_status ws = wait_step(slot, seqs[slot]);
+                if (ws != SLAM_OK) return ws;
+            }
             if (syncs == 0) mark();  // 2: the first step's counters are in
             syncs++;
             checked++;
@@ -3607,6 +3714,47 @@ slam_status slamhot_lba_plan_bench(int n_prob, const slam_lba_problem* probs, co
         *fill_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
         *arena_mb = LY.total / 1e6;
     }
+    return SLAM_OK;
+}
+
+// Sanitizer builds (tests/cpp/plan_stress.cpp under TSan / ASan, `make sanitize-plan`): nthreads
+// host threads, each with a PlanPool and an arena of its own (one per solver handle, as slam_lba
+// holds them), plan rounds x ncounts calls of the first counts[c] windows each, so every pool gains
+// workers between calls (4 -> 8 -> 128 windows) while the other threads plan too.  Every thread's
+// host plan of a call must equal the others' byte for byte (SLAM_EINVAL otherwise).
+slam_status slamhot_lba_plan_stress(int nthreads, int rounds, const int* counts, int ncounts, int n_prob,
+                                    const slam_lba_problem* probs, const slam_lba_options* opt) {
+    if (nthreads < 1 || rounds < 1 || ncounts < 1 || !counts || !probs || !opt) return SLAM_EINVAL;
+    const int ncalls = rounds * ncounts;
+    std::vector<std::vector<unsigned long long>> hashes(nthreads, std::vector<unsigned long long>(ncalls, 0));
+    std::vector<slam_status> st(nthreads, SLAM_OK);
+    auto body = [&](int t) {
+        PlanPool pool;
+        std::vector<unsigned char> arena;
+        for (int r = 0; r < rounds; r++)
+            for (int c = 0; c < ncounts; c++) {
+                const int n = std::min(counts[c], n_prob);
+                PlanSizes Z;
+                std::vector<int> hidx_all, np_of;
+                slam_status s = plan_sizes(n, probs, Z, hidx_all, np_of, &pool);
+                if (s != SLAM_OK) { st[t] = s; return; }
+                const Layout LY = make_layout(Z);
+                arena.assign(LY.total, 0);
+                s = plan_fill(n, probs, hidx_all, np_of, opt, Z, bind(arena.data(), LY), &pool);
+                if (s != SLAM_OK) { st[t] = s; return; }
+                unsigned long long h = 1469598103934665603ull;
+                for (size_t i = 0; i < LY.host_bytes; i++) h = (h ^ arena[i]) * 1099511628211ull;
+                hashes[t][r * ncounts + c] = h;
+            }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nthreads; t++) th.emplace_back(body, t);
+    body(0);
+    for (auto& x : th) x.join();
+    for (int t = 0; t < nthreads; t++)
+        if (st[t] != SLAM_OK) return st[t];
+    for (int t = 1; t < nthreads; t++)
+        if (hashes[t] != hashes[0]) return SLAM_EINVAL;
     return SLAM_OK;
 }
 #endif

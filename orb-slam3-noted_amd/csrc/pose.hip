@@ -68,7 +68,7 @@ __device__ inline void prob(const Hub& h, bool stereo, double c, double& r0, dou
     lba::huber_cc(c, stereo ? h.delta_stereo : h.delta_mono, stereo ? h.dsqr_stereo : h.dsqr_mono, r0, r1);
 }
 
-// linearizeOplus (OptimizableTypes.cpp:49-63 @0x1630; types_six_dof_expmap.cpp:388-423 @0x1280)
+// linearizeOplus (OptimizableTypes.cpp:49-63 @0x1630; types_six_dof_expmap.cpp:375-404 @0x1280)
 __device__ inline void pjac(const PEdge& e, const double* P, const PFrame& F, double* A) {
     const double X[3] = {e.Xw[0], e.Xw[1], e.Xw[2]};
     double Xc[3];

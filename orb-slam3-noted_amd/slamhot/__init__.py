@@ -19,7 +19,7 @@ LIB_PATH = PKG_ROOT / "lib" / "libslamhot.so"
 KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
                      ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
 
-SLAM_OK, SLAM_EINVAL, SLAM_ENOMEM, SLAM_EHIP, SLAM_ECAP, SLAM_ENODEV, SLAM_EEMPTY = 0, -1, -2, -3, -4, -5, -6
+SLAM_OK, SLAM_EINVAL, SLAM_ENOMEM, SLAM_EHIP, SLAM_ECAP, SLAM_ENODEV, SLAM_EEMPTY, SLAM_ETIMEDOUT = 0, -1, -2, -3, -4, -5, -6, -7
 
 
 class SlamError(RuntimeError):

@@ -43,12 +43,50 @@ def test_gpus_launcher_fails_when_a_rank_fails():
     p = _run(["--gpus", "2", "--legs", "dry", "--steps", "2", "--warmup", "0"], {"SLAMHOT_DRY_FAIL_RANK": "1"})
     assert p.returncode == 3, (p.returncode, p.stderr[-3000:])
     assert p.stdout.strip() == ""
-    # the first rank to fail sets the status (rank 0 then fails too, on the closed connection)
-    assert "rank 1 exited with 3" in p.stderr
+    # the rank whose leg failed is named (rank 0's leg child was stopped because of it)
+    assert "leg dry failed on rank 1" in p.stderr, p.stderr[-3000:]
 
 
-def test_gpus_launcher_kills_a_hung_job():
-    # far more steps than the timeout allows: the launcher kills both ranks and reports 124
-    p = _run(["--gpus", "2", "--legs", "dry", "--steps", "100000", "--warmup", "0", "--launch-timeout", "4"])
-    assert p.returncode == 124, (p.returncode, p.stderr[-3000:])
-    assert p.stdout.strip() == ""
+def test_hung_leg_in_one_rank_is_an_error_record():
+    """A leg that hangs in one rank (a host stall: no progress, no exit) ends at its deadline as an
+    error entry naming the leg, the rank and where it stopped, and the line (the first leg's value)
+    is still printed, well inside the job deadline."""
+    p = _run(["--gpus", "2", "--legs", "dry,dryaux", "--steps", "2", "--warmup", "0", "--leg-timeout-scale", "0.2"],
+             {"SLAMHOT_DRY_HANG": "dryaux:1"})
+    assert p.returncode == 0, (p.returncode, p.stderr[-3000:])
+    r = _line(p)
+    assert r["value"] > 0 and r["n_gpus"] == 2
+    e = r["dryaux"]
+    assert e["error"] == "timeout" and e["rank"] == 1, e
+    assert e["phase"].startswith("compute"), e
+    assert e["ranks"]["0"].startswith("timeout (collective"), e
+    assert r["legs"]["wall_s"]["dryaux"]["status"] == "error"
+    assert "leg dryaux FAILED: timeout on rank 1" in p.stderr
+    # every Python thread's stack of the stalled child is on stderr
+    assert "in dry_leg" in p.stderr
+
+
+def test_single_rank_hung_leg_keeps_the_line():
+    """N = 1, as the driver runs bench.py: the hung second leg is recorded, the first leg's value
+    printed, and the job ends near the leg's deadline (not the driver's limit)."""
+    p = _run(["--legs", "dry,dryaux", "--steps", "2", "--warmup", "0", "--leg-timeout-scale", "0.15"],
+             {"SLAMHOT_DRY_HANG": "dryaux:0"})
+    assert p.returncode == 0, (p.returncode, p.stderr[-3000:])
+    r = _line(p)
+    assert r["value"] > 0 and r["dryaux"]["error"] == "timeout" and r["dryaux"]["rank"] == 0
+    assert r["legs"]["job_wall_s"] < 60
+
+
+def test_hung_first_leg_fails_the_job_by_name():
+    p = _run(["--legs", "dry", "--steps", "2", "--warmup", "0", "--leg-timeout-scale", "0.15"],
+             {"SLAMHOT_DRY_HANG": "dry:0"})
+    assert p.returncode != 0 and p.stdout.strip() == ""
+    assert "leg dry timeout on rank 0" in p.stderr, p.stderr[-2000:]
+
+
+def test_job_deadline_skips_legs_that_cannot_start():
+    """A leg starts only with the time left of the job deadline: none left, nothing runs, and the job
+    fails naming the first leg."""
+    p = _run(["--legs", "dry,dryaux", "--steps", "2", "--warmup", "0", "--job-deadline", "1"])
+    assert p.returncode != 0 and p.stdout.strip() == ""
+    assert "leg dry skipped" in p.stderr, p.stderr[-2000:]

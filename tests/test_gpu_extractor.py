@@ -143,16 +143,20 @@ def test_kitti_stereo_settings(gpu_extractor_factory):
         assert len(kg) > 1800
 
 
-@pytest.mark.parametrize("scale,levels,nf", [(1.3, 6, 1000), (1.15, 10, 1500), (2.0, 3, 800), (1.2, 1, 500)])
+@pytest.mark.parametrize("scale,levels,nf", [(1.3, 6, 1000), (1.15, 10, 1500), (2.0, 3, 800), (1.2, 1, 500),
+                                             (1.05, 16, 1200)])
 def test_non_default_pyramid(gpu_extractor_factory, scale, levels, nf):
     """Other ORBextractor.scaleFactor / nLevels: the level geometry, per-level feature split and
-    the scale tables follow the parameters (ORBextractor.cc:408-468, 1152-1177)."""
+    the scale tables follow the parameters (ORBextractor.cc:408-468, 1152-1177).  16 levels is the
+    most the plan takes (kMaxLevels): k_orb3's level lookup reads every level's first slot, and the
+    last level's keypoints must come out bit-exact too."""
     ex = gpu_extractor_factory(nfeatures=nf, scaleFactor=scale, nlevels=levels, max_size=(752, 480))
     img = synth.frame(410 + levels, 752, 480)
     kg, dg, mg = ex(img)
     p = ob.params(nfeatures=nf, scale=scale, nlevels=levels)
     ko, do, mo = ob.extract(img, p)
     _compare(kg, dg, mg, ko, do, mo)
+    assert (kg["octave"] == levels - 1).sum() > 0  # the last level holds keypoints
     sc, isc, s2, is2, nfl = ob.levels(p)
     assert np.array_equal(ex.GetScaleFactors(), sc) and np.array_equal(ex.GetInverseScaleSigmaSquares(), is2)
     assert np.array_equal(ex.GetFeaturesPerLevel(), nfl)
