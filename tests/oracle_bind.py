@@ -143,7 +143,7 @@ def pyramid(img: np.ndarray, p: OrbParams | None = None):
     p = p or params()
     img = np.ascontiguousarray(img, dtype=np.uint8)
     h, w = img.shape
-    cap = w * h * 4
+    cap = w * h * max(4, p.nlevels)  # every level is at most the image (16 levels at 1.05: ~8.6x)
     out = np.zeros(cap, np.uint8)
     lw = np.zeros(p.nlevels, np.int32)
     lh = np.zeros(p.nlevels, np.int32)
