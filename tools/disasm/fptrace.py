@@ -273,6 +273,35 @@ class Tracer:
                 out += [a[2 + ((imm >> 2) & 1)], a[2 + ((imm >> 3) & 1)]]
             self.set_pd(d, out)
             return True
+        if ins == "vpermpd":  # 4-lane permute by immediate (the packed quaternion products)
+            imm, s_, d = ops
+            imm = int(imm[1:], 16)
+            a = self.pd_operand(s_, reloc, 4)
+            self.set_pd(d, [a[(imm >> (2 * k)) & 3] for k in range(4)])
+            return True
+        if ins == "vblendpd":  # AT&T: $imm, src2, src1, dst -- lane k from src2 where bit k is set
+            imm, s2, s1, d = ops
+            imm = int(imm[1:], 16)
+            w = wid(d)
+            a = self.pd_operand(s1, reloc, w)
+            b = self.pd_operand(s2, reloc, w)
+            self.set_pd(d, [b[k] if (imm >> k) & 1 else a[k] for k in range(w)])
+            return True
+        if ins in ("vextractf64x2", "vextractf128"):
+            imm, s_, d = ops
+            imm = int(imm[1:], 16)
+            a = self.pd_operand(s_, reloc, 4)
+            self.set_pd(d, a[2 * imm:2 * imm + 2])
+            return True
+        if ins == "vbroadcastsd":
+            s_, d = ops
+            v = self.as_f64(self.reg("xmm" + s_[4:]), 0) if X(s_) else self.pd_operand(s_, reloc, 1)[0]
+            self.set_pd(d, [v] * wid(d))
+            return True
+        if ins == "vmovq" and X(ops[0]) and X(ops[1]):  # low double kept, upper lane zeroed
+            v = self.as_f64(self.reg("xmm" + ops[0][4:]), 0)
+            self.set_pd(ops[1], [v, self.const(0.0, "f64")])
+            return True
         if ins == "vxorpd" and ops[0] != ops[1]:
             s2, s1, d = ops
             w = wid(d)
@@ -404,6 +433,9 @@ class Tracer:
             elif X(dst):
                 if src.startswith("%"):
                     g = self.gpr.get(R(src))
+                    if g and g[0] == "constq":
+                        self.regs[R(dst)] = [self.const(g[1], "f64")] + [None] * 7
+                        return
                     self.regs[R(dst)] = (list(g[1]) + [None] * 4)[:4] if g and g[0] == "xmmval" else [None] * 4
                     return
                 a = self.addr(src, reloc)
@@ -552,7 +584,11 @@ class Tracer:
                 d = R(dst)
                 a = self.addr(src, reloc)
                 if a[0] == "const":
-                    self.gpr[R32.get(d, d)] = ("got:" + str(reloc), 0)
+                    # a 64-bit constant moved through a GPR (`mov .LCn(%rip),%rax; vmovq %rax,%xmm0`)
+                    try:
+                        self.gpr[R32.get(d, d)] = ("constq", struct.unpack("<d", self.const_bytes(reloc, 8))[0])
+                    except Exception:
+                        self.gpr[R32.get(d, d)] = ("got:" + str(reloc), 0)
                     return
                 if d in R32:
                     self.gpr[R32[d]] = ("m32", self.load32(a) if a[0] != "const" else None)

@@ -83,12 +83,15 @@ int main(int argc, char** argv) {
     // the tile kernel on the same system (tile scratch, x)
     double* dT;
     hipMalloc(&dT, (size_t)t16_tiles_bytes());
+    int* dErr;
+    hipMalloc(&dErr, sizeof(int));
+    hipMemset(dErr, 0, sizeof(int));
     float total16 = 0;
     for (int r = 0; r < reps + 1; r++) {
         if (r == 1) hipMemcpyToSymbol(HIP_SYMBOL(g_t16_phase), zero, sizeof(zero));
         k_fill_tiles<<<256, 256>>>(dA0, n, ld, dT);
         hipEventRecord(e0);
-        k_ldlt_t16<<<1, kT16Waves * 64>>>(dW, dC, dA0, dT, dx);
+        k_ldlt_t16<<<1, kT16Waves * 64>>>(dW, dC, dA0, dT, dx, dErr);
         hipEventRecord(e1);
         hipEventSynchronize(e1);
         float ms;
