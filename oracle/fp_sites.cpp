@@ -130,5 +130,31 @@ void oracle_fp64_cam_pose_stereo(const double* X, double fx, double fy, double c
 double oracle_fp64_chi2_2(const double* e, double info) { return g2o_oracle::chi2_2_cc(e, info); }
 double oracle_fp64_chi2_3(const double* e, double info) { return g2o_oracle::chi2_3_cc(e, info); }
 void oracle_fp64_huber(double e, double delta, float dsqr, double* rho) { g2o_oracle::huber_cc(e, delta, dsqr, rho); }
+// round 6: the SE3Quat product, SE3Quat::exp, oplusImpl and the body edge (q as x y z w, t as x y z;
+// outputs q then t)
+void oracle_fp64_se3_mul(const double* qa, const double* ta, const double* qb, const double* tb, double* out) {
+    const g2o_oracle::SE3 r = g2o_oracle::se3_mul_cc(se3_of(qa, ta), se3_of(qb, tb));
+    out[0] = r.r.x;
+    out[1] = r.r.y;
+    out[2] = r.r.z;
+    out[3] = r.r.w;
+    for (int i = 0; i < 3; i++) out[4 + i] = r.t[i];
+}
+void oracle_fp64_se3_exp(const double* u, double* out) {
+    const g2o_oracle::SE3 r = g2o_oracle::se3_exp_cc(u);
+    out[0] = r.r.x;
+    out[1] = r.r.y;
+    out[2] = r.r.z;
+    out[3] = r.r.w;
+    for (int i = 0; i < 3; i++) out[4 + i] = r.t[i];
+}
+void oracle_fp64_body_error(const double* qrl, const double* trl, const double* q, const double* t, const double* X,
+                            const double* K, const double* obs, double* err) {
+    g2o_oracle::body_error_cc(se3_of(qrl, trl), se3_of(q, t), X, K, obs, err);
+}
+void oracle_fp64_lin_body(const double* qrl, const double* trl, const double* q, const double* t, const double* X,
+                          const float* Kf, double* A, double* B) {
+    g2o_oracle::lin_body_cc(se3_of(qrl, trl), se3_of(q, t), X, Kf, A, B);
+}
 
 }  // extern "C"

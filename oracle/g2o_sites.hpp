@@ -230,4 +230,146 @@ inline void lin_stereo_cc(const SE3& T, const double* X, double fx, double fy, d
     B[17] = B[5] - bf / z_2;
 }
 
+// ---- round 6: SE3Quat products, SE3Quat::exp and the body edge --------------------------------
+
+// Eigen's quaternion product a * b as compiled (packed vpermpd / fmadd code; EdgeSE3ProjectXYZToBody::
+// computeError COMDAT @0xb1-0x15e and linearizeOplus @0xfeb-0x1074 in OptimizableTypes.cpp.o, and
+// VertexSE3Expmap::oplusImpl COMDAT @0xb7-0x150, all the same form): each component is one product
+// and three fused terms, in this order.
+inline Quat quat_mul_cc(const Quat& a, const Quat& b) {
+    Quat r;
+    r.w = std::fma(-a.z, b.z, std::fma(-b.y, a.y, std::fma(b.w, a.w, -(b.x * a.x))));
+    r.x = std::fma(-a.z, b.y, std::fma(b.z, a.y, std::fma(a.w, b.x, b.w * a.x)));
+    r.y = std::fma(-a.x, b.z, std::fma(b.x, a.z, std::fma(a.w, b.y, b.w * a.y)));
+    r.z = std::fma(-a.y, b.x, std::fma(b.y, a.x, std::fma(a.w, b.z, b.w * a.z)));
+    return r;
+}
+
+// SE3Quat::normalizeRotation (se3quat.h:280-285) as compiled: w >= 0, then Eigen's normalize()
+// with its packed squared norm (z^2 + x^2) + (w^2 + y^2), dividing only when it is > 0.
+inline void normalize_cc(Quat& q) {
+    if (q.w < 0) {
+        q.x = -q.x;
+        q.y = -q.y;
+        q.z = -q.z;
+        q.w = -q.w;
+    }
+    const double n2 = (q.z * q.z + q.x * q.x) + (q.w * q.w + q.y * q.y);
+    if (n2 > 0.0) {
+        const double n = std::sqrt(n2);
+        q.x /= n;
+        q.y /= n;
+        q.z /= n;
+        q.w /= n;
+    }
+}
+
+// SE3Quat::operator* (se3quat.h:104-110) as compiled: t = a.t + a.r._transformVector(b.t),
+// r = normalize(a.r * b.r).
+inline SE3 se3_mul_cc(const SE3& a, const SE3& b) {
+    SE3 r;
+    double rt[3];
+    tv_cc(a.r, b.t, rt);
+    for (int i = 0; i < 3; i++) r.t[i] = a.t[i] + rt[i];
+    r.r = quat_mul_cc(a.r, b.r);
+    normalize_cc(r.r);
+    return r;
+}
+
+// g2o::SE3Quat::exp (se3quat.h:223-257) as compiled (OptimizableTypes.cpp.o COMDAT, the copy
+// VertexSE3Expmap::oplusImpl calls; same code in types_six_dof_expmap.cpp.o).  theta =
+// sqrt(fma(w2, w2, w0^2 + w1^2)); Omega^2 by Eigen's lazy 3x3 product, every entry a product and two
+// fused terms in the order the object uses, zero operands kept; R = fma(b, S, fma(a, W, I)),
+// V = fma(c, S, fma(b, W, I)) with a = sin/theta, b = (1 - cos)/theta^2, c = (theta - sin)/pow(theta, 3)
+// (glibc sincos / pow, as the object calls them); below 1e-5 R = S + (I + W) and V = R.  t = V
+// upsilon (rows 0 and 1 from column 0, row 2 from column 1), the quaternion from R on the positive
+// trace branch (trace summed (R22 + R11) + R00), then normalizeRotation.  The trace <= 0 branch of
+// Eigen's conversion (rotations of 120 degrees or more in one update) is not reached by LM steps and
+// keeps g2o_math.hpp's unpinned form.
+inline SE3 se3_exp_cc(const double* u) {
+    const double w0 = u[0], w1 = u[1], w2 = u[2], v0 = u[3], v1 = u[4], v2 = u[5];
+    const double theta = std::sqrt(std::fma(w2, w2, w0 * w0 + w1 * w1));
+    const double nw0 = -w0, nw1 = -w1, nw2 = -w2;
+    // Omega^2 (S[3 * i + j])
+    double S[9];
+    S[0] = std::fma(nw1, w1, std::fma(w2, nw2, 0.0 * 0.0));
+    S[1] = std::fma(w1, w0, std::fma(nw2, 0.0, nw2 * 0.0));
+    S[2] = std::fma(w1, 0.0, std::fma(nw0, nw2, 0.0 * w1));
+    S[3] = std::fma(nw1, nw0, std::fma(w2, 0.0, w2 * 0.0));
+    S[4] = std::fma(nw0, w0, std::fma(0.0, 0.0, nw2 * w2));
+    S[5] = std::fma(nw0, 0.0, std::fma(nw0, 0.0, w2 * w1));
+    S[6] = std::fma(nw1, 0.0, std::fma(nw1, 0.0, w0 * w2));
+    S[7] = std::fma(w1, w2, std::fma(0.0, w0, w0 * 0.0));
+    S[8] = std::fma(nw1, w1, std::fma(nw0, w0, 0.0));
+    const double W[9] = {0.0, nw2, w1, w2, 0.0, nw0, nw1, w0, 0.0};
+    double R[9], V[9];
+    if (theta < 0.00001) {
+        // (I + Omega) entry by entry as the object forms it: 1.0 on the diagonal, w + 0.0 above / 0.0 - w
+        const double IW[9] = {1.0, 0.0 - w2, w1 + 0.0, w2 + 0.0, 1.0, 0.0 - w0, 0.0 - w1, w0 + 0.0, 1.0};
+        for (int k = 0; k < 9; k++) R[k] = S[k] + IW[k];
+        for (int k = 0; k < 9; k++) V[k] = R[k];
+    } else {
+        const double a = std::sin(theta) / theta;
+        const double b = (1.0 - std::cos(theta)) / (theta * theta);
+        const double c = (theta - std::sin(theta)) / std::pow(theta, 3.0);
+        for (int k = 0; k < 9; k++) {
+            const double I = (k % 4 == 0) ? 1.0 : 0.0;
+            R[k] = std::fma(b, S[k], std::fma(a, W[k], I));
+            V[k] = std::fma(c, S[k], std::fma(b, W[k], I));
+        }
+    }
+    SE3 T;
+    T.t[0] = std::fma(V[2], v2, std::fma(v1, V[1], v0 * V[0]));
+    T.t[1] = std::fma(V[5], v2, std::fma(v1, V[4], v0 * V[3]));
+    T.t[2] = std::fma(v0, V[6], std::fma(v2, V[8], v1 * V[7]));
+    const double tr = (R[8] + R[4]) + R[0];
+    if (tr > 0.0) {
+        const double st = std::sqrt(tr + 1.0);
+        const double s = 0.5 / st;
+        T.r.w = st * 0.5;
+        T.r.x = (R[7] - R[5]) * s;
+        T.r.y = (R[2] - R[6]) * s;
+        T.r.z = (R[3] - R[1]) * s;
+    } else {
+        T.r = quat_from_R(R);
+    }
+    normalize_cc(T.r);
+    return T;
+}
+
+// VertexSE3Expmap::oplusImpl (types_six_dof_expmap.h:71-74): estimate <- exp(update) * estimate
+inline SE3 oplus_cc(const double* upd, const SE3& est) { return se3_mul_cc(se3_exp_cc(upd), est); }
+
+// ORB_SLAM3::EdgeSE3ProjectXYZToBody::computeError (OptimizableTypes.h:127-132, COMDAT in
+// OptimizableTypes.cpp.o): obs - pCamera->project((mTrl * T_lw).map(X_w)), the product and the
+// mapping as compiled (se3_mul_cc, map_cc), K = mpCamera2's fx, fy, cx, cy widened.
+inline void body_error_cc(const SE3& Trl, const SE3& T, const double* Xw, const double* K, const double* obs,
+                          double* err) {
+    double Xr[3], uv[2];
+    map_cc(se3_mul_cc(Trl, T), Xw, Xr);
+    project_cc(K, Xr, uv);
+    err[0] = obs[0] - uv[0];
+    err[1] = obs[1] - uv[1];
+}
+
+// ORB_SLAM3::EdgeSE3ProjectXYZToBody::linearizeOplus (OptimizableTypes.cpp:192-215, @0xf30) as
+// compiled: X_l = T.map(X_w), X_r = mTrl.map(X_l) (map_cc); Xi = -projectJac(X_r) * R(mTrl * T)
+// with the product's rotation (quat_mul_cc + normalize_cc, its translation unused); Xj =
+// (-projectJac(X_r) * R(mTrl)) * SE3deriv(X_l), both products mul23_cc with every SE3deriv entry
+// (zeros and ones kept).  A 2x3, B 2x6 row-major; Kf = mpCamera2's float fx, fy.
+inline void lin_body_cc(const SE3& Trl, const SE3& T, const double* Xw, const float* Kf, double* A, double* B) {
+    double Xl[3], Xr[3], n[6], Rrw[9], Rrl[9], M[6], S[18];
+    Quat q = quat_mul_cc(Trl.r, T.r);
+    normalize_cc(q);
+    map_cc(T, Xw, Xl);
+    map_cc(Trl, Xl, Xr);
+    neg_project_jac_cc(Kf, Xr, n);
+    rot_cc(q, Rrw);
+    mul23_cc(n, Rrw, 3, A);
+    rot_cc(Trl.r, Rrl);
+    mul23_cc(n, Rrl, 3, M);
+    se3_deriv(Xl, S);
+    mul23_cc(M, S, 6, B);
+}
+
 }  // namespace g2o_oracle

@@ -79,12 +79,10 @@ struct Solver {
         double Xc[3];
         if (e.body) {
             // EdgeSE3ProjectXYZToBody::computeError (OptimizableTypes.h:127-132):
-            // obs - pCamera->project((mTrl * T_lw).map(X_w)), the composed SE3Quat mapping
-            // (not pinned to the objects: the inlined SE3Quat product)
+            // obs - pCamera->project((mTrl * T_lw).map(X_w)), as compiled (round 6: body_error_cc)
             const KCam& K2 = kc2[e.kf];
-            se3_map(se3_mul(trl[e.kf], pose[e.kf]), &pt[3 * e.pt], Xc);
-            e.err[0] = e.obs[0] - (K2.fx * Xc[0] / Xc[2] + K2.cx);
-            e.err[1] = e.obs[1] - (K2.fy * Xc[1] / Xc[2] + K2.cy);
+            const double Kd[4] = {K2.fx, K2.fy, K2.cx, K2.cy};
+            body_error_cc(trl[e.kf], pose[e.kf], &pt[3 * e.pt], Kd, e.obs, e.err);
             return;
         }
         const KCam& K = kc[e.kf];
@@ -114,8 +112,8 @@ struct Solver {
 
     bool depth_positive(const Edge& e) const {
         double Xc[3];
-        if (e.body)  // OptimizableTypes.h:134-138
-            se3_map(se3_mul(trl[e.kf], pose[e.kf]), &pt[3 * e.pt], Xc);
+        if (e.body)  // OptimizableTypes.h:134-138, the product and mapping as computeError's
+            map_cc(se3_mul_cc(trl[e.kf], pose[e.kf]), &pt[3 * e.pt], Xc);
         else  // isDepthPositive: _transformVector + t, z > 0 (Optimizer.cc.o final scan)
             map_cc(pose[e.kf], &pt[3 * e.pt], Xc);
         return Xc[2] > 0.0;
@@ -150,37 +148,12 @@ struct Solver {
         lin_stereo_cc(T, &pt[3 * e.pt], fx, fy, bf, e.A, e.B);  // types_six_dof_expmap.cpp.o @0xcf0
     }
 
-    // EdgeSE3ProjectXYZToBody::linearizeOplus (OptimizableTypes.cpp:192-215):
-    //   Xi = -projectJac(X_r) * (mTrl * T_lw).rotation().toRotationMatrix()
-    //   Xj = -projectJac(X_r) * mTrl.rotation().toRotationMatrix() * SE3deriv(X_l)
-    // with X_l = T_lw.map(X_w), X_r = mTrl.map(X_l); products left to right (Eigen evaluates
-    // the inner 2x3 product first).
+    // EdgeSE3ProjectXYZToBody::linearizeOplus (OptimizableTypes.cpp:192-215) as compiled
+    // (OptimizableTypes.cpp.o @0xf30, round 6: lin_body_cc): Xi = -projectJac(X_r) R(mTrl * T_lw),
+    // Xj = (-projectJac(X_r) R(mTrl)) SE3deriv(X_l).
     void linearize_body(Edge& e) {
-        const SE3& T = pose[e.kf];
-        const SE3& Trl = trl[e.kf];
-        const double fx2 = kc2[e.kf].fx, fy2 = kc2[e.kf].fy;
-        double Xl[3], Xr[3], Rrw[9], Rrl[9];
-        se3_map(T, &pt[3 * e.pt], Xl);
-        se3_map(Trl, Xl, Xr);
-        rot_matrix(se3_mul(Trl, T).r, Rrw);
-        rot_matrix(Trl.r, Rrl);
-        const double x = Xr[0], y = Xr[1], z = Xr[2];
-        const double pj[6] = {-(fx2 / z), -0.0, -((-fx2) * x / (z * z)),
-                              -0.0, -(fy2 / z), -((-fy2) * y / (z * z))};
-        for (int r = 0; r < 2; r++)
-            for (int c = 0; c < 3; c++)
-                e.A[3 * r + c] = pj[3 * r + 0] * Rrw[0 + c] + pj[3 * r + 1] * Rrw[3 + c] + pj[3 * r + 2] * Rrw[6 + c];
-        double M[6];
-        for (int r = 0; r < 2; r++)
-            for (int c = 0; c < 3; c++)
-                M[3 * r + c] = pj[3 * r + 0] * Rrl[0 + c] + pj[3 * r + 1] * Rrl[3 + c] + pj[3 * r + 2] * Rrl[6 + c];
-        const double xl = Xl[0], yl = Xl[1], zl = Xl[2];
-        const double S[18] = {0.0, zl, -yl, 1.0, 0.0, 0.0,
-                              -zl, 0.0, xl, 0.0, 1.0, 0.0,
-                              yl, -xl, 0.0, 0.0, 0.0, 1.0};
-        for (int r = 0; r < 2; r++)
-            for (int c = 0; c < 6; c++)
-                e.B[6 * r + c] = M[3 * r + 0] * S[0 + c] + M[3 * r + 1] * S[6 + c] + M[3 * r + 2] * S[12 + c];
+        const float Kf[2] = {(float)kc2[e.kf].fx, (float)kc2[e.kf].fy};
+        lin_body_cc(trl[e.kf], pose[e.kf], &pt[3 * e.pt], Kf, e.A, e.B);
     }
 
     // BaseBinaryEdge::constructQuadraticForm, robust branch (base_binary_edge.hpp:55-120),
@@ -368,7 +341,7 @@ struct Solver {
     void update() {
         for (size_t k = 0; k < pose.size(); k++) {
             const int h = hidx[k];
-            if (h >= 0) pose[k] = se3_mul(se3_exp(&x[6 * h]), pose[k]);
+            if (h >= 0) pose[k] = oplus_cc(&x[6 * h], pose[k]);  // as compiled (g2o_sites.hpp, round 6)
         }
         for (int l = 0; l < npt(); l++)
             for (int c = 0; c < 3; c++) pt[3 * l + c] += x[6 * np + 3 * l + c];

@@ -176,7 +176,7 @@ struct PoseSolver {
             std::memcpy(Hl, H, sizeof(H));
             for (int j = 0; j < 6; j++) Hl[7 * j] += lambda;
             const bool ok2 = solve6(Hl, b, x);
-            est = se3_mul(se3_exp(x), est);
+            est = oplus_cc(x, est);  // VertexSE3Expmap::oplusImpl as compiled (g2o_sites.hpp, round 6)
             double tempChi = active_errors();
             if (!ok2) tempChi = std::numeric_limits<double>::max();
             rho = currentChi - tempChi;

@@ -132,24 +132,8 @@ __device__ __forceinline__ Intr right_cam(const Cam& c, int kf) {
     return Intr{a.x, a.y, a.z, a.w, 0.0, 0.f};
 }
 
-// (mTrl * T_lw) as a pose record: SE3Quat::operator* (se3quat.h:104-110)
-__device__ inline void body_pose(const double* Trl, const double* P, double* Q) {
-    double rt[3];
-    quat_rotate(load_q(Trl), P + 4, rt);
-    Quat a = load_q(Trl), b = load_q(P);
-    Quat r;
-    r.w = a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z;
-    r.x = a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y;
-    r.y = a.w * b.y + a.y * b.w + a.z * b.x - a.x * b.z;
-    r.z = a.w * b.z + a.z * b.w + a.x * b.y - a.y * b.x;
-    normalize_rotation(r);
-    Q[0] = r.x;
-    Q[1] = r.y;
-    Q[2] = r.z;
-    Q[3] = r.w;
-    for (int i = 0; i < 3; i++) Q[4 + i] = Trl[4 + i] + rt[i];
-    Q[7] = 0.0;
-}
+// (mTrl * T_lw) as a pose record: SE3Quat::operator* (se3quat.h:104-110) as compiled (round 6)
+__device__ inline void body_pose(const double* Trl, const double* P, double* Q) { se3_mul_cc(Trl, P, Q); }
 
 // ---------------------------------------------------------------- edge math
 __device__ inline void edge_error(const EdgeS& e, const Cam& cam, const double* P, const double* X,
@@ -160,7 +144,7 @@ __device__ inline void edge_error(const EdgeS& e, const Cam& cam, const double* 
         double Q[8];
         const Intr K2 = right_cam(cam, e.kf);
         body_pose(cam.trl + 8 * (long long)e.kf, P, Q);
-        se3_map(Q, X, Xc);
+        map_cc(Q, X, Xc);  // as compiled (OptimizableTypes.cpp.o COMDAT; oracle body_error_cc)
         err[0] = (double)e.obs[0] - (K2.fx * Xc[0] / Xc[2] + K2.cx);
         err[1] = (double)e.obs[1] - (K2.fy * Xc[1] / Xc[2] + K2.cy);
         err[2] = 0.0;
@@ -211,32 +195,31 @@ __device__ inline void robustify(const Huber& hk, bool stereo, double c, double&
 // X_r = mTrl.map(X_l): A = -J(X_r) R(mTrl*T), B = (-J(X_r) R(mTrl)) SE3deriv(X_l), left to right.
 __device__ inline void body_jacobians(const EdgeS& e, const Cam& cam, const double* P, const double* X, double* A,
                                       double* B) {
+    // as compiled (OptimizableTypes.cpp.o @0xf30; oracle lin_body_cc): the product's rotation
+    // (quat_mul_cc + normalize_cc), both mappings map_cc, -projectJac(X_r) with float fx, fy, the
+    // three products mul23_cc (every SE3deriv entry kept)
     const double* Trl = cam.trl + 8 * (long long)e.kf;
     const Intr K2 = right_cam(cam, e.kf);
-    double Xl[3], Xr[3], Q[8], Rrw[9], Rrl[9];
-    se3_map(P, X, Xl);
-    se3_map(Trl, Xl, Xr);
-    body_pose(Trl, P, Q);
-    rot_matrix(load_q(Q), Rrw);
-    rot_matrix(load_q(Trl), Rrl);
-    const double x = Xr[0], y = Xr[1], z = Xr[2];
-    const double pj[6] = {-(K2.fx / z), -0.0, -((-K2.fx) * x / (z * z)),
-                          -0.0, -(K2.fy / z), -((-K2.fy) * y / (z * z))};
-    double M[6];
-#pragma unroll
-    for (int r = 0; r < 2; r++)
-#pragma unroll
-        for (int cc = 0; cc < 3; cc++) {
-            A[3 * r + cc] = pj[3 * r + 0] * Rrw[0 + cc] + pj[3 * r + 1] * Rrw[3 + cc] + pj[3 * r + 2] * Rrw[6 + cc];
-            M[3 * r + cc] = pj[3 * r + 0] * Rrl[0 + cc] + pj[3 * r + 1] * Rrl[3 + cc] + pj[3 * r + 2] * Rrl[6 + cc];
-        }
+    double Xl[3], Xr[3], Rrw[9], Rrl[9], n[6], M[6];
+    Quat q = quat_mul_cc(load_q(Trl), load_q(P));
+    normalize_cc(q);
+    map_cc(P, X, Xl);
+    map_cc(Trl, Xl, Xr);
+    const double z2 = Xr[2] * Xr[2];
+    const float fxf = (float)K2.fx, fyf = (float)K2.fy;
+    n[0] = -((double)fxf / Xr[2]);
+    n[1] = -0.0;
+    n[2] = -((double)(-fxf) * Xr[0] / z2);
+    n[3] = -0.0;
+    n[4] = -((double)fyf / Xr[2]);
+    n[5] = -((double)(-fyf) * Xr[1] / z2);
+    rot_cc(q, Rrw);
+    mul23_cc<3>(n, Rrw, A);
+    rot_cc(load_q(Trl), Rrl);
+    mul23_cc<3>(n, Rrl, M);
     const double xl = Xl[0], yl = Xl[1], zl = Xl[2];
     const double S[18] = {0.0, zl, -yl, 1.0, 0.0, 0.0, -zl, 0.0, xl, 0.0, 1.0, 0.0, yl, -xl, 0.0, 0.0, 0.0, 1.0};
-#pragma unroll
-    for (int r = 0; r < 2; r++)
-#pragma unroll
-        for (int cc = 0; cc < 6; cc++)
-            B[6 * r + cc] = M[3 * r + 0] * S[0 + cc] + M[3 * r + 1] * S[6 + cc] + M[3 * r + 2] * S[12 + cc];
+    mul23_cc<6>(M, S, B);
     A[6] = A[7] = A[8] = 0;
 #pragma unroll
     for (int cc = 0; cc < 6; cc++) B[12 + cc] = 0;
@@ -2307,7 +2290,7 @@ __device__ __forceinline__ void finalize_edge_body(int ei, int ne_total, const E
     if (is_body(e)) {  // isDepthPositive in the right camera (OptimizableTypes.h:134-138)
         double Q[8];
         body_pose(trl + 8 * (long long)e.kf, P, Q);
-        se3_map(Q, X, Xc);
+        map_cc(Q, X, Xc);
     } else {
         map_cc(P, X, Xc);  // isDepthPositive: _transformVector + t (Optimizer.cc.o final scan)
     }

@@ -169,61 +169,113 @@ __device__ inline void huber_cc(double c, double delta, float dsqr, double& rho0
     }
 }
 
-// VertexSE3Expmap::oplusImpl: T <- exp(upd) * T (types_six_dof_expmap.h:71-74, se3quat.h:223-257,
-// including the small-angle branch R = I + W + W^2), on pose records.
+// ---- round 6: the SE3Quat product, SE3Quat::exp and oplusImpl as the reference's objects compute
+// them (oracle/g2o_sites.hpp quat_mul_cc / normalize_cc / se3_exp_cc, pinned by
+// tests/test_fp64_sites.py against OptimizableTypes.cpp.o's EdgeSE3ProjectXYZToBody, oplusImpl and
+// SE3Quat::exp; sin / cos / pow are the device's, glibc's in the reference).
+// Eigen's quaternion product a * b as compiled: one product and three fused terms per component.
+__device__ inline Quat quat_mul_cc(const Quat& a, const Quat& b) {
+    Quat r;
+    r.w = __builtin_fma(-a.z, b.z, __builtin_fma(-b.y, a.y, __builtin_fma(b.w, a.w, -(b.x * a.x))));
+    r.x = __builtin_fma(-a.z, b.y, __builtin_fma(b.z, a.y, __builtin_fma(a.w, b.x, b.w * a.x)));
+    r.y = __builtin_fma(-a.x, b.z, __builtin_fma(b.x, a.z, __builtin_fma(a.w, b.y, b.w * a.y)));
+    r.z = __builtin_fma(-a.y, b.x, __builtin_fma(b.y, a.x, __builtin_fma(a.w, b.z, b.w * a.z)));
+    return r;
+}
+
+// normalizeRotation as compiled: w >= 0, squared norm (z^2 + x^2) + (w^2 + y^2), divide when > 0
+__device__ inline void normalize_cc(Quat& q) {
+    if (q.w < 0) {
+        q.x = -q.x;
+        q.y = -q.y;
+        q.z = -q.z;
+        q.w = -q.w;
+    }
+    const double n2 = (q.z * q.z + q.x * q.x) + (q.w * q.w + q.y * q.y);
+    if (n2 > 0.0) {
+        const double n = sqrt(n2);
+        q.x /= n;
+        q.y /= n;
+        q.z /= n;
+        q.w /= n;
+    }
+}
+
+// SE3Quat::operator* as compiled on pose records: Q = A * B (t = A.t + A.r._transformVector(B.t))
+__device__ inline void se3_mul_cc(const double* A, const double* B, double* Qo) {
+    double rt[3];
+    tv_cc(load_q(A), B + 4, rt);
+    Quat r = quat_mul_cc(load_q(A), load_q(B));
+    normalize_cc(r);
+    Qo[0] = r.x;
+    Qo[1] = r.y;
+    Qo[2] = r.z;
+    Qo[3] = r.w;
+    Qo[4] = A[4] + rt[0];
+    Qo[5] = A[5] + rt[1];
+    Qo[6] = A[6] + rt[2];
+    Qo[7] = 0.0;
+}
+
+// VertexSE3Expmap::oplusImpl: T <- exp(upd) * T (types_six_dof_expmap.h:71-74), SE3Quat::exp
+// (se3quat.h:223-257) with its small-angle branch, both as compiled (g2o_sites.hpp se3_exp_cc).
 __device__ inline void se3_exp_mul(const double* upd, const double* cur, double* nxt) {
-    const double* u = upd;
-    const double om[3] = {u[0], u[1], u[2]}, up[3] = {u[3], u[4], u[5]};
-    const double theta = sqrt(om[0] * om[0] + om[1] * om[1] + om[2] * om[2]);
-    const double Wm[9] = {0, -om[2], om[1], om[2], 0, -om[0], -om[1], om[0], 0};
-    double W2[9];
-#pragma unroll
-    for (int i = 0; i < 3; i++)
-#pragma unroll
-        for (int j = 0; j < 3; j++)
-            W2[3 * i + j] = Wm[3 * i + 0] * Wm[0 + j] + Wm[3 * i + 1] * Wm[3 + j] + Wm[3 * i + 2] * Wm[6 + j];
+    const double w0 = upd[0], w1 = upd[1], w2 = upd[2], v0 = upd[3], v1 = upd[4], v2 = upd[5];
+    const double theta = sqrt(__builtin_fma(w2, w2, w0 * w0 + w1 * w1));
+    const double nw0 = -w0, nw1 = -w1, nw2 = -w2;
+    double S[9];
+    S[0] = __builtin_fma(nw1, w1, __builtin_fma(w2, nw2, 0.0 * 0.0));
+    S[1] = __builtin_fma(w1, w0, __builtin_fma(nw2, 0.0, nw2 * 0.0));
+    S[2] = __builtin_fma(w1, 0.0, __builtin_fma(nw0, nw2, 0.0 * w1));
+    S[3] = __builtin_fma(nw1, nw0, __builtin_fma(w2, 0.0, w2 * 0.0));
+    S[4] = __builtin_fma(nw0, w0, __builtin_fma(0.0, 0.0, nw2 * w2));
+    S[5] = __builtin_fma(nw0, 0.0, __builtin_fma(nw0, 0.0, w2 * w1));
+    S[6] = __builtin_fma(nw1, 0.0, __builtin_fma(nw1, 0.0, w0 * w2));
+    S[7] = __builtin_fma(w1, w2, __builtin_fma(0.0, w0, w0 * 0.0));
+    S[8] = __builtin_fma(nw1, w1, __builtin_fma(nw0, w0, 0.0));
+    const double Wm[9] = {0.0, nw2, w1, w2, 0.0, nw0, nw1, w0, 0.0};
     double R[9], V[9];
     if (theta < 0.00001) {
+        const double IW[9] = {1.0, 0.0 - w2, w1 + 0.0, w2 + 0.0, 1.0, 0.0 - w0, 0.0 - w1, w0 + 0.0, 1.0};
 #pragma unroll
         for (int i = 0; i < 9; i++) {
-            R[i] = ((i % 4 == 0) ? 1.0 : 0.0) + Wm[i] + W2[i];
+            R[i] = S[i] + IW[i];
             V[i] = R[i];
         }
     } else {
         const double st = sin(theta), ct = cos(theta);
         const double a = st / theta;
-        const double b = (1 - ct) / (theta * theta);
-        const double c = (theta - st) / pow(theta, 3);
+        const double b = (1.0 - ct) / (theta * theta);
+        const double c = (theta - st) / pow(theta, 3.0);
 #pragma unroll
         for (int i = 0; i < 9; i++) {
             const double I = (i % 4 == 0) ? 1.0 : 0.0;
-            R[i] = I + a * Wm[i] + b * W2[i];
-            V[i] = I + b * Wm[i] + c * W2[i];
+            R[i] = __builtin_fma(b, S[i], __builtin_fma(a, Wm[i], I));
+            V[i] = __builtin_fma(c, S[i], __builtin_fma(b, Wm[i], I));
         }
     }
-    Quat qe = quat_from_R(R);
-    double te[3];
-#pragma unroll
-    for (int i = 0; i < 3; i++) te[i] = V[3 * i + 0] * up[0] + V[3 * i + 1] * up[1] + V[3 * i + 2] * up[2];
-    normalize_rotation(qe);
-    // exp * T  (SE3Quat::operator*)
-    const Quat qt = load_q(cur);
-    double rt[3];
-    quat_rotate(qe, cur + 4, rt);
-    Quat r;
-    r.w = qe.w * qt.w - qe.x * qt.x - qe.y * qt.y - qe.z * qt.z;
-    r.x = qe.w * qt.x + qe.x * qt.w + qe.y * qt.z - qe.z * qt.y;
-    r.y = qe.w * qt.y + qe.y * qt.w + qe.z * qt.x - qe.x * qt.z;
-    r.z = qe.w * qt.z + qe.z * qt.w + qe.x * qt.y - qe.y * qt.x;
-    normalize_rotation(r);
-    nxt[0] = r.x;
-    nxt[1] = r.y;
-    nxt[2] = r.z;
-    nxt[3] = r.w;
-    nxt[4] = te[0] + rt[0];
-    nxt[5] = te[1] + rt[1];
-    nxt[6] = te[2] + rt[2];
-    nxt[7] = 0.0;
+    double E[8];
+    E[4] = __builtin_fma(V[2], v2, __builtin_fma(v1, V[1], v0 * V[0]));
+    E[5] = __builtin_fma(V[5], v2, __builtin_fma(v1, V[4], v0 * V[3]));
+    E[6] = __builtin_fma(v0, V[6], __builtin_fma(v2, V[8], v1 * V[7]));
+    const double tr = (R[8] + R[4]) + R[0];
+    Quat qe;
+    if (tr > 0.0) {
+        const double sq = sqrt(tr + 1.0);
+        const double s = 0.5 / sq;
+        qe.w = sq * 0.5;
+        qe.x = (R[7] - R[5]) * s;
+        qe.y = (R[2] - R[6]) * s;
+        qe.z = (R[3] - R[1]) * s;
+    } else {
+        qe = quat_from_R(R);  // not reached by LM steps (rotations of 120 degrees or more)
+    }
+    normalize_cc(qe);
+    E[0] = qe.x;
+    E[1] = qe.y;
+    E[2] = qe.z;
+    E[3] = qe.w;
+    se3_mul_cc(E, cur, nxt);  // exp * T
 }
 
 // Eigen 3x3 inverse by cofactors (Eigen/src/LU/InverseImpl.h)

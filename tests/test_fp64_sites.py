@@ -115,6 +115,49 @@ SITES = {
                         + ["arg_rdi+0x140", "arg_rdi+0x148", "arg_rdi+0x160"],
                         [(f"store:*(arg_rdi+0x118)+0x{o:x}", 0) for o in CM(3, 6) if o not in (0x60, 0x50, 0x70)]),
 }
+
+# round 6: SE3Quat products (the body edge, oplusImpl), SE3Quat::exp, EdgeSE3ProjectXYZToBody
+BODY_ERR = "@.text._ZN9ORB_SLAM323EdgeSE3ProjectXYZToBody12computeErrorEv"
+OPLUS = "@.text._ZN3g2o15VertexSE3Expmap9oplusImplEPKd"
+EXP = "@.text._ZN3g2o7SE3Quat3expERKN5Eigen6MatrixIdLi6ELi1ELi0ELi6ELi1EEE"
+TRL_Q = [f"arg_rdi+0x{o:x}" for o in (0x140, 0x148, 0x150, 0x158)]   # mTrl rotation x, y, z, w
+PJC = lambda k: [f"*0x50#{k}.out[{j}]" for j in (0, 4, 8, 2, 6, 10)]  # noqa: E731 projectJac row-major
+_PQ = [f"arg_r12+0x{o:x}" for o in (0xc0, 0xc8, 0xd0, 0xd8)]
+_OPLUS_IN = ([f"rsp+0x{o:x}" for o in (0x80, 0x88, 0x90, 0x98)] + _PQ + ["rsp+0xa0", "rsp+0xa8", "rsp+0xb0"]
+             + [f"_transformVector#1.out[{k}]" for k in (0, 2, 4)])
+_OPLUS_OUT = ST("arg_r12", (0xc0, 0xc8, 0xd0, 0xd8, 0xe0, 0xe8, 0xf0))
+_EXP_OUT = [(f"laststore:arg_rdi+0x{o:x}", 0) for o in (0, 8, 0x10, 0x18)] + ST("arg_rdi", (0x20, 0x28)) \
+    + [("store:rsp-0x190", 0)]
+SITES.update({
+    # VertexSE3Expmap::oplusImpl after its SE3Quat::exp call: exp(update) * estimate, w >= 0 (the
+    # branch skipped) and w < 0 (the negation taken: the range runs straight through it)
+    "oplus_mul": (O / "OptimizableTypes.cpp.o", ["0x62:0x152" + OPLUS, "0x15a:0x1b0" + OPLUS], _OPLUS_IN, _OPLUS_OUT),
+    "oplus_mul_neg": (O / "OptimizableTypes.cpp.o", ["0x62:0x1b0" + OPLUS], _OPLUS_IN, _OPLUS_OUT),
+    # SE3Quat::exp: theta >= 1e-5 (sincos / pow) and the small-angle branch, positive-trace quaternion
+    "exp_large": (O / "OptimizableTypes.cpp.o",
+                  [a + EXP for a in ("0x0:0xe6", "0x4b8:0x8f6", "0x264:0x2b4", "0x948:0x955", "0x95b:0x9b8",
+                                     "0x406:0x442", "0x448:0x469", "0x46b:0x482")],
+                  [f"arg_rsi+0x{8 * k:x}" for k in range(6)], _EXP_OUT),
+    "exp_small": (O / "OptimizableTypes.cpp.o",
+                  [a + EXP for a in ("0x0:0xe6", "0xec:0x2b4", "0x948:0x955", "0x95b:0x9b8", "0x406:0x442",
+                                     "0x448:0x469", "0x46b:0x482")],
+                  [f"arg_rsi+0x{8 * k:x}" for k in range(6)], _EXP_OUT),
+    # ORB_SLAM3::EdgeSE3ProjectXYZToBody::computeError: (mTrl * T).map(X), project, obs - proj
+    "err_body": (O / "OptimizableTypes.cpp.o", ["0x0:0x166" + BODY_ERR, "0x174:0x20f" + BODY_ERR],
+                 TRL_Q + ["arg_rdi+0x160", "arg_rdi+0x168", "rsp+0x90"] + Q(V1)
+                 + [f"_transformVector#1.out[{k}]" for k in (0, 2, 4)]
+                 + [f"_transformVector#2.out[{k}]" for k in (0, 2, 4)]
+                 + ["arg_rdi+0xa0", "arg_rdi+0xa8", "*%r14#3.out[0]", "*%r14#3.out[2]"],
+                 [(f"laststore:rsp+0x{o:x}", 0) for o in (0x60, 0x68, 0x70, 0x78)] + ST("rsp", (0x80, 0x88, 0x90))
+                 + ST("rsp", (0x20, 0x28, 0x30)) + ST("arg_rdi", (0xe0, 0xe8))),
+    # ORB_SLAM3::EdgeSE3ProjectXYZToBody::linearizeOplus (@0xf30), the product's w >= 0 branch
+    "lin_body": (O / "OptimizableTypes.cpp.o", ["0xf30:0x1076", "0x1087:0x1605"],
+                 TRL_Q + ["arg_rdi+0x160", "arg_rdi+0x168", "arg_rdi+0x170"] + Q(V1)
+                 + [f"{V1}+0xe0", f"{V1}+0xe8", "rsp+0x130"]
+                 + [f"_transformVector#{c}.out[{k}]" for c in (2, 3, 4) for k in (0, 2, 4)] + PJC(5) + PJC(6),
+                 [(f"store:*(arg_rdi+0x118)+0x{o:x}", 0) for o in CM(2, 3)]
+                 + [(f"store:*(arg_rdi+0x128)+0x{o:x}", 0) for o in CM(2, 6)]),
+})
 NOUT = {k: len(v[3]) for k, v in SITES.items()}
 
 
@@ -150,7 +193,9 @@ def orc():
                  "cam_stereo": [D] + [C.c_double] * 4 + [C.c_float, D],
                  "cam_pose_stereo": [D] + [C.c_double] * 5 + [D],
                  "chi2_2": [D, C.c_double], "chi2_3": [D, C.c_double],
-                 "huber": [C.c_double, C.c_double, C.c_float, D]}.items():
+                 "huber": [C.c_double, C.c_double, C.c_float, D],
+                 "se3_mul": [D, D, D, D, D], "se3_exp": [D, D], "body_error": [D, D, D, D, D, D, D, D],
+                 "lin_body": [D, D, D, D, D, Fp, D, D]}.items():
         f = getattr(L, f"oracle_fp64_{n}")
         f.argtypes = a
         f.restype = C.c_double if n.startswith("chi2") else None
@@ -370,3 +415,104 @@ def test_linearize_stereo(ref, orc):
         r = site(ref, "lin_pose_stereo", list(t) + list(tv) + [fx, fy, bf])
         orc.oracle_fp64_lin_pose_stereo(dv(*q), dv(*t), dv(*X), fx, fy, bf, B)
         assert same(r, np.array(B[:])[keep]) and B[4] == 0 and B[9] == 0 and B[16] == 0
+
+
+# ---- round 6 -------------------------------------------------------------------------------------
+
+def rand_q(rng, wsign=None):
+    q = rng.normal(size=4)
+    q /= np.linalg.norm(q)
+    if wsign is not None and np.sign(q[3]) != wsign:
+        q[3] = -q[3]
+    return q
+
+
+def test_se3_product_oplus(ref, orc):
+    """VertexSE3Expmap::oplusImpl's product exp(update) * estimate (quaternion product, normalizeRotation
+    with both signs of w, t = a.t + a.r * b.t): the oracle's se3_mul_cc against the object."""
+    rng = np.random.default_rng(61)
+    o = out(7)
+    n_neg = 0
+    for _ in range(N):
+        a, b = rand_q(rng), rand_q(rng)
+        ta, tb = rng.normal(size=3) * 3, rng.normal(size=3) * 3
+        tv = site(ref, "tv", list(a) + list(tb))
+        orc.oracle_fp64_se3_mul(dv(*a), dv(*ta), dv(*b), dv(*tb), o)
+        # the sign of the product's w picks the object's branch: the oracle's own w before normalising
+        w = np.fma(-a[2], b[2], np.fma(-b[1], a[1], np.fma(b[3], a[3], -(b[0] * a[0])))) if hasattr(np, "fma") else None
+        neg = o[3] < 0 or (w is not None and w < 0)
+        r = site(ref, "oplus_mul_neg" if neg else "oplus_mul", list(a) + list(b) + list(ta) + list(tv))
+        if not same(r, o[:]):  # w exactly representable near 0: try the other branch before failing
+            r = site(ref, "oplus_mul" if neg else "oplus_mul_neg", list(a) + list(b) + list(ta) + list(tv))
+            neg = not neg
+        n_neg += neg
+        assert same(r, o[:]), (r, o[:])
+    assert 0 < n_neg < N  # both branches exercised
+
+
+def test_se3_exp(ref, orc):
+    """SE3Quat::exp on LM-sized updates: |omega| from 1e-9 to 0.5 (both sides of the 1e-5 branch)."""
+    rng = np.random.default_rng(62)
+    o = out(7)
+    for k in range(N):
+        mag = 10 ** rng.uniform(-9, np.log10(0.5))
+        u = list(rng.normal(size=3) / np.sqrt(3) * mag) + list(rng.normal(size=3) * 10 ** rng.uniform(-6, 0))
+        theta = np.sqrt(u[0] ** 2 + u[1] ** 2 + u[2] ** 2)
+        r = site(ref, "exp_small" if theta < 1e-5 else "exp_large", u)
+        orc.oracle_fp64_se3_exp(dv(*u), o)
+        assert same(r, o[:]), (k, u, r, o[:])
+
+
+def test_body_edge_error(ref, orc):
+    """EdgeSE3ProjectXYZToBody::computeError: obs - project((mTrl * T).map(X)), composed across its
+    _transformVector / Pinhole::project calls."""
+    rng = np.random.default_rng(63)
+    err = out(2)
+    for _ in range(N):
+        qrl, trl = rand_q(rng, 1.0), np.array([-0.11, 0.0, 0.0]) + rng.normal(size=3) * 0.01
+        q, t = rand_pose(rng)
+        X = rand_point(rng, q, t)
+        K = rand_cam(rng).astype(np.float64)
+        obs = rng.uniform(0, 752, 2)
+        tv1 = site(ref, "tv", list(qrl) + list(t))
+        base = list(qrl) + list(trl) + list(q) + list(tv1)
+        r = site(ref, "err_body", base + [0, 0, 0] + list(obs) + [0, 0])
+        qrw, trw = r[:4], r[4:7]
+        if qrw[3] < 0:  # the object's negation branch is not in the traced range
+            continue
+        tv2 = site(ref, "tv", list(qrw) + list(X))
+        r = site(ref, "err_body", base + list(tv2) + list(obs) + [0, 0])
+        Xr = r[7:10]
+        p = site(ref, "proj", list(K) + list(Xr))
+        r = site(ref, "err_body", base + list(tv2) + list(obs) + list(p))
+        orc.oracle_fp64_body_error(dv(*qrl), dv(*trl), dv(*q), dv(*t), dv(*X), dv(*K), dv(*obs), err)
+        assert same(r[10:], err[:]), (r[10:], err[:])
+        o = out(7)
+        orc.oracle_fp64_se3_mul(dv(*qrl), dv(*trl), dv(*q), dv(*t), o)
+        assert same(r[:7], o[:])
+
+
+def test_linearize_body(ref, orc):
+    """EdgeSE3ProjectXYZToBody::linearizeOplus (Xi 2x3, Xj 2x6) composed across its four
+    _transformVector calls and two projectJac calls."""
+    rng = np.random.default_rng(64)
+    A, B = out(6), out(12)
+    for _ in range(N):
+        qrl, trl = rand_q(rng, 1.0), np.array([-0.11, 0.0, 0.0]) + rng.normal(size=3) * 0.01
+        q, t = rand_pose(rng)
+        X = rand_point(rng, q, t)
+        K = rand_cam(rng)
+        o = out(7)
+        orc.oracle_fp64_se3_mul(dv(*qrl), dv(*trl), dv(*q), dv(*t), o)
+        if o[3] < 0 and abs(o[3]) > 0:  # only the traced (w >= 0) branch
+            continue
+        tv2 = site(ref, "tv", list(q) + list(X))
+        Xl = np.array([t[0] + tv2[0], t[1] + tv2[1], tv2[2] + t[2]])
+        tv4 = site(ref, "tv", list(qrl) + list(Xl))
+        Xr = np.array([trl[0] + tv4[0], trl[1] + tv4[1], tv4[2] + trl[2]])
+        pj = _pj(ref, K, Xr)
+        # _pj gives the projectJac entries row-major; the site inputs are those of the sret slots
+        r = site(ref, "lin_body", list(qrl) + list(trl) + list(q) + [t[0], t[1], t[2]] + list(tv2) + list(tv2)
+                 + list(tv4) + pj + pj)
+        orc.oracle_fp64_lin_body(dv(*qrl), dv(*trl), dv(*q), dv(*t), dv(*X), (C.c_float * 2)(*K[:2]), A, B)
+        assert same(r[:6], A[:]) and same(r[6:], B[:]), (r, A[:], B[:])

@@ -199,6 +199,9 @@ class Tracer:
         return lanes
 
     def pd_operand(self, o, reloc, w):
+        if o.endswith("}") and "{1to" in o:  # AVX-512 embedded broadcast of one double
+            v = self.load_pd(o[:o.index("{")], reloc, 1)[0]
+            return [v] * w
         if o[:4] in ("%xmm", "%ymm", "%zmm"):
             lanes = self.reg("xmm" + o[4:])
             return [self.as_f64(lanes, k) if lanes[2 * k] is not None else None for k in range(w)]
@@ -611,6 +614,25 @@ class Tracer:
             callee = (reloc or " ".join(ops)).split("(")[0].replace("-0x4", "").split("::")[-1]
             tag = f"{callee}#{self.ncall}"
             self.event("call", extra=tag)
+            if callee in ("sincos", "pow") and self.packed:
+                # glibc's sincos(x, &s, &c) / pow(x, y) as pure functions of their arguments (the
+                # emitted C calls the same glibc; SE3Quat::exp, round 6)
+                x = self.as_f64(self.reg("xmm0"), 0)
+                if callee == "pow":
+                    y = self.as_f64(self.reg("xmm1"), 0)
+                    res = self.mk("pow", [x, y], "f64")
+                    for k in range(32):
+                        self.regs.pop(f"xmm{k}", None)
+                    self.set_pd("%xmm0", [res, None])
+                    return
+                for reg, fn in (("rdi", "sin"), ("rsi", "cos")):
+                    g = self.gpr.get(reg)
+                    a = (g[0], g[1])
+                    self.mem[a] = self.mk(fn, [x], "f64")
+                    self.mem[(a[0], a[1] + 4)] = None
+                for k in range(32):
+                    self.regs.pop(f"xmm{k}", None)
+                return
             if callee in ("roundf", "round", "floorf", "ceilf"):  # pure libm: its value, not an input
                 x = self.reg("xmm0")[0]
                 res = self.mk(callee, [x], "f32" if callee.endswith("f") else "f64")
@@ -807,8 +829,10 @@ def emit_c(tr: Tracer, fname: str, inputs: list[str], outputs: list[tuple[str, i
             e = f"{'fabsf' if n.ty == 'f32' else 'fabs'}({a[0]})"
         elif n.op in ("ceil", "floor", "trunc", "rint"):
             e = f"{n.op}{'f' if n.ty == 'f32' else ''}({a[0]})"
-        elif n.op in ("roundf", "round", "floorf", "ceilf"):
+        elif n.op in ("roundf", "round", "floorf", "ceilf", "sin", "cos"):
             e = f"{n.op}({a[0]})"
+        elif n.op == "pow":
+            e = f"pow({a[0]}, {a[1]})"
         elif n.op == "i2f":
             e = f"({t}){a[0]}"
         else:
