@@ -1706,12 +1706,57 @@ __device__ __forceinline__ void t16_diag(Lds& L, int k, double4_t dt, int lane) 
     }
 }
 
-__global__ void __launch_bounds__(kT16Waves * 64) k_ldlt_t16(const WinDesc* __restrict__ wins, WinCtl* __restrict__ ctl,
-                                                             const double* __restrict__ Hs, double* __restrict__ Ts,
-                                                             double* __restrict__ xp_out, int* __restrict__ err_word) {
-    __shared__ T16Lds L;
-    const WinDesc W = wins[blockIdx.x];
-    WinCtl& C = ctl[blockIdx.x];
+// Global hand-off words of the helper-assisted factorization (per window, zero between launches):
+// pub[c] counts the published TRSM tiles of column c (W and L written through to L2), rdy[j] the
+// tiles of column j the helpers have brought through panel j - 3.
+struct T16Sync {
+    int pub[kT16Max];
+    int rdy[kT16Max];
+};
+
+// loads / stores that bypass the CU's L1 (global sc1): the helper hand-offs
+__device__ __forceinline__ double4_t t16_load_sc1(const double* tile, int lane) {
+    double4_t v;
+#pragma unroll
+    for (int u = 0; u < 4; u++) v[u] = __hip_atomic_load(tile + 4 * lane + u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return v;
+}
+__device__ __forceinline__ void t16_store_sc1(double* tile, int lane, const double4_t& v) {
+#pragma unroll
+    for (int u = 0; u < 4; u++) __hip_atomic_store(tile + 4 * lane + u, v[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// every store of this wave has left for L2 (the hand-off counters are added after it)
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// A global counter reaches v (sc1 polls), bounded like the LDS waits: false when it gave up.
+__device__ __forceinline__ bool t16_wait_global(const int* w, int v) {
+    for (unsigned spin = 0; __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < v; spin++) {
+        if (spin >= kT16SpinCap) return false;
+        __builtin_amdgcn_s_sleep(2);
+    }
+    return true;
+}
+
+// Look-ahead of the helper-assisted form: the main workgroup applies the last kT16LA panels of
+// every column itself, the helpers the ones before (panels 0 .. j - kT16LA - 1 of column j), so a
+// helper's hand-off has kT16LA - 1 main iterations of slack.
+#ifndef SLAMHOT_T16_LA
+#define SLAMHOT_T16_LA 4
+#endif
+constexpr int kT16LA = SLAMHOT_T16_LA;
+
+// kHelp: the main workgroup of the helper-assisted form (k_ldlt_t16x): columns j > kT16LA receive
+// their trailing updates of panels 0 .. j - kT16LA - 1 from helper workgroups (ldlt_t16_helper);
+// this workgroup applies the last kT16LA (iteration k updates columns k + 1 .. k + kT16LA) and
+// everything else as in k_ldlt_t16, and publishes each TRSM tile's W and L for the helpers.  The
+// sequence of operations on every tile is the same, so x is bit-identical to the one-workgroup form.
+template <bool kHelp>
+__device__ __forceinline__ void ldlt_t16_body(T16Lds& L, int win, const WinDesc* __restrict__ wins,
+                                              WinCtl* __restrict__ ctl, const double* __restrict__ Hs,
+                                              double* __restrict__ Ts, double* __restrict__ Wg, T16Sync* __restrict__ sync,
+                                              double* __restrict__ xp_out, int* __restrict__ err_word) {
+    const WinDesc W = wins[win];
+    WinCtl& C = ctl[win];
     if (!C.need_trial) return;
     const int n = W.n, ld = W.ld, T = (n + 15) >> 4, rhs = ldlt_npad(n);
     if (T == 0) {  // no free pose: an empty system solves trivially
@@ -1720,7 +1765,9 @@ __global__ void __launch_bounds__(kT16Waves * 64) k_ldlt_t16(const WinDesc* __re
     }
     const int ntiles = T * (T + 1) / 2;
     const double* A = Hs + W.hs_off;
-    double* Tw = Ts + blockIdx_win_tiles(blockIdx.x);
+    double* Tw = Ts + blockIdx_win_tiles(win);
+    double* Gw = kHelp ? Wg + blockIdx_win_tiles(win) : nullptr;  // W tiles for the helpers
+    T16Sync* Sy = kHelp ? sync + win : nullptr;
     const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int lr = lane & 15, lq = lane >> 4;  // register u of a tile holds [lr][lq + 4u]
     if (tid == 0) {
@@ -1763,7 +1810,13 @@ __global__ void __launch_bounds__(kT16Waves * 64) k_ldlt_t16(const WinDesc* __re
             l[u] = acc[u] * dkk[q];
             part = __builtin_fma(l[u], L.wb[kk & 1][q], part);
         }
-        t16_store(Tw + 256 * t, lane, l);
+        const bool pub = kHelp && kk + kT16LA + 1 < T;  // a panel some helper tile still needs
+        if (pub) {
+            t16_store_sc1(Tw + 256 * t, lane, l);
+            t16_store_sc1(Gw + 256 * t, lane, acc);
+        } else {
+            t16_store(Tw + 256 * t, lane, l);
+        }
         part += __shfl_xor(part, 16);
         part += __shfl_xor(part, 32);
         if (lq == 0) L.y[16 * i + lr] -= part;
@@ -1771,6 +1824,10 @@ __global__ void __launch_bounds__(kT16Waves * 64) k_ldlt_t16(const WinDesc* __re
         if (lane == 0) {
             if (i == kk + 1) __hip_atomic_store(&L.tr_first, kk, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             __hip_atomic_fetch_add(&L.trsm_cnt[kk], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        if (pub) {  // to the helpers: the tile's W and L are in L2 before the count says so
+            drain_stores();
+            if (lane == 0) __hip_atomic_fetch_add(&Sy->pub[kk], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     };
     // bounded: gives up after kT16SpinCap polls, or at once when another wave gave up (L.hang)
@@ -1867,12 +1924,32 @@ __global__ void __launch_bounds__(kT16Waves * 64) k_ldlt_t16(const WinDesc* __re
                 pending = false;
             };
             // then columns > k + 1, one tile ahead in flight (deeper prefetch measured slower,
-            // profiles/r04e_t16_prefetch.txt)
+            // profiles/r04e_t16_prefetch.txt).  kHelp: columns k + 2 .. k + kT16LA only (the helpers
+            // bring the later ones through panel k); column k + kT16LA arrives from the helpers now
+            // (its tiles read from L2 once they are published), the others this workgroup updated
+            const int tend = kHelp ? L.col0[min(k + kT16LA + 1, T)] : ntiles;
+            const int jh = k + kT16LA;  // the column that comes from the helpers in this iteration
+            // a helper tile is waited for only with this wave's critical work done: its tiles come
+            // last in the range (column-major), the tile before it is updated (and the Dn tile
+            // handed to wave 0) first, and the wave's column-(k + 1) TRSMs are flushed first
+            auto from_help = [&](int tt) { return kHelp && jh > kT16LA && (L.tij[tt] & 255) == jh; };
+            bool waited = false;
+            auto ld_help = [&](int tt) {
+                if (pending) {
+                    wait_at_least(&L.diag_ready, k + 1);
+                    if (k > 0) wait_at_least(&L.done_cnt[k - 1], kNw);
+                    flush();
+                }
+                if (!waited && !t16_wait_global(&Sy->rdy[jh], T - jh)) give_up(kT16SpinCap);
+                waited = true;
+                return t16_load_sc1(Tw + 256 * tt, lane);
+            };
             int t = first_at(c1);
-            double4_t cur = t < ntiles ? t16_load(Tw + 256 * t, lane) : double4_t{0.0, 0.0, 0.0, 0.0};
-            while (t < ntiles) {
+            double4_t cur = t >= tend ? double4_t{0.0, 0.0, 0.0, 0.0} : from_help(t) ? ld_help(t) : t16_load(Tw + 256 * t, lane);
+            while (t < tend) {
                 const int tn = t + kNw;
-                const double4_t nxt = tn < ntiles ? t16_load(Tw + 256 * tn, lane) : double4_t{0.0, 0.0, 0.0, 0.0};
+                const bool nh = tn < tend && from_help(tn);  // loaded after this tile, not ahead
+                const double4_t nxt = tn < tend && !nh ? t16_load(Tw + 256 * tn, lane) : double4_t{0.0, 0.0, 0.0, 0.0};
                 const double4_t v = update(t, cur);
                 if (t == c1) {  // the next panel's diagonal tile: to wave 0 through the LDS
                     t16_store(L.Dn[k & 1], lane, v);
@@ -1881,7 +1958,7 @@ __global__ void __launch_bounds__(kT16Waves * 64) k_ldlt_t16(const WinDesc* __re
                     t16_store(Tw + 256 * t, lane, v);
                 }
                 if (pending && ready()) flush();
-                cur = nxt;
+                cur = nh ? ld_help(tn) : nxt;
                 t = tn;
             }
             if (pending) {
@@ -1989,7 +2066,110 @@ __global__ void __launch_bounds__(kT16Waves * 64) k_ldlt_t16(const WinDesc* __re
         C.ok2 = L.hang ? 0 : 1;
         if (L.hang) atomicAdd(err_word, 1);
     }
+    if (kHelp && tid < kT16Max) {  // every helper has published its last column: reset for the next launch
+        Sy->pub[tid] = 0;
+        Sy->rdy[tid] = 0;
+    }
 }
+
+__global__ void __launch_bounds__(kT16Waves * 64) k_ldlt_t16(const WinDesc* __restrict__ wins, WinCtl* __restrict__ ctl,
+                                                             const double* __restrict__ Hs, double* __restrict__ Ts,
+                                                             double* __restrict__ xp_out, int* __restrict__ err_word) {
+    __shared__ T16Lds L;
+    ldlt_t16_body<false>(L, blockIdx.x, wins, ctl, Hs, Ts, nullptr, nullptr, xp_out, err_word);
+}
+
+// A helper workgroup of window w (one of kT16Helpers): its 16 waves own the tiles (i, j), j > kT16LA,
+// round robin in column-major order, keep them in registers, and apply panels p = 0 .. j - kT16LA - 1
+// as the main workgroup publishes them (pub[p] = T - p - 1: W_ip from the W copy, L_jp from the tile
+// scratch, both sc1 loads), the same MFMA sequence as the main workgroup's update; after its last
+// panel a tile goes back to the scratch (sc1) and rdy[j] counts it.
+#ifndef SLAMHOT_T16_HELPERS
+#define SLAMHOT_T16_HELPERS 2
+#endif
+constexpr int kT16Helpers = SLAMHOT_T16_HELPERS;
+constexpr int kT16HelperOwn = (kT16Max - kT16LA - 1) * (kT16Max - kT16LA) / 2 / (16 * kT16Helpers) + 1;  // tiles per wave
+__device__ __forceinline__ void ldlt_t16_helper(int win, int h, const WinDesc* __restrict__ wins,
+                                                const WinCtl* __restrict__ ctl, double* __restrict__ Ts,
+                                                const double* __restrict__ Wg, T16Sync* __restrict__ sync,
+                                                int* __restrict__ err_word) {
+    const WinDesc W = wins[win];
+    if (!ctl[win].need_trial) return;
+    const int T = (W.n + 15) >> 4;
+    if (T < kT16LA + 2) return;  // no column has a helper panel
+    double* Tw = Ts + blockIdx_win_tiles(win);
+    const double* Gw = Wg + blockIdx_win_tiles(win);
+    T16Sync* Sy = sync + win;
+    const int lane = threadIdx.x & 63, hw = h * 16 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    constexpr int NW = 16 * kT16Helpers;
+    auto col0 = [&](int j) { return j * T - j * (j - 1) / 2; };
+    // this wave's tiles: the m-th helper tile in column-major order (columns kT16LA + 1 .. T-1),
+    // m = hw + NW o (decoded per o, so the arrays stay in registers)
+    constexpr int J0 = kT16LA + 1;
+    int ti[kT16HelperOwn], tj[kT16HelperOwn];
+    double4_t cur[kT16HelperOwn];
+    const int nhelp = (T - J0) * (T - J0 + 1) / 2;
+    int nown = 0, jmax = -1;
+#pragma unroll
+    for (int o = 0; o < kT16HelperOwn; o++) {
+        const int m = hw + NW * o;
+        int i = 0, j = 0;
+        if (m < nhelp) {
+            int c = 0;
+            for (j = J0; j < T; j++) {
+                if (m < c + T - j) break;
+                c += T - j;
+            }
+            i = j + (m - c);
+            nown = o + 1;
+            jmax = j;
+        }
+        ti[o] = i;
+        tj[o] = j;
+    }
+#pragma unroll
+    for (int o = 0; o < kT16HelperOwn; o++)
+        if (o < nown) cur[o] = t16_load(Tw + 256 * (col0(tj[o]) + ti[o] - tj[o]), lane);  // k_schur's tiles
+    for (int p = 0; p + J0 <= jmax; p++) {
+        if (!t16_wait_global(&Sy->pub[p], T - p - 1)) {
+            if (lane == 0) atomicAdd(err_word, 1);
+            return;
+        }
+#pragma unroll
+        for (int o = 0; o < kT16HelperOwn; o++) {
+            if (o >= nown || p > tj[o] - J0) continue;
+            const double4_t a = t16_load_sc1(Tw + 256 * (col0(p) + tj[o] - p), lane);  // L_jp
+            const double4_t bw = t16_load_sc1(Gw + 256 * (col0(p) + ti[o] - p), lane);  // W_ip
+            double4_t acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int u = 0; u < 4; u++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], bw[u], acc, 0, 0, 0);
+            cur[o] = cur[o] - acc;
+            if (p == tj[o] - J0) {
+                t16_store_sc1(Tw + 256 * (col0(tj[o]) + ti[o] - tj[o]), lane, cur[o]);
+                drain_stores();
+                if (lane == 0) __hip_atomic_fetch_add(&Sy->rdy[tj[o]], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+}
+
+// The helper-assisted factorization for a few windows (LocalMapping's one-window call): block b
+// is window b % 8's main workgroup (b < 8) or its helper b / 8 - 1 -- blocks of equal b % 8 share
+// an XCD under the round-robin dispatch (speed only: the hand-offs are agent-scope).  The grid
+// is 8 x (1 + kT16Helpers) blocks; windows >= nw exit.
+__global__ void __launch_bounds__(kT16Waves * 64) k_ldlt_t16x(int nw, const WinDesc* __restrict__ wins, WinCtl* __restrict__ ctl,
+                                                              const double* __restrict__ Hs, double* __restrict__ Ts,
+                                                              double* __restrict__ Wg, T16Sync* __restrict__ sync,
+                                                              double* __restrict__ xp_out, int* __restrict__ err_word) {
+    __shared__ T16Lds L;
+    const int w = blockIdx.x & 7, slot = blockIdx.x >> 3;
+    if (w >= nw) return;
+    if (slot == 0)
+        ldlt_t16_body<true>(L, w, wins, ctl, Hs, Ts, Wg, sync, xp_out, err_word);
+    else
+        ldlt_t16_helper(w, slot - 1, wins, ctl, Ts, Wg, sync, err_word);
+}
+
 
 // Identity padding of the dense systems (rows/cols n..npad-1) and a zero rhs tail; the
 // factorization keeps it invariant, so it is written once per solve.
@@ -2645,6 +2825,7 @@ struct slam_lba {
     size_t harena_cap = 0;
     DevBuf arena, cnt;
     DevBuf poses, pts, err, rho, lin, Hll, bl, Hpp, bp, pd, xp, xl, Hs, Ts;
+    DevBuf Wg, tsync;            // helper-assisted LDL^T (k_ldlt_t16x): W tiles, hand-off words
     DevBuf bm, bmp, pbase, pls;  // pose bitmaps, their word prefixes, pose list bases, pose edge lists
     DevBuf ppt;                  // the point of every pose-list entry
     DevBuf pcnt;                 // free-pose edges per pose (pose list lengths)
@@ -3318,6 +3499,18 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
     const bool use_t16 = Z.max_n <= 16 * kT16Max && !(ldlt_env && !std::strcmp(ldlt_env, "panel"));
     SLAM_HIP_TRY(s->Hs.ensure(sizeof(double) * std::max<long long>(Z.hs_total, 1)));
     if (use_t16) SLAM_HIP_TRY(s->Ts.ensure((size_t)t16_tiles_bytes() * nw));
+    // SLAMHOT_LDLT_HELP=1: up to 8 windows factor with helper workgroups on other CUs (k_ldlt_t16x).
+    // Measured slower than the one-workgroup kernel at n = 288 (115-128 vs 107 us, x bit-identical,
+    // profiles/r06_ldlt_helpers.txt), so it is not the default.
+    const char* help_env = std::getenv("SLAMHOT_LDLT_HELP");
+    const bool use_help = use_t16 && nw <= 8 && help_env && std::atoi(help_env) != 0;
+    if (use_help) {
+        SLAM_HIP_TRY(s->Wg.ensure((size_t)t16_tiles_bytes() * 8));
+        if (s->tsync.cap < sizeof(T16Sync) * 8) {  // zero once; every launch leaves the words at zero
+            SLAM_HIP_TRY(s->tsync.ensure(sizeof(T16Sync) * 8));
+            SLAM_HIP_TRY(hipMemsetAsync(s->tsync.p, 0, sizeof(T16Sync) * 8, S));
+        }
+    }
     // read-back region: [KF poses | points | control records | outlier flags], 256-byte sections
     auto up256 = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t o_pt = up256(sizeof(float) * 16 * std::max(H.nkf, 1));
@@ -3546,7 +3739,11 @@ slam_status slamhot_lba_solve(slam_lba* s, int n_prob, const slam_lba_problem* p
                                                     as<int>(s->ct_off), as<int4>(s->ct), dW, dC, as<double>(s->Hpp),
                                                     as<double>(s->bp), as<double>(s->lin), as<double>(s->pd),
                                                     as<double>(s->Hs), tiles);
-        if (use_t16)
+        if (use_help)
+            k_ldlt_t16x<<<8 * (1 + kT16Helpers), kT16Waves * 64, 0, S>>>(nw, dW, dC, as<double>(s->Hs), as<double>(s->Ts),
+                                                                         as<double>(s->Wg), as<T16Sync>(s->tsync),
+                                                                         as<double>(s->xp), dTally + 6);
+        else if (use_t16)
             k_ldlt_t16<<<nw, kT16Waves * 64, 0, S>>>(dW, dC, as<double>(s->Hs), as<double>(s->Ts), as<double>(s->xp),
                                                      dTally + 6);
         else

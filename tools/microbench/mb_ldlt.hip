@@ -4,6 +4,7 @@
 #include "../../orb-slam3-noted_amd/csrc/lba.hip"
 
 #include <cstdio>
+#include <cstring>
 #include <random>
 
 // row-major lower triangle (identity-padded) -> the tile-major scratch k_ldlt_t16 reads
@@ -108,6 +109,35 @@ int main(int argc, char** argv) {
         for (int j = 0; j < n; j++) s += (j <= i ? A[(size_t)i * ld + j] : A[(size_t)j * ld + i]) * x16[j];
         r16 = std::max(r16, std::fabs(s - b[i]));
     }
+    // the helper-assisted form (k_ldlt_t16x: one main workgroup + kT16Helpers helpers) on the same system
+    double* dWg;
+    T16Sync* dSync;
+    hipMalloc(&dWg, (size_t)t16_tiles_bytes() * 8);
+    hipMalloc(&dSync, sizeof(T16Sync) * 8);
+    hipMemset(dSync, 0, sizeof(T16Sync) * 8);
+    float total16x = 0;
+    for (int r = 0; r < reps + 1; r++) {
+        if (r == 1) hipMemcpyToSymbol(HIP_SYMBOL(g_t16_phase), zero, sizeof(zero));
+        k_fill_tiles<<<256, 256>>>(dA0, n, ld, dT);
+        hipEventRecord(e0);
+        k_ldlt_t16x<<<8 * (1 + kT16Helpers), kT16Waves * 64>>>(1, dW, dC, dA0, dT, dWg, dSync, dx, dErr);
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+        float ms;
+        hipEventElapsedTime(&ms, e0, e1);
+        if (r) total16x += ms;
+    }
+    unsigned long long p16x[8];
+    hipMemcpyFromSymbol(p16x, HIP_SYMBOL(g_t16_phase), sizeof(p16x));
+    std::vector<double> x16x(n);
+    hipMemcpy(x16x.data(), dx, sizeof(double) * n, hipMemcpyDeviceToHost);
+    int errw = 0;
+    hipMemcpy(&errw, dErr, sizeof(int), hipMemcpyDeviceToHost);
+    const bool same16x = std::memcmp(x16x.data(), x16.data(), sizeof(double) * n) == 0;
+    if (n <= 16 * kT16Max)
+        printf("n=%d t16x %.1f us  x %s the one-workgroup kernel's  err_word %d  phases(us): diag0 %.1f w0-wait %.1f end-wait %.1f backsolve %.1f [w0: update %.1f diag %.1f]\n",
+               n, 1e3 * total16x / reps, same16x ? "bit-identical to" : "DIFFERS from", errw, p16x[1] / 100.0 / reps,
+               p16x[3] / 100.0 / reps, p16x[4] / 100.0 / reps, p16x[5] / 100.0 / reps, p16x[6] / 100.0 / reps, p16x[7] / 100.0 / reps);
     if (argc > 3) {  // x of the tile kernel, for bit-for-bit comparisons between builds
         FILE* f = fopen(argv[3], "wb");
         if (f) {
