@@ -90,3 +90,23 @@ def test_job_deadline_skips_legs_that_cannot_start():
     p = _run(["--legs", "dry,dryaux", "--steps", "2", "--warmup", "0", "--job-deadline", "1"])
     assert p.returncode != 0 and p.stdout.strip() == ""
     assert "leg dry skipped" in p.stderr, p.stderr[-2000:]
+
+
+def test_torchrun_launch_runs_legs_in_children():
+    """The driver's N > 1 form: `python -m torch.distributed.run --nproc-per-node N ... bench.py`.
+    Each rank process (torchrun's worker, on the agent's store) runs its legs in child processes with
+    a process group of their own, and exactly one JSON line reaches stdout."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), str(ROOT / "bench.py"), "--gpus", "2",
+                        "--legs", "dry,dryaux", "--steps", "2", "--warmup", "0"],
+                       env=env, capture_output=True, text=True, timeout=240, cwd=str(ROOT))
+    assert p.returncode == 0, p.stderr[-3000:]
+    r = _line(p)
+    assert r["n_gpus"] == 2 and len(r["rank_digests"]) == 2
+    assert r["dryaux"]["value"] > 0 and r["legs"]["wall_s"]["dryaux"]["status"] == "ok"
