@@ -367,6 +367,10 @@ def parse_args(argv=None):
                     help="seconds from a rank's start by which every leg must have ended (legs that would "
                          "start later are skipped and recorded as such)")
     ap.add_argument("--leg-timeout-scale", type=float, default=1.0, help="multiplies every leg's own cap (LEG_CAP_S)")
+    ap.add_argument("--in-process", action="store_true",
+                    help="run every leg in this process, one after another (N = 1 only): for profilers such as "
+                         "rocprofv3, whose preloaded library initialises the GPU in this process, which must then "
+                         "start no other program")
     ap.add_argument("--leg-child", default=None, help=argparse.SUPPRESS)      # internal: run one leg here
     ap.add_argument("--leg-deadline", type=float, default=0.0, help=argparse.SUPPRESS)
     return ap.parse_args(argv)
@@ -387,6 +391,10 @@ def main():
     if args.leg_child:
         sys.exit(child_main(args))
     legs = leg_list(args)
+    if args.in_process:
+        if args.gpus != 1 or int(os.environ.get("WORLD_SIZE", "1")) != 1:
+            raise SystemExit("bench.py: --in-process runs one rank (--gpus 1)")
+        sys.exit(in_process_main(args, legs))
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # the driver's `python bench.py --gpus N`: one child process per GPU, before any GPU call
         sys.exit(launch_ranks(args.gpus, sys.argv[1:], args.launch_timeout))
@@ -618,6 +626,51 @@ def rank_main(args, legs):
         add_full_socket(result)
         print(json.dumps(result), flush=True)
     return 0
+
+
+def in_process_main(args, legs):
+    """--in-process: every leg in this process, in order (no child processes, no per-leg deadline),
+    merged into the same JSON line as rank_main's."""
+    result = {
+        "metric": "ORB extract+match frames/s and LocalBA iters/s per GPU; ATE vs reference",
+        "value": None, "unit": "frames/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": None, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (rendered textured-room stereo sequences / procedural frames, slamhot/synth.py)",
+    }
+    wall = {}
+    import tempfile
+    with tempfile.TemporaryDirectory(prefix="slamhot_bench_") as scratch:
+        os.environ["SLAMHOT_BENCH_SCRATCH"] = scratch
+        for leg in legs:
+            t0 = time.monotonic()
+            progress(f"leg {leg} start (in process)")
+            payload = run_leg(args, leg)
+            wall[leg] = {"s": round(time.monotonic() - t0, 1), "status": "ok"}
+            progress(f"leg {leg} done in {wall[leg]['s']:.1f} s")
+            merge_leg(result, leg, payload)
+    result["legs"] = {"isolation": "in process (--in-process): every leg in one process, in order", "wall_s": wall,
+                      "job_wall_s": round(time.monotonic() - T_START, 1)}
+    add_full_socket(result)
+    print(json.dumps(result), flush=True)
+    return 0
+
+
+def run_leg(args, leg, world=1, rank=0, local_rank=0):
+    """One leg in this process (N = 1): the device, the context, the leg function; its result dict."""
+    import torch
+    dry = leg in ("dry", "dryaux")
+    gpu = local_rank
+    if dry:
+        device = torch.device("cpu")
+    else:
+        device = torch.device("cuda", gpu)
+        torch.cuda.set_device(device)
+    PHASE.update(rank=rank, leg=leg, file=None)
+    ctx = dict(args=args, rank=rank, world=world, local_rank=gpu, dist=None, device=device, leg=leg,
+               cpu=(rank == 0 and world == 1 and not args.no_cpu_baseline))
+    fn = {"dry": dry_leg, "dryaux": dry_leg, "headline": headline_leg, "extract": extract_leg, "lba": lba_leg,
+          "pose": pose_leg, "track": track_leg, "localmap": localmap_leg, "projection": projection_leg}[leg]
+    return fn(ctx)
 
 
 def child_main(args):
