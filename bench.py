@@ -334,7 +334,10 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--legs", default="headline,extract,lba,pose,track,localmap,projection",
                     help="comma list of legs to run (headline = configs[2] extract+match)")
-    ap.add_argument("--pairs", type=int, default=128, help="headline: stereo frames per GPU per step")
+    # 256 stereo frames per step: the same steady-state rate as 128 (121-124k frames/s at 100 steps), but the
+    # pipeline fill and drain of a short timed region weigh half as much (20 steps: 118.7-119.7k against
+    # 112.2-116.0k with 128, profiles/r06j_pairs.txt)
+    ap.add_argument("--pairs", type=int, default=256, help="headline: stereo frames per GPU per step")
     ap.add_argument("--inflight", type=int, default=4, help="batches in flight (handles / streams) per leg (3 / 4 / 5: headline 103.0k / 105.6k / 95.8k, profiles/r04h_inflight.txt)")
     ap.add_argument("--batch", type=int, default=256, help="extract leg: frames per GPU per step")
     ap.add_argument("--width", type=int, default=640)

@@ -3,7 +3,7 @@
 # into profiles/TAG_*, recomputing the PMC summaries locally.  Usage: tools/save_profiles.sh TAG
 set -e
 T=$1
-python3 tools/parse_counters.py gpurun_out/pmc k_fast_wave 128 752 2 > /dev/null
+python3 tools/parse_counters.py gpurun_out/pmc k_fast_wave 256 752 2 > /dev/null
 python3 tools/lba_pmc.py gpurun_out/pmc_lba $T > /dev/null
 cp gpurun_out/bench_$T.json profiles/${T}_bench.json
 cp gpurun_out/prof_default.json profiles/${T}_bench_under_rocprof.json
