@@ -33,6 +33,19 @@ constexpr int kRowsThreads = 1024;
 // 0.125 -> 0.120 ms per 128 pairs, headline +0.6% against 128 threads (interleaved A/B)
 constexpr int kMatchThreads = 64;
 constexpr int kMedianThreads = 1024;
+#ifndef SLAMHOT_ST_CAND
+#define SLAMHOT_ST_CAND 4
+#endif
+constexpr int kStCand = SLAMHOT_ST_CAND;  // band candidates per step of k_stereo_match
+
+// one band-table entry: the right keypoint's index with the two fields the candidate filter reads
+// (octave, x), so a candidate costs one 8-byte load instead of an index and a 28-byte keypoint
+struct StEnt {
+    uint16_t idx;
+    int16_t octave;
+    float x;
+};
+static_assert(sizeof(StEnt) == 8, "one 8-byte load per candidate");
 
 struct StereoGeom {
     const uint8_t* base[2][kStMaxLevels];  // level l of frame 0 (left, right)
@@ -46,7 +59,7 @@ struct StereoGeom {
 
 __global__ void __launch_bounds__(kRowsThreads) k_stereo_rows(StereoGeom G, const slam_keypoint* kps_r,
                                                              const int32_t* n_r, int32_t* row_off,
-                                                             uint16_t* ent) {
+                                                             StEnt* ent) {
     __shared__ int cnt[kStMaxRows];
     __shared__ int scan_tmp[kRowsThreads / 64 + 1];
     const int f = blockIdx.x, t = threadIdx.x;
@@ -78,12 +91,14 @@ __global__ void __launch_bounds__(kRowsThreads) k_stereo_rows(StereoGeom G, cons
     }
     if (t == kRowsThreads - 1) off[nrows] = incl;
     __syncthreads();
-    uint16_t* E = ent + (size_t)f * G.ent_cap;
+    StEnt* E = ent + (size_t)f * G.ent_cap;
     for (int i = t; i < nr; i += kRowsThreads) {
-        const float y = K[i].y;
-        const float r = 2.0f * G.scale[K[i].octave];
+        const float y = K[i].y, x = K[i].x;
+        const int oct = K[i].octave;
+        const float r = 2.0f * G.scale[oct];
         const int maxr = (int)ceilf(y + r), minr = (int)floorf(y - r);
-        for (int yi = max(minr, 0); yi <= min(maxr, nrows - 1); yi++) E[atomicAdd(&cnt[yi], 1)] = (uint16_t)i;
+        for (int yi = max(minr, 0); yi <= min(maxr, nrows - 1); yi++)
+            E[atomicAdd(&cnt[yi], 1)] = StEnt{(uint16_t)i, (int16_t)oct, x};
     }
 }
 
@@ -95,7 +110,7 @@ __device__ __forceinline__ int ham32(const uint4 a0, const uint4 a1, const uint4
 __global__ void __launch_bounds__(kMatchThreads) k_stereo_match(StereoGeom G, const slam_keypoint* kps_l,
                                                                const uint8_t* desc_l, const int32_t* n_l,
                                                                const slam_keypoint* kps_r, const uint8_t* desc_r,
-                                                               const int32_t* row_off, const uint16_t* ent,
+                                                               const int32_t* row_off, const StEnt* ent,
                                                                float* uright, float* depth, int32_t* sad) {
     const int f = blockIdx.y;
     const int iL = blockIdx.x * kMatchThreads + threadIdx.x;
@@ -117,35 +132,35 @@ __global__ void __launch_bounds__(kMatchThreads) k_stereo_match(StereoGeom G, co
         if (row >= 0 && row < G.nrows && !(maxU < 0)) {
             const uint4* dl = reinterpret_cast<const uint4*>(desc_l + o * 32);
             const uint4 a0 = dl[0], a1 = dl[1];
-            const slam_keypoint* KR = kps_r + (size_t)f * G.cap;
             const uint8_t* DR = desc_r + (size_t)f * G.cap * 32;
-            const uint16_t* E = ent + (size_t)f * G.ent_cap;
+            const StEnt* E = ent + (size_t)f * G.ent_cap;
             const int c0 = off[row], c1 = off[row + 1];
-            // candidates four at a time: their indices, then keypoints, then descriptors are
-            // loaded together (three dependent rounds per four candidates instead of per one)
-            for (int c = c0; c < c1; c += 4) {
-                int iR[4];
-                bool ok[4];
+            // candidates kStCand at a time: their band entries (index, octave, x), then the
+            // descriptors of those that pass the octave / u filter, loaded together (two dependent
+            // rounds per kStCand candidates)
+            for (int c = c0; c < c1; c += kStCand) {
+                int iR[kStCand];
+                bool ok[kStCand];
 #pragma unroll
-                for (int q = 0; q < 4; q++) iR[q] = c + q < c1 ? (int)E[c + q] : -1;
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
+                for (int q = 0; q < kStCand; q++) {
                     ok[q] = false;
-                    if (iR[q] >= 0) {
-                        const slam_keypoint k = KR[iR[q]];
-                        ok[q] = !(k.octave < levelL - 1 || k.octave > levelL + 1) && k.x >= minU && k.x <= maxU;
+                    iR[q] = -1;
+                    if (c + q < c1) {
+                        const StEnt en = E[c + q];
+                        iR[q] = en.idx;
+                        ok[q] = !(en.octave < levelL - 1 || en.octave > levelL + 1) && en.x >= minU && en.x <= maxU;
                     }
                 }
-                uint4 d0[4], d1[4];
+                uint4 d0[kStCand], d1[kStCand];
 #pragma unroll
-                for (int q = 0; q < 4; q++)
+                for (int q = 0; q < kStCand; q++)
                     if (ok[q]) {
                         const uint4* dr = reinterpret_cast<const uint4*>(DR + (size_t)iR[q] * 32);
                         d0[q] = dr[0];
                         d1[q] = dr[1];
                     }
 #pragma unroll
-                for (int q = 0; q < 4; q++)
+                for (int q = 0; q < kStCand; q++)
                     if (ok[q]) {
                         const int d = ham32(a0, a1, d0[q], d1[q]);
                         if (d < bestDist || (d == bestDist && d < 100 && iR[q] < bestIdxR)) {
@@ -421,7 +436,7 @@ slam_status slamhot_stereo_match_batch_device(slam_stereo* st, slam_extractor* l
     (void)hipSetDevice(st->device);
     slam_status s;
     if ((s = grow(&st->d_rowoff, &st->cap_rowoff, (size_t)nframes * (G.nrows + 1) * sizeof(int32_t))) ||
-        (s = grow(&st->d_ent, &st->cap_ent, (size_t)nframes * G.ent_cap * sizeof(uint16_t))))
+        (s = grow(&st->d_ent, &st->cap_ent, (size_t)nframes * G.ent_cap * sizeof(StEnt))))
         return s;
     int32_t* sad = (int32_t*)d_sad;
     if (!sad) {
@@ -431,11 +446,11 @@ slam_status slamhot_stereo_match_batch_device(slam_stereo* st, slam_extractor* l
     hipStream_t strm = hip_stream ? (hipStream_t)hip_stream : st->stream;
     hipLaunchKernelGGL(k_stereo_rows, dim3(nframes), dim3(kRowsThreads), 0, strm, G,
                        (const slam_keypoint*)d_kps_right, (const int32_t*)d_n_right, (int32_t*)st->d_rowoff,
-                       (uint16_t*)st->d_ent);
+                       (StEnt*)st->d_ent);
     hipLaunchKernelGGL(k_stereo_match, dim3((cap + kMatchThreads - 1) / kMatchThreads, nframes), dim3(kMatchThreads),
                        0, strm, G, (const slam_keypoint*)d_kps_left, (const uint8_t*)d_desc_left,
                        (const int32_t*)d_n_left, (const slam_keypoint*)d_kps_right, (const uint8_t*)d_desc_right,
-                       (const int32_t*)st->d_rowoff, (const uint16_t*)st->d_ent, (float*)d_uright, (float*)d_depth,
+                       (const int32_t*)st->d_rowoff, (const StEnt*)st->d_ent, (float*)d_uright, (float*)d_depth,
                        sad);
     hipLaunchKernelGGL(k_stereo_median, dim3(nframes), dim3(kMedianThreads), 0, strm, cap,
                        (const int32_t*)d_n_left, (const int32_t*)sad, (float*)d_uright, (float*)d_depth);
