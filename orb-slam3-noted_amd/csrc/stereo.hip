@@ -37,6 +37,10 @@ constexpr int kMedianThreads = 1024;
 #define SLAMHOT_ST_CAND 4
 #endif
 constexpr int kStCand = SLAMHOT_ST_CAND;  // band candidates per step of k_stereo_match
+#ifndef SLAMHOT_ST_SADROWS
+#define SLAMHOT_ST_SADROWS 2
+#endif
+constexpr int kSadRows = SLAMHOT_ST_SADROWS;  // SAD window rows whose loads are issued together
 
 // one band-table entry: the right keypoint's index with the two fields the candidate filter reads
 // (octave, x), so a candidate costs one 8-byte load instead of an index and a 28-byte keypoint
@@ -196,32 +200,43 @@ __global__ void __launch_bounds__(kMatchThreads) k_stereo_match(StereoGeom G, co
                 // the rows (3 bytes of slack before the pitch), else the byte form
                 const bool packed = ux0 + 2 * w + 4 <= pl && ur0 + L + w + 4 <= pr;
                 if (packed) {
-                    for (int yy = 0; yy < 2 * w + 1; yy++) {
-                        const uint8_t* ra = PL + (size_t)yy * pl;
-                        const uint8_t* rb = PR + (size_t)yy * pr;
-                        const uint32_t* da = reinterpret_cast<const uint32_t*>((uintptr_t)ra & ~(uintptr_t)3);
-                        const uint32_t* db = reinterpret_cast<const uint32_t*>((uintptr_t)rb & ~(uintptr_t)3);
-                        const int sa = (int)((uintptr_t)ra & 3), sb = (int)((uintptr_t)rb & 3);
-                        uint32_t wa[4], wb[7];
+                    // kSadRows rows' dword loads issued together, then their sums
+                    for (int y0 = 0; y0 < 2 * w + 1; y0 += kSadRows) {
+                        uint32_t wa[kSadRows][4], wb[kSadRows][7];
+                        int sa[kSadRows], sb[kSadRows];
 #pragma unroll
-                        for (int q = 0; q < 4; q++) wa[q] = q * 4 < sa + 2 * w + 1 ? da[q] : 0u;
+                        for (int rr = 0; rr < kSadRows; rr++) {
+                            const int yy = min(y0 + rr, 2 * w);
+                            const uint8_t* ra = PL + (size_t)yy * pl;
+                            const uint8_t* rb = PR + (size_t)yy * pr;
+                            const uint32_t* da = reinterpret_cast<const uint32_t*>((uintptr_t)ra & ~(uintptr_t)3);
+                            const uint32_t* db = reinterpret_cast<const uint32_t*>((uintptr_t)rb & ~(uintptr_t)3);
+                            sa[rr] = (int)((uintptr_t)ra & 3);
+                            sb[rr] = (int)((uintptr_t)rb & 3);
 #pragma unroll
-                        for (int q = 0; q < 7; q++) wb[q] = q * 4 < sb + 2 * w + 2 * L + 1 ? db[q] : 0u;
-                        const uint32_t A0 = __builtin_amdgcn_alignbyte(wa[1], wa[0], sa);
-                        const uint32_t A1 = __builtin_amdgcn_alignbyte(wa[2], wa[1], sa);
-                        const uint32_t A2 = __builtin_amdgcn_alignbyte(wa[3], wa[2], sa) & 0x00FFFFFFu;
-                        uint32_t Bn[6];  // right bytes 0..23 of the row, dword aligned
+                            for (int q = 0; q < 4; q++) wa[rr][q] = q * 4 < sa[rr] + 2 * w + 1 ? da[q] : 0u;
 #pragma unroll
-                        for (int q = 0; q < 6; q++) Bn[q] = __builtin_amdgcn_alignbyte(wb[q + 1], wb[q], sb);
+                            for (int q = 0; q < 7; q++) wb[rr][q] = q * 4 < sb[rr] + 2 * w + 2 * L + 1 ? db[q] : 0u;
+                        }
 #pragma unroll
-                        for (int k = 0; k < 2 * L + 1; k++) {
-                            const int qd = k >> 2, sh = k & 3;
-                            const uint32_t B0 = __builtin_amdgcn_alignbyte(Bn[qd + 1], Bn[qd], sh);
-                            const uint32_t B1 = __builtin_amdgcn_alignbyte(Bn[qd + 2], Bn[qd + 1], sh);
-                            const uint32_t B2 = __builtin_amdgcn_alignbyte(Bn[qd + 3], Bn[qd + 2], sh) & 0x00FFFFFFu;
-                            acc[k] = (int)__builtin_amdgcn_sad_u8(A2, B2,
-                                                                 __builtin_amdgcn_sad_u8(A1, B1,
-                                                                                         __builtin_amdgcn_sad_u8(A0, B0, (uint32_t)acc[k])));
+                        for (int rr = 0; rr < kSadRows; rr++) {
+                            if (y0 + rr > 2 * w) break;
+                            const uint32_t A0 = __builtin_amdgcn_alignbyte(wa[rr][1], wa[rr][0], sa[rr]);
+                            const uint32_t A1 = __builtin_amdgcn_alignbyte(wa[rr][2], wa[rr][1], sa[rr]);
+                            const uint32_t A2 = __builtin_amdgcn_alignbyte(wa[rr][3], wa[rr][2], sa[rr]) & 0x00FFFFFFu;
+                            uint32_t Bn[6];  // right bytes 0..23 of the row, dword aligned
+#pragma unroll
+                            for (int q = 0; q < 6; q++) Bn[q] = __builtin_amdgcn_alignbyte(wb[rr][q + 1], wb[rr][q], sb[rr]);
+#pragma unroll
+                            for (int k = 0; k < 2 * L + 1; k++) {
+                                const int qd = k >> 2, sh = k & 3;
+                                const uint32_t B0 = __builtin_amdgcn_alignbyte(Bn[qd + 1], Bn[qd], sh);
+                                const uint32_t B1 = __builtin_amdgcn_alignbyte(Bn[qd + 2], Bn[qd + 1], sh);
+                                const uint32_t B2 = __builtin_amdgcn_alignbyte(Bn[qd + 3], Bn[qd + 2], sh) & 0x00FFFFFFu;
+                                acc[k] = (int)__builtin_amdgcn_sad_u8(A2, B2,
+                                                                     __builtin_amdgcn_sad_u8(A1, B1,
+                                                                                             __builtin_amdgcn_sad_u8(A0, B0, (uint32_t)acc[k])));
+                            }
                         }
                     }
                 } else {
