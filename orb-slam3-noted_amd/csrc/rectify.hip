@@ -28,6 +28,9 @@ constexpr int kRemapThreads = 256;
 #define SLAMHOT_REMAP_FPB 16
 #endif
 constexpr int kFramesPerBlock = SLAMHOT_REMAP_FPB;  // experiment builds: -DSLAMHOT_REMAP_FPB=<n>
+#ifndef SLAMHOT_REMAP_XCD
+#define SLAMHOT_REMAP_XCD 1
+#endif
 
 struct MapEntry {
     int16_t sx, sy;
@@ -138,7 +141,19 @@ __global__ void __launch_bounds__(256) k_remap_tiled(const MapEntry* map, const 
                                                      int64_t sstride, uint8_t* dst, int dp, int64_t dstride) {
     __shared__ __attribute__((aligned(16))) uint8_t box[kBoxMax];
     constexpr int kPer = 4;  // box dwords per thread (register double buffer across frames)
-    const int tile = blockIdx.x, tx = tile % tiles_x, ty = tile / tiles_x;
+#if SLAMHOT_REMAP_XCD
+    // XCD-aware order (cdna_hip_programming.md T1): the dispatcher deals consecutive workgroups
+    // round-robin over the 8 XCDs; remapped, each XCD takes a contiguous run of (tile, frame group)
+    // in tile-fastest order, so the source rows two neighbouring tiles' boxes share are fetched into
+    // one L2 instead of two.  Speed only: any placement is correct.
+    const int nwg = (int)(gridDim.x * gridDim.y), orig = (int)(blockIdx.x + gridDim.x * blockIdx.y);
+    const int xq = nwg >> 3, xr = nwg & 7, xcd = orig & 7;
+    const int wg = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (orig >> 3);
+    const int tile = wg % (int)gridDim.x, fgrp = wg / (int)gridDim.x;
+#else
+    const int tile = blockIdx.x, fgrp = blockIdx.y;
+#endif
+    const int tx = tile % tiles_x, ty = tile / tiles_x;
     const int4 B = boxes[tile];
     const int lx = (threadIdx.x & 15) * 4, ly = threadIdx.x >> 4;  // 16 threads x 4 px per row, 16 rows
     const int x0 = tx * kTileW + lx, y = ty * kTileH + ly;
@@ -147,7 +162,7 @@ __global__ void __launch_bounds__(256) k_remap_tiled(const MapEntry* map, const 
     MapEntry e[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) e[k] = live ? map[(size_t)y * dw + min(x0 + k, dw - 1)] : MapEntry{0, 0, 0};
-    const int f0 = blockIdx.y * kFramesPerBlock, f1 = min(nframes, f0 + kFramesPerBlock);
+    const int f0 = fgrp * kFramesPerBlock, f1 = min(nframes, f0 + kFramesPerBlock);
     const bool aligned = nx == 4 && ((dp | (int)(dstride & 3)) & 3) == 0;
     const bool aligned_src = ((sp | (int)(sstride & 3) | (int)((uintptr_t)src & 3)) & 3) == 0;
     // box rows start at the 4-byte-aligned column ax <= B.x; thread (qr, qc) owns dword qc of rows
