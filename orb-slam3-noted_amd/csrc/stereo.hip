@@ -40,7 +40,10 @@ constexpr int kStCand = SLAMHOT_ST_CAND;  // band candidates per step of k_stere
 #ifndef SLAMHOT_ST_SADROWS
 #define SLAMHOT_ST_SADROWS 2
 #endif
-constexpr int kSadRows = SLAMHOT_ST_SADROWS;  // SAD window rows whose loads are issued together
+constexpr int kSadRows = SLAMHOT_ST_SADROWS;
+#ifndef SLAMHOT_ST_XCD
+#define SLAMHOT_ST_XCD 1
+#endif  // SAD window rows whose loads are issued together
 
 // one band-table entry: the right keypoint's index with the two fields the candidate filter reads
 // (octave, x), so a candidate costs one 8-byte load instead of an index and a 28-byte keypoint
@@ -116,8 +119,20 @@ __global__ void __launch_bounds__(kMatchThreads) k_stereo_match(StereoGeom G, co
                                                                const slam_keypoint* kps_r, const uint8_t* desc_r,
                                                                const int32_t* row_off, const StEnt* ent,
                                                                float* uright, float* depth, int32_t* sad) {
+#if SLAMHOT_ST_XCD
+    // XCD-aware order (cdna_hip_programming.md T1): consecutive workgroups go round-robin to the 8
+    // XCDs; remapped, each XCD takes a contiguous run of (keypoint chunk, frame), so one frame's
+    // chunks -- which all read that frame's band table, right descriptors and pyramid windows --
+    // share one L2.  Speed only: any placement is correct.
+    const int nwg = (int)(gridDim.x * gridDim.y), orig = (int)(blockIdx.x + gridDim.x * blockIdx.y);
+    const int xq = nwg >> 3, xr = nwg & 7, xcd = orig & 7;
+    const int wg = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (orig >> 3);
+    const int f = wg / (int)gridDim.x;
+    const int iL = (wg - f * (int)gridDim.x) * kMatchThreads + threadIdx.x;
+#else
     const int f = blockIdx.y;
     const int iL = blockIdx.x * kMatchThreads + threadIdx.x;
+#endif
     if (iL >= G.cap) return;
     const size_t o = (size_t)f * G.cap + iL;
     float ur_out = -1.0f, dep_out = -1.0f;
