@@ -190,6 +190,9 @@ constexpr int kBowCap = 8192;        // features per side held in LDS
 #endif
 constexpr int kBowThreads = SLAMHOT_BOW_THREADS;  // 16 waves per pair: a wave per common node in turn
 constexpr int kBowNodeChunks = 4;    // B candidates per node held in registers: 4 x 64
+#ifndef SLAMHOT_BOW_XCD
+#define SLAMHOT_BOW_XCD 1
+#endif
 
 __device__ __forceinline__ int rot_bin(float a, float b) {
     // ORBmatcher.cc:391-396: float difference, +360 if negative, std::round(rot * (1/30))
@@ -235,7 +238,15 @@ __global__ void __launch_bounds__(kBowThreads) k_bow_match(const DevBowPair* pai
     __shared__ int16_t common[2 * 4096];  // (ia, ib) of common nodes
     __shared__ int hist[32];
     __shared__ int s_ncommon, s_keep[3], s_count;
+#if SLAMHOT_BOW_XCD
+    // XCD-aware order (cdna_hip_programming.md T1): a run of consecutive pairs per XCD, so the
+    // frames that neighbouring pairs share (a sequence's frame is the next pair's KeyFrame) are
+    // read into one L2.  Speed only: any placement is correct.
+    const int nwg = (int)gridDim.x, orig = (int)blockIdx.x, xq = nwg >> 3, xr = nwg & 7, xcd = orig & 7;
+    const DevBowPair pr = pairs[(xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (orig >> 3)];
+#else
     const DevBowPair pr = pairs[blockIdx.x];
+#endif
     if (pr.general) return;  // k_bow_match_any's pair
     const DevBowSide& A = pr.A;
     const DevBowSide& B = pr.B;
