@@ -72,6 +72,22 @@ def test_stereo_small_and_wide_baselines():
     right.close()
 
 
+@pytest.mark.parametrize("levels, scale", [(12, 1.1), (16, 1.05), (4, 1.6)])
+def test_stereo_non_default_pyramids(levels, scale):
+    """Octaves past 7 and wide / narrow row bands (2 * scale[octave]): the band table's packed
+    octave and x, and the SAD windows on every level, against the oracle (odd width, 733 x 461)."""
+    import slamhot
+    il, ir = _pairs([(7, 3.0, 30.0, 2.0), (8, 1.0, 12.0, 2.0)], 733, 461)
+    F, H, W = il.shape
+    kw = dict(nfeatures=1500, scaleFactor=scale, nlevels=levels, max_size=(W, H), max_batch=F)
+    left, right = slamhot.ORBextractor(**kw), slamhot.ORBextractor(**kw)
+    out = slamhot.ComputeStereoMatches(left, right, il, ir, MBF, MB)
+    assert _check(left, right, out, 1500) > 100
+    assert max(int(o[0]["octave"].max()) for o in out) >= min(levels - 1, 8)
+    left.close()
+    right.close()
+
+
 def test_stereo_same_image_and_empty_right():
     """Right == left + noise (disparities around 0: the disparity <= 0 branch) and a flat
     right image (no right keypoints: every mvuRight stays -1)."""
