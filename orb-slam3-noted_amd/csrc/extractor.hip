@@ -1969,6 +1969,7 @@ struct slam_extractor {
     // taken from other batches' FAST / orb and level 0 keeps its keys in L2 (one VGA frame:
     // level 0 115 us + levels 1-7 49 us as two launches)
     OctGroup oct_small{};
+    OctGroup oct_all{};  // every level in one launch at the levels-1.. budget (SLAMHOT_OCT_MERGE=1, A/B)
     int octree_max_cells = 1;
     // per-stage HIP-event timing (slamhot_extractor_set_profiling)
     bool profiling = false;
@@ -2216,6 +2217,14 @@ static slam_status ensure_plan(slam_extractor* ex, int W, int H) {
         G.lds = octree_lds_bytes(P.max_nodes, G.keycap, max_cells);
         lds_attr = std::max(lds_attr, G.lds);
     }
+    ex->oct_all.l0 = 0;
+    ex->oct_all.nl = P.nlevels;
+    {
+        const char* e = std::getenv("SLAMHOT_OCT_MERGE_KB");  // A/B: the merged launch's LDS budget per wave
+        ex->oct_all.keycap = keycap_for((size_t)(e ? std::max(1, std::atoi(e)) : 20) * 1024);
+    }
+    ex->oct_all.lds = octree_lds_bytes(P.max_nodes, ex->oct_all.keycap, max_cells);
+    lds_attr = std::max(lds_attr, ex->oct_all.lds);
     ex->oct_small.l0 = 0;
     ex->oct_small.nl = P.nlevels;
     ex->oct_small.keycap = keycap_for(96 * 1024);
@@ -2289,6 +2298,7 @@ static slam_status launch_range(slam_extractor* ex, int f0, int nframes, const u
     const bool oct_multi_small = env_flag("SLAMHOT_OCT_SMALL", true);
     const bool oct_multi_l0 = env_flag("SLAMHOT_OCT_L0", false);
     const bool oct_multi_rest = env_flag("SLAMHOT_OCT_REST", false);  // levels 1-7 group multi-wave (A/B)
+    const bool oct_merge = env_flag("SLAMHOT_OCT_MERGE", false);      // one launch for every level (A/B)
     hipEvent_t e0 = nullptr;
     auto begin = [&](int, hipStream_t st_ = nullptr) {
         if (ex->profiling) { e0 = ex->ev(); (void)hipEventRecord(e0, st_ ? st_ : s); }
@@ -2348,8 +2358,8 @@ static slam_status launch_range(slam_extractor* ex, int f0, int nframes, const u
     if (fast_done) SLAM_HIP_TRY(hipEventRecord(fast_done, s));
     begin(kStOctree);
     const bool small = nframes <= kSmallBatch;
-    for (int g = 0; g < (small ? 1 : ex->n_oct) && !SKIP(kStOctree); g++) {
-        const slam_extractor::OctGroup& G = small ? ex->oct_small : ex->oct[g];
+    for (int g = 0; g < (small || oct_merge ? 1 : ex->n_oct) && !SKIP(kStOctree); g++) {
+        const slam_extractor::OctGroup& G = small ? ex->oct_small : oct_merge ? ex->oct_all : ex->oct[g];
         // the per-image call (small batches) and, for large batches, level 0 run the multi-wave
         // form; levels 1-7 of large batches one wave per (frame, level)
         if (small ? oct_multi_small : (G.l0 == 0 ? oct_multi_l0 : oct_multi_rest))
