@@ -63,6 +63,43 @@ def test_odd_sizes_bitexact(gpu_extractor_factory, size):
     _compare(kg, dg, mg, ko, do, mo)
 
 
+@pytest.mark.parametrize("size", [(4095, 480), (3000, 320), (1920, 1080)])
+def test_extreme_sizes_bitexact(gpu_extractor_factory, size):
+    """The widest accepted image (4095 columns: level pitch 4096; 9-10 DistributeOctTree roots per
+    level), a 3000 x 320 strip (12-15 roots, near the 16-root table), and full HD, 2000 features;
+    pyramid and keypoints bit-exact."""
+    w, h = size
+    ex = gpu_extractor_factory(nfeatures=2000, max_size=size)
+    img = synth.frame(77, w, h)
+    kg, dg, mg = ex(img)
+    ko, do, mo = ob.extract(img, ob.params(nfeatures=2000))
+    _compare(kg, dg, mg, ko, do, mo)
+    ref = ob.pyramid(img)
+    for l in range(8):
+        assert np.array_equal(ex.pyramid_level(l), ref[l]), l
+
+
+def test_root_table_limits_rejected():
+    """More than 16 DistributeOctTree roots on a level (an aspect ratio beyond ~16:1, e.g. 4095 x
+    250: 19-29 roots) is outside the device's root table: SLAM_EINVAL at create, no launch."""
+    import slamhot
+    with pytest.raises(slamhot.SlamError) as e:
+        slamhot.ORBextractor(nfeatures=1000, max_size=(4095, 250))
+    assert e.value.status == slamhot.SLAM_EINVAL
+
+
+def test_portrait_geometry_rejected():
+    """An image more than ~2x taller than wide: DistributeOctTree's root count
+    round((maxX - minX) / (maxY - minY)) is 0 on some level and the reference divides by it and
+    reads an empty node list (ORBextractor.cc:541-560, undefined behaviour; the restated oracle
+    crashes the same way, so it is not run here).  The device extractor refuses the geometry
+    when the handle is created: SLAM_EINVAL, no launch."""
+    import slamhot
+    with pytest.raises(slamhot.SlamError) as e:
+        slamhot.ORBextractor(nfeatures=1000, max_size=(256, 2400))
+    assert e.value.status == slamhot.SLAM_EINVAL
+
+
 @pytest.mark.parametrize("lap", [(0, 0), (0, 1000), (100, 400)])
 def test_lapping_order(gpu_extractor_factory, lap):
     ex = gpu_extractor_factory(nfeatures=1000, max_size=(640, 480))
