@@ -47,6 +47,16 @@ def test_pose_batch_and_small_frames(popt):
     assert g["n_inliers"] == 0 and np.array_equal(g["Tcw"], tiny["Tcw"])
 
 
+@pytest.mark.parametrize("outliers", [0.6, 0.95])
+def test_pose_mostly_outliers(popt, outliers):
+    """Most observations are gross outliers: the chi2 gates of the four rounds
+    (Optimizer.cc PoseOptimization, 5.991 / 7.815) flag nearly every edge, the later rounds run
+    on few inliers, and the outcome (flags, inlier count, pose) still equals the oracle's."""
+    frames = [synth.pose_frame(40 + i, outlier_frac=outliers, stereo_frac=0.5 * i) for i in range(2)]
+    for f, g in zip(frames, popt.solve(frames)):
+        _check(g, ob.pose_optimization(f))
+
+
 def test_pose_large_initial_error(popt):
     f = synth.pose_frame(20, rot_deg=5.0, trans_m=0.3, outlier_frac=0.3)
     _check(popt.solve(f), ob.pose_optimization(f))
