@@ -248,6 +248,13 @@ __global__ void __launch_bounds__(kBowThreads) k_bow_match(const DevBowPair* pai
     const DevBowPair pr = pairs[blockIdx.x];
 #endif
     if (pr.general) return;  // k_bow_match_any's pair
+#ifdef SLAMHOT_BOW_TRACE
+    // phase clocks of one workgroup (experiment builds): start, init, merge-join, per-wave node loop end
+    const bool btr = blockIdx.x == 37;
+    const long long bt0 = (long long)__builtin_amdgcn_s_memtime();
+    long long bt1 = 0, bt2 = 0;
+    int bnodes = 0, bfeat = 0;
+#endif
     const DevBowSide& A = pr.A;
     const DevBowSide& B = pr.B;
     // wave index via v_readfirstlane: wave-uniform, so the per-node records load into SGPRs
@@ -259,6 +266,9 @@ __global__ void __launch_bounds__(kBowThreads) k_bow_match(const DevBowPair* pai
     if (tid < 32) hist[tid] = 0;
     if (tid == 0) s_ncommon = 0;
     __syncthreads();
+#ifdef SLAMHOT_BOW_TRACE
+    bt1 = (long long)__builtin_amdgcn_s_memtime();
+#endif
     // common node ids (merge-join of two ascending lists)
     for (int ia = tid; ia < A.n_nodes; ia += blockDim.x) {
         const uint32_t id = A.node_id[ia];
@@ -277,9 +287,16 @@ __global__ void __launch_bounds__(kBowThreads) k_bow_match(const DevBowPair* pai
     }
     __syncthreads();
     const int ncommon = min(s_ncommon, 4096);
+#ifdef SLAMHOT_BOW_TRACE
+    bt2 = (long long)__builtin_amdgcn_s_memtime();
+#endif
     for (int c = wave; c < ncommon; c += nwaves) {
         const int ia = common[2 * c], ib = common[2 * c + 1];
         const int a0 = A.node_off[ia], a1 = A.node_off[ia + 1];
+#ifdef SLAMHOT_BOW_TRACE
+        bnodes++;
+        bfeat += a1 - a0;
+#endif
         const int b0 = B.node_off[ib], b1 = B.node_off[ib + 1];
         const int nbn = min(b1 - b0, 64 * kBowNodeChunks);
         // chunks holding candidates (wave-uniform): most vocabulary nodes hold a few features, so
@@ -349,20 +366,30 @@ __global__ void __launch_bounds__(kBowThreads) k_bow_match(const DevBowPair* pai
                 for (int k = 0; k < kBowNodeChunks; k++) {
                     if (64 * k + lane == bpos) {
                         bok[k] = false;
-                        matchA[idxA] = (int16_t)bidx[k];
-                        if (check_ori)
-                            binA[idxA] = (int8_t)rot_bin(A.angle[(size_t)idxA * A.angle_stride],
-                                                         B.angle[(size_t)bidx[k] * B.angle_stride]);
+                        matchA[idxA] = (int16_t)bidx[k];  // its rotation bin after the node loop
                     }
                 }
             }
           }
         }
     }
+#ifdef SLAMHOT_BOW_TRACE
+    if (btr && lane == 0)
+        printf("BOWTRACE wave %d nodes %d feat %d init %lld join %lld loop %lld (ncommon %d nA %d nB %d)\n", wave, bnodes,
+               bfeat, bt1 - bt0, bt2 - bt1, (long long)__builtin_amdgcn_s_memtime() - bt2, ncommon, A.n, B.n);
+#endif
     __syncthreads();
     if (check_ori) {
-        for (int i = tid; i < A.n; i += blockDim.x)
-            if (matchA[i] >= 0) atomicAdd(&hist[binA[i]], 1);
+        // the rotation bins of the tentative matches (ORBmatcher.cc:389-398), in parallel: their
+        // two angle loads per match no longer sit on a wave's sequential greedy chain
+        for (int i = tid; i < A.n; i += blockDim.x) {
+            const int m = matchA[i];
+            if (m >= 0) {
+                const int bn = rot_bin(A.angle[(size_t)i * A.angle_stride], B.angle[(size_t)m * B.angle_stride]);
+                binA[i] = (int8_t)bn;
+                atomicAdd(&hist[bn], 1);
+            }
+        }
         __syncthreads();
         if (tid == 0) three_maxima(hist, s_keep);
         __syncthreads();
@@ -458,18 +485,21 @@ __global__ void __launch_bounds__(512) k_bow_match_any(const DevBowPair* pairs, 
             if (pass && lane == 0) {
                 const int bidx = (int)B.node_feat[b0 + bpos];
                 pr.taken[bidx] = 1;
-                pr.a2b[idxA] = bidx;
-                if (check_ori)
-                    pr.bins[idxA] = (int8_t)rot_bin(A.angle[(size_t)idxA * A.angle_stride],
-                                                     B.angle[(size_t)bidx * B.angle_stride]);
+                pr.a2b[idxA] = bidx;  // its rotation bin after the node loop
             }
             __threadfence_block();  // the taken flag is read by the whole wave next
         }
     }
     __syncthreads();
     if (check_ori) {
-        for (int i = tid; i < A.n; i += blockDim.x)
-            if (pr.a2b[i] >= 0) atomicAdd(&hist[pr.bins[i]], 1);
+        for (int i = tid; i < A.n; i += blockDim.x) {
+            const int m = pr.a2b[i];
+            if (m >= 0) {
+                const int bn = rot_bin(A.angle[(size_t)i * A.angle_stride], B.angle[(size_t)m * B.angle_stride]);
+                pr.bins[i] = (int8_t)bn;
+                atomicAdd(&hist[bn], 1);
+            }
+        }
         __syncthreads();
         if (tid == 0) three_maxima(hist, s_keep);
         __syncthreads();
