@@ -173,6 +173,20 @@ def test_bow_match_batch_device(gpu_vocab, vocab_arrays):
         assert np.array_equal(b2a[p, : n[b]], b2a_o)
         total += no
     assert total > 100
+    # the same list again (its upload is skipped: same stream, same contents), then the reversed
+    # list (uploaded): each pair's results follow it
+    for plist in (pairs, pairs[::-1]):
+        d_a2b.fill_(0)
+        d_b2a.fill_(0)
+        d_nm.fill_(0)
+        torch.cuda.synchronize()
+        m.bow_match_batch_device(gpu_vocab, F, d_kps.data_ptr(), d_desc.data_ptr(), cap, d_n.data_ptr(), plist,
+                                 d_a2b.data_ptr(), d_b2a.data_ptr(), d_nm.data_ptr(), d_valid=d_valid.data_ptr())
+        assert m.bow_match_batch_status() == 0
+        order = [pairs.index(pp) for pp in plist]
+        assert np.array_equal(d_nm.cpu().numpy(), nm[order])
+        assert np.array_equal(d_a2b.cpu().numpy(), a2b[order])
+        assert np.array_equal(d_b2a.cpu().numpy(), b2a[order])
     m.close()
     ex.close()
 
