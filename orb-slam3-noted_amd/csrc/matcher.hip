@@ -191,6 +191,11 @@ constexpr int kBowCap = 8192;        // features per side held in LDS
 #endif
 constexpr int kBowThreads = SLAMHOT_BOW_THREADS;  // 16 waves per pair: a wave per common node in turn
 constexpr int kBowNodeChunks = 4;    // B candidates per node held in registers: 4 x 64
+#ifndef SLAMHOT_BOW_ROWS
+#define SLAMHOT_BOW_ROWS 1
+#endif
+constexpr bool kBowRows = SLAMHOT_BOW_ROWS != 0;  // nodes of <= kBowRow B candidates: four per wave
+constexpr int kBowRow = 16;
 #ifndef SLAMHOT_BOW_XCD
 #define SLAMHOT_BOW_XCD 1
 #endif
@@ -238,7 +243,7 @@ __global__ void __launch_bounds__(kBowThreads) k_bow_match(const DevBowPair* pai
     __shared__ int8_t binA[kBowCap];
     __shared__ int16_t common[2 * 4096];  // (ia, ib) of common nodes
     __shared__ int hist[32];
-    __shared__ int s_ncommon, s_keep[3], s_count;
+    __shared__ int s_ncommon, s_nsmall, s_keep[3], s_count;
 #if SLAMHOT_BOW_XCD
     // XCD-aware order (cdna_hip_programming.md T1): a run of consecutive pairs per XCD, so the
     // frames that neighbouring pairs share (a sequence's frame is the next pair's KeyFrame) are
@@ -265,12 +270,14 @@ __global__ void __launch_bounds__(kBowThreads) k_bow_match(const DevBowPair* pai
         binA[i] = -1;
     }
     if (tid < 32) hist[tid] = 0;
-    if (tid == 0) s_ncommon = 0;
+    if (tid == 0) s_ncommon = s_nsmall = 0;
     __syncthreads();
 #ifdef SLAMHOT_BOW_TRACE
     bt1 = (long long)__builtin_amdgcn_s_memtime();
 #endif
-    // common node ids (merge-join of two ascending lists)
+    // common node ids (merge-join of two ascending lists): nodes with more than kBowRow B candidates
+    // from the front of `common`, the others (the row form below) from its back; A.n_nodes <= 4096
+    // (the tile condition), so the two never meet
     for (int ia = tid; ia < A.n_nodes; ia += blockDim.x) {
         const uint32_t id = A.node_id[ia];
         int lo = 0, hi = B.n_nodes;
@@ -279,15 +286,14 @@ __global__ void __launch_bounds__(kBowThreads) k_bow_match(const DevBowPair* pai
             if (B.node_id[mid] < id) lo = mid + 1; else hi = mid;
         }
         if (lo < B.n_nodes && B.node_id[lo] == id) {
-            const int k = atomicAdd(&s_ncommon, 1);
-            if (k < 4096) {
-                common[2 * k] = (int16_t)ia;
-                common[2 * k + 1] = (int16_t)lo;
-            }
+            const bool small = kBowRows && B.node_off[lo + 1] - B.node_off[lo] <= kBowRow;
+            const int k = small ? 4095 - atomicAdd(&s_nsmall, 1) : atomicAdd(&s_ncommon, 1);
+            common[2 * k] = (int16_t)ia;
+            common[2 * k + 1] = (int16_t)lo;
         }
     }
     __syncthreads();
-    const int ncommon = min(s_ncommon, 4096);
+    const int ncommon = s_ncommon, nsmall = s_nsmall;
 #ifdef SLAMHOT_BOW_TRACE
     bt2 = (long long)__builtin_amdgcn_s_memtime();
 #endif
@@ -372,6 +378,69 @@ __global__ void __launch_bounds__(kBowThreads) k_bow_match(const DevBowPair* pai
                 }
             }
           }
+        }
+    }
+    // Nodes with at most kBowRow B candidates, four per wave: DPP row r (lanes 16r .. 16r+15) runs
+    // the greedy loop of its own node -- lane = B candidate, the row's A feature t broadcast to the
+    // row by ds_bpermute, best and second best by row-local DPP minima -- so a wave advances four
+    // nodes per step.  Same decisions as the wave loop above: the same (distance << 16 | position)
+    // keys, TH_LOW / nnratio test and taken flags, per node in A order.
+    if (kBowRows) {
+        const int row = lane >> 4, l16 = lane & 15;
+        for (int g = wave; 4 * g < nsmall; g += nwaves) {
+            const int c = 4 * g + row;
+            const bool live = c < nsmall;
+            const int ia = live ? common[2 * (4095 - c)] : 0, ib = live ? common[2 * (4095 - c) + 1] : 0;
+            const int a0 = live ? A.node_off[ia] : 0, a1 = live ? A.node_off[ia + 1] : 0;
+            const int b0 = live ? B.node_off[ib] : 0, nbn = live ? B.node_off[ib + 1] - b0 : 0;
+            // this lane's B candidate
+            bool bok = false;
+            int bidx = -1;
+            uint4 bd0 = make_uint4(0, 0, 0, 0), bd1 = bd0;
+            if (l16 < nbn) {
+                bidx = (int)B.node_feat[b0 + l16];
+                bok = !B.valid || B.valid[bidx];
+                const uint4* d = reinterpret_cast<const uint4*>(B.desc + (size_t)bidx * 32);
+                bd0 = d[0];
+                bd1 = d[1];
+            }
+            // A features in chunks of 16 per row, lane l16 holding feature t0 + l16 of its row
+            int na = a1 - a0;
+#pragma unroll
+            for (int o = 16; o < 64; o <<= 1) na = max(na, __shfl_xor(na, o, 64));
+            for (int t0 = 0; t0 < na; t0 += 16) {
+                int my_idx = -1;
+                uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
+                if (a0 + t0 + l16 < a1) {
+                    const int ix = (int)A.node_feat[a0 + t0 + l16];
+                    if (!A.valid || A.valid[ix]) {
+                        my_idx = ix;
+                        const uint4* dm = reinterpret_cast<const uint4*>(A.desc + (size_t)ix * 32);
+                        m0 = dm[0];
+                        m1 = dm[1];
+                    }
+                }
+                const int tn = min(16, na - t0);
+                for (int t = 0; t < tn; t++) {
+                    const int src = (lane & ~15) | t;
+                    const int idxA = __shfl(my_idx, src, 64);  // -1: past the row's node, or not valid
+                    const uint4 q0 = make_uint4(__shfl((int)m0.x, src, 64), __shfl((int)m0.y, src, 64),
+                                                __shfl((int)m0.z, src, 64), __shfl((int)m0.w, src, 64));
+                    const uint4 q1 = make_uint4(__shfl((int)m1.x, src, 64), __shfl((int)m1.y, src, 64),
+                                                __shfl((int)m1.z, src, 64), __shfl((int)m1.w, src, 64));
+                    const bool cand = bok && idxA >= 0;
+                    const int dist = cand ? hamming32(q0, q1, bd0, bd1) : 1024;
+                    const uint32_t bestkey = row16_min_u32(cand ? (((uint32_t)dist << 16) | (uint32_t)l16) : 0xFFFFFFFFu);
+                    const int best1 = bestkey == 0xFFFFFFFFu ? 256 : (int)(bestkey >> 16);
+                    const int bpos = (int)(bestkey & 0xFFFF);
+                    const int sec = (int)row16_min_u32((cand && l16 != bpos) ? (uint32_t)dist : 256u);
+                    const bool pass = (strict ? best1 < 50 : best1 <= 50) && ((float)best1 < nnratio * (float)sec);
+                    if (pass && l16 == bpos) {  // the owner lane takes its candidate
+                        bok = false;
+                        matchA[idxA] = (int16_t)bidx;
+                    }
+                }
+            }
         }
     }
 #ifdef SLAMHOT_BOW_TRACE
