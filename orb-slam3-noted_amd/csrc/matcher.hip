@@ -194,8 +194,15 @@ constexpr int kBowNodeChunks = 4;    // B candidates per node held in registers:
 #ifndef SLAMHOT_BOW_ROWS
 #define SLAMHOT_BOW_ROWS 1
 #endif
-constexpr bool kBowRows = SLAMHOT_BOW_ROWS != 0;  // nodes of <= kBowRow B candidates: four per wave
-constexpr int kBowRow = 16;
+constexpr bool kBowRows = SLAMHOT_BOW_ROWS != 0;  // nodes of <= 16 / 32 B candidates: four / two per wave
+#ifndef SLAMHOT_BOW_G32
+#define SLAMHOT_BOW_G32 1
+#endif
+constexpr bool kBowG32 = SLAMHOT_BOW_G32 != 0;  // the 32-lane groups (else 17..32 stay on the wave loop)
+#ifndef SLAMHOT_BOW_G64
+#define SLAMHOT_BOW_G64 1
+#endif
+constexpr bool kBowG64 = SLAMHOT_BOW_G64 != 0;  // 33..64 candidates: one node per wave in the group form
 #ifndef SLAMHOT_BOW_XCD
 #define SLAMHOT_BOW_XCD 1
 #endif
@@ -237,13 +244,91 @@ __device__ inline void three_maxima(const int* hist, int* keep) {
     keep[2] = ind3;
 }
 
+// The greedy SearchByBoW loop (ORBmatcher.cc:292-425, 853-930) for nodes of at most G B candidates,
+// 64 / G nodes per wave: lane group r (lanes G r .. G r + G - 1) runs the node common[first + k]
+// for k = (64 / G) g + r -- lane = B candidate, the group's A feature t broadcast to the group by
+// ds_bpermute, best and second best by group minima (DPP inside rows of 16, then swizzles across
+// rows for G = 32 / 64).  The same (distance << 16 | position) keys, TH_LOW / nnratio test and
+// taken flags as the wave loop, per node in A order: the same matches.
+template <int G>
+__device__ __forceinline__ uint32_t group_min(uint32_t x) {
+    x = row16_min_u32(x);
+    if constexpr (G >= 32) x = min(x, (uint32_t)__shfl_xor((int)x, 16, 64));
+    if constexpr (G == 64) x = min(x, (uint32_t)__shfl_xor((int)x, 32, 64));
+    return x;
+}
+
+template <int G>
+__device__ __forceinline__ void bow_groups(const DevBowSide& A, const DevBowSide& B, const int16_t* common, int first,
+                                           int n, int wave, int nwaves, int lane, float nnratio, int strict,
+                                           int16_t* matchA) {
+    constexpr int NG = 64 / G;
+    const int grp = lane / G, lg = lane & (G - 1);
+    for (int g = wave; NG * g < n; g += nwaves) {
+        const int c = NG * g + grp;
+        const bool live = c < n;
+        const int e = live ? first + c : 0;
+        const int ia = live ? common[2 * e] : 0, ib = live ? common[2 * e + 1] : 0;
+        const int a0 = live ? A.node_off[ia] : 0, a1 = live ? A.node_off[ia + 1] : 0;
+        const int b0 = live ? B.node_off[ib] : 0, nbn = live ? B.node_off[ib + 1] - b0 : 0;
+        // this lane's B candidate
+        bool bok = false;
+        int bidx = -1;
+        uint4 bd0 = make_uint4(0, 0, 0, 0), bd1 = bd0;
+        if (lg < nbn) {
+            bidx = (int)B.node_feat[b0 + lg];
+            bok = !B.valid || B.valid[bidx];
+            const uint4* d = reinterpret_cast<const uint4*>(B.desc + (size_t)bidx * 32);
+            bd0 = d[0];
+            bd1 = d[1];
+        }
+        // A features in chunks of G per group, lane lg holding feature t0 + lg of its group's node
+        int na = a1 - a0;
+#pragma unroll
+        for (int o = G; o < 64; o <<= 1) na = max(na, __shfl_xor(na, o, 64));
+        for (int t0 = 0; t0 < na; t0 += G) {
+            int my_idx = -1;
+            uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
+            if (a0 + t0 + lg < a1) {
+                const int ix = (int)A.node_feat[a0 + t0 + lg];
+                if (!A.valid || A.valid[ix]) {
+                    my_idx = ix;
+                    const uint4* dm = reinterpret_cast<const uint4*>(A.desc + (size_t)ix * 32);
+                    m0 = dm[0];
+                    m1 = dm[1];
+                }
+            }
+            const int tn = min(G, na - t0);
+            for (int t = 0; t < tn; t++) {
+                const int src = (lane & ~(G - 1)) | t;
+                const int idxA = __shfl(my_idx, src, 64);  // -1: past the group's node, or not valid
+                const uint4 q0 = make_uint4(__shfl((int)m0.x, src, 64), __shfl((int)m0.y, src, 64),
+                                            __shfl((int)m0.z, src, 64), __shfl((int)m0.w, src, 64));
+                const uint4 q1 = make_uint4(__shfl((int)m1.x, src, 64), __shfl((int)m1.y, src, 64),
+                                            __shfl((int)m1.z, src, 64), __shfl((int)m1.w, src, 64));
+                const bool cand = bok && idxA >= 0;
+                const int dist = cand ? hamming32(q0, q1, bd0, bd1) : 1024;
+                const uint32_t bestkey = group_min<G>(cand ? (((uint32_t)dist << 16) | (uint32_t)lg) : 0xFFFFFFFFu);
+                const int best1 = bestkey == 0xFFFFFFFFu ? 256 : (int)(bestkey >> 16);
+                const int bpos = (int)(bestkey & 0xFFFF);
+                const int sec = (int)group_min<G>((cand && lg != bpos) ? (uint32_t)dist : 256u);
+                const bool pass = (strict ? best1 < 50 : best1 <= 50) && ((float)best1 < nnratio * (float)sec);
+                if (pass && lg == bpos) {  // the owner lane takes its candidate
+                    bok = false;
+                    matchA[idxA] = (int16_t)bidx;
+                }
+            }
+        }
+    }
+}
+
 __global__ void __launch_bounds__(kBowThreads) k_bow_match(const DevBowPair* pairs, float nnratio,
                                                    int check_ori, int strict) {
     __shared__ int16_t matchA[kBowCap];   // B index matched by A feature, -1 none
     __shared__ int8_t binA[kBowCap];
     __shared__ int16_t common[2 * 4096];  // (ia, ib) of common nodes
     __shared__ int hist[32];
-    __shared__ int s_ncommon, s_nsmall, s_keep[3], s_count;
+    __shared__ int s_ncommon, s_n32, s_n64, s_nsmall, s_keep[3], s_count;
 #if SLAMHOT_BOW_XCD
     // XCD-aware order (cdna_hip_programming.md T1): a run of consecutive pairs per XCD, so the
     // frames that neighbouring pairs share (a sequence's frame is the next pair's KeyFrame) are
@@ -270,14 +355,17 @@ __global__ void __launch_bounds__(kBowThreads) k_bow_match(const DevBowPair* pai
         binA[i] = -1;
     }
     if (tid < 32) hist[tid] = 0;
-    if (tid == 0) s_ncommon = s_nsmall = 0;
+    if (tid == 0) s_ncommon = s_n32 = s_n64 = s_nsmall = 0;
     __syncthreads();
 #ifdef SLAMHOT_BOW_TRACE
     bt1 = (long long)__builtin_amdgcn_s_memtime();
 #endif
-    // common node ids (merge-join of two ascending lists): nodes with more than kBowRow B candidates
-    // from the front of `common`, the others (the row form below) from its back; A.n_nodes <= 4096
-    // (the tile condition), so the two never meet
+    // common node ids (merge-join of two ascending lists), by B candidate count: more than 64 (the
+    // wave loop) from the front of `common`, then 17..32, then 33..64, at most 16 from the back; a thread's
+    // finds (<= kBowPer, A.n_nodes <= 4096 by the tile condition) wait in registers for the counts
+    constexpr int kBowPer = (4096 + kBowThreads - 1) / kBowThreads;
+    int fia[kBowPer], flo[kBowPer], fcl[kBowPer];
+    int nf = 0;
     for (int ia = tid; ia < A.n_nodes; ia += blockDim.x) {
         const uint32_t id = A.node_id[ia];
         int lo = 0, hi = B.n_nodes;
@@ -285,15 +373,30 @@ __global__ void __launch_bounds__(kBowThreads) k_bow_match(const DevBowPair* pai
             const int mid = (lo + hi) >> 1;
             if (B.node_id[mid] < id) lo = mid + 1; else hi = mid;
         }
-        if (lo < B.n_nodes && B.node_id[lo] == id) {
-            const bool small = kBowRows && B.node_off[lo + 1] - B.node_off[lo] <= kBowRow;
-            const int k = small ? 4095 - atomicAdd(&s_nsmall, 1) : atomicAdd(&s_ncommon, 1);
-            common[2 * k] = (int16_t)ia;
-            common[2 * k + 1] = (int16_t)lo;
+        if (lo < B.n_nodes && B.node_id[lo] == id && nf < kBowPer) {
+            const int nb = B.node_off[lo + 1] - B.node_off[lo];
+            const int cl = !kBowRows ? 0 : nb <= 16 ? 2 : (kBowG32 && nb <= 32) ? 1 : (kBowG64 && nb <= 64) ? 3 : 0;
+            atomicAdd(cl == 0 ? &s_ncommon : cl == 1 ? &s_n32 : cl == 2 ? &s_nsmall : &s_n64, 1);
+            fia[nf] = ia;
+            flo[nf] = lo;
+            fcl[nf] = cl;
+            nf++;
         }
     }
     __syncthreads();
-    const int ncommon = s_ncommon, nsmall = s_nsmall;
+    const int ncommon = s_ncommon, n32 = s_n32, n16 = s_nsmall, n64 = s_n64;
+    if (tid == 0) s_ncommon = s_n32 = s_nsmall = s_n64 = 0;  // placement cursors
+    __syncthreads();
+    for (int k = 0; k < nf; k++) {
+        const int cl = fcl[k];
+        const int pos = cl == 0   ? atomicAdd(&s_ncommon, 1)
+                        : cl == 1 ? ncommon + atomicAdd(&s_n32, 1)
+                        : cl == 3 ? ncommon + n32 + atomicAdd(&s_n64, 1)
+                                  : 4095 - atomicAdd(&s_nsmall, 1);
+        common[2 * pos] = (int16_t)fia[k];
+        common[2 * pos + 1] = (int16_t)flo[k];
+    }
+    __syncthreads();
 #ifdef SLAMHOT_BOW_TRACE
     bt2 = (long long)__builtin_amdgcn_s_memtime();
 #endif
@@ -380,68 +483,11 @@ __global__ void __launch_bounds__(kBowThreads) k_bow_match(const DevBowPair* pai
           }
         }
     }
-    // Nodes with at most kBowRow B candidates, four per wave: DPP row r (lanes 16r .. 16r+15) runs
-    // the greedy loop of its own node -- lane = B candidate, the row's A feature t broadcast to the
-    // row by ds_bpermute, best and second best by row-local DPP minima -- so a wave advances four
-    // nodes per step.  Same decisions as the wave loop above: the same (distance << 16 | position)
-    // keys, TH_LOW / nnratio test and taken flags, per node in A order.
+    // nodes of at most 16 / 32 / 64 B candidates: four / two / one per wave (bow_groups)
     if (kBowRows) {
-        const int row = lane >> 4, l16 = lane & 15;
-        for (int g = wave; 4 * g < nsmall; g += nwaves) {
-            const int c = 4 * g + row;
-            const bool live = c < nsmall;
-            const int ia = live ? common[2 * (4095 - c)] : 0, ib = live ? common[2 * (4095 - c) + 1] : 0;
-            const int a0 = live ? A.node_off[ia] : 0, a1 = live ? A.node_off[ia + 1] : 0;
-            const int b0 = live ? B.node_off[ib] : 0, nbn = live ? B.node_off[ib + 1] - b0 : 0;
-            // this lane's B candidate
-            bool bok = false;
-            int bidx = -1;
-            uint4 bd0 = make_uint4(0, 0, 0, 0), bd1 = bd0;
-            if (l16 < nbn) {
-                bidx = (int)B.node_feat[b0 + l16];
-                bok = !B.valid || B.valid[bidx];
-                const uint4* d = reinterpret_cast<const uint4*>(B.desc + (size_t)bidx * 32);
-                bd0 = d[0];
-                bd1 = d[1];
-            }
-            // A features in chunks of 16 per row, lane l16 holding feature t0 + l16 of its row
-            int na = a1 - a0;
-#pragma unroll
-            for (int o = 16; o < 64; o <<= 1) na = max(na, __shfl_xor(na, o, 64));
-            for (int t0 = 0; t0 < na; t0 += 16) {
-                int my_idx = -1;
-                uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
-                if (a0 + t0 + l16 < a1) {
-                    const int ix = (int)A.node_feat[a0 + t0 + l16];
-                    if (!A.valid || A.valid[ix]) {
-                        my_idx = ix;
-                        const uint4* dm = reinterpret_cast<const uint4*>(A.desc + (size_t)ix * 32);
-                        m0 = dm[0];
-                        m1 = dm[1];
-                    }
-                }
-                const int tn = min(16, na - t0);
-                for (int t = 0; t < tn; t++) {
-                    const int src = (lane & ~15) | t;
-                    const int idxA = __shfl(my_idx, src, 64);  // -1: past the row's node, or not valid
-                    const uint4 q0 = make_uint4(__shfl((int)m0.x, src, 64), __shfl((int)m0.y, src, 64),
-                                                __shfl((int)m0.z, src, 64), __shfl((int)m0.w, src, 64));
-                    const uint4 q1 = make_uint4(__shfl((int)m1.x, src, 64), __shfl((int)m1.y, src, 64),
-                                                __shfl((int)m1.z, src, 64), __shfl((int)m1.w, src, 64));
-                    const bool cand = bok && idxA >= 0;
-                    const int dist = cand ? hamming32(q0, q1, bd0, bd1) : 1024;
-                    const uint32_t bestkey = row16_min_u32(cand ? (((uint32_t)dist << 16) | (uint32_t)l16) : 0xFFFFFFFFu);
-                    const int best1 = bestkey == 0xFFFFFFFFu ? 256 : (int)(bestkey >> 16);
-                    const int bpos = (int)(bestkey & 0xFFFF);
-                    const int sec = (int)row16_min_u32((cand && l16 != bpos) ? (uint32_t)dist : 256u);
-                    const bool pass = (strict ? best1 < 50 : best1 <= 50) && ((float)best1 < nnratio * (float)sec);
-                    if (pass && l16 == bpos) {  // the owner lane takes its candidate
-                        bok = false;
-                        matchA[idxA] = (int16_t)bidx;
-                    }
-                }
-            }
-        }
+        bow_groups<16>(A, B, common, 4096 - n16, n16, wave, nwaves, lane, nnratio, strict, matchA);
+        bow_groups<32>(A, B, common, ncommon, n32, wave, nwaves, lane, nnratio, strict, matchA);
+        bow_groups<64>(A, B, common, ncommon + n32, n64, wave, nwaves, lane, nnratio, strict, matchA);
     }
 #ifdef SLAMHOT_BOW_TRACE
     if (btr && lane == 0)

@@ -262,6 +262,31 @@ def _kps(rng, n):
     return k
 
 
+@pytest.mark.parametrize("ncentres", [6, 14, 30, 60])
+def test_search_by_bow_node_size_classes(gpu_vocab, ncentres):
+    """Clustered descriptors whose FeatureVector nodes hold ~15 to ~150 candidates: the lane-group
+    forms of k_bow_match (nodes of <= 16 / 32 / 64 B candidates, four / two / one per wave) and its
+    wave loop (65..256) on one pair, against the oracle, KF-Frame and strict KF-KF."""
+    import slamhot
+    rng = np.random.default_rng(50 + ncentres)
+    centres = rng.integers(0, 256, (ncentres, 32), dtype=np.uint8)
+    d0, d1 = _clustered_desc(rng, 1100, centres, 2), _clustered_desc(rng, 1000, centres, 2)
+    k0, k1 = _kps(rng, len(d0)), _kps(rng, len(d1))
+    valid = (rng.random(len(d0)) < 0.9).astype(np.uint8)
+    A = _side(gpu_vocab, k0, d0, valid)
+    B = _side(gpu_vocab, k1, d1, None)
+    sizes = np.diff(B[4])
+    assert sizes.max() <= 256  # the tiled kernel, not the general one
+    m = slamhot.ORBmatcher(0.9, True)
+    ng, b2a_g = m.SearchByBoW_KF_F(A, B)
+    no, _, b2a_o = ob.search_by_bow(A, B, 0.9, True, False)
+    assert ng == no and np.array_equal(b2a_g, b2a_o)
+    ng, a2b_g = m.SearchByBoW_KF_KF(A, B)
+    no, a2b_o, _ = ob.search_by_bow(A, B, 0.9, True, True)
+    assert ng == no and np.array_equal(a2b_g, a2b_o)
+    m.close()
+
+
 @pytest.mark.parametrize("strict", [False, True])
 def test_search_by_bow_general_path_big_nodes(gpu_vocab, strict):
     """A node of B over 4 x 64 candidates: the unbounded kernel gives the oracle's matches."""
