@@ -245,8 +245,8 @@ __device__ inline void three_maxima(const int* hist, int* keep) {
 }
 
 // The greedy SearchByBoW loop (ORBmatcher.cc:292-425, 853-930) for nodes of at most G B candidates,
-// 64 / G nodes per wave: lane group r (lanes G r .. G r + G - 1) runs the node common[first + k]
-// for k = (64 / G) g + r -- lane = B candidate, the group's A feature t broadcast to the group by
+// 64 / G nodes per wave (work item g): lane group r (lanes G r .. G r + G - 1) runs the node
+// common[first + k] for k = (64 / G) g + r -- lane = B candidate, the group's A feature t broadcast to the group by
 // ds_bpermute, best and second best by group minima (DPP inside rows of 16, then swizzles across
 // rows for G = 32 / 64).  The same (distance << 16 | position) keys, TH_LOW / nnratio test and
 // taken flags as the wave loop, per node in A order: the same matches.
@@ -259,12 +259,11 @@ __device__ __forceinline__ uint32_t group_min(uint32_t x) {
 }
 
 template <int G>
-__device__ __forceinline__ void bow_groups(const DevBowSide& A, const DevBowSide& B, const int16_t* common, int first,
-                                           int n, int wave, int nwaves, int lane, float nnratio, int strict,
-                                           int16_t* matchA) {
+__device__ __forceinline__ void bow_group(const DevBowSide& A, const DevBowSide& B, const int16_t* common, int first,
+                                          int n, int g, int lane, float nnratio, int strict, int16_t* matchA) {
     constexpr int NG = 64 / G;
     const int grp = lane / G, lg = lane & (G - 1);
-    for (int g = wave; NG * g < n; g += nwaves) {
+    {
         const int c = NG * g + grp;
         const bool live = c < n;
         const int e = live ? first + c : 0;
@@ -328,7 +327,7 @@ __global__ void __launch_bounds__(kBowThreads) k_bow_match(const DevBowPair* pai
     __shared__ int8_t binA[kBowCap];
     __shared__ int16_t common[2 * 4096];  // (ia, ib) of common nodes
     __shared__ int hist[32];
-    __shared__ int s_ncommon, s_n32, s_n64, s_nsmall, s_keep[3], s_count;
+    __shared__ int s_ncommon, s_n32, s_n64, s_nsmall, s_next, s_keep[3], s_count;
 #if SLAMHOT_BOW_XCD
     // XCD-aware order (cdna_hip_programming.md T1): a run of consecutive pairs per XCD, so the
     // frames that neighbouring pairs share (a sequence's frame is the next pair's KeyFrame) are
@@ -348,14 +347,15 @@ __global__ void __launch_bounds__(kBowThreads) k_bow_match(const DevBowPair* pai
 #endif
     const DevBowSide& A = pr.A;
     const DevBowSide& B = pr.B;
-    // wave index via v_readfirstlane: wave-uniform, so the per-node records load into SGPRs
-    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), nwaves = blockDim.x >> 6;
+    // a wave's work item comes back from the LDS counter through v_readfirstlane: wave-uniform, so
+    // the per-node records load into SGPRs
+    const int tid = threadIdx.x, lane = tid & 63;
     for (int i = tid; i < A.n; i += blockDim.x) {
         matchA[i] = -1;
         binA[i] = -1;
     }
     if (tid < 32) hist[tid] = 0;
-    if (tid == 0) s_ncommon = s_n32 = s_n64 = s_nsmall = 0;
+    if (tid == 0) s_ncommon = s_n32 = s_n64 = s_nsmall = s_next = 0;
     __syncthreads();
 #ifdef SLAMHOT_BOW_TRACE
     bt1 = (long long)__builtin_amdgcn_s_memtime();
@@ -400,7 +400,24 @@ __global__ void __launch_bounds__(kBowThreads) k_bow_match(const DevBowPair* pai
 #ifdef SLAMHOT_BOW_TRACE
     bt2 = (long long)__builtin_amdgcn_s_memtime();
 #endif
-    for (int c = wave; c < ncommon; c += nwaves) {
+    // work items, largest first, taken by the waves from an LDS counter (the node sizes differ ~10x,
+    // so a static round-robin left one wave with the big nodes after its share of the small ones):
+    // wave-loop nodes (> 64 B candidates), then the 64-, 32- and 16-lane group items
+    const int i64 = n64, i32 = (n32 + 1) >> 1, i16 = (n16 + 3) >> 2;
+    const int nitems = ncommon + i64 + i32 + i16;
+    for (;;) {
+        int it = 0;
+        if (lane == 0) it = atomicAdd(&s_next, 1);
+        it = __builtin_amdgcn_readfirstlane(it);
+        if (it >= nitems) break;
+        if (it >= ncommon) {
+            it -= ncommon;
+            if (it < i64) bow_group<64>(A, B, common, ncommon + n32, n64, it, lane, nnratio, strict, matchA);
+            else if ((it -= i64) < i32) bow_group<32>(A, B, common, ncommon, n32, it, lane, nnratio, strict, matchA);
+            else bow_group<16>(A, B, common, 4096 - n16, n16, it - i32, lane, nnratio, strict, matchA);
+            continue;
+        }
+        const int c = it;
         const int ia = common[2 * c], ib = common[2 * c + 1];
         const int a0 = A.node_off[ia], a1 = A.node_off[ia + 1];
 #ifdef SLAMHOT_BOW_TRACE
@@ -483,15 +500,9 @@ __global__ void __launch_bounds__(kBowThreads) k_bow_match(const DevBowPair* pai
           }
         }
     }
-    // nodes of at most 16 / 32 / 64 B candidates: four / two / one per wave (bow_groups)
-    if (kBowRows) {
-        bow_groups<16>(A, B, common, 4096 - n16, n16, wave, nwaves, lane, nnratio, strict, matchA);
-        bow_groups<32>(A, B, common, ncommon, n32, wave, nwaves, lane, nnratio, strict, matchA);
-        bow_groups<64>(A, B, common, ncommon + n32, n64, wave, nwaves, lane, nnratio, strict, matchA);
-    }
 #ifdef SLAMHOT_BOW_TRACE
     if (btr && lane == 0)
-        printf("BOWTRACE wave %d nodes %d feat %d init %lld join %lld loop %lld (ncommon %d nA %d nB %d)\n", wave, bnodes,
+        printf("BOWTRACE wave %d nodes %d feat %d init %lld join %lld loop %lld (ncommon %d nA %d nB %d)\n", tid >> 6, bnodes,
                bfeat, bt1 - bt0, bt2 - bt1, (long long)__builtin_amdgcn_s_memtime() - bt2, ncommon, A.n, B.n);
 #endif
     __syncthreads();
