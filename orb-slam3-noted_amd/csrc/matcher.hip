@@ -670,6 +670,54 @@ namespace {
 // keeps nodes ascending: a bitonic sort of (node << 16 | i) gives exactly that CSR.
 // ---------------------------------------------------------------------------------------
 constexpr int kFvMax = 8192;  // features per frame (LDS sort keys: 64 KB)
+#ifndef SLAMHOT_FV_REG
+#define SLAMHOT_FV_REG 1
+#endif
+
+// Bitonic sort of P <= 2 * 1024 keys with thread t holding elements 2t and 2t+1 in registers:
+// partner distance 1 is inside the thread, 2..64 inside the wave (lane xor j/2), and only
+// j >= 128 goes through LDS (10 of the 66 stages at P = 2048, 20 barriers instead of 66).
+__device__ __forceinline__ void bitonic_reg2(uint64_t* keys, int P, int tid) {
+    const int e = 2 * tid;
+    const bool live = e < P;
+    uint64_t v0 = live ? keys[e] : ~0ull, v1 = live ? keys[e + 1] : ~0ull;
+    for (int k = 2; k <= P; k <<= 1) {
+        const bool up = (e & k) == 0;
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            if (j == 1) {
+                if ((v0 > v1) == up) {
+                    const uint64_t t = v0;
+                    v0 = v1;
+                    v1 = t;
+                }
+                continue;
+            }
+            uint64_t p0, p1;
+            if (j <= 64) {
+                p0 = __shfl_xor(v0, j >> 1, 64);
+                p1 = __shfl_xor(v1, j >> 1, 64);
+            } else {
+                __syncthreads();  // the previous LDS stage's reads are done
+                if (live) {
+                    keys[e] = v0;
+                    keys[e + 1] = v1;
+                }
+                __syncthreads();
+                p0 = live ? keys[e ^ j] : ~0ull;
+                p1 = live ? keys[(e + 1) ^ j] : ~0ull;
+            }
+            const bool takemin = ((e & j) == 0) == up;
+            v0 = takemin ? min(v0, p0) : max(v0, p0);
+            v1 = takemin ? min(v1, p1) : max(v1, p1);
+        }
+    }
+    __syncthreads();
+    if (live) {
+        keys[e] = v0;
+        keys[e + 1] = v1;
+    }
+    __syncthreads();
+}
 
 __global__ void __launch_bounds__(1024) k_featvec(int cap, const int32_t* __restrict__ n_per_frame,
                                                   const int32_t* __restrict__ node, const double* __restrict__ weight,
@@ -686,21 +734,25 @@ __global__ void __launch_bounds__(1024) k_featvec(int cap, const int32_t* __rest
         keys[i] = (i < n && weight[base + i] > 0) ? (((uint64_t)(uint32_t)node[base + i] << 16) | (uint64_t)i)
                                                    : ~0ull;
     __syncthreads();
-    for (int k = 2; k <= P; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = tid; i < P; i += blockDim.x) {
-                const int x = i ^ j;
-                if (x > i) {
-                    const uint64_t a = keys[i], b = keys[x];
-                    const bool up = (i & k) == 0;
-                    if ((a > b) == up) {
-                        keys[i] = b;
-                        keys[x] = a;
+    if (SLAMHOT_FV_REG && P <= 2 * (int)blockDim.x) {
+        bitonic_reg2(keys, P, tid);
+    } else {
+        for (int k = 2; k <= P; k <<= 1)
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                for (int i = tid; i < P; i += blockDim.x) {
+                    const int x = i ^ j;
+                    if (x > i) {
+                        const uint64_t a = keys[i], b = keys[x];
+                        const bool up = (i & k) == 0;
+                        if ((a > b) == up) {
+                            keys[i] = b;
+                            keys[x] = a;
+                        }
                     }
                 }
+                __syncthreads();
             }
-            __syncthreads();
-        }
+    }
     // node boundaries -> CSR (chunks of blockDim.x, block-wide scan of the head flags)
     int carry = 0, nvalid = 0;
     for (int c0 = 0; c0 < P; c0 += blockDim.x) {

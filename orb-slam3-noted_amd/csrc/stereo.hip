@@ -311,43 +311,113 @@ __global__ void __launch_bounds__(kMatchThreads) k_stereo_match(StereoGeom G, co
     sad[o] = sad_out;
 }
 
+#ifndef SLAMHOT_ST_SELECT
+#define SLAMHOT_ST_SELECT 1
+#endif
+
+// The (m/2)-th smallest of keys[0..m) — the element std::sort would put at m/2
+// (Frame.cc:950-951) — by MSD radix select: 8 bits per pass from the highest non-zero byte
+// of the maximum (SADs of an 11 x 11 window fit 15 bits: two passes), a 256-bin LDS
+// histogram per pass, one wave scans it.  Replaces a full bitonic sort (55 barriers at 1024).
+__device__ __forceinline__ uint32_t radix_select_mid(const uint32_t* keys, int m, uint32_t vmax, uint32_t* hist,
+                                                     uint32_t* s_sel, int t) {
+    const uint32_t kth = (uint32_t)(m / 2);
+    if (vmax == 0) return 0;
+    const int top = 31 - __builtin_clz(vmax);
+    uint32_t prefix = 0, mask = 0, k = kth;
+    for (int shift = (top / 8) * 8; shift >= 0; shift -= 8) {
+        if (t < 256) hist[t] = 0;
+        __syncthreads();
+        for (int i = t; i < m; i += kMedianThreads) {
+            const uint32_t v = keys[i];
+            if ((v & mask) == prefix) atomicAdd(&hist[(v >> shift) & 255u], 1u);
+        }
+        __syncthreads();
+        if (t < 64) {
+            const uint32_t h0 = hist[4 * t], h1 = hist[4 * t + 1], h2 = hist[4 * t + 2], h3 = hist[4 * t + 3];
+            const uint32_t own = h0 + h1 + h2 + h3;
+            uint32_t inc = own;  // inclusive scan over the wave
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(inc, o, 64);
+                if (t >= o) inc += y;
+            }
+            uint32_t before = inc - own;
+            if (k >= before && k < inc) {  // exactly one lane holds the k-th
+                uint32_t b = 4 * t, c = before;
+                if (k >= c + h0) { c += h0; b++;
+                    if (k >= c + h1) { c += h1; b++;
+                        if (k >= c + h2) { c += h2; b++; } } }
+                s_sel[0] = b;
+                s_sel[1] = k - c;
+            }
+        }
+        __syncthreads();
+        prefix |= s_sel[0] << shift;
+        mask |= 255u << shift;
+        k = s_sel[1];
+        __syncthreads();  // s_sel and hist are rewritten by the next pass
+    }
+    return prefix;
+}
+
 __global__ void __launch_bounds__(kMedianThreads) k_stereo_median(int cap, const int32_t* n_l, const int32_t* sad,
                                                                  float* uright, float* depth) {
     __shared__ uint32_t keys[kStMaxSort];
+    __shared__ uint32_t hist[256], s_sel[2];
     __shared__ int count;
+    __shared__ uint32_t s_max;
     const int f = blockIdx.x, t = threadIdx.x;
     const int n = n_l[f];
     const int32_t* S = sad + (size_t)f * cap;
-    if (t == 0) count = 0;
+    if (t == 0) {
+        count = 0;
+        s_max = 0;
+    }
     __syncthreads();
+    uint32_t vmax = 0;
     for (int i = t; i < n; i += kMedianThreads) {
         const int v = S[i];
-        if (v >= 0) keys[atomicAdd(&count, 1)] = (uint32_t)v;
+        if (v >= 0) {
+            keys[atomicAdd(&count, 1)] = (uint32_t)v;
+            vmax = max(vmax, (uint32_t)v);
+        }
+    }
+    if (SLAMHOT_ST_SELECT) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) vmax = max(vmax, (uint32_t)__shfl_xor((int)vmax, o, 64));
+        if ((t & 63) == 0) atomicMax(&s_max, vmax);
     }
     __syncthreads();
     const int m = count;
     if (m == 0) return;  // the reference reads vDistIdx[0] of an empty vector here
-    int np = 1;
-    while (np < m) np <<= 1;
-    for (int i = m + t; i < np; i += kMedianThreads) keys[i] = 0xFFFFFFFFu;
-    __syncthreads();
-    for (int k = 2; k <= np; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = t; i < np; i += kMedianThreads) {
-                const int p = i ^ j;
-                if (p > i) {
-                    const uint32_t x = keys[i], y = keys[p];
-                    const bool up = (i & k) == 0;
-                    if ((x > y) == up) {
-                        keys[i] = y;
-                        keys[p] = x;
+    uint32_t mid;
+    if (SLAMHOT_ST_SELECT) {
+        mid = radix_select_mid(keys, m, s_max, hist, s_sel, t);
+    } else {
+        int np = 1;
+        while (np < m) np <<= 1;
+        for (int i = m + t; i < np; i += kMedianThreads) keys[i] = 0xFFFFFFFFu;
+        __syncthreads();
+        for (int k = 2; k <= np; k <<= 1) {
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                for (int i = t; i < np; i += kMedianThreads) {
+                    const int p = i ^ j;
+                    if (p > i) {
+                        const uint32_t x = keys[i], y = keys[p];
+                        const bool up = (i & k) == 0;
+                        if ((x > y) == up) {
+                            keys[i] = y;
+                            keys[p] = x;
+                        }
                     }
                 }
+                __syncthreads();
             }
-            __syncthreads();
         }
+        mid = keys[m / 2];
     }
-    const float median = (float)(int)keys[m / 2];
+    const float median = (float)(int)mid;
     const float thDist = 1.5f * 1.4f * median;
     for (int i = t; i < n; i += kMedianThreads) {
         const int v = S[i];
