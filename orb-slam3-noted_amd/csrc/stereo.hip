@@ -12,7 +12,7 @@
 //                    11-byte left slice and one 21-byte right slice — parabola fit and the
 //                    disparity gate (:917-946).  Integer SADs are exact, the float arithmetic
 //                    is the reference's operation for operation (no contraction).
-//   k_stereo_median  one workgroup per frame: bitonic sort of the kept SADs in LDS, median,
+//   k_stereo_median  one workgroup per frame: radix select of the median kept SAD in LDS,
 //                    cut at 1.5f*1.4f*median (:950-963).
 #include <hip/hip_runtime.h>
 
