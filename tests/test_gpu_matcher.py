@@ -246,6 +246,58 @@ def test_bow_match_batch_empty_frames(gpu_vocab, vocab_arrays):
     ex.close()
 
 
+@pytest.mark.parametrize("nfeatures, lo", [(500, 300), (1500, 1025), (3000, 2049)])
+def test_bow_match_batch_feature_counts(gpu_vocab, vocab_arrays, nfeatures, lo):
+    """k_featvec's two sorts: keypoint counts padding to 512 / 2048 (registers and wave shuffles,
+    LDS only for partner distances >= 128) and past 2048 (the LDS bitonic), then SearchByBoW,
+    against the oracle's FeatureVector and SearchByBoW."""
+    import torch
+
+    import slamhot
+    par, leaf, dn, wn = vocab_arrays
+    img0 = synth.frame(31, 1024, 768)
+    imgs = np.stack([img0, synth.shifted(img0, 5, -3, 4.0, 41)])
+    F, H, W = imgs.shape
+    dev = torch.device("cuda", 0)
+    ex = slamhot.ORBextractor(nfeatures=nfeatures, max_size=(W, H), max_batch=F)
+    cap = ex.cap
+    d_img = torch.from_numpy(imgs).to(dev)
+    d_kps = torch.zeros((F, cap, 28), dtype=torch.uint8, device=dev)
+    d_desc = torch.zeros((F, cap, 32), dtype=torch.uint8, device=dev)
+    d_n = torch.zeros(F, dtype=torch.int32, device=dev)
+    d_mono = torch.zeros(F, dtype=torch.int32, device=dev)
+    pairs = [(0, 1), (1, 0)]
+    d_a2b = torch.zeros((len(pairs), cap), dtype=torch.int32, device=dev)
+    d_b2a = torch.zeros((len(pairs), cap), dtype=torch.int32, device=dev)
+    d_nm = torch.zeros(len(pairs), dtype=torch.int32, device=dev)
+    m = slamhot.ORBmatcher(0.75, True)
+    torch.cuda.synchronize()
+    ex.extract_batch_device(d_img.data_ptr(), F, W, H, d_kps.data_ptr(), d_desc.data_ptr(), cap, d_n.data_ptr(),
+                            d_mono.data_ptr())
+    torch.cuda.synchronize()
+    m.bow_match_batch_device(gpu_vocab, F, d_kps.data_ptr(), d_desc.data_ptr(), cap, d_n.data_ptr(), pairs,
+                             d_a2b.data_ptr(), d_b2a.data_ptr(), d_nm.data_ptr())
+    assert m.bow_match_batch_status() == 0
+    n = d_n.cpu().numpy()
+    assert n.min() >= lo, n
+    kps = d_kps.cpu().numpy().view(ob.KP_DTYPE)
+    desc = d_desc.cpu().numpy()
+    a2b, b2a, nm = d_a2b.cpu().numpy(), d_b2a.cpu().numpy(), d_nm.cpu().numpy()
+    for p, (a, b) in enumerate(pairs):
+        ka, da = kps[a, : n[a]].ravel(), desc[a, : n[a]]
+        kb, db = kps[b, : n[b]].ravel(), desc[b, : n[b]]
+        _, wta, nia = ob.vocab_transform(par, leaf, dn, wn, 6, da, 4)
+        _, wtb, nib = ob.vocab_transform(par, leaf, dn, wn, 6, db, 4)
+        A = (da, ka["angle"], None) + synth.feature_vector(nia, wta)
+        B = (db, kb["angle"], None) + synth.feature_vector(nib, wtb)
+        no, a2b_o, b2a_o = ob.search_by_bow(A, B, 0.75, True, False)
+        assert nm[p] == no and no > 50
+        assert np.array_equal(a2b[p, : n[a]], a2b_o)
+        assert np.array_equal(b2a[p, : n[b]], b2a_o)
+    m.close()
+    ex.close()
+
+
 def _clustered_desc(rng, n, centres, flips=1):
     """n descriptors drawn around a few centres (a few random bit flips each): most land in one
     vocabulary node, so nodes far above k_bow_match's 256-candidate tile appear."""
